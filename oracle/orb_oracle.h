@@ -1,0 +1,142 @@
+/*
+ * ORACLE / TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the ORB-SLAM2 hot path (reference: YHY138/ORB-SLAM2-,
+ * mounted at /root/reference/ORB-SLAM2注释版, abbreviated R/ below).  Only
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+ * this library, and only as the checker / CPU baseline.  The product
+ * (orb-slam2-_amd/) never links or calls it.
+ *
+ * Parity status:
+ *  - The reference cannot be compiled here (OpenCV / Eigen absent)
+ *    and ships no tests or golden vectors.
+ *  - OpenCV primitives (resize INTER_LINEAR 8U, GaussianBlur 7x7 8U, FAST-9,
+ *    fastAtan2, cvRound) are restated from their published scalar algorithms
+ *    (OpenCV 2.4/3.x non-IPP, non-SIMD path): PARITY UNPINNED against a real
+ *    OpenCV build (none exists offline); pinned by the committed fixtures in
+ *    tests/golden/ that this restatement generated.
+ *  - glibc sinf/cosf: restated and pinned bit-exactly (exhaustive over
+ *    [0, 2*pi]) against the host libm (tests/test_sincosf.py).
+ *  - DistributeOctTree's equal-size tie break (pointer order, R/src/ORBextractor.cpp:736)
+ *    is allocator dependent; pinned here to node creation order.
+ *  - FP contraction pinned OFF; build with -ffp-contract=off.
+ */
+#ifndef ORB_ORACLE_H
+#define ORB_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {            /* == cv::KeyPoint memory layout (28 bytes) */
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} oracle_keypoint;
+
+typedef struct {
+    int nfeatures;
+    float scaleFactor;
+    int nlevels;
+    int iniThFAST;
+    int minThFAST;
+} oracle_orb_params;
+
+/* Extractor constant tables (R/src/ORBextractor.cpp:418-502). Arrays sized nlevels; umax sized 16. */
+void oracle_orb_tables(const oracle_orb_params* p, float* scale, float* inv_scale,
+                       float* sigma2, float* inv_sigma2, int* features_per_level, int* umax);
+
+/* Level geometry: cvRound(W*invScale) x cvRound(H*invScale) (R/src/ORBextractor.cpp:1203). */
+void oracle_level_sizes(const oracle_orb_params* p, int w, int h, int* lw, int* lh);
+
+/* cv::resize(src, dst, dsize, 0, 0, INTER_LINEAR) for 8UC1, scalar fixed-point path. */
+void oracle_resize_linear_u8(const uint8_t* src, int sw, int sh, size_t sstride,
+                             uint8_t* dst, int dw, int dh, size_t dstride);
+
+/* cv::GaussianBlur(src, dst, Size(7,7), 2, 2, BORDER_REFLECT_101) for 8UC1. */
+void oracle_gaussian_blur7_u8(const uint8_t* src, int w, int h, size_t stride,
+                              uint8_t* dst, size_t dstride);
+
+/* cv::FAST(roi, kps, threshold, nonmax=true), TYPE_9_16, on the ROI [x0,x0+w) x [y0,y0+h)
+ * of img.  Writes ROI-relative (x, y, score) triples; returns the count (<= cap). */
+int oracle_fast_roi(const uint8_t* img, size_t stride, int x0, int y0, int w, int h,
+                    int threshold, int* out_xys, int cap);
+
+/* OpenCV fastAtan2 (degrees, [0,360)). */
+float oracle_fast_atan2(float y, float x);
+
+/* glibc-exact sinf/cosf (see sincosf_glibc.h); returns 0 on success. */
+int oracle_sincosf(float x, float* s, float* c);
+
+/* Full ORBextractor::operator() (R/src/ORBextractor.cpp:1120-1188).
+ * Returns number of keypoints N (possibly > capacity: then only the status is
+ * -7 (E2BIG) and *n_out = N).  Empty image (w==0||h==0) -> returns 0 and leaves
+ * outputs untouched, *n_out untouched (N13).
+ * Optional outputs (may be NULL):
+ *   level_counts[nlevels] : keypoints per level after DistributeOctTree
+ *   pre_counts[nlevels]   : FAST keypoints per level before distribution
+ *   pyramid               : concatenation of all levels (row-major, stride=width)
+ *   blurred               : concatenation of all blurred levels
+ */
+int oracle_orb_extract(const oracle_orb_params* p, const uint8_t* img, int w, int h, size_t stride,
+                       oracle_keypoint* kps, uint8_t* desc, int capacity, int* n_out,
+                       int* level_counts, int* pre_counts, uint8_t* pyramid, uint8_t* blurred);
+
+/* DistributeOctTree on explicit inputs (for unit tests): keys are (x,y,response)
+ * triples in level-interior coordinates; writes the indices of the retained keys
+ * (into the input array) in output order; returns count. */
+int oracle_distribute_octree(const float* kx, const float* ky, const float* kresp, int nkeys,
+                             int minX, int maxX, int minY, int maxY, int N, int* out_idx);
+
+/* ORBmatcher::DescriptorDistance (R/src/ORBmatcher.cpp:1901-1917). */
+int oracle_descriptor_distance(const uint8_t* a, const uint8_t* b);
+
+/* Frame grid geometry + undistorted keypoint view used by the matcher. */
+typedef struct {
+    int n;                       /* number of keypoints */
+    const float* x;              /* mvKeysUn[i].pt.x */
+    const float* y;
+    const float* angle;
+    const int32_t* octave;
+    const uint8_t* desc;         /* n x 32 */
+    const float* uright;         /* mvuRight (may be NULL: all -1) */
+    float min_x, min_y, max_x, max_y;          /* mnMinX.. */
+    float grid_w_inv, grid_h_inv;              /* mfGridElementWidthInv.. */
+} oracle_frame;
+
+/* Frame::GetFeaturesInArea (R/src/Frame.cpp:387-440) with grid built by
+ * AssignFeaturesToGrid/PosInGrid (R/src/Frame.cpp:244-260,442-452). Returns count. */
+int oracle_features_in_area(const oracle_frame* f, float x, float y, float r,
+                            int minLevel, int maxLevel, int* out, int cap);
+
+/* ORBmatcher::SearchForInitialization (R/src/ORBmatcher.cpp:499-617).
+ * prev_xy: 2*N1 floats (in/out, vbPrevMatched); matches12: N1 ints (out). Returns nmatches. */
+int oracle_search_for_initialization(const oracle_frame* f1, const oracle_frame* f2,
+                                     float nnratio, int check_ori, float* prev_xy,
+                                     int* matches12, int window);
+
+/* ORBmatcher::SearchByProjection(Frame& Cur, const Frame& Last, th, bMono)
+ * (R/src/ORBmatcher.cpp:1564-1718).  Last-frame map points are given per last
+ * keypoint (last_has_mp, world xyz, 32-B descriptor); Tcw poses are row-major
+ * 3x4 float.  cur_mp (in/out, cur->n ints): -1 = empty slot, -2 = pre-occupied
+ * by a map point with observations, >=0 = index of the last-frame keypoint whose
+ * map point this call assigned.  Returns nmatches. */
+typedef struct {
+    float fx, fy, cx, cy, mbf, mb;
+} oracle_camera;
+int oracle_search_by_projection_ff(const oracle_frame* cur, const float* Tcw_cur,
+                                   const oracle_frame* last, const float* Tcw_last,
+                                   const int32_t* last_has_mp, const uint8_t* last_outlier,
+                                   const float* last_mp_xyz, const uint8_t* last_mp_desc,
+                                   const float* scale_factors, const oracle_camera* cam,
+                                   float th, int bMono, int check_ori, int32_t* cur_mp);
+
+/* Brute-force Hamming k=2 (best, second) with lowest-index tie break. */
+void oracle_hamming_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt,
+                         int32_t* best_idx, int32_t* best_d, int32_t* second_d);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,5 @@
+"""MI355X-native ORB-SLAM2 hot path: ORBextractor / ORBmatcher /
+Optimizer::LocalBundleAdjustment over hand-written gfx950 HIP kernels.
+Import as `orb_slam2_amd` (see pkgload.py)."""
+from . import _abi  # noqa: F401
+from .extractor import ORBextractor  # noqa: F401

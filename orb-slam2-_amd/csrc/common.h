@@ -1,0 +1,60 @@
+// Shared host/device helpers for liborbslam2_amd (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+
+#include "../../include/orbslam2_amd.h"
+
+#define ORB_HIP_TRY(expr)                                                                   \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess) {                                                             \
+            std::fprintf(stderr, "[orbslam2_amd] %s failed: %s (%s:%d)\n", #expr,           \
+                         hipGetErrorString(e_), __FILE__, __LINE__);                        \
+            return ORB_EGPU;                                                                \
+        }                                                                                   \
+    } while (0)
+
+namespace orbamd {
+
+constexpr int kMaxLevels = 16;
+constexpr int kWave = 64;
+
+// Returns ORB_OK when a gfx950 device `dev` is usable, else ORB_ENODEV.
+int check_device(int dev);
+
+// 8-bit row pitch used for every device image (multiple of 64 bytes).
+inline int pitch_of(int w) { return (w + 63) & ~63; }
+
+__device__ __forceinline__ int wave_lane() { return threadIdx.x & 63; }
+
+// Inclusive wave64 scan of a 64-bit value.
+__device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint64_t t = __shfl_up(v, d, 64);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ int wave_incl_scan_i32(int v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        int t = __shfl_up(v, d, 64);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ int wave_reduce_sum_i32(int v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+}  // namespace orbamd

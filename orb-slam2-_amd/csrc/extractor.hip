@@ -1,0 +1,1481 @@
+// MI355X-native ORB extractor: ORBextractor::operator() (R/src/ORBextractor.cpp:1120-1188)
+// as six gfx950 kernels over a batch of frames:
+//   k_resize      A2  pyramid level l from level l-1 (INTER_LINEAR 8U fixed point)
+//   k_fast_score  A3  per-pixel FAST-9/16 corner score S (threshold independent)
+//   k_cell_detect A3  per-cell threshold choice (iniThFAST, retry minThFAST), cell-local NMS,
+//                     raster-order compaction  (R/src/ORBextractor.cpp:851-896)
+//   k_octree      A4  DistributeOctTree, phase-parallel emulation of the std::list algorithm
+//                     (R/src/ORBextractor.cpp:571-817), one workgroup per (frame, level)
+//   k_blur        A6  GaussianBlur 7x7 sigma 2 REFLECT_101 (8-bit fixed point)
+//   k_orient_desc A5+A7+A8  IC_Angle, steered BRIEF, output assembly, one wave per keypoint
+// R/ = /root/reference/ORB-SLAM2注释版/.  All arithmetic follows the oracle's pinned
+// semantics (oracle/orb_oracle.c); this file is compiled with -ffp-contract=off.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "common.h"
+
+namespace orbamd {
+
+constexpr int kEdge = 19;          // EDGE_THRESHOLD
+constexpr int kMinBorder = kEdge - 3;
+constexpr int kPatch = 31;
+constexpr int kHalfPatch = 15;
+
+__constant__ int8_t c_pattern[256 * 4] = {
+#include "orb_pattern.inc"
+};
+
+struct LevelGeom {
+    int w, h, pitch;
+    long long off;        // byte offset of this level in a frame's pyramid slab
+    int nCols, nRows, wCell, hCell;
+    int maxBX, maxBY;     // maxBorderX / maxBorderY (minBorder = 16)
+    int cellBase;         // first cell of this level in the frame's cell array
+    int slotBase;         // first FAST key slot of this level in the frame's slot array
+    int cellCap;          // key slots per cell
+    int N;                // DistributeOctTree quota (mnFeaturesPerLevel)
+    int nIni;
+    float hX;
+    int nodeCap;          // node-table capacity == max keypoints out of this level
+    int outBase;          // first retained-key slot of this level (per frame)
+    float scale;          // mvScaleFactor[level]
+    float size;           // (float)(int)(PATCH_SIZE * scale)
+    double rsx, rsy;      // 1/((double)dst/src) for the resize producing this level
+    int tileBase, tilesX; // 64x16 tiles (score / blur kernels)
+};
+
+struct Geom {
+    int nlevels;
+    int w, h;
+    long long frameBytes;
+    int cellsPerFrame, slotsPerFrame, outPerFrame, tilesPerFrame, maxNodeCap;
+    int iniTh, minTh, tmin;
+    float factorPI;
+    int umax[16];
+    LevelGeom lv[kMaxLevels];
+};
+
+// ------------------------------------------------------------------ host geometry
+
+static void host_tables(const orb_extractor_params& p, float* scale, float* inv_scale, float* sigma2,
+                        float* inv_sigma2, int* fpl) {
+    const int n = p.nlevels;
+    const double sf = (double)p.scaleFactor;     // `double scaleFactor` member
+    float s[kMaxLevels], s2[kMaxLevels];
+    s[0] = 1.0f;
+    s2[0] = 1.0f;
+    for (int i = 1; i < n; i++) {
+        s[i] = (float)((double)s[i - 1] * sf);
+        s2[i] = s[i] * s[i];
+    }
+    for (int i = 0; i < n; i++) {
+        if (scale) scale[i] = s[i];
+        if (sigma2) sigma2[i] = s2[i];
+        if (inv_scale) inv_scale[i] = 1.0f / s[i];
+        if (inv_sigma2) inv_sigma2[i] = 1.0f / s2[i];
+    }
+    if (fpl) {
+        float factor = (float)(1.0 / sf);
+        float nDesired = (float)p.nfeatures * (1.0f - factor) / (1.0f - (float)std::pow((double)factor, (double)n));
+        int sum = 0;
+        for (int l = 0; l < n - 1; l++) {
+            fpl[l] = (int)std::nearbyint(nDesired);
+            sum += fpl[l];
+            nDesired *= factor;
+        }
+        fpl[n - 1] = std::max(p.nfeatures - sum, 0);
+    }
+}
+
+static void host_umax(int* umax) {
+    int v, v0;
+    int vmax = (int)std::floor((float)kHalfPatch * std::sqrt(2.f) / 2 + 1);
+    int vmin = (int)std::ceil((float)kHalfPatch * std::sqrt(2.f) / 2);
+    const double hp2 = kHalfPatch * kHalfPatch;
+    for (v = 0; v <= vmax; ++v) umax[v] = (int)std::nearbyint(std::sqrt(hp2 - v * v));
+    for (v = kHalfPatch, v0 = 0; v >= vmin; --v) {
+        while (umax[v0] == umax[v0 + 1]) ++v0;
+        umax[v] = v0;
+        ++v0;
+    }
+}
+
+static int build_geom(const orb_extractor_params& p, int w, int h, Geom* g) {
+    if (p.nlevels < 1 || p.nlevels > kMaxLevels) return ORB_EINVAL;
+    std::memset(g, 0, sizeof(*g));
+    g->nlevels = p.nlevels;
+    g->w = w;
+    g->h = h;
+    float scale[kMaxLevels], inv[kMaxLevels];
+    int fpl[kMaxLevels];
+    host_tables(p, scale, inv, nullptr, nullptr, fpl);
+    host_umax(g->umax);
+    g->iniTh = std::min(std::max(p.iniThFAST, 0), 255);
+    g->minTh = std::min(std::max(p.minThFAST, 0), 255);
+    g->tmin = std::min(g->iniTh, g->minTh);
+    g->factorPI = (float)(3.14159265358979323846 / 180.f);
+    long long off = 0;
+    int cells = 0, slots = 0, outs = 0, tiles = 0, maxNC = 0;
+    for (int l = 0; l < p.nlevels; l++) {
+        LevelGeom& L = g->lv[l];
+        L.w = (int)std::nearbyint((float)w * inv[l]);
+        L.h = (int)std::nearbyint((float)h * inv[l]);
+        if (L.w < 2 * kEdge + 8 || L.h < 2 * kEdge + 8) return ORB_EINVAL;
+        if (L.w - 2 * kMinBorder >= 4096 || L.h - 2 * kMinBorder >= 4096) return ORB_EINVAL;
+        L.pitch = pitch_of(L.w);
+        L.off = off;
+        off += (long long)L.pitch * (L.h + 1);   // +1 row of slack for 4-byte tails
+        L.maxBX = L.w - kEdge + 3;
+        L.maxBY = L.h - kEdge + 3;
+        const float width = (float)(L.maxBX - kMinBorder);
+        const float height = (float)(L.maxBY - kMinBorder);
+        L.nCols = (int)(width / 30.f);
+        L.nRows = (int)(height / 30.f);
+        if (L.nCols < 1 || L.nRows < 1) return ORB_EINVAL;
+        L.wCell = (int)std::ceil(width / (float)L.nCols);
+        L.hCell = (int)std::ceil(height / (float)L.nRows);
+        L.cellBase = cells;
+        cells += L.nCols * L.nRows;
+        L.cellCap = ((L.wCell + 1) / 2) * ((L.hCell + 1) / 2) + 1;
+        L.slotBase = slots;
+        slots += L.nCols * L.nRows * L.cellCap;
+        L.N = fpl[l];
+        L.nIni = (int)std::round((float)(L.maxBX - kMinBorder) / (float)(L.maxBY - kMinBorder));
+        if (L.nIni < 1) return ORB_EINVAL;
+        L.hX = (float)(L.maxBX - kMinBorder) / (float)L.nIni;
+        L.nodeCap = std::max(L.N, 4 * L.nIni) + 8;
+        maxNC = std::max(maxNC, L.nodeCap);
+        L.outBase = outs;
+        outs += L.nodeCap;
+        L.scale = scale[l];
+        L.size = (float)(int)((float)kPatch * scale[l]);
+        if (l > 0) {
+            const LevelGeom& S = g->lv[l - 1];
+            L.rsx = 1. / ((double)L.w / S.w);
+            L.rsy = 1. / ((double)L.h / S.h);
+        }
+        L.tilesX = (L.w + 63) / 64;
+        L.tileBase = tiles;
+        tiles += L.tilesX * ((L.h + 15) / 16);
+    }
+    g->frameBytes = (off + 255) & ~255LL;
+    g->cellsPerFrame = cells;
+    g->slotsPerFrame = slots;
+    g->outPerFrame = outs;
+    g->tilesPerFrame = tiles;
+    g->maxNodeCap = maxNC;
+    return ORB_OK;
+}
+
+// ------------------------------------------------------------------ device helpers
+
+__device__ __forceinline__ int level_of_tile(const Geom& g, int tile) {
+    int l = 0;
+    while (l + 1 < g.nlevels && tile >= g.lv[l + 1].tileBase) l++;
+    return l;
+}
+__device__ __forceinline__ int level_of_cell(const Geom& g, int c) {
+    int l = 0;
+    while (l + 1 < g.nlevels && c >= g.lv[l + 1].cellBase) l++;
+    return l;
+}
+__device__ __forceinline__ int reflect101(int i, int n) {
+    while (i < 0 || i >= n) {
+        if (i < 0) i = -i;
+        if (i >= n) i = 2 * n - 2 - i;
+    }
+    return i;
+}
+
+// ------------------------------------------------------------------ A2: resize
+
+__global__ __launch_bounds__(256) void k_resize(Geom g, int l, uint8_t* __restrict__ pyr) {
+    const LevelGeom& D = g.lv[l];
+    const LevelGeom& S = g.lv[l - 1];
+    const int b = blockIdx.z;
+    const int dy = blockIdx.y * 4 + threadIdx.y;
+    const int dx0 = (blockIdx.x * 64 + threadIdx.x) * 4;
+    if (dy >= D.h || dx0 >= D.w) return;
+    const uint8_t* src = pyr + (size_t)b * g.frameBytes + S.off;
+    uint8_t* dst = pyr + (size_t)b * g.frameBytes + D.off;
+    float fy = (float)(((double)dy + 0.5) * D.rsy - 0.5);
+    int sy = (int)floorf(fy);
+    fy -= (float)sy;
+    const int b0 = __float2int_rn((1.f - fy) * 2048.f), b1 = __float2int_rn(fy * 2048.f);
+    const int y0 = min(max(sy, 0), S.h - 1), y1 = min(max(sy + 1, 0), S.h - 1);
+    const uint8_t* S0 = src + (size_t)y0 * S.pitch;
+    const uint8_t* S1 = src + (size_t)y1 * S.pitch;
+    uint32_t packed = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int dx = dx0 + k;
+        if (dx < D.w) {
+            float fx = (float)(((double)dx + 0.5) * D.rsx - 0.5);
+            int sx = (int)floorf(fx);
+            fx -= (float)sx;
+            if (sx < 0) { fx = 0.f; sx = 0; }
+            if (sx >= S.w - 1) { fx = 0.f; sx = S.w - 1; }
+            const int a0 = __float2int_rn((1.f - fx) * 2048.f), a1 = __float2int_rn(fx * 2048.f);
+            const int sx1 = min(sx + 1, S.w - 1);
+            const int r0 = S0[sx] * a0 + S0[sx1] * a1;
+            const int r1 = S1[sx] * a0 + S1[sx1] * a1;
+            int v = (r0 * b0 + r1 * b1 + (1 << 21)) >> 22;
+            v = min(max(v, 0), 255);
+            packed |= (uint32_t)v << (8 * k);
+        }
+    }
+    *reinterpret_cast<uint32_t*>(dst + (size_t)dy * D.pitch + dx0) = packed;
+}
+
+// ------------------------------------------------------------------ A3: FAST score
+
+// S = max over the 16 circular 9-arcs of min(v - p) (dark) or min(p - v) (bright), minus 1.
+// OpenCV's cornerScore<16>(threshold t) == S for every pixel that is a corner at t, and a
+// pixel is a corner at t iff S >= t.  Stored as S if S >= tmin else 0.
+__device__ __forceinline__ int fast_score(const int v, const int p[16]) {
+    int d[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) d[k] = v - p[k];
+    int m2[16], M2[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        m2[k] = min(d[k], d[(k + 1) & 15]);
+        M2[k] = max(d[k], d[(k + 1) & 15]);
+    }
+    int m4[16], M4[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        m4[k] = min(m2[k], m2[(k + 2) & 15]);
+        M4[k] = max(M2[k], M2[(k + 2) & 15]);
+    }
+    int A = -1024, Bp = 1024;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int m8 = min(m4[k], m4[(k + 4) & 15]);
+        const int M8 = max(M4[k], M4[(k + 4) & 15]);
+        A = max(A, min(m8, d[(k + 8) & 15]));
+        Bp = min(Bp, max(M8, d[(k + 8) & 15]));
+    }
+    return max(A, -Bp) - 1;
+}
+
+constexpr int kTileW = 64, kTileH = 16, kHalo = 3;
+constexpr int kLdsW = kTileW + 2 * kHalo, kLdsH = kTileH + 2 * kHalo;
+
+__global__ __launch_bounds__(256) void k_fast_score(Geom g, const uint8_t* __restrict__ pyr,
+                                                    uint8_t* __restrict__ score) {
+    __shared__ uint8_t tile[kLdsH][kLdsW + 2];
+    const int b = blockIdx.y;
+    const int l = level_of_tile(g, blockIdx.x);
+    const LevelGeom& L = g.lv[l];
+    const int t = blockIdx.x - L.tileBase;
+    const int tx0 = (t % L.tilesX) * kTileW, ty0 = (t / L.tilesX) * kTileH;
+    const uint8_t* img = pyr + (size_t)b * g.frameBytes + L.off;
+    uint8_t* out = score + (size_t)b * g.frameBytes + L.off;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < kLdsH * kLdsW; i += 256) {
+        const int r = i / kLdsW, c = i % kLdsW;
+        const int y = min(max(ty0 - kHalo + r, 0), L.h - 1);
+        const int x = min(max(tx0 - kHalo + c, 0), L.w - 1);
+        tile[r][c] = img[(size_t)y * L.pitch + x];
+    }
+    __syncthreads();
+    const int ly = tid / 16, lx0 = (tid % 16) * 4;
+    const int y = ty0 + ly;
+    if (y >= L.h) return;
+    uint32_t packed = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int x = tx0 + lx0 + k;
+        int s = 0;
+        if (x >= 3 && x <= L.w - 4 && y >= 3 && y <= L.h - 4) {
+            const int cy = ly + kHalo, cx = lx0 + k + kHalo;
+            int p[16];
+            p[0] = tile[cy + 3][cx + 0];  p[1] = tile[cy + 3][cx + 1];
+            p[2] = tile[cy + 2][cx + 2];  p[3] = tile[cy + 1][cx + 3];
+            p[4] = tile[cy + 0][cx + 3];  p[5] = tile[cy - 1][cx + 3];
+            p[6] = tile[cy - 2][cx + 2];  p[7] = tile[cy - 3][cx + 1];
+            p[8] = tile[cy - 3][cx + 0];  p[9] = tile[cy - 3][cx - 1];
+            p[10] = tile[cy - 2][cx - 2]; p[11] = tile[cy - 1][cx - 3];
+            p[12] = tile[cy + 0][cx - 3]; p[13] = tile[cy + 1][cx - 3];
+            p[14] = tile[cy + 2][cx - 2]; p[15] = tile[cy + 3][cx - 1];
+            const int S = fast_score(tile[cy][cx], p);
+            s = (S >= g.tmin && S > 0) ? S : 0;
+        }
+        packed |= (uint32_t)s << (8 * k);
+    }
+    if (tx0 + lx0 < L.pitch) *reinterpret_cast<uint32_t*>(out + (size_t)y * L.pitch + tx0 + lx0) = packed;
+}
+
+// ------------------------------------------------------------------ A3: per-cell detect
+
+constexpr int kCellMax = 64;   // max region side handled in LDS (wCell, hCell <= 60 by construction)
+
+__device__ __forceinline__ bool nms_keep(const uint8_t* reg, int rw, int rh, int x, int y, int t) {
+    const int m = reg[y * rw + x];
+    if (m < t) return false;
+#pragma unroll
+    for (int dy = -1; dy <= 1; dy++) {
+#pragma unroll
+        for (int dx = -1; dx <= 1; dx++) {
+            if (dx == 0 && dy == 0) continue;
+            const int xx = x + dx, yy = y + dy;
+            int nv = 0;
+            if (xx >= 0 && xx < rw && yy >= 0 && yy < rh) {
+                nv = reg[yy * rw + xx];
+                if (nv < t) nv = 0;
+            }
+            if (m <= nv) return false;
+        }
+    }
+    return true;
+}
+
+__global__ __launch_bounds__(256) void k_cell_detect(Geom g, const uint8_t* __restrict__ score,
+                                                     uint32_t* __restrict__ slots, int* __restrict__ cellCount,
+                                                     int* __restrict__ status) {
+    __shared__ uint8_t reg_all[4][kCellMax * kCellMax];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int b = blockIdx.y;
+    const int c = blockIdx.x * 4 + wid;
+    if (c >= g.cellsPerFrame) return;
+    const int l = level_of_cell(g, c);
+    const LevelGeom& L = g.lv[l];
+    const int ci = c - L.cellBase;
+    const int i = ci / L.nCols, j = ci % L.nCols;
+    int* cnt_out = cellCount + (size_t)b * g.cellsPerFrame + c;
+    const int iniY = kMinBorder + i * L.hCell;
+    int maxY = iniY + L.hCell + 6;
+    const int iniX = kMinBorder + j * L.wCell;
+    int maxX = iniX + L.wCell + 6;
+    if (iniY >= L.maxBY - 3 || iniX >= L.maxBX - 6) {
+        if (lane == 0) *cnt_out = 0;
+        return;
+    }
+    if (maxY > L.maxBY) maxY = L.maxBY;
+    if (maxX > L.maxBX) maxX = L.maxBX;
+    const int rw = maxX - iniX - 6, rh = maxY - iniY - 6;   // detection region
+    if (rw <= 0 || rh <= 0) {
+        if (lane == 0) *cnt_out = 0;
+        return;
+    }
+    if (rw > kCellMax || rh > kCellMax) {
+        if (lane == 0) { *cnt_out = 0; atomicOr(status, 1); }
+        return;
+    }
+    uint8_t* reg = reg_all[wid];
+    const uint8_t* sm = score + (size_t)b * g.frameBytes + L.off;
+    const int rx0 = iniX + 3, ry0 = iniY + 3;
+    for (int p = lane; p < rw * rh; p += 64) {
+        const int y = p / rw, x = p % rw;
+        reg[p] = sm[(size_t)(ry0 + y) * L.pitch + rx0 + x];
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    int n20 = 0;
+    for (int p0 = 0; p0 < rw * rh; p0 += 64) {
+        const int p = p0 + lane;
+        bool k = false;
+        if (p < rw * rh) k = nms_keep(reg, rw, rh, p % rw, p / rw, g.iniTh);
+        n20 += __popcll(__ballot(k));
+    }
+    const int t = n20 > 0 ? g.iniTh : g.minTh;
+    uint32_t* out = slots + (size_t)b * g.slotsPerFrame + L.slotBase + (size_t)ci * L.cellCap;
+    int n = 0;
+    for (int p0 = 0; p0 < rw * rh; p0 += 64) {
+        const int p = p0 + lane;
+        bool k = false;
+        int x = 0, y = 0, m = 0;
+        if (p < rw * rh) {
+            x = p % rw;
+            y = p / rw;
+            k = nms_keep(reg, rw, rh, x, y, t);
+            m = reg[p];
+        }
+        const uint64_t mask = __ballot(k);
+        const int before = __popcll(mask & ((1ull << lane) - 1ull));
+        if (k && n + before < L.cellCap) {
+            // DistributeOctTree coordinates: absolute - minBorder (R/src/ORBextractor.cpp:889-890)
+            const uint32_t kx = (uint32_t)(rx0 + x - kMinBorder), ky = (uint32_t)(ry0 + y - kMinBorder);
+            out[n + before] = kx | (ky << 12) | ((uint32_t)m << 24);
+        }
+        n += __popcll(mask);
+    }
+    if (lane == 0) {
+        if (n > L.cellCap) { atomicOr(status, 2); n = L.cellCap; }
+        *cnt_out = n;
+    }
+}
+
+// ------------------------------------------------------------------ A4: octree
+
+constexpr int OT_T = 256;
+constexpr int OT_V = 8;
+constexpr int OT_TILE = OT_T * OT_V;
+
+__device__ __forceinline__ int kx_of(uint32_t k) { return (int)(k & 0xFFFu); }
+__device__ __forceinline__ int ky_of(uint32_t k) { return (int)((k >> 12) & 0xFFFu); }
+__device__ __forceinline__ int kr_of(uint32_t k) { return (int)(k >> 24); }
+
+struct NodeTab {     // one table set in LDS (SoA)
+    int* start;      // [cap+1]
+    int* cnt;
+    uint32_t* b0;    // x0 | y0 << 16
+    uint32_t* b1;    // x1 | y1 << 16
+    int* seq;
+    int* flag;       // bit0 nomore, bit1 candidate
+};
+
+// Block-wide exclusive scan of an int array in LDS (length m), in place; returns the total.
+__device__ int block_scan_lds(int* a, int m, int* wsum) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int chunk = (m + OT_T - 1) / OT_T;
+    const int s0 = min(tid * chunk, m), s1 = min(s0 + chunk, m);
+    int local = 0;
+    for (int i = s0; i < s1; i++) local += a[i];
+    int incl = wave_incl_scan_i32(local);
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    int wofs = 0, total = 0;
+    for (int w = 0; w < OT_T / 64; w++) {
+        if (w < wid) wofs += wsum[w];
+        total += wsum[w];
+    }
+    int run = wofs + incl - local;
+    for (int i = s0; i < s1; i++) {
+        const int v = a[i];
+        a[i] = run;
+        run += v;
+    }
+    __syncthreads();
+    return total;
+}
+
+// Splits the node rectangle like ExtractorNode::DivideNode (R/src/ORBextractor.cpp:515-541).
+__device__ __forceinline__ void node_split(uint32_t b0, uint32_t b1, int& mx, int& my) {
+    const int x0 = (int)(b0 & 0xFFFF), y0 = (int)(b0 >> 16);
+    const int x1 = (int)(b1 & 0xFFFF), y1 = (int)(b1 >> 16);
+    const int halfX = (int)ceilf((float)(x1 - x0) / 2);
+    const int halfY = (int)ceilf((float)(y1 - y0) / 2);
+    mx = x0 + halfX;
+    my = y0 + halfY;
+}
+__device__ __forceinline__ void child_bounds(uint32_t b0, uint32_t b1, int q, uint32_t& c0, uint32_t& c1) {
+    const int x0 = (int)(b0 & 0xFFFF), y0 = (int)(b0 >> 16);
+    const int x1 = (int)(b1 & 0xFFFF), y1 = (int)(b1 >> 16);
+    int mx, my;
+    node_split(b0, b1, mx, my);
+    const int cx0 = (q & 1) ? mx : x0, cx1 = (q & 1) ? x1 : mx;
+    const int cy0 = (q & 2) ? my : y0, cy1 = (q & 2) ? y1 : my;
+    c0 = (uint32_t)cx0 | ((uint32_t)cy0 << 16);
+    c1 = (uint32_t)cx1 | ((uint32_t)cy1 << 16);
+}
+// quadrant of a key: n1=0 (x<mx,y<my), n2=1 (x>=mx,y<my), n3=2 (x<mx,y>=my), n4=3
+__device__ __forceinline__ int key_quadrant(uint32_t key, int mx, int my) {
+    return (kx_of(key) < mx ? 0 : 1) | (ky_of(key) < my ? 0 : 2);
+}
+
+__device__ __forceinline__ int node_of(const int* start, int m, int k) {
+    int lo = 0, hi = m - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (start[mid] <= k) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+// Packed 4 x 16-bit counters (quadrant histograms) for an intra-tile scan.
+__device__ __forceinline__ uint64_t qbit(int q) { return 1ull << (16 * q); }
+__device__ __forceinline__ int qfield(uint64_t v, int q) { return (int)((v >> (16 * q)) & 0xFFFFull); }
+
+// One tile pass of the segmented quadrant scan: returns this thread's exclusive prefix
+// (packed, tile-local) of its first key; fills tile total into *tot (all threads).
+__device__ __forceinline__ uint64_t tile_scan(uint64_t local, uint64_t* wtot, uint64_t& total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint64_t incl = wave_incl_scan_u64(local);
+    if (lane == 63) wtot[wid] = incl;
+    __syncthreads();
+    uint64_t wofs = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < OT_T / 64; w++) {
+        const uint64_t v = wtot[w];
+        if (w < wid) wofs += v;
+        tot += v;
+    }
+    total = tot;
+    __syncthreads();
+    return wofs + incl - local;
+}
+
+struct OctScratch {
+    uint4* P0;      // [cap+1] prefix of active-key quadrant counts at node starts
+    int* ne;        // nonempty children of a processed node
+    int* push;      // push base of a processed node
+    int* newpos;    // new list position of an unprocessed node
+    int* rank;      // processing rank
+    int* order;     // node at rank
+    int* proc;      // processed flag
+    int* tmp;       // scan scratch
+};
+
+__global__ __launch_bounds__(OT_T) void k_octree(Geom g, const uint32_t* __restrict__ slots,
+                                                 const int* __restrict__ cellCount, uint32_t* __restrict__ keyA,
+                                                 uint32_t* __restrict__ keyB, uint32_t* __restrict__ outKeys,
+                                                 int* __restrict__ levelCount, int* __restrict__ status) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int l = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+    const LevelGeom& L = g.lv[l];
+    const int cap = g.maxNodeCap;
+    // carve LDS
+    unsigned char* p = smem;
+    auto carve = [&](size_t bytes) { unsigned char* r = p; p += (bytes + 15) & ~(size_t)15; return r; };
+    OctScratch S;
+    S.P0 = (uint4*)carve(sizeof(uint4) * (cap + 1));
+    NodeTab T[2];
+    for (int s = 0; s < 2; s++) {
+        T[s].start = (int*)carve(sizeof(int) * (cap + 1));
+        T[s].cnt = (int*)carve(sizeof(int) * cap);
+        T[s].b0 = (uint32_t*)carve(sizeof(uint32_t) * cap);
+        T[s].b1 = (uint32_t*)carve(sizeof(uint32_t) * cap);
+        T[s].seq = (int*)carve(sizeof(int) * cap);
+        T[s].flag = (int*)carve(sizeof(int) * cap);
+    }
+    S.ne = (int*)carve(sizeof(int) * cap);
+    S.push = (int*)carve(sizeof(int) * cap);
+    S.newpos = (int*)carve(sizeof(int) * cap);
+    S.rank = (int*)carve(sizeof(int) * cap);
+    S.order = (int*)carve(sizeof(int) * cap);
+    S.proc = (int*)carve(sizeof(int) * cap);
+    S.tmp = (int*)carve(sizeof(int) * (cap + 1));
+    int* cellOff = (int*)carve(sizeof(int) * (L.nCols * L.nRows + 1 + 64));
+    uint64_t* wtot = (uint64_t*)carve(sizeof(uint64_t) * 8);
+    int* wsum = (int*)carve(sizeof(int) * 8);
+    int* sc = (int*)carve(sizeof(int) * 32);    // uniform scalars
+    uint4* carry_s = (uint4*)carve(sizeof(uint4));
+
+    const size_t kbase = (size_t)b * g.slotsPerFrame + L.slotBase;
+    uint32_t* kA = keyA + kbase;
+    uint32_t* kB = keyB + kbase;
+    const int ncell = L.nCols * L.nRows;
+
+    // ---- gather cell lists into a contiguous key array (cell order i-major, j-minor)
+    for (int c = tid; c < ncell; c += OT_T) cellOff[c] = cellCount[(size_t)b * g.cellsPerFrame + L.cellBase + c];
+    __syncthreads();
+    const int n = block_scan_lds(cellOff, ncell, wsum);
+    if (tid == 0) cellOff[ncell] = n;
+    __syncthreads();
+    {
+        const uint32_t* src = slots + kbase;
+        for (int c = tid >> 6; c < ncell; c += OT_T / 64) {
+            const int o = cellOff[c], cn = cellOff[c + 1] - o;
+            for (int q = tid & 63; q < cn; q += 64) kA[o + q] = src[(size_t)c * L.cellCap + q];
+        }
+    }
+    __syncthreads();
+    int* outCount = levelCount + (size_t)b * g.nlevels + l;
+    uint32_t* outK = outKeys + (size_t)b * g.outPerFrame + L.outBase;
+    if (n == 0) {
+        if (tid == 0) *outCount = 0;
+        return;
+    }
+
+    // ---- initial nodes (R/src/ORBextractor.cpp:577-627): stable partition by x / hX
+    const int nIni = L.nIni;
+    const float hX = L.hX;
+    const int H = L.maxBY - kMinBorder;
+    if (tid == 0) sc[0] = 0;
+    __syncthreads();
+    {
+        int base = 0;
+        for (int part = 0; part < nIni; part++) {
+            int partCount = 0;
+            for (int t0 = 0; t0 < n; t0 += OT_TILE) {
+                const int k0 = t0 + tid * OT_V;
+                int local = 0;
+                uint32_t kk[OT_V];
+#pragma unroll
+                for (int v = 0; v < OT_V; v++) {
+                    const int k = k0 + v;
+                    kk[v] = k < n ? kA[k] : 0u;
+                    if (k < n && (int)((float)kx_of(kk[v]) / hX) == part) local++;
+                }
+                uint64_t tot;
+                int run = base + partCount + (int)tile_scan((uint64_t)local, wtot, tot);
+#pragma unroll
+                for (int v = 0; v < OT_V; v++) {
+                    const int k = k0 + v;
+                    if (k < n && (int)((float)kx_of(kk[v]) / hX) == part) kB[run++] = kk[v];
+                }
+                partCount += (int)tot;
+            }
+            // nodes are pushed back in part order; empty initial nodes are erased
+            if (partCount > 0 && tid == 0) {
+                const int idx = sc[0];
+                T[0].start[idx] = base;
+                T[0].cnt[idx] = partCount;
+                const int x0 = (int)(hX * (float)part), x1 = (int)(hX * (float)(part + 1));
+                T[0].b0[idx] = (uint32_t)x0;
+                T[0].b1[idx] = (uint32_t)x1 | ((uint32_t)H << 16);
+                T[0].seq[idx] = idx;
+                T[0].flag[idx] = partCount == 1 ? 1 : 0;
+                sc[0] = idx + 1;
+            }
+            base += partCount;
+            __syncthreads();
+        }
+    }
+    int m = sc[0];  // list size (uniform)
+    __syncthreads();
+    {   // keys now live in kB
+        uint32_t* t = kA; kA = kB; kB = t;
+    }
+    int cur = 0;            // table holding the current list
+    int phase = 0;          // 0 = outer pass, 1 = inner (size-ordered) pass
+    int nIter = 0;
+    while (true) {
+        if (++nIter > 4096) { if (tid == 0) atomicOr(status, 4); break; }
+        NodeTab& O = T[cur];
+        NodeTab& Nw = T[cur ^ 1];
+        const int prevSize = m;
+        // active flags: outer -> every node with >1 keys (== !bNoMore); inner -> candidates
+        // Pass B: quadrant prefix at node starts
+        if (tid == 0) *carry_s = make_uint4(0, 0, 0, 0);
+        __syncthreads();
+        for (int t0 = 0; t0 < n; t0 += OT_TILE) {
+            const int k0 = t0 + tid * OT_V;
+            uint64_t local = 0;
+            int qv[OT_V];
+            int nd = k0 < n ? node_of(O.start, m, k0) : 0;
+            int ndv[OT_V];
+#pragma unroll
+            for (int v = 0; v < OT_V; v++) {
+                const int k = k0 + v;
+                qv[v] = -1;
+                ndv[v] = nd;
+                if (k < n) {
+                    while (nd + 1 < m && O.start[nd + 1] <= k) nd++;
+                    ndv[v] = nd;
+                    const bool act = phase == 0 ? (O.cnt[nd] > 1) : ((O.flag[nd] & 2) != 0);
+                    if (act) {
+                        int mx, my;
+                        node_split(O.b0[nd], O.b1[nd], mx, my);
+                        qv[v] = key_quadrant(kA[k], mx, my);
+                        local += qbit(qv[v]);
+                    }
+                }
+            }
+            uint64_t tot;
+            const uint64_t ex = tile_scan(local, wtot, tot);
+            const uint4 carry = *carry_s;
+            uint4 R = make_uint4(carry.x + qfield(ex, 0), carry.y + qfield(ex, 1), carry.z + qfield(ex, 2),
+                                 carry.w + qfield(ex, 3));
+#pragma unroll
+            for (int v = 0; v < OT_V; v++) {
+                const int k = k0 + v;
+                if (k < n) {
+                    if (O.start[ndv[v]] == k) S.P0[ndv[v]] = R;
+                    if (qv[v] == 0) R.x++;
+                    else if (qv[v] == 1) R.y++;
+                    else if (qv[v] == 2) R.z++;
+                    else if (qv[v] == 3) R.w++;
+                }
+            }
+            __syncthreads();
+            if (tid == 0) {
+                uint4 c2 = carry;
+                c2.x += qfield(tot, 0); c2.y += qfield(tot, 1); c2.z += qfield(tot, 2); c2.w += qfield(tot, 3);
+                *carry_s = c2;
+            }
+            __syncthreads();
+        }
+        if (tid == 0) S.P0[m] = *carry_s;
+        __syncthreads();
+        // node level: child counts, ne, active
+        for (int i = tid; i < m; i += OT_T) {
+            const bool act = phase == 0 ? (O.cnt[i] > 1) : ((O.flag[i] & 2) != 0);
+            int ne = 0;
+            if (act) {
+                const uint4 a = S.P0[i], c = S.P0[i + 1];
+                ne = (c.x != a.x) + (c.y != a.y) + (c.z != a.z) + (c.w != a.w);
+            }
+            S.ne[i] = act ? ne : -1;
+        }
+        __syncthreads();
+        // processing order + push bases
+        if (phase == 0) {
+            for (int i = tid; i < m; i += OT_T) S.tmp[i] = S.ne[i] > 0 ? S.ne[i] : 0;
+            __syncthreads();
+            const int C = block_scan_lds(S.tmp, m, wsum);
+            for (int i = tid; i < m; i += OT_T) {
+                S.push[i] = S.tmp[i];
+                S.proc[i] = S.ne[i] >= 0 ? 1 : 0;
+            }
+            if (tid == 0) sc[1] = C;
+            __syncthreads();
+        } else {
+            // rank = number of candidates ordered after (count, seq) descending
+            for (int i = tid; i < m; i += OT_T) {
+                if (S.ne[i] < 0) { S.rank[i] = -1; continue; }
+                const int ci = O.cnt[i], si = O.seq[i];
+                int r = 0;
+                for (int j2 = 0; j2 < m; j2++) {
+                    if (S.ne[j2] < 0) continue;
+                    const int cj = O.cnt[j2], sj = O.seq[j2];
+                    if (cj > ci || (cj == ci && sj > si)) r++;
+                }
+                S.rank[i] = r;
+                S.order[r] = i;
+            }
+            if (tid == 0) sc[2] = 0;
+            __syncthreads();
+            for (int i = tid; i < m; i += OT_T) if (S.ne[i] >= 0) atomicAdd(&sc[2], 1);
+            __syncthreads();
+            const int nc = sc[2];
+            for (int r = tid; r < nc; r += OT_T) S.tmp[r] = S.ne[S.order[r]];
+            __syncthreads();
+            block_scan_lds(S.tmp, nc, wsum);
+            if (tid == 0) sc[3] = 0x7fffffff;
+            __syncthreads();
+            for (int r = tid; r < nc; r += OT_T) {
+                const int i = S.order[r];
+                S.push[i] = S.tmp[r];
+                const int inclNe = S.tmp[r] + S.ne[i];
+                if (prevSize + inclNe - (r + 1) >= L.N) atomicMin(&sc[3], r);
+            }
+            __syncthreads();
+            const int jstop = sc[3];
+            for (int i = tid; i < m; i += OT_T) S.proc[i] = (S.ne[i] >= 0 && S.rank[i] <= jstop) ? 1 : 0;
+            if (tid == 0) {
+                int C = 0;
+                if (jstop != 0x7fffffff) {
+                    const int i = S.order[jstop];
+                    C = S.push[i] + S.ne[i];
+                } else if (nc > 0) {
+                    const int i = S.order[nc - 1];
+                    C = S.push[i] + S.ne[i];
+                }
+                sc[1] = C;
+            }
+            __syncthreads();
+        }
+        const int C = sc[1];
+        // new positions of unprocessed nodes
+        for (int i = tid; i < m; i += OT_T) S.tmp[i] = S.proc[i] ? 0 : 1;
+        __syncthreads();
+        const int nUnproc = block_scan_lds(S.tmp, m, wsum);
+        const int newM = C + nUnproc;
+        if (newM > cap) {
+            if (tid == 0) atomicOr(status, 8);
+            break;
+        }
+        for (int i = tid; i < m; i += OT_T) S.newpos[i] = S.proc[i] ? -1 : C + S.tmp[i];
+        __syncthreads();
+        // fill the new table
+        if (tid == 0) sc[4] = 0;
+        __syncthreads();
+        for (int i = tid; i < m; i += OT_T) {
+            if (!S.proc[i]) {
+                const int j2 = S.newpos[i];
+                Nw.cnt[j2] = O.cnt[i];
+                Nw.b0[j2] = O.b0[i];
+                Nw.b1[j2] = O.b1[i];
+                Nw.seq[j2] = 0;
+                Nw.flag[j2] = O.cnt[i] == 1 ? 1 : 0;
+            } else {
+                const uint4 a = S.P0[i], c = S.P0[i + 1];
+                const int cc[4] = {(int)(c.x - a.x), (int)(c.y - a.y), (int)(c.z - a.z), (int)(c.w - a.w)};
+                int r = 0;
+                for (int q = 0; q < 4; q++) {
+                    if (cc[q] == 0) continue;
+                    const int push = S.push[i] + r;
+                    const int j2 = C - 1 - push;
+                    uint32_t c0, c1;
+                    child_bounds(O.b0[i], O.b1[i], q, c0, c1);
+                    Nw.cnt[j2] = cc[q];
+                    Nw.b0[j2] = c0;
+                    Nw.b1[j2] = c1;
+                    Nw.seq[j2] = push;
+                    Nw.flag[j2] = cc[q] == 1 ? 1 : 2;
+                    if (cc[q] > 1) atomicAdd(&sc[4], 1);
+                    r++;
+                }
+            }
+        }
+        __syncthreads();
+        const int nToExpand = sc[4];
+        for (int i = tid; i < newM; i += OT_T) Nw.start[i] = Nw.cnt[i];
+        __syncthreads();
+        block_scan_lds(Nw.start, newM, wsum);
+        if (tid == 0) Nw.start[newM] = n;
+        __syncthreads();
+        // Pass C: move keys (stable within every child / unprocessed node)
+        if (tid == 0) *carry_s = make_uint4(0, 0, 0, 0);
+        __syncthreads();
+        for (int t0 = 0; t0 < n; t0 += OT_TILE) {
+            const int k0 = t0 + tid * OT_V;
+            uint64_t local = 0;
+            int qv[OT_V], ndv[OT_V];
+            uint32_t kk[OT_V];
+            int nd = k0 < n ? node_of(O.start, m, k0) : 0;
+#pragma unroll
+            for (int v = 0; v < OT_V; v++) {
+                const int k = k0 + v;
+                qv[v] = -1;
+                ndv[v] = nd;
+                kk[v] = 0;
+                if (k < n) {
+                    while (nd + 1 < m && O.start[nd + 1] <= k) nd++;
+                    ndv[v] = nd;
+                    kk[v] = kA[k];
+                    if (S.ne[nd] >= 0) {
+                        int mx, my;
+                        node_split(O.b0[nd], O.b1[nd], mx, my);
+                        qv[v] = key_quadrant(kk[v], mx, my);
+                        local += qbit(qv[v]);
+                    }
+                }
+            }
+            uint64_t tot;
+            const uint64_t ex = tile_scan(local, wtot, tot);
+            const uint4 carry = *carry_s;
+            uint4 R = make_uint4(carry.x + qfield(ex, 0), carry.y + qfield(ex, 1), carry.z + qfield(ex, 2),
+                                 carry.w + qfield(ex, 3));
+#pragma unroll
+            for (int v = 0; v < OT_V; v++) {
+                const int k = k0 + v;
+                if (k >= n) continue;
+                const int i = ndv[v];
+                const int q = qv[v];
+                if (S.proc[i]) {
+                    const uint4 a = S.P0[i], c = S.P0[i + 1];
+                    const int cc[4] = {(int)(c.x - a.x), (int)(c.y - a.y), (int)(c.z - a.z), (int)(c.w - a.w)};
+                    const unsigned rq = q == 0 ? R.x - a.x : q == 1 ? R.y - a.y : q == 2 ? R.z - a.z : R.w - a.w;
+                    int r = 0;
+                    for (int qq = 0; qq < q; qq++) r += cc[qq] > 0;
+                    const int j2 = C - 1 - (S.push[i] + r);
+                    kB[Nw.start[j2] + (int)rq] = kk[v];
+                } else {
+                    kB[Nw.start[S.newpos[i]] + (k - O.start[i])] = kk[v];
+                }
+                if (q == 0) R.x++;
+                else if (q == 1) R.y++;
+                else if (q == 2) R.z++;
+                else if (q == 3) R.w++;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                uint4 c2 = carry;
+                c2.x += qfield(tot, 0); c2.y += qfield(tot, 1); c2.z += qfield(tot, 2); c2.w += qfield(tot, 3);
+                *carry_s = c2;
+            }
+            __syncthreads();
+        }
+        { uint32_t* t = kA; kA = kB; kB = t; }
+        cur ^= 1;
+        m = newM;
+        // termination logic of R/src/ORBextractor.cpp:722-791
+        if (m >= L.N || m == prevSize) break;
+        if (phase == 0) {
+            if (m + nToExpand * 3 > L.N) phase = 1;
+        }
+        __syncthreads();
+    }
+    __syncthreads();
+    // retain the best point in each node (first max wins, R/src/ORBextractor.cpp:796-814)
+    NodeTab& F = T[cur];
+    for (int i = tid; i < m; i += OT_T) {
+        const int s0 = F.start[i], s1 = s0 + F.cnt[i];
+        uint32_t best = kA[s0];
+        for (int k = s0 + 1; k < s1; k++) {
+            const uint32_t v = kA[k];
+            if (kr_of(v) > kr_of(best)) best = v;
+        }
+        if (i < L.nodeCap) outK[i] = best;
+    }
+    if (tid == 0) {
+        if (m > L.nodeCap) atomicOr(status, 16);
+        *outCount = min(m, L.nodeCap);
+    }
+}
+
+// ------------------------------------------------------------------ A6: blur
+
+// Separable 7-tap integer blur; every LDS access is dword-aligned (the compiler otherwise
+// merges neighbouring byte reads into ds_read_u16 at odd addresses, which mis-read on gfx950).
+constexpr int kRowSumW = kTileW + 4;
+__global__ __launch_bounds__(256) void k_blur(Geom g, const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blurred,
+                                              int k0, int k1, int k2, int k3) {
+    __shared__ __attribute__((aligned(16))) uint32_t tile32[kLdsH][(kLdsW + 2) / 4];
+    __shared__ __attribute__((aligned(16))) int rowsum[kLdsH][kRowSumW];
+    const int b = blockIdx.y;
+    const int l = level_of_tile(g, blockIdx.x);
+    const LevelGeom& L = g.lv[l];
+    const int t = blockIdx.x - L.tileBase;
+    const int tx0 = (t % L.tilesX) * kTileW, ty0 = (t / L.tilesX) * kTileH;
+    const uint8_t* img = pyr + (size_t)b * g.frameBytes + L.off;
+    uint8_t* out = blurred + (size_t)b * g.frameBytes + L.off;
+    const int tid = threadIdx.x;
+    constexpr int kWords = (kLdsW + 2) / 4;   // 18 words = 72 bytes per row
+    for (int i = tid; i < kLdsH * kWords; i += 256) {
+        const int r = i / kWords, wd = i % kWords;
+        const int y = reflect101(ty0 - kHalo + r, L.h);
+        const uint8_t* row = img + (size_t)y * L.pitch;
+        uint32_t v = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int c = wd * 4 + k;
+            const int x = reflect101(tx0 - kHalo + min(c, kLdsW - 1), L.w);
+            v |= (uint32_t)row[x] << (8 * k);
+        }
+        tile32[r][wd] = v;
+    }
+    __syncthreads();
+    const int kk[7] = {k3, k2, k1, k0, k1, k2, k3};
+    for (int i = tid; i < kLdsH * (kTileW / 4); i += 256) {
+        const int r = i / (kTileW / 4), gq = i % (kTileW / 4);
+        const uint32_t w0 = tile32[r][gq], w1 = tile32[r][gq + 1], w2 = tile32[r][gq + 2];
+        int px[12];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            px[k] = (w0 >> (8 * k)) & 0xff;
+            px[4 + k] = (w1 >> (8 * k)) & 0xff;
+            px[8 + k] = (w2 >> (8 * k)) & 0xff;
+        }
+        int4 s4;
+        int sv[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            int s = 0;
+#pragma unroll
+            for (int q = 0; q < 7; q++) s += kk[q] * px[k + q];
+            sv[k] = s;
+        }
+        s4.x = sv[0]; s4.y = sv[1]; s4.z = sv[2]; s4.w = sv[3];
+        *reinterpret_cast<int4*>(&rowsum[r][gq * 4]) = s4;
+    }
+    __syncthreads();
+    const int ly = tid / 16, lx0 = (tid % 16) * 4;
+    const int y = ty0 + ly;
+    if (y >= L.h) return;
+    int acc[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int q = 0; q < 7; q++) {
+        const int4 v = *reinterpret_cast<const int4*>(&rowsum[ly + q][lx0]);
+        acc[0] += kk[q] * v.x;
+        acc[1] += kk[q] * v.y;
+        acc[2] += kk[q] * v.z;
+        acc[3] += kk[q] * v.w;
+    }
+    // acc >= 0: unsigned shift + min.  (A signed clamp-of-ashr pair is lowered by ROCm 7.2 to
+    // v_ashr_pk_u8_i32, whose untouched high half then leaks into the packed word.)
+    uint32_t packed = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t v = min(((uint32_t)acc[k] + (1u << 15)) >> 16, 255u);
+        packed |= v << (8 * k);
+    }
+    *reinterpret_cast<uint32_t*>(out + (size_t)y * L.pitch + tx0 + lx0) = packed;
+}
+
+// ------------------------------------------------------------------ A5/A7: orientation + descriptor
+
+__device__ float fast_atan2_dev(float y, float x) {
+    const double RAD2DEG = 180.0 / 3.14159265358979323846;
+    const float p1 = 0.9997878412794807f * (float)RAD2DEG;
+    const float p3 = -0.3258083974640975f * (float)RAD2DEG;
+    const float p5 = 0.1555786518463281f * (float)RAD2DEG;
+    const float p7 = -0.04432655554792128f * (float)RAD2DEG;
+    const float ax = fabsf(x), ay = fabsf(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + (float)2.220446049250313080847e-16);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + (float)2.220446049250313080847e-16);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+// glibc 2.35 x86_64 sinf/cosf (FMA variant) restated for |y| < 120 — see DESIGN.md §sincosf.
+struct SinCosTab { double sign[4], hpi_inv, hpi, c0, c1, s1, c2, s2, c3, s3, c4; };
+__constant__ SinCosTab c_sct[2] = {
+    {{1.0, -1.0, -1.0, 1.0}, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0, 0x1p0, -0x1.ffffffd0c621cp-2,
+     -0x1.555545995a603p-3, 0x1.55553e1068f19p-5, 0x1.1107605230bc4p-7, -0x1.6c087e89a359dp-10,
+     -0x1.994eb3774cf24p-13, 0x1.99343027bf8c3p-16},
+    {{1.0, -1.0, -1.0, 1.0}, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0, -0x1p0, 0x1.ffffffd0c621cp-2,
+     -0x1.555545995a603p-3, -0x1.55553e1068f19p-5, 0x1.1107605230bc4p-7, 0x1.6c087e89a359dp-10,
+     -0x1.994eb3774cf24p-13, -0x1.99343027bf8c3p-16},
+};
+__device__ __forceinline__ float sin_poly(double x, double x2, const SinCosTab& p) {
+    const double x3 = x * x2;
+    const double s1 = __fma_rn(x2, p.s3, p.s2);
+    const double x5 = x2 * x3;
+    const double s = __fma_rn(x3, p.s1, x);
+    return (float)__fma_rn(s1, x5, s);
+}
+__device__ __forceinline__ float cos_poly(double x2, const SinCosTab& p) {
+    const double x4 = x2 * x2;
+    const double c1 = __fma_rn(x2, p.c1, p.c0);
+    const double c2 = __fma_rn(x2, p.c4, p.c3);
+    const double x6 = x2 * x4;
+    const double c = __fma_rn(x4, p.c2, c1);
+    return (float)__fma_rn(c2, x6, c);
+}
+__device__ void glibc_sincosf(float y, float& s, float& c) {
+    const uint32_t top = (__float_as_uint(y) >> 20) & 0x7ff;
+    const double x = (double)y;
+    if (top < 0x3f4) {
+        if (top < 0x398) { s = y; c = 1.0f; return; }
+        const double x2 = x * x;
+        s = sin_poly(x, x2, c_sct[0]);
+        c = cos_poly(x2, c_sct[0]);
+        return;
+    }
+    const double r = x * c_sct[0].hpi_inv;
+    const int n = (((int)r) + 0x800000) >> 24;
+    const double xr = __fma_rn(-(double)n, c_sct[0].hpi, x);
+    const double x2 = xr * xr;
+    const SinCosTab& q = c_sct[(n & 2) ? 1 : 0];
+    const double xs = xr * c_sct[0].sign[n & 3];
+    if ((n & 1) == 0) {
+        s = sin_poly(xs, x2, q);
+        c = cos_poly(x2, q);
+    } else {
+        s = cos_poly(x2, q);
+        c = sin_poly(xs, x2, q);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __restrict__ pyr,
+                                                     const uint8_t* __restrict__ blurred,
+                                                     const uint32_t* __restrict__ outKeys,
+                                                     const int* __restrict__ levelCount, orb_keypoint* __restrict__ kps,
+                                                     uint8_t* __restrict__ desc, int cap, int32_t* __restrict__ counts) {
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int b = blockIdx.y;
+    const int q = blockIdx.x * 4 + wid;
+    const int* lc = levelCount + (size_t)b * g.nlevels;
+    if (q == 0 && lane == 0) {
+        int tot = 0;
+        for (int l = 0; l < g.nlevels; l++) tot += lc[l];
+        counts[b] = tot;
+    }
+    if (q >= g.outPerFrame) return;
+    int l = 0;
+    while (l + 1 < g.nlevels && q >= g.lv[l + 1].outBase) l++;
+    const LevelGeom& L = g.lv[l];
+    const int local = q - L.outBase;
+    if (local >= lc[l]) return;
+    int outIdx = local;
+    for (int l2 = 0; l2 < l; l2++) outIdx += lc[l2];
+    if (outIdx >= cap) return;
+    const uint32_t key = outKeys[(size_t)b * g.outPerFrame + q];
+    const int x = kx_of(key) + kMinBorder, y = ky_of(key) + kMinBorder, resp = kr_of(key);
+    // IC_Angle on the un-blurred level (R/src/ORBextractor.cpp:79-108)
+    const uint8_t* img = pyr + (size_t)b * g.frameBytes + L.off;
+    const uint8_t* ctr = img + (size_t)y * L.pitch + x;
+    int m01 = 0, m10 = 0;
+    for (int t = lane; t < 31 * 31; t += 64) {
+        const int v = t / 31 - 15, u = t % 31 - 15;
+        if (abs(u) <= g.umax[abs(v)]) {
+            const int I = ctr[v * L.pitch + u];
+            m10 += u * I;
+            m01 += v * I;
+        }
+    }
+    m10 = wave_reduce_sum_i32(m10);
+    m01 = wave_reduce_sum_i32(m01);
+    const float angle = fast_atan2_dev((float)m01, (float)m10);
+    // steered BRIEF on the blurred level (R/src/ORBextractor.cpp:113-155)
+    float bs, ac;
+    glibc_sincosf(angle * g.factorPI, bs, ac);
+    const float a = ac, bb = bs;
+    const uint8_t* bimg = blurred + (size_t)b * g.frameBytes + L.off;
+    const uint8_t* bc = bimg + (size_t)y * L.pitch + x;
+    const int step = L.pitch;
+    uint64_t words[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int pi = r * 64 + lane;   // pair index: byte pi/8, bit pi%8
+        const float x0 = (float)c_pattern[4 * pi], y0 = (float)c_pattern[4 * pi + 1];
+        const float x1 = (float)c_pattern[4 * pi + 2], y1 = (float)c_pattern[4 * pi + 3];
+        const int t0 = bc[__float2int_rn(x0 * bb + y0 * a) * step + __float2int_rn(x0 * a - y0 * bb)];
+        const int t1 = bc[__float2int_rn(x1 * bb + y1 * a) * step + __float2int_rn(x1 * a - y1 * bb)];
+        words[r] = __ballot(t0 < t1);
+    }
+    if (lane < 4) {
+        uint64_t wv = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
+        reinterpret_cast<uint64_t*>(desc + ((size_t)b * cap + outIdx) * 32)[lane] = wv;
+    }
+    if (lane == 0) {
+        orb_keypoint kp;
+        kp.x = (float)x;
+        kp.y = (float)y;
+        if (l != 0) {
+            kp.x = kp.x * L.scale;
+            kp.y = kp.y * L.scale;
+        }
+        kp.size = L.size;
+        kp.angle = angle;
+        kp.response = (float)resp;
+        kp.octave = l;
+        kp.class_id = -1;
+        kps[(size_t)b * cap + outIdx] = kp;
+    }
+}
+
+// Copies B packed w x h frames into the pitched level-0 slots of the pyramid slab.
+__global__ __launch_bounds__(64) void k_load_frames(Geom g, const uint8_t* __restrict__ src, size_t frameStride,
+                                                    uint8_t* __restrict__ pyr) {
+    const int b = blockIdx.z, y = blockIdx.y;
+    const int x0 = (blockIdx.x * 64 + threadIdx.x) * 4;
+    const LevelGeom& L = g.lv[0];
+    if (x0 >= L.w) return;
+    const uint8_t* s = src + (size_t)b * frameStride + (size_t)y * L.w;
+    uint32_t v = 0;
+    for (int k = 0; k < 4; k++)
+        if (x0 + k < L.w) v |= (uint32_t)s[x0 + k] << (8 * k);
+    *reinterpret_cast<uint32_t*>(pyr + (size_t)b * g.frameBytes + L.off + (size_t)y * L.pitch + x0) = v;
+}
+
+// ------------------------------------------------------------------ host handle
+
+int check_device(int dev) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || dev < 0 || dev >= n) return ORB_ENODEV;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return ORB_ENODEV;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        std::fprintf(stderr, "[orbslam2_amd] device %d is %s, this build targets gfx950 only\n", dev, prop.gcnArchName);
+        return ORB_ENODEV;
+    }
+    return ORB_OK;
+}
+
+}  // namespace orbamd
+
+using namespace orbamd;
+
+struct orb_extractor {
+    orb_extractor_params p;
+    int device = 0;
+    int maxW = 0, maxH = 0, maxB = 0;
+    hipStream_t stream = nullptr;
+    Geom g;                     // geometry of the last call
+    int gw = -1, gh = -1;
+    int blurK[4];
+    size_t capFrames = 0, capFrameBytes = 0, capSlots = 0, capOut = 0, capCells = 0;
+    uint8_t *d_pyr = nullptr, *d_blur = nullptr, *d_score = nullptr;
+    uint32_t *d_slots = nullptr, *d_keyA = nullptr, *d_keyB = nullptr, *d_outKeys = nullptr;
+    int *d_cellCount = nullptr, *d_levelCount = nullptr, *d_status = nullptr;
+    // host-path outputs
+    orb_keypoint* d_kps = nullptr;
+    uint8_t* d_desc = nullptr;
+    int32_t* d_counts = nullptr;
+    size_t capHostOut = 0;
+    uint8_t* h_stage = nullptr;
+    size_t h_stage_bytes = 0;
+    void* h_out = nullptr;
+    size_t h_out_bytes = 0;
+    // pyramid download cache
+    std::vector<uint8_t> h_levels;
+    std::vector<char> h_level_valid;
+    int lastB = 0;
+};
+
+static void free_dev(void* p) {
+    if (p) (void)hipFree(p);
+}
+
+static void release_buffers(orb_extractor* ex) {
+    free_dev(ex->d_pyr); free_dev(ex->d_blur); free_dev(ex->d_score);
+    free_dev(ex->d_slots); free_dev(ex->d_keyA); free_dev(ex->d_keyB); free_dev(ex->d_outKeys);
+    free_dev(ex->d_cellCount); free_dev(ex->d_levelCount); free_dev(ex->d_status);
+    free_dev(ex->d_kps); free_dev(ex->d_desc); free_dev(ex->d_counts);
+    ex->d_pyr = ex->d_blur = ex->d_score = nullptr;
+    ex->d_slots = ex->d_keyA = ex->d_keyB = ex->d_outKeys = nullptr;
+    ex->d_cellCount = ex->d_levelCount = ex->d_status = nullptr;
+    ex->d_kps = nullptr; ex->d_desc = nullptr; ex->d_counts = nullptr;
+    ex->capFrames = ex->capFrameBytes = ex->capSlots = ex->capOut = ex->capCells = ex->capHostOut = 0;
+}
+
+static int ensure_geom(orb_extractor* ex, int w, int h) {
+    if (w == ex->gw && h == ex->gh) return ORB_OK;
+    Geom g;
+    int st = build_geom(ex->p, w, h, &g);
+    if (st) return st;
+    ex->g = g;
+    ex->gw = w;
+    ex->gh = h;
+    return ORB_OK;
+}
+
+static int ensure_capacity(orb_extractor* ex, int B) {
+    const Geom& g = ex->g;
+    const size_t fb = (size_t)g.frameBytes, sl = (size_t)g.slotsPerFrame, ou = (size_t)g.outPerFrame,
+                 ce = (size_t)g.cellsPerFrame;
+    if ((size_t)B <= ex->capFrames && fb <= ex->capFrameBytes && sl <= ex->capSlots && ou <= ex->capOut &&
+        ce <= ex->capCells)
+        return ORB_OK;
+    ORB_HIP_TRY(hipStreamSynchronize(ex->stream));
+    release_buffers(ex);
+    const size_t nb = std::max<size_t>(B, 1);
+#define ALLOC(ptr, bytes) \
+    if (hipMalloc((void**)&(ptr), (bytes)) != hipSuccess) { release_buffers(ex); return ORB_ENOMEM; }
+    ALLOC(ex->d_pyr, nb * fb);
+    ALLOC(ex->d_blur, nb * fb);
+    ALLOC(ex->d_score, nb * fb);
+    ALLOC(ex->d_slots, nb * sl * 4);
+    ALLOC(ex->d_keyA, nb * sl * 4);
+    ALLOC(ex->d_keyB, nb * sl * 4);
+    ALLOC(ex->d_outKeys, nb * ou * 4);
+    ALLOC(ex->d_cellCount, nb * ce * 4);
+    ALLOC(ex->d_levelCount, nb * kMaxLevels * 4);
+    ALLOC(ex->d_status, 64);
+    ALLOC(ex->d_kps, nb * ou * sizeof(orb_keypoint));
+    ALLOC(ex->d_desc, nb * ou * 32);
+    ALLOC(ex->d_counts, nb * 4 + 64);
+#undef ALLOC
+    ex->capFrames = nb;
+    ex->capFrameBytes = fb;
+    ex->capSlots = sl;
+    ex->capOut = ou;
+    ex->capCells = ce;
+    ex->capHostOut = ou;
+    ORB_HIP_TRY(hipMemset(ex->d_pyr, 0, nb * fb));
+    ORB_HIP_TRY(hipMemset(ex->d_blur, 0, nb * fb));
+    ORB_HIP_TRY(hipMemset(ex->d_score, 0, nb * fb));
+    return ORB_OK;
+}
+
+static size_t octree_lds_bytes(const Geom& g) {
+    const size_t cap = (size_t)g.maxNodeCap;
+    auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
+    size_t s = r16(sizeof(uint4) * (cap + 1));
+    s += 2 * (r16(4 * (cap + 1)) + 5 * r16(4 * cap));
+    s += 6 * r16(4 * cap) + r16(4 * (cap + 1));
+    int maxCells = 0;
+    for (int l = 0; l < g.nlevels; l++) maxCells = std::max(maxCells, g.lv[l].nCols * g.lv[l].nRows);
+    s += r16(4 * (maxCells + 1 + 64));
+    s += r16(8 * 8) + r16(4 * 8) + r16(4 * 32) + r16(16);
+    return s;
+}
+
+// Enqueues the full pipeline for B frames already resident in d_pyr level 0.
+static int run_pipeline(orb_extractor* ex, int B, orb_keypoint* d_kps, uint8_t* d_desc, int cap, int32_t* d_counts,
+                        hipStream_t st) {
+    const Geom& g = ex->g;
+    ORB_HIP_TRY(hipMemsetAsync(ex->d_status, 0, 4, st));
+    for (int l = 1; l < g.nlevels; l++) {
+        const LevelGeom& L = g.lv[l];
+        dim3 grid((L.w + 255) / 256, (L.h + 3) / 4, B), block(64, 4);
+        hipLaunchKernelGGL(k_resize, grid, block, 0, st, g, l, ex->d_pyr);
+    }
+    hipLaunchKernelGGL(k_fast_score, dim3(g.tilesPerFrame, B), dim3(256), 0, st, g, ex->d_pyr, ex->d_score);
+    hipLaunchKernelGGL(k_cell_detect, dim3((g.cellsPerFrame + 3) / 4, B), dim3(256), 0, st, g, ex->d_score,
+                       ex->d_slots, ex->d_cellCount, ex->d_status);
+    const size_t lds = octree_lds_bytes(g);
+    hipLaunchKernelGGL(k_octree, dim3(g.nlevels, B), dim3(OT_T), lds, st, g, ex->d_slots, ex->d_cellCount,
+                       ex->d_keyA, ex->d_keyB, ex->d_outKeys, ex->d_levelCount, ex->d_status);
+    hipLaunchKernelGGL(k_blur, dim3(g.tilesPerFrame, B), dim3(256), 0, st, g, ex->d_pyr, ex->d_blur, ex->blurK[0],
+                       ex->blurK[1], ex->blurK[2], ex->blurK[3]);
+    hipLaunchKernelGGL(k_orient_desc, dim3((g.outPerFrame + 3) / 4, B), dim3(256), 0, st, g, ex->d_pyr, ex->d_blur,
+                       ex->d_outKeys, ex->d_levelCount, d_kps, d_desc, cap, d_counts);
+    ORB_HIP_TRY(hipGetLastError());
+    return ORB_OK;
+}
+
+static void gauss7_int(int k[7]) {
+    float cf[7];
+    const double sigma = 2.0, scale2X = -0.5 / (sigma * sigma);
+    double sum = 0;
+    for (int i = 0; i < 7; i++) {
+        const double x = i - 3.0;
+        cf[i] = (float)std::exp(scale2X * x * x);
+        sum += cf[i];
+    }
+    sum = 1. / sum;
+    for (int i = 0; i < 7; i++) {
+        cf[i] = (float)(cf[i] * sum);
+        k[i] = (int)std::nearbyint(cf[i] * 256.0f);
+    }
+}
+
+extern "C" {
+
+int orb_extractor_create(const orb_extractor_params* params, int device, int max_w, int max_h, int max_batch,
+                         orb_extractor** out) {
+    if (!params || !out || max_w <= 0 || max_h <= 0 || max_batch <= 0) return ORB_EINVAL;
+    if (params->nlevels < 1 || params->nlevels > kMaxLevels || params->nfeatures < 0 || !(params->scaleFactor > 1.0f))
+        return ORB_EINVAL;
+    int st = check_device(device);
+    if (st) return st;
+    ORB_HIP_TRY(hipSetDevice(device));
+    orb_extractor* ex = new orb_extractor();
+    ex->p = *params;
+    ex->device = device;
+    ex->maxW = max_w;
+    ex->maxH = max_h;
+    ex->maxB = max_batch;
+    int k[7];
+    gauss7_int(k);
+    ex->blurK[0] = k[3]; ex->blurK[1] = k[2]; ex->blurK[2] = k[1]; ex->blurK[3] = k[0];
+    if (hipStreamCreateWithFlags(&ex->stream, hipStreamNonBlocking) != hipSuccess) { delete ex; return ORB_EGPU; }
+    st = ensure_geom(ex, max_w, max_h);
+    if (!st) st = ensure_capacity(ex, max_batch);
+    if (st) { orb_extractor_destroy(ex); return st; }
+    *out = ex;
+    return ORB_OK;
+}
+
+void orb_extractor_destroy(orb_extractor* ex) {
+    if (!ex) return;
+    (void)hipSetDevice(ex->device);
+    if (ex->stream) (void)hipStreamSynchronize(ex->stream);
+    release_buffers(ex);
+    if (ex->h_stage) (void)hipHostFree(ex->h_stage);
+    if (ex->h_out) (void)hipHostFree(ex->h_out);
+    if (ex->stream) (void)hipStreamDestroy(ex->stream);
+    delete ex;
+}
+
+int orb_extractor_levels(const orb_extractor* ex) { return ex ? ex->p.nlevels : ORB_EINVAL; }
+
+int orb_extractor_scale_tables(const orb_extractor* ex, float* scale, float* inv_scale, float* sigma2,
+                               float* inv_sigma2) {
+    if (!ex) return ORB_EINVAL;
+    host_tables(ex->p, scale, inv_scale, sigma2, inv_sigma2, nullptr);
+    return ORB_OK;
+}
+
+int orb_extractor_features_per_level(const orb_extractor* ex, int* per_level) {
+    if (!ex || !per_level) return ORB_EINVAL;
+    host_tables(ex->p, nullptr, nullptr, nullptr, nullptr, per_level);
+    return ORB_OK;
+}
+
+static int ensure_pinned(void** p, size_t* cur, size_t need) {
+    if (*cur >= need) return ORB_OK;
+    if (*p) (void)hipHostFree(*p);
+    *p = nullptr;
+    *cur = 0;
+    if (hipHostMalloc(p, need, hipHostMallocDefault) != hipSuccess) return ORB_ENOMEM;
+    *cur = need;
+    return ORB_OK;
+}
+
+int orb_extract(orb_extractor* ex, const uint8_t* img, int w, int h, size_t stride, orb_keypoint* kps, uint8_t* desc,
+                int capacity, int* n_out) {
+    if (!ex) return ORB_EINVAL;
+    if (!img || w <= 0 || h <= 0) return ORB_OK;   // R/src/ORBextractor.cpp:1123-1124
+    if (stride < (size_t)w || capacity < 0) return ORB_EINVAL;
+    ORB_HIP_TRY(hipSetDevice(ex->device));
+    int st = ensure_geom(ex, w, h);
+    if (st) return st;
+    st = ensure_capacity(ex, 1);
+    if (st) return st;
+    const Geom& g = ex->g;
+    const LevelGeom& L0 = g.lv[0];
+    const size_t imgBytes = (size_t)L0.pitch * h;
+    st = ensure_pinned((void**)&ex->h_stage, &ex->h_stage_bytes, imgBytes);
+    if (st) return st;
+    for (int y = 0; y < h; y++) std::memcpy(ex->h_stage + (size_t)y * L0.pitch, img + (size_t)y * stride, (size_t)w);
+    ORB_HIP_TRY(hipMemcpyAsync(ex->d_pyr + L0.off, ex->h_stage, imgBytes, hipMemcpyHostToDevice, ex->stream));
+    const int cap = (int)ex->capHostOut;
+    st = run_pipeline(ex, 1, ex->d_kps, ex->d_desc, cap, ex->d_counts, ex->stream);
+    if (st) return st;
+    st = ensure_pinned(&ex->h_out, &ex->h_out_bytes, 64 + (size_t)cap * (sizeof(orb_keypoint) + 32));
+    if (st) return st;
+    int32_t* h_cnt = (int32_t*)ex->h_out;
+    ORB_HIP_TRY(hipMemcpyAsync(h_cnt, ex->d_counts, 4, hipMemcpyDeviceToHost, ex->stream));
+    ORB_HIP_TRY(hipMemcpyAsync(h_cnt + 1, ex->d_status, 4, hipMemcpyDeviceToHost, ex->stream));
+    ORB_HIP_TRY(hipStreamSynchronize(ex->stream));
+    ex->lastB = 1;
+    ex->h_level_valid.assign(g.nlevels, 0);
+    if (h_cnt[1] != 0) {
+        std::fprintf(stderr, "[orbslam2_amd] extractor status 0x%x\n", h_cnt[1]);
+        return ORB_EOVERFLOW;
+    }
+    const int N = h_cnt[0];
+    if (n_out) *n_out = N;
+    if (N > capacity) return ORB_E2BIG;
+    if (N > 0) {
+        orb_keypoint* hk = (orb_keypoint*)((char*)ex->h_out + 64);
+        uint8_t* hd = (uint8_t*)(hk + cap);
+        ORB_HIP_TRY(hipMemcpyAsync(hk, ex->d_kps, (size_t)N * sizeof(orb_keypoint), hipMemcpyDeviceToHost, ex->stream));
+        ORB_HIP_TRY(hipMemcpyAsync(hd, ex->d_desc, (size_t)N * 32, hipMemcpyDeviceToHost, ex->stream));
+        ORB_HIP_TRY(hipStreamSynchronize(ex->stream));
+        if (kps) std::memcpy(kps, hk, (size_t)N * sizeof(orb_keypoint));
+        if (desc) std::memcpy(desc, hd, (size_t)N * 32);
+    }
+    return N;
+}
+
+int orb_extract_batch_device(orb_extractor* ex, const uint8_t* d_imgs, size_t img_stride_frame, int B, int w, int h,
+                             orb_keypoint* d_kps, uint8_t* d_desc, int cap, int32_t* d_counts, void* stream) {
+    if (!ex || !d_imgs || B <= 0 || w <= 0 || h <= 0 || !d_kps || !d_desc || !d_counts || cap < 0) return ORB_EINVAL;
+    if (img_stride_frame < (size_t)w * h) return ORB_EINVAL;
+    ORB_HIP_TRY(hipSetDevice(ex->device));
+    int st = ensure_geom(ex, w, h);
+    if (st) return st;
+    st = ensure_capacity(ex, B);
+    if (st) return st;
+    hipStream_t s = stream ? (hipStream_t)stream : ex->stream;
+    const Geom& g = ex->g;
+    const LevelGeom& L0 = g.lv[0];
+    hipLaunchKernelGGL(k_load_frames, dim3((w + 255) / 256, h, B), dim3(64), 0, s, g, d_imgs, img_stride_frame,
+                       ex->d_pyr);
+    ORB_HIP_TRY(hipGetLastError());
+    ex->lastB = B;
+    ex->h_level_valid.assign((size_t)B * g.nlevels, 0);
+    return run_pipeline(ex, B, d_kps, d_desc, cap, d_counts, s);
+}
+
+int orb_pyramid_level(orb_extractor* ex, int frame, int level, const uint8_t** host, int* w, int* h, size_t* stride) {
+    if (!ex || level < 0 || level >= ex->p.nlevels || frame < 0 || frame >= ex->lastB || ex->gw < 0) return ORB_EINVAL;
+    ORB_HIP_TRY(hipSetDevice(ex->device));
+    const Geom& g = ex->g;
+    const size_t per = (size_t)g.frameBytes;
+    if (ex->h_levels.size() < per * ex->lastB) ex->h_levels.resize(per * ex->lastB);
+    if (ex->h_level_valid.size() < (size_t)ex->lastB * g.nlevels) ex->h_level_valid.assign((size_t)ex->lastB * g.nlevels, 0);
+    const LevelGeom& L = g.lv[level];
+    uint8_t* dst = ex->h_levels.data() + per * frame + L.off;
+    char& valid = ex->h_level_valid[(size_t)frame * g.nlevels + level];
+    if (!valid) {
+        ORB_HIP_TRY(hipStreamSynchronize(ex->stream));
+        ORB_HIP_TRY(hipMemcpy(dst, ex->d_pyr + per * frame + L.off, (size_t)L.pitch * L.h, hipMemcpyDeviceToHost));
+        valid = 1;
+    }
+    if (host) *host = dst;
+    if (w) *w = L.w;
+    if (h) *h = L.h;
+    if (stride) *stride = (size_t)L.pitch;
+    return ORB_OK;
+}
+
+int orb_pyramid_level_device(orb_extractor* ex, int frame, int level, int blurred, const uint8_t** dptr, int* w,
+                             int* h, size_t* pitch) {
+    if (!ex || level < 0 || level >= ex->p.nlevels || frame < 0 || frame >= (int)ex->capFrames || ex->gw < 0)
+        return ORB_EINVAL;
+    const Geom& g = ex->g;
+    const LevelGeom& L = g.lv[level];
+    const uint8_t* base = blurred ? ex->d_blur : ex->d_pyr;
+    if (dptr) *dptr = base + (size_t)frame * g.frameBytes + L.off;
+    if (w) *w = L.w;
+    if (h) *h = L.h;
+    if (pitch) *pitch = (size_t)L.pitch;
+    return ORB_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,201 @@
+"""ctypes binding of the CPU oracle (oracle/build/liborb_oracle.so).
+
+TEST INFRASTRUCTURE: used only by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, as the checker.  Never imported by the product package.
+"""
+import ctypes as C
+import pathlib
+import subprocess
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+LIB_PATH = ROOT / "oracle" / "build" / "liborb_oracle.so"
+
+
+class KeyPoint(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("size", C.c_float), ("angle", C.c_float),
+                ("response", C.c_float), ("octave", C.c_int32), ("class_id", C.c_int32)]
+
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+
+
+class Params(C.Structure):
+    _fields_ = [("nfeatures", C.c_int), ("scaleFactor", C.c_float), ("nlevels", C.c_int),
+                ("iniThFAST", C.c_int), ("minThFAST", C.c_int)]
+
+
+class Frame(C.Structure):
+    _fields_ = [("n", C.c_int), ("x", C.c_void_p), ("y", C.c_void_p), ("angle", C.c_void_p),
+                ("octave", C.c_void_p), ("desc", C.c_void_p), ("uright", C.c_void_p),
+                ("min_x", C.c_float), ("min_y", C.c_float), ("max_x", C.c_float), ("max_y", C.c_float),
+                ("grid_w_inv", C.c_float), ("grid_h_inv", C.c_float)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float),
+                ("mbf", C.c_float), ("mb", C.c_float)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            subprocess.check_call(["make", "-s", "-C", str(ROOT / "oracle")])
+        _lib = C.CDLL(str(LIB_PATH))
+    return _lib
+
+
+def P(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+def params(nfeatures=1000, scale=1.2, nlevels=8, ini=20, minth=7):
+    return Params(nfeatures, scale, nlevels, ini, minth)
+
+
+def tables(p):
+    n = p.nlevels
+    s, inv, s2, inv2 = (np.zeros(n, np.float32) for _ in range(4))
+    fpl = np.zeros(n, np.int32)
+    umax = np.zeros(16, np.int32)
+    lib().oracle_orb_tables(C.byref(p), P(s), P(inv), P(s2), P(inv2), P(fpl), P(umax))
+    return dict(scale=s, inv_scale=inv, sigma2=s2, inv_sigma2=inv2, features_per_level=fpl, umax=umax)
+
+
+def level_sizes(p, w, h):
+    lw = np.zeros(p.nlevels, np.int32)
+    lh = np.zeros(p.nlevels, np.int32)
+    lib().oracle_level_sizes(C.byref(p), w, h, P(lw), P(lh))
+    return lw, lh
+
+
+def extract(p, img, want_pyramid=False):
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    cap = 4 * p.nfeatures + 64
+    kps = np.zeros(cap, KP_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    n = C.c_int(0)
+    lc = np.zeros(p.nlevels, np.int32)
+    pc = np.zeros(p.nlevels, np.int32)
+    lw, lh = level_sizes(p, w, h)
+    tot = int((lw.astype(np.int64) * lh).sum())
+    pyr = np.zeros(tot, np.uint8) if want_pyramid else None
+    blr = np.zeros(tot, np.uint8) if want_pyramid else None
+    st = lib().oracle_orb_extract(C.byref(p), P(img), w, h, C.c_size_t(w), P(kps), P(desc), cap,
+                                  C.byref(n), P(lc), P(pc), P(pyr), P(blr))
+    if st < 0:
+        raise RuntimeError(f"oracle_orb_extract failed: {st}")
+    out = dict(kps=kps[:n.value].copy(), desc=desc[:n.value].copy(), level_counts=lc, pre_counts=pc)
+    if want_pyramid:
+        out["pyramid"], out["blurred"], out["sizes"] = pyr, blr, (lw, lh)
+    return out
+
+
+def resize(src, dw, dh):
+    src = np.ascontiguousarray(src, np.uint8)
+    dst = np.zeros((dh, dw), np.uint8)
+    lib().oracle_resize_linear_u8(P(src), src.shape[1], src.shape[0], C.c_size_t(src.shape[1]),
+                                  P(dst), dw, dh, C.c_size_t(dw))
+    return dst
+
+
+def blur(src):
+    src = np.ascontiguousarray(src, np.uint8)
+    dst = np.zeros_like(src)
+    lib().oracle_gaussian_blur7_u8(P(src), src.shape[1], src.shape[0], C.c_size_t(src.shape[1]),
+                                   P(dst), C.c_size_t(src.shape[1]))
+    return dst
+
+
+def fast_roi(img, x0, y0, w, h, thr):
+    img = np.ascontiguousarray(img, np.uint8)
+    cap = w * h
+    out = np.zeros(3 * cap, np.int32)
+    n = lib().oracle_fast_roi(P(img), C.c_size_t(img.shape[1]), x0, y0, w, h, thr, P(out), cap)
+    return out[:3 * n].reshape(-1, 3)
+
+
+def fast_atan2(y, x):
+    f = lib().oracle_fast_atan2
+    f.restype = C.c_float
+    f.argtypes = [C.c_float, C.c_float]
+    return f(y, x)
+
+
+def sincosf(x):
+    s, c = C.c_float(), C.c_float()
+    lib().oracle_sincosf(C.c_float(x), C.byref(s), C.byref(c))
+    return s.value, c.value
+
+
+def distribute_octree(kx, ky, kr, minX, maxX, minY, maxY, N):
+    kx = np.ascontiguousarray(kx, np.float32)
+    ky = np.ascontiguousarray(ky, np.float32)
+    kr = np.ascontiguousarray(kr, np.float32)
+    out = np.zeros(len(kx) + 1, np.int32)
+    n = lib().oracle_distribute_octree(P(kx), P(ky), P(kr), len(kx), minX, maxX, minY, maxY, N, P(out))
+    return out[:n]
+
+
+def descriptor_distance(a, b):
+    a = np.ascontiguousarray(a, np.uint8)
+    b = np.ascontiguousarray(b, np.uint8)
+    return lib().oracle_descriptor_distance(P(a), P(b))
+
+
+class FrameView:
+    """Keeps numpy arrays alive for an oracle_frame struct."""
+
+    def __init__(self, kps, desc, width, height, uright=None):
+        self.x = np.ascontiguousarray(kps["x"], np.float32)
+        self.y = np.ascontiguousarray(kps["y"], np.float32)
+        self.angle = np.ascontiguousarray(kps["angle"], np.float32)
+        self.octave = np.ascontiguousarray(kps["octave"], np.int32)
+        self.desc = np.ascontiguousarray(desc, np.uint8)
+        self.uright = None if uright is None else np.ascontiguousarray(uright, np.float32)
+        self.s = Frame(len(self.x), P(self.x), P(self.y), P(self.angle), P(self.octave), P(self.desc),
+                       P(self.uright), 0.0, 0.0, float(width), float(height),
+                       np.float32(64) / np.float32(width), np.float32(48) / np.float32(height))
+
+
+def search_for_initialization(f1, f2, prev_xy, nnratio=0.9, check_ori=True, window=100):
+    prev = np.ascontiguousarray(prev_xy, np.float32).copy()
+    m12 = np.zeros(f1.s.n, np.int32)
+    n = lib().oracle_search_for_initialization(C.byref(f1.s), C.byref(f2.s), C.c_float(nnratio),
+                                               int(check_ori), P(prev), P(m12), window)
+    return n, m12, prev
+
+
+def search_by_projection_ff(cur, Tcw, last, Tlw, has_mp, outlier, mp_xyz, mp_desc, scale_factors,
+                            cam, th, mono, check_ori=True, cur_mp=None):
+    if cur_mp is None:
+        cur_mp = np.full(cur.s.n, -1, np.int32)
+    cur_mp = np.ascontiguousarray(cur_mp, np.int32).copy()
+    Tcw = np.ascontiguousarray(Tcw, np.float32)
+    Tlw = np.ascontiguousarray(Tlw, np.float32)
+    has_mp = np.ascontiguousarray(has_mp, np.int32)
+    outlier = np.ascontiguousarray(outlier, np.uint8)
+    mp_xyz = np.ascontiguousarray(mp_xyz, np.float32)
+    mp_desc = np.ascontiguousarray(mp_desc, np.uint8)
+    sf = np.ascontiguousarray(scale_factors, np.float32)
+    n = lib().oracle_search_by_projection_ff(C.byref(cur.s), P(Tcw), C.byref(last.s), P(Tlw), P(has_mp),
+                                             P(outlier), P(mp_xyz), P(mp_desc), P(sf), C.byref(cam),
+                                             C.c_float(th), int(mono), int(check_ori), P(cur_mp))
+    return n, cur_mp
+
+
+def hamming_knn2(q, t):
+    q = np.ascontiguousarray(q, np.uint8)
+    t = np.ascontiguousarray(t, np.uint8)
+    bi = np.zeros(len(q), np.int32)
+    bd = np.zeros(len(q), np.int32)
+    sd = np.zeros(len(q), np.int32)
+    lib().oracle_hamming_knn2(P(q), len(q), P(t), len(t), P(bi), P(bd), P(sd))
+    return bi, bd, sd
