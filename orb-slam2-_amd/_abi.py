@@ -56,6 +56,15 @@ def lib() -> C.CDLL:
             "orb_extract_batch_device": [vp, vp, sz, i32, i32, i32, vp, vp, i32, vp, vp],
             "orb_pyramid_level": [vp, i32, i32, vp, vp, vp, vp],
             "orb_pyramid_level_device": [vp, i32, i32, i32, vp, vp, vp, vp],
+            "orb_matcher_create": [i32, f32, i32, vp],
+            "orb_matcher_destroy": [vp],
+            "orb_descriptor_distance": [vp, vp],
+            "orb_search_for_initialization": [vp, vp, vp, vp, vp, i32],
+            "orb_search_by_projection_frame": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32, i32, vp],
+            "orb_hamming_knn2": [vp, vp, i32, vp, i32, vp, vp, vp],
+            "orb_hamming_knn2_batch_device": [vp, vp, vp, vp, vp, i32, i32, i32, vp, vp, vp, vp],
+            "orb_search_for_initialization_batch_device": [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32,
+                                                           vp, vp, vp],
         }
         for name, args in sig.items():
             fn = getattr(_lib, name)

@@ -1,2 +1,841 @@
-// placeholder, filled in below
+// MI355X-native ORBmatcher cores (R/src/ORBmatcher.cpp; R/ = /root/reference/ORB-SLAM2注释版/).
+//
+// The reference's searches are sequential and greedy: a later query sees the
+// matches (and stolen matches) of every earlier one.  They are
+// restated as two gfx950 kernels per frame pair:
+//   k_cand_*   — parallel: one wave per query enumerates the GetFeaturesInArea
+//                candidates (R/src/Frame.cpp:387-440) and their Hamming distances
+//                (wave64 XOR + v_bcnt over 8 dwords, R/src/ORBmatcher.cpp:1901-1917);
+//   k_resolve_* — one wave per frame pair replays the queries in order, keeping the
+//                greedy state (vMatchedDistance / vnMatches21 / occupied slots) in
+//                LDS and reducing each query's candidates with wave reductions whose
+//                tie-break is the reference's candidate order (cell-major, then index).
+// The rotation-consistency histogram (HISTO_LENGTH=30, ComputeThreeMaxima) runs at
+// the end of the resolve kernel.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstring>
+#include <vector>
+
 #include "common.h"
+
+namespace orbamd {
+
+constexpr int kGridCols = 64;    // FRAME_GRID_COLS (R/include/Frame.h:38)
+constexpr int kGridRows = 48;    // FRAME_GRID_ROWS
+constexpr int kHisto = 30;       // HISTO_LENGTH
+constexpr int kThLow = 50;       // TH_LOW
+constexpr int kThHigh = 100;     // TH_HIGH
+constexpr int kMaxCand = 1024;   // per-query candidate list capacity (overflow -> status)
+
+struct GridParams {
+    float min_x, min_y, max_x, max_y, winv, hinv;
+};
+
+__device__ __forceinline__ int hamming32(const uint8_t* a, const uint8_t* b) {
+    const uint4* pa = reinterpret_cast<const uint4*>(a);
+    const uint4* pb = reinterpret_cast<const uint4*>(b);
+    const uint4 a0 = pa[0], a1 = pa[1], b0 = pb[0], b1 = pb[1];
+    return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+           __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+// PosInGrid (R/src/Frame.cpp:442-452); returns cell key ix*48+iy or -1.
+__device__ __forceinline__ int grid_cell(const GridParams& g, float x, float y) {
+    const int px = (int)roundf((x - g.min_x) * g.winv);
+    const int py = (int)roundf((y - g.min_y) * g.hinv);
+    if (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) return -1;
+    return px * kGridRows + py;
+}
+
+struct AreaQuery {
+    int cx0, cx1, cy0, cy1;   // inclusive cell ranges; cx0 > cx1 -> empty
+    bool checkLevels;
+    int minLevel, maxLevel;
+    float x, y, r;
+};
+
+// GetFeaturesInArea bounds (R/src/Frame.cpp:392-408).
+__device__ __forceinline__ AreaQuery make_area(const GridParams& g, float x, float y, float r, int minLevel,
+                                               int maxLevel) {
+    AreaQuery q;
+    q.x = x; q.y = y; q.r = r;
+    q.minLevel = minLevel; q.maxLevel = maxLevel;
+    q.checkLevels = (minLevel > 0) || (maxLevel >= 0);
+    q.cx0 = max(0, (int)floorf((x - g.min_x - r) * g.winv));
+    q.cx1 = min(kGridCols - 1, (int)ceilf((x - g.min_x + r) * g.winv));
+    q.cy0 = max(0, (int)floorf((y - g.min_y - r) * g.hinv));
+    q.cy1 = min(kGridRows - 1, (int)ceilf((y - g.min_y + r) * g.hinv));
+    if (q.cx0 >= kGridCols || q.cx1 < 0 || q.cy0 >= kGridRows || q.cy1 < 0) q.cx0 = 1, q.cx1 = 0;
+    return q;
+}
+
+__device__ __forceinline__ bool in_area(const AreaQuery& q, int cell, int octave, float kx, float ky) {
+    if (cell < 0) return false;
+    const int ix = cell / kGridRows, iy = cell % kGridRows;
+    if (ix < q.cx0 || ix > q.cx1 || iy < q.cy0 || iy > q.cy1) return false;
+    if (q.checkLevels) {
+        if (octave < q.minLevel) return false;
+        if (q.maxLevel >= 0 && octave > q.maxLevel) return false;
+    }
+    const float dx = kx - q.x, dy = ky - q.y;
+    return fabsf(dx) < q.r && fabsf(dy) < q.r;
+}
+
+__device__ __forceinline__ int rot_bin(float rot) {
+    const float factor = kHisto / 360.0f;
+    if (rot < 0.0f) rot += 360.0f;
+    int bin = (int)roundf(rot * factor);
+    if (bin == kHisto) bin = 0;
+    return bin;
+}
+
+// ---------------------------------------------------------------- wave reductions
+
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const unsigned long long o = __shfl_xor(v, d, 64);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+__device__ __forceinline__ int wave_min_i32(int v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = min(v, __shfl_xor(v, d, 64));
+    return v;
+}
+
+// Best (dist, order) and the multiset-second-smallest distance of a candidate set: this
+// is exactly what the reference's `if(dist<best){best2=best;...} else if(dist<best2)` loop
+// returns for any visiting order, with ties resolved by the visiting order.
+struct Best2 {
+    int best, best2, idx;
+};
+__device__ __forceinline__ Best2 wave_best2(int d, unsigned order, int idx, bool valid) {
+    const unsigned long long key = valid ? (((unsigned long long)(unsigned)d << 40) | ((unsigned long long)order << 20) |
+                                            (unsigned long long)(unsigned)idx)
+                                         : ~0ull;
+    const unsigned long long m = wave_min_u64(key);
+    Best2 r;
+    if (m == ~0ull) { r.best = INT_MAX; r.best2 = INT_MAX; r.idx = -1; return r; }
+    r.best = (int)(m >> 40);
+    r.idx = (int)(m & 0xFFFFFull);
+    // second: another candidate with the same distance, else the smallest larger distance
+    const bool isArg = valid && key == m;
+    const int d2 = (valid && !isArg) ? d : INT_MAX;
+    r.best2 = wave_min_i32(d2);
+    return r;
+}
+
+// ---------------------------------------------------------------- SearchForInitialization
+
+struct SfiPair {
+    const orb_keypoint* k1; const uint8_t* d1; int n1;
+    const orb_keypoint* k2; const uint8_t* d2; int n2;
+    const float* prev;      // 2*n1, NULL -> k1 positions
+};
+
+// Candidate lists for F1 level-0 keypoints: cand[b][i1][*] = (i2 | dist << 20), in
+// ascending i2; ncand[b][i1].
+__global__ __launch_bounds__(256) void k_cand_sfi(const orb_keypoint* __restrict__ kps1, const uint8_t* __restrict__ desc1,
+                                                  const int32_t* __restrict__ n1s, const orb_keypoint* __restrict__ kps2,
+                                                  const uint8_t* __restrict__ desc2, const int32_t* __restrict__ n2s,
+                                                  const float* __restrict__ prev, int cap, GridParams g, float window,
+                                                  uint32_t* __restrict__ cand, int* __restrict__ ncand, int* __restrict__ status) {
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int b = blockIdx.y;
+    const int i1 = blockIdx.x * 4 + wid;
+    const int n1 = min((int)n1s[b], cap), n2 = min((int)n2s[b], cap);
+    if (i1 >= n1) return;
+    const orb_keypoint* K1 = kps1 + (size_t)b * cap;
+    const orb_keypoint* K2 = kps2 + (size_t)b * cap;
+    int* nc = ncand + (size_t)b * cap + i1;
+    const orb_keypoint kp1 = K1[i1];
+    if (kp1.octave > 0) { if (lane == 0) *nc = 0; return; }
+    float px, py;
+    if (prev) { px = prev[((size_t)b * cap + i1) * 2]; py = prev[((size_t)b * cap + i1) * 2 + 1]; }
+    else { px = kp1.x; py = kp1.y; }
+    const AreaQuery q = make_area(g, px, py, window, kp1.octave, kp1.octave);
+    uint32_t* out = cand + ((size_t)b * cap + i1) * kMaxCand;
+    const uint8_t* dq = desc1 + ((size_t)b * cap + i1) * 32;
+    int n = 0;
+    for (int j0 = 0; j0 < n2; j0 += 64) {
+        const int j = j0 + lane;
+        bool ok = false;
+        int d = 0;
+        if (j < n2 && q.cx0 <= q.cx1) {
+            const orb_keypoint k2 = K2[j];
+            ok = in_area(q, grid_cell(g, k2.x, k2.y), k2.octave, k2.x, k2.y);
+            if (ok) d = hamming32(dq, desc2 + ((size_t)b * cap + j) * 32);
+        }
+        const uint64_t m = __ballot(ok);
+        const int pos = n + __popcll(m & ((1ull << lane) - 1ull));
+        if (ok && pos < kMaxCand) out[pos] = (uint32_t)j | ((uint32_t)d << 20);
+        n += __popcll(m);
+    }
+    if (lane == 0) {
+        if (n > kMaxCand) { atomicOr(status, 1); n = kMaxCand; }
+        *nc = n;
+    }
+}
+
+// Sequential replay of R/src/ORBmatcher.cpp:512-616 for one frame pair per workgroup (one wave).
+__global__ __launch_bounds__(64) void k_resolve_sfi(const orb_keypoint* __restrict__ kps1, const int32_t* __restrict__ n1s,
+                                                    const orb_keypoint* __restrict__ kps2, const int32_t* __restrict__ n2s,
+                                                    int cap, GridParams g, float nnratio, int checkOri,
+                                                    const uint32_t* __restrict__ cand, const int* __restrict__ ncand,
+                                                    float* __restrict__ prev, int32_t* __restrict__ matches12,
+                                                    int32_t* __restrict__ nmatches_out, int32_t* __restrict__ histIdx,
+                                                    uint8_t* __restrict__ histBin) {
+    extern __shared__ __attribute__((aligned(16))) int sm[];
+    const int lane = threadIdx.x;
+    const int b = blockIdx.x;
+    const int n1 = min((int)n1s[b], cap), n2 = min((int)n2s[b], cap);
+    int* vMD = sm;                   // vMatchedDistance [n2]
+    int* v21 = sm + cap;             // vnMatches21 [n2]
+    int* ckey = sm + 2 * cap;        // grid cell key per F2 keypoint
+    int* hcount = sm + 3 * cap;      // [kHisto]
+    const orb_keypoint* K1 = kps1 + (size_t)b * cap;
+    const orb_keypoint* K2 = kps2 + (size_t)b * cap;
+    int32_t* m12 = matches12 + (size_t)b * cap;
+    int32_t* hI = histIdx + (size_t)b * cap;
+    uint8_t* hB = histBin + (size_t)b * cap;
+    for (int j = lane; j < n2; j += 64) {
+        vMD[j] = INT_MAX;
+        v21[j] = -1;
+        ckey[j] = grid_cell(g, K2[j].x, K2[j].y);
+    }
+    for (int i = lane; i < n1; i += 64) m12[i] = -1;
+    if (lane < kHisto) hcount[lane] = 0;
+    __syncthreads();
+    int nmatches = 0, nh = 0;
+    for (int i1 = 0; i1 < n1; i1++) {
+        const int nc = ncand[(size_t)b * cap + i1];
+        if (nc == 0) continue;   // also octave > 0 (no candidates listed)
+        const uint32_t* C = cand + ((size_t)b * cap + i1) * kMaxCand;
+        Best2 acc;
+        acc.best = INT_MAX; acc.best2 = INT_MAX; acc.idx = -1;
+        unsigned accOrder = 0xFFFFFu;
+        for (int c0 = 0; c0 < nc; c0 += 64) {
+            const int c = c0 + lane;
+            bool valid = false;
+            int d = 0, j = 0;
+            unsigned order = 0;
+            if (c < nc) {
+                const uint32_t e = C[c];
+                j = (int)(e & 0xFFFFFu);
+                d = (int)(e >> 20);
+                valid = vMD[j] > d;            // `if(vMatchedDistance[i2]<=dist) continue;`
+                order = (unsigned)ckey[j];     // candidates are visited cell-major (ix, iy), then by index
+            }
+            const Best2 r = wave_best2(d, order, j, valid);
+            // merge chunk result into the running (best, best2, idx): the earlier chunk wins ties
+            // only if its order is smaller — orders are compared explicitly.
+            if (r.idx >= 0) {
+                const unsigned rOrder = (unsigned)ckey[r.idx];
+                const bool rFirst = (r.best < acc.best) ||
+                                    (r.best == acc.best && (rOrder < accOrder || (rOrder == accOrder && r.idx < acc.idx)));
+                int nb2;
+                if (rFirst) {
+                    nb2 = min(acc.best, r.best2);
+                    acc.idx = r.idx;
+                    accOrder = rOrder;
+                    acc.best = r.best;
+                } else {
+                    nb2 = min(acc.best2, r.best);
+                }
+                acc.best2 = nb2;
+            }
+        }
+        if (acc.idx >= 0 && acc.best <= kThLow && (float)acc.best < (float)acc.best2 * nnratio) {
+            const int bi = acc.idx;
+            const int prevOwner = v21[bi];
+            if (lane == 0) {
+                if (prevOwner >= 0) m12[prevOwner] = -1;
+                m12[i1] = bi;
+                v21[bi] = i1;
+                vMD[bi] = acc.best;
+                if (checkOri) {
+                    const int bin = rot_bin(K1[i1].angle - K2[bi].angle);
+                    hI[nh] = i1;
+                    hB[nh] = (uint8_t)bin;
+                    hcount[bin]++;
+                }
+            }
+            if (prevOwner >= 0) nmatches--;
+            nmatches++;
+            if (checkOri) nh++;
+            __syncthreads();
+        }
+    }
+    __syncthreads();
+    if (checkOri) {
+        // ComputeThreeMaxima (R/src/ORBmatcher.cpp:1854-1895)
+        int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+        for (int i = 0; i < kHisto; i++) {
+            const int s = hcount[i];
+            if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
+            else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
+            else if (s > max3) { max3 = s; ind3 = i; }
+        }
+        if ((float)max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+        else if ((float)max3 < 0.1f * (float)max1) { ind3 = -1; }
+        // drop matches in every other bin (order irrelevant: a match's entry is unique per i1 state)
+        int removed = 0;
+        for (int e = lane; e < nh; e += 64) {
+            const int bin = hB[e];
+            if (bin == ind1 || bin == ind2 || bin == ind3) continue;
+            const int idx1 = hI[e];
+            if (m12[idx1] >= 0) { m12[idx1] = -1; removed++; }
+        }
+        nmatches -= wave_reduce_sum_i32(removed);
+    }
+    __syncthreads();
+    if (prev) {
+        for (int i = lane; i < n1; i += 64) {
+            const int j = m12[i];
+            if (j >= 0) {
+                prev[((size_t)b * cap + i) * 2] = K2[j].x;
+                prev[((size_t)b * cap + i) * 2 + 1] = K2[j].y;
+            }
+        }
+    }
+    if (lane == 0) nmatches_out[b] = nmatches;
+}
+
+// ---------------------------------------------------------------- SearchByProjection(Frame, Frame)
+
+struct SbpCam {
+    float fx, fy, cx, cy, mbf, mb;
+};
+
+// One wave per last-frame keypoint: projection + candidates (R/src/ORBmatcher.cpp:1590-1671).
+__global__ __launch_bounds__(256) void k_cand_sbp(const orb_keypoint* __restrict__ kc, const uint8_t* __restrict__ dc,
+                                                  const float* __restrict__ urc, int nc_, const orb_keypoint* __restrict__ kl,
+                                                  int nl, const int32_t* __restrict__ hasMp, const uint8_t* __restrict__ outl,
+                                                  const float* __restrict__ mpXYZ, const uint8_t* __restrict__ mpDesc,
+                                                  const float* __restrict__ Tcw, const float* __restrict__ sf, SbpCam cam,
+                                                  GridParams g, float th, int bForward, int bBackward,
+                                                  uint32_t* __restrict__ cand, int* __restrict__ ncand, int* __restrict__ status) {
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int i = blockIdx.x * 4 + wid;
+    if (i >= nl) return;
+    int* ncount = ncand + i;
+    if (!hasMp[i] || outl[i]) { if (lane == 0) *ncount = 0; return; }
+    float x3[3];
+    const float* X = mpXYZ + 3 * (size_t)i;
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        const double s = (double)Tcw[4 * r] * X[0] + (double)Tcw[4 * r + 1] * X[1] + (double)Tcw[4 * r + 2] * X[2];
+        x3[r] = (float)(s + (double)Tcw[4 * r + 3]);
+    }
+    const float xc = x3[0], yc = x3[1];
+    const float invzc = (float)(1.0 / (double)x3[2]);
+    if (invzc < 0) { if (lane == 0) *ncount = 0; return; }
+    const float u = cam.fx * xc * invzc + cam.cx;
+    const float v = cam.fy * yc * invzc + cam.cy;
+    if (u < g.min_x || u > g.max_x || v < g.min_y || v > g.max_y) { if (lane == 0) *ncount = 0; return; }
+    const int nLastOctave = kl[i].octave;
+    const float radius = th * sf[nLastOctave];
+    AreaQuery q;
+    if (bForward) q = make_area(g, u, v, radius, nLastOctave, -1);
+    else if (bBackward) q = make_area(g, u, v, radius, 0, nLastOctave);
+    else q = make_area(g, u, v, radius, nLastOctave - 1, nLastOctave + 1);
+    const float ur = u - cam.mbf * invzc;
+    uint32_t* out = cand + (size_t)i * kMaxCand;
+    const uint8_t* dq = mpDesc + (size_t)i * 32;
+    int n = 0;
+    for (int j0 = 0; j0 < nc_; j0 += 64) {
+        const int j = j0 + lane;
+        bool ok = false;
+        int d = 0;
+        if (j < nc_ && q.cx0 <= q.cx1) {
+            const orb_keypoint k2 = kc[j];
+            ok = in_area(q, grid_cell(g, k2.x, k2.y), k2.octave, k2.x, k2.y);
+            if (ok && urc && urc[j] > 0) {
+                const float er = fabsf(ur - urc[j]);
+                if (er > radius) ok = false;
+            }
+            if (ok) d = hamming32(dq, dc + (size_t)j * 32);
+        }
+        const uint64_t m = __ballot(ok);
+        const int pos = n + __popcll(m & ((1ull << lane) - 1ull));
+        if (ok && pos < kMaxCand) out[pos] = (uint32_t)j | ((uint32_t)d << 20);
+        n += __popcll(m);
+    }
+    if (lane == 0) {
+        if (n > kMaxCand) { atomicOr(status, 1); n = kMaxCand; }
+        *ncount = n;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_resolve_sbp(const orb_keypoint* __restrict__ kc, int ncur,
+                                                    const orb_keypoint* __restrict__ kl, int nl, GridParams g,
+                                                    int checkOri, const uint32_t* __restrict__ cand,
+                                                    const int* __restrict__ ncand, int32_t* __restrict__ curMp,
+                                                    int32_t* __restrict__ nmatches_out, int32_t* __restrict__ histIdx,
+                                                    uint8_t* __restrict__ histBin) {
+    extern __shared__ __attribute__((aligned(16))) int sm[];
+    const int lane = threadIdx.x;
+    int* ckey = sm;              // [ncur]
+    int* hcount = sm + ncur;     // [kHisto]
+    for (int j = lane; j < ncur; j += 64) ckey[j] = grid_cell(g, kc[j].x, kc[j].y);
+    if (lane < kHisto) hcount[lane] = 0;
+    __syncthreads();
+    int nmatches = 0, nh = 0;
+    for (int i = 0; i < nl; i++) {
+        const int nc = ncand[i];
+        if (nc == 0) continue;
+        const uint32_t* C = cand + (size_t)i * kMaxCand;
+        unsigned long long accKey = ~0ull;
+        for (int c0 = 0; c0 < nc; c0 += 64) {
+            const int c = c0 + lane;
+            unsigned long long key = ~0ull;
+            if (c < nc) {
+                const uint32_t e = C[c];
+                const int j = (int)(e & 0xFFFFFu), d = (int)(e >> 20);
+                if (curMp[j] == -1)     // occupied slots are skipped (R :1649-1651)
+                    key = ((unsigned long long)(unsigned)d << 40) | ((unsigned long long)(unsigned)ckey[j] << 20) |
+                          (unsigned long long)(unsigned)j;
+            }
+            const unsigned long long m = wave_min_u64(key);
+            accKey = m < accKey ? m : accKey;
+        }
+        if (accKey == ~0ull) continue;
+        const int bestDist = (int)(accKey >> 40), bestIdx2 = (int)(accKey & 0xFFFFFull);
+        if (bestDist <= kThHigh) {
+            if (lane == 0) {
+                curMp[bestIdx2] = i;
+                if (checkOri) {
+                    const int bin = rot_bin(kl[i].angle - kc[bestIdx2].angle);
+                    histIdx[nh] = bestIdx2;
+                    histBin[nh] = (uint8_t)bin;
+                    hcount[bin]++;
+                }
+            }
+            nmatches++;
+            if (checkOri) nh++;
+            __syncthreads();
+        }
+    }
+    __syncthreads();
+    if (checkOri) {
+        int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+        for (int i = 0; i < kHisto; i++) {
+            const int s = hcount[i];
+            if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
+            else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
+            else if (s > max3) { max3 = s; ind3 = i; }
+        }
+        if ((float)max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+        else if ((float)max3 < 0.1f * (float)max1) { ind3 = -1; }
+        int removed = 0;
+        for (int e = lane; e < nh; e += 64) {
+            const int bin = histBin[e];
+            if (bin == ind1 || bin == ind2 || bin == ind3) continue;
+            curMp[histIdx[e]] = -1;
+            removed++;
+        }
+        nmatches -= wave_reduce_sum_i32(removed);
+    }
+    if (lane == 0) *nmatches_out = nmatches;
+}
+
+// ---------------------------------------------------------------- brute-force 2-NN
+
+// One wave per query row: lanes stride over train rows; ties -> lowest train index.
+__global__ __launch_bounds__(256) void k_knn2(const uint8_t* __restrict__ q, const int32_t* __restrict__ nqs,
+                                              const uint8_t* __restrict__ t, const int32_t* __restrict__ nts, int qStride,
+                                              int tStride, int32_t* __restrict__ bi, int32_t* __restrict__ bd,
+                                              int32_t* __restrict__ sd) {
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int b = blockIdx.y;
+    const int i = blockIdx.x * 4 + wid;
+    const int nq = nqs[b], nt = nts[b];
+    if (i >= nq) return;
+    const uint8_t* dq = q + ((size_t)b * qStride + i) * 32;
+    const uint4 a0 = reinterpret_cast<const uint4*>(dq)[0], a1 = reinterpret_cast<const uint4*>(dq)[1];
+    const uint8_t* T = t + (size_t)b * tStride * 32;
+    unsigned long long best = ~0ull;
+    int second = INT_MAX;
+    for (int j = lane; j < nt; j += 64) {
+        const uint4* pb = reinterpret_cast<const uint4*>(T + (size_t)j * 32);
+        const uint4 b0 = pb[0], b1 = pb[1];
+        const int d = __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+                      __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+        const unsigned long long key = ((unsigned long long)d << 32) | (unsigned)j;
+        if (key < best) {
+            if (best != ~0ull) second = min(second, (int)(best >> 32));
+            best = key;
+        } else {
+            second = min(second, d);
+        }
+    }
+    const unsigned long long m = wave_min_u64(best);
+    // lanes whose best lost contribute it as a second candidate
+    const int mine = (best != ~0ull && best != m) ? (int)(best >> 32) : INT_MAX;
+    const int s2 = wave_min_i32(min(second, mine));
+    if (lane == 0) {
+        const size_t o = (size_t)b * qStride + i;
+        if (m == ~0ull) { bi[o] = -1; bd[o] = INT_MAX; sd[o] = INT_MAX; }
+        else { bi[o] = (int)(m & 0xFFFFFFFFull); bd[o] = (int)(m >> 32); sd[o] = s2; }
+    }
+}
+
+}  // namespace orbamd
+
+using namespace orbamd;
+
+// ---------------------------------------------------------------- host handle
+
+struct orb_matcher {
+    int device = 0;
+    float nnratio = 0.6f;
+    int checkOri = 1;
+    hipStream_t stream = nullptr;
+    // device scratch (grown on demand)
+    size_t capPairs = 0, capPts = 0;
+    orb_keypoint *d_k1 = nullptr, *d_k2 = nullptr;
+    uint8_t *d_d1 = nullptr, *d_d2 = nullptr;
+    float* d_prev = nullptr;
+    float* d_ur = nullptr;
+    int32_t *d_n = nullptr, *d_m12 = nullptr, *d_nm = nullptr, *d_hI = nullptr;
+    uint8_t* d_hB = nullptr;
+    uint32_t* d_cand = nullptr;
+    int *d_ncand = nullptr, *d_status = nullptr;
+    // SBP extras
+    int32_t* d_hasMp = nullptr;
+    uint8_t* d_outl = nullptr;
+    float *d_xyz = nullptr, *d_T = nullptr, *d_sf = nullptr;
+    uint8_t* d_mpd = nullptr;
+    void* h_pin = nullptr;
+    size_t h_pin_bytes = 0;
+};
+
+static void mfree(orb_matcher* m) {
+    void* ptrs[] = {m->d_k1, m->d_k2, m->d_d1, m->d_d2, m->d_prev, m->d_ur, m->d_n, m->d_m12, m->d_nm, m->d_hI,
+                    m->d_hB, m->d_cand, m->d_ncand, m->d_status, m->d_hasMp, m->d_outl, m->d_xyz, m->d_T,
+                    m->d_sf, m->d_mpd};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    m->d_k1 = m->d_k2 = nullptr; m->d_d1 = m->d_d2 = nullptr; m->d_prev = m->d_ur = nullptr;
+    m->d_n = m->d_m12 = m->d_nm = m->d_hI = nullptr; m->d_hB = nullptr; m->d_cand = nullptr;
+    m->d_ncand = m->d_status = nullptr; m->d_hasMp = nullptr; m->d_outl = nullptr;
+    m->d_xyz = m->d_T = m->d_sf = nullptr; m->d_mpd = nullptr;
+    m->capPairs = m->capPts = 0;
+}
+
+static int mensure(orb_matcher* m, size_t pairs, size_t pts) {
+    if (pairs <= m->capPairs && pts <= m->capPts) return ORB_OK;
+    ORB_HIP_TRY(hipStreamSynchronize(m->stream));
+    pairs = std::max(pairs, m->capPairs);
+    pts = std::max(pts, m->capPts);
+    mfree(m);
+    const size_t P = pairs * pts;
+#define MALLOC(p, bytes) \
+    if (hipMalloc((void**)&(p), (bytes)) != hipSuccess) { mfree(m); return ORB_ENOMEM; }
+    MALLOC(m->d_k1, P * sizeof(orb_keypoint));
+    MALLOC(m->d_k2, P * sizeof(orb_keypoint));
+    MALLOC(m->d_d1, P * 32);
+    MALLOC(m->d_d2, P * 32);
+    MALLOC(m->d_prev, P * 8);
+    MALLOC(m->d_ur, P * 4);
+    MALLOC(m->d_n, pairs * 8 + 64);
+    MALLOC(m->d_m12, P * 4);
+    MALLOC(m->d_nm, pairs * 4 + 64);
+    MALLOC(m->d_hI, P * 4);
+    MALLOC(m->d_hB, P);
+    MALLOC(m->d_cand, P * kMaxCand * 4);
+    MALLOC(m->d_ncand, P * 4);
+    MALLOC(m->d_status, 64);
+    MALLOC(m->d_hasMp, P * 4);
+    MALLOC(m->d_outl, P);
+    MALLOC(m->d_xyz, P * 12);
+    MALLOC(m->d_T, 64 * 4);
+    MALLOC(m->d_sf, 64 * 4);
+    MALLOC(m->d_mpd, P * 32);
+#undef MALLOC
+    m->capPairs = pairs;
+    m->capPts = pts;
+    return ORB_OK;
+}
+
+static int mpin(orb_matcher* m, size_t bytes) {
+    if (m->h_pin_bytes >= bytes) return ORB_OK;
+    if (m->h_pin) (void)hipHostFree(m->h_pin);
+    m->h_pin = nullptr;
+    m->h_pin_bytes = 0;
+    if (hipHostMalloc(&m->h_pin, bytes, hipHostMallocDefault) != hipSuccess) return ORB_ENOMEM;
+    m->h_pin_bytes = bytes;
+    return ORB_OK;
+}
+
+static GridParams grid_of(const orb_frame_view* f) {
+    GridParams g;
+    g.min_x = f->min_x; g.min_y = f->min_y; g.max_x = f->max_x; g.max_y = f->max_y;
+    g.winv = f->grid_w_inv; g.hinv = f->grid_h_inv;
+    return g;
+}
+
+static void pack_view(const orb_frame_view* f, orb_keypoint* k) {
+    for (int i = 0; i < f->n; i++) {
+        k[i].x = f->x[i]; k[i].y = f->y[i]; k[i].size = 0.f; k[i].angle = f->angle[i];
+        k[i].response = 0.f; k[i].octave = f->octave[i]; k[i].class_id = -1;
+    }
+}
+
+extern "C" {
+
+int orb_descriptor_distance(const uint8_t* a, const uint8_t* b) {
+    if (!a || !b) return ORB_EINVAL;
+    int dist = 0;
+    for (int i = 0; i < 8; i++) {
+        uint32_t pa, pb;
+        std::memcpy(&pa, a + 4 * i, 4);
+        std::memcpy(&pb, b + 4 * i, 4);
+        dist += __builtin_popcount(pa ^ pb);
+    }
+    return dist;
+}
+
+int orb_matcher_create(int device, float nnratio, int check_ori, orb_matcher** out) {
+    if (!out) return ORB_EINVAL;
+    int st = check_device(device);
+    if (st) return st;
+    ORB_HIP_TRY(hipSetDevice(device));
+    orb_matcher* m = new orb_matcher();
+    m->device = device;
+    m->nnratio = nnratio;
+    m->checkOri = check_ori ? 1 : 0;
+    if (hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess) { delete m; return ORB_EGPU; }
+    *out = m;
+    return ORB_OK;
+}
+
+void orb_matcher_destroy(orb_matcher* m) {
+    if (!m) return;
+    (void)hipSetDevice(m->device);
+    if (m->stream) (void)hipStreamSynchronize(m->stream);
+    mfree(m);
+    if (m->h_pin) (void)hipHostFree(m->h_pin);
+    if (m->stream) (void)hipStreamDestroy(m->stream);
+    delete m;
+}
+
+int orb_search_for_initialization(orb_matcher* m, const orb_frame_view* f1, const orb_frame_view* f2, float* prev_xy,
+                                  int32_t* matches12, int window) {
+    if (!m || !f1 || !f2 || !prev_xy || !matches12 || f1->n < 0 || f2->n < 0) return ORB_EINVAL;
+    if (f2->n >= (1 << 20)) return ORB_EINVAL;
+    ORB_HIP_TRY(hipSetDevice(m->device));
+    const int cap = std::max(std::max(f1->n, f2->n), 1);
+    int st = mensure(m, 1, cap);
+    if (st) return st;
+    const size_t bytes = (size_t)cap * (2 * sizeof(orb_keypoint) + 64 + 8 + 4) + 64;
+    st = mpin(m, bytes);
+    if (st) return st;
+    char* h = (char*)m->h_pin;
+    orb_keypoint* hk1 = (orb_keypoint*)h;
+    orb_keypoint* hk2 = hk1 + cap;
+    uint8_t* hd1 = (uint8_t*)(hk2 + cap);
+    uint8_t* hd2 = hd1 + (size_t)cap * 32;
+    float* hprev = (float*)(hd2 + (size_t)cap * 32);
+    int32_t* hn = (int32_t*)(hprev + 2 * (size_t)cap);
+    pack_view(f1, hk1);
+    pack_view(f2, hk2);
+    std::memcpy(hd1, f1->desc, (size_t)f1->n * 32);
+    std::memcpy(hd2, f2->desc, (size_t)f2->n * 32);
+    std::memcpy(hprev, prev_xy, (size_t)f1->n * 8);
+    hn[0] = f1->n;
+    hn[1] = f2->n;
+    hipStream_t s = m->stream;
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_k1, hk1, (size_t)f1->n * sizeof(orb_keypoint), hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_k2, hk2, (size_t)f2->n * sizeof(orb_keypoint), hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_d1, hd1, (size_t)f1->n * 32, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_d2, hd2, (size_t)f2->n * 32, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_prev, hprev, (size_t)f1->n * 8, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_n, hn, 8, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemsetAsync(m->d_status, 0, 4, s));
+    const GridParams g = grid_of(f2);
+    hipLaunchKernelGGL(k_cand_sfi, dim3((cap + 3) / 4, 1), dim3(256), 0, s, m->d_k1, m->d_d1, m->d_n, m->d_k2, m->d_d2,
+                       m->d_n + 1, m->d_prev, cap, g, (float)window, m->d_cand, m->d_ncand, m->d_status);
+    const size_t lds = (3 * (size_t)cap + kHisto + 4) * 4;
+    hipLaunchKernelGGL(k_resolve_sfi, dim3(1), dim3(64), lds, s, m->d_k1, m->d_n, m->d_k2, m->d_n + 1, cap, g,
+                       m->nnratio, m->checkOri, m->d_cand, m->d_ncand, m->d_prev, m->d_m12, m->d_nm, m->d_hI, m->d_hB);
+    ORB_HIP_TRY(hipGetLastError());
+    int32_t* hm = (int32_t*)hd1;   // reuse pinned space
+    ORB_HIP_TRY(hipMemcpyAsync(hm, m->d_m12, (size_t)f1->n * 4, hipMemcpyDeviceToHost, s));
+    ORB_HIP_TRY(hipMemcpyAsync(hprev, m->d_prev, (size_t)f1->n * 8, hipMemcpyDeviceToHost, s));
+    ORB_HIP_TRY(hipMemcpyAsync(hn, m->d_nm, 4, hipMemcpyDeviceToHost, s));
+    ORB_HIP_TRY(hipMemcpyAsync(hn + 1, m->d_status, 4, hipMemcpyDeviceToHost, s));
+    ORB_HIP_TRY(hipStreamSynchronize(s));
+    if (hn[1]) return ORB_EOVERFLOW;
+    std::memcpy(matches12, hm, (size_t)f1->n * 4);
+    std::memcpy(prev_xy, hprev, (size_t)f1->n * 8);
+    return hn[0];
+}
+
+int orb_search_for_initialization_batch_device(orb_matcher* m, const orb_keypoint* d_kps1, const uint8_t* d_desc1,
+                                               const int32_t* d_n1, const orb_keypoint* d_kps2, const uint8_t* d_desc2,
+                                               const int32_t* d_n2, int nb, int cap, int width, int height, int window,
+                                               int32_t* d_matches12, int32_t* d_nmatches, void* stream) {
+    if (!m || nb <= 0 || cap <= 0 || width <= 0 || height <= 0) return ORB_EINVAL;
+    ORB_HIP_TRY(hipSetDevice(m->device));
+    int st = mensure(m, nb, cap);
+    if (st) return st;
+    hipStream_t s = stream ? (hipStream_t)stream : m->stream;
+    GridParams g;
+    g.min_x = 0.f; g.min_y = 0.f; g.max_x = (float)width; g.max_y = (float)height;
+    g.winv = (float)kGridCols / (float)width;
+    g.hinv = (float)kGridRows / (float)height;
+    hipLaunchKernelGGL(k_cand_sfi, dim3((cap + 3) / 4, nb), dim3(256), 0, s, d_kps1, d_desc1, d_n1, d_kps2, d_desc2, d_n2,
+                       (const float*)nullptr, cap, g, (float)window, m->d_cand, m->d_ncand, m->d_status);
+    const size_t lds = (3 * (size_t)cap + kHisto + 4) * 4;
+    hipLaunchKernelGGL(k_resolve_sfi, dim3(nb), dim3(64), lds, s, d_kps1, d_n1, d_kps2, d_n2, cap, g, m->nnratio,
+                       m->checkOri, m->d_cand, m->d_ncand, (float*)nullptr, d_matches12, d_nmatches, m->d_hI, m->d_hB);
+    ORB_HIP_TRY(hipGetLastError());
+    return ORB_OK;
+}
+
+int orb_search_by_projection_frame(orb_matcher* m, const orb_frame_view* cur, const float* Tcw_cur,
+                                   const orb_frame_view* last, const float* Tcw_last, const int32_t* last_has_mp,
+                                   const uint8_t* last_outlier, const float* last_mp_xyz, const uint8_t* last_mp_desc,
+                                   const float* scale_factors, const float cam[6], float th, int mono, int32_t* cur_mp) {
+    if (!m || !cur || !last || !Tcw_cur || !Tcw_last || !last_has_mp || !last_outlier || !last_mp_xyz ||
+        !last_mp_desc || !scale_factors || !cam || !cur_mp)
+        return ORB_EINVAL;
+    if (cur->n >= (1 << 20)) return ORB_EINVAL;
+    ORB_HIP_TRY(hipSetDevice(m->device));
+    const int cap = std::max(std::max(cur->n, last->n), 1);
+    int st = mensure(m, 1, cap);
+    if (st) return st;
+    // tlc = Rlw * twc + tlw with twc = -Rcw^T tcw (float Mat products, double accumulation)
+    float twc[3], tlc[3];
+    for (int c = 0; c < 3; c++) {
+        double s = 0;
+        for (int r = 0; r < 3; r++) s += (double)Tcw_cur[4 * r + c] * (double)Tcw_cur[4 * r + 3];
+        twc[c] = (float)(-s);
+    }
+    for (int r = 0; r < 3; r++) {
+        const double s = (double)Tcw_last[4 * r] * twc[0] + (double)Tcw_last[4 * r + 1] * twc[1] +
+                         (double)Tcw_last[4 * r + 2] * twc[2];
+        tlc[r] = (float)(s + (double)Tcw_last[4 * r + 3]);
+    }
+    SbpCam c;
+    c.fx = cam[0]; c.fy = cam[1]; c.cx = cam[2]; c.cy = cam[3]; c.mbf = cam[4]; c.mb = cam[5];
+    const int bForward = tlc[2] > c.mb && !mono;
+    const int bBackward = -tlc[2] > c.mb && !mono;
+    const size_t bytes = (size_t)cap * (2 * sizeof(orb_keypoint) + 32 + 32 + 4 + 4 + 1 + 12 + 4) + 1024;
+    st = mpin(m, bytes);
+    if (st) return st;
+    char* h = (char*)m->h_pin;
+    orb_keypoint* hkc = (orb_keypoint*)h;
+    orb_keypoint* hkl = hkc + cap;
+    uint8_t* hdc = (uint8_t*)(hkl + cap);
+    uint8_t* hmd = hdc + (size_t)cap * 32;
+    float* hur = (float*)(hmd + (size_t)cap * 32);
+    int32_t* hcm = (int32_t*)(hur + cap);
+    float* hxyz = (float*)(hcm + cap);
+    int32_t* hhas = (int32_t*)(hxyz + 3 * (size_t)cap);
+    uint8_t* hout = (uint8_t*)(hhas + cap);
+    float* hT = (float*)(((uintptr_t)(hout + cap) + 15) & ~(uintptr_t)15);
+    float* hsf = hT + 16;
+    int32_t* hn = (int32_t*)(hsf + 32);
+    pack_view(cur, hkc);
+    pack_view(last, hkl);
+    std::memcpy(hdc, cur->desc, (size_t)cur->n * 32);
+    std::memcpy(hmd, last_mp_desc, (size_t)last->n * 32);
+    for (int i = 0; i < cur->n; i++) hur[i] = cur->uright ? cur->uright[i] : -1.f;
+    std::memcpy(hcm, cur_mp, (size_t)cur->n * 4);
+    std::memcpy(hxyz, last_mp_xyz, (size_t)last->n * 12);
+    std::memcpy(hhas, last_has_mp, (size_t)last->n * 4);
+    std::memcpy(hout, last_outlier, (size_t)last->n);
+    std::memcpy(hT, Tcw_cur, 12 * 4);
+    int maxOct = 0;
+    for (int i = 0; i < last->n; i++) maxOct = std::max(maxOct, (int)last->octave[i]);
+    for (int i = 0; i <= maxOct && i < 32; i++) hsf[i] = scale_factors[i];
+    hipStream_t s = m->stream;
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_k2, hkc, (size_t)cur->n * sizeof(orb_keypoint), hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_k1, hkl, (size_t)last->n * sizeof(orb_keypoint), hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_d2, hdc, (size_t)cur->n * 32, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_mpd, hmd, (size_t)last->n * 32, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_ur, hur, (size_t)cur->n * 4, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_m12, hcm, (size_t)cur->n * 4, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_xyz, hxyz, (size_t)last->n * 12, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_hasMp, hhas, (size_t)last->n * 4, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_outl, hout, (size_t)last->n, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_T, hT, 12 * 4, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_sf, hsf, 32 * 4, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemsetAsync(m->d_status, 0, 4, s));
+    const GridParams g = grid_of(cur);
+    if (last->n > 0) {
+        hipLaunchKernelGGL(k_cand_sbp, dim3((last->n + 3) / 4), dim3(256), 0, s, m->d_k2, m->d_d2,
+                           cur->uright ? (const float*)m->d_ur : (const float*)nullptr, cur->n, m->d_k1, last->n,
+                           m->d_hasMp, m->d_outl, m->d_xyz, m->d_mpd, m->d_T, m->d_sf, c, g, th, bForward, bBackward,
+                           m->d_cand, m->d_ncand, m->d_status);
+    }
+    const size_t lds = ((size_t)cur->n + kHisto + 4) * 4;
+    hipLaunchKernelGGL(k_resolve_sbp, dim3(1), dim3(64), lds, s, m->d_k2, cur->n, m->d_k1, last->n, g, m->checkOri,
+                       m->d_cand, m->d_ncand, m->d_m12, m->d_nm, m->d_hI, m->d_hB);
+    ORB_HIP_TRY(hipGetLastError());
+    ORB_HIP_TRY(hipMemcpyAsync(hcm, m->d_m12, (size_t)cur->n * 4, hipMemcpyDeviceToHost, s));
+    ORB_HIP_TRY(hipMemcpyAsync(hn, m->d_nm, 4, hipMemcpyDeviceToHost, s));
+    ORB_HIP_TRY(hipMemcpyAsync(hn + 1, m->d_status, 4, hipMemcpyDeviceToHost, s));
+    ORB_HIP_TRY(hipStreamSynchronize(s));
+    if (hn[1]) return ORB_EOVERFLOW;
+    std::memcpy(cur_mp, hcm, (size_t)cur->n * 4);
+    return hn[0];
+}
+
+int orb_hamming_knn2(orb_matcher* m, const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* best_idx,
+                     int32_t* best_d, int32_t* second_d) {
+    if (!m || nq < 0 || nt < 0 || (nq && (!q || !best_idx || !best_d || !second_d)) || (nt && !t)) return ORB_EINVAL;
+    if (nq == 0) return ORB_OK;
+    ORB_HIP_TRY(hipSetDevice(m->device));
+    const int cap = std::max(std::max(nq, nt), 1);
+    int st = mensure(m, 1, cap);
+    if (st) return st;
+    st = mpin(m, (size_t)cap * 64 + (size_t)nq * 12 + 64);
+    if (st) return st;
+    uint8_t* hq = (uint8_t*)m->h_pin;
+    uint8_t* ht = hq + (size_t)cap * 32;
+    int32_t* hn = (int32_t*)(ht + (size_t)cap * 32);
+    int32_t* hout = hn + 4;
+    std::memcpy(hq, q, (size_t)nq * 32);
+    if (nt) std::memcpy(ht, t, (size_t)nt * 32);
+    hn[0] = nq;
+    hn[1] = nt;
+    hipStream_t s = m->stream;
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_d1, hq, (size_t)nq * 32, hipMemcpyHostToDevice, s));
+    if (nt) ORB_HIP_TRY(hipMemcpyAsync(m->d_d2, ht, (size_t)nt * 32, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_n, hn, 8, hipMemcpyHostToDevice, s));
+    int32_t* d_bi = m->d_m12;
+    int32_t* d_bd = m->d_hI;
+    int32_t* d_sd = (int32_t*)m->d_ncand;
+    hipLaunchKernelGGL(k_knn2, dim3((nq + 3) / 4, 1), dim3(256), 0, s, m->d_d1, m->d_n, m->d_d2, m->d_n + 1, cap, cap,
+                       d_bi, d_bd, d_sd);
+    ORB_HIP_TRY(hipGetLastError());
+    ORB_HIP_TRY(hipMemcpyAsync(hout, d_bi, (size_t)nq * 4, hipMemcpyDeviceToHost, s));
+    ORB_HIP_TRY(hipMemcpyAsync(hout + nq, d_bd, (size_t)nq * 4, hipMemcpyDeviceToHost, s));
+    ORB_HIP_TRY(hipMemcpyAsync(hout + 2 * (size_t)nq, d_sd, (size_t)nq * 4, hipMemcpyDeviceToHost, s));
+    ORB_HIP_TRY(hipStreamSynchronize(s));
+    std::memcpy(best_idx, hout, (size_t)nq * 4);
+    std::memcpy(best_d, hout + nq, (size_t)nq * 4);
+    std::memcpy(second_d, hout + 2 * (size_t)nq, (size_t)nq * 4);
+    return ORB_OK;
+}
+
+int orb_hamming_knn2_batch_device(orb_matcher* m, const uint8_t* d_q, const int32_t* d_nq, const uint8_t* d_t,
+                                  const int32_t* d_nt, int nb, int q_stride_rows, int t_stride_rows, int32_t* d_best_idx,
+                                  int32_t* d_best_d, int32_t* d_second_d, void* stream) {
+    if (!m || !d_q || !d_nq || !d_t || !d_nt || nb <= 0 || q_stride_rows <= 0 || t_stride_rows <= 0) return ORB_EINVAL;
+    ORB_HIP_TRY(hipSetDevice(m->device));
+    hipStream_t s = stream ? (hipStream_t)stream : m->stream;
+    hipLaunchKernelGGL(k_knn2, dim3((q_stride_rows + 3) / 4, nb), dim3(256), 0, s, d_q, d_nq, d_t, d_nt, q_stride_rows,
+                       t_stride_rows, d_best_idx, d_best_d, d_second_d);
+    ORB_HIP_TRY(hipGetLastError());
+    return ORB_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,125 @@
+"""Host mirror of ORB_SLAM2::ORBmatcher (R/include/ORBmatcher.h:37-143) over
+the HIP C-ABI: DescriptorDistance, SearchForInitialization,
+SearchByProjection(Frame&, const Frame&, th, bMono) and a brute-force 2-NN."""
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+
+from . import _abi
+
+FRAME_GRID_COLS = 64
+FRAME_GRID_ROWS = 48
+
+
+@dataclass
+class Frame:
+    """The subset of ORB_SLAM2::Frame the matcher reads (R/include/Frame.h)."""
+    mvKeysUn: np.ndarray                 # KEYPOINT_DTYPE
+    mDescriptors: np.ndarray             # [N, 32] uint8
+    width: int = 640
+    height: int = 480
+    mvuRight: Optional[np.ndarray] = None
+    mnMinX: float = 0.0
+    mnMinY: float = 0.0
+    mnMaxX: Optional[float] = None
+    mnMaxY: Optional[float] = None
+    mTcw: Optional[np.ndarray] = None    # 4x4 float32
+    mvScaleFactors: Optional[np.ndarray] = None
+    extra: dict = field(default_factory=dict)
+
+    def __post_init__(self):
+        if self.mnMaxX is None:
+            self.mnMaxX = float(self.width)
+        if self.mnMaxY is None:
+            self.mnMaxY = float(self.height)
+
+    @property
+    def N(self):
+        return len(self.mvKeysUn)
+
+    def view(self):
+        """orb_frame_view; keeps the arrays alive on the returned object."""
+        k = self.mvKeysUn
+        x = np.ascontiguousarray(k["x"], np.float32)
+        y = np.ascontiguousarray(k["y"], np.float32)
+        a = np.ascontiguousarray(k["angle"], np.float32)
+        o = np.ascontiguousarray(k["octave"], np.int32)
+        d = np.ascontiguousarray(self.mDescriptors, np.uint8)
+        ur = None if self.mvuRight is None else np.ascontiguousarray(self.mvuRight, np.float32)
+        winv = np.float32(FRAME_GRID_COLS) / np.float32(self.mnMaxX - self.mnMinX)
+        hinv = np.float32(FRAME_GRID_ROWS) / np.float32(self.mnMaxY - self.mnMinY)
+        v = _abi.FrameView(len(x), _abi.ptr(x), _abi.ptr(y), _abi.ptr(a), _abi.ptr(o), _abi.ptr(d), _abi.ptr(ur),
+                           self.mnMinX, self.mnMinY, self.mnMaxX, self.mnMaxY, float(winv), float(hinv))
+        v._keep = (x, y, a, o, d, ur)
+        return v
+
+
+class ORBmatcher:
+    TH_HIGH = 100
+    TH_LOW = 50
+    HISTO_LENGTH = 30
+
+    def __init__(self, nnratio: float = 0.6, checkOri: bool = True, device: int = 0):
+        self.mfNNratio, self.mbCheckOrientation = float(nnratio), bool(checkOri)
+        h = C.c_void_p()
+        _abi.check("orb_matcher_create", _abi.lib().orb_matcher_create(device, C.c_float(nnratio), int(checkOri),
+                                                                        C.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _abi.lib().orb_matcher_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    @staticmethod
+    def DescriptorDistance(a, b) -> int:
+        a = np.ascontiguousarray(a, np.uint8)
+        b = np.ascontiguousarray(b, np.uint8)
+        return _abi.check("orb_descriptor_distance", _abi.lib().orb_descriptor_distance(_abi.ptr(a), _abi.ptr(b)))
+
+    def SearchForInitialization(self, F1: Frame, F2: Frame, vbPrevMatched: np.ndarray, windowSize: int = 10):
+        """Returns (nmatches, vnMatches12); vbPrevMatched ([N1, 2] float32) is updated in place."""
+        prev = np.ascontiguousarray(vbPrevMatched, np.float32)
+        m12 = np.zeros(F1.N, np.int32)
+        v1, v2 = F1.view(), F2.view()
+        n = _abi.check("orb_search_for_initialization", _abi.lib().orb_search_for_initialization(
+            self._h, C.byref(v1), C.byref(v2), _abi.ptr(prev), _abi.ptr(m12), int(windowSize)))
+        if prev is not vbPrevMatched:
+            vbPrevMatched[...] = prev
+        return n, m12
+
+    def SearchByProjection(self, CurrentFrame: Frame, LastFrame: Frame, th: float, bMono: bool,
+                           last_has_mp, last_outlier, last_mp_xyz, last_mp_desc, cam, cur_mp=None):
+        """SearchByProjection(Frame&, const Frame&, th, bMono).  Map points of the last
+        frame are passed explicitly per last keypoint; returns (nmatches, cur_mp) where
+        cur_mp[i2] = index of the last-frame keypoint whose map point was assigned."""
+        if cur_mp is None:
+            cur_mp = np.full(CurrentFrame.N, -1, np.int32)
+        cur_mp = np.ascontiguousarray(cur_mp, np.int32).copy()
+        vc, vl = CurrentFrame.view(), LastFrame.view()
+        Tc = np.ascontiguousarray(np.asarray(CurrentFrame.mTcw, np.float32)[:3, :4])
+        Tl = np.ascontiguousarray(np.asarray(LastFrame.mTcw, np.float32)[:3, :4])
+        has = np.ascontiguousarray(last_has_mp, np.int32)
+        out = np.ascontiguousarray(last_outlier, np.uint8)
+        xyz = np.ascontiguousarray(last_mp_xyz, np.float32)
+        md = np.ascontiguousarray(last_mp_desc, np.uint8)
+        sf = np.ascontiguousarray(CurrentFrame.mvScaleFactors, np.float32)
+        camv = np.ascontiguousarray(cam, np.float32)
+        n = _abi.check("orb_search_by_projection_frame", _abi.lib().orb_search_by_projection_frame(
+            self._h, C.byref(vc), _abi.ptr(Tc), C.byref(vl), _abi.ptr(Tl), _abi.ptr(has), _abi.ptr(out),
+            _abi.ptr(xyz), _abi.ptr(md), _abi.ptr(sf), _abi.ptr(camv), C.c_float(th), int(bMono),
+            _abi.ptr(cur_mp)))
+        return n, cur_mp
+
+    def knn2(self, q, t):
+        q = np.ascontiguousarray(q, np.uint8)
+        t = np.ascontiguousarray(t, np.uint8)
+        bi, bd, sd = (np.zeros(len(q), np.int32) for _ in range(3))
+        _abi.check("orb_hamming_knn2", _abi.lib().orb_hamming_knn2(
+            self._h, _abi.ptr(q), len(q), _abi.ptr(t), len(t), _abi.ptr(bi), _abi.ptr(bd), _abi.ptr(sd)))
+        return bi, bd, sd
