@@ -1,0 +1,228 @@
+"""Benchmark: frames/s of ORB extract + match at 640x480 (BASELINE.json config 2:
+synthetic 640x480 grayscale stream, 1000 features/frame, 8 levels, 1 MI355X),
+plus local-BA ms/iter on the 20 KF x 3000 point problem when --lba is on.
+
+A step = one batch of B frames already resident in HBM: ORBextractor::operator()
+on every frame (liborbslam2_amd.so, HIP) followed by
+ORBmatcher::SearchForInitialization(frame t-1, frame t, window 100, nnratio 0.9,
+checkOri) for every consecutive pair.  Multi-GPU: one process per GPU, frames
+shard across ranks with no data-path collective (weak scaling); the only
+collectives are the timing barrier and the max-over-ranks of the elapsed time.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import concurrent.futures as cf
+import ctypes as C
+import json
+import os
+import pathlib
+import sys
+import time
+
+ROOT = pathlib.Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import pkgload  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md)
+STAGES = ["resize", "fast_score", "cell_detect", "octree", "blur", "orient_desc"]
+KERNELS = ["k_resize", "k_fast_score", "k_cell_detect", "k_octree", "k_blur", "k_orient_desc"]
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=64, help="frames per step per GPU")
+    ap.add_argument("--width", type=int, default=640)
+    ap.add_argument("--height", type=int, default=480)
+    ap.add_argument("--nfeatures", type=int, default=1000)
+    ap.add_argument("--pool", type=int, default=256, help="distinct synthetic frames resident in HBM")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    return ap.parse_args()
+
+
+def algorithmic_bytes(stage, lw, lh, n_pre, n_out):
+    """Per-frame algorithmic HBM bytes of each stage."""
+    P = (lw.astype(np.int64) * lh).tolist()
+    if stage == "resize":
+        return sum(P[l - 1] + P[l] for l in range(1, len(P)))
+    if stage in ("fast_score", "blur"):
+        return 2 * sum(P)
+    if stage == "cell_detect":
+        return sum(P) + 4 * n_pre
+    if stage == "octree":
+        return 4 * (n_pre + n_out)
+    if stage == "orient_desc":
+        return n_out * (749 + 512 + 28 + 32)
+    raise KeyError(stage)
+
+
+def cpu_baseline(frames, nfeatures, budget_s):
+    """Oracle (C restatement of the reference, -O2, 1 thread per frame) on a bounded sample."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_ref as O
+    p = O.params(nfeatures)
+    W, H = frames.shape[2], frames.shape[1]
+    threads = max(1, min(16, os.cpu_count() or 1))
+
+    def one(i):
+        a = O.extract(p, frames[i])
+        return a
+
+    # calibrate on 4 frames, then size the sample to the budget
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(threads) as pool:
+        list(pool.map(one, range(min(4 * threads, len(frames)))))
+    t_cal = (time.perf_counter() - t0) / min(4 * threads, len(frames))
+    n = int(max(threads, min(len(frames) - 1, budget_s / max(t_cal, 1e-4))))
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(threads) as pool:
+        res = list(pool.map(one, range(n + 1)))
+
+        def match(i):
+            a, b = res[i], res[i + 1]
+            fa = O.FrameView(a["kps"], a["desc"], W, H)
+            fb = O.FrameView(b["kps"], b["desc"], W, H)
+            prev = np.stack([a["kps"]["x"], a["kps"]["y"]], 1).astype(np.float32).reshape(-1)
+            return O.search_for_initialization(fa, fb, prev, nnratio=0.9, window=100)[0]
+
+        list(pool.map(match, range(n)))
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 2), "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{n + 1} frames extracted + {n} SearchForInitialization pairs, {W}x{H}, "
+                      f"{nfeatures} feat, oracle C restatement, {threads} host threads (1 frame per thread)"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    amd = pkgload.load()
+    from orb_slam2_amd import _abi, synth
+
+    W, H, B, NF = args.width, args.height, args.batch, args.nfeatures
+    # ---- synthetic stream resident in HBM (seed per rank: shards are independent streams)
+    cv = synth.canvas(0x5EED0002 + 1000 * rank, W, H)
+    pool_np = np.stack([synth.frame(cv, W, H, t) for t in range(max(args.pool, B))])
+    pool = torch.from_numpy(pool_np).to(dev)
+    ex = amd.ORBextractor(NF, 1.2, 8, 20, 7, device=local, max_w=W, max_h=H, max_batch=B)
+    lw, lh, cells = (np.zeros(8, np.int32) for _ in range(3))
+    cap = C.c_int()
+    _abi.check("orb_extractor_geometry", _abi.lib().orb_extractor_geometry(
+        ex._h, W, H, _abi.ptr(lw), _abi.ptr(lh), _abi.ptr(cells), C.byref(cap)))
+    cap = cap.value
+    m = amd.ORBmatcher(0.9, True, device=local)
+    # frame slot 0 holds the previous step's last frame (pair t-1, t across step boundaries)
+    kps = torch.zeros((B + 1, cap, 7), dtype=torch.int32, device=dev)
+    desc = torch.zeros((B + 1, cap, 32), dtype=torch.uint8, device=dev)
+    counts = torch.zeros(B + 1, dtype=torch.int32, device=dev)
+    m12 = torch.zeros((B, cap), dtype=torch.int32, device=dev)
+    nm = torch.zeros(B, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    lib = _abi.lib()
+    row_kp, row_d = cap * 28, cap * 32
+
+    def step(s):
+        start = (s * B) % (pool.shape[0] - B + 1)
+        imgs = pool[start:start + B]
+        kps[0].copy_(kps[B])
+        desc[0].copy_(desc[B])
+        counts[0:1].copy_(counts[B:B + 1])
+        _abi.check("orb_extract_batch_device", lib.orb_extract_batch_device(
+            ex._h, C.c_void_p(imgs.data_ptr()), H * W, B, W, H, C.c_void_p(kps.data_ptr() + row_kp),
+            C.c_void_p(desc.data_ptr() + row_d), cap, C.c_void_p(counts.data_ptr() + 4), C.c_void_p(stream)))
+        _abi.check("orb_search_for_initialization_batch_device", lib.orb_search_for_initialization_batch_device(
+            m._h, C.c_void_p(kps.data_ptr()), C.c_void_p(desc.data_ptr()), C.c_void_p(counts.data_ptr()),
+            C.c_void_p(kps.data_ptr() + row_kp), C.c_void_p(desc.data_ptr() + row_d),
+            C.c_void_p(counts.data_ptr() + 4), B, cap, W, H, 100, C.c_void_p(m12.data_ptr()),
+            C.c_void_p(nm.data_ptr()), C.c_void_p(stream)))
+
+    for s in range(args.warmup):
+        step(s)
+    torch.cuda.synchronize(dev)
+    if not args.no_profile:
+        lib.orb_extractor_profile(ex._h, 1)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        step(args.warmup + s)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+    # stage times (HIP events recorded on the launch stream during the timed region)
+    stage_ms = np.zeros(6)
+    ncalls = C.c_int(0)
+    if not args.no_profile:
+        lib.orb_extractor_stage_times(ex._h, _abi.ptr(stage_ms), 6, C.byref(ncalls))
+        lib.orb_extractor_profile(ex._h, 0)
+    frames_total = B * args.steps * world
+    value = frames_total / dt
+    cnt = counts[1:].cpu().numpy()
+    nmatch = nm.cpu().numpy()
+
+    result = {
+        "metric": "frames/sec ORB extract+match @640x480",
+        "value": round(value, 2),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000 * dt / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic",
+        "config": {"workload": f"synthetic {W}x{H} grayscale stream, {NF} feat/frame, 8 levels, scale 1.2, "
+                               f"FAST 20/7; extract + SearchForInitialization(t-1,t; window 100, nnratio 0.9, "
+                               f"checkOri) per frame; {B} frames per step per GPU, HBM-resident",
+                   "batch_per_gpu": B, "width": W, "height": H, "nfeatures": NF,
+                   "parallelism": f"frame-sharded x{world}"},
+        "keypoints_per_frame": float(np.mean(cnt)),
+        "matches_per_pair": float(np.mean(nmatch)),
+    }
+    if not args.no_profile and ncalls.value > 0:
+        per_launch_ms = stage_ms / ncalls.value
+        dom = int(np.argmax(per_launch_ms))
+        n_out = float(np.mean(cnt))
+        pre = np.zeros(8, np.int32)
+        lib.orb_extractor_last_counts(ex._h, 0, _abi.ptr(pre), None)
+        n_pre = float(pre.sum())
+        bytes_per_launch = algorithmic_bytes(STAGES[dom], lw, lh, n_pre, n_out) * B
+        achieved = bytes_per_launch / (per_launch_ms[dom] * 1e-3) / 1e9
+        result["roofline"] = {"bound": "hbm", "kernel": KERNELS[dom], "achieved": round(achieved, 2),
+                              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                              "traffic": None,
+                              "launch_ms": round(float(per_launch_ms[dom]), 4)}
+        result["stage_ms_per_batch"] = {k: round(float(v), 4) for k, v in zip(STAGES, per_launch_ms)}
+    if rank == 0 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(pool_np[: min(len(pool_np), 512)], NF, args.cpu_seconds)
+        result["speedup_vs_cpu_baseline"] = round(value / result["cpu_baseline"]["value"], 1)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -96,6 +96,25 @@ int orb_pyramid_level(orb_extractor* ex, int frame, int level, const uint8_t** h
 int orb_pyramid_level_device(orb_extractor* ex, int frame, int level, int blurred,
                              const uint8_t** dptr, int* w, int* h, size_t* pitch);
 
+/* Stage profiling: while enabled, every extraction records HIP events on its
+ * launch stream around the six kernel stages (0 resize, 1 fast_score,
+ * 2 cell_detect, 3 octree, 4 blur, 5 orient_desc).  orb_extractor_stage_times
+ * waits for them, writes the summed milliseconds per stage to ms[0..n_stages)
+ * and the number of profiled calls to *n_calls, then resets; returns the number
+ * of stages. */
+int orb_extractor_profile(orb_extractor* ex, int enable);
+int orb_extractor_stage_times(orb_extractor* ex, double* ms, int n_stages, int* n_calls);
+
+/* Level geometry for a w x h input (level sizes, FAST cells per level) and the
+ * per-frame keypoint capacity the device batch path needs (cap >= this value
+ * never truncates). */
+int orb_extractor_geometry(orb_extractor* ex, int w, int h, int* level_w, int* level_h,
+                           int* cells_per_level, int* max_keypoints_per_frame);
+
+/* Per-level FAST keypoint counts before DistributeOctTree and retained counts
+ * after it, for frame `frame` of the last extraction (diagnostics / roofline). */
+int orb_extractor_last_counts(orb_extractor* ex, int frame, int* pre_counts, int* level_counts);
+
 /* --------------------------------------------------------------- matcher */
 
 typedef struct orb_matcher orb_matcher;

@@ -56,6 +56,10 @@ def lib() -> C.CDLL:
             "orb_extract_batch_device": [vp, vp, sz, i32, i32, i32, vp, vp, i32, vp, vp],
             "orb_pyramid_level": [vp, i32, i32, vp, vp, vp, vp],
             "orb_pyramid_level_device": [vp, i32, i32, i32, vp, vp, vp, vp],
+            "orb_extractor_profile": [vp, i32],
+            "orb_extractor_stage_times": [vp, vp, i32, vp],
+            "orb_extractor_geometry": [vp, i32, i32, vp, vp, vp, vp],
+            "orb_extractor_last_counts": [vp, i32, vp, vp],
             "orb_matcher_create": [i32, f32, i32, vp],
             "orb_matcher_destroy": [vp],
             "orb_descriptor_distance": [vp, vp],

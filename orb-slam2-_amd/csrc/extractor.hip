@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <array>
 #include <mutex>
 #include <vector>
 
@@ -1167,6 +1168,10 @@ int check_device(int dev) {
 
 using namespace orbamd;
 
+// Pipeline stages timed by orb_extractor_stage_times(): resize, fast_score, cell_detect,
+// octree, blur, orient_desc.
+constexpr int kStages = 6;
+
 struct orb_extractor {
     orb_extractor_params p;
     int device = 0;
@@ -1192,6 +1197,12 @@ struct orb_extractor {
     std::vector<uint8_t> h_levels;
     std::vector<char> h_level_valid;
     int lastB = 0;
+    // stage profiling (HIP events on the launch stream)
+    bool profile = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::array<hipEvent_t, kStages + 1>> ev_sets;
+    double stage_ms[kStages] = {0};
+    int stage_calls = 0;
 };
 
 static void free_dev(void* p) {
@@ -1273,26 +1284,57 @@ static size_t octree_lds_bytes(const Geom& g) {
 }
 
 // Enqueues the full pipeline for B frames already resident in d_pyr level 0.
+static hipEvent_t ev_get(orb_extractor* ex) {
+    if (!ex->ev_pool.empty()) {
+        hipEvent_t e = ex->ev_pool.back();
+        ex->ev_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+// Enqueues the full pipeline for B frames already resident in d_pyr level 0.
 static int run_pipeline(orb_extractor* ex, int B, orb_keypoint* d_kps, uint8_t* d_desc, int cap, int32_t* d_counts,
                         hipStream_t st) {
     const Geom& g = ex->g;
+    std::array<hipEvent_t, kStages + 1> ev{};
+    const bool prof = ex->profile;
+    if (prof) {
+        for (auto& e : ev) {
+            e = ev_get(ex);
+            if (!e) return ORB_EGPU;
+        }
+    }
+    auto mark = [&](int i) {
+        if (prof) (void)hipEventRecord(ev[i], st);
+    };
     ORB_HIP_TRY(hipMemsetAsync(ex->d_status, 0, 4, st));
+    mark(0);
     for (int l = 1; l < g.nlevels; l++) {
         const LevelGeom& L = g.lv[l];
         dim3 grid((L.w + 255) / 256, (L.h + 3) / 4, B), block(64, 4);
         hipLaunchKernelGGL(k_resize, grid, block, 0, st, g, l, ex->d_pyr);
     }
+    mark(1);
     hipLaunchKernelGGL(k_fast_score, dim3(g.tilesPerFrame, B), dim3(256), 0, st, g, ex->d_pyr, ex->d_score);
+    mark(2);
     hipLaunchKernelGGL(k_cell_detect, dim3((g.cellsPerFrame + 3) / 4, B), dim3(256), 0, st, g, ex->d_score,
                        ex->d_slots, ex->d_cellCount, ex->d_status);
+    mark(3);
     const size_t lds = octree_lds_bytes(g);
     hipLaunchKernelGGL(k_octree, dim3(g.nlevels, B), dim3(OT_T), lds, st, g, ex->d_slots, ex->d_cellCount,
                        ex->d_keyA, ex->d_keyB, ex->d_outKeys, ex->d_levelCount, ex->d_status);
+    mark(4);
     hipLaunchKernelGGL(k_blur, dim3(g.tilesPerFrame, B), dim3(256), 0, st, g, ex->d_pyr, ex->d_blur, ex->blurK[0],
                        ex->blurK[1], ex->blurK[2], ex->blurK[3]);
+    mark(5);
     hipLaunchKernelGGL(k_orient_desc, dim3((g.outPerFrame + 3) / 4, B), dim3(256), 0, st, g, ex->d_pyr, ex->d_blur,
                        ex->d_outKeys, ex->d_levelCount, d_kps, d_desc, cap, d_counts);
+    mark(6);
     ORB_HIP_TRY(hipGetLastError());
+    if (prof) ex->ev_sets.push_back(ev);
     return ORB_OK;
 }
 
@@ -1344,6 +1386,9 @@ void orb_extractor_destroy(orb_extractor* ex) {
     (void)hipSetDevice(ex->device);
     if (ex->stream) (void)hipStreamSynchronize(ex->stream);
     release_buffers(ex);
+    for (auto& set : ex->ev_sets)
+        for (auto e : set) ex->ev_pool.push_back(e);
+    for (auto e : ex->ev_pool) (void)hipEventDestroy(e);
     if (ex->h_stage) (void)hipHostFree(ex->h_stage);
     if (ex->h_out) (void)hipHostFree(ex->h_out);
     if (ex->stream) (void)hipStreamDestroy(ex->stream);
@@ -1433,7 +1478,6 @@ int orb_extract_batch_device(orb_extractor* ex, const uint8_t* d_imgs, size_t im
     if (st) return st;
     hipStream_t s = stream ? (hipStream_t)stream : ex->stream;
     const Geom& g = ex->g;
-    const LevelGeom& L0 = g.lv[0];
     hipLaunchKernelGGL(k_load_frames, dim3((w + 255) / 256, h, B), dim3(64), 0, s, g, d_imgs, img_stride_frame,
                        ex->d_pyr);
     ORB_HIP_TRY(hipGetLastError());
@@ -1475,6 +1519,68 @@ int orb_pyramid_level_device(orb_extractor* ex, int frame, int level, int blurre
     if (w) *w = L.w;
     if (h) *h = L.h;
     if (pitch) *pitch = (size_t)L.pitch;
+    return ORB_OK;
+}
+
+int orb_extractor_profile(orb_extractor* ex, int enable) {
+    if (!ex) return ORB_EINVAL;
+    ex->profile = enable != 0;
+    return ORB_OK;
+}
+
+int orb_extractor_stage_times(orb_extractor* ex, double* ms, int n_stages, int* n_calls) {
+    if (!ex || (n_stages > 0 && !ms)) return ORB_EINVAL;
+    ORB_HIP_TRY(hipSetDevice(ex->device));
+    for (auto& set : ex->ev_sets) {
+        ORB_HIP_TRY(hipEventSynchronize(set[kStages]));
+        for (int i = 0; i < kStages; i++) {
+            float t = 0.f;
+            ORB_HIP_TRY(hipEventElapsedTime(&t, set[i], set[i + 1]));
+            ex->stage_ms[i] += t;
+        }
+        ex->stage_calls++;
+        for (auto e : set) ex->ev_pool.push_back(e);
+    }
+    ex->ev_sets.clear();
+    for (int i = 0; i < n_stages && i < kStages; i++) ms[i] = ex->stage_ms[i];
+    if (n_calls) *n_calls = ex->stage_calls;
+    for (int i = 0; i < kStages; i++) ex->stage_ms[i] = 0;
+    ex->stage_calls = 0;
+    return kStages;
+}
+
+int orb_extractor_geometry(orb_extractor* ex, int w, int h, int* level_w, int* level_h, int* cells_per_level,
+                           int* max_keypoints_per_frame) {
+    if (!ex || w <= 0 || h <= 0) return ORB_EINVAL;
+    int st = ensure_geom(ex, w, h);
+    if (st) return st;
+    const Geom& g = ex->g;
+    for (int l = 0; l < g.nlevels; l++) {
+        if (level_w) level_w[l] = g.lv[l].w;
+        if (level_h) level_h[l] = g.lv[l].h;
+        if (cells_per_level) cells_per_level[l] = g.lv[l].nCols * g.lv[l].nRows;
+    }
+    if (max_keypoints_per_frame) *max_keypoints_per_frame = g.outPerFrame;
+    return ORB_OK;
+}
+
+int orb_extractor_last_counts(orb_extractor* ex, int frame, int* pre_counts, int* level_counts) {
+    if (!ex || frame < 0 || frame >= ex->lastB || ex->gw < 0) return ORB_EINVAL;
+    ORB_HIP_TRY(hipSetDevice(ex->device));
+    const Geom& g = ex->g;
+    std::vector<int> cc(g.cellsPerFrame), lc(g.nlevels);
+    ORB_HIP_TRY(hipStreamSynchronize(ex->stream));
+    ORB_HIP_TRY(hipDeviceSynchronize());
+    ORB_HIP_TRY(hipMemcpy(cc.data(), ex->d_cellCount + (size_t)frame * g.cellsPerFrame, cc.size() * 4,
+                          hipMemcpyDeviceToHost));
+    ORB_HIP_TRY(hipMemcpy(lc.data(), ex->d_levelCount + (size_t)frame * g.nlevels, lc.size() * 4,
+                          hipMemcpyDeviceToHost));
+    for (int l = 0; l < g.nlevels; l++) {
+        int s = 0;
+        for (int c = 0; c < g.lv[l].nCols * g.lv[l].nRows; c++) s += cc[g.lv[l].cellBase + c];
+        if (pre_counts) pre_counts[l] = s;
+        if (level_counts) level_counts[l] = lc[l];
+    }
     return ORB_OK;
 }
 
