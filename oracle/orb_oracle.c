@@ -1077,3 +1077,26 @@ void oracle_hamming_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt,
         best_idx[i] = bi; best_d[i] = b; second_d[i] = b2;
     }
 }
+
+/* Compares the glibc restatement against the host libm sinf/cosf for every
+ * stride-th float in [0, 6.2832]; returns the number of mismatching inputs. */
+long oracle_sincosf_check(unsigned stride, long* n_checked)
+{
+    const float lim = 6.2832f;
+    uint32_t ulim;
+    memcpy(&ulim, &lim, 4);
+    long bad = 0, n = 0;
+    if (stride == 0) stride = 1;
+    for (uint64_t u = 0; u <= ulim; u += stride) {
+        float y, s, c;
+        uint32_t u32 = (uint32_t)u;
+        memcpy(&y, &u32, 4);
+        oracle_sincosf_glibc(y, &s, &c);
+        volatile float yy = y;
+        const float rs = sinf(yy), rc = cosf(yy);
+        if (memcmp(&s, &rs, 4) || memcmp(&c, &rc, 4)) bad++;
+        n++;
+    }
+    if (n_checked) *n_checked = n;
+    return bad;
+}

@@ -67,6 +67,7 @@ int oracle_fast_roi(const uint8_t* img, size_t stride, int x0, int y0, int w, in
 float oracle_fast_atan2(float y, float x);
 
 /* glibc-exact sinf/cosf (see sincosf_glibc.h); returns 0 on success. */
+long oracle_sincosf_check(unsigned stride, long* n_checked);
 int oracle_sincosf(float x, float* s, float* c);
 
 /* Full ORBextractor::operator() (R/src/ORBextractor.cpp:1120-1188).
