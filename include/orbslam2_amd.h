@@ -192,7 +192,88 @@ int orb_search_for_initialization_batch_device(orb_matcher* m, const orb_keypoin
                                                int32_t* d_nmatches, void* stream);
 
 /* ------------------------------------------------------------ local BA */
-/* (see lba section below; declared in the same header) */
+
+/* The g2o graph Optimizer::LocalBundleAdjustment builds (R/src/Optimizer.cpp:629-782),
+ * as plain arrays.  Poses are VertexSE3Expmap estimates (Eigen quaternion coeffs
+ * x,y,z,w and translation, f64; lba_pose_from_Tcw converts a float Tcw the way
+ * Converter::toSE3Quat does); pose_fixed is setFixed (mnId==0 or a fixed camera);
+ * ids are the g2o vertex ids (KeyFrame::mnId, MapPoint::mnId+maxKFid+1), used only
+ * for g2o's index ordering.  Edges: vertex 0 = point, vertex 1 = pose; stereo
+ * edges carry (u, v, ur); information = I * invSigma2[octave] (float value);
+ * cam = fx, fy, cx, cy, bf of the observing keyframe.  point_bad is the
+ * MapPoint::isBad() snapshot the outlier passes test (NULL = none bad). */
+typedef struct {
+    int n_poses;
+    const double* pose_q;
+    const double* pose_t;
+    const uint8_t* pose_fixed;
+    const int64_t* pose_id;
+    int n_points;
+    const double* point_xyz;
+    const int64_t* point_id;
+    const uint8_t* point_bad;
+    int n_edges;
+    const int32_t* edge_point;
+    const int32_t* edge_pose;
+    const uint8_t* edge_stereo;
+    const double* edge_obs;
+    const double* edge_info;
+    const double* edge_cam;
+} lba_problem;
+
+typedef struct {
+    int iters1, iters2;              /* optimize(5), optimize(10) */
+    double chi2_mono, chi2_stereo;   /* 5.991, 7.815 */
+    double huber_mono, huber_stereo; /* (float)sqrt(5.991), (float)sqrt(7.815) */
+    int max_trials;                  /* maxTrialsAfterFailure (10) */
+    int fixed_iterations;            /* 1: ignore g2o's early termination (parity mode) */
+} lba_options;
+
+typedef struct {
+    double* pose_q;       /* out [n_poses][4] */
+    double* pose_t;       /* out [n_poses][3] */
+    double* point_xyz;    /* out [n_points][3] */
+    uint8_t* edge_erase;  /* out: the (KF, MapPoint) pairs of vToErase (R :850-880) */
+    double* edge_chi2;    /* out: e->chi2() at the final check */
+    int iterations[2];    /* outer iterations of each optimize() call */
+    int trials;           /* LM trials in total */
+    double* trace;        /* optional [64][4]: per outer iteration iniChi, chi2, lambda, trials */
+    int n_trace;
+    int aborted;          /* 1: *stop was set on entry, nothing optimised or written (R :784-786) */
+} lba_result;
+
+typedef struct lba_context lba_context;
+
+/* All-reduce callback for multi-GPU local BA: reduces `count` doubles at
+ * `offset_doubles` of the workspace registered with lba_set_comm across all
+ * ranks (op 0 = sum, 1 = max), ordered after the work already enqueued on the
+ * context's stream (lba_set_stream).  Return 0 on success. */
+typedef int (*lba_allreduce_fn)(void* user, size_t offset_doubles, size_t count, int op);
+
+int lba_create(int device, lba_context** out);
+void lba_destroy(lba_context* c);
+int lba_set_stream(lba_context* c, void* stream);
+/* Shards the landmarks over `world` ranks (rank r owns the contiguous index range
+ * [r*M/world, (r+1)*M/world)); every rank passes the same full problem. */
+int lba_set_comm(lba_context* c, int rank, int world, double* d_workspace, size_t ws_doubles,
+                 lba_allreduce_fn fn, void* user);
+
+/* Optimizer::LocalBundleAdjustment's optimisation (R/src/Optimizer.cpp:784-880):
+ * optimize(5) with Huber kernels, chi2/depth outlier pass, optimize(10) on the
+ * inliers without kernels, final chi2/depth check.  *stop (mbAbortBA) is polled
+ * like SparseOptimizer::terminate().  The caller applies the results under
+ * Map::mMutexMapUpdate exactly as R :883-917 do. */
+int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const volatile uint8_t* stop,
+              lba_result* r);
+
+/* Stage timing of the LM loop (HIP events): ms4 = linearise, Schur, solve, update. */
+int lba_profile(lba_context* c, int enable);
+int lba_stats(lba_context* c, double* ms4, int* iters, int* trials);
+
+/* Converter::toSE3Quat(const cv::Mat& Tcw) / Converter::toCvMat(const SE3Quat&)
+ * (R/src/Converter.cpp:47-57, 59-63): row-major 4x4 float <-> quaternion + t. */
+void lba_pose_from_Tcw(const float Tcw[16], double q[4], double t[3]);
+void lba_pose_to_Tcw(const double q[4], const double t[3], float Tcw[16]);
 
 #ifdef __cplusplus
 }

@@ -1,1 +1,686 @@
+/*
+ * ORACLE / TEST INFRASTRUCTURE ONLY — restatement of the reference's local bundle
+ * adjustment (see lba_oracle.h for anchors and parity status).
+ */
 #include "lba_oracle.h"
+
+#include <float.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------ SE3Quat (G/types/se3quat.h) */
+
+static void quat_to_R(const double q[4], double R[9])
+{   /* Eigen QuaternionBase::toRotationMatrix */
+    const double x = q[0], y = q[1], z = q[2], w = q[3];
+    const double tx = 2 * x, ty = 2 * y, tz = 2 * z;
+    const double twx = tx * w, twy = ty * w, twz = tz * w;
+    const double txx = tx * x, txy = ty * x, txz = tz * x;
+    const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
+    R[0] = 1 - (tyy + tzz); R[1] = txy - twz;       R[2] = txz + twy;
+    R[3] = txy + twz;       R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
+}
+
+static void cross3(const double a[3], const double b[3], double o[3])
+{
+    o[0] = a[1] * b[2] - a[2] * b[1];
+    o[1] = a[2] * b[0] - a[0] * b[2];
+    o[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+static void quat_rot(const double q[4], const double v[3], double o[3])
+{   /* Eigen _transformVector: uv = 2 q.vec x v; v + w uv + q.vec x uv */
+    double uv[3], c[3];
+    cross3(q, v, uv);
+    uv[0] += uv[0]; uv[1] += uv[1]; uv[2] += uv[2];
+    cross3(q, uv, c);
+    for (int i = 0; i < 3; i++) o[i] = v[i] + q[3] * uv[i] + c[i];
+}
+
+static void quat_mul(const double a[4], const double b[4], double o[4])
+{
+    double r[4];
+    r[3] = a[3] * b[3] - a[0] * b[0] - a[1] * b[1] - a[2] * b[2];
+    r[0] = a[3] * b[0] + a[0] * b[3] + a[1] * b[2] - a[2] * b[1];
+    r[1] = a[3] * b[1] + a[1] * b[3] + a[2] * b[0] - a[0] * b[2];
+    r[2] = a[3] * b[2] + a[2] * b[3] + a[0] * b[1] - a[1] * b[0];
+    memcpy(o, r, sizeof(r));
+}
+
+static void normalize_rotation(double q[4])
+{   /* SE3Quat::normalizeRotation */
+    if (q[3] < 0) { q[0] = -q[0]; q[1] = -q[1]; q[2] = -q[2]; q[3] = -q[3]; }
+    const double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    q[0] /= n; q[1] /= n; q[2] /= n; q[3] /= n;
+}
+
+void oracle_quat_from_matrix(const double m[9], double q[4])
+{   /* Eigen quaternionbase_assign_impl<Matrix3>, then normalizeRotation */
+    const double t = m[0] + m[4] + m[8];
+    if (t > 0) {
+        double s = sqrt(t + 1.0);
+        q[3] = 0.5 * s;
+        s = 0.5 / s;
+        q[0] = (m[7] - m[5]) * s;
+        q[1] = (m[2] - m[6]) * s;
+        q[2] = (m[3] - m[1]) * s;
+    } else {
+        int i = 0;
+        if (m[4] > m[0]) i = 1;
+        if (m[8] > m[i * 3 + i]) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        double s = sqrt(m[i * 3 + i] - m[j * 3 + j] - m[k * 3 + k] + 1.0);
+        q[i] = 0.5 * s;
+        s = 0.5 / s;
+        q[3] = (m[k * 3 + j] - m[j * 3 + k]) * s;
+        q[j] = (m[j * 3 + i] + m[i * 3 + j]) * s;
+        q[k] = (m[k * 3 + i] + m[i * 3 + k]) * s;
+    }
+    normalize_rotation(q);
+}
+
+static void mat3_mul(const double A[9], const double B[9], double C[9])
+{
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+            C[i * 3 + j] = A[i * 3] * B[j] + A[i * 3 + 1] * B[3 + j] + A[i * 3 + 2] * B[6 + j];
+}
+
+void oracle_se3_exp_left(const double upd[6], const double q[4], const double t[3], double qo[4], double to[3])
+{   /* SE3Quat::exp(update) * T  (VertexSE3Expmap::oplusImpl) */
+    const double* w = upd;
+    const double* u = upd + 3;
+    const double theta = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+    const double O[9] = {0, -w[2], w[1], w[2], 0, -w[0], -w[1], w[0], 0};
+    double O2[9], R[9], V[9];
+    mat3_mul(O, O, O2);
+    if (theta < 0.00001) {
+        for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0 ? 1.0 : 0.0) + O[i] + O2[i];
+        memcpy(V, R, sizeof(R));
+    } else {
+        const double a = sin(theta) / theta, b = (1 - cos(theta)) / (theta * theta);
+        const double c = (theta - sin(theta)) / pow(theta, 3);
+        for (int i = 0; i < 9; i++) {
+            const double I = (i % 4 == 0 ? 1.0 : 0.0);
+            R[i] = I + a * O[i] + b * O2[i];
+            V[i] = I + b * O[i] + c * O2[i];
+        }
+    }
+    double qe[4], te[3];
+    oracle_quat_from_matrix(R, qe);
+    for (int i = 0; i < 3; i++) te[i] = V[i * 3] * u[0] + V[i * 3 + 1] * u[1] + V[i * 3 + 2] * u[2];
+    double rt[3];
+    quat_rot(qe, t, rt);
+    for (int i = 0; i < 3; i++) to[i] = te[i] + rt[i];
+    quat_mul(qe, q, qo);
+    normalize_rotation(qo);
+}
+
+/* ------------------------------------------------------------ edges */
+
+typedef struct {
+    const lba_problem_t* p;
+    const lba_options_t* o;
+    double *pq, *pt, *X;            /* current estimates */
+    double *bq, *bt, *bX;           /* push() backup */
+    double* err;                    /* [n_edges][3] last computed error (stale after pop, like g2o) */
+    uint8_t *level, *robust;
+    /* active structure */
+    int* act_edges; int n_act;
+    int* pose_idx; int P;           /* pose -> hessian index or -1 */
+    int* point_idx; int M;
+    /* system */
+    double* Hpp;    /* [P][6][6] diagonal blocks + dense S assembly */
+    double* S;      /* [6P][6P] */
+    double* bp;     /* [6P] */
+    double* Hll;    /* [M][9] */
+    double* bl;     /* [M][3] */
+    double* Hpl;    /* [n_edges][18] (6x3 per active edge with a free pose) */
+    double* x;      /* [6P + 3M] */
+    double* Dinv;   /* [M][9] */
+    int* pt_edge_start; int* pt_edges;   /* active edges grouped by point index (ascending pose index) */
+    double lambda, ni;
+    int nBad;
+} lba_ctx;
+
+static void transform(const lba_ctx* c, int pose, int pt, double Xc[3])
+{
+    double r[3];
+    quat_rot(c->pq + 4 * pose, c->X + 3 * pt, r);
+    for (int i = 0; i < 3; i++) Xc[i] = r[i] + c->pt[3 * pose + i];
+}
+
+static void compute_error(lba_ctx* c, int e)
+{
+    const lba_problem_t* p = c->p;
+    double Xc[3];
+    transform(c, p->edge_pose[e], p->edge_point[e], Xc);
+    const double* cam = p->edge_cam + 5 * e;
+    const double* obs = p->edge_obs + 3 * e;
+    double* er = c->err + 3 * e;
+    if (!p->edge_stereo[e]) {
+        const double u = Xc[0] / Xc[2], v = Xc[1] / Xc[2];
+        er[0] = obs[0] - (u * cam[0] + cam[2]);
+        er[1] = obs[1] - (v * cam[1] + cam[3]);
+        er[2] = 0;
+    } else {   /* EdgeStereoSE3ProjectXYZ::cam_project: float invz, float bf */
+        const float invz = (float)(1.0f / Xc[2]);
+        const double r0 = Xc[0] * invz * cam[0] + cam[2];
+        const double r1 = Xc[1] * invz * cam[1] + cam[3];
+        const float bff = (float)cam[4];
+        const double r2 = r0 - (double)(bff * invz);
+        er[0] = obs[0] - r0;
+        er[1] = obs[1] - r1;
+        er[2] = obs[2] - r2;
+    }
+}
+
+static double edge_chi2(const lba_ctx* c, int e)
+{
+    const double* er = c->err + 3 * e;
+    const double w = c->p->edge_info[e];
+    double s = er[0] * (w * er[0]) + er[1] * (w * er[1]);
+    if (c->p->edge_stereo[e]) s += er[2] * (w * er[2]);
+    return s;
+}
+
+static double huber_delta(const lba_ctx* c, int e)
+{
+    return c->p->edge_stereo[e] ? c->o->huber_stereo : c->o->huber_mono;
+}
+
+static double robust_chi2(const lba_ctx* c, int e)
+{
+    const double chi = edge_chi2(c, e);
+    if (!c->robust[e]) return chi;
+    const double d = huber_delta(c, e), dsqr = d * d;
+    if (chi <= dsqr) return chi;
+    return 2 * sqrt(chi) * d - dsqr;
+}
+
+static int depth_positive(const lba_ctx* c, int e)
+{
+    double Xc[3];
+    transform(c, c->p->edge_pose[e], c->p->edge_point[e], Xc);
+    return Xc[2] > 0.0;
+}
+
+/* Jacobians (G/types/types_six_dof_expmap.cpp:112-245): A = d e / d X (rows x 3), B = d e / d xi (rows x 6) */
+static int linearize(const lba_ctx* c, int e, double A[9], double B[18])
+{
+    const lba_problem_t* p = c->p;
+    const int pose = p->edge_pose[e];
+    double R[9], Xc[3];
+    quat_to_R(c->pq + 4 * pose, R);
+    transform(c, pose, p->edge_point[e], Xc);
+    const double x = Xc[0], y = Xc[1], z = Xc[2], z_2 = z * z;
+    const double* cam = p->edge_cam + 5 * e;
+    const double fx = cam[0], fy = cam[1], bf = cam[4];
+    if (!p->edge_stereo[e]) {
+        const double tmp[6] = {fx, 0, -x / z * fx, 0, fy, -y / z * fy};
+        for (int r = 0; r < 2; r++)
+            for (int k = 0; k < 3; k++)
+                A[r * 3 + k] = -1. / z * (tmp[r * 3] * R[k] + tmp[r * 3 + 1] * R[3 + k] + tmp[r * 3 + 2] * R[6 + k]);
+    } else {
+        for (int k = 0; k < 3; k++) {
+            A[0 * 3 + k] = -fx * R[0 * 3 + k] / z + fx * x * R[2 * 3 + k] / z_2;
+            A[1 * 3 + k] = -fy * R[1 * 3 + k] / z + fy * y * R[2 * 3 + k] / z_2;
+            A[2 * 3 + k] = A[0 * 3 + k] - bf * R[2 * 3 + k] / z_2;
+        }
+    }
+    B[0] = x * y / z_2 * fx;      B[1] = -(1 + (x * x / z_2)) * fx; B[2] = y / z * fx;
+    B[3] = -1. / z * fx;          B[4] = 0;                         B[5] = x / z_2 * fx;
+    B[6] = (1 + y * y / z_2) * fy; B[7] = -x * y / z_2 * fy;        B[8] = -x / z * fy;
+    B[9] = 0;                     B[10] = -1. / z * fy;             B[11] = y / z_2 * fy;
+    if (p->edge_stereo[e]) {
+        B[12] = B[0] - bf * y / z_2; B[13] = B[1] + bf * x / z_2; B[14] = B[2];
+        B[15] = B[3];                B[16] = 0;                   B[17] = B[5] - bf / z_2;
+        return 3;
+    }
+    return 2;
+}
+
+/* ------------------------------------------------------------ structure (initializeOptimization) */
+
+static int cmp_i64_idx_base;
+static const int64_t* g_ids;
+static int cmp_by_id(const void* a, const void* b)
+{
+    const int64_t x = g_ids[*(const int*)a], y = g_ids[*(const int*)b];
+    return x < y ? -1 : (x > y ? 1 : 0);
+}
+
+static void init_optimization(lba_ctx* c, int level)
+{
+    const lba_problem_t* p = c->p;
+    c->n_act = 0;
+    uint8_t* pose_act = (uint8_t*)calloc(p->n_poses + 1, 1);
+    uint8_t* pt_act = (uint8_t*)calloc(p->n_points + 1, 1);
+    for (int e = 0; e < p->n_edges; e++) {
+        if (c->level[e] != level) continue;
+        /* allVerticesFixed() is false: points are never fixed */
+        c->act_edges[c->n_act++] = e;
+        pose_act[p->edge_pose[e]] = 1;
+        pt_act[p->edge_point[e]] = 1;
+    }
+    /* index mapping: free active poses by id, then active points by id (G/core/sparse_optimizer.cpp:166-190) */
+    int* order = (int*)malloc(sizeof(int) * (p->n_poses + p->n_points + 1));
+    int n = 0;
+    for (int i = 0; i < p->n_poses; i++) if (pose_act[i] && !p->pose_fixed[i]) order[n++] = i;
+    g_ids = p->pose_id;
+    qsort(order, n, sizeof(int), cmp_by_id);
+    for (int i = 0; i < p->n_poses; i++) c->pose_idx[i] = -1;
+    for (int k = 0; k < n; k++) c->pose_idx[order[k]] = k;
+    c->P = n;
+    n = 0;
+    for (int i = 0; i < p->n_points; i++) if (pt_act[i]) order[n++] = i;
+    g_ids = p->point_id;
+    qsort(order, n, sizeof(int), cmp_by_id);
+    for (int i = 0; i < p->n_points; i++) c->point_idx[i] = -1;
+    for (int k = 0; k < n; k++) c->point_idx[order[k]] = k;
+    c->M = n;
+    /* edges per point index, sorted by pose index */
+    memset(c->pt_edge_start, 0, sizeof(int) * (c->M + 1));
+    for (int k = 0; k < c->n_act; k++) c->pt_edge_start[c->point_idx[p->edge_point[c->act_edges[k]]] + 1]++;
+    for (int i = 0; i < c->M; i++) c->pt_edge_start[i + 1] += c->pt_edge_start[i];
+    int* fill = (int*)malloc(sizeof(int) * (c->M + 1));
+    memcpy(fill, c->pt_edge_start, sizeof(int) * (c->M + 1));
+    for (int k = 0; k < c->n_act; k++) {
+        const int e = c->act_edges[k];
+        c->pt_edges[fill[c->point_idx[p->edge_point[e]]]++] = e;
+    }
+    for (int m = 0; m < c->M; m++) {   /* insertion sort by pose hessian index (fixed poses last) */
+        int* a = c->pt_edges + c->pt_edge_start[m];
+        const int len = c->pt_edge_start[m + 1] - c->pt_edge_start[m];
+        for (int i = 1; i < len; i++) {
+            const int v = a[i];
+            const int kv = c->pose_idx[p->edge_pose[v]] < 0 ? 1 << 30 : c->pose_idx[p->edge_pose[v]];
+            int j = i - 1;
+            while (j >= 0) {
+                const int kj = c->pose_idx[p->edge_pose[a[j]]] < 0 ? 1 << 30 : c->pose_idx[p->edge_pose[a[j]]];
+                if (kj <= kv) break;
+                a[j + 1] = a[j];
+                j--;
+            }
+            a[j + 1] = v;
+        }
+    }
+    free(fill);
+    free(order);
+    free(pose_act);
+    free(pt_act);
+}
+
+/* ------------------------------------------------------------ buildSystem */
+
+static void build_system(lba_ctx* c)
+{
+    const lba_problem_t* p = c->p;
+    const int np = 6 * c->P;
+    memset(c->Hpp, 0, sizeof(double) * 36 * c->P);
+    memset(c->bp, 0, sizeof(double) * np);
+    memset(c->Hll, 0, sizeof(double) * 9 * c->M);
+    memset(c->bl, 0, sizeof(double) * 3 * c->M);
+    memset(c->S, 0, sizeof(double) * np * np);     /* off-diagonal pose blocks stay zero in Hpp */
+    for (int k = 0; k < c->n_act; k++) {
+        const int e = c->act_edges[k];
+        double A[9], B[18];
+        const int D = linearize(c, e, A, B);
+        const double w = p->edge_info[e];
+        const double* er = c->err + 3 * e;
+        double rho1 = 1.0;
+        if (c->robust[e]) {
+            const double chi = edge_chi2(c, e), d = huber_delta(c, e);
+            if (chi > d * d) rho1 = d / sqrt(chi);
+        }
+        const double W = rho1 * w;          /* weightedOmega = rho' * Omega (diagonal) */
+        double om_r[3];
+        for (int r = 0; r < D; r++) om_r[r] = -(w * er[r]) * rho1;
+        const int li = c->point_idx[p->edge_point[e]];
+        const int pi = c->pose_idx[p->edge_pose[e]];
+        double* hl = c->Hll + 9 * li;
+        double* bl = c->bl + 3 * li;
+        for (int i = 0; i < 3; i++) {
+            for (int r = 0; r < D; r++) bl[i] += A[r * 3 + i] * om_r[r];
+            for (int j = 0; j < 3; j++) {
+                double s = 0;
+                for (int r = 0; r < D; r++) s += A[r * 3 + i] * W * A[r * 3 + j];
+                hl[i * 3 + j] += s;
+            }
+        }
+        if (pi >= 0) {
+            double* hp = c->Hpp + 36 * pi;
+            double* bp = c->bp + 6 * pi;
+            double* hpl = c->Hpl + 18 * e;
+            for (int i = 0; i < 6; i++) {
+                for (int r = 0; r < D; r++) bp[i] += B[r * 6 + i] * om_r[r];
+                for (int j = 0; j < 6; j++) {
+                    double s = 0;
+                    for (int r = 0; r < D; r++) s += B[r * 6 + i] * W * B[r * 6 + j];
+                    hp[i * 6 + j] += s;
+                }
+                for (int j = 0; j < 3; j++) {
+                    double s = 0;
+                    for (int r = 0; r < D; r++) s += B[r * 6 + i] * W * A[r * 3 + j];
+                    hpl[i * 3 + j] = s;
+                }
+            }
+        }
+    }
+}
+
+static double lambda_init(const lba_ctx* c)
+{
+    double m = 0.;
+    for (int i = 0; i < c->P; i++)
+        for (int j = 0; j < 6; j++) m = fmax(fabs(c->Hpp[36 * i + j * 7]), m);
+    for (int i = 0; i < c->M; i++)
+        for (int j = 0; j < 3; j++) m = fmax(fabs(c->Hll[9 * i + j * 4]), m);
+    return 1e-5 * m;
+}
+
+static void inv3(const double m[9], double o[9])
+{   /* Eigen compute_inverse_size3_helper */
+    double c[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+            c[i * 3 + j] = m[i1 * 3 + j1] * m[i2 * 3 + j2] - m[i1 * 3 + j2] * m[i2 * 3 + j1];
+        }
+    const double det = c[0] * m[0] + c[3] * m[3] + c[6] * m[6];
+    const double invdet = 1.0 / det;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) o[j * 3 + i] = c[i * 3 + j] * invdet;
+}
+
+/* BlockSolver::solve with lambda on the diagonal; returns 0 if the LDL^T fails */
+static int schur_solve(lba_ctx* c, double lambda)
+{
+    const lba_problem_t* p = c->p;
+    const int np = 6 * c->P;
+    double* S = c->S;
+    memset(S, 0, sizeof(double) * np * np);
+    for (int i = 0; i < c->P; i++)
+        for (int r = 0; r < 6; r++)
+            for (int q = 0; q < 6; q++) S[(6 * i + r) * np + 6 * i + q] = c->Hpp[36 * i + r * 6 + q] + (r == q ? lambda : 0.);
+    double* coef = (double*)calloc(np + 1, sizeof(double));
+    for (int l = 0; l < c->M; l++) {
+        double D[9];
+        memcpy(D, c->Hll + 9 * l, sizeof(D));
+        D[0] += lambda; D[4] += lambda; D[8] += lambda;
+        double* Di = c->Dinv + 9 * l;
+        inv3(D, Di);
+        const double* b = c->bl + 3 * l;
+        double db[3];
+        for (int i = 0; i < 3; i++) db[i] = Di[i * 3] * b[0] + Di[i * 3 + 1] * b[1] + Di[i * 3 + 2] * b[2];
+        const int s0 = c->pt_edge_start[l], s1 = c->pt_edge_start[l + 1];
+        for (int a = s0; a < s1; a++) {
+            const int e1 = c->pt_edges[a];
+            const int i1 = c->pose_idx[p->edge_pose[e1]];
+            if (i1 < 0) continue;
+            const double* Bi = c->Hpl + 18 * e1;
+            double BD[18];
+            for (int r = 0; r < 6; r++)
+                for (int q = 0; q < 3; q++)
+                    BD[r * 3 + q] = Bi[r * 3] * Di[q] + Bi[r * 3 + 1] * Di[3 + q] + Bi[r * 3 + 2] * Di[6 + q];
+            for (int r = 0; r < 6; r++) coef[6 * i1 + r] += Bi[r * 3] * db[0] + Bi[r * 3 + 1] * db[1] + Bi[r * 3 + 2] * db[2];
+            for (int bb = a; bb < s1; bb++) {
+                const int e2 = c->pt_edges[bb];
+                const int i2 = c->pose_idx[p->edge_pose[e2]];
+                if (i2 < 0) continue;
+                const double* Bj = c->Hpl + 18 * e2;
+                for (int r = 0; r < 6; r++)
+                    for (int q = 0; q < 6; q++) {
+                        const double v = BD[r * 3] * Bj[q * 3] + BD[r * 3 + 1] * Bj[q * 3 + 1] + BD[r * 3 + 2] * Bj[q * 3 + 2];
+                        S[(6 * i1 + r) * np + 6 * i2 + q] -= v;
+                    }
+            }
+        }
+    }
+    /* symmetric fill of the lower triangle from the upper blocks */
+    for (int r = 0; r < np; r++)
+        for (int q = 0; q < r; q++) S[r * np + q] = S[q * np + r];
+    double* bs = (double*)malloc(sizeof(double) * (np + 1));
+    for (int i = 0; i < np; i++) bs[i] = c->bp[i] - coef[i];
+    /* dense LDL^T (no pivoting); fails only on an exactly zero pivot, like SimplicialLDLT */
+    int ok = 1;
+    double* d = (double*)malloc(sizeof(double) * (np + 1));
+    for (int j = 0; j < np && ok; j++) {
+        double dj = S[j * np + j];
+        for (int k = 0; k < j; k++) dj -= S[j * np + k] * S[j * np + k] * d[k];
+        if (dj == 0.0 || !isfinite(dj)) { ok = 0; break; }
+        d[j] = dj;
+        for (int i = j + 1; i < np; i++) {
+            double v = S[i * np + j];
+            for (int k = 0; k < j; k++) v -= S[i * np + k] * S[j * np + k] * d[k];
+            S[i * np + j] = v / dj;
+        }
+    }
+    double* xp = c->x;
+    if (ok) {
+        for (int i = 0; i < np; i++) {
+            double v = bs[i];
+            for (int k = 0; k < i; k++) v -= S[i * np + k] * xp[k];
+            xp[i] = v;
+        }
+        for (int i = 0; i < np; i++) xp[i] /= d[i];
+        for (int i = np - 1; i >= 0; i--) {
+            double v = xp[i];
+            for (int k = i + 1; k < np; k++) v -= S[k * np + i] * xp[k];
+            xp[i] = v;
+        }
+        /* landmarks: x_l = Dinv (b_l - Hpl^T x_p) */
+        for (int l = 0; l < c->M; l++) {
+            double cl[3] = {c->bl[3 * l], c->bl[3 * l + 1], c->bl[3 * l + 2]};
+            for (int a = c->pt_edge_start[l]; a < c->pt_edge_start[l + 1]; a++) {
+                const int e = c->pt_edges[a];
+                const int i1 = c->pose_idx[p->edge_pose[e]];
+                if (i1 < 0) continue;
+                const double* Bi = c->Hpl + 18 * e;
+                for (int q = 0; q < 3; q++)
+                    for (int r = 0; r < 6; r++) cl[q] += Bi[r * 3 + q] * (-xp[6 * i1 + r]);
+            }
+            const double* Di = c->Dinv + 9 * l;
+            double* xl = c->x + np + 3 * l;
+            for (int q = 0; q < 3; q++) xl[q] = Di[q * 3] * cl[0] + Di[q * 3 + 1] * cl[1] + Di[q * 3 + 2] * cl[2];
+        }
+    }
+    free(d);
+    free(bs);
+    free(coef);
+    return ok;
+}
+
+static void push_state(lba_ctx* c)
+{
+    memcpy(c->bq, c->pq, sizeof(double) * 4 * c->p->n_poses);
+    memcpy(c->bt, c->pt, sizeof(double) * 3 * c->p->n_poses);
+    memcpy(c->bX, c->X, sizeof(double) * 3 * c->p->n_points);
+}
+static void pop_state(lba_ctx* c)
+{
+    memcpy(c->pq, c->bq, sizeof(double) * 4 * c->p->n_poses);
+    memcpy(c->pt, c->bt, sizeof(double) * 3 * c->p->n_poses);
+    memcpy(c->X, c->bX, sizeof(double) * 3 * c->p->n_points);
+}
+
+static void update(lba_ctx* c)
+{
+    const lba_problem_t* p = c->p;
+    for (int i = 0; i < p->n_poses; i++) {
+        const int k = c->pose_idx[i];
+        if (k < 0) continue;
+        double q[4], t[3];
+        oracle_se3_exp_left(c->x + 6 * k, c->pq + 4 * i, c->pt + 3 * i, q, t);
+        memcpy(c->pq + 4 * i, q, sizeof(q));
+        memcpy(c->pt + 3 * i, t, sizeof(t));
+    }
+    for (int i = 0; i < p->n_points; i++) {
+        const int k = c->point_idx[i];
+        if (k < 0) continue;
+        for (int j = 0; j < 3; j++) c->X[3 * i + j] += c->x[6 * c->P + 3 * k + j];
+    }
+}
+
+static double active_robust_chi2(lba_ctx* c)
+{
+    double s = 0;
+    for (int k = 0; k < c->n_act; k++) s += robust_chi2(c, c->act_edges[k]);
+    return s;
+}
+static void compute_active_errors(lba_ctx* c)
+{
+    for (int k = 0; k < c->n_act; k++) compute_error(c, c->act_edges[k]);
+}
+
+enum { LM_OK = 0, LM_TERMINATE = 1 };
+
+/* OptimizationAlgorithmLevenberg::solve (G/core/optimization_algorithm_levenberg.cpp:61-164) */
+static int lm_iteration(lba_ctx* c, int iteration, const volatile uint8_t* stop, lba_result_t* r)
+{
+    compute_active_errors(c);
+    double currentChi = active_robust_chi2(c);
+    double tempChi = currentChi;
+    const double iniChi = currentChi;
+    build_system(c);
+    if (iteration == 0) {
+        c->lambda = lambda_init(c);
+        c->ni = 2;
+        c->nBad = 0;
+    }
+    double rho = 0;
+    int qmax = 0;
+    const int nx = 6 * c->P + 3 * c->M;
+    do {
+        push_state(c);
+        const double lam = c->lambda;
+        const int ok2 = schur_solve(c, lam);
+        if (!ok2) memset(c->x, 0, sizeof(double) * nx);   /* _x is left unchanged on failure; update is harmless */
+        update(c);
+        compute_active_errors(c);
+        tempChi = active_robust_chi2(c);
+        if (!ok2) tempChi = DBL_MAX;
+        rho = currentChi - tempChi;
+        double scale = 0.;
+        for (int j = 0; j < 6 * c->P; j++) scale += c->x[j] * (lam * c->x[j] + c->bp[j]);
+        for (int j = 0; j < 3 * c->M; j++) scale += c->x[6 * c->P + j] * (lam * c->x[6 * c->P + j] + c->bl[j]);
+        scale += 1e-3;
+        rho /= scale;
+        if (rho > 0 && isfinite(tempChi)) {
+            double alpha = 1. - pow((2 * rho - 1), 3);
+            alpha = fmin(alpha, 2. / 3.);
+            const double sf = fmax(1. / 3., alpha);
+            c->lambda *= sf;
+            c->ni = 2;
+            currentChi = tempChi;
+        } else {
+            c->lambda *= c->ni;
+            c->ni *= 2;
+            pop_state(c);
+        }
+        qmax++;
+        r->trials++;
+    } while (rho < 0 && qmax < c->o->max_trials && !(stop && *stop));
+    if (r->trace && r->n_trace < 64) {
+        double* t = r->trace + 4 * r->n_trace++;
+        t[0] = iniChi; t[1] = currentChi; t[2] = c->lambda; t[3] = qmax;
+    }
+    if (c->o->fixed_iterations) return LM_OK;
+    if (qmax == c->o->max_trials || rho == 0) return LM_TERMINATE;
+    if ((iniChi - currentChi) * 1e3 < iniChi) c->nBad++;
+    else c->nBad = 0;
+    if (c->nBad >= 3) return LM_TERMINATE;
+    return LM_OK;
+}
+
+static int optimize(lba_ctx* c, int iterations, const volatile uint8_t* stop, lba_result_t* r)
+{
+    if (c->P + c->M == 0) return 0;
+    int it = 0, ok = 1;
+    for (int i = 0; i < iterations && !(stop && *stop) && ok; i++) {
+        ok = lm_iteration(c, i, stop, r) == LM_OK;
+        it++;
+    }
+    return it;
+}
+
+int oracle_lba_solve(const lba_problem_t* p, const lba_options_t* o, const volatile uint8_t* stop, lba_result_t* r)
+{
+    lba_ctx c;
+    memset(&c, 0, sizeof(c));
+    c.p = p;
+    c.o = o;
+    const int NP = p->n_poses, NM = p->n_points, NE = p->n_edges;
+    c.pq = (double*)malloc(sizeof(double) * 4 * (NP + 1));
+    c.pt = (double*)malloc(sizeof(double) * 3 * (NP + 1));
+    c.X = (double*)malloc(sizeof(double) * 3 * (NM + 1));
+    c.bq = (double*)malloc(sizeof(double) * 4 * (NP + 1));
+    c.bt = (double*)malloc(sizeof(double) * 3 * (NP + 1));
+    c.bX = (double*)malloc(sizeof(double) * 3 * (NM + 1));
+    c.err = (double*)calloc(3 * (NE + 1), sizeof(double));
+    c.level = (uint8_t*)calloc(NE + 1, 1);
+    c.robust = (uint8_t*)malloc(NE + 1);
+    memset(c.robust, 1, NE + 1);
+    c.act_edges = (int*)malloc(sizeof(int) * (NE + 1));
+    c.pose_idx = (int*)malloc(sizeof(int) * (NP + 1));
+    c.point_idx = (int*)malloc(sizeof(int) * (NM + 1));
+    c.Hpp = (double*)malloc(sizeof(double) * 36 * (NP + 1));
+    c.S = (double*)malloc(sizeof(double) * 36 * (NP + 1) * (NP + 1));
+    c.bp = (double*)malloc(sizeof(double) * 6 * (NP + 1));
+    c.Hll = (double*)malloc(sizeof(double) * 9 * (NM + 1));
+    c.bl = (double*)malloc(sizeof(double) * 3 * (NM + 1));
+    c.Hpl = (double*)malloc(sizeof(double) * 18 * (NE + 1));
+    c.x = (double*)malloc(sizeof(double) * (6 * NP + 3 * NM + 1));
+    c.Dinv = (double*)malloc(sizeof(double) * 9 * (NM + 1));
+    c.pt_edge_start = (int*)malloc(sizeof(int) * (NM + 2));
+    c.pt_edges = (int*)malloc(sizeof(int) * (NE + 1));
+    memcpy(c.pq, p->pose_q, sizeof(double) * 4 * NP);
+    memcpy(c.pt, p->pose_t, sizeof(double) * 3 * NP);
+    memcpy(c.X, p->point_xyz, sizeof(double) * 3 * NM);
+    r->iterations[0] = r->iterations[1] = 0;
+    r->trials = 0;
+    r->n_trace = 0;
+    int status = 0;
+    if (stop && *stop) {
+        status = 1;
+        goto done;
+    }
+    /* optimize(5) on every edge with Huber kernels (R/src/Optimizer.cpp:789-790) */
+    init_optimization(&c, 0);
+    r->iterations[0] = optimize(&c, o->iters1, stop, r);
+    int bDoMore = !(stop && *stop);
+    if (bDoMore) {
+        /* outlier pass (R/src/Optimizer.cpp:805-836) */
+        for (int e = 0; e < NE; e++) {
+            if (p->point_bad && p->point_bad[p->edge_point[e]]) continue;
+            const double thr = p->edge_stereo[e] ? o->chi2_stereo : o->chi2_mono;
+            if (edge_chi2(&c, e) > thr || !depth_positive(&c, e)) c.level[e] = 1;
+            c.robust[e] = 0;
+        }
+        init_optimization(&c, 0);
+        r->iterations[1] = optimize(&c, o->iters2, stop, r);
+    }
+    /* final check (R/src/Optimizer.cpp:850-880): e->chi2() uses each edge's last computed error */
+    for (int e = 0; e < NE; e++) {
+        const double chi = edge_chi2(&c, e);
+        if (r->edge_chi2) r->edge_chi2[e] = chi;
+        uint8_t er = 0;
+        if (!(p->point_bad && p->point_bad[p->edge_point[e]])) {
+            const double thr = p->edge_stereo[e] ? o->chi2_stereo : o->chi2_mono;
+            er = (chi > thr || !depth_positive(&c, e)) ? 1 : 0;
+        }
+        if (r->edge_erase) r->edge_erase[e] = er;
+    }
+    if (r->pose_q) memcpy(r->pose_q, c.pq, sizeof(double) * 4 * NP);
+    if (r->pose_t) memcpy(r->pose_t, c.pt, sizeof(double) * 3 * NP);
+    if (r->point_xyz) memcpy(r->point_xyz, c.X, sizeof(double) * 3 * NM);
+done:
+    free(c.pq); free(c.pt); free(c.X); free(c.bq); free(c.bt); free(c.bX); free(c.err);
+    free(c.level); free(c.robust); free(c.act_edges); free(c.pose_idx); free(c.point_idx);
+    free(c.Hpp); free(c.S); free(c.bp); free(c.Hll); free(c.bl); free(c.Hpl); free(c.x); free(c.Dinv);
+    free(c.pt_edge_start); free(c.pt_edges);
+    (void)cmp_i64_idx_base;
+    return status;
+}

@@ -4,3 +4,4 @@ Import as `orb_slam2_amd` (see pkgload.py)."""
 from . import _abi  # noqa: F401
 from .extractor import ORBextractor  # noqa: F401
 from .matcher import ORBmatcher, Frame  # noqa: F401
+from .optimizer import Optimizer, LocalBA  # noqa: F401

@@ -1,2 +1,1172 @@
-// placeholder, filled in below
+// MI355X-native Optimizer::LocalBundleAdjustment (R/src/Optimizer.cpp:564-918) — the g2o
+// Levenberg–Marquardt / BlockSolver<6,3> Schur pipeline it runs, rebuilt for gfx950 in f64.
+// R/ = /root/reference/ORB-SLAM2注释版/, G/ = R/Thirdparty/g2o/g2o/.
+//
+// Per LM outer iteration (G/core/optimization_algorithm_levenberg.cpp:61-164):
+//   k_edge_errors     computeActiveErrors + robust chi2 per edge (one thread per edge)
+//   k_edge_linearize  EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ Jacobians + Huber-weighted
+//                     quadratic-form blocks per edge (G/core/base_binary_edge.hpp:54-120)
+//   k_point_reduce    Hll, b_l per landmark; k_pose_reduce: Hpp, b_p per pose (one wave per pose)
+// Per LM trial (lambda):
+//   k_point_schur     D^-1 = (Hll + lambda I)^-1, per-edge Hpl D^-1 and Hpl D^-1 b_l
+//   k_schur_pairs     reduced camera matrix S = Hpp + lambda I - sum W D^-1 W^T, one wave per
+//                     6x6 pose-pair block, deterministic contribution order (G/core/block_solver.hpp:382-433)
+//   k_ldlt_solve      dense LDL^T of S in one workgroup (LinearSolverEigen's SimplicialLDLT role)
+//   k_backsub / k_update / k_edge_errors / reductions: x_l, oplus (SE3Quat::exp * T), chi2, scale.
+// The LM control flow (rho test, lambda schedule, Raul's stop rule, push/pop, the two
+// optimize() rounds and the chi2 outlier passes) runs on the host exactly as g2o/ORB-SLAM2 do,
+// reading back two scalars per trial.  Every reduction has a fixed order, so results are
+// bitwise reproducible run to run.  With a communicator (lba_set_comm) the landmarks are
+// sharded over ranks and S, b_s and the chi2 / scale scalars are all-reduced (RCCL via the
+// caller's callback); every rank then solves the same reduced system.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
 #include "common.h"
+
+namespace orbamd {
+
+// ------------------------------------------------------------------ device math (SE3Quat)
+
+__device__ __forceinline__ void d_cross(const double a[3], const double b[3], double o[3]) {
+    o[0] = a[1] * b[2] - a[2] * b[1];
+    o[1] = a[2] * b[0] - a[0] * b[2];
+    o[2] = a[0] * b[1] - a[1] * b[0];
+}
+__device__ __forceinline__ void d_quat_rot(const double q[4], const double v[3], double o[3]) {
+    double uv[3], c[3];
+    d_cross(q, v, uv);
+    uv[0] += uv[0]; uv[1] += uv[1]; uv[2] += uv[2];
+    d_cross(q, uv, c);
+    for (int i = 0; i < 3; i++) o[i] = v[i] + q[3] * uv[i] + c[i];
+}
+__device__ __forceinline__ void d_quat_to_R(const double q[4], double R[9]) {
+    const double x = q[0], y = q[1], z = q[2], w = q[3];
+    const double tx = 2 * x, ty = 2 * y, tz = 2 * z;
+    const double twx = tx * w, twy = ty * w, twz = tz * w;
+    const double txx = tx * x, txy = ty * x, txz = tz * x;
+    const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
+    R[0] = 1 - (tyy + tzz); R[1] = txy - twz;       R[2] = txz + twy;
+    R[3] = txy + twz;       R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
+}
+__host__ __device__ inline void hd_normalize_rotation(double q[4]) {
+    if (q[3] < 0) { q[0] = -q[0]; q[1] = -q[1]; q[2] = -q[2]; q[3] = -q[3]; }
+    const double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    q[0] /= n; q[1] /= n; q[2] /= n; q[3] /= n;
+}
+// Eigen Quaterniond(const Matrix3d&) + SE3Quat::normalizeRotation
+__host__ __device__ inline void hd_quat_from_matrix(const double m[9], double q[4]) {
+    const double t = m[0] + m[4] + m[8];
+    if (t > 0) {
+        double s = sqrt(t + 1.0);
+        q[3] = 0.5 * s;
+        s = 0.5 / s;
+        q[0] = (m[7] - m[5]) * s;
+        q[1] = (m[2] - m[6]) * s;
+        q[2] = (m[3] - m[1]) * s;
+    } else {
+        int i = 0;
+        if (m[4] > m[0]) i = 1;
+        if (m[8] > m[i * 3 + i]) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        double s = sqrt(m[i * 3 + i] - m[j * 3 + j] - m[k * 3 + k] + 1.0);
+        q[i] = 0.5 * s;
+        s = 0.5 / s;
+        q[3] = (m[k * 3 + j] - m[j * 3 + k]) * s;
+        q[j] = (m[j * 3 + i] + m[i * 3 + j]) * s;
+        q[k] = (m[k * 3 + i] + m[i * 3 + k]) * s;
+    }
+    hd_normalize_rotation(q);
+}
+// T <- exp(upd) * T  (VertexSE3Expmap::oplusImpl, SE3Quat::exp, SE3Quat::operator*)
+__device__ void d_se3_exp_left(const double upd[6], double q[4], double t[3]) {
+    const double w0 = upd[0], w1 = upd[1], w2 = upd[2];
+    const double theta = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
+    const double O[9] = {0, -w2, w1, w2, 0, -w0, -w1, w0, 0};
+    double O2[9], R[9], V[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+            O2[i * 3 + j] = O[i * 3] * O[j] + O[i * 3 + 1] * O[3 + j] + O[i * 3 + 2] * O[6 + j];
+    if (theta < 0.00001) {
+        for (int i = 0; i < 9; i++) { R[i] = (i % 4 == 0 ? 1.0 : 0.0) + O[i] + O2[i]; V[i] = R[i]; }
+    } else {
+        const double a = sin(theta) / theta, b = (1 - cos(theta)) / (theta * theta);
+        const double c = (theta - sin(theta)) / pow(theta, 3);
+        for (int i = 0; i < 9; i++) {
+            const double I = (i % 4 == 0 ? 1.0 : 0.0);
+            R[i] = I + a * O[i] + b * O2[i];
+            V[i] = I + b * O[i] + c * O2[i];
+        }
+    }
+    double qe[4], te[3], rt[3];
+    hd_quat_from_matrix(R, qe);
+    for (int i = 0; i < 3; i++) te[i] = V[i * 3] * upd[3] + V[i * 3 + 1] * upd[4] + V[i * 3 + 2] * upd[5];
+    d_quat_rot(qe, t, rt);
+    for (int i = 0; i < 3; i++) t[i] = te[i] + rt[i];
+    double r[4];
+    r[3] = qe[3] * q[3] - qe[0] * q[0] - qe[1] * q[1] - qe[2] * q[2];
+    r[0] = qe[3] * q[0] + qe[0] * q[3] + qe[1] * q[2] - qe[2] * q[1];
+    r[1] = qe[3] * q[1] + qe[1] * q[3] + qe[2] * q[0] - qe[0] * q[2];
+    r[2] = qe[3] * q[2] + qe[2] * q[3] + qe[0] * q[1] - qe[1] * q[0];
+    hd_normalize_rotation(r);
+    for (int i = 0; i < 4; i++) q[i] = r[i];
+}
+
+// ------------------------------------------------------------------ device state
+
+struct LbaDev {
+    // problem
+    double *q, *t, *X;          // estimates
+    double *bq, *bt, *bX;       // push() backup
+    const uint8_t* fixed;
+    const int32_t *ept, *eps;   // edge -> point, pose
+    const uint8_t* est;         // stereo flag
+    const double *obs, *info, *cam;
+    uint8_t* robust;
+    double* err;                // [NE][3] last computed error
+    // active structure (per optimize())
+    const int32_t* act;         // active edges
+    int nact;
+    const int32_t* poseIdx;     // pose -> hessian index or -1
+    const int32_t* ptLocal;     // global point -> local index or -1 (owned points only)
+    const int32_t* ptGlob;      // local -> global point
+    const int32_t* actPos;      // edge -> position in act (or -1)
+    int P, M;                   // free active poses, owned active points
+    const int32_t *ptStart, *ptEdges;     // CSR by local point (edge ids, sorted by pose index)
+    const int32_t *poStart, *poEdges;     // CSR by pose index (edge ids)
+    const int32_t *prStart, *prE1, *prE2; // CSR by pose-pair block (i<=j), contributions
+    // linearisation (indexed by act position)
+    double *Hll_e, *Hpp_e, *Hpl_e, *bl_e, *bp_e, *BD, *coef, *echi;
+    // reduced per vertex
+    double *Hll, *bl, *Dinv, *Hpp, *bp;
+    double *S, *bs, *x;         // x: [6P + 3M]
+    double* red;                // reduction scratch
+    int* flags;                 // [0] LDLT failure
+};
+
+__device__ __forceinline__ void d_transform(const LbaDev& d, int pose, int pt, double Xc[3]) {
+    double r[3];
+    d_quat_rot(d.q + 4 * pose, d.X + 3 * pt, r);
+    for (int i = 0; i < 3; i++) Xc[i] = r[i] + d.t[3 * pose + i];
+}
+
+__device__ __forceinline__ double d_edge_chi2(const LbaDev& d, int e) {
+    const double* er = d.err + 3 * e;
+    const double w = d.info[e];
+    double s = er[0] * (w * er[0]) + er[1] * (w * er[1]);
+    if (d.est[e]) s += er[2] * (w * er[2]);
+    return s;
+}
+
+// computeError for the active edges; echi[k] = robust chi2 (activeRobustChi2 term)
+__global__ __launch_bounds__(256) void k_edge_errors(LbaDev d, double hmono, double hstereo) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= d.nact) return;
+    const int e = d.act[k];
+    double Xc[3];
+    d_transform(d, d.eps[e], d.ept[e], Xc);
+    const double* cam = d.cam + 5 * e;
+    const double* obs = d.obs + 3 * e;
+    double* er = d.err + 3 * e;
+    if (!d.est[e]) {
+        const double u = Xc[0] / Xc[2], v = Xc[1] / Xc[2];
+        er[0] = obs[0] - (u * cam[0] + cam[2]);
+        er[1] = obs[1] - (v * cam[1] + cam[3]);
+        er[2] = 0;
+    } else {
+        const float invz = (float)(1.0f / Xc[2]);
+        const double r0 = Xc[0] * invz * cam[0] + cam[2];
+        const double r1 = Xc[1] * invz * cam[1] + cam[3];
+        const float bff = (float)cam[4];
+        const double r2 = r0 - (double)(bff * invz);
+        er[0] = obs[0] - r0;
+        er[1] = obs[1] - r1;
+        er[2] = obs[2] - r2;
+    }
+    double chi = d_edge_chi2(d, e);
+    if (d.robust[e]) {
+        const double delta = d.est[e] ? hstereo : hmono, dsqr = delta * delta;
+        if (chi > dsqr) chi = 2 * sqrt(chi) * delta - dsqr;
+    }
+    d.echi[k] = chi;
+}
+
+// Jacobians + Huber-weighted quadratic-form blocks per active edge.
+// Hll_e: 3x3 upper (00 01 02 11 12 22); Hpp_e: 6x6 upper row-major (21); Hpl_e: 6x3; bl_e: 3; bp_e: 6
+__global__ __launch_bounds__(256) void k_edge_linearize(LbaDev d, double hmono, double hstereo) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= d.nact) return;
+    const int e = d.act[k];
+    const int pose = d.eps[e];
+    double R[9], Xc[3];
+    d_quat_to_R(d.q + 4 * pose, R);
+    d_transform(d, pose, d.ept[e], Xc);
+    const double x = Xc[0], y = Xc[1], z = Xc[2], z_2 = z * z;
+    const double* cam = d.cam + 5 * e;
+    const double fx = cam[0], fy = cam[1], bf = cam[4];
+    const bool st = d.est[e] != 0;
+    const int D = st ? 3 : 2;
+    double A[9], B[18];
+    if (!st) {
+        const double tmp[6] = {fx, 0, -x / z * fx, 0, fy, -y / z * fy};
+        for (int r = 0; r < 2; r++)
+            for (int c = 0; c < 3; c++)
+                A[r * 3 + c] = -1. / z * (tmp[r * 3] * R[c] + tmp[r * 3 + 1] * R[3 + c] + tmp[r * 3 + 2] * R[6 + c]);
+        A[6] = A[7] = A[8] = 0;
+    } else {
+        for (int c = 0; c < 3; c++) {
+            A[c] = -fx * R[c] / z + fx * x * R[6 + c] / z_2;
+            A[3 + c] = -fy * R[3 + c] / z + fy * y * R[6 + c] / z_2;
+            A[6 + c] = A[c] - bf * R[6 + c] / z_2;
+        }
+    }
+    B[0] = x * y / z_2 * fx;       B[1] = -(1 + (x * x / z_2)) * fx; B[2] = y / z * fx;
+    B[3] = -1. / z * fx;           B[4] = 0;                         B[5] = x / z_2 * fx;
+    B[6] = (1 + y * y / z_2) * fy; B[7] = -x * y / z_2 * fy;         B[8] = -x / z * fy;
+    B[9] = 0;                      B[10] = -1. / z * fy;             B[11] = y / z_2 * fy;
+    if (st) {
+        B[12] = B[0] - bf * y / z_2; B[13] = B[1] + bf * x / z_2; B[14] = B[2];
+        B[15] = B[3];                B[16] = 0;                   B[17] = B[5] - bf / z_2;
+    } else {
+        for (int i = 12; i < 18; i++) B[i] = 0;
+    }
+    const double w = d.info[e];
+    const double* er = d.err + 3 * e;
+    double rho1 = 1.0;
+    if (d.robust[e]) {
+        const double chi = d_edge_chi2(d, e);
+        const double delta = st ? hstereo : hmono;
+        if (chi > delta * delta) rho1 = delta / sqrt(chi);
+    }
+    const double W = rho1 * w;
+    double om[3];
+    for (int r = 0; r < 3; r++) om[r] = r < D ? -(w * er[r]) * rho1 : 0.0;
+    double* hl = d.Hll_e + 6 * (size_t)k;
+    double* bl = d.bl_e + 3 * (size_t)k;
+    {
+        int o = 0;
+        for (int i = 0; i < 3; i++) {
+            double s = 0;
+            for (int r = 0; r < D; r++) s += A[r * 3 + i] * om[r];
+            bl[i] = s;
+            for (int j = i; j < 3; j++) {
+                double h = 0;
+                for (int r = 0; r < D; r++) h += A[r * 3 + i] * W * A[r * 3 + j];
+                hl[o++] = h;
+            }
+        }
+    }
+    if (d.poseIdx[pose] >= 0) {
+        double* hp = d.Hpp_e + 21 * (size_t)k;
+        double* bp = d.bp_e + 6 * (size_t)k;
+        double* hpl = d.Hpl_e + 18 * (size_t)k;
+        int o = 0;
+        for (int i = 0; i < 6; i++) {
+            double s = 0;
+            for (int r = 0; r < D; r++) s += B[r * 6 + i] * om[r];
+            bp[i] = s;
+            for (int j = i; j < 6; j++) {
+                double h = 0;
+                for (int r = 0; r < D; r++) h += B[r * 6 + i] * W * B[r * 6 + j];
+                hp[o++] = h;
+            }
+            for (int j = 0; j < 3; j++) {
+                double h = 0;
+                for (int r = 0; r < D; r++) h += B[r * 6 + i] * W * A[r * 3 + j];
+                hpl[i * 3 + j] = h;
+            }
+        }
+    }
+}
+
+// Hll, b_l per owned landmark (edges in pose-index order)
+__global__ __launch_bounds__(256) void k_point_reduce(LbaDev d) {
+    const int l = blockIdx.x * 256 + threadIdx.x;
+    if (l >= d.M) return;
+    double h[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
+    for (int a = d.ptStart[l]; a < d.ptStart[l + 1]; a++) {
+        const int k = d.actPos[d.ptEdges[a]];
+        for (int i = 0; i < 6; i++) h[i] += d.Hll_e[6 * (size_t)k + i];
+        for (int i = 0; i < 3; i++) b[i] += d.bl_e[3 * (size_t)k + i];
+    }
+    double* H = d.Hll + 9 * (size_t)l;
+    H[0] = h[0]; H[1] = h[1]; H[2] = h[2];
+    H[3] = h[1]; H[4] = h[3]; H[5] = h[4];
+    H[6] = h[2]; H[7] = h[4]; H[8] = h[5];
+    for (int i = 0; i < 3; i++) d.bl[3 * (size_t)l + i] = b[i];
+}
+
+// Hpp, b_p per pose: one wave per pose, lanes stride over the pose's edges, fixed tree.
+__global__ __launch_bounds__(64) void k_pose_reduce(LbaDev d) {
+    const int p = blockIdx.x, lane = threadIdx.x;
+    double acc[27];
+    for (int i = 0; i < 27; i++) acc[i] = 0;
+    for (int a = d.poStart[p] + lane; a < d.poStart[p + 1]; a += 64) {
+        const int k = d.actPos[d.poEdges[a]];
+        for (int i = 0; i < 21; i++) acc[i] += d.Hpp_e[21 * (size_t)k + i];
+        for (int i = 0; i < 6; i++) acc[21 + i] += d.bp_e[6 * (size_t)k + i];
+    }
+    for (int i = 0; i < 27; i++) {
+        double v = acc[i];
+        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+        acc[i] = v;
+    }
+    if (lane == 0) {
+        double* H = d.Hpp + 36 * (size_t)p;
+        int o = 0;
+        for (int i = 0; i < 6; i++)
+            for (int j = i; j < 6; j++) {
+                H[i * 6 + j] = acc[o];
+                H[j * 6 + i] = acc[o];
+                o++;
+            }
+        for (int i = 0; i < 6; i++) d.bp[6 * (size_t)p + i] = acc[21 + i];
+    }
+}
+
+// Per landmark with lambda: Dinv (Eigen 3x3 cofactor inverse), BD_e = Hpl_e Dinv, coef_e = Hpl_e Dinv b_l
+__global__ __launch_bounds__(256) void k_point_schur(LbaDev d, double lambda) {
+    const int l = blockIdx.x * 256 + threadIdx.x;
+    if (l >= d.M) return;
+    double m[9];
+    for (int i = 0; i < 9; i++) m[i] = d.Hll[9 * (size_t)l + i];
+    m[0] += lambda; m[4] += lambda; m[8] += lambda;
+    double c[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+            c[i * 3 + j] = m[i1 * 3 + j1] * m[i2 * 3 + j2] - m[i1 * 3 + j2] * m[i2 * 3 + j1];
+        }
+    const double det = c[0] * m[0] + c[3] * m[3] + c[6] * m[6];
+    const double invdet = 1.0 / det;
+    double Di[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) Di[j * 3 + i] = c[i * 3 + j] * invdet;
+    for (int i = 0; i < 9; i++) d.Dinv[9 * (size_t)l + i] = Di[i];
+    const double* b = d.bl + 3 * (size_t)l;
+    double db[3];
+    for (int i = 0; i < 3; i++) db[i] = Di[i * 3] * b[0] + Di[i * 3 + 1] * b[1] + Di[i * 3 + 2] * b[2];
+    for (int a = d.ptStart[l]; a < d.ptStart[l + 1]; a++) {
+        const int e = d.ptEdges[a];
+        if (d.poseIdx[d.eps[e]] < 0) continue;
+        const int k = d.actPos[e];
+        const double* Bi = d.Hpl_e + 18 * (size_t)k;
+        double* BD = d.BD + 18 * (size_t)k;
+        double* cf = d.coef + 6 * (size_t)k;
+        for (int r = 0; r < 6; r++) {
+            for (int q = 0; q < 3; q++)
+                BD[r * 3 + q] = Bi[r * 3] * Di[q] + Bi[r * 3 + 1] * Di[3 + q] + Bi[r * 3 + 2] * Di[6 + q];
+            cf[r] = Bi[r * 3] * db[0] + Bi[r * 3 + 1] * db[1] + Bi[r * 3 + 2] * db[2];
+        }
+    }
+}
+
+// S block (i,j), i<=j: (i==j ? Hpp_i + lambda I : 0) - sum_contrib BD_e1 Hpl_e2^T.
+// One wave per block; each lane accumulates its strided contributions, then a fixed butterfly.
+__global__ __launch_bounds__(64) void k_schur_pairs(LbaDev d, double lambda, int addDiag, const int32_t* pairI,
+                                                    const int32_t* pairJ) {
+    const int pr = blockIdx.x, lane = threadIdx.x;
+    const int bi = pairI[pr], bj = pairJ[pr];
+    double acc[36];
+    for (int i = 0; i < 36; i++) acc[i] = 0;
+    for (int c = d.prStart[pr] + lane; c < d.prStart[pr + 1]; c += 64) {
+        const double* BD = d.BD + 18 * (size_t)d.actPos[d.prE1[c]];
+        const double* Bj = d.Hpl_e + 18 * (size_t)d.actPos[d.prE2[c]];
+        for (int r = 0; r < 6; r++)
+            for (int q = 0; q < 6; q++)
+                acc[r * 6 + q] += BD[r * 3] * Bj[q * 3] + BD[r * 3 + 1] * Bj[q * 3 + 1] + BD[r * 3 + 2] * Bj[q * 3 + 2];
+    }
+    for (int i = 0; i < 36; i++) {
+        double v = acc[i];
+        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+        acc[i] = v;
+    }
+    if (lane < 36) {
+        const int r = lane / 6, q = lane % 6;
+        double v = 0.0;
+        if (bi == bj && addDiag) {     // rank 0 carries the (already all-reduced) Hpp + lambda I
+            v = d.Hpp[36 * (size_t)bi + lane];
+            if (r == q) v += lambda;
+        }
+        double s = 0;
+        for (int i = 0; i < 36; i++) s = (i == lane) ? acc[i] : s;
+        v -= s;
+        const int n = 6 * d.P;
+        d.S[(size_t)(6 * bi + r) * n + 6 * bj + q] = v;
+        d.S[(size_t)(6 * bj + q) * n + 6 * bi + r] = v;
+    }
+}
+
+// b_s = b_p - sum_e coef_e, one wave per pose
+__global__ __launch_bounds__(64) void k_bschur(LbaDev d, int addBp) {
+    const int p = blockIdx.x, lane = threadIdx.x;
+    double acc[6] = {0, 0, 0, 0, 0, 0};
+    for (int a = d.poStart[p] + lane; a < d.poStart[p + 1]; a += 64) {
+        const double* cf = d.coef + 6 * (size_t)d.actPos[d.poEdges[a]];
+        for (int i = 0; i < 6; i++) acc[i] += cf[i];
+    }
+    for (int i = 0; i < 6; i++) {
+        double v = acc[i];
+        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+        acc[i] = v;
+    }
+    if (lane < 6) {
+        double s = 0;
+        for (int i = 0; i < 6; i++) s = (i == lane) ? acc[i] : s;
+        d.bs[6 * p + lane] = (addBp ? d.bp[6 * p + lane] : 0.0) - s;
+    }
+}
+
+// Dense LDL^T (no pivoting, fails on a zero pivot like SimplicialLDLT) + solve, one workgroup.
+// A is n x n row-major (full symmetric) in global memory (L2-resident); solution into x[0..n).
+__global__ __launch_bounds__(1024) void k_ldlt_solve(double* __restrict__ A, const double* __restrict__ b, int n,
+                                                     double* __restrict__ x, int* __restrict__ flags) {
+    extern __shared__ __attribute__((aligned(16))) double sh[];
+    double* dg = sh;            // [n] pivots
+    double* col = sh + n;       // [n] current column L(:,j)
+    double* y = sh + 2 * n;     // [n]
+    const int tid = threadIdx.x, nt = blockDim.x;
+    __shared__ int fail;
+    if (tid == 0) fail = 0;
+    __syncthreads();
+    for (int j = 0; j < n; j++) {
+        const double dj = A[(size_t)j * n + j];
+        if (dj == 0.0 || !isfinite(dj)) {
+            if (tid == 0) fail = 1;
+            break;
+        }
+        for (int i = j + 1 + tid; i < n; i += nt) col[i] = A[(size_t)i * n + j] / dj;
+        if (tid == 0) dg[j] = dj;
+        __syncthreads();
+        // trailing update of the lower triangle: A[i][k] -= (L_ij * L_kj) * d_j, j < k <= i
+        const int m = n - j - 1;
+        const long tot = (long)m * (m + 1) / 2;
+        for (long t = tid; t < tot; t += nt) {
+            // map t -> (i, k) with k <= i over the m x m trailing triangle
+            int i = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+            while ((long)i * (i + 1) / 2 > t) i--;
+            while ((long)(i + 1) * (i + 2) / 2 <= t) i++;
+            const int k = (int)(t - (long)i * (i + 1) / 2);
+            const int ii = j + 1 + i, kk = j + 1 + k;
+            A[(size_t)ii * n + kk] -= (col[ii] * col[kk]) * dj;
+        }
+        for (int i = j + 1 + tid; i < n; i += nt) A[(size_t)i * n + j] = col[i];
+        __syncthreads();
+    }
+    __syncthreads();
+    if (fail) {
+        if (tid == 0) flags[0] = 1;
+        return;
+    }
+    // forward L y = b (unit lower), diagonal, backward L^T x = z: wave 0 alone, fixed order.
+    // Lane 0 publishes each y[i] / x[i]; the wave is lock-step, wave_barrier keeps the order.
+    if (tid >= 64) return;
+    const int lane = tid;
+    for (int i = 0; i < n; i++) {
+        double s = 0;
+        for (int k = lane; k < i; k += 64) s += A[(size_t)i * n + k] * y[k];
+        for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+        if (lane == 0) y[i] = b[i] - s;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    for (int i = lane; i < n; i += 64) y[i] = y[i] / dg[i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    for (int i = n - 1; i >= 0; i--) {
+        double s = 0;
+        for (int k = i + 1 + lane; k < n; k += 64) s += A[(size_t)k * n + i] * col[k];
+        for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+        if (lane == 0) col[i] = y[i] - s;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    for (int i = lane; i < n; i += 64) x[i] = col[i];
+    if (lane == 0) flags[0] = 0;
+}
+
+// x_l = Dinv (b_l - sum_e Hpl_e^T x_p(pose_e))
+__global__ __launch_bounds__(256) void k_backsub(LbaDev d) {
+    const int l = blockIdx.x * 256 + threadIdx.x;
+    if (l >= d.M) return;
+    double cl[3] = {d.bl[3 * (size_t)l], d.bl[3 * (size_t)l + 1], d.bl[3 * (size_t)l + 2]};
+    for (int a = d.ptStart[l]; a < d.ptStart[l + 1]; a++) {
+        const int e = d.ptEdges[a];
+        const int pi = d.poseIdx[d.eps[e]];
+        if (pi < 0) continue;
+        const double* Bi = d.Hpl_e + 18 * (size_t)d.actPos[e];
+        for (int q = 0; q < 3; q++)
+            for (int r = 0; r < 6; r++) cl[q] += Bi[r * 3 + q] * (-d.x[6 * pi + r]);
+    }
+    const double* Di = d.Dinv + 9 * (size_t)l;
+    double* xl = d.x + 6 * (size_t)d.P + 3 * (size_t)l;
+    for (int q = 0; q < 3; q++) xl[q] = Di[q * 3] * cl[0] + Di[q * 3 + 1] * cl[1] + Di[q * 3 + 2] * cl[2];
+}
+
+// push (backup) + oplus for all free poses and owned points
+__global__ __launch_bounds__(256) void k_update(LbaDev d, int nposes, const int32_t* freePoses, int applyPoses) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < d.M) {
+        const int g = d.ptGlob[i];
+        for (int j = 0; j < 3; j++) {
+            d.bX[3 * (size_t)g + j] = d.X[3 * (size_t)g + j];
+            d.X[3 * (size_t)g + j] += d.x[6 * (size_t)d.P + 3 * (size_t)i + j];
+        }
+    }
+    if (i < nposes && applyPoses) {
+        const int p = freePoses[i];
+        const int k = d.poseIdx[p];
+        double q[4], t[3], u[6];
+        for (int j = 0; j < 4; j++) { q[j] = d.q[4 * p + j]; d.bq[4 * p + j] = q[j]; }
+        for (int j = 0; j < 3; j++) { t[j] = d.t[3 * p + j]; d.bt[3 * p + j] = t[j]; }
+        for (int j = 0; j < 6; j++) u[j] = d.x[6 * k + j];
+        d_se3_exp_left(u, q, t);
+        for (int j = 0; j < 4; j++) d.q[4 * p + j] = q[j];
+        for (int j = 0; j < 3; j++) d.t[3 * p + j] = t[j];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_pop(LbaDev d, int nposes, const int32_t* freePoses) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < d.M) {
+        const int g = d.ptGlob[i];
+        for (int j = 0; j < 3; j++) d.X[3 * (size_t)g + j] = d.bX[3 * (size_t)g + j];
+    }
+    if (i < nposes) {
+        const int p = freePoses[i];
+        for (int j = 0; j < 4; j++) d.q[4 * p + j] = d.bq[4 * p + j];
+        for (int j = 0; j < 3; j++) d.t[3 * p + j] = d.bt[3 * p + j];
+    }
+}
+
+// Deterministic single-workgroup sum of n doubles (fixed stride assignment + fixed tree).
+__global__ __launch_bounds__(1024) void k_sum(const double* __restrict__ v, int n, double* __restrict__ out) {
+    __shared__ double sh[1024];
+    const int tid = threadIdx.x;
+    double s = 0;
+    for (int i = tid; i < n; i += 1024) s += v[i];
+    sh[tid] = s;
+    __syncthreads();
+    for (int w = 512; w >= 1; w >>= 1) {
+        if (tid < w) sh[tid] += sh[tid + w];
+        __syncthreads();
+    }
+    if (tid == 0) *out = sh[0];
+}
+
+// scale terms: x_j (lambda x_j + b_j) for poses (when includePoses) and owned points
+__global__ __launch_bounds__(256) void k_scale_terms(LbaDev d, double lambda, int includePoses, double* __restrict__ out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int np = 6 * d.P, n = np + 3 * d.M;
+    if (i >= n) return;
+    const double xi = d.x[i];
+    double b;
+    if (i < np) b = includePoses ? d.bp[i] : 0.0;   // only rank 0 contributes the replicated pose part
+    else b = d.bl[i - np];
+    out[i] = (i < np && !includePoses) ? 0.0 : xi * (lambda * xi + b);
+}
+
+// max |diag| of Hpp (global) and Hll (owned): computeLambdaInit's maxDiagonal
+__global__ __launch_bounds__(1024) void k_maxdiag(const double* __restrict__ Hpp, int P, const double* __restrict__ Hll,
+                                                   int M, double* __restrict__ out) {
+    __shared__ double sh[1024];
+    const int tid = threadIdx.x;
+    double m = 0;
+    for (int i = tid; i < 6 * P; i += 1024) m = fmax(m, fabs(Hpp[36 * (i / 6) + 7 * (i % 6)]));
+    for (int i = tid; i < 3 * M; i += 1024) m = fmax(m, fabs(Hll[9 * (i / 3) + 4 * (i % 3)]));
+    sh[tid] = m;
+    __syncthreads();
+    for (int w = 512; w >= 1; w >>= 1) {
+        if (tid < w) sh[tid] = fmax(sh[tid], sh[tid + w]);
+        __syncthreads();
+    }
+    if (tid == 0) *out = sh[0];
+}
+
+// chi2 / depth of every edge (final check and outlier pass): chi2() uses the stored error
+__global__ __launch_bounds__(256) void k_edge_check(LbaDev d, int ne, double* __restrict__ chi2,
+                                                    uint8_t* __restrict__ depthPos) {
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= ne) return;
+    chi2[e] = d_edge_chi2(d, e);
+    double Xc[3];
+    d_transform(d, d.eps[e], d.ept[e], Xc);
+    depthPos[e] = Xc[2] > 0.0 ? 1 : 0;
+}
+
+}  // namespace orbamd
+
+using namespace orbamd;
+
+// ------------------------------------------------------------------ host side
+
+// Keep in sync with lba_problem / lba_options / lba_result in include/orbslam2_amd.h.
+struct lba_context {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool ownStream = true;
+    // communicator
+    int rank = 0, world = 1;
+    double* ws = nullptr;          // caller-owned device workspace (doubles)
+    size_t wsDoubles = 0;
+    lba_allreduce_fn allreduce = nullptr;
+    void* commUser = nullptr;
+    // device buffers
+    std::vector<void*> allocs;
+    // stats
+    double ms_linearize = 0, ms_schur = 0, ms_solve = 0, ms_update = 0;
+    int n_iters = 0, n_trials = 0;
+    bool profile = false;
+    std::vector<hipEvent_t> ev;
+};
+
+static void lba_free_all(lba_context* c) {
+    for (void* p : c->allocs)
+        if (p) (void)hipFree(p);
+    c->allocs.clear();
+}
+
+template <typename T>
+static int dalloc(lba_context* c, T** p, size_t n) {
+    *p = nullptr;
+    if (n == 0) n = 1;
+    if (hipMalloc((void**)p, n * sizeof(T)) != hipSuccess) return ORB_ENOMEM;
+    c->allocs.push_back(*p);
+    return ORB_OK;
+}
+
+#define TRY(x)                 \
+    do {                       \
+        int s_ = (x);          \
+        if (s_) return s_;     \
+    } while (0)
+
+namespace {
+
+struct HostStructure {
+    std::vector<int32_t> act, poseIdx, ptLocal, ptGlob, actPos, ptStart, ptEdges, poStart, poEdges, prStart, prE1,
+        prE2, pairI, pairJ, freePoses;
+    int P = 0, M = 0;
+};
+
+// initializeOptimization(level) (G/core/sparse_optimizer.cpp:199-267) restricted to the
+// landmarks owned by this rank (contiguous range of point indices).
+void build_structure(const lba_problem* p, const std::vector<uint8_t>& level, int lvl, int rank, int world,
+                     HostStructure& s) {
+    const int NP = p->n_poses, NM = p->n_points, NE = p->n_edges;
+    const int own0 = (int)((long long)NM * rank / world), own1 = (int)((long long)NM * (rank + 1) / world);
+    std::vector<uint8_t> poseAct(NP, 0), ptAct(NM, 0);
+    // every rank must see the same pose index mapping: poses active on any rank count
+    for (int e = 0; e < NE; e++) {
+        if (level[e] != lvl) continue;
+        poseAct[p->edge_pose[e]] = 1;
+        ptAct[p->edge_point[e]] = 1;
+    }
+    s.act.clear();
+    for (int e = 0; e < NE; e++) {
+        if (level[e] != lvl) continue;
+        const int pt = p->edge_point[e];
+        if (pt < own0 || pt >= own1) continue;
+        s.act.push_back(e);
+    }
+    std::vector<int> order;
+    for (int i = 0; i < NP; i++)
+        if (poseAct[i] && !p->pose_fixed[i]) order.push_back(i);
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return p->pose_id[a] < p->pose_id[b]; });
+    s.poseIdx.assign(NP, -1);
+    for (size_t k = 0; k < order.size(); k++) s.poseIdx[order[k]] = (int)k;
+    s.freePoses = order;
+    s.P = (int)order.size();
+    order.clear();
+    for (int i = own0; i < own1; i++)
+        if (ptAct[i]) order.push_back(i);
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return p->point_id[a] < p->point_id[b]; });
+    s.ptLocal.assign(NM, -1);
+    for (size_t k = 0; k < order.size(); k++) s.ptLocal[order[k]] = (int)k;
+    s.ptGlob = order;
+    s.M = (int)order.size();
+    s.actPos.assign(NE, -1);
+    for (size_t k = 0; k < s.act.size(); k++) s.actPos[s.act[k]] = (int)k;
+    // CSR by local point, edges sorted by pose index (fixed poses last)
+    s.ptStart.assign(s.M + 1, 0);
+    for (int e : s.act) s.ptStart[s.ptLocal[p->edge_point[e]] + 1]++;
+    for (int i = 0; i < s.M; i++) s.ptStart[i + 1] += s.ptStart[i];
+    s.ptEdges.assign(s.act.size(), 0);
+    {
+        std::vector<int> fill(s.ptStart.begin(), s.ptStart.end() - 1);
+        for (int e : s.act) s.ptEdges[fill[s.ptLocal[p->edge_point[e]]]++] = e;
+        for (int l = 0; l < s.M; l++) {
+            auto key = [&](int e) { const int k = s.poseIdx[p->edge_pose[e]]; return k < 0 ? (1 << 30) : k; };
+            std::stable_sort(s.ptEdges.begin() + s.ptStart[l], s.ptEdges.begin() + s.ptStart[l + 1],
+                             [&](int a, int b) { return key(a) < key(b); });
+        }
+    }
+    // CSR by pose (edges with a free pose, edge order)
+    s.poStart.assign(s.P + 1, 0);
+    for (int e : s.act) {
+        const int k = s.poseIdx[p->edge_pose[e]];
+        if (k >= 0) s.poStart[k + 1]++;
+    }
+    for (int i = 0; i < s.P; i++) s.poStart[i + 1] += s.poStart[i];
+    s.poEdges.assign(s.poStart[s.P], 0);
+    {
+        std::vector<int> fill(s.poStart.begin(), s.poStart.end() - 1);
+        for (int e : s.act) {
+            const int k = s.poseIdx[p->edge_pose[e]];
+            if (k >= 0) s.poEdges[fill[k]++] = e;
+        }
+    }
+    // pose-pair blocks (i <= j) with their contributions (landmark order, then edge order)
+    const int P = s.P;
+    const int npairs = P * (P + 1) / 2;
+    s.pairI.resize(npairs);
+    s.pairJ.resize(npairs);
+    std::vector<int> pairOf((size_t)P * P, -1);
+    {
+        int k = 0;
+        for (int i = 0; i < P; i++)
+            for (int j = i; j < P; j++) {
+                s.pairI[k] = i;
+                s.pairJ[k] = j;
+                pairOf[(size_t)i * P + j] = k++;
+            }
+    }
+    std::vector<int> cnt(npairs + 1, 0);
+    for (int l = 0; l < s.M; l++)
+        for (int a = s.ptStart[l]; a < s.ptStart[l + 1]; a++) {
+            const int i1 = s.poseIdx[p->edge_pose[s.ptEdges[a]]];
+            if (i1 < 0) continue;
+            for (int b = a; b < s.ptStart[l + 1]; b++) {
+                const int i2 = s.poseIdx[p->edge_pose[s.ptEdges[b]]];
+                if (i2 < 0) continue;
+                cnt[pairOf[(size_t)i1 * P + i2] + 1]++;
+            }
+        }
+    for (int i = 0; i < npairs; i++) cnt[i + 1] += cnt[i];
+    s.prStart = cnt;
+    s.prE1.assign(cnt[npairs], 0);
+    s.prE2.assign(cnt[npairs], 0);
+    std::vector<int> fill(cnt.begin(), cnt.end() - 1);
+    for (int l = 0; l < s.M; l++)
+        for (int a = s.ptStart[l]; a < s.ptStart[l + 1]; a++) {
+            const int i1 = s.poseIdx[p->edge_pose[s.ptEdges[a]]];
+            if (i1 < 0) continue;
+            for (int b = a; b < s.ptStart[l + 1]; b++) {
+                const int i2 = s.poseIdx[p->edge_pose[s.ptEdges[b]]];
+                if (i2 < 0) continue;
+                const int pr = pairOf[(size_t)i1 * P + i2];
+                s.prE1[fill[pr]] = s.ptEdges[a];
+                s.prE2[fill[pr]] = s.ptEdges[b];
+                fill[pr]++;
+            }
+        }
+}
+
+template <typename T>
+int upload(lba_context* c, T** dst, const std::vector<T>& v) {
+    TRY(dalloc(c, dst, v.size()));
+    if (!v.empty()) ORB_HIP_TRY(hipMemcpyAsync(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, c->stream));
+    return ORB_OK;
+}
+
+}  // namespace
+
+static int comm_allreduce(lba_context* c, double* dbuf, size_t n, int op) {
+    if (c->world <= 1) return ORB_OK;
+    if (!c->allreduce || !c->ws || n > c->wsDoubles) return ORB_EINVAL;
+    if (dbuf != c->ws) ORB_HIP_TRY(hipMemcpyAsync(c->ws, dbuf, n * 8, hipMemcpyDeviceToDevice, c->stream));
+    if (c->allreduce(c->commUser, 0, n, op) != 0) return ORB_EGPU;
+    if (dbuf != c->ws) ORB_HIP_TRY(hipMemcpyAsync(dbuf, c->ws, n * 8, hipMemcpyDeviceToDevice, c->stream));
+    return ORB_OK;
+}
+
+extern "C" {
+
+int lba_create(int device, lba_context** out) {
+    if (!out) return ORB_EINVAL;
+    int st = check_device(device);
+    if (st) return st;
+    ORB_HIP_TRY(hipSetDevice(device));
+    lba_context* c = new lba_context();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return ORB_EGPU; }
+    *out = c;
+    return ORB_OK;
+}
+
+void lba_destroy(lba_context* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    lba_free_all(c);
+    for (auto e : c->ev) (void)hipEventDestroy(e);
+    if (c->stream && c->ownStream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int lba_set_stream(lba_context* c, void* stream) {
+    if (!c) return ORB_EINVAL;
+    if (c->stream && c->ownStream) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipStreamDestroy(c->stream);
+    }
+    if (stream) {
+        c->stream = (hipStream_t)stream;
+        c->ownStream = false;
+    } else {
+        if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return ORB_EGPU;
+        c->ownStream = true;
+    }
+    return ORB_OK;
+}
+
+int lba_set_comm(lba_context* c, int rank, int world, double* d_workspace, size_t ws_doubles, lba_allreduce_fn fn,
+                 void* user) {
+    if (!c || world < 1 || rank < 0 || rank >= world) return ORB_EINVAL;
+    if (world > 1 && (!d_workspace || !fn)) return ORB_EINVAL;
+    c->rank = rank;
+    c->world = world;
+    c->ws = d_workspace;
+    c->wsDoubles = ws_doubles;
+    c->allreduce = fn;
+    c->commUser = user;
+    return ORB_OK;
+}
+
+int lba_stats(lba_context* c, double* ms4, int* iters, int* trials) {
+    if (!c) return ORB_EINVAL;
+    if (ms4) { ms4[0] = c->ms_linearize; ms4[1] = c->ms_schur; ms4[2] = c->ms_solve; ms4[3] = c->ms_update; }
+    if (iters) *iters = c->n_iters;
+    if (trials) *trials = c->n_trials;
+    return ORB_OK;
+}
+
+int lba_profile(lba_context* c, int enable) {
+    if (!c) return ORB_EINVAL;
+    c->profile = enable != 0;
+    c->ms_linearize = c->ms_schur = c->ms_solve = c->ms_update = 0;
+    c->n_iters = c->n_trials = 0;
+    return ORB_OK;
+}
+
+void lba_pose_from_Tcw(const float Tcw[16], double q[4], double t[3]) {
+    // Converter::toSE3Quat (R/src/Converter.cpp:47-57): float Mat -> Matrix3d -> SE3Quat
+    double R[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) R[i * 3 + j] = (double)Tcw[i * 4 + j];
+    hd_quat_from_matrix(R, q);
+    for (int i = 0; i < 3; i++) t[i] = (double)Tcw[i * 4 + 3];
+}
+
+void lba_pose_to_Tcw(const double q[4], const double t[3], float Tcw[16]) {
+    // Converter::toCvMat(SE3Quat): to_homogeneous_matrix() cast to float
+    const double x = q[0], y = q[1], z = q[2], w = q[3];
+    const double tx = 2 * x, ty = 2 * y, tz = 2 * z;
+    const double twx = tx * w, twy = ty * w, twz = tz * w;
+    const double txx = tx * x, txy = ty * x, txz = tz * x;
+    const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
+    const double R[9] = {1 - (tyy + tzz), txy - twz, txz + twy, txy + twz, 1 - (txx + tzz), tyz - twx,
+                         txz - twy, tyz + twx, 1 - (txx + tyy)};
+    for (int i = 0; i < 3; i++) {
+        for (int j = 0; j < 3; j++) Tcw[i * 4 + j] = (float)R[i * 3 + j];
+        Tcw[i * 4 + 3] = (float)t[i];
+    }
+    Tcw[12] = Tcw[13] = Tcw[14] = 0.f;
+    Tcw[15] = 1.f;
+}
+
+int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const volatile uint8_t* stop, lba_result* r) {
+    if (!c || !p || !o || !r || p->n_poses < 0 || p->n_points < 0 || p->n_edges < 0) return ORB_EINVAL;
+    ORB_HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const int NP = p->n_poses, NM = p->n_points, NE = p->n_edges;
+    r->iterations[0] = r->iterations[1] = 0;
+    r->trials = 0;
+    r->n_trace = 0;
+    r->aborted = 0;
+    if (stop && *stop) {      // R/src/Optimizer.cpp:784-786: return before optimizing, no write-back
+        r->aborted = 1;
+        return ORB_OK;
+    }
+    lba_free_all(c);
+    LbaDev d;
+    std::memset(&d, 0, sizeof(d));
+    double *q, *t, *X, *obs, *info, *cam;
+    uint8_t *fixed, *est, *robust;
+    int32_t *ept, *eps;
+    TRY(dalloc(c, &q, 4 * (size_t)NP)); TRY(dalloc(c, &t, 3 * (size_t)NP)); TRY(dalloc(c, &X, 3 * (size_t)NM));
+    TRY(dalloc(c, &d.bq, 4 * (size_t)NP)); TRY(dalloc(c, &d.bt, 3 * (size_t)NP)); TRY(dalloc(c, &d.bX, 3 * (size_t)NM));
+    TRY(dalloc(c, &fixed, NP)); TRY(dalloc(c, &ept, NE)); TRY(dalloc(c, &eps, NE)); TRY(dalloc(c, &est, NE));
+    TRY(dalloc(c, &obs, 3 * (size_t)NE)); TRY(dalloc(c, &info, NE)); TRY(dalloc(c, &cam, 5 * (size_t)NE));
+    TRY(dalloc(c, &robust, NE)); TRY(dalloc(c, &d.err, 3 * (size_t)NE));
+    ORB_HIP_TRY(hipMemcpyAsync(q, p->pose_q, 32 * (size_t)NP, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(t, p->pose_t, 24 * (size_t)NP, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(X, p->point_xyz, 24 * (size_t)NM, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(fixed, p->pose_fixed, NP, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(ept, p->edge_point, 4 * (size_t)NE, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(eps, p->edge_pose, 4 * (size_t)NE, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(est, p->edge_stereo, NE, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(obs, p->edge_obs, 24 * (size_t)NE, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(info, p->edge_info, 8 * (size_t)NE, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(cam, p->edge_cam, 40 * (size_t)NE, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemsetAsync(robust, 1, NE, s));
+    ORB_HIP_TRY(hipMemsetAsync(d.err, 0, 24 * (size_t)NE, s));
+    d.q = q; d.t = t; d.X = X; d.fixed = fixed; d.ept = ept; d.eps = eps; d.est = est; d.obs = obs; d.info = info;
+    d.cam = cam; d.robust = robust;
+    // per-edge / per-vertex scratch sized for the full problem
+    TRY(dalloc(c, &d.Hll_e, 6 * (size_t)NE)); TRY(dalloc(c, &d.Hpp_e, 21 * (size_t)NE));
+    TRY(dalloc(c, &d.Hpl_e, 18 * (size_t)NE)); TRY(dalloc(c, &d.bl_e, 3 * (size_t)NE));
+    TRY(dalloc(c, &d.bp_e, 6 * (size_t)NE)); TRY(dalloc(c, &d.BD, 18 * (size_t)NE));
+    TRY(dalloc(c, &d.coef, 6 * (size_t)NE)); TRY(dalloc(c, &d.echi, (size_t)NE + 6 * (size_t)NP + 3 * (size_t)NM));
+    TRY(dalloc(c, &d.Hll, 9 * (size_t)NM)); TRY(dalloc(c, &d.bl, 3 * (size_t)NM)); TRY(dalloc(c, &d.Dinv, 9 * (size_t)NM));
+    TRY(dalloc(c, &d.Hpp, 36 * (size_t)NP)); TRY(dalloc(c, &d.bp, 6 * (size_t)NP));
+    const size_t nS = (size_t)6 * NP;
+    TRY(dalloc(c, &d.S, nS * nS + nS));   // S followed by b_s (contiguous for one all-reduce)
+    d.bs = d.S + nS * nS;
+    TRY(dalloc(c, &d.x, 6 * (size_t)NP + 3 * (size_t)NM));
+    TRY(dalloc(c, &d.red, 16));
+    TRY(dalloc(c, &d.flags, 4));
+    double* h_scal = nullptr;
+    if (hipHostMalloc((void**)&h_scal, 64, hipHostMallocDefault) != hipSuccess) return ORB_ENOMEM;
+    struct PinGuard { double* p; ~PinGuard() { if (p) (void)hipHostFree(p); } } pg{h_scal};
+    double* d_chi2 = nullptr;
+    uint8_t* d_depth = nullptr;
+    TRY(dalloc(c, &d_chi2, NE));
+    TRY(dalloc(c, &d_depth, NE));
+
+    std::vector<uint8_t> level(NE, 0), robustH(NE, 1);
+    const double hm = o->huber_mono, hsv = o->huber_stereo;
+    const int maxTrials = o->max_trials > 0 ? o->max_trials : 10;
+    auto stopped = [&]() { return stop && *stop; };
+
+    // events for stage timing
+    auto evt = [&]() -> hipEvent_t {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        c->ev.push_back(e);
+        return e;
+    };
+    hipEvent_t e0 = evt(), e1 = evt(), e2 = evt(), e3 = evt(), e4 = evt();
+    auto elapsed = [&](hipEvent_t a, hipEvent_t b) {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, a, b);
+        return (double)ms;
+    };
+
+    HostStructure hs;
+    int32_t* d_freePoses = nullptr;
+    int32_t *d_pairI = nullptr, *d_pairJ = nullptr;
+    const bool root = c->rank == 0;
+
+    // global sum of the owned-point partials (and replicated pose part) of a scalar vector
+    auto reduce_sum = [&](const double* v, int n, double* out) -> int {
+        hipLaunchKernelGGL(k_sum, dim3(1), dim3(1024), 0, s, v, n, out);
+        return ORB_OK;
+    };
+
+    auto init_opt = [&](int lvl) -> int {
+        build_structure(p, level, lvl, c->rank, c->world, hs);
+        int32_t *act, *poseIdx, *ptLocal, *ptGlob, *actPos, *ptStart, *ptEdges, *poStart, *poEdges, *prStart, *prE1, *prE2;
+        TRY(upload(c, &act, hs.act)); TRY(upload(c, &poseIdx, hs.poseIdx)); TRY(upload(c, &ptLocal, hs.ptLocal));
+        TRY(upload(c, &ptGlob, hs.ptGlob)); TRY(upload(c, &actPos, hs.actPos)); TRY(upload(c, &ptStart, hs.ptStart));
+        TRY(upload(c, &ptEdges, hs.ptEdges)); TRY(upload(c, &poStart, hs.poStart)); TRY(upload(c, &poEdges, hs.poEdges));
+        TRY(upload(c, &prStart, hs.prStart)); TRY(upload(c, &prE1, hs.prE1)); TRY(upload(c, &prE2, hs.prE2));
+        TRY(upload(c, &d_freePoses, hs.freePoses)); TRY(upload(c, &d_pairI, hs.pairI)); TRY(upload(c, &d_pairJ, hs.pairJ));
+        ORB_HIP_TRY(hipMemcpyAsync(robust, robustH.data(), NE, hipMemcpyHostToDevice, s));
+        d.act = act; d.nact = (int)hs.act.size(); d.poseIdx = poseIdx; d.ptLocal = ptLocal; d.ptGlob = ptGlob;
+        d.actPos = actPos; d.P = hs.P; d.M = hs.M; d.ptStart = ptStart; d.ptEdges = ptEdges; d.poStart = poStart;
+        d.poEdges = poEdges; d.prStart = prStart; d.prE1 = prE1; d.prE2 = prE2;
+        d.bs = d.S + (size_t)36 * d.P * d.P;   // b_s right after the 6P x 6P matrix: one all-reduce
+        return ORB_OK;
+    };
+
+    auto grid = [](int n) { return dim3((unsigned)std::max(1, (n + 255) / 256)); };
+
+    // computeActiveErrors + activeRobustChi2 (global over ranks)
+    auto errors_chi2 = [&](double* out_dev) -> int {
+        if (d.nact > 0) hipLaunchKernelGGL(k_edge_errors, grid(d.nact), dim3(256), 0, s, d, hm, hsv);
+        TRY(reduce_sum(d.echi, d.nact, out_dev));
+        TRY(comm_allreduce(c, out_dev, 1, 0));
+        return ORB_OK;
+    };
+
+    // one optimize() call (G/core/sparse_optimizer.cpp:354-419)
+    auto optimize = [&](int iterations, int& itersDone) -> int {
+        itersDone = 0;
+        if (hs.P + hs.M == 0 && c->world == 1) return ORB_OK;
+        double lambda = 0, ni = 2;
+        int nBad = 0;
+        bool ok = true;
+        for (int it = 0; it < iterations && !stopped() && ok; it++) {
+            if (c->profile) (void)hipEventRecord(e0, s);
+            TRY(errors_chi2(d.red));
+            if (d.nact > 0) hipLaunchKernelGGL(k_edge_linearize, grid(d.nact), dim3(256), 0, s, d, hm, hsv);
+            if (d.M > 0) hipLaunchKernelGGL(k_point_reduce, grid(d.M), dim3(256), 0, s, d);
+            if (d.P > 0) hipLaunchKernelGGL(k_pose_reduce, dim3(d.P), dim3(64), 0, s, d);
+            if (c->world > 1 && d.P > 0) {
+                TRY(comm_allreduce(c, d.Hpp, 36 * (size_t)d.P, 0));
+                TRY(comm_allreduce(c, d.bp, 6 * (size_t)d.P, 0));
+            }
+            if (it == 0) {
+                hipLaunchKernelGGL(k_maxdiag, dim3(1), dim3(1024), 0, s, d.Hpp, d.P, d.Hll, d.M, d.red + 1);
+                TRY(comm_allreduce(c, d.red + 1, 1, 1));
+            }
+            ORB_HIP_TRY(hipMemcpyAsync(h_scal, d.red, 16, hipMemcpyDeviceToHost, s));
+            if (c->profile) (void)hipEventRecord(e1, s);
+            ORB_HIP_TRY(hipStreamSynchronize(s));
+            if (c->profile) c->ms_linearize += elapsed(e0, e1);
+            double currentChi = h_scal[0];
+            const double iniChi = currentChi;
+            double tempChi = currentChi;
+            if (it == 0) {
+                lambda = 1e-5 * h_scal[1];   // computeLambdaInit, tau = 1e-5
+                ni = 2;
+                nBad = 0;
+            }
+            double rho = 0;
+            int qmax = 0;
+            do {
+                const double lam = lambda;
+                if (c->profile) (void)hipEventRecord(e0, s);
+                if (d.M > 0) hipLaunchKernelGGL(k_point_schur, grid(d.M), dim3(256), 0, s, d, lam);
+                const int npairs = d.P * (d.P + 1) / 2;
+                if (npairs > 0) {
+                    hipLaunchKernelGGL(k_schur_pairs, dim3(npairs), dim3(64), 0, s, d, lam, root ? 1 : 0, d_pairI, d_pairJ);
+                    hipLaunchKernelGGL(k_bschur, dim3(d.P), dim3(64), 0, s, d, root ? 1 : 0);
+                }
+                if (c->profile) (void)hipEventRecord(e1, s);
+                if (c->world > 1 && d.P > 0) TRY(comm_allreduce(c, d.S, (size_t)36 * d.P * d.P + 6 * (size_t)d.P, 0));
+                if (d.P > 0) {
+                    const int n = 6 * d.P;
+                    hipLaunchKernelGGL(k_ldlt_solve, dim3(1), dim3(1024), 3 * (size_t)n * 8, s, d.S, d.bs, n, d.x, d.flags);
+                } else {
+                    ORB_HIP_TRY(hipMemsetAsync(d.flags, 0, 4, s));
+                }
+                if (c->profile) (void)hipEventRecord(e2, s);
+                if (d.M > 0) hipLaunchKernelGGL(k_backsub, grid(d.M), dim3(256), 0, s, d);
+                hipLaunchKernelGGL(k_update, grid(std::max(d.M, d.P)), dim3(256), 0, s, d, d.P, d_freePoses, 1);
+                TRY(errors_chi2(d.red));
+                const int nx = 6 * d.P + 3 * d.M;
+                hipLaunchKernelGGL(k_scale_terms, grid(nx), dim3(256), 0, s, d, lam, root ? 1 : 0, d.echi);
+                TRY(reduce_sum(d.echi, nx, d.red + 2));
+                TRY(comm_allreduce(c, d.red + 2, 1, 0));
+                ORB_HIP_TRY(hipMemcpyAsync(h_scal, d.red, 24, hipMemcpyDeviceToHost, s));
+                ORB_HIP_TRY(hipMemcpyAsync(h_scal + 4, d.flags, 4, hipMemcpyDeviceToHost, s));
+                if (c->profile) (void)hipEventRecord(e3, s);
+                ORB_HIP_TRY(hipStreamSynchronize(s));
+                if (c->profile) {
+                    c->ms_schur += elapsed(e0, e1);
+                    c->ms_solve += elapsed(e1, e2);
+                    c->ms_update += elapsed(e2, e3);
+                }
+                const int failed = *(int32_t*)(h_scal + 4);
+                tempChi = h_scal[0];
+                if (failed) tempChi = DBL_MAX;
+                rho = currentChi - tempChi;
+                double scale = h_scal[2];
+                scale += 1e-3;
+                rho /= scale;
+                if (rho > 0 && std::isfinite(tempChi)) {
+                    double alpha = 1. - std::pow((2 * rho - 1), 3);
+                    alpha = std::min(alpha, 2. / 3.);
+                    const double sf = std::max(1. / 3., alpha);
+                    lambda *= sf;
+                    ni = 2;
+                    currentChi = tempChi;
+                } else {
+                    lambda *= ni;
+                    ni *= 2;
+                    hipLaunchKernelGGL(k_pop, grid(std::max(d.M, d.P)), dim3(256), 0, s, d, d.P, d_freePoses);
+                }
+                qmax++;
+                r->trials++;
+                c->n_trials++;
+            } while (rho < 0 && qmax < maxTrials && !stopped());
+            if (r->trace && r->n_trace < 64) {
+                double* tr = r->trace + 4 * r->n_trace++;
+                tr[0] = iniChi; tr[1] = currentChi; tr[2] = lambda; tr[3] = qmax;
+            }
+            itersDone++;
+            c->n_iters++;
+            if (o->fixed_iterations) continue;
+            if (qmax == maxTrials || rho == 0) { ok = false; continue; }
+            if ((iniChi - currentChi) * 1e3 < iniChi) nBad++;
+            else nBad = 0;
+            if (nBad >= 3) ok = false;
+        }
+        return ORB_OK;
+    };
+
+    // ---- R/src/Optimizer.cpp:789-841
+    TRY(init_opt(0));
+    TRY(optimize(o->iters1, r->iterations[0]));
+    const bool bDoMore = !stopped();
+    auto edge_check = [&](std::vector<double>& chi, std::vector<uint8_t>& dep) -> int {
+        if (NE > 0) hipLaunchKernelGGL(k_edge_check, grid(NE), dim3(256), 0, s, d, NE, d_chi2, d_depth);
+        chi.resize(NE);
+        dep.resize(NE);
+        if (NE > 0) {
+            ORB_HIP_TRY(hipMemcpyAsync(chi.data(), d_chi2, 8 * (size_t)NE, hipMemcpyDeviceToHost, s));
+            ORB_HIP_TRY(hipMemcpyAsync(dep.data(), d_depth, NE, hipMemcpyDeviceToHost, s));
+        }
+        ORB_HIP_TRY(hipStreamSynchronize(s));
+        return ORB_OK;
+    };
+    std::vector<double> chi;
+    std::vector<uint8_t> dep;
+    const int own0 = (int)((long long)NM * c->rank / c->world), own1 = (int)((long long)NM * (c->rank + 1) / c->world);
+    if (bDoMore) {
+        TRY(edge_check(chi, dep));
+        for (int e = 0; e < NE; e++) {
+            if (p->point_bad && p->point_bad[p->edge_point[e]]) continue;
+            const double thr = p->edge_stereo[e] ? o->chi2_stereo : o->chi2_mono;
+            if (chi[e] > thr || !dep[e]) level[e] = 1;
+            robustH[e] = 0;
+        }
+        // every rank only knows the errors of its own edges: share the level decisions
+        if (c->world > 1) {
+            std::vector<double> lv(NE);
+            for (int e = 0; e < NE; e++) {
+                const int pt = p->edge_point[e];
+                lv[e] = (pt >= own0 && pt < own1) ? (double)level[e] : 0.0;
+            }
+            if (NE > (int)c->wsDoubles) return ORB_EINVAL;
+            ORB_HIP_TRY(hipMemcpyAsync(c->ws, lv.data(), 8 * (size_t)NE, hipMemcpyHostToDevice, s));
+            ORB_HIP_TRY(hipStreamSynchronize(s));
+            if (c->allreduce(c->commUser, 0, NE, 0) != 0) return ORB_EGPU;
+            ORB_HIP_TRY(hipMemcpyAsync(lv.data(), c->ws, 8 * (size_t)NE, hipMemcpyDeviceToHost, s));
+            ORB_HIP_TRY(hipStreamSynchronize(s));
+            for (int e = 0; e < NE; e++) level[e] = lv[e] > 0.5 ? 1 : 0;
+        }
+        TRY(init_opt(0));
+        TRY(optimize(o->iters2, r->iterations[1]));
+    }
+    // ---- final check (R/src/Optimizer.cpp:850-880) and write-back data
+    TRY(edge_check(chi, dep));
+    for (int e = 0; e < NE; e++) {
+        const int pt = p->edge_point[e];
+        const bool mine = pt >= own0 && pt < own1;
+        if (r->edge_chi2) r->edge_chi2[e] = mine ? chi[e] : 0.0;
+        uint8_t er = 0;
+        if (mine && !(p->point_bad && p->point_bad[pt])) {
+            const double thr = p->edge_stereo[e] ? o->chi2_stereo : o->chi2_mono;
+            er = (chi[e] > thr || !dep[e]) ? 1 : 0;
+        }
+        if (r->edge_erase) r->edge_erase[e] = er;
+    }
+    if (r->pose_q) ORB_HIP_TRY(hipMemcpyAsync(r->pose_q, q, 32 * (size_t)NP, hipMemcpyDeviceToHost, s));
+    if (r->pose_t) ORB_HIP_TRY(hipMemcpyAsync(r->pose_t, t, 24 * (size_t)NP, hipMemcpyDeviceToHost, s));
+    if (r->point_xyz) ORB_HIP_TRY(hipMemcpyAsync(r->point_xyz, X, 24 * (size_t)NM, hipMemcpyDeviceToHost, s));
+    ORB_HIP_TRY(hipStreamSynchronize(s));
+    ORB_HIP_TRY(hipGetLastError());
+    return ORB_OK;
+}
+
+}  // extern "C"

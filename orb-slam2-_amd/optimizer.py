@@ -1,0 +1,169 @@
+"""Host mirror of ORB_SLAM2::Optimizer::LocalBundleAdjustment
+(R/include/Optimizer.h:45, R/src/Optimizer.cpp:564-918) over the HIP C-ABI.
+
+The graph-gathering part of the reference (local / fixed keyframes, local map
+points, edge construction, R :569-782) is host bookkeeping on Map/KeyFrame/
+MapPoint objects; callers pass the resulting graph as arrays (see
+synth.ba_problem for the layout).  lba_solve runs the optimisation and the
+outlier passes on the GPU; apply_results mirrors the write-back (R :883-917)."""
+import ctypes as C
+
+import numpy as np
+
+from . import _abi
+
+
+class LbaProblem(C.Structure):
+    _fields_ = [("n_poses", C.c_int), ("pose_q", C.c_void_p), ("pose_t", C.c_void_p), ("pose_fixed", C.c_void_p),
+                ("pose_id", C.c_void_p), ("n_points", C.c_int), ("point_xyz", C.c_void_p), ("point_id", C.c_void_p),
+                ("point_bad", C.c_void_p), ("n_edges", C.c_int), ("edge_point", C.c_void_p),
+                ("edge_pose", C.c_void_p), ("edge_stereo", C.c_void_p), ("edge_obs", C.c_void_p),
+                ("edge_info", C.c_void_p), ("edge_cam", C.c_void_p)]
+
+
+class LbaOptions(C.Structure):
+    _fields_ = [("iters1", C.c_int), ("iters2", C.c_int), ("chi2_mono", C.c_double), ("chi2_stereo", C.c_double),
+                ("huber_mono", C.c_double), ("huber_stereo", C.c_double), ("max_trials", C.c_int),
+                ("fixed_iterations", C.c_int)]
+
+
+class LbaResult(C.Structure):
+    _fields_ = [("pose_q", C.c_void_p), ("pose_t", C.c_void_p), ("point_xyz", C.c_void_p),
+                ("edge_erase", C.c_void_p), ("edge_chi2", C.c_void_p), ("iterations", C.c_int * 2),
+                ("trials", C.c_int), ("trace", C.c_void_p), ("n_trace", C.c_int), ("aborted", C.c_int)]
+
+
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_size_t, C.c_size_t, C.c_int)
+
+
+def options(iters1=5, iters2=10, fixed_iterations=False):
+    """Constants of R/src/Optimizer.cpp:696-697, 790, 814, 841 and g2o's maxTrialsAfterFailure."""
+    return LbaOptions(iters1, iters2, 5.991, 7.815, float(np.float32(np.sqrt(5.991))),
+                      float(np.float32(np.sqrt(7.815))), 10, int(fixed_iterations))
+
+
+def _sig():
+    lib = _abi.lib()
+    if getattr(lib, "_lba_sig", False):
+        return lib
+    vp, i32, sz = C.c_void_p, C.c_int, C.c_size_t
+    for name, args, res in [("lba_create", [i32, vp], C.c_int), ("lba_destroy", [vp], None),
+                            ("lba_set_stream", [vp, vp], C.c_int),
+                            ("lba_set_comm", [vp, i32, i32, vp, sz, ALLREDUCE_FN, vp], C.c_int),
+                            ("lba_solve", [vp, vp, vp, vp, vp], C.c_int), ("lba_profile", [vp, i32], C.c_int),
+                            ("lba_stats", [vp, vp, vp, vp], C.c_int), ("lba_pose_from_Tcw", [vp, vp, vp], None),
+                            ("lba_pose_to_Tcw", [vp, vp, vp], None)]:
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    lib._lba_sig = True
+    return lib
+
+
+def pose_from_Tcw(T):
+    """Converter::toSE3Quat on a float Tcw."""
+    T = np.ascontiguousarray(np.asarray(T, np.float32).reshape(4, 4))
+    q, t = np.zeros(4), np.zeros(3)
+    _sig().lba_pose_from_Tcw(_abi.ptr(T), _abi.ptr(q), _abi.ptr(t))
+    return q, t
+
+
+def pose_to_Tcw(q, t):
+    """Converter::toCvMat(SE3Quat) (float 4x4)."""
+    T = np.zeros((4, 4), np.float32)
+    _sig().lba_pose_to_Tcw(_abi.ptr(np.ascontiguousarray(q, np.float64)), _abi.ptr(np.ascontiguousarray(t, np.float64)),
+                           _abi.ptr(T))
+    return T
+
+
+class LocalBA:
+    """A reusable GPU context (one HIP stream) for LocalBundleAdjustment."""
+
+    def __init__(self, device=0):
+        h = C.c_void_p()
+        _abi.check("lba_create", _sig().lba_create(device, C.byref(h)))
+        self._h = h
+        self._comm = None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _sig().lba_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def set_stream(self, stream_handle):
+        _abi.check("lba_set_stream", _sig().lba_set_stream(self._h, C.c_void_p(stream_handle) if stream_handle else None))
+
+    def set_comm(self, rank, world, workspace, allreduce):
+        """workspace: a float64 device tensor; allreduce(offset, count, op) reduces a slice of it."""
+        def cb(user, offset, count, op):
+            try:
+                allreduce(int(offset), int(count), int(op))
+                return 0
+            except Exception as exc:  # noqa: BLE001 - reported through the C status
+                print(f"lba allreduce failed: {exc}")
+                return 1
+        self._comm = (ALLREDUCE_FN(cb), workspace)
+        _abi.check("lba_set_comm", _sig().lba_set_comm(self._h, rank, world, C.c_void_p(workspace.data_ptr()),
+                                                        workspace.numel(), self._comm[0], None))
+
+    def profile(self, enable=True):
+        _sig().lba_profile(self._h, int(enable))
+
+    def stats(self):
+        ms = np.zeros(4)
+        it, tr = C.c_int(), C.c_int()
+        _sig().lba_stats(self._h, _abi.ptr(ms), C.byref(it), C.byref(tr))
+        return dict(linearize_ms=ms[0], schur_ms=ms[1], solve_ms=ms[2], update_ms=ms[3], iterations=it.value,
+                    trials=tr.value)
+
+    def solve(self, prob, opts=None, stop=None):
+        """prob: dict of arrays (synth.ba_problem layout).  stop: a 1-byte ctypes array
+        polled like mbAbortBA.  Returns a dict with the optimised estimates."""
+        opts = opts or options()
+        nk = len(prob["Tcw"])
+        qs, ts = zip(*[pose_from_Tcw(T) for T in prob["Tcw"]]) if nk else ((), ())
+        q = np.ascontiguousarray(np.array(qs, np.float64).reshape(nk, 4))
+        t = np.ascontiguousarray(np.array(ts, np.float64).reshape(nk, 3))
+        a = {k: np.ascontiguousarray(v) for k, v in prob.items()}
+        P = _abi.ptr
+        pr = LbaProblem(nk, P(q), P(t), P(a["pose_fixed"]), P(a["pose_id"]), len(a["point_xyz"]), P(a["point_xyz"]),
+                        P(a["point_id"]), P(a.get("point_bad")), len(a["edge_point"]), P(a["edge_point"]),
+                        P(a["edge_pose"]), P(a["edge_stereo"]), P(a["edge_obs"]), P(a["edge_info"]), P(a["edge_cam"]))
+        ne = len(a["edge_point"])
+        out = dict(pose_q=np.zeros((nk, 4)), pose_t=np.zeros((nk, 3)), point_xyz=a["point_xyz"].copy(),
+                   edge_erase=np.zeros(ne, np.uint8), edge_chi2=np.zeros(ne), trace=np.zeros((64, 4)))
+        r = LbaResult(P(out["pose_q"]), P(out["pose_t"]), P(out["point_xyz"]), P(out["edge_erase"]),
+                      P(out["edge_chi2"]), (C.c_int * 2)(0, 0), 0, P(out["trace"]), 0, 0)
+        flag = stop if stop is not None else (C.c_uint8 * 1)(0)
+        _abi.check("lba_solve", _sig().lba_solve(self._h, C.byref(pr), C.byref(opts), flag, C.byref(r)))
+        out["iterations"] = (r.iterations[0], r.iterations[1])
+        out["trials"] = r.trials
+        out["trace"] = out["trace"][: r.n_trace]
+        out["aborted"] = bool(r.aborted)
+        out["init_q"], out["init_t"] = q, t
+        return out
+
+
+class Optimizer:
+    """Namespace mirroring ORB_SLAM2::Optimizer's static interface for this path."""
+
+    _ctx = {}
+
+    @staticmethod
+    def LocalBundleAdjustment(problem, pbStopFlag=None, device=0, opts=None):
+        ctx = Optimizer._ctx.get(device)
+        if ctx is None:
+            ctx = Optimizer._ctx[device] = LocalBA(device)
+        return ctx.solve(problem, opts, pbStopFlag)
+
+
+def apply_results(problem, result):
+    """Write-back of R/src/Optimizer.cpp:883-917 on the array form: returns the
+    (keyframe, point) observations to erase and float Tcw / world positions."""
+    erase = [(int(problem["edge_pose"][e]), int(problem["edge_point"][e]))
+             for e in np.nonzero(result["edge_erase"])[0]]
+    Tcw = np.stack([pose_to_Tcw(q, t) for q, t in zip(result["pose_q"], result["pose_t"])])
+    return erase, Tcw, result["point_xyz"].astype(np.float32)

@@ -52,3 +52,103 @@ def frame(cv: np.ndarray, W: int, H: int, t: int) -> np.ndarray:
 def stream(seed: int, W: int, H: int, n: int) -> np.ndarray:
     cv = canvas(seed, W, H)
     return np.stack([frame(cv, W, H, t) for t in range(n)])
+
+
+# ---------------------------------------------------------------- local-BA problem
+
+TUM1 = (517.306408, 516.469215, 318.643040, 255.313989)
+KITTI_BF = 386.1448
+
+
+def _rot(axis_angle):
+    th = float(np.linalg.norm(axis_angle))
+    if th < 1e-12:
+        return np.eye(3)
+    k = axis_angle / th
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
+
+
+def ba_problem(seed=42, n_local=20, n_fixed=4, n_points=3000, stereo_frac=0.0, W=640, H=480,
+               k_range=(2, 8), outlier_frac=0.05, arc=2.0):
+    """Synthetic LocalBundleAdjustment graph: n_local optimised keyframes (id 0 fixed,
+    as mnId==0 is in the reference) on an `arc`-metre arc facing a 4 x 3 x 3 m point
+    volume, n_fixed fixed cameras (lFixedCameras), n_points points each observed by
+    k ~ U{k_range} keyframes it projects into; octave ~ U{0..7} with the extractor's
+    invSigma2, pixel noise N(0, 1.2^octave), outlier_frac outliers at +20 px, poses
+    perturbed by 0.01 rad / 1 cm, points by 2 cm.  Poses are float32 Tcw (KeyFrame::GetPose)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    fx, fy, cx, cy = TUM1
+    nk = n_local + n_fixed
+    centre = np.array([0.0, 0.0, 5.0])
+    radius = 5.0
+    half = arc / radius / 2
+    th = list(np.linspace(-half, half, n_local))
+    for i in range(n_fixed):
+        s = 1 if i % 2 == 0 else -1
+        th.append(s * (half + 0.05 * (i // 2 + 1)))
+    Rcw, tcw = [], []
+    for t in th:
+        C = centre + radius * np.array([np.sin(t), 0.0, -np.cos(t)])
+        z = (centre - C) / np.linalg.norm(centre - C)
+        x = np.array([np.cos(t), 0.0, np.sin(t)])
+        y = np.cross(z, x)
+        Rwc = np.stack([x, y, z], 1) @ _rot(rng.normal(0, 0.02, 3))
+        R = Rwc.T
+        Rcw.append(R)
+        tcw.append(-R @ C)
+    Rcw, tcw = np.array(Rcw), np.array(tcw)
+    inv_sigma2 = (np.float32(1.0) / np.array([np.float32(1.2) ** (2 * l) for l in range(8)], np.float32))
+    pts, e_pt, e_kf, e_st, e_obs, e_oct = [], [], [], [], [], []
+    while len(pts) < n_points:
+        X = np.array([rng.uniform(-2, 2), rng.uniform(-1.5, 1.5), rng.uniform(3.5, 6.5)])
+        Xc = np.einsum("kij,j->ki", Rcw, X) + tcw
+        u = fx * Xc[:, 0] / Xc[:, 2] + cx
+        v = fy * Xc[:, 1] / Xc[:, 2] + cy
+        vis = np.nonzero((Xc[:, 2] > 0.1) & (u >= 0) & (u < W) & (v >= 0) & (v < H))[0]
+        if len(vis) < 2:
+            continue
+        k = min(int(rng.integers(k_range[0], k_range[1] + 1)), len(vis))
+        obs_kf = np.sort(rng.choice(vis, size=k, replace=False))
+        pi = len(pts)
+        pts.append(X)
+        for kf in obs_kf:
+            lvl = int(rng.integers(0, 8))
+            sig = 1.2 ** lvl
+            uo = u[kf] + rng.normal(0, sig)
+            vo = v[kf] + rng.normal(0, sig)
+            if rng.random() < outlier_frac:
+                uo += 20.0
+            stereo = rng.random() < stereo_frac
+            ur = uo - KITTI_BF / Xc[kf, 2] + rng.normal(0, sig) if stereo else -1.0
+            e_pt.append(pi)
+            e_kf.append(int(kf))
+            e_st.append(1 if stereo else 0)
+            e_obs.append([np.float32(uo), np.float32(vo), np.float32(ur)])
+            e_oct.append(lvl)
+    pts = np.array(pts)
+    # perturb the optimised keyframes (not id 0) and the points
+    Tcw = np.zeros((nk, 4, 4), np.float32)
+    for i in range(nk):
+        R, t = Rcw[i], tcw[i]
+        if 0 < i < n_local:
+            R = _rot(rng.normal(0, 0.01 / np.sqrt(3), 3)) @ R
+            t = t + rng.normal(0, 0.01 / np.sqrt(3), 3)
+        Tcw[i, :3, :3] = R
+        Tcw[i, :3, 3] = t
+        Tcw[i, 3, 3] = 1
+    Xp = (pts + rng.normal(0, 0.02 / np.sqrt(3), pts.shape)).astype(np.float32).astype(np.float64)
+    fixed = np.zeros(nk, np.uint8)
+    fixed[0] = 1
+    fixed[n_local:] = 1
+    ne = len(e_pt)
+    cam = np.tile(np.array([fx, fy, cx, cy, np.float32(KITTI_BF)], np.float64), (ne, 1))
+    return {
+        "Tcw": Tcw, "pose_fixed": fixed, "pose_id": np.arange(nk, dtype=np.int64),
+        "point_xyz": Xp, "point_id": np.arange(n_points, dtype=np.int64) + nk,
+        "point_bad": np.zeros(n_points, np.uint8),
+        "edge_point": np.array(e_pt, np.int32), "edge_pose": np.array(e_kf, np.int32),
+        "edge_stereo": np.array(e_st, np.uint8), "edge_obs": np.array(e_obs, np.float64),
+        "edge_info": inv_sigma2[np.array(e_oct)].astype(np.float64), "edge_cam": cam,
+        "edge_octave": np.array(e_oct, np.int32),
+    }

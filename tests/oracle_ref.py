@@ -199,3 +199,62 @@ def hamming_knn2(q, t):
     sd = np.zeros(len(q), np.int32)
     lib().oracle_hamming_knn2(P(q), len(q), P(t), len(t), P(bi), P(bd), P(sd))
     return bi, bd, sd
+
+
+# ---------------------------------------------------------------- local BA oracle
+
+class LbaProblem(C.Structure):
+    _fields_ = [("n_poses", C.c_int), ("pose_q", C.c_void_p), ("pose_t", C.c_void_p), ("pose_fixed", C.c_void_p),
+                ("pose_id", C.c_void_p), ("n_points", C.c_int), ("point_xyz", C.c_void_p), ("point_id", C.c_void_p),
+                ("point_bad", C.c_void_p), ("n_edges", C.c_int), ("edge_point", C.c_void_p),
+                ("edge_pose", C.c_void_p), ("edge_stereo", C.c_void_p), ("edge_obs", C.c_void_p),
+                ("edge_info", C.c_void_p), ("edge_cam", C.c_void_p)]
+
+
+class LbaOptions(C.Structure):
+    _fields_ = [("iters1", C.c_int), ("iters2", C.c_int), ("chi2_mono", C.c_double), ("chi2_stereo", C.c_double),
+                ("huber_mono", C.c_double), ("huber_stereo", C.c_double), ("max_trials", C.c_int),
+                ("fixed_iterations", C.c_int)]
+
+
+class LbaResult(C.Structure):
+    _fields_ = [("pose_q", C.c_void_p), ("pose_t", C.c_void_p), ("point_xyz", C.c_void_p),
+                ("edge_erase", C.c_void_p), ("edge_chi2", C.c_void_p), ("iterations", C.c_int * 2),
+                ("trials", C.c_int), ("trace", C.c_void_p), ("n_trace", C.c_int)]
+
+
+def lba_options(iters1=5, iters2=10, fixed_iterations=False):
+    return LbaOptions(iters1, iters2, 5.991, 7.815, float(np.float32(np.sqrt(5.991))),
+                      float(np.float32(np.sqrt(7.815))), 10, int(fixed_iterations))
+
+
+def quat_from_Tcw(T):
+    R = np.ascontiguousarray(np.asarray(T, np.float32)[:3, :3].astype(np.float64))
+    q = np.zeros(4)
+    lib().oracle_quat_from_matrix(P(R), P(q))
+    return q, np.asarray(T, np.float32)[:3, 3].astype(np.float64)
+
+
+def lba_solve(prob, options=None, stop=False):
+    options = options or lba_options()
+    nk = len(prob["Tcw"])
+    qs, ts = zip(*[quat_from_Tcw(T) for T in prob["Tcw"]])
+    keep = dict(q=np.ascontiguousarray(qs), t=np.ascontiguousarray(ts))
+    arr = {k: np.ascontiguousarray(v) for k, v in prob.items()}
+    pr = LbaProblem(nk, P(keep["q"]), P(keep["t"]), P(arr["pose_fixed"]), P(arr["pose_id"]),
+                    len(arr["point_xyz"]), P(arr["point_xyz"]), P(arr["point_id"]), P(arr["point_bad"]),
+                    len(arr["edge_point"]), P(arr["edge_point"]), P(arr["edge_pose"]), P(arr["edge_stereo"]),
+                    P(arr["edge_obs"]), P(arr["edge_info"]), P(arr["edge_cam"]))
+    out = dict(pose_q=np.zeros((nk, 4)), pose_t=np.zeros((nk, 3)), point_xyz=np.zeros_like(arr["point_xyz"]),
+               edge_erase=np.zeros(len(arr["edge_point"]), np.uint8), edge_chi2=np.zeros(len(arr["edge_point"])),
+               trace=np.zeros((64, 4)))
+    r = LbaResult(P(out["pose_q"]), P(out["pose_t"]), P(out["point_xyz"]), P(out["edge_erase"]),
+                  P(out["edge_chi2"]), (C.c_int * 2)(0, 0), 0, P(out["trace"]), 0)
+    flag = (C.c_uint8 * 1)(1 if stop else 0)
+    st = lib().oracle_lba_solve(C.byref(pr), C.byref(options), flag, C.byref(r))
+    out["status"] = st
+    out["iterations"] = (r.iterations[0], r.iterations[1])
+    out["trials"] = r.trials
+    out["trace"] = out["trace"][: r.n_trace]
+    out["init_q"], out["init_t"] = keep["q"], keep["t"]
+    return out
