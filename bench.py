@@ -46,6 +46,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-lba", action="store_true")
+    ap.add_argument("--lba-solves", type=int, default=5, help="timed LocalBundleAdjustment calls")
+    ap.add_argument("--lba-points", type=int, default=3000)
+    ap.add_argument("--lba-kf", type=int, default=20)
     return ap.parse_args()
 
 
@@ -101,6 +105,65 @@ def cpu_baseline(frames, nfeatures, budget_s):
                       f"{nfeatures} feat, oracle C restatement, {threads} host threads (1 frame per thread)"}
 
 
+def bench_lba(args, amd, dev, local, rank, world):
+    """Local BA (BASELINE.json config 4: 20 KF x 3000 points), landmarks sharded over ranks
+    with RCCL all-reduce of the reduced camera system.  ms/iter = wall time of the
+    optimisation / LM outer iterations executed (both optimize() rounds)."""
+    from orb_slam2_amd import synth
+    pb = synth.ba_problem(n_local=args.lba_kf, n_points=args.lba_points)
+    nk, ne = len(pb["Tcw"]), len(pb["edge_point"])
+    ctx = amd.LocalBA(local)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    if world > 1:
+        ws = torch.zeros(max(36 * nk * nk + 6 * nk, ne) + 64, dtype=torch.float64, device=dev)
+
+        def ar(off, cnt, op):
+            torch.distributed.all_reduce(ws[off:off + cnt], op=torch.distributed.ReduceOp.SUM if op == 0
+                                         else torch.distributed.ReduceOp.MAX)
+        ctx.set_comm(rank, world, ws, ar)
+    ctx.solve(pb)                      # warm-up (allocations, code objects)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    ctx.profile(True)
+    iters, times = 0, []
+    for _ in range(args.lba_solves):
+        t0 = time.perf_counter()
+        r = ctx.solve(pb)
+        times.append(time.perf_counter() - t0)
+        iters += sum(r["iterations"])
+    st = ctx.stats()
+    tot = sum(times)
+    if world > 1:
+        t = torch.tensor([tot], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        tot = float(t.item())
+    out = {"config": f"{args.lba_kf} KF (+4 fixed) x {args.lba_points} points, {ne} mono edges, "
+                     f"landmarks sharded x{world}",
+           "ms_per_iter": round(1000 * tot / max(iters, 1), 4),
+           "solve_ms": round(1000 * tot / args.lba_solves, 3),
+           "iterations_per_solve": iters / args.lba_solves, "trials": st["trials"] / args.lba_solves,
+           "stage_ms_per_solve": {k: round(st[k] / args.lba_solves, 4) for k in
+                                  ("linearize_ms", "schur_ms", "solve_ms", "update_ms")},
+           "n_gpus": world}
+    if rank == 0 and not args.no_cpu:
+        sys.path.insert(0, str(ROOT / "tests"))
+        import oracle_ref as O
+        t0 = time.perf_counter()
+        n, it = 0, 0
+        while time.perf_counter() - t0 < 3.0 or n < 2:
+            rr = O.lba_solve(pb)
+            it += sum(rr["iterations"])
+            n += 1
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"ms_per_iter": round(1000 * dt / it, 4), "solve_ms": round(1000 * dt / n, 3),
+                               "cores": 1, "kind": "port",
+                               "sample": f"{n} LocalBundleAdjustment solves, oracle C restatement of g2o "
+                                         f"LM+Schur (dense LDLT), 1 thread (reference builds g2o without OpenMP)"}
+        out["speedup_vs_cpu"] = round(out["cpu_baseline"]["ms_per_iter"] / out["ms_per_iter"], 2)
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -110,6 +173,8 @@ def main():
         torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    # all work (torch copies, HIP kernels, collectives) on one explicit non-default stream
+    torch.cuda.set_stream(torch.cuda.Stream(dev))
     amd = pkgload.load()
     from orb_slam2_amd import _abi, synth
 
@@ -181,7 +246,7 @@ def main():
     nmatch = nm.cpu().numpy()
 
     result = {
-        "metric": "frames/sec ORB extract+match @640x480",
+        "metric": "frames/sec ORB extract+match @640x480; local-BA ms/iter",
         "value": round(value, 2),
         "unit": "frames/s",
         "n_gpus": world,
@@ -215,6 +280,8 @@ def main():
                               "traffic": None,
                               "launch_ms": round(float(per_launch_ms[dom]), 4)}
         result["stage_ms_per_batch"] = {k: round(float(v), 4) for k, v in zip(STAGES, per_launch_ms)}
+    if not args.no_lba:
+        result["lba"] = bench_lba(args, amd, dev, local, rank, world)
     if rank == 0 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(pool_np[: min(len(pool_np), 512)], NF, args.cpu_seconds)
         result["speedup_vs_cpu_baseline"] = round(value / result["cpu_baseline"]["value"], 1)

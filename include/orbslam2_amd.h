@@ -252,7 +252,10 @@ typedef int (*lba_allreduce_fn)(void* user, size_t offset_doubles, size_t count,
 
 int lba_create(int device, lba_context** out);
 void lba_destroy(lba_context* c);
-int lba_set_stream(lba_context* c, void* stream);
+/* use_given = 1: run on `stream` (a hipStream_t; NULL = the legacy default stream), e.g.
+ * the caller's torch stream so its all-reduces are ordered with the solver's work;
+ * use_given = 0: a private non-blocking stream (the default). */
+int lba_set_stream(lba_context* c, void* stream, int use_given);
 /* Shards the landmarks over `world` ranks (rank r owns the contiguous index range
  * [r*M/world, (r+1)*M/world)); every rank passes the same full problem. */
 int lba_set_comm(lba_context* c, int rank, int world, double* d_workspace, size_t ws_doubles,

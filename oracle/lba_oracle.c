@@ -143,7 +143,16 @@ typedef struct {
     int* pt_edge_start; int* pt_edges;   /* active edges grouped by point index (ascending pose index) */
     double lambda, ni;
     int nBad;
+    /* landmark sharding (oracle_lba_solve_dist): this rank owns points [own0, own1) */
+    int rank, world, own0, own1;
+    oracle_allreduce_fn ar;
+    void* ar_user;
 } lba_ctx;
+
+static void allreduce(lba_ctx* c, double* v, int n, int op)
+{
+    if (c->world > 1 && n > 0) c->ar(c->ar_user, v, n, op);
+}
 
 static void transform(const lba_ctx* c, int pose, int pt, double Xc[3])
 {
@@ -261,9 +270,11 @@ static void init_optimization(lba_ctx* c, int level)
     for (int e = 0; e < p->n_edges; e++) {
         if (c->level[e] != level) continue;
         /* allVerticesFixed() is false: points are never fixed */
+        pose_act[p->edge_pose[e]] = 1;         /* pose mapping is global across ranks */
+        const int pt = p->edge_point[e];
+        if (pt < c->own0 || pt >= c->own1) continue;
         c->act_edges[c->n_act++] = e;
-        pose_act[p->edge_pose[e]] = 1;
-        pt_act[p->edge_point[e]] = 1;
+        pt_act[pt] = 1;
     }
     /* index mapping: free active poses by id, then active points by id (G/core/sparse_optimizer.cpp:166-190) */
     int* order = (int*)malloc(sizeof(int) * (p->n_poses + p->n_points + 1));
@@ -371,13 +382,20 @@ static void build_system(lba_ctx* c)
     }
 }
 
-static double lambda_init(const lba_ctx* c)
+static void share_pose_system(lba_ctx* c)
+{
+    allreduce(c, c->Hpp, 36 * c->P, 0);
+    allreduce(c, c->bp, 6 * c->P, 0);
+}
+
+static double lambda_init(lba_ctx* c)
 {
     double m = 0.;
     for (int i = 0; i < c->P; i++)
         for (int j = 0; j < 6; j++) m = fmax(fabs(c->Hpp[36 * i + j * 7]), m);
     for (int i = 0; i < c->M; i++)
         for (int j = 0; j < 3; j++) m = fmax(fabs(c->Hll[9 * i + j * 4]), m);
+    allreduce(c, &m, 1, 1);
     return 1e-5 * m;
 }
 
@@ -402,7 +420,8 @@ static int schur_solve(lba_ctx* c, double lambda)
     const int np = 6 * c->P;
     double* S = c->S;
     memset(S, 0, sizeof(double) * np * np);
-    for (int i = 0; i < c->P; i++)
+    const int root = c->rank == 0;
+    for (int i = 0; i < c->P && root; i++)
         for (int r = 0; r < 6; r++)
             for (int q = 0; q < 6; q++) S[(6 * i + r) * np + 6 * i + q] = c->Hpp[36 * i + r * 6 + q] + (r == q ? lambda : 0.);
     double* coef = (double*)calloc(np + 1, sizeof(double));
@@ -443,7 +462,9 @@ static int schur_solve(lba_ctx* c, double lambda)
     for (int r = 0; r < np; r++)
         for (int q = 0; q < r; q++) S[r * np + q] = S[q * np + r];
     double* bs = (double*)malloc(sizeof(double) * (np + 1));
-    for (int i = 0; i < np; i++) bs[i] = c->bp[i] - coef[i];
+    for (int i = 0; i < np; i++) bs[i] = (root ? c->bp[i] : 0.0) - coef[i];
+    allreduce(c, S, np * np, 0);
+    allreduce(c, bs, np, 0);
     /* dense LDL^T (no pivoting); fails only on an exactly zero pivot, like SimplicialLDLT */
     int ok = 1;
     double* d = (double*)malloc(sizeof(double) * (np + 1));
@@ -528,6 +549,7 @@ static double active_robust_chi2(lba_ctx* c)
 {
     double s = 0;
     for (int k = 0; k < c->n_act; k++) s += robust_chi2(c, c->act_edges[k]);
+    allreduce(c, &s, 1, 0);
     return s;
 }
 static void compute_active_errors(lba_ctx* c)
@@ -545,6 +567,7 @@ static int lm_iteration(lba_ctx* c, int iteration, const volatile uint8_t* stop,
     double tempChi = currentChi;
     const double iniChi = currentChi;
     build_system(c);
+    share_pose_system(c);
     if (iteration == 0) {
         c->lambda = lambda_init(c);
         c->ni = 2;
@@ -564,8 +587,10 @@ static int lm_iteration(lba_ctx* c, int iteration, const volatile uint8_t* stop,
         if (!ok2) tempChi = DBL_MAX;
         rho = currentChi - tempChi;
         double scale = 0.;
-        for (int j = 0; j < 6 * c->P; j++) scale += c->x[j] * (lam * c->x[j] + c->bp[j]);
+        if (c->rank == 0)
+            for (int j = 0; j < 6 * c->P; j++) scale += c->x[j] * (lam * c->x[j] + c->bp[j]);
         for (int j = 0; j < 3 * c->M; j++) scale += c->x[6 * c->P + j] * (lam * c->x[6 * c->P + j] + c->bl[j]);
+        allreduce(c, &scale, 1, 0);
         scale += 1e-3;
         rho /= scale;
         if (rho > 0 && isfinite(tempChi)) {
@@ -597,7 +622,7 @@ static int lm_iteration(lba_ctx* c, int iteration, const volatile uint8_t* stop,
 
 static int optimize(lba_ctx* c, int iterations, const volatile uint8_t* stop, lba_result_t* r)
 {
-    if (c->P + c->M == 0) return 0;
+    if (c->P + c->M == 0 && c->world == 1) return 0;
     int it = 0, ok = 1;
     for (int i = 0; i < iterations && !(stop && *stop) && ok; i++) {
         ok = lm_iteration(c, i, stop, r) == LM_OK;
@@ -608,10 +633,22 @@ static int optimize(lba_ctx* c, int iterations, const volatile uint8_t* stop, lb
 
 int oracle_lba_solve(const lba_problem_t* p, const lba_options_t* o, const volatile uint8_t* stop, lba_result_t* r)
 {
+    return oracle_lba_solve_dist(p, o, stop, r, 0, 1, NULL, NULL);
+}
+
+int oracle_lba_solve_dist(const lba_problem_t* p, const lba_options_t* o, const volatile uint8_t* stop,
+                          lba_result_t* r, int rank, int world, oracle_allreduce_fn ar, void* user)
+{
     lba_ctx c;
     memset(&c, 0, sizeof(c));
     c.p = p;
     c.o = o;
+    c.rank = rank;
+    c.world = world;
+    c.ar = ar;
+    c.ar_user = user;
+    c.own0 = (int)((long long)p->n_points * rank / world);
+    c.own1 = (int)((long long)p->n_points * (rank + 1) / world);
     const int NP = p->n_poses, NM = p->n_points, NE = p->n_edges;
     c.pq = (double*)malloc(sizeof(double) * 4 * (NP + 1));
     c.pt = (double*)malloc(sizeof(double) * 3 * (NP + 1));
@@ -659,15 +696,26 @@ int oracle_lba_solve(const lba_problem_t* p, const lba_options_t* o, const volat
             if (edge_chi2(&c, e) > thr || !depth_positive(&c, e)) c.level[e] = 1;
             c.robust[e] = 0;
         }
+        if (world > 1) {   /* each rank decided only its own edges: share the level vector */
+            double* lv = (double*)calloc(NE + 1, sizeof(double));
+            for (int e = 0; e < NE; e++) {
+                const int pt = p->edge_point[e];
+                lv[e] = (pt >= c.own0 && pt < c.own1) ? (double)c.level[e] : 0.0;
+            }
+            allreduce(&c, lv, NE, 0);
+            for (int e = 0; e < NE; e++) c.level[e] = lv[e] > 0.5 ? 1 : 0;
+            free(lv);
+        }
         init_optimization(&c, 0);
         r->iterations[1] = optimize(&c, o->iters2, stop, r);
     }
     /* final check (R/src/Optimizer.cpp:850-880): e->chi2() uses each edge's last computed error */
     for (int e = 0; e < NE; e++) {
-        const double chi = edge_chi2(&c, e);
+        const int mine = p->edge_point[e] >= c.own0 && p->edge_point[e] < c.own1;
+        const double chi = mine ? edge_chi2(&c, e) : 0.0;
         if (r->edge_chi2) r->edge_chi2[e] = chi;
         uint8_t er = 0;
-        if (!(p->point_bad && p->point_bad[p->edge_point[e]])) {
+        if (mine && !(p->point_bad && p->point_bad[p->edge_point[e]])) {
             const double thr = p->edge_stereo[e] ? o->chi2_stereo : o->chi2_mono;
             er = (chi > thr || !depth_positive(&c, e)) ? 1 : 0;
         }

@@ -66,6 +66,13 @@ typedef struct {
 int oracle_lba_solve(const lba_problem_t* p, const lba_options_t* o, const volatile uint8_t* stop,
                      lba_result_t* r);
 
+/* Landmark-sharded variant (the multi-GPU algorithm of liborbslam2_amd): rank
+ * `rank` of `world` owns points [rank*M/world, (rank+1)*M/world); `ar` all-reduces
+ * n doubles in place across ranks (op 0 sum, 1 max). */
+typedef void (*oracle_allreduce_fn)(void* user, double* v, int n, int op);
+int oracle_lba_solve_dist(const lba_problem_t* p, const lba_options_t* o, const volatile uint8_t* stop,
+                          lba_result_t* r, int rank, int world, oracle_allreduce_fn ar, void* user);
+
 /* Helpers shared with tests: Converter::toSE3Quat / SE3Quat::exp semantics. */
 void oracle_quat_from_matrix(const double R[9], double q[4]);
 void oracle_se3_exp_left(const double upd[6], const double q[4], const double t[3], double qo[4], double to[3]);

@@ -424,72 +424,68 @@ __global__ __launch_bounds__(64) void k_bschur(LbaDev d, int addBp) {
     }
 }
 
-// Dense LDL^T (no pivoting, fails on a zero pivot like SimplicialLDLT) + solve, one workgroup.
-// A is n x n row-major (full symmetric) in global memory (L2-resident); solution into x[0..n).
-__global__ __launch_bounds__(1024) void k_ldlt_solve(double* __restrict__ A, const double* __restrict__ b, int n,
+// Dense LDL^T (no pivoting; fails only on a zero pivot, like SimplicialLDLT) + solve, one
+// workgroup of 1024 threads.  The n x n matrix is staged in LDS when it fits (n <= 136, i.e.
+// up to 22 free keyframes), otherwise factored in place in global memory (L2-resident).
+// Right-looking elimination: per column j, L(:,j) = A(:,j)/d_j, then the trailing lower
+// triangle A(i,k) -= (L_ij L_kj) d_j.  The triangular solves run column-oriented on one wave.
+template <bool kLds>
+__global__ __launch_bounds__(1024) void k_ldlt_solve(double* __restrict__ Ag, const double* __restrict__ b, int n,
                                                      double* __restrict__ x, int* __restrict__ flags) {
     extern __shared__ __attribute__((aligned(16))) double sh[];
-    double* dg = sh;            // [n] pivots
-    double* col = sh + n;       // [n] current column L(:,j)
-    double* y = sh + 2 * n;     // [n]
+    double* A = kLds ? sh : Ag;
+    double* dg = sh + (kLds ? (size_t)n * n : 0);
+    double* col = dg + n;
+    double* y = col + n;
     const int tid = threadIdx.x, nt = blockDim.x;
-    __shared__ int fail;
-    if (tid == 0) fail = 0;
+    if (kLds)
+        for (int t = tid; t < n * n; t += nt) A[t] = Ag[t];
+    for (int t = tid; t < n; t += nt) y[t] = b[t];
     __syncthreads();
+    int fail = 0;
     for (int j = 0; j < n; j++) {
         const double dj = A[(size_t)j * n + j];
-        if (dj == 0.0 || !isfinite(dj)) {
-            if (tid == 0) fail = 1;
+        if (dj == 0.0 || !isfinite(dj)) {   // uniform: every thread reads the same value
+            fail = 1;
             break;
         }
         for (int i = j + 1 + tid; i < n; i += nt) col[i] = A[(size_t)i * n + j] / dj;
         if (tid == 0) dg[j] = dj;
         __syncthreads();
-        // trailing update of the lower triangle: A[i][k] -= (L_ij * L_kj) * d_j, j < k <= i
         const int m = n - j - 1;
-        const long tot = (long)m * (m + 1) / 2;
-        for (long t = tid; t < tot; t += nt) {
-            // map t -> (i, k) with k <= i over the m x m trailing triangle
-            int i = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
-            while ((long)i * (i + 1) / 2 > t) i--;
-            while ((long)(i + 1) * (i + 2) / 2 <= t) i++;
-            const int k = (int)(t - (long)i * (i + 1) / 2);
+        for (int t = tid; t < m * m; t += nt) {
+            const int i = t / m, k = t % m;
+            if (k > i) continue;
             const int ii = j + 1 + i, kk = j + 1 + k;
             A[(size_t)ii * n + kk] -= (col[ii] * col[kk]) * dj;
         }
         for (int i = j + 1 + tid; i < n; i += nt) A[(size_t)i * n + j] = col[i];
         __syncthreads();
     }
-    __syncthreads();
     if (fail) {
         if (tid == 0) flags[0] = 1;
         return;
     }
-    // forward L y = b (unit lower), diagonal, backward L^T x = z: wave 0 alone, fixed order.
-    // Lane 0 publishes each y[i] / x[i]; the wave is lock-step, wave_barrier keeps the order.
     if (tid >= 64) return;
-    const int lane = tid;
-    for (int i = 0; i < n; i++) {
-        double s = 0;
-        for (int k = lane; k < i; k += 64) s += A[(size_t)i * n + k] * y[k];
-        for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
-        if (lane == 0) y[i] = b[i] - s;
+    // forward substitution, column oriented: y_k final -> y_i -= L_ik y_k (i > k)
+    for (int k = 0; k < n; k++) {
+        const double yk = y[k];
+        for (int i = k + 1 + tid; i < n; i += 64) y[i] -= A[(size_t)i * n + k] * yk;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
     }
-    for (int i = lane; i < n; i += 64) y[i] = y[i] / dg[i];
+    for (int i = tid; i < n; i += 64) y[i] = y[i] / dg[i];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    for (int i = n - 1; i >= 0; i--) {
-        double s = 0;
-        for (int k = i + 1 + lane; k < n; k += 64) s += A[(size_t)k * n + i] * col[k];
-        for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
-        if (lane == 0) col[i] = y[i] - s;
+    // backward substitution with L^T: x_k final -> y_i -= L_ki x_k (i < k)
+    for (int k = n - 1; k >= 0; k--) {
+        const double xk = y[k];
+        for (int i = tid; i < k; i += 64) y[i] -= A[(size_t)k * n + i] * xk;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
     }
-    for (int i = lane; i < n; i += 64) x[i] = col[i];
-    if (lane == 0) flags[0] = 0;
+    for (int i = tid; i < n; i += 64) x[i] = y[i];
+    if (tid == 0) flags[0] = 0;
 }
 
 // x_l = Dinv (b_l - sum_e Hpl_e^T x_p(pose_e))
@@ -811,13 +807,14 @@ void lba_destroy(lba_context* c) {
     delete c;
 }
 
-int lba_set_stream(lba_context* c, void* stream) {
+int lba_set_stream(lba_context* c, void* stream, int use_given) {
     if (!c) return ORB_EINVAL;
     if (c->stream && c->ownStream) {
         (void)hipStreamSynchronize(c->stream);
         (void)hipStreamDestroy(c->stream);
     }
-    if (stream) {
+    c->stream = nullptr;
+    if (use_given) {   // NULL = the device's legacy default stream
         c->stream = (hipStream_t)stream;
         c->ownStream = false;
     } else {
@@ -1045,7 +1042,12 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
                 if (c->world > 1 && d.P > 0) TRY(comm_allreduce(c, d.S, (size_t)36 * d.P * d.P + 6 * (size_t)d.P, 0));
                 if (d.P > 0) {
                     const int n = 6 * d.P;
-                    hipLaunchKernelGGL(k_ldlt_solve, dim3(1), dim3(1024), 3 * (size_t)n * 8, s, d.S, d.bs, n, d.x, d.flags);
+                    if ((size_t)n * n * 8 + 3 * (size_t)n * 8 <= 160 * 1024)
+                        hipLaunchKernelGGL(k_ldlt_solve<true>, dim3(1), dim3(1024), ((size_t)n * n + 3 * (size_t)n) * 8, s,
+                                           d.S, d.bs, n, d.x, d.flags);
+                    else
+                        hipLaunchKernelGGL(k_ldlt_solve<false>, dim3(1), dim3(1024), 3 * (size_t)n * 8, s, d.S, d.bs, n,
+                                           d.x, d.flags);
                 } else {
                     ORB_HIP_TRY(hipMemsetAsync(d.flags, 0, 4, s));
                 }

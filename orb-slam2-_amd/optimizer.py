@@ -48,7 +48,7 @@ def _sig():
         return lib
     vp, i32, sz = C.c_void_p, C.c_int, C.c_size_t
     for name, args, res in [("lba_create", [i32, vp], C.c_int), ("lba_destroy", [vp], None),
-                            ("lba_set_stream", [vp, vp], C.c_int),
+                            ("lba_set_stream", [vp, vp, i32], C.c_int),
                             ("lba_set_comm", [vp, i32, i32, vp, sz, ALLREDUCE_FN, vp], C.c_int),
                             ("lba_solve", [vp, vp, vp, vp, vp], C.c_int), ("lba_profile", [vp, i32], C.c_int),
                             ("lba_stats", [vp, vp, vp, vp], C.c_int), ("lba_pose_from_Tcw", [vp, vp, vp], None),
@@ -94,7 +94,9 @@ class LocalBA:
         self.close()
 
     def set_stream(self, stream_handle):
-        _abi.check("lba_set_stream", _sig().lba_set_stream(self._h, C.c_void_p(stream_handle) if stream_handle else None))
+        """Run on the given hipStream_t handle (e.g. torch.cuda.current_stream().cuda_stream;
+        0 = the legacy default stream) so torch collectives are ordered with the solver."""
+        _abi.check("lba_set_stream", _sig().lba_set_stream(self._h, C.c_void_p(stream_handle or 0), 1))
 
     def set_comm(self, rank, world, workspace, allreduce):
         """workspace: a float64 device tensor; allreduce(offset, count, op) reduces a slice of it."""
