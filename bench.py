@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=64, help="frames per step per GPU")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="independent frame sequences per GPU, each on its own HIP stream (batch split)")
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--nfeatures", type=int, default=1000)
@@ -183,37 +185,61 @@ def main():
     cv = synth.canvas(0x5EED0002 + 1000 * rank, W, H)
     pool_np = np.stack([synth.frame(cv, W, H, t) for t in range(max(args.pool, B))])
     pool = torch.from_numpy(pool_np).to(dev)
-    ex = amd.ORBextractor(NF, 1.2, 8, 20, 7, device=local, max_w=W, max_h=H, max_batch=B)
+    S = max(1, min(args.streams, B))
+    assert B % S == 0, "--batch must be a multiple of --streams"
+    Bs = B // S
+
+    class Pipe:
+        """One frame sequence: its own extractor / matcher handles, buffers and HIP stream, so
+        the latency-bound stages of one sequence overlap the others on the GPU."""
+
+        def __init__(self, k):
+            self.k = k
+            self.ts = torch.cuda.Stream(dev)
+            self.stream = self.ts.cuda_stream
+            self.ex = amd.ORBextractor(NF, 1.2, 8, 20, 7, device=local, max_w=W, max_h=H, max_batch=Bs)
+            self.m = amd.ORBmatcher(0.9, True, device=local)
+            # frame slot 0 holds the previous step's last frame (pair t-1, t across step boundaries)
+            self.kps = torch.zeros((Bs + 1, cap, 7), dtype=torch.int32, device=dev)
+            self.desc = torch.zeros((Bs + 1, cap, 32), dtype=torch.uint8, device=dev)
+            self.counts = torch.zeros(Bs + 1, dtype=torch.int32, device=dev)
+            self.m12 = torch.zeros((Bs, cap), dtype=torch.int32, device=dev)
+            self.nm = torch.zeros(Bs, dtype=torch.int32, device=dev)
+
+        def step(self, s):
+            n_pool = pool.shape[0]
+            start = (s * B + self.k * Bs) % (n_pool - Bs + 1)
+            imgs = pool[start:start + Bs]
+            with torch.cuda.stream(self.ts):
+                self.kps[0].copy_(self.kps[Bs])
+                self.desc[0].copy_(self.desc[Bs])
+                self.counts[0:1].copy_(self.counts[Bs:Bs + 1])
+            kps, desc, counts = self.kps, self.desc, self.counts
+            _abi.check("orb_extract_batch_device", lib.orb_extract_batch_device(
+                self.ex._h, C.c_void_p(imgs.data_ptr()), H * W, Bs, W, H, C.c_void_p(kps.data_ptr() + row_kp),
+                C.c_void_p(desc.data_ptr() + row_d), cap, C.c_void_p(counts.data_ptr() + 4),
+                C.c_void_p(self.stream)))
+            _abi.check("orb_search_for_initialization_batch_device", lib.orb_search_for_initialization_batch_device(
+                self.m._h, C.c_void_p(kps.data_ptr()), C.c_void_p(desc.data_ptr()), C.c_void_p(counts.data_ptr()),
+                C.c_void_p(kps.data_ptr() + row_kp), C.c_void_p(desc.data_ptr() + row_d),
+                C.c_void_p(counts.data_ptr() + 4), Bs, cap, W, H, 100, C.c_void_p(self.m12.data_ptr()),
+                C.c_void_p(self.nm.data_ptr()), C.c_void_p(self.stream)))
+
+    ex0 = amd.ORBextractor(NF, 1.2, 8, 20, 7, device=local, max_w=W, max_h=H, max_batch=1)
     lw, lh, cells = (np.zeros(8, np.int32) for _ in range(3))
     cap = C.c_int()
     _abi.check("orb_extractor_geometry", _abi.lib().orb_extractor_geometry(
-        ex._h, W, H, _abi.ptr(lw), _abi.ptr(lh), _abi.ptr(cells), C.byref(cap)))
+        ex0._h, W, H, _abi.ptr(lw), _abi.ptr(lh), _abi.ptr(cells), C.byref(cap)))
     cap = cap.value
-    m = amd.ORBmatcher(0.9, True, device=local)
-    # frame slot 0 holds the previous step's last frame (pair t-1, t across step boundaries)
-    kps = torch.zeros((B + 1, cap, 7), dtype=torch.int32, device=dev)
-    desc = torch.zeros((B + 1, cap, 32), dtype=torch.uint8, device=dev)
-    counts = torch.zeros(B + 1, dtype=torch.int32, device=dev)
-    m12 = torch.zeros((B, cap), dtype=torch.int32, device=dev)
-    nm = torch.zeros(B, dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev).cuda_stream
     lib = _abi.lib()
     row_kp, row_d = cap * 28, cap * 32
+    torch.cuda.synchronize(dev)
+    pipes = [Pipe(k) for k in range(S)]
+    ex = pipes[0].ex
 
     def step(s):
-        start = (s * B) % (pool.shape[0] - B + 1)
-        imgs = pool[start:start + B]
-        kps[0].copy_(kps[B])
-        desc[0].copy_(desc[B])
-        counts[0:1].copy_(counts[B:B + 1])
-        _abi.check("orb_extract_batch_device", lib.orb_extract_batch_device(
-            ex._h, C.c_void_p(imgs.data_ptr()), H * W, B, W, H, C.c_void_p(kps.data_ptr() + row_kp),
-            C.c_void_p(desc.data_ptr() + row_d), cap, C.c_void_p(counts.data_ptr() + 4), C.c_void_p(stream)))
-        _abi.check("orb_search_for_initialization_batch_device", lib.orb_search_for_initialization_batch_device(
-            m._h, C.c_void_p(kps.data_ptr()), C.c_void_p(desc.data_ptr()), C.c_void_p(counts.data_ptr()),
-            C.c_void_p(kps.data_ptr() + row_kp), C.c_void_p(desc.data_ptr() + row_d),
-            C.c_void_p(counts.data_ptr() + 4), B, cap, W, H, 100, C.c_void_p(m12.data_ptr()),
-            C.c_void_p(nm.data_ptr()), C.c_void_p(stream)))
+        for p in pipes:
+            p.step(s)
 
     for s in range(args.warmup):
         step(s)
@@ -242,8 +268,8 @@ def main():
         lib.orb_extractor_profile(ex._h, 0)
     frames_total = B * args.steps * world
     value = frames_total / dt
-    cnt = counts[1:].cpu().numpy()
-    nmatch = nm.cpu().numpy()
+    cnt = torch.cat([p.counts[1:] for p in pipes]).cpu().numpy()
+    nmatch = torch.cat([p.nm for p in pipes]).cpu().numpy()
 
     result = {
         "metric": "frames/sec ORB extract+match @640x480; local-BA ms/iter",
@@ -260,8 +286,9 @@ def main():
         "data": "synthetic",
         "config": {"workload": f"synthetic {W}x{H} grayscale stream, {NF} feat/frame, 8 levels, scale 1.2, "
                                f"FAST 20/7; extract + SearchForInitialization(t-1,t; window 100, nnratio 0.9, "
-                               f"checkOri) per frame; {B} frames per step per GPU, HBM-resident",
-                   "batch_per_gpu": B, "width": W, "height": H, "nfeatures": NF,
+                               f"checkOri) per frame; {B} frames per step per GPU as {S} independent "
+                               f"sequences on {S} HIP streams, HBM-resident",
+                   "batch_per_gpu": B, "streams_per_gpu": S, "width": W, "height": H, "nfeatures": NF,
                    "parallelism": f"frame-sharded x{world}"},
         "keypoints_per_frame": float(np.mean(cnt)),
         "matches_per_pair": float(np.mean(nmatch)),
@@ -273,7 +300,7 @@ def main():
         pre = np.zeros(8, np.int32)
         lib.orb_extractor_last_counts(ex._h, 0, _abi.ptr(pre), None)
         n_pre = float(pre.sum())
-        bytes_per_launch = algorithmic_bytes(STAGES[dom], lw, lh, n_pre, n_out) * B
+        bytes_per_launch = algorithmic_bytes(STAGES[dom], lw, lh, n_pre, n_out) * Bs
         achieved = bytes_per_launch / (per_launch_ms[dom] * 1e-3) / 1e9
         result["roofline"] = {"bound": "hbm", "kernel": KERNELS[dom], "achieved": round(achieved, 2),
                               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),

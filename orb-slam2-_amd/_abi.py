@@ -4,11 +4,14 @@ The HIP library is the only compute path: if it is missing or no gfx950 GPU
 is present, every entry point raises — there is no CPU fallback.
 """
 import ctypes as C
+import os
 import pathlib
 
 import numpy as np
 
-LIB_PATH = pathlib.Path(__file__).resolve().parent / "lib" / "liborbslam2_amd.so"
+# ORB_SLAM2_AMD_LIB selects an instrumented build of the same sources (tools/build_variant.py)
+LIB_PATH = pathlib.Path(os.environ.get("ORB_SLAM2_AMD_LIB") or
+                        pathlib.Path(__file__).resolve().parent / "lib" / "liborbslam2_amd.so")
 
 ORB_OK = 0
 ERRORS = {-22: "ORB_EINVAL", -7: "ORB_E2BIG", -12: "ORB_ENOMEM", -19: "ORB_ENODEV", -5: "ORB_EGPU",

@@ -55,7 +55,7 @@ struct Geom {
     int nlevels;
     int w, h;
     long long frameBytes;
-    int cellsPerFrame, slotsPerFrame, outPerFrame, tilesPerFrame, maxNodeCap;
+    int cellsPerFrame, slotsPerFrame, outPerFrame, tilesPerFrame, maxNodeCap, maxLevelSlots;
     int iniTh, minTh, tmin;
     float factorPI;
     int umax[16];
@@ -146,6 +146,7 @@ static int build_geom(const orb_extractor_params& p, int w, int h, Geom* g) {
         L.cellCap = ((L.wCell + 1) / 2) * ((L.hCell + 1) / 2) + 1;
         L.slotBase = slots;
         slots += L.nCols * L.nRows * L.cellCap;
+        g->maxLevelSlots = std::max(g->maxLevelSlots, L.nCols * L.nRows * L.cellCap);
         L.N = fpl[l];
         L.nIni = (int)std::round((float)(L.maxBX - kMinBorder) / (float)(L.maxBY - kMinBorder));
         if (L.nIni < 1) return ORB_EINVAL;
@@ -240,105 +241,160 @@ __global__ __launch_bounds__(256) void k_resize(Geom g, int l, uint8_t* __restri
 // OpenCV's cornerScore<16>(threshold t) == S for every pixel that is a corner at t, and a
 // pixel is a corner at t iff S >= t.  Stored as S if S >= tmin else 0.
 __device__ __forceinline__ int fast_score(const int v, const int p[16]) {
+    // 9-arc minima / maxima as min3 / max3 of three 3-arcs (v_min3_i32 / v_max3_i32)
     int d[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) d[k] = v - p[k];
-    int m2[16], M2[16];
+    int mn3[16], mx3[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        m2[k] = min(d[k], d[(k + 1) & 15]);
-        M2[k] = max(d[k], d[(k + 1) & 15]);
-    }
-    int m4[16], M4[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        m4[k] = min(m2[k], m2[(k + 2) & 15]);
-        M4[k] = max(M2[k], M2[(k + 2) & 15]);
+        mn3[k] = min(min(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
+        mx3[k] = max(max(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
     }
     int A = -1024, Bp = 1024;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        const int m8 = min(m4[k], m4[(k + 4) & 15]);
-        const int M8 = max(M4[k], M4[(k + 4) & 15]);
-        A = max(A, min(m8, d[(k + 8) & 15]));
-        Bp = min(Bp, max(M8, d[(k + 8) & 15]));
+        A = max(A, min(min(mn3[k], mn3[(k + 3) & 15]), mn3[(k + 6) & 15]));
+        Bp = min(Bp, max(max(mx3[k], mx3[(k + 3) & 15]), mx3[(k + 6) & 15]));
     }
     return max(A, -Bp) - 1;
 }
 
-constexpr int kTileW = 64, kTileH = 16, kHalo = 3;
-constexpr int kLdsW = kTileW + 2 * kHalo, kLdsH = kTileH + 2 * kHalo;
+constexpr int kTileW = 64, kTileH = 16;
+constexpr int kImgW = kTileW + 8, kImgH = kTileH + 8;   // image tile + 4-px halo (ring 3 + score halo 1)
+constexpr int kScW = kTileW + 2, kScH = kTileH + 2;     // score tile + 1-px halo (NMS neighbours)
 
+// Detection regions of the FAST cells (R/src/ORBextractor.cpp:851-883): cell (i, j) detects
+// rows [19 + i*hCell, min(19 + (i+1)*hCell, maxBY - 3)) and columns
+// [19 + j*wCell, min(19 + (j+1)*wCell, maxBX - 3)) — the windows' 3-px FAST margins make the
+// regions a partition, so every pixel belongs to at most one cell.
+// Cell index of a column / row of the level, or -1 outside every detection region.
+__device__ __forceinline__ int region_col(const LevelGeom& L, int x) {
+    if (x < kEdge || x >= L.maxBX - 3) return -1;
+    const int j = (x - kEdge) / L.wCell;
+    return j < L.nCols ? j : -1;
+}
+__device__ __forceinline__ int region_row(const LevelGeom& L, int y) {
+    if (y < kEdge || y >= L.maxBY - 3) return -1;
+    const int i = (y - kEdge) / L.hCell;
+    return i < L.nRows ? i : -1;
+}
+
+// Fused FAST score + cell-local non-maximum suppression, one 64x16 tile per workgroup.
+//  1. a 4-point pre-test (compass pixels 0/4/8/12 — any 9-arc contains two adjacent ones)
+//     selects the pixels that can reach S >= tmin; they are compacted into an LDS list;
+//  2. the full score S runs on the list only (S = 0 for everything else, as cv::FAST's score
+//     buffer holds 0 for non-corners);
+//  3. NMS against the 8 neighbours inside the same cell region.  With scores of non-corners at
+//     threshold t set to 0, "S > every neighbour" does not depend on t (a neighbour >= S is a
+//     corner at t whenever S is), so one map serves both FAST passes of the cell:
+//     nms[x,y] = S if (x,y) is a local maximum, else 0; the keypoints at t are nms >= t.
 __global__ __launch_bounds__(256) void k_fast_score(Geom g, const uint8_t* __restrict__ pyr,
-                                                    uint8_t* __restrict__ score) {
-    __shared__ uint8_t tile[kLdsH][kLdsW + 2];
+                                                    uint8_t* __restrict__ nms) {
+    __shared__ uint32_t img32[kImgH * kImgW / 4];
+    __shared__ uint8_t sc[kScH * kScW];
+    __shared__ uint16_t list[kScH * kScW];
+    __shared__ uint32_t outT[kTileH * kTileW / 4];
+    __shared__ int8_t colCell[kScW], rowCell[kScH];   // cell of each halo-tile column / row (-1: none)
+    __shared__ int cnt;
     const int b = blockIdx.y;
     const int l = level_of_tile(g, blockIdx.x);
     const LevelGeom& L = g.lv[l];
     const int t = blockIdx.x - L.tileBase;
     const int tx0 = (t % L.tilesX) * kTileW, ty0 = (t / L.tilesX) * kTileH;
     const uint8_t* img = pyr + (size_t)b * g.frameBytes + L.off;
-    uint8_t* out = score + (size_t)b * g.frameBytes + L.off;
-    const int tid = threadIdx.x;
-    for (int i = tid; i < kLdsH * kLdsW; i += 256) {
-        const int r = i / kLdsW, c = i % kLdsW;
-        const int y = min(max(ty0 - kHalo + r, 0), L.h - 1);
-        const int x = min(max(tx0 - kHalo + c, 0), L.w - 1);
-        tile[r][c] = img[(size_t)y * L.pitch + x];
+    uint8_t* out = nms + (size_t)b * g.frameBytes + L.off;
+    const int tid = threadIdx.x, lane = tid & 63;
+    for (int q = tid; q < kImgH * kImgW / 4; q += 256) {
+        const int r = q / (kImgW / 4), c4 = q % (kImgW / 4);
+        const int gx = tx0 - 4 + 4 * c4;
+        const int gy = min(max(ty0 - 4 + r, 0), L.h - 1);
+        img32[q] = (gx >= 0 && gx + 4 <= L.pitch) ? *reinterpret_cast<const uint32_t*>(img + (size_t)gy * L.pitch + gx) : 0u;
+    }
+    for (int q = tid; q < kScH * kScW; q += 256) sc[q] = 0;
+    if (tid < kTileH * kTileW / 4) outT[tid] = 0u;
+    if (tid < kScW) colCell[tid] = (int8_t)region_col(L, tx0 - 1 + tid);
+    else if (tid < kScW + kScH) rowCell[tid - kScW] = (int8_t)region_row(L, ty0 - 1 + tid - kScW);
+    if (tid == 0) cnt = 0;
+    __syncthreads();
+    const uint8_t* im = reinterpret_cast<const uint8_t*>(img32);
+    const int tpre = max(g.tmin, 1);
+    for (int p0 = 0; p0 < kScH * kScW; p0 += 256) {
+        const int p = p0 + tid;
+        bool ok = false;
+        if (p < kScH * kScW) {
+            const int sx = p % kScW - 1, sy = p / kScW - 1;
+            if (colCell[sx + 1] >= 0 && rowCell[sy + 1] >= 0) {
+                const int c = (sy + 4) * kImgW + sx + 4;
+                const int v = im[c];
+                const int q0 = im[c + 3 * kImgW], q4 = im[c + 3], q8 = im[c - 3 * kImgW], q12 = im[c - 3];
+                const unsigned dk = (unsigned)(q0 < v - tpre) | ((unsigned)(q4 < v - tpre) << 1) |
+                                    ((unsigned)(q8 < v - tpre) << 2) | ((unsigned)(q12 < v - tpre) << 3);
+                const unsigned br = (unsigned)(q0 > v + tpre) | ((unsigned)(q4 > v + tpre) << 1) |
+                                    ((unsigned)(q8 > v + tpre) << 2) | ((unsigned)(q12 > v + tpre) << 3);
+                const unsigned dk2 = dk & (((dk << 1) | (dk >> 3)) & 15u);
+                const unsigned br2 = br & (((br << 1) | (br >> 3)) & 15u);
+                ok = (dk2 | br2) != 0;
+            }
+        }
+        const uint64_t m = __ballot(ok);
+        int base = 0;
+        if (lane == 0 && m) base = atomicAdd(&cnt, __popcll(m));
+        base = __shfl(base, 0, 64);
+        if (ok) list[base + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)p;
+    }
+    __syncthreads();
+    const int n = cnt;
+    for (int k = tid; k < n; k += 256) {
+        const int p = list[k];
+        const int sx = p % kScW - 1, sy = p / kScW - 1;
+        const int cy = sy + 4, cx = sx + 4;
+        int q[16];
+        q[0] = im[(cy + 3) * kImgW + cx + 0];  q[1] = im[(cy + 3) * kImgW + cx + 1];
+        q[2] = im[(cy + 2) * kImgW + cx + 2];  q[3] = im[(cy + 1) * kImgW + cx + 3];
+        q[4] = im[(cy + 0) * kImgW + cx + 3];  q[5] = im[(cy - 1) * kImgW + cx + 3];
+        q[6] = im[(cy - 2) * kImgW + cx + 2];  q[7] = im[(cy - 3) * kImgW + cx + 1];
+        q[8] = im[(cy - 3) * kImgW + cx + 0];  q[9] = im[(cy - 3) * kImgW + cx - 1];
+        q[10] = im[(cy - 2) * kImgW + cx - 2]; q[11] = im[(cy - 1) * kImgW + cx - 3];
+        q[12] = im[(cy + 0) * kImgW + cx - 3]; q[13] = im[(cy + 1) * kImgW + cx - 3];
+        q[14] = im[(cy + 2) * kImgW + cx - 2]; q[15] = im[(cy + 3) * kImgW + cx - 1];
+        const int S = fast_score(im[cy * kImgW + cx], q);
+        sc[p] = (uint8_t)((S >= g.tmin && S > 0) ? S : 0);
+    }
+    __syncthreads();
+    uint8_t* o8 = reinterpret_cast<uint8_t*>(outT);
+    for (int k = tid; k < n; k += 256) {
+        const int p = list[k];
+        const int s = sc[p];
+        const int sx = p % kScW - 1, sy = p / kScW - 1;
+        if (s == 0 || sx < 0 || sx >= kTileW || sy < 0 || sy >= kTileH) continue;
+        const int cc = colCell[sx + 1], cr = rowCell[sy + 1];
+        int nb = 0;
+#pragma unroll
+        for (int dy = -1; dy <= 1; dy++) {
+#pragma unroll
+            for (int dx = -1; dx <= 1; dx++) {
+                if (dx == 0 && dy == 0) continue;
+                if (colCell[sx + 1 + dx] == cc && rowCell[sy + 1 + dy] == cr) nb = max(nb, (int)sc[p + dy * kScW + dx]);
+            }
+        }
+        if (s > nb) o8[sy * kTileW + sx] = (uint8_t)s;
     }
     __syncthreads();
     const int ly = tid / 16, lx0 = (tid % 16) * 4;
     const int y = ty0 + ly;
-    if (y >= L.h) return;
-    uint32_t packed = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int x = tx0 + lx0 + k;
-        int s = 0;
-        if (x >= 3 && x <= L.w - 4 && y >= 3 && y <= L.h - 4) {
-            const int cy = ly + kHalo, cx = lx0 + k + kHalo;
-            int p[16];
-            p[0] = tile[cy + 3][cx + 0];  p[1] = tile[cy + 3][cx + 1];
-            p[2] = tile[cy + 2][cx + 2];  p[3] = tile[cy + 1][cx + 3];
-            p[4] = tile[cy + 0][cx + 3];  p[5] = tile[cy - 1][cx + 3];
-            p[6] = tile[cy - 2][cx + 2];  p[7] = tile[cy - 3][cx + 1];
-            p[8] = tile[cy - 3][cx + 0];  p[9] = tile[cy - 3][cx - 1];
-            p[10] = tile[cy - 2][cx - 2]; p[11] = tile[cy - 1][cx - 3];
-            p[12] = tile[cy + 0][cx - 3]; p[13] = tile[cy + 1][cx - 3];
-            p[14] = tile[cy + 2][cx - 2]; p[15] = tile[cy + 3][cx - 1];
-            const int S = fast_score(tile[cy][cx], p);
-            s = (S >= g.tmin && S > 0) ? S : 0;
-        }
-        packed |= (uint32_t)s << (8 * k);
-    }
-    if (tx0 + lx0 < L.pitch) *reinterpret_cast<uint32_t*>(out + (size_t)y * L.pitch + tx0 + lx0) = packed;
+    if (y < L.h && tx0 + lx0 < L.pitch)
+        *reinterpret_cast<uint32_t*>(out + (size_t)y * L.pitch + tx0 + lx0) = outT[tid];
 }
 
 // ------------------------------------------------------------------ A3: per-cell detect
 
 constexpr int kCellMax = 64;   // max region side handled in LDS (wCell, hCell <= 60 by construction)
 
-__device__ __forceinline__ bool nms_keep(const uint8_t* reg, int rw, int rh, int x, int y, int t) {
-    const int m = reg[y * rw + x];
-    if (m < t) return false;
-#pragma unroll
-    for (int dy = -1; dy <= 1; dy++) {
-#pragma unroll
-        for (int dx = -1; dx <= 1; dx++) {
-            if (dx == 0 && dy == 0) continue;
-            const int xx = x + dx, yy = y + dy;
-            int nv = 0;
-            if (xx >= 0 && xx < rw && yy >= 0 && yy < rh) {
-                nv = reg[yy * rw + xx];
-                if (nv < t) nv = 0;
-            }
-            if (m <= nv) return false;
-        }
-    }
-    return true;
-}
-
-__global__ __launch_bounds__(256) void k_cell_detect(Geom g, const uint8_t* __restrict__ score,
+// One wave per FAST cell (R/src/ORBextractor.cpp:851-896): the cell's detection region of the
+// NMS map is staged in LDS; if no pixel reaches iniThFAST the cell falls back to minThFAST
+// (:879-883); keys are emitted in raster order, as cv::FAST returns them.
+__global__ __launch_bounds__(256) void k_cell_detect(Geom g, const uint8_t* __restrict__ nms,
                                                      uint32_t* __restrict__ slots, int* __restrict__ cellCount,
                                                      int* __restrict__ status) {
     __shared__ uint8_t reg_all[4][kCellMax * kCellMax];
@@ -371,39 +427,42 @@ __global__ __launch_bounds__(256) void k_cell_detect(Geom g, const uint8_t* __re
         return;
     }
     uint8_t* reg = reg_all[wid];
-    const uint8_t* sm = score + (size_t)b * g.frameBytes + L.off;
+    const uint8_t* sm = nms + (size_t)b * g.frameBytes + L.off;
     const int rx0 = iniX + 3, ry0 = iniY + 3;
-    for (int p = lane; p < rw * rh; p += 64) {
-        const int y = p / rw, x = p % rw;
-        reg[p] = sm[(size_t)(ry0 + y) * L.pitch + rx0 + x];
+    const int np = rw * rh;
+    for (int p0 = 0; p0 < np; p0 += 64 * 8) {   // 8 loads in flight per lane
+        uint8_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int p = p0 + u * 64 + lane;
+            v[u] = p < np ? sm[(size_t)(ry0 + p / rw) * L.pitch + rx0 + p % rw] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int p = p0 + u * 64 + lane;
+            if (p < np) reg[p] = v[u];
+        }
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    int n20 = 0;
-    for (int p0 = 0; p0 < rw * rh; p0 += 64) {
+    bool any = false;
+    for (int p0 = 0; p0 < np && !any; p0 += 64) {
         const int p = p0 + lane;
-        bool k = false;
-        if (p < rw * rh) k = nms_keep(reg, rw, rh, p % rw, p / rw, g.iniTh);
-        n20 += __popcll(__ballot(k));
+        const int v = p < np ? reg[p] : 0;
+        any = __ballot(v > 0 && v >= g.iniTh) != 0;
     }
-    const int t = n20 > 0 ? g.iniTh : g.minTh;
+    const int t = any ? g.iniTh : g.minTh;
     uint32_t* out = slots + (size_t)b * g.slotsPerFrame + L.slotBase + (size_t)ci * L.cellCap;
     int n = 0;
-    for (int p0 = 0; p0 < rw * rh; p0 += 64) {
+    for (int p0 = 0; p0 < np; p0 += 64) {
         const int p = p0 + lane;
-        bool k = false;
-        int x = 0, y = 0, m = 0;
-        if (p < rw * rh) {
-            x = p % rw;
-            y = p / rw;
-            k = nms_keep(reg, rw, rh, x, y, t);
-            m = reg[p];
-        }
+        const int m = p < np ? reg[p] : 0;
+        const bool k = m > 0 && m >= t;
         const uint64_t mask = __ballot(k);
         const int before = __popcll(mask & ((1ull << lane) - 1ull));
         if (k && n + before < L.cellCap) {
             // DistributeOctTree coordinates: absolute - minBorder (R/src/ORBextractor.cpp:889-890)
-            const uint32_t kx = (uint32_t)(rx0 + x - kMinBorder), ky = (uint32_t)(ry0 + y - kMinBorder);
+            const uint32_t kx = (uint32_t)(rx0 + p % rw - kMinBorder), ky = (uint32_t)(ry0 + p / rw - kMinBorder);
             out[n + before] = kx | (ky << 12) | ((uint32_t)m << 24);
         }
         n += __popcll(mask);
@@ -415,6 +474,14 @@ __global__ __launch_bounds__(256) void k_cell_detect(Geom g, const uint8_t* __re
 }
 
 // ------------------------------------------------------------------ A4: octree
+
+#ifdef ORB_TIMING   // instrumented variant (tools/build_variant.py)
+#define TSTAMP(v) const long long v = clock64()
+#define TACC(acc, a) acc += clock64() - (a)
+#else
+#define TSTAMP(v)
+#define TACC(acc, a)
+#endif
 
 constexpr int OT_T = 256;
 constexpr int OT_V = 8;
@@ -525,67 +592,39 @@ struct OctScratch {
     int* tmp;       // scan scratch
 };
 
-__global__ __launch_bounds__(OT_T) void k_octree(Geom g, const uint32_t* __restrict__ slots,
-                                                 const int* __restrict__ cellCount, uint32_t* __restrict__ keyA,
-                                                 uint32_t* __restrict__ keyB, uint32_t* __restrict__ outKeys,
-                                                 int* __restrict__ levelCount, int* __restrict__ status) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int l = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
-    const LevelGeom& L = g.lv[l];
-    const int cap = g.maxNodeCap;
-    // carve LDS
-    unsigned char* p = smem;
-    auto carve = [&](size_t bytes) { unsigned char* r = p; p += (bytes + 15) & ~(size_t)15; return r; };
-    OctScratch S;
-    S.P0 = (uint4*)carve(sizeof(uint4) * (cap + 1));
-    NodeTab T[2];
-    for (int s = 0; s < 2; s++) {
-        T[s].start = (int*)carve(sizeof(int) * (cap + 1));
-        T[s].cnt = (int*)carve(sizeof(int) * cap);
-        T[s].b0 = (uint32_t*)carve(sizeof(uint32_t) * cap);
-        T[s].b1 = (uint32_t*)carve(sizeof(uint32_t) * cap);
-        T[s].seq = (int*)carve(sizeof(int) * cap);
-        T[s].flag = (int*)carve(sizeof(int) * cap);
+struct OctCtx {          // LDS carve-up shared by both key-storage variants
+    unsigned char* tabBase;
+    size_t tabStride;
+    int cap;
+    __device__ NodeTab tab(int s) const {
+        unsigned char* q = tabBase + (size_t)s * tabStride;
+        auto r16 = [](size_t v) { return (v + 15) & ~(size_t)15; };
+        NodeTab t;
+        t.start = (int*)q; q += r16(4 * (size_t)(cap + 1));
+        t.cnt = (int*)q; q += r16(4 * (size_t)cap);
+        t.b0 = (uint32_t*)q; q += r16(4 * (size_t)cap);
+        t.b1 = (uint32_t*)q; q += r16(4 * (size_t)cap);
+        t.seq = (int*)q; q += r16(4 * (size_t)cap);
+        t.flag = (int*)q;
+        return t;
     }
-    S.ne = (int*)carve(sizeof(int) * cap);
-    S.push = (int*)carve(sizeof(int) * cap);
-    S.newpos = (int*)carve(sizeof(int) * cap);
-    S.rank = (int*)carve(sizeof(int) * cap);
-    S.order = (int*)carve(sizeof(int) * cap);
-    S.proc = (int*)carve(sizeof(int) * cap);
-    S.tmp = (int*)carve(sizeof(int) * (cap + 1));
-    int* cellOff = (int*)carve(sizeof(int) * (L.nCols * L.nRows + 1 + 64));
-    uint64_t* wtot = (uint64_t*)carve(sizeof(uint64_t) * 8);
-    int* wsum = (int*)carve(sizeof(int) * 8);
-    int* sc = (int*)carve(sizeof(int) * 32);    // uniform scalars
-    uint4* carry_s = (uint4*)carve(sizeof(uint4));
+};
 
-    const size_t kbase = (size_t)b * g.slotsPerFrame + L.slotBase;
-    uint32_t* kA = keyA + kbase;
-    uint32_t* kB = keyB + kbase;
-    const int ncell = L.nCols * L.nRows;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
-    // ---- gather cell lists into a contiguous key array (cell order i-major, j-minor)
-    for (int c = tid; c < ncell; c += OT_T) cellOff[c] = cellCount[(size_t)b * g.cellsPerFrame + L.cellBase + c];
-    __syncthreads();
-    const int n = block_scan_lds(cellOff, ncell, wsum);
-    if (tid == 0) cellOff[ncell] = n;
-    __syncthreads();
-    {
-        const uint32_t* src = slots + kbase;
-        for (int c = tid >> 6; c < ncell; c += OT_T / 64) {
-            const int o = cellOff[c], cn = cellOff[c + 1] - o;
-            for (int q = tid & 63; q < cn; q += 64) kA[o + q] = src[(size_t)c * L.cellCap + q];
-        }
-    }
-    __syncthreads();
-    int* outCount = levelCount + (size_t)b * g.nlevels + l;
-    uint32_t* outK = outKeys + (size_t)b * g.outPerFrame + L.outBase;
-    if (n == 0) {
-        if (tid == 0) *outCount = 0;
-        return;
-    }
-
+// DistributeOctTree on n keys held in kA (kB: scratch of the same size); KP is the key
+// storage: LDS (lds_u32, the common case) or global memory for very dense levels.
+template <typename KP>
+__device__ __forceinline__ void octree_run(const Geom& g, const LevelGeom& L, int l, int b, int n, KP* kA, KP* kB, const OctCtx& C_,
+                           OctScratch& S, uint64_t* wtot, int* wsum, int* sc, uint4* carry_s, uint32_t* outK,
+                           int* outCount, int* status) {
+    const int tid = threadIdx.x;
+    const int cap = C_.cap;
+    (void)cap;
+    TSTAMP(t_begin);
+    long long tB = 0, tN = 0, tO0 = 0, tO1 = 0, tF = 0, tC = 0;
+    int np0 = 0, np1 = 0;
+    (void)tB; (void)tN; (void)tO0; (void)tO1; (void)tF; (void)tC; (void)np0; (void)np1;
     // ---- initial nodes (R/src/ORBextractor.cpp:577-627): stable partition by x / hX
     const int nIni = L.nIni;
     const float hX = L.hX;
@@ -593,6 +632,7 @@ __global__ __launch_bounds__(OT_T) void k_octree(Geom g, const uint32_t* __restr
     if (tid == 0) sc[0] = 0;
     __syncthreads();
     {
+        const NodeTab T0 = C_.tab(0);
         int base = 0;
         for (int part = 0; part < nIni; part++) {
             int partCount = 0;
@@ -618,34 +658,39 @@ __global__ __launch_bounds__(OT_T) void k_octree(Geom g, const uint32_t* __restr
             // nodes are pushed back in part order; empty initial nodes are erased
             if (partCount > 0 && tid == 0) {
                 const int idx = sc[0];
-                T[0].start[idx] = base;
-                T[0].cnt[idx] = partCount;
+                T0.start[idx] = base;
+                T0.cnt[idx] = partCount;
                 const int x0 = (int)(hX * (float)part), x1 = (int)(hX * (float)(part + 1));
-                T[0].b0[idx] = (uint32_t)x0;
-                T[0].b1[idx] = (uint32_t)x1 | ((uint32_t)H << 16);
-                T[0].seq[idx] = idx;
-                T[0].flag[idx] = partCount == 1 ? 1 : 0;
+                T0.b0[idx] = (uint32_t)x0;
+                T0.b1[idx] = (uint32_t)x1 | ((uint32_t)H << 16);
+                T0.seq[idx] = idx;
+                T0.flag[idx] = partCount == 1 ? 1 : 0;
                 sc[0] = idx + 1;
             }
             base += partCount;
             __syncthreads();
         }
     }
+    TSTAMP(t_init);
     int m = sc[0];  // list size (uniform)
     __syncthreads();
     {   // keys now live in kB
-        uint32_t* t = kA; kA = kB; kB = t;
+        KP* t = kA; kA = kB; kB = t;
     }
     int cur = 0;            // table holding the current list
     int phase = 0;          // 0 = outer pass, 1 = inner (size-ordered) pass
     int nIter = 0;
     while (true) {
         if (++nIter > 4096) { if (tid == 0) atomicOr(status, 4); break; }
-        NodeTab& O = T[cur];
-        NodeTab& Nw = T[cur ^ 1];
+        const NodeTab O = C_.tab(cur);
+        const NodeTab Nw = C_.tab(cur ^ 1);
         const int prevSize = m;
         // active flags: outer -> every node with >1 keys (== !bNoMore); inner -> candidates
         // Pass B: quadrant prefix at node starts
+        TSTAMP(t_pb);
+#ifdef ORB_TIMING
+        if (phase == 0) np0++; else np1++;
+#endif
         if (tid == 0) *carry_s = make_uint4(0, 0, 0, 0);
         __syncthreads();
         for (int t0 = 0; t0 < n; t0 += OT_TILE) {
@@ -697,6 +742,8 @@ __global__ __launch_bounds__(OT_T) void k_octree(Geom g, const uint32_t* __restr
         }
         if (tid == 0) S.P0[m] = *carry_s;
         __syncthreads();
+        TACC(tB, t_pb);
+        TSTAMP(t_nl);
         // node level: child counts, ne, active
         for (int i = tid; i < m; i += OT_T) {
             const bool act = phase == 0 ? (O.cnt[i] > 1) : ((O.flag[i] & 2) != 0);
@@ -708,6 +755,8 @@ __global__ __launch_bounds__(OT_T) void k_octree(Geom g, const uint32_t* __restr
             S.ne[i] = act ? ne : -1;
         }
         __syncthreads();
+        TACC(tN, t_nl);
+        TSTAMP(t_or);
         // processing order + push bases
         if (phase == 0) {
             for (int i = tid; i < m; i += OT_T) S.tmp[i] = S.ne[i] > 0 ? S.ne[i] : 0;
@@ -765,6 +814,8 @@ __global__ __launch_bounds__(OT_T) void k_octree(Geom g, const uint32_t* __restr
             }
             __syncthreads();
         }
+        if (phase == 0) { TACC(tO0, t_or); } else { TACC(tO1, t_or); }
+        TSTAMP(t_fi);
         const int C = sc[1];
         // new positions of unprocessed nodes
         for (int i = tid; i < m; i += OT_T) S.tmp[i] = S.proc[i] ? 0 : 1;
@@ -815,6 +866,8 @@ __global__ __launch_bounds__(OT_T) void k_octree(Geom g, const uint32_t* __restr
         block_scan_lds(Nw.start, newM, wsum);
         if (tid == 0) Nw.start[newM] = n;
         __syncthreads();
+        TACC(tF, t_fi);
+        TSTAMP(t_pc);
         // Pass C: move keys (stable within every child / unprocessed node)
         if (tid == 0) *carry_s = make_uint4(0, 0, 0, 0);
         __syncthreads();
@@ -855,10 +908,11 @@ __global__ __launch_bounds__(OT_T) void k_octree(Geom g, const uint32_t* __restr
                 const int q = qv[v];
                 if (S.proc[i]) {
                     const uint4 a = S.P0[i], c = S.P0[i + 1];
-                    const int cc[4] = {(int)(c.x - a.x), (int)(c.y - a.y), (int)(c.z - a.z), (int)(c.w - a.w)};
+                    // rank of child q among the non-empty children (n1..n4 order)
+                    const unsigned ne = (unsigned)(c.x != a.x) | ((unsigned)(c.y != a.y) << 1) |
+                                        ((unsigned)(c.z != a.z) << 2) | ((unsigned)(c.w != a.w) << 3);
                     const unsigned rq = q == 0 ? R.x - a.x : q == 1 ? R.y - a.y : q == 2 ? R.z - a.z : R.w - a.w;
-                    int r = 0;
-                    for (int qq = 0; qq < q; qq++) r += cc[qq] > 0;
+                    const int r = __popc(ne & ((1u << q) - 1u));
                     const int j2 = C - 1 - (S.push[i] + r);
                     kB[Nw.start[j2] + (int)rq] = kk[v];
                 } else {
@@ -877,7 +931,8 @@ __global__ __launch_bounds__(OT_T) void k_octree(Geom g, const uint32_t* __restr
             }
             __syncthreads();
         }
-        { uint32_t* t = kA; kA = kB; kB = t; }
+        TACC(tC, t_pc);
+        { KP* t = kA; kA = kB; kB = t; }
         cur ^= 1;
         m = newM;
         // termination logic of R/src/ORBextractor.cpp:722-791
@@ -889,7 +944,7 @@ __global__ __launch_bounds__(OT_T) void k_octree(Geom g, const uint32_t* __restr
     }
     __syncthreads();
     // retain the best point in each node (first max wins, R/src/ORBextractor.cpp:796-814)
-    NodeTab& F = T[cur];
+    const NodeTab F = C_.tab(cur);
     for (int i = tid; i < m; i += OT_T) {
         const int s0 = F.start[i], s1 = s0 + F.cnt[i];
         uint32_t best = kA[s0];
@@ -903,12 +958,104 @@ __global__ __launch_bounds__(OT_T) void k_octree(Geom g, const uint32_t* __restr
         if (m > L.nodeCap) atomicOr(status, 16);
         *outCount = min(m, L.nodeCap);
     }
+#ifdef ORB_TIMING
+    if (tid == 0 && b == 0 && (l == 0 || l == 7))
+        printf("octree l%d n %d m %d: init %lld passes %d+%d B %lld N %lld O0 %lld O1 %lld F %lld C %lld total %lld\n", l, n, m,
+               t_init - t_begin, np0, np1, tB, tN, tO0, tO1, tF, tC, clock64() - t_begin);
+#endif
+}
+
+__global__ __launch_bounds__(OT_T) void k_octree(Geom g, const uint32_t* __restrict__ slots,
+                                                 const int* __restrict__ cellCount, uint32_t* __restrict__ keyA,
+                                                 uint32_t* __restrict__ keyB, uint32_t* __restrict__ outKeys,
+                                                 int* __restrict__ levelCount, int* __restrict__ status,
+                                                 int ldsKeyCap) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int l = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+    const LevelGeom& L = g.lv[l];
+    const int cap = g.maxNodeCap;
+    // carve LDS (layout mirrored by octree_lds_bytes on the host)
+    unsigned char* p = smem;
+    auto carve = [&](size_t bytes) { unsigned char* r = p; p += (bytes + 15) & ~(size_t)15; return r; };
+    OctScratch S;
+    S.P0 = (uint4*)carve(sizeof(uint4) * (cap + 1));
+    OctCtx C_;
+    C_.cap = cap;
+    C_.tabStride = ((4 * (size_t)(cap + 1) + 15) & ~(size_t)15) + 5 * ((4 * (size_t)cap + 15) & ~(size_t)15);
+    C_.tabBase = carve(2 * C_.tabStride);
+    S.ne = (int*)carve(sizeof(int) * cap);
+    S.push = (int*)carve(sizeof(int) * cap);
+    S.newpos = (int*)carve(sizeof(int) * cap);
+    S.rank = (int*)carve(sizeof(int) * cap);
+    S.order = (int*)carve(sizeof(int) * cap);
+    S.proc = (int*)carve(sizeof(int) * cap);
+    S.tmp = (int*)carve(sizeof(int) * (cap + 1));
+    int* cellOff = (int*)carve(sizeof(int) * (L.nCols * L.nRows + 1 + 64));
+    uint64_t* wtot = (uint64_t*)carve(sizeof(uint64_t) * 8);
+    int* wsum = (int*)carve(sizeof(int) * 8);
+    int* sc = (int*)carve(sizeof(int) * 32);    // uniform scalars
+    uint4* carry_s = (uint4*)carve(sizeof(uint4));
+    lds_u32* keysL = (lds_u32*)carve(sizeof(uint32_t) * ldsKeyCap);   // LDS ping-pong key buffers
+
+    const size_t kbase = (size_t)b * g.slotsPerFrame + L.slotBase;
+    const int ncell = L.nCols * L.nRows;
+
+    // ---- cell lists -> one contiguous key array (cell order i-major, j-minor)
+    for (int c = tid; c < ncell; c += OT_T) cellOff[c] = cellCount[(size_t)b * g.cellsPerFrame + L.cellBase + c];
+    __syncthreads();
+    const int n = block_scan_lds(cellOff, ncell, wsum);
+    if (tid == 0) cellOff[ncell] = n;
+    __syncthreads();
+    int* outCount = levelCount + (size_t)b * g.nlevels + l;
+    uint32_t* outK = outKeys + (size_t)b * g.outPerFrame + L.outBase;
+    if (n == 0) {
+        if (tid == 0) *outCount = 0;
+        return;
+    }
+    const bool inLds = 2 * n <= ldsKeyCap;   // typical levels hold a few thousand keys
+    {
+        // one thread per key (independent loads, all in flight): cell by binary search
+        const uint32_t* src = slots + kbase;
+        uint32_t* kg = keyA + kbase;
+        for (int k0 = 0; k0 < n; k0 += OT_T * 4) {
+            uint32_t v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int k = k0 + u * OT_T + tid;
+                v[u] = 0;
+                if (k < n) {
+                    int lo = 0, hi = ncell - 1;
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (cellOff[mid] <= k) lo = mid; else hi = mid - 1;
+                    }
+                    v[u] = src[(size_t)lo * L.cellCap + (k - cellOff[lo])];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int k = k0 + u * OT_T + tid;
+                if (k < n) {
+                    if (inLds) keysL[k] = v[u];
+                    else kg[k] = v[u];
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (inLds)
+        octree_run<lds_u32>(g, L, l, b, n, keysL, keysL + n, C_, S, wtot, wsum, sc, carry_s, outK, outCount, status);
+    else
+        octree_run<uint32_t>(g, L, l, b, n, keyA + kbase, keyB + kbase, C_, S, wtot, wsum, sc, carry_s, outK,
+                             outCount, status);
 }
 
 // ------------------------------------------------------------------ A6: blur
 
 // Separable 7-tap integer blur; every LDS access is dword-aligned (the compiler otherwise
 // merges neighbouring byte reads into ds_read_u16 at odd addresses, which mis-read on gfx950).
+constexpr int kHalo = 3;   // blur radius
+constexpr int kLdsW = kTileW + 2 * kHalo, kLdsH = kTileH + 2 * kHalo;
 constexpr int kRowSumW = kTileW + 4;
 __global__ __launch_bounds__(256) void k_blur(Geom g, const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blurred,
                                               int k0, int k1, int k2, int k3) {
@@ -922,17 +1069,22 @@ __global__ __launch_bounds__(256) void k_blur(Geom g, const uint8_t* __restrict_
     const uint8_t* img = pyr + (size_t)b * g.frameBytes + L.off;
     uint8_t* out = blurred + (size_t)b * g.frameBytes + L.off;
     const int tid = threadIdx.x;
-    constexpr int kWords = (kLdsW + 2) / 4;   // 18 words = 72 bytes per row
+    constexpr int kWords = (kLdsW + 2) / 4;   // 18 words = 72 bytes per row, from column tx0 - 4
+    // interior tiles read aligned dwords; tiles touching a level edge apply BORDER_REFLECT_101 per byte
+    const bool interior = tx0 >= 4 && tx0 + kTileW + kHalo < L.w && ty0 >= kHalo && ty0 + kTileH + kHalo <= L.h;
     for (int i = tid; i < kLdsH * kWords; i += 256) {
         const int r = i / kWords, wd = i % kWords;
-        const int y = reflect101(ty0 - kHalo + r, L.h);
-        const uint8_t* row = img + (size_t)y * L.pitch;
         uint32_t v = 0;
+        if (interior) {
+            v = *reinterpret_cast<const uint32_t*>(img + (size_t)(ty0 - kHalo + r) * L.pitch + tx0 - 4 + 4 * wd);
+        } else {
+            const int y = reflect101(ty0 - kHalo + r, L.h);
+            const uint8_t* row = img + (size_t)y * L.pitch;
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int c = wd * 4 + k;
-            const int x = reflect101(tx0 - kHalo + min(c, kLdsW - 1), L.w);
-            v |= (uint32_t)row[x] << (8 * k);
+            for (int k = 0; k < 4; k++) {
+                const int x = reflect101(tx0 - 4 + 4 * wd + k, L.w);
+                v |= (uint32_t)row[x] << (8 * k);
+            }
         }
         tile32[r][wd] = v;
     }
@@ -948,13 +1100,13 @@ __global__ __launch_bounds__(256) void k_blur(Geom g, const uint8_t* __restrict_
             px[4 + k] = (w1 >> (8 * k)) & 0xff;
             px[8 + k] = (w2 >> (8 * k)) & 0xff;
         }
-        int4 s4;
+    int4 s4;
         int sv[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             int s = 0;
 #pragma unroll
-            for (int q = 0; q < 7; q++) s += kk[q] * px[k + q];
+            for (int q = 0; q < 7; q++) s += kk[q] * px[k + 1 + q];
             sv[k] = s;
         }
         s4.x = sv[0]; s4.y = sv[1]; s4.z = sv[2]; s4.w = sv[3];
@@ -1136,18 +1288,29 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
     }
 }
 
-// Copies B packed w x h frames into the pitched level-0 slots of the pyramid slab.
-__global__ __launch_bounds__(64) void k_load_frames(Geom g, const uint8_t* __restrict__ src, size_t frameStride,
-                                                    uint8_t* __restrict__ pyr) {
-    const int b = blockIdx.z, y = blockIdx.y;
-    const int x0 = (blockIdx.x * 64 + threadIdx.x) * 4;
+// Copies B packed w x h frames into the pitched level-0 slots of the pyramid slab: 16 bytes
+// per thread when rows are 16-byte aligned (w % 16 == 0 and an aligned source), else bytes.
+__global__ __launch_bounds__(256) void k_load_frames(Geom g, const uint8_t* __restrict__ src, size_t frameStride,
+                                                     uint8_t* __restrict__ pyr, int vec16) {
+    const int b = blockIdx.y;
     const LevelGeom& L = g.lv[0];
-    if (x0 >= L.w) return;
-    const uint8_t* s = src + (size_t)b * frameStride + (size_t)y * L.w;
-    uint32_t v = 0;
-    for (int k = 0; k < 4; k++)
-        if (x0 + k < L.w) v |= (uint32_t)s[x0 + k] << (8 * k);
-    *reinterpret_cast<uint32_t*>(pyr + (size_t)b * g.frameBytes + L.off + (size_t)y * L.pitch + x0) = v;
+    const uint8_t* s = src + (size_t)b * frameStride;
+    uint8_t* d = pyr + (size_t)b * g.frameBytes + L.off;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (vec16) {
+        const int perRow = L.w / 16;
+        if (i >= perRow * L.h) return;
+        const int y = i / perRow, x = (i % perRow) * 16;
+        *reinterpret_cast<uint4*>(d + (size_t)y * L.pitch + x) = *reinterpret_cast<const uint4*>(s + (size_t)y * L.w + x);
+    } else {
+        const int perRow = (L.w + 3) / 4;
+        if (i >= perRow * L.h) return;
+        const int y = i / perRow, x = (i % perRow) * 4;
+        uint32_t v = 0;
+        for (int k = 0; k < 4; k++)
+            if (x + k < L.w) v |= (uint32_t)s[(size_t)y * L.w + x + k] << (8 * k);
+        *reinterpret_cast<uint32_t*>(d + (size_t)y * L.pitch + x) = v;
+    }
 }
 
 // ------------------------------------------------------------------ host handle
@@ -1323,9 +1486,13 @@ static int run_pipeline(orb_extractor* ex, int B, orb_keypoint* d_kps, uint8_t* 
     hipLaunchKernelGGL(k_cell_detect, dim3((g.cellsPerFrame + 3) / 4, B), dim3(256), 0, st, g, ex->d_score,
                        ex->d_slots, ex->d_cellCount, ex->d_status);
     mark(3);
-    const size_t lds = octree_lds_bytes(g);
+    // LDS key buffers sized so that two workgroups still fit a CU (<= 80 KB each)
+    const size_t ldsBase = octree_lds_bytes(g);
+    const int keyCap = (int)std::max<long long>(0, std::min<long long>(2LL * g.maxLevelSlots,
+                                                                          ((long long)81920 - (long long)ldsBase) / 4 - 8));
+    const size_t lds = ldsBase + 16 + 4 * (size_t)keyCap;
     hipLaunchKernelGGL(k_octree, dim3(g.nlevels, B), dim3(OT_T), lds, st, g, ex->d_slots, ex->d_cellCount,
-                       ex->d_keyA, ex->d_keyB, ex->d_outKeys, ex->d_levelCount, ex->d_status);
+                       ex->d_keyA, ex->d_keyB, ex->d_outKeys, ex->d_levelCount, ex->d_status, keyCap);
     mark(4);
     hipLaunchKernelGGL(k_blur, dim3(g.tilesPerFrame, B), dim3(256), 0, st, g, ex->d_pyr, ex->d_blur, ex->blurK[0],
                        ex->blurK[1], ex->blurK[2], ex->blurK[3]);
@@ -1478,8 +1645,10 @@ int orb_extract_batch_device(orb_extractor* ex, const uint8_t* d_imgs, size_t im
     if (st) return st;
     hipStream_t s = stream ? (hipStream_t)stream : ex->stream;
     const Geom& g = ex->g;
-    hipLaunchKernelGGL(k_load_frames, dim3((w + 255) / 256, h, B), dim3(64), 0, s, g, d_imgs, img_stride_frame,
-                       ex->d_pyr);
+    const int vec16 = (w % 16 == 0) && (img_stride_frame % 16 == 0) && ((uintptr_t)d_imgs % 16 == 0);
+    const int items = vec16 ? (w / 16) * h : ((w + 3) / 4) * h;
+    hipLaunchKernelGGL(k_load_frames, dim3((items + 255) / 256, B), dim3(256), 0, s, g, d_imgs, img_stride_frame,
+                       ex->d_pyr, vec16);
     ORB_HIP_TRY(hipGetLastError());
     ex->lastB = B;
     ex->h_level_valid.assign((size_t)B * g.nlevels, 0);

@@ -950,7 +950,7 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
         c->ev.push_back(e);
         return e;
     };
-    hipEvent_t e0 = evt(), e1 = evt(), e2 = evt(), e3 = evt(), e4 = evt();
+    hipEvent_t e0 = evt(), e1 = evt(), e2 = evt(), e3 = evt();
     auto elapsed = [&](hipEvent_t a, hipEvent_t b) {
         float ms = 0;
         (void)hipEventElapsedTime(&ms, a, b);

@@ -131,149 +131,452 @@ __device__ __forceinline__ Best2 wave_best2(int d, unsigned order, int idx, bool
 
 // ---------------------------------------------------------------- SearchForInitialization
 
-struct SfiPair {
-    const orb_keypoint* k1; const uint8_t* d1; int n1;
-    const orb_keypoint* k2; const uint8_t* d2; int n2;
-    const float* prev;      // 2*n1, NULL -> k1 positions
-};
+constexpr int kTopK = 8;   // candidates kept per query, in the reference's preference order
+constexpr int kRange = 256;  // queries staged in LDS at a time by k_resolve_sfi
 
-// Candidate lists for F1 level-0 keypoints: cand[b][i1][*] = (i2 | dist << 20), in
-// ascending i2; ncand[b][i1].
+#ifdef ORB_TIMING   // instrumented variant (tools/build_variant.py): per-phase clocks of one wave
+#define TSTAMP(v) const long long v = clock64()
+#define TACC(acc, a) acc += clock64() - (a)
+#else
+#define TSTAMP(v)
+#define TACC(acc, a)
+#endif
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// F2's octave-0 keypoints bucketed by grid cell, in the order Frame::AssignFeaturesToGrid
+// fills mGrid (R/src/Frame.cpp:244-260): per pair, cellStart[0..3072] (prefix over cell key
+// ix*48+iy) and the keypoint index / position of each bucket entry.  SearchForInitialization
+// only asks for level-0 keypoints (minLevel = maxLevel = 0), so only those are bucketed.
+constexpr int kCells = kGridCols * kGridRows;
+
+__global__ __launch_bounds__(256) void k_grid_sfi(const orb_keypoint* __restrict__ kps2, const int32_t* __restrict__ n2s,
+                                                  int cap, GridParams g, int* __restrict__ cellStart,
+                                                  int* __restrict__ gj, float2* __restrict__ gxy) {
+    __shared__ int cnt[kCells + 1];
+    __shared__ int wsum[4];
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int n2 = min((int)n2s[b], cap);
+    const orb_keypoint* K2 = kps2 + (size_t)b * cap;
+    int* CS = cellStart + (size_t)b * (kCells + 1);
+    int* GJ = gj + (size_t)b * cap;
+    float2* GXY = gxy + (size_t)b * cap;
+    for (int c = tid; c <= kCells; c += 256) cnt[c] = 0;
+    __syncthreads();
+    for (int j = tid; j < n2; j += 256) {
+        const orb_keypoint k = K2[j];
+        if (k.octave != 0) continue;
+        const int c = grid_cell(g, k.x, k.y);
+        if (c >= 0) atomicAdd(&cnt[c], 1);
+    }
+    __syncthreads();
+    // exclusive scan of the 3072 counts: 12 per thread
+    constexpr int kPer = kCells / 256;
+    int loc[kPer], s = 0;
+#pragma unroll
+    for (int u = 0; u < kPer; u++) { loc[u] = cnt[tid * kPer + u]; s += loc[u]; }
+    const int incl = wave_incl_scan_i32(s);
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    int run = incl - s;
+    for (int w = 0; w < wid; w++) run += wsum[w];
+    const int total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kPer; u++) {
+        cnt[tid * kPer + u] = run;
+        CS[tid * kPer + u] = run;
+        run += loc[u];
+    }
+    if (tid == 0) CS[kCells] = total;
+    __syncthreads();
+    for (int j = tid; j < n2; j += 256) {
+        const orb_keypoint k = K2[j];
+        if (k.octave != 0) continue;
+        const int c = grid_cell(g, k.x, k.y);
+        if (c < 0) continue;
+        const int pos = atomicAdd(&cnt[c], 1);
+        GJ[pos] = j;
+    }
+    __syncthreads();
+    // restore ascending keypoint order inside every cell (insertion sort; cells hold a few)
+    for (int c = tid; c < kCells; c += 256) {
+        const int s0 = CS[c], s1 = CS[c + 1];
+        for (int a = s0 + 1; a < s1; a++) {
+            const int v = GJ[a];
+            int q = a - 1;
+            while (q >= s0 && GJ[q] > v) { GJ[q + 1] = GJ[q]; q--; }
+            GJ[q + 1] = v;
+        }
+    }
+    __syncthreads();
+    for (int p = tid; p < total; p += 256) {
+        const orb_keypoint k = K2[GJ[p]];
+        GXY[p] = make_float2(k.x, k.y);
+    }
+}
+
+// Candidate lists for F1 level-0 keypoints, enumerated exactly as GetFeaturesInArea returns
+// them (R/src/Frame.cpp:387-440: cell column ix outer, row iy inner, bucket order), so a
+// candidate's list position is its visiting order in the reference's loop.
+//   cand[b][i1][*] = (i2 | dist << 20) in visiting order, ncand[b][i1] = list length;
+//   topk[b][i1][0..7] = the kTopK smallest (dist, position) entries, packed the same way
+//   (0xFFFFFFFF past the end).  For the reference's loop (R/src/ORBmatcher.cpp:523-549)
+//   the first entry of this order not skipped by vMatchedDistance is bestIdx2 and the next
+//   one carries bestDist2, so the sequential replay reads only this prefix.
 __global__ __launch_bounds__(256) void k_cand_sfi(const orb_keypoint* __restrict__ kps1, const uint8_t* __restrict__ desc1,
-                                                  const int32_t* __restrict__ n1s, const orb_keypoint* __restrict__ kps2,
-                                                  const uint8_t* __restrict__ desc2, const int32_t* __restrict__ n2s,
-                                                  const float* __restrict__ prev, int cap, GridParams g, float window,
-                                                  uint32_t* __restrict__ cand, int* __restrict__ ncand, int* __restrict__ status) {
+                                                  const int32_t* __restrict__ n1s, const uint8_t* __restrict__ desc2,
+                                                  const int* __restrict__ cellStart, const int* __restrict__ gj,
+                                                  const float2* __restrict__ gxy, const float* __restrict__ prev,
+                                                  int cap, GridParams g, float window, uint32_t* __restrict__ cand,
+                                                  int* __restrict__ ncand, uint32_t* __restrict__ topk,
+                                                  int* __restrict__ status) {
+    __shared__ int segOff[4][kGridCols + 1];
+    __shared__ uint32_t sj[4][kMaxCand];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int b = blockIdx.y;
     const int i1 = blockIdx.x * 4 + wid;
-    const int n1 = min((int)n1s[b], cap), n2 = min((int)n2s[b], cap);
+    const int n1 = min((int)n1s[b], cap);
     if (i1 >= n1) return;
     const orb_keypoint* K1 = kps1 + (size_t)b * cap;
-    const orb_keypoint* K2 = kps2 + (size_t)b * cap;
     int* nc = ncand + (size_t)b * cap + i1;
     const orb_keypoint kp1 = K1[i1];
     if (kp1.octave > 0) { if (lane == 0) *nc = 0; return; }
     float px, py;
     if (prev) { px = prev[((size_t)b * cap + i1) * 2]; py = prev[((size_t)b * cap + i1) * 2 + 1]; }
     else { px = kp1.x; py = kp1.y; }
-    const AreaQuery q = make_area(g, px, py, window, kp1.octave, kp1.octave);
+    const AreaQuery q = make_area(g, px, py, window, 0, 0);
     uint32_t* out = cand + ((size_t)b * cap + i1) * kMaxCand;
-    const uint8_t* dq = desc1 + ((size_t)b * cap + i1) * 32;
+    const int* CS = cellStart + (size_t)b * (kCells + 1);
+    const int* GJ = gj + (size_t)b * cap;
+    const float2* GXY = gxy + (size_t)b * cap;
+    const uint4* dq4 = reinterpret_cast<const uint4*>(desc1 + ((size_t)b * cap + i1) * 32);
+    const uint4 qa = dq4[0], qb = dq4[1];
+    int* so = segOff[wid];
+    uint32_t* J = sj[wid];
+    // one lane per grid column of the window: bucket range [cy0, cy1] of that column
+    const int ncx = q.cx1 - q.cx0 + 1;   // <= 64
+    int segS = 0, segL = 0;
+    if (lane < ncx) {
+        const int c0 = (q.cx0 + lane) * kGridRows + q.cy0;
+        segS = CS[c0];
+        segL = CS[c0 + (q.cy1 - q.cy0) + 1] - segS;
+    }
+    const int incl = wave_incl_scan_i32(segL);
+    const int T = __shfl(incl, 63, 64);
+    if (lane < ncx) so[lane] = incl - segL;
+    if (lane == 0) so[kGridCols] = T;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     int n = 0;
-    for (int j0 = 0; j0 < n2; j0 += 64) {
-        const int j = j0 + lane;
+    for (int t0 = 0; t0 < T; t0 += 64) {
+        const int t = t0 + lane;
         bool ok = false;
-        int d = 0;
-        if (j < n2 && q.cx0 <= q.cx1) {
-            const orb_keypoint k2 = K2[j];
-            ok = in_area(q, grid_cell(g, k2.x, k2.y), k2.octave, k2.x, k2.y);
-            if (ok) d = hamming32(dq, desc2 + ((size_t)b * cap + j) * 32);
+        int d = 0, j = 0;
+        int seg = 0;   // window column of entry t: last column whose offset <= t
+        if (t < T) {
+            int lo = 0, hi = ncx - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (so[mid] <= t) lo = mid; else hi = mid - 1;
+            }
+            seg = lo;
+        }
+        const int base = __shfl(segS, seg, 64);
+        if (t < T) {
+            const int p = base + (t - so[seg]);
+            const float2 xy = GXY[p];
+            ok = fabsf(xy.x - q.x) < q.r && fabsf(xy.y - q.y) < q.r;
+            if (ok) {
+                j = GJ[p];
+                const uint4* d4 = reinterpret_cast<const uint4*>(desc2 + ((size_t)b * cap + j) * 32);
+                const uint4 a0 = d4[0], a1 = d4[1];
+                d = __popc(a0.x ^ qa.x) + __popc(a0.y ^ qa.y) + __popc(a0.z ^ qa.z) + __popc(a0.w ^ qa.w) +
+                    __popc(a1.x ^ qb.x) + __popc(a1.y ^ qb.y) + __popc(a1.z ^ qb.z) + __popc(a1.w ^ qb.w);
+            }
         }
         const uint64_t m = __ballot(ok);
         const int pos = n + __popcll(m & ((1ull << lane) - 1ull));
-        if (ok && pos < kMaxCand) out[pos] = (uint32_t)j | ((uint32_t)d << 20);
+        if (ok && pos < kMaxCand) {
+            const uint32_t e = (uint32_t)j | ((uint32_t)d << 20);
+            out[pos] = e;
+            J[pos] = e;
+        }
         n += __popcll(m);
     }
-    if (lane == 0) {
-        if (n > kMaxCand) { atomicOr(status, 1); n = kMaxCand; }
-        *nc = n;
+    if (n > kMaxCand) {
+        if (lane == 0) atomicOr(status, 1);
+        n = kMaxCand;
+    }
+    if (lane == 0) *nc = n;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // top-K by (dist, list position): 32-bit keys dist << 11 | position
+    uint32_t run = ~0u;
+    for (int c0 = 0; c0 < n; c0 += 64) {
+        uint32_t v = (c0 + lane < n) ? ((J[c0 + lane] >> 20) << 11) | (uint32_t)(c0 + lane) : ~0u;
+#pragma unroll
+        for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+            for (int jj = k >> 1; jj > 0; jj >>= 1) {
+                const uint32_t o = __shfl_xor(v, jj, 64);
+                const bool takeMin = ((lane & jj) == 0) == ((lane & k) == 0);
+                v = takeMin ? min(o, v) : max(o, v);
+            }
+        }
+        if (c0 == 0) {
+            run = v;
+        } else {
+            const uint32_t rev = __shfl(v, (kTopK - 1 - lane) & 63, 64);
+            uint32_t t = lane < kTopK ? min(run, rev) : ~0u;
+#pragma unroll
+            for (int s2 = kTopK >> 1; s2 > 0; s2 >>= 1) {
+                const uint32_t o = __shfl_xor(t, s2, 64);
+                t = ((lane & s2) == 0) ? min(o, t) : max(o, t);
+            }
+            run = t;
+        }
+    }
+    if (lane < kTopK) {
+        uint32_t* tk = topk + ((size_t)b * cap + i1) * kTopK;
+        tk[lane] = run == ~0u ? ~0u : J[run & 0x7FFu];
     }
 }
 
-// Sequential replay of R/src/ORBmatcher.cpp:512-616 for one frame pair per workgroup (one wave).
+// Sequential replay of R/src/ORBmatcher.cpp:512-616 for one frame pair per workgroup (one
+// wave).  Active queries (non-empty window) are staged in LDS with their top-K lists; one
+// query then costs one LDS probe of vMatchedDistance by K lanes and a ballot.  Only when
+// fewer than two of the K survive the skip test and more candidates exist does the wave
+// rescan the query's full list.
+// vnMatches12 is rebuilt at the end: a query keeps its match iff vnMatches21 still points
+// back to it (a later query that stole the keypoint overwrote vnMatches21), and every query
+// that ever matched sits in the rotation histogram, as rotHist[bin].push_back(i1) does.
 __global__ __launch_bounds__(64) void k_resolve_sfi(const orb_keypoint* __restrict__ kps1, const int32_t* __restrict__ n1s,
                                                     const orb_keypoint* __restrict__ kps2, const int32_t* __restrict__ n2s,
                                                     int cap, GridParams g, float nnratio, int checkOri,
                                                     const uint32_t* __restrict__ cand, const int* __restrict__ ncand,
-                                                    float* __restrict__ prev, int32_t* __restrict__ matches12,
-                                                    int32_t* __restrict__ nmatches_out, int32_t* __restrict__ histIdx,
-                                                    uint8_t* __restrict__ histBin) {
+                                                    const uint32_t* __restrict__ topk, float* __restrict__ prev,
+                                                    int32_t* __restrict__ matches12, int32_t* __restrict__ nmatches_out) {
+    TSTAMP(t_begin);
+    long long tStage = 0, tLoop = 0;
+    int nFall = 0, nAct = 0, nMatch = 0;
+    (void)tStage; (void)tLoop; (void)nFall; (void)nAct; (void)nMatch;
     extern __shared__ __attribute__((aligned(16))) int sm[];
     const int lane = threadIdx.x;
     const int b = blockIdx.x;
     const int n1 = min((int)n1s[b], cap), n2 = min((int)n2s[b], cap);
     int* vMD = sm;                   // vMatchedDistance [n2]
     int* v21 = sm + cap;             // vnMatches21 [n2]
-    int* ckey = sm + 2 * cap;        // grid cell key per F2 keypoint
-    int* hcount = sm + 3 * cap;      // [kHisto]
+    int* ckey = sm + 2 * cap;        // grid cell key per F2 keypoint (full-rescan order)
+    int* mt = sm + 3 * cap;          // i2 each query matched when it was processed, or -1
+    int* hcount = sm + 4 * cap;      // [kHisto]
     const orb_keypoint* K1 = kps1 + (size_t)b * cap;
     const orb_keypoint* K2 = kps2 + (size_t)b * cap;
     int32_t* m12 = matches12 + (size_t)b * cap;
-    int32_t* hI = histIdx + (size_t)b * cap;
-    uint8_t* hB = histBin + (size_t)b * cap;
-    for (int j = lane; j < n2; j += 64) {
-        vMD[j] = INT_MAX;
-        v21[j] = -1;
-        ckey[j] = grid_cell(g, K2[j].x, K2[j].y);
+    const uint32_t* TK = topk + (size_t)b * cap * kTopK;
+    const int* NC = ncand + (size_t)b * cap;
+    for (int j0 = 0; j0 < n2; j0 += 256) {
+        float kx[4], ky[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int j = j0 + u * 64 + lane;
+            kx[u] = j < n2 ? K2[j].x : 0.f;
+            ky[u] = j < n2 ? K2[j].y : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int j = j0 + u * 64 + lane;
+            if (j < n2) {
+                vMD[j] = INT_MAX;
+                v21[j] = -1;
+                ckey[j] = grid_cell(g, kx[u], ky[u]);
+            }
+        }
     }
-    for (int i = lane; i < n1; i += 64) m12[i] = -1;
+    for (int i = lane; i < n1; i += 64) mt[i] = -1;
     if (lane < kHisto) hcount[lane] = 0;
     __syncthreads();
-    int nmatches = 0, nh = 0;
-    for (int i1 = 0; i1 < n1; i1++) {
-        const int nc = ncand[(size_t)b * cap + i1];
-        if (nc == 0) continue;   // also octave > 0 (no candidates listed)
-        const uint32_t* C = cand + ((size_t)b * cap + i1) * kMaxCand;
-        Best2 acc;
-        acc.best = INT_MAX; acc.best2 = INT_MAX; acc.idx = -1;
-        unsigned accOrder = 0xFFFFFu;
-        for (int c0 = 0; c0 < nc; c0 += 64) {
-            const int c = c0 + lane;
-            bool valid = false;
-            int d = 0, j = 0;
-            unsigned order = 0;
-            if (c < nc) {
-                const uint32_t e = C[c];
-                j = (int)(e & 0xFFFFFu);
-                d = (int)(e >> 20);
-                valid = vMD[j] > d;            // `if(vMatchedDistance[i2]<=dist) continue;`
-                order = (unsigned)ckey[j];     // candidates are visited cell-major (ix, iy), then by index
+    // Queries are taken in ranges of kRange: the active ones (a non-empty window) are
+    // compacted and their top-K lists bulk-loaded into LDS, so the serial replay below
+    // touches only LDS.
+    int* qidx = hcount + 32;                       // [kRange]
+    int* qnc = qidx + kRange;                      // [kRange]
+    uint32_t* qtk = (uint32_t*)(qnc + kRange);     // [kRange * kTopK]
+    const int myK = lane & (kTopK - 1);
+    TSTAMP(t_init);
+    for (int r0 = 0; r0 < n1; r0 += kRange) {
+        TSTAMP(t_r0);
+        const int rEnd = min(n1, r0 + kRange);
+        int na = 0;
+        // all loads of a stage are issued before any is consumed (global latency paid once)
+        int ncv[kRange / 64];
+#pragma unroll
+        for (int u = 0; u < kRange / 64; u++) {
+            const int i = r0 + u * 64 + lane;
+            ncv[u] = i < rEnd ? NC[i] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kRange / 64; u++) {
+            const int i = r0 + u * 64 + lane;
+            const uint64_t m = __ballot(ncv[u] > 0);
+            if (ncv[u] > 0) {
+                const int pos = na + __popcll(m & ((1ull << lane) - 1ull));
+                qidx[pos] = i;
+                qnc[pos] = ncv[u];
             }
-            const Best2 r = wave_best2(d, order, j, valid);
-            // merge chunk result into the running (best, best2, idx): the earlier chunk wins ties
-            // only if its order is smaller — orders are compared explicitly.
-            if (r.idx >= 0) {
-                const unsigned rOrder = (unsigned)ckey[r.idx];
-                const bool rFirst = (r.best < acc.best) ||
-                                    (r.best == acc.best && (rOrder < accOrder || (rOrder == accOrder && r.idx < acc.idx)));
-                int nb2;
-                if (rFirst) {
-                    nb2 = min(acc.best, r.best2);
-                    acc.idx = r.idx;
-                    accOrder = rOrder;
-                    acc.best = r.best;
-                } else {
-                    nb2 = min(acc.best2, r.best);
-                }
-                acc.best2 = nb2;
+            na += __popcll(m);
+        }
+        wave_lds_sync();
+        for (int t0 = 0; t0 < na * kTopK; t0 += 64 * 8) {
+            uint32_t tv[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int t = t0 + u * 64 + lane;
+                tv[u] = t < na * kTopK ? TK[(size_t)qidx[t / kTopK] * kTopK + (t % kTopK)] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int t = t0 + u * 64 + lane;
+                if (t < na * kTopK) qtk[t] = tv[u];
             }
         }
-        if (acc.idx >= 0 && acc.best <= kThLow && (float)acc.best < (float)acc.best2 * nnratio) {
-            const int bi = acc.idx;
-            const int prevOwner = v21[bi];
-            if (lane == 0) {
-                if (prevOwner >= 0) m12[prevOwner] = -1;
-                m12[i1] = bi;
-                v21[bi] = i1;
-                vMD[bi] = acc.best;
-                if (checkOri) {
-                    const int bin = rot_bin(K1[i1].angle - K2[bi].angle);
-                    hI[nh] = i1;
-                    hB[nh] = (uint8_t)bin;
-                    hcount[bin]++;
+        wave_lds_sync();
+        TACC(tStage, t_r0);
+        TSTAMP(t_l0);
+        // Eight queries at a time: lane 8q+k probes vMatchedDistance for the k-th preferred
+        // candidate of query a0+q in one LDS gather; the queries are then decided in order from
+        // the ballot, and a match clears the probe bits of later queries of the batch that
+        // see the same keypoint at a distance >= the new vMatchedDistance.
+        for (int a0 = 0; a0 < na; a0 += 8) {
+            const int a = a0 + (lane >> 3);
+            uint32_t e = ~0u;
+            int nc = 0, qi = -1;
+            if (a < na) { nc = qnc[a]; e = qtk[a * kTopK + myK]; qi = qidx[a]; }
+            const int j = (int)(e & 0xFFFFFu), d = (int)(e >> 20);
+            bool valid = false;
+            if (a < na && myK < min(nc, kTopK)) valid = vMD[j] > d;   // `if(vMatchedDistance[i2]<=dist) continue;`
+            // per-lane float bits of (float)dist and of (float)dist * nnratio: for non-negative
+            // floats the ratio test `bestDist < (float)bestDist2*mfNNratio` is an unsigned compare
+            const float fd = (float)d;
+            const uint32_t fdb = __float_as_uint(fd), thrb = __float_as_uint(fd * nnratio);
+            uint64_t vm = __ballot(valid);
+            const uint64_t bigNc = __ballot(myK == 0 && nc > kTopK);
+            const int qEnd = min(8, na - a0);
+#ifdef ORB_TIMING
+            nAct += qEnd;
+#endif
+            for (int qq = 0; qq < qEnd; qq++) {
+                const uint32_t mk = (uint32_t)(vm >> (qq * 8)) & 0xFFu;
+                int bestd, bi;
+                uint32_t bestb, thr;
+                if (__popc(mk) >= 2 || ((bigNc >> (qq * 8)) & 1ull) == 0) {
+                    if (mk == 0) continue;
+                    const int l1 = qq * 8 + __ffs(mk) - 1;
+                    const uint32_t mk2 = mk & (mk - 1u);
+                    bestd = __builtin_amdgcn_readlane(d, l1);
+                    bi = __builtin_amdgcn_readlane(j, l1);
+                    bestb = __builtin_amdgcn_readlane(fdb, l1);
+                    thr = mk2 ? __builtin_amdgcn_readlane(thrb, qq * 8 + __ffs(mk2) - 1) : 0x7F800000u;
+                } else {
+#ifdef ORB_TIMING
+                    nFall++;
+#endif
+                    // fewer than two of the top-K survive: rescan the query's whole list
+                    const int ncq = __builtin_amdgcn_readlane(nc, qq * 8);
+                    const int iq = __builtin_amdgcn_readlane(qi, qq * 8);
+                    const uint32_t* C = cand + ((size_t)b * cap + iq) * kMaxCand;
+                    Best2 acc;
+                    acc.best = INT_MAX; acc.best2 = INT_MAX; acc.idx = -1;
+                    unsigned accOrder = 0xFFFFFu;
+                    for (int c0 = 0; c0 < ncq; c0 += 64) {
+                        const int c = c0 + lane;
+                        bool ok = false;
+                        int dd = 0, jj = 0;
+                        unsigned order = 0;
+                        if (c < ncq) {
+                            const uint32_t ce = C[c];
+                            jj = (int)(ce & 0xFFFFFu);
+                            dd = (int)(ce >> 20);
+                            ok = vMD[jj] > dd;
+                            order = (unsigned)ckey[jj];
+                        }
+                        const Best2 r = wave_best2(dd, order, jj, ok);
+                        if (r.idx >= 0) {
+                            const unsigned rOrder = (unsigned)ckey[r.idx];
+                            const bool rFirst = (r.best < acc.best) ||
+                                                (r.best == acc.best && (rOrder < accOrder || (rOrder == accOrder && r.idx < acc.idx)));
+                            if (rFirst) {
+                                acc.best2 = min(acc.best, r.best2);
+                                acc.idx = r.idx;
+                                accOrder = rOrder;
+                                acc.best = r.best;
+                            } else {
+                                acc.best2 = min(acc.best2, r.best);
+                            }
+                        }
+                    }
+                    bi = __builtin_amdgcn_readfirstlane(acc.idx);
+                    if (bi < 0) continue;
+                    bestd = __builtin_amdgcn_readfirstlane(acc.best);
+                    const int b2 = __builtin_amdgcn_readfirstlane(acc.best2);
+                    bestb = __float_as_uint((float)bestd);
+                    thr = __float_as_uint((float)b2 * nnratio);
+                }
+                if (bestd <= kThLow && bestb < thr) {
+#ifdef ORB_TIMING
+                    nMatch++;
+#endif
+                    const int i1 = __builtin_amdgcn_readlane(qi, qq * 8);
+                    if (lane == 0) {
+                        v21[bi] = i1;
+                        vMD[bi] = bestd;
+                        mt[i1] = bi;
+                    }
+                    // later queries of the batch now see vMatchedDistance[bi] == bestd
+                    valid = valid && !(j == bi && bestd <= d);
+                    vm = __ballot(valid);
                 }
             }
-            if (prevOwner >= 0) nmatches--;
-            nmatches++;
-            if (checkOri) nh++;
-            __syncthreads();
+            wave_lds_sync();
+        }
+        wave_lds_sync();
+        TACC(tLoop, t_l0);
+    }
+    TSTAMP(t_loopend);
+    __syncthreads();
+    // rotation bin of every query that ever matched (stolen ones included); a query keeps its
+    // match iff vnMatches21 still points back to it
+    for (int i0 = 0; i0 < n1; i0 += 256) {
+        int jv[4];
+        float a1[4], a2[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int i = i0 + u * 64 + lane;
+            jv[u] = i < n1 ? mt[i] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int i = i0 + u * 64 + lane;
+            a1[u] = jv[u] >= 0 ? K1[i].angle : 0.f;
+            a2[u] = jv[u] >= 0 ? K2[jv[u]].angle : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int i = i0 + u * 64 + lane;
+            if (jv[u] < 0) continue;
+            const int bin = rot_bin(a1[u] - a2[u]);
+            if (checkOri) atomicAdd(&hcount[bin], 1);
+            mt[i] = v21[jv[u]] == i ? (jv[u] | (bin << 24)) : -1;
         }
     }
     __syncthreads();
+    int ind1 = -1, ind2 = -1, ind3 = -1;
     if (checkOri) {
         // ComputeThreeMaxima (R/src/ORBmatcher.cpp:1854-1895)
-        int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+        int max1 = 0, max2 = 0, max3 = 0;
         for (int i = 0; i < kHisto; i++) {
             const int s = hcount[i];
             if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
@@ -282,27 +585,50 @@ __global__ __launch_bounds__(64) void k_resolve_sfi(const orb_keypoint* __restri
         }
         if ((float)max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
         else if ((float)max3 < 0.1f * (float)max1) { ind3 = -1; }
-        // drop matches in every other bin (order irrelevant: a match's entry is unique per i1 state)
-        int removed = 0;
-        for (int e = lane; e < nh; e += 64) {
-            const int bin = hB[e];
-            if (bin == ind1 || bin == ind2 || bin == ind3) continue;
-            const int idx1 = hI[e];
-            if (m12[idx1] >= 0) { m12[idx1] = -1; removed++; }
-        }
-        nmatches -= wave_reduce_sum_i32(removed);
     }
-    __syncthreads();
-    if (prev) {
-        for (int i = lane; i < n1; i += 64) {
-            const int j = m12[i];
+    int kept = 0;
+    for (int i0 = 0; i0 < n1; i0 += 256) {
+        int jv[4];
+        float px[4], py[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int i = i0 + u * 64 + lane;
+            int j = i < n1 ? mt[i] : -1;
             if (j >= 0) {
-                prev[((size_t)b * cap + i) * 2] = K2[j].x;
-                prev[((size_t)b * cap + i) * 2 + 1] = K2[j].y;
+                const int bin = j >> 24;
+                j &= 0xFFFFFF;
+                if (checkOri && bin != ind1 && bin != ind2 && bin != ind3) j = -1;
+            }
+            jv[u] = j;
+        }
+        if (prev) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                px[u] = jv[u] >= 0 ? K2[jv[u]].x : 0.f;
+                py[u] = jv[u] >= 0 ? K2[jv[u]].y : 0.f;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int i = i0 + u * 64 + lane;
+            if (i >= n1) continue;
+            m12[i] = jv[u];
+            if (jv[u] >= 0) {
+                kept++;
+                if (prev) {
+                    prev[((size_t)b * cap + i) * 2] = px[u];
+                    prev[((size_t)b * cap + i) * 2 + 1] = py[u];
+                }
             }
         }
     }
-    if (lane == 0) nmatches_out[b] = nmatches;
+    kept = wave_reduce_sum_i32(kept);
+    if (lane == 0) nmatches_out[b] = kept;
+#ifdef ORB_TIMING
+    if (lane == 0 && b == 0)
+        printf("resolve b0: init %lld stage %lld loop %lld final %lld total %lld (cycles) n1 %d n2 %d act %d fall %d match %d\n",
+               t_init - t_begin, tStage, tLoop, clock64() - t_loopend, clock64() - t_begin, n1, n2, nAct, nFall, nMatch);
+#endif
 }
 
 // ---------------------------------------------------------------- SearchByProjection(Frame, Frame)
@@ -504,6 +830,9 @@ struct orb_matcher {
     int32_t *d_n = nullptr, *d_m12 = nullptr, *d_nm = nullptr, *d_hI = nullptr;
     uint8_t* d_hB = nullptr;
     uint32_t* d_cand = nullptr;
+    uint32_t* d_topk = nullptr;
+    int *d_cs = nullptr, *d_gj = nullptr;   // SFI grid buckets
+    float2* d_gxy = nullptr;
     int *d_ncand = nullptr, *d_status = nullptr;
     // SBP extras
     int32_t* d_hasMp = nullptr;
@@ -516,12 +845,13 @@ struct orb_matcher {
 
 static void mfree(orb_matcher* m) {
     void* ptrs[] = {m->d_k1, m->d_k2, m->d_d1, m->d_d2, m->d_prev, m->d_ur, m->d_n, m->d_m12, m->d_nm, m->d_hI,
-                    m->d_hB, m->d_cand, m->d_ncand, m->d_status, m->d_hasMp, m->d_outl, m->d_xyz, m->d_T,
+                    m->d_hB, m->d_cand, m->d_topk, m->d_cs, m->d_gj, m->d_gxy, m->d_ncand, m->d_status, m->d_hasMp, m->d_outl, m->d_xyz, m->d_T,
                     m->d_sf, m->d_mpd};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     m->d_k1 = m->d_k2 = nullptr; m->d_d1 = m->d_d2 = nullptr; m->d_prev = m->d_ur = nullptr;
-    m->d_n = m->d_m12 = m->d_nm = m->d_hI = nullptr; m->d_hB = nullptr; m->d_cand = nullptr;
+    m->d_n = m->d_m12 = m->d_nm = m->d_hI = nullptr; m->d_hB = nullptr; m->d_cand = nullptr; m->d_topk = nullptr;
+    m->d_cs = m->d_gj = nullptr; m->d_gxy = nullptr;
     m->d_ncand = m->d_status = nullptr; m->d_hasMp = nullptr; m->d_outl = nullptr;
     m->d_xyz = m->d_T = m->d_sf = nullptr; m->d_mpd = nullptr;
     m->capPairs = m->capPts = 0;
@@ -548,6 +878,10 @@ static int mensure(orb_matcher* m, size_t pairs, size_t pts) {
     MALLOC(m->d_hI, P * 4);
     MALLOC(m->d_hB, P);
     MALLOC(m->d_cand, P * kMaxCand * 4);
+    MALLOC(m->d_topk, P * kTopK * 4);
+    MALLOC(m->d_cs, pairs * (kCells + 1) * 4);
+    MALLOC(m->d_gj, P * 4);
+    MALLOC(m->d_gxy, P * 8);
     MALLOC(m->d_ncand, P * 4);
     MALLOC(m->d_status, 64);
     MALLOC(m->d_hasMp, P * 4);
@@ -658,11 +992,14 @@ int orb_search_for_initialization(orb_matcher* m, const orb_frame_view* f1, cons
     ORB_HIP_TRY(hipMemcpyAsync(m->d_n, hn, 8, hipMemcpyHostToDevice, s));
     ORB_HIP_TRY(hipMemsetAsync(m->d_status, 0, 4, s));
     const GridParams g = grid_of(f2);
-    hipLaunchKernelGGL(k_cand_sfi, dim3((cap + 3) / 4, 1), dim3(256), 0, s, m->d_k1, m->d_d1, m->d_n, m->d_k2, m->d_d2,
-                       m->d_n + 1, m->d_prev, cap, g, (float)window, m->d_cand, m->d_ncand, m->d_status);
-    const size_t lds = (3 * (size_t)cap + kHisto + 4) * 4;
+    hipLaunchKernelGGL(k_grid_sfi, dim3(1), dim3(256), 0, s, m->d_k2, m->d_n + 1, cap, g, m->d_cs, m->d_gj, m->d_gxy);
+    hipLaunchKernelGGL(k_cand_sfi, dim3((cap + 3) / 4, 1), dim3(256), 0, s, m->d_k1, m->d_d1, m->d_n, m->d_d2, m->d_cs,
+                       m->d_gj, m->d_gxy, m->d_prev, cap, g, (float)window, m->d_cand, m->d_ncand, m->d_topk,
+                       m->d_status);
+    const size_t lds = (4 * (size_t)cap + 32 + (2 + kTopK) * kRange) * 4;
+    if (lds > 65536) return ORB_E2BIG;
     hipLaunchKernelGGL(k_resolve_sfi, dim3(1), dim3(64), lds, s, m->d_k1, m->d_n, m->d_k2, m->d_n + 1, cap, g,
-                       m->nnratio, m->checkOri, m->d_cand, m->d_ncand, m->d_prev, m->d_m12, m->d_nm, m->d_hI, m->d_hB);
+                       m->nnratio, m->checkOri, m->d_cand, m->d_ncand, m->d_topk, m->d_prev, m->d_m12, m->d_nm);
     ORB_HIP_TRY(hipGetLastError());
     int32_t* hm = (int32_t*)hd1;   // reuse pinned space
     ORB_HIP_TRY(hipMemcpyAsync(hm, m->d_m12, (size_t)f1->n * 4, hipMemcpyDeviceToHost, s));
@@ -689,11 +1026,14 @@ int orb_search_for_initialization_batch_device(orb_matcher* m, const orb_keypoin
     g.min_x = 0.f; g.min_y = 0.f; g.max_x = (float)width; g.max_y = (float)height;
     g.winv = (float)kGridCols / (float)width;
     g.hinv = (float)kGridRows / (float)height;
-    hipLaunchKernelGGL(k_cand_sfi, dim3((cap + 3) / 4, nb), dim3(256), 0, s, d_kps1, d_desc1, d_n1, d_kps2, d_desc2, d_n2,
-                       (const float*)nullptr, cap, g, (float)window, m->d_cand, m->d_ncand, m->d_status);
-    const size_t lds = (3 * (size_t)cap + kHisto + 4) * 4;
+    hipLaunchKernelGGL(k_grid_sfi, dim3(nb), dim3(256), 0, s, d_kps2, d_n2, cap, g, m->d_cs, m->d_gj, m->d_gxy);
+    hipLaunchKernelGGL(k_cand_sfi, dim3((cap + 3) / 4, nb), dim3(256), 0, s, d_kps1, d_desc1, d_n1, d_desc2, m->d_cs,
+                       m->d_gj, m->d_gxy, (const float*)nullptr, cap, g, (float)window, m->d_cand, m->d_ncand,
+                       m->d_topk, m->d_status);
+    const size_t lds = (4 * (size_t)cap + 32 + (2 + kTopK) * kRange) * 4;
+    if (lds > 65536) return ORB_E2BIG;
     hipLaunchKernelGGL(k_resolve_sfi, dim3(nb), dim3(64), lds, s, d_kps1, d_n1, d_kps2, d_n2, cap, g, m->nnratio,
-                       m->checkOri, m->d_cand, m->d_ncand, (float*)nullptr, d_matches12, d_nmatches, m->d_hI, m->d_hB);
+                       m->checkOri, m->d_cand, m->d_ncand, m->d_topk, (float*)nullptr, d_matches12, d_nmatches);
     ORB_HIP_TRY(hipGetLastError());
     return ORB_OK;
 }
