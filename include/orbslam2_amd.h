@@ -97,8 +97,9 @@ int orb_pyramid_level_device(orb_extractor* ex, int frame, int level, int blurre
                              const uint8_t** dptr, int* w, int* h, size_t* pitch);
 
 /* Stage profiling: while enabled, every extraction records HIP events on its
- * launch stream around the six kernel stages (0 resize, 1 fast_score,
- * 2 cell_detect, 3 octree, 4 blur, 5 orient_desc).  orb_extractor_stage_times
+ * launch stream around the six kernel stages (0 resize, 1 FAST detection per
+ * cell incl. NMS and the minThFAST retry, 2 reserved (always 0), 3 octree,
+ * 4 blur, 5 orient_desc).  orb_extractor_stage_times
  * waits for them, writes the summed milliseconds per stage to ms[0..n_stages)
  * and the number of profiled calls to *n_calls, then resets; returns the number
  * of stages. */

@@ -1,9 +1,8 @@
 // MI355X-native ORB extractor: ORBextractor::operator() (R/src/ORBextractor.cpp:1120-1188)
-// as six gfx950 kernels over a batch of frames:
+// as five gfx950 kernels over a batch of frames:
 //   k_resize      A2  pyramid level l from level l-1 (INTER_LINEAR 8U fixed point)
-//   k_fast_score  A3  per-pixel FAST-9/16 corner score S (threshold independent)
-//   k_cell_detect A3  per-cell threshold choice (iniThFAST, retry minThFAST), cell-local NMS,
-//                     raster-order compaction  (R/src/ORBextractor.cpp:851-896)
+//   k_fast_cell   A3  one wave per FAST cell: SWAR pre-test, FAST-9/16 score, cell-local NMS,
+//                     iniThFAST / minThFAST retry, raster-order keys (R/src/ORBextractor.cpp:851-896)
 //   k_octree      A4  DistributeOctTree, phase-parallel emulation of the std::list algorithm
 //                     (R/src/ORBextractor.cpp:571-817), one workgroup per (frame, level)
 //   k_blur        A6  GaussianBlur 7x7 sigma 2 REFLECT_101 (8-bit fixed point)
@@ -56,6 +55,7 @@ struct Geom {
     int w, h;
     long long frameBytes;
     int cellsPerFrame, slotsPerFrame, outPerFrame, tilesPerFrame, maxNodeCap, maxLevelSlots;
+    int maxCellW, maxCellH;   // largest FAST cell detection region
     int iniTh, minTh, tmin;
     float factorPI;
     int umax[16];
@@ -147,6 +147,9 @@ static int build_geom(const orb_extractor_params& p, int w, int h, Geom* g) {
         L.slotBase = slots;
         slots += L.nCols * L.nRows * L.cellCap;
         g->maxLevelSlots = std::max(g->maxLevelSlots, L.nCols * L.nRows * L.cellCap);
+        g->maxCellW = std::max(g->maxCellW, L.wCell);
+        g->maxCellH = std::max(g->maxCellH, L.hCell);
+        if (L.wCell > 64) return ORB_EINVAL;   // a region row must fit the 64 lanes of a wave
         L.N = fpl[l];
         L.nIni = (int)std::round((float)(L.maxBX - kMinBorder) / (float)(L.maxBY - kMinBorder));
         if (L.nIni < 1) return ORB_EINVAL;
@@ -260,144 +263,37 @@ __device__ __forceinline__ int fast_score(const int v, const int p[16]) {
     return max(A, -Bp) - 1;
 }
 
-constexpr int kTileW = 64, kTileH = 16;
-constexpr int kImgW = kTileW + 8, kImgH = kTileH + 8;   // image tile + 4-px halo (ring 3 + score halo 1)
-constexpr int kScW = kTileW + 2, kScH = kTileH + 2;     // score tile + 1-px halo (NMS neighbours)
+constexpr int kTileW = 64, kTileH = 16;   // blur tiles
 
-// Detection regions of the FAST cells (R/src/ORBextractor.cpp:851-883): cell (i, j) detects
-// rows [19 + i*hCell, min(19 + (i+1)*hCell, maxBY - 3)) and columns
-// [19 + j*wCell, min(19 + (j+1)*wCell, maxBX - 3)) — the windows' 3-px FAST margins make the
-// regions a partition, so every pixel belongs to at most one cell.
-// Cell index of a column / row of the level, or -1 outside every detection region.
-__device__ __forceinline__ int region_col(const LevelGeom& L, int x) {
-    if (x < kEdge || x >= L.maxBX - 3) return -1;
-    const int j = (x - kEdge) / L.wCell;
-    return j < L.nCols ? j : -1;
-}
-__device__ __forceinline__ int region_row(const LevelGeom& L, int y) {
-    if (y < kEdge || y >= L.maxBY - 3) return -1;
-    const int i = (y - kEdge) / L.hCell;
-    return i < L.nRows ? i : -1;
+// ------------------------------------------------------------------ A3: FAST per cell (fused)
+
+// Per-wave LDS of k_fast_cell for regions up to maxW x maxH (host and device agree on it).
+__host__ __device__ inline int fc_patch_stride(int maxW) { return ((maxW + 8 + 3) & ~3) + 4; }
+__host__ __device__ inline int fc_wave_bytes(int maxW, int maxH) {
+    const int patch = (maxH + 6) * fc_patch_stride(maxW);
+    const int sc = maxH * 64;
+    const int list = maxW * maxH * 4;
+    return ((patch + 15) & ~15) + sc + list;
 }
 
-// Fused FAST score + cell-local non-maximum suppression, one 64x16 tile per workgroup.
-//  1. a 4-point pre-test (compass pixels 0/4/8/12 — any 9-arc contains two adjacent ones)
-//     selects the pixels that can reach S >= tmin; they are compacted into an LDS list;
-//  2. the full score S runs on the list only (S = 0 for everything else, as cv::FAST's score
-//     buffer holds 0 for non-corners);
-//  3. NMS against the 8 neighbours inside the same cell region.  With scores of non-corners at
-//     threshold t set to 0, "S > every neighbour" does not depend on t (a neighbour >= S is a
-//     corner at t whenever S is), so one map serves both FAST passes of the cell:
-//     nms[x,y] = S if (x,y) is a local maximum, else 0; the keypoints at t are nms >= t.
-__global__ __launch_bounds__(256) void k_fast_score(Geom g, const uint8_t* __restrict__ pyr,
-                                                    uint8_t* __restrict__ nms) {
-    __shared__ uint32_t img32[kImgH * kImgW / 4];
-    __shared__ uint8_t sc[kScH * kScW];
-    __shared__ uint16_t list[kScH * kScW];
-    __shared__ uint32_t outT[kTileH * kTileW / 4];
-    __shared__ int8_t colCell[kScW], rowCell[kScH];   // cell of each halo-tile column / row (-1: none)
-    __shared__ int cnt;
-    const int b = blockIdx.y;
-    const int l = level_of_tile(g, blockIdx.x);
-    const LevelGeom& L = g.lv[l];
-    const int t = blockIdx.x - L.tileBase;
-    const int tx0 = (t % L.tilesX) * kTileW, ty0 = (t / L.tilesX) * kTileH;
-    const uint8_t* img = pyr + (size_t)b * g.frameBytes + L.off;
-    uint8_t* out = nms + (size_t)b * g.frameBytes + L.off;
-    const int tid = threadIdx.x, lane = tid & 63;
-    for (int q = tid; q < kImgH * kImgW / 4; q += 256) {
-        const int r = q / (kImgW / 4), c4 = q % (kImgW / 4);
-        const int gx = tx0 - 4 + 4 * c4;
-        const int gy = min(max(ty0 - 4 + r, 0), L.h - 1);
-        img32[q] = (gx >= 0 && gx + 4 <= L.pitch) ? *reinterpret_cast<const uint32_t*>(img + (size_t)gy * L.pitch + gx) : 0u;
-    }
-    for (int q = tid; q < kScH * kScW; q += 256) sc[q] = 0;
-    if (tid < kTileH * kTileW / 4) outT[tid] = 0u;
-    if (tid < kScW) colCell[tid] = (int8_t)region_col(L, tx0 - 1 + tid);
-    else if (tid < kScW + kScH) rowCell[tid - kScW] = (int8_t)region_row(L, ty0 - 1 + tid - kScW);
-    if (tid == 0) cnt = 0;
-    __syncthreads();
-    const uint8_t* im = reinterpret_cast<const uint8_t*>(img32);
-    const int tpre = max(g.tmin, 1);
-    for (int p0 = 0; p0 < kScH * kScW; p0 += 256) {
-        const int p = p0 + tid;
-        bool ok = false;
-        if (p < kScH * kScW) {
-            const int sx = p % kScW - 1, sy = p / kScW - 1;
-            if (colCell[sx + 1] >= 0 && rowCell[sy + 1] >= 0) {
-                const int c = (sy + 4) * kImgW + sx + 4;
-                const int v = im[c];
-                const int q0 = im[c + 3 * kImgW], q4 = im[c + 3], q8 = im[c - 3 * kImgW], q12 = im[c - 3];
-                const unsigned dk = (unsigned)(q0 < v - tpre) | ((unsigned)(q4 < v - tpre) << 1) |
-                                    ((unsigned)(q8 < v - tpre) << 2) | ((unsigned)(q12 < v - tpre) << 3);
-                const unsigned br = (unsigned)(q0 > v + tpre) | ((unsigned)(q4 > v + tpre) << 1) |
-                                    ((unsigned)(q8 > v + tpre) << 2) | ((unsigned)(q12 > v + tpre) << 3);
-                const unsigned dk2 = dk & (((dk << 1) | (dk >> 3)) & 15u);
-                const unsigned br2 = br & (((br << 1) | (br >> 3)) & 15u);
-                ok = (dk2 | br2) != 0;
-            }
-        }
-        const uint64_t m = __ballot(ok);
-        int base = 0;
-        if (lane == 0 && m) base = atomicAdd(&cnt, __popcll(m));
-        base = __shfl(base, 0, 64);
-        if (ok) list[base + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)p;
-    }
-    __syncthreads();
-    const int n = cnt;
-    for (int k = tid; k < n; k += 256) {
-        const int p = list[k];
-        const int sx = p % kScW - 1, sy = p / kScW - 1;
-        const int cy = sy + 4, cx = sx + 4;
-        int q[16];
-        q[0] = im[(cy + 3) * kImgW + cx + 0];  q[1] = im[(cy + 3) * kImgW + cx + 1];
-        q[2] = im[(cy + 2) * kImgW + cx + 2];  q[3] = im[(cy + 1) * kImgW + cx + 3];
-        q[4] = im[(cy + 0) * kImgW + cx + 3];  q[5] = im[(cy - 1) * kImgW + cx + 3];
-        q[6] = im[(cy - 2) * kImgW + cx + 2];  q[7] = im[(cy - 3) * kImgW + cx + 1];
-        q[8] = im[(cy - 3) * kImgW + cx + 0];  q[9] = im[(cy - 3) * kImgW + cx - 1];
-        q[10] = im[(cy - 2) * kImgW + cx - 2]; q[11] = im[(cy - 1) * kImgW + cx - 3];
-        q[12] = im[(cy + 0) * kImgW + cx - 3]; q[13] = im[(cy + 1) * kImgW + cx - 3];
-        q[14] = im[(cy + 2) * kImgW + cx - 2]; q[15] = im[(cy + 3) * kImgW + cx - 1];
-        const int S = fast_score(im[cy * kImgW + cx], q);
-        sc[p] = (uint8_t)((S >= g.tmin && S > 0) ? S : 0);
-    }
-    __syncthreads();
-    uint8_t* o8 = reinterpret_cast<uint8_t*>(outT);
-    for (int k = tid; k < n; k += 256) {
-        const int p = list[k];
-        const int s = sc[p];
-        const int sx = p % kScW - 1, sy = p / kScW - 1;
-        if (s == 0 || sx < 0 || sx >= kTileW || sy < 0 || sy >= kTileH) continue;
-        const int cc = colCell[sx + 1], cr = rowCell[sy + 1];
-        int nb = 0;
-#pragma unroll
-        for (int dy = -1; dy <= 1; dy++) {
-#pragma unroll
-            for (int dx = -1; dx <= 1; dx++) {
-                if (dx == 0 && dy == 0) continue;
-                if (colCell[sx + 1 + dx] == cc && rowCell[sy + 1 + dy] == cr) nb = max(nb, (int)sc[p + dy * kScW + dx]);
-            }
-        }
-        if (s > nb) o8[sy * kTileW + sx] = (uint8_t)s;
-    }
-    __syncthreads();
-    const int ly = tid / 16, lx0 = (tid % 16) * 4;
-    const int y = ty0 + ly;
-    if (y < L.h && tx0 + lx0 < L.pitch)
-        *reinterpret_cast<uint32_t*>(out + (size_t)y * L.pitch + tx0 + lx0) = outT[tid];
-}
-
-// ------------------------------------------------------------------ A3: per-cell detect
-
-constexpr int kCellMax = 64;   // max region side handled in LDS (wCell, hCell <= 60 by construction)
-
-// One wave per FAST cell (R/src/ORBextractor.cpp:851-896): the cell's detection region of the
-// NMS map is staged in LDS; if no pixel reaches iniThFAST the cell falls back to minThFAST
-// (:879-883); keys are emitted in raster order, as cv::FAST returns them.
-__global__ __launch_bounds__(256) void k_cell_detect(Geom g, const uint8_t* __restrict__ nms,
-                                                     uint32_t* __restrict__ slots, int* __restrict__ cellCount,
-                                                     int* __restrict__ status) {
-    __shared__ uint8_t reg_all[4][kCellMax * kCellMax];
+// One wave per FAST cell (R/src/ORBextractor.cpp:851-896): cv::FAST on the cell's window,
+// restated without an intermediate score map.
+//  1. the window (detection region + 3-px ring margin) is staged in LDS, rows realigned so
+//     that region column 0 sits on a dword boundary;
+//  2. SWAR pre-test, 4 pixels per lane-task: ring pixels 0/4/8/12 (any 9-arc holds two adjacent
+//     ones) against the centre for 4 pixels at once, in 16-bit lanes (even / odd bytes) with a
+//     512 bias so no lane borrows from its neighbour; survivors are compacted (wave prefix);
+//  3. full score S (max over the 16 circular 9-arcs, min3/max3 form) for survivors only; the
+//     score buffer holds S >= tmin, 0 elsewhere (cv::FAST's non-corners);
+//  4. NMS of the scored pixels against their 8 neighbours; outside the region the window's
+//     FAST sees 0.  With non-corners at threshold t scoring 0, "S > every neighbour"
+//     does not depend on t (a neighbour >= S is a corner at t whenever S is), so both passes
+//     (iniThFAST, then minThFAST if the cell is empty, :879-883) read the same maxima;
+//  5. keys emitted in raster order, as cv::FAST returns them.
+__global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __restrict__ pyr,
+                                                   uint32_t* __restrict__ slots, int* __restrict__ cellCount,
+                                                   int* __restrict__ status, int maxW, int maxH) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int b = blockIdx.y;
     const int c = blockIdx.x * 4 + wid;
@@ -422,54 +318,169 @@ __global__ __launch_bounds__(256) void k_cell_detect(Geom g, const uint8_t* __re
         if (lane == 0) *cnt_out = 0;
         return;
     }
-    if (rw > kCellMax || rh > kCellMax) {
+    if (rw > maxW || rh > maxH || rw > 64) {
         if (lane == 0) { *cnt_out = 0; atomicOr(status, 1); }
         return;
     }
-    uint8_t* reg = reg_all[wid];
-    const uint8_t* sm = nms + (size_t)b * g.frameBytes + L.off;
+    const int PWS = fc_patch_stride(maxW), W32 = PWS >> 2;
+    unsigned char* base = dsm + (size_t)wid * fc_wave_bytes(maxW, maxH);
+    uint32_t* patch32 = reinterpret_cast<uint32_t*>(base);
+    const uint8_t* patch = base;
+    uint8_t* sc = base + (((maxH + 6) * PWS + 15) & ~15);
+    uint32_t* list = reinterpret_cast<uint32_t*>(sc + maxH * 64);   // y*64+x | kept score << 16
+    const uint8_t* img = pyr + (size_t)b * g.frameBytes + L.off;
     const int rx0 = iniX + 3, ry0 = iniY + 3;
-    const int np = rw * rh;
-    for (int p0 = 0; p0 < np; p0 += 64 * 8) {   // 8 loads in flight per lane
-        uint8_t v[8];
+
+    // 1. window rows ry0-3 .. ry0+rh+2, columns from rx0-4 (patch column 4 = region column 0)
+    {
+        const int gx0 = rx0 - 4, sh = gx0 & 3, ga = gx0 - sh;
+        const int NW = (rw + 8 + 3) >> 2;           // dwords per patch row
+        const int R = 64 / NW, k = lane % NW, r0 = lane / NW;
+        const int rows = rh + 6;
+        for (int rb = 0; rb < rows; rb += 4 * R) {
+            uint32_t a0[4], a1[4];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const int p = p0 + u * 64 + lane;
-            v[u] = p < np ? sm[(size_t)(ry0 + p / rw) * L.pitch + rx0 + p % rw] : 0;
+            for (int u = 0; u < 4; u++) {
+                const int r = rb + u * R + r0;
+                a0[u] = a1[u] = 0;
+                if (r0 < R && r < rows) {
+                    const uint8_t* src = img + (size_t)(ry0 - 3 + r) * L.pitch + ga + 4 * k;
+                    a0[u] = *reinterpret_cast<const uint32_t*>(src);
+                    a1[u] = *reinterpret_cast<const uint32_t*>(src + 4);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int r = rb + u * R + r0;
+                if (r0 < R && r < rows) patch32[r * W32 + k] = __builtin_amdgcn_alignbyte(a1[u], a0[u], sh);
+            }
         }
+        for (int q = lane; q < rh * 16; q += 64) reinterpret_cast<uint32_t*>(sc)[q] = 0u;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+
+    // 2. SWAR pre-test: task (row y, column group gq) covers region columns 4gq .. 4gq+3
+    const uint32_t tpre = (uint32_t)max(g.tmin, 1);
+    const uint32_t T1 = (tpre + 1u) * 0x00010001u;
+    int n = 0;
+    {
+        const int NG = (rw + 3) >> 2;
+        const int R = 64 / NG, gq = lane % NG, r0 = lane / NG;
+        for (int yb = 0; yb < rh; yb += R) {
+            const int y = yb + r0;
+            uint32_t want = 0;
+            if (r0 < R && y < rh) {
+                const int rowC = (y + 3) * W32 + gq + 1;   // dword holding region columns 4gq..4gq+3
+                const uint32_t cL = patch32[rowC - 1], cC = patch32[rowC], cR = patch32[rowC + 1];
+                const uint32_t pUp = patch32[rowC - 3 * W32], pDn = patch32[rowC + 3 * W32];
+                const uint32_t pRt = __builtin_amdgcn_alignbyte(cR, cC, 3);   // ring 4 (dx = +3)
+                const uint32_t pLt = __builtin_amdgcn_alignbyte(cC, cL, 1);   // ring 12 (dx = -3)
+                const uint32_t vE = __builtin_amdgcn_perm(0u, cC, 0x0c020c00u);
+                const uint32_t vO = __builtin_amdgcn_perm(0u, cC, 0x0c030c01u);
+                const uint32_t vEb = vE + 0x02000200u, vOb = vO + 0x02000200u;
+                const uint32_t vEt = vE + T1, vOt = vO + T1;
+                // dark: v > p + t <=> 512 + v - (p + t + 1) >= 512; bright: 512 + p - (v + t + 1) >= 512
+                auto flags = [&](uint32_t p, uint32_t& dk, uint32_t& br) {
+                    const uint32_t pE = __builtin_amdgcn_perm(0u, p, 0x0c020c00u);
+                    const uint32_t pO = __builtin_amdgcn_perm(0u, p, 0x0c030c01u);
+                    dk = ((vEb - (pE + T1)) & 0x02000200u) | (((vOb - (pO + T1)) & 0x02000200u) << 1);
+                    br = (((pE + 0x02000200u) - vEt) & 0x02000200u) | ((((pO + 0x02000200u) - vOt) & 0x02000200u) << 1);
+                };
+                uint32_t d0, b0, d4, b4, d8, b8, d12, b12;
+                flags(pDn, d0, b0);
+                flags(pRt, d4, b4);
+                flags(pUp, d8, b8);
+                flags(pLt, d12, b12);
+                const uint32_t pass = (d0 & d4) | (d4 & d8) | (d8 & d12) | (d12 & d0) | (b0 & b4) | (b4 & b8) |
+                                      (b8 & b12) | (b12 & b0);
+                // bits 9, 10, 25, 26 = columns 4gq .. 4gq+3
+                want = ((pass >> 9) & 3u) | ((pass >> 23) & 12u);
+                const int valid = rw - 4 * gq;   // columns of this group inside the region
+                if (valid < 4) want &= (1u << valid) - 1u;
+            }
+            const int cntW = __popc(want);
+            const int incl = wave_incl_scan_i32(cntW);
+            int pos = n + incl - cntW;
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const int p = p0 + u * 64 + lane;
-            if (p < np) reg[p] = v[u];
+            for (int kk = 0; kk < 4; kk++)
+                if (want & (1u << kk)) list[pos++] = (uint32_t)(y * 64 + 4 * gq + kk);
+            n += __shfl(incl, 63, 64);
         }
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    bool any = false;
-    for (int p0 = 0; p0 < np && !any; p0 += 64) {
-        const int p = p0 + lane;
-        const int v = p < np ? reg[p] : 0;
-        any = __ballot(v > 0 && v >= g.iniTh) != 0;
+
+    // 3. full score of the survivors.  The list is in raster order: lanes are row-major over
+    //    (row, column group) and each lane appends its group's columns in order.
+    for (int k = lane; k < n; k += 64) {
+        const int p = (int)list[k];
+        const int y = p >> 6, x = p & 63;
+        const int cc = (y + 3) * PWS + x + 4;
+        int q[16];
+        q[0] = patch[cc + 3 * PWS];      q[1] = patch[cc + 3 * PWS + 1];
+        q[2] = patch[cc + 2 * PWS + 2];  q[3] = patch[cc + PWS + 3];
+        q[4] = patch[cc + 3];            q[5] = patch[cc - PWS + 3];
+        q[6] = patch[cc - 2 * PWS + 2];  q[7] = patch[cc - 3 * PWS + 1];
+        q[8] = patch[cc - 3 * PWS];      q[9] = patch[cc - 3 * PWS - 1];
+        q[10] = patch[cc - 2 * PWS - 2]; q[11] = patch[cc - PWS - 3];
+        q[12] = patch[cc - 3];           q[13] = patch[cc + PWS - 3];
+        q[14] = patch[cc + 2 * PWS - 2]; q[15] = patch[cc + 3 * PWS - 1];
+        const int S = fast_score(patch[cc], q);
+        if (S >= g.tmin && S > 0) sc[y * 64 + x] = (uint8_t)S;
     }
-    const int t = any ? g.iniTh : g.minTh;
-    uint32_t* out = slots + (size_t)b * g.slotsPerFrame + L.slotBase + (size_t)ci * L.cellCap;
-    int n = 0;
-    for (int p0 = 0; p0 < np; p0 += 64) {
-        const int p = p0 + lane;
-        const int m = p < np ? reg[p] : 0;
-        const bool k = m > 0 && m >= t;
-        const uint64_t mask = __ballot(k);
-        const int before = __popcll(mask & ((1ull << lane) - 1ull));
-        if (k && n + before < L.cellCap) {
-            // DistributeOctTree coordinates: absolute - minBorder (R/src/ORBextractor.cpp:889-890)
-            const uint32_t kx = (uint32_t)(rx0 + p % rw - kMinBorder), ky = (uint32_t)(ry0 + p / rw - kMinBorder);
-            out[n + before] = kx | (ky << 12) | ((uint32_t)m << 24);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+
+    // 4. local maxima among the scored pixels (neighbours outside the region count as 0)
+    bool anyIni = false;
+    for (int k = lane; k < n; k += 64) {
+        const int p = (int)list[k] & 0xFFFF;
+        const int y = p >> 6, x = p & 63;
+        const int s = sc[p];
+        int keep = 0;
+        if (s > 0) {
+            int nb = 0;
+#pragma unroll
+            for (int dy = -1; dy <= 1; dy++) {
+#pragma unroll
+                for (int dx = -1; dx <= 1; dx++) {
+                    if (dx == 0 && dy == 0) continue;
+                    const int xx = x + dx, yy = y + dy;
+                    if (xx >= 0 && xx < rw && yy >= 0 && yy < rh) nb = max(nb, (int)sc[p + dy * 64 + dx]);
+                }
+            }
+            keep = s > nb ? s : 0;
         }
-        n += __popcll(mask);
+        list[k] = (uint32_t)p | ((uint32_t)keep << 16);
+        anyIni |= keep > 0 && keep >= g.iniTh;
+    }
+    anyIni = __ballot(anyIni) != 0;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+
+    // 5. keys at the cell's threshold, in raster order
+    const int t = anyIni ? g.iniTh : g.minTh;
+    uint32_t* out = slots + (size_t)b * g.slotsPerFrame + L.slotBase + (size_t)ci * L.cellCap;
+    int nk = 0;
+    for (int k0 = 0; k0 < n; k0 += 64) {
+        const int k = k0 + lane;
+        const uint32_t e = k < n ? list[k] : 0u;
+        const int keep = (int)(e >> 16);
+        const bool emit = keep > 0 && keep >= t;
+        const uint64_t mask = __ballot(emit);
+        const int before = __popcll(mask & ((1ull << lane) - 1ull));
+        if (emit && nk + before < L.cellCap) {
+            // DistributeOctTree coordinates: absolute - minBorder (R/src/ORBextractor.cpp:889-890)
+            const int p = (int)(e & 0xFFFFu);
+            const uint32_t kx = (uint32_t)(rx0 + (p & 63) - kMinBorder), ky = (uint32_t)(ry0 + (p >> 6) - kMinBorder);
+            out[nk + before] = kx | (ky << 12) | ((uint32_t)keep << 24);
+        }
+        nk += __popcll(mask);
     }
     if (lane == 0) {
-        if (n > L.cellCap) { atomicOr(status, 2); n = L.cellCap; }
-        *cnt_out = n;
+        if (nk > L.cellCap) { atomicOr(status, 2); nk = L.cellCap; }
+        *cnt_out = nk;
     }
 }
 
@@ -1331,8 +1342,8 @@ int check_device(int dev) {
 
 using namespace orbamd;
 
-// Pipeline stages timed by orb_extractor_stage_times(): resize, fast_score, cell_detect,
-// octree, blur, orient_desc.
+// Pipeline stages timed by orb_extractor_stage_times(): resize, fast (k_fast_cell), a reserved
+// stage (0 since FAST and the per-cell pass were fused), octree, blur, orient_desc.
 constexpr int kStages = 6;
 
 struct orb_extractor {
@@ -1344,7 +1355,7 @@ struct orb_extractor {
     int gw = -1, gh = -1;
     int blurK[4];
     size_t capFrames = 0, capFrameBytes = 0, capSlots = 0, capOut = 0, capCells = 0;
-    uint8_t *d_pyr = nullptr, *d_blur = nullptr, *d_score = nullptr;
+    uint8_t *d_pyr = nullptr, *d_blur = nullptr;
     uint32_t *d_slots = nullptr, *d_keyA = nullptr, *d_keyB = nullptr, *d_outKeys = nullptr;
     int *d_cellCount = nullptr, *d_levelCount = nullptr, *d_status = nullptr;
     // host-path outputs
@@ -1373,11 +1384,11 @@ static void free_dev(void* p) {
 }
 
 static void release_buffers(orb_extractor* ex) {
-    free_dev(ex->d_pyr); free_dev(ex->d_blur); free_dev(ex->d_score);
+    free_dev(ex->d_pyr); free_dev(ex->d_blur);
     free_dev(ex->d_slots); free_dev(ex->d_keyA); free_dev(ex->d_keyB); free_dev(ex->d_outKeys);
     free_dev(ex->d_cellCount); free_dev(ex->d_levelCount); free_dev(ex->d_status);
     free_dev(ex->d_kps); free_dev(ex->d_desc); free_dev(ex->d_counts);
-    ex->d_pyr = ex->d_blur = ex->d_score = nullptr;
+    ex->d_pyr = ex->d_blur = nullptr;
     ex->d_slots = ex->d_keyA = ex->d_keyB = ex->d_outKeys = nullptr;
     ex->d_cellCount = ex->d_levelCount = ex->d_status = nullptr;
     ex->d_kps = nullptr; ex->d_desc = nullptr; ex->d_counts = nullptr;
@@ -1409,7 +1420,6 @@ static int ensure_capacity(orb_extractor* ex, int B) {
     if (hipMalloc((void**)&(ptr), (bytes)) != hipSuccess) { release_buffers(ex); return ORB_ENOMEM; }
     ALLOC(ex->d_pyr, nb * fb);
     ALLOC(ex->d_blur, nb * fb);
-    ALLOC(ex->d_score, nb * fb);
     ALLOC(ex->d_slots, nb * sl * 4);
     ALLOC(ex->d_keyA, nb * sl * 4);
     ALLOC(ex->d_keyB, nb * sl * 4);
@@ -1429,7 +1439,6 @@ static int ensure_capacity(orb_extractor* ex, int B) {
     ex->capHostOut = ou;
     ORB_HIP_TRY(hipMemset(ex->d_pyr, 0, nb * fb));
     ORB_HIP_TRY(hipMemset(ex->d_blur, 0, nb * fb));
-    ORB_HIP_TRY(hipMemset(ex->d_score, 0, nb * fb));
     return ORB_OK;
 }
 
@@ -1481,10 +1490,14 @@ static int run_pipeline(orb_extractor* ex, int B, orb_keypoint* d_kps, uint8_t* 
         hipLaunchKernelGGL(k_resize, grid, block, 0, st, g, l, ex->d_pyr);
     }
     mark(1);
-    hipLaunchKernelGGL(k_fast_score, dim3(g.tilesPerFrame, B), dim3(256), 0, st, g, ex->d_pyr, ex->d_score);
+    {
+        // FAST + NMS + cell retry fused per cell (stage 1); stage 2 (the former separate
+        // cell pass) is empty
+        const size_t lds = 4 * (size_t)fc_wave_bytes(g.maxCellW, g.maxCellH);
+        hipLaunchKernelGGL(k_fast_cell, dim3((g.cellsPerFrame + 3) / 4, B), dim3(256), lds, st, g, ex->d_pyr,
+                           ex->d_slots, ex->d_cellCount, ex->d_status, g.maxCellW, g.maxCellH);
+    }
     mark(2);
-    hipLaunchKernelGGL(k_cell_detect, dim3((g.cellsPerFrame + 3) / 4, B), dim3(256), 0, st, g, ex->d_score,
-                       ex->d_slots, ex->d_cellCount, ex->d_status);
     mark(3);
     // LDS key buffers sized so that two workgroups still fit a CU (<= 80 KB each)
     const size_t ldsBase = octree_lds_bytes(g);
