@@ -29,8 +29,8 @@ import torch  # noqa: E402
 import pkgload  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md)
-STAGES = ["resize", "fast_detect", "reserved", "octree", "blur", "orient_desc"]
-KERNELS = ["k_resize", "k_fast_cell", None, "k_octree", "k_blur", "k_orient_desc"]
+STAGES = ["resize", "fast_detect", "reserved", "octree", "reserved2", "orient_blur_desc"]
+KERNELS = ["k_resize", "k_fast_cell", None, "k_octree", None, "k_orient_desc"]
 
 
 def parse():
@@ -60,14 +60,12 @@ def algorithmic_bytes(stage, lw, lh, n_pre, n_out):
     P = (lw.astype(np.int64) * lh).tolist()
     if stage == "resize":
         return sum(P[l - 1] + P[l] for l in range(1, len(P)))
-    if stage == "blur":
-        return 2 * sum(P)
     if stage == "fast_detect":
         return sum(P) + 4 * n_pre
     if stage == "octree":
         return 4 * (n_pre + n_out)
-    if stage == "orient_desc":
-        return n_out * (749 + 512 + 28 + 32)
+    if stage == "orient_blur_desc":
+        return n_out * (43 * 43 + 28 + 32)   # raw 43x43 window per keypoint in, keypoint + descriptor out
     raise KeyError(stage)
 
 
@@ -307,7 +305,7 @@ def main():
                               "traffic": None,
                               "launch_ms": round(float(per_launch_ms[dom]), 4)}
         result["stage_ms_per_batch"] = {k: round(float(v), 4) for k, v in zip(STAGES, per_launch_ms)
-                                        if k != "reserved"}
+                                        if not k.startswith("reserved")}
     if not args.no_lba:
         result["lba"] = bench_lba(args, amd, dev, local, rank, world)
     if rank == 0 and not args.no_cpu:

@@ -92,14 +92,16 @@ int orb_extract_batch_device(orb_extractor* ex, const uint8_t* d_imgs, size_t im
 int orb_pyramid_level(orb_extractor* ex, int frame, int level, const uint8_t** host, int* w,
                       int* h, size_t* stride);
 
-/* Device pointer of the blurred or raw level (for on-device consumers). */
+/* Device pointer of the blurred or raw level (for on-device consumers).  The
+ * blurred pyramid is computed on the first such request after an extraction
+ * (the extraction itself evaluates the Gaussian only where descriptors sample). */
 int orb_pyramid_level_device(orb_extractor* ex, int frame, int level, int blurred,
                              const uint8_t** dptr, int* w, int* h, size_t* pitch);
 
 /* Stage profiling: while enabled, every extraction records HIP events on its
  * launch stream around the six kernel stages (0 resize, 1 FAST detection per
  * cell incl. NMS and the minThFAST retry, 2 reserved (always 0), 3 octree,
- * 4 blur, 5 orient_desc).  orb_extractor_stage_times
+ * 4 reserved (always 0), 5 orientation + Gaussian + descriptor).  orb_extractor_stage_times
  * waits for them, writes the summed milliseconds per stage to ms[0..n_stages)
  * and the number of profiled calls to *n_calls, then resets; returns the number
  * of stages. */

@@ -5,8 +5,9 @@
 //                     iniThFAST / minThFAST retry, raster-order keys (R/src/ORBextractor.cpp:851-896)
 //   k_octree      A4  DistributeOctTree, phase-parallel emulation of the std::list algorithm
 //                     (R/src/ORBextractor.cpp:571-817), one workgroup per (frame, level)
-//   k_blur        A6  GaussianBlur 7x7 sigma 2 REFLECT_101 (8-bit fixed point)
-//   k_orient_desc A5+A7+A8  IC_Angle, steered BRIEF, output assembly, one wave per keypoint
+//   k_orient_desc A5+A6+A7+A8  IC_Angle, 7x7 Gaussian where the descriptor samples, steered
+//                     BRIEF, output assembly, one wave per keypoint
+//   k_blur        A6  full blurred pyramid, only on demand (orb_pyramid_level_device)
 // R/ = /root/reference/ORB-SLAM2注释版/.  All arithmetic follows the oracle's pinned
 // semantics (oracle/orb_oracle.c); this file is compiled with -ffp-contract=off.
 #include <hip/hip_runtime.h>
@@ -1221,11 +1222,26 @@ __device__ void glibc_sincosf(float y, float& s, float& c) {
     }
 }
 
+// Fused A5 + A6 + A7 + A8, one wave per retained keypoint (4 per workgroup):
+//  1. the raw level patch rows y-21..y+21, columns x-24..x+23 is staged in LDS (dword loads,
+//     realigned; BORDER_REFLECT_101 per byte for the few keypoints within 21 px of an edge);
+//  2. IC_Angle (R/src/ORBextractor.cpp:79-108) from the patch: per row and dword,
+//     v_dot4_u32_u8 against (u + 16) and 1 weights masked to |u| <= umax[|v|];
+//  3. the 7x7 Gaussian (8-bit kernel, R :1166-1167) only where the descriptor samples: the
+//     horizontal pass over the 43 x 37 window (two dot4 per output, u16 row sums <= 65535),
+//     the vertical pass per sample point — the same integer sums as the full-image filter;
+//  4. steered BRIEF (R :113-155) with glibc sincosf, 4 ballots -> 32 bytes.
+constexpr int kOdPW = 48;                // patch row stride (bytes): columns x-24 .. x+23
+constexpr int kOdRows = 43;              // rows y-21 .. y+21
+constexpr int kOdRsW = 40;               // row-sum stride (u16): columns x-18 .. x+18 (37 used)
+constexpr int kOdWaveBytes = kOdRows * kOdPW + kOdRows * kOdRsW * 2;
+
 __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __restrict__ pyr,
-                                                     const uint8_t* __restrict__ blurred,
                                                      const uint32_t* __restrict__ outKeys,
                                                      const int* __restrict__ levelCount, orb_keypoint* __restrict__ kps,
-                                                     uint8_t* __restrict__ desc, int cap, int32_t* __restrict__ counts) {
+                                                     uint8_t* __restrict__ desc, int cap, int32_t* __restrict__ counts,
+                                                     uint32_t kA, uint32_t kB) {
+    __shared__ __attribute__((aligned(16))) unsigned char od_sm[4][kOdWaveBytes];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int b = blockIdx.y;
     const int q = blockIdx.x * 4 + wid;
@@ -1246,37 +1262,110 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
     if (outIdx >= cap) return;
     const uint32_t key = outKeys[(size_t)b * g.outPerFrame + q];
     const int x = kx_of(key) + kMinBorder, y = ky_of(key) + kMinBorder, resp = kr_of(key);
-    // IC_Angle on the un-blurred level (R/src/ORBextractor.cpp:79-108)
     const uint8_t* img = pyr + (size_t)b * g.frameBytes + L.off;
-    const uint8_t* ctr = img + (size_t)y * L.pitch + x;
-    int m01 = 0, m10 = 0;
-    for (int t = lane; t < 31 * 31; t += 64) {
-        const int v = t / 31 - 15, u = t % 31 - 15;
-        if (abs(u) <= g.umax[abs(v)]) {
-            const int I = ctr[v * L.pitch + u];
-            m10 += u * I;
-            m01 += v * I;
+    uint32_t* P32 = reinterpret_cast<uint32_t*>(od_sm[wid]);
+    uint16_t* RS = reinterpret_cast<uint16_t*>(od_sm[wid] + kOdRows * kOdPW);
+
+    // 1. patch
+    if (x - 24 >= 0 && x + 24 <= L.w && y - 21 >= 0 && y + 21 < L.h) {
+        const int gx0 = x - 24, sh = gx0 & 3, ga = gx0 - sh;
+        for (int t0 = 0; t0 < kOdRows * 12; t0 += 64 * 4) {
+            uint32_t a0[4], a1[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int t = t0 + u * 64 + lane;
+                a0[u] = a1[u] = 0;
+                if (t < kOdRows * 12) {
+                    const uint8_t* src = img + (size_t)(y - 21 + t / 12) * L.pitch + ga + 4 * (t % 12);
+                    a0[u] = *reinterpret_cast<const uint32_t*>(src);
+                    a1[u] = *reinterpret_cast<const uint32_t*>(src + 4);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int t = t0 + u * 64 + lane;
+                if (t < kOdRows * 12) P32[t] = __builtin_amdgcn_alignbyte(a1[u], a0[u], sh);
+            }
+        }
+    } else {
+        uint8_t* P8w = od_sm[wid];
+        for (int t = lane; t < kOdRows * kOdPW; t += 64) {
+            const int r = t / kOdPW, cc = t % kOdPW;
+            P8w[t] = img[(size_t)reflect101(y - 21 + r, L.h) * L.pitch + reflect101(x - 24 + cc, L.w)];
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+
+    // 2. moments: lane = (row group vr, dword d); patch dword 2+d holds u = 4d-16 .. 4d-13
+    int m10 = 0, m01 = 0;
+    {
+        const int d = lane & 7, vr = lane >> 3;
+        for (int it = 0; it < 4; it++) {
+            const int v = it * 8 + vr - 15;
+            if (v > 15) continue;
+            const int um = g.umax[abs(v)];
+            uint32_t wu = 0, w1 = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int u = 4 * d + j - 16;
+                if (abs(u) <= um) {
+                    wu |= (uint32_t)(u + 16) << (8 * j);
+                    w1 |= 1u << (8 * j);
+                }
+            }
+            const uint32_t pw = P32[(21 + v) * 12 + 2 + d];
+            const int s1 = (int)__builtin_amdgcn_udot4(pw, w1, 0u, false);
+            m10 += (int)__builtin_amdgcn_udot4(pw, wu, 0u, false) - 16 * s1;
+            m01 += v * s1;
         }
     }
     m10 = wave_reduce_sum_i32(m10);
     m01 = wave_reduce_sum_i32(m01);
     const float angle = fast_atan2_dev((float)m01, (float)m10);
-    // steered BRIEF on the blurred level (R/src/ORBextractor.cpp:113-155)
+
+    // 3a. horizontal Gaussian pass: RS[r][c] = sum_q k_q * raw(y-21+r, x-18+c-3+q), c < 37.
+    //     Task (r, group gq) computes columns 4gq .. 4gq+3 from patch dwords gq .. gq+3.
+    for (int t = lane; t < kOdRows * 10; t += 64) {
+        const int r = t / 10, gq = t % 10;
+        const uint32_t* row = P32 + r * 12 + gq;
+        const uint32_t d0 = row[0], d1 = row[1], d2 = row[2], d3 = gq < 9 ? row[3] : 0u;
+        // output column 4gq+i reads patch bytes 4gq+i+3 .. 4gq+i+9
+        const uint32_t A0 = __builtin_amdgcn_alignbyte(d1, d0, 3), B0 = __builtin_amdgcn_alignbyte(d2, d1, 3);
+        const uint32_t A1 = d1, B1 = d2;
+        const uint32_t A2 = __builtin_amdgcn_alignbyte(d2, d1, 1), B2 = __builtin_amdgcn_alignbyte(d3, d2, 1);
+        const uint32_t A3 = __builtin_amdgcn_alignbyte(d2, d1, 2), B3 = __builtin_amdgcn_alignbyte(d3, d2, 2);
+        const uint32_t s0 = __builtin_amdgcn_udot4(B0, kB, __builtin_amdgcn_udot4(A0, kA, 0u, false), false);
+        const uint32_t s1 = __builtin_amdgcn_udot4(B1, kB, __builtin_amdgcn_udot4(A1, kA, 0u, false), false);
+        const uint32_t s2 = __builtin_amdgcn_udot4(B2, kB, __builtin_amdgcn_udot4(A2, kA, 0u, false), false);
+        const uint32_t s3 = __builtin_amdgcn_udot4(B3, kB, __builtin_amdgcn_udot4(A3, kA, 0u, false), false);
+        uint32_t* rs32 = reinterpret_cast<uint32_t*>(RS + r * kOdRsW + 4 * gq);
+        rs32[0] = s0 | (s1 << 16);
+        rs32[1] = s2 | (s3 << 16);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+
+    // 3b + 4. steered BRIEF: blurred(y+Y, x+X) = (sum_q k_q RS[Y+18+q][X+18] + 2^15) >> 16
     float bs, ac;
     glibc_sincosf(angle * g.factorPI, bs, ac);
     const float a = ac, bb = bs;
-    const uint8_t* bimg = blurred + (size_t)b * g.frameBytes + L.off;
-    const uint8_t* bc = bimg + (size_t)y * L.pitch + x;
-    const int step = L.pitch;
+    const int k0 = (int)(kA & 0xff), k1 = (int)((kA >> 8) & 0xff), k2 = (int)((kA >> 16) & 0xff),
+              k3 = (int)(kA >> 24);   // taps 0..3 (3 = centre); taps 4..6 mirror 2..0
+    auto sample = [&](float px, float py) -> int {
+        const int X = __float2int_rn(px * a - py * bb), Y = __float2int_rn(px * bb + py * a);
+        const uint16_t* c0 = RS + (Y + 18) * kOdRsW + X + 18;
+        const uint32_t acc = (uint32_t)(k0 * (c0[0] + c0[6 * kOdRsW]) + k1 * (c0[kOdRsW] + c0[5 * kOdRsW]) +
+                                        k2 * (c0[2 * kOdRsW] + c0[4 * kOdRsW]) + k3 * c0[3 * kOdRsW]);
+        return (int)min((acc + (1u << 15)) >> 16, 255u);
+    };
     uint64_t words[4];
 #pragma unroll
     for (int r = 0; r < 4; r++) {
         const int pi = r * 64 + lane;   // pair index: byte pi/8, bit pi%8
         const float x0 = (float)c_pattern[4 * pi], y0 = (float)c_pattern[4 * pi + 1];
         const float x1 = (float)c_pattern[4 * pi + 2], y1 = (float)c_pattern[4 * pi + 3];
-        const int t0 = bc[__float2int_rn(x0 * bb + y0 * a) * step + __float2int_rn(x0 * a - y0 * bb)];
-        const int t1 = bc[__float2int_rn(x1 * bb + y1 * a) * step + __float2int_rn(x1 * a - y1 * bb)];
-        words[r] = __ballot(t0 < t1);
+        words[r] = __ballot(sample(x0, y0) < sample(x1, y1));
     }
     if (lane < 4) {
         uint64_t wv = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
@@ -1342,8 +1431,8 @@ int check_device(int dev) {
 
 using namespace orbamd;
 
-// Pipeline stages timed by orb_extractor_stage_times(): resize, fast (k_fast_cell), a reserved
-// stage (0 since FAST and the per-cell pass were fused), octree, blur, orient_desc.
+// Pipeline stages timed by orb_extractor_stage_times(): resize, fast (k_fast_cell), reserved (0),
+// octree, reserved (0: the Gaussian runs inside k_orient_desc), orient_desc.
 constexpr int kStages = 6;
 
 struct orb_extractor {
@@ -1354,6 +1443,8 @@ struct orb_extractor {
     Geom g;                     // geometry of the last call
     int gw = -1, gh = -1;
     int blurK[4];
+    bool blurValid = false;          // d_blur holds the blurred pyramid of the last extraction
+    hipStream_t lastStream = nullptr;
     size_t capFrames = 0, capFrameBytes = 0, capSlots = 0, capOut = 0, capCells = 0;
     uint8_t *d_pyr = nullptr, *d_blur = nullptr;
     uint32_t *d_slots = nullptr, *d_keyA = nullptr, *d_keyB = nullptr, *d_outKeys = nullptr;
@@ -1507,12 +1598,19 @@ static int run_pipeline(orb_extractor* ex, int B, orb_keypoint* d_kps, uint8_t* 
     hipLaunchKernelGGL(k_octree, dim3(g.nlevels, B), dim3(OT_T), lds, st, g, ex->d_slots, ex->d_cellCount,
                        ex->d_keyA, ex->d_keyB, ex->d_outKeys, ex->d_levelCount, ex->d_status, keyCap);
     mark(4);
-    hipLaunchKernelGGL(k_blur, dim3(g.tilesPerFrame, B), dim3(256), 0, st, g, ex->d_pyr, ex->d_blur, ex->blurK[0],
-                       ex->blurK[1], ex->blurK[2], ex->blurK[3]);
+    // the Gaussian is evaluated inside k_orient_desc where the descriptor samples (stage 4 empty);
+    // the full blurred pyramid is produced on demand by orb_pyramid_level_device(blurred = 1)
     mark(5);
-    hipLaunchKernelGGL(k_orient_desc, dim3((g.outPerFrame + 3) / 4, B), dim3(256), 0, st, g, ex->d_pyr, ex->d_blur,
-                       ex->d_outKeys, ex->d_levelCount, d_kps, d_desc, cap, d_counts);
+    {
+        const int* k = ex->blurK;   // centre, +-1, +-2, +-3
+        const uint32_t kA = (uint32_t)k[3] | ((uint32_t)k[2] << 8) | ((uint32_t)k[1] << 16) | ((uint32_t)k[0] << 24);
+        const uint32_t kB = (uint32_t)k[1] | ((uint32_t)k[2] << 8) | ((uint32_t)k[3] << 16);
+        hipLaunchKernelGGL(k_orient_desc, dim3((g.outPerFrame + 3) / 4, B), dim3(256), 0, st, g, ex->d_pyr,
+                           ex->d_outKeys, ex->d_levelCount, d_kps, d_desc, cap, d_counts, kA, kB);
+    }
     mark(6);
+    ex->blurValid = false;
+    ex->lastStream = st;
     ORB_HIP_TRY(hipGetLastError());
     if (prof) ex->ev_sets.push_back(ev);
     return ORB_OK;
@@ -1696,6 +1794,15 @@ int orb_pyramid_level_device(orb_extractor* ex, int frame, int level, int blurre
         return ORB_EINVAL;
     const Geom& g = ex->g;
     const LevelGeom& L = g.lv[level];
+    if (blurred && !ex->blurValid && ex->lastB > 0) {
+        ORB_HIP_TRY(hipSetDevice(ex->device));
+        hipStream_t st = ex->lastStream ? ex->lastStream : ex->stream;
+        hipLaunchKernelGGL(k_blur, dim3(g.tilesPerFrame, ex->lastB), dim3(256), 0, st, g, ex->d_pyr, ex->d_blur,
+                           ex->blurK[0], ex->blurK[1], ex->blurK[2], ex->blurK[3]);
+        ORB_HIP_TRY(hipGetLastError());
+        ORB_HIP_TRY(hipStreamSynchronize(st));
+        ex->blurValid = true;
+    }
     const uint8_t* base = blurred ? ex->d_blur : ex->d_pyr;
     if (dptr) *dptr = base + (size_t)frame * g.frameBytes + L.off;
     if (w) *w = L.w;

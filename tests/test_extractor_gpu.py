@@ -57,6 +57,31 @@ def test_pyramid_matches_oracle(amd):
         assert np.array_equal(a, b), f"level {lvl}: {np.count_nonzero(a != b)} px differ"
 
 
+def test_blurred_pyramid_on_demand_matches_oracle(amd):
+    """orb_pyramid_level_device(blurred=1): the full GaussianBlur pyramid (k_blur, run on
+    demand) equals the oracle's per-level blur (REFLECT_101, 8-bit kernel)."""
+    import ctypes as C
+    from orb_slam2_amd import _abi
+    hip = C.CDLL("libamdhip64.so")
+    W, H = 640, 480
+    img = _frames(W, H, 0x5EED0003, 1)[0]
+    ex = amd.ORBextractor(1000, 1.2, 8, 20, 7, max_w=W, max_h=H)
+    ex(img)
+    ref = O.extract(O.params(1000), img, want_pyramid=True)
+    lw, lh = ref["sizes"]
+    off = 0
+    for lvl in range(8):
+        p, w, h, st = C.c_void_p(), C.c_int(), C.c_int(), C.c_size_t()
+        _abi.check("orb_pyramid_level_device", _abi.lib().orb_pyramid_level_device(
+            ex._h, 0, lvl, 1, C.byref(p), C.byref(w), C.byref(h), C.byref(st)))
+        buf = np.zeros((h.value, st.value), np.uint8)
+        assert hip.hipMemcpy(C.c_void_p(buf.ctypes.data), p, C.c_size_t(buf.nbytes), 2) == 0
+        a = buf[:, :w.value]
+        b = ref["blurred"][off:off + lw[lvl] * lh[lvl]].reshape(lh[lvl], lw[lvl])
+        off += lw[lvl] * lh[lvl]
+        assert np.array_equal(a, b), f"level {lvl}: {np.count_nonzero(a != b)} px differ"
+
+
 def test_empty_image_leaves_outputs(amd):
     ex = amd.ORBextractor(1000, 1.2, 8, 20, 7, max_w=640, max_h=480)
     sentinel = (np.zeros(3, np.uint8), np.ones((3, 32), np.uint8))
