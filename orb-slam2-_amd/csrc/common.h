@@ -41,6 +41,18 @@ __device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) {
     return v;
 }
 
+// Inclusive wave64 prefix sum with DPP row shifts and row broadcasts (gfx9: row_shr:1/2/4/8,
+// row_bcast:15 into rows 1 and 3, row_bcast:31 into rows 2 and 3) — VALU only, no LDS.
+__device__ __forceinline__ int wave_incl_scan_dpp(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);   // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);   // row_bcast:31
+    return v;
+}
+
 __device__ __forceinline__ int wave_incl_scan_i32(int v) {
     const int lane = threadIdx.x & 63;
 #pragma unroll

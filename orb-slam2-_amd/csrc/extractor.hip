@@ -21,6 +21,15 @@
 
 #include "common.h"
 
+#ifdef ORB_TIMING   // instrumented variant (tools/build_variant.py)
+#define TSTAMP(v) const long long v = clock64()
+#define TACC(acc, a) acc += clock64() - (a)
+#else
+#define TSTAMP(v)
+#define TACC(acc, a)
+#endif
+
+
 namespace orbamd {
 
 constexpr int kEdge = 19;          // EDGE_THRESHOLD
@@ -48,6 +57,7 @@ struct LevelGeom {
     float scale;          // mvScaleFactor[level]
     float size;           // (float)(int)(PATCH_SIZE * scale)
     double rsx, rsy;      // 1/((double)dst/src) for the resize producing this level
+    int rzX, rzY;         // offsets (uint2 units) of this level's resize column / row tables
     int tileBase, tilesX; // 64x16 tiles (score / blur kernels)
 };
 
@@ -201,42 +211,114 @@ __device__ __forceinline__ int reflect101(int i, int n) {
 
 // ------------------------------------------------------------------ A2: resize
 
-__global__ __launch_bounds__(256) void k_resize(Geom g, int l, uint8_t* __restrict__ pyr) {
+// One workgroup = 256 output columns x 16 output rows of level l; the source window is staged
+// in LDS with dword loads; each thread computes 4 columns x 4 rows, so the x coefficients
+// (cv::resize's fixed-point alpha, 11 fractional bits) are computed once per column.
+constexpr int kRzCols = 256, kRzRows = 16;
+
+// cv::resize INTER_LINEAR 8U coefficients of one destination column (x) or row (y): source
+// index pair and 11-bit weights, {i0 | i1 << 16, w0 | w1 << 16}.  Computed on the host with
+// the same IEEE float / double operations (build flags pin -ffp-contract=off on both sides).
+static void rz_coef_host(double rs, int d, int srcN, bool clampFrac, uint32_t out[2]) {
+    float f = (float)(((double)d + 0.5) * rs - 0.5);
+    int s0 = (int)std::floor(f);
+    f -= (float)s0;
+    if (clampFrac) {   // columns: cv::resize clamps the x index and zeroes the fraction
+        if (s0 < 0) { f = 0.f; s0 = 0; }
+        if (s0 >= srcN - 1) { f = 0.f; s0 = srcN - 1; }
+    }
+    const int w0 = (int)std::nearbyint((1.f - f) * 2048.f), w1 = (int)std::nearbyint(f * 2048.f);
+    int i0, i1;
+    if (clampFrac) {
+        i0 = s0;
+        i1 = std::min(s0 + 1, srcN - 1);
+    } else {           // rows: indices clamped, weights kept
+        i0 = std::min(std::max(s0, 0), srcN - 1);
+        i1 = std::min(std::max(s0 + 1, 0), srcN - 1);
+    }
+    out[0] = (uint32_t)i0 | ((uint32_t)i1 << 16);
+    out[1] = (uint32_t)w0 | ((uint32_t)w1 << 16);
+}
+
+__global__ __launch_bounds__(256) void k_resize(Geom g, int l, uint8_t* __restrict__ pyr, const uint2* __restrict__ rztab,
+                                                int srcW32, int srcRows) {
+    extern __shared__ uint32_t rz[];   // [srcRows][srcW32] source window
     const LevelGeom& D = g.lv[l];
     const LevelGeom& S = g.lv[l - 1];
-    const int b = blockIdx.z;
-    const int dy = blockIdx.y * 4 + threadIdx.y;
-    const int dx0 = (blockIdx.x * 64 + threadIdx.x) * 4;
-    if (dy >= D.h || dx0 >= D.w) return;
+    const int b = blockIdx.z, tid = threadIdx.x;
+    const int X0 = blockIdx.x * kRzCols, Y0 = blockIdx.y * kRzRows;
     const uint8_t* src = pyr + (size_t)b * g.frameBytes + S.off;
     uint8_t* dst = pyr + (size_t)b * g.frameBytes + D.off;
-    float fy = (float)(((double)dy + 0.5) * D.rsy - 0.5);
-    int sy = (int)floorf(fy);
-    fy -= (float)sy;
-    const int b0 = __float2int_rn((1.f - fy) * 2048.f), b1 = __float2int_rn(fy * 2048.f);
-    const int y0 = min(max(sy, 0), S.h - 1), y1 = min(max(sy + 1, 0), S.h - 1);
-    const uint8_t* S0 = src + (size_t)y0 * S.pitch;
-    const uint8_t* S1 = src + (size_t)y1 * S.pitch;
-    uint32_t packed = 0;
+    const uint2* XT = rztab + D.rzX;
+    const uint2* YT = rztab + D.rzY;
+    // source window of the block (indices are monotonic in the destination coordinate)
+    const int sxLo = (int)(XT[X0].x & 0xFFFF), sxHi = (int)(XT[min(X0 + kRzCols - 1, D.w - 1)].x >> 16);
+    const int yLo = (int)(YT[Y0].x & 0xFFFF), yHi = (int)(YT[min(Y0 + kRzRows - 1, D.h - 1)].x >> 16);
+    const int cA = sxLo & ~3;
+    const int words = (sxHi - cA) / 4 + 1, rows = yHi - yLo + 1;
+    const bool staged = words <= srcW32 && rows <= srcRows;
+    if (staged) {
+        // (row, word) walk without per-element division: step 256 = dq rows + dr words
+        const int dq = 256 / words, dr = 256 - dq * words;
+        int r = tid / words, wq = tid - r * words;
+        while (r < rows) {   // 8 loads in flight per thread before the LDS stores
+            uint32_t v[8];
+            int rr[8], ww[8];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int dx = dx0 + k;
-        if (dx < D.w) {
-            float fx = (float)(((double)dx + 0.5) * D.rsx - 0.5);
-            int sx = (int)floorf(fx);
-            fx -= (float)sx;
-            if (sx < 0) { fx = 0.f; sx = 0; }
-            if (sx >= S.w - 1) { fx = 0.f; sx = S.w - 1; }
-            const int a0 = __float2int_rn((1.f - fx) * 2048.f), a1 = __float2int_rn(fx * 2048.f);
-            const int sx1 = min(sx + 1, S.w - 1);
-            const int r0 = S0[sx] * a0 + S0[sx1] * a1;
-            const int r1 = S1[sx] * a0 + S1[sx1] * a1;
-            int v = (r0 * b0 + r1 * b1 + (1 << 21)) >> 22;
-            v = min(max(v, 0), 255);
-            packed |= (uint32_t)v << (8 * k);
+            for (int u = 0; u < 8; u++) {
+                rr[u] = r;
+                ww[u] = wq;
+                v[u] = r < rows ? *reinterpret_cast<const uint32_t*>(src + (size_t)(yLo + r) * S.pitch + cA + 4 * wq) : 0u;
+                r += dq;
+                wq += dr;
+                if (wq >= words) { wq -= words; r++; }
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (rr[u] < rows) rz[rr[u] * srcW32 + ww[u]] = v[u];
         }
     }
-    *reinterpret_cast<uint32_t*>(dst + (size_t)dy * D.pitch + dx0) = packed;
+    __syncthreads();
+    const int cx = tid & 63, ry = tid >> 6;
+    const int dx0 = X0 + 4 * cx;
+    if (dx0 >= D.w) return;
+    int lx0[4], lx1[4], a0[4], a1[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint2 c = XT[min(dx0 + k, D.w - 1)];
+        lx0[k] = (int)(c.x & 0xFFFF) - cA;
+        lx1[k] = (int)(c.x >> 16) - cA;
+        a0[k] = (int)(c.y & 0xFFFF);
+        a1[k] = (int)(c.y >> 16);
+    }
+    const uint8_t* win = reinterpret_cast<const uint8_t*>(rz);
+    for (int r = 0; r < 4; r++) {
+        const int dy = Y0 + ry * 4 + r;
+        if (dy >= D.h) break;
+        const uint2 c = YT[dy];
+        const int y0 = (int)(c.x & 0xFFFF), y1 = (int)(c.x >> 16), b0 = (int)(c.y & 0xFFFF), b1 = (int)(c.y >> 16);
+        const uint8_t *R0, *R1;
+        int o0 = 0;
+        if (staged) {
+            R0 = win + (size_t)(y0 - yLo) * srcW32 * 4;
+            R1 = win + (size_t)(y1 - yLo) * srcW32 * 4;
+        } else {
+            R0 = src + (size_t)y0 * S.pitch;
+            R1 = src + (size_t)y1 * S.pitch;
+            o0 = cA;
+        }
+        uint32_t packed = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int v0 = R0[o0 + lx0[k]] * a0[k] + R0[o0 + lx1[k]] * a1[k];
+            const int v1 = R1[o0 + lx0[k]] * a0[k] + R1[o0 + lx1[k]] * a1[k];
+            const uint32_t v = min((uint32_t)(v0 * b0 + v1 * b1 + (1 << 21)) >> 22, 255u);
+            packed |= v << (8 * k);
+        }
+        const int valid = D.w - dx0;   // pitch padding stays 0
+        if (valid < 4) packed &= (1u << (8 * valid)) - 1u;
+        *reinterpret_cast<uint32_t*>(dst + (size_t)dy * D.pitch + dx0) = packed;
+    }
 }
 
 // ------------------------------------------------------------------ A3: FAST score
@@ -270,11 +352,13 @@ constexpr int kTileW = 64, kTileH = 16;   // blur tiles
 
 // Per-wave LDS of k_fast_cell for regions up to maxW x maxH (host and device agree on it).
 __host__ __device__ inline int fc_patch_stride(int maxW) { return ((maxW + 8 + 3) & ~3) + 4; }
+__host__ __device__ inline int fc_score_stride(int maxW) { return maxW <= 32 ? 32 : 64; }
 __host__ __device__ inline int fc_wave_bytes(int maxW, int maxH) {
-    const int patch = (maxH + 6) * fc_patch_stride(maxW);
-    const int sc = maxH * 64;
-    const int list = maxW * maxH * 4;
-    return ((patch + 15) & ~15) + sc + list;
+    const int patch = ((maxH + 6) * fc_patch_stride(maxW) + 15) & ~15;
+    const int sc = (maxH * fc_score_stride(maxW) + 15) & ~15;
+    const int list = (maxW * maxH * 2 + 15) & ~15;   // u16 y*64+x of the pre-test survivors
+    const int keep = (maxW * maxH + 15) & ~15;       // u8 suppressed score per survivor
+    return patch + sc + list + keep;
 }
 
 // One wave per FAST cell (R/src/ORBextractor.cpp:851-896): cv::FAST on the cell's window,
@@ -294,6 +378,7 @@ __host__ __device__ inline int fc_wave_bytes(int maxW, int maxH) {
 __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __restrict__ pyr,
                                                    uint32_t* __restrict__ slots, int* __restrict__ cellCount,
                                                    int* __restrict__ status, int maxW, int maxH) {
+    TSTAMP(t_fc0);
     extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int b = blockIdx.y;
@@ -323,43 +408,45 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
         if (lane == 0) { *cnt_out = 0; atomicOr(status, 1); }
         return;
     }
-    const int PWS = fc_patch_stride(maxW), W32 = PWS >> 2;
+    const int PWS = fc_patch_stride(maxW), W32 = PWS >> 2, SCS = fc_score_stride(maxW);
     unsigned char* base = dsm + (size_t)wid * fc_wave_bytes(maxW, maxH);
     uint32_t* patch32 = reinterpret_cast<uint32_t*>(base);
     const uint8_t* patch = base;
     uint8_t* sc = base + (((maxH + 6) * PWS + 15) & ~15);
-    uint32_t* list = reinterpret_cast<uint32_t*>(sc + maxH * 64);   // y*64+x | kept score << 16
+    uint16_t* list = reinterpret_cast<uint16_t*>(sc + ((maxH * SCS + 15) & ~15));
+    uint8_t* kp = reinterpret_cast<uint8_t*>(list) + ((maxW * maxH * 2 + 15) & ~15);
     const uint8_t* img = pyr + (size_t)b * g.frameBytes + L.off;
     const int rx0 = iniX + 3, ry0 = iniY + 3;
 
-    // 1. window rows ry0-3 .. ry0+rh+2, columns from rx0-4 (patch column 4 = region column 0)
+    // 1. window rows ry0-3 .. ry0+rh+2, columns from rx0-4 (patch column 4 = region column 0):
+    //    lane (row r0 + R*u, dword k) loads one aligned dword, all loads in flight at once; the
+    //    realigned dword takes its upper bytes from the next lane (next dword of the row)
     {
         const int gx0 = rx0 - 4, sh = gx0 & 3, ga = gx0 - sh;
         const int NW = (rw + 8 + 3) >> 2;           // dwords per patch row
-        const int R = 64 / NW, k = lane % NW, r0 = lane / NW;
+        const int NW1 = NW + 1;                     // aligned source dwords per row
+        const int R = 64 / NW1, k = lane % NW1, r0 = lane / NW1;
         const int rows = rh + 6;
-        for (int rb = 0; rb < rows; rb += 4 * R) {
-            uint32_t a0[4], a1[4];
+        for (int rb = 0; rb < rows; rb += 8 * R) {
+            uint32_t a[8];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
+            for (int u = 0; u < 8; u++) {
                 const int r = rb + u * R + r0;
-                a0[u] = a1[u] = 0;
-                if (r0 < R && r < rows) {
-                    const uint8_t* src = img + (size_t)(ry0 - 3 + r) * L.pitch + ga + 4 * k;
-                    a0[u] = *reinterpret_cast<const uint32_t*>(src);
-                    a1[u] = *reinterpret_cast<const uint32_t*>(src + 4);
-                }
+                a[u] = (r0 < R && r < rows) ? *reinterpret_cast<const uint32_t*>(img + (size_t)(ry0 - 3 + r) * L.pitch + ga + 4 * k)
+                                            : 0u;
             }
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
+            for (int u = 0; u < 8; u++) {
+                const uint32_t nx = __shfl_down(a[u], 1, 64);
                 const int r = rb + u * R + r0;
-                if (r0 < R && r < rows) patch32[r * W32 + k] = __builtin_amdgcn_alignbyte(a1[u], a0[u], sh);
+                if (r0 < R && r < rows && k < NW) patch32[r * W32 + k] = __builtin_amdgcn_alignbyte(nx, a[u], sh);
             }
         }
-        for (int q = lane; q < rh * 16; q += 64) reinterpret_cast<uint32_t*>(sc)[q] = 0u;
+        for (int q = lane; q < rh * SCS / 4; q += 64) reinterpret_cast<uint32_t*>(sc)[q] = 0u;
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    TSTAMP(t_fc1);
 
     // 2. SWAR pre-test: task (row y, column group gq) covers region columns 4gq .. 4gq+3
     const uint32_t tpre = (uint32_t)max(g.tmin, 1);
@@ -401,21 +488,22 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
                 if (valid < 4) want &= (1u << valid) - 1u;
             }
             const int cntW = __popc(want);
-            const int incl = wave_incl_scan_i32(cntW);
+            const int incl = wave_incl_scan_dpp(cntW);
             int pos = n + incl - cntW;
 #pragma unroll
             for (int kk = 0; kk < 4; kk++)
-                if (want & (1u << kk)) list[pos++] = (uint32_t)(y * 64 + 4 * gq + kk);
+                if (want & (1u << kk)) list[pos++] = (uint16_t)(y * 64 + 4 * gq + kk);
             n += __shfl(incl, 63, 64);
         }
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 
+    TSTAMP(t_fc2);
     // 3. full score of the survivors.  The list is in raster order: lanes are row-major over
     //    (row, column group) and each lane appends its group's columns in order.
     for (int k = lane; k < n; k += 64) {
-        const int p = (int)list[k];
+        const int p = list[k];
         const int y = p >> 6, x = p & 63;
         const int cc = (y + 3) * PWS + x + 4;
         int q[16];
@@ -428,17 +516,19 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
         q[12] = patch[cc - 3];           q[13] = patch[cc + PWS - 3];
         q[14] = patch[cc + 2 * PWS - 2]; q[15] = patch[cc + 3 * PWS - 1];
         const int S = fast_score(patch[cc], q);
-        if (S >= g.tmin && S > 0) sc[y * 64 + x] = (uint8_t)S;
+        if (S >= g.tmin && S > 0) sc[y * SCS + x] = (uint8_t)S;
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 
+    TSTAMP(t_fc3);
     // 4. local maxima among the scored pixels (neighbours outside the region count as 0)
     bool anyIni = false;
     for (int k = lane; k < n; k += 64) {
-        const int p = (int)list[k] & 0xFFFF;
+        const int p = list[k];
         const int y = p >> 6, x = p & 63;
-        const int s = sc[p];
+        const int si = y * SCS + x;
+        const int s = sc[si];
         int keep = 0;
         if (s > 0) {
             int nb = 0;
@@ -448,32 +538,32 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
                 for (int dx = -1; dx <= 1; dx++) {
                     if (dx == 0 && dy == 0) continue;
                     const int xx = x + dx, yy = y + dy;
-                    if (xx >= 0 && xx < rw && yy >= 0 && yy < rh) nb = max(nb, (int)sc[p + dy * 64 + dx]);
+                    if (xx >= 0 && xx < rw && yy >= 0 && yy < rh) nb = max(nb, (int)sc[si + dy * SCS + dx]);
                 }
             }
             keep = s > nb ? s : 0;
         }
-        list[k] = (uint32_t)p | ((uint32_t)keep << 16);
+        kp[k] = (uint8_t)keep;
         anyIni |= keep > 0 && keep >= g.iniTh;
     }
     anyIni = __ballot(anyIni) != 0;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 
+    TSTAMP(t_fc4);
     // 5. keys at the cell's threshold, in raster order
     const int t = anyIni ? g.iniTh : g.minTh;
     uint32_t* out = slots + (size_t)b * g.slotsPerFrame + L.slotBase + (size_t)ci * L.cellCap;
     int nk = 0;
     for (int k0 = 0; k0 < n; k0 += 64) {
         const int k = k0 + lane;
-        const uint32_t e = k < n ? list[k] : 0u;
-        const int keep = (int)(e >> 16);
+        const int keep = k < n ? (int)kp[k] : 0;
         const bool emit = keep > 0 && keep >= t;
         const uint64_t mask = __ballot(emit);
         const int before = __popcll(mask & ((1ull << lane) - 1ull));
         if (emit && nk + before < L.cellCap) {
             // DistributeOctTree coordinates: absolute - minBorder (R/src/ORBextractor.cpp:889-890)
-            const int p = (int)(e & 0xFFFFu);
+            const int p = list[k];
             const uint32_t kx = (uint32_t)(rx0 + (p & 63) - kMinBorder), ky = (uint32_t)(ry0 + (p >> 6) - kMinBorder);
             out[nk + before] = kx | (ky << 12) | ((uint32_t)keep << 24);
         }
@@ -483,17 +573,14 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
         if (nk > L.cellCap) { atomicOr(status, 2); nk = L.cellCap; }
         *cnt_out = nk;
     }
+#ifdef ORB_TIMING
+    if (lane == 0 && b == 0 && (c == 0 || c == 100 || c == 500))
+        printf("fast_cell c%d rw %d rh %d n %d keys %d: load %lld pretest %lld score %lld nms %lld emit %lld\n", c, rw, rh,
+               n, nk, t_fc1 - t_fc0, t_fc2 - t_fc1, t_fc3 - t_fc2, t_fc4 - t_fc3, clock64() - t_fc4);
+#endif
 }
 
 // ------------------------------------------------------------------ A4: octree
-
-#ifdef ORB_TIMING   // instrumented variant (tools/build_variant.py)
-#define TSTAMP(v) const long long v = clock64()
-#define TACC(acc, a) acc += clock64() - (a)
-#else
-#define TSTAMP(v)
-#define TACC(acc, a)
-#endif
 
 constexpr int OT_T = 256;
 constexpr int OT_V = 8;
@@ -1443,6 +1530,7 @@ struct orb_extractor {
     Geom g;                     // geometry of the last call
     int gw = -1, gh = -1;
     int blurK[4];
+    uint2* d_rztab = nullptr;        // resize coefficient tables of the current geometry
     bool blurValid = false;          // d_blur holds the blurred pyramid of the last extraction
     hipStream_t lastStream = nullptr;
     size_t capFrames = 0, capFrameBytes = 0, capSlots = 0, capOut = 0, capCells = 0;
@@ -1491,6 +1579,29 @@ static int ensure_geom(orb_extractor* ex, int w, int h) {
     Geom g;
     int st = build_geom(ex->p, w, h, &g);
     if (st) return st;
+    // resize coefficient tables (per level: destination columns, then rows)
+    std::vector<uint2> tab;
+    for (int l = 1; l < g.nlevels; l++) {
+        LevelGeom& L = g.lv[l];
+        const LevelGeom& S = g.lv[l - 1];
+        L.rzX = (int)tab.size();
+        for (int x = 0; x < L.w; x++) {
+            uint32_t c[2];
+            rz_coef_host(L.rsx, x, S.w, true, c);
+            tab.push_back(make_uint2(c[0], c[1]));
+        }
+        L.rzY = (int)tab.size();
+        for (int y = 0; y < L.h; y++) {
+            uint32_t c[2];
+            rz_coef_host(L.rsy, y, S.h, false, c);
+            tab.push_back(make_uint2(c[0], c[1]));
+        }
+    }
+    ORB_HIP_TRY(hipSetDevice(ex->device));
+    if (ex->d_rztab) (void)hipFree(ex->d_rztab);
+    ex->d_rztab = nullptr;
+    if (hipMalloc((void**)&ex->d_rztab, std::max<size_t>(tab.size(), 1) * sizeof(uint2)) != hipSuccess) return ORB_ENOMEM;
+    ORB_HIP_TRY(hipMemcpy(ex->d_rztab, tab.data(), tab.size() * sizeof(uint2), hipMemcpyHostToDevice));
     ex->g = g;
     ex->gw = w;
     ex->gh = h;
@@ -1577,8 +1688,13 @@ static int run_pipeline(orb_extractor* ex, int B, orb_keypoint* d_kps, uint8_t* 
     mark(0);
     for (int l = 1; l < g.nlevels; l++) {
         const LevelGeom& L = g.lv[l];
-        dim3 grid((L.w + 255) / 256, (L.h + 3) / 4, B), block(64, 4);
-        hipLaunchKernelGGL(k_resize, grid, block, 0, st, g, l, ex->d_pyr);
+        // source window bound of one 256 x 16 block: ceil(256 * rsx) + 2 columns (+3 for dword
+        // alignment), ceil(16 * rsy) + 2 rows
+        const int srcW32 = (int)std::ceil(kRzCols * L.rsx) / 4 + 3;
+        const int srcRows = (int)std::ceil(kRzRows * L.rsy) + 3;
+        dim3 grid((L.w + kRzCols - 1) / kRzCols, (L.h + kRzRows - 1) / kRzRows, B);
+        hipLaunchKernelGGL(k_resize, grid, dim3(256), (size_t)srcW32 * srcRows * 4, st, g, l, ex->d_pyr, ex->d_rztab,
+                           srcW32, srcRows);
     }
     mark(1);
     {
@@ -1664,6 +1780,7 @@ void orb_extractor_destroy(orb_extractor* ex) {
     (void)hipSetDevice(ex->device);
     if (ex->stream) (void)hipStreamSynchronize(ex->stream);
     release_buffers(ex);
+    if (ex->d_rztab) (void)hipFree(ex->d_rztab);
     for (auto& set : ex->ev_sets)
         for (auto e : set) ex->ev_pool.push_back(e);
     for (auto e : ex->ev_pool) (void)hipEventDestroy(e);

@@ -362,8 +362,9 @@ __global__ __launch_bounds__(64) void k_resolve_sfi(const orb_keypoint* __restri
                                                     int32_t* __restrict__ matches12, int32_t* __restrict__ nmatches_out) {
     TSTAMP(t_begin);
     long long tStage = 0, tLoop = 0;
-    int nFall = 0, nAct = 0, nMatch = 0;
-    (void)tStage; (void)tLoop; (void)nFall; (void)nAct; (void)nMatch;
+    int nFall = 0, nAct = 0, nMatch = 0, nBatch = 0;
+    long long tFall = 0, tA = 0, tB = 0;
+    (void)tStage; (void)tLoop; (void)nFall; (void)nAct; (void)nMatch; (void)nBatch; (void)tFall; (void)tA; (void)tB;
     extern __shared__ __attribute__((aligned(16))) int sm[];
     const int lane = threadIdx.x;
     const int b = blockIdx.x;
@@ -405,6 +406,12 @@ __global__ __launch_bounds__(64) void k_resolve_sfi(const orb_keypoint* __restri
     int* qidx = hcount + 32;                       // [kRange]
     int* qnc = qidx + kRange;                      // [kRange]
     uint32_t* qtk = (uint32_t*)(qnc + kRange);     // [kRange * kTopK]
+    int* bq = (int*)(qtk + kRange * kTopK);        // [8] per-batch decisions: keypoint (or -1)
+    int* dq = bq + 8;                              // [8] and distance
+#ifdef ORB_TIMING
+    int* nMatchL = dq + 8;
+    if (lane == 0) nMatchL[0] = 0;
+#endif
     const int myK = lane & (kTopK - 1);
     TSTAMP(t_init);
     for (int r0 = 0; r0 < n1; r0 += kRange) {
@@ -446,101 +453,135 @@ __global__ __launch_bounds__(64) void k_resolve_sfi(const orb_keypoint* __restri
         wave_lds_sync();
         TACC(tStage, t_r0);
         TSTAMP(t_l0);
-        // Eight queries at a time: lane 8q+k probes vMatchedDistance for the k-th preferred
-        // candidate of query a0+q in one LDS gather; the queries are then decided in order from
-        // the ballot, and a match clears the probe bits of later queries of the batch that
-        // see the same keypoint at a distance >= the new vMatchedDistance.
-        for (int a0 = 0; a0 < na; a0 += 8) {
-            const int a = a0 + (lane >> 3);
+        // Eight queries at a time, decided in parallel: lane 8q+k probes vMatchedDistance for
+        // the k-th preferred candidate of query a0+q (one LDS gather), every query takes its
+        // first / second surviving candidate from the ballot.  A decision stands unless an
+        // earlier query of the same batch matched one of its candidates up to its second
+        // survivor at a distance <= its own (that candidate would now be skipped); the batch
+        // commits up to the first such query (or the first needing a full-list rescan) and
+        // the next batch starts there, so every commit sees exactly the sequential state.
+        int a0 = 0;
+        while (a0 < na) {
+            TSTAMP(t_b0);
+#ifdef ORB_TIMING
+            nBatch++;
+#endif
+            const int q = lane >> 3;
+            const int a = a0 + q;
             uint32_t e = ~0u;
             int nc = 0, qi = -1;
             if (a < na) { nc = qnc[a]; e = qtk[a * kTopK + myK]; qi = qidx[a]; }
             const int j = (int)(e & 0xFFFFFu), d = (int)(e >> 20);
             bool valid = false;
             if (a < na && myK < min(nc, kTopK)) valid = vMD[j] > d;   // `if(vMatchedDistance[i2]<=dist) continue;`
-            // per-lane float bits of (float)dist and of (float)dist * nnratio: for non-negative
-            // floats the ratio test `bestDist < (float)bestDist2*mfNNratio` is an unsigned compare
-            const float fd = (float)d;
-            const uint32_t fdb = __float_as_uint(fd), thrb = __float_as_uint(fd * nnratio);
-            uint64_t vm = __ballot(valid);
-            const uint64_t bigNc = __ballot(myK == 0 && nc > kTopK);
+            const uint64_t vm = __ballot(valid);
+            TACC(tA, t_b0);
+            TSTAMP(t_b1);
+            const uint32_t mk = (uint32_t)(vm >> (q * 8)) & 0xFFu;
+            const uint32_t mk2 = mk & (mk - 1u);
+            const int f = mk ? __ffs(mk) - 1 : 0, f2 = mk2 ? __ffs(mk2) - 1 : 0;
+            uint32_t e1 = 0u, e2 = 0u;
+            if (a < na) { e1 = qtk[a * kTopK + f]; e2 = qtk[a * kTopK + f2]; }
+            const int bestd = (int)(e1 >> 20), bi = (int)(e1 & 0xFFFFFu);
+            const int best2 = mk2 ? (int)(e2 >> 20) : INT_MAX;
+            const bool fallback = a < na && __popc(mk) < 2 && nc > kTopK;
+            const bool match = a < na && !fallback && mk != 0 && bestd <= kThLow &&
+                               (float)bestd < (float)best2 * nnratio;
+            // publish every query's decision (bi, dist; -1 = none) to its 8 lanes' peers via LDS
+            if (myK == 0) { bq[q] = match ? bi : -1; dq[q] = bestd; }
+            wave_lds_sync();
+            int qbi[8], qbd[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) { qbi[u] = bq[u]; qbd[u] = dq[u]; }
+            // conflicts: an earlier match of the batch on one of my candidates up to my second
+            // survivor, at a distance <= mine (it would now be skipped)
+            const int lim = mk2 ? f2 : kTopK - 1;
+            bool hit = false;
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                hit |= u < q && valid && myK <= lim && qbi[u] == j && qbd[u] <= d;
+            }
+            const uint64_t stop = __ballot(hit) | __ballot(fallback && myK == 0);
             const int qEnd = min(8, na - a0);
+            const int qs = stop ? min(qEnd, (__ffsll((unsigned long long)stop) - 1) >> 3) : qEnd;
 #ifdef ORB_TIMING
-            nAct += qEnd;
+            nAct += qs;
 #endif
-            for (int qq = 0; qq < qEnd; qq++) {
-                const uint32_t mk = (uint32_t)(vm >> (qq * 8)) & 0xFFu;
-                int bestd, bi;
-                uint32_t bestb, thr;
-                if (__popc(mk) >= 2 || ((bigNc >> (qq * 8)) & 1ull) == 0) {
-                    if (mk == 0) continue;
-                    const int l1 = qq * 8 + __ffs(mk) - 1;
-                    const uint32_t mk2 = mk & (mk - 1u);
-                    bestd = __builtin_amdgcn_readlane(d, l1);
-                    bi = __builtin_amdgcn_readlane(j, l1);
-                    bestb = __builtin_amdgcn_readlane(fdb, l1);
-                    thr = mk2 ? __builtin_amdgcn_readlane(thrb, qq * 8 + __ffs(mk2) - 1) : 0x7F800000u;
-                } else {
+            // commit queries < qs: every match records mt; vnMatches21 / vMatchedDistance take the
+            // last committed match of each keypoint (stealing within the batch)
+            if (myK == 0 && q < qs && match) {
 #ifdef ORB_TIMING
-                    nFall++;
+                atomicAdd(&nMatchL[0], 1);
 #endif
-                    // fewer than two of the top-K survive: rescan the query's whole list
-                    const int ncq = __builtin_amdgcn_readlane(nc, qq * 8);
-                    const int iq = __builtin_amdgcn_readlane(qi, qq * 8);
-                    const uint32_t* C = cand + ((size_t)b * cap + iq) * kMaxCand;
-                    Best2 acc;
-                    acc.best = INT_MAX; acc.best2 = INT_MAX; acc.idx = -1;
-                    unsigned accOrder = 0xFFFFFu;
-                    for (int c0 = 0; c0 < ncq; c0 += 64) {
-                        const int c = c0 + lane;
-                        bool ok = false;
-                        int dd = 0, jj = 0;
-                        unsigned order = 0;
-                        if (c < ncq) {
-                            const uint32_t ce = C[c];
-                            jj = (int)(ce & 0xFFFFFu);
-                            dd = (int)(ce >> 20);
-                            ok = vMD[jj] > dd;
-                            order = (unsigned)ckey[jj];
-                        }
-                        const Best2 r = wave_best2(dd, order, jj, ok);
-                        if (r.idx >= 0) {
-                            const unsigned rOrder = (unsigned)ckey[r.idx];
-                            const bool rFirst = (r.best < acc.best) ||
-                                                (r.best == acc.best && (rOrder < accOrder || (rOrder == accOrder && r.idx < acc.idx)));
-                            if (rFirst) {
-                                acc.best2 = min(acc.best, r.best2);
-                                acc.idx = r.idx;
-                                accOrder = rOrder;
-                                acc.best = r.best;
-                            } else {
-                                acc.best2 = min(acc.best2, r.best);
-                            }
-                        }
-                    }
-                    bi = __builtin_amdgcn_readfirstlane(acc.idx);
-                    if (bi < 0) continue;
-                    bestd = __builtin_amdgcn_readfirstlane(acc.best);
-                    const int b2 = __builtin_amdgcn_readfirstlane(acc.best2);
-                    bestb = __float_as_uint((float)bestd);
-                    thr = __float_as_uint((float)b2 * nnratio);
-                }
-                if (bestd <= kThLow && bestb < thr) {
-#ifdef ORB_TIMING
-                    nMatch++;
-#endif
-                    const int i1 = __builtin_amdgcn_readlane(qi, qq * 8);
-                    if (lane == 0) {
-                        v21[bi] = i1;
-                        vMD[bi] = bestd;
-                        mt[i1] = bi;
-                    }
-                    // later queries of the batch now see vMatchedDistance[bi] == bestd
-                    valid = valid && !(j == bi && bestd <= d);
-                    vm = __ballot(valid);
+                mt[qi] = bi;
+                bool sup = false;
+#pragma unroll
+                for (int u = 0; u < 8; u++) sup |= u > q && u < qs && qbi[u] == bi;
+                if (!sup) {
+                    v21[bi] = qi;
+                    vMD[bi] = bestd;
                 }
             }
             wave_lds_sync();
+            TACC(tB, t_b1);
+            if (qs < qEnd && ((stop >> (qs * 8)) & 1ull) && __builtin_amdgcn_readlane((int)fallback, qs * 8)) {
+                TSTAMP(t_f0);
+#ifdef ORB_TIMING
+                nFall++; nAct++;
+#endif
+                // fewer than two of the top-K survive: rescan the query's whole list
+                const int ncq = __builtin_amdgcn_readlane(nc, qs * 8);
+                const int iq = __builtin_amdgcn_readlane(qi, qs * 8);
+                const uint32_t* C = cand + ((size_t)b * cap + iq) * kMaxCand;
+                Best2 acc;
+                acc.best = INT_MAX; acc.best2 = INT_MAX; acc.idx = -1;
+                unsigned accOrder = 0xFFFFFu;
+                for (int c0 = 0; c0 < ncq; c0 += 64) {
+                    const int c = c0 + lane;
+                    bool ok = false;
+                    int dd = 0, jj = 0;
+                    unsigned order = 0;
+                    if (c < ncq) {
+                        const uint32_t ce = C[c];
+                        jj = (int)(ce & 0xFFFFFu);
+                        dd = (int)(ce >> 20);
+                        ok = vMD[jj] > dd;
+                        order = (unsigned)ckey[jj];
+                    }
+                    const Best2 r = wave_best2(dd, order, jj, ok);
+                    if (r.idx >= 0) {
+                        const unsigned rOrder = (unsigned)ckey[r.idx];
+                        const bool rFirst = (r.best < acc.best) ||
+                                            (r.best == acc.best && (rOrder < accOrder || (rOrder == accOrder && r.idx < acc.idx)));
+                        if (rFirst) {
+                            acc.best2 = min(acc.best, r.best2);
+                            acc.idx = r.idx;
+                            accOrder = rOrder;
+                            acc.best = r.best;
+                        } else {
+                            acc.best2 = min(acc.best2, r.best);
+                        }
+                    }
+                }
+                const int fbi = __builtin_amdgcn_readfirstlane(acc.idx);
+                const int fbd = __builtin_amdgcn_readfirstlane(acc.best);
+                const int fb2 = __builtin_amdgcn_readfirstlane(acc.best2);
+                if (fbi >= 0 && fbd <= kThLow && (float)fbd < (float)fb2 * nnratio) {
+#ifdef ORB_TIMING
+                    nMatch++;
+#endif
+                    if (lane == 0) {
+                        v21[fbi] = iq;
+                        vMD[fbi] = fbd;
+                        mt[iq] = fbi;
+                    }
+                }
+                wave_lds_sync();
+                TACC(tFall, t_f0);
+                a0 += qs + 1;
+            } else {
+                a0 += qs;
+            }
         }
         wave_lds_sync();
         TACC(tLoop, t_l0);
@@ -626,8 +667,10 @@ __global__ __launch_bounds__(64) void k_resolve_sfi(const orb_keypoint* __restri
     if (lane == 0) nmatches_out[b] = kept;
 #ifdef ORB_TIMING
     if (lane == 0 && b == 0)
-        printf("resolve b0: init %lld stage %lld loop %lld final %lld total %lld (cycles) n1 %d n2 %d act %d fall %d match %d\n",
-               t_init - t_begin, tStage, tLoop, clock64() - t_loopend, clock64() - t_begin, n1, n2, nAct, nFall, nMatch);
+        printf("resolve b0: init %lld stage %lld loop %lld (gather %lld decide %lld fallback %lld) final %lld total %lld "
+               "n1 %d n2 %d act %d fall %d match %d batches %d\n",
+               t_init - t_begin, tStage, tLoop, tA, tB, tFall, clock64() - t_loopend, clock64() - t_begin, n1, n2, nAct, nFall,
+               nMatch + nMatchL[0], nBatch);
 #endif
 }
 
@@ -996,7 +1039,7 @@ int orb_search_for_initialization(orb_matcher* m, const orb_frame_view* f1, cons
     hipLaunchKernelGGL(k_cand_sfi, dim3((cap + 3) / 4, 1), dim3(256), 0, s, m->d_k1, m->d_d1, m->d_n, m->d_d2, m->d_cs,
                        m->d_gj, m->d_gxy, m->d_prev, cap, g, (float)window, m->d_cand, m->d_ncand, m->d_topk,
                        m->d_status);
-    const size_t lds = (4 * (size_t)cap + 32 + (2 + kTopK) * kRange) * 4;
+    const size_t lds = (4 * (size_t)cap + 32 + (2 + kTopK) * kRange + 32) * 4;
     if (lds > 65536) return ORB_E2BIG;
     hipLaunchKernelGGL(k_resolve_sfi, dim3(1), dim3(64), lds, s, m->d_k1, m->d_n, m->d_k2, m->d_n + 1, cap, g,
                        m->nnratio, m->checkOri, m->d_cand, m->d_ncand, m->d_topk, m->d_prev, m->d_m12, m->d_nm);
@@ -1030,7 +1073,7 @@ int orb_search_for_initialization_batch_device(orb_matcher* m, const orb_keypoin
     hipLaunchKernelGGL(k_cand_sfi, dim3((cap + 3) / 4, nb), dim3(256), 0, s, d_kps1, d_desc1, d_n1, d_desc2, m->d_cs,
                        m->d_gj, m->d_gxy, (const float*)nullptr, cap, g, (float)window, m->d_cand, m->d_ncand,
                        m->d_topk, m->d_status);
-    const size_t lds = (4 * (size_t)cap + 32 + (2 + kTopK) * kRange) * 4;
+    const size_t lds = (4 * (size_t)cap + 32 + (2 + kTopK) * kRange + 32) * 4;
     if (lds > 65536) return ORB_E2BIG;
     hipLaunchKernelGGL(k_resolve_sfi, dim3(nb), dim3(64), lds, s, d_kps1, d_n1, d_kps2, d_n2, cap, g, m->nnratio,
                        m->checkOri, m->d_cand, m->d_ncand, m->d_topk, (float*)nullptr, d_matches12, d_nmatches);

@@ -1,0 +1,11 @@
+#!/bin/bash
+# One rocprofv3 PMC pass (counters given as arguments) over a short bench.py run -> gpurun_out/pmc_<tag>
+# usage: tools/pmc_run.sh TAG COUNTER... ; counters only with --kernel-trace (no sys/runtime traces)
+set -e
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=$1; shift
+export TMPDIR=/tmp
+cd /tmp
+timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-trace --output-format csv -d $R/gpurun_out/pmc_$TAG -o run -- \
+    python3 $R/bench.py --no-cpu --no-lba --steps 5 --warmup 2 --streams 1 > $R/gpurun_out/pmc_$TAG.log 2>&1
+echo pmc done
