@@ -30,6 +30,14 @@
 
 #include "common.h"
 
+#ifdef ORB_TIMING   // instrumented variant (tools/build_variant.py)
+#define TSTAMP(v) const long long v = clock64()
+#define TACC(acc, a) acc += clock64() - (a)
+#else
+#define TSTAMP(v)
+#define TACC(acc, a)
+#endif
+
 namespace orbamd {
 
 // ------------------------------------------------------------------ device math (SE3Quat)
@@ -138,14 +146,15 @@ struct LbaDev {
     const int32_t* ptLocal;     // global point -> local index or -1 (owned points only)
     const int32_t* ptGlob;      // local -> global point
     const int32_t* actPos;      // edge -> position in act (or -1)
+    const int32_t *actPt, *actPi; // per act position: local point, pose hessian index (-1 fixed)
     int P, M;                   // free active poses, owned active points
     const int32_t *ptStart, *ptEdges;     // CSR by local point (edge ids, sorted by pose index)
     const int32_t *poStart, *poEdges;     // CSR by pose index (edge ids)
-    const int32_t *prStart, *prE1, *prE2; // CSR by pose-pair block (i<=j), contributions
+    const int32_t *prStart, *prE1, *prE2; // CSR by pose-pair block (i<=j), contributions (act positions)
     // linearisation (indexed by act position)
     double *Hll_e, *Hpp_e, *Hpl_e, *bl_e, *bp_e, *BD, *coef, *echi;
     // reduced per vertex
-    double *Hll, *bl, *Dinv, *Hpp, *bp;
+    double *Hll, *bl, *Dinv, *db, *Hpp, *bp;   // db = Dinv b_l
     double *S, *bs, *x;         // x: [6P + 3M]
     double* red;                // reduction scratch
     int* flags;                 // [0] LDLT failure
@@ -331,7 +340,8 @@ __global__ __launch_bounds__(64) void k_pose_reduce(LbaDev d) {
     }
 }
 
-// Per landmark with lambda: Dinv (Eigen 3x3 cofactor inverse), BD_e = Hpl_e Dinv, coef_e = Hpl_e Dinv b_l
+// Per landmark with lambda: Dinv (Eigen 3x3 cofactor inverse) and db = Dinv b_l
+// (G/core/block_solver.hpp:380-398).
 __global__ __launch_bounds__(256) void k_point_schur(LbaDev d, double lambda) {
     const int l = blockIdx.x * 256 + threadIdx.x;
     if (l >= d.M) return;
@@ -351,53 +361,59 @@ __global__ __launch_bounds__(256) void k_point_schur(LbaDev d, double lambda) {
         for (int j = 0; j < 3; j++) Di[j * 3 + i] = c[i * 3 + j] * invdet;
     for (int i = 0; i < 9; i++) d.Dinv[9 * (size_t)l + i] = Di[i];
     const double* b = d.bl + 3 * (size_t)l;
-    double db[3];
-    for (int i = 0; i < 3; i++) db[i] = Di[i * 3] * b[0] + Di[i * 3 + 1] * b[1] + Di[i * 3 + 2] * b[2];
-    for (int a = d.ptStart[l]; a < d.ptStart[l + 1]; a++) {
-        const int e = d.ptEdges[a];
-        if (d.poseIdx[d.eps[e]] < 0) continue;
-        const int k = d.actPos[e];
-        const double* Bi = d.Hpl_e + 18 * (size_t)k;
-        double* BD = d.BD + 18 * (size_t)k;
-        double* cf = d.coef + 6 * (size_t)k;
-        for (int r = 0; r < 6; r++) {
-            for (int q = 0; q < 3; q++)
-                BD[r * 3 + q] = Bi[r * 3] * Di[q] + Bi[r * 3 + 1] * Di[3 + q] + Bi[r * 3 + 2] * Di[6 + q];
-            cf[r] = Bi[r * 3] * db[0] + Bi[r * 3 + 1] * db[1] + Bi[r * 3 + 2] * db[2];
-        }
+    for (int i = 0; i < 3; i++) d.db[3 * (size_t)l + i] = Di[i * 3] * b[0] + Di[i * 3 + 1] * b[1] + Di[i * 3 + 2] * b[2];
+}
+
+// Per active edge with a free pose: BD_e = Hpl_e Dinv, coef_e = Hpl_e Dinv b_l.
+__global__ __launch_bounds__(256) void k_edge_schur(LbaDev d) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= d.nact || d.actPi[k] < 0) return;
+    const int l = d.actPt[k];
+    double Di[9], db[3];
+    for (int i = 0; i < 9; i++) Di[i] = d.Dinv[9 * (size_t)l + i];
+    for (int i = 0; i < 3; i++) db[i] = d.db[3 * (size_t)l + i];
+    const double* Bi = d.Hpl_e + 18 * (size_t)k;
+    double* BD = d.BD + 18 * (size_t)k;
+    double* cf = d.coef + 6 * (size_t)k;
+    for (int r = 0; r < 6; r++) {
+        for (int q = 0; q < 3; q++)
+            BD[r * 3 + q] = Bi[r * 3] * Di[q] + Bi[r * 3 + 1] * Di[3 + q] + Bi[r * 3 + 2] * Di[6 + q];
+        cf[r] = Bi[r * 3] * db[0] + Bi[r * 3 + 1] * db[1] + Bi[r * 3 + 2] * db[2];
     }
 }
 
-// S block (i,j), i<=j: (i==j ? Hpp_i + lambda I : 0) - sum_contrib BD_e1 Hpl_e2^T.
-// One wave per block; each lane accumulates its strided contributions, then a fixed butterfly.
-__global__ __launch_bounds__(64) void k_schur_pairs(LbaDev d, double lambda, int addDiag, const int32_t* pairI,
-                                                    const int32_t* pairJ) {
-    const int pr = blockIdx.x, lane = threadIdx.x;
+// S_ij block of the reduced camera system, one workgroup per pose pair (i <= j):
+// S_ij = [i == j](Hpp_i + lambda I) - sum_c BD_c Hpl_c'^T over the landmarks c seen by both
+// (G/core/block_solver.hpp:408-440).  Thread t owns output element t % 36 of contribution
+// group t / 36 (7 groups); the group partial sums meet in LDS.
+constexpr int kSpGroups = 7;
+__global__ __launch_bounds__(256) void k_schur_pairs(LbaDev d, double lambda, int addDiag, const int32_t* pairI,
+                                                     const int32_t* pairJ) {
+    __shared__ double part[kSpGroups][36];
+    const int pr = blockIdx.x, tid = threadIdx.x;
     const int bi = pairI[pr], bj = pairJ[pr];
-    double acc[36];
-    for (int i = 0; i < 36; i++) acc[i] = 0;
-    for (int c = d.prStart[pr] + lane; c < d.prStart[pr + 1]; c += 64) {
-        const double* BD = d.BD + 18 * (size_t)d.actPos[d.prE1[c]];
-        const double* Bj = d.Hpl_e + 18 * (size_t)d.actPos[d.prE2[c]];
-        for (int r = 0; r < 6; r++)
-            for (int q = 0; q < 6; q++)
-                acc[r * 6 + q] += BD[r * 3] * Bj[q * 3] + BD[r * 3 + 1] * Bj[q * 3 + 1] + BD[r * 3 + 2] * Bj[q * 3 + 2];
+    const int o = tid % 36, grp = tid / 36;
+    const int r = o / 6, q = o % 6;
+    if (grp < kSpGroups) {
+        double acc = 0.0;
+        const int c0 = d.prStart[pr], c1 = d.prStart[pr + 1];
+        for (int c = c0 + grp; c < c1; c += kSpGroups) {
+            const double* BD = d.BD + 18 * (size_t)d.prE1[c] + r * 3;
+            const double* Bj = d.Hpl_e + 18 * (size_t)d.prE2[c] + q * 3;
+            acc += BD[0] * Bj[0] + BD[1] * Bj[1] + BD[2] * Bj[2];
+        }
+        part[grp][o] = acc;
     }
-    for (int i = 0; i < 36; i++) {
-        double v = acc[i];
-        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-        acc[i] = v;
-    }
-    if (lane < 36) {
-        const int r = lane / 6, q = lane % 6;
+    __syncthreads();
+    if (tid < 36) {
+        double sacc = 0.0;
+        for (int g2 = 0; g2 < kSpGroups; g2++) sacc += part[g2][tid];
         double v = 0.0;
         if (bi == bj && addDiag) {     // rank 0 carries the (already all-reduced) Hpp + lambda I
-            v = d.Hpp[36 * (size_t)bi + lane];
+            v = d.Hpp[36 * (size_t)bi + tid];
             if (r == q) v += lambda;
         }
-        double s = 0;
-        for (int i = 0; i < 36; i++) s = (i == lane) ? acc[i] : s;
-        v -= s;
+        v -= sacc;
         const int n = 6 * d.P;
         d.S[(size_t)(6 * bi + r) * n + 6 * bj + q] = v;
         d.S[(size_t)(6 * bj + q) * n + 6 * bi + r] = v;
@@ -425,67 +441,223 @@ __global__ __launch_bounds__(64) void k_bschur(LbaDev d, int addBp) {
 }
 
 // Dense LDL^T (no pivoting; fails only on a zero pivot, like SimplicialLDLT) + solve, one
-// workgroup of 1024 threads.  The n x n matrix is staged in LDS when it fits (n <= 136, i.e.
+// workgroup of 256 threads.  The n x n matrix is staged in LDS when it fits (n <= 136, i.e.
 // up to 22 free keyframes), otherwise factored in place in global memory (L2-resident).
-// Right-looking elimination: per column j, L(:,j) = A(:,j)/d_j, then the trailing lower
-// triangle A(i,k) -= (L_ij L_kj) d_j.  The triangular solves run column-oriented on one wave.
+// Right-looking elimination in panels of kLdltW columns: wave 0 factors a panel (column j:
+// L(:,j) = A(:,j)/d_j, then the panel's later columns take A(i,k) -= (L_ij L_kj) d_j) with
+// wave-level ordering only, then all threads apply the panel's rank-1 updates to the
+// trailing lower triangle, each element in column order — the same rounding sequence as the
+// column-by-column algorithm, with two workgroup barriers per panel instead of per column.
+// The triangular solves run column-oriented on one wave.
+constexpr int kLdltW = 8;     // panel width (columns per pair of workgroup barriers)
+constexpr int kLdltT = 256;
+constexpr int kLdltMaxN = 192; // panel rows held in registers: 3 per lane
+
+__device__ __forceinline__ double shfl_d(double v, int src) { return __shfl(v, src, 64); }
+
+// Dense LDL^T (no pivoting; fails only on a zero pivot, like SimplicialLDLT) + solve, one
+// workgroup of 256 threads; the n x n matrix is staged in LDS when it fits (n <= 136, i.e. up
+// to 22 free keyframes), otherwise factored in place in global memory (L2-resident).
+// Right-looking elimination in panels of kLdltW columns:
+//  * wave 0 factors the panel in registers (3 panel rows per lane, pivots and L entries
+//    broadcast with shuffles): L(:,j) = A(:,j)/d_j, then A(i,k) -= (L_ij L_kj) d_j for the
+//    panel's later columns;
+//  * all threads apply the panel's rank-1 updates to the trailing lower triangle in 4 x 4
+//    register tiles, each element taking the updates in column order.
+// Every element therefore sees exactly the operation sequence of the column-by-column
+// algorithm (same rounding), with two workgroup barriers per panel instead of per column.
+// The triangular solves are blocked the same way on one wave.
 template <bool kLds>
-__global__ __launch_bounds__(1024) void k_ldlt_solve(double* __restrict__ Ag, const double* __restrict__ b, int n,
-                                                     double* __restrict__ x, int* __restrict__ flags) {
+__global__ __launch_bounds__(kLdltT) void k_ldlt_solve(double* __restrict__ Ag, const double* __restrict__ b, int n,
+                                                       double* __restrict__ x, int* __restrict__ flags) {
     extern __shared__ __attribute__((aligned(16))) double sh[];
+    TSTAMP(t_l0);
+    long long tPanel = 0, tTrail = 0;
+    (void)tPanel; (void)tTrail;
     double* A = kLds ? sh : Ag;
     double* dg = sh + (kLds ? (size_t)n * n : 0);
-    double* col = dg + n;
-    double* y = col + n;
-    const int tid = threadIdx.x, nt = blockDim.x;
-    if (kLds)
-        for (int t = tid; t < n * n; t += nt) A[t] = Ag[t];
-    for (int t = tid; t < n; t += nt) y[t] = b[t];
-    __syncthreads();
-    int fail = 0;
-    for (int j = 0; j < n; j++) {
-        const double dj = A[(size_t)j * n + j];
-        if (dj == 0.0 || !isfinite(dj)) {   // uniform: every thread reads the same value
-            fail = 1;
-            break;
+    double* y = dg + n;
+    __shared__ int failS;
+    const int tid = threadIdx.x, lane = tid & 63;
+    if (kLds) {
+        for (int t0 = 0; t0 < n * n; t0 += kLdltT * 8) {   // 8 loads in flight per thread
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] = t0 + u * kLdltT + tid < n * n ? Ag[t0 + u * kLdltT + tid] : 0.0;
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (t0 + u * kLdltT + tid < n * n) A[t0 + u * kLdltT + tid] = v[u];
         }
-        for (int i = j + 1 + tid; i < n; i += nt) col[i] = A[(size_t)i * n + j] / dj;
-        if (tid == 0) dg[j] = dj;
-        __syncthreads();
-        const int m = n - j - 1;
-        for (int t = tid; t < m * m; t += nt) {
-            const int i = t / m, k = t % m;
-            if (k > i) continue;
-            const int ii = j + 1 + i, kk = j + 1 + k;
-            A[(size_t)ii * n + kk] -= (col[ii] * col[kk]) * dj;
-        }
-        for (int i = j + 1 + tid; i < n; i += nt) A[(size_t)i * n + j] = col[i];
-        __syncthreads();
     }
-    if (fail) {
+    for (int t = tid; t < n; t += kLdltT) y[t] = b[t];
+    if (tid == 0) failS = 0;
+    __syncthreads();
+#ifdef ORB_TIMING
+    const long long t_p_first = clock64() - t_l0;
+#endif
+    for (int jb = 0; jb < n; jb += kLdltW) {
+        const int je = min(jb + kLdltW, n);
+        TSTAMP(t_p0);
+        if (tid < 64) {
+            // ---- panel [jb, je) on wave 0: lane holds rows jb + lane + 64u
+            double P[3][kLdltW];
+#pragma unroll
+            for (int u = 0; u < 3; u++) {
+                const int r = jb + lane + 64 * u;
+#pragma unroll
+                for (int c = 0; c < kLdltW; c++) P[u][c] = (r < n && jb + c < je) ? A[(size_t)r * n + jb + c] : 0.0;
+            }
+            bool bad = false;
+#pragma unroll
+            for (int c = 0; c < kLdltW; c++) {
+                const int j = jb + c;
+                if (j < je && !bad) {
+                    const double dj = shfl_d(P[0][c], c);   // A(j, j): row j is lane c, slot 0
+                    if (dj == 0.0 || !isfinite(dj)) {
+                        bad = true;
+                    } else {
+#pragma unroll
+                        for (int u = 0; u < 3; u++)
+                            if (jb + lane + 64 * u > j) P[u][c] = P[u][c] / dj;
+                        if (lane == 0) dg[j] = dj;
+#pragma unroll
+                        for (int k = c + 1; k < kLdltW; k++) {
+                            const double lk = shfl_d(P[0][c], k);   // L(jb+k, j)
+#pragma unroll
+                            for (int u = 0; u < 3; u++)
+                                if (jb + k < je && jb + lane + 64 * u >= jb + k) P[u][k] -= (P[u][c] * lk) * dj;
+                        }
+                    }
+                }
+            }
+            if (bad && lane == 0) failS = 1;
+#pragma unroll
+            for (int u = 0; u < 3; u++) {
+                const int r = jb + lane + 64 * u;
+#pragma unroll
+                for (int c = 0; c < kLdltW; c++)
+                    if (r < n && jb + c < je) A[(size_t)r * n + jb + c] = P[u][c];
+            }
+        }
+        __syncthreads();
+        TACC(tPanel, t_p0);
+        TSTAMP(t_t0);
+        if (failS) break;
+        // ---- trailing lower triangle (rows, columns >= je) in 4 x 4 tiles; 16 x 16 thread
+        //      grid: thread (ty, tx) owns tile rows ty+16a and tile columns tx+16c (c <= a)
+        {
+            const int m = n - je, T = (m + 3) >> 2;
+            const int ty = tid >> 4, tx = tid & 15;
+            double d[kLdltW];
+#pragma unroll
+            for (int p = 0; p < kLdltW; p++) d[p] = jb + p < je ? dg[jb + p] : 0.0;
+            for (int ti = ty; ti < T; ti += 16) {
+                double li[4][kLdltW];
+#pragma unroll
+                for (int a2 = 0; a2 < 4; a2++) {
+                    const int i = je + 4 * ti + a2;
+#pragma unroll
+                    for (int p = 0; p < kLdltW; p++) li[a2][p] = (i < n && jb + p < je) ? A[(size_t)i * n + jb + p] : 0.0;
+                }
+                for (int tk = tx; tk <= ti; tk += 16) {
+                    double lk[4][kLdltW];
+#pragma unroll
+                    for (int b2 = 0; b2 < 4; b2++) {
+                        const int k = je + 4 * tk + b2;
+#pragma unroll
+                        for (int p = 0; p < kLdltW; p++) lk[b2][p] = (k < n && jb + p < je) ? A[(size_t)k * n + jb + p] : 0.0;
+                    }
+                    double v[4][4];
+#pragma unroll
+                    for (int a2 = 0; a2 < 4; a2++)
+#pragma unroll
+                        for (int b2 = 0; b2 < 4; b2++) {
+                            const int i = je + 4 * ti + a2, k = je + 4 * tk + b2;
+                            v[a2][b2] = (i < n && k <= i) ? A[(size_t)i * n + k] : 0.0;
+                        }
+#pragma unroll
+                    for (int p = 0; p < kLdltW; p++)
+                        if (jb + p < je)
+#pragma unroll
+                            for (int a2 = 0; a2 < 4; a2++)
+#pragma unroll
+                                for (int b2 = 0; b2 < 4; b2++) v[a2][b2] -= (li[a2][p] * lk[b2][p]) * d[p];
+#pragma unroll
+                    for (int a2 = 0; a2 < 4; a2++)
+#pragma unroll
+                        for (int b2 = 0; b2 < 4; b2++) {
+                            const int i = je + 4 * ti + a2, k = je + 4 * tk + b2;
+                            if (i < n && k <= i) A[(size_t)i * n + k] = v[a2][b2];
+                        }
+                }
+            }
+        }
+        __syncthreads();
+        TACC(tTrail, t_t0);
+    }
+    TSTAMP(t_l1);
+    if (failS) {
         if (tid == 0) flags[0] = 1;
         return;
     }
     if (tid >= 64) return;
-    // forward substitution, column oriented: y_k final -> y_i -= L_ik y_k (i > k)
-    for (int k = 0; k < n; k++) {
-        const double yk = y[k];
-        for (int i = k + 1 + tid; i < n; i += 64) y[i] -= A[(size_t)i * n + k] * yk;
+    // ---- forward substitution (column order per element: y_i -= L_ik y_k, k ascending),
+    //      blocked by kLdltW: the block's own rows on lanes 0..W-1, later rows 3 per lane
+    for (int kb = 0; kb < n; kb += kLdltW) {
+        const int ke = min(kb + kLdltW, n);
+        double yb = (lane < ke - kb) ? y[kb + lane] : 0.0;
+#pragma unroll
+        for (int c = 0; c < kLdltW; c++) {
+            if (kb + c >= ke) break;
+            const double yc = shfl_d(yb, c);
+            if (lane > c && lane < ke - kb) yb -= A[(size_t)(kb + lane) * n + kb + c] * yc;
+        }
+        double ys[kLdltW];
+#pragma unroll
+        for (int c = 0; c < kLdltW; c++) ys[c] = shfl_d(yb, c);
+        if (lane < ke - kb) y[kb + lane] = yb;
+        for (int i = ke + lane; i < n; i += 64) {
+            double v = y[i];
+#pragma unroll
+            for (int c = 0; c < kLdltW; c++)
+                if (kb + c < ke) v -= A[(size_t)i * n + kb + c] * ys[c];
+            y[i] = v;
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
     }
-    for (int i = tid; i < n; i += 64) y[i] = y[i] / dg[i];
+    for (int i = lane; i < n; i += 64) y[i] = y[i] / dg[i];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    // backward substitution with L^T: x_k final -> y_i -= L_ki x_k (i < k)
-    for (int k = n - 1; k >= 0; k--) {
-        const double xk = y[k];
-        for (int i = tid; i < k; i += 64) y[i] -= A[(size_t)k * n + i] * xk;
+    // ---- backward substitution with L^T (per element: y_i -= L_ki x_k, k descending)
+    for (int ke = n; ke > 0; ke -= kLdltW) {
+        const int kb = max(ke - kLdltW, 0), w = ke - kb;
+        double xb = lane < w ? y[kb + lane] : 0.0;
+#pragma unroll
+        for (int c = kLdltW - 1; c >= 0; c--) {
+            if (c >= w) continue;
+            const double xc = shfl_d(xb, c);
+            if (lane < c) xb -= A[(size_t)(kb + c) * n + kb + lane] * xc;
+        }
+        double xs[kLdltW];
+#pragma unroll
+        for (int c = 0; c < kLdltW; c++) xs[c] = shfl_d(xb, c);
+        if (lane < w) y[kb + lane] = xb;
+        for (int i = lane; i < kb; i += 64) {
+            double v = y[i];
+#pragma unroll
+            for (int c = kLdltW - 1; c >= 0; c--)
+                if (c < w) v -= A[(size_t)(kb + c) * n + i] * xs[c];
+            y[i] = v;
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
     }
-    for (int i = tid; i < n; i += 64) x[i] = y[i];
+    for (int i = lane; i < n; i += 64) x[i] = y[i];
     if (tid == 0) flags[0] = 0;
+#ifdef ORB_TIMING
+    if (tid == 0) printf("ldlt n %d: stage %lld panel %lld trailing %lld solves %lld\n", n, t_p_first, tPanel, tTrail, clock64() - t_l1);
+#endif
 }
 
 // x_l = Dinv (b_l - sum_e Hpl_e^T x_p(pose_e))
@@ -648,7 +820,7 @@ namespace {
 
 struct HostStructure {
     std::vector<int32_t> act, poseIdx, ptLocal, ptGlob, actPos, ptStart, ptEdges, poStart, poEdges, prStart, prE1,
-        prE2, pairI, pairJ, freePoses;
+        prE2, pairI, pairJ, freePoses, actPt, actPi;
     int P = 0, M = 0;
 };
 
@@ -690,6 +862,12 @@ void build_structure(const lba_problem* p, const std::vector<uint8_t>& level, in
     s.M = (int)order.size();
     s.actPos.assign(NE, -1);
     for (size_t k = 0; k < s.act.size(); k++) s.actPos[s.act[k]] = (int)k;
+    s.actPt.resize(s.act.size());
+    s.actPi.resize(s.act.size());
+    for (size_t k = 0; k < s.act.size(); k++) {
+        s.actPt[k] = s.ptLocal[p->edge_point[s.act[k]]];
+        s.actPi[k] = s.poseIdx[p->edge_pose[s.act[k]]];
+    }
     // CSR by local point, edges sorted by pose index (fixed poses last)
     s.ptStart.assign(s.M + 1, 0);
     for (int e : s.act) s.ptStart[s.ptLocal[p->edge_point[e]] + 1]++;
@@ -758,8 +936,8 @@ void build_structure(const lba_problem* p, const std::vector<uint8_t>& level, in
                 const int i2 = s.poseIdx[p->edge_pose[s.ptEdges[b]]];
                 if (i2 < 0) continue;
                 const int pr = pairOf[(size_t)i1 * P + i2];
-                s.prE1[fill[pr]] = s.ptEdges[a];
-                s.prE2[fill[pr]] = s.ptEdges[b];
+                s.prE1[fill[pr]] = s.actPos[s.ptEdges[a]];   // act positions (BD / Hpl_e rows)
+                s.prE2[fill[pr]] = s.actPos[s.ptEdges[b]];
                 fill[pr]++;
             }
         }
@@ -923,6 +1101,7 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
     TRY(dalloc(c, &d.bp_e, 6 * (size_t)NE)); TRY(dalloc(c, &d.BD, 18 * (size_t)NE));
     TRY(dalloc(c, &d.coef, 6 * (size_t)NE)); TRY(dalloc(c, &d.echi, (size_t)NE + 6 * (size_t)NP + 3 * (size_t)NM));
     TRY(dalloc(c, &d.Hll, 9 * (size_t)NM)); TRY(dalloc(c, &d.bl, 3 * (size_t)NM)); TRY(dalloc(c, &d.Dinv, 9 * (size_t)NM));
+    TRY(dalloc(c, &d.db, 3 * (size_t)NM));
     TRY(dalloc(c, &d.Hpp, 36 * (size_t)NP)); TRY(dalloc(c, &d.bp, 6 * (size_t)NP));
     const size_t nS = (size_t)6 * NP;
     TRY(dalloc(c, &d.S, nS * nS + nS));   // S followed by b_s (contiguous for one all-reduce)
@@ -971,6 +1150,8 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
     auto init_opt = [&](int lvl) -> int {
         build_structure(p, level, lvl, c->rank, c->world, hs);
         int32_t *act, *poseIdx, *ptLocal, *ptGlob, *actPos, *ptStart, *ptEdges, *poStart, *poEdges, *prStart, *prE1, *prE2;
+        int32_t *actPt, *actPi;
+        TRY(upload(c, &actPt, hs.actPt)); TRY(upload(c, &actPi, hs.actPi));
         TRY(upload(c, &act, hs.act)); TRY(upload(c, &poseIdx, hs.poseIdx)); TRY(upload(c, &ptLocal, hs.ptLocal));
         TRY(upload(c, &ptGlob, hs.ptGlob)); TRY(upload(c, &actPos, hs.actPos)); TRY(upload(c, &ptStart, hs.ptStart));
         TRY(upload(c, &ptEdges, hs.ptEdges)); TRY(upload(c, &poStart, hs.poStart)); TRY(upload(c, &poEdges, hs.poEdges));
@@ -980,6 +1161,7 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
         d.act = act; d.nact = (int)hs.act.size(); d.poseIdx = poseIdx; d.ptLocal = ptLocal; d.ptGlob = ptGlob;
         d.actPos = actPos; d.P = hs.P; d.M = hs.M; d.ptStart = ptStart; d.ptEdges = ptEdges; d.poStart = poStart;
         d.poEdges = poEdges; d.prStart = prStart; d.prE1 = prE1; d.prE2 = prE2;
+        d.actPt = actPt; d.actPi = actPi;
         d.bs = d.S + (size_t)36 * d.P * d.P;   // b_s right after the 6P x 6P matrix: one all-reduce
         return ORB_OK;
     };
@@ -1033,20 +1215,22 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
                 const double lam = lambda;
                 if (c->profile) (void)hipEventRecord(e0, s);
                 if (d.M > 0) hipLaunchKernelGGL(k_point_schur, grid(d.M), dim3(256), 0, s, d, lam);
+                if (d.nact > 0) hipLaunchKernelGGL(k_edge_schur, grid(d.nact), dim3(256), 0, s, d);
                 const int npairs = d.P * (d.P + 1) / 2;
                 if (npairs > 0) {
-                    hipLaunchKernelGGL(k_schur_pairs, dim3(npairs), dim3(64), 0, s, d, lam, root ? 1 : 0, d_pairI, d_pairJ);
+                    hipLaunchKernelGGL(k_schur_pairs, dim3(npairs), dim3(256), 0, s, d, lam, root ? 1 : 0, d_pairI, d_pairJ);
                     hipLaunchKernelGGL(k_bschur, dim3(d.P), dim3(64), 0, s, d, root ? 1 : 0);
                 }
                 if (c->profile) (void)hipEventRecord(e1, s);
                 if (c->world > 1 && d.P > 0) TRY(comm_allreduce(c, d.S, (size_t)36 * d.P * d.P + 6 * (size_t)d.P, 0));
                 if (d.P > 0) {
                     const int n = 6 * d.P;
+                    if (n > kLdltMaxN) return ORB_E2BIG;   // panel rows are held in registers
                     if ((size_t)n * n * 8 + 3 * (size_t)n * 8 <= 160 * 1024)
-                        hipLaunchKernelGGL(k_ldlt_solve<true>, dim3(1), dim3(1024), ((size_t)n * n + 3 * (size_t)n) * 8, s,
+                        hipLaunchKernelGGL(k_ldlt_solve<true>, dim3(1), dim3(kLdltT), ((size_t)n * n + 2 * (size_t)n) * 8, s,
                                            d.S, d.bs, n, d.x, d.flags);
                     else
-                        hipLaunchKernelGGL(k_ldlt_solve<false>, dim3(1), dim3(1024), 3 * (size_t)n * 8, s, d.S, d.bs, n,
+                        hipLaunchKernelGGL(k_ldlt_solve<false>, dim3(1), dim3(kLdltT), 2 * (size_t)n * 8, s, d.S, d.bs, n,
                                            d.x, d.flags);
                 } else {
                     ORB_HIP_TRY(hipMemsetAsync(d.flags, 0, 4, s));
