@@ -169,6 +169,23 @@ int orb_search_by_projection_frame(orb_matcher* m, const orb_frame_view* cur, co
                                    const float* scale_factors, const float cam[6], float th,
                                    int mono, int32_t* cur_mp);
 
+/* ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>& vpMapPoints, float th)
+ * — R/src/ORBmatcher.cpp:63-163 (Tracking::SearchLocalPoints, R/src/Tracking.cpp:1413-1460).
+ * Map points in vector order (n_mp):
+ *   mp_in_view[i]  = mbTrackInView && !isBad();
+ *   mp_proj[3i..]  = mTrackProjX, mTrackProjY, mTrackProjXR (from Frame::isInFrustum);
+ *   mp_level[i]    = mnTrackScaleLevel; mp_view_cos[i] = mTrackViewCos;
+ *   mp_desc        = GetDescriptor() (32 B each); mp_has_obs[i] = Observations() > 0.
+ * scale_factors = F.mvScaleFactors.  cur_mp (in/out, f->n ints) is F.mvpMapPoints:
+ *   -1 empty, -2 holds a map point with observations (skipped), -3 holds one without
+ *   (not skipped, may be overwritten); a slot matched by this call receives the map point's
+ *   index i.  The matcher's nnratio applies (ratio test only within one scale level).
+ * Returns nmatches. */
+int orb_search_by_projection_local(orb_matcher* m, const orb_frame_view* f, int n_mp, const uint8_t* mp_in_view,
+                                   const float* mp_proj, const int32_t* mp_level, const float* mp_view_cos,
+                                   const uint8_t* mp_desc, const uint8_t* mp_has_obs, const float* scale_factors,
+                                   float th, int32_t* cur_mp);
+
 /* Brute-force 2-NN Hamming matching (all pairs; ties -> lowest train index):
  * for every query i, best_idx[i], best_d[i], second_d[i] (INT32_MAX when absent).
  * Host arrays in and out. */

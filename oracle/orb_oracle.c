@@ -1064,6 +1064,58 @@ int oracle_search_by_projection_ff(const oracle_frame* cur, const float* Tcw,
     return nmatches;
 }
 
+int oracle_search_by_projection_local(const oracle_frame* f, int n_mp, const uint8_t* in_view,
+                                      const float* proj, const int32_t* level, const float* view_cos,
+                                      const uint8_t* mp_desc, const uint8_t* has_obs,
+                                      const float* scale_factors, float nnratio, float th, int32_t* cur_mp)
+{
+    int nmatches = 0;
+    ogrid g;
+    build_grid(f, &g);
+    const int bFactor = th != 1.0f;
+    int* cand = (int*)malloc(sizeof(int) * (f->n + 1));
+    for (int i = 0; i < n_mp; i++) {
+        if (!in_view[i]) continue;
+        const int nPredictedLevel = level[i];
+        float r = view_cos[i] > 0.998f ? 2.5f : 4.0f;   /* RadiusByViewingCos */
+        if (bFactor) r *= th;
+        const float rad = r * scale_factors[nPredictedLevel];
+        const int nc = features_in_area(f, &g, proj[3 * i], proj[3 * i + 1], rad, nPredictedLevel - 1,
+                                        nPredictedLevel, cand, f->n);
+        if (nc == 0) continue;
+        const uint8_t* dMP = mp_desc + (size_t)i * 32;
+        int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+        for (int q = 0; q < nc; q++) {
+            const int idx = cand[q];
+            const int s = cur_mp[idx];
+            if (s == -2 || (s >= 0 && has_obs[s])) continue;   /* mvpMapPoints[idx]->Observations()>0 */
+            if (f->uright && f->uright[idx] > 0) {
+                const float er = fabsf(proj[3 * i + 2] - f->uright[idx]);
+                if (er > rad) continue;
+            }
+            const int dist = oracle_descriptor_distance(dMP, f->desc + (size_t)idx * 32);
+            if (dist < bestDist) {
+                bestDist2 = bestDist;
+                bestDist = dist;
+                bestLevel2 = bestLevel;
+                bestLevel = f->octave[idx];
+                bestIdx = idx;
+            } else if (dist < bestDist2) {
+                bestLevel2 = f->octave[idx];
+                bestDist2 = dist;
+            }
+        }
+        if (bestDist <= TH_HIGH) {
+            if (bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2) continue;
+            cur_mp[bestIdx] = i;
+            nmatches++;
+        }
+    }
+    free(cand);
+    free_grid(&g);
+    return nmatches;
+}
+
 void oracle_hamming_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt,
                          int32_t* best_idx, int32_t* best_d, int32_t* second_d)
 {

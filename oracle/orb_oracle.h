@@ -133,6 +133,19 @@ int oracle_search_by_projection_ff(const oracle_frame* cur, const float* Tcw_cur
                                    const float* scale_factors, const oracle_camera* cam,
                                    float th, int bMono, int check_ori, int32_t* cur_mp);
 
+/* ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>& vpMapPoints, th)
+ * (R/src/ORBmatcher.cpp:63-163) with RadiusByViewingCos (:166-172).  Map points are given
+ * in vector order: in_view = mbTrackInView && !isBad(); proj = (mTrackProjX, mTrackProjY,
+ * mTrackProjXR); level = mnTrackScaleLevel; view_cos = mTrackViewCos; desc = GetDescriptor();
+ * has_obs = Observations() > 0.  cur_mp (in/out, F.N ints) holds the slots mvpMapPoints:
+ * -1 empty, -2 occupied by a map point with observations (skipped), -3 occupied by one
+ * without (not skipped, may be overwritten); on return a slot matched by this call holds the
+ * map point's index.  Returns nmatches. */
+int oracle_search_by_projection_local(const oracle_frame* f, int n_mp, const uint8_t* in_view,
+                                      const float* proj, const int32_t* level, const float* view_cos,
+                                      const uint8_t* mp_desc, const uint8_t* has_obs,
+                                      const float* scale_factors, float nnratio, float th, int32_t* cur_mp);
+
 /* Brute-force Hamming k=2 (best, second) with lowest-index tie break. */
 void oracle_hamming_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt,
                          int32_t* best_idx, int32_t* best_d, int32_t* second_d);

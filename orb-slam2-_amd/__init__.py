@@ -3,5 +3,5 @@ Optimizer::LocalBundleAdjustment over hand-written gfx950 HIP kernels.
 Import as `orb_slam2_amd` (see pkgload.py)."""
 from . import _abi  # noqa: F401
 from .extractor import ORBextractor  # noqa: F401
-from .matcher import ORBmatcher, Frame  # noqa: F401
+from .matcher import ORBmatcher, Frame, LocalMapPoints  # noqa: F401
 from .optimizer import Optimizer, LocalBA  # noqa: F401

@@ -812,6 +812,118 @@ __global__ __launch_bounds__(64) void k_resolve_sbp(const orb_keypoint* __restri
     if (lane == 0) *nmatches_out = nmatches;
 }
 
+// ---------------------------------------------------------------- SearchByProjection(Frame, local map points)
+
+// One wave per local map point: RadiusByViewingCos window, GetFeaturesInArea(level-1, level),
+// the stereo reprojection gate and the Hamming distances (R/src/ORBmatcher.cpp:63-137).
+__global__ __launch_bounds__(256) void k_cand_sbl(const orb_keypoint* __restrict__ kc, const uint8_t* __restrict__ dc,
+                                                  const float* __restrict__ urc, int nc_, int nmp,
+                                                  const uint8_t* __restrict__ inView, const float* __restrict__ proj,
+                                                  const int32_t* __restrict__ lvl, const float* __restrict__ vcos,
+                                                  const uint8_t* __restrict__ mpDesc, const float* __restrict__ sf,
+                                                  GridParams g, float th, uint32_t* __restrict__ cand,
+                                                  int* __restrict__ ncand, int* __restrict__ status) {
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int i = blockIdx.x * 4 + wid;
+    if (i >= nmp) return;
+    int* ncount = ncand + i;
+    if (!inView[i]) { if (lane == 0) *ncount = 0; return; }
+    const int level = lvl[i];
+    float r = vcos[i] > 0.998f ? 2.5f : 4.0f;   // RadiusByViewingCos (R :166-172)
+    if (th != 1.0f) r *= th;
+    const float rad = r * sf[level];
+    const float px = proj[3 * (size_t)i], py = proj[3 * (size_t)i + 1], pxr = proj[3 * (size_t)i + 2];
+    const AreaQuery q = make_area(g, px, py, rad, level - 1, level);
+    uint32_t* out = cand + (size_t)i * kMaxCand;
+    const uint8_t* dq = mpDesc + (size_t)i * 32;
+    int n = 0;
+    for (int j0 = 0; j0 < nc_; j0 += 64) {
+        const int j = j0 + lane;
+        bool ok = false;
+        int d = 0;
+        if (j < nc_ && q.cx0 <= q.cx1) {
+            const orb_keypoint k2 = kc[j];
+            ok = in_area(q, grid_cell(g, k2.x, k2.y), k2.octave, k2.x, k2.y);
+            if (ok && urc && urc[j] > 0) {
+                const float er = fabsf(pxr - urc[j]);
+                if (er > rad) ok = false;
+            }
+            if (ok) d = hamming32(dq, dc + (size_t)j * 32);
+        }
+        const uint64_t m = __ballot(ok);
+        const int pos = n + __popcll(m & ((1ull << lane) - 1ull));
+        if (ok && pos < kMaxCand) out[pos] = (uint32_t)j | ((uint32_t)d << 20);
+        n += __popcll(m);
+    }
+    if (lane == 0) {
+        if (n > kMaxCand) { atomicOr(status, 1); n = kMaxCand; }
+        *ncount = n;
+    }
+}
+
+// Sequential replay over the map points (R :66-160), one wave: a slot matched earlier in the
+// call by a map point with observations is skipped by later ones.  Best / second candidate in
+// the reference's visiting order (cell-major, then index) from two wave minima per chunk.
+__global__ __launch_bounds__(64) void k_resolve_sbl(const orb_keypoint* __restrict__ kc, int ncur, int nmp, GridParams g,
+                                                    float nnratio, const uint8_t* __restrict__ hasObs,
+                                                    const uint32_t* __restrict__ cand, const int* __restrict__ ncand,
+                                                    int32_t* __restrict__ curMpG, int32_t* __restrict__ nmatches_out) {
+    extern __shared__ __attribute__((aligned(16))) int sm[];
+    const int lane = threadIdx.x;
+    int* ckey = sm;              // [ncur]
+    int* curMp = sm + ncur;      // [ncur] slot state (see orb_search_by_projection_local)
+    for (int j = lane; j < ncur; j += 64) {
+        ckey[j] = grid_cell(g, kc[j].x, kc[j].y);
+        curMp[j] = curMpG[j];
+    }
+    __syncthreads();
+    int nmatches = 0;
+    for (int i = 0; i < nmp; i++) {
+        const int nc = ncand[i];
+        if (nc == 0) continue;
+        const uint32_t* C = cand + (size_t)i * kMaxCand;
+        unsigned long long k1 = ~0ull, k2 = ~0ull;   // best and second (dist, visit order, index)
+        for (int c0 = 0; c0 < nc; c0 += 64) {
+            const int c = c0 + lane;
+            unsigned long long key = ~0ull;
+            if (c < nc) {
+                const uint32_t e = C[c];
+                const int j = (int)(e & 0xFFFFFu), d = (int)(e >> 20);
+                const int st = curMp[j];
+                if (!(st == -2 || (st >= 0 && hasObs[st])))   // `mvpMapPoints[idx]->Observations()>0`
+                    key = ((unsigned long long)(unsigned)d << 40) | ((unsigned long long)(unsigned)ckey[j] << 20) |
+                          (unsigned long long)(unsigned)j;
+            }
+            const unsigned long long m1 = wave_min_u64(key);
+            const unsigned long long m2 = wave_min_u64(key == m1 ? ~0ull : key);
+            if (m1 < k1) {
+                k2 = k1 < m2 ? k1 : m2;
+                k1 = m1;
+            } else {
+                k2 = k2 < m1 ? k2 : m1;
+            }
+        }
+        if (k1 == ~0ull) continue;
+        const int bestDist = (int)(k1 >> 40), bestIdx = (int)(k1 & 0xFFFFFull);
+        if (bestDist > kThHigh) continue;
+        const int bestLevel = kc[bestIdx].octave;
+        int bestDist2 = 256, bestLevel2 = -1;
+        if (k2 != ~0ull) {
+            bestDist2 = (int)(k2 >> 40);
+            bestLevel2 = kc[(int)(k2 & 0xFFFFFull)].octave;
+        }
+        // ratio test only if best and second share the scale level (R :151-153)
+        if (bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2) continue;
+        if (lane == 0) curMp[bestIdx] = i;
+        nmatches++;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    for (int j = lane; j < ncur; j += 64) curMpG[j] = curMp[j];
+    if (lane == 0) *nmatches_out = nmatches;
+}
+
 // ---------------------------------------------------------------- brute-force 2-NN
 
 // One wave per query row: lanes stride over train rows; ties -> lowest train index.
@@ -1168,6 +1280,89 @@ int orb_search_by_projection_frame(orb_matcher* m, const orb_frame_view* cur, co
     ORB_HIP_TRY(hipStreamSynchronize(s));
     if (hn[1]) return ORB_EOVERFLOW;
     std::memcpy(cur_mp, hcm, (size_t)cur->n * 4);
+    return hn[0];
+}
+
+int orb_search_by_projection_local(orb_matcher* m, const orb_frame_view* f, int n_mp, const uint8_t* mp_in_view,
+                                   const float* mp_proj, const int32_t* mp_level, const float* mp_view_cos,
+                                   const uint8_t* mp_desc, const uint8_t* mp_has_obs, const float* scale_factors,
+                                   float th, int32_t* cur_mp) {
+    if (!m || !f || n_mp < 0 || !cur_mp || !scale_factors || f->n < 0) return ORB_EINVAL;
+    if (n_mp > 0 && (!mp_in_view || !mp_proj || !mp_level || !mp_view_cos || !mp_desc || !mp_has_obs)) return ORB_EINVAL;
+    if (f->n >= (1 << 20)) return ORB_EINVAL;
+    if (n_mp == 0 || f->n == 0) return 0;
+    int maxLevel = 0;
+    for (int i = 0; i < f->n; i++) maxLevel = std::max(maxLevel, (int)f->octave[i]);
+    for (int i = 0; i < n_mp; i++) {
+        if (!mp_in_view[i]) continue;
+        if (mp_level[i] < 0 || mp_level[i] > 31) return ORB_EINVAL;
+        maxLevel = std::max(maxLevel, (int)mp_level[i]);
+    }
+    ORB_HIP_TRY(hipSetDevice(m->device));
+    const int cap = std::max(std::max(f->n, n_mp), 1);
+    int st = mensure(m, 1, cap);
+    if (st) return st;
+    const size_t lds = (size_t)2 * f->n * 4;
+    if (lds > 65536) return ORB_E2BIG;
+    const size_t bytes = (size_t)f->n * (sizeof(orb_keypoint) + 32 + 4 + 4) + (size_t)n_mp * (1 + 12 + 4 + 4 + 32 + 1) +
+                         32 * 4 + 1024;
+    st = mpin(m, bytes);
+    if (st) return st;
+    char* h = (char*)m->h_pin;
+    orb_keypoint* hk = (orb_keypoint*)h;
+    uint8_t* hd = (uint8_t*)(hk + f->n);
+    float* hur = (float*)(hd + (size_t)f->n * 32);
+    int32_t* hcm = (int32_t*)(hur + f->n);
+    float* hproj = (float*)(hcm + f->n);
+    int32_t* hlvl = (int32_t*)(hproj + 3 * (size_t)n_mp);
+    float* hcos = (float*)(hlvl + n_mp);
+    float* hsf = hcos + n_mp;
+    int32_t* hn = (int32_t*)(hsf + 32);
+    uint8_t* hmd = (uint8_t*)(hn + 4);
+    uint8_t* hin = hmd + (size_t)n_mp * 32;
+    uint8_t* hobs = hin + n_mp;
+    pack_view(f, hk);
+    std::memcpy(hd, f->desc, (size_t)f->n * 32);
+    for (int i = 0; i < f->n; i++) hur[i] = f->uright ? f->uright[i] : -1.f;
+    std::memcpy(hcm, cur_mp, (size_t)f->n * 4);
+    std::memcpy(hproj, mp_proj, (size_t)n_mp * 12);
+    std::memcpy(hlvl, mp_level, (size_t)n_mp * 4);
+    std::memcpy(hcos, mp_view_cos, (size_t)n_mp * 4);
+    for (int i = 0; i <= maxLevel && i < 32; i++) hsf[i] = scale_factors[i];
+    std::memcpy(hmd, mp_desc, (size_t)n_mp * 32);
+    std::memcpy(hin, mp_in_view, (size_t)n_mp);
+    std::memcpy(hobs, mp_has_obs, (size_t)n_mp);
+    hipStream_t s = m->stream;
+    // device layout reuses the matcher scratch: current frame in k2 / d2 / ur / m12, map points in
+    // xyz (projections), hasMp (levels), T (view cos, when it fits) and mpd (descriptors)
+    float* d_cos = (float*)m->d_prev;   // >= 8 bytes per slot
+    uint8_t* d_in = m->d_outl;
+    uint8_t* d_obs = m->d_hB;
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_k2, hk, (size_t)f->n * sizeof(orb_keypoint), hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_d2, hd, (size_t)f->n * 32, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_ur, hur, (size_t)f->n * 4, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_m12, hcm, (size_t)f->n * 4, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_xyz, hproj, (size_t)n_mp * 12, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_hasMp, hlvl, (size_t)n_mp * 4, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(d_cos, hcos, (size_t)n_mp * 4, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_sf, hsf, 32 * 4, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_mpd, hmd, (size_t)n_mp * 32, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(d_in, hin, (size_t)n_mp, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(d_obs, hobs, (size_t)n_mp, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemsetAsync(m->d_status, 0, 4, s));
+    const GridParams g = grid_of(f);
+    hipLaunchKernelGGL(k_cand_sbl, dim3((n_mp + 3) / 4), dim3(256), 0, s, m->d_k2, m->d_d2,
+                       f->uright ? (const float*)m->d_ur : (const float*)nullptr, f->n, n_mp, d_in, m->d_xyz,
+                       m->d_hasMp, d_cos, m->d_mpd, m->d_sf, g, th, m->d_cand, m->d_ncand, m->d_status);
+    hipLaunchKernelGGL(k_resolve_sbl, dim3(1), dim3(64), lds, s, m->d_k2, f->n, n_mp, g, m->nnratio, d_obs, m->d_cand,
+                       m->d_ncand, m->d_m12, m->d_nm);
+    ORB_HIP_TRY(hipGetLastError());
+    ORB_HIP_TRY(hipMemcpyAsync(hcm, m->d_m12, (size_t)f->n * 4, hipMemcpyDeviceToHost, s));
+    ORB_HIP_TRY(hipMemcpyAsync(hn, m->d_nm, 4, hipMemcpyDeviceToHost, s));
+    ORB_HIP_TRY(hipMemcpyAsync(hn + 1, m->d_status, 4, hipMemcpyDeviceToHost, s));
+    ORB_HIP_TRY(hipStreamSynchronize(s));
+    if (hn[1]) return ORB_EOVERFLOW;
+    std::memcpy(cur_mp, hcm, (size_t)f->n * 4);
     return hn[0];
 }
 

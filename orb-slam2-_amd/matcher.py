@@ -1,6 +1,7 @@
 """Host mirror of ORB_SLAM2::ORBmatcher (R/include/ORBmatcher.h:37-143) over
 the HIP C-ABI: DescriptorDistance, SearchForInitialization,
-SearchByProjection(Frame&, const Frame&, th, bMono) and a brute-force 2-NN."""
+SearchByProjection(Frame&, const Frame&, th, bMono),
+SearchByProjection(Frame&, const vector<MapPoint*>&, th) and a brute-force 2-NN."""
 import ctypes as C
 from dataclasses import dataclass, field
 from typing import Optional
@@ -54,6 +55,21 @@ class Frame:
                            self.mnMinX, self.mnMinY, self.mnMaxX, self.mnMaxY, float(winv), float(hinv))
         v._keep = (x, y, a, o, d, ur)
         return v
+
+
+@dataclass
+class LocalMapPoints:
+    """What SearchByProjection(Frame&, vector<MapPoint*>, th) reads of each local map point
+    after Frame::isInFrustum (R/src/Frame.cpp:307-376), in vector order."""
+    in_view: np.ndarray      # mbTrackInView && !isBad()   [n] bool
+    proj: np.ndarray         # mTrackProjX, mTrackProjY, mTrackProjXR   [n, 3] float32
+    level: np.ndarray        # mnTrackScaleLevel   [n] int32
+    view_cos: np.ndarray     # mTrackViewCos   [n] float32
+    desc: np.ndarray         # GetDescriptor()   [n, 32] uint8
+    has_obs: np.ndarray      # Observations() > 0   [n] bool
+
+    def __len__(self):
+        return len(self.in_view)
 
 
 class ORBmatcher:
@@ -114,6 +130,23 @@ class ORBmatcher:
             self._h, C.byref(vc), _abi.ptr(Tc), C.byref(vl), _abi.ptr(Tl), _abi.ptr(has), _abi.ptr(out),
             _abi.ptr(xyz), _abi.ptr(md), _abi.ptr(sf), _abi.ptr(camv), C.c_float(th), int(bMono),
             _abi.ptr(cur_mp)))
+        return n, cur_mp
+
+    def SearchByProjectionLocal(self, F: Frame, vpMapPoints: LocalMapPoints, th: float = 3.0, cur_mp=None):
+        """SearchByProjection(Frame&, const vector<MapPoint*>&, th).  cur_mp mirrors
+        F.mvpMapPoints (-1 empty, -2 map point with observations, -3 without); returns
+        (nmatches, cur_mp) with matched slots set to the map point index."""
+        if cur_mp is None:
+            cur_mp = np.full(F.N, -1, np.int32)
+        cur_mp = np.ascontiguousarray(cur_mp, np.int32).copy()
+        v = F.view()
+        mp = vpMapPoints
+        arrs = [np.ascontiguousarray(mp.in_view, np.uint8), np.ascontiguousarray(mp.proj, np.float32),
+                np.ascontiguousarray(mp.level, np.int32), np.ascontiguousarray(mp.view_cos, np.float32),
+                np.ascontiguousarray(mp.desc, np.uint8), np.ascontiguousarray(mp.has_obs, np.uint8),
+                np.ascontiguousarray(F.mvScaleFactors, np.float32)]
+        n = _abi.check("orb_search_by_projection_local", _abi.lib().orb_search_by_projection_local(
+            self._h, C.byref(v), len(mp), *[_abi.ptr(a) for a in arrs], C.c_float(th), _abi.ptr(cur_mp)))
         return n, cur_mp
 
     def knn2(self, q, t):

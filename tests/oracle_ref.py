@@ -191,6 +191,20 @@ def search_by_projection_ff(cur, Tcw, last, Tlw, has_mp, outlier, mp_xyz, mp_des
     return n, cur_mp
 
 
+def search_by_projection_local(f, in_view, proj, level, view_cos, mp_desc, has_obs, scale_factors, nnratio, th,
+                               cur_mp=None):
+    if cur_mp is None:
+        cur_mp = np.full(f.s.n, -1, np.int32)
+    cur_mp = np.ascontiguousarray(cur_mp, np.int32).copy()
+    arrs = [np.ascontiguousarray(in_view, np.uint8), np.ascontiguousarray(proj, np.float32),
+            np.ascontiguousarray(level, np.int32), np.ascontiguousarray(view_cos, np.float32),
+            np.ascontiguousarray(mp_desc, np.uint8), np.ascontiguousarray(has_obs, np.uint8),
+            np.ascontiguousarray(scale_factors, np.float32)]
+    n = lib().oracle_search_by_projection_local(C.byref(f.s), len(arrs[0]), *[P(a) for a in arrs], C.c_float(nnratio),
+                                                C.c_float(th), P(cur_mp))
+    return n, cur_mp
+
+
 def hamming_knn2(q, t):
     q = np.ascontiguousarray(q, np.uint8)
     t = np.ascontiguousarray(t, np.uint8)

@@ -128,3 +128,52 @@ def test_descriptor_distance(amd):
         x = rng.integers(0, 256, 32, dtype=np.uint8)
         y = rng.integers(0, 256, 32, dtype=np.uint8)
         assert amd.ORBmatcher.DescriptorDistance(x, y) == O.descriptor_distance(x, y)
+
+
+def _sbl_setup(W=640, H=480, nf=1000, seed=0x5EED0001, stereo=False, n_mp=700, rs=21):
+    """Local map points near the current frame's keypoints: projections within ~1 px of a
+    keypoint (plus strays), descriptors with a few flipped bits, random levels around the
+    keypoint octave, viewing cosines on both sides of 0.998, 10 % out of view, 5 % without
+    observations; some slots of mvpMapPoints pre-occupied (with / without observations)."""
+    from orb_slam2_amd import synth
+    cv = synth.canvas(seed, W, H)
+    p = O.params(nf)
+    b = O.extract(p, synth.frame(cv, W, H, 1))
+    rng = np.random.default_rng(rs)
+    kc = b["kps"]
+    src = rng.integers(0, len(kc), n_mp)
+    proj = np.zeros((n_mp, 3), np.float32)
+    proj[:, 0] = kc["x"][src] + rng.normal(0, 1.0, n_mp)
+    proj[:, 1] = kc["y"][src] + rng.normal(0, 1.0, n_mp)
+    stray = rng.random(n_mp) < 0.1
+    proj[stray, 0] = rng.uniform(0, W, stray.sum())
+    proj[stray, 1] = rng.uniform(0, H, stray.sum())
+    level = np.clip(kc["octave"][src] + rng.integers(-1, 2, n_mp), 0, 7).astype(np.int32)
+    view_cos = np.where(rng.random(n_mp) < 0.5, 0.999, 0.99).astype(np.float32)
+    desc = b["desc"][src].copy()
+    for _ in range(3):
+        desc[np.arange(n_mp), rng.integers(0, 32, n_mp)] ^= (1 << rng.integers(0, 8, n_mp)).astype(np.uint8)
+    in_view = rng.random(n_mp) > 0.1
+    has_obs = rng.random(n_mp) > 0.05
+    ur = None
+    if stereo:
+        ur = np.where(rng.random(len(kc)) < 0.7, kc["x"] - 12.0, -1).astype(np.float32)
+        proj[:, 2] = proj[:, 0] - 12.0 + rng.normal(0, 2.0, n_mp)
+    init = np.full(len(kc), -1, np.int32)
+    init[::23] = -2
+    init[5::31] = -3
+    sf = O.tables(p)["scale"]
+    return b, in_view, proj, level, view_cos, desc, has_obs, ur, init, sf
+
+
+@pytest.mark.parametrize("stereo,th,nn", [(False, 3.0, 0.8), (True, 3.0, 0.8), (False, 1.0, 0.8), (True, 5.0, 0.6)])
+def test_search_by_projection_local(amd, stereo, th, nn):
+    b, in_view, proj, level, vcos, desc, has_obs, ur, init, sf = _sbl_setup(stereo=stereo)
+    f = O.FrameView(b["kps"], b["desc"], 640, 480, uright=ur)
+    n_ref, mp_ref = O.search_by_projection_local(f, in_view, proj, level, vcos, desc, has_obs, sf, nn, th, init)
+    m = amd.ORBmatcher(nn, True)
+    F = amd.Frame(b["kps"], b["desc"], 640, 480, mvuRight=ur, mvScaleFactors=sf)
+    mp = amd.LocalMapPoints(in_view, proj, level, vcos, desc, has_obs)
+    n, cur = m.SearchByProjectionLocal(F, mp, th, init)
+    assert n == n_ref and np.array_equal(cur, mp_ref)
+    assert n > 200

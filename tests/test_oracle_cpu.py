@@ -166,3 +166,101 @@ def test_descriptor_distance_popcount():
         b = rng.integers(0, 256, 32, dtype=np.uint8)
         assert O.descriptor_distance(a, b) == int(np.unpackbits(a ^ b).sum())
     assert O.descriptor_distance(np.zeros(32, np.uint8), np.full(32, 255, np.uint8)) == 256
+
+
+def _py_features_in_area(kx, ky, oct_, W, H, x, y, r, minL, maxL):
+    """Frame::AssignFeaturesToGrid + GetFeaturesInArea restated in Python (R/src/Frame.cpp:244-260, 387-452)."""
+    winv, hinv = np.float32(64) / np.float32(W), np.float32(48) / np.float32(H)
+    grid = [[[] for _ in range(48)] for _ in range(64)]
+    for i in range(len(kx)):
+        px = int(np.round(np.float32(kx[i]) * winv))
+        py = int(np.round(np.float32(ky[i]) * hinv))
+        if 0 <= px < 64 and 0 <= py < 48:
+            grid[px][py].append(i)
+    x, y, r = np.float32(x), np.float32(y), np.float32(r)
+    cx0 = max(0, int(np.floor((x - r) * winv)))
+    if cx0 >= 64:
+        return []
+    cx1 = min(63, int(np.ceil((x + r) * winv)))
+    if cx1 < 0:
+        return []
+    cy0 = max(0, int(np.floor((y - r) * hinv)))
+    if cy0 >= 48:
+        return []
+    cy1 = min(47, int(np.ceil((y + r) * hinv)))
+    if cy1 < 0:
+        return []
+    check = minL > 0 or maxL >= 0
+    out = []
+    for ix in range(cx0, cx1 + 1):
+        for iy in range(cy0, cy1 + 1):
+            for i in grid[ix][iy]:
+                if check:
+                    if oct_[i] < minL:
+                        continue
+                    if maxL >= 0 and oct_[i] > maxL:
+                        continue
+                if abs(np.float32(kx[i]) - x) < r and abs(np.float32(ky[i]) - y) < r:
+                    out.append(i)
+    return out
+
+
+def test_search_by_projection_local_oracle_vs_python():
+    """The C oracle of SearchByProjection(Frame&, vector<MapPoint*>, th) against a literal
+    Python restatement of R/src/ORBmatcher.cpp:63-163 on a small random frame."""
+    rng = np.random.default_rng(3)
+    n, n_mp = 260, 220
+    from orb_slam2_amd import _abi
+    k = np.zeros(n, _abi.KEYPOINT_DTYPE)
+    k["x"] = rng.uniform(20, 620, n).astype(np.float32)
+    k["y"] = rng.uniform(20, 460, n).astype(np.float32)
+    k["octave"] = rng.integers(0, 4, n)
+    d = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    ur = np.where(rng.random(n) < 0.5, k["x"] - 10, -1).astype(np.float32)
+    src = rng.integers(0, n, n_mp)
+    proj = np.stack([k["x"][src] + rng.normal(0, 2, n_mp), k["y"][src] + rng.normal(0, 2, n_mp),
+                     k["x"][src] - 10 + rng.normal(0, 3, n_mp)], 1).astype(np.float32)
+    level = np.clip(k["octave"][src] + rng.integers(-1, 2, n_mp), 0, 3).astype(np.int32)
+    vcos = np.where(rng.random(n_mp) < 0.5, 0.999, 0.9).astype(np.float32)
+    md = d[src].copy()
+    md[np.arange(n_mp), rng.integers(0, 32, n_mp)] ^= 0x0F
+    md[rng.random(n_mp) < 0.3] = d[rng.integers(0, n, 1)]    # many near-ties
+    in_view = rng.random(n_mp) > 0.1
+    has_obs = rng.random(n_mp) > 0.2
+    sf = (np.float32(1.2) ** np.arange(8)).astype(np.float32)
+    init = np.full(n, -1, np.int32)
+    init[::13] = -2
+    init[4::17] = -3
+    th, nn = 2.0, 0.8
+    f = O.FrameView(k, d, 640, 480, uright=ur)
+    n_c, mp_c = O.search_by_projection_local(f, in_view, proj, level, vcos, md, has_obs, sf, nn, th, init)
+    cur = init.copy()
+    nm = 0
+    pop = lambda a: bin(int(a)).count("1")
+    for i in range(n_mp):
+        if not in_view[i]:
+            continue
+        L = int(level[i])
+        r = np.float32(2.5) if vcos[i] > np.float32(0.998) else np.float32(4.0)
+        r = np.float32(r * np.float32(th))
+        rad = np.float32(r * sf[L])
+        cand = _py_features_in_area(k["x"], k["y"], k["octave"], 640, 480, proj[i, 0], proj[i, 1], rad, L - 1, L)
+        bd, bl, bd2, bl2, bi = 256, -1, 256, -1, -1
+        for idx in cand:
+            s = cur[idx]
+            if s == -2 or (s >= 0 and has_obs[s]):
+                continue
+            if ur[idx] > 0 and abs(np.float32(proj[i, 2]) - ur[idx]) > rad:
+                continue
+            dist = sum(pop(a ^ b) for a, b in zip(md[i], d[idx]))
+            if dist < bd:
+                bd2, bl2, bd, bl, bi = bd, bl, dist, int(k["octave"][idx]), idx
+            elif dist < bd2:
+                bl2, bd2 = int(k["octave"][idx]), dist
+        if bd <= 100:
+            if bl == bl2 and np.float32(bd) > np.float32(nn) * np.float32(bd2):
+                continue
+            cur[bi] = i
+            nm += 1
+    assert nm == n_c and np.array_equal(cur, mp_c)
+    assert nm > 30
