@@ -118,6 +118,25 @@ int orb_extractor_geometry(orb_extractor* ex, int w, int h, int* level_w, int* l
  * after it, for frame `frame` of the last extraction (diagnostics / roofline). */
 int orb_extractor_last_counts(orb_extractor* ex, int frame, int* pre_counts, int* level_counts);
 
+/* Frame::ComputeStereoMatches (R/src/Frame.cpp:551-770) on the device, reading the two
+ * extractors' pyramids in place (no mvImagePyramid download).  `left` / `right` hold the
+ * extraction of the left / right image (frame 0 of their last call, same geometry); the
+ * keypoints / descriptors are those extractions' outputs (mvKeys / mvKeysRight, host).
+ * mbf = baseline x fx; mb = the baseline as the call sees it — the reference passes 0
+ * (its constructor sets mb afterwards), so maxD = mbf/mb = +inf.  Writes
+ * mvuRight / mvDepth (n_l floats, -1 = none); returns the number of stereo matches. */
+int orb_compute_stereo_matches(orb_extractor* left, orb_extractor* right, const orb_keypoint* kps_l,
+                               const uint8_t* desc_l, int n_l, const orb_keypoint* kps_r, const uint8_t* desc_r,
+                               int n_r, float mbf, float mb, float* uright, float* depth);
+
+/* Batched device form for stereo streams: the last orb_extract_batch_device call of `ex`
+ * held frames 2p (left) and 2p+1 (right) of n_pairs stereo pairs, with outputs d_kps /
+ * d_desc / d_counts as that call wrote them (cap keypoints per frame).  Writes
+ * d_uright / d_depth ([n_pairs][cap]) and d_nstereo[p].  Asynchronous on `stream`. */
+int orb_compute_stereo_matches_batch_device(orb_extractor* ex, const orb_keypoint* d_kps, const uint8_t* d_desc,
+                                            const int32_t* d_counts, int cap, int n_pairs, float mbf, float mb,
+                                            float* d_uright, float* d_depth, int32_t* d_nstereo, void* stream);
+
 /* --------------------------------------------------------------- matcher */
 
 typedef struct orb_matcher orb_matcher;

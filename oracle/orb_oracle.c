@@ -1116,6 +1116,133 @@ int oracle_search_by_projection_local(const oracle_frame* f, int n_mp, const uin
     return nmatches;
 }
 
+typedef struct { int dist, idx; } odistidx;
+static int cmp_distidx(const void* a, const void* b)
+{
+    const odistidx* x = (const odistidx*)a;
+    const odistidx* y = (const odistidx*)b;
+    if (x->dist != y->dist) return x->dist < y->dist ? -1 : 1;
+    return x->idx < y->idx ? -1 : (x->idx > y->idx);
+}
+
+int oracle_compute_stereo_matches(const uint8_t* const* pyr_l, const uint8_t* const* pyr_r, const int* lw,
+                                  const int* lh, const float* scale, const float* inv_scale,
+                                  const oracle_keypoint* kl, const uint8_t* dl, int nl,
+                                  const oracle_keypoint* kr, const uint8_t* dr, int nr,
+                                  float mbf, float mb, float* uright, float* depth)
+{
+    for (int i = 0; i < nl; i++) { uright[i] = -1.0f; depth[i] = -1.0f; }
+    const int thOrbDist = (TH_HIGH + TH_LOW) / 2;
+    const int nRows = lh[0];
+    /* vRowIndices: every right keypoint in the rows [floor(y - 2 s), ceil(y + 2 s)] */
+    int* rcount = (int*)calloc((size_t)nRows + 1, sizeof(int));
+    for (int iR = 0; iR < nr; iR++) {
+        const float kpY = kr[iR].y;
+        const float r = 2.0f * scale[kr[iR].octave];
+        const int maxr = (int)ceilf(kpY + r), minr = (int)floorf(kpY - r);
+        for (int yi = minr; yi <= maxr; yi++)
+            if (yi >= 0 && yi < nRows) rcount[yi + 1]++;
+    }
+    for (int y = 0; y < nRows; y++) rcount[y + 1] += rcount[y];
+    int* rows = (int*)malloc(sizeof(int) * ((size_t)rcount[nRows] + 1));
+    int* fill = (int*)malloc(sizeof(int) * ((size_t)nRows + 1));
+    memcpy(fill, rcount, sizeof(int) * (size_t)nRows);
+    for (int iR = 0; iR < nr; iR++) {
+        const float kpY = kr[iR].y;
+        const float r = 2.0f * scale[kr[iR].octave];
+        const int maxr = (int)ceilf(kpY + r), minr = (int)floorf(kpY - r);
+        for (int yi = minr; yi <= maxr; yi++)
+            if (yi >= 0 && yi < nRows) rows[fill[yi]++] = iR;
+    }
+    const float minZ = mb;
+    const float minD = 0;
+    const float maxD = mbf / minZ;
+    odistidx* vd = (odistidx*)malloc(sizeof(odistidx) * ((size_t)nl + 1));
+    int nvd = 0;
+    for (int iL = 0; iL < nl; iL++) {
+        const oracle_keypoint* kpL = &kl[iL];
+        const int levelL = kpL->octave;
+        const float vL = kpL->y, uL = kpL->x;
+        const int row = (int)vL;                 /* vRowIndices[vL]: float -> size_t */
+        if (row < 0 || row >= nRows || rcount[row] == rcount[row + 1]) continue;
+        const float minU = uL - maxD, maxU = uL - minD;
+        if (maxU < 0) continue;
+        int bestDist = TH_HIGH;
+        int bestIdxR = 0;
+        for (int c = rcount[row]; c < rcount[row + 1]; c++) {
+            const int iR = rows[c];
+            if (kr[iR].octave < levelL - 1 || kr[iR].octave > levelL + 1) continue;
+            const float uR = kr[iR].x;
+            if (uR >= minU && uR <= maxU) {
+                const int dist = oracle_descriptor_distance(dl + (size_t)iL * 32, dr + (size_t)iR * 32);
+                if (dist < bestDist) { bestDist = dist; bestIdxR = iR; }
+            }
+        }
+        if (bestDist >= thOrbDist) continue;
+        /* SAD refinement on level kpL.octave (coordinates rounded half away from zero: round()) */
+        const float uR0 = kr[bestIdxR].x;
+        const float sf = inv_scale[levelL];
+        const float scaleduL = roundf(kpL->x * sf);
+        const float scaledvL = roundf(kpL->y * sf);
+        const float scaleduR0 = roundf(uR0 * sf);
+        const int w = 5, L = 5;
+        const int W = lw[levelL];
+        const uint8_t* IL = pyr_l[levelL];
+        const uint8_t* IR = pyr_r[levelL];
+        const int cy = (int)scaledvL, cxl = (int)scaleduL, cxr0 = (int)scaleduR0;
+        const float iniu = scaleduR0 + L - w;
+        const float endu = scaleduR0 + L + w + 1;
+        if (iniu < 0 || endu >= lw[levelL]) continue;
+        int bestSad = INT_MAX, bestincR = 0;
+        float vDists[11];
+        const float cL = (float)IL[(size_t)cy * W + cxl];
+        for (int incR = -L; incR <= L; incR++) {
+            const float cR = (float)IR[(size_t)cy * W + cxr0 + incR];
+            double acc = 0.0;                    /* cv::norm(NORM_L1) of CV_32F: double sum */
+            for (int dy = -w; dy <= w; dy++)
+                for (int dx = -w; dx <= w; dx++) {
+                    const float a = (float)IL[(size_t)(cy + dy) * W + cxl + dx] - cL;
+                    const float b = (float)IR[(size_t)(cy + dy) * W + cxr0 + incR + dx] - cR;
+                    acc += fabs((double)a - (double)b);
+                }
+            const float dist = (float)acc;
+            if (dist < (float)bestSad) { bestSad = (int)dist; bestincR = incR; }
+            vDists[L + incR] = dist;
+        }
+        if (bestincR == -L || bestincR == L) continue;
+        const float dist1 = vDists[L + bestincR - 1], dist2 = vDists[L + bestincR], dist3 = vDists[L + bestincR + 1];
+        const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
+        if (deltaR < -1 || deltaR > 1) continue;
+        float bestuR = scale[levelL] * ((float)scaleduR0 + (float)bestincR + deltaR);
+        float disparity = uL - bestuR;
+        if (disparity >= minD && disparity < maxD) {
+            if (disparity <= 0) {
+                disparity = (float)0.01;
+                bestuR = (float)((double)uL - 0.01);
+            }
+            depth[iL] = mbf / disparity;
+            uright[iL] = bestuR;
+            vd[nvd].dist = bestSad;
+            vd[nvd].idx = iL;
+            nvd++;
+        }
+    }
+    int kept = nvd;
+    if (nvd > 0) {
+        qsort(vd, (size_t)nvd, sizeof(odistidx), cmp_distidx);
+        const float median = (float)vd[nvd / 2].dist;
+        const float thDist = 1.5f * 1.4f * median;
+        for (int i = nvd - 1; i >= 0; i--) {
+            if ((float)vd[i].dist < thDist) break;
+            uright[vd[i].idx] = -1;
+            depth[vd[i].idx] = -1;
+            kept--;
+        }
+    }
+    free(vd); free(fill); free(rows); free(rcount);
+    return kept;
+}
+
 void oracle_hamming_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt,
                          int32_t* best_idx, int32_t* best_d, int32_t* second_d)
 {

@@ -146,6 +146,20 @@ int oracle_search_by_projection_local(const oracle_frame* f, int n_mp, const uin
                                       const uint8_t* mp_desc, const uint8_t* has_obs,
                                       const float* scale_factors, float nnratio, float th, int32_t* cur_mp);
 
+/* Frame::ComputeStereoMatches (R/src/Frame.cpp:551-770): row-band candidates, best Hamming
+ * distance below (TH_HIGH+TH_LOW)/2, 11x11 SAD over +-5 px on the keypoint's pyramid level,
+ * parabola sub-pixel fit, disparity gate and the 2.1 x median SAD cut.  pyr_l / pyr_r:
+ * nlevels level images (row stride = level width) of the left / right extractors'
+ * mvImagePyramid; lw / lh: level sizes.  scale / inv_scale: mvScaleFactors /
+ * mvInvScaleFactors.  mb is the baseline as seen by the call — 0 in the reference, whose
+ * constructor sets mb only afterwards, giving maxD = mbf/0 = +inf.  Writes
+ * uright / depth (N_left floats, -1 = none); returns the number of stereo matches kept. */
+int oracle_compute_stereo_matches(const uint8_t* const* pyr_l, const uint8_t* const* pyr_r, const int* lw,
+                                  const int* lh, const float* scale, const float* inv_scale,
+                                  const oracle_keypoint* kl, const uint8_t* dl, int nl,
+                                  const oracle_keypoint* kr, const uint8_t* dr, int nr,
+                                  float mbf, float mb, float* uright, float* depth);
+
 /* Brute-force Hamming k=2 (best, second) with lowest-index tie break. */
 void oracle_hamming_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt,
                          int32_t* best_idx, int32_t* best_d, int32_t* second_d);

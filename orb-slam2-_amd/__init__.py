@@ -5,3 +5,4 @@ from . import _abi  # noqa: F401
 from .extractor import ORBextractor  # noqa: F401
 from .matcher import ORBmatcher, Frame, LocalMapPoints  # noqa: F401
 from .optimizer import Optimizer, LocalBA  # noqa: F401
+from .stereo import ComputeStereoMatches  # noqa: F401

@@ -69,6 +69,8 @@ def lib() -> C.CDLL:
             "orb_search_for_initialization": [vp, vp, vp, vp, vp, i32],
             "orb_search_by_projection_frame": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32, i32, vp],
             "orb_search_by_projection_local": [vp, vp, i32, vp, vp, vp, vp, vp, vp, vp, f32, vp],
+            "orb_compute_stereo_matches": [vp, vp, vp, vp, i32, vp, vp, i32, f32, f32, vp, vp],
+            "orb_compute_stereo_matches_batch_device": [vp, vp, vp, vp, i32, i32, f32, f32, vp, vp, vp, vp],
             "orb_hamming_knn2": [vp, vp, i32, vp, i32, vp, vp, vp],
             "orb_hamming_knn2_batch_device": [vp, vp, vp, vp, vp, i32, i32, i32, vp, vp, vp, vp],
             "orb_search_for_initialization_batch_device": [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32,

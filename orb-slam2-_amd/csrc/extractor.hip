@@ -1500,6 +1500,189 @@ __global__ __launch_bounds__(256) void k_load_frames(Geom g, const uint8_t* __re
     }
 }
 
+// ------------------------------------------------------------------ stereo: Frame::ComputeStereoMatches
+
+struct StereoTabs {
+    float scale[kMaxLevels], inv[kMaxLevels];
+};
+
+// One wave per left keypoint (R/src/Frame.cpp:551-747): right keypoints of the row band
+// [floor(y - 2s), ceil(y + 2s)] (vRowIndices, ascending index), octave within +-1 and
+// uL - maxD <= uR <= uL; best Hamming distance (strict <, below TH_HIGH); if below
+// (TH_HIGH+TH_LOW)/2, the 11 x 11 SAD (centre-normalised windows, cv::norm L1 of integer-valued
+// floats = exact integer sums) at 11 offsets on the keypoint's level, parabola fit and the
+// disparity gate.  Pair p's left / right data: kL + p*kStride etc.; pyramids pyrL + p*pyStride.
+__global__ __launch_bounds__(256) void k_stereo_match(Geom g, StereoTabs tb, const uint8_t* __restrict__ pyrL,
+                                                      const uint8_t* __restrict__ pyrR, size_t pyStride,
+                                                      const orb_keypoint* __restrict__ kL, const uint8_t* __restrict__ dL,
+                                                      const int32_t* __restrict__ nLs, const orb_keypoint* __restrict__ kR,
+                                                      const uint8_t* __restrict__ dR, const int32_t* __restrict__ nRs,
+                                                      int kStride, int cntStride, int kCap, float mbf, float maxD,
+                                                      float* __restrict__ ur, float* __restrict__ depth,
+                                                      int32_t* __restrict__ sad, int outStride) {
+    __shared__ int rowsad[4][128];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int p = blockIdx.y;
+    const int iL = blockIdx.x * 4 + wid;
+    const int nl = nLs[(size_t)p * cntStride], nr = nRs[(size_t)p * cntStride];
+    if (iL >= min(nl, kCap)) return;
+    const orb_keypoint* KL = kL + (size_t)p * kStride;
+    const orb_keypoint* KR = kR + (size_t)p * kStride;
+    float* UR = ur + (size_t)p * outStride;
+    float* DP = depth + (size_t)p * outStride;
+    int32_t* SD = sad + (size_t)p * outStride;
+    const orb_keypoint kp = KL[iL];
+    const int levelL = kp.octave;
+    const float uL = kp.x, vL = kp.y;
+    const int row = (int)vL;   // vRowIndices[vL]: float -> size_t
+    const float minU = uL - maxD, maxU = uL;   // minD = 0
+    bool done = maxU < 0 || row < 0 || row >= g.lv[0].h || levelL < 0 || levelL >= g.nlevels;
+    unsigned long long best = ~0ull;
+    if (!done) {
+        const uint4* q4 = reinterpret_cast<const uint4*>(dL + ((size_t)p * kStride + iL) * 32);
+        const uint4 qa = q4[0], qb = q4[1];
+        for (int j0 = 0; j0 < min(nr, kCap); j0 += 64) {
+            const int j = j0 + lane;
+            unsigned long long key = ~0ull;
+            if (j < min(nr, kCap)) {
+                const orb_keypoint k2 = KR[j];
+                const float r = 2.0f * tb.scale[k2.octave];
+                const int maxr = (int)ceilf(k2.y + r), minr = (int)floorf(k2.y - r);
+                if (row >= minr && row <= maxr && k2.octave >= levelL - 1 && k2.octave <= levelL + 1 && k2.x >= minU &&
+                    k2.x <= maxU) {
+                    const uint4* d4 = reinterpret_cast<const uint4*>(dR + ((size_t)p * kStride + j) * 32);
+                    const uint4 a0 = d4[0], a1 = d4[1];
+                    const int dist = __popc(a0.x ^ qa.x) + __popc(a0.y ^ qa.y) + __popc(a0.z ^ qa.z) +
+                                     __popc(a0.w ^ qa.w) + __popc(a1.x ^ qb.x) + __popc(a1.y ^ qb.y) +
+                                     __popc(a1.z ^ qb.z) + __popc(a1.w ^ qb.w);
+                    if (dist < 100) key = ((unsigned long long)(unsigned)dist << 32) | (unsigned)j;   // TH_HIGH
+                }
+            }
+            for (int o = 32; o >= 1; o >>= 1) {
+                const unsigned long long v = __shfl_xor(key, o, 64);
+                key = v < key ? v : key;
+            }
+            best = key < best ? key : best;
+        }
+        done = best == ~0ull || (int)(best >> 32) >= 75;   // thOrbDist = (TH_HIGH+TH_LOW)/2
+    }
+    float outU = -1.0f, outD = -1.0f;
+    int outS = -1;
+    if (!done) {
+        const int bestIdxR = (int)(best & 0xFFFFFFFFull);
+        const float uR0 = KR[bestIdxR].x;
+        const float sf = tb.inv[levelL];
+        const int cx = (int)roundf(uL * sf), cy = (int)roundf(vL * sf), cr = (int)roundf(uR0 * sf);
+        const LevelGeom& Lg = g.lv[levelL];
+        // iniu = scaleduR0 + L - w, endu = scaleduR0 + L + w + 1 (R :705-708); the windows must also lie
+        // inside the level (the reference's cv::Mat ranges would assert otherwise)
+        const bool ok = cr >= 0 && cr + 11 < Lg.w && cr - 10 >= 0 && cx - 5 >= 0 && cx + 5 < Lg.w && cy - 5 >= 0 &&
+                        cy + 5 < Lg.h;
+        if (ok) {
+            const uint8_t* IL = pyrL + (size_t)p * pyStride + Lg.off;
+            const uint8_t* IR = pyrR + (size_t)p * pyStride + Lg.off;
+            const int P = Lg.pitch;
+            const int cL = IL[(size_t)cy * P + cx];
+            for (int c = lane; c < 121; c += 64) {
+                const int inc = c / 11 - 5, dy = c % 11 - 5;
+                const int cR = IR[(size_t)cy * P + cr + inc];
+                const uint8_t* rl = IL + (size_t)(cy + dy) * P + cx - 5;
+                const uint8_t* rr = IR + (size_t)(cy + dy) * P + cr + inc - 5;
+                int acc = 0;
+#pragma unroll
+                for (int dx = 0; dx < 11; dx++) acc += abs(((int)rl[dx] - cL) - ((int)rr[dx] - cR));
+                rowsad[wid][c] = acc;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            int vD[11];
+#pragma unroll
+            for (int i = 0; i < 11; i++) {
+                int sacc = 0;
+#pragma unroll
+                for (int dy = 0; dy < 11; dy++) sacc += rowsad[wid][i * 11 + dy];
+                vD[i] = sacc;
+            }
+            int bestSad = INT_MAX, bestinc = 0;
+#pragma unroll
+            for (int i = 0; i < 11; i++)
+                if ((float)vD[i] < (float)bestSad) { bestSad = vD[i]; bestinc = i - 5; }
+            if (bestinc != -5 && bestinc != 5) {
+                const float d1 = (float)vD[bestinc + 4], d2 = (float)vD[bestinc + 5], d3 = (float)vD[bestinc + 6];
+                const float deltaR = (d1 - d3) / (2.0f * (d1 + d3 - 2.0f * d2));
+                if (!(deltaR < -1 || deltaR > 1)) {
+                    float bestuR = tb.scale[levelL] * (((float)cr + (float)bestinc) + deltaR);
+                    float disparity = uL - bestuR;
+                    if (disparity >= 0 && disparity < maxD) {
+                        if (disparity <= 0) {
+                            disparity = 0.01f;
+                            bestuR = (float)((double)uL - 0.01);
+                        }
+                        outD = mbf / disparity;
+                        outU = bestuR;
+                        outS = bestSad;
+                    }
+                }
+            }
+        }
+    }
+    if (lane == 0) {
+        UR[iL] = outU;
+        DP[iL] = outD;
+        SD[iL] = outS;
+    }
+}
+
+// The 2.1 x median SAD cut (R/src/Frame.cpp:749-769), one workgroup per stereo pair: the
+// median of the kept (SAD, index) pairs in ascending order, then every entry at or above
+// 1.5f*1.4f*median is dropped.  n_kept[p] receives the surviving count.
+__global__ __launch_bounds__(1024) void k_stereo_median(const int32_t* __restrict__ nLs, int cntStride, int kCap,
+                                                        float* __restrict__ ur, float* __restrict__ depth,
+                                                        const int32_t* __restrict__ sad, int outStride,
+                                                        int32_t* __restrict__ nKept, unsigned long long* __restrict__ keys) {
+    __shared__ int cnt, med, kept;
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const int n = min((int)nLs[(size_t)p * cntStride], kCap);
+    float* UR = ur + (size_t)p * outStride;
+    float* DP = depth + (size_t)p * outStride;
+    const int32_t* SD = sad + (size_t)p * outStride;
+    unsigned long long* K = keys + (size_t)p * outStride;
+    if (tid == 0) { cnt = 0; med = -1; kept = 0; }
+    __syncthreads();
+    for (int i = tid; i < n; i += 1024) {
+        const int s = SD[i];
+        if (s >= 0) K[atomicAdd(&cnt, 1)] = ((unsigned long long)(unsigned)s << 32) | (unsigned)i;
+    }
+    __syncthreads();
+    const int m = cnt;
+    if (m == 0) {
+        if (tid == 0) nKept[p] = 0;
+        return;
+    }
+    for (int i = tid; i < m; i += 1024) {
+        const unsigned long long k = K[i];
+        int rank = 0;
+        for (int j = 0; j < m; j++) rank += K[j] < k;
+        if (rank == m / 2) med = (int)(k >> 32);
+    }
+    __syncthreads();
+    const float thDist = 1.5f * 1.4f * (float)med;
+    int mine = 0;
+    for (int i = tid; i < m; i += 1024) {
+        const unsigned long long k = K[i];
+        const int idx = (int)(k & 0xFFFFFFFFull);
+        if ((float)(int)(k >> 32) < thDist) {
+            mine++;
+        } else {
+            UR[idx] = -1.0f;
+            DP[idx] = -1.0f;
+        }
+    }
+    atomicAdd(&kept, mine);
+    __syncthreads();
+    if (tid == 0) nKept[p] = kept;
+}
+
 // ------------------------------------------------------------------ host handle
 
 int check_device(int dev) {
@@ -1531,6 +1714,11 @@ struct orb_extractor {
     int gw = -1, gh = -1;
     int blurK[4];
     uint2* d_rztab = nullptr;        // resize coefficient tables of the current geometry
+    // stereo scratch (orb_compute_stereo_matches*)
+    void* d_st = nullptr;
+    size_t st_bytes = 0;
+    void* h_st = nullptr;
+    size_t h_st_bytes = 0;
     bool blurValid = false;          // d_blur holds the blurred pyramid of the last extraction
     hipStream_t lastStream = nullptr;
     size_t capFrames = 0, capFrameBytes = 0, capSlots = 0, capOut = 0, capCells = 0;
@@ -1781,6 +1969,8 @@ void orb_extractor_destroy(orb_extractor* ex) {
     if (ex->stream) (void)hipStreamSynchronize(ex->stream);
     release_buffers(ex);
     if (ex->d_rztab) (void)hipFree(ex->d_rztab);
+    if (ex->d_st) (void)hipFree(ex->d_st);
+    if (ex->h_st) (void)hipHostFree(ex->h_st);
     for (auto& set : ex->ev_sets)
         for (auto e : set) ex->ev_pool.push_back(e);
     for (auto e : ex->ev_pool) (void)hipEventDestroy(e);
@@ -1987,6 +2177,104 @@ int orb_extractor_last_counts(orb_extractor* ex, int frame, int* pre_counts, int
         if (pre_counts) pre_counts[l] = s;
         if (level_counts) level_counts[l] = lc[l];
     }
+    return ORB_OK;
+}
+
+static int stereo_scratch(orb_extractor* ex, size_t bytes) {
+    if (ex->st_bytes >= bytes) return ORB_OK;
+    if (ex->d_st) (void)hipFree(ex->d_st);
+    ex->d_st = nullptr;
+    ex->st_bytes = 0;
+    if (hipMalloc(&ex->d_st, bytes) != hipSuccess) return ORB_ENOMEM;
+    ex->st_bytes = bytes;
+    return ORB_OK;
+}
+
+static StereoTabs stereo_tabs(const orb_extractor* ex) {
+    StereoTabs tb;
+    std::memset(&tb, 0, sizeof(tb));
+    host_tables(ex->p, tb.scale, tb.inv, nullptr, nullptr, nullptr);
+    return tb;
+}
+
+int orb_compute_stereo_matches(orb_extractor* left, orb_extractor* right, const orb_keypoint* kps_l,
+                               const uint8_t* desc_l, int n_l, const orb_keypoint* kps_r, const uint8_t* desc_r,
+                               int n_r, float mbf, float mb, float* uright, float* depth) {
+    if (!left || !right || n_l < 0 || n_r < 0 || (n_l && (!kps_l || !desc_l || !uright || !depth)) || (n_r && (!kps_r || !desc_r)))
+        return ORB_EINVAL;
+    for (int i = 0; i < n_l; i++) { uright[i] = -1.0f; depth[i] = -1.0f; }
+    if (n_l == 0) return 0;
+    if (left->gw < 0 || left->gw != right->gw || left->gh != right->gh || left->lastB < 1 || right->lastB < 1 ||
+        left->p.nlevels != right->p.nlevels || left->device != right->device)
+        return ORB_EINVAL;   // both extractors must hold an extraction of the same geometry
+    ORB_HIP_TRY(hipSetDevice(left->device));
+    const int cap = std::max(n_l, n_r);
+    const size_t kb = (size_t)cap * sizeof(orb_keypoint), db = (size_t)cap * 32, ob = (size_t)cap * 4;
+    const size_t bytes = 2 * kb + 2 * db + 3 * ob + (size_t)cap * 8 + 64;
+    int st = stereo_scratch(left, bytes);
+    if (st) return st;
+    st = ensure_pinned(&left->h_st, &left->h_st_bytes, bytes);
+    if (st) return st;
+    char* d = (char*)left->d_st;
+    orb_keypoint* dkl = (orb_keypoint*)d;
+    orb_keypoint* dkr = (orb_keypoint*)(d + kb);
+    uint8_t* ddl = (uint8_t*)(d + 2 * kb);
+    uint8_t* ddr = ddl + db;
+    float* dur = (float*)(ddr + db);
+    float* ddp = dur + cap;
+    int32_t* dsd = (int32_t*)(ddp + cap);
+    unsigned long long* dkeys = (unsigned long long*)(((uintptr_t)(dsd + cap) + 7) & ~(uintptr_t)7);
+    int32_t* dn = (int32_t*)(dkeys + cap);
+    char* h = (char*)left->h_st;
+    int32_t* hn = (int32_t*)(h + bytes - 16);
+    hn[0] = n_l;
+    hn[1] = n_r;
+    hipStream_t s = left->stream;
+    // the right extractor's pyramid must be complete before this stream reads it
+    ORB_HIP_TRY(hipStreamSynchronize(right->lastStream ? right->lastStream : right->stream));
+    ORB_HIP_TRY(hipMemcpyAsync(dkl, kps_l, (size_t)n_l * sizeof(orb_keypoint), hipMemcpyHostToDevice, s));
+    if (n_r) ORB_HIP_TRY(hipMemcpyAsync(dkr, kps_r, (size_t)n_r * sizeof(orb_keypoint), hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(ddl, desc_l, (size_t)n_l * 32, hipMemcpyHostToDevice, s));
+    if (n_r) ORB_HIP_TRY(hipMemcpyAsync(ddr, desc_r, (size_t)n_r * 32, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(dn, hn, 8, hipMemcpyHostToDevice, s));
+    const float maxD = mbf / mb;   // mb = 0 in the reference: +inf
+    hipLaunchKernelGGL(k_stereo_match, dim3((n_l + 3) / 4, 1), dim3(256), 0, s, left->g, stereo_tabs(left),
+                       left->d_pyr, right->d_pyr, (size_t)0, dkl, ddl, dn, dkr, ddr, dn + 1, cap, 1, cap, mbf, maxD, dur,
+                       ddp, dsd, cap);
+    hipLaunchKernelGGL(k_stereo_median, dim3(1), dim3(1024), 0, s, dn, 1, cap, dur, ddp, dsd, cap, dn + 2, dkeys);
+    ORB_HIP_TRY(hipGetLastError());
+    float* hur = (float*)h;
+    float* hdp = hur + cap;
+    ORB_HIP_TRY(hipMemcpyAsync(hur, dur, (size_t)n_l * 4, hipMemcpyDeviceToHost, s));
+    ORB_HIP_TRY(hipMemcpyAsync(hdp, ddp, (size_t)n_l * 4, hipMemcpyDeviceToHost, s));
+    ORB_HIP_TRY(hipMemcpyAsync(hn + 2, dn + 2, 4, hipMemcpyDeviceToHost, s));
+    ORB_HIP_TRY(hipStreamSynchronize(s));
+    std::memcpy(uright, hur, (size_t)n_l * 4);
+    std::memcpy(depth, hdp, (size_t)n_l * 4);
+    return hn[2];
+}
+
+int orb_compute_stereo_matches_batch_device(orb_extractor* ex, const orb_keypoint* d_kps, const uint8_t* d_desc,
+                                            const int32_t* d_counts, int cap, int n_pairs, float mbf, float mb,
+                                            float* d_uright, float* d_depth, int32_t* d_nstereo, void* stream) {
+    if (!ex || !d_kps || !d_desc || !d_counts || cap <= 0 || n_pairs <= 0 || !d_uright || !d_depth || !d_nstereo)
+        return ORB_EINVAL;
+    if (ex->gw < 0 || ex->lastB < 2 * n_pairs) return ORB_EINVAL;   // frames 2p (left), 2p+1 (right)
+    ORB_HIP_TRY(hipSetDevice(ex->device));
+    const size_t bytes = (size_t)n_pairs * cap * (4 + 8) + 64;
+    int st = stereo_scratch(ex, bytes);
+    if (st) return st;
+    int32_t* dsd = (int32_t*)ex->d_st;
+    unsigned long long* dkeys = (unsigned long long*)(((uintptr_t)(dsd + (size_t)n_pairs * cap) + 7) & ~(uintptr_t)7);
+    hipStream_t s = stream ? (hipStream_t)stream : ex->stream;
+    const Geom& g = ex->g;
+    const float maxD = mbf / mb;
+    hipLaunchKernelGGL(k_stereo_match, dim3((cap + 3) / 4, n_pairs), dim3(256), 0, s, g, stereo_tabs(ex), ex->d_pyr,
+                       ex->d_pyr + g.frameBytes, (size_t)(2 * g.frameBytes), d_kps, d_desc, d_counts, d_kps + cap,
+                       d_desc + (size_t)cap * 32, d_counts + 1, 2 * cap, 2, cap, mbf, maxD, d_uright, d_depth, dsd, cap);
+    hipLaunchKernelGGL(k_stereo_median, dim3(n_pairs), dim3(1024), 0, s, d_counts, 2, cap, d_uright, d_depth, dsd, cap,
+                       d_nstereo, dkeys);
+    ORB_HIP_TRY(hipGetLastError());
     return ORB_OK;
 }
 

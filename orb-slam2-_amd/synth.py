@@ -49,6 +49,26 @@ def frame(cv: np.ndarray, W: int, H: int, t: int) -> np.ndarray:
     return np.ascontiguousarray(cv[oy:oy + H, ox:ox + W])
 
 
+def disparity_field(W: int, H: int, lo: int = 5, hi: int = 60) -> np.ndarray:
+    """Smooth integer disparity field d(x, y) in [lo, hi]."""
+    y, x = np.mgrid[0:H, 0:W].astype(np.float64)
+    f = 0.5 + 0.25 * np.sin(2 * np.pi * x / W * 1.3 + 0.7) + 0.25 * np.cos(2 * np.pi * y / H * 0.9 + 0.3)
+    return np.rint(lo + (hi - lo) * f).astype(np.int32)
+
+
+def stereo_pair(cv: np.ndarray, W: int, H: int, t: int):
+    """Left = frame t of the canvas crop; right(x, y) = left(x + d(x, y), y) with the smooth
+    disparity field, so a left point at u appears at u - d in the right image."""
+    ox = (W // 2 + 2 * t) % W
+    oy = (H // 2 + t) % H
+    big = cv[oy:oy + H, ox:ox + W + 64]
+    left = np.ascontiguousarray(big[:, :W])
+    d = disparity_field(W, H)
+    xs = np.minimum(np.arange(W)[None, :] + d, big.shape[1] - 1)
+    right = np.ascontiguousarray(np.take_along_axis(big, xs, axis=1))
+    return left, right
+
+
 def stream(seed: int, W: int, H: int, n: int) -> np.ndarray:
     cv = canvas(seed, W, H)
     return np.stack([frame(cv, W, H, t) for t in range(n)])

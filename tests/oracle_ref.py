@@ -205,6 +205,25 @@ def search_by_projection_local(f, in_view, proj, level, view_cos, mp_desc, has_o
     return n, cur_mp
 
 
+def compute_stereo_matches(params, ex_l, ex_r, mbf, mb=0.0):
+    """ex_l / ex_r: oracle extract(..., want_pyramid=True) outputs of the left / right images."""
+    t = tables(params)
+    lw, lh = ex_l["sizes"]
+    lw = np.ascontiguousarray(lw, np.int32)
+    lh = np.ascontiguousarray(lh, np.int32)
+    offs = np.concatenate([[0], np.cumsum(lw.astype(np.int64) * lh)])
+    pl = (C.c_void_p * len(lw))(*[ex_l["pyramid"].ctypes.data + int(offs[i]) for i in range(len(lw))])
+    pr = (C.c_void_p * len(lw))(*[ex_r["pyramid"].ctypes.data + int(offs[i]) for i in range(len(lw))])
+    kl, kr = np.ascontiguousarray(ex_l["kps"]), np.ascontiguousarray(ex_r["kps"])
+    dl, dr = np.ascontiguousarray(ex_l["desc"], np.uint8), np.ascontiguousarray(ex_r["desc"], np.uint8)
+    ur = np.zeros(len(kl), np.float32)
+    dep = np.zeros(len(kl), np.float32)
+    n = lib().oracle_compute_stereo_matches(pl, pr, P(lw), P(lh), P(t["scale"]), P(t["inv_scale"]), P(kl), P(dl),
+                                            len(kl), P(kr), P(dr), len(kr), C.c_float(mbf), C.c_float(mb), P(ur),
+                                            P(dep))
+    return n, ur, dep
+
+
 def hamming_knn2(q, t):
     q = np.ascontiguousarray(q, np.uint8)
     t = np.ascontiguousarray(t, np.uint8)

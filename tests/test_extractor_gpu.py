@@ -103,3 +103,69 @@ def test_noise_image_retry_threshold(amd):
     ref = O.extract(O.params(1000), img)
     kps, desc = ex(img)
     _compare(ref, kps, desc)
+
+
+@pytest.mark.parametrize("W,H,nf,seed,mbf", [(752, 480, 1200, 0x5EED0005, 47.9), (640, 480, 1000, 0x5EED0006, 40.0)])
+def test_compute_stereo_matches(amd, W, H, nf, seed, mbf):
+    """Frame::ComputeStereoMatches on the GPU (pyramids read in place) vs the oracle on a
+    synthetic stereo pair with a smooth disparity field."""
+    from orb_slam2_amd import synth
+    cv = synth.canvas(seed, W, H)
+    left, right = synth.stereo_pair(cv, W, H, 0)
+    p = O.params(nf)
+    a = O.extract(p, left, want_pyramid=True)
+    b = O.extract(p, right, want_pyramid=True)
+    n_ref, ur_ref, dep_ref = O.compute_stereo_matches(p, a, b, mbf)
+    exL = amd.ORBextractor(nf, 1.2, 8, 20, 7, max_w=W, max_h=H)
+    exR = amd.ORBextractor(nf, 1.2, 8, 20, 7, max_w=W, max_h=H)
+    kl, dl = exL(left)
+    kr, dr = exR(right)
+    _compare(a, kl, dl)
+    _compare(b, kr, dr)
+    n, ur, dep = amd.ComputeStereoMatches(exL, exR, kl, dl, kr, dr, mbf)
+    assert n == n_ref
+    assert np.array_equal(ur, ur_ref) and np.array_equal(dep, dep_ref)
+    assert n > 300
+
+
+def test_compute_stereo_matches_batch_device(amd):
+    """Device batch form: 3 stereo pairs extracted as frames (2p, 2p+1) of one batch."""
+    import torch
+    from orb_slam2_amd import synth, _abi
+    import ctypes as C
+    W, H, nf, mbf = 752, 480, 1200, 47.9
+    cv = synth.canvas(0x5EED0005, W, H)
+    pairs = [synth.stereo_pair(cv, W, H, t) for t in range(3)]
+    imgs = np.stack([im for pr in pairs for im in pr])
+    dev = torch.device("cuda", 0)
+    ex = amd.ORBextractor(nf, 1.2, 8, 20, 7, max_w=W, max_h=H, max_batch=6)
+    cap = C.c_int()
+    _abi.check("geom", _abi.lib().orb_extractor_geometry(ex._h, W, H, None, None, None, C.byref(cap)))
+    cap = cap.value
+    ti = torch.from_numpy(imgs).to(dev)
+    kps = torch.zeros((6, cap, 7), dtype=torch.int32, device=dev)
+    desc = torch.zeros((6, cap, 32), dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(6, dtype=torch.int32, device=dev)
+    ur = torch.zeros((3, cap), dtype=torch.float32, device=dev)
+    dep = torch.zeros((3, cap), dtype=torch.float32, device=dev)
+    ns = torch.zeros(3, dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    lib = _abi.lib()
+    _abi.check("x", lib.orb_extract_batch_device(ex._h, C.c_void_p(ti.data_ptr()), H * W, 6, W, H,
+                                                  C.c_void_p(kps.data_ptr()), C.c_void_p(desc.data_ptr()), cap,
+                                                  C.c_void_p(cnt.data_ptr()), C.c_void_p(s)))
+    _abi.check("s", lib.orb_compute_stereo_matches_batch_device(
+        ex._h, C.c_void_p(kps.data_ptr()), C.c_void_p(desc.data_ptr()), C.c_void_p(cnt.data_ptr()), cap, 3,
+        C.c_float(mbf), C.c_float(0.0), C.c_void_p(ur.data_ptr()), C.c_void_p(dep.data_ptr()),
+        C.c_void_p(ns.data_ptr()), C.c_void_p(s)))
+    torch.cuda.synchronize(dev)
+    p = O.params(nf)
+    for i, (l, r) in enumerate(pairs):
+        a = O.extract(p, l, want_pyramid=True)
+        b = O.extract(p, r, want_pyramid=True)
+        n_ref, ur_ref, dep_ref = O.compute_stereo_matches(p, a, b, mbf)
+        nl = len(a["kps"])
+        assert int(cnt[2 * i]) == nl
+        assert int(ns[i]) == n_ref
+        assert np.array_equal(ur[i, :nl].cpu().numpy(), ur_ref)
+        assert np.array_equal(dep[i, :nl].cpu().numpy(), dep_ref)

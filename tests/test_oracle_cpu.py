@@ -264,3 +264,85 @@ def test_search_by_projection_local_oracle_vs_python():
             nm += 1
     assert nm == n_c and np.array_equal(cur, mp_c)
     assert nm > 30
+
+
+def test_compute_stereo_matches_oracle_vs_python():
+    """The C oracle of Frame::ComputeStereoMatches against a literal Python restatement of
+    R/src/Frame.cpp:551-770 (with mb = 0 at call time) on a synthetic stereo pair."""
+    from orb_slam2_amd import synth
+    W, H = 752, 480
+    cv = synth.canvas(0x5EED0005, W, H)
+    left, right = synth.stereo_pair(cv, W, H, 0)
+    p = O.params(1200)
+    a = O.extract(p, left, want_pyramid=True)
+    b = O.extract(p, right, want_pyramid=True)
+    mbf = 47.9
+    n_c, ur_c, dep_c = O.compute_stereo_matches(p, a, b, mbf)
+    t = O.tables(p)
+    lw, lh = a["sizes"]
+    offs = np.concatenate([[0], np.cumsum(np.asarray(lw, np.int64) * lh)])
+    lev = lambda pyr, l: pyr[offs[l]:offs[l + 1]].reshape(lh[l], lw[l]).astype(np.int64)
+    kl, kr = a["kps"], b["kps"]
+    popc = np.array([bin(i).count("1") for i in range(256)])
+    rows = [[] for _ in range(lh[0])]
+    for iR in range(len(kr)):
+        r = np.float32(2.0) * t["scale"][kr["octave"][iR]]
+        for yi in range(int(np.floor(kr["y"][iR] - r)), int(np.ceil(kr["y"][iR] + r)) + 1):
+            rows[yi].append(iR)
+    maxD = np.float32(np.inf)
+    ur = np.full(len(kl), -1.0, np.float32)
+    dep = np.full(len(kl), -1.0, np.float32)
+    vd = []
+    for iL in range(len(kl)):
+        lv, uL, vL = int(kl["octave"][iL]), np.float32(kl["x"][iL]), np.float32(kl["y"][iL])
+        cands = rows[int(vL)]
+        if not cands:
+            continue
+        best, bi = 100, 0
+        for iR in cands:
+            if kr["octave"][iR] < lv - 1 or kr["octave"][iR] > lv + 1:
+                continue
+            if kr["x"][iR] <= uL:
+                dist = int(popc[a["desc"][iL] ^ b["desc"][iR]].sum())
+                if dist < best:
+                    best, bi = dist, iR
+        if best >= 75:
+            continue
+        sf = t["inv_scale"][lv]
+        rnd = lambda v: np.float32(np.sign(v) * np.floor(np.abs(v) + np.float32(0.5)))   # round(): half away
+        cx, cy, cr = int(rnd(np.float32(uL * sf))), int(rnd(np.float32(vL * sf))), int(rnd(np.float32(kr["x"][bi] * sf)))
+        if cr < 0 or cr + 11 >= lw[lv]:
+            continue
+        IL, IR = lev(a["pyramid"], lv), lev(b["pyramid"], lv)
+        wl = IL[cy - 5:cy + 6, cx - 5:cx + 6] - IL[cy, cx]
+        dists = []
+        for inc in range(-5, 6):
+            wr = IR[cy - 5:cy + 6, cr + inc - 5:cr + inc + 6] - IR[cy, cr + inc]
+            dists.append(float(np.abs(wl - wr).sum()))
+        bs = int(np.argmin(dists))
+        binc = bs - 5
+        if binc in (-5, 5):
+            continue
+        d1, d2, d3 = (np.float32(dists[bs - 1]), np.float32(dists[bs]), np.float32(dists[bs + 1]))
+        with np.errstate(divide="ignore", invalid="ignore"):
+            delta = np.float32((d1 - d3) / (np.float32(2.0) * (d1 + d3 - np.float32(2.0) * d2)))
+        if not (-1 <= delta <= 1):
+            continue
+        bu = np.float32(t["scale"][lv] * np.float32(np.float32(np.float32(cr) + np.float32(binc)) + delta))
+        disp = np.float32(uL - bu)
+        if disp >= 0 and disp < maxD:
+            if disp <= 0:
+                disp, bu = np.float32(0.01), np.float32(np.float64(uL) - 0.01)
+            dep[iL] = np.float32(np.float32(mbf) / disp)
+            ur[iL] = bu
+            vd.append((int(dists[bs]), iL))
+    vd.sort()
+    if vd:
+        th = np.float32(np.float32(1.5) * np.float32(1.4)) * np.float32(vd[len(vd) // 2][0])
+        for dist, iL in reversed(vd):
+            if np.float32(dist) < th:
+                break
+            ur[iL] = -1
+            dep[iL] = -1
+    assert np.array_equal(ur, ur_c) and np.array_equal(dep, dep_c)
+    assert n_c == int((ur >= 0).sum()) and n_c > 300
