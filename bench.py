@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--lba-solves", type=int, default=5, help="timed LocalBundleAdjustment calls")
     ap.add_argument("--lba-points", type=int, default=3000)
     ap.add_argument("--lba-kf", type=int, default=20)
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the secondary legs (brute-force 2-NN, stereo config 5, KITTI config 3)")
     return ap.parse_args()
 
 
@@ -161,6 +163,121 @@ def bench_lba(args, amd, dev, local, rank, world):
                                "sample": f"{n} LocalBundleAdjustment solves, oracle C restatement of g2o "
                                          f"LM+Schur (dense LDLT), 1 thread (reference builds g2o without OpenMP)"}
         out["speedup_vs_cpu"] = round(out["cpu_baseline"]["ms_per_iter"] / out["ms_per_iter"], 2)
+    return out
+
+
+def _extract_leg(amd, dev, frames, nf, steps, warmup, pairs_fn=None):
+    """Times batched extraction of an HBM-resident frame array (one step = all frames)
+    plus an optional per-step device function; returns (seconds per step, extractor, buffers)."""
+    from orb_slam2_amd import _abi
+    B, H, W = frames.shape
+    ex = amd.ORBextractor(nf, 1.2, 8, 20, 7, device=dev.index or 0, max_w=W, max_h=H, max_batch=B)
+    cap = C.c_int()
+    _abi.check("geom", _abi.lib().orb_extractor_geometry(ex._h, W, H, None, None, None, C.byref(cap)))
+    cap = cap.value
+    imgs = torch.from_numpy(frames).to(dev)
+    kps = torch.zeros((B, cap, 7), dtype=torch.int32, device=dev)
+    desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(B, dtype=torch.int32, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    lib = _abi.lib()
+    buf = dict(ex=ex, cap=cap, kps=kps, desc=desc, cnt=cnt, stream=st, lib=lib)
+
+    def step():
+        _abi.check("x", lib.orb_extract_batch_device(ex._h, C.c_void_p(imgs.data_ptr()), H * W, B, W, H,
+                                                      C.c_void_p(kps.data_ptr()), C.c_void_p(desc.data_ptr()), cap,
+                                                      C.c_void_p(cnt.data_ptr()), C.c_void_p(st)))
+        if pairs_fn is not None:
+            pairs_fn(buf)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    return (time.perf_counter() - t0) / steps, buf
+
+
+def bench_extras(args, amd, dev):
+    """Secondary legs of SURVEY §8d: (ii) all-pairs 2-NN Hamming throughput (integer-VALU
+    roofline: 16 lane-ops per 256-bit pair), config 5 stereo (EuRoC 752x480, 1200 feat,
+    extraction of both images + ComputeStereoMatches), config 3 (KITTI 1241x376, 2000 feat,
+    extract + SearchForInitialization)."""
+    from orb_slam2_amd import synth, _abi
+    lib = _abi.lib()
+    out = {}
+    # ---- (ii) brute-force 2-NN between consecutive frames' descriptors (1000 x 1000 per pair)
+    W, H, B = 640, 480, 64
+    cv = synth.canvas(0x5EED0002, W, H)
+    frames = np.stack([synth.frame(cv, W, H, t) for t in range(B + 1)])
+    _, buf = _extract_leg(amd, dev, frames, 1000, 1, 1)
+    m = amd.ORBmatcher(0.9, True, device=dev.index or 0)
+    cap = buf["cap"]
+    nq = buf["cnt"][:-1].clone()
+    bi = torch.zeros((B, cap), dtype=torch.int32, device=dev)
+    bd = torch.zeros_like(bi)
+    sd = torch.zeros_like(bi)
+    d = buf["desc"]
+    st = buf["stream"]
+
+    def knn():
+        _abi.check("knn", lib.orb_hamming_knn2_batch_device(
+            m._h, C.c_void_p(d.data_ptr()), C.c_void_p(nq.data_ptr()), C.c_void_p(d.data_ptr() + cap * 32),
+            C.c_void_p(buf["cnt"].data_ptr() + 4), B, cap, cap, C.c_void_p(bi.data_ptr()), C.c_void_p(bd.data_ptr()),
+            C.c_void_p(sd.data_ptr()), C.c_void_p(st)))
+    for _ in range(3):
+        knn()
+    torch.cuda.synchronize(dev)
+    reps = 20
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        knn()
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) / reps
+    c = buf["cnt"].cpu().numpy().astype(np.int64)
+    pairs = float((c[:-1] * c[1:]).sum())
+    peak_pairs = 256 * 64 * 2.4e9 / 16
+    out["knn2_bruteforce"] = {"pairs_per_s": round(pairs / dt, 1), "ms_per_batch": round(dt * 1e3, 4),
+                              "frame_pairs": B, "roofline": {"bound": "valu", "unit": "pairs/s",
+                                                             "peak": peak_pairs, "frac": round(pairs / dt / peak_pairs, 4)}}
+    # ---- config 5: stereo pairs (left frames 2p, right 2p+1), extraction + ComputeStereoMatches
+    W, H, P = 752, 480, 32
+    cv = synth.canvas(0x5EED0005, W, H)
+    fr = np.stack([im for t in range(P) for im in synth.stereo_pair(cv, W, H, t)])
+    ur = torch.zeros((P, 4096), dtype=torch.float32, device=dev)
+    dep = torch.zeros_like(ur)
+    ns = torch.zeros(P, dtype=torch.int32, device=dev)
+
+    def stereo(b):
+        _abi.check("stereo", lib.orb_compute_stereo_matches_batch_device(
+            b["ex"]._h, C.c_void_p(b["kps"].data_ptr()), C.c_void_p(b["desc"].data_ptr()),
+            C.c_void_p(b["cnt"].data_ptr()), b["cap"], P, C.c_float(47.9), C.c_float(0.0), C.c_void_p(ur.data_ptr()),
+            C.c_void_p(dep.data_ptr()), C.c_void_p(ns.data_ptr()), C.c_void_p(b["stream"])))
+    dt, b = _extract_leg(amd, dev, fr, 1200, 10, 3, stereo)
+    out["stereo_euroc_752x480"] = {"stereo_frames_per_s": round(P / dt, 1), "ms_per_step": round(dt * 1e3, 4),
+                                   "pairs_per_step": P, "stereo_matches_per_frame": float(ns.float().mean()),
+                                   "config": "synthetic stereo pairs (smooth disparity 5..60 px), 1200 feat, mb=0 "
+                                             "(reference call order), both images extracted + ComputeStereoMatches"}
+    # ---- config 3: KITTI geometry, 2000 features, extract + SearchForInitialization
+    W, H, B = 1241, 376, 64
+    cv = synth.canvas(0x5EED0003, W, H)
+    fr = np.stack([synth.frame(cv, W, H, t) for t in range(B)])
+    m12 = torch.zeros((B - 1, 8192), dtype=torch.int32, device=dev)
+    nm = torch.zeros(B - 1, dtype=torch.int32, device=dev)
+
+    def sfi(b):
+        cp = b["cap"]
+        _abi.check("sfi", lib.orb_search_for_initialization_batch_device(
+            m._h, C.c_void_p(b["kps"].data_ptr()), C.c_void_p(b["desc"].data_ptr()), C.c_void_p(b["cnt"].data_ptr()),
+            C.c_void_p(b["kps"].data_ptr() + cp * 28), C.c_void_p(b["desc"].data_ptr() + cp * 32),
+            C.c_void_p(b["cnt"].data_ptr() + 4), B - 1, cp, W, H, 100, C.c_void_p(m12.data_ptr()),
+            C.c_void_p(nm.data_ptr()), C.c_void_p(b["stream"])))
+    dt, b = _extract_leg(amd, dev, fr, 2000, 10, 3, sfi)
+    out["kitti_1241x376"] = {"frames_per_s": round(B / dt, 1), "ms_per_step": round(dt * 1e3, 4),
+                             "keypoints_per_frame": float(b["cnt"].float().mean()),
+                             "matches_per_pair": float(nm.float().mean())}
     return out
 
 
@@ -306,8 +423,15 @@ def main():
                               "launch_ms": round(float(per_launch_ms[dom]), 4)}
         result["stage_ms_per_batch"] = {k: round(float(v), 4) for k, v in zip(STAGES, per_launch_ms)
                                         if not k.startswith("reserved")}
+    # whole-pipeline roofline of SURVEY §8d: B_ext = P0 + 2 sum_{l>=1} P_l + N_kp (28 + 32) per frame
+    P = (lw.astype(np.int64) * lh)
+    b_ext = float(P[0] + 2 * P[1:].sum()) + float(np.mean(cnt)) * 60.0
+    result["pipeline_roofline"] = {"bytes_per_frame": b_ext, "achieved_gbs": round(b_ext * value / 1e9, 2),
+                                   "peak_gbs": HBM_PEAK_GBS, "frac": round(b_ext * value / 1e9 / HBM_PEAK_GBS, 5)}
     if not args.no_lba:
         result["lba"] = bench_lba(args, amd, dev, local, rank, world)
+    if world == 1 and not args.no_extras:
+        result["extras"] = bench_extras(args, amd, dev)
     if rank == 0 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(pool_np[: min(len(pool_np), 512)], NF, args.cpu_seconds)
         result["speedup_vs_cpu_baseline"] = round(value / result["cpu_baseline"]["value"], 1)
