@@ -31,6 +31,24 @@ import pkgload  # noqa: E402
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md)
 STAGES = ["resize", "fast_detect", "reserved", "octree", "reserved2", "orient_blur_desc"]
 KERNELS = ["k_resize", "k_fast_cell", None, "k_octree", None, "k_orient_desc"]
+PMC_TRAFFIC = ROOT / "profiles" / "r01_pmc_traffic.json"   # tools/pmc_run.sh + tools/pmc_traffic.py
+
+
+def pmc_traffic(kernel, W, H, NF, Bs):
+    """HBM bytes per bench stage launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes.
+
+    PMC counters cannot be read inside the timed run (gpurun forbids mixing them with traces, and
+    counter collection serialises dispatches), so they come from a separate profiling pass of this
+    same bench configuration; None when that pass does not match the current configuration."""
+    try:
+        doc = json.loads(PMC_TRAFFIC.read_text())
+        cfg = doc["config"]
+        if (int(cfg["width"]), int(cfg["height"]), int(cfg["nfeatures"]), int(cfg["frames_per_launch"])) \
+                != (W, H, NF, Bs):
+            return None
+        return int(doc["kernels"][kernel]["traffic_bytes_per_batch"])
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def parse():
@@ -360,7 +378,11 @@ def main():
         step(s)
     torch.cuda.synchronize(dev)
     if not args.no_profile:
-        lib.orb_extractor_profile(ex._h, 1)
+        # every stream's extractor records its stage events: with S streams sharing the chip a
+        # launch overlapped by another stream's kernels runs longer than one that is alone, and the
+        # rocprofv3 per-kernel average (profiles/) is over all of them
+        for p in pipes:
+            lib.orb_extractor_profile(p.ex._h, 1)
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
@@ -379,8 +401,12 @@ def main():
     stage_ms = np.zeros(6)
     ncalls = C.c_int(0)
     if not args.no_profile:
-        lib.orb_extractor_stage_times(ex._h, _abi.ptr(stage_ms), 6, C.byref(ncalls))
-        lib.orb_extractor_profile(ex._h, 0)
+        for p in pipes:
+            sm, nc = np.zeros(6), C.c_int(0)
+            lib.orb_extractor_stage_times(p.ex._h, _abi.ptr(sm), 6, C.byref(nc))
+            lib.orb_extractor_profile(p.ex._h, 0)
+            stage_ms += sm
+            ncalls.value += nc.value
     frames_total = B * args.steps * world
     value = frames_total / dt
     cnt = torch.cat([p.counts[1:] for p in pipes]).cpu().numpy()
@@ -421,6 +447,11 @@ def main():
                               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                               "traffic": None,
                               "launch_ms": round(float(per_launch_ms[dom]), 4)}
+        tr = pmc_traffic(KERNELS[dom], W, H, NF, Bs)
+        if tr is not None:
+            result["roofline"]["traffic"] = tr
+            result["roofline"]["traffic_unit"] = "bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)"
+            result["roofline"]["traffic_source"] = PMC_TRAFFIC.name
         result["stage_ms_per_batch"] = {k: round(float(v), 4) for k, v in zip(STAGES, per_launch_ms)
                                         if not k.startswith("reserved")}
     # whole-pipeline roofline of SURVEY §8d: B_ext = P0 + 2 sum_{l>=1} P_l + N_kp (28 + 32) per frame

@@ -69,4 +69,19 @@ __device__ __forceinline__ int wave_reduce_sum_i32(int v) {
     return v;
 }
 
+// XCD-aware 2-D block index.  Workgroups are dealt round-robin over the 8 XCDs (dispatch id d
+// lands on XCD d % 8; observed placement, MI355X_MICROARCH.md "Workgroup dispatch"), so blocks
+// that are neighbours in (x, y) order land on different L2s and each XCD re-fetches the lines the
+// neighbours share.  Remap so each XCD walks one contiguous range of logical blocks (frames and
+// image rows stay on one L2).  Speed only: the map is a bijection on [0, gx*gy) whatever the
+// placement (the tail beyond the last multiple of 8 keeps its own index).
+__device__ __forceinline__ void xcd_block_2d(int& bx, int& by) {
+    const int gx = gridDim.x, G = gx * gridDim.y;
+    int d = blockIdx.y * gx + blockIdx.x;
+    const int q = G >> 3;
+    if (d < (q << 3)) d = (d & 7) * q + (d >> 3);
+    by = d / gx;
+    bx = d - by * gx;
+}
+
 }  // namespace orbamd

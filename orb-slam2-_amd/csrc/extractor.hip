@@ -381,8 +381,9 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
     TSTAMP(t_fc0);
     extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int b = blockIdx.y;
-    const int c = blockIdx.x * 4 + wid;
+    int bx, b;
+    xcd_block_2d(bx, b);
+    const int c = bx * 4 + wid;
     if (c >= g.cellsPerFrame) return;
     const int l = level_of_cell(g, c);
     const LevelGeom& L = g.lv[l];
@@ -1330,8 +1331,9 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
                                                      uint32_t kA, uint32_t kB) {
     __shared__ __attribute__((aligned(16))) unsigned char od_sm[4][kOdWaveBytes];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int b = blockIdx.y;
-    const int q = blockIdx.x * 4 + wid;
+    int bx, b;
+    xcd_block_2d(bx, b);
+    const int q = bx * 4 + wid;
     const int* lc = levelCount + (size_t)b * g.nlevels;
     if (q == 0 && lane == 0) {
         int tot = 0;

@@ -237,8 +237,9 @@ __global__ __launch_bounds__(256) void k_cand_sfi(const orb_keypoint* __restrict
     __shared__ int segOff[4][kGridCols + 1];
     __shared__ uint32_t sj[4][kMaxCand];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int b = blockIdx.y;
-    const int i1 = blockIdx.x * 4 + wid;
+    int bx, b;
+    xcd_block_2d(bx, b);
+    const int i1 = bx * 4 + wid;
     const int n1 = min((int)n1s[b], cap);
     if (i1 >= n1) return;
     const orb_keypoint* K1 = kps1 + (size_t)b * cap;
@@ -932,8 +933,9 @@ __global__ __launch_bounds__(256) void k_knn2(const uint8_t* __restrict__ q, con
                                               int tStride, int32_t* __restrict__ bi, int32_t* __restrict__ bd,
                                               int32_t* __restrict__ sd) {
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int b = blockIdx.y;
-    const int i = blockIdx.x * 4 + wid;
+    int bx, b;
+    xcd_block_2d(bx, b);
+    const int i = bx * 4 + wid;
     const int nq = nqs[b], nt = nts[b];
     if (i >= nq) return;
     const uint8_t* dq = q + ((size_t)b * qStride + i) * 32;
