@@ -296,7 +296,81 @@ def bench_extras(args, amd, dev):
     out["kitti_1241x376"] = {"frames_per_s": round(B / dt, 1), "ms_per_step": round(dt * 1e3, 4),
                              "keypoints_per_frame": float(b["cnt"].float().mean()),
                              "matches_per_pair": float(nm.float().mean())}
+    out["batch_sweep_640x480"] = batch_sweep(amd, dev, m)
     return out
+
+
+def batch_sweep(amd, dev, m):
+    """extract + SearchForInitialization at batch sizes B in {1, 8, 64} on one stream,
+    HBM-resident (B-1 in-batch pairs; B=1 is extraction alone), and the PCIe-inclusive rate at
+    B=64: pinned host frames copied in, keypoints + descriptors + matches copied back, per step."""
+    from orb_slam2_amd import synth, _abi
+    lib = _abi.lib()
+    W, H, NF = 640, 480, 1000
+    cv = synth.canvas(0x5EED0002, W, H)
+    res = {}
+    for B in (1, 8, 64):
+        fr = np.stack([synth.frame(cv, W, H, t) for t in range(B)])
+        m12 = torch.zeros((max(B - 1, 1), 4096), dtype=torch.int32, device=dev)
+        nm = torch.zeros(max(B - 1, 1), dtype=torch.int32, device=dev)
+
+        def sfi(b, B=B, m12=m12, nm=nm):
+            if B < 2:
+                return
+            cp = b["cap"]
+            _abi.check("sfi", lib.orb_search_for_initialization_batch_device(
+                m._h, C.c_void_p(b["kps"].data_ptr()), C.c_void_p(b["desc"].data_ptr()),
+                C.c_void_p(b["cnt"].data_ptr()), C.c_void_p(b["kps"].data_ptr() + cp * 28),
+                C.c_void_p(b["desc"].data_ptr() + cp * 32), C.c_void_p(b["cnt"].data_ptr() + 4), B - 1, cp, W, H,
+                100, C.c_void_p(m12.data_ptr()), C.c_void_p(nm.data_ptr()), C.c_void_p(b["stream"])))
+        dt, b = _extract_leg(amd, dev, fr, NF, 20 if B < 64 else 10, 3, sfi)
+        res[f"B{B}"] = {"frames_per_s": round(B / dt, 1), "ms_per_step": round(dt * 1e3, 4)}
+    # PCIe-inclusive, B = 64: H2D of the frames, extraction + matching, D2H of the results
+    B = 64
+    fr = np.stack([synth.frame(cv, W, H, t) for t in range(B)])
+    host_in = torch.from_numpy(fr).pin_memory()
+    ex = amd.ORBextractor(NF, 1.2, 8, 20, 7, device=dev.index or 0, max_w=W, max_h=H, max_batch=B)
+    cap = C.c_int()
+    _abi.check("geom", lib.orb_extractor_geometry(ex._h, W, H, None, None, None, C.byref(cap)))
+    cap = cap.value
+    imgs = torch.empty((B, H, W), dtype=torch.uint8, device=dev)
+    kps = torch.zeros((B, cap, 7), dtype=torch.int32, device=dev)
+    desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(B, dtype=torch.int32, device=dev)
+    m12 = torch.zeros((B - 1, cap), dtype=torch.int32, device=dev)
+    nm = torch.zeros(B - 1, dtype=torch.int32, device=dev)
+    h_kps = torch.empty(kps.shape, dtype=kps.dtype).pin_memory()
+    h_desc = torch.empty(desc.shape, dtype=desc.dtype).pin_memory()
+    h_m12 = torch.empty(m12.shape, dtype=m12.dtype).pin_memory()
+    st = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        imgs.copy_(host_in, non_blocking=True)
+        _abi.check("x", lib.orb_extract_batch_device(ex._h, C.c_void_p(imgs.data_ptr()), H * W, B, W, H,
+                                                      C.c_void_p(kps.data_ptr()), C.c_void_p(desc.data_ptr()), cap,
+                                                      C.c_void_p(cnt.data_ptr()), C.c_void_p(st)))
+        _abi.check("sfi", lib.orb_search_for_initialization_batch_device(
+            m._h, C.c_void_p(kps.data_ptr()), C.c_void_p(desc.data_ptr()), C.c_void_p(cnt.data_ptr()),
+            C.c_void_p(kps.data_ptr() + cap * 28), C.c_void_p(desc.data_ptr() + cap * 32),
+            C.c_void_p(cnt.data_ptr() + 4), B - 1, cap, W, H, 100, C.c_void_p(m12.data_ptr()),
+            C.c_void_p(nm.data_ptr()), C.c_void_p(st)))
+        h_kps.copy_(kps, non_blocking=True)
+        h_desc.copy_(desc, non_blocking=True)
+        h_m12.copy_(m12, non_blocking=True)
+
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize(dev)
+    reps = 10
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        step()
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) / reps
+    res["B64_pcie_inclusive"] = {"frames_per_s": round(B / dt, 1), "ms_per_step": round(dt * 1e3, 4),
+                                 "h2d_bytes": int(host_in.numel()),
+                                 "d2h_bytes": int(kps.numel() * 4 + desc.numel() + m12.numel() * 4)}
+    return res
 
 
 def main():
