@@ -465,31 +465,37 @@ static int schur_solve(lba_ctx* c, double lambda)
     for (int i = 0; i < np; i++) bs[i] = (root ? c->bp[i] : 0.0) - coef[i];
     allreduce(c, S, np * np, 0);
     allreduce(c, bs, np, 0);
-    /* dense LDL^T (no pivoting); fails only on an exactly zero pivot, like SimplicialLDLT */
+    /* dense LDL^T (no pivoting); fails only on an exactly zero pivot, like SimplicialLDLT.
+     * Crout order, one fused multiply-add per update: with W(i,k) = A(i,k) before the
+     * division by d_k (kept in the upper triangle at (k, i)) and L(i,k) = W(i,k) / d_k (lower),
+     * A(i,j) = fma(-W(i,k), L(j,k), A(i,j)) for k = 0 .. j-1.  SimplicialLDLT's own order
+     * (AMD-permuted, sparse) is not reproducible without Eigen; this recurrence is the one the
+     * GPU factorisation (k_ldlt_solve) follows element for element. */
     int ok = 1;
     double* d = (double*)malloc(sizeof(double) * (np + 1));
     for (int j = 0; j < np && ok; j++) {
         double dj = S[j * np + j];
-        for (int k = 0; k < j; k++) dj -= S[j * np + k] * S[j * np + k] * d[k];
+        for (int k = 0; k < j; k++) dj = fma(-S[k * np + j], S[j * np + k], dj);
         if (dj == 0.0 || !isfinite(dj)) { ok = 0; break; }
         d[j] = dj;
         for (int i = j + 1; i < np; i++) {
             double v = S[i * np + j];
-            for (int k = 0; k < j; k++) v -= S[i * np + k] * S[j * np + k] * d[k];
-            S[i * np + j] = v / dj;
+            for (int k = 0; k < j; k++) v = fma(-S[k * np + i], S[j * np + k], v);
+            S[j * np + i] = v;        /* W(i, j) */
+            S[i * np + j] = v / dj;   /* L(i, j) */
         }
     }
     double* xp = c->x;
     if (ok) {
         for (int i = 0; i < np; i++) {
             double v = bs[i];
-            for (int k = 0; k < i; k++) v -= S[i * np + k] * xp[k];
+            for (int k = 0; k < i; k++) v = fma(-S[i * np + k], xp[k], v);
             xp[i] = v;
         }
         for (int i = 0; i < np; i++) xp[i] /= d[i];
         for (int i = np - 1; i >= 0; i--) {
             double v = xp[i];
-            for (int k = i + 1; k < np; k++) v -= S[k * np + i] * xp[k];
+            for (int k = i + 1; k < np; k++) v = fma(-S[k * np + i], xp[k], v);
             xp[i] = v;
         }
         /* landmarks: x_l = Dinv (b_l - Hpl^T x_p) */

@@ -440,42 +440,46 @@ __global__ __launch_bounds__(64) void k_bschur(LbaDev d, int addBp) {
     }
 }
 
-// Dense LDL^T (no pivoting; fails only on a zero pivot, like SimplicialLDLT) + solve, one
-// workgroup of 256 threads.  The n x n matrix is staged in LDS when it fits (n <= 136, i.e.
-// up to 22 free keyframes), otherwise factored in place in global memory (L2-resident).
-// Right-looking elimination in panels of kLdltW columns: wave 0 factors a panel (column j:
-// L(:,j) = A(:,j)/d_j, then the panel's later columns take A(i,k) -= (L_ij L_kj) d_j) with
-// wave-level ordering only, then all threads apply the panel's rank-1 updates to the
-// trailing lower triangle, each element in column order — the same rounding sequence as the
-// column-by-column algorithm, with two workgroup barriers per panel instead of per column.
-// The triangular solves run column-oriented on one wave.
 constexpr int kLdltW = 8;     // panel width (columns per pair of workgroup barriers)
-constexpr int kLdltT = 256;
+constexpr int kLdltT = 512;   // 8 waves: 2 per SIMD for the trailing update
 constexpr int kLdltMaxN = 192; // panel rows held in registers: 3 per lane
 
-__device__ __forceinline__ double shfl_d(double v, int src) { return __shfl(v, src, 64); }
+// Broadcast of lane `src` (a compile-time constant at every call site) through two
+// v_readlane_b32 into SGPRs: a few cycles, against a ds_bpermute round trip for __shfl.
+__device__ __forceinline__ double shfl_d(double v, int src) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, src);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), src);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
 
 // Dense LDL^T (no pivoting; fails only on a zero pivot, like SimplicialLDLT) + solve, one
-// workgroup of 256 threads; the n x n matrix is staged in LDS when it fits (n <= 136, i.e. up
-// to 22 free keyframes), otherwise factored in place in global memory (L2-resident).
-// Right-looking elimination in panels of kLdltW columns:
+// workgroup of kLdltT threads; the n x n matrix is staged in LDS when it fits (n <= 136, i.e.
+// up to 22 free keyframes), otherwise factored in place in global memory (L2-resident).
+// Element recurrence (oracle/lba_oracle.c states it column by column): with W(i,k) the value
+// of A(i,k) before the division by d_k and L(i,k) = W(i,k)/d_k,
+//     A(i,j) = fma(-W(i,k), L(j,k), A(i,j))   for k = 0 .. j-1 in order,
+// one fused multiply-add per update (against (L_ik L_jk) d_k, three rounded operations).
+// W is kept in the upper triangle, L in the lower.  Right-looking in panels of kLdltW columns:
 //  * wave 0 factors the panel in registers (3 panel rows per lane, pivots and L entries
-//    broadcast with shuffles): L(:,j) = A(:,j)/d_j, then A(i,k) -= (L_ij L_kj) d_j for the
-//    panel's later columns;
-//  * all threads apply the panel's rank-1 updates to the trailing lower triangle in 4 x 4
-//    register tiles, each element taking the updates in column order.
-// Every element therefore sees exactly the operation sequence of the column-by-column
-// algorithm (same rounding), with two workgroup barriers per panel instead of per column.
-// The triangular solves are blocked the same way on one wave.
+//    broadcast with v_readlane);
+//  * all threads apply the panel's updates to the trailing lower triangle in 4 x 4 register
+//    tiles, each element taking them in column order;
+// so every element sees the recurrence's exact operation sequence, with two workgroup barriers
+// per panel.  The triangular solves (y_i = fma(-L_ik, y_k, y_i), k in order) are blocked the
+// same way on one wave.
 template <bool kLds>
 __global__ __launch_bounds__(kLdltT) void k_ldlt_solve(double* __restrict__ Ag, const double* __restrict__ b, int n,
                                                        double* __restrict__ x, int* __restrict__ flags) {
     extern __shared__ __attribute__((aligned(16))) double sh[];
     TSTAMP(t_l0);
-    long long tPanel = 0, tTrail = 0;
-    (void)tPanel; (void)tTrail;
+    long long tPanel = 0, tTrail = 0, tPLoad = 0, tPCol = 0, tFLoad = 0, tFChain = 0, tFRows = 0;
+    (void)tPanel; (void)tTrail; (void)tPLoad; (void)tPCol; (void)tFLoad; (void)tFChain; (void)tFRows;
+    // LDS rows padded to an odd number of doubles: the panel's column accesses (lanes one row
+    // apart) then spread over the banks instead of hitting a few of them
+    const int ld = kLds ? (n | 1) : n;
     double* A = kLds ? sh : Ag;
-    double* dg = sh + (kLds ? (size_t)n * n : 0);
+    double* dg = sh + (kLds ? (size_t)n * ld : 0);
     double* y = dg + n;
     __shared__ int failS;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -485,8 +489,10 @@ __global__ __launch_bounds__(kLdltT) void k_ldlt_solve(double* __restrict__ Ag, 
 #pragma unroll
             for (int u = 0; u < 8; u++) v[u] = t0 + u * kLdltT + tid < n * n ? Ag[t0 + u * kLdltT + tid] : 0.0;
 #pragma unroll
-            for (int u = 0; u < 8; u++)
-                if (t0 + u * kLdltT + tid < n * n) A[t0 + u * kLdltT + tid] = v[u];
+            for (int u = 0; u < 8; u++) {
+                const int t = t0 + u * kLdltT + tid;
+                if (t < n * n) A[(size_t)(t / n) * ld + t % n] = v[u];
+            }
         }
     }
     for (int t = tid; t < n; t += kLdltT) y[t] = b[t];
@@ -499,15 +505,26 @@ __global__ __launch_bounds__(kLdltT) void k_ldlt_solve(double* __restrict__ Ag, 
         const int je = min(jb + kLdltW, n);
         TSTAMP(t_p0);
         if (tid < 64) {
-            // ---- panel [jb, je) on wave 0: lane holds rows jb + lane + 64u
+            // ---- panel [jb, je) on wave 0: lane holds rows jb + lane + 64u (zeros past row n
+            //      and column je; those are never stored).  Column j: d_j = A(j,j); W(i,j) =
+            //      A(i,j) before the division goes to the upper triangle at (j, i), L(i,j) =
+            //      W(i,j)/d_j to the lower; the panel's later columns take
+            //      A(i,k) = fma(-W(i,j), L(k,j), A(i,k)).  Every lane runs the same code: the
+            //      values computed on or above the diagonal are not stored.
             double P[3][kLdltW];
 #pragma unroll
             for (int u = 0; u < 3; u++) {
                 const int r = jb + lane + 64 * u;
 #pragma unroll
-                for (int c = 0; c < kLdltW; c++) P[u][c] = (r < n && jb + c < je) ? A[(size_t)r * n + jb + c] : 0.0;
+                for (int c = 0; c < kLdltW; c++) P[u][c] = (r < n && jb + c < je) ? A[(size_t)r * ld + jb + c] : 0.0;
             }
+            double Wp[3][kLdltW] = {};   // W of the panel's columns, stored after the column loop
             bool bad = false;
+#ifdef ORB_TIMING
+            __builtin_amdgcn_s_waitcnt(0);
+#endif
+            TACC(tPLoad, t_p0);
+            TSTAMP(t_pc0);
 #pragma unroll
             for (int c = 0; c < kLdltW; c++) {
                 const int j = jb + c;
@@ -516,56 +533,66 @@ __global__ __launch_bounds__(kLdltT) void k_ldlt_solve(double* __restrict__ Ag, 
                     if (dj == 0.0 || !isfinite(dj)) {
                         bad = true;
                     } else {
+                        double w[3];
 #pragma unroll
-                        for (int u = 0; u < 3; u++)
-                            if (jb + lane + 64 * u > j) P[u][c] = P[u][c] / dj;
-                        if (lane == 0) dg[j] = dj;
-#pragma unroll
-                        for (int k = c + 1; k < kLdltW; k++) {
-                            const double lk = shfl_d(P[0][c], k);   // L(jb+k, j)
-#pragma unroll
-                            for (int u = 0; u < 3; u++)
-                                if (jb + k < je && jb + lane + 64 * u >= jb + k) P[u][k] -= (P[u][c] * lk) * dj;
+                        for (int u = 0; u < 3; u++) {
+                            w[u] = P[u][c];
+                            Wp[u][c] = w[u];
+                            P[u][c] = w[u] / dj;
                         }
+                        if (lane == 0) dg[j] = dj;
+                        double lkv[kLdltW];
+#pragma unroll
+                        for (int k = c + 1; k < kLdltW; k++) lkv[k] = shfl_d(P[0][c], k);   // L(jb+k, j)
+#pragma unroll
+                        for (int k = c + 1; k < kLdltW; k++)
+#pragma unroll
+                            for (int u = 0; u < 3; u++) P[u][k] = __builtin_fma(-w[u], lkv[k], P[u][k]);
                     }
                 }
             }
             if (bad && lane == 0) failS = 1;
+#ifdef ORB_TIMING
+            if (P[0][kLdltW - 1] == 12345.0) failS = 2;   // keeps the timer after the column loop
+#endif
+            TACC(tPCol, t_pc0);
 #pragma unroll
             for (int u = 0; u < 3; u++) {
                 const int r = jb + lane + 64 * u;
 #pragma unroll
                 for (int c = 0; c < kLdltW; c++)
-                    if (r < n && jb + c < je) A[(size_t)r * n + jb + c] = P[u][c];
+                    if (r < n && r > jb + c && jb + c < je) {
+                        A[(size_t)r * ld + jb + c] = P[u][c];      // L(r, jb+c), strict lower
+                        A[(size_t)(jb + c) * ld + r] = Wp[u][c];   // W(r, jb+c) at (jb+c, r)
+                    }
             }
         }
         __syncthreads();
         TACC(tPanel, t_p0);
         TSTAMP(t_t0);
         if (failS) break;
-        // ---- trailing lower triangle (rows, columns >= je) in 4 x 4 tiles; 16 x 16 thread
-        //      grid: thread (ty, tx) owns tile rows ty+16a and tile columns tx+16c (c <= a)
+        // ---- trailing lower triangle (rows, columns >= je) in 4 x 4 tiles: thread (ty, tx)
+        //      owns tile rows ty + 32a and tile columns tx + 16c (c <= a); element (i, k) takes
+        //      A(i,k) = fma(-W(i,p), L(k,p), A(i,k)) for the panel's columns p in order
         {
             const int m = n - je, T = (m + 3) >> 2;
             const int ty = tid >> 4, tx = tid & 15;
-            double d[kLdltW];
+            for (int ti = ty; ti < T; ti += kLdltT / 16) {
+                double wi[4][kLdltW];
 #pragma unroll
-            for (int p = 0; p < kLdltW; p++) d[p] = jb + p < je ? dg[jb + p] : 0.0;
-            for (int ti = ty; ti < T; ti += 16) {
-                double li[4][kLdltW];
+                for (int p = 0; p < kLdltW; p++)
 #pragma unroll
-                for (int a2 = 0; a2 < 4; a2++) {
-                    const int i = je + 4 * ti + a2;
-#pragma unroll
-                    for (int p = 0; p < kLdltW; p++) li[a2][p] = (i < n && jb + p < je) ? A[(size_t)i * n + jb + p] : 0.0;
-                }
+                    for (int a2 = 0; a2 < 4; a2++) {
+                        const int i = je + 4 * ti + a2;
+                        wi[a2][p] = (i < n && jb + p < je) ? A[(size_t)(jb + p) * ld + i] : 0.0;   // W(i, jb+p)
+                    }
                 for (int tk = tx; tk <= ti; tk += 16) {
                     double lk[4][kLdltW];
 #pragma unroll
                     for (int b2 = 0; b2 < 4; b2++) {
                         const int k = je + 4 * tk + b2;
 #pragma unroll
-                        for (int p = 0; p < kLdltW; p++) lk[b2][p] = (k < n && jb + p < je) ? A[(size_t)k * n + jb + p] : 0.0;
+                        for (int p = 0; p < kLdltW; p++) lk[b2][p] = (k < n && jb + p < je) ? A[(size_t)k * ld + jb + p] : 0.0;
                     }
                     double v[4][4];
 #pragma unroll
@@ -573,21 +600,20 @@ __global__ __launch_bounds__(kLdltT) void k_ldlt_solve(double* __restrict__ Ag, 
 #pragma unroll
                         for (int b2 = 0; b2 < 4; b2++) {
                             const int i = je + 4 * ti + a2, k = je + 4 * tk + b2;
-                            v[a2][b2] = (i < n && k <= i) ? A[(size_t)i * n + k] : 0.0;
+                            v[a2][b2] = (i < n && k <= i) ? A[(size_t)i * ld + k] : 0.0;
                         }
 #pragma unroll
                     for (int p = 0; p < kLdltW; p++)
-                        if (jb + p < je)
 #pragma unroll
-                            for (int a2 = 0; a2 < 4; a2++)
+                        for (int a2 = 0; a2 < 4; a2++)
 #pragma unroll
-                                for (int b2 = 0; b2 < 4; b2++) v[a2][b2] -= (li[a2][p] * lk[b2][p]) * d[p];
+                            for (int b2 = 0; b2 < 4; b2++) v[a2][b2] = __builtin_fma(-wi[a2][p], lk[b2][p], v[a2][b2]);
 #pragma unroll
                     for (int a2 = 0; a2 < 4; a2++)
 #pragma unroll
                         for (int b2 = 0; b2 < 4; b2++) {
                             const int i = je + 4 * ti + a2, k = je + 4 * tk + b2;
-                            if (i < n && k <= i) A[(size_t)i * n + k] = v[a2][b2];
+                            if (i < n && k <= i) A[(size_t)i * ld + k] = v[a2][b2];
                         }
                 }
             }
@@ -602,29 +628,57 @@ __global__ __launch_bounds__(kLdltT) void k_ldlt_solve(double* __restrict__ Ag, 
     }
     if (tid >= 64) return;
     // ---- forward substitution (column order per element: y_i -= L_ik y_k, k ascending),
-    //      blocked by kLdltW: the block's own rows on lanes 0..W-1, later rows 3 per lane
+    //      blocked by kLdltW: the block's own rows on lanes 0..W-1, later rows 3 per lane.
+    //      The block's L entries are loaded before its dependent chain starts.
     for (int kb = 0; kb < n; kb += kLdltW) {
-        const int ke = min(kb + kLdltW, n);
-        double yb = (lane < ke - kb) ? y[kb + lane] : 0.0;
+        const int ke = min(kb + kLdltW, n), w = ke - kb;
+        double Ab[kLdltW], Ar[3][kLdltW], yr[3];
+#pragma unroll
+        for (int c = 0; c < kLdltW; c++) Ab[c] = (lane < w && c < lane) ? A[(size_t)(kb + lane) * ld + kb + c] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 3; u++) {
+            const int i = ke + lane + 64 * u;
+            yr[u] = i < n ? y[i] : 0.0;
+#pragma unroll
+            for (int c = 0; c < kLdltW; c++) Ar[u][c] = (i < n && c < w) ? A[(size_t)i * ld + kb + c] : 0.0;
+        }
+        double yb = (lane < w) ? y[kb + lane] : 0.0;
+#ifdef ORB_TIMING
+        TSTAMP(t_f0);
+        __builtin_amdgcn_s_waitcnt(0);
+        TACC(tFLoad, t_f0);
+        TSTAMP(t_f1);
+#endif
 #pragma unroll
         for (int c = 0; c < kLdltW; c++) {
-            if (kb + c >= ke) break;
+            if (c >= w) break;
             const double yc = shfl_d(yb, c);
-            if (lane > c && lane < ke - kb) yb -= A[(size_t)(kb + lane) * n + kb + c] * yc;
+            if (lane > c && lane < w) yb = __builtin_fma(-Ab[c], yc, yb);
         }
         double ys[kLdltW];
 #pragma unroll
         for (int c = 0; c < kLdltW; c++) ys[c] = shfl_d(yb, c);
-        if (lane < ke - kb) y[kb + lane] = yb;
-        for (int i = ke + lane; i < n; i += 64) {
-            double v = y[i];
+#ifdef ORB_TIMING
+        if (ys[kLdltW - 1] == 12345.0) y[0] = 1.0;
+        TACC(tFChain, t_f1);
+        TSTAMP(t_f2);
+#endif
+        if (lane < w) y[kb + lane] = yb;
+#pragma unroll
+        for (int u = 0; u < 3; u++) {
+            const int i = ke + lane + 64 * u;
+            double v = yr[u];
 #pragma unroll
             for (int c = 0; c < kLdltW; c++)
-                if (kb + c < ke) v -= A[(size_t)i * n + kb + c] * ys[c];
-            y[i] = v;
+                if (c < w) v = __builtin_fma(-Ar[u][c], ys[c], v);
+            if (i < n) y[i] = v;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
+#ifdef ORB_TIMING
+        __builtin_amdgcn_s_waitcnt(0);
+        TACC(tFRows, t_f2);
+#endif
     }
     for (int i = lane; i < n; i += 64) y[i] = y[i] / dg[i];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -632,23 +686,35 @@ __global__ __launch_bounds__(kLdltT) void k_ldlt_solve(double* __restrict__ Ag, 
     // ---- backward substitution with L^T (per element: y_i -= L_ki x_k, k descending)
     for (int ke = n; ke > 0; ke -= kLdltW) {
         const int kb = max(ke - kLdltW, 0), w = ke - kb;
+        double Ab[kLdltW], Ar[3][kLdltW], yr[3];
+#pragma unroll
+        for (int c = 0; c < kLdltW; c++) Ab[c] = (lane < c && c < w) ? A[(size_t)(kb + c) * ld + kb + lane] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 3; u++) {
+            const int i = lane + 64 * u;
+            yr[u] = i < kb ? y[i] : 0.0;
+#pragma unroll
+            for (int c = 0; c < kLdltW; c++) Ar[u][c] = (i < kb && c < w) ? A[(size_t)(kb + c) * ld + i] : 0.0;
+        }
         double xb = lane < w ? y[kb + lane] : 0.0;
 #pragma unroll
         for (int c = kLdltW - 1; c >= 0; c--) {
             if (c >= w) continue;
             const double xc = shfl_d(xb, c);
-            if (lane < c) xb -= A[(size_t)(kb + c) * n + kb + lane] * xc;
+            if (lane < c) xb = __builtin_fma(-Ab[c], xc, xb);
         }
         double xs[kLdltW];
 #pragma unroll
         for (int c = 0; c < kLdltW; c++) xs[c] = shfl_d(xb, c);
         if (lane < w) y[kb + lane] = xb;
-        for (int i = lane; i < kb; i += 64) {
-            double v = y[i];
+#pragma unroll
+        for (int u = 0; u < 3; u++) {
+            const int i = lane + 64 * u;
+            double v = yr[u];
 #pragma unroll
             for (int c = kLdltW - 1; c >= 0; c--)
-                if (c < w) v -= A[(size_t)(kb + c) * n + i] * xs[c];
-            y[i] = v;
+                if (c < w) v = __builtin_fma(-Ar[u][c], xs[c], v);
+            if (i < kb) y[i] = v;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -656,7 +722,7 @@ __global__ __launch_bounds__(kLdltT) void k_ldlt_solve(double* __restrict__ Ag, 
     for (int i = lane; i < n; i += 64) x[i] = y[i];
     if (tid == 0) flags[0] = 0;
 #ifdef ORB_TIMING
-    if (tid == 0) printf("ldlt n %d: stage %lld panel %lld trailing %lld solves %lld\n", n, t_p_first, tPanel, tTrail, clock64() - t_l1);
+    if (tid == 0) printf("ldlt n %d: stage %lld panel %lld (load %lld cols %lld) trailing %lld solves %lld (fwd load %lld chain %lld rows %lld)\n", n, t_p_first, tPanel, tPLoad, tPCol, tTrail, clock64() - t_l1, tFLoad, tFChain, tFRows);
 #endif
 }
 
@@ -786,28 +852,66 @@ struct lba_context {
     size_t wsDoubles = 0;
     lba_allreduce_fn allreduce = nullptr;
     void* commUser = nullptr;
-    // device buffers
-    std::vector<void*> allocs;
+    // device buffers: a grow-only arena reused across solves (hipMalloc / hipFree per buffer
+    // and per call cost more than a small LBA's whole LM loop; hipFree also synchronises)
+    std::vector<std::pair<char*, size_t>> chunks;   // (base, size); the last one is bumped
+    size_t used = 0, usedTotal = 0, peak = 0;
     // stats
     double ms_linearize = 0, ms_schur = 0, ms_solve = 0, ms_update = 0;
     int n_iters = 0, n_trials = 0;
     bool profile = false;
-    std::vector<hipEvent_t> ev;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};   // stage timing
+    hipEvent_t evSync = nullptr;                               // LM decision hand-off
+    double* h_scal = nullptr;                                  // pinned LM scalars
 };
 
+// Resets the arena for a new solve; if the last solve spilled into several chunks, they are
+// replaced by one chunk of the peak size (the device is idle between solves).
 static void lba_free_all(lba_context* c) {
-    for (void* p : c->allocs)
-        if (p) (void)hipFree(p);
-    c->allocs.clear();
+    if (c->chunks.size() > 1) {
+        for (auto& ch : c->chunks) (void)hipFree(ch.first);
+        c->chunks.clear();
+        char* p = nullptr;
+        if (hipMalloc((void**)&p, c->peak) == hipSuccess) c->chunks.push_back({p, c->peak});
+    }
+    c->used = 0;
+    c->usedTotal = 0;
+}
+
+static void lba_release(lba_context* c) {
+    for (auto& ch : c->chunks) (void)hipFree(ch.first);
+    c->chunks.clear();
+    c->used = c->usedTotal = c->peak = 0;
 }
 
 template <typename T>
 static int dalloc(lba_context* c, T** p, size_t n) {
     *p = nullptr;
     if (n == 0) n = 1;
-    if (hipMalloc((void**)p, n * sizeof(T)) != hipSuccess) return ORB_ENOMEM;
-    c->allocs.push_back(*p);
+    const size_t bytes = (n * sizeof(T) + 255) & ~(size_t)255;
+    if (c->chunks.empty() || c->used + bytes > c->chunks.back().second) {
+        const size_t prev = c->chunks.empty() ? 0 : c->chunks.back().second;
+        const size_t sz = std::max(bytes, std::max((size_t)4 << 20, 2 * prev));
+        char* base = nullptr;
+        if (hipMalloc((void**)&base, sz) != hipSuccess) return ORB_ENOMEM;
+        c->chunks.push_back({base, sz});
+        c->used = 0;
+    }
+    *p = reinterpret_cast<T*>(c->chunks.back().first + c->used);
+    c->used += bytes;
+    c->usedTotal += bytes;
+    c->peak = std::max(c->peak, c->usedTotal);
     return ORB_OK;
+}
+
+// Waits for the stream by spinning on an event (a blocking hipStreamSynchronize sleeps and
+// adds tens of microseconds per LM trial).
+static int lba_wait(lba_context* c) {
+    if (hipEventRecord(c->evSync, c->stream) != hipSuccess) return ORB_EGPU;
+    hipError_t e;
+    while ((e = hipEventQuery(c->evSync)) == hipErrorNotReady) {
+    }
+    return e == hipSuccess ? ORB_OK : ORB_EGPU;
 }
 
 #define TRY(x)                 \
@@ -971,6 +1075,10 @@ int lba_create(int device, lba_context** out) {
     lba_context* c = new lba_context();
     c->device = device;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return ORB_EGPU; }
+    bool ok = hipEventCreateWithFlags(&c->evSync, hipEventDisableTiming) == hipSuccess &&
+              hipHostMalloc((void**)&c->h_scal, 64, hipHostMallocDefault) == hipSuccess;
+    for (auto& e : c->ev) ok = ok && hipEventCreate(&e) == hipSuccess;
+    if (!ok) { lba_destroy(c); return ORB_EGPU; }
     *out = c;
     return ORB_OK;
 }
@@ -979,8 +1087,11 @@ void lba_destroy(lba_context* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    lba_free_all(c);
-    for (auto e : c->ev) (void)hipEventDestroy(e);
+    lba_release(c);
+    for (auto e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->evSync) (void)hipEventDestroy(c->evSync);
+    if (c->h_scal) (void)hipHostFree(c->h_scal);
     if (c->stream && c->ownStream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1109,9 +1220,7 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
     TRY(dalloc(c, &d.x, 6 * (size_t)NP + 3 * (size_t)NM));
     TRY(dalloc(c, &d.red, 16));
     TRY(dalloc(c, &d.flags, 4));
-    double* h_scal = nullptr;
-    if (hipHostMalloc((void**)&h_scal, 64, hipHostMallocDefault) != hipSuccess) return ORB_ENOMEM;
-    struct PinGuard { double* p; ~PinGuard() { if (p) (void)hipHostFree(p); } } pg{h_scal};
+    double* h_scal = c->h_scal;
     double* d_chi2 = nullptr;
     uint8_t* d_depth = nullptr;
     TRY(dalloc(c, &d_chi2, NE));
@@ -1122,14 +1231,7 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
     const int maxTrials = o->max_trials > 0 ? o->max_trials : 10;
     auto stopped = [&]() { return stop && *stop; };
 
-    // events for stage timing
-    auto evt = [&]() -> hipEvent_t {
-        hipEvent_t e;
-        if (hipEventCreate(&e) != hipSuccess) return nullptr;
-        c->ev.push_back(e);
-        return e;
-    };
-    hipEvent_t e0 = evt(), e1 = evt(), e2 = evt(), e3 = evt();
+    hipEvent_t e0 = c->ev[0], e1 = c->ev[1], e2 = c->ev[2], e3 = c->ev[3];   // stage timing
     auto elapsed = [&](hipEvent_t a, hipEvent_t b) {
         float ms = 0;
         (void)hipEventElapsedTime(&ms, a, b);
@@ -1199,7 +1301,7 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
             }
             ORB_HIP_TRY(hipMemcpyAsync(h_scal, d.red, 16, hipMemcpyDeviceToHost, s));
             if (c->profile) (void)hipEventRecord(e1, s);
-            ORB_HIP_TRY(hipStreamSynchronize(s));
+            TRY(lba_wait(c));
             if (c->profile) c->ms_linearize += elapsed(e0, e1);
             double currentChi = h_scal[0];
             const double iniChi = currentChi;
@@ -1226,8 +1328,8 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
                 if (d.P > 0) {
                     const int n = 6 * d.P;
                     if (n > kLdltMaxN) return ORB_E2BIG;   // panel rows are held in registers
-                    if ((size_t)n * n * 8 + 3 * (size_t)n * 8 <= 160 * 1024)
-                        hipLaunchKernelGGL(k_ldlt_solve<true>, dim3(1), dim3(kLdltT), ((size_t)n * n + 2 * (size_t)n) * 8, s,
+                    if ((size_t)n * (n | 1) * 8 + 3 * (size_t)n * 8 <= 160 * 1024)
+                        hipLaunchKernelGGL(k_ldlt_solve<true>, dim3(1), dim3(kLdltT), ((size_t)n * (n | 1) + 2 * (size_t)n) * 8, s,
                                            d.S, d.bs, n, d.x, d.flags);
                     else
                         hipLaunchKernelGGL(k_ldlt_solve<false>, dim3(1), dim3(kLdltT), 2 * (size_t)n * 8, s, d.S, d.bs, n,
@@ -1246,7 +1348,7 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
                 ORB_HIP_TRY(hipMemcpyAsync(h_scal, d.red, 24, hipMemcpyDeviceToHost, s));
                 ORB_HIP_TRY(hipMemcpyAsync(h_scal + 4, d.flags, 4, hipMemcpyDeviceToHost, s));
                 if (c->profile) (void)hipEventRecord(e3, s);
-                ORB_HIP_TRY(hipStreamSynchronize(s));
+                TRY(lba_wait(c));
                 if (c->profile) {
                     c->ms_schur += elapsed(e0, e1);
                     c->ms_solve += elapsed(e1, e2);
@@ -1302,7 +1404,7 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
             ORB_HIP_TRY(hipMemcpyAsync(chi.data(), d_chi2, 8 * (size_t)NE, hipMemcpyDeviceToHost, s));
             ORB_HIP_TRY(hipMemcpyAsync(dep.data(), d_depth, NE, hipMemcpyDeviceToHost, s));
         }
-        ORB_HIP_TRY(hipStreamSynchronize(s));
+        TRY(lba_wait(c));
         return ORB_OK;
     };
     std::vector<double> chi;
@@ -1325,10 +1427,10 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
             }
             if (NE > (int)c->wsDoubles) return ORB_EINVAL;
             ORB_HIP_TRY(hipMemcpyAsync(c->ws, lv.data(), 8 * (size_t)NE, hipMemcpyHostToDevice, s));
-            ORB_HIP_TRY(hipStreamSynchronize(s));
+            TRY(lba_wait(c));
             if (c->allreduce(c->commUser, 0, NE, 0) != 0) return ORB_EGPU;
             ORB_HIP_TRY(hipMemcpyAsync(lv.data(), c->ws, 8 * (size_t)NE, hipMemcpyDeviceToHost, s));
-            ORB_HIP_TRY(hipStreamSynchronize(s));
+            TRY(lba_wait(c));
             for (int e = 0; e < NE; e++) level[e] = lv[e] > 0.5 ? 1 : 0;
         }
         TRY(init_opt(0));
@@ -1350,7 +1452,7 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
     if (r->pose_q) ORB_HIP_TRY(hipMemcpyAsync(r->pose_q, q, 32 * (size_t)NP, hipMemcpyDeviceToHost, s));
     if (r->pose_t) ORB_HIP_TRY(hipMemcpyAsync(r->pose_t, t, 24 * (size_t)NP, hipMemcpyDeviceToHost, s));
     if (r->point_xyz) ORB_HIP_TRY(hipMemcpyAsync(r->point_xyz, X, 24 * (size_t)NM, hipMemcpyDeviceToHost, s));
-    ORB_HIP_TRY(hipStreamSynchronize(s));
+    TRY(lba_wait(c));
     ORB_HIP_TRY(hipGetLastError());
     return ORB_OK;
 }
