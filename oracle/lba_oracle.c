@@ -493,11 +493,10 @@ static int schur_solve(lba_ctx* c, double lambda)
             xp[i] = v;
         }
         for (int i = 0; i < np; i++) xp[i] /= d[i];
-        for (int i = np - 1; i >= 0; i--) {
-            double v = xp[i];
-            for (int k = i + 1; k < np; k++) v = fma(-S[k * np + i], xp[k], v);
-            xp[i] = v;
-        }
+        /* back substitution with L^T, column-oriented: x_k is final once every k' > k has
+         * been applied, then x_i = fma(-L(k,i), x_k, x_i) for i < k (k descending per element) */
+        for (int k = np - 1; k >= 0; k--)
+            for (int i = 0; i < k; i++) xp[i] = fma(-S[k * np + i], xp[k], xp[i]);
         /* landmarks: x_l = Dinv (b_l - Hpl^T x_p) */
         for (int l = 0; l < c->M; l++) {
             double cl[3] = {c->bl[3 * l], c->bl[3 * l + 1], c->bl[3 * l + 2]};

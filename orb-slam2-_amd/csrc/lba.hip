@@ -129,6 +129,23 @@ __device__ void d_se3_exp_left(const double upd[6], double q[4], double t[3]) {
 
 // ------------------------------------------------------------------ device state
 
+// Levenberg-Marquardt control state of one optimize() call, kept on the device so the host
+// can enqueue trials without waiting for each decision (G/core/optimization_algorithm_levenberg.cpp:61-189).
+struct LmState {
+    double lambda, ni, currentChi, iniChi, rho;
+    int phase;      // 0: linearise next, 1: trial next, 2: done
+    int it, qmax, nBad, itersDone, trials, pop;
+    int traceBase;  // first trace row of this optimize() call
+};
+
+// Kernels of the LM loop run only in their phase (`want`): 0 linearisation, 1 trial,
+// 3 linearisation of iteration 0 (lambda init), -1 always.
+__device__ __forceinline__ bool lm_off(const LmState* st, int want) {
+    if (!st || want < 0) return false;
+    if (want == 3) return st->phase != 0 || st->it != 0;
+    return st->phase != want;
+}
+
 struct LbaDev {
     // problem
     double *q, *t, *X;          // estimates
@@ -158,6 +175,7 @@ struct LbaDev {
     double *S, *bs, *x;         // x: [6P + 3M]
     double* red;                // reduction scratch
     int* flags;                 // [0] LDLT failure
+    LmState* lm;                // LM control state (device)
 };
 
 __device__ __forceinline__ void d_transform(const LbaDev& d, int pose, int pt, double Xc[3]) {
@@ -175,7 +193,8 @@ __device__ __forceinline__ double d_edge_chi2(const LbaDev& d, int e) {
 }
 
 // computeError for the active edges; echi[k] = robust chi2 (activeRobustChi2 term)
-__global__ __launch_bounds__(256) void k_edge_errors(LbaDev d, double hmono, double hstereo) {
+__global__ __launch_bounds__(256) void k_edge_errors(LbaDev d, double hmono, double hstereo, int want) {
+    if (lm_off(d.lm, want)) return;
     const int k = blockIdx.x * 256 + threadIdx.x;
     if (k >= d.nact) return;
     const int e = d.act[k];
@@ -210,6 +229,7 @@ __global__ __launch_bounds__(256) void k_edge_errors(LbaDev d, double hmono, dou
 // Jacobians + Huber-weighted quadratic-form blocks per active edge.
 // Hll_e: 3x3 upper (00 01 02 11 12 22); Hpp_e: 6x6 upper row-major (21); Hpl_e: 6x3; bl_e: 3; bp_e: 6
 __global__ __launch_bounds__(256) void k_edge_linearize(LbaDev d, double hmono, double hstereo) {
+    if (lm_off(d.lm, 0)) return;
     const int k = blockIdx.x * 256 + threadIdx.x;
     if (k >= d.nact) return;
     const int e = d.act[k];
@@ -297,6 +317,7 @@ __global__ __launch_bounds__(256) void k_edge_linearize(LbaDev d, double hmono, 
 
 // Hll, b_l per owned landmark (edges in pose-index order)
 __global__ __launch_bounds__(256) void k_point_reduce(LbaDev d) {
+    if (lm_off(d.lm, 0)) return;
     const int l = blockIdx.x * 256 + threadIdx.x;
     if (l >= d.M) return;
     double h[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
@@ -314,6 +335,7 @@ __global__ __launch_bounds__(256) void k_point_reduce(LbaDev d) {
 
 // Hpp, b_p per pose: one wave per pose, lanes stride over the pose's edges, fixed tree.
 __global__ __launch_bounds__(64) void k_pose_reduce(LbaDev d) {
+    if (lm_off(d.lm, 0)) return;
     const int p = blockIdx.x, lane = threadIdx.x;
     double acc[27];
     for (int i = 0; i < 27; i++) acc[i] = 0;
@@ -342,7 +364,9 @@ __global__ __launch_bounds__(64) void k_pose_reduce(LbaDev d) {
 
 // Per landmark with lambda: Dinv (Eigen 3x3 cofactor inverse) and db = Dinv b_l
 // (G/core/block_solver.hpp:380-398).
-__global__ __launch_bounds__(256) void k_point_schur(LbaDev d, double lambda) {
+__global__ __launch_bounds__(256) void k_point_schur(LbaDev d) {
+    if (lm_off(d.lm, 1)) return;
+    const double lambda = d.lm->lambda;
     const int l = blockIdx.x * 256 + threadIdx.x;
     if (l >= d.M) return;
     double m[9];
@@ -366,6 +390,7 @@ __global__ __launch_bounds__(256) void k_point_schur(LbaDev d, double lambda) {
 
 // Per active edge with a free pose: BD_e = Hpl_e Dinv, coef_e = Hpl_e Dinv b_l.
 __global__ __launch_bounds__(256) void k_edge_schur(LbaDev d) {
+    if (lm_off(d.lm, 1)) return;
     const int k = blockIdx.x * 256 + threadIdx.x;
     if (k >= d.nact || d.actPi[k] < 0) return;
     const int l = d.actPt[k];
@@ -387,8 +412,10 @@ __global__ __launch_bounds__(256) void k_edge_schur(LbaDev d) {
 // (G/core/block_solver.hpp:408-440).  Thread t owns output element t % 36 of contribution
 // group t / 36 (7 groups); the group partial sums meet in LDS.
 constexpr int kSpGroups = 7;
-__global__ __launch_bounds__(256) void k_schur_pairs(LbaDev d, double lambda, int addDiag, const int32_t* pairI,
+__global__ __launch_bounds__(256) void k_schur_pairs(LbaDev d, int addDiag, const int32_t* pairI,
                                                      const int32_t* pairJ) {
+    if (lm_off(d.lm, 1)) return;
+    const double lambda = d.lm->lambda;
     __shared__ double part[kSpGroups][36];
     const int pr = blockIdx.x, tid = threadIdx.x;
     const int bi = pairI[pr], bj = pairJ[pr];
@@ -422,6 +449,7 @@ __global__ __launch_bounds__(256) void k_schur_pairs(LbaDev d, double lambda, in
 
 // b_s = b_p - sum_e coef_e, one wave per pose
 __global__ __launch_bounds__(64) void k_bschur(LbaDev d, int addBp) {
+    if (lm_off(d.lm, 1)) return;
     const int p = blockIdx.x, lane = threadIdx.x;
     double acc[6] = {0, 0, 0, 0, 0, 0};
     for (int a = d.poStart[p] + lane; a < d.poStart[p + 1]; a += 64) {
@@ -468,13 +496,80 @@ __device__ __forceinline__ double shfl_d(double v, int src) {
 // so every element sees the recurrence's exact operation sequence, with two workgroup barriers
 // per panel.  The triangular solves (y_i = fma(-L_ik, y_k, y_i), k in order) are blocked the
 // same way on one wave.
+// Panel [jb, je) of the factorisation on one wave, rows jb + lane + 64u for u < NS (NS = slots
+// that hold rows: the matrix has n - jb rows left).  Column j: d_j = A(j,j); W(i,j) = A(i,j)
+// before the division goes to the upper triangle at (j, i), L(i,j) = W(i,j)/d_j to the lower;
+// the panel's later columns take A(i,k) = fma(-W(i,j), L(k,j), A(i,k)), and the forward
+// substitution advances with the factorisation: y_i = fma(-L(i,j), y_j, y_i) for i > j once
+// y_j is final.  Values computed on or above the diagonal are not stored.  Returns false on a
+// zero or non-finite pivot.
+template <int NS>
+__device__ __forceinline__ bool ldlt_panel(double* __restrict__ A, int ld, int n, int jb, int je, double* __restrict__ dg,
+                                           double* __restrict__ y, int lane) {
+    double P[NS][kLdltW], Wp[NS][kLdltW], Y[NS];
+#pragma unroll
+    for (int u = 0; u < NS; u++) {
+        const int r = jb + lane + 64 * u;
+        Y[u] = r < n ? y[r] : 0.0;
+#pragma unroll
+        for (int c = 0; c < kLdltW; c++) {
+            P[u][c] = (r < n && jb + c < je) ? A[(size_t)r * ld + jb + c] : 0.0;
+            Wp[u][c] = 0.0;
+        }
+    }
+    bool bad = false;
+#pragma unroll
+    for (int c = 0; c < kLdltW; c++) {
+        const int j = jb + c;
+        if (j < je && !bad) {
+            const double dj = shfl_d(P[0][c], c);   // A(j, j): row j is lane c, slot 0
+            if (dj == 0.0 || !isfinite(dj)) {
+                bad = true;
+            } else {
+#pragma unroll
+                for (int u = 0; u < NS; u++) {
+                    Wp[u][c] = P[u][c];
+                    P[u][c] = P[u][c] / dj;
+                }
+                if (lane == 0) dg[j] = dj;
+                const double yj = shfl_d(Y[0], c);   // final: every k < j has been applied
+#pragma unroll
+                for (int u = 0; u < NS; u++)
+                    if (jb + lane + 64 * u > j) Y[u] = __builtin_fma(-P[u][c], yj, Y[u]);
+                double lkv[kLdltW];
+#pragma unroll
+                for (int k = c + 1; k < kLdltW; k++) lkv[k] = shfl_d(P[0][c], k);   // L(jb+k, j)
+#pragma unroll
+                for (int k = c + 1; k < kLdltW; k++)
+#pragma unroll
+                    for (int u = 0; u < NS; u++) P[u][k] = __builtin_fma(-Wp[u][c], lkv[k], P[u][k]);
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < NS; u++) {
+        const int r = jb + lane + 64 * u;
+        if (r < n) y[r] = Y[u];
+#pragma unroll
+        for (int c = 0; c < kLdltW; c++)
+            if (r < n && r > jb + c && jb + c < je) {
+                A[(size_t)r * ld + jb + c] = P[u][c];      // L(r, jb+c), strict lower
+                A[(size_t)(jb + c) * ld + r] = Wp[u][c];   // W(r, jb+c) at (jb+c, r)
+            }
+    }
+    return !bad;
+}
+
 template <bool kLds>
 __global__ __launch_bounds__(kLdltT) void k_ldlt_solve(double* __restrict__ Ag, const double* __restrict__ b, int n,
-                                                       double* __restrict__ x, int* __restrict__ flags) {
+                                                       double* __restrict__ x, int* __restrict__ flags,
+                                                       const LmState* st) {
+    if (lm_off(st, 1)) return;
     extern __shared__ __attribute__((aligned(16))) double sh[];
     TSTAMP(t_l0);
     long long tPanel = 0, tTrail = 0, tPLoad = 0, tPCol = 0, tFLoad = 0, tFChain = 0, tFRows = 0;
     (void)tPanel; (void)tTrail; (void)tPLoad; (void)tPCol; (void)tFLoad; (void)tFChain; (void)tFRows;
+    // (forward substitution runs inside the panels; tPLoad/tPCol/tF* stay 0 in this layout)
     // LDS rows padded to an odd number of doubles: the panel's column accesses (lanes one row
     // apart) then spread over the banks instead of hitting a few of them
     const int ld = kLds ? (n | 1) : n;
@@ -505,117 +600,55 @@ __global__ __launch_bounds__(kLdltT) void k_ldlt_solve(double* __restrict__ Ag, 
         const int je = min(jb + kLdltW, n);
         TSTAMP(t_p0);
         if (tid < 64) {
-            // ---- panel [jb, je) on wave 0: lane holds rows jb + lane + 64u (zeros past row n
-            //      and column je; those are never stored).  Column j: d_j = A(j,j); W(i,j) =
-            //      A(i,j) before the division goes to the upper triangle at (j, i), L(i,j) =
-            //      W(i,j)/d_j to the lower; the panel's later columns take
-            //      A(i,k) = fma(-W(i,j), L(k,j), A(i,k)).  Every lane runs the same code: the
-            //      values computed on or above the diagonal are not stored.
-            double P[3][kLdltW];
-#pragma unroll
-            for (int u = 0; u < 3; u++) {
-                const int r = jb + lane + 64 * u;
-#pragma unroll
-                for (int c = 0; c < kLdltW; c++) P[u][c] = (r < n && jb + c < je) ? A[(size_t)r * ld + jb + c] : 0.0;
-            }
-            double Wp[3][kLdltW] = {};   // W of the panel's columns, stored after the column loop
-            bool bad = false;
-#ifdef ORB_TIMING
-            __builtin_amdgcn_s_waitcnt(0);
-#endif
-            TACC(tPLoad, t_p0);
-            TSTAMP(t_pc0);
-#pragma unroll
-            for (int c = 0; c < kLdltW; c++) {
-                const int j = jb + c;
-                if (j < je && !bad) {
-                    const double dj = shfl_d(P[0][c], c);   // A(j, j): row j is lane c, slot 0
-                    if (dj == 0.0 || !isfinite(dj)) {
-                        bad = true;
-                    } else {
-                        double w[3];
-#pragma unroll
-                        for (int u = 0; u < 3; u++) {
-                            w[u] = P[u][c];
-                            Wp[u][c] = w[u];
-                            P[u][c] = w[u] / dj;
-                        }
-                        if (lane == 0) dg[j] = dj;
-                        double lkv[kLdltW];
-#pragma unroll
-                        for (int k = c + 1; k < kLdltW; k++) lkv[k] = shfl_d(P[0][c], k);   // L(jb+k, j)
-#pragma unroll
-                        for (int k = c + 1; k < kLdltW; k++)
-#pragma unroll
-                            for (int u = 0; u < 3; u++) P[u][k] = __builtin_fma(-w[u], lkv[k], P[u][k]);
-                    }
-                }
-            }
-            if (bad && lane == 0) failS = 1;
-#ifdef ORB_TIMING
-            if (P[0][kLdltW - 1] == 12345.0) failS = 2;   // keeps the timer after the column loop
-#endif
-            TACC(tPCol, t_pc0);
-#pragma unroll
-            for (int u = 0; u < 3; u++) {
-                const int r = jb + lane + 64 * u;
-#pragma unroll
-                for (int c = 0; c < kLdltW; c++)
-                    if (r < n && r > jb + c && jb + c < je) {
-                        A[(size_t)r * ld + jb + c] = P[u][c];      // L(r, jb+c), strict lower
-                        A[(size_t)(jb + c) * ld + r] = Wp[u][c];   // W(r, jb+c) at (jb+c, r)
-                    }
-            }
+            const int ns = (n - jb + 63) >> 6;
+            const bool okp = ns == 1   ? ldlt_panel<1>(A, ld, n, jb, je, dg, y, lane)
+                             : ns == 2 ? ldlt_panel<2>(A, ld, n, jb, je, dg, y, lane)
+                                       : ldlt_panel<3>(A, ld, n, jb, je, dg, y, lane);
+            if (!okp && lane == 0) failS = 1;
         }
         __syncthreads();
         TACC(tPanel, t_p0);
         TSTAMP(t_t0);
         if (failS) break;
-        // ---- trailing lower triangle (rows, columns >= je) in 4 x 4 tiles: thread (ty, tx)
-        //      owns tile rows ty + 32a and tile columns tx + 16c (c <= a); element (i, k) takes
+        // ---- trailing lower triangle (rows, columns >= je) in 4 x 4 tiles, one tile per thread
+        //      (triangular numbering t -> (ti, tk), tk <= ti); element (i, k) takes
         //      A(i,k) = fma(-W(i,p), L(k,p), A(i,k)) for the panel's columns p in order
         {
-            const int m = n - je, T = (m + 3) >> 2;
-            const int ty = tid >> 4, tx = tid & 15;
-            for (int ti = ty; ti < T; ti += kLdltT / 16) {
-                double wi[4][kLdltW];
+            const int m = n - je, T = (m + 3) >> 2, nt = T * (T + 1) / 2;
+            for (int t = tid; t < nt; t += kLdltT) {
+                int ti = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
+                while ((ti + 1) * (ti + 2) / 2 <= t) ti++;
+                while (ti * (ti + 1) / 2 > t) ti--;
+                const int tk = t - ti * (ti + 1) / 2;
+                double wi[4][kLdltW], lk[4][kLdltW], v[4][4];
 #pragma unroll
                 for (int p = 0; p < kLdltW; p++)
 #pragma unroll
                     for (int a2 = 0; a2 < 4; a2++) {
-                        const int i = je + 4 * ti + a2;
+                        const int i = je + 4 * ti + a2, k = je + 4 * tk + a2;
                         wi[a2][p] = (i < n && jb + p < je) ? A[(size_t)(jb + p) * ld + i] : 0.0;   // W(i, jb+p)
+                        lk[a2][p] = (k < n && jb + p < je) ? A[(size_t)k * ld + jb + p] : 0.0;     // L(k, jb+p)
                     }
-                for (int tk = tx; tk <= ti; tk += 16) {
-                    double lk[4][kLdltW];
+#pragma unroll
+                for (int a2 = 0; a2 < 4; a2++)
 #pragma unroll
                     for (int b2 = 0; b2 < 4; b2++) {
-                        const int k = je + 4 * tk + b2;
-#pragma unroll
-                        for (int p = 0; p < kLdltW; p++) lk[b2][p] = (k < n && jb + p < je) ? A[(size_t)k * ld + jb + p] : 0.0;
+                        const int i = je + 4 * ti + a2, k = je + 4 * tk + b2;
+                        v[a2][b2] = (i < n && k <= i) ? A[(size_t)i * ld + k] : 0.0;
                     }
-                    double v[4][4];
+#pragma unroll
+                for (int p = 0; p < kLdltW; p++)
 #pragma unroll
                     for (int a2 = 0; a2 < 4; a2++)
 #pragma unroll
-                        for (int b2 = 0; b2 < 4; b2++) {
-                            const int i = je + 4 * ti + a2, k = je + 4 * tk + b2;
-                            v[a2][b2] = (i < n && k <= i) ? A[(size_t)i * ld + k] : 0.0;
-                        }
+                        for (int b2 = 0; b2 < 4; b2++) v[a2][b2] = __builtin_fma(-wi[a2][p], lk[b2][p], v[a2][b2]);
 #pragma unroll
-                    for (int p = 0; p < kLdltW; p++)
+                for (int a2 = 0; a2 < 4; a2++)
 #pragma unroll
-                        for (int a2 = 0; a2 < 4; a2++)
-#pragma unroll
-                            for (int b2 = 0; b2 < 4; b2++) v[a2][b2] = __builtin_fma(-wi[a2][p], lk[b2][p], v[a2][b2]);
-#pragma unroll
-                    for (int a2 = 0; a2 < 4; a2++)
-#pragma unroll
-                        for (int b2 = 0; b2 < 4; b2++) {
-                            const int i = je + 4 * ti + a2, k = je + 4 * tk + b2;
-                            if (i < n && k <= i) A[(size_t)i * ld + k] = v[a2][b2];
-                        }
-                }
+                    for (int b2 = 0; b2 < 4; b2++) {
+                        const int i = je + 4 * ti + a2, k = je + 4 * tk + b2;
+                        if (i < n && k <= i) A[(size_t)i * ld + k] = v[a2][b2];
+                    }
             }
         }
         __syncthreads();
@@ -627,59 +660,6 @@ __global__ __launch_bounds__(kLdltT) void k_ldlt_solve(double* __restrict__ Ag, 
         return;
     }
     if (tid >= 64) return;
-    // ---- forward substitution (column order per element: y_i -= L_ik y_k, k ascending),
-    //      blocked by kLdltW: the block's own rows on lanes 0..W-1, later rows 3 per lane.
-    //      The block's L entries are loaded before its dependent chain starts.
-    for (int kb = 0; kb < n; kb += kLdltW) {
-        const int ke = min(kb + kLdltW, n), w = ke - kb;
-        double Ab[kLdltW], Ar[3][kLdltW], yr[3];
-#pragma unroll
-        for (int c = 0; c < kLdltW; c++) Ab[c] = (lane < w && c < lane) ? A[(size_t)(kb + lane) * ld + kb + c] : 0.0;
-#pragma unroll
-        for (int u = 0; u < 3; u++) {
-            const int i = ke + lane + 64 * u;
-            yr[u] = i < n ? y[i] : 0.0;
-#pragma unroll
-            for (int c = 0; c < kLdltW; c++) Ar[u][c] = (i < n && c < w) ? A[(size_t)i * ld + kb + c] : 0.0;
-        }
-        double yb = (lane < w) ? y[kb + lane] : 0.0;
-#ifdef ORB_TIMING
-        TSTAMP(t_f0);
-        __builtin_amdgcn_s_waitcnt(0);
-        TACC(tFLoad, t_f0);
-        TSTAMP(t_f1);
-#endif
-#pragma unroll
-        for (int c = 0; c < kLdltW; c++) {
-            if (c >= w) break;
-            const double yc = shfl_d(yb, c);
-            if (lane > c && lane < w) yb = __builtin_fma(-Ab[c], yc, yb);
-        }
-        double ys[kLdltW];
-#pragma unroll
-        for (int c = 0; c < kLdltW; c++) ys[c] = shfl_d(yb, c);
-#ifdef ORB_TIMING
-        if (ys[kLdltW - 1] == 12345.0) y[0] = 1.0;
-        TACC(tFChain, t_f1);
-        TSTAMP(t_f2);
-#endif
-        if (lane < w) y[kb + lane] = yb;
-#pragma unroll
-        for (int u = 0; u < 3; u++) {
-            const int i = ke + lane + 64 * u;
-            double v = yr[u];
-#pragma unroll
-            for (int c = 0; c < kLdltW; c++)
-                if (c < w) v = __builtin_fma(-Ar[u][c], ys[c], v);
-            if (i < n) y[i] = v;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-#ifdef ORB_TIMING
-        __builtin_amdgcn_s_waitcnt(0);
-        TACC(tFRows, t_f2);
-#endif
-    }
     for (int i = lane; i < n; i += 64) y[i] = y[i] / dg[i];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -728,6 +708,7 @@ __global__ __launch_bounds__(kLdltT) void k_ldlt_solve(double* __restrict__ Ag, 
 
 // x_l = Dinv (b_l - sum_e Hpl_e^T x_p(pose_e))
 __global__ __launch_bounds__(256) void k_backsub(LbaDev d) {
+    if (lm_off(d.lm, 1)) return;
     const int l = blockIdx.x * 256 + threadIdx.x;
     if (l >= d.M) return;
     double cl[3] = {d.bl[3 * (size_t)l], d.bl[3 * (size_t)l + 1], d.bl[3 * (size_t)l + 2]};
@@ -746,6 +727,7 @@ __global__ __launch_bounds__(256) void k_backsub(LbaDev d) {
 
 // push (backup) + oplus for all free poses and owned points
 __global__ __launch_bounds__(256) void k_update(LbaDev d, int nposes, const int32_t* freePoses, int applyPoses) {
+    if (lm_off(d.lm, 1)) return;
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i < d.M) {
         const int g = d.ptGlob[i];
@@ -768,6 +750,7 @@ __global__ __launch_bounds__(256) void k_update(LbaDev d, int nposes, const int3
 }
 
 __global__ __launch_bounds__(256) void k_pop(LbaDev d, int nposes, const int32_t* freePoses) {
+    if (d.lm && !d.lm->pop) return;   // only after a rejected trial
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i < d.M) {
         const int g = d.ptGlob[i];
@@ -781,7 +764,9 @@ __global__ __launch_bounds__(256) void k_pop(LbaDev d, int nposes, const int32_t
 }
 
 // Deterministic single-workgroup sum of n doubles (fixed stride assignment + fixed tree).
-__global__ __launch_bounds__(1024) void k_sum(const double* __restrict__ v, int n, double* __restrict__ out) {
+__global__ __launch_bounds__(1024) void k_sum(const double* __restrict__ v, int n, double* __restrict__ out,
+                                               const LmState* st, int want) {
+    if (lm_off(st, want)) return;
     __shared__ double sh[1024];
     const int tid = threadIdx.x;
     double s = 0;
@@ -796,7 +781,9 @@ __global__ __launch_bounds__(1024) void k_sum(const double* __restrict__ v, int 
 }
 
 // scale terms: x_j (lambda x_j + b_j) for poses (when includePoses) and owned points
-__global__ __launch_bounds__(256) void k_scale_terms(LbaDev d, double lambda, int includePoses, double* __restrict__ out) {
+__global__ __launch_bounds__(256) void k_scale_terms(LbaDev d, int includePoses, double* __restrict__ out) {
+    if (lm_off(d.lm, 1)) return;
+    const double lambda = d.lm->lambda;
     const int i = blockIdx.x * 256 + threadIdx.x;
     const int np = 6 * d.P, n = np + 3 * d.M;
     if (i >= n) return;
@@ -809,7 +796,8 @@ __global__ __launch_bounds__(256) void k_scale_terms(LbaDev d, double lambda, in
 
 // max |diag| of Hpp (global) and Hll (owned): computeLambdaInit's maxDiagonal
 __global__ __launch_bounds__(1024) void k_maxdiag(const double* __restrict__ Hpp, int P, const double* __restrict__ Hll,
-                                                   int M, double* __restrict__ out) {
+                                                   int M, double* __restrict__ out, const LmState* st) {
+    if (lm_off(st, 3)) return;
     __shared__ double sh[1024];
     const int tid = threadIdx.x;
     double m = 0;
@@ -822,6 +810,93 @@ __global__ __launch_bounds__(1024) void k_maxdiag(const double* __restrict__ Hpp
         __syncthreads();
     }
     if (tid == 0) *out = sh[0];
+}
+
+// Collective staging for a guarded all-reduce: the phase's buffer, or zeros when the phase is
+// skipped (every rank skips alike, so the sum stays zero and is not copied back).
+__global__ __launch_bounds__(256) void k_pack(double* __restrict__ ws, const double* __restrict__ buf, size_t n,
+                                              const LmState* st, int want) {
+    const bool off = lm_off(st, want);
+    for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) ws[i] = off ? 0.0 : buf[i];
+}
+__global__ __launch_bounds__(256) void k_unpack(double* __restrict__ buf, const double* __restrict__ ws, size_t n,
+                                                const LmState* st, int want) {
+    if (lm_off(st, want)) return;
+    for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) buf[i] = ws[i];
+}
+
+// t^3 rounded once (double-double product): the host path used std::pow(t, 3), which glibc
+// rounds correctly except in vanishingly rare cases.
+__device__ __forceinline__ double cube_rn(double t) {
+    const double p = t * t, ep = __builtin_fma(t, t, -p);
+    const double q = p * t, eq = __builtin_fma(p, t, -q);
+    return q + __builtin_fma(ep, t, eq);
+}
+
+// Start of an LM iteration (G/core/optimization_algorithm_levenberg.cpp:61-90): currentChi
+// from the linearisation's robust chi2 (red[0]), lambda from computeLambdaInit (red[1]) at it 0.
+__global__ void k_lm_begin(LmState* st, const double* __restrict__ red) {
+    if (threadIdx.x != 0 || st->phase != 0) return;
+    st->pop = 0;
+    st->currentChi = red[0];
+    st->iniChi = red[0];
+    if (st->it == 0) {
+        st->lambda = 1e-5 * red[1];   // tau = 1e-5
+        st->ni = 2;
+        st->nBad = 0;
+    }
+    st->qmax = 0;
+    st->phase = 1;
+}
+
+// Decision after a trial (:120-160) and the end-of-iteration bookkeeping of
+// SparseOptimizer::optimize / OptimizationAlgorithmLevenberg (termination on qmax == max
+// trials, rho == 0 or three iterations without 1e-3 relative progress).
+__global__ void k_lm_decide(LmState* st, const double* __restrict__ red, const int* __restrict__ flags, int maxTrials,
+                            int iterations, int fixedIterations, double* __restrict__ trace) {
+    if (threadIdx.x != 0) return;
+    st->pop = 0;
+    if (st->phase != 1) return;
+    const double tempChi = flags[0] ? DBL_MAX : red[0];
+    double rho = st->currentChi - tempChi;
+    const double scale = red[2] + 1e-3;
+    rho /= scale;
+    if (rho > 0 && isfinite(tempChi)) {
+        double alpha = 1. - cube_rn(2 * rho - 1);
+        alpha = fmin(alpha, 2. / 3.);
+        const double sf = fmax(1. / 3., alpha);
+        st->lambda *= sf;
+        st->ni = 2;
+        st->currentChi = tempChi;
+    } else {
+        st->lambda *= st->ni;
+        st->ni *= 2;
+        st->pop = 1;
+    }
+    st->rho = rho;
+    st->qmax++;
+    st->trials++;
+    if (rho < 0 && st->qmax < maxTrials) return;   // next trial of this iteration
+    const int row = st->traceBase + st->itersDone;
+    if (trace && row < 64) {
+        trace[4 * row] = st->iniChi;
+        trace[4 * row + 1] = st->currentChi;
+        trace[4 * row + 2] = st->lambda;
+        trace[4 * row + 3] = st->qmax;
+    }
+    st->itersDone++;
+    st->it++;
+    bool go = true;
+    if (!fixedIterations) {
+        if (st->qmax == maxTrials || rho == 0) {
+            go = false;
+        } else {
+            if ((st->iniChi - st->currentChi) * 1e3 < st->iniChi) st->nBad++;
+            else st->nBad = 0;
+            if (st->nBad >= 3) go = false;
+        }
+    }
+    st->phase = (go && st->it < iterations) ? 0 : 2;
 }
 
 // chi2 / depth of every edge (final check and outlier pass): chi2() uses the stored error
@@ -862,7 +937,8 @@ struct lba_context {
     bool profile = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};   // stage timing
     hipEvent_t evSync = nullptr;                               // LM decision hand-off
-    double* h_scal = nullptr;                                  // pinned LM scalars
+    double* h_scal = nullptr;                                  // pinned LM scalars / state (4 KB)
+    std::vector<hipEvent_t> slotEv;                            // per-slot stage timing
 };
 
 // Resets the arena for a new solve; if the last solve spilled into several chunks, they are
@@ -1056,12 +1132,15 @@ int upload(lba_context* c, T** dst, const std::vector<T>& v) {
 
 }  // namespace
 
-static int comm_allreduce(lba_context* c, double* dbuf, size_t n, int op) {
+// All-reduce of an LM-loop buffer: staged through the workspace by guarded kernels, so a
+// slot whose phase is skipped reduces zeros and leaves the buffer alone.
+static int comm_allreduce_g(lba_context* c, double* dbuf, size_t n, int op, const LmState* st, int want) {
     if (c->world <= 1) return ORB_OK;
     if (!c->allreduce || !c->ws || n > c->wsDoubles) return ORB_EINVAL;
-    if (dbuf != c->ws) ORB_HIP_TRY(hipMemcpyAsync(c->ws, dbuf, n * 8, hipMemcpyDeviceToDevice, c->stream));
+    const unsigned g = (unsigned)std::min<size_t>(1024, (n + 255) / 256);
+    hipLaunchKernelGGL(k_pack, dim3(g), dim3(256), 0, c->stream, c->ws, dbuf, n, st, want);
     if (c->allreduce(c->commUser, 0, n, op) != 0) return ORB_EGPU;
-    if (dbuf != c->ws) ORB_HIP_TRY(hipMemcpyAsync(dbuf, c->ws, n * 8, hipMemcpyDeviceToDevice, c->stream));
+    hipLaunchKernelGGL(k_unpack, dim3(g), dim3(256), 0, c->stream, dbuf, c->ws, n, st, want);
     return ORB_OK;
 }
 
@@ -1076,7 +1155,7 @@ int lba_create(int device, lba_context** out) {
     c->device = device;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return ORB_EGPU; }
     bool ok = hipEventCreateWithFlags(&c->evSync, hipEventDisableTiming) == hipSuccess &&
-              hipHostMalloc((void**)&c->h_scal, 64, hipHostMallocDefault) == hipSuccess;
+              hipHostMalloc((void**)&c->h_scal, 4096, hipHostMallocDefault) == hipSuccess;
     for (auto& e : c->ev) ok = ok && hipEventCreate(&e) == hipSuccess;
     if (!ok) { lba_destroy(c); return ORB_EGPU; }
     *out = c;
@@ -1091,6 +1170,7 @@ void lba_destroy(lba_context* c) {
     for (auto e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->evSync) (void)hipEventDestroy(c->evSync);
+    for (auto e : c->slotEv) (void)hipEventDestroy(e);
     if (c->h_scal) (void)hipHostFree(c->h_scal);
     if (c->stream && c->ownStream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -1220,7 +1300,9 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
     TRY(dalloc(c, &d.x, 6 * (size_t)NP + 3 * (size_t)NM));
     TRY(dalloc(c, &d.red, 16));
     TRY(dalloc(c, &d.flags, 4));
-    double* h_scal = c->h_scal;
+    TRY(dalloc(c, &d.lm, 1));
+    double* d_trace = nullptr;
+    TRY(dalloc(c, &d_trace, 4 * 64));
     double* d_chi2 = nullptr;
     uint8_t* d_depth = nullptr;
     TRY(dalloc(c, &d_chi2, NE));
@@ -1231,7 +1313,6 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
     const int maxTrials = o->max_trials > 0 ? o->max_trials : 10;
     auto stopped = [&]() { return stop && *stop; };
 
-    hipEvent_t e0 = c->ev[0], e1 = c->ev[1], e2 = c->ev[2], e3 = c->ev[3];   // stage timing
     auto elapsed = [&](hipEvent_t a, hipEvent_t b) {
         float ms = 0;
         (void)hipEventElapsedTime(&ms, a, b);
@@ -1244,10 +1325,6 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
     const bool root = c->rank == 0;
 
     // global sum of the owned-point partials (and replicated pose part) of a scalar vector
-    auto reduce_sum = [&](const double* v, int n, double* out) -> int {
-        hipLaunchKernelGGL(k_sum, dim3(1), dim3(1024), 0, s, v, n, out);
-        return ORB_OK;
-    };
 
     auto init_opt = [&](int lvl) -> int {
         build_structure(p, level, lvl, c->rank, c->world, hs);
@@ -1270,124 +1347,119 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
 
     auto grid = [](int n) { return dim3((unsigned)std::max(1, (n + 255) / 256)); };
 
-    // computeActiveErrors + activeRobustChi2 (global over ranks)
-    auto errors_chi2 = [&](double* out_dev) -> int {
-        if (d.nact > 0) hipLaunchKernelGGL(k_edge_errors, grid(d.nact), dim3(256), 0, s, d, hm, hsv);
-        TRY(reduce_sum(d.echi, d.nact, out_dev));
-        TRY(comm_allreduce(c, out_dev, 1, 0));
+    // computeActiveErrors + activeRobustChi2 (global over ranks) -> red[0], in phase `want`
+    auto errors_chi2 = [&](int want) -> int {
+        if (d.nact > 0) hipLaunchKernelGGL(k_edge_errors, grid(d.nact), dim3(256), 0, s, d, hm, hsv, want);
+        hipLaunchKernelGGL(k_sum, dim3(1), dim3(1024), 0, s, d.echi, d.nact, d.red, d.lm, want);
+        TRY(comm_allreduce_g(c, d.red, 1, 0, d.lm, want));
         return ORB_OK;
     };
 
-    // one optimize() call (G/core/sparse_optimizer.cpp:354-419)
+    // One LM "slot": the linearisation of an iteration (runs only when the device state says a
+    // new iteration starts) followed by one trial (runs only while the iteration's trial loop
+    // is open) and its decision.  Slots are enqueued back to back without host round trips.
+    auto enqueue_slot = [&](int iterations, hipEvent_t* ev) -> int {
+        const bool prof = ev != nullptr;
+        if (prof) (void)hipEventRecord(ev[0], s);
+        // ---- linearisation (G/core/sparse_optimizer.cpp:384-394, block_solver.hpp:502-561)
+        TRY(errors_chi2(0));
+        if (d.nact > 0) hipLaunchKernelGGL(k_edge_linearize, grid(d.nact), dim3(256), 0, s, d, hm, hsv);
+        if (d.M > 0) hipLaunchKernelGGL(k_point_reduce, grid(d.M), dim3(256), 0, s, d);
+        if (d.P > 0) hipLaunchKernelGGL(k_pose_reduce, dim3(d.P), dim3(64), 0, s, d);
+        if (d.P > 0) {
+            TRY(comm_allreduce_g(c, d.Hpp, 36 * (size_t)d.P, 0, d.lm, 0));
+            TRY(comm_allreduce_g(c, d.bp, 6 * (size_t)d.P, 0, d.lm, 0));
+        }
+        hipLaunchKernelGGL(k_maxdiag, dim3(1), dim3(1024), 0, s, d.Hpp, d.P, d.Hll, d.M, d.red + 1, d.lm);
+        TRY(comm_allreduce_g(c, d.red + 1, 1, 1, d.lm, 3));
+        hipLaunchKernelGGL(k_lm_begin, dim3(1), dim3(64), 0, s, d.lm, d.red);
+        if (prof) (void)hipEventRecord(ev[1], s);
+        // ---- trial: Schur complement, reduced solve, back-substitution, update, new chi2
+        if (d.M > 0) hipLaunchKernelGGL(k_point_schur, grid(d.M), dim3(256), 0, s, d);
+        if (d.nact > 0) hipLaunchKernelGGL(k_edge_schur, grid(d.nact), dim3(256), 0, s, d);
+        const int npairs = d.P * (d.P + 1) / 2;
+        if (npairs > 0) {
+            hipLaunchKernelGGL(k_schur_pairs, dim3(npairs), dim3(256), 0, s, d, root ? 1 : 0, d_pairI, d_pairJ);
+            hipLaunchKernelGGL(k_bschur, dim3(d.P), dim3(64), 0, s, d, root ? 1 : 0);
+        }
+        if (d.P > 0) TRY(comm_allreduce_g(c, d.S, (size_t)36 * d.P * d.P + 6 * (size_t)d.P, 0, d.lm, 1));
+        if (prof) (void)hipEventRecord(ev[2], s);
+        if (d.P > 0) {
+            const int n = 6 * d.P;
+            if ((size_t)n * (n | 1) * 8 + 3 * (size_t)n * 8 <= 160 * 1024)
+                hipLaunchKernelGGL(k_ldlt_solve<true>, dim3(1), dim3(kLdltT), ((size_t)n * (n | 1) + 2 * (size_t)n) * 8, s,
+                                   d.S, d.bs, n, d.x, d.flags, d.lm);
+            else
+                hipLaunchKernelGGL(k_ldlt_solve<false>, dim3(1), dim3(kLdltT), 2 * (size_t)n * 8, s, d.S, d.bs, n,
+                                   d.x, d.flags, d.lm);
+        } else {
+            ORB_HIP_TRY(hipMemsetAsync(d.flags, 0, 4, s));
+        }
+        if (prof) (void)hipEventRecord(ev[3], s);
+        if (d.M > 0) hipLaunchKernelGGL(k_backsub, grid(d.M), dim3(256), 0, s, d);
+        hipLaunchKernelGGL(k_update, grid(std::max(d.M, d.P)), dim3(256), 0, s, d, d.P, d_freePoses, 1);
+        TRY(errors_chi2(1));
+        const int nx = 6 * d.P + 3 * d.M;
+        hipLaunchKernelGGL(k_scale_terms, grid(nx), dim3(256), 0, s, d, root ? 1 : 0, d.echi);
+        hipLaunchKernelGGL(k_sum, dim3(1), dim3(1024), 0, s, d.echi, nx, d.red + 2, d.lm, 1);
+        TRY(comm_allreduce_g(c, d.red + 2, 1, 0, d.lm, 1));
+        hipLaunchKernelGGL(k_lm_decide, dim3(1), dim3(64), 0, s, d.lm, d.red, d.flags, maxTrials, iterations,
+                           o->fixed_iterations ? 1 : 0, d_trace);
+        hipLaunchKernelGGL(k_pop, grid(std::max(d.M, d.P)), dim3(256), 0, s, d, d.P, d_freePoses);
+        if (prof) (void)hipEventRecord(ev[4], s);
+        return ORB_OK;
+    };
+
+    // one optimize() call (G/core/sparse_optimizer.cpp:354-419).  The host enqueues as many
+    // slots as iterations remain (one trial each), then reads the device state once: more
+    // slots only when trials were rejected.  The stop flag is polled between those groups.
     auto optimize = [&](int iterations, int& itersDone) -> int {
         itersDone = 0;
         if (hs.P + hs.M == 0 && c->world == 1) return ORB_OK;
-        double lambda = 0, ni = 2;
-        int nBad = 0;
-        bool ok = true;
-        for (int it = 0; it < iterations && !stopped() && ok; it++) {
-            if (c->profile) (void)hipEventRecord(e0, s);
-            TRY(errors_chi2(d.red));
-            if (d.nact > 0) hipLaunchKernelGGL(k_edge_linearize, grid(d.nact), dim3(256), 0, s, d, hm, hsv);
-            if (d.M > 0) hipLaunchKernelGGL(k_point_reduce, grid(d.M), dim3(256), 0, s, d);
-            if (d.P > 0) hipLaunchKernelGGL(k_pose_reduce, dim3(d.P), dim3(64), 0, s, d);
-            if (c->world > 1 && d.P > 0) {
-                TRY(comm_allreduce(c, d.Hpp, 36 * (size_t)d.P, 0));
-                TRY(comm_allreduce(c, d.bp, 6 * (size_t)d.P, 0));
+        if (iterations <= 0 || stopped()) return ORB_OK;
+        if (6 * d.P > kLdltMaxN) return ORB_E2BIG;   // panel rows are held in registers
+        LmState* hst = reinterpret_cast<LmState*>(reinterpret_cast<char*>(c->h_scal) + 512);
+        std::memset(hst, 0, sizeof(LmState));
+        hst->ni = 2;
+        hst->traceBase = r->trace ? r->n_trace : 64;
+        ORB_HIP_TRY(hipMemcpyAsync(d.lm, hst, sizeof(LmState), hipMemcpyHostToDevice, s));
+        int known = 0;
+        for (;;) {
+            const int G = std::max(1, iterations - known);
+            if (c->profile && c->slotEv.size() < 5 * (size_t)G) {
+                while (c->slotEv.size() < 5 * (size_t)G) {
+                    hipEvent_t e;
+                    if (hipEventCreate(&e) != hipSuccess) return ORB_EGPU;
+                    c->slotEv.push_back(e);
+                }
             }
-            if (it == 0) {
-                hipLaunchKernelGGL(k_maxdiag, dim3(1), dim3(1024), 0, s, d.Hpp, d.P, d.Hll, d.M, d.red + 1);
-                TRY(comm_allreduce(c, d.red + 1, 1, 1));
-            }
-            ORB_HIP_TRY(hipMemcpyAsync(h_scal, d.red, 16, hipMemcpyDeviceToHost, s));
-            if (c->profile) (void)hipEventRecord(e1, s);
+            for (int g = 0; g < G; g++) TRY(enqueue_slot(iterations, c->profile ? &c->slotEv[5 * (size_t)g] : nullptr));
+            ORB_HIP_TRY(hipMemcpyAsync(hst, d.lm, sizeof(LmState), hipMemcpyDeviceToHost, s));
             TRY(lba_wait(c));
-            if (c->profile) c->ms_linearize += elapsed(e0, e1);
-            double currentChi = h_scal[0];
-            const double iniChi = currentChi;
-            double tempChi = currentChi;
-            if (it == 0) {
-                lambda = 1e-5 * h_scal[1];   // computeLambdaInit, tau = 1e-5
-                ni = 2;
-                nBad = 0;
+            if (c->profile) {
+                for (int g = 0; g < G; g++) {
+                    hipEvent_t* ev = &c->slotEv[5 * (size_t)g];
+                    c->ms_linearize += elapsed(ev[0], ev[1]);
+                    c->ms_schur += elapsed(ev[1], ev[2]);
+                    c->ms_solve += elapsed(ev[2], ev[3]);
+                    c->ms_update += elapsed(ev[3], ev[4]);
+                }
             }
-            double rho = 0;
-            int qmax = 0;
-            do {
-                const double lam = lambda;
-                if (c->profile) (void)hipEventRecord(e0, s);
-                if (d.M > 0) hipLaunchKernelGGL(k_point_schur, grid(d.M), dim3(256), 0, s, d, lam);
-                if (d.nact > 0) hipLaunchKernelGGL(k_edge_schur, grid(d.nact), dim3(256), 0, s, d);
-                const int npairs = d.P * (d.P + 1) / 2;
-                if (npairs > 0) {
-                    hipLaunchKernelGGL(k_schur_pairs, dim3(npairs), dim3(256), 0, s, d, lam, root ? 1 : 0, d_pairI, d_pairJ);
-                    hipLaunchKernelGGL(k_bschur, dim3(d.P), dim3(64), 0, s, d, root ? 1 : 0);
-                }
-                if (c->profile) (void)hipEventRecord(e1, s);
-                if (c->world > 1 && d.P > 0) TRY(comm_allreduce(c, d.S, (size_t)36 * d.P * d.P + 6 * (size_t)d.P, 0));
-                if (d.P > 0) {
-                    const int n = 6 * d.P;
-                    if (n > kLdltMaxN) return ORB_E2BIG;   // panel rows are held in registers
-                    if ((size_t)n * (n | 1) * 8 + 3 * (size_t)n * 8 <= 160 * 1024)
-                        hipLaunchKernelGGL(k_ldlt_solve<true>, dim3(1), dim3(kLdltT), ((size_t)n * (n | 1) + 2 * (size_t)n) * 8, s,
-                                           d.S, d.bs, n, d.x, d.flags);
-                    else
-                        hipLaunchKernelGGL(k_ldlt_solve<false>, dim3(1), dim3(kLdltT), 2 * (size_t)n * 8, s, d.S, d.bs, n,
-                                           d.x, d.flags);
-                } else {
-                    ORB_HIP_TRY(hipMemsetAsync(d.flags, 0, 4, s));
-                }
-                if (c->profile) (void)hipEventRecord(e2, s);
-                if (d.M > 0) hipLaunchKernelGGL(k_backsub, grid(d.M), dim3(256), 0, s, d);
-                hipLaunchKernelGGL(k_update, grid(std::max(d.M, d.P)), dim3(256), 0, s, d, d.P, d_freePoses, 1);
-                TRY(errors_chi2(d.red));
-                const int nx = 6 * d.P + 3 * d.M;
-                hipLaunchKernelGGL(k_scale_terms, grid(nx), dim3(256), 0, s, d, lam, root ? 1 : 0, d.echi);
-                TRY(reduce_sum(d.echi, nx, d.red + 2));
-                TRY(comm_allreduce(c, d.red + 2, 1, 0));
-                ORB_HIP_TRY(hipMemcpyAsync(h_scal, d.red, 24, hipMemcpyDeviceToHost, s));
-                ORB_HIP_TRY(hipMemcpyAsync(h_scal + 4, d.flags, 4, hipMemcpyDeviceToHost, s));
-                if (c->profile) (void)hipEventRecord(e3, s);
+            known = hst->itersDone;
+            if (hst->phase == 2 || stopped()) break;
+        }
+        itersDone = hst->itersDone;
+        r->trials += hst->trials;
+        c->n_trials += hst->trials;
+        c->n_iters += itersDone;
+        if (r->trace && r->n_trace < 64) {
+            const int rows = std::min(64 - r->n_trace, itersDone);
+            if (rows > 0) {
+                ORB_HIP_TRY(hipMemcpyAsync(r->trace + 4 * r->n_trace, d_trace + 4 * r->n_trace, 32 * (size_t)rows,
+                                           hipMemcpyDeviceToHost, s));
                 TRY(lba_wait(c));
-                if (c->profile) {
-                    c->ms_schur += elapsed(e0, e1);
-                    c->ms_solve += elapsed(e1, e2);
-                    c->ms_update += elapsed(e2, e3);
-                }
-                const int failed = *(int32_t*)(h_scal + 4);
-                tempChi = h_scal[0];
-                if (failed) tempChi = DBL_MAX;
-                rho = currentChi - tempChi;
-                double scale = h_scal[2];
-                scale += 1e-3;
-                rho /= scale;
-                if (rho > 0 && std::isfinite(tempChi)) {
-                    double alpha = 1. - std::pow((2 * rho - 1), 3);
-                    alpha = std::min(alpha, 2. / 3.);
-                    const double sf = std::max(1. / 3., alpha);
-                    lambda *= sf;
-                    ni = 2;
-                    currentChi = tempChi;
-                } else {
-                    lambda *= ni;
-                    ni *= 2;
-                    hipLaunchKernelGGL(k_pop, grid(std::max(d.M, d.P)), dim3(256), 0, s, d, d.P, d_freePoses);
-                }
-                qmax++;
-                r->trials++;
-                c->n_trials++;
-            } while (rho < 0 && qmax < maxTrials && !stopped());
-            if (r->trace && r->n_trace < 64) {
-                double* tr = r->trace + 4 * r->n_trace++;
-                tr[0] = iniChi; tr[1] = currentChi; tr[2] = lambda; tr[3] = qmax;
+                r->n_trace += rows;
             }
-            itersDone++;
-            c->n_iters++;
-            if (o->fixed_iterations) continue;
-            if (qmax == maxTrials || rho == 0) { ok = false; continue; }
-            if ((iniChi - currentChi) * 1e3 < iniChi) nBad++;
-            else nBad = 0;
-            if (nBad >= 3) ok = false;
         }
         return ORB_OK;
     };
