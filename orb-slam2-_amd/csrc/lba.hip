@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "common.h"
+#include "se3.h"
 
 #ifdef ORB_TIMING   // instrumented variant (tools/build_variant.py)
 #define TSTAMP(v) const long long v = clock64()
@@ -39,93 +40,6 @@
 #endif
 
 namespace orbamd {
-
-// ------------------------------------------------------------------ device math (SE3Quat)
-
-__device__ __forceinline__ void d_cross(const double a[3], const double b[3], double o[3]) {
-    o[0] = a[1] * b[2] - a[2] * b[1];
-    o[1] = a[2] * b[0] - a[0] * b[2];
-    o[2] = a[0] * b[1] - a[1] * b[0];
-}
-__device__ __forceinline__ void d_quat_rot(const double q[4], const double v[3], double o[3]) {
-    double uv[3], c[3];
-    d_cross(q, v, uv);
-    uv[0] += uv[0]; uv[1] += uv[1]; uv[2] += uv[2];
-    d_cross(q, uv, c);
-    for (int i = 0; i < 3; i++) o[i] = v[i] + q[3] * uv[i] + c[i];
-}
-__device__ __forceinline__ void d_quat_to_R(const double q[4], double R[9]) {
-    const double x = q[0], y = q[1], z = q[2], w = q[3];
-    const double tx = 2 * x, ty = 2 * y, tz = 2 * z;
-    const double twx = tx * w, twy = ty * w, twz = tz * w;
-    const double txx = tx * x, txy = ty * x, txz = tz * x;
-    const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
-    R[0] = 1 - (tyy + tzz); R[1] = txy - twz;       R[2] = txz + twy;
-    R[3] = txy + twz;       R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
-    R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
-}
-__host__ __device__ inline void hd_normalize_rotation(double q[4]) {
-    if (q[3] < 0) { q[0] = -q[0]; q[1] = -q[1]; q[2] = -q[2]; q[3] = -q[3]; }
-    const double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
-    q[0] /= n; q[1] /= n; q[2] /= n; q[3] /= n;
-}
-// Eigen Quaterniond(const Matrix3d&) + SE3Quat::normalizeRotation
-__host__ __device__ inline void hd_quat_from_matrix(const double m[9], double q[4]) {
-    const double t = m[0] + m[4] + m[8];
-    if (t > 0) {
-        double s = sqrt(t + 1.0);
-        q[3] = 0.5 * s;
-        s = 0.5 / s;
-        q[0] = (m[7] - m[5]) * s;
-        q[1] = (m[2] - m[6]) * s;
-        q[2] = (m[3] - m[1]) * s;
-    } else {
-        int i = 0;
-        if (m[4] > m[0]) i = 1;
-        if (m[8] > m[i * 3 + i]) i = 2;
-        const int j = (i + 1) % 3, k = (j + 1) % 3;
-        double s = sqrt(m[i * 3 + i] - m[j * 3 + j] - m[k * 3 + k] + 1.0);
-        q[i] = 0.5 * s;
-        s = 0.5 / s;
-        q[3] = (m[k * 3 + j] - m[j * 3 + k]) * s;
-        q[j] = (m[j * 3 + i] + m[i * 3 + j]) * s;
-        q[k] = (m[k * 3 + i] + m[i * 3 + k]) * s;
-    }
-    hd_normalize_rotation(q);
-}
-// T <- exp(upd) * T  (VertexSE3Expmap::oplusImpl, SE3Quat::exp, SE3Quat::operator*)
-__device__ void d_se3_exp_left(const double upd[6], double q[4], double t[3]) {
-    const double w0 = upd[0], w1 = upd[1], w2 = upd[2];
-    const double theta = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
-    const double O[9] = {0, -w2, w1, w2, 0, -w0, -w1, w0, 0};
-    double O2[9], R[9], V[9];
-    for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 3; j++)
-            O2[i * 3 + j] = O[i * 3] * O[j] + O[i * 3 + 1] * O[3 + j] + O[i * 3 + 2] * O[6 + j];
-    if (theta < 0.00001) {
-        for (int i = 0; i < 9; i++) { R[i] = (i % 4 == 0 ? 1.0 : 0.0) + O[i] + O2[i]; V[i] = R[i]; }
-    } else {
-        const double a = sin(theta) / theta, b = (1 - cos(theta)) / (theta * theta);
-        const double c = (theta - sin(theta)) / pow(theta, 3);
-        for (int i = 0; i < 9; i++) {
-            const double I = (i % 4 == 0 ? 1.0 : 0.0);
-            R[i] = I + a * O[i] + b * O2[i];
-            V[i] = I + b * O[i] + c * O2[i];
-        }
-    }
-    double qe[4], te[3], rt[3];
-    hd_quat_from_matrix(R, qe);
-    for (int i = 0; i < 3; i++) te[i] = V[i * 3] * upd[3] + V[i * 3 + 1] * upd[4] + V[i * 3 + 2] * upd[5];
-    d_quat_rot(qe, t, rt);
-    for (int i = 0; i < 3; i++) t[i] = te[i] + rt[i];
-    double r[4];
-    r[3] = qe[3] * q[3] - qe[0] * q[0] - qe[1] * q[1] - qe[2] * q[2];
-    r[0] = qe[3] * q[0] + qe[0] * q[3] + qe[1] * q[2] - qe[2] * q[1];
-    r[1] = qe[3] * q[1] + qe[1] * q[3] + qe[2] * q[0] - qe[0] * q[2];
-    r[2] = qe[3] * q[2] + qe[2] * q[3] + qe[0] * q[1] - qe[1] * q[0];
-    hd_normalize_rotation(r);
-    for (int i = 0; i < 4; i++) q[i] = r[i];
-}
 
 // ------------------------------------------------------------------ device state
 
