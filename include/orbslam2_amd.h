@@ -309,6 +309,12 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
               lba_result* r);
 
 /* Stage timing of the LM loop (HIP events): ms4 = linearise, Schur, solve, update. */
+/* The reduced camera system solver on its own (LinearSolverEigen::solve's role,
+ * G/solvers/linear_solver_eigen.h:94-120): x = S^-1 b for a symmetric positive-definite
+ * row-major n x n S by the blocked MFMA LDL^T lba_solve runs per LM trial (no pivoting).
+ * Host buffers; synchronous on the context's stream.  Returns ORB_EINVAL when a pivot is
+ * zero or non-finite (the factorisation failure g2o turns into chi2 = inf). */
+int lba_dense_solve(lba_context* c, const double* S, const double* b, int n, double* x);
 int lba_profile(lba_context* c, int enable);
 int lba_stats(lba_context* c, double* ms4, int* iters, int* trials);
 

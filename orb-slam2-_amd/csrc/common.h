@@ -69,6 +69,20 @@ __device__ __forceinline__ int wave_reduce_sum_i32(int v) {
     return v;
 }
 
+// Raw buffer resource over `bytes` bytes at `base` (gfx9 dword 3: 32-bit data format) and a
+// 64-bit load through it.  A byte offset at or past `bytes` reads 0 with no fault, so a guarded
+// gather can issue its loads unconditionally (an out-of-range offset instead of a branch): the
+// compiler then keeps them all in flight rather than waiting on each one behind an exec mask.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+constexpr int kBufOob = 0x7ffffff0;   // an offset past any buffer this library builds
+__device__ __forceinline__ double buf_ld_f64(__amdgpu_buffer_rsrc_t r, int byteoff) {
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    const u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(r, byteoff, 0, 0);
+    return __longlong_as_double((long long)(((unsigned long long)x.y << 32) | x.x));
+}
+
 // XCD-aware 2-D block index.  Workgroups are dealt round-robin over the 8 XCDs (dispatch id d
 // lands on XCD d % 8; observed placement, MI355X_MICROARCH.md "Workgroup dispatch"), so blocks
 // that are neighbours in (x, y) order land on different L2s and each XCD re-fetches the lines the

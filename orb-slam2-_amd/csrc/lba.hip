@@ -3,40 +3,47 @@
 // R/ = /root/reference/ORB-SLAM2注释版/, G/ = R/Thirdparty/g2o/g2o/.
 //
 // Per LM outer iteration (G/core/optimization_algorithm_levenberg.cpp:61-164):
-//   k_edge_errors     computeActiveErrors + robust chi2 per edge (one thread per edge)
-//   k_edge_linearize  EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ Jacobians + Huber-weighted
-//                     quadratic-form blocks per edge (G/core/base_binary_edge.hpp:54-120)
-//   k_point_reduce    Hll, b_l per landmark; k_pose_reduce: Hpp, b_p per pose (one wave per pose)
+//   k_edge_lin        computeActiveErrors + EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ Jacobians
+//                     and Huber-weighted quadratic-form blocks per edge (base_binary_edge.hpp:54-120)
+//   k_vertex_reduce   Hpp, b_p per free pose and Hll, b_l per landmark
+//   k_lm_begin_fused  chi2, lambda init, LM bookkeeping (single workgroup)
 // Per LM trial (lambda):
-//   k_point_schur     D^-1 = (Hll + lambda I)^-1, per-edge Hpl D^-1 and Hpl D^-1 b_l
-//   k_schur_pairs     reduced camera matrix S = Hpp + lambda I - sum W D^-1 W^T, one wave per
-//                     6x6 pose-pair block, deterministic contribution order (G/core/block_solver.hpp:382-433)
-//   k_ldlt_solve      dense LDL^T of S in one workgroup (LinearSolverEigen's SimplicialLDLT role)
-//   k_backsub / k_update / k_edge_errors / reductions: x_l, oplus (SE3Quat::exp * T), chi2, scale.
-// The LM control flow (rho test, lambda schedule, Raul's stop rule, push/pop, the two
-// optimize() rounds and the chi2 outlier passes) runs on the host exactly as g2o/ORB-SLAM2 do,
-// reading back two scalars per trial.  Every reduction has a fixed order, so results are
+//   k_point_schur     D^-1 = (Hll + lambda I)^-1 per landmark, Hpl D^-1 and Hpl D^-1 b_l per edge
+//   k_schur_pairs     reduced camera matrix S = Hpp + lambda I - sum W D^-1 W^T and b_s, one
+//                     workgroup per 6x6 pose-pair block (G/core/block_solver.hpp:382-440)
+//   k_ldlt_solve      dense LDL^T of S in one workgroup, trailing updates on the f64 MFMA units
+//                     (LinearSolverEigen's SimplicialLDLT role)
+//   k_backsub_update  x_l, push + oplus (SE3Quat::exp * T, X += x_l)
+//   k_edge_errors / k_lm_decide_fused: trial chi2, scale, rho test, lambda, pop on rejection.
+// The LM control state lives on the device: a "slot" (linearisation + one trial) is enqueued
+// without host round trips, its kernels run only in their phase, and in a single process the
+// slot is a HIP graph replayed per trial.  Every reduction has a fixed order, so results are
 // bitwise reproducible run to run.  With a communicator (lba_set_comm) the landmarks are
-// sharded over ranks and S, b_s and the chi2 / scale scalars are all-reduced (RCCL via the
-// caller's callback); every rank then solves the same reduced system.
+// sharded over ranks, the bookkeeping runs as separate kernels around the all-reduces of Hpp,
+// b_p, S, b_s and the chi2 / scale scalars (RCCL via the caller's callback), and every rank
+// solves the same reduced system.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cfloat>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <numeric>
 #include <vector>
 
 #include "common.h"
+#include "lba_host.h"
 #include "se3.h"
 
 #ifdef ORB_TIMING   // instrumented variant (tools/build_variant.py)
 #define TSTAMP(v) const long long v = clock64()
 #define TACC(acc, a) acc += clock64() - (a)
+#define HSTAMP(i) hT[i] = std::chrono::steady_clock::now()
 #else
 #define TSTAMP(v)
 #define TACC(acc, a)
+#define HSTAMP(i)
 #endif
 
 namespace orbamd {
@@ -83,7 +90,7 @@ struct LbaDev {
     const int32_t *poStart, *poEdges;     // CSR by pose index (edge ids)
     const int32_t *prStart, *prE1, *prE2; // CSR by pose-pair block (i<=j), contributions (act positions)
     // linearisation (indexed by act position)
-    double *Hll_e, *Hpp_e, *Hpl_e, *bl_e, *bp_e, *BD, *coef, *echi;
+    double *Hll_e, *Hpp_e, *Hpl_e, *bl_e, *bp_e, *echi;
     // reduced per vertex
     double *Hll, *bl, *Dinv, *db, *Hpp, *bp;   // db = Dinv b_l
     double *S, *bs, *x;         // x: [6P + 3M]
@@ -106,11 +113,8 @@ __device__ __forceinline__ double d_edge_chi2(const LbaDev& d, int e) {
     return s;
 }
 
-// computeError for the active edges; echi[k] = robust chi2 (activeRobustChi2 term)
-__global__ __launch_bounds__(256) void k_edge_errors(LbaDev d, double hmono, double hstereo, int want) {
-    if (lm_off(d.lm, want)) return;
-    const int k = blockIdx.x * 256 + threadIdx.x;
-    if (k >= d.nact) return;
+// computeError of active edge k; echi[k] = its robust chi2 (activeRobustChi2 term)
+__device__ __forceinline__ void edge_error(const LbaDev& d, int k, double hmono, double hstereo) {
     const int e = d.act[k];
     double Xc[3];
     d_transform(d, d.eps[e], d.ept[e], Xc);
@@ -140,12 +144,15 @@ __global__ __launch_bounds__(256) void k_edge_errors(LbaDev d, double hmono, dou
     d.echi[k] = chi;
 }
 
+__global__ __launch_bounds__(256) void k_edge_errors(LbaDev d, double hmono, double hstereo, int want) {
+    if (lm_off(d.lm, want)) return;
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k < d.nact) edge_error(d, k, hmono, hstereo);
+}
+
 // Jacobians + Huber-weighted quadratic-form blocks per active edge.
 // Hll_e: 3x3 upper (00 01 02 11 12 22); Hpp_e: 6x6 upper row-major (21); Hpl_e: 6x3; bl_e: 3; bp_e: 6
-__global__ __launch_bounds__(256) void k_edge_linearize(LbaDev d, double hmono, double hstereo) {
-    if (lm_off(d.lm, 0)) return;
-    const int k = blockIdx.x * 256 + threadIdx.x;
-    if (k >= d.nact) return;
+__device__ __forceinline__ void edge_linearize(const LbaDev& d, int k, double hmono, double hstereo) {
     const int e = d.act[k];
     const int pose = d.eps[e];
     double R[9], Xc[3];
@@ -191,17 +198,19 @@ __global__ __launch_bounds__(256) void k_edge_linearize(LbaDev d, double hmono, 
     const double W = rho1 * w;
     double om[3];
     for (int r = 0; r < 3; r++) om[r] = r < D ? -(w * er[r]) * rho1 : 0.0;
+    // the products below run over all 3 rows: a mono edge's third Jacobian row and om[2] are
+    // zero, so the extra terms add exact zeros (constant trip counts keep A, B in registers)
     double* hl = d.Hll_e + 6 * (size_t)k;
     double* bl = d.bl_e + 3 * (size_t)k;
     {
         int o = 0;
         for (int i = 0; i < 3; i++) {
             double s = 0;
-            for (int r = 0; r < D; r++) s += A[r * 3 + i] * om[r];
+            for (int r = 0; r < 3; r++) s += A[r * 3 + i] * om[r];
             bl[i] = s;
             for (int j = i; j < 3; j++) {
                 double h = 0;
-                for (int r = 0; r < D; r++) h += A[r * 3 + i] * W * A[r * 3 + j];
+                for (int r = 0; r < 3; r++) h += A[r * 3 + i] * W * A[r * 3 + j];
                 hl[o++] = h;
             }
         }
@@ -213,26 +222,69 @@ __global__ __launch_bounds__(256) void k_edge_linearize(LbaDev d, double hmono, 
         int o = 0;
         for (int i = 0; i < 6; i++) {
             double s = 0;
-            for (int r = 0; r < D; r++) s += B[r * 6 + i] * om[r];
+            for (int r = 0; r < 3; r++) s += B[r * 6 + i] * om[r];
             bp[i] = s;
             for (int j = i; j < 6; j++) {
                 double h = 0;
-                for (int r = 0; r < D; r++) h += B[r * 6 + i] * W * B[r * 6 + j];
+                for (int r = 0; r < 3; r++) h += B[r * 6 + i] * W * B[r * 6 + j];
                 hp[o++] = h;
             }
             for (int j = 0; j < 3; j++) {
                 double h = 0;
-                for (int r = 0; r < D; r++) h += B[r * 6 + i] * W * A[r * 3 + j];
+                for (int r = 0; r < 3; r++) h += B[r * 6 + i] * W * A[r * 3 + j];
                 hpl[i * 3 + j] = h;
             }
         }
     }
 }
 
-// Hll, b_l per owned landmark (edges in pose-index order)
-__global__ __launch_bounds__(256) void k_point_reduce(LbaDev d) {
+// Phase-0 linearisation of active edge k (computeActiveErrors + linearizeOplus +
+// constructQuadraticForm, G/core/sparse_optimizer.cpp:384-394, block_solver.hpp:502-561).
+__global__ __launch_bounds__(256) void k_edge_lin(LbaDev d, double hmono, double hstereo) {
     if (lm_off(d.lm, 0)) return;
-    const int l = blockIdx.x * 256 + threadIdx.x;
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= d.nact) return;
+    edge_error(d, k, hmono, hstereo);
+    edge_linearize(d, k, hmono, hstereo);
+}
+
+// Vertex blocks: workgroups [0, P) reduce Hpp, b_p of one free pose over its edges (256
+// threads, fixed lane/tree order); the rest reduce Hll, b_l of 256 owned landmarks each (one
+// thread per landmark, edges in pose-index order).
+__global__ __launch_bounds__(256) void k_vertex_reduce(LbaDev d) {
+    if (lm_off(d.lm, 0)) return;
+    const int tid = threadIdx.x;
+    if ((int)blockIdx.x < d.P) {
+        const int p = blockIdx.x, lane = tid & 63, wave = tid >> 6;
+        __shared__ double part[4][28];
+        double acc[27];
+        for (int i = 0; i < 27; i++) acc[i] = 0;
+        for (int a = d.poStart[p] + tid; a < d.poStart[p + 1]; a += 256) {
+            const int k = d.actPos[d.poEdges[a]];
+            for (int i = 0; i < 21; i++) acc[i] += d.Hpp_e[21 * (size_t)k + i];
+            for (int i = 0; i < 6; i++) acc[21 + i] += d.bp_e[6 * (size_t)k + i];
+        }
+        for (int i = 0; i < 27; i++) {
+            double v = acc[i];
+            for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+            if (lane == 0) part[wave][i] = v;
+        }
+        __syncthreads();
+        if (tid < 27) {
+            const double v = (part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]);
+            if (tid < 21) {
+                int i = 0, o = tid;
+                while (o >= 6 - i) { o -= 6 - i; i++; }
+                const int j = i + o;
+                d.Hpp[36 * (size_t)p + i * 6 + j] = v;
+                d.Hpp[36 * (size_t)p + j * 6 + i] = v;
+            } else {
+                d.bp[6 * (size_t)p + tid - 21] = v;
+            }
+        }
+        return;
+    }
+    const int l = ((int)blockIdx.x - d.P) * 256 + tid;
     if (l >= d.M) return;
     double h[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
     for (int a = d.ptStart[l]; a < d.ptStart[l + 1]; a++) {
@@ -247,37 +299,8 @@ __global__ __launch_bounds__(256) void k_point_reduce(LbaDev d) {
     for (int i = 0; i < 3; i++) d.bl[3 * (size_t)l + i] = b[i];
 }
 
-// Hpp, b_p per pose: one wave per pose, lanes stride over the pose's edges, fixed tree.
-__global__ __launch_bounds__(64) void k_pose_reduce(LbaDev d) {
-    if (lm_off(d.lm, 0)) return;
-    const int p = blockIdx.x, lane = threadIdx.x;
-    double acc[27];
-    for (int i = 0; i < 27; i++) acc[i] = 0;
-    for (int a = d.poStart[p] + lane; a < d.poStart[p + 1]; a += 64) {
-        const int k = d.actPos[d.poEdges[a]];
-        for (int i = 0; i < 21; i++) acc[i] += d.Hpp_e[21 * (size_t)k + i];
-        for (int i = 0; i < 6; i++) acc[21 + i] += d.bp_e[6 * (size_t)k + i];
-    }
-    for (int i = 0; i < 27; i++) {
-        double v = acc[i];
-        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-        acc[i] = v;
-    }
-    if (lane == 0) {
-        double* H = d.Hpp + 36 * (size_t)p;
-        int o = 0;
-        for (int i = 0; i < 6; i++)
-            for (int j = i; j < 6; j++) {
-                H[i * 6 + j] = acc[o];
-                H[j * 6 + i] = acc[o];
-                o++;
-            }
-        for (int i = 0; i < 6; i++) d.bp[6 * (size_t)p + i] = acc[21 + i];
-    }
-}
-
-// Per landmark with lambda: Dinv (Eigen 3x3 cofactor inverse) and db = Dinv b_l
-// (G/core/block_solver.hpp:380-398).
+// Per landmark with lambda (G/core/block_solver.hpp:380-398): D^-1 = (Hll + lambda I)^-1
+// (Eigen's 3x3 cofactor inverse) and D^-1 b_l.
 __global__ __launch_bounds__(256) void k_point_schur(LbaDev d) {
     if (lm_off(d.lm, 1)) return;
     const double lambda = d.lm->lambda;
@@ -298,93 +321,94 @@ __global__ __launch_bounds__(256) void k_point_schur(LbaDev d) {
     for (int i = 0; i < 3; i++)
         for (int j = 0; j < 3; j++) Di[j * 3 + i] = c[i * 3 + j] * invdet;
     for (int i = 0; i < 9; i++) d.Dinv[9 * (size_t)l + i] = Di[i];
-    const double* b = d.bl + 3 * (size_t)l;
-    for (int i = 0; i < 3; i++) d.db[3 * (size_t)l + i] = Di[i * 3] * b[0] + Di[i * 3 + 1] * b[1] + Di[i * 3 + 2] * b[2];
+    const double* bl = d.bl + 3 * (size_t)l;
+    for (int i = 0; i < 3; i++) d.db[3 * (size_t)l + i] = Di[i * 3] * bl[0] + Di[i * 3 + 1] * bl[1] + Di[i * 3 + 2] * bl[2];
 }
 
-// Per active edge with a free pose: BD_e = Hpl_e Dinv, coef_e = Hpl_e Dinv b_l.
-__global__ __launch_bounds__(256) void k_edge_schur(LbaDev d) {
+// Reduced camera system (G/core/block_solver.hpp:408-440): one workgroup per pose-pair block
+// (i <= j), S_ij = [i == j](Hpp_i + lambda I) - sum_c (Hpl_c D_l^-1) Hpl_c'^T over the
+// landmarks l seen by both.  Thread t accumulates the whole 6 x 6 product of contributions
+// t, t + 256, ... in registers (Hpl D^-1 formed on the fly); the 256 partials meet in LDS
+// (fixed order).  The diagonal blocks also form b_s,i = b_p,i - sum_e Hpl_e D_l^-1 b_l over
+// pose i's edges (rank 0 carries Hpp + lambda I and b_p).
+constexpr int kSpT = 256;
+__global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag, const int32_t* __restrict__ pairI,
+                                                      const int32_t* __restrict__ pairJ) {
     if (lm_off(d.lm, 1)) return;
-    const int k = blockIdx.x * 256 + threadIdx.x;
-    if (k >= d.nact || d.actPi[k] < 0) return;
-    const int l = d.actPt[k];
-    double Di[9], db[3];
-    for (int i = 0; i < 9; i++) Di[i] = d.Dinv[9 * (size_t)l + i];
-    for (int i = 0; i < 3; i++) db[i] = d.db[3 * (size_t)l + i];
-    const double* Bi = d.Hpl_e + 18 * (size_t)k;
-    double* BD = d.BD + 18 * (size_t)k;
-    double* cf = d.coef + 6 * (size_t)k;
-    for (int r = 0; r < 6; r++) {
-        for (int q = 0; q < 3; q++)
-            BD[r * 3 + q] = Bi[r * 3] * Di[q] + Bi[r * 3 + 1] * Di[3 + q] + Bi[r * 3 + 2] * Di[6 + q];
-        cf[r] = Bi[r * 3] * db[0] + Bi[r * 3 + 1] * db[1] + Bi[r * 3 + 2] * db[2];
-    }
-}
-
-// S_ij block of the reduced camera system, one workgroup per pose pair (i <= j):
-// S_ij = [i == j](Hpp_i + lambda I) - sum_c BD_c Hpl_c'^T over the landmarks c seen by both
-// (G/core/block_solver.hpp:408-440).  Thread t owns output element t % 36 of contribution
-// group t / 36 (7 groups); the group partial sums meet in LDS.
-constexpr int kSpGroups = 7;
-__global__ __launch_bounds__(256) void k_schur_pairs(LbaDev d, int addDiag, const int32_t* pairI,
-                                                     const int32_t* pairJ) {
-    if (lm_off(d.lm, 1)) return;
-    const double lambda = d.lm->lambda;
-    __shared__ double part[kSpGroups][36];
-    const int pr = blockIdx.x, tid = threadIdx.x;
+    __shared__ double part[42][kSpT + 1];
+    const int pr = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const int bi = pairI[pr], bj = pairJ[pr];
-    const int o = tid % 36, grp = tid / 36;
-    const int r = o / 6, q = o % 6;
-    if (grp < kSpGroups) {
-        double acc = 0.0;
-        const int c0 = d.prStart[pr], c1 = d.prStart[pr + 1];
-        for (int c = c0 + grp; c < c1; c += kSpGroups) {
-            const double* BD = d.BD + 18 * (size_t)d.prE1[c] + r * 3;
-            const double* Bj = d.Hpl_e + 18 * (size_t)d.prE2[c] + q * 3;
-            acc += BD[0] * Bj[0] + BD[1] * Bj[1] + BD[2] * Bj[2];
+    double acc[42];
+#pragma unroll
+    for (int i = 0; i < 42; i++) acc[i] = 0.0;
+    const int c0 = d.prStart[pr], c1 = d.prStart[pr + 1];
+    for (int c = c0 + tid; c < c1; c += kSpT) {
+        const int e1 = d.prE1[c];
+        const double2* Bi = reinterpret_cast<const double2*>(d.Hpl_e + 18 * (size_t)e1);
+        const double2* Bj = reinterpret_cast<const double2*>(d.Hpl_e + 18 * (size_t)d.prE2[c]);
+        const double* Dl = d.Dinv + 9 * (size_t)d.actPt[e1];
+        double w[18], v[18], Di[9], u[18];
+#pragma unroll
+        for (int h = 0; h < 9; h++) {
+            const double2 x = Bi[h], y = Bj[h];
+            w[2 * h] = x.x; w[2 * h + 1] = x.y;
+            v[2 * h] = y.x; v[2 * h + 1] = y.y;
+            Di[h] = Dl[h];
         }
-        part[grp][o] = acc;
+#pragma unroll
+        for (int r = 0; r < 6; r++)   // Hpl D^-1 (the BD product of block_solver.hpp:419)
+#pragma unroll
+            for (int q = 0; q < 3; q++)
+                u[r * 3 + q] = w[r * 3] * Di[q] + w[r * 3 + 1] * Di[3 + q] + w[r * 3 + 2] * Di[6 + q];
+#pragma unroll
+        for (int r = 0; r < 6; r++)
+#pragma unroll
+            for (int q = 0; q < 6; q++)
+                acc[r * 6 + q] += u[r * 3] * v[q * 3] + u[r * 3 + 1] * v[q * 3 + 1] + u[r * 3 + 2] * v[q * 3 + 2];
     }
+    const bool diag = bi == bj;
+    if (diag) {
+        for (int a = d.poStart[bi] + tid; a < d.poStart[bi + 1]; a += kSpT) {
+            const int k = d.actPos[d.poEdges[a]];
+            const double* B = d.Hpl_e + 18 * (size_t)k;
+            const double* db = d.db + 3 * (size_t)d.actPt[k];
+            const double b0 = db[0], b1 = db[1], b2 = db[2];
+#pragma unroll
+            for (int i = 0; i < 6; i++) acc[36 + i] += B[i * 3] * b0 + B[i * 3 + 1] * b1 + B[i * 3 + 2] * b2;
+        }
+    }
+    const int nv = diag ? 42 : 36;
+#pragma unroll
+    for (int i = 0; i < 42; i++)
+        if (i < nv) part[i][tid] = acc[i];
     __syncthreads();
-    if (tid < 36) {
-        double sacc = 0.0;
-        for (int g2 = 0; g2 < kSpGroups; g2++) sacc += part[g2][tid];
-        double v = 0.0;
-        if (bi == bj && addDiag) {     // rank 0 carries the (already all-reduced) Hpp + lambda I
-            v = d.Hpp[36 * (size_t)bi + tid];
-            if (r == q) v += lambda;
-        }
-        v -= sacc;
+    // value v = t >> 2, quarter q = t & 3 sums part[v][64q .. 64q + 63]; quarters meet by xor
+    const int t = tid, v = t >> 2, q = t & 3;
+    double sum = 0.0;
+    if (v < nv) {
+#pragma unroll 8
+        for (int i = 0; i < 64; i++) sum += part[v][64 * q + i];
+    }
+    sum += __shfl_xor(sum, 1, 64);
+    sum += __shfl_xor(sum, 2, 64);
+    (void)lane;
+    if (v < nv && q == 0) {
         const int n = 6 * d.P;
-        d.S[(size_t)(6 * bi + r) * n + 6 * bj + q] = v;
-        d.S[(size_t)(6 * bj + q) * n + 6 * bi + r] = v;
+        if (v < 36) {
+            const int r = v / 6, qq = v % 6;
+            double val = 0.0;
+            if (diag && addDiag) {
+                val = d.Hpp[36 * (size_t)bi + v];
+                if (r == qq) val += d.lm->lambda;
+            }
+            val -= sum;
+            d.S[(size_t)(6 * bi + r) * n + 6 * bj + qq] = val;
+            d.S[(size_t)(6 * bj + qq) * n + 6 * bi + r] = val;
+        } else {
+            d.bs[6 * bi + v - 36] = (addDiag ? d.bp[6 * bi + v - 36] : 0.0) - sum;
+        }
     }
 }
-
-// b_s = b_p - sum_e coef_e, one wave per pose
-__global__ __launch_bounds__(64) void k_bschur(LbaDev d, int addBp) {
-    if (lm_off(d.lm, 1)) return;
-    const int p = blockIdx.x, lane = threadIdx.x;
-    double acc[6] = {0, 0, 0, 0, 0, 0};
-    for (int a = d.poStart[p] + lane; a < d.poStart[p + 1]; a += 64) {
-        const double* cf = d.coef + 6 * (size_t)d.actPos[d.poEdges[a]];
-        for (int i = 0; i < 6; i++) acc[i] += cf[i];
-    }
-    for (int i = 0; i < 6; i++) {
-        double v = acc[i];
-        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-        acc[i] = v;
-    }
-    if (lane < 6) {
-        double s = 0;
-        for (int i = 0; i < 6; i++) s = (i == lane) ? acc[i] : s;
-        d.bs[6 * p + lane] = (addBp ? d.bp[6 * p + lane] : 0.0) - s;
-    }
-}
-
-constexpr int kLdltW = 8;     // panel width (columns per pair of workgroup barriers)
-constexpr int kLdltT = 512;   // 8 waves: 2 per SIMD for the trailing update
-constexpr int kLdltMaxN = 192; // panel rows held in registers: 3 per lane
 
 // Broadcast of lane `src` (a compile-time constant at every call site) through two
 // v_readlane_b32 into SGPRs: a few cycles, against a ds_bpermute round trip for __shfl.
@@ -395,262 +419,340 @@ __device__ __forceinline__ double shfl_d(double v, int src) {
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
-// Dense LDL^T (no pivoting; fails only on a zero pivot, like SimplicialLDLT) + solve, one
-// workgroup of kLdltT threads; the n x n matrix is staged in LDS when it fits (n <= 136, i.e.
-// up to 22 free keyframes), otherwise factored in place in global memory (L2-resident).
-// Element recurrence (oracle/lba_oracle.c states it column by column): with W(i,k) the value
-// of A(i,k) before the division by d_k and L(i,k) = W(i,k)/d_k,
-//     A(i,j) = fma(-W(i,k), L(j,k), A(i,j))   for k = 0 .. j-1 in order,
-// one fused multiply-add per update (against (L_ik L_jk) d_k, three rounded operations).
-// W is kept in the upper triangle, L in the lower.  Right-looking in panels of kLdltW columns:
-//  * wave 0 factors the panel in registers (3 panel rows per lane, pivots and L entries
-//    broadcast with v_readlane);
-//  * all threads apply the panel's updates to the trailing lower triangle in 4 x 4 register
-//    tiles, each element taking them in column order;
-// so every element sees the recurrence's exact operation sequence, with two workgroup barriers
-// per panel.  The triangular solves (y_i = fma(-L_ik, y_k, y_i), k in order) are blocked the
-// same way on one wave.
-// Panel [jb, je) of the factorisation on one wave, rows jb + lane + 64u for u < NS (NS = slots
-// that hold rows: the matrix has n - jb rows left).  Column j: d_j = A(j,j); W(i,j) = A(i,j)
-// before the division goes to the upper triangle at (j, i), L(i,j) = W(i,j)/d_j to the lower;
-// the panel's later columns take A(i,k) = fma(-W(i,j), L(k,j), A(i,k)), and the forward
-// substitution advances with the factorisation: y_i = fma(-L(i,j), y_j, y_i) for i > j once
-// y_j is final.  Values computed on or above the diagonal are not stored.  Returns false on a
-// zero or non-finite pivot.
-template <int NS>
-__device__ __forceinline__ bool ldlt_panel(double* __restrict__ A, int ld, int n, int jb, int je, double* __restrict__ dg,
-                                           double* __restrict__ y, int lane) {
-    double P[NS][kLdltW], Wp[NS][kLdltW], Y[NS];
-#pragma unroll
-    for (int u = 0; u < NS; u++) {
-        const int r = jb + lane + 64 * u;
-        Y[u] = r < n ? y[r] : 0.0;
-#pragma unroll
-        for (int c = 0; c < kLdltW; c++) {
-            P[u][c] = (r < n && jb + c < je) ? A[(size_t)r * ld + jb + c] : 0.0;
-            Wp[u][c] = 0.0;
-        }
-    }
-    bool bad = false;
-#pragma unroll
-    for (int c = 0; c < kLdltW; c++) {
-        const int j = jb + c;
-        if (j < je && !bad) {
-            const double dj = shfl_d(P[0][c], c);   // A(j, j): row j is lane c, slot 0
-            if (dj == 0.0 || !isfinite(dj)) {
-                bad = true;
-            } else {
-#pragma unroll
-                for (int u = 0; u < NS; u++) {
-                    Wp[u][c] = P[u][c];
-                    P[u][c] = P[u][c] / dj;
-                }
-                if (lane == 0) dg[j] = dj;
-                const double yj = shfl_d(Y[0], c);   // final: every k < j has been applied
-#pragma unroll
-                for (int u = 0; u < NS; u++)
-                    if (jb + lane + 64 * u > j) Y[u] = __builtin_fma(-P[u][c], yj, Y[u]);
-                double lkv[kLdltW];
-#pragma unroll
-                for (int k = c + 1; k < kLdltW; k++) lkv[k] = shfl_d(P[0][c], k);   // L(jb+k, j)
-#pragma unroll
-                for (int k = c + 1; k < kLdltW; k++)
-#pragma unroll
-                    for (int u = 0; u < NS; u++) P[u][k] = __builtin_fma(-Wp[u][c], lkv[k], P[u][k]);
-            }
-        }
-    }
-#pragma unroll
-    for (int u = 0; u < NS; u++) {
-        const int r = jb + lane + 64 * u;
-        if (r < n) y[r] = Y[u];
-#pragma unroll
-        for (int c = 0; c < kLdltW; c++)
-            if (r < n && r > jb + c && jb + c < je) {
-                A[(size_t)r * ld + jb + c] = P[u][c];      // L(r, jb+c), strict lower
-                A[(size_t)(jb + c) * ld + r] = Wp[u][c];   // W(r, jb+c) at (jb+c, r)
-            }
-    }
-    return !bad;
+// ------------------------------------------------------------------ reduced camera solve
+// Dense LDL^T of S (no pivoting; fails only on a zero or non-finite pivot, like
+// SimplicialLDLT, G/solvers/linear_solver_eigen.h:94-120) + both triangular solves, one
+// workgroup of kLdlT threads.  Blocked right-looking in 16-column panels (one f64 MFMA tile
+// edge).  The matrix is padded to np = 16 * ceil(n / 16) with the identity and held in LDS
+// when it fits (np <= 128, i.e. up to 21 free keyframes), otherwise in a global scratch
+// (L2-resident).  W(i,j) = A(i,j) before the scaling by 1/d_j is kept in the upper triangle
+// at (j, i), L(i,j) = W(i,j) / d_j in the lower.  Per panel [jb, jb+16):
+//  1. wave 0 factors the panel with its rows (up to 192, three per lane) in registers: pivots
+//     and L entries broadcast with v_readlane, 1/d_j by v_rcp_f64 + two Newton steps, the
+//     forward substitution folded in; rows beyond 192 (large systems) follow one per thread;
+//  2. trailing lower triangle: A(I, K) -= W(I, panel) L(K, panel)^T per 16 x 16 tile with four
+//     v_mfma_f64_16x16x4_f64 (tiles dealt round-robin to the 8 waves).
+// Then y /= d and the backward substitution with L^T on one wave in 16-row blocks.  The
+// oracle (oracle/lba_oracle.c) runs the unblocked column recurrence with IEEE divisions; the
+// two agree to rounding (tests compare the LM traces to 1e-9 relative).
+constexpr int kNB = 16;
+constexpr int kLdlT = 512;
+constexpr int kLdlLdsMaxN = 128;   // padded order held in LDS: (128 * 129 + 3 * 128 + 64) * 8 B = 133 KB
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ double rcp_nr(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    double e = __builtin_fma(-d, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-d, r, 1.0);
+    return __builtin_fma(r, e, r);
 }
 
+// Panel [jb, jb+16) on wave 0 for rows jb + lane + 64u, u < NS (rows >= np are skipped):
+// column j = jb + c: d_j = A(j, j) (lane c, slot 0), W(i, j) = A(i, j) goes to the upper
+// triangle at (j, i), L(i, j) = W(i, j) / d_j to the lower, the panel's later columns take
+// A(i, k) = fma(-L(i, j), W(k, j), A(i, k)), and the forward substitution advances with the
+// factorisation (y_i = fma(-L(i, j), y_j, y_i) once y_j is final).  W(jb+k, j) reaches the
+// other lanes by v_readlane for k = c+1 (the next pivot's column) and as a broadcast LDS read
+// of the row just stored for k > c+1.  Branch-free: a zero or non-finite pivot only clears
+// the returned flag; stores a lane must not make go to its `dummy` slot.
+template <int NS>
+__device__ __forceinline__ bool ldlt_panel(double* __restrict__ A, int ld, int np, int jb, double* __restrict__ dg,
+                                           double* __restrict__ rdg, double* __restrict__ y, double* dummy,
+                                           int lane) {
+    double P[NS][kNB], Y[NS];
+#pragma unroll
+    for (int u = 0; u < NS; u++) {   // rows past np read row np-1 (never stored): no exec-masked loads
+        const int r = min(jb + lane + 64 * u, np - 1);
+        Y[u] = y[r];
+#pragma unroll
+        for (int c = 0; c < kNB; c++) P[u][c] = A[(size_t)r * ld + jb + c];
+    }
+    // Software-pipelined by one column: column c's updates of columns k > c+1 are issued
+    // between the steps of the next pivot's reciprocal (the dependent chain
+    // readlane -> v_rcp_f64 -> Newton -> scale -> column c+1 update -> readlane), so the
+    // in-order wave has independent work while the chain's results are in flight.
+    double dj = shfl_d(P[0][0], 0);
+    bool ok = dj != 0.0 && isfinite(dj);
+    double rd = rcp_nr(dj);
+#pragma unroll
+    for (int c = 0; c < kNB; c++) {
+        const int j = jb + c;
+        const double yj = shfl_d(Y[0], c);   // final: every k < j has been applied
+        double w[NS], l[NS];
+#pragma unroll
+        for (int u = 0; u < NS; u++) {
+            const int r = jb + lane + 64 * u;
+            w[u] = P[u][c];
+            l[u] = w[u] * rd;
+            P[u][c] = l[u];
+            const bool st = r < np && lane + 64 * u > c;
+            *(st ? A + (size_t)j * ld + r : dummy + lane) = w[u];   // W(r, j)
+            *(st ? A + (size_t)r * ld + j : dummy + lane) = l[u];   // L(r, j)
+        }
+        if (lane == 0) { dg[j] = dj; rdg[j] = rd; }
+        double wk[kNB];
+        const double* Wrow = A + (size_t)j * ld + jb;
+#pragma unroll
+        for (int k = c + 2; k < kNB; k++) wk[k] = Wrow[k];   // W(jb+k, j): broadcast LDS reads
+        double djn = 1.0, r0 = 1.0, e0 = 0.0, r1 = 1.0, e1 = 0.0;
+        if (c + 1 < kNB) {   // next pivot: column c+1 first
+            const double w1 = shfl_d(w[0], c + 1);   // W(j+1, j)
+#pragma unroll
+            for (int u = 0; u < NS; u++) P[u][c + 1] = __builtin_fma(-l[u], w1, P[u][c + 1]);
+            djn = shfl_d(P[0][c + 1], c + 1);
+            r0 = __builtin_amdgcn_rcp(djn);
+        }
+        // the deferred updates, in three groups between the reciprocal's steps
+        const int nk = kNB - 2 - c > 0 ? kNB - 2 - c : 0;   // folded: the loop is unrolled
+        const int g1 = c + 2 + (nk + 2) / 3, g2 = c + 2 + 2 * (nk + 2) / 3;
+#pragma unroll
+        for (int k = c + 2; k < kNB && k < g1; k++)
+#pragma unroll
+            for (int u = 0; u < NS; u++) P[u][k] = __builtin_fma(-l[u], wk[k], P[u][k]);
+        if (c + 1 < kNB) { e0 = __builtin_fma(-djn, r0, 1.0); r1 = __builtin_fma(r0, e0, r0); }
+#pragma unroll
+        for (int u = 0; u < NS; u++)
+            if (lane + 64 * u > c) Y[u] = __builtin_fma(-l[u], yj, Y[u]);
+#pragma unroll
+        for (int k = g1; k < kNB && k < g2; k++)
+#pragma unroll
+            for (int u = 0; u < NS; u++) P[u][k] = __builtin_fma(-l[u], wk[k], P[u][k]);
+        if (c + 1 < kNB) { e1 = __builtin_fma(-djn, r1, 1.0); r1 = __builtin_fma(r1, e1, r1); }
+#pragma unroll
+        for (int k = g2; k < kNB; k++)
+#pragma unroll
+            for (int u = 0; u < NS; u++) P[u][k] = __builtin_fma(-l[u], wk[k], P[u][k]);
+        if (c + 1 < kNB) {
+            ok = ok && djn != 0.0 && isfinite(djn);
+            dj = djn;
+            rd = r1;
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < NS; u++) {
+        const int r = jb + lane + 64 * u;
+        if (r < np) y[r] = Y[u];
+    }
+    return ok;
+}
+
+constexpr int kPanelRows = 192;   // rows of a panel factored in wave 0's registers (3 per lane)
+
 template <bool kLds>
-__global__ __launch_bounds__(kLdltT) void k_ldlt_solve(double* __restrict__ Ag, const double* __restrict__ b, int n,
-                                                       double* __restrict__ x, int* __restrict__ flags,
-                                                       const LmState* st) {
+__global__ __launch_bounds__(kLdlT) void k_ldlt_solve(const double* __restrict__ Sg, const double* __restrict__ b,
+                                                      int n, double* __restrict__ work, double* __restrict__ x,
+                                                      int* __restrict__ flags, const LmState* st) {
     if (lm_off(st, 1)) return;
     extern __shared__ __attribute__((aligned(16))) double sh[];
     TSTAMP(t_l0);
-    long long tPanel = 0, tTrail = 0, tPLoad = 0, tPCol = 0, tFLoad = 0, tFChain = 0, tFRows = 0;
-    (void)tPanel; (void)tTrail; (void)tPLoad; (void)tPCol; (void)tFLoad; (void)tFChain; (void)tFRows;
-    // (forward substitution runs inside the panels; tPLoad/tPCol/tF* stay 0 in this layout)
-    // LDS rows padded to an odd number of doubles: the panel's column accesses (lanes one row
-    // apart) then spread over the banks instead of hitting a few of them
-    const int ld = kLds ? (n | 1) : n;
-    double* A = kLds ? sh : Ag;
-    double* dg = sh + (kLds ? (size_t)n * ld : 0);
-    double* y = dg + n;
+    long long tDiag = 0, tRows = 0, tTrail = 0;
+    (void)tDiag; (void)tRows; (void)tTrail;
+#ifdef ORB_TIMING
+    long long tp[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tpb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+    const int np = (n + kNB - 1) & ~(kNB - 1);
+    const int ld = np + 1;   // odd: column-strided lanes spread over the LDS banks
+    double* A = kLds ? sh : work;
+    double* dg = sh + (kLds ? (size_t)np * ld : 0);
+    double* rdg = dg + np;
+    double* y = rdg + np;
+    double* dummy = y + np;   // 64 per-lane sinks for masked-off panel stores
     __shared__ int failS;
-    const int tid = threadIdx.x, lane = tid & 63;
-    if (kLds) {
-        for (int t0 = 0; t0 < n * n; t0 += kLdltT * 8) {   // 8 loads in flight per thread
-            double v[8];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // ---- stage S (n x n, row-major) into the padded np x np image (identity padding);
+    //      wave w copies rows w, w + 8, ... in 64-column chunks, 16 unconditional loads
+    //      (clamped addresses) in flight per lane, no integer division
+    {
+        constexpr int kW = kLdlT / 64;
+        const __amdgpu_buffer_rsrc_t rs = buf_rsrc(Sg, (uint32_t)n * n * 8);
+        for (int j0 = 0; j0 < np; j0 += 64) {
+            const int j = j0 + lane;
+            for (int i0 = wave; i0 < np; i0 += kW * 16) {
+                double v[16];
 #pragma unroll
-            for (int u = 0; u < 8; u++) v[u] = t0 + u * kLdltT + tid < n * n ? Ag[t0 + u * kLdltT + tid] : 0.0;
+                for (int u = 0; u < 16; u++) {   // padding: offset out of range -> 0, plus identity
+                    const int i = i0 + kW * u;
+                    const bool in = i < n && j < n;
+                    v[u] = buf_ld_f64(rs, in ? (i * n + j) * 8 : kBufOob) + ((!in && i == j) ? 1.0 : 0.0);
+                }
 #pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const int t = t0 + u * kLdltT + tid;
-                if (t < n * n) A[(size_t)(t / n) * ld + t % n] = v[u];
+                for (int u = 0; u < 16; u++) {
+                    const int i = i0 + kW * u;
+                    if (i < np && j < np) A[(size_t)i * ld + j] = v[u];
+                }
             }
         }
+        for (int t = tid; t < np; t += kLdlT) y[t] = t < n ? b[t] : 0.0;
     }
-    for (int t = tid; t < n; t += kLdltT) y[t] = b[t];
+    TSTAMP(t_sa);
     if (tid == 0) failS = 0;
     __syncthreads();
-#ifdef ORB_TIMING
-    const long long t_p_first = clock64() - t_l0;
-#endif
-    for (int jb = 0; jb < n; jb += kLdltW) {
-        const int je = min(jb + kLdltW, n);
-        TSTAMP(t_p0);
-        if (tid < 64) {
-            const int ns = (n - jb + 63) >> 6;
-            const bool okp = ns == 1   ? ldlt_panel<1>(A, ld, n, jb, je, dg, y, lane)
-                             : ns == 2 ? ldlt_panel<2>(A, ld, n, jb, je, dg, y, lane)
-                                       : ldlt_panel<3>(A, ld, n, jb, je, dg, y, lane);
+    TSTAMP(t_f0);
+    const int T = np / kNB;
+    for (int kb = 0; kb < T; kb++) {
+        const int jb = kb * kNB;
+        TSTAMP(t_d0);
+        // ---- 1. panel: rows [jb, jb + 192) in wave 0's registers
+        if (wave == 0) {
+            const int ns = min(np - jb, kPanelRows);
+            bool okp;
+            if (ns <= 64) okp = ldlt_panel<1>(A, ld, jb + ns, jb, dg, rdg, y, dummy, lane);
+            else if (kLds || ns <= 128) okp = ldlt_panel<2>(A, ld, jb + ns, jb, dg, rdg, y, dummy, lane);   // LDS: np <= 128
+            else okp = ldlt_panel<3>(A, ld, jb + ns, jb, dg, rdg, y, dummy, lane);
             if (!okp && lane == 0) failS = 1;
         }
+#ifdef ORB_TIMING
+        const long long t_d1 = clock64();
+#endif
         __syncthreads();
-        TACC(tPanel, t_p0);
-        TSTAMP(t_t0);
+        TACC(tDiag, t_d0);
+#ifdef ORB_TIMING
+        if (kb < 8) { tp[kb] = t_d1 - t_d0; tpb[kb] = clock64() - t_d1; }
+#endif
         if (failS) break;
-        // ---- trailing lower triangle (rows, columns >= je) in 4 x 4 tiles, one tile per thread
-        //      (triangular numbering t -> (ti, tk), tk <= ti); element (i, k) takes
-        //      A(i,k) = fma(-W(i,p), L(k,p), A(i,k)) for the panel's columns p in order
+        TSTAMP(t_r0);
+        // ---- 1b. rows beyond the register panel (large systems only), one thread per row:
+        //          W(i, jb+c) = A(i, jb+c) - sum_{k<c} W(i, jb+k) L(jb+c, jb+k)
+        if (np - jb > kPanelRows) {
+            for (int i = jb + kPanelRows + tid; i < np; i += kLdlT) {
+                double w[kNB];
+                double Y = y[i];
+#pragma unroll
+                for (int c = 0; c < kNB; c++) {
+                    double v = A[(size_t)i * ld + jb + c];
+                    const double* Lc = A + (size_t)(jb + c) * ld + jb;
+#pragma unroll
+                    for (int k = 0; k < c; k++) v = __builtin_fma(-w[k], Lc[k], v);
+                    w[c] = v;
+                }
+#pragma unroll
+                for (int c = 0; c < kNB; c++) {
+                    const double l = w[c] * rdg[jb + c];
+                    A[(size_t)i * ld + jb + c] = l;
+                    A[(size_t)(jb + c) * ld + i] = w[c];
+                    Y = __builtin_fma(-l, y[jb + c], Y);
+                }
+                y[i] = Y;
+            }
+            __syncthreads();
+        }
+        TACC(tRows, t_r0);
+        TSTAMP(t_t0);
+        // ---- 2. trailing lower triangle, 16 x 16 tiles (I >= K > kb) on the MFMA units:
+        //         A(I, K) -= W(I, panel) L(K, panel)^T, four v_mfma_f64_16x16x4_f64 per tile
         {
-            const int m = n - je, T = (m + 3) >> 2, nt = T * (T + 1) / 2;
-            for (int t = tid; t < nt; t += kLdltT) {
+            const int m = T - kb - 1, nt = m * (m + 1) / 2;
+            const int li = lane & 15, lk = lane >> 4;
+            for (int t = wave; t < nt; t += kLdlT / 64) {
                 int ti = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
                 while ((ti + 1) * (ti + 2) / 2 <= t) ti++;
                 while (ti * (ti + 1) / 2 > t) ti--;
                 const int tk = t - ti * (ti + 1) / 2;
-                double wi[4][kLdltW], lk[4][kLdltW], v[4][4];
+                const int I0 = (kb + 1 + ti) * kNB, K0 = (kb + 1 + tk) * kNB;
+                double a[kNB / 4], bb[kNB / 4];
+                dbl4 acc;
 #pragma unroll
-                for (int p = 0; p < kLdltW; p++)
+                for (int s = 0; s < kNB / 4; s++) {
+                    const int p = jb + 4 * s + lk;
+                    a[s] = -A[(size_t)p * ld + I0 + li];        // -W(I0 + li, p)
+                    bb[s] = A[(size_t)(K0 + li) * ld + p];      //  L(K0 + li, p)
+                }
 #pragma unroll
-                    for (int a2 = 0; a2 < 4; a2++) {
-                        const int i = je + 4 * ti + a2, k = je + 4 * tk + a2;
-                        wi[a2][p] = (i < n && jb + p < je) ? A[(size_t)(jb + p) * ld + i] : 0.0;   // W(i, jb+p)
-                        lk[a2][p] = (k < n && jb + p < je) ? A[(size_t)k * ld + jb + p] : 0.0;     // L(k, jb+p)
-                    }
+                for (int q = 0; q < 4; q++) acc[q] = A[(size_t)(I0 + lk + 4 * q) * ld + K0 + li];
 #pragma unroll
-                for (int a2 = 0; a2 < 4; a2++)
+                for (int s = 0; s < kNB / 4; s++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], bb[s], acc, 0, 0, 0);
 #pragma unroll
-                    for (int b2 = 0; b2 < 4; b2++) {
-                        const int i = je + 4 * ti + a2, k = je + 4 * tk + b2;
-                        v[a2][b2] = (i < n && k <= i) ? A[(size_t)i * ld + k] : 0.0;
-                    }
-#pragma unroll
-                for (int p = 0; p < kLdltW; p++)
-#pragma unroll
-                    for (int a2 = 0; a2 < 4; a2++)
-#pragma unroll
-                        for (int b2 = 0; b2 < 4; b2++) v[a2][b2] = __builtin_fma(-wi[a2][p], lk[b2][p], v[a2][b2]);
-#pragma unroll
-                for (int a2 = 0; a2 < 4; a2++)
-#pragma unroll
-                    for (int b2 = 0; b2 < 4; b2++) {
-                        const int i = je + 4 * ti + a2, k = je + 4 * tk + b2;
-                        if (i < n && k <= i) A[(size_t)i * ld + k] = v[a2][b2];
-                    }
+                for (int q = 0; q < 4; q++) A[(size_t)(I0 + lk + 4 * q) * ld + K0 + li] = acc[q];
             }
         }
         __syncthreads();
         TACC(tTrail, t_t0);
     }
-    TSTAMP(t_l1);
+    TSTAMP(t_s0);
     if (failS) {
         if (tid == 0) flags[0] = 1;
         return;
     }
-    if (tid >= 64) return;
-    for (int i = lane; i < n; i += 64) y[i] = y[i] / dg[i];
+    if (wave != 0) return;
+    for (int i = lane; i < np; i += 64) y[i] = y[i] * rdg[i];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    // ---- backward substitution with L^T (per element: y_i -= L_ki x_k, k descending)
-    for (int ke = n; ke > 0; ke -= kLdltW) {
-        const int kb = max(ke - kLdltW, 0), w = ke - kb;
-        double Ab[kLdltW], Ar[3][kLdltW], yr[3];
+    // ---- backward substitution with L^T: x_i = y_i - sum_{k > i} L(k, i) x_k, k descending,
+    //      in 16-row blocks from the bottom on wave 0
+    for (int kb = np - kNB; kb >= 0; kb -= kNB) {
+        const int r = lane & 15;
+        double Ab[kNB];
 #pragma unroll
-        for (int c = 0; c < kLdltW; c++) Ab[c] = (lane < c && c < w) ? A[(size_t)(kb + c) * ld + kb + lane] : 0.0;
+        for (int c = 0; c < kNB; c++) Ab[c] = A[(size_t)(kb + c) * ld + kb + r];   // L(kb+c, kb+r), used for r < c
+        double xb = y[kb + r];
 #pragma unroll
-        for (int u = 0; u < 3; u++) {
-            const int i = lane + 64 * u;
-            yr[u] = i < kb ? y[i] : 0.0;
-#pragma unroll
-            for (int c = 0; c < kLdltW; c++) Ar[u][c] = (i < kb && c < w) ? A[(size_t)(kb + c) * ld + i] : 0.0;
-        }
-        double xb = lane < w ? y[kb + lane] : 0.0;
-#pragma unroll
-        for (int c = kLdltW - 1; c >= 0; c--) {
-            if (c >= w) continue;
+        for (int c = kNB - 1; c > 0; c--) {
             const double xc = shfl_d(xb, c);
-            if (lane < c) xb = __builtin_fma(-Ab[c], xc, xb);
+            xb = r < c ? __builtin_fma(-Ab[c], xc, xb) : xb;
         }
-        double xs[kLdltW];
+        double xs[kNB];
 #pragma unroll
-        for (int c = 0; c < kLdltW; c++) xs[c] = shfl_d(xb, c);
-        if (lane < w) y[kb + lane] = xb;
+        for (int c = 0; c < kNB; c++) xs[c] = shfl_d(xb, c);
+        if (lane < kNB) y[kb + r] = xb;
+        for (int i0 = 0; i0 < kb; i0 += 128) {   // two rows per lane per pass
+            const int i1 = i0 + lane, i2 = i0 + 64 + lane;
+            const int c1 = min(i1, kb - 1), c2 = min(i2, kb - 1);   // clamped reads, guarded stores
+            double v1 = y[c1], v2 = y[c2];
+            double l1[kNB], l2[kNB];
 #pragma unroll
-        for (int u = 0; u < 3; u++) {
-            const int i = lane + 64 * u;
-            double v = yr[u];
+            for (int c = 0; c < kNB; c++) {
+                l1[c] = A[(size_t)(kb + c) * ld + c1];
+                l2[c] = A[(size_t)(kb + c) * ld + c2];
+            }
 #pragma unroll
-            for (int c = kLdltW - 1; c >= 0; c--)
-                if (c < w) v = __builtin_fma(-Ar[u][c], xs[c], v);
-            if (i < kb) y[i] = v;
+            for (int c = kNB - 1; c >= 0; c--) {
+                v1 = __builtin_fma(-l1[c], xs[c], v1);
+                v2 = __builtin_fma(-l2[c], xs[c], v2);
+            }
+            if (i1 < kb) y[i1] = v1;
+            if (i2 < kb) y[i2] = v2;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
     }
     for (int i = lane; i < n; i += 64) x[i] = y[i];
-    if (tid == 0) flags[0] = 0;
+    if (lane == 0) flags[0] = 0;
 #ifdef ORB_TIMING
-    if (tid == 0) printf("ldlt n %d: stage %lld panel %lld (load %lld cols %lld) trailing %lld solves %lld (fwd load %lld chain %lld rows %lld)\n", n, t_p_first, tPanel, tPLoad, tPCol, tTrail, clock64() - t_l1, tFLoad, tFChain, tFRows);
+    if (lane == 0) printf("ldlt n %d: stage %lld (own %lld) panel %lld rows %lld trailing %lld solve %lld | panels %lld %lld %lld %lld %lld %lld %lld %lld | bar %lld %lld\n", n, t_f0 - t_l0, t_sa - t_l0, tDiag, tRows, tTrail, clock64() - t_s0, tp[0], tp[1], tp[2], tp[3], tp[4], tp[5], tp[6], tp[7], tpb[0], tpb[1]);
 #endif
 }
 
-// x_l = Dinv (b_l - sum_e Hpl_e^T x_p(pose_e))
-__global__ __launch_bounds__(256) void k_backsub(LbaDev d) {
-    if (lm_off(d.lm, 1)) return;
-    const int l = blockIdx.x * 256 + threadIdx.x;
-    if (l >= d.M) return;
-    double cl[3] = {d.bl[3 * (size_t)l], d.bl[3 * (size_t)l + 1], d.bl[3 * (size_t)l + 2]};
-    for (int a = d.ptStart[l]; a < d.ptStart[l + 1]; a++) {
-        const int e = d.ptEdges[a];
-        const int pi = d.poseIdx[d.eps[e]];
-        if (pi < 0) continue;
-        const double* Bi = d.Hpl_e + 18 * (size_t)d.actPos[e];
-        for (int q = 0; q < 3; q++)
-            for (int r = 0; r < 6; r++) cl[q] += Bi[r * 3 + q] * (-d.x[6 * pi + r]);
-    }
-    const double* Di = d.Dinv + 9 * (size_t)l;
-    double* xl = d.x + 6 * (size_t)d.P + 3 * (size_t)l;
-    for (int q = 0; q < 3; q++) xl[q] = Di[q * 3] * cl[0] + Di[q * 3 + 1] * cl[1] + Di[q * 3 + 2] * cl[2];
-}
 
-// push (backup) + oplus for all free poses and owned points
-__global__ __launch_bounds__(256) void k_update(LbaDev d, int nposes, const int32_t* freePoses, int applyPoses) {
+// Back-substitution and update (G/core/block_solver.hpp:462-484, sparse_optimizer.cpp:422-435):
+// thread l: x_l = D^-1 (b_l - sum_e Hpl_e^T x_p(pose_e)), push() of X_l and X_l += x_l; the
+// first P threads also push and apply T <- exp(x_p) T to their free pose.
+__global__ __launch_bounds__(256) void k_backsub_update(LbaDev d, const int32_t* __restrict__ freePoses) {
     if (lm_off(d.lm, 1)) return;
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i < d.M) {
-        const int g = d.ptGlob[i];
-        for (int j = 0; j < 3; j++) {
-            d.bX[3 * (size_t)g + j] = d.X[3 * (size_t)g + j];
-            d.X[3 * (size_t)g + j] += d.x[6 * (size_t)d.P + 3 * (size_t)i + j];
+        const int l = i;
+        double cl[3] = {d.bl[3 * (size_t)l], d.bl[3 * (size_t)l + 1], d.bl[3 * (size_t)l + 2]};
+        for (int a = d.ptStart[l]; a < d.ptStart[l + 1]; a++) {
+            const int e = d.ptEdges[a];
+            const int pi = d.poseIdx[d.eps[e]];
+            if (pi < 0) continue;
+            const double* Bi = d.Hpl_e + 18 * (size_t)d.actPos[e];
+            for (int q = 0; q < 3; q++)
+                for (int r = 0; r < 6; r++) cl[q] += Bi[r * 3 + q] * (-d.x[6 * pi + r]);
+        }
+        const double* Di = d.Dinv + 9 * (size_t)l;
+        double* xl = d.x + 6 * (size_t)d.P + 3 * (size_t)l;
+        const int g = d.ptGlob[l];
+        for (int q = 0; q < 3; q++) {
+            const double v = Di[q * 3] * cl[0] + Di[q * 3 + 1] * cl[1] + Di[q * 3 + 2] * cl[2];
+            xl[q] = v;
+            const double X = d.X[3 * (size_t)g + q];
+            d.bX[3 * (size_t)g + q] = X;
+            d.X[3 * (size_t)g + q] = X + v;
         }
     }
-    if (i < nposes && applyPoses) {
+    if (i < d.P) {
         const int p = freePoses[i];
         const int k = d.poseIdx[p];
         double q[4], t[3], u[6];
@@ -663,6 +765,7 @@ __global__ __launch_bounds__(256) void k_update(LbaDev d, int nposes, const int3
     }
 }
 
+// pop() after a rejected trial (communicator path; k_lm_decide_fused does it in one process)
 __global__ __launch_bounds__(256) void k_pop(LbaDev d, int nposes, const int32_t* freePoses) {
     if (d.lm && !d.lm->pop) return;   // only after a rejected trial
     const int i = blockIdx.x * 256 + threadIdx.x;
@@ -749,31 +852,31 @@ __device__ __forceinline__ double cube_rn(double t) {
 
 // Start of an LM iteration (G/core/optimization_algorithm_levenberg.cpp:61-90): currentChi
 // from the linearisation's robust chi2 (red[0]), lambda from computeLambdaInit (red[1]) at it 0.
-__global__ void k_lm_begin(LmState* st, const double* __restrict__ red) {
-    if (threadIdx.x != 0 || st->phase != 0) return;
+__device__ void lm_begin(LmState* st, double chi, double maxDiag) {
     st->pop = 0;
-    st->currentChi = red[0];
-    st->iniChi = red[0];
+    st->currentChi = chi;
+    st->iniChi = chi;
     if (st->it == 0) {
-        st->lambda = 1e-5 * red[1];   // tau = 1e-5
+        st->lambda = 1e-5 * maxDiag;   // tau = 1e-5
         st->ni = 2;
         st->nBad = 0;
     }
     st->qmax = 0;
     st->phase = 1;
 }
+__global__ void k_lm_begin(LmState* st, const double* __restrict__ red) {
+    if (threadIdx.x != 0 || st->phase != 0) return;
+    lm_begin(st, red[0], red[1]);
+}
 
 // Decision after a trial (:120-160) and the end-of-iteration bookkeeping of
 // SparseOptimizer::optimize / OptimizationAlgorithmLevenberg (termination on qmax == max
 // trials, rho == 0 or three iterations without 1e-3 relative progress).
-__global__ void k_lm_decide(LmState* st, const double* __restrict__ red, const int* __restrict__ flags, int maxTrials,
-                            int iterations, int fixedIterations, double* __restrict__ trace) {
-    if (threadIdx.x != 0) return;
-    st->pop = 0;
-    if (st->phase != 1) return;
-    const double tempChi = flags[0] ? DBL_MAX : red[0];
+__device__ void lm_decide(LmState* st, double chiSum, double scaleSum, int fail, int maxTrials, int iterations,
+                          int fixedIterations, double* __restrict__ trace) {
+    const double tempChi = fail ? DBL_MAX : chiSum;
     double rho = st->currentChi - tempChi;
-    const double scale = red[2] + 1e-3;
+    const double scale = scaleSum + 1e-3;
     rho /= scale;
     if (rho > 0 && isfinite(tempChi)) {
         double alpha = 1. - cube_rn(2 * rho - 1);
@@ -811,6 +914,98 @@ __global__ void k_lm_decide(LmState* st, const double* __restrict__ red, const i
         }
     }
     st->phase = (go && st->it < iterations) ? 0 : 2;
+}
+__global__ void k_lm_decide(LmState* st, const double* __restrict__ red, const int* __restrict__ flags, int maxTrials,
+                            int iterations, int fixedIterations, double* __restrict__ trace) {
+    if (threadIdx.x != 0) return;
+    st->pop = 0;
+    if (st->phase != 1) return;
+    lm_decide(st, red[0], red[2], flags[0], maxTrials, iterations, fixedIterations, trace);
+}
+
+// Fixed-order single-workgroup sum (the k_sum order): thread t adds v(t), v(t + 1024), ...,
+// then a shared-memory tree.  `f(i)` yields term i.
+template <typename F>
+__device__ __forceinline__ double block_sum_1024(int n, F f, double* sh) {
+    const int tid = threadIdx.x;
+    double s = 0;
+    for (int i = tid; i < n; i += 1024) s += f(i);
+    sh[tid] = s;
+    __syncthreads();
+    for (int w = 512; w >= 1; w >>= 1) {
+        if (tid < w) sh[tid] += sh[tid + w];
+        __syncthreads();
+    }
+    const double r = sh[0];
+    __syncthreads();
+    return r;
+}
+
+// Single process: the start of an LM iteration in one workgroup — the linearisation's robust
+// chi2 (k_sum), computeLambdaInit's max diagonal at iteration 0 (k_maxdiag) and lm_begin.
+__global__ __launch_bounds__(1024) void k_lm_begin_fused(LbaDev d) {
+    __shared__ double sh[1024];
+    __shared__ int go, first;
+    LmState* st = d.lm;
+    const int tid = threadIdx.x;
+    if (tid == 0) { go = st->phase == 0; first = st->it == 0; }
+    __syncthreads();
+    if (!go) return;
+    const double chi = block_sum_1024(d.nact, [&](int i) { return d.echi[i]; }, sh);
+    double m = 0;
+    if (first) {
+        for (int i = tid; i < 6 * d.P; i += 1024) m = fmax(m, fabs(d.Hpp[36 * (i / 6) + 7 * (i % 6)]));
+        for (int i = tid; i < 3 * d.M; i += 1024) m = fmax(m, fabs(d.Hll[9 * (i / 3) + 4 * (i % 3)]));
+        sh[tid] = m;
+        __syncthreads();
+        for (int w = 512; w >= 1; w >>= 1) {
+            if (tid < w) sh[tid] = fmax(sh[tid], sh[tid + w]);
+            __syncthreads();
+        }
+        m = sh[0];
+    }
+    if (tid == 0) lm_begin(st, chi, m);
+}
+
+// Single process: the end of an LM trial in one workgroup — the trial's robust chi2, the
+// scale x^T (lambda x + b) (k_scale_terms + k_sum order), the rho decision (lm_decide) and,
+// after a rejected trial, pop() of every free pose and owned point.
+__global__ __launch_bounds__(1024) void k_lm_decide_fused(LbaDev d, const int32_t* __restrict__ freePoses,
+                                                          int maxTrials, int iterations, int fixedIterations,
+                                                          double* __restrict__ trace) {
+    __shared__ double sh[1024];
+    __shared__ int go, pop;
+    LmState* st = d.lm;
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        st->pop = 0;
+        go = st->phase == 1;
+        pop = 0;
+    }
+    __syncthreads();
+    if (!go) return;
+    const double lambda = st->lambda;
+    const double chi = block_sum_1024(d.nact, [&](int i) { return d.echi[i]; }, sh);
+    const int np = 6 * d.P, nx = np + 3 * d.M;
+    const double scl = block_sum_1024(nx, [&](int i) {
+        const double xi = d.x[i], b = i < np ? d.bp[i] : d.bl[i - np];
+        return xi * (lambda * xi + b);
+    }, sh);
+    if (tid == 0) {
+        lm_decide(st, chi, scl, d.flags[0], maxTrials, iterations, fixedIterations, trace);
+        pop = st->pop;
+    }
+    __syncthreads();
+    if (!pop) return;
+    for (int i = tid; i < d.M; i += 1024) {
+        const int g = d.ptGlob[i];
+        for (int j = 0; j < 3; j++) d.X[3 * (size_t)g + j] = d.bX[3 * (size_t)g + j];
+    }
+    for (int i = tid; i < d.P; i += 1024) {
+        const int p = freePoses[i];
+        for (int j = 0; j < 4; j++) d.q[4 * p + j] = d.bq[4 * p + j];
+        for (int j = 0; j < 3; j++) d.t[3 * p + j] = d.bt[3 * p + j];
+    }
 }
 
 // chi2 / depth of every edge (final check and outlier pass): chi2() uses the stored error
@@ -853,6 +1048,16 @@ struct lba_context {
     hipEvent_t evSync = nullptr;                               // LM decision hand-off
     double* h_scal = nullptr;                                  // pinned LM scalars / state (4 KB)
     std::vector<hipEvent_t> slotEv;                            // per-slot stage timing
+    // grow-only pinned staging: [0] problem upload, [1] per-optimize() structure, [2] downloads
+    char* stage[3] = {nullptr, nullptr, nullptr};
+    size_t stageCap[3] = {0, 0, 0};
+    // instantiated LM-slot graphs keyed by every captured launch parameter: a solve of the same
+    // shape reuses them (the arena hands out the same addresses in the same order)
+    struct SlotGraph {
+        std::vector<char> key;
+        hipGraphExec_t exec = nullptr;
+    };
+    std::vector<SlotGraph> graphs;
 };
 
 // Resets the arena for a new solve; if the last solve spilled into several chunks, they are
@@ -894,6 +1099,56 @@ static int dalloc(lba_context* c, T** p, size_t n) {
     return ORB_OK;
 }
 
+#define TRY(x)                 \
+    do {                       \
+        int s_ = (x);          \
+        if (s_) return s_;     \
+    } while (0)
+
+static int stage_reserve(lba_context* c, int slot, size_t bytes) {
+    if (c->stageCap[slot] >= bytes) return ORB_OK;
+    if (c->stage[slot]) (void)hipHostFree(c->stage[slot]);
+    c->stage[slot] = nullptr;
+    c->stageCap[slot] = 0;
+    const size_t cap = std::max(bytes + bytes / 2, (size_t)1 << 16);
+    if (hipHostMalloc((void**)&c->stage[slot], cap, hipHostMallocDefault) != hipSuccess) return ORB_ENOMEM;
+    c->stageCap[slot] = cap;
+    return ORB_OK;
+}
+
+// Host-to-device batch: the arrays are packed at 256-byte offsets into pinned staging slot
+// `slot` and sent with one copy into one arena block (a pageable copy costs ~10 us each).  A
+// slot is reused only after the stream has passed its previous copy (every caller waits on
+// the stream between two uses of the same slot).
+struct UpItem {
+    void** dst;
+    const void* src;
+    size_t bytes;
+};
+static int upload_batch(lba_context* c, int slot, const std::vector<UpItem>& items) {
+    size_t total = 0;
+    for (const auto& it : items) total += (it.bytes + 255) & ~(size_t)255;
+    char* dbase = nullptr;
+    TRY(dalloc(c, &dbase, std::max<size_t>(total, 1)));
+    TRY(stage_reserve(c, slot, total));
+    size_t off = 0;
+    for (const auto& it : items) {
+        if (it.bytes) std::memcpy(c->stage[slot] + off, it.src, it.bytes);
+        *it.dst = dbase + off;
+        off += (it.bytes + 255) & ~(size_t)255;
+    }
+    if (total) ORB_HIP_TRY(hipMemcpyAsync(dbase, c->stage[slot], total, hipMemcpyHostToDevice, c->stream));
+    return ORB_OK;
+}
+template <typename T>
+static UpItem up(T** dst, const std::vector<T>& v) {
+    return UpItem{reinterpret_cast<void**>(dst), v.data(), v.size() * sizeof(T)};
+}
+template <typename T>
+static UpItem up(T** dst, const T* src, size_t n) {
+    return UpItem{reinterpret_cast<void**>(dst), src, n * sizeof(T)};
+}
+
 // Waits for the stream by spinning on an event (a blocking hipStreamSynchronize sleeps and
 // adds tens of microseconds per LM trial).
 static int lba_wait(lba_context* c) {
@@ -904,138 +1159,10 @@ static int lba_wait(lba_context* c) {
     return e == hipSuccess ? ORB_OK : ORB_EGPU;
 }
 
-#define TRY(x)                 \
-    do {                       \
-        int s_ = (x);          \
-        if (s_) return s_;     \
-    } while (0)
 
 namespace {
 
-struct HostStructure {
-    std::vector<int32_t> act, poseIdx, ptLocal, ptGlob, actPos, ptStart, ptEdges, poStart, poEdges, prStart, prE1,
-        prE2, pairI, pairJ, freePoses, actPt, actPi;
-    int P = 0, M = 0;
-};
 
-// initializeOptimization(level) (G/core/sparse_optimizer.cpp:199-267) restricted to the
-// landmarks owned by this rank (contiguous range of point indices).
-void build_structure(const lba_problem* p, const std::vector<uint8_t>& level, int lvl, int rank, int world,
-                     HostStructure& s) {
-    const int NP = p->n_poses, NM = p->n_points, NE = p->n_edges;
-    const int own0 = (int)((long long)NM * rank / world), own1 = (int)((long long)NM * (rank + 1) / world);
-    std::vector<uint8_t> poseAct(NP, 0), ptAct(NM, 0);
-    // every rank must see the same pose index mapping: poses active on any rank count
-    for (int e = 0; e < NE; e++) {
-        if (level[e] != lvl) continue;
-        poseAct[p->edge_pose[e]] = 1;
-        ptAct[p->edge_point[e]] = 1;
-    }
-    s.act.clear();
-    for (int e = 0; e < NE; e++) {
-        if (level[e] != lvl) continue;
-        const int pt = p->edge_point[e];
-        if (pt < own0 || pt >= own1) continue;
-        s.act.push_back(e);
-    }
-    std::vector<int> order;
-    for (int i = 0; i < NP; i++)
-        if (poseAct[i] && !p->pose_fixed[i]) order.push_back(i);
-    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return p->pose_id[a] < p->pose_id[b]; });
-    s.poseIdx.assign(NP, -1);
-    for (size_t k = 0; k < order.size(); k++) s.poseIdx[order[k]] = (int)k;
-    s.freePoses = order;
-    s.P = (int)order.size();
-    order.clear();
-    for (int i = own0; i < own1; i++)
-        if (ptAct[i]) order.push_back(i);
-    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return p->point_id[a] < p->point_id[b]; });
-    s.ptLocal.assign(NM, -1);
-    for (size_t k = 0; k < order.size(); k++) s.ptLocal[order[k]] = (int)k;
-    s.ptGlob = order;
-    s.M = (int)order.size();
-    s.actPos.assign(NE, -1);
-    for (size_t k = 0; k < s.act.size(); k++) s.actPos[s.act[k]] = (int)k;
-    s.actPt.resize(s.act.size());
-    s.actPi.resize(s.act.size());
-    for (size_t k = 0; k < s.act.size(); k++) {
-        s.actPt[k] = s.ptLocal[p->edge_point[s.act[k]]];
-        s.actPi[k] = s.poseIdx[p->edge_pose[s.act[k]]];
-    }
-    // CSR by local point, edges sorted by pose index (fixed poses last)
-    s.ptStart.assign(s.M + 1, 0);
-    for (int e : s.act) s.ptStart[s.ptLocal[p->edge_point[e]] + 1]++;
-    for (int i = 0; i < s.M; i++) s.ptStart[i + 1] += s.ptStart[i];
-    s.ptEdges.assign(s.act.size(), 0);
-    {
-        std::vector<int> fill(s.ptStart.begin(), s.ptStart.end() - 1);
-        for (int e : s.act) s.ptEdges[fill[s.ptLocal[p->edge_point[e]]]++] = e;
-        for (int l = 0; l < s.M; l++) {
-            auto key = [&](int e) { const int k = s.poseIdx[p->edge_pose[e]]; return k < 0 ? (1 << 30) : k; };
-            std::stable_sort(s.ptEdges.begin() + s.ptStart[l], s.ptEdges.begin() + s.ptStart[l + 1],
-                             [&](int a, int b) { return key(a) < key(b); });
-        }
-    }
-    // CSR by pose (edges with a free pose, edge order)
-    s.poStart.assign(s.P + 1, 0);
-    for (int e : s.act) {
-        const int k = s.poseIdx[p->edge_pose[e]];
-        if (k >= 0) s.poStart[k + 1]++;
-    }
-    for (int i = 0; i < s.P; i++) s.poStart[i + 1] += s.poStart[i];
-    s.poEdges.assign(s.poStart[s.P], 0);
-    {
-        std::vector<int> fill(s.poStart.begin(), s.poStart.end() - 1);
-        for (int e : s.act) {
-            const int k = s.poseIdx[p->edge_pose[e]];
-            if (k >= 0) s.poEdges[fill[k]++] = e;
-        }
-    }
-    // pose-pair blocks (i <= j) with their contributions (landmark order, then edge order)
-    const int P = s.P;
-    const int npairs = P * (P + 1) / 2;
-    s.pairI.resize(npairs);
-    s.pairJ.resize(npairs);
-    std::vector<int> pairOf((size_t)P * P, -1);
-    {
-        int k = 0;
-        for (int i = 0; i < P; i++)
-            for (int j = i; j < P; j++) {
-                s.pairI[k] = i;
-                s.pairJ[k] = j;
-                pairOf[(size_t)i * P + j] = k++;
-            }
-    }
-    std::vector<int> cnt(npairs + 1, 0);
-    for (int l = 0; l < s.M; l++)
-        for (int a = s.ptStart[l]; a < s.ptStart[l + 1]; a++) {
-            const int i1 = s.poseIdx[p->edge_pose[s.ptEdges[a]]];
-            if (i1 < 0) continue;
-            for (int b = a; b < s.ptStart[l + 1]; b++) {
-                const int i2 = s.poseIdx[p->edge_pose[s.ptEdges[b]]];
-                if (i2 < 0) continue;
-                cnt[pairOf[(size_t)i1 * P + i2] + 1]++;
-            }
-        }
-    for (int i = 0; i < npairs; i++) cnt[i + 1] += cnt[i];
-    s.prStart = cnt;
-    s.prE1.assign(cnt[npairs], 0);
-    s.prE2.assign(cnt[npairs], 0);
-    std::vector<int> fill(cnt.begin(), cnt.end() - 1);
-    for (int l = 0; l < s.M; l++)
-        for (int a = s.ptStart[l]; a < s.ptStart[l + 1]; a++) {
-            const int i1 = s.poseIdx[p->edge_pose[s.ptEdges[a]]];
-            if (i1 < 0) continue;
-            for (int b = a; b < s.ptStart[l + 1]; b++) {
-                const int i2 = s.poseIdx[p->edge_pose[s.ptEdges[b]]];
-                if (i2 < 0) continue;
-                const int pr = pairOf[(size_t)i1 * P + i2];
-                s.prE1[fill[pr]] = s.actPos[s.ptEdges[a]];   // act positions (BD / Hpl_e rows)
-                s.prE2[fill[pr]] = s.actPos[s.ptEdges[b]];
-                fill[pr]++;
-            }
-        }
-}
 
 template <typename T>
 int upload(lba_context* c, T** dst, const std::vector<T>& v) {
@@ -1086,6 +1213,9 @@ void lba_destroy(lba_context* c) {
     if (c->evSync) (void)hipEventDestroy(c->evSync);
     for (auto e : c->slotEv) (void)hipEventDestroy(e);
     if (c->h_scal) (void)hipHostFree(c->h_scal);
+    for (auto p : c->stage)
+        if (p) (void)hipHostFree(p);
+    for (auto& g : c->graphs) (void)hipGraphExecDestroy(g.exec);
     if (c->stream && c->ownStream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1128,6 +1258,32 @@ int lba_stats(lba_context* c, double* ms4, int* iters, int* trials) {
     return ORB_OK;
 }
 
+int lba_dense_solve(lba_context* c, const double* S, const double* b, int n, double* x) {
+    if (!c || !S || !b || !x || n <= 0) return ORB_EINVAL;
+    ORB_HIP_TRY(hipSetDevice(c->device));
+    lba_free_all(c);
+    hipStream_t s = c->stream;
+    const int np = (n + kNB - 1) & ~(kNB - 1);
+    double *dS, *db, *dx, *dw = nullptr;
+    int* df;
+    TRY(dalloc(c, &dS, (size_t)n * n)); TRY(dalloc(c, &db, n)); TRY(dalloc(c, &dx, n)); TRY(dalloc(c, &df, 1));
+    if (np > kLdlLdsMaxN) TRY(dalloc(c, &dw, (size_t)np * (np + 1)));
+    ORB_HIP_TRY(hipMemcpyAsync(dS, S, 8 * (size_t)n * n, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(db, b, 8 * (size_t)n, hipMemcpyHostToDevice, s));
+    if (np <= kLdlLdsMaxN)
+        hipLaunchKernelGGL(k_ldlt_solve<true>, dim3(1), dim3(kLdlT), ((size_t)np * (np + 1) + 3 * (size_t)np + 64) * 8, s,
+                           dS, db, n, nullptr, dx, df, nullptr);
+    else
+        hipLaunchKernelGGL(k_ldlt_solve<false>, dim3(1), dim3(kLdlT), (3 * (size_t)np + 64) * 8, s, dS, db, n, dw, dx, df,
+                           nullptr);
+    ORB_HIP_TRY(hipGetLastError());
+    int fail = 0;
+    ORB_HIP_TRY(hipMemcpyAsync(x, dx, 8 * (size_t)n, hipMemcpyDeviceToHost, s));
+    ORB_HIP_TRY(hipMemcpyAsync(&fail, df, 4, hipMemcpyDeviceToHost, s));
+    ORB_HIP_TRY(hipStreamSynchronize(s));
+    return fail ? ORB_EINVAL : ORB_OK;
+}
+
 int lba_profile(lba_context* c, int enable) {
     if (!c) return ORB_EINVAL;
     c->profile = enable != 0;
@@ -1163,6 +1319,9 @@ void lba_pose_to_Tcw(const double q[4], const double t[3], float Tcw[16]) {
 }
 
 int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const volatile uint8_t* stop, lba_result* r) {
+#ifdef ORB_TIMING
+    const auto hEntry = std::chrono::steady_clock::now();
+#endif
     if (!c || !p || !o || !r || p->n_poses < 0 || p->n_points < 0 || p->n_edges < 0) return ORB_EINVAL;
     ORB_HIP_TRY(hipSetDevice(c->device));
     hipStream_t s = c->stream;
@@ -1179,32 +1338,23 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
     LbaDev d;
     std::memset(&d, 0, sizeof(d));
     double *q, *t, *X, *obs, *info, *cam;
-    uint8_t *fixed, *est, *robust;
+    uint8_t *fixed, *est, *robust = nullptr;
     int32_t *ept, *eps;
-    TRY(dalloc(c, &q, 4 * (size_t)NP)); TRY(dalloc(c, &t, 3 * (size_t)NP)); TRY(dalloc(c, &X, 3 * (size_t)NM));
     TRY(dalloc(c, &d.bq, 4 * (size_t)NP)); TRY(dalloc(c, &d.bt, 3 * (size_t)NP)); TRY(dalloc(c, &d.bX, 3 * (size_t)NM));
-    TRY(dalloc(c, &fixed, NP)); TRY(dalloc(c, &ept, NE)); TRY(dalloc(c, &eps, NE)); TRY(dalloc(c, &est, NE));
-    TRY(dalloc(c, &obs, 3 * (size_t)NE)); TRY(dalloc(c, &info, NE)); TRY(dalloc(c, &cam, 5 * (size_t)NE));
-    TRY(dalloc(c, &robust, NE)); TRY(dalloc(c, &d.err, 3 * (size_t)NE));
-    ORB_HIP_TRY(hipMemcpyAsync(q, p->pose_q, 32 * (size_t)NP, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(t, p->pose_t, 24 * (size_t)NP, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(X, p->point_xyz, 24 * (size_t)NM, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(fixed, p->pose_fixed, NP, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(ept, p->edge_point, 4 * (size_t)NE, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(eps, p->edge_pose, 4 * (size_t)NE, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(est, p->edge_stereo, NE, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(obs, p->edge_obs, 24 * (size_t)NE, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(info, p->edge_info, 8 * (size_t)NE, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(cam, p->edge_cam, 40 * (size_t)NE, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemsetAsync(robust, 1, NE, s));
+    TRY(dalloc(c, &d.err, 3 * (size_t)NE));
+    TRY(upload_batch(c, 0, {up(&q, p->pose_q, 4 * (size_t)NP), up(&t, p->pose_t, 3 * (size_t)NP),
+                            up(&X, p->point_xyz, 3 * (size_t)NM), up(&fixed, p->pose_fixed, NP),
+                            up(&ept, p->edge_point, NE), up(&eps, p->edge_pose, NE), up(&est, p->edge_stereo, NE),
+                            up(&obs, p->edge_obs, 3 * (size_t)NE), up(&info, p->edge_info, NE),
+                            up(&cam, p->edge_cam, 5 * (size_t)NE)}));
     ORB_HIP_TRY(hipMemsetAsync(d.err, 0, 24 * (size_t)NE, s));
     d.q = q; d.t = t; d.X = X; d.fixed = fixed; d.ept = ept; d.eps = eps; d.est = est; d.obs = obs; d.info = info;
     d.cam = cam; d.robust = robust;
     // per-edge / per-vertex scratch sized for the full problem
     TRY(dalloc(c, &d.Hll_e, 6 * (size_t)NE)); TRY(dalloc(c, &d.Hpp_e, 21 * (size_t)NE));
     TRY(dalloc(c, &d.Hpl_e, 18 * (size_t)NE)); TRY(dalloc(c, &d.bl_e, 3 * (size_t)NE));
-    TRY(dalloc(c, &d.bp_e, 6 * (size_t)NE)); TRY(dalloc(c, &d.BD, 18 * (size_t)NE));
-    TRY(dalloc(c, &d.coef, 6 * (size_t)NE)); TRY(dalloc(c, &d.echi, (size_t)NE + 6 * (size_t)NP + 3 * (size_t)NM));
+    TRY(dalloc(c, &d.bp_e, 6 * (size_t)NE));
+    TRY(dalloc(c, &d.echi, (size_t)NE + 6 * (size_t)NP + 3 * (size_t)NM));
     TRY(dalloc(c, &d.Hll, 9 * (size_t)NM)); TRY(dalloc(c, &d.bl, 3 * (size_t)NM)); TRY(dalloc(c, &d.Dinv, 9 * (size_t)NM));
     TRY(dalloc(c, &d.db, 3 * (size_t)NM));
     TRY(dalloc(c, &d.Hpp, 36 * (size_t)NP)); TRY(dalloc(c, &d.bp, 6 * (size_t)NP));
@@ -1217,6 +1367,11 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
     TRY(dalloc(c, &d.lm, 1));
     double* d_trace = nullptr;
     TRY(dalloc(c, &d_trace, 4 * 64));
+    double* d_ldlw = nullptr;   // global image of the padded reduced matrix when it exceeds LDS
+    {
+        const size_t npMax = ((size_t)6 * NP + kNB - 1) & ~(size_t)(kNB - 1);
+        if (npMax > (size_t)kLdlLdsMaxN) TRY(dalloc(c, &d_ldlw, npMax * (npMax + 1)));
+    }
     double* d_chi2 = nullptr;
     uint8_t* d_depth = nullptr;
     TRY(dalloc(c, &d_chi2, NE));
@@ -1244,13 +1399,13 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
         build_structure(p, level, lvl, c->rank, c->world, hs);
         int32_t *act, *poseIdx, *ptLocal, *ptGlob, *actPos, *ptStart, *ptEdges, *poStart, *poEdges, *prStart, *prE1, *prE2;
         int32_t *actPt, *actPi;
-        TRY(upload(c, &actPt, hs.actPt)); TRY(upload(c, &actPi, hs.actPi));
-        TRY(upload(c, &act, hs.act)); TRY(upload(c, &poseIdx, hs.poseIdx)); TRY(upload(c, &ptLocal, hs.ptLocal));
-        TRY(upload(c, &ptGlob, hs.ptGlob)); TRY(upload(c, &actPos, hs.actPos)); TRY(upload(c, &ptStart, hs.ptStart));
-        TRY(upload(c, &ptEdges, hs.ptEdges)); TRY(upload(c, &poStart, hs.poStart)); TRY(upload(c, &poEdges, hs.poEdges));
-        TRY(upload(c, &prStart, hs.prStart)); TRY(upload(c, &prE1, hs.prE1)); TRY(upload(c, &prE2, hs.prE2));
-        TRY(upload(c, &d_freePoses, hs.freePoses)); TRY(upload(c, &d_pairI, hs.pairI)); TRY(upload(c, &d_pairJ, hs.pairJ));
-        ORB_HIP_TRY(hipMemcpyAsync(robust, robustH.data(), NE, hipMemcpyHostToDevice, s));
+        TRY(upload_batch(c, 1, {up(&actPt, hs.actPt), up(&actPi, hs.actPi), up(&act, hs.act), up(&poseIdx, hs.poseIdx),
+                                up(&ptLocal, hs.ptLocal), up(&ptGlob, hs.ptGlob), up(&actPos, hs.actPos),
+                                up(&ptStart, hs.ptStart), up(&ptEdges, hs.ptEdges), up(&poStart, hs.poStart),
+                                up(&poEdges, hs.poEdges), up(&prStart, hs.prStart), up(&prE1, hs.prE1),
+                                up(&prE2, hs.prE2), up(&d_freePoses, hs.freePoses), up(&d_pairI, hs.pairI),
+                                up(&d_pairJ, hs.pairJ), up(&robust, robustH)}));
+        d.robust = robust;
         d.act = act; d.nact = (int)hs.act.size(); d.poseIdx = poseIdx; d.ptLocal = ptLocal; d.ptGlob = ptGlob;
         d.actPos = actPos; d.P = hs.P; d.M = hs.M; d.ptStart = ptStart; d.ptEdges = ptEdges; d.poStart = poStart;
         d.poEdges = poEdges; d.prStart = prStart; d.prE1 = prE1; d.prE2 = prE2;
@@ -1261,65 +1416,67 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
 
     auto grid = [](int n) { return dim3((unsigned)std::max(1, (n + 255) / 256)); };
 
-    // computeActiveErrors + activeRobustChi2 (global over ranks) -> red[0], in phase `want`
-    auto errors_chi2 = [&](int want) -> int {
-        if (d.nact > 0) hipLaunchKernelGGL(k_edge_errors, grid(d.nact), dim3(256), 0, s, d, hm, hsv, want);
-        hipLaunchKernelGGL(k_sum, dim3(1), dim3(1024), 0, s, d.echi, d.nact, d.red, d.lm, want);
-        TRY(comm_allreduce_g(c, d.red, 1, 0, d.lm, want));
-        return ORB_OK;
-    };
 
     // One LM "slot": the linearisation of an iteration (runs only when the device state says a
     // new iteration starts) followed by one trial (runs only while the iteration's trial loop
     // is open) and its decision.  Slots are enqueued back to back without host round trips.
     auto enqueue_slot = [&](int iterations, hipEvent_t* ev) -> int {
         const bool prof = ev != nullptr;
+        const bool single = c->world == 1;   // no collectives: the LM bookkeeping fuses into single kernels
         if (prof) (void)hipEventRecord(ev[0], s);
         // ---- linearisation (G/core/sparse_optimizer.cpp:384-394, block_solver.hpp:502-561)
-        TRY(errors_chi2(0));
-        if (d.nact > 0) hipLaunchKernelGGL(k_edge_linearize, grid(d.nact), dim3(256), 0, s, d, hm, hsv);
-        if (d.M > 0) hipLaunchKernelGGL(k_point_reduce, grid(d.M), dim3(256), 0, s, d);
-        if (d.P > 0) hipLaunchKernelGGL(k_pose_reduce, dim3(d.P), dim3(64), 0, s, d);
-        if (d.P > 0) {
-            TRY(comm_allreduce_g(c, d.Hpp, 36 * (size_t)d.P, 0, d.lm, 0));
-            TRY(comm_allreduce_g(c, d.bp, 6 * (size_t)d.P, 0, d.lm, 0));
+        if (d.nact > 0) hipLaunchKernelGGL(k_edge_lin, grid(d.nact), dim3(256), 0, s, d, hm, hsv);
+        if (d.P + d.M > 0)
+            hipLaunchKernelGGL(k_vertex_reduce, dim3(d.P + (d.M + 255) / 256), dim3(256), 0, s, d);
+        if (single) {
+            hipLaunchKernelGGL(k_lm_begin_fused, dim3(1), dim3(1024), 0, s, d);
+        } else {
+            hipLaunchKernelGGL(k_sum, dim3(1), dim3(1024), 0, s, d.echi, d.nact, d.red, d.lm, 0);
+            TRY(comm_allreduce_g(c, d.red, 1, 0, d.lm, 0));
+            if (d.P > 0) {
+                TRY(comm_allreduce_g(c, d.Hpp, 36 * (size_t)d.P, 0, d.lm, 0));
+                TRY(comm_allreduce_g(c, d.bp, 6 * (size_t)d.P, 0, d.lm, 0));
+            }
+            hipLaunchKernelGGL(k_maxdiag, dim3(1), dim3(1024), 0, s, d.Hpp, d.P, d.Hll, d.M, d.red + 1, d.lm);
+            TRY(comm_allreduce_g(c, d.red + 1, 1, 1, d.lm, 3));
+            hipLaunchKernelGGL(k_lm_begin, dim3(1), dim3(64), 0, s, d.lm, d.red);
         }
-        hipLaunchKernelGGL(k_maxdiag, dim3(1), dim3(1024), 0, s, d.Hpp, d.P, d.Hll, d.M, d.red + 1, d.lm);
-        TRY(comm_allreduce_g(c, d.red + 1, 1, 1, d.lm, 3));
-        hipLaunchKernelGGL(k_lm_begin, dim3(1), dim3(64), 0, s, d.lm, d.red);
         if (prof) (void)hipEventRecord(ev[1], s);
-        // ---- trial: Schur complement, reduced solve, back-substitution, update, new chi2
+        // ---- trial: Schur complement, reduced solve, back-substitution + update, new chi2
         if (d.M > 0) hipLaunchKernelGGL(k_point_schur, grid(d.M), dim3(256), 0, s, d);
-        if (d.nact > 0) hipLaunchKernelGGL(k_edge_schur, grid(d.nact), dim3(256), 0, s, d);
         const int npairs = d.P * (d.P + 1) / 2;
-        if (npairs > 0) {
-            hipLaunchKernelGGL(k_schur_pairs, dim3(npairs), dim3(256), 0, s, d, root ? 1 : 0, d_pairI, d_pairJ);
-            hipLaunchKernelGGL(k_bschur, dim3(d.P), dim3(64), 0, s, d, root ? 1 : 0);
-        }
+        if (npairs > 0) hipLaunchKernelGGL(k_schur_pairs, dim3(npairs), dim3(kSpT), 0, s, d, root ? 1 : 0, d_pairI, d_pairJ);
         if (d.P > 0) TRY(comm_allreduce_g(c, d.S, (size_t)36 * d.P * d.P + 6 * (size_t)d.P, 0, d.lm, 1));
         if (prof) (void)hipEventRecord(ev[2], s);
         if (d.P > 0) {
-            const int n = 6 * d.P;
-            if ((size_t)n * (n | 1) * 8 + 3 * (size_t)n * 8 <= 160 * 1024)
-                hipLaunchKernelGGL(k_ldlt_solve<true>, dim3(1), dim3(kLdltT), ((size_t)n * (n | 1) + 2 * (size_t)n) * 8, s,
-                                   d.S, d.bs, n, d.x, d.flags, d.lm);
+            const int n = 6 * d.P, np = (n + kNB - 1) & ~(kNB - 1);
+            if (np <= kLdlLdsMaxN)
+                hipLaunchKernelGGL(k_ldlt_solve<true>, dim3(1), dim3(kLdlT), ((size_t)np * (np + 1) + 3 * (size_t)np + 64) * 8,
+                                   s, d.S, d.bs, n, nullptr, d.x, d.flags, d.lm);
             else
-                hipLaunchKernelGGL(k_ldlt_solve<false>, dim3(1), dim3(kLdltT), 2 * (size_t)n * 8, s, d.S, d.bs, n,
-                                   d.x, d.flags, d.lm);
+                hipLaunchKernelGGL(k_ldlt_solve<false>, dim3(1), dim3(kLdlT), (3 * (size_t)np + 64) * 8, s, d.S, d.bs, n,
+                                   d_ldlw, d.x, d.flags, d.lm);
         } else {
             ORB_HIP_TRY(hipMemsetAsync(d.flags, 0, 4, s));
         }
         if (prof) (void)hipEventRecord(ev[3], s);
-        if (d.M > 0) hipLaunchKernelGGL(k_backsub, grid(d.M), dim3(256), 0, s, d);
-        hipLaunchKernelGGL(k_update, grid(std::max(d.M, d.P)), dim3(256), 0, s, d, d.P, d_freePoses, 1);
-        TRY(errors_chi2(1));
-        const int nx = 6 * d.P + 3 * d.M;
-        hipLaunchKernelGGL(k_scale_terms, grid(nx), dim3(256), 0, s, d, root ? 1 : 0, d.echi);
-        hipLaunchKernelGGL(k_sum, dim3(1), dim3(1024), 0, s, d.echi, nx, d.red + 2, d.lm, 1);
-        TRY(comm_allreduce_g(c, d.red + 2, 1, 0, d.lm, 1));
-        hipLaunchKernelGGL(k_lm_decide, dim3(1), dim3(64), 0, s, d.lm, d.red, d.flags, maxTrials, iterations,
-                           o->fixed_iterations ? 1 : 0, d_trace);
-        hipLaunchKernelGGL(k_pop, grid(std::max(d.M, d.P)), dim3(256), 0, s, d, d.P, d_freePoses);
+        if (d.M + d.P > 0)
+            hipLaunchKernelGGL(k_backsub_update, grid(std::max(d.M, d.P)), dim3(256), 0, s, d, d_freePoses);
+        if (d.nact > 0) hipLaunchKernelGGL(k_edge_errors, grid(d.nact), dim3(256), 0, s, d, hm, hsv, 1);
+        if (single) {
+            hipLaunchKernelGGL(k_lm_decide_fused, dim3(1), dim3(1024), 0, s, d, d_freePoses, maxTrials, iterations,
+                               o->fixed_iterations ? 1 : 0, d_trace);
+        } else {
+            hipLaunchKernelGGL(k_sum, dim3(1), dim3(1024), 0, s, d.echi, d.nact, d.red, d.lm, 1);
+            TRY(comm_allreduce_g(c, d.red, 1, 0, d.lm, 1));
+            const int nx = 6 * d.P + 3 * d.M;
+            hipLaunchKernelGGL(k_scale_terms, grid(nx), dim3(256), 0, s, d, root ? 1 : 0, d.echi);
+            hipLaunchKernelGGL(k_sum, dim3(1), dim3(1024), 0, s, d.echi, nx, d.red + 2, d.lm, 1);
+            TRY(comm_allreduce_g(c, d.red + 2, 1, 0, d.lm, 1));
+            hipLaunchKernelGGL(k_lm_decide, dim3(1), dim3(64), 0, s, d.lm, d.red, d.flags, maxTrials, iterations,
+                               o->fixed_iterations ? 1 : 0, d_trace);
+            hipLaunchKernelGGL(k_pop, grid(std::max(d.M, d.P)), dim3(256), 0, s, d, d.P, d_freePoses);
+        }
         if (prof) (void)hipEventRecord(ev[4], s);
         return ORB_OK;
     };
@@ -1331,12 +1488,49 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
         itersDone = 0;
         if (hs.P + hs.M == 0 && c->world == 1) return ORB_OK;
         if (iterations <= 0 || stopped()) return ORB_OK;
-        if (6 * d.P > kLdltMaxN) return ORB_E2BIG;   // panel rows are held in registers
         LmState* hst = reinterpret_cast<LmState*>(reinterpret_cast<char*>(c->h_scal) + 512);
         std::memset(hst, 0, sizeof(LmState));
         hst->ni = 2;
         hst->traceBase = r->trace ? r->n_trace : 64;
         ORB_HIP_TRY(hipMemcpyAsync(d.lm, hst, sizeof(LmState), hipMemcpyHostToDevice, s));
+        // Single process, no stage events: the slot's ~20 launches are captured once per
+        // optimize() into a HIP graph and replayed, so the LM loop pays one graph launch per
+        // slot instead of a host dispatch per kernel.  (With a communicator the all-reduce is
+        // a host callback and the slot is enqueued kernel by kernel.)
+        hipGraphExec_t gexec = nullptr;
+        if (c->world == 1 && !c->profile && s != nullptr) {
+            struct {
+                LbaDev d;
+                const void* ptrs[6];
+                double h[2];
+                int v[4];
+            } k;
+            std::memset(&k, 0, sizeof(k));
+            k.d = d;
+            k.ptrs[0] = d_pairI; k.ptrs[1] = d_pairJ; k.ptrs[2] = d_freePoses; k.ptrs[3] = d_trace;
+            k.ptrs[4] = d_ldlw; k.ptrs[5] = s;
+            k.h[0] = hm; k.h[1] = hsv;
+            k.v[0] = iterations; k.v[1] = maxTrials; k.v[2] = o->fixed_iterations; k.v[3] = root;
+            std::vector<char> key(reinterpret_cast<const char*>(&k), reinterpret_cast<const char*>(&k) + sizeof(k));
+            for (auto& g : c->graphs)
+                if (g.key == key) gexec = g.exec;
+            if (!gexec) {
+                hipGraph_t g = nullptr;
+                ORB_HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+                const int st = enqueue_slot(iterations, nullptr);
+                const hipError_t ce = hipStreamEndCapture(s, &g);
+                if (st) { if (g) (void)hipGraphDestroy(g); return st; }
+                if (ce != hipSuccess) return ORB_EGPU;
+                const hipError_t ie = hipGraphInstantiate(&gexec, g, nullptr, nullptr, 0);
+                (void)hipGraphDestroy(g);
+                if (ie != hipSuccess) return ORB_EGPU;
+                if (c->graphs.size() >= 4) {
+                    (void)hipGraphExecDestroy(c->graphs.front().exec);
+                    c->graphs.erase(c->graphs.begin());
+                }
+                c->graphs.push_back({std::move(key), gexec});
+            }
+        }
         int known = 0;
         for (;;) {
             const int G = std::max(1, iterations - known);
@@ -1347,7 +1541,10 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
                     c->slotEv.push_back(e);
                 }
             }
-            for (int g = 0; g < G; g++) TRY(enqueue_slot(iterations, c->profile ? &c->slotEv[5 * (size_t)g] : nullptr));
+            for (int g = 0; g < G; g++) {
+                if (gexec) ORB_HIP_TRY(hipGraphLaunch(gexec, s));
+                else TRY(enqueue_slot(iterations, c->profile ? &c->slotEv[5 * (size_t)g] : nullptr));
+            }
             ORB_HIP_TRY(hipMemcpyAsync(hst, d.lm, sizeof(LmState), hipMemcpyDeviceToHost, s));
             TRY(lba_wait(c));
             if (c->profile) {
@@ -1378,19 +1575,31 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
         return ORB_OK;
     };
 
+#ifdef ORB_TIMING
+    std::chrono::steady_clock::time_point hT[10];
+#endif
+    HSTAMP(0);
     // ---- R/src/Optimizer.cpp:789-841
     TRY(init_opt(0));
+    HSTAMP(1);
     TRY(optimize(o->iters1, r->iterations[0]));
+    HSTAMP(2);
     const bool bDoMore = !stopped();
     auto edge_check = [&](std::vector<double>& chi, std::vector<uint8_t>& dep) -> int {
         if (NE > 0) hipLaunchKernelGGL(k_edge_check, grid(NE), dim3(256), 0, s, d, NE, d_chi2, d_depth);
         chi.resize(NE);
         dep.resize(NE);
+        TRY(stage_reserve(c, 2, 9 * (size_t)NE + 64));   // pinned: one pageable D2H costs more than the kernel
+        char* h = c->stage[2];
         if (NE > 0) {
-            ORB_HIP_TRY(hipMemcpyAsync(chi.data(), d_chi2, 8 * (size_t)NE, hipMemcpyDeviceToHost, s));
-            ORB_HIP_TRY(hipMemcpyAsync(dep.data(), d_depth, NE, hipMemcpyDeviceToHost, s));
+            ORB_HIP_TRY(hipMemcpyAsync(h, d_chi2, 8 * (size_t)NE, hipMemcpyDeviceToHost, s));
+            ORB_HIP_TRY(hipMemcpyAsync(h + 8 * (size_t)NE, d_depth, NE, hipMemcpyDeviceToHost, s));
         }
         TRY(lba_wait(c));
+        if (NE > 0) {
+            std::memcpy(chi.data(), h, 8 * (size_t)NE);
+            std::memcpy(dep.data(), h + 8 * (size_t)NE, NE);
+        }
         return ORB_OK;
     };
     std::vector<double> chi;
@@ -1419,9 +1628,12 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
             TRY(lba_wait(c));
             for (int e = 0; e < NE; e++) level[e] = lv[e] > 0.5 ? 1 : 0;
         }
+        HSTAMP(3);
         TRY(init_opt(0));
+        HSTAMP(4);
         TRY(optimize(o->iters2, r->iterations[1]));
     }
+    HSTAMP(5);
     // ---- final check (R/src/Optimizer.cpp:850-880) and write-back data
     TRY(edge_check(chi, dep));
     for (int e = 0; e < NE; e++) {
@@ -1435,10 +1647,24 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
         }
         if (r->edge_erase) r->edge_erase[e] = er;
     }
-    if (r->pose_q) ORB_HIP_TRY(hipMemcpyAsync(r->pose_q, q, 32 * (size_t)NP, hipMemcpyDeviceToHost, s));
-    if (r->pose_t) ORB_HIP_TRY(hipMemcpyAsync(r->pose_t, t, 24 * (size_t)NP, hipMemcpyDeviceToHost, s));
-    if (r->point_xyz) ORB_HIP_TRY(hipMemcpyAsync(r->point_xyz, X, 24 * (size_t)NM, hipMemcpyDeviceToHost, s));
-    TRY(lba_wait(c));
+    {   // estimates back through pinned staging (q, t, X are contiguous in the problem batch)
+        const size_t bq = ((32 * (size_t)NP + 255) & ~(size_t)255), bt = ((24 * (size_t)NP + 255) & ~(size_t)255);
+        const size_t tot = bq + bt + 24 * (size_t)NM;
+        TRY(stage_reserve(c, 2, tot));
+        char* h = c->stage[2];
+        ORB_HIP_TRY(hipMemcpyAsync(h, q, tot, hipMemcpyDeviceToHost, s));
+        TRY(lba_wait(c));
+        if (r->pose_q) std::memcpy(r->pose_q, h, 32 * (size_t)NP);
+        if (r->pose_t) std::memcpy(r->pose_t, h + bq, 24 * (size_t)NP);
+        if (r->point_xyz) std::memcpy(r->point_xyz, h + bq + bt, 24 * (size_t)NM);
+    }
+#ifdef ORB_TIMING
+    HSTAMP(6);
+    auto us = [&](int a, int b) { return std::chrono::duration<double, std::micro>(hT[b] - hT[a]).count(); };
+    std::printf("lba host: init1 %.0f opt1 %.0f check %.0f init2 %.0f opt2 %.0f final %.0f us (entry->init %.0f)\n",
+                us(0, 1), us(1, 2), us(2, 3), us(3, 4), us(4, 5), us(5, 6),
+                std::chrono::duration<double, std::micro>(hT[0] - hEntry).count());
+#endif
     ORB_HIP_TRY(hipGetLastError());
     return ORB_OK;
 }

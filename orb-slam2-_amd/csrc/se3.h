@@ -32,6 +32,17 @@ __host__ __device__ inline void hd_normalize_rotation(double q[4]) {
     const double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
     q[0] /= n; q[1] /= n; q[2] /= n; q[3] /= n;
 }
+// Eigen's branch for a non-positive trace with the largest diagonal entry at I
+template <int I>
+__host__ __device__ inline void quat_from_matrix_major(const double m[9], double q[4]) {
+    constexpr int J = (I + 1) % 3, K = (J + 1) % 3;
+    double s = sqrt(m[I * 3 + I] - m[J * 3 + J] - m[K * 3 + K] + 1.0);
+    q[I] = 0.5 * s;
+    s = 0.5 / s;
+    q[3] = (m[K * 3 + J] - m[J * 3 + K]) * s;
+    q[J] = (m[J * 3 + I] + m[I * 3 + J]) * s;
+    q[K] = (m[K * 3 + I] + m[I * 3 + K]) * s;
+}
 // Eigen Quaterniond(const Matrix3d&) + SE3Quat::normalizeRotation
 __host__ __device__ inline void hd_quat_from_matrix(const double m[9], double q[4]) {
     const double t = m[0] + m[4] + m[8];
@@ -45,14 +56,11 @@ __host__ __device__ inline void hd_quat_from_matrix(const double m[9], double q[
     } else {
         int i = 0;
         if (m[4] > m[0]) i = 1;
-        if (m[8] > m[i * 3 + i]) i = 2;
-        const int j = (i + 1) % 3, k = (j + 1) % 3;
-        double s = sqrt(m[i * 3 + i] - m[j * 3 + j] - m[k * 3 + k] + 1.0);
-        q[i] = 0.5 * s;
-        s = 0.5 / s;
-        q[3] = (m[k * 3 + j] - m[j * 3 + k]) * s;
-        q[j] = (m[j * 3 + i] + m[i * 3 + j]) * s;
-        q[k] = (m[k * 3 + i] + m[i * 3 + k]) * s;
+        if (m[8] > (i ? m[4] : m[0])) i = 2;
+        // the three cases spelled out so every index is a constant (no scratch-indexed arrays)
+        if (i == 0) quat_from_matrix_major<0>(m, q);
+        else if (i == 1) quat_from_matrix_major<1>(m, q);
+        else quat_from_matrix_major<2>(m, q);
     }
     hd_normalize_rotation(q);
 }

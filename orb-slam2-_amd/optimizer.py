@@ -51,7 +51,8 @@ def _sig():
                             ("lba_set_stream", [vp, vp, i32], C.c_int),
                             ("lba_set_comm", [vp, i32, i32, vp, sz, ALLREDUCE_FN, vp], C.c_int),
                             ("lba_solve", [vp, vp, vp, vp, vp], C.c_int), ("lba_profile", [vp, i32], C.c_int),
-                            ("lba_stats", [vp, vp, vp, vp], C.c_int), ("lba_pose_from_Tcw", [vp, vp, vp], None),
+                            ("lba_stats", [vp, vp, vp, vp], C.c_int),
+                            ("lba_dense_solve", [vp, vp, vp, i32, vp], C.c_int), ("lba_pose_from_Tcw", [vp, vp, vp], None),
                             ("lba_pose_to_Tcw", [vp, vp, vp], None)]:
         fn = getattr(lib, name)
         fn.argtypes = args
@@ -110,6 +111,14 @@ class LocalBA:
         self._comm = (ALLREDUCE_FN(cb), workspace)
         _abi.check("lba_set_comm", _sig().lba_set_comm(self._h, rank, world, C.c_void_p(workspace.data_ptr()),
                                                         workspace.numel(), self._comm[0], None))
+
+    def dense_solve(self, S, b):
+        """x = S^-1 b through the reduced-camera-system LDL^T (lba_dense_solve)."""
+        S = np.ascontiguousarray(S, dtype=np.float64)
+        b = np.ascontiguousarray(b, dtype=np.float64)
+        x = np.zeros(len(b))
+        _abi.check("lba_dense_solve", _sig().lba_dense_solve(self._h, _abi.ptr(S), _abi.ptr(b), len(b), _abi.ptr(x)))
+        return x
 
     def profile(self, enable=True):
         _sig().lba_profile(self._h, int(enable))

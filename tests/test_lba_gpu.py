@@ -64,3 +64,24 @@ def test_bad_points_skip_outlier_pass(amd):
     ref = O.lba_solve(pb)
     got = amd.LocalBA().solve(pb)
     _compare(ref, got)
+
+
+@pytest.mark.parametrize("n,seed", [(6, 0), (114, 1), (120, 2), (128, 3), (130, 4), (180, 5), (301, 6)])
+def test_dense_solve_vs_numpy(amd, n, seed):
+    """Reduced camera system solve (blocked MFMA LDL^T, LDS and global images) against a
+    float64 numpy solve of the same SPD system: relative residual at f64 rounding level."""
+    rng = np.random.default_rng(seed)
+    G = rng.standard_normal((n, n + 8))
+    S = G @ G.T + n * np.eye(n)
+    b = rng.standard_normal(n)
+    x = amd.LocalBA().dense_solve(S, b)
+    ref = np.linalg.solve(S, b)
+    assert np.abs(x - ref).max() <= 1e-10 * np.abs(ref).max()
+    assert np.abs(S @ x - b).max() <= 1e-11 * np.abs(b).max() * n
+
+
+def test_dense_solve_zero_pivot_fails(amd):
+    S = np.eye(20)
+    S[7, 7] = 0.0
+    with pytest.raises(amd._abi.OrbError):
+        amd.LocalBA().dense_solve(S, np.ones(20))
