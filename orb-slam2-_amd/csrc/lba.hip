@@ -81,14 +81,11 @@ struct LbaDev {
     const int32_t* act;         // active edges
     int nact;
     const int32_t* poseIdx;     // pose -> hessian index or -1
-    const int32_t* ptLocal;     // global point -> local index or -1 (owned points only)
     const int32_t* ptGlob;      // local -> global point
-    const int32_t* actPos;      // edge -> position in act (or -1)
     const int32_t *actPt, *actPi; // per act position: local point, pose hessian index (-1 fixed)
     int P, M;                   // free active poses, owned active points
-    const int32_t *ptStart, *ptEdges;     // CSR by local point (edge ids, sorted by pose index)
-    const int32_t *poStart, *poEdges;     // CSR by pose index (edge ids)
-    const int32_t *prStart, *prE1, *prE2; // CSR by pose-pair block (i<=j), contributions (act positions)
+    const int32_t *ptStart, *ptAct;         // CSR by local point (act positions, sorted by pose index)
+    const int32_t *poStart, *poAct, *poPt;  // CSR by pose index (act positions sorted by landmark; landmarks)
     // linearisation (indexed by act position)
     double *Hll_e, *Hpp_e, *Hpl_e, *bl_e, *bp_e, *echi;
     // reduced per vertex
@@ -260,7 +257,7 @@ __global__ __launch_bounds__(256) void k_vertex_reduce(LbaDev d) {
         double acc[27];
         for (int i = 0; i < 27; i++) acc[i] = 0;
         for (int a = d.poStart[p] + tid; a < d.poStart[p + 1]; a += 256) {
-            const int k = d.actPos[d.poEdges[a]];
+            const int k = d.poAct[a];
             for (int i = 0; i < 21; i++) acc[i] += d.Hpp_e[21 * (size_t)k + i];
             for (int i = 0; i < 6; i++) acc[21 + i] += d.bp_e[6 * (size_t)k + i];
         }
@@ -288,7 +285,7 @@ __global__ __launch_bounds__(256) void k_vertex_reduce(LbaDev d) {
     if (l >= d.M) return;
     double h[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
     for (int a = d.ptStart[l]; a < d.ptStart[l + 1]; a++) {
-        const int k = d.actPos[d.ptEdges[a]];
+        const int k = d.ptAct[a];
         for (int i = 0; i < 6; i++) h[i] += d.Hll_e[6 * (size_t)k + i];
         for (int i = 0; i < 3; i++) b[i] += d.bl_e[3 * (size_t)k + i];
     }
@@ -326,27 +323,50 @@ __global__ __launch_bounds__(256) void k_point_schur(LbaDev d) {
 }
 
 // Reduced camera system (G/core/block_solver.hpp:408-440): one workgroup per pose-pair block
-// (i <= j), S_ij = [i == j](Hpp_i + lambda I) - sum_c (Hpl_c D_l^-1) Hpl_c'^T over the
-// landmarks l seen by both.  Thread t accumulates the whole 6 x 6 product of contributions
-// t, t + 256, ... in registers (Hpl D^-1 formed on the fly); the 256 partials meet in LDS
-// (fixed order).  The diagonal blocks also form b_s,i = b_p,i - sum_e Hpl_e D_l^-1 b_l over
-// pose i's edges (rank 0 carries Hpp + lambda I and b_p).
+// (i <= j, row-major triangular order), S_ij = [i == j](Hpp_i + lambda I) - sum_l (Hpl_il
+// D_l^-1) Hpl_jl^T over the landmarks l seen by both.  The landmarks shared by poses i and j
+// are found by intersecting their landmark-sorted edge lists (pose j's list staged in LDS,
+// one binary search per edge of pose i).  Thread t accumulates the whole 6 x 6 product of
+// pose i's edges t, t + 256, ... in registers (Hpl D^-1 formed on the fly); the 256 partials
+// meet in LDS in a fixed order, so the result is reproducible run to run.  The diagonal
+// blocks also form b_s,i = b_p,i - sum_e Hpl_e D_l^-1 b_l over pose i's edges (rank 0
+// carries Hpp + lambda I and b_p).
 constexpr int kSpT = 256;
-__global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag, const int32_t* __restrict__ pairI,
-                                                      const int32_t* __restrict__ pairJ) {
+constexpr int kSpList = 4096;   // pose j's landmark list held in LDS up to this length
+__global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag) {
     if (lm_off(d.lm, 1)) return;
     __shared__ double part[42][kSpT + 1];
-    const int pr = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
-    const int bi = pairI[pr], bj = pairJ[pr];
+    __shared__ int32_t listJ[kSpList];
+    const int tid = threadIdx.x;
+    int bi = 0, rem = blockIdx.x;
+    while (rem >= d.P - bi) { rem -= d.P - bi; bi++; }
+    const int bj = bi + rem;
+    const bool diag = bi == bj;
+    const int a0 = d.poStart[bi], a1 = d.poStart[bi + 1], b0 = d.poStart[bj], nb = d.poStart[bj + 1] - b0;
+    const bool inLds = nb <= kSpList;
+    if (!diag && inLds)
+        for (int t = tid; t < nb; t += kSpT) listJ[t] = d.poPt[b0 + t];
+    __syncthreads();
+    const int32_t* Lj = inLds ? listJ : d.poPt + b0;
     double acc[42];
 #pragma unroll
     for (int i = 0; i < 42; i++) acc[i] = 0.0;
-    const int c0 = d.prStart[pr], c1 = d.prStart[pr + 1];
-    for (int c = c0 + tid; c < c1; c += kSpT) {
-        const int e1 = d.prE1[c];
+    for (int a = a0 + tid; a < a1; a += kSpT) {
+        const int e1 = d.poAct[a], l = d.poPt[a];
+        int e2 = e1;
+        if (!diag) {   // lower_bound of l in pose j's sorted landmark list
+            int lo = 0, hi = nb;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (Lj[mid] < l) lo = mid + 1;
+                else hi = mid;
+            }
+            if (lo == nb || Lj[lo] != l) continue;
+            e2 = d.poAct[b0 + lo];
+        }
         const double2* Bi = reinterpret_cast<const double2*>(d.Hpl_e + 18 * (size_t)e1);
-        const double2* Bj = reinterpret_cast<const double2*>(d.Hpl_e + 18 * (size_t)d.prE2[c]);
-        const double* Dl = d.Dinv + 9 * (size_t)d.actPt[e1];
+        const double2* Bj = reinterpret_cast<const double2*>(d.Hpl_e + 18 * (size_t)e2);
+        const double* Dl = d.Dinv + 9 * (size_t)l;
         double w[18], v[18], Di[9], u[18];
 #pragma unroll
         for (int h = 0; h < 9; h++) {
@@ -356,7 +376,7 @@ __global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag, con
             Di[h] = Dl[h];
         }
 #pragma unroll
-        for (int r = 0; r < 6; r++)   // Hpl D^-1 (the BD product of block_solver.hpp:419)
+        for (int r = 0; r < 6; r++)   // Hpl D^-1 (the product of block_solver.hpp:419)
 #pragma unroll
             for (int q = 0; q < 3; q++)
                 u[r * 3 + q] = w[r * 3] * Di[q] + w[r * 3 + 1] * Di[3 + q] + w[r * 3 + 2] * Di[6 + q];
@@ -365,16 +385,11 @@ __global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag, con
 #pragma unroll
             for (int q = 0; q < 6; q++)
                 acc[r * 6 + q] += u[r * 3] * v[q * 3] + u[r * 3 + 1] * v[q * 3 + 1] + u[r * 3 + 2] * v[q * 3 + 2];
-    }
-    const bool diag = bi == bj;
-    if (diag) {
-        for (int a = d.poStart[bi] + tid; a < d.poStart[bi + 1]; a += kSpT) {
-            const int k = d.actPos[d.poEdges[a]];
-            const double* B = d.Hpl_e + 18 * (size_t)k;
-            const double* db = d.db + 3 * (size_t)d.actPt[k];
-            const double b0 = db[0], b1 = db[1], b2 = db[2];
+        if (diag) {
+            const double* db = d.db + 3 * (size_t)l;
+            const double g0 = db[0], g1 = db[1], g2 = db[2];
 #pragma unroll
-            for (int i = 0; i < 6; i++) acc[36 + i] += B[i * 3] * b0 + B[i * 3 + 1] * b1 + B[i * 3 + 2] * b2;
+            for (int i = 0; i < 6; i++) acc[36 + i] += w[i * 3] * g0 + w[i * 3 + 1] * g1 + w[i * 3 + 2] * g2;
         }
     }
     const int nv = diag ? 42 : 36;
@@ -383,7 +398,7 @@ __global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag, con
         if (i < nv) part[i][tid] = acc[i];
     __syncthreads();
     // value v = t >> 2, quarter q = t & 3 sums part[v][64q .. 64q + 63]; quarters meet by xor
-    const int t = tid, v = t >> 2, q = t & 3;
+    const int v = tid >> 2, q = tid & 3;
     double sum = 0.0;
     if (v < nv) {
 #pragma unroll 8
@@ -391,7 +406,6 @@ __global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag, con
     }
     sum += __shfl_xor(sum, 1, 64);
     sum += __shfl_xor(sum, 2, 64);
-    (void)lane;
     if (v < nv && q == 0) {
         const int n = 6 * d.P;
         if (v < 36) {
@@ -734,10 +748,10 @@ __global__ __launch_bounds__(256) void k_backsub_update(LbaDev d, const int32_t*
         const int l = i;
         double cl[3] = {d.bl[3 * (size_t)l], d.bl[3 * (size_t)l + 1], d.bl[3 * (size_t)l + 2]};
         for (int a = d.ptStart[l]; a < d.ptStart[l + 1]; a++) {
-            const int e = d.ptEdges[a];
-            const int pi = d.poseIdx[d.eps[e]];
-            if (pi < 0) continue;
-            const double* Bi = d.Hpl_e + 18 * (size_t)d.actPos[e];
+            const int k = d.ptAct[a];
+            const int pi = d.actPi[k];
+            if (pi < 0) break;   // fixed poses are last
+            const double* Bi = d.Hpl_e + 18 * (size_t)k;
             for (int q = 0; q < 3; q++)
                 for (int r = 0; r < 6; r++) cl[q] += Bi[r * 3 + q] * (-d.x[6 * pi + r]);
         }
@@ -1390,25 +1404,20 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
 
     HostStructure hs;
     int32_t* d_freePoses = nullptr;
-    int32_t *d_pairI = nullptr, *d_pairJ = nullptr;
     const bool root = c->rank == 0;
 
     // global sum of the owned-point partials (and replicated pose part) of a scalar vector
 
     auto init_opt = [&](int lvl) -> int {
         build_structure(p, level, lvl, c->rank, c->world, hs);
-        int32_t *act, *poseIdx, *ptLocal, *ptGlob, *actPos, *ptStart, *ptEdges, *poStart, *poEdges, *prStart, *prE1, *prE2;
-        int32_t *actPt, *actPi;
-        TRY(upload_batch(c, 1, {up(&actPt, hs.actPt), up(&actPi, hs.actPi), up(&act, hs.act), up(&poseIdx, hs.poseIdx),
-                                up(&ptLocal, hs.ptLocal), up(&ptGlob, hs.ptGlob), up(&actPos, hs.actPos),
-                                up(&ptStart, hs.ptStart), up(&ptEdges, hs.ptEdges), up(&poStart, hs.poStart),
-                                up(&poEdges, hs.poEdges), up(&prStart, hs.prStart), up(&prE1, hs.prE1),
-                                up(&prE2, hs.prE2), up(&d_freePoses, hs.freePoses), up(&d_pairI, hs.pairI),
-                                up(&d_pairJ, hs.pairJ), up(&robust, robustH)}));
+        int32_t *act, *poseIdx, *ptGlob, *actPt, *actPi, *ptStart, *ptAct, *poStart, *poAct, *poPt;
+        TRY(upload_batch(c, 1, {up(&act, hs.act), up(&poseIdx, hs.poseIdx), up(&ptGlob, hs.ptGlob), up(&actPt, hs.actPt),
+                                up(&actPi, hs.actPi), up(&ptStart, hs.ptStart), up(&ptAct, hs.ptAct),
+                                up(&poStart, hs.poStart), up(&poAct, hs.poAct), up(&poPt, hs.poPt),
+                                up(&d_freePoses, hs.freePoses), up(&robust, robustH)}));
         d.robust = robust;
-        d.act = act; d.nact = (int)hs.act.size(); d.poseIdx = poseIdx; d.ptLocal = ptLocal; d.ptGlob = ptGlob;
-        d.actPos = actPos; d.P = hs.P; d.M = hs.M; d.ptStart = ptStart; d.ptEdges = ptEdges; d.poStart = poStart;
-        d.poEdges = poEdges; d.prStart = prStart; d.prE1 = prE1; d.prE2 = prE2;
+        d.act = act; d.nact = (int)hs.act.size(); d.poseIdx = poseIdx; d.ptGlob = ptGlob;
+        d.P = hs.P; d.M = hs.M; d.ptStart = ptStart; d.ptAct = ptAct; d.poStart = poStart; d.poAct = poAct; d.poPt = poPt;
         d.actPt = actPt; d.actPi = actPi;
         d.bs = d.S + (size_t)36 * d.P * d.P;   // b_s right after the 6P x 6P matrix: one all-reduce
         return ORB_OK;
@@ -1445,7 +1454,7 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
         // ---- trial: Schur complement, reduced solve, back-substitution + update, new chi2
         if (d.M > 0) hipLaunchKernelGGL(k_point_schur, grid(d.M), dim3(256), 0, s, d);
         const int npairs = d.P * (d.P + 1) / 2;
-        if (npairs > 0) hipLaunchKernelGGL(k_schur_pairs, dim3(npairs), dim3(kSpT), 0, s, d, root ? 1 : 0, d_pairI, d_pairJ);
+        if (npairs > 0) hipLaunchKernelGGL(k_schur_pairs, dim3(npairs), dim3(kSpT), 0, s, d, root ? 1 : 0);
         if (d.P > 0) TRY(comm_allreduce_g(c, d.S, (size_t)36 * d.P * d.P + 6 * (size_t)d.P, 0, d.lm, 1));
         if (prof) (void)hipEventRecord(ev[2], s);
         if (d.P > 0) {
@@ -1507,7 +1516,7 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
             } k;
             std::memset(&k, 0, sizeof(k));
             k.d = d;
-            k.ptrs[0] = d_pairI; k.ptrs[1] = d_pairJ; k.ptrs[2] = d_freePoses; k.ptrs[3] = d_trace;
+            k.ptrs[0] = nullptr; k.ptrs[1] = nullptr; k.ptrs[2] = d_freePoses; k.ptrs[3] = d_trace;
             k.ptrs[4] = d_ldlw; k.ptrs[5] = s;
             k.h[0] = hm; k.h[1] = hsv;
             k.v[0] = iterations; k.v[1] = maxTrials; k.v[2] = o->fixed_iterations; k.v[3] = root;

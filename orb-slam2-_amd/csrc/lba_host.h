@@ -11,9 +11,14 @@
 
 namespace orbamd {
 
+// act: active edges (edge order); poseIdx: pose -> Hessian index or -1; ptGlob: owned landmark
+// local -> global index; actPt / actPi: per active edge its local landmark and pose Hessian
+// index (-1 fixed).  CSR by landmark (ptStart, ptAct: act positions sorted by pose index,
+// fixed poses last) and CSR by free pose (poStart, poAct: act positions sorted by landmark;
+// poPt: their landmarks) — the Schur kernel intersects two poses' landmark lists instead of
+// reading a precomputed pair list.
 struct HostStructure {
-    std::vector<int32_t> act, poseIdx, ptLocal, ptGlob, actPos, ptStart, ptEdges, poStart, poEdges, prStart, prE1,
-        prE2, pairI, pairJ, freePoses, actPt, actPi;
+    std::vector<int32_t> act, poseIdx, ptLocal, ptGlob, actPt, actPi, ptStart, ptAct, poStart, poAct, poPt, freePoses;
     int P = 0, M = 0;
 };
 
@@ -53,92 +58,46 @@ inline void build_structure(const lba_problem* p, const std::vector<uint8_t>& le
     for (size_t k = 0; k < order.size(); k++) s.ptLocal[order[k]] = (int)k;
     s.ptGlob = order;
     s.M = (int)order.size();
-    s.actPos.assign(NE, -1);
-    for (size_t k = 0; k < s.act.size(); k++) s.actPos[s.act[k]] = (int)k;
-    s.actPt.resize(s.act.size());
-    s.actPi.resize(s.act.size());
-    for (size_t k = 0; k < s.act.size(); k++) {
+    const int NA = (int)s.act.size();
+    s.actPt.resize(NA);
+    s.actPi.resize(NA);
+    for (int k = 0; k < NA; k++) {
         s.actPt[k] = s.ptLocal[p->edge_point[s.act[k]]];
         s.actPi[k] = s.poseIdx[p->edge_pose[s.act[k]]];
     }
-    // Edges bucketed by pose key (Hessian index, fixed poses last as key P) with a stable
-    // counting sort; scattering the buckets in key order into per-landmark lists gives the CSR
-    // by landmark with each list sorted by pose index (fixed last, edge order among them), and
-    // the free-pose buckets are the CSR by pose (edge order) as they stand.
-    const int P = s.P, NA = (int)s.act.size();
-    std::vector<int32_t> key(NA), byKey(NA), kStart(P + 2, 0);
-    for (int k = 0; k < NA; k++) {
-        const int pi = s.actPi[k];
-        key[k] = pi < 0 ? P : pi;
-        kStart[key[k] + 1]++;
-    }
+    // CSR by landmark sorted by pose key (Hessian index, fixed poses last as key P): a stable
+    // counting sort by key, scattered in key order into the landmark buckets
+    const int P = s.P;
+    std::vector<int32_t> byKey(NA), kStart(P + 2, 0);
+    for (int k = 0; k < NA; k++) kStart[(s.actPi[k] < 0 ? P : s.actPi[k]) + 1]++;
     for (int i = 0; i <= P; i++) kStart[i + 1] += kStart[i];
     {
         std::vector<int32_t> fill(kStart.begin(), kStart.end() - 1);
-        for (int k = 0; k < NA; k++) byKey[fill[key[k]]++] = k;   // act positions
+        for (int k = 0; k < NA; k++) byKey[fill[s.actPi[k] < 0 ? P : s.actPi[k]]++] = k;
     }
     s.ptStart.assign(s.M + 1, 0);
     for (int k = 0; k < NA; k++) s.ptStart[s.actPt[k] + 1]++;
     for (int i = 0; i < s.M; i++) s.ptStart[i + 1] += s.ptStart[i];
-    s.ptEdges.resize(NA);
-    std::vector<int32_t> ptPos(NA);   // act positions, landmark-major (parallel to ptEdges)
+    s.ptAct.resize(NA);
     {
         std::vector<int32_t> fill(s.ptStart.begin(), s.ptStart.end() - 1);
         for (int t = 0; t < NA; t++) {
-            const int k = byKey[t], at = fill[s.actPt[k]]++;
-            ptPos[at] = k;
-            s.ptEdges[at] = s.act[k];
+            const int k = byKey[t];
+            s.ptAct[fill[s.actPt[k]]++] = k;
         }
     }
+    // CSR by free pose sorted by landmark: the landmark-major list scattered into pose buckets
     s.poStart.assign(kStart.begin(), kStart.begin() + P + 1);
-    s.poEdges.resize(kStart[P]);
-    for (int t = 0; t < kStart[P]; t++) s.poEdges[t] = s.act[byKey[t]];
-    // pose-pair blocks (i <= j) with their contributions (landmark order, then edge order)
-    const int npairs = P * (P + 1) / 2;
-    s.pairI.resize(npairs);
-    s.pairJ.resize(npairs);
-    std::vector<int> pairOf((size_t)P * P, -1);
+    s.poAct.resize(kStart[P]);
+    s.poPt.resize(kStart[P]);
     {
-        int k = 0;
-        for (int i = 0; i < P; i++)
-            for (int j = i; j < P; j++) {
-                s.pairI[k] = i;
-                s.pairJ[k] = j;
-                pairOf[(size_t)i * P + j] = k++;
-            }
-    }
-    std::vector<int> cnt(npairs + 1, 0);
-    for (int l = 0; l < s.M; l++) {
-        const int a0 = s.ptStart[l], a1 = s.ptStart[l + 1];
-        for (int a = a0; a < a1; a++) {
-            const int i1 = key[ptPos[a]];
-            if (i1 == P) break;   // fixed poses are last
-            const int* row = pairOf.data() + (size_t)i1 * P;
-            for (int b = a; b < a1; b++) {
-                const int i2 = key[ptPos[b]];
-                if (i2 == P) break;
-                cnt[row[i2] + 1]++;
-            }
-        }
-    }
-    for (int i = 0; i < npairs; i++) cnt[i + 1] += cnt[i];
-    s.prStart = cnt;
-    s.prE1.resize(cnt[npairs]);
-    s.prE2.resize(cnt[npairs]);
-    std::vector<int> fill(cnt.begin(), cnt.end() - 1);
-    for (int l = 0; l < s.M; l++) {
-        const int a0 = s.ptStart[l], a1 = s.ptStart[l + 1];
-        for (int a = a0; a < a1; a++) {
-            const int i1 = key[ptPos[a]];
-            if (i1 == P) break;
-            const int* row = pairOf.data() + (size_t)i1 * P;
-            for (int b = a; b < a1; b++) {
-                const int i2 = key[ptPos[b]];
-                if (i2 == P) break;
-                const int at = fill[row[i2]]++;
-                s.prE1[at] = ptPos[a];   // act positions (Hpl_e rows)
-                s.prE2[at] = ptPos[b];
-            }
+        std::vector<int32_t> fill(kStart.begin(), kStart.begin() + P);
+        for (int t = 0; t < NA; t++) {
+            const int k = s.ptAct[t], i = s.actPi[k];
+            if (i < 0) continue;
+            const int at = fill[i]++;
+            s.poAct[at] = k;
+            s.poPt[at] = s.actPt[k];
         }
     }
 }

@@ -32,7 +32,7 @@ int main() {
         const auto t0 = std::chrono::steady_clock::now();
         orbamd::build_structure(&p, level, 0, 0, 1, hs);
         const auto t1 = std::chrono::steady_clock::now();
-        std::printf("edges %d contributions %zu: %.1f us\n", p.n_edges, hs.prE1.size(),
+        std::printf("edges %d active %zu: %.1f us\n", p.n_edges, hs.act.size(),
                     std::chrono::duration<double, std::micro>(t1 - t0).count());
     }
     return 0;
