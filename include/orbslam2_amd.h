@@ -321,6 +321,8 @@ int lba_stats(lba_context* c, double* ms4, int* iters, int* trials);
 /* Converter::toSE3Quat(const cv::Mat& Tcw) / Converter::toCvMat(const SE3Quat&)
  * (R/src/Converter.cpp:47-57, 59-63): row-major 4x4 float <-> quaternion + t. */
 void lba_pose_from_Tcw(const float Tcw[16], double q[4], double t[3]);
+/* lba_pose_from_Tcw over n row-major 4x4 float poses (q: n x 4, t: n x 3). */
+void lba_poses_from_Tcw(const float* Tcw, int n, double* q, double* t);
 void lba_pose_to_Tcw(const double q[4], const double t[3], float Tcw[16]);
 
 #ifdef __cplusplus

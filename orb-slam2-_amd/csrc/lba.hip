@@ -92,9 +92,21 @@ struct LbaDev {
     double *Hll, *bl, *Dinv, *db, *Hpp, *bp;   // db = Dinv b_l
     double *S, *bs, *x;         // x: [6P + 3M]
     double* red;                // reduction scratch
+    double *partChi, *partScale, *partMax;   // per-workgroup partials (single-process LM kernels)
     int* flags;                 // [0] LDLT failure
     LmState* lm;                // LM control state (device)
 };
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ double wave_max_d(double v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return v;
+}
 
 __device__ __forceinline__ void d_transform(const LbaDev& d, int pose, int pt, double Xc[3]) {
     double r[3];
@@ -110,8 +122,8 @@ __device__ __forceinline__ double d_edge_chi2(const LbaDev& d, int e) {
     return s;
 }
 
-// computeError of active edge k; echi[k] = its robust chi2 (activeRobustChi2 term)
-__device__ __forceinline__ void edge_error(const LbaDev& d, int k, double hmono, double hstereo) {
+// computeError of active edge k; echi[k] = its robust chi2 (activeRobustChi2 term), returned
+__device__ __forceinline__ double edge_error(const LbaDev& d, int k, double hmono, double hstereo) {
     const int e = d.act[k];
     double Xc[3];
     d_transform(d, d.eps[e], d.ept[e], Xc);
@@ -139,12 +151,16 @@ __device__ __forceinline__ void edge_error(const LbaDev& d, int k, double hmono,
         if (chi > dsqr) chi = 2 * sqrt(chi) * delta - dsqr;
     }
     d.echi[k] = chi;
+    return chi;
 }
 
-__global__ __launch_bounds__(256) void k_edge_errors(LbaDev d, double hmono, double hstereo, int want) {
+// Trial errors (one wave per 64 edges); partChi[block] = the wave's robust chi2 sum.
+__global__ __launch_bounds__(64) void k_edge_errors(LbaDev d, double hmono, double hstereo, int want) {
     if (lm_off(d.lm, want)) return;
-    const int k = blockIdx.x * 256 + threadIdx.x;
-    if (k < d.nact) edge_error(d, k, hmono, hstereo);
+    const int k = blockIdx.x * 64 + threadIdx.x;
+    const double chi = k < d.nact ? edge_error(d, k, hmono, hstereo) : 0.0;
+    const double sum = wave_sum_d(chi);
+    if (threadIdx.x == 0) d.partChi[blockIdx.x] = sum;
 }
 
 // Jacobians + Huber-weighted quadratic-form blocks per active edge.
@@ -237,71 +253,113 @@ __device__ __forceinline__ void edge_linearize(const LbaDev& d, int k, double hm
 
 // Phase-0 linearisation of active edge k (computeActiveErrors + linearizeOplus +
 // constructQuadraticForm, G/core/sparse_optimizer.cpp:384-394, block_solver.hpp:502-561).
-__global__ __launch_bounds__(256) void k_edge_lin(LbaDev d, double hmono, double hstereo) {
+// One wave per 64 edges (a launch wide enough to reach every CU); partChi[block] as above.
+__global__ __launch_bounds__(64) void k_edge_lin(LbaDev d, double hmono, double hstereo) {
     if (lm_off(d.lm, 0)) return;
-    const int k = blockIdx.x * 256 + threadIdx.x;
-    if (k >= d.nact) return;
-    edge_error(d, k, hmono, hstereo);
-    edge_linearize(d, k, hmono, hstereo);
+    const int k = blockIdx.x * 64 + threadIdx.x;
+    double chi = 0.0;
+    if (k < d.nact) {
+        chi = edge_error(d, k, hmono, hstereo);
+        edge_linearize(d, k, hmono, hstereo);
+    }
+    const double sum = wave_sum_d(chi);
+    if (threadIdx.x == 0) d.partChi[blockIdx.x] = sum;
 }
 
-// Vertex blocks: workgroups [0, P) reduce Hpp, b_p of one free pose over its edges (256
-// threads, fixed lane/tree order); the rest reduce Hll, b_l of 256 owned landmarks each (one
-// thread per landmark, edges in pose-index order).
+// Vertex blocks (256 threads): workgroups [0, P) reduce Hpp, b_p of one free pose over its
+// edges (thread partials meet in LDS in a fixed order); the rest reduce Hll, b_l of 64 owned
+// landmarks each, four lanes per landmark (edges in pose-index order, lanes combined by xor).
+// partMax[block] = the block's largest |diagonal| (computeLambdaInit).
+constexpr int kLanesPerPt = 4;
 __global__ __launch_bounds__(256) void k_vertex_reduce(LbaDev d) {
     if (lm_off(d.lm, 0)) return;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    __shared__ double part[27][257];
+    __shared__ double wmax[4];
     if ((int)blockIdx.x < d.P) {
-        const int p = blockIdx.x, lane = tid & 63, wave = tid >> 6;
-        __shared__ double part[4][28];
+        const int p = blockIdx.x;
         double acc[27];
+#pragma unroll
         for (int i = 0; i < 27; i++) acc[i] = 0;
         for (int a = d.poStart[p] + tid; a < d.poStart[p + 1]; a += 256) {
             const int k = d.poAct[a];
+#pragma unroll
             for (int i = 0; i < 21; i++) acc[i] += d.Hpp_e[21 * (size_t)k + i];
+#pragma unroll
             for (int i = 0; i < 6; i++) acc[21 + i] += d.bp_e[6 * (size_t)k + i];
         }
-        for (int i = 0; i < 27; i++) {
-            double v = acc[i];
-            for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-            if (lane == 0) part[wave][i] = v;
+#pragma unroll
+        for (int i = 0; i < 27; i++) part[i][tid] = acc[i];
+        __syncthreads();
+        // value v = t >> 3 (27 values x 8 eighths of 32 partials), eighths meet by xor
+        const int v = tid >> 3, e8 = tid & 7;
+        double sum = 0.0;
+        if (v < 27) {
+#pragma unroll 8
+            for (int i = 0; i < 32; i++) sum += part[v][32 * e8 + i];
         }
+        sum += __shfl_xor(sum, 1, 64);
+        sum += __shfl_xor(sum, 2, 64);
+        sum += __shfl_xor(sum, 4, 64);
+        __syncthreads();
+        if (v < 27 && e8 == 0) part[v][0] = sum;
         __syncthreads();
         if (tid < 27) {
-            const double v = (part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]);
+            const double val = part[tid][0];
             if (tid < 21) {
                 int i = 0, o = tid;
                 while (o >= 6 - i) { o -= 6 - i; i++; }
                 const int j = i + o;
-                d.Hpp[36 * (size_t)p + i * 6 + j] = v;
-                d.Hpp[36 * (size_t)p + j * 6 + i] = v;
+                d.Hpp[36 * (size_t)p + i * 6 + j] = val;
+                d.Hpp[36 * (size_t)p + j * 6 + i] = val;
             } else {
-                d.bp[6 * (size_t)p + tid - 21] = v;
+                d.bp[6 * (size_t)p + tid - 21] = val;
             }
+        }
+        if (tid == 0) {   // diagonal entries sit at upper-row offsets 0, 6, 11, 15, 18, 20
+            double m = 0;
+            const int dia[6] = {0, 6, 11, 15, 18, 20};
+            for (int i = 0; i < 6; i++) m = fmax(m, fabs(part[dia[i]][0]));
+            d.partMax[blockIdx.x] = m;
         }
         return;
     }
-    const int l = ((int)blockIdx.x - d.P) * 256 + tid;
-    if (l >= d.M) return;
+    const int l = ((int)blockIdx.x - d.P) * (256 / kLanesPerPt) + (tid / kLanesPerPt), sub = tid % kLanesPerPt;
     double h[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
-    for (int a = d.ptStart[l]; a < d.ptStart[l + 1]; a++) {
-        const int k = d.ptAct[a];
-        for (int i = 0; i < 6; i++) h[i] += d.Hll_e[6 * (size_t)k + i];
-        for (int i = 0; i < 3; i++) b[i] += d.bl_e[3 * (size_t)k + i];
+    if (l < d.M) {
+        for (int a = d.ptStart[l] + sub; a < d.ptStart[l + 1]; a += kLanesPerPt) {
+            const int k = d.ptAct[a];
+#pragma unroll
+            for (int i = 0; i < 6; i++) h[i] += d.Hll_e[6 * (size_t)k + i];
+#pragma unroll
+            for (int i = 0; i < 3; i++) b[i] += d.bl_e[3 * (size_t)k + i];
+        }
     }
-    double* H = d.Hll + 9 * (size_t)l;
-    H[0] = h[0]; H[1] = h[1]; H[2] = h[2];
-    H[3] = h[1]; H[4] = h[3]; H[5] = h[4];
-    H[6] = h[2]; H[7] = h[4]; H[8] = h[5];
-    for (int i = 0; i < 3; i++) d.bl[3 * (size_t)l + i] = b[i];
+#pragma unroll
+    for (int i = 0; i < 6; i++) { h[i] += __shfl_xor(h[i], 1, 64); h[i] += __shfl_xor(h[i], 2, 64); }
+#pragma unroll
+    for (int i = 0; i < 3; i++) { b[i] += __shfl_xor(b[i], 1, 64); b[i] += __shfl_xor(b[i], 2, 64); }
+    double m = 0.0;
+    if (l < d.M && sub == 0) {
+        double* H = d.Hll + 9 * (size_t)l;
+        H[0] = h[0]; H[1] = h[1]; H[2] = h[2];
+        H[3] = h[1]; H[4] = h[3]; H[5] = h[4];
+        H[6] = h[2]; H[7] = h[4]; H[8] = h[5];
+        for (int i = 0; i < 3; i++) d.bl[3 * (size_t)l + i] = b[i];
+        m = fmax(fabs(h[0]), fmax(fabs(h[3]), fabs(h[5])));
+    }
+    m = wave_max_d(m);
+    if (lane == 0) wmax[wave] = m;
+    __syncthreads();
+    if (tid == 0) d.partMax[blockIdx.x] = fmax(fmax(wmax[0], wmax[1]), fmax(wmax[2], wmax[3]));
 }
 
 // Per landmark with lambda (G/core/block_solver.hpp:380-398): D^-1 = (Hll + lambda I)^-1
 // (Eigen's 3x3 cofactor inverse) and D^-1 b_l.
-__global__ __launch_bounds__(256) void k_point_schur(LbaDev d) {
+__global__ __launch_bounds__(64) void k_point_schur(LbaDev d) {
     if (lm_off(d.lm, 1)) return;
     const double lambda = d.lm->lambda;
-    const int l = blockIdx.x * 256 + threadIdx.x;
+    const int l = blockIdx.x * 64 + threadIdx.x;
     if (l >= d.M) return;
     double m[9];
     for (int i = 0; i < 9; i++) m[i] = d.Hll[9 * (size_t)l + i];
@@ -738,45 +796,72 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_solve(const double* __restrict__
 }
 
 
-// Back-substitution and update (G/core/block_solver.hpp:462-484, sparse_optimizer.cpp:422-435):
-// thread l: x_l = D^-1 (b_l - sum_e Hpl_e^T x_p(pose_e)), push() of X_l and X_l += x_l; the
-// first P threads also push and apply T <- exp(x_p) T to their free pose.
+// Back-substitution and update (G/core/block_solver.hpp:462-484, sparse_optimizer.cpp:422-435),
+// 64 landmarks per 256-thread block, four lanes per landmark: x_l = D^-1 (b_l - sum_e
+// Hpl_e^T x_p(pose_e)), push() of X_l and X_l += x_l.  The block after the landmark blocks
+// pushes and applies T <- exp(x_p) T to the free poses.  partScale[block] = the block's share
+// of x^T (lambda x + b) (OptimizationAlgorithmLevenberg::computeScale).
 __global__ __launch_bounds__(256) void k_backsub_update(LbaDev d, const int32_t* __restrict__ freePoses) {
     if (lm_off(d.lm, 1)) return;
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i < d.M) {
-        const int l = i;
-        double cl[3] = {d.bl[3 * (size_t)l], d.bl[3 * (size_t)l + 1], d.bl[3 * (size_t)l + 2]};
-        for (int a = d.ptStart[l]; a < d.ptStart[l + 1]; a++) {
-            const int k = d.ptAct[a];
-            const int pi = d.actPi[k];
-            if (pi < 0) break;   // fixed poses are last
-            const double* Bi = d.Hpl_e + 18 * (size_t)k;
-            for (int q = 0; q < 3; q++)
-                for (int r = 0; r < 6; r++) cl[q] += Bi[r * 3 + q] * (-d.x[6 * pi + r]);
+    const double lambda = d.lm->lambda;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    __shared__ double wsum[4];
+    const int nPtBlocks = (d.M + 63) / 64;
+    double sc = 0.0;
+    if ((int)blockIdx.x < nPtBlocks) {
+        const int l = blockIdx.x * 64 + tid / kLanesPerPt, sub = tid % kLanesPerPt;
+        double cl[3] = {0.0, 0.0, 0.0};
+        if (l < d.M) {
+            for (int a = d.ptStart[l] + sub; a < d.ptStart[l + 1]; a += kLanesPerPt) {
+                const int k = d.ptAct[a];
+                const int pi = d.actPi[k];
+                if (pi < 0) break;   // fixed poses are last
+                const double* Bi = d.Hpl_e + 18 * (size_t)k;
+                const double* xp = d.x + 6 * pi;
+#pragma unroll
+                for (int q = 0; q < 3; q++)
+#pragma unroll
+                    for (int r = 0; r < 6; r++) cl[q] += Bi[r * 3 + q] * (-xp[r]);
+            }
         }
-        const double* Di = d.Dinv + 9 * (size_t)l;
-        double* xl = d.x + 6 * (size_t)d.P + 3 * (size_t)l;
-        const int g = d.ptGlob[l];
-        for (int q = 0; q < 3; q++) {
-            const double v = Di[q * 3] * cl[0] + Di[q * 3 + 1] * cl[1] + Di[q * 3 + 2] * cl[2];
-            xl[q] = v;
-            const double X = d.X[3 * (size_t)g + q];
-            d.bX[3 * (size_t)g + q] = X;
-            d.X[3 * (size_t)g + q] = X + v;
+#pragma unroll
+        for (int q = 0; q < 3; q++) { cl[q] += __shfl_xor(cl[q], 1, 64); cl[q] += __shfl_xor(cl[q], 2, 64); }
+        if (l < d.M && sub == 0) {
+            const double* bl = d.bl + 3 * (size_t)l;
+            const double c0 = bl[0] + cl[0], c1 = bl[1] + cl[1], c2 = bl[2] + cl[2];
+            const double* Di = d.Dinv + 9 * (size_t)l;
+            double* xl = d.x + 6 * (size_t)d.P + 3 * (size_t)l;
+            const int g = d.ptGlob[l];
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                const double v = Di[q * 3] * c0 + Di[q * 3 + 1] * c1 + Di[q * 3 + 2] * c2;
+                xl[q] = v;
+                const double X = d.X[3 * (size_t)g + q];
+                d.bX[3 * (size_t)g + q] = X;
+                d.X[3 * (size_t)g + q] = X + v;
+                sc += v * (lambda * v + bl[q]);
+            }
+        }
+    } else {
+        for (int i = tid; i < d.P; i += 256) {
+            const int p = freePoses[i];
+            const int k = d.poseIdx[p];
+            double q[4], t[3], u[6];
+            for (int j = 0; j < 4; j++) { q[j] = d.q[4 * p + j]; d.bq[4 * p + j] = q[j]; }
+            for (int j = 0; j < 3; j++) { t[j] = d.t[3 * p + j]; d.bt[3 * p + j] = t[j]; }
+            for (int j = 0; j < 6; j++) {
+                u[j] = d.x[6 * k + j];
+                sc += u[j] * (lambda * u[j] + d.bp[6 * k + j]);
+            }
+            d_se3_exp_left(u, q, t);
+            for (int j = 0; j < 4; j++) d.q[4 * p + j] = q[j];
+            for (int j = 0; j < 3; j++) d.t[3 * p + j] = t[j];
         }
     }
-    if (i < d.P) {
-        const int p = freePoses[i];
-        const int k = d.poseIdx[p];
-        double q[4], t[3], u[6];
-        for (int j = 0; j < 4; j++) { q[j] = d.q[4 * p + j]; d.bq[4 * p + j] = q[j]; }
-        for (int j = 0; j < 3; j++) { t[j] = d.t[3 * p + j]; d.bt[3 * p + j] = t[j]; }
-        for (int j = 0; j < 6; j++) u[j] = d.x[6 * k + j];
-        d_se3_exp_left(u, q, t);
-        for (int j = 0; j < 4; j++) d.q[4 * p + j] = q[j];
-        for (int j = 0; j < 3; j++) d.t[3 * p + j] = t[j];
-    }
+    sc = wave_sum_d(sc);
+    if (lane == 0) wsum[wave] = sc;
+    __syncthreads();
+    if (tid == 0) d.partScale[blockIdx.x] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
 }
 
 // pop() after a rejected trial (communicator path; k_lm_decide_fused does it in one process)
@@ -937,57 +1022,27 @@ __global__ void k_lm_decide(LmState* st, const double* __restrict__ red, const i
     lm_decide(st, red[0], red[2], flags[0], maxTrials, iterations, fixedIterations, trace);
 }
 
-// Fixed-order single-workgroup sum (the k_sum order): thread t adds v(t), v(t + 1024), ...,
-// then a shared-memory tree.  `f(i)` yields term i.
-template <typename F>
-__device__ __forceinline__ double block_sum_1024(int n, F f, double* sh) {
-    const int tid = threadIdx.x;
-    double s = 0;
-    for (int i = tid; i < n; i += 1024) s += f(i);
-    sh[tid] = s;
-    __syncthreads();
-    for (int w = 512; w >= 1; w >>= 1) {
-        if (tid < w) sh[tid] += sh[tid + w];
-        __syncthreads();
-    }
-    const double r = sh[0];
-    __syncthreads();
-    return r;
-}
-
-// Single process: the start of an LM iteration in one workgroup — the linearisation's robust
-// chi2 (k_sum), computeLambdaInit's max diagonal at iteration 0 (k_maxdiag) and lm_begin.
-__global__ __launch_bounds__(1024) void k_lm_begin_fused(LbaDev d) {
-    __shared__ double sh[1024];
-    __shared__ int go, first;
+// Single process: the start of an LM iteration in one wave — the linearisation's robust chi2
+// (sum of k_edge_lin's per-wave partials), computeLambdaInit's max diagonal at iteration 0
+// (k_vertex_reduce's per-block maxima) and lm_begin.
+__global__ __launch_bounds__(64) void k_lm_begin_fused(LbaDev d, int nChi, int nMax) {
     LmState* st = d.lm;
-    const int tid = threadIdx.x;
-    if (tid == 0) { go = st->phase == 0; first = st->it == 0; }
-    __syncthreads();
-    if (!go) return;
-    const double chi = block_sum_1024(d.nact, [&](int i) { return d.echi[i]; }, sh);
-    double m = 0;
-    if (first) {
-        for (int i = tid; i < 6 * d.P; i += 1024) m = fmax(m, fabs(d.Hpp[36 * (i / 6) + 7 * (i % 6)]));
-        for (int i = tid; i < 3 * d.M; i += 1024) m = fmax(m, fabs(d.Hll[9 * (i / 3) + 4 * (i % 3)]));
-        sh[tid] = m;
-        __syncthreads();
-        for (int w = 512; w >= 1; w >>= 1) {
-            if (tid < w) sh[tid] = fmax(sh[tid], sh[tid + w]);
-            __syncthreads();
-        }
-        m = sh[0];
-    }
-    if (tid == 0) lm_begin(st, chi, m);
+    if (st->phase != 0) return;
+    const int lane = threadIdx.x;
+    double c = 0.0, m = 0.0;
+    for (int i = lane; i < nChi; i += 64) c += d.partChi[i];
+    for (int i = lane; i < nMax; i += 64) m = fmax(m, d.partMax[i]);
+    c = wave_sum_d(c);
+    m = wave_max_d(m);
+    if (lane == 0) lm_begin(st, c, m);
 }
 
-// Single process: the end of an LM trial in one workgroup — the trial's robust chi2, the
-// scale x^T (lambda x + b) (k_scale_terms + k_sum order), the rho decision (lm_decide) and,
+// Single process: the end of an LM trial in one workgroup — the trial's robust chi2 and the
+// scale x^T (lambda x + b) from the producers' partials, the rho decision (lm_decide) and,
 // after a rejected trial, pop() of every free pose and owned point.
 __global__ __launch_bounds__(1024) void k_lm_decide_fused(LbaDev d, const int32_t* __restrict__ freePoses,
                                                           int maxTrials, int iterations, int fixedIterations,
-                                                          double* __restrict__ trace) {
-    __shared__ double sh[1024];
+                                                          double* __restrict__ trace, int nChi, int nScale) {
     __shared__ int go, pop;
     LmState* st = d.lm;
     const int tid = threadIdx.x;
@@ -998,16 +1053,16 @@ __global__ __launch_bounds__(1024) void k_lm_decide_fused(LbaDev d, const int32_
     }
     __syncthreads();
     if (!go) return;
-    const double lambda = st->lambda;
-    const double chi = block_sum_1024(d.nact, [&](int i) { return d.echi[i]; }, sh);
-    const int np = 6 * d.P, nx = np + 3 * d.M;
-    const double scl = block_sum_1024(nx, [&](int i) {
-        const double xi = d.x[i], b = i < np ? d.bp[i] : d.bl[i - np];
-        return xi * (lambda * xi + b);
-    }, sh);
-    if (tid == 0) {
-        lm_decide(st, chi, scl, d.flags[0], maxTrials, iterations, fixedIterations, trace);
-        pop = st->pop;
+    if (tid < 64) {
+        double c = 0.0, sc = 0.0;
+        for (int i = tid; i < nChi; i += 64) c += d.partChi[i];
+        for (int i = tid; i < nScale; i += 64) sc += d.partScale[i];
+        c = wave_sum_d(c);
+        sc = wave_sum_d(sc);
+        if (tid == 0) {
+            lm_decide(st, c, sc, d.flags[0], maxTrials, iterations, fixedIterations, trace);
+            pop = st->pop;
+        }
     }
     __syncthreads();
     if (!pop) return;
@@ -1315,6 +1370,10 @@ void lba_pose_from_Tcw(const float Tcw[16], double q[4], double t[3]) {
     for (int i = 0; i < 3; i++) t[i] = (double)Tcw[i * 4 + 3];
 }
 
+void lba_poses_from_Tcw(const float* Tcw, int n, double* q, double* t) {
+    for (int i = 0; i < n; i++) lba_pose_from_Tcw(Tcw + 16 * (size_t)i, q + 4 * (size_t)i, t + 3 * (size_t)i);
+}
+
 void lba_pose_to_Tcw(const double q[4], const double t[3], float Tcw[16]) {
     // Converter::toCvMat(SE3Quat): to_homogeneous_matrix() cast to float
     const double x = q[0], y = q[1], z = q[2], w = q[3];
@@ -1377,6 +1436,9 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
     d.bs = d.S + nS * nS;
     TRY(dalloc(c, &d.x, 6 * (size_t)NP + 3 * (size_t)NM));
     TRY(dalloc(c, &d.red, 16));
+    TRY(dalloc(c, &d.partChi, (size_t)NE / 64 + 2));
+    TRY(dalloc(c, &d.partScale, (size_t)NM / 64 + 3));
+    TRY(dalloc(c, &d.partMax, (size_t)NP + (size_t)NM / 64 + 2));
     TRY(dalloc(c, &d.flags, 4));
     TRY(dalloc(c, &d.lm, 1));
     double* d_trace = nullptr;
@@ -1434,11 +1496,11 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
         const bool single = c->world == 1;   // no collectives: the LM bookkeeping fuses into single kernels
         if (prof) (void)hipEventRecord(ev[0], s);
         // ---- linearisation (G/core/sparse_optimizer.cpp:384-394, block_solver.hpp:502-561)
-        if (d.nact > 0) hipLaunchKernelGGL(k_edge_lin, grid(d.nact), dim3(256), 0, s, d, hm, hsv);
-        if (d.P + d.M > 0)
-            hipLaunchKernelGGL(k_vertex_reduce, dim3(d.P + (d.M + 255) / 256), dim3(256), 0, s, d);
+        const int nbE = (d.nact + 63) / 64, nbV = d.P + (d.M + 63) / 64, nbB = (d.M + 63) / 64 + 1;
+        if (d.nact > 0) hipLaunchKernelGGL(k_edge_lin, dim3(nbE), dim3(64), 0, s, d, hm, hsv);
+        if (nbV > 0) hipLaunchKernelGGL(k_vertex_reduce, dim3(nbV), dim3(256), 0, s, d);
         if (single) {
-            hipLaunchKernelGGL(k_lm_begin_fused, dim3(1), dim3(1024), 0, s, d);
+            hipLaunchKernelGGL(k_lm_begin_fused, dim3(1), dim3(64), 0, s, d, nbE, nbV);
         } else {
             hipLaunchKernelGGL(k_sum, dim3(1), dim3(1024), 0, s, d.echi, d.nact, d.red, d.lm, 0);
             TRY(comm_allreduce_g(c, d.red, 1, 0, d.lm, 0));
@@ -1452,7 +1514,7 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
         }
         if (prof) (void)hipEventRecord(ev[1], s);
         // ---- trial: Schur complement, reduced solve, back-substitution + update, new chi2
-        if (d.M > 0) hipLaunchKernelGGL(k_point_schur, grid(d.M), dim3(256), 0, s, d);
+        if (d.M > 0) hipLaunchKernelGGL(k_point_schur, dim3((d.M + 63) / 64), dim3(64), 0, s, d);
         const int npairs = d.P * (d.P + 1) / 2;
         if (npairs > 0) hipLaunchKernelGGL(k_schur_pairs, dim3(npairs), dim3(kSpT), 0, s, d, root ? 1 : 0);
         if (d.P > 0) TRY(comm_allreduce_g(c, d.S, (size_t)36 * d.P * d.P + 6 * (size_t)d.P, 0, d.lm, 1));
@@ -1469,12 +1531,11 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
             ORB_HIP_TRY(hipMemsetAsync(d.flags, 0, 4, s));
         }
         if (prof) (void)hipEventRecord(ev[3], s);
-        if (d.M + d.P > 0)
-            hipLaunchKernelGGL(k_backsub_update, grid(std::max(d.M, d.P)), dim3(256), 0, s, d, d_freePoses);
-        if (d.nact > 0) hipLaunchKernelGGL(k_edge_errors, grid(d.nact), dim3(256), 0, s, d, hm, hsv, 1);
+        hipLaunchKernelGGL(k_backsub_update, dim3(nbB), dim3(256), 0, s, d, d_freePoses);
+        if (d.nact > 0) hipLaunchKernelGGL(k_edge_errors, dim3(nbE), dim3(64), 0, s, d, hm, hsv, 1);
         if (single) {
             hipLaunchKernelGGL(k_lm_decide_fused, dim3(1), dim3(1024), 0, s, d, d_freePoses, maxTrials, iterations,
-                               o->fixed_iterations ? 1 : 0, d_trace);
+                               o->fixed_iterations ? 1 : 0, d_trace, nbE, nbB);
         } else {
             hipLaunchKernelGGL(k_sum, dim3(1), dim3(1024), 0, s, d.echi, d.nact, d.red, d.lm, 1);
             TRY(comm_allreduce_g(c, d.red, 1, 0, d.lm, 1));
@@ -1502,44 +1563,48 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
         hst->ni = 2;
         hst->traceBase = r->trace ? r->n_trace : 64;
         ORB_HIP_TRY(hipMemcpyAsync(d.lm, hst, sizeof(LmState), hipMemcpyHostToDevice, s));
-        // Single process, no stage events: the slot's ~20 launches are captured once per
-        // optimize() into a HIP graph and replayed, so the LM loop pays one graph launch per
-        // slot instead of a host dispatch per kernel.  (With a communicator the all-reduce is
-        // a host callback and the slot is enqueued kernel by kernel.)
-        hipGraphExec_t gexec = nullptr;
-        if (c->world == 1 && !c->profile && s != nullptr) {
+        // Single process, no stage events: the slots are captured into HIP graphs and
+        // replayed, so the LM loop pays one graph launch per group of slots instead of a host
+        // dispatch per kernel.  (With a communicator the all-reduce is a host callback and the
+        // slot is enqueued kernel by kernel.)
+        // graphs of `iterations` slots (the first group) and of one slot (the slots after
+        // rejected trials), looked up by every captured launch parameter
+        auto slot_graph = [&](int nslots, hipGraphExec_t* out) -> int {
+            *out = nullptr;
+            if (c->world != 1 || c->profile || s == nullptr) return ORB_OK;
             struct {
                 LbaDev d;
-                const void* ptrs[6];
+                const void* ptrs[4];
                 double h[2];
-                int v[4];
+                int v[5];
             } k;
             std::memset(&k, 0, sizeof(k));
             k.d = d;
-            k.ptrs[0] = nullptr; k.ptrs[1] = nullptr; k.ptrs[2] = d_freePoses; k.ptrs[3] = d_trace;
-            k.ptrs[4] = d_ldlw; k.ptrs[5] = s;
+            k.ptrs[0] = d_freePoses; k.ptrs[1] = d_trace; k.ptrs[2] = d_ldlw; k.ptrs[3] = s;
             k.h[0] = hm; k.h[1] = hsv;
-            k.v[0] = iterations; k.v[1] = maxTrials; k.v[2] = o->fixed_iterations; k.v[3] = root;
+            k.v[0] = iterations; k.v[1] = maxTrials; k.v[2] = o->fixed_iterations; k.v[3] = root; k.v[4] = nslots;
             std::vector<char> key(reinterpret_cast<const char*>(&k), reinterpret_cast<const char*>(&k) + sizeof(k));
             for (auto& g : c->graphs)
-                if (g.key == key) gexec = g.exec;
-            if (!gexec) {
-                hipGraph_t g = nullptr;
-                ORB_HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-                const int st = enqueue_slot(iterations, nullptr);
-                const hipError_t ce = hipStreamEndCapture(s, &g);
-                if (st) { if (g) (void)hipGraphDestroy(g); return st; }
-                if (ce != hipSuccess) return ORB_EGPU;
-                const hipError_t ie = hipGraphInstantiate(&gexec, g, nullptr, nullptr, 0);
-                (void)hipGraphDestroy(g);
-                if (ie != hipSuccess) return ORB_EGPU;
-                if (c->graphs.size() >= 4) {
-                    (void)hipGraphExecDestroy(c->graphs.front().exec);
-                    c->graphs.erase(c->graphs.begin());
-                }
-                c->graphs.push_back({std::move(key), gexec});
+                if (g.key == key) { *out = g.exec; return ORB_OK; }
+            hipGraph_t g = nullptr;
+            ORB_HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+            int st = ORB_OK;
+            for (int i = 0; i < nslots && !st; i++) st = enqueue_slot(iterations, nullptr);
+            const hipError_t ce = hipStreamEndCapture(s, &g);
+            if (st) { if (g) (void)hipGraphDestroy(g); return st; }
+            if (ce != hipSuccess) return ORB_EGPU;
+            const hipError_t ie = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
+            (void)hipGraphDestroy(g);
+            if (ie != hipSuccess) return ORB_EGPU;
+            if (c->graphs.size() >= 8) {
+                (void)hipGraphExecDestroy(c->graphs.front().exec);
+                c->graphs.erase(c->graphs.begin());
             }
-        }
+            c->graphs.push_back({std::move(key), *out});
+            return ORB_OK;
+        };
+        hipGraphExec_t gAll = nullptr, gOne = nullptr;
+        TRY(slot_graph(iterations, &gAll));
         int known = 0;
         for (;;) {
             const int G = std::max(1, iterations - known);
@@ -1550,9 +1615,14 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
                     c->slotEv.push_back(e);
                 }
             }
-            for (int g = 0; g < G; g++) {
-                if (gexec) ORB_HIP_TRY(hipGraphLaunch(gexec, s));
-                else TRY(enqueue_slot(iterations, c->profile ? &c->slotEv[5 * (size_t)g] : nullptr));
+            if (gAll && G == iterations) {
+                ORB_HIP_TRY(hipGraphLaunch(gAll, s));
+            } else {
+                if (gAll && !gOne) TRY(slot_graph(1, &gOne));
+                for (int g = 0; g < G; g++) {
+                    if (gOne) ORB_HIP_TRY(hipGraphLaunch(gOne, s));
+                    else TRY(enqueue_slot(iterations, c->profile ? &c->slotEv[5 * (size_t)g] : nullptr));
+                }
             }
             ORB_HIP_TRY(hipMemcpyAsync(hst, d.lm, sizeof(LmState), hipMemcpyDeviceToHost, s));
             TRY(lba_wait(c));

@@ -53,7 +53,8 @@ def _sig():
                             ("lba_solve", [vp, vp, vp, vp, vp], C.c_int), ("lba_profile", [vp, i32], C.c_int),
                             ("lba_stats", [vp, vp, vp, vp], C.c_int),
                             ("lba_dense_solve", [vp, vp, vp, i32, vp], C.c_int), ("lba_pose_from_Tcw", [vp, vp, vp], None),
-                            ("lba_pose_to_Tcw", [vp, vp, vp], None)]:
+                            ("lba_pose_to_Tcw", [vp, vp, vp], None),
+                            ("lba_poses_from_Tcw", [vp, i32, vp, vp], None)]:
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res
@@ -135,9 +136,9 @@ class LocalBA:
         polled like mbAbortBA.  Returns a dict with the optimised estimates."""
         opts = opts or options()
         nk = len(prob["Tcw"])
-        qs, ts = zip(*[pose_from_Tcw(T) for T in prob["Tcw"]]) if nk else ((), ())
-        q = np.ascontiguousarray(np.array(qs, np.float64).reshape(nk, 4))
-        t = np.ascontiguousarray(np.array(ts, np.float64).reshape(nk, 3))
+        Tcw = np.ascontiguousarray(prob["Tcw"], np.float32)
+        q, t = np.zeros((nk, 4)), np.zeros((nk, 3))
+        _sig().lba_poses_from_Tcw(_abi.ptr(Tcw), nk, _abi.ptr(q), _abi.ptr(t))   # Converter::toSE3Quat
         a = {k: np.ascontiguousarray(v) for k, v in prob.items()}
         P = _abi.ptr
         pr = LbaProblem(nk, P(q), P(t), P(a["pose_fixed"]), P(a["pose_id"]), len(a["point_xyz"]), P(a["point_xyz"]),

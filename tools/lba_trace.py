@@ -16,7 +16,7 @@ for k in ks[1:]:
         cur = []
     cur.append(k)
 groups.append(cur)
-big = [g for g in groups if len(g) > 50]
+big = [g for g in groups if len(g) > 20]
 print(f"{len(groups)} groups, {len(big)} LM loops")
 for g in big[-4:]:
     span = (g[-1][1] - g[0][0]) / 1e3
