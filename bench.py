@@ -125,6 +125,52 @@ def cpu_baseline(frames, nfeatures, budget_s):
                       f"{nfeatures} feat, oracle C restatement, {threads} host threads (1 frame per thread)"}
 
 
+F64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector and matrix (MI355X_MICROARCH.md)
+
+
+def lba_roofline(pb, out, world):
+    """Per-trial rooflines of the local-BA stages from the profiled pass's HIP-event stage times
+    (stage_ms_per_solve / trials):
+      * reduced solve (k_ldlt_solve): MFMA f64 flops of the blocked LDL^T's trailing updates,
+        8192 per 16x16x16 tile update, T = ceil(6P/16) block columns;
+      * Schur complement (k_point_schur + k_schur_pairs): SURVEY 8d's algorithmic
+        F_schur = sum_p [40 + 144 k_p + 216 k_p (k_p + 1) / 2] (k_p = free observers), on the
+        f64 VALU (sparse: a densified MFMA GEMM would do ~15x the flops);
+      * linearisation (k_edge_lin + k_vertex_reduce): SURVEY 8d's E (112 read + 160 written) +
+        M 168 bytes against HBM."""
+    trials = max(out["trials"], 1)
+    st = out["stage_ms_per_solve"]
+    fixed = pb["pose_fixed"].astype(bool)
+    free_edge = ~fixed[pb["edge_pose"]]
+    kp = np.bincount(pb["edge_point"][free_edge], minlength=len(pb["point_xyz"]))
+    P = int(np.count_nonzero(~fixed & np.isin(np.arange(len(fixed)), pb["edge_pose"])))
+    T = (6 * P + 15) // 16
+    tiles = sum((T - k - 1) * (T - k) // 2 for k in range(T))
+    mfma_flops = tiles * 8192
+    f_schur = float(np.sum(40 + 144 * kp + 216 * kp * (kp + 1) / 2)) / world
+    E, M = len(pb["edge_point"]) / world, len(pb["point_xyz"]) / world
+    lin_bytes = E * (112 + 160) + M * 168
+    t_solve = st["solve_ms"] / trials * 1e-3
+    t_schur = st["schur_ms"] / trials * 1e-3
+    t_lin = st["linearize_ms"] / trials * 1e-3
+
+    def r(x, n=4):
+        return round(x, n)
+    return {
+        "reduced_solve": {"bound": "mfma", "unit": "TFLOP/s", "flops_per_trial": mfma_flops,
+                          "us": r(t_solve * 1e6, 2), "achieved": r(mfma_flops / t_solve / 1e12, 5),
+                          "peak": F64_PEAK_TFLOPS, "frac": r(mfma_flops / t_solve / 1e12 / F64_PEAK_TFLOPS, 7),
+                          "note": f"n = {6 * P}, {tiles} 16x16 tile updates of 4 v_mfma_f64_16x16x4 each; "
+                                  "latency-bound pivot chain on one workgroup"},
+        "schur": {"bound": "valu", "unit": "TFLOP/s", "flops_per_trial": int(f_schur), "us": r(t_schur * 1e6, 2),
+                  "achieved": r(f_schur / t_schur / 1e12, 5), "peak": F64_PEAK_TFLOPS,
+                  "frac": r(f_schur / t_schur / 1e12 / F64_PEAK_TFLOPS, 6)},
+        "linearize": {"bound": "hbm", "unit": "GB/s", "bytes_per_iteration": int(lin_bytes), "us": r(t_lin * 1e6, 2),
+                      "achieved": r(lin_bytes / t_lin / 1e9, 2), "peak": 8000.0,
+                      "frac": r(lin_bytes / t_lin / 1e9 / 8000.0, 6)},
+    }
+
+
 def bench_lba(args, amd, dev, local, rank, world):
     """Local BA (BASELINE.json config 4: 20 KF x 3000 points), landmarks sharded over ranks
     with RCCL all-reduce of the reduced camera system.  ms/iter = wall time of the
@@ -175,6 +221,7 @@ def bench_lba(args, amd, dev, local, rank, world):
            "stage_ms_per_solve": {k: round(st[k] / args.lba_solves, 4) for k in
                                   ("linearize_ms", "schur_ms", "solve_ms", "update_ms")},
            "n_gpus": world}
+    out["roofline"] = lba_roofline(pb, out, world)
     if rank == 0 and not args.no_cpu:
         sys.path.insert(0, str(ROOT / "tests"))
         import oracle_ref as O
