@@ -321,6 +321,42 @@ int lba_stats(lba_context* c, double* ms4, int* iters, int* trials);
 /* Converter::toSE3Quat(const cv::Mat& Tcw) / Converter::toCvMat(const SE3Quat&)
  * (R/src/Converter.cpp:47-57, 59-63): row-major 4x4 float <-> quaternion + t. */
 void lba_pose_from_Tcw(const float Tcw[16], double q[4], double t[3]);
+/* ---------------------------------------------------------------- PoseOptimization
+ * Optimizer::PoseOptimization(Frame*) (R/src/Optimizer.cpp:306-535, declared
+ * R/include/Optimizer.h:44) over a batch of frames.  Frame b's edges are
+ * [edge_start[b], edge_start[b+1]): one per keypoint with a map point, obs = (u, v, ur) with
+ * ur < 0 for a monocular observation (Frame::mvuRight), xw = MapPoint::GetWorldPos (float
+ * values), info = mvInvLevelSigma2[octave] (float value); cam = fx, fy, cx, cy, mbf; pose =
+ * Converter::toSE3Quat(pFrame->mTcw).  Results: the optimised pose (pFrame->SetPose), the
+ * per-edge outlier flags (Frame::mvbOutlier) and the return value nInitialCorrespondences -
+ * nBad (0 and the pose untouched below 3 edges). */
+typedef struct {
+    int n_frames;
+    int n_edges;
+    const double* pose_q;       /* [B][4] x, y, z, w */
+    const double* pose_t;       /* [B][3] */
+    const double* cam;          /* [B][5] */
+    const int32_t* edge_start;  /* [B + 1] */
+    const double* edge_obs;     /* [E][3] */
+    const double* edge_xw;      /* [E][3] */
+    const double* edge_info;    /* [E] */
+} pose_batch;
+
+typedef struct {
+    double* pose_q;      /* [B][4] */
+    double* pose_t;      /* [B][3] */
+    uint8_t* outlier;    /* [E] */
+    int32_t* n_inliers;  /* [B] */
+} pose_batch_result;
+
+/* Host buffers, synchronous.  iters (optional, [B][5]): LM iterations of rounds 0-3, trials. */
+int pose_optimize_batch(int device, const pose_batch* p, pose_batch_result* r, int32_t* iters);
+/* Device-resident form, asynchronous on `stream`: every pointer of p and r in device memory;
+ * d_work holds 3 * n_edges doubles and d_flags 2 * n_edges bytes of per-edge state; d_iters
+ * ([B][5]) may be NULL. */
+int pose_optimize_batch_device(const pose_batch* p, const pose_batch_result* r, double* d_work, uint8_t* d_flags,
+                               int32_t* d_iters, void* stream);
+
 /* lba_pose_from_Tcw over n row-major 4x4 float poses (q: n x 4, t: n x 3). */
 void lba_poses_from_Tcw(const float* Tcw, int n, double* q, double* t);
 void lba_pose_to_Tcw(const double q[4], const double t[3], float Tcw[16]);

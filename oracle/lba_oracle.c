@@ -737,3 +737,323 @@ done:
     (void)cmp_i64_idx_base;
     return status;
 }
+
+/* ======================================================================== PoseOptimization
+ * Optimizer::PoseOptimization (R/src/Optimizer.cpp:306-535): one VertexSE3Expmap, unary
+ * EdgeSE3ProjectXYZOnlyPose / EdgeStereoSE3ProjectXYZOnlyPose edges
+ * (G/types/types_six_dof_expmap.h:210-320, .cpp:285-390), Huber (float)sqrt(5.991) /
+ * (float)sqrt(7.815), LM (optimization_algorithm_levenberg.cpp:61-189) with
+ * BlockSolver_6_3 + LinearSolverDense (an LDL^T of the 6x6 H + lambda I; Eigen's pivoted LDLT is
+ * restated without pivoting: same solution to rounding), four rounds of optimize(10) from the
+ * frame's initial pose with the chi2 inlier/outlier reclassification between rounds and the
+ * robust kernel dropped after round 2. */
+
+typedef struct {
+    const pose_problem_t* p;
+    double q[4], t[3];     /* current estimate */
+    double bq[4], bt[3];   /* push() */
+    uint8_t* level;        /* 0 active, 1 outlier */
+    uint8_t* robust;
+    double* err;           /* [n][3] last computed error */
+    double H[36], b[6], x[6];
+    double lambda, ni;
+    int nBad;
+} pose_ctx;
+
+static void pose_compute_error(pose_ctx* c, int e)
+{   /* computeError(): obs - cam_project(v1->estimate().map(Xw)) */
+    const pose_problem_t* p = c->p;
+    const double* X = p->xw + 3 * e;
+    const double* obs = p->obs + 3 * e;
+    double Xc[3];
+    quat_rot(c->q, X, Xc);
+    for (int i = 0; i < 3; i++) Xc[i] += c->t[i];
+    double* er = c->err + 3 * e;
+    if (obs[2] < 0) {   /* EdgeSE3ProjectXYZOnlyPose: project2d then *f + c (all double) */
+        const double u = Xc[0] / Xc[2], v = Xc[1] / Xc[2];
+        er[0] = obs[0] - (u * p->fx + p->cx);
+        er[1] = obs[1] - (v * p->fy + p->cy);
+        er[2] = 0;
+    } else {            /* EdgeStereoSE3ProjectXYZOnlyPose: float invz, double member bf */
+        const float invz = (float)(1.0f / Xc[2]);
+        const double r0 = Xc[0] * invz * p->fx + p->cx;
+        const double r1 = Xc[1] * invz * p->fy + p->cy;
+        const double r2 = r0 - p->bf * invz;
+        er[0] = obs[0] - r0;
+        er[1] = obs[1] - r1;
+        er[2] = obs[2] - r2;
+    }
+}
+
+static double pose_chi2(const pose_ctx* c, int e)
+{
+    const double* er = c->err + 3 * e;
+    const double w = c->p->info[e];
+    double s = er[0] * (w * er[0]) + er[1] * (w * er[1]);
+    if (c->p->obs[3 * e + 2] >= 0) s += er[2] * (w * er[2]);
+    return s;
+}
+
+static double pose_robust_chi2(const pose_ctx* c, int e)
+{
+    double chi = pose_chi2(c, e);
+    if (c->robust[e]) {
+        const double delta = c->p->obs[3 * e + 2] >= 0 ? (double)(float)sqrt(7.815) : (double)(float)sqrt(5.991);
+        const double dsqr = delta * delta;
+        if (chi > dsqr) chi = 2 * sqrt(chi) * delta - dsqr;
+    }
+    return chi;
+}
+
+/* The GPU kernel's fixed reduction order (csrc/pose.hip), restated so that the LM decisions
+ * (rho signs near convergence) agree exactly: thread t of 256 adds the terms of edges t, t + 256,
+ * ... in order; each wave of 64 combines its lanes by an xor butterfly (offsets 32 .. 1) and
+ * keeps lane 0's value; the four waves add as (w0 + w1) + (w2 + w3).  g2o adds the edges in
+ * order — the same sum to rounding. */
+enum { POSE_T = 256 };
+
+static double pose_wave_lane0(double* v)
+{   /* xor butterfly over 64 lanes, lane 0's result */
+    for (int o = 32; o >= 1; o >>= 1) {
+        double nv[64];
+        for (int i = 0; i < 64; i++) nv[i] = v[i] + v[i ^ o];
+        memcpy(v, nv, sizeof(nv));
+    }
+    return v[0];
+}
+
+static double pose_block_sum(double* th /* [256] per-thread partials */)
+{
+    double w[4];
+    for (int k = 0; k < 4; k++) w[k] = pose_wave_lane0(th + 64 * k);
+    return (w[0] + w[1]) + (w[2] + w[3]);
+}
+
+static double pose_active_errors(pose_ctx* c)
+{   /* computeActiveErrors + activeRobustChi2 */
+    double th[POSE_T] = {0};
+    for (int e = 0; e < c->p->n; e++) {
+        if (c->level[e]) continue;
+        pose_compute_error(c, e);
+        th[e % POSE_T] += pose_robust_chi2(c, e);
+    }
+    return pose_block_sum(th);
+}
+
+/* linearizeOplus (types_six_dof_expmap.cpp:285-308, 355-388) + BaseUnaryEdge::constructQuadraticForm;
+ * per-thread partials of the 21 upper H entries and b (GPU order), then per value eight groups of
+ * 32 consecutive threads added in order and combined by an xor butterfly (offsets 1, 2, 4). */
+static void pose_build_system(pose_ctx* c)
+{
+    const pose_problem_t* p = c->p;
+    static double part[27][POSE_T];
+    memset(part, 0, sizeof(part));
+    for (int e = 0; e < p->n; e++) {
+        if (c->level[e]) continue;
+        double* acc = NULL;
+        const int th = e % POSE_T;
+        const double* X = p->xw + 3 * e;
+        double Xc[3];
+        quat_rot(c->q, X, Xc);
+        for (int i = 0; i < 3; i++) Xc[i] += c->t[i];
+        const double x = Xc[0], y = Xc[1], invz = 1.0 / Xc[2], invz_2 = invz * invz;
+        const int st = p->obs[3 * e + 2] >= 0;
+        double J[18] = {0};
+        J[0] = x * y * invz_2 * p->fx;       J[1] = -(1 + (x * x * invz_2)) * p->fx; J[2] = y * invz * p->fx;
+        J[3] = -invz * p->fx;                J[4] = 0;                               J[5] = x * invz_2 * p->fx;
+        J[6] = (1 + y * y * invz_2) * p->fy; J[7] = -x * y * invz_2 * p->fy;         J[8] = -x * invz * p->fy;
+        J[9] = 0;                            J[10] = -invz * p->fy;                  J[11] = y * invz_2 * p->fy;
+        if (st) {
+            J[12] = J[0] - p->bf * y * invz_2; J[13] = J[1] + p->bf * x * invz_2; J[14] = J[2];
+            J[15] = J[3];                      J[16] = 0;                         J[17] = J[5] - p->bf * invz_2;
+        }
+        const double w = p->info[e];
+        const double* er = c->err + 3 * e;
+        double rho1 = 1.0;
+        if (c->robust[e]) {
+            const double chi = pose_chi2(c, e);
+            const double delta = st ? (double)(float)sqrt(7.815) : (double)(float)sqrt(5.991);
+            if (chi > delta * delta) rho1 = delta / sqrt(chi);
+        }
+        const double W = rho1 * w;
+        double om[3];
+        for (int r = 0; r < 3; r++) om[r] = (r < 2 || st) ? -(w * er[r]) * rho1 : 0.0;
+        (void)acc;
+        int o = 0;
+        for (int i = 0; i < 6; i++) {   /* all three rows: a mono edge's third row adds exact zeros */
+            double sb = 0;
+            for (int r = 0; r < 3; r++) sb += J[r * 6 + i] * om[r];
+            part[21 + i][th] += sb;
+            for (int j = i; j < 6; j++) {
+                double h = 0;
+                for (int r = 0; r < 3; r++) h += J[r * 6 + i] * W * J[r * 6 + j];
+                part[o++][th] += h;
+            }
+        }
+    }
+    double res[27];
+    for (int v = 0; v < 27; v++) {
+        double g[8];
+        for (int k = 0; k < 8; k++) {
+            double sg = 0.0;
+            for (int i = 0; i < 32; i++) sg += part[v][32 * k + i];
+            g[k] = sg;
+        }
+        for (int o = 1; o <= 4; o <<= 1) {
+            double ng[8];
+            for (int k = 0; k < 8; k++) ng[k] = g[k] + g[k ^ o];
+            memcpy(g, ng, sizeof(g));
+        }
+        res[v] = g[0];
+    }
+    int o = 0;
+    for (int i = 0; i < 6; i++)
+        for (int j = i; j < 6; j++) {
+            c->H[i * 6 + j] = res[o];
+            c->H[j * 6 + i] = res[o];
+            o++;
+        }
+    for (int i = 0; i < 6; i++) c->b[i] = res[21 + i];
+}
+
+/* H + lambda I = L D L^T (no pivoting), x = (H + lambda I)^-1 b; 0 when a pivot is not positive
+ * (Eigen::LDLT::isPositive) */
+static int pose_solve(pose_ctx* c, double lambda)
+{
+    double A[36], d[6], y[6];
+    memcpy(A, c->H, sizeof(A));
+    for (int i = 0; i < 6; i++) A[i * 7] += lambda;
+    for (int j = 0; j < 6; j++) {
+        double dj = A[j * 6 + j];
+        for (int k = 0; k < j; k++) dj -= A[j * 6 + k] * A[j * 6 + k] * d[k];
+        if (!(dj > 0.0) || !isfinite(dj)) return 0;
+        d[j] = dj;
+        for (int i = j + 1; i < 6; i++) {
+            double v = A[i * 6 + j];
+            for (int k = 0; k < j; k++) v -= A[i * 6 + k] * A[j * 6 + k] * d[k];
+            A[i * 6 + j] = v / dj;
+        }
+    }
+    for (int i = 0; i < 6; i++) {
+        double v = c->b[i];
+        for (int k = 0; k < i; k++) v -= A[i * 6 + k] * y[k];
+        y[i] = v;
+    }
+    for (int i = 5; i >= 0; i--) {
+        double v = y[i] / d[i];
+        for (int k = i + 1; k < 6; k++) v -= A[k * 6 + i] * c->x[k];
+        c->x[i] = v;
+    }
+    return 1;
+}
+
+static int pose_lm_iteration(pose_ctx* c, int iteration, pose_result_t* r)
+{
+    double currentChi = pose_active_errors(c);
+    double tempChi = currentChi;
+    const double iniChi = currentChi;
+    pose_build_system(c);
+    if (iteration == 0) {
+        double m = 0;
+        for (int j = 0; j < 6; j++) m = fmax(fabs(c->H[j * 7]), m);
+        c->lambda = 1e-5 * m;
+        c->ni = 2;
+        c->nBad = 0;
+    }
+    double rho = 0;
+    int qmax = 0;
+    do {
+        memcpy(c->bq, c->q, sizeof(c->q));
+        memcpy(c->bt, c->t, sizeof(c->t));
+        const double lam = c->lambda;
+        const int ok2 = pose_solve(c, lam);
+        if (!ok2) memset(c->x, 0, sizeof(c->x));
+        double qn[4], tn[3];
+        oracle_se3_exp_left(c->x, c->q, c->t, qn, tn);
+        memcpy(c->q, qn, sizeof(qn));
+        memcpy(c->t, tn, sizeof(tn));
+        tempChi = pose_active_errors(c);
+        if (!ok2) tempChi = DBL_MAX;
+        rho = currentChi - tempChi;
+        double scale = 0.;
+        for (int j = 0; j < 6; j++) scale += c->x[j] * (lam * c->x[j] + c->b[j]);
+        scale += 1e-3;
+        rho /= scale;
+        if (rho > 0 && isfinite(tempChi)) {
+            double alpha = 1. - pow((2 * rho - 1), 3);
+            alpha = fmin(alpha, 2. / 3.);
+            c->lambda *= fmax(1. / 3., alpha);
+            c->ni = 2;
+            currentChi = tempChi;
+        } else {
+            c->lambda *= c->ni;
+            c->ni *= 2;
+            memcpy(c->q, c->bq, sizeof(c->q));
+            memcpy(c->t, c->bt, sizeof(c->t));
+        }
+        qmax++;
+        r->trials++;
+    } while (rho < 0 && qmax < 10);
+    if (qmax == 10 || rho == 0) return LM_TERMINATE;
+    if ((iniChi - currentChi) * 1e3 < iniChi) c->nBad++;
+    else c->nBad = 0;
+    if (c->nBad >= 3) return LM_TERMINATE;
+    return LM_OK;
+}
+
+int oracle_pose_optimization(const pose_problem_t* p, pose_result_t* r)
+{
+    const int n = p->n;
+    memcpy(r->pose_q, p->pose_q, sizeof(r->pose_q));
+    memcpy(r->pose_t, p->pose_t, sizeof(r->pose_t));
+    r->trials = 0;
+    for (int i = 0; i < 4; i++) r->iterations[i] = 0;
+    for (int e = 0; e < n; e++) r->outlier[e] = 0;
+    r->n_inliers = 0;
+    if (n < 3) return 0;   /* nInitialCorrespondences < 3: return 0, pose untouched */
+    pose_ctx c;
+    memset(&c, 0, sizeof(c));
+    c.p = p;
+    c.level = (uint8_t*)calloc(n, 1);
+    c.robust = (uint8_t*)malloc(n);
+    c.err = (double*)calloc(3 * (size_t)n, sizeof(double));
+    memset(c.robust, 1, n);
+    const double chi2Mono = 5.991, chi2Stereo = 7.815;
+    int nBad = 0;
+    for (int it = 0; it < 4; it++) {
+        memcpy(c.q, p->pose_q, sizeof(c.q));   /* vSE3->setEstimate(toSE3Quat(pFrame->mTcw)) */
+        memcpy(c.t, p->pose_t, sizeof(c.t));
+        int nact = 0;
+        for (int e = 0; e < n; e++) nact += c.level[e] == 0;
+        if (nact > 0) {   /* an empty level-0 graph has no vertex to optimise (optimize returns -1) */
+            int ok = 1;
+            for (int i = 0; i < 10 && ok; i++) {
+                ok = pose_lm_iteration(&c, i, r) == LM_OK;
+                r->iterations[it]++;
+            }
+        }
+        nBad = 0;
+        for (int e = 0; e < n; e++) {
+            if (c.level[e]) pose_compute_error(&c, e);
+            const double chi2 = pose_chi2(&c, e);
+            const double thr = p->obs[3 * e + 2] >= 0 ? chi2Stereo : chi2Mono;
+            if ((float)chi2 > (float)thr) {   /* const float chi2 = e->chi2(); chi2 > chi2Mono[it] */
+                r->outlier[e] = 1;
+                c.level[e] = 1;
+                nBad++;
+            } else {
+                r->outlier[e] = 0;
+                c.level[e] = 0;
+            }
+            if (it == 2) c.robust[e] = 0;
+        }
+        if (n < 10) break;   /* optimizer.edges().size() counts every edge of the graph */
+    }
+    memcpy(r->pose_q, c.q, sizeof(c.q));
+    memcpy(r->pose_t, c.t, sizeof(c.t));
+    r->n_inliers = n - nBad;
+    free(c.level);
+    free(c.robust);
+    free(c.err);
+    return 0;
+}

@@ -73,6 +73,29 @@ typedef void (*oracle_allreduce_fn)(void* user, double* v, int n, int op);
 int oracle_lba_solve_dist(const lba_problem_t* p, const lba_options_t* o, const volatile uint8_t* stop,
                           lba_result_t* r, int rank, int world, oracle_allreduce_fn ar, void* user);
 
+/* Optimizer::PoseOptimization(Frame*) (R/src/Optimizer.cpp:306-535) on one frame: the edges are
+ * the frame's keypoints with a map point, obs = (u, v, ur) with ur < 0 for a monocular
+ * observation (Frame::mvuRight), xw the map point (float values), info = invSigma2 of the
+ * keypoint octave. */
+typedef struct {
+    double pose_q[4], pose_t[3];   /* Converter::toSE3Quat(pFrame->mTcw) */
+    int n;
+    const double* obs;             /* [n][3] */
+    const double* xw;              /* [n][3] */
+    const double* info;            /* [n] */
+    double fx, fy, cx, cy, bf;
+} pose_problem_t;
+
+typedef struct {
+    double pose_q[4], pose_t[3];   /* optimised pose (input pose when n < 3) */
+    uint8_t* outlier;              /* [n] Frame::mvbOutlier */
+    int n_inliers;                 /* return value: nInitialCorrespondences - nBad */
+    int iterations[4];             /* LM iterations per round */
+    int trials;
+} pose_result_t;
+
+int oracle_pose_optimization(const pose_problem_t* p, pose_result_t* r);
+
 /* Helpers shared with tests: Converter::toSE3Quat / SE3Quat::exp semantics. */
 void oracle_quat_from_matrix(const double R[9], double q[4]);
 void oracle_se3_exp_left(const double upd[6], const double q[4], const double t[3], double qo[4], double to[3]);

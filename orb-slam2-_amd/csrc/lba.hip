@@ -34,6 +34,7 @@
 
 #include "common.h"
 #include "lba_host.h"
+#include "lm_common.h"
 #include "se3.h"
 
 #ifdef ORB_TIMING   // instrumented variant (tools/build_variant.py)
@@ -562,7 +563,10 @@ __device__ __forceinline__ bool ldlt_panel(double* __restrict__ A, int ld, int n
             *(st ? A + (size_t)j * ld + r : dummy + lane) = w[u];   // W(r, j)
             *(st ? A + (size_t)r * ld + j : dummy + lane) = l[u];   // L(r, j)
         }
-        if (lane == 0) { dg[j] = dj; rdg[j] = rd; }
+        // (lane 0 stores d_j, 1/d_j; the others write their sink: no branch in the column loop,
+        // which keeps it one basic block for the scheduler)
+        *(lane == 0 ? dg + j : dummy + lane) = dj;
+        *(lane == 0 ? rdg + j : dummy + lane) = rd;
         double wk[kNB];
         const double* Wrow = A + (size_t)j * ld + jb;
 #pragma unroll
@@ -575,6 +579,9 @@ __device__ __forceinline__ bool ldlt_panel(double* __restrict__ A, int ld, int n
             djn = shfl_d(P[0][c + 1], c + 1);
             r0 = __builtin_amdgcn_rcp(djn);
         }
+        // sched_barrier: without it the scheduler sinks every update to just before its column
+        // becomes the pivot, turning the right-looking step into a dependent fma chain there
+        __builtin_amdgcn_sched_barrier(0);
         // the deferred updates, in three groups between the reciprocal's steps
         const int nk = kNB - 2 - c > 0 ? kNB - 2 - c : 0;   // folded: the loop is unrolled
         const int g1 = c + 2 + (nk + 2) / 3, g2 = c + 2 + 2 * (nk + 2) / 3;
@@ -586,15 +593,18 @@ __device__ __forceinline__ bool ldlt_panel(double* __restrict__ A, int ld, int n
 #pragma unroll
         for (int u = 0; u < NS; u++)
             if (lane + 64 * u > c) Y[u] = __builtin_fma(-l[u], yj, Y[u]);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int k = g1; k < kNB && k < g2; k++)
 #pragma unroll
             for (int u = 0; u < NS; u++) P[u][k] = __builtin_fma(-l[u], wk[k], P[u][k]);
         if (c + 1 < kNB) { e1 = __builtin_fma(-djn, r1, 1.0); r1 = __builtin_fma(r1, e1, r1); }
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int k = g2; k < kNB; k++)
 #pragma unroll
             for (int u = 0; u < NS; u++) P[u][k] = __builtin_fma(-l[u], wk[k], P[u][k]);
+        __builtin_amdgcn_sched_barrier(0);
         if (c + 1 < kNB) {
             ok = ok && djn != 0.0 && isfinite(djn);
             dj = djn;
@@ -941,13 +951,6 @@ __global__ __launch_bounds__(256) void k_unpack(double* __restrict__ buf, const 
     for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) buf[i] = ws[i];
 }
 
-// t^3 rounded once (double-double product): the host path used std::pow(t, 3), which glibc
-// rounds correctly except in vanishingly rare cases.
-__device__ __forceinline__ double cube_rn(double t) {
-    const double p = t * t, ep = __builtin_fma(t, t, -p);
-    const double q = p * t, eq = __builtin_fma(p, t, -q);
-    return q + __builtin_fma(ep, t, eq);
-}
 
 // Start of an LM iteration (G/core/optimization_algorithm_levenberg.cpp:61-90): currentChi
 // from the linearisation's robust chi2 (red[0]), lambda from computeLambdaInit (red[1]) at it 0.

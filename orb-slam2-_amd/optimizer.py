@@ -1,5 +1,6 @@
 """Host mirror of ORB_SLAM2::Optimizer::LocalBundleAdjustment
-(R/include/Optimizer.h:45, R/src/Optimizer.cpp:564-918) over the HIP C-ABI.
+(R/include/Optimizer.h:45, R/src/Optimizer.cpp:564-918) and Optimizer::PoseOptimization
+(R/include/Optimizer.h:44, R/src/Optimizer.cpp:306-535) over the HIP C-ABI.
 
 The graph-gathering part of the reference (local / fixed keyframes, local map
 points, edge construction, R :569-782) is host bookkeeping on Map/KeyFrame/
@@ -165,6 +166,11 @@ class Optimizer:
     _ctx = {}
 
     @staticmethod
+    def PoseOptimization(frames, device=0):
+        """Batched Optimizer::PoseOptimization (see the module-level PoseOptimization)."""
+        return PoseOptimization(frames, device)
+
+    @staticmethod
     def LocalBundleAdjustment(problem, pbStopFlag=None, device=0, opts=None):
         ctx = Optimizer._ctx.get(device)
         if ctx is None:
@@ -179,3 +185,60 @@ def apply_results(problem, result):
              for e in np.nonzero(result["edge_erase"])[0]]
     Tcw = np.stack([pose_to_Tcw(q, t) for q, t in zip(result["pose_q"], result["pose_t"])])
     return erase, Tcw, result["point_xyz"].astype(np.float32)
+
+
+class PoseBatch(C.Structure):
+    _fields_ = [("n_frames", C.c_int), ("n_edges", C.c_int), ("pose_q", C.c_void_p), ("pose_t", C.c_void_p),
+                ("cam", C.c_void_p), ("edge_start", C.c_void_p), ("edge_obs", C.c_void_p), ("edge_xw", C.c_void_p),
+                ("edge_info", C.c_void_p)]
+
+
+class PoseBatchResult(C.Structure):
+    _fields_ = [("pose_q", C.c_void_p), ("pose_t", C.c_void_p), ("outlier", C.c_void_p), ("n_inliers", C.c_void_p)]
+
+
+def _pose_sig():
+    lib = _abi.lib()
+    if not getattr(lib, "_pose_sig", False):
+        lib.pose_optimize_batch.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        lib.pose_optimize_batch.restype = C.c_int
+        lib.pose_optimize_batch_device.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                   C.c_void_p]
+        lib.pose_optimize_batch_device.restype = C.c_int
+        lib._pose_sig = True
+    return lib
+
+
+def pack_pose_frames(frames):
+    """Frame dicts (synth.pose_problems layout: Tcw float 4x4, obs [n,3] with ur < 0 for mono,
+    xw [n,3], info [n], cam (fx, fy, cx, cy, bf)) -> the flat arrays of pose_batch."""
+    B = len(frames)
+    Tcw = np.ascontiguousarray(np.stack([f["Tcw"] for f in frames]).astype(np.float32))
+    q, t = np.zeros((B, 4)), np.zeros((B, 3))
+    _sig().lba_poses_from_Tcw(_abi.ptr(Tcw), B, _abi.ptr(q), _abi.ptr(t))   # Converter::toSE3Quat
+    counts = [len(f["info"]) for f in frames]
+    start = np.zeros(B + 1, np.int32)
+    start[1:] = np.cumsum(counts)
+    cat = (lambda k: np.ascontiguousarray(np.concatenate([np.asarray(f[k], np.float64) for f in frames]))
+           if B else np.zeros(0))
+    return dict(pose_q=q, pose_t=t, cam=np.ascontiguousarray(np.array([f["cam"] for f in frames], np.float64)),
+                edge_start=start, edge_obs=cat("obs").reshape(-1, 3), edge_xw=cat("xw").reshape(-1, 3),
+                edge_info=cat("info"))
+
+
+def PoseOptimization(frames, device=0):
+    """ORB_SLAM2::Optimizer::PoseOptimization(Frame*) (R/src/Optimizer.cpp:306-535) over a batch
+    of frames on the GPU.  Returns per frame the optimised pose (q, t as SE3Quat), mvbOutlier and
+    the return value (nInitialCorrespondences - nBad), plus LM iterations per round / trials."""
+    a = pack_pose_frames(frames)
+    B, E = len(frames), int(a["edge_start"][-1])
+    pb = PoseBatch(B, E, _abi.ptr(a["pose_q"]), _abi.ptr(a["pose_t"]), _abi.ptr(a["cam"]), _abi.ptr(a["edge_start"]),
+                   _abi.ptr(a["edge_obs"]), _abi.ptr(a["edge_xw"]), _abi.ptr(a["edge_info"]))
+    q, t = np.zeros((B, 4)), np.zeros((B, 3))
+    outl, ninl, iters = np.zeros(E, np.uint8), np.zeros(B, np.int32), np.zeros((B, 5), np.int32)
+    r = PoseBatchResult(_abi.ptr(q), _abi.ptr(t), _abi.ptr(outl), _abi.ptr(ninl))
+    _abi.check("pose_optimize_batch", _pose_sig().pose_optimize_batch(device, C.byref(pb), C.byref(r),
+                                                                        _abi.ptr(iters)))
+    s = a["edge_start"]
+    return [dict(pose_q=q[b], pose_t=t[b], outlier=outl[s[b]:s[b + 1]], n_inliers=int(ninl[b]),
+                 iterations=tuple(int(x) for x in iters[b, :4]), trials=int(iters[b, 4])) for b in range(B)]

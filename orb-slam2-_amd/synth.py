@@ -172,3 +172,48 @@ def ba_problem(seed=42, n_local=20, n_fixed=4, n_points=3000, stereo_frac=0.0, W
         "edge_info": inv_sigma2[np.array(e_oct)].astype(np.float64), "edge_cam": cam,
         "edge_octave": np.array(e_oct, np.int32),
     }
+
+
+def pose_problems(n_frames=8, seed=5, n_points=600, stereo_frac=0.0, outlier_frac=0.1, W=640, H=480,
+                  rot_noise=0.01, trans_noise=0.02):
+    """Synthetic Optimizer::PoseOptimization inputs (Tracking's motion-model / local-map step):
+    per frame a true camera, n_points map points (float world positions) in view, keypoint
+    observations = projection + N(0, 1.2^octave) px with octave ~ U{0..7}, outlier_frac of them
+    displaced by +20 px, stereo_frac of them with a right coordinate ur = u - bf/z (+ noise),
+    the others monocular (ur = -1, Frame::mvuRight); the initial pose (pFrame->mTcw, float) is
+    the true one perturbed by rot_noise rad / trans_noise m.  TUM1 intrinsics, KITTI bf."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    fx, fy, cx, cy = TUM1
+    inv_sigma2 = (np.float32(1.0) / np.array([np.float32(1.2) ** (2 * l) for l in range(8)], np.float32))
+    frames = []
+    for f in range(n_frames):
+        R = _rot(rng.normal(0, 0.3, 3))
+        t = rng.normal(0, 0.5, 3)
+        X, obs, oct_ = [], [], []
+        while len(X) < n_points:
+            u, v = rng.uniform(0, W), rng.uniform(0, H)
+            z = rng.uniform(1.0, 8.0)
+            Xc = np.array([(u - cx) / fx * z, (v - cy) / fy * z, z])
+            Xw = R.T @ (Xc - t)
+            Xw32 = Xw.astype(np.float32).astype(np.float64)
+            Xc2 = R @ Xw32 + t
+            uu, vv = fx * Xc2[0] / Xc2[2] + cx, fy * Xc2[1] / Xc2[2] + cy
+            lvl = int(rng.integers(0, 8))
+            sig = 1.2 ** lvl
+            uo, vo = uu + rng.normal(0, sig), vv + rng.normal(0, sig)
+            if rng.random() < outlier_frac:
+                uo += 20.0
+            ur = uo - KITTI_BF / Xc2[2] + rng.normal(0, sig) if rng.random() < stereo_frac else -1.0
+            X.append(Xw32)
+            obs.append([np.float32(uo), np.float32(vo), np.float32(ur)])
+            oct_.append(lvl)
+        Rp = _rot(rng.normal(0, rot_noise / np.sqrt(3), 3)) @ R
+        tp = t + rng.normal(0, trans_noise / np.sqrt(3), 3)
+        T = np.eye(4, dtype=np.float32)
+        T[:3, :3] = Rp
+        T[:3, 3] = tp
+        frames.append({"Tcw": T, "obs": np.array(obs, np.float64), "xw": np.array(X, np.float64),
+                       "info": inv_sigma2[np.array(oct_)].astype(np.float64),
+                       "cam": (fx, fy, cx, cy, float(np.float32(KITTI_BF))),
+                       "true_R": R, "true_t": t})
+    return frames

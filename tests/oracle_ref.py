@@ -291,3 +291,31 @@ def lba_solve(prob, options=None, stop=False):
     out["trace"] = out["trace"][: r.n_trace]
     out["init_q"], out["init_t"] = keep["q"], keep["t"]
     return out
+
+
+class PoseProblem(C.Structure):
+    _fields_ = [("pose_q", C.c_double * 4), ("pose_t", C.c_double * 3), ("n", C.c_int), ("obs", C.c_void_p),
+                ("xw", C.c_void_p), ("info", C.c_void_p), ("fx", C.c_double), ("fy", C.c_double),
+                ("cx", C.c_double), ("cy", C.c_double), ("bf", C.c_double)]
+
+
+class PoseResult(C.Structure):
+    _fields_ = [("pose_q", C.c_double * 4), ("pose_t", C.c_double * 3), ("outlier", C.c_void_p),
+                ("n_inliers", C.c_int), ("iterations", C.c_int * 4), ("trials", C.c_int)]
+
+
+def pose_optimization(frame):
+    """oracle_pose_optimization on one frame of synth.pose_problems: the optimised pose, the
+    mvbOutlier flags, the return value and per-round LM iterations."""
+    q, t = quat_from_Tcw(frame["Tcw"])
+    obs = np.ascontiguousarray(frame["obs"], np.float64)
+    xw = np.ascontiguousarray(frame["xw"], np.float64)
+    info = np.ascontiguousarray(frame["info"], np.float64)
+    n = len(info)
+    pr = PoseProblem((C.c_double * 4)(*q), (C.c_double * 3)(*t), n, P(obs), P(xw), P(info), *frame["cam"])
+    out = np.zeros(n, np.uint8)
+    r = PoseResult()
+    r.outlier = P(out)
+    lib().oracle_pose_optimization(C.byref(pr), C.byref(r))
+    return dict(pose_q=np.array(r.pose_q[:]), pose_t=np.array(r.pose_t[:]), outlier=out, n_inliers=r.n_inliers,
+                iterations=tuple(r.iterations), trials=r.trials)

@@ -12,7 +12,7 @@ HEADER = ROOT / "include" / "orbslam2_amd.h"
 
 def declared():
     text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
-    return sorted(set(re.findall(r"\b(orb_[a-z0-9_]+|lba_[a-z0-9_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(orb_[a-z0-9_]+|lba_[a-z0-9_]+|pose_[a-z0-9_]+)\s*\(", text)))
 
 
 def test_header_declares_entry_points():
