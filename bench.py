@@ -353,6 +353,62 @@ def bench_extras(args, amd, dev):
                              "keypoints_per_frame": float(b["cnt"].float().mean()),
                              "matches_per_pair": float(nm.float().mean())}
     out["batch_sweep_640x480"] = batch_sweep(amd, dev, m)
+    out["pose_optimization"] = bench_pose(args, amd, dev)
+    return out
+
+
+def bench_pose(args, amd, dev, n_frames=256, n_points=600):
+    """SURVEY §8f-2: Optimizer::PoseOptimization over a batch of synthetic frames (600 matched
+    map points each, 10 % displaced, 30 % stereo), inputs resident in HBM, one workgroup per
+    frame; against the oracle (C restatement of the reference, 1 thread per frame, 16 threads)."""
+    from orb_slam2_amd import synth, _abi, optimizer as opt
+    frames = synth.pose_problems(n_frames=n_frames, n_points=n_points, stereo_frac=0.3, seed=21)
+    a = opt.pack_pose_frames(frames)
+    B, E = n_frames, int(a["edge_start"][-1])
+    T = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in a.items()}
+    pq = torch.zeros((B, 4), dtype=torch.float64, device=dev)
+    pt = torch.zeros((B, 3), dtype=torch.float64, device=dev)
+    outl = torch.zeros(E, dtype=torch.uint8, device=dev)
+    ninl = torch.zeros(B, dtype=torch.int32, device=dev)
+    work = torch.zeros(3 * E, dtype=torch.float64, device=dev)
+    flags = torch.zeros(2 * E, dtype=torch.uint8, device=dev)
+    iters = torch.zeros((B, 5), dtype=torch.int32, device=dev)
+    dp = lambda x: C.c_void_p(x.data_ptr())   # noqa: E731
+    pb = opt.PoseBatch(B, E, dp(T["pose_q"]), dp(T["pose_t"]), dp(T["cam"]), dp(T["edge_start"]), dp(T["edge_obs"]),
+                       dp(T["edge_xw"]), dp(T["edge_info"]))
+    pr = opt.PoseBatchResult(dp(pq), dp(pt), dp(outl), dp(ninl))
+    lib = opt._pose_sig()
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def run():
+        _abi.check("pose", lib.pose_optimize_batch_device(C.byref(pb), C.byref(pr), dp(work), dp(flags), dp(iters),
+                                                          C.c_void_p(stream)))
+    for _ in range(2):
+        run()
+    torch.cuda.synchronize(dev)
+    reps = 10
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        run()
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) / reps
+    it = iters.cpu().numpy()
+    out = {"frames_per_s": round(B / dt, 1), "ms_per_batch": round(dt * 1e3, 4), "frames_per_batch": B,
+           "edges_per_frame": n_points, "lm_iterations_per_frame": float(it[:, :4].sum(1).mean()),
+           "trials_per_frame": float(it[:, 4].mean()),
+           "inliers_per_frame": float(ninl.float().mean())}
+    if not args.no_cpu:
+        sys.path.insert(0, str(ROOT / "tests"))
+        import oracle_ref as O
+        sample = frames[:64]
+        threads = max(1, min(16, os.cpu_count() or 1))
+        t0 = time.perf_counter()
+        with cf.ThreadPoolExecutor(threads) as ex:
+            list(ex.map(O.pose_optimization, sample))
+        dc = time.perf_counter() - t0
+        out["cpu_baseline"] = {"frames_per_s": round(len(sample) / dc, 1), "cores": threads, "kind": "port",
+                               "sample": f"{len(sample)} frames, oracle C restatement of PoseOptimization, "
+                                         f"1 frame per thread"}
     return out
 
 

@@ -846,7 +846,7 @@ static double pose_active_errors(pose_ctx* c)
 static void pose_build_system(pose_ctx* c)
 {
     const pose_problem_t* p = c->p;
-    static double part[27][POSE_T];
+    double part[27][POSE_T];   /* 55 KB on the stack: the oracle runs one frame per thread in bench.py */
     memset(part, 0, sizeof(part));
     for (int e = 0; e < p->n; e++) {
         if (c->level[e]) continue;
