@@ -164,6 +164,17 @@ typedef struct {
 /* ORBmatcher::DescriptorDistance — R/src/ORBmatcher.cpp:1901-1917 (host inline helper). */
 int orb_descriptor_distance(const uint8_t* a, const uint8_t* b);
 
+/* MapPoint::ComputeDistinctiveDescriptors (R/src/MapPoint.cpp:306-385) for n_points map points:
+ * point m's descriptors (one per observation by a non-bad keyframe, in mObservations order) are
+ * rows [start[m], start[m+1]) of desc (32 B each).  best_idx[m] = index within the point's list
+ * of the descriptor with the least median distance to the others (the new mDescriptor), -1 for
+ * an empty list; best_desc (optional, [n_points][32]) receives that row.  Host buffers. */
+int orb_distinctive_descriptors(int device, const uint8_t* desc, const int32_t* start, int n_points, int32_t* best_idx,
+                                uint8_t* best_desc);
+/* Device-resident form (asynchronous on `stream`); start is relative to d_desc. */
+int orb_distinctive_descriptors_device(const uint8_t* d_desc, const int32_t* d_start, int n_points,
+                                       int32_t* d_best_idx, uint8_t* d_best_desc, void* stream);
+
 /* ORBmatcher::SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12,
  * windowSize) — R/src/ORBmatcher.cpp:499-617.  prev_xy (2*F1.n floats) is
  * updated in place; matches12 (F1.n ints) receives the F2 index or -1.

@@ -1279,3 +1279,40 @@ long oracle_sincosf_check(unsigned stride, long* n_checked)
     if (n_checked) *n_checked = n;
     return bad;
 }
+
+/* MapPoint::ComputeDistinctiveDescriptors (R/src/MapPoint.cpp:306-385), literally: the N x N
+ * distance table, each row sorted, its element 0.5 * (N - 1) (truncated) as the median, the
+ * least median winning with strict <.  Returns the index, -1 for N = 0. */
+static int cmp_int(const void* a, const void* b)
+{
+    const int x = *(const int*)a, y = *(const int*)b;
+    return (x > y) - (x < y);
+}
+
+int oracle_distinctive_descriptor(const uint8_t* desc, int N)
+{
+    if (N <= 0) return -1;
+    int* dist = (int*)malloc(sizeof(int) * (size_t)N * N);
+    int* row = (int*)malloc(sizeof(int) * (size_t)N);
+    for (int i = 0; i < N; i++) {
+        dist[(size_t)i * N + i] = 0;
+        for (int j = i + 1; j < N; j++) {
+            const int d = oracle_descriptor_distance(desc + (size_t)i * 32, desc + (size_t)j * 32);
+            dist[(size_t)i * N + j] = d;
+            dist[(size_t)j * N + i] = d;
+        }
+    }
+    int best = INT_MAX, bestIdx = 0;
+    for (int i = 0; i < N; i++) {
+        memcpy(row, dist + (size_t)i * N, sizeof(int) * (size_t)N);
+        qsort(row, N, sizeof(int), cmp_int);
+        const int median = row[(size_t)(0.5 * (N - 1))];
+        if (median < best) {
+            best = median;
+            bestIdx = i;
+        }
+    }
+    free(dist);
+    free(row);
+    return bestIdx;
+}

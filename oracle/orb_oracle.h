@@ -164,6 +164,10 @@ int oracle_compute_stereo_matches(const uint8_t* const* pyr_l, const uint8_t* co
 void oracle_hamming_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt,
                          int32_t* best_idx, int32_t* best_d, int32_t* second_d);
 
+/* MapPoint::ComputeDistinctiveDescriptors on one point's N observed descriptors: the index of
+ * the descriptor with the least median distance (-1 for N = 0). */
+int oracle_distinctive_descriptor(const uint8_t* desc, int N);
+
 #ifdef __cplusplus
 }
 #endif

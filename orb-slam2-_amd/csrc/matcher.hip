@@ -1077,6 +1077,56 @@ static void pack_view(const orb_frame_view* f, orb_keypoint* k) {
     }
 }
 
+// ------------------------------------------------------------------ distinctive descriptors
+// MapPoint::ComputeDistinctiveDescriptors (R/src/MapPoint.cpp:306-385) for a batch of map
+// points: point m's observed descriptors are rows [start[m], start[m+1]) (observation order,
+// bad keyframes already left out).  One 64-lane workgroup per point: the descriptors are staged
+// in LDS (up to kDdLds rows, else read from HBM), lane i takes rows i, i + 64, ... and finds the
+// row's median distance — vDists[0.5 * (N - 1)] of the sorted row, self distance 0 included —
+// as the smallest v with #{j : d(i, j) <= v} > (N - 1) / 2, by binary search over 0..256; the
+// least median wins, ties to the lower index (strict <).  best_idx[m] = -1 for an empty list.
+constexpr int kDdLds = 1024;
+__global__ __launch_bounds__(64) void k_distinctive(const uint8_t* __restrict__ desc, const int32_t* __restrict__ start,
+                                                    int32_t* __restrict__ best_idx, uint8_t* __restrict__ best_desc) {
+    __shared__ uint4 sd[kDdLds * 2];
+    const int m = blockIdx.x, lane = threadIdx.x;
+    const int s0 = start[m], N = start[m + 1] - s0;
+    const uint4* g = reinterpret_cast<const uint4*>(desc + (size_t)s0 * 32);
+    const bool lds = N <= kDdLds;
+    if (lds)
+        for (int t = lane; t < 2 * N; t += 64) sd[t] = g[t];
+    __syncthreads();
+    const uint4* D = lds ? sd : g;
+    const int k = (int)(0.5 * (N - 1));   // size_t(0.5 * (N - 1)) in the reference's vDists index
+    int best = INT_MAX, bi = 0x7fffffff;
+    for (int i = lane; i < N; i += 64) {
+        const uint4 a0 = D[2 * i], a1 = D[2 * i + 1];
+        int lo = 0, hi = 256;   // smallest v with count(d <= v) >= k + 1
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            int cnt = 0;
+            for (int j = 0; j < N; j++) {
+                const uint4 b0 = D[2 * j], b1 = D[2 * j + 1];
+                const int dd = __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+                               __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+                cnt += dd <= mid;
+            }
+            if (cnt >= k + 1) hi = mid;
+            else lo = mid + 1;
+        }
+        if (lo < best) { best = lo; bi = i; }
+    }
+    // lexicographic (median, index) minimum over the wave
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const int ob = __shfl_xor(best, o, 64), oi = __shfl_xor(bi, o, 64);
+        if (ob < best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    }
+    if (lane == 0) best_idx[m] = N > 0 ? bi : -1;
+    if (best_desc && N > 0 && lane < 2)
+        reinterpret_cast<uint4*>(best_desc + (size_t)m * 32)[lane] = g[2 * bi + lane];
+}
+
 extern "C" {
 
 int orb_descriptor_distance(const uint8_t* a, const uint8_t* b) {
@@ -1416,6 +1466,53 @@ int orb_hamming_knn2_batch_device(orb_matcher* m, const uint8_t* d_q, const int3
                        t_stride_rows, d_best_idx, d_best_d, d_second_d);
     ORB_HIP_TRY(hipGetLastError());
     return ORB_OK;
+}
+
+// MapPoint::ComputeDistinctiveDescriptors over a batch (device-resident, asynchronous).
+int orb_distinctive_descriptors_device(const uint8_t* d_desc, const int32_t* d_start, int n_points,
+                                       int32_t* d_best_idx, uint8_t* d_best_desc, void* stream) {
+    if (n_points < 0 || (n_points > 0 && (!d_desc || !d_start || !d_best_idx))) return ORB_EINVAL;
+    if (n_points == 0) return ORB_OK;
+    hipLaunchKernelGGL(k_distinctive, dim3(n_points), dim3(64), 0, (hipStream_t)stream, d_desc, d_start, d_best_idx,
+                       d_best_desc);
+    ORB_HIP_TRY(hipGetLastError());
+    return ORB_OK;
+}
+
+int orb_distinctive_descriptors(int device, const uint8_t* desc, const int32_t* start, int n_points, int32_t* best_idx,
+                                uint8_t* best_desc) {
+    if (n_points < 0 || (n_points > 0 && (!desc || !start || !best_idx))) return ORB_EINVAL;
+    int st = check_device(device);
+    if (st) return st;
+    if (n_points == 0) return ORB_OK;
+    for (int m = 0; m < n_points; m++)
+        if (start[m + 1] < start[m]) return ORB_EINVAL;
+    ORB_HIP_TRY(hipSetDevice(device));
+    const size_t T = (size_t)start[n_points] - (size_t)start[0];
+    char* base = nullptr;
+    const size_t bD = ((T * 32 + 255) & ~(size_t)255), bS = (((size_t)n_points + 1) * 4 + 255) & ~(size_t)255,
+                 bI = ((size_t)n_points * 4 + 255) & ~(size_t)255;
+    ORB_HIP_TRY(hipMalloc(&base, bD + bS + bI + (size_t)n_points * 32 + 256));
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) { (void)hipFree(base); return ORB_EGPU; }
+    uint8_t* dD = (uint8_t*)base;
+    int32_t* dS = (int32_t*)(base + bD);
+    int32_t* dI = (int32_t*)(base + bD + bS);
+    uint8_t* dB = (uint8_t*)(base + bD + bS + bI);
+    std::vector<int32_t> rel((size_t)n_points + 1);
+    for (int m = 0; m <= n_points; m++) rel[m] = start[m] - start[0];
+    int rc = ORB_OK;
+    if (T) (void)hipMemcpyAsync(dD, desc + (size_t)start[0] * 32, T * 32, hipMemcpyHostToDevice, s);
+    (void)hipMemcpyAsync(dS, rel.data(), rel.size() * 4, hipMemcpyHostToDevice, s);
+    rc = orb_distinctive_descriptors_device(dD, dS, n_points, dI, best_desc ? dB : nullptr, s);
+    if (rc == ORB_OK) {
+        (void)hipMemcpyAsync(best_idx, dI, (size_t)n_points * 4, hipMemcpyDeviceToHost, s);
+        if (best_desc) (void)hipMemcpyAsync(best_desc, dB, (size_t)n_points * 32, hipMemcpyDeviceToHost, s);
+        if (hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
+    }
+    (void)hipStreamDestroy(s);
+    (void)hipFree(base);
+    return rc;
 }
 
 }  // extern "C"

@@ -156,3 +156,23 @@ class ORBmatcher:
         _abi.check("orb_hamming_knn2", _abi.lib().orb_hamming_knn2(
             self._h, _abi.ptr(q), len(q), _abi.ptr(t), len(t), _abi.ptr(bi), _abi.ptr(bd), _abi.ptr(sd)))
         return bi, bd, sd
+
+
+def ComputeDistinctiveDescriptors(descriptor_lists, device=0):
+    """MapPoint::ComputeDistinctiveDescriptors (R/src/MapPoint.cpp:306-385) for a batch of map
+    points on the GPU.  descriptor_lists: per map point an (N, 32) uint8 array of its observed
+    descriptors (mObservations order, non-bad keyframes).  Returns (best index per point, -1 for
+    an empty list; the chosen 32-byte descriptors, (M, 32))."""
+    lists = [np.ascontiguousarray(np.asarray(d, np.uint8).reshape(-1, 32)) for d in descriptor_lists]
+    M = len(lists)
+    start = np.zeros(M + 1, np.int32)
+    start[1:] = np.cumsum([len(d) for d in lists])
+    desc = np.ascontiguousarray(np.concatenate(lists) if M and start[-1] else np.zeros((0, 32), np.uint8))
+    best = np.zeros(M, np.int32)
+    out = np.zeros((M, 32), np.uint8)
+    lib = _abi.lib()
+    lib.orb_distinctive_descriptors.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+    lib.orb_distinctive_descriptors.restype = C.c_int
+    _abi.check("orb_distinctive_descriptors",
+               lib.orb_distinctive_descriptors(device, _abi.ptr(desc), _abi.ptr(start), M, _abi.ptr(best), _abi.ptr(out)))
+    return best, out

@@ -319,3 +319,9 @@ def pose_optimization(frame):
     lib().oracle_pose_optimization(C.byref(pr), C.byref(r))
     return dict(pose_q=np.array(r.pose_q[:]), pose_t=np.array(r.pose_t[:]), outlier=out, n_inliers=r.n_inliers,
                 iterations=tuple(r.iterations), trials=r.trials)
+
+
+def distinctive_descriptor(desc):
+    """oracle_distinctive_descriptor on one point's (N, 32) descriptor list."""
+    d = np.ascontiguousarray(np.asarray(desc, np.uint8).reshape(-1, 32))
+    return int(lib().oracle_distinctive_descriptor(P(d), len(d)))
