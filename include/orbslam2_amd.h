@@ -164,6 +164,31 @@ typedef struct {
 /* ORBmatcher::DescriptorDistance — R/src/ORBmatcher.cpp:1901-1917 (host inline helper). */
 int orb_descriptor_distance(const uint8_t* a, const uint8_t* b);
 
+/* Keyframe geometry read by ORBmatcher::Fuse: rows 0..2 of GetPose(), GetCameraCenter(), fx, fy,
+ * cx, cy, mbf, mfLogScaleFactor, mnScaleLevels, mvScaleFactors, mvInvLevelSigma2. */
+typedef struct {
+    float Tcw[12];
+    float Ow[3];
+    float fx, fy, cx, cy, bf;
+    float log_scale_factor;
+    int n_levels;
+    const float* scale_factors;
+    const float* inv_level_sigma2;
+} orb_kf_params;
+
+/* ORBmatcher::Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, float th) — the matching
+ * step of R/src/ORBmatcher.cpp:995-1121 for every map point of the vector:
+ *   kf = the keyframe as a frame view (mvKeysUn, mDescriptors, mvuRight, grid bounds);
+ *   mp_valid[i] = pMP && !pMP->isBad() && !pMP->IsInKeyFrame(pKF); mp_xyz / mp_normal =
+ *   GetWorldPos / GetNormal; mp_min_dist / mp_max_dist = mfMinDistance / mfMaxDistance;
+ *   mp_desc = GetDescriptor().
+ * best_idx[i] = the keyframe keypoint the point fuses into (-1: none within TH_LOW) and
+ * best_dist[i] its distance (256: no candidate).  The replace / add resolution (:1123-1150)
+ * mutates the map and stays with the caller, in vector order.  Host buffers. */
+int orb_fuse(int device, const orb_frame_view* kf, const orb_kf_params* kp, int n_mp, const uint8_t* mp_valid,
+             const float* mp_xyz, const float* mp_normal, const float* mp_min_dist, const float* mp_max_dist,
+             const uint8_t* mp_desc, float th, int32_t* best_idx, int32_t* best_dist);
+
 /* MapPoint::ComputeDistinctiveDescriptors (R/src/MapPoint.cpp:306-385) for n_points map points:
  * point m's descriptors (one per observation by a non-bad keyframe, in mObservations order) are
  * rows [start[m], start[m+1]) of desc (32 B each).  best_idx[m] = index within the point's list

@@ -1316,3 +1316,74 @@ int oracle_distinctive_descriptor(const uint8_t* desc, int N)
     free(row);
     return bestIdx;
 }
+
+/* ORBmatcher::Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, float th), the matching
+ * step (R/src/ORBmatcher.cpp:995-1121) per map point; the replace / add resolution (:1123-1150)
+ * mutates the map and stays with the caller.  OpenCV's small float products are restated as:
+ * Rcw * p3Dw + tcw with double-accumulated rows rounded to float (as in SearchByProjection),
+ * cv::norm(PO) = sqrt of the float sum ((x*x + y*y) + z*z) in double, PO.dot(Pn) = the float sum
+ * ((px*nx + py*ny) + pz*nz) widened to double — OpenCV-version dependent, parity unpinned there;
+ * PredictScale's log(ratio) in double (MapPoint.cpp:500, R/src/MapPoint.cpp:489-507). */
+void oracle_fuse(const oracle_frame* kf, const oracle_kf_params* kp, int n_mp, const uint8_t* mp_valid,
+                 const float* mp_xyz, const float* mp_normal, const float* mp_min_dist, const float* mp_max_dist,
+                 const uint8_t* mp_desc, float th, int32_t* best_idx, int32_t* best_dist)
+{
+    ogrid g;
+    build_grid(kf, &g);
+    int* cand = (int*)malloc(sizeof(int) * (size_t)(kf->n > 0 ? kf->n : 1));
+    for (int i = 0; i < n_mp; i++) {
+        best_idx[i] = -1;
+        best_dist[i] = 256;
+        if (!mp_valid[i]) continue;
+        const float* X = mp_xyz + 3 * (size_t)i;
+        float p3[3];
+        for (int r = 0; r < 3; r++) {
+            const double s = (double)kp->Tcw[4 * r] * X[0] + (double)kp->Tcw[4 * r + 1] * X[1] + (double)kp->Tcw[4 * r + 2] * X[2];
+            p3[r] = (float)(s + (double)kp->Tcw[4 * r + 3]);
+        }
+        if (p3[2] < 0.0f) continue;
+        const float invz = 1 / p3[2];
+        const float x = p3[0] * invz, y = p3[1] * invz;
+        const float u = kp->fx * x + kp->cx, v = kp->fy * y + kp->cy;
+        if (!(u >= kf->min_x && u < kf->max_x && v >= kf->min_y && v < kf->max_y)) continue;   /* IsInImage */
+        const float ur = u - kp->bf * invz;
+        const float maxDistance = 1.2f * mp_max_dist[i], minDistance = 0.8f * mp_min_dist[i];
+        const float PO[3] = {X[0] - kp->Ow[0], X[1] - kp->Ow[1], X[2] - kp->Ow[2]};
+        const float ss = (PO[0] * PO[0] + PO[1] * PO[1]) + PO[2] * PO[2];
+        const float dist3D = (float)sqrt((double)ss);
+        if (dist3D < minDistance || dist3D > maxDistance) continue;
+        const float* Pn = mp_normal + 3 * (size_t)i;
+        const float dot = (PO[0] * Pn[0] + PO[1] * Pn[1]) + PO[2] * Pn[2];
+        if ((double)dot < 0.5 * dist3D) continue;
+        const float ratio = mp_max_dist[i] / dist3D;
+        int nPredictedLevel = (int)ceil(log((double)ratio) / (double)kp->log_scale_factor);
+        if (nPredictedLevel < 0) nPredictedLevel = 0;
+        else if (nPredictedLevel >= kp->n_levels) nPredictedLevel = kp->n_levels - 1;
+        const float radius = th * kp->scale_factors[nPredictedLevel];
+        const int nc = features_in_area(kf, &g, u, v, radius, -1, -1, cand, kf->n);
+        int bestDist = 256, bestIdx = -1;
+        for (int c = 0; c < nc; c++) {
+            const int idx = cand[c];
+            const int kpLevel = kf->octave[idx];
+            if (kpLevel < nPredictedLevel - 1 || kpLevel > nPredictedLevel) continue;
+            const float ex = u - kf->x[idx], ey = v - kf->y[idx];
+            if (kf->uright && kf->uright[idx] >= 0) {
+                const float er = ur - kf->uright[idx];
+                const float e2 = ex * ex + ey * ey + er * er;
+                if ((double)(e2 * kp->inv_level_sigma2[kpLevel]) > 7.8) continue;
+            } else {
+                const float e2 = ex * ex + ey * ey;
+                if ((double)(e2 * kp->inv_level_sigma2[kpLevel]) > 5.99) continue;
+            }
+            const int dist = oracle_descriptor_distance(mp_desc + (size_t)i * 32, kf->desc + (size_t)idx * 32);
+            if (dist < bestDist) {
+                bestDist = dist;
+                bestIdx = idx;
+            }
+        }
+        best_dist[i] = bestDist;
+        if (bestDist <= TH_LOW) best_idx[i] = bestIdx;
+    }
+    free(cand);
+    free_grid(&g);
+}

@@ -168,6 +168,24 @@ void oracle_hamming_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt,
  * the descriptor with the least median distance (-1 for N = 0). */
 int oracle_distinctive_descriptor(const uint8_t* desc, int N);
 
+/* Keyframe geometry Fuse reads: rows 0..2 of GetPose(), GetCameraCenter(), intrinsics, mbf,
+ * mfLogScaleFactor, mnScaleLevels, mvScaleFactors, mvInvLevelSigma2. */
+typedef struct {
+    float Tcw[12];
+    float Ow[3];
+    float fx, fy, cx, cy, bf;
+    float log_scale_factor;
+    int n_levels;
+    const float* scale_factors;
+    const float* inv_level_sigma2;
+} oracle_kf_params;
+
+/* ORBmatcher::Fuse(pKF, vpMapPoints, th) matching step per map point: best_idx[i] = the keyframe
+ * keypoint it fuses into (-1: none within TH_LOW), best_dist[i] = its distance (256: none). */
+void oracle_fuse(const oracle_frame* kf, const oracle_kf_params* kp, int n_mp, const uint8_t* mp_valid,
+                 const float* mp_xyz, const float* mp_normal, const float* mp_min_dist, const float* mp_max_dist,
+                 const uint8_t* mp_desc, float th, int32_t* best_idx, int32_t* best_dist);
+
 #ifdef __cplusplus
 }
 #endif

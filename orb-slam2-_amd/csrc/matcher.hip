@@ -1077,6 +1077,102 @@ static void pack_view(const orb_frame_view* f, orb_keypoint* k) {
     }
 }
 
+// ------------------------------------------------------------------ Fuse
+// ORBmatcher::Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, float th), matching step
+// (R/src/ORBmatcher.cpp:995-1121): one wave per map point.  The projection, IsInImage, the scale
+// invariance distances, the viewing-angle test and PredictScale are evaluated uniformly by the
+// wave (OpenCV's float products restated as in oracle_fuse); the lanes then take the keyframe's
+// keypoints j, j + 64, ..., keep those GetFeaturesInArea returns (grid cells of the search
+// square, |dx| < r, |dy| < r), apply the level band [nPredictedLevel - 1, nPredictedLevel] and
+// the chi2 gate (7.8 stereo / 5.99 mono), and the wave takes the least distance with the first
+// candidate in GetFeaturesInArea order (cell ix-major, then keypoint index) winning ties — the
+// reference's strict < over that order.  best_idx = -1 unless the distance is <= TH_LOW.
+struct FuseKf {
+    float Tcw[12], Ow[3];
+    float fx, fy, cx, cy, bf, logsf;
+    int nlev;
+    float sf[32], isig2[32];
+};
+
+__global__ __launch_bounds__(256) void k_fuse(const orb_keypoint* __restrict__ kk, const uint8_t* __restrict__ kd,
+                                              const float* __restrict__ kur, int nk, GridParams g, FuseKf K, int n_mp,
+                                              const uint8_t* __restrict__ valid, const float* __restrict__ xyz,
+                                              const float* __restrict__ nrm, const float* __restrict__ mind,
+                                              const float* __restrict__ maxd, const uint8_t* __restrict__ mdesc,
+                                              float th, int32_t* __restrict__ best_idx, int32_t* __restrict__ best_dist) {
+    const int lane = threadIdx.x & 63;
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n_mp) return;
+    int out = -1, outd = 256;
+    bool go = valid[i] != 0;
+    const float* X = xyz + 3 * (size_t)i;
+    float u = 0, v = 0, ur = 0, radius = 0;
+    int lev = 0;
+    if (go) {
+        float p3[3];
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            const double s = (double)K.Tcw[4 * r] * X[0] + (double)K.Tcw[4 * r + 1] * X[1] + (double)K.Tcw[4 * r + 2] * X[2];
+            p3[r] = (float)(s + (double)K.Tcw[4 * r + 3]);
+        }
+        go = !(p3[2] < 0.0f);
+        const float invz = 1 / p3[2];
+        const float x = p3[0] * invz, y = p3[1] * invz;
+        u = K.fx * x + K.cx;
+        v = K.fy * y + K.cy;
+        go = go && u >= g.min_x && u < g.max_x && v >= g.min_y && v < g.max_y;   // KeyFrame::IsInImage
+        ur = u - K.bf * invz;
+        const float maxDistance = 1.2f * maxd[i], minDistance = 0.8f * mind[i];
+        const float PO[3] = {X[0] - K.Ow[0], X[1] - K.Ow[1], X[2] - K.Ow[2]};
+        const float ss = (PO[0] * PO[0] + PO[1] * PO[1]) + PO[2] * PO[2];
+        const float dist3D = (float)sqrt((double)ss);
+        go = go && !(dist3D < minDistance || dist3D > maxDistance);
+        const float* Pn = nrm + 3 * (size_t)i;
+        const float dot = (PO[0] * Pn[0] + PO[1] * Pn[1]) + PO[2] * Pn[2];
+        go = go && !((double)dot < 0.5 * dist3D);
+        const float ratio = maxd[i] / dist3D;
+        lev = (int)ceil(log((double)ratio) / (double)K.logsf);
+        if (lev < 0) lev = 0;
+        else if (lev >= K.nlev) lev = K.nlev - 1;
+        radius = th * K.sf[lev];
+    }
+    if (go) {
+        const AreaQuery q = make_area(g, u, v, radius, -1, -1);
+        const uint8_t* dq = mdesc + (size_t)i * 32;
+        int bd = 256, bk = 0x7fffffff;   // (distance, cell * 2^16 + index) lexicographic minimum
+        for (int j = lane; j < nk && q.cx0 <= q.cx1; j += 64) {
+            const orb_keypoint k2 = kk[j];
+            const int cell = grid_cell(g, k2.x, k2.y);
+            if (!in_area(q, cell, k2.octave, k2.x, k2.y)) continue;
+            const int kl = k2.octave;
+            if (kl < lev - 1 || kl > lev) continue;
+            const float ex = u - k2.x, ey = v - k2.y;
+            if (kur && kur[j] >= 0) {
+                const float er = ur - kur[j];
+                const float e2 = ex * ex + ey * ey + er * er;
+                if ((double)(e2 * K.isig2[kl]) > 7.8) continue;
+            } else {
+                const float e2 = ex * ex + ey * ey;
+                if ((double)(e2 * K.isig2[kl]) > 5.99) continue;
+            }
+            const int d = hamming32(dq, kd + (size_t)j * 32);
+            const int key = (cell << 16) | j;
+            if (d < bd || (d == bd && key < bk)) { bd = d; bk = key; }
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            const int od = __shfl_xor(bd, o, 64), ok = __shfl_xor(bk, o, 64);
+            if (od < bd || (od == bd && ok < bk)) { bd = od; bk = ok; }
+        }
+        outd = bd;
+        if (bd <= 50) out = bk & 0xffff;   // TH_LOW
+    }
+    if (lane == 0) {
+        best_idx[i] = out;
+        best_dist[i] = outd;
+    }
+}
+
 // ------------------------------------------------------------------ distinctive descriptors
 // MapPoint::ComputeDistinctiveDescriptors (R/src/MapPoint.cpp:306-385) for a batch of map
 // points: point m's observed descriptors are rows [start[m], start[m+1]) (observation order,
@@ -1508,6 +1604,78 @@ int orb_distinctive_descriptors(int device, const uint8_t* desc, const int32_t* 
     if (rc == ORB_OK) {
         (void)hipMemcpyAsync(best_idx, dI, (size_t)n_points * 4, hipMemcpyDeviceToHost, s);
         if (best_desc) (void)hipMemcpyAsync(best_desc, dB, (size_t)n_points * 32, hipMemcpyDeviceToHost, s);
+        if (hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
+    }
+    (void)hipStreamDestroy(s);
+    (void)hipFree(base);
+    return rc;
+}
+
+int orb_fuse(int device, const orb_frame_view* kf, const orb_kf_params* kp, int n_mp, const uint8_t* mp_valid,
+             const float* mp_xyz, const float* mp_normal, const float* mp_min_dist, const float* mp_max_dist,
+             const uint8_t* mp_desc, float th, int32_t* best_idx, int32_t* best_dist) {
+    if (!kf || !kp || n_mp < 0 || kf->n < 0 || kf->n >= (1 << 16)) return ORB_EINVAL;
+    if (n_mp > 0 && (!mp_valid || !mp_xyz || !mp_normal || !mp_min_dist || !mp_max_dist || !mp_desc || !best_idx ||
+                     !best_dist))
+        return ORB_EINVAL;
+    if (kp->n_levels < 1 || kp->n_levels > 32 || !kp->scale_factors || !kp->inv_level_sigma2) return ORB_EINVAL;
+    int st = check_device(device);
+    if (st) return st;
+    if (n_mp == 0) return ORB_OK;
+    for (int i = 0; i < kf->n; i++)
+        if (kf->octave[i] < 0 || kf->octave[i] >= kp->n_levels) return ORB_EINVAL;
+    ORB_HIP_TRY(hipSetDevice(device));
+    FuseKf K;
+    std::memcpy(K.Tcw, kp->Tcw, sizeof(K.Tcw));
+    std::memcpy(K.Ow, kp->Ow, sizeof(K.Ow));
+    K.fx = kp->fx; K.fy = kp->fy; K.cx = kp->cx; K.cy = kp->cy; K.bf = kp->bf; K.logsf = kp->log_scale_factor;
+    K.nlev = kp->n_levels;
+    for (int l = 0; l < 32; l++) {
+        K.sf[l] = l < kp->n_levels ? kp->scale_factors[l] : 0.f;
+        K.isig2[l] = l < kp->n_levels ? kp->inv_level_sigma2[l] : 0.f;
+    }
+    const int nk = kf->n;
+    std::vector<orb_keypoint> hk((size_t)std::max(nk, 1));
+    pack_view(kf, hk.data());
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t bK = al((size_t)nk * sizeof(orb_keypoint) + 1), bD = al((size_t)nk * 32 + 1), bU = al((size_t)nk * 4 + 1),
+                 bV = al((size_t)n_mp), bX = al((size_t)n_mp * 12), bM = al((size_t)n_mp * 4), bMD = al((size_t)n_mp * 32),
+                 bO = al((size_t)n_mp * 4);
+    char* base = nullptr;
+    ORB_HIP_TRY(hipMalloc(&base, bK + bD + bU + bV + 2 * bX + 2 * bM + bMD + 2 * bO));
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) { (void)hipFree(base); return ORB_EGPU; }
+    char* c = base;
+    auto take = [&](size_t b) { char* r = c; c += b; return r; };
+    orb_keypoint* dK = (orb_keypoint*)take(bK);
+    uint8_t* dD = (uint8_t*)take(bD);
+    float* dU = (float*)take(bU);
+    uint8_t* dV = (uint8_t*)take(bV);
+    float* dX = (float*)take(bX);
+    float* dN = (float*)take(bX);
+    float* dMin = (float*)take(bM);
+    float* dMax = (float*)take(bM);
+    uint8_t* dMD = (uint8_t*)take(bMD);
+    int32_t* dBI = (int32_t*)take(bO);
+    int32_t* dBD = (int32_t*)take(bO);
+    if (nk) {
+        (void)hipMemcpyAsync(dK, hk.data(), (size_t)nk * sizeof(orb_keypoint), hipMemcpyHostToDevice, s);
+        (void)hipMemcpyAsync(dD, kf->desc, (size_t)nk * 32, hipMemcpyHostToDevice, s);
+        if (kf->uright) (void)hipMemcpyAsync(dU, kf->uright, (size_t)nk * 4, hipMemcpyHostToDevice, s);
+    }
+    (void)hipMemcpyAsync(dV, mp_valid, (size_t)n_mp, hipMemcpyHostToDevice, s);
+    (void)hipMemcpyAsync(dX, mp_xyz, (size_t)n_mp * 12, hipMemcpyHostToDevice, s);
+    (void)hipMemcpyAsync(dN, mp_normal, (size_t)n_mp * 12, hipMemcpyHostToDevice, s);
+    (void)hipMemcpyAsync(dMin, mp_min_dist, (size_t)n_mp * 4, hipMemcpyHostToDevice, s);
+    (void)hipMemcpyAsync(dMax, mp_max_dist, (size_t)n_mp * 4, hipMemcpyHostToDevice, s);
+    (void)hipMemcpyAsync(dMD, mp_desc, (size_t)n_mp * 32, hipMemcpyHostToDevice, s);
+    const GridParams g = grid_of(kf);
+    hipLaunchKernelGGL(k_fuse, dim3((n_mp + 3) / 4), dim3(256), 0, s, dK, dD, kf->uright ? (const float*)dU : nullptr,
+                       nk, g, K, n_mp, dV, dX, dN, dMin, dMax, dMD, th, dBI, dBD);
+    int rc = hipGetLastError() == hipSuccess ? ORB_OK : ORB_EGPU;
+    if (rc == ORB_OK) {
+        (void)hipMemcpyAsync(best_idx, dBI, (size_t)n_mp * 4, hipMemcpyDeviceToHost, s);
+        (void)hipMemcpyAsync(best_dist, dBD, (size_t)n_mp * 4, hipMemcpyDeviceToHost, s);
         if (hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
     }
     (void)hipStreamDestroy(s);

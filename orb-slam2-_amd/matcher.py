@@ -176,3 +176,35 @@ def ComputeDistinctiveDescriptors(descriptor_lists, device=0):
     _abi.check("orb_distinctive_descriptors",
                lib.orb_distinctive_descriptors(device, _abi.ptr(desc), _abi.ptr(start), M, _abi.ptr(best), _abi.ptr(out)))
     return best, out
+
+
+class KfParams(C.Structure):
+    _fields_ = [("Tcw", C.c_float * 12), ("Ow", C.c_float * 3), ("fx", C.c_float), ("fy", C.c_float),
+                ("cx", C.c_float), ("cy", C.c_float), ("bf", C.c_float), ("log_scale_factor", C.c_float),
+                ("n_levels", C.c_int), ("scale_factors", C.c_void_p), ("inv_level_sigma2", C.c_void_p)]
+
+
+def Fuse(kf: Frame, Tcw, Ow, cam, log_scale_factor, scale_factors, inv_level_sigma2, mp_valid, mp_xyz, mp_normal,
+         mp_min_dist, mp_max_dist, mp_desc, th=3.0, device=0):
+    """ORBmatcher::Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, float th) matching step
+    (R/src/ORBmatcher.cpp:995-1121) on the GPU: per map point the keyframe keypoint it fuses into
+    (-1 = none) and the distance.  kf: the keyframe as a Frame (mvKeysUn, mDescriptors, mvuRight,
+    bounds); Tcw 3x4 float, Ow = camera centre, cam = (fx, fy, cx, cy, mbf)."""
+    sf = np.ascontiguousarray(scale_factors, np.float32)
+    isg = np.ascontiguousarray(inv_level_sigma2, np.float32)
+    kp = KfParams((C.c_float * 12)(*np.asarray(Tcw, np.float32).reshape(-1)[:12]),
+                  (C.c_float * 3)(*np.asarray(Ow, np.float32)), *[float(np.float32(v)) for v in cam],
+                  float(np.float32(log_scale_factor)), len(sf), _abi.ptr(sf), _abi.ptr(isg))
+    a = [np.ascontiguousarray(x, t) for x, t in ((mp_valid, np.uint8), (mp_xyz, np.float32), (mp_normal, np.float32),
+                                                  (mp_min_dist, np.float32), (mp_max_dist, np.float32),
+                                                  (mp_desc, np.uint8))]
+    n = len(a[0])
+    bi, bd = np.zeros(n, np.int32), np.zeros(n, np.int32)
+    v = kf.view()
+    lib = _abi.lib()
+    lib.orb_fuse.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int] + [C.c_void_p] * 6 + [C.c_float, C.c_void_p,
+                                                                                           C.c_void_p]
+    lib.orb_fuse.restype = C.c_int
+    _abi.check("orb_fuse", lib.orb_fuse(device, C.byref(v), C.byref(kp), n, *[_abi.ptr(x) for x in a], th,
+                                        _abi.ptr(bi), _abi.ptr(bd)))
+    return bi, bd

@@ -217,3 +217,64 @@ def pose_problems(n_frames=8, seed=5, n_points=600, stereo_frac=0.0, outlier_fra
                        "cam": (fx, fy, cx, cy, float(np.float32(KITTI_BF))),
                        "true_R": R, "true_t": t})
     return frames
+
+
+def fuse_problem(seed=3, n_kps=1000, n_mp=800, true_frac=0.6, stereo_frac=0.3, W=640, H=480, nlevels=8):
+    """Synthetic ORBmatcher::Fuse input: a keyframe (identity-ish pose, TUM1 intrinsics, KITTI bf)
+    with n_kps keypoints (octave U{0..7}, random descriptors, stereo_frac with a right
+    coordinate), and n_mp map points — true_frac of them the back-projection of a keypoint at a
+    random depth (plus < 1 px of projection noise, descriptor = the keypoint's with U{0..60} bits
+    flipped), the rest random points in front of the camera.  Distance ranges follow
+    MapPoint::UpdateNormalAndDepth (mfMaxDistance = dist * 1.2^octave, mfMinDistance =
+    mfMaxDistance / 1.2^7); normals are the viewing ray plus noise."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    fx, fy, cx, cy = TUM1
+    bf = float(np.float32(KITTI_BF))
+    sf = np.array([np.float32(1.2) ** l for l in range(nlevels)], np.float32)
+    isig2 = (np.float32(1.0) / (sf * sf)).astype(np.float32)
+    R = _rot(rng.normal(0, 0.05, 3)).astype(np.float32)
+    t = rng.normal(0, 0.1, 3).astype(np.float32)
+    Tcw = np.zeros((3, 4), np.float32)
+    Tcw[:, :3], Tcw[:, 3] = R, t
+    Ow = (-R.T.astype(np.float64) @ t.astype(np.float64)).astype(np.float32)
+    kx = rng.uniform(0, W, n_kps).astype(np.float32)
+    ky = rng.uniform(0, H, n_kps).astype(np.float32)
+    oct_ = rng.integers(0, nlevels, n_kps).astype(np.int32)
+    desc = rng.integers(0, 256, (n_kps, 32), dtype=np.uint8)
+    depth = rng.uniform(1.0, 8.0, n_kps)
+    ur = np.where(rng.random(n_kps) < stereo_frac, kx - bf / depth, -1.0).astype(np.float32)
+    xyz, nrm, mind, maxd, mdesc = [], [], [], [], []
+    for i in range(n_mp):
+        if rng.random() < true_frac:
+            j = int(rng.integers(0, n_kps))
+            z = depth[j]
+            Xc = np.array([(kx[j] + rng.normal(0, 0.5) - cx) / fx * z, (ky[j] + rng.normal(0, 0.5) - cy) / fy * z, z])
+            d = desc[j].copy()
+            nb = int(rng.integers(0, 61))
+            bits = np.unpackbits(d)
+            bits[rng.choice(256, nb, replace=False)] ^= 1
+            d = np.packbits(bits)
+            lvl = int(oct_[j])
+        else:
+            Xc = np.array([rng.uniform(-3, 3), rng.uniform(-2, 2), rng.uniform(0.5, 9)])
+            d = rng.integers(0, 256, 32, dtype=np.uint8)
+            lvl = int(rng.integers(0, nlevels))
+        Xw = (R.T.astype(np.float64) @ (Xc - t.astype(np.float64))).astype(np.float32)
+        PO = Xw.astype(np.float64) - Ow
+        dist = np.linalg.norm(PO)
+        n = PO / dist + rng.normal(0, 0.1, 3)
+        n /= np.linalg.norm(n)
+        xyz.append(Xw)
+        nrm.append(n.astype(np.float32))
+        mx = np.float32(dist * float(sf[lvl]))
+        maxd.append(mx)
+        mind.append(np.float32(mx / sf[nlevels - 1]))
+        mdesc.append(d)
+    valid = (rng.random(n_mp) > 0.05).astype(np.uint8)
+    return {"kf": {"x": kx, "y": ky, "octave": oct_, "desc": desc, "uright": ur, "angle": np.zeros(n_kps, np.float32),
+                   "W": W, "H": H},
+            "kp": {"Tcw": Tcw, "Ow": Ow, "cam": (fx, fy, cx, cy, bf), "log_scale_factor": float(np.log(np.float32(1.2))),
+                   "n_levels": nlevels, "scale_factors": sf, "inv_level_sigma2": isig2},
+            "mp_valid": valid, "mp_xyz": np.array(xyz, np.float32), "mp_normal": np.array(nrm, np.float32),
+            "mp_min_dist": np.array(mind, np.float32), "mp_max_dist": np.array(maxd, np.float32),
+            "mp_desc": np.array(mdesc, np.uint8)}

@@ -325,3 +325,33 @@ def distinctive_descriptor(desc):
     """oracle_distinctive_descriptor on one point's (N, 32) descriptor list."""
     d = np.ascontiguousarray(np.asarray(desc, np.uint8).reshape(-1, 32))
     return int(lib().oracle_distinctive_descriptor(P(d), len(d)))
+
+
+class KfParams(C.Structure):
+    _fields_ = [("Tcw", C.c_float * 12), ("Ow", C.c_float * 3), ("fx", C.c_float), ("fy", C.c_float),
+                ("cx", C.c_float), ("cy", C.c_float), ("bf", C.c_float), ("log_scale_factor", C.c_float),
+                ("n_levels", C.c_int), ("scale_factors", C.c_void_p), ("inv_level_sigma2", C.c_void_p)]
+
+
+def kf_params(kp):
+    sf = np.ascontiguousarray(kp["scale_factors"], np.float32)
+    isg = np.ascontiguousarray(kp["inv_level_sigma2"], np.float32)
+    s = KfParams((C.c_float * 12)(*np.asarray(kp["Tcw"], np.float32).reshape(-1)),
+                 (C.c_float * 3)(*np.asarray(kp["Ow"], np.float32)), *[float(np.float32(v)) for v in kp["cam"]],
+                 float(np.float32(kp["log_scale_factor"])), int(kp["n_levels"]), P(sf), P(isg))
+    s._keep = (sf, isg)
+    return s
+
+
+def fuse(prob, th=3.0):
+    """oracle_fuse on a synth.fuse_problem: (best_idx, best_dist) per map point."""
+    kf = prob["kf"]
+    fv = FrameView(kf, kf["desc"], kf["W"], kf["H"], kf["uright"])
+    kp = kf_params(prob["kp"])
+    n = len(prob["mp_valid"])
+    a = {k: np.ascontiguousarray(prob[k]) for k in ("mp_valid", "mp_xyz", "mp_normal", "mp_min_dist", "mp_max_dist",
+                                                    "mp_desc")}
+    bi, bd = np.zeros(n, np.int32), np.zeros(n, np.int32)
+    lib().oracle_fuse(C.byref(fv.s), C.byref(kp), n, P(a["mp_valid"]), P(a["mp_xyz"]), P(a["mp_normal"]),
+                      P(a["mp_min_dist"]), P(a["mp_max_dist"]), P(a["mp_desc"]), C.c_float(th), P(bi), P(bd))
+    return bi, bd
