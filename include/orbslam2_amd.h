@@ -189,6 +189,24 @@ int orb_fuse(int device, const orb_frame_view* kf, const orb_kf_params* kp, int 
              const float* mp_xyz, const float* mp_normal, const float* mp_min_dist, const float* mp_max_dist,
              const uint8_t* mp_desc, float th, int32_t* best_idx, int32_t* best_dist);
 
+/* ORBmatcher::SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo) —
+ * R/src/ORBmatcher.cpp:785-983 (LocalMapping::CreateNewMapPoints, R/src/LocalMapping.cpp:374).
+ *   kf1 / kf2: the keyframes as frame views (mvKeysUn incl. angle and octave, mDescriptors,
+ *   mvuRight); has_mp1/2[i] != 0 when GetMapPoint(i) is set;
+ *   mFeatVec of each keyframe: n_nodes ascending node ids, CSR start[n_nodes + 1] into the
+ *   feature-index lists (DBoW2 insertion order);
+ *   F12 = LocalMapping::ComputeF12 (row-major 3x3 float); (ex, ey) = KF1's camera centre
+ *   projected into KF2 (:799-803); scale_factors2 / level_sigma2 = pKF2->mvScaleFactors /
+ *   mvLevelSigma2 (n_levels2 entries); check_ori = mbCheckOrientation.
+ * matches12 (kf1->n ints) receives the KF2 keypoint or -1; vMatchedPairs are its (i, j) pairs in
+ * i order.  Returns nmatches; ORB_E2BIG when a node holds more than 2048 KF2 features. */
+int orb_search_for_triangulation(int device, const orb_frame_view* kf1, const orb_frame_view* kf2,
+                                 const uint8_t* has_mp1, const uint8_t* has_mp2, int n_nodes1, const uint32_t* nodes1,
+                                 const int32_t* start1, const int32_t* fidx1, int n_nodes2, const uint32_t* nodes2,
+                                 const int32_t* start2, const int32_t* fidx2, const float F12[9], float ex, float ey,
+                                 const float* scale_factors2, const float* level_sigma2, int n_levels2, int only_stereo,
+                                 int check_ori, int32_t* matches12);
+
 /* MapPoint::ComputeDistinctiveDescriptors (R/src/MapPoint.cpp:306-385) for n_points map points:
  * point m's descriptors (one per observation by a non-bad keyframe, in mObservations order) are
  * rows [start[m], start[m+1]) of desc (32 B each).  best_idx[m] = index within the point's list

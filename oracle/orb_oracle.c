@@ -1387,3 +1387,87 @@ void oracle_fuse(const oracle_frame* kf, const oracle_kf_params* kp, int n_mp, c
     free(cand);
     free_grid(&g);
 }
+
+/* ORBmatcher::SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo)
+ * (R/src/ORBmatcher.cpp:785-983) with CheckDistEpipolarLine (:175-203).  The FeatureVectors
+ * (pKF->mFeatVec) come as ascending node ids with CSR lists of feature indices.  matches12[i]
+ * = the KF2 keypoint matched to KF1 keypoint i or -1 (vMatchedPairs = its pairs in i order). */
+static int epipolar_ok(float x1, float y1, float x2, float y2, const float* F, double sigma2)
+{
+    const float a = x1 * F[0] + y1 * F[3] + F[6];
+    const float b = x1 * F[1] + y1 * F[4] + F[7];
+    const float c = x1 * F[2] + y1 * F[5] + F[8];
+    const float num = a * x2 + b * y2 + c;
+    const float den = a * a + b * b;
+    if (den == 0) return 0;
+    const float dsqr = num * num / den;
+    return (double)dsqr < 3.84 * sigma2;
+}
+
+int oracle_search_for_triangulation(const oracle_frame* k1, const oracle_frame* k2, const uint8_t* has_mp1,
+                                    const uint8_t* has_mp2, int n1, const uint32_t* nodes1, const int32_t* start1,
+                                    const int32_t* idx1, int n2, const uint32_t* nodes2, const int32_t* start2,
+                                    const int32_t* idx2, const float* F12, float ex, float ey,
+                                    const float* scale_factors2, const float* level_sigma2, int only_stereo,
+                                    int check_ori, int32_t* matches12)
+{
+    uint8_t* matched2 = (uint8_t*)calloc(k2->n > 0 ? k2->n : 1, 1);
+    for (int i = 0; i < k1->n; i++) matches12[i] = -1;
+    int nmatches = 0;
+    int* hist = (int*)calloc((size_t)HISTO_LENGTH, sizeof(int));
+    int a = 0, b = 0;
+    while (a < n1 && b < n2) {
+        if (nodes1[a] == nodes2[b]) {
+            for (int p1 = start1[a]; p1 < start1[a + 1]; p1++) {
+                const int i1 = idx1[p1];
+                if (has_mp1[i1]) continue;
+                const int bStereo1 = k1->uright && k1->uright[i1] >= 0;
+                if (only_stereo && !bStereo1) continue;
+                int bestDist = TH_LOW, bestIdx2 = -1;
+                for (int p2 = start2[b]; p2 < start2[b + 1]; p2++) {
+                    const int i2 = idx2[p2];
+                    if (matched2[i2] || has_mp2[i2]) continue;
+                    const int bStereo2 = k2->uright && k2->uright[i2] >= 0;
+                    if (only_stereo && !bStereo2) continue;
+                    const int dist = oracle_descriptor_distance(k1->desc + (size_t)i1 * 32, k2->desc + (size_t)i2 * 32);
+                    if (dist > TH_LOW || dist > bestDist) continue;
+                    if (!bStereo1 && !bStereo2) {
+                        const float distex = ex - k2->x[i2], distey = ey - k2->y[i2];
+                        if (distex * distex + distey * distey < 100 * scale_factors2[k2->octave[i2]]) continue;
+                    }
+                    if (epipolar_ok(k1->x[i1], k1->y[i1], k2->x[i2], k2->y[i2], F12, level_sigma2[k2->octave[i2]])) {
+                        bestIdx2 = i2;
+                        bestDist = dist;
+                    }
+                }
+                if (bestIdx2 >= 0) {
+                    matches12[i1] = bestIdx2;
+                    matched2[bestIdx2] = 1;
+                    nmatches++;
+                }
+            }
+            a++;
+            b++;
+        } else if (nodes1[a] < nodes2[b]) {
+            while (a < n1 && nodes1[a] < nodes2[b]) a++;   /* lower_bound */
+        } else {
+            while (b < n2 && nodes2[b] < nodes1[a]) b++;
+        }
+    }
+    if (check_ori) {
+        for (int i = 0; i < k1->n; i++)
+            if (matches12[i] >= 0) hist[rot_bin(k1->angle[i] - k2->angle[matches12[i]])]++;
+        int ind1, ind2, ind3;
+        three_maxima(hist, &ind1, &ind2, &ind3);
+        for (int i = 0; i < k1->n; i++) {
+            if (matches12[i] < 0) continue;
+            const int bin = rot_bin(k1->angle[i] - k2->angle[matches12[i]]);
+            if (bin == ind1 || bin == ind2 || bin == ind3) continue;
+            matches12[i] = -1;
+            nmatches--;
+        }
+    }
+    free(hist);
+    free(matched2);
+    return nmatches;
+}

@@ -186,6 +186,15 @@ void oracle_fuse(const oracle_frame* kf, const oracle_kf_params* kp, int n_mp, c
                  const float* mp_xyz, const float* mp_normal, const float* mp_min_dist, const float* mp_max_dist,
                  const uint8_t* mp_desc, float th, int32_t* best_idx, int32_t* best_dist);
 
+/* ORBmatcher::SearchForTriangulation (R/src/ORBmatcher.cpp:785-983): FeatureVectors as ascending
+ * node ids + CSR feature lists; F12 row-major; (ex, ey) the epipole; returns nmatches. */
+int oracle_search_for_triangulation(const oracle_frame* k1, const oracle_frame* k2, const uint8_t* has_mp1,
+                                    const uint8_t* has_mp2, int n1, const uint32_t* nodes1, const int32_t* start1,
+                                    const int32_t* idx1, int n2, const uint32_t* nodes2, const int32_t* start2,
+                                    const int32_t* idx2, const float* F12, float ex, float ey,
+                                    const float* scale_factors2, const float* level_sigma2, int only_stereo,
+                                    int check_ori, int32_t* matches12);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1173,6 +1173,127 @@ __global__ __launch_bounds__(256) void k_fuse(const orb_keypoint* __restrict__ k
     }
 }
 
+// ------------------------------------------------------------------ SearchForTriangulation
+// ORBmatcher::SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo)
+// (R/src/ORBmatcher.cpp:785-983).  Keypoints only meet inside a common vocabulary node, and a
+// keyframe-2 keypoint lies in one node, so nodes are independent: one wave per common node runs
+// the node's keyframe-1 features in order (the reference's greedy vbMatched2 sequence), the
+// lanes taking the node's keyframe-2 features.  For each feature the wave keeps the candidate
+// the reference's running `dist > bestDist -> continue` loop ends with — the least distance
+// <= TH_LOW passing the epipole and CheckDistEpipolarLine (:175-203) tests, ties to the later
+// candidate — and the owning lane marks it matched in a register bitmask.  A second one-
+// workgroup kernel applies the rotation-consistency histogram (ComputeThreeMaxima).
+constexpr int kSftMaxNode = 2048;   // keyframe-2 features of one node (32 bitmask slots per lane)
+struct SftParams {
+    float F[9];
+    float ex, ey;
+    float sf2[32], sig2[32];
+    int onlyStereo;
+};
+
+__global__ __launch_bounds__(64) void k_sft(const orb_keypoint* __restrict__ k1, const uint8_t* __restrict__ d1,
+                                            const float* __restrict__ ur1, const uint8_t* __restrict__ mp1,
+                                            const orb_keypoint* __restrict__ k2, const uint8_t* __restrict__ d2,
+                                            const float* __restrict__ ur2, const uint8_t* __restrict__ mp2,
+                                            const int4* __restrict__ nodes, const int32_t* __restrict__ idx1,
+                                            const int32_t* __restrict__ idx2, SftParams P,
+                                            int32_t* __restrict__ matches12) {
+    const int lane = threadIdx.x;
+    const int4 nd = nodes[blockIdx.x];   // KF1 list [x, y), KF2 list [z, w)
+    const int c2 = nd.w - nd.z;
+    uint32_t taken = 0;                  // bit r: candidate lane + 64 r matched (vbMatched2)
+    for (int p1 = nd.x; p1 < nd.y; p1++) {
+        const int i1 = idx1[p1];
+        if (mp1[i1]) continue;
+        const bool st1 = ur1 && ur1[i1] >= 0;
+        if (P.onlyStereo && !st1) continue;
+        const orb_keypoint a = k1[i1];
+        const uint4* da = reinterpret_cast<const uint4*>(d1 + (size_t)i1 * 32);
+        const uint4 a0 = da[0], a1 = da[1];
+        const float ea = a.x * P.F[0] + a.y * P.F[3] + P.F[6];   // CheckDistEpipolarLine's line
+        const float eb = a.x * P.F[1] + a.y * P.F[4] + P.F[7];
+        const float ec = a.x * P.F[2] + a.y * P.F[5] + P.F[8];
+        int best = 0x7fffffff;   // (dist << 16) | (65535 - position): least dist, ties to the later
+        for (int r = 0; r * 64 < c2; r++) {
+            const int pos = r * 64 + lane;
+            if (pos >= c2 || ((taken >> r) & 1u)) continue;
+            const int i2 = idx2[nd.z + pos];
+            if (mp2[i2]) continue;
+            const bool st2 = ur2 && ur2[i2] >= 0;
+            if (P.onlyStereo && !st2) continue;
+            const uint4* db = reinterpret_cast<const uint4*>(d2 + (size_t)i2 * 32);
+            const uint4 b0 = db[0], b1 = db[1];
+            const int dist = __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+                             __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+            if (dist > 50) continue;   // TH_LOW
+            const orb_keypoint b = k2[i2];
+            if (!st1 && !st2) {
+                const float dex = P.ex - b.x, dey = P.ey - b.y;
+                if (dex * dex + dey * dey < 100 * P.sf2[b.octave]) continue;
+            }
+            const float num = ea * b.x + eb * b.y + ec;
+            const float den = ea * ea + eb * eb;
+            if (den == 0) continue;
+            const float dsqr = num * num / den;
+            if (!((double)dsqr < 3.84 * P.sig2[b.octave])) continue;
+            const int key = (dist << 16) | (65535 - pos);
+            best = min(best, key);
+        }
+        best = wave_min_i32(best);
+        if (best != 0x7fffffff) {
+            const int pos = 65535 - (best & 0xffff);
+            if ((pos & 63) == lane) taken |= 1u << (pos >> 6);
+            if (lane == 0) matches12[i1] = idx2[nd.z + pos];
+        }
+    }
+}
+
+// The rotation-consistency filter of SearchForTriangulation (:944-961) over all matches: bin
+// counts in LDS, ComputeThreeMaxima, matches outside the three bins dropped; *nmatches.
+__global__ __launch_bounds__(256) void k_sft_rot(const orb_keypoint* __restrict__ k1, const orb_keypoint* __restrict__ k2,
+                                                 int n1, int checkOri, int32_t* __restrict__ matches12,
+                                                 int32_t* __restrict__ nmatches) {
+    __shared__ int hcount[kHisto];
+    __shared__ int ind[3], total;
+    const int tid = threadIdx.x;
+    if (tid < kHisto) hcount[tid] = 0;
+    if (tid == 0) total = 0;
+    __syncthreads();
+    for (int i = tid; i < n1; i += 256) {
+        const int j = matches12[i];
+        if (j < 0) continue;
+        if (checkOri) atomicAdd(&hcount[rot_bin(k1[i].angle - k2[j].angle)], 1);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        int max1 = 0, max2 = 0, max3 = 0;
+        for (int i = 0; i < kHisto; i++) {
+            const int s = hcount[i];
+            if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
+            else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
+            else if (s > max3) { max3 = s; ind3 = i; }
+        }
+        if ((float)max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+        else if ((float)max3 < 0.1f * (float)max1) { ind3 = -1; }
+        ind[0] = ind1; ind[1] = ind2; ind[2] = ind3;
+    }
+    __syncthreads();
+    int kept = 0;
+    for (int i = tid; i < n1; i += 256) {
+        const int j = matches12[i];
+        if (j < 0) continue;
+        if (checkOri) {
+            const int bin = rot_bin(k1[i].angle - k2[j].angle);
+            if (bin != ind[0] && bin != ind[1] && bin != ind[2]) { matches12[i] = -1; continue; }
+        }
+        kept++;
+    }
+    atomicAdd(&total, kept);
+    __syncthreads();
+    if (tid == 0) *nmatches = total;
+}
+
 // ------------------------------------------------------------------ distinctive descriptors
 // MapPoint::ComputeDistinctiveDescriptors (R/src/MapPoint.cpp:306-385) for a batch of map
 // points: point m's observed descriptors are rows [start[m], start[m+1]) (observation order,
@@ -1681,6 +1802,96 @@ int orb_fuse(int device, const orb_frame_view* kf, const orb_kf_params* kp, int 
     (void)hipStreamDestroy(s);
     (void)hipFree(base);
     return rc;
+}
+
+int orb_search_for_triangulation(int device, const orb_frame_view* kf1, const orb_frame_view* kf2,
+                                 const uint8_t* has_mp1, const uint8_t* has_mp2, int n_nodes1, const uint32_t* nodes1,
+                                 const int32_t* start1, const int32_t* fidx1, int n_nodes2, const uint32_t* nodes2,
+                                 const int32_t* start2, const int32_t* fidx2, const float F12[9], float ex, float ey,
+                                 const float* scale_factors2, const float* level_sigma2, int n_levels2, int only_stereo,
+                                 int check_ori, int32_t* matches12) {
+    if (!kf1 || !kf2 || !has_mp1 || !has_mp2 || !F12 || !scale_factors2 || !level_sigma2 || !matches12) return ORB_EINVAL;
+    if (n_nodes1 < 0 || n_nodes2 < 0 || kf1->n < 0 || kf2->n < 0 || n_levels2 < 1 || n_levels2 > 32) return ORB_EINVAL;
+    int st = check_device(device);
+    if (st) return st;
+    for (int i = 0; i < kf1->n; i++) matches12[i] = -1;
+    // common nodes (the reference's lower_bound walk) and their list ranges
+    std::vector<int4> common;
+    for (int a = 0, b = 0; a < n_nodes1 && b < n_nodes2;) {
+        if (nodes1[a] == nodes2[b]) {
+            if (start2[b + 1] - start2[b] > kSftMaxNode) return ORB_E2BIG;
+            if (start1[a + 1] > start1[a] && start2[b + 1] > start2[b])
+                common.push_back(make_int4(start1[a], start1[a + 1], start2[b], start2[b + 1]));
+            a++;
+            b++;
+        } else if (nodes1[a] < nodes2[b]) {
+            a++;
+        } else {
+            b++;
+        }
+    }
+    const int L1 = n_nodes1 ? start1[n_nodes1] : 0, L2 = n_nodes2 ? start2[n_nodes2] : 0;
+    for (int t = 0; t < L1; t++)
+        if (fidx1[t] < 0 || fidx1[t] >= kf1->n) return ORB_EINVAL;
+    for (int t = 0; t < L2; t++)
+        if (fidx2[t] < 0 || fidx2[t] >= kf2->n) return ORB_EINVAL;
+    for (int i = 0; i < kf2->n; i++)
+        if (kf2->octave[i] < 0 || kf2->octave[i] >= n_levels2) return ORB_EINVAL;
+    if (common.empty() || kf1->n == 0) return 0;
+    ORB_HIP_TRY(hipSetDevice(device));
+    SftParams P;
+    std::memcpy(P.F, F12, sizeof(P.F));
+    P.ex = ex; P.ey = ey; P.onlyStereo = only_stereo ? 1 : 0;
+    for (int l = 0; l < 32; l++) {
+        P.sf2[l] = l < n_levels2 ? scale_factors2[l] : 0.f;
+        P.sig2[l] = l < n_levels2 ? level_sigma2[l] : 0.f;
+    }
+    const int n1 = kf1->n, n2 = kf2->n;
+    std::vector<orb_keypoint> hk1((size_t)n1), hk2((size_t)std::max(n2, 1));
+    pack_view(kf1, hk1.data());
+    pack_view(kf2, hk2.data());
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t tot = al((size_t)n1 * sizeof(orb_keypoint)) + al((size_t)n2 * sizeof(orb_keypoint) + 1) +
+                       al((size_t)n1 * 32) + al((size_t)n2 * 32 + 1) + 2 * al((size_t)n1 * 4) + 2 * al((size_t)n2 * 4 + 1) +
+                       al((size_t)n1) + al((size_t)n2 + 1) + al(common.size() * 16) + al((size_t)L1 * 4 + 1) +
+                       al((size_t)L2 * 4 + 1) + al(4) + 4096;
+    char* base = nullptr;
+    ORB_HIP_TRY(hipMalloc(&base, tot));
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) { (void)hipFree(base); return ORB_EGPU; }
+    char* c = base;
+    auto put = [&](const void* src, size_t bytes) {
+        char* r = c;
+        c += al(bytes + 1);
+        if (src && bytes) (void)hipMemcpyAsync(r, src, bytes, hipMemcpyHostToDevice, s);
+        return r;
+    };
+    auto* dK1 = (orb_keypoint*)put(hk1.data(), (size_t)n1 * sizeof(orb_keypoint));
+    auto* dK2 = (orb_keypoint*)put(hk2.data(), (size_t)n2 * sizeof(orb_keypoint));
+    auto* dD1 = (uint8_t*)put(kf1->desc, (size_t)n1 * 32);
+    auto* dD2 = (uint8_t*)put(kf2->desc, (size_t)n2 * 32);
+    auto* dU1 = (float*)put(kf1->uright, kf1->uright ? (size_t)n1 * 4 : 0);
+    auto* dU2 = (float*)put(kf2->uright, kf2->uright ? (size_t)n2 * 4 : 0);
+    auto* dM1 = (uint8_t*)put(has_mp1, (size_t)n1);
+    auto* dM2 = (uint8_t*)put(has_mp2, (size_t)n2);
+    auto* dN = (int4*)put(common.data(), common.size() * 16);
+    auto* dI1 = (int32_t*)put(fidx1, (size_t)L1 * 4);
+    auto* dI2 = (int32_t*)put(fidx2, (size_t)L2 * 4);
+    auto* dMt = (int32_t*)put(matches12, (size_t)n1 * 4);
+    auto* dNm = (int32_t*)put(nullptr, 4);
+    hipLaunchKernelGGL(k_sft, dim3((unsigned)common.size()), dim3(64), 0, s, dK1, dD1, kf1->uright ? dU1 : nullptr, dM1,
+                       dK2, dD2, kf2->uright ? dU2 : nullptr, dM2, dN, dI1, dI2, P, dMt);
+    hipLaunchKernelGGL(k_sft_rot, dim3(1), dim3(256), 0, s, dK1, dK2, n1, check_ori ? 1 : 0, dMt, dNm);
+    int rc = hipGetLastError() == hipSuccess ? ORB_OK : ORB_EGPU;
+    int nm = 0;
+    if (rc == ORB_OK) {
+        (void)hipMemcpyAsync(matches12, dMt, (size_t)n1 * 4, hipMemcpyDeviceToHost, s);
+        (void)hipMemcpyAsync(&nm, dNm, 4, hipMemcpyDeviceToHost, s);
+        if (hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
+    }
+    (void)hipStreamDestroy(s);
+    (void)hipFree(base);
+    return rc == ORB_OK ? nm : rc;
 }
 
 }  // extern "C"

@@ -208,3 +208,28 @@ def Fuse(kf: Frame, Tcw, Ow, cam, log_scale_factor, scale_factors, inv_level_sig
     _abi.check("orb_fuse", lib.orb_fuse(device, C.byref(v), C.byref(kp), n, *[_abi.ptr(x) for x in a], th,
                                         _abi.ptr(bi), _abi.ptr(bd)))
     return bi, bd
+
+
+def SearchForTriangulation(kf1: Frame, kf2: Frame, has_mp1, has_mp2, featvec1, featvec2, F12, epipole,
+                           scale_factors2, level_sigma2, bOnlyStereo=False, checkOri=True, device=0):
+    """ORBmatcher::SearchForTriangulation (R/src/ORBmatcher.cpp:785-983) on the GPU.
+    featvecN = (node ids ascending, CSR start, feature indices) of pKF->mFeatVec; F12 3x3 float;
+    epipole = (ex, ey).  Returns (nmatches, matches12) — vMatchedPairs = [(i, matches12[i]) for
+    matches12[i] >= 0]."""
+    v1, v2 = kf1.view(), kf2.view()
+    fv = [tuple(np.ascontiguousarray(x, t) for x, t in zip(f, (np.uint32, np.int32, np.int32))) for f in (featvec1, featvec2)]
+    hm1, hm2 = np.ascontiguousarray(has_mp1, np.uint8), np.ascontiguousarray(has_mp2, np.uint8)
+    F = np.ascontiguousarray(np.asarray(F12, np.float32).reshape(-1))
+    sf = np.ascontiguousarray(scale_factors2, np.float32)
+    s2 = np.ascontiguousarray(level_sigma2, np.float32)
+    m = np.zeros(kf1.N, np.int32)
+    lib = _abi.lib()
+    vp = C.c_void_p
+    lib.orb_search_for_triangulation.argtypes = [C.c_int, vp, vp, vp, vp, C.c_int, vp, vp, vp, C.c_int, vp, vp, vp, vp,
+                                                 C.c_float, C.c_float, vp, vp, C.c_int, C.c_int, C.c_int, vp]
+    lib.orb_search_for_triangulation.restype = C.c_int
+    n = _abi.check("orb_search_for_triangulation", lib.orb_search_for_triangulation(
+        device, C.byref(v1), C.byref(v2), _abi.ptr(hm1), _abi.ptr(hm2), len(fv[0][0]), *[_abi.ptr(x) for x in fv[0]],
+        len(fv[1][0]), *[_abi.ptr(x) for x in fv[1]], _abi.ptr(F), float(epipole[0]), float(epipole[1]), _abi.ptr(sf),
+        _abi.ptr(s2), len(sf), int(bOnlyStereo), int(checkOri), _abi.ptr(m)))
+    return n, m

@@ -278,3 +278,63 @@ def fuse_problem(seed=3, n_kps=1000, n_mp=800, true_frac=0.6, stereo_frac=0.3, W
             "mp_valid": valid, "mp_xyz": np.array(xyz, np.float32), "mp_normal": np.array(nrm, np.float32),
             "mp_min_dist": np.array(mind, np.float32), "mp_max_dist": np.array(maxd, np.float32),
             "mp_desc": np.array(mdesc, np.uint8)}
+
+
+def triangulation_problem(seed=4, n_points=800, extra=150, stereo_frac=0.3, mp_frac=0.3, n_nodes=3000, W=640, H=480):
+    """Synthetic ORBmatcher::SearchForTriangulation input: two keyframes 0.3 m apart viewing
+    n_points 3-D points (each keyframe keeps ~85 % of them, plus `extra` unrelated keypoints);
+    observations = projection + N(0, 0.7 px), octave U{0..7}, descriptors = the point's with
+    U{0..30} bits flipped, angles = the point's plus N(0, 3 deg); vocabulary nodes: a point's
+    features share node (id * 7919) mod n_nodes, extras take random nodes; mp_frac of the
+    keypoints already carry a map point.  F12 = K1^-T [t12]x R12 K2^-1 (LocalMapping::ComputeF12),
+    (ex, ey) = keyframe 1's centre projected into keyframe 2."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    fx, fy, cx, cy = TUM1
+    K = np.array([[fx, 0, cx], [0, fy, cy], [0, 0, 1]], np.float32)
+    R1, t1 = np.eye(3), np.zeros(3)
+    R2 = _rot(np.array([0.0, 0.05, 0.01]))
+    t2 = np.array([-0.3, 0.02, 0.01])
+    pts = np.stack([rng.uniform(-2, 2, n_points), rng.uniform(-1.5, 1.5, n_points), rng.uniform(2, 8, n_points)], 1)
+    base = rng.integers(0, 256, (n_points, 32), dtype=np.uint8)
+    ang = rng.uniform(0, 360, n_points)
+    sf = np.array([np.float32(1.2) ** l for l in range(8)], np.float32)
+    sig2 = (sf * sf).astype(np.float32)
+
+    def kf(R, t):
+        xs, ys, os, ds, us, an, nodes = [], [], [], [], [], [], []
+        keep = rng.random(n_points) < 0.85
+        for i in np.nonzero(keep)[0]:
+            Xc = R @ pts[i] + t
+            u, v = fx * Xc[0] / Xc[2] + cx + rng.normal(0, 0.7), fy * Xc[1] / Xc[2] + cy + rng.normal(0, 0.7)
+            if not (0 <= u < W and 0 <= v < H):
+                continue
+            bits = np.unpackbits(base[i])
+            bits[rng.choice(256, int(rng.integers(0, 31)), replace=False)] ^= 1
+            xs.append(u); ys.append(v); os.append(int(rng.integers(0, 8))); ds.append(np.packbits(bits))
+            us.append(u - KITTI_BF / Xc[2] if rng.random() < stereo_frac else -1.0)
+            an.append((ang[i] + rng.normal(0, 3)) % 360)
+            nodes.append((i * 7919) % n_nodes)
+        for _ in range(extra):
+            xs.append(rng.uniform(0, W)); ys.append(rng.uniform(0, H)); os.append(int(rng.integers(0, 8)))
+            ds.append(rng.integers(0, 256, 32, dtype=np.uint8)); us.append(-1.0); an.append(rng.uniform(0, 360))
+            nodes.append(int(rng.integers(0, n_nodes)))
+        nodes = np.array(nodes)
+        order = np.argsort(nodes, kind="stable")
+        un, starts = np.unique(nodes[order], return_index=True)
+        start = np.append(starts, len(nodes)).astype(np.int32)
+        n = len(xs)
+        return {"x": np.array(xs, np.float32), "y": np.array(ys, np.float32), "octave": np.array(os, np.int32),
+                "angle": np.array(an, np.float32), "desc": np.array(ds, np.uint8), "uright": np.array(us, np.float32),
+                "has_mp": (rng.random(n) < mp_frac).astype(np.uint8), "nodes": un.astype(np.uint32),
+                "start": start, "fidx": order.astype(np.int32), "W": W, "H": H}
+    k1, k2 = kf(R1, t1), kf(R2, t2)
+    R12 = (R1 @ R2.T).astype(np.float32)
+    t12 = (-R1 @ R2.T @ t2 + t1).astype(np.float32)
+    tx = np.array([[0, -t12[2], t12[1]], [t12[2], 0, -t12[0]], [-t12[1], t12[0], 0]], np.float32)
+    Kinv = np.linalg.inv(K.astype(np.float64)).astype(np.float32)
+    F12 = (Kinv.T @ tx @ R12 @ Kinv).astype(np.float32)
+    C1 = -R1.T @ t1
+    C2 = R2 @ C1 + t2
+    ex, ey = np.float32(fx * C2[0] / C2[2] + cx), np.float32(fy * C2[1] / C2[2] + cy)
+    return {"kf1": k1, "kf2": k2, "F12": F12, "ex": float(ex), "ey": float(ey), "scale_factors": sf,
+            "level_sigma2": sig2}

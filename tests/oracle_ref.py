@@ -355,3 +355,18 @@ def fuse(prob, th=3.0):
     lib().oracle_fuse(C.byref(fv.s), C.byref(kp), n, P(a["mp_valid"]), P(a["mp_xyz"]), P(a["mp_normal"]),
                       P(a["mp_min_dist"]), P(a["mp_max_dist"]), P(a["mp_desc"]), C.c_float(th), P(bi), P(bd))
     return bi, bd
+
+
+def search_for_triangulation(p, only_stereo=False, check_ori=True):
+    """oracle_search_for_triangulation on a synth.triangulation_problem: (nmatches, matches12)."""
+    k1, k2 = p["kf1"], p["kf2"]
+    f1 = FrameView(k1, k1["desc"], k1["W"], k1["H"], k1["uright"])
+    f2 = FrameView(k2, k2["desc"], k2["W"], k2["H"], k2["uright"])
+    a = {k: np.ascontiguousarray(v) for k, v in (("F", p["F12"].reshape(-1)), ("sf", p["scale_factors"]),
+                                                 ("s2", p["level_sigma2"]))}
+    m = np.zeros(len(k1["x"]), np.int32)
+    n = lib().oracle_search_for_triangulation(
+        C.byref(f1.s), C.byref(f2.s), P(k1["has_mp"]), P(k2["has_mp"]), len(k1["nodes"]), P(k1["nodes"]),
+        P(k1["start"]), P(k1["fidx"]), len(k2["nodes"]), P(k2["nodes"]), P(k2["start"]), P(k2["fidx"]), P(a["F"]),
+        C.c_float(p["ex"]), C.c_float(p["ey"]), P(a["sf"]), P(a["s2"]), int(only_stereo), int(check_ori), P(m))
+    return n, m
