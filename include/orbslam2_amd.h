@@ -218,6 +218,39 @@ int orb_distinctive_descriptors(int device, const uint8_t* desc, const int32_t* 
 int orb_distinctive_descriptors_device(const uint8_t* d_desc, const int32_t* d_start, int n_points,
                                        int32_t* d_best_idx, uint8_t* d_best_desc, void* stream);
 
+/* DBoW2 ORB vocabulary (ORBVocabulary = TemplatedVocabulary<FORB::TDescriptor, FORB>,
+ * R/include/ORBVocabulary.h; D/DBoW2/TemplatedVocabulary.h m_nodes / m_L) flattened:
+ *   node 0 is the root; desc[i] = m_nodes[i].descriptor (32 B, root's unused);
+ *   children of node i = child_idx[child_start[i] .. child_start[i+1]) in m_nodes[i].children
+ *   order (empty list: leaf); word_id[i] / weight[i] = m_nodes[i].word_id / weight (leaves). */
+typedef struct {
+    int n_nodes;
+    int L;
+    const uint8_t* desc;
+    const int32_t* child_start;
+    const int32_t* child_idx;
+    const int32_t* word_id;
+    const double* weight;
+} orb_vocabulary;
+typedef struct orb_vocab orb_vocab;
+
+/* Uploads the vocabulary once (device-resident handle; the loader / TemplatedVocabulary
+ * constructor stays on the host). */
+int orb_vocabulary_create(int device, const orb_vocabulary* voc, orb_vocab** out);
+void orb_vocabulary_destroy(orb_vocab* h);
+/* TemplatedVocabulary::transform(feature, word_id, weight, &nid, levelsup) —
+ * D/DBoW2/TemplatedVocabulary.h:1242-1283 — for n descriptors ([n][32] B): the per-feature part
+ * of transform(features, BowVector&, FeatureVector&, levelsup) (:1151-1190; ORB-SLAM2 calls it
+ * with levelsup 4 from Frame::ComputeBoW / KeyFrame::ComputeBoW).  node_id = the node passed at
+ * level L - levelsup (0 when that level is <= 0).  The BowVector (weights > 0 summed per word in
+ * feature order, then L1-normalised) and FeatureVector (feature indices per node in feature
+ * order) assembly stays with the caller.  Host buffers. */
+int orb_vocabulary_transform(orb_vocab* h, const uint8_t* desc, int n, int levelsup, int32_t* word_id, double* weight,
+                             int32_t* node_id);
+/* Device-resident form (asynchronous on `stream`, or the handle's stream when NULL). */
+int orb_vocabulary_transform_device(orb_vocab* h, const uint8_t* d_desc, int n, int levelsup, int32_t* d_word_id,
+                                    double* d_weight, int32_t* d_node_id, void* stream);
+
 /* ORBmatcher::SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12,
  * windowSize) — R/src/ORBmatcher.cpp:499-617.  prev_xy (2*F1.n floats) is
  * updated in place; matches12 (F1.n ints) receives the F2 index or -1.

@@ -1471,3 +1471,105 @@ int oracle_search_for_triangulation(const oracle_frame* k1, const oracle_frame* 
     free(matched2);
     return nmatches;
 }
+
+/* TemplatedVocabulary::transform(feature, word_id, weight, &nid, levelsup)
+ * (D/DBoW2/TemplatedVocabulary.h:1242-1283): descend from the root taking, per level, the child
+ * with the least FORB::distance (FORB.cpp:82-103), the first child on ties (the loop starts from
+ * children[0] and replaces only on a strict <), record the node reached at level L - levelsup,
+ * stop at a leaf.  When that level is <= 0 the node id is 0 (:1250); a leaf shallower than it
+ * leaves the reference's nid unassigned — 0 here. */
+void oracle_vocab_transform(const oracle_vocabulary* v, const uint8_t* desc, int n, int levelsup, int32_t* word_id,
+                            double* weight, int32_t* node_id)
+{
+    const int nid_level = v->L - levelsup;
+    for (int i = 0; i < n; i++) {
+        const uint8_t* f = desc + (size_t)i * 32;
+        int final_id = 0, level = 0, nid = 0;
+        while (v->child_start[final_id + 1] > v->child_start[final_id]) {
+            ++level;
+            const int* ch = v->child_idx + v->child_start[final_id];
+            const int nch = v->child_start[final_id + 1] - v->child_start[final_id];
+            int best = ch[0];
+            int best_d = oracle_descriptor_distance(f, v->desc + (size_t)best * 32);
+            for (int c = 1; c < nch; c++) {
+                const int d = oracle_descriptor_distance(f, v->desc + (size_t)ch[c] * 32);
+                if (d < best_d) {
+                    best_d = d;
+                    best = ch[c];
+                }
+            }
+            final_id = best;
+            if (level == nid_level) nid = final_id;
+        }
+        word_id[i] = v->word_id[final_id];
+        weight[i] = v->weight[final_id];
+        node_id[i] = nid;
+    }
+}
+
+typedef struct { int32_t key, feat; } okeyfeat;
+static int cmp_keyfeat(const void* a, const void* b)
+{
+    const okeyfeat* x = (const okeyfeat*)a;
+    const okeyfeat* y = (const okeyfeat*)b;
+    if (x->key != y->key) return x->key < y->key ? -1 : 1;
+    return x->feat < y->feat ? -1 : (x->feat > y->feat);
+}
+
+/* transform(features, BowVector&, FeatureVector&, levelsup), TF_IDF + L1
+ * (TemplatedVocabulary.h:1151-1190): features with weight > 0 add their weight to the word's
+ * entry (BowVector::addWeight — in feature order, so a (word, feature)-sorted pass sums in that
+ * same order) and their index to the node's list (FeatureVector::addFeature); then
+ * BowVector::normalize(L1): the |value| sum in ascending word order, each value divided by it. */
+int oracle_bow_transform(const oracle_vocabulary* v, const uint8_t* desc, int n, int levelsup, int32_t* bow_words,
+                         double* bow_values, int32_t* fv_nodes, int32_t* fv_start, int32_t* fv_idx, int* n_fv)
+{
+    int32_t* wid = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+    int32_t* nid = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+    double* w = (double*)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+    okeyfeat* kw = (okeyfeat*)malloc(sizeof(okeyfeat) * (size_t)(n > 0 ? n : 1));
+    okeyfeat* kn = (okeyfeat*)malloc(sizeof(okeyfeat) * (size_t)(n > 0 ? n : 1));
+    oracle_vocab_transform(v, desc, n, levelsup, wid, w, nid);
+    int m = 0;
+    for (int i = 0; i < n; i++)
+        if (w[i] > 0) {
+            kw[m].key = wid[i];
+            kw[m].feat = i;
+            kn[m].key = nid[i];
+            kn[m].feat = i;
+            m++;
+        }
+    qsort(kw, (size_t)m, sizeof(okeyfeat), cmp_keyfeat);
+    qsort(kn, (size_t)m, sizeof(okeyfeat), cmp_keyfeat);
+    int nw = 0;
+    for (int k = 0; k < m; k++) {
+        if (nw > 0 && bow_words[nw - 1] == kw[k].key) {
+            bow_values[nw - 1] += w[kw[k].feat];
+        } else {
+            bow_words[nw] = kw[k].key;
+            bow_values[nw] = w[kw[k].feat];
+            nw++;
+        }
+    }
+    double norm = 0.0;
+    for (int k = 0; k < nw; k++) norm += fabs(bow_values[k]);
+    if (norm > 0.0)
+        for (int k = 0; k < nw; k++) bow_values[k] /= norm;
+    int nf = 0;
+    for (int k = 0; k < m; k++) {
+        if (nf == 0 || fv_nodes[nf - 1] != kn[k].key) {
+            fv_nodes[nf] = kn[k].key;
+            fv_start[nf] = k;
+            nf++;
+        }
+        fv_idx[k] = kn[k].feat;
+    }
+    fv_start[nf] = m;
+    *n_fv = nf;
+    free(wid);
+    free(nid);
+    free(w);
+    free(kw);
+    free(kn);
+    return nw;
+}

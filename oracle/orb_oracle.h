@@ -195,6 +195,32 @@ int oracle_search_for_triangulation(const oracle_frame* k1, const oracle_frame* 
                                     const float* scale_factors2, const float* level_sigma2, int only_stereo,
                                     int check_ori, int32_t* matches12);
 
+/* DBoW2 vocabulary (TemplatedVocabulary<FORB::TDescriptor, FORB>) flattened: node 0 = root;
+ * children of node i = child_idx[child_start[i] .. child_start[i+1]) in m_nodes[i].children
+ * order; word_id / weight per node (leaves). */
+typedef struct {
+    int n_nodes;
+    int L;
+    const uint8_t* desc;
+    const int32_t* child_start;
+    const int32_t* child_idx;
+    const int32_t* word_id;
+    const double* weight;
+} oracle_vocabulary;
+
+/* TemplatedVocabulary::transform(feature, word_id, weight, &nid, levelsup)
+ * (D/DBoW2/TemplatedVocabulary.h:1242-1283) for n descriptors. */
+void oracle_vocab_transform(const oracle_vocabulary* v, const uint8_t* desc, int n, int levelsup, int32_t* word_id,
+                            double* weight, int32_t* node_id);
+
+/* TemplatedVocabulary::transform(features, BowVector&, FeatureVector&, levelsup) for the TF_IDF /
+ * L1 configuration ORB-SLAM2 loads (ORBvoc.txt header "10 6 0 0"; :1151-1190, BowVector.cpp
+ * addWeight / normalize(L1), FeatureVector.cpp addFeature).  Outputs in std::map order:
+ * bow_words / bow_values (n_words), fv_nodes (n_fv) with fv_start[n_fv + 1] into fv_idx.
+ * Each output array holds at most n entries.  Returns n_words; *n_fv receives the node count. */
+int oracle_bow_transform(const oracle_vocabulary* v, const uint8_t* desc, int n, int levelsup, int32_t* bow_words,
+                         double* bow_values, int32_t* fv_nodes, int32_t* fv_start, int32_t* fv_idx, int* n_fv);
+
 #ifdef __cplusplus
 }
 #endif

@@ -7,3 +7,4 @@ from .matcher import ORBmatcher, Frame, LocalMapPoints, ComputeDistinctiveDescri
     SearchForTriangulation  # noqa: F401
 from .optimizer import Optimizer, LocalBA, PoseOptimization  # noqa: F401
 from .stereo import ComputeStereoMatches  # noqa: F401
+from .vocabulary import ORBVocabulary  # noqa: F401

@@ -14,7 +14,7 @@ PKG = pathlib.Path(__file__).resolve().parent
 CSRC = PKG / "csrc"
 LIB_DIR = PKG / "lib"
 LIB = LIB_DIR / "liborbslam2_amd.so"
-SOURCES = ["extractor.hip", "matcher.hip", "lba.hip", "pose.hip"]
+SOURCES = ["extractor.hip", "matcher.hip", "lba.hip", "pose.hip", "bow.hip"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
          "-Wall", "-Wno-unused-function", "-Wno-unused-result"]
 

@@ -338,3 +338,63 @@ def triangulation_problem(seed=4, n_points=800, extra=150, stereo_frac=0.3, mp_f
     ex, ey = np.float32(fx * C2[0] / C2[2] + cx), np.float32(fy * C2[1] / C2[2] + cy)
     return {"kf1": k1, "kf2": k2, "F12": F12, "ex": float(ex), "ey": float(ey), "scale_factors": sf,
             "level_sigma2": sig2}
+
+
+def vocabulary(k=10, L=4, seed=7, early_leaf=0.08, stop_frac=0.05, dup_frac=0.03):
+    """A synthetic DBoW2 ORB vocabulary in loader node order (breadth first): (parent, is_leaf,
+    desc, weight), entry 0 the root.  Children perturb their parent's descriptor (~1/8 of the
+    bits flipped; the root's children are random), so descents are meaningful; a fraction of
+    inner nodes stop early (leaves at uneven depth), duplicate their previous sibling's
+    descriptor (ties: the first child wins) or carry weight 0 (stopped words).  k=10, L=6 has
+    the 10^6-word shape of ORBvoc.txt."""
+    rng = np.random.default_rng(seed)
+    parent = [np.zeros(1, np.int64)]
+    leaf = [np.zeros(1, bool)]
+    desc = [np.zeros((1, 32), np.uint8)]
+    frontier = np.zeros(1, np.int64)           # node ids expanded at the next level
+    fdesc = np.zeros((1, 32), np.uint8)
+    n = 1
+    for depth in range(1, L + 1):
+        m = len(frontier)
+        if m == 0:
+            break
+        par = np.repeat(frontier, k)
+        pd = np.repeat(fdesc, k, axis=0)
+        if depth == 1:
+            d = rng.integers(0, 256, (m * k, 32), dtype=np.uint8)
+        else:
+            flip = (rng.integers(0, 256, (m * k, 32), dtype=np.uint8) & rng.integers(0, 256, (m * k, 32), dtype=np.uint8)
+                    & rng.integers(0, 256, (m * k, 32), dtype=np.uint8))
+            d = pd ^ flip
+        dup = rng.random(m * k) < dup_frac
+        dup[::k] = False
+        d[dup] = d[np.flatnonzero(dup) - 1]
+        is_leaf = np.full(m * k, depth == L)
+        if depth < L and depth >= 2:
+            is_leaf |= rng.random(m * k) < early_leaf
+        ids = np.arange(n, n + m * k, dtype=np.int64)
+        parent.append(par)
+        leaf.append(is_leaf)
+        desc.append(d)
+        n += m * k
+        frontier = ids[~is_leaf]
+        fdesc = d[~is_leaf]
+    parent = np.concatenate(parent)
+    leaf = np.concatenate(leaf)
+    desc = np.concatenate(desc)
+    weight = np.where(leaf, rng.uniform(0.5, 9.0, n), 0.0)
+    weight[leaf & (rng.random(n) < stop_frac)] = 0.0
+    return parent, leaf, desc, weight
+
+
+def bow_features(voc_desc, voc_leaf, n, seed=11, random_frac=0.1):
+    """n query descriptors: leaf descriptors with ~1/8 of the bits flipped, a fraction uniform
+    random."""
+    rng = np.random.default_rng(seed)
+    leaves = np.flatnonzero(voc_leaf)
+    f = voc_desc[rng.choice(leaves, n)].copy()
+    f ^= (rng.integers(0, 256, (n, 32), dtype=np.uint8) & rng.integers(0, 256, (n, 32), dtype=np.uint8)
+          & rng.integers(0, 256, (n, 32), dtype=np.uint8))
+    r = rng.random(n) < random_frac
+    f[r] = rng.integers(0, 256, (int(r.sum()), 32), dtype=np.uint8)
+    return f

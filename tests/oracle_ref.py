@@ -370,3 +370,65 @@ def search_for_triangulation(p, only_stereo=False, check_ori=True):
         P(k1["start"]), P(k1["fidx"]), len(k2["nodes"]), P(k2["nodes"]), P(k2["start"]), P(k2["fidx"]), P(a["F"]),
         C.c_float(p["ex"]), C.c_float(p["ey"]), P(a["sf"]), P(a["s2"]), int(only_stereo), int(check_ori), P(m))
     return n, m
+
+
+class Vocabulary(C.Structure):
+    _fields_ = [("n_nodes", C.c_int), ("L", C.c_int), ("desc", C.c_void_p), ("child_start", C.c_void_p),
+                ("child_idx", C.c_void_p), ("word_id", C.c_void_p), ("weight", C.c_void_p)]
+
+
+def flatten_vocabulary(parent, is_leaf, desc, weight):
+    """Loader node order -> (child_start, child_idx, word_id): each node appended to its parent's
+    children in node order, word ids to leaves in node order (TemplatedVocabulary.h:1362-1450)."""
+    parent = np.asarray(parent, np.int64)
+    n = len(parent)
+    children = [[] for _ in range(n)]
+    for i in range(1, n):
+        children[int(parent[i])].append(i)
+    start = np.zeros(n + 1, np.int32)
+    start[1:] = np.cumsum([len(c) for c in children])
+    idx = np.array([c for ch in children for c in ch], np.int32)
+    wid = np.zeros(n, np.int32)
+    nw = 0
+    for i in range(1, n):
+        if is_leaf[i]:
+            wid[i] = nw
+            nw += 1
+    return start, idx, wid
+
+
+class OracleVocabulary:
+    def __init__(self, parent, is_leaf, desc, weight, L):
+        self.start, self.idx, self.wid = flatten_vocabulary(parent, is_leaf, desc, weight)
+        self.desc = np.ascontiguousarray(desc, np.uint8)
+        self.weight = np.ascontiguousarray(weight, np.float64)
+        self.s = Vocabulary(len(self.wid), L, P(self.desc), P(self.start), P(self.idx), P(self.wid), P(self.weight))
+
+
+def vocab_transform(voc, features, levelsup):
+    """oracle_vocab_transform: per-feature (word id, weight, node id at level L - levelsup)."""
+    f = np.ascontiguousarray(np.asarray(features, np.uint8).reshape(-1, 32))
+    n = len(f)
+    wid = np.zeros(n, np.int32)
+    w = np.zeros(n, np.float64)
+    nid = np.zeros(n, np.int32)
+    lib().oracle_vocab_transform(C.byref(voc.s), P(f), n, levelsup, P(wid), P(w), P(nid))
+    return wid, w, nid
+
+
+def bow_transform(voc, features, levelsup):
+    """oracle_bow_transform (TF_IDF, L1): (BowVector dict, FeatureVector dict) in map order."""
+    f = np.ascontiguousarray(np.asarray(features, np.uint8).reshape(-1, 32))
+    n = len(f)
+    m = max(n, 1)
+    words = np.zeros(m, np.int32)
+    vals = np.zeros(m, np.float64)
+    nodes = np.zeros(m, np.int32)
+    start = np.zeros(m + 1, np.int32)
+    idx = np.zeros(m, np.int32)
+    nf = C.c_int(0)
+    nw = lib().oracle_bow_transform(C.byref(voc.s), P(f), n, levelsup, P(words), P(vals), P(nodes), P(start), P(idx),
+                                    C.byref(nf))
+    bow = {int(words[i]): float(vals[i]) for i in range(nw)}
+    fv = {int(nodes[i]): [int(x) for x in idx[start[i]:start[i + 1]]] for i in range(nf.value)}
+    return bow, fv
