@@ -354,6 +354,7 @@ def bench_extras(args, amd, dev):
                              "matches_per_pair": float(nm.float().mean())}
     out["batch_sweep_640x480"] = batch_sweep(amd, dev, m)
     out["pose_optimization"] = bench_pose(args, amd, dev)
+    out["bow_transform"] = bench_bow(args, amd, dev)
     return out
 
 
@@ -409,6 +410,63 @@ def bench_pose(args, amd, dev, n_frames=256, n_points=600):
         out["cpu_baseline"] = {"frames_per_s": round(len(sample) / dc, 1), "cores": threads, "kind": "port",
                                "sample": f"{len(sample)} frames, oracle C restatement of PoseOptimization, "
                                          f"1 frame per thread"}
+    return out
+
+
+def bench_bow(args, amd, dev, n_frames=64, n_feat=1000):
+    """SURVEY §8f-4: DBoW2 TemplatedVocabulary::transform (ComputeBoW, levelsup 4) for a batch of
+    frames' descriptors resident in HBM against a synthetic vocabulary of the ORBvoc.txt shape
+    (k=10, L=6, 10^6 words, 35.6 MB of node descriptors); against the oracle C restatement."""
+    from orb_slam2_amd import synth, _abi
+    parent, leaf, desc, weight = synth.vocabulary(k=10, L=6, seed=7, early_leaf=0.0, dup_frac=0.0)
+    voc = amd.ORBVocabulary.from_nodes(parent, leaf, desc, weight, k=10, L=6)
+    n = n_frames * n_feat
+    feats = synth.bow_features(desc, leaf, n, seed=13)
+    d_f = torch.from_numpy(feats).to(dev)
+    d_w = torch.zeros(n, dtype=torch.int32, device=dev)
+    d_g = torch.zeros(n, dtype=torch.float64, device=dev)
+    d_n = torch.zeros(n, dtype=torch.int32, device=dev)
+    lib = _abi.lib()
+    lib.orb_vocabulary_transform_device.argtypes = [C.c_void_p] * 2 + [C.c_int, C.c_int] + [C.c_void_p] * 4
+    lib.orb_vocabulary_transform_device.restype = C.c_int
+    h = voc._handle()
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    dp = lambda x: C.c_void_p(x.data_ptr())   # noqa: E731
+
+    def run():
+        _abi.check("bow", lib.orb_vocabulary_transform_device(h, dp(d_f), n, 4, dp(d_w), dp(d_g), dp(d_n),
+                                                              C.c_void_p(stream)))
+    for _ in range(3):
+        run()
+    torch.cuda.synchronize(dev)
+    reps = 20
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        run()
+    e1.record()
+    torch.cuda.synchronize(dev)
+    dt = e0.elapsed_time(e1) / 1e3 / reps
+    # bytes a descriptor touches: its 32 B in, per level one 8 B (first child, count) record and 10
+    # adjacent 32 B child descriptors, 4 + 8 + 4 B word / weight / node id out plus the 4 B node map
+    per = 32 + 6 * (8 + 10 * 32) + 20
+    out = {"descriptors_per_s": round(n / dt, 1), "frames_per_s": round(n_frames / dt, 1),
+           "ms_per_batch": round(dt * 1e3, 4), "frames_per_batch": n_frames, "descriptors_per_frame": n_feat,
+           "vocabulary": "k=10 L=6, 1111111 nodes, 10^6 words (synthetic, ORBvoc.txt shape)",
+           "touched_GBps": round(n * per / dt / 1e9, 1), "touched_bytes_per_descriptor": per}
+    if not args.no_cpu:
+        sys.path.insert(0, str(ROOT / "tests"))
+        import oracle_ref as O
+        ov = O.OracleVocabulary(parent, leaf, desc, weight, 6)
+        m = 20000
+        t0 = time.perf_counter()
+        rw, _, _ = O.vocab_transform(ov, feats[:m], 4)
+        dc = time.perf_counter() - t0
+        ok = bool(np.array_equal(rw, d_w[:m].cpu().numpy()))
+        out["cpu_baseline"] = {"descriptors_per_s": round(m / dc, 1), "cores": 1, "kind": "port",
+                               "sample": f"{m} descriptors, oracle C restatement of transform, 1 thread",
+                               "word_ids_match": ok}
+    del voc
     return out
 
 

@@ -247,7 +247,7 @@ void orb_vocabulary_destroy(orb_vocab* h);
  * order) assembly stays with the caller.  Host buffers. */
 int orb_vocabulary_transform(orb_vocab* h, const uint8_t* desc, int n, int levelsup, int32_t* word_id, double* weight,
                              int32_t* node_id);
-/* Device-resident form (asynchronous on `stream`, or the handle's stream when NULL). */
+/* Device-resident form (asynchronous on `stream`; NULL is the null stream). */
 int orb_vocabulary_transform_device(orb_vocab* h, const uint8_t* d_desc, int n, int levelsup, int32_t* d_word_id,
                                     double* d_weight, int32_t* d_node_id, void* stream);
 

@@ -17,14 +17,24 @@
 
 namespace orbamd {
 
+// Device layout: the tree renumbered breadth first, so the children of every node are one
+// contiguous run of node records (their 32-byte descriptors adjacent in HBM, one 2-int record
+// (first child, count) per node); orig maps back to the caller's node ids for the FeatureVector.
 struct VocDev {
-    const uint4* desc;         // [n][2]
-    const int32_t* cstart;     // [n + 1]
-    const int32_t* cidx;
+    const uint4* desc;         // [n][2], breadth-first order
+    const int2* fc;            // [n] (first child, child count)
     const int32_t* word;       // [n]
     const double* weight;      // [n]
+    const int32_t* orig;       // [n] caller's node id
     int L;
 };
+
+constexpr int kBowChunk = 10;   // children compared per batch of independent loads (k = 10 in ORBvoc)
+
+__device__ __forceinline__ int hamming256(uint4 a0, uint4 a1, uint4 b0, uint4 b1) {
+    return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+           __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
 
 __global__ __launch_bounds__(256) void k_bow_transform(VocDev v, const uint4* __restrict__ feats, int n, int levelsup,
                                                        int32_t* __restrict__ word_id, double* __restrict__ weight,
@@ -33,25 +43,34 @@ __global__ __launch_bounds__(256) void k_bow_transform(VocDev v, const uint4* __
     if (i >= n) return;
     const uint4 a0 = feats[2 * i], a1 = feats[2 * i + 1];
     const int nid_level = v.L - levelsup;
-    int nid = 0, node = 0, level = 0;
+    int nid = -1, node = 0, level = 0;
     for (;;) {
-        const int c0 = v.cstart[node], c1 = v.cstart[node + 1];
-        if (c0 == c1) break;   // isLeaf
+        const int2 fc = v.fc[node];
+        if (fc.y == 0) break;   // isLeaf
         ++level;
-        int best = c0, bestD = 0x7fffffff;
-        for (int c = c0; c < c1; c++) {
-            const int id = v.cidx[c];
-            const uint4 b0 = v.desc[2 * id], b1 = v.desc[2 * id + 1];
-            const int d = __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
-                          __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
-            if (d < bestD) { bestD = d; best = id; }
+        int best = fc.x, bestD = 0x7fffffff;
+        for (int base = 0; base < fc.y; base += kBowChunk) {
+            // a chunk's loads are issued together; indices past the last child repeat it, which
+            // cannot win under the strict < (the reference's first-child-wins tie rule)
+            uint4 b[2 * kBowChunk];
+#pragma unroll
+            for (int j = 0; j < kBowChunk; j++) {
+                const int id = fc.x + min(base + j, fc.y - 1);
+                b[2 * j] = v.desc[2 * id];
+                b[2 * j + 1] = v.desc[2 * id + 1];
+            }
+#pragma unroll
+            for (int j = 0; j < kBowChunk; j++) {
+                const int d = hamming256(a0, a1, b[2 * j], b[2 * j + 1]);
+                if (d < bestD) { bestD = d; best = fc.x + min(base + j, fc.y - 1); }
+            }
         }
         node = best;
         if (level == nid_level) nid = node;
     }
     word_id[i] = v.word[node];
     weight[i] = v.weight[node];
-    node_id[i] = nid;
+    node_id[i] = nid < 0 ? 0 : v.orig[nid];
 }
 
 }  // namespace orbamd
@@ -83,15 +102,40 @@ int orb_vocabulary_create(int device, const orb_vocabulary* voc, orb_vocab** out
         if (voc->child_idx[c] <= 0 || voc->child_idx[c] >= n) return ORB_EINVAL;
     int st = check_device(device);
     if (st) return st;
+    // breadth-first renumbering: children of each node become consecutive ids in their order
+    std::vector<int32_t> orig(n), renum(n, -1);
+    std::vector<int2> fc(n);
+    orig[0] = 0;
+    renum[0] = 0;
+    int next = 1;
+    for (int q = 0; q < next; q++) {
+        const int o = orig[q];
+        const int c0 = voc->child_start[o], c1 = voc->child_start[o + 1];
+        fc[q] = make_int2(next, c1 - c0);
+        for (int c = c0; c < c1; c++) {
+            const int ch = voc->child_idx[c];
+            if (renum[ch] >= 0 || next >= n) return ORB_EINVAL;   // not a tree
+            renum[ch] = next;
+            orig[next++] = ch;
+        }
+    }
+    std::vector<uint8_t> desc((size_t)next * 32);
+    std::vector<int32_t> word(next);
+    std::vector<double> weight(next);
+    for (int q = 0; q < next; q++) {
+        memcpy(&desc[(size_t)q * 32], voc->desc + (size_t)orig[q] * 32, 32);
+        word[q] = voc->word_id[orig[q]];
+        weight[q] = voc->weight[orig[q]];
+    }
     ORB_HIP_TRY(hipSetDevice(device));
     orb_vocab* h = new orb_vocab();
     h->device = device;
-    h->n_nodes = n;
+    h->n_nodes = next;
     h->L = voc->L;
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    const size_t bD = al((size_t)n * 32), bS = al(((size_t)n + 1) * 4), bC = al((size_t)nc * 4 + 4), bW = al((size_t)n * 4),
-                 bG = al((size_t)n * 8);
-    if (hipMalloc(&h->base, bD + bS + bC + bW + bG) != hipSuccess) { delete h; return ORB_ENOMEM; }
+    const size_t bD = al((size_t)next * 32), bF = al((size_t)next * 8), bW = al((size_t)next * 4),
+                 bG = al((size_t)next * 8), bO = al((size_t)next * 4);
+    if (hipMalloc(&h->base, bD + bF + bW + bG + bO) != hipSuccess) { delete h; return ORB_ENOMEM; }
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
         (void)hipFree(h->base);
         delete h;
@@ -101,14 +145,14 @@ int orb_vocabulary_create(int device, const orb_vocabulary* voc, orb_vocab** out
     auto put = [&](const void* src, size_t bytes, size_t cap) {
         char* r = c;
         c += cap;
-        if (bytes) (void)hipMemcpyAsync(r, src, bytes, hipMemcpyHostToDevice, h->stream);
+        (void)hipMemcpyAsync(r, src, bytes, hipMemcpyHostToDevice, h->stream);
         return r;
     };
-    h->v.desc = (const uint4*)put(voc->desc, (size_t)n * 32, bD);
-    h->v.cstart = (const int32_t*)put(voc->child_start, ((size_t)n + 1) * 4, bS);
-    h->v.cidx = (const int32_t*)put(voc->child_idx, (size_t)nc * 4, bC);
-    h->v.word = (const int32_t*)put(voc->word_id, (size_t)n * 4, bW);
-    h->v.weight = (const double*)put(voc->weight, (size_t)n * 8, bG);
+    h->v.desc = (const uint4*)put(desc.data(), (size_t)next * 32, bD);
+    h->v.fc = (const int2*)put(fc.data(), (size_t)next * 8, bF);
+    h->v.word = (const int32_t*)put(word.data(), (size_t)next * 4, bW);
+    h->v.weight = (const double*)put(weight.data(), (size_t)next * 8, bG);
+    h->v.orig = (const int32_t*)put(orig.data(), (size_t)next * 4, bO);
     h->v.L = voc->L;
     if (hipStreamSynchronize(h->stream) != hipSuccess) { orb_vocabulary_destroy(h); return ORB_EGPU; }
     *out = h;
@@ -130,7 +174,7 @@ int orb_vocabulary_transform_device(orb_vocab* h, const uint8_t* d_desc, int n, 
     if (!h || n < 0 || (n > 0 && (!d_desc || !d_word_id || !d_weight || !d_node_id))) return ORB_EINVAL;
     if (n == 0) return ORB_OK;
     ORB_HIP_TRY(hipSetDevice(h->device));
-    hipLaunchKernelGGL(k_bow_transform, dim3((n + 255) / 256), dim3(256), 0, stream ? (hipStream_t)stream : h->stream,
+    hipLaunchKernelGGL(k_bow_transform, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
                        h->v, reinterpret_cast<const uint4*>(d_desc), n, levelsup, d_word_id, d_weight, d_node_id);
     ORB_HIP_TRY(hipGetLastError());
     return ORB_OK;
