@@ -207,6 +207,30 @@ int orb_search_for_triangulation(int device, const orb_frame_view* kf1, const or
                                  const float* scale_factors2, const float* level_sigma2, int n_levels2, int only_stereo,
                                  int check_ori, int32_t* matches12);
 
+/* ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>& vpMapPointMatches) —
+ * R/src/ORBmatcher.cpp:220-372 (Tracking::TrackReferenceKeyFrame, Relocalization).
+ *   kf / f: the keyframe (mvKeysUn, mDescriptors) and the frame (mvKeys angles, mDescriptors)
+ *   as frame views; kf_ok[i] != 0 when GetMapPointMatches()[i] is set and not bad;
+ *   mFeatVec of each: n_nodes ascending node ids, CSR start[n_nodes + 1] into feature indices;
+ *   nn_ratio = mfNNratio, check_ori = mbCheckOrientation.
+ * matches_f (f->n ints) receives, per frame feature, the keyframe feature whose map point it
+ * matched (vpMapPointMatches[j] = vpMapPointsKF[matches_f[j]]) or -1.  Returns nmatches;
+ * ORB_E2BIG when a node holds more than 2048 frame features.  Host buffers. */
+int orb_search_by_bow_frame(int device, const orb_frame_view* kf, const uint8_t* kf_ok, int n_nodes_kf,
+                            const uint32_t* nodes_kf, const int32_t* start_kf, const int32_t* fidx_kf,
+                            const orb_frame_view* f, int n_nodes_f, const uint32_t* nodes_f, const int32_t* start_f,
+                            const int32_t* fidx_f, float nn_ratio, int check_ori, int32_t* matches_f);
+
+/* ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& vpMatches12) —
+ * R/src/ORBmatcher.cpp:632-760 (LoopClosing::ComputeSim3).  okN[i] != 0 when keyframe N's map
+ * point i is set and not bad.  matches12 (kf1->n ints) receives the keyframe-2 feature whose map
+ * point becomes vpMatches12[i], or -1.  Returns nmatches.  Host buffers. */
+int orb_search_by_bow_kf(int device, const orb_frame_view* kf1, const uint8_t* ok1, int n_nodes1,
+                         const uint32_t* nodes1, const int32_t* start1, const int32_t* fidx1,
+                         const orb_frame_view* kf2, const uint8_t* ok2, int n_nodes2, const uint32_t* nodes2,
+                         const int32_t* start2, const int32_t* fidx2, float nn_ratio, int check_ori,
+                         int32_t* matches12);
+
 /* MapPoint::ComputeDistinctiveDescriptors (R/src/MapPoint.cpp:306-385) for n_points map points:
  * point m's descriptors (one per observation by a non-bad keyframe, in mObservations order) are
  * rows [start[m], start[m+1]) of desc (32 B each).  best_idx[m] = index within the point's list

@@ -1573,3 +1573,151 @@ int oracle_bow_transform(const oracle_vocabulary* v, const uint8_t* desc, int n,
     free(kn);
     return nw;
 }
+
+/* std::map::lower_bound over an ascending node-id array. */
+static int fv_lower_bound(const uint32_t* nodes, int n, uint32_t key)
+{
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) / 2;
+        if (nodes[mid] < key) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+/* R/src/ORBmatcher.cpp:220-372, literally: the lower_bound walk over both feature vectors, per
+ * common node every keyframe feature with a good map point in list order takes the running
+ * (bestDist1, bestIdxF, bestDist2) over the node's not yet matched frame features; kept when
+ * bestDist1 <= TH_LOW and bestDist1 < mfNNratio * bestDist2 (floats); rotation histogram keyed
+ * by the frame feature, ComputeThreeMaxima, matches outside the three bins dropped. */
+int oracle_search_by_bow_frame(const oracle_frame* kf, const uint8_t* kf_ok, int n1, const uint32_t* nodes1,
+                               const int32_t* start1, const int32_t* idx1, const oracle_frame* f, int n2,
+                               const uint32_t* nodes2, const int32_t* start2, const int32_t* idx2, float nnratio,
+                               int check_ori, int32_t* matches_f)
+{
+    int* hist = (int*)malloc(sizeof(int) * HISTO_LENGTH * (size_t)(f->n + 1));
+    int hsize[HISTO_LENGTH] = {0};
+    for (int j = 0; j < f->n; j++) matches_f[j] = -1;
+    int nmatches = 0;
+    int a = 0, b = 0;
+    while (a < n1 && b < n2) {
+        if (nodes1[a] == nodes2[b]) {
+            for (int p = start1[a]; p < start1[a + 1]; p++) {
+                const int realIdxKF = idx1[p];
+                if (!kf_ok[realIdxKF]) continue;
+                const uint8_t* dKF = kf->desc + (size_t)realIdxKF * 32;
+                int bestDist1 = 256, bestIdxF = -1, bestDist2 = 256;
+                for (int q = start2[b]; q < start2[b + 1]; q++) {
+                    const int realIdxF = idx2[q];
+                    if (matches_f[realIdxF] >= 0) continue;
+                    const int dist = oracle_descriptor_distance(dKF, f->desc + (size_t)realIdxF * 32);
+                    if (dist < bestDist1) {
+                        bestDist2 = bestDist1;
+                        bestDist1 = dist;
+                        bestIdxF = realIdxF;
+                    } else if (dist < bestDist2) {
+                        bestDist2 = dist;
+                    }
+                }
+                if (bestDist1 <= TH_LOW) {
+                    if ((float)bestDist1 < nnratio * (float)bestDist2) {
+                        matches_f[bestIdxF] = realIdxKF;
+                        if (check_ori) {
+                            const int bin = rot_bin(kf->angle[realIdxKF] - f->angle[bestIdxF]);
+                            hist[(size_t)bin * (f->n + 1) + hsize[bin]++] = bestIdxF;
+                        }
+                        nmatches++;
+                    }
+                }
+            }
+            a++;
+            b++;
+        } else if (nodes1[a] < nodes2[b]) {
+            a = fv_lower_bound(nodes1, n1, nodes2[b]);
+        } else {
+            b = fv_lower_bound(nodes2, n2, nodes1[a]);
+        }
+    }
+    if (check_ori) {
+        int i1, i2, i3;
+        three_maxima(hsize, &i1, &i2, &i3);
+        for (int i = 0; i < HISTO_LENGTH; i++) {
+            if (i == i1 || i == i2 || i == i3) continue;
+            for (int j = 0; j < hsize[i]; j++) {
+                matches_f[hist[(size_t)i * (f->n + 1) + j]] = -1;
+                nmatches--;
+            }
+        }
+    }
+    free(hist);
+    return nmatches;
+}
+
+/* R/src/ORBmatcher.cpp:632-760, literally: as above with both sides keyframes — candidates need
+ * a good map point and !vbMatched2, bestDist1 < TH_LOW (strict), histogram keyed by idx1. */
+int oracle_search_by_bow_kf(const oracle_frame* k1, const uint8_t* ok1, int n1, const uint32_t* nodes1,
+                            const int32_t* start1, const int32_t* idx1, const oracle_frame* k2, const uint8_t* ok2,
+                            int n2, const uint32_t* nodes2, const int32_t* start2, const int32_t* idx2, float nnratio,
+                            int check_ori, int32_t* matches12)
+{
+    int* hist = (int*)malloc(sizeof(int) * HISTO_LENGTH * (size_t)(k1->n + 1));
+    uint8_t* matched2 = (uint8_t*)calloc((size_t)k2->n + 1, 1);
+    int hsize[HISTO_LENGTH] = {0};
+    for (int i = 0; i < k1->n; i++) matches12[i] = -1;
+    int nmatches = 0;
+    int a = 0, b = 0;
+    while (a < n1 && b < n2) {
+        if (nodes1[a] == nodes2[b]) {
+            for (int p = start1[a]; p < start1[a + 1]; p++) {
+                const int i1 = idx1[p];
+                if (!ok1[i1]) continue;
+                const uint8_t* d1 = k1->desc + (size_t)i1 * 32;
+                int bestDist1 = 256, bestIdx2 = -1, bestDist2 = 256;
+                for (int q = start2[b]; q < start2[b + 1]; q++) {
+                    const int i2 = idx2[q];
+                    if (matched2[i2] || !ok2[i2]) continue;
+                    const int dist = oracle_descriptor_distance(d1, k2->desc + (size_t)i2 * 32);
+                    if (dist < bestDist1) {
+                        bestDist2 = bestDist1;
+                        bestDist1 = dist;
+                        bestIdx2 = i2;
+                    } else if (dist < bestDist2) {
+                        bestDist2 = dist;
+                    }
+                }
+                if (bestDist1 < TH_LOW) {
+                    if ((float)bestDist1 < nnratio * (float)bestDist2) {
+                        matches12[i1] = bestIdx2;
+                        matched2[bestIdx2] = 1;
+                        if (check_ori) {
+                            const int bin = rot_bin(k1->angle[i1] - k2->angle[bestIdx2]);
+                            hist[(size_t)bin * (k1->n + 1) + hsize[bin]++] = i1;
+                        }
+                        nmatches++;
+                    }
+                }
+            }
+            a++;
+            b++;
+        } else if (nodes1[a] < nodes2[b]) {
+            a = fv_lower_bound(nodes1, n1, nodes2[b]);
+        } else {
+            b = fv_lower_bound(nodes2, n2, nodes1[a]);
+        }
+    }
+    if (check_ori) {
+        int i1, i2, i3;
+        three_maxima(hsize, &i1, &i2, &i3);
+        for (int i = 0; i < HISTO_LENGTH; i++) {
+            if (i == i1 || i == i2 || i == i3) continue;
+            for (int j = 0; j < hsize[i]; j++) {
+                matches12[hist[(size_t)i * (k1->n + 1) + j]] = -1;
+                nmatches--;
+            }
+        }
+    }
+    free(hist);
+    free(matched2);
+    return nmatches;
+}

@@ -221,6 +221,21 @@ void oracle_vocab_transform(const oracle_vocabulary* v, const uint8_t* desc, int
 int oracle_bow_transform(const oracle_vocabulary* v, const uint8_t* desc, int n, int levelsup, int32_t* bow_words,
                          double* bow_values, int32_t* fv_nodes, int32_t* fv_start, int32_t* fv_idx, int* n_fv);
 
+/* ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&) (R/src/ORBmatcher.cpp:220-372):
+ * kf_ok[i] = the keyframe's map point i is set and not bad; matches_f[j] = keyframe feature
+ * matched to frame feature j or -1.  Returns nmatches. */
+int oracle_search_by_bow_frame(const oracle_frame* kf, const uint8_t* kf_ok, int n1, const uint32_t* nodes1,
+                               const int32_t* start1, const int32_t* idx1, const oracle_frame* f, int n2,
+                               const uint32_t* nodes2, const int32_t* start2, const int32_t* idx2, float nnratio,
+                               int check_ori, int32_t* matches_f);
+
+/* ORBmatcher::SearchByBoW(KeyFrame*, KeyFrame*, vector<MapPoint*>&) (R/src/ORBmatcher.cpp:632-760):
+ * matches12[i] = keyframe-2 feature matched to keyframe-1 feature i or -1.  Returns nmatches. */
+int oracle_search_by_bow_kf(const oracle_frame* k1, const uint8_t* ok1, int n1, const uint32_t* nodes1,
+                            const int32_t* start1, const int32_t* idx1, const oracle_frame* k2, const uint8_t* ok2,
+                            int n2, const uint32_t* nodes2, const int32_t* start2, const int32_t* idx2, float nnratio,
+                            int check_ori, int32_t* matches12);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1294,6 +1294,57 @@ __global__ __launch_bounds__(256) void k_sft_rot(const orb_keypoint* __restrict_
     if (tid == 0) *nmatches = total;
 }
 
+// ------------------------------------------------------------------ SearchByBoW
+// ORBmatcher::SearchByBoW(pKF, F, vpMapPointMatches) (R/src/ORBmatcher.cpp:220-372) and
+// SearchByBoW(pKF1, pKF2, vpMatches12) (:632-760): over the vocabulary nodes both feature
+// vectors hold, each side-1 feature of the node (in list order) takes its nearest unmatched
+// side-2 feature of the node.  Side-2 features belong to one node only, so nodes are independent:
+// one wave per common node, walking the node's side-1 features in order (the reference's greedy
+// vpMapPointMatches / vbMatched2 sequence), the lanes taking its side-2 features.  The wave
+// reduces the reference's running (bestDist1, bestIdx, bestDist2): the least distance, its first
+// position (strict <), and the second least of the multiset; the match is kept when bestDist1
+// passes TH_LOW (<= for the frame overload, < for the keyframe one) and the ratio test.
+constexpr int kSbbMaxNode = 2048;
+__global__ __launch_bounds__(64) void k_sbb(const uint8_t* __restrict__ d1, const uint8_t* __restrict__ ok1,
+                                            const uint8_t* __restrict__ d2, const uint8_t* __restrict__ ok2,
+                                            const int4* __restrict__ nodes, const int32_t* __restrict__ idx1,
+                                            const int32_t* __restrict__ idx2, int thIncl, float ratio,
+                                            int32_t* __restrict__ matches12) {
+    const int lane = threadIdx.x;
+    const int4 nd = nodes[blockIdx.x];   // side-1 list [x, y), side-2 list [z, w)
+    const int c2 = nd.w - nd.z;
+    uint32_t taken = 0;                  // bit r: candidate lane + 64 r matched
+    for (int p1 = nd.x; p1 < nd.y; p1++) {
+        const int i1 = idx1[p1];
+        if (!ok1[i1]) continue;
+        const uint4* da = reinterpret_cast<const uint4*>(d1 + (size_t)i1 * 32);
+        const uint4 a0 = da[0], a1 = da[1];
+        int key1 = 0x7fffffff, dd2 = 256;    // lane's (dist << 16 | pos) minimum, second least dist
+        for (int r = 0; r * 64 < c2; r++) {
+            const int pos = r * 64 + lane;
+            if (pos >= c2 || ((taken >> r) & 1u)) continue;
+            const int i2 = idx2[nd.z + pos];
+            if (ok2 && !ok2[i2]) continue;
+            const uint4* db = reinterpret_cast<const uint4*>(d2 + (size_t)i2 * 32);
+            const uint4 b0 = db[0], b1 = db[1];
+            const int dist = __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+                             __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+            const int key = (dist << 16) | pos;
+            if (key < key1) { dd2 = min(dd2, key1 >> 16); key1 = key; }
+            else dd2 = min(dd2, dist);
+        }
+        const int g1 = wave_min_i32(key1);
+        if (g1 == 0x7fffffff) continue;
+        const int best1 = g1 >> 16;
+        const int best2 = wave_min_i32(key1 == g1 ? dd2 : min(dd2, key1 >> 16));
+        if (best1 <= thIncl && (float)best1 < ratio * (float)min(best2, 256)) {
+            const int pos = g1 & 0xffff;
+            if ((pos & 63) == lane) taken |= 1u << (pos >> 6);
+            if (lane == 0) matches12[i1] = idx2[nd.z + pos];
+        }
+    }
+}
+
 // ------------------------------------------------------------------ distinctive descriptors
 // MapPoint::ComputeDistinctiveDescriptors (R/src/MapPoint.cpp:306-385) for a batch of map
 // points: point m's observed descriptors are rows [start[m], start[m+1]) (observation order,
@@ -1892,6 +1943,113 @@ int orb_search_for_triangulation(int device, const orb_frame_view* kf1, const or
     (void)hipStreamDestroy(s);
     (void)hipFree(base);
     return rc == ORB_OK ? nm : rc;
+}
+
+}  // extern "C"
+
+// Shared host body of both SearchByBoW overloads: side 1 / side 2 views, per-feature eligibility
+// (ok2 may be NULL: every side-2 feature), the two mFeatVec CSR forms; matches12 by side-1 index.
+static int search_by_bow(int device, const orb_frame_view* v1, const uint8_t* ok1, int n_nodes1, const uint32_t* nodes1,
+                         const int32_t* start1, const int32_t* fidx1, const orb_frame_view* v2, const uint8_t* ok2,
+                         int n_nodes2, const uint32_t* nodes2, const int32_t* start2, const int32_t* fidx2,
+                         int thIncl, float ratio, int check_ori, int32_t* matches12) {
+    if (!v1 || !v2 || !ok1 || !matches12 || n_nodes1 < 0 || n_nodes2 < 0 || v1->n < 0 || v2->n < 0) return ORB_EINVAL;
+    if ((n_nodes1 && (!nodes1 || !start1 || !fidx1)) || (n_nodes2 && (!nodes2 || !start2 || !fidx2))) return ORB_EINVAL;
+    int st = check_device(device);
+    if (st) return st;
+    for (int i = 0; i < v1->n; i++) matches12[i] = -1;
+    std::vector<int4> common;
+    for (int a = 0, b = 0; a < n_nodes1 && b < n_nodes2;) {
+        if (nodes1[a] == nodes2[b]) {
+            if (start2[b + 1] - start2[b] > kSbbMaxNode) return ORB_E2BIG;
+            if (start1[a + 1] > start1[a] && start2[b + 1] > start2[b])
+                common.push_back(make_int4(start1[a], start1[a + 1], start2[b], start2[b + 1]));
+            a++;
+            b++;
+        } else if (nodes1[a] < nodes2[b]) {
+            a++;
+        } else {
+            b++;
+        }
+    }
+    const int L1 = n_nodes1 ? start1[n_nodes1] : 0, L2 = n_nodes2 ? start2[n_nodes2] : 0;
+    for (int t = 0; t < L1; t++)
+        if (fidx1[t] < 0 || fidx1[t] >= v1->n) return ORB_EINVAL;
+    for (int t = 0; t < L2; t++)
+        if (fidx2[t] < 0 || fidx2[t] >= v2->n) return ORB_EINVAL;
+    if (common.empty() || v1->n == 0) return 0;
+    ORB_HIP_TRY(hipSetDevice(device));
+    const int n1 = v1->n, n2 = v2->n;
+    std::vector<orb_keypoint> hk1((size_t)n1), hk2((size_t)std::max(n2, 1));
+    pack_view(v1, hk1.data());
+    pack_view(v2, hk2.data());
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t tot = al((size_t)n1 * sizeof(orb_keypoint) + 1) + al((size_t)n2 * sizeof(orb_keypoint) + 1) +
+                       al((size_t)n1 * 32 + 1) + al((size_t)n2 * 32 + 1) + al((size_t)n1 + 1) + al((size_t)n2 + 1) +
+                       al(common.size() * 16 + 1) + al((size_t)L1 * 4 + 1) + al((size_t)L2 * 4 + 1) +
+                       al((size_t)n1 * 4 + 1) + al(4 + 1) + 4096;
+    char* base = nullptr;
+    ORB_HIP_TRY(hipMalloc(&base, tot));
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) { (void)hipFree(base); return ORB_EGPU; }
+    char* c = base;
+    auto put = [&](const void* src, size_t bytes) {
+        char* r = c;
+        c += al(bytes + 1);
+        if (src && bytes) (void)hipMemcpyAsync(r, src, bytes, hipMemcpyHostToDevice, s);
+        return r;
+    };
+    auto* dK1 = (orb_keypoint*)put(hk1.data(), (size_t)n1 * sizeof(orb_keypoint));
+    auto* dK2 = (orb_keypoint*)put(hk2.data(), (size_t)n2 * sizeof(orb_keypoint));
+    auto* dD1 = (uint8_t*)put(v1->desc, (size_t)n1 * 32);
+    auto* dD2 = (uint8_t*)put(v2->desc, (size_t)n2 * 32);
+    auto* dO1 = (uint8_t*)put(ok1, (size_t)n1);
+    auto* dO2 = (uint8_t*)put(ok2, ok2 ? (size_t)n2 : 0);
+    auto* dN = (int4*)put(common.data(), common.size() * 16);
+    auto* dI1 = (int32_t*)put(fidx1, (size_t)L1 * 4);
+    auto* dI2 = (int32_t*)put(fidx2, (size_t)L2 * 4);
+    auto* dMt = (int32_t*)put(matches12, (size_t)n1 * 4);
+    auto* dNm = (int32_t*)put(nullptr, 4);
+    hipLaunchKernelGGL(k_sbb, dim3((unsigned)common.size()), dim3(64), 0, s, dD1, dO1, dD2, ok2 ? dO2 : nullptr, dN,
+                       dI1, dI2, thIncl, ratio, dMt);
+    hipLaunchKernelGGL(k_sft_rot, dim3(1), dim3(256), 0, s, dK1, dK2, n1, check_ori ? 1 : 0, dMt, dNm);
+    int rc = hipGetLastError() == hipSuccess ? ORB_OK : ORB_EGPU;
+    int nm = 0;
+    if (rc == ORB_OK) {
+        (void)hipMemcpyAsync(matches12, dMt, (size_t)n1 * 4, hipMemcpyDeviceToHost, s);
+        (void)hipMemcpyAsync(&nm, dNm, 4, hipMemcpyDeviceToHost, s);
+        if (hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
+    }
+    (void)hipStreamDestroy(s);
+    (void)hipFree(base);
+    return rc == ORB_OK ? nm : rc;
+}
+
+extern "C" {
+
+int orb_search_by_bow_frame(int device, const orb_frame_view* kf, const uint8_t* kf_ok, int n_nodes_kf,
+                            const uint32_t* nodes_kf, const int32_t* start_kf, const int32_t* fidx_kf,
+                            const orb_frame_view* f, int n_nodes_f, const uint32_t* nodes_f, const int32_t* start_f,
+                            const int32_t* fidx_f, float nn_ratio, int check_ori, int32_t* matches_f) {
+    if (!kf || !f || !matches_f || f->n < 0) return ORB_EINVAL;
+    std::vector<int32_t> m12((size_t)std::max(kf->n, 1));
+    const int n = search_by_bow(device, kf, kf_ok, n_nodes_kf, nodes_kf, start_kf, fidx_kf, f, nullptr, n_nodes_f,
+                                nodes_f, start_f, fidx_f, 50 /* bestDist1 <= TH_LOW */, nn_ratio, check_ori, m12.data());
+    if (n < 0) return n;
+    for (int j = 0; j < f->n; j++) matches_f[j] = -1;
+    for (int i = 0; i < kf->n; i++)
+        if (m12[i] >= 0) matches_f[m12[i]] = i;
+    return n;
+}
+
+int orb_search_by_bow_kf(int device, const orb_frame_view* kf1, const uint8_t* ok1, int n_nodes1,
+                         const uint32_t* nodes1, const int32_t* start1, const int32_t* fidx1,
+                         const orb_frame_view* kf2, const uint8_t* ok2, int n_nodes2, const uint32_t* nodes2,
+                         const int32_t* start2, const int32_t* fidx2, float nn_ratio, int check_ori,
+                         int32_t* matches12) {
+    if (!ok2) return ORB_EINVAL;
+    return search_by_bow(device, kf1, ok1, n_nodes1, nodes1, start1, fidx1, kf2, ok2, n_nodes2, nodes2, start2, fidx2,
+                         49 /* bestDist1 < TH_LOW */, nn_ratio, check_ori, matches12);
 }
 
 }  // extern "C"

@@ -72,6 +72,18 @@ class LocalMapPoints:
         return len(self.in_view)
 
 
+def _featvec(fv):
+    """A DBoW2 FeatureVector as (node ids uint32 ascending, CSR start int32, feature indices int32):
+    accepts that tuple or the node -> feature-list dict of ORBVocabulary.transform."""
+    if isinstance(fv, dict):
+        keys = sorted(fv)
+        start = np.zeros(len(keys) + 1, np.int32)
+        start[1:] = np.cumsum([len(fv[k]) for k in keys])
+        idx = np.array([i for k in keys for i in fv[k]], np.int32)
+        return np.array(keys, np.uint32), start, idx
+    return tuple(np.ascontiguousarray(x, t) for x, t in zip(fv, (np.uint32, np.int32, np.int32)))
+
+
 class ORBmatcher:
     TH_HIGH = 100
     TH_LOW = 50
@@ -79,6 +91,7 @@ class ORBmatcher:
 
     def __init__(self, nnratio: float = 0.6, checkOri: bool = True, device: int = 0):
         self.mfNNratio, self.mbCheckOrientation = float(nnratio), bool(checkOri)
+        self.device = device
         h = C.c_void_p()
         _abi.check("orb_matcher_create", _abi.lib().orb_matcher_create(device, C.c_float(nnratio), int(checkOri),
                                                                         C.byref(h)))
@@ -148,6 +161,46 @@ class ORBmatcher:
         n = _abi.check("orb_search_by_projection_local", _abi.lib().orb_search_by_projection_local(
             self._h, C.byref(v), len(mp), *[_abi.ptr(a) for a in arrs], C.c_float(th), _abi.ptr(cur_mp)))
         return n, cur_mp
+
+    def SearchByBoW(self, pKF: Frame, kf_ok, kf_featvec, F: Frame, f_featvec):
+        """SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>& vpMapPointMatches)
+        (R/src/ORBmatcher.cpp:220-372) on the GPU.  kf_ok[i]: the keyframe's map point i is set
+        and not bad; featvecs as (node ids ascending, CSR start, feature indices) or the dict
+        ORBVocabulary.transform returns.  Returns (nmatches, matches) — per frame feature the
+        keyframe feature whose map point it takes, -1 for none."""
+        fk, ff = _featvec(kf_featvec), _featvec(f_featvec)
+        ok = np.ascontiguousarray(kf_ok, np.uint8)
+        m = np.zeros(F.N, np.int32)
+        v1, v2 = pKF.view(), F.view()
+        lib = _abi.lib()
+        vp = C.c_void_p
+        lib.orb_search_by_bow_frame.argtypes = [C.c_int, vp, vp, C.c_int, vp, vp, vp, vp, C.c_int, vp, vp, vp,
+                                                C.c_float, C.c_int, vp]
+        lib.orb_search_by_bow_frame.restype = C.c_int
+        n = _abi.check("orb_search_by_bow_frame", lib.orb_search_by_bow_frame(
+            self.device, C.byref(v1), _abi.ptr(ok), len(fk[0]), *[_abi.ptr(x) for x in fk], C.byref(v2), len(ff[0]),
+            *[_abi.ptr(x) for x in ff], self.mfNNratio, int(self.mbCheckOrientation), _abi.ptr(m)))
+        return n, m
+
+    def SearchByBoWKF(self, pKF1: Frame, ok1, featvec1, pKF2: Frame, ok2, featvec2):
+        """SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& vpMatches12)
+        (R/src/ORBmatcher.cpp:632-760) on the GPU.  okN[i]: keyframe N's map point i is set and
+        not bad.  Returns (nmatches, matches12) — per keyframe-1 feature the keyframe-2 feature
+        whose map point becomes vpMatches12[i], -1 for none."""
+        f1, f2 = _featvec(featvec1), _featvec(featvec2)
+        o1, o2 = np.ascontiguousarray(ok1, np.uint8), np.ascontiguousarray(ok2, np.uint8)
+        m = np.zeros(pKF1.N, np.int32)
+        v1, v2 = pKF1.view(), pKF2.view()
+        lib = _abi.lib()
+        vp = C.c_void_p
+        lib.orb_search_by_bow_kf.argtypes = [C.c_int, vp, vp, C.c_int, vp, vp, vp, vp, vp, C.c_int, vp, vp, vp,
+                                             C.c_float, C.c_int, vp]
+        lib.orb_search_by_bow_kf.restype = C.c_int
+        n = _abi.check("orb_search_by_bow_kf", lib.orb_search_by_bow_kf(
+            self.device, C.byref(v1), _abi.ptr(o1), len(f1[0]), *[_abi.ptr(x) for x in f1], C.byref(v2),
+            _abi.ptr(o2), len(f2[0]), *[_abi.ptr(x) for x in f2], self.mfNNratio, int(self.mbCheckOrientation),
+            _abi.ptr(m)))
+        return n, m
 
     def knn2(self, q, t):
         q = np.ascontiguousarray(q, np.uint8)

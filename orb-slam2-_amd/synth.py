@@ -398,3 +398,32 @@ def bow_features(voc_desc, voc_leaf, n, seed=11, random_frac=0.1):
     r = rng.random(n) < random_frac
     f[r] = rng.integers(0, 256, (int(r.sum()), 32), dtype=np.uint8)
     return f
+
+
+def bow_match_problem(voc, seed=9, n_land=900, keep=0.8, extra=200, mp_frac=0.75, rot_deg=25.0, W=640, H=480):
+    """Synthetic ORBmatcher::SearchByBoW input over a vocabulary from vocabulary(): two views of
+    n_land landmark descriptors (near vocabulary leaves); each view keeps ~keep of them with
+    U{0..20} bits flipped, plus `extra` random features; angles = the landmark's + N(0, 3 deg),
+    the second view turned by rot_deg; mp_frac of the features carry a good map point.  The
+    feature vectors come from transforming each view's descriptors with the vocabulary."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    base = bow_features(voc[2], voc[1], n_land, seed=seed + 1)
+    ang = rng.uniform(0, 360, n_land)
+
+    def view(turn):
+        sel = np.flatnonzero(rng.random(n_land) < keep)
+        d = base[sel].copy()
+        for r in range(len(sel)):
+            bits = np.unpackbits(d[r])
+            bits[rng.choice(256, int(rng.integers(0, 21)), replace=False)] ^= 1
+            d[r] = np.packbits(bits)
+        a = (ang[sel] + turn + rng.normal(0, 3, len(sel))) % 360
+        d = np.concatenate([d, rng.integers(0, 256, (extra, 32), dtype=np.uint8)])
+        a = np.concatenate([a, rng.uniform(0, 360, extra)])
+        perm = rng.permutation(len(d))
+        n = len(d)
+        return {"x": rng.uniform(0, W, n).astype(np.float32), "y": rng.uniform(0, H, n).astype(np.float32),
+                "octave": rng.integers(0, 8, n).astype(np.int32), "angle": a[perm].astype(np.float32),
+                "desc": np.ascontiguousarray(d[perm]), "uright": None,
+                "has_mp": (rng.random(n) < mp_frac).astype(np.uint8), "W": W, "H": H}
+    return view(0.0), view(rot_deg)

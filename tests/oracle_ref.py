@@ -432,3 +432,34 @@ def bow_transform(voc, features, levelsup):
     bow = {int(words[i]): float(vals[i]) for i in range(nw)}
     fv = {int(nodes[i]): [int(x) for x in idx[start[i]:start[i + 1]]] for i in range(nf.value)}
     return bow, fv
+
+
+def search_by_bow_frame(kf, kf_ok, fv_kf, f, fv_f, nnratio=0.7, check_ori=True):
+    """oracle_search_by_bow_frame: (nmatches, per frame feature the keyframe feature or -1)."""
+    v1 = FrameView(kf, kf["desc"], kf["W"], kf["H"])
+    v2 = FrameView(f, f["desc"], f["W"], f["H"])
+    ok = np.ascontiguousarray(kf_ok, np.uint8)
+    m = np.zeros(len(f["x"]), np.int32)
+    n = lib().oracle_search_by_bow_frame(C.byref(v1.s), P(ok), len(fv_kf[0]), *[P(x) for x in fv_kf], C.byref(v2.s),
+                                         len(fv_f[0]), *[P(x) for x in fv_f], C.c_float(nnratio), int(check_ori), P(m))
+    return n, m
+
+
+def search_by_bow_kf(k1, ok1, fv1, k2, ok2, fv2, nnratio=0.75, check_ori=True):
+    """oracle_search_by_bow_kf: (nmatches, per keyframe-1 feature the keyframe-2 feature or -1)."""
+    v1 = FrameView(k1, k1["desc"], k1["W"], k1["H"])
+    v2 = FrameView(k2, k2["desc"], k2["W"], k2["H"])
+    o1, o2 = np.ascontiguousarray(ok1, np.uint8), np.ascontiguousarray(ok2, np.uint8)
+    m = np.zeros(len(k1["x"]), np.int32)
+    n = lib().oracle_search_by_bow_kf(C.byref(v1.s), P(o1), len(fv1[0]), *[P(x) for x in fv1], C.byref(v2.s), P(o2),
+                                      len(fv2[0]), *[P(x) for x in fv2], C.c_float(nnratio), int(check_ori), P(m))
+    return n, m
+
+
+def featvec_arrays(fv):
+    """FeatureVector dict (node -> feature list) -> (node ids uint32, CSR start int32, indices int32)."""
+    keys = sorted(fv)
+    start = np.zeros(len(keys) + 1, np.int32)
+    start[1:] = np.cumsum([len(fv[k]) for k in keys])
+    idx = np.array([i for k in keys for i in fv[k]], np.int32)
+    return np.array(keys, np.uint32), start, idx
