@@ -419,6 +419,16 @@ int lba_set_comm(lba_context* c, int rank, int world, double* d_workspace, size_
 int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const volatile uint8_t* stop,
               lba_result* r);
 
+/* Optimizer::BundleAdjustment(vpKFs, vpMP, nIterations, pbStopFlag, nLoopKF, bRobust) —
+ * R/src/Optimizer.cpp:78-277 (global BA: Tracking initialisation with 20 iterations, LoopClosing's
+ * RunGlobalBundleAdjustment with 10): one optimize(o->iters1) over every edge of the problem, Huber
+ * kernels with deltas o->huber_mono / o->huber_stereo ((float)sqrt(5.99), (float)sqrt(7.815)) only
+ * when robust; no outlier pass (edge_erase all 0).  Poses with pose_id 0 are the fixed ones the
+ * caller marks; points without edges are left out (vbNotIncludedMP) and returned unchanged.  *stop
+ * (setForceStopFlag) ends the iterations; the estimates are written back either way. */
+int lba_solve_global(lba_context* c, const lba_problem* p, const lba_options* o, int robust,
+                     const volatile uint8_t* stop, lba_result* r);
+
 /* Stage timing of the LM loop (HIP events): ms4 = linearise, Schur, solve, update. */
 /* The reduced camera system solver on its own (LinearSolverEigen::solve's role,
  * G/solvers/linear_solver_eigen.h:94-120): x = S^-1 b for a symmetric positive-definite

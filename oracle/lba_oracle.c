@@ -636,13 +636,31 @@ static int optimize(lba_ctx* c, int iterations, const volatile uint8_t* stop, lb
     return it;
 }
 
+static int lba_run(const lba_problem_t* p, const lba_options_t* o, const volatile uint8_t* stop, lba_result_t* r,
+                   int rank, int world, oracle_allreduce_fn ar, void* user, int global, int robust);
+
 int oracle_lba_solve(const lba_problem_t* p, const lba_options_t* o, const volatile uint8_t* stop, lba_result_t* r)
 {
-    return oracle_lba_solve_dist(p, o, stop, r, 0, 1, NULL, NULL);
+    return lba_run(p, o, stop, r, 0, 1, NULL, NULL, 0, 1);
 }
 
 int oracle_lba_solve_dist(const lba_problem_t* p, const lba_options_t* o, const volatile uint8_t* stop,
                           lba_result_t* r, int rank, int world, oracle_allreduce_fn ar, void* user)
+{
+    return lba_run(p, o, stop, r, rank, world, ar, user, 0, 1);
+}
+
+/* Optimizer::BundleAdjustment (R/src/Optimizer.cpp:78-277): one optimize(nIterations) = iters1
+ * over every edge, Huber kernels (deltas (float)sqrt(5.99) / (float)sqrt(7.815)) only when
+ * bRobust, no outlier pass; the force-stop flag only ends the iterations (no early return). */
+int oracle_global_ba(const lba_problem_t* p, const lba_options_t* o, int robust, const volatile uint8_t* stop,
+                     lba_result_t* r)
+{
+    return lba_run(p, o, stop, r, 0, 1, NULL, NULL, 1, robust);
+}
+
+static int lba_run(const lba_problem_t* p, const lba_options_t* o, const volatile uint8_t* stop, lba_result_t* r,
+                   int rank, int world, oracle_allreduce_fn ar, void* user, int global, int robust)
 {
     lba_ctx c;
     memset(&c, 0, sizeof(c));
@@ -664,7 +682,7 @@ int oracle_lba_solve_dist(const lba_problem_t* p, const lba_options_t* o, const 
     c.err = (double*)calloc(3 * (NE + 1), sizeof(double));
     c.level = (uint8_t*)calloc(NE + 1, 1);
     c.robust = (uint8_t*)malloc(NE + 1);
-    memset(c.robust, 1, NE + 1);
+    memset(c.robust, robust ? 1 : 0, NE + 1);
     c.act_edges = (int*)malloc(sizeof(int) * (NE + 1));
     c.pose_idx = (int*)malloc(sizeof(int) * (NP + 1));
     c.point_idx = (int*)malloc(sizeof(int) * (NM + 1));
@@ -685,14 +703,15 @@ int oracle_lba_solve_dist(const lba_problem_t* p, const lba_options_t* o, const 
     r->trials = 0;
     r->n_trace = 0;
     int status = 0;
-    if (stop && *stop) {
+    if (!global && stop && *stop) {
         status = 1;
         goto done;
     }
-    /* optimize(5) on every edge with Huber kernels (R/src/Optimizer.cpp:789-790) */
+    /* optimize(5) on every edge with Huber kernels (R/src/Optimizer.cpp:789-790); global BA:
+     * optimize(nIterations), R/src/Optimizer.cpp:230-231 */
     init_optimization(&c, 0);
     r->iterations[0] = optimize(&c, o->iters1, stop, r);
-    int bDoMore = !(stop && *stop);
+    int bDoMore = !global && !(stop && *stop);
     if (bDoMore) {
         /* outlier pass (R/src/Optimizer.cpp:805-836) */
         for (int e = 0; e < NE; e++) {
@@ -720,7 +739,7 @@ int oracle_lba_solve_dist(const lba_problem_t* p, const lba_options_t* o, const 
         const double chi = mine ? edge_chi2(&c, e) : 0.0;
         if (r->edge_chi2) r->edge_chi2[e] = chi;
         uint8_t er = 0;
-        if (mine && !(p->point_bad && p->point_bad[p->edge_point[e]])) {
+        if (!global && mine && !(p->point_bad && p->point_bad[p->edge_point[e]])) {
             const double thr = p->edge_stereo[e] ? o->chi2_stereo : o->chi2_mono;
             er = (chi > thr || !depth_positive(&c, e)) ? 1 : 0;
         }

@@ -73,6 +73,13 @@ typedef void (*oracle_allreduce_fn)(void* user, double* v, int n, int op);
 int oracle_lba_solve_dist(const lba_problem_t* p, const lba_options_t* o, const volatile uint8_t* stop,
                           lba_result_t* r, int rank, int world, oracle_allreduce_fn ar, void* user);
 
+/* Optimizer::BundleAdjustment(vpKFs, vpMP, nIterations, pbStopFlag, nLoopKF, bRobust)
+ * (R/src/Optimizer.cpp:78-277): optimize(o->iters1) over every edge, Huber kernels with deltas
+ * o->huber_mono / o->huber_stereo ((float)sqrt(5.99) / (float)sqrt(7.815)) when robust; no outlier
+ * pass, edge_erase all 0; *stop ends the iterations but the estimates are still written. */
+int oracle_global_ba(const lba_problem_t* p, const lba_options_t* o, int robust, const volatile uint8_t* stop,
+                     lba_result_t* r);
+
 /* Optimizer::PoseOptimization(Frame*) (R/src/Optimizer.cpp:306-535) on one frame: the edges are
  * the frame's keypoints with a map point, obs = (u, v, ur) with ur < 0 for a monocular
  * observation (Frame::mvuRight), xw the map point (float values), info = invSigma2 of the

@@ -1394,7 +1394,20 @@ void lba_pose_to_Tcw(const double q[4], const double t[3], float Tcw[16]) {
     Tcw[15] = 1.f;
 }
 
+static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, const volatile uint8_t* stop,
+                   lba_result* r, bool global, bool robustKernels);
+
 int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const volatile uint8_t* stop, lba_result* r) {
+    return lba_run(c, p, o, stop, r, false, true);
+}
+
+int lba_solve_global(lba_context* c, const lba_problem* p, const lba_options* o, int robust,
+                     const volatile uint8_t* stop, lba_result* r) {
+    return lba_run(c, p, o, stop, r, true, robust != 0);
+}
+
+static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, const volatile uint8_t* stop,
+                   lba_result* r, bool global, bool robustKernels) {
 #ifdef ORB_TIMING
     const auto hEntry = std::chrono::steady_clock::now();
 #endif
@@ -1406,7 +1419,7 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
     r->trials = 0;
     r->n_trace = 0;
     r->aborted = 0;
-    if (stop && *stop) {      // R/src/Optimizer.cpp:784-786: return before optimizing, no write-back
+    if (!global && stop && *stop) {   // R/src/Optimizer.cpp:784-786: return before optimizing, no write-back
         r->aborted = 1;
         return ORB_OK;
     }
@@ -1456,7 +1469,7 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
     TRY(dalloc(c, &d_chi2, NE));
     TRY(dalloc(c, &d_depth, NE));
 
-    std::vector<uint8_t> level(NE, 0), robustH(NE, 1);
+    std::vector<uint8_t> level(NE, 0), robustH(NE, robustKernels ? 1 : 0);
     const double hm = o->huber_mono, hsv = o->huber_stereo;
     const int maxTrials = o->max_trials > 0 ? o->max_trials : 10;
     auto stopped = [&]() { return stop && *stop; };
@@ -1666,7 +1679,7 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
     HSTAMP(1);
     TRY(optimize(o->iters1, r->iterations[0]));
     HSTAMP(2);
-    const bool bDoMore = !stopped();
+    const bool bDoMore = !global && !stopped();   // global BA: one optimize(nIterations), R :230-231
     auto edge_check = [&](std::vector<double>& chi, std::vector<uint8_t>& dep) -> int {
         if (NE > 0) hipLaunchKernelGGL(k_edge_check, grid(NE), dim3(256), 0, s, d, NE, d_chi2, d_depth);
         chi.resize(NE);
@@ -1723,7 +1736,7 @@ int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const 
         const bool mine = pt >= own0 && pt < own1;
         if (r->edge_chi2) r->edge_chi2[e] = mine ? chi[e] : 0.0;
         uint8_t er = 0;
-        if (mine && !(p->point_bad && p->point_bad[pt])) {
+        if (!global && mine && !(p->point_bad && p->point_bad[pt])) {
             const double thr = p->edge_stereo[e] ? o->chi2_stereo : o->chi2_mono;
             er = (chi[e] > thr || !dep[e]) ? 1 : 0;
         }

@@ -43,6 +43,13 @@ def options(iters1=5, iters2=10, fixed_iterations=False):
                       float(np.float32(np.sqrt(7.815))), 10, int(fixed_iterations))
 
 
+def global_options(nIterations=10, fixed_iterations=False):
+    """Optimizer::BundleAdjustment's constants (R/src/Optimizer.cpp:117-118): thHuber2D =
+    (float)sqrt(5.99), thHuber3D = (float)sqrt(7.815); nIterations in iters1."""
+    return LbaOptions(nIterations, 0, 5.991, 7.815, float(np.float32(np.sqrt(5.99))),
+                      float(np.float32(np.sqrt(7.815))), 10, int(fixed_iterations))
+
+
 def _sig():
     lib = _abi.lib()
     if getattr(lib, "_lba_sig", False):
@@ -52,6 +59,7 @@ def _sig():
                             ("lba_set_stream", [vp, vp, i32], C.c_int),
                             ("lba_set_comm", [vp, i32, i32, vp, sz, ALLREDUCE_FN, vp], C.c_int),
                             ("lba_solve", [vp, vp, vp, vp, vp], C.c_int), ("lba_profile", [vp, i32], C.c_int),
+                            ("lba_solve_global", [vp, vp, vp, i32, vp, vp], C.c_int),
                             ("lba_stats", [vp, vp, vp, vp], C.c_int),
                             ("lba_dense_solve", [vp, vp, vp, i32, vp], C.c_int), ("lba_pose_from_Tcw", [vp, vp, vp], None),
                             ("lba_pose_to_Tcw", [vp, vp, vp], None),
@@ -132,10 +140,12 @@ class LocalBA:
         return dict(linearize_ms=ms[0], schur_ms=ms[1], solve_ms=ms[2], update_ms=ms[3], iterations=it.value,
                     trials=tr.value)
 
-    def solve(self, prob, opts=None, stop=None):
+    def solve(self, prob, opts=None, stop=None, global_ba=False, robust=True):
         """prob: dict of arrays (synth.ba_problem layout).  stop: a 1-byte ctypes array
-        polled like mbAbortBA.  Returns a dict with the optimised estimates."""
-        opts = opts or options()
+        polled like mbAbortBA.  global_ba: Optimizer::BundleAdjustment instead of the local BA
+        flow (lba_solve_global; opts from global_options, robust = bRobust).  Returns a dict
+        with the optimised estimates."""
+        opts = opts or (global_options() if global_ba else options())
         nk = len(prob["Tcw"])
         Tcw = np.ascontiguousarray(prob["Tcw"], np.float32)
         q, t = np.zeros((nk, 4)), np.zeros((nk, 3))
@@ -151,7 +161,11 @@ class LocalBA:
         r = LbaResult(P(out["pose_q"]), P(out["pose_t"]), P(out["point_xyz"]), P(out["edge_erase"]),
                       P(out["edge_chi2"]), (C.c_int * 2)(0, 0), 0, P(out["trace"]), 0, 0)
         flag = stop if stop is not None else (C.c_uint8 * 1)(0)
-        _abi.check("lba_solve", _sig().lba_solve(self._h, C.byref(pr), C.byref(opts), flag, C.byref(r)))
+        if global_ba:
+            _abi.check("lba_solve_global", _sig().lba_solve_global(self._h, C.byref(pr), C.byref(opts), int(robust), flag,
+                                                                    C.byref(r)))
+        else:
+            _abi.check("lba_solve", _sig().lba_solve(self._h, C.byref(pr), C.byref(opts), flag, C.byref(r)))
         out["iterations"] = (r.iterations[0], r.iterations[1])
         out["trials"] = r.trials
         out["trace"] = out["trace"][: r.n_trace]
@@ -176,6 +190,17 @@ class Optimizer:
         if ctx is None:
             ctx = Optimizer._ctx[device] = LocalBA(device)
         return ctx.solve(problem, opts, pbStopFlag)
+
+    @staticmethod
+    def BundleAdjustment(problem, nIterations=5, pbStopFlag=None, bRobust=True, device=0, fixed_iterations=False):
+        """Optimizer::BundleAdjustment (R/src/Optimizer.cpp:78-277) on the array form: every
+        keyframe pose (pose_fixed = mnId == 0) and map point of `problem`; GlobalBundleAdjustemnt
+        passes nIterations 20 (initialisation) or 10 (loop closing) and bRobust false there."""
+        ctx = Optimizer._ctx.get(device)
+        if ctx is None:
+            ctx = Optimizer._ctx[device] = LocalBA(device)
+        return ctx.solve(problem, global_options(nIterations, fixed_iterations), pbStopFlag, global_ba=True,
+                         robust=bRobust)
 
 
 def apply_results(problem, result):

@@ -268,7 +268,18 @@ def quat_from_Tcw(T):
     return q, np.asarray(T, np.float32)[:3, 3].astype(np.float64)
 
 
-def lba_solve(prob, options=None, stop=False):
+def global_ba_options(n_iterations=10, fixed_iterations=False):
+    """Optimizer::BundleAdjustment's Huber deltas (R/src/Optimizer.cpp:117-118)."""
+    return LbaOptions(n_iterations, 0, 5.991, 7.815, float(np.float32(np.sqrt(5.99))),
+                      float(np.float32(np.sqrt(7.815))), 10, int(fixed_iterations))
+
+
+def global_ba(prob, n_iterations=10, robust=True, stop=False, fixed_iterations=False):
+    """oracle_global_ba (Optimizer::BundleAdjustment) on a synth.ba_problem layout."""
+    return lba_solve(prob, global_ba_options(n_iterations, fixed_iterations), stop, global_robust=int(robust))
+
+
+def lba_solve(prob, options=None, stop=False, global_robust=None):
     options = options or lba_options()
     nk = len(prob["Tcw"])
     qs, ts = zip(*[quat_from_Tcw(T) for T in prob["Tcw"]])
@@ -284,7 +295,10 @@ def lba_solve(prob, options=None, stop=False):
     r = LbaResult(P(out["pose_q"]), P(out["pose_t"]), P(out["point_xyz"]), P(out["edge_erase"]),
                   P(out["edge_chi2"]), (C.c_int * 2)(0, 0), 0, P(out["trace"]), 0)
     flag = (C.c_uint8 * 1)(1 if stop else 0)
-    st = lib().oracle_lba_solve(C.byref(pr), C.byref(options), flag, C.byref(r))
+    if global_robust is None:
+        st = lib().oracle_lba_solve(C.byref(pr), C.byref(options), flag, C.byref(r))
+    else:
+        st = lib().oracle_global_ba(C.byref(pr), C.byref(options), global_robust, flag, C.byref(r))
     out["status"] = st
     out["iterations"] = (r.iterations[0], r.iterations[1])
     out["trials"] = r.trials
