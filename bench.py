@@ -355,6 +355,7 @@ def bench_extras(args, amd, dev):
     out["batch_sweep_640x480"] = batch_sweep(amd, dev, m)
     out["pose_optimization"] = bench_pose(args, amd, dev)
     out["bow_transform"] = bench_bow(args, amd, dev)
+    out["global_ba"] = bench_gba(args, amd, dev)
     return out
 
 
@@ -410,6 +411,37 @@ def bench_pose(args, amd, dev, n_frames=256, n_points=600):
         out["cpu_baseline"] = {"frames_per_s": round(len(sample) / dc, 1), "cores": threads, "kind": "port",
                                "sample": f"{len(sample)} frames, oracle C restatement of PoseOptimization, "
                                          f"1 frame per thread"}
+    return out
+
+
+def bench_gba(args, amd, dev, n_kf=60, n_points=8000, iters=10):
+    """SURVEY §8f-2: Optimizer::BundleAdjustment (LoopClosing's 10 iterations, bRobust false) on a
+    synthetic 60-keyframe, 8000-point map (reduced camera system 360 x 360): wall time of the
+    whole call (host structure build, transfers, kernels); against the oracle on the same map."""
+    from orb_slam2_amd import synth
+    pb = synth.ba_problem(n_local=n_kf, n_fixed=0, n_points=n_points, seed=17, arc=6.0)
+    ctx = amd.LocalBA()
+    from orb_slam2_amd import optimizer as opt
+    o = opt.global_options(iters)
+    ctx.solve(pb, o, global_ba=True, robust=False)
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        r = ctx.solve(pb, o, global_ba=True, robust=False)
+    dt = (time.perf_counter() - t0) / reps
+    it = r["iterations"][0]
+    out = {"ms_per_call": round(dt * 1e3, 3), "ms_per_iteration": round(dt * 1e3 / max(it, 1), 3),
+           "iterations": it, "keyframes": n_kf, "points": n_points, "edges": int(len(pb["edge_point"]))}
+    if not args.no_cpu:
+        sys.path.insert(0, str(ROOT / "tests"))
+        import oracle_ref as O
+        t0 = time.perf_counter()
+        ref = O.global_ba(pb, iters, robust=False)
+        dc = time.perf_counter() - t0
+        out["cpu_baseline"] = {"ms_per_call": round(dc * 1e3, 2), "cores": 1, "kind": "port",
+                               "sample": "the same map, oracle C restatement of g2o LM + Schur, 1 thread",
+                               "same_iterations": ref["iterations"][0] == it}
+    ctx.close()
     return out
 
 
