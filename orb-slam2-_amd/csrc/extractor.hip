@@ -352,13 +352,17 @@ constexpr int kTileW = 64, kTileH = 16;   // blur tiles
 
 // Per-wave LDS of k_fast_cell for regions up to maxW x maxH (host and device agree on it).
 __host__ __device__ inline int fc_patch_stride(int maxW) { return ((maxW + 8 + 3) & ~3) + 4; }
-__host__ __device__ inline int fc_score_stride(int maxW) { return maxW <= 32 ? 32 : 64; }
+__host__ __device__ inline int fc_score_stride(int maxW) { return (maxW + 3) & ~3; }
+// patch (window bytes; after scoring it holds the u8 suppressed score per survivor), score map,
+// u16 y*64+x list of the pre-test survivors.  ~5.9 KB per wave for 36 x 36 regions: six
+// 4-wave workgroups per CU.
 __host__ __device__ inline int fc_wave_bytes(int maxW, int maxH) {
-    const int patch = ((maxH + 6) * fc_patch_stride(maxW) + 15) & ~15;
+    int patch = ((maxH + 6) * fc_patch_stride(maxW) + 15) & ~15;
+    const int keep = (maxW * maxH + 15) & ~15;
+    if (patch < keep) patch = keep;
     const int sc = (maxH * fc_score_stride(maxW) + 15) & ~15;
-    const int list = (maxW * maxH * 2 + 15) & ~15;   // u16 y*64+x of the pre-test survivors
-    const int keep = (maxW * maxH + 15) & ~15;       // u8 suppressed score per survivor
-    return patch + sc + list + keep;
+    const int list = (maxW * maxH * 2 + 15) & ~15;
+    return patch + sc + list;
 }
 
 // One wave per FAST cell (R/src/ORBextractor.cpp:851-896): cv::FAST on the cell's window,
@@ -413,9 +417,10 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
     unsigned char* base = dsm + (size_t)wid * fc_wave_bytes(maxW, maxH);
     uint32_t* patch32 = reinterpret_cast<uint32_t*>(base);
     const uint8_t* patch = base;
-    uint8_t* sc = base + (((maxH + 6) * PWS + 15) & ~15);
+    const int patchBytes = max(((maxH + 6) * PWS + 15) & ~15, (maxW * maxH + 15) & ~15);
+    uint8_t* sc = base + patchBytes;
     uint16_t* list = reinterpret_cast<uint16_t*>(sc + ((maxH * SCS + 15) & ~15));
-    uint8_t* kp = reinterpret_cast<uint8_t*>(list) + ((maxW * maxH * 2 + 15) & ~15);
+    uint8_t* kp = base;   // the window is dead once every survivor is scored (phase 3)
     const uint8_t* img = pyr + (size_t)b * g.frameBytes + L.off;
     const int rx0 = iniX + 3, ry0 = iniY + 3;
 
@@ -501,6 +506,40 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 
     TSTAMP(t_fc2);
+    // 2b. second necessary test on the survivors: any 9-arc holds four cyclically consecutive
+    //     even ring pixels (0, 2, .., 14), so they must all be dark or all bright at the same
+    //     strict threshold; the list is compacted in place (order kept: a chunk's entries are all
+    //     read before any is written, and every write lands at or below its source index).
+    {
+        const int tv = (int)tpre;
+        int n2 = 0;
+        for (int k0 = 0; k0 < n; k0 += 64) {
+            const int k = k0 + lane;
+            const int p = k < n ? (int)list[k] : 0;
+            const int y = p >> 6, x = p & 63;
+            const int cc = (y + 3) * PWS + x + 4;
+            const int v = patch[cc];
+            const int e[8] = {patch[cc + 3 * PWS], patch[cc + 2 * PWS + 2], patch[cc + 3], patch[cc - 2 * PWS + 2],
+                              patch[cc - 3 * PWS], patch[cc - 2 * PWS - 2], patch[cc - 3], patch[cc + 2 * PWS - 2]};
+            uint32_t dk = 0, br = 0;
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                dk |= (uint32_t)(v - e[i] > tv) << i;
+                br |= (uint32_t)(e[i] - v > tv) << i;
+            }
+            dk |= dk << 8;
+            br |= br << 8;
+            const uint32_t run = (dk & (dk >> 1) & (dk >> 2) & (dk >> 3)) | (br & (br >> 1) & (br >> 2) & (br >> 3));
+            const bool pass = k < n && (run & 0xffu) != 0;
+            const uint64_t m = __ballot(pass);
+            if (pass) list[n2 + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)p;
+            n2 += __popcll(m);
+        }
+        n = n2;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+
     // 3. full score of the survivors.  The list is in raster order: lanes are row-major over
     //    (row, column group) and each lane appends its group's columns in order.
     for (int k = lane; k < n; k += 64) {
