@@ -299,6 +299,24 @@ int orb_search_by_projection_frame(orb_matcher* m, const orb_frame_view* cur, co
                                    const float* scale_factors, const float cam[6], float th,
                                    int mono, int32_t* cur_mp);
 
+/* ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const set<MapPoint*>&
+ * sAlreadyFound, float th, int ORBdist) — R/src/ORBmatcher.cpp:1719-1800 (Tracking::Relocalization).
+ *   cur: the frame (mvKeysUn, mDescriptors, bounds, grid); Tcw_cur: rows 0..2 of mTcw; Ow: its
+ *   camera centre -Rcw^T tcw as the reference computes it; cam = fx, fy, cx, cy;
+ *   kf: the keyframe as a frame view (mvKeysUn angles; kf->n = its N);
+ *   mp_valid[i] != 0 when GetMapPointMatches()[i] is set, not bad and not in sAlreadyFound;
+ *   mp_xyz / mp_min_dist / mp_max_dist / mp_desc = GetWorldPos, mfMinDistance, mfMaxDistance,
+ *   GetDescriptor; log_scale_factor / n_levels / scale_factors = the frame's mfLogScaleFactor,
+ *   mnScaleLevels, mvScaleFactors.
+ * cur_mp (in/out, cur->n ints): -1 = mvpMapPoints[i2] empty, any other negative value = set
+ * before the call, >= 0 on return = the keyframe map point index this call assigned.
+ * Returns nmatches (after the rotation filter when the matcher checks orientation). */
+int orb_search_by_projection_kf(orb_matcher* m, const orb_frame_view* cur, const float* Tcw_cur, const float Ow[3],
+                                const orb_frame_view* kf, const uint8_t* mp_valid, const float* mp_xyz,
+                                const float* mp_min_dist, const float* mp_max_dist, const uint8_t* mp_desc,
+                                const float cam[4], float log_scale_factor, int n_levels, const float* scale_factors,
+                                float th, int orb_dist, int32_t* cur_mp);
+
 /* ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>& vpMapPoints, float th)
  * — R/src/ORBmatcher.cpp:63-163 (Tracking::SearchLocalPoints, R/src/Tracking.cpp:1413-1460).
  * Map points in vector order (n_mp):

@@ -1721,3 +1721,79 @@ int oracle_search_by_bow_kf(const oracle_frame* k1, const uint8_t* ok1, int n1, 
     free(matched2);
     return nmatches;
 }
+
+/* R/src/ORBmatcher.cpp:1719-1800, literally; OpenCV's float products restated as in
+ * oracle_fuse (double-accumulated rows rounded to float, cv::norm = sqrt of the float sum in
+ * double), PredictScale's log in double (R/src/MapPoint.cpp:509-524). */
+int oracle_search_by_projection_kf(const oracle_frame* cur, const float* Tcw, const float* Ow, const oracle_frame* kf,
+                                   const uint8_t* mp_valid, const float* mp_xyz, const float* mp_min_dist,
+                                   const float* mp_max_dist, const uint8_t* mp_desc, const float* cam4,
+                                   float log_scale_factor, int n_levels, const float* scale_factors, float th,
+                                   int orb_dist, int check_ori, int32_t* cur_mp)
+{
+    int nmatches = 0;
+    ogrid g;
+    build_grid(cur, &g);
+    int* hist_idx = (int*)malloc(sizeof(int) * (kf->n + 1));
+    int* hist_bin = (int*)malloc(sizeof(int) * (kf->n + 1));
+    int nh = 0;
+    int* cand = (int*)malloc(sizeof(int) * (cur->n + 1));
+    for (int i = 0; i < kf->n; i++) {
+        if (!mp_valid[i]) continue;
+        const float* X = mp_xyz + 3 * (size_t)i;
+        float x3Dc[3];
+        mat34_apply(Tcw, X, x3Dc);
+        const float xc = x3Dc[0], yc = x3Dc[1];
+        const float invzc = (float)(1.0 / (double)x3Dc[2]);
+        const float u = cam4[0] * xc * invzc + cam4[2];
+        const float v = cam4[1] * yc * invzc + cam4[3];
+        if (u < cur->min_x || u > cur->max_x) continue;
+        if (v < cur->min_y || v > cur->max_y) continue;
+        const float PO[3] = {X[0] - Ow[0], X[1] - Ow[1], X[2] - Ow[2]};
+        const float ss = (PO[0] * PO[0] + PO[1] * PO[1]) + PO[2] * PO[2];
+        const float dist3D = (float)sqrt((double)ss);
+        const float maxDistance = 1.2f * mp_max_dist[i], minDistance = 0.8f * mp_min_dist[i];
+        if (dist3D < minDistance || dist3D > maxDistance) continue;
+        const float ratio = mp_max_dist[i] / dist3D;
+        int lev = (int)ceil(log((double)ratio) / (double)log_scale_factor);
+        if (lev < 0) lev = 0;
+        else if (lev >= n_levels) lev = n_levels - 1;
+        const float radius = th * scale_factors[lev];
+        const int nc = features_in_area(cur, &g, u, v, radius, lev - 1, lev + 1, cand, cur->n);
+        if (nc == 0) continue;
+        const uint8_t* dMP = mp_desc + (size_t)i * 32;
+        int bestDist = 256, bestIdx2 = -1;
+        for (int q = 0; q < nc; q++) {
+            const int i2 = cand[q];
+            if (cur_mp[i2] != -1) continue;          /* CurrentFrame.mvpMapPoints[i2] set */
+            const int dist = oracle_descriptor_distance(dMP, cur->desc + (size_t)i2 * 32);
+            if (dist < bestDist) { bestDist = dist; bestIdx2 = i2; }
+        }
+        if (bestDist <= orb_dist) {
+            cur_mp[bestIdx2] = i;
+            nmatches++;
+            if (check_ori) {
+                hist_idx[nh] = bestIdx2;
+                hist_bin[nh] = rot_bin(kf->angle[i] - cur->angle[bestIdx2]);
+                nh++;
+            }
+        }
+    }
+    if (check_ori) {
+        int hsize[HISTO_LENGTH] = {0};
+        for (int q = 0; q < nh; q++) hsize[hist_bin[q]]++;
+        int ind1, ind2, ind3;
+        three_maxima(hsize, &ind1, &ind2, &ind3);
+        for (int b = 0; b < HISTO_LENGTH; b++) {
+            if (b == ind1 || b == ind2 || b == ind3) continue;
+            for (int q = 0; q < nh; q++) {
+                if (hist_bin[q] != b) continue;
+                cur_mp[hist_idx[q]] = -1;
+                nmatches--;
+            }
+        }
+    }
+    free(cand); free(hist_idx); free(hist_bin);
+    free_grid(&g);
+    return nmatches;
+}

@@ -236,6 +236,18 @@ int oracle_search_by_bow_kf(const oracle_frame* k1, const uint8_t* ok1, int n1, 
                             int n2, const uint32_t* nodes2, const int32_t* start2, const int32_t* idx2, float nnratio,
                             int check_ori, int32_t* matches12);
 
+/* ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const set<MapPoint*>&
+ * sAlreadyFound, float th, int ORBdist) (R/src/ORBmatcher.cpp:1719-1800, Tracking::Relocalization):
+ * per keyframe map point i (mp_valid = set, not bad, not already found): projection with
+ * Tcw (3x4), Ow = the frame's camera centre, mp_min/max_dist = mfMinDistance / mfMaxDistance,
+ * PredictScale on the frame (log_scale_factor, n_levels), window levels level-1 .. level+1.
+ * cur_mp as for oracle_search_by_projection_ff (new matches hold i).  Returns nmatches. */
+int oracle_search_by_projection_kf(const oracle_frame* cur, const float* Tcw, const float* Ow, const oracle_frame* kf,
+                                   const uint8_t* mp_valid, const float* mp_xyz, const float* mp_min_dist,
+                                   const float* mp_max_dist, const uint8_t* mp_desc, const float* cam4,
+                                   float log_scale_factor, int n_levels, const float* scale_factors, float th,
+                                   int orb_dist, int check_ori, int32_t* cur_mp);
+
 #ifdef __cplusplus
 }
 #endif

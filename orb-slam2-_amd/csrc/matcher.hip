@@ -667,7 +667,7 @@ __global__ __launch_bounds__(64) void k_resolve_sfi(const orb_keypoint* __restri
     kept = wave_reduce_sum_i32(kept);
     if (lane == 0) nmatches_out[b] = kept;
 #ifdef ORB_TIMING
-    if (lane == 0 && b == 0)
+    if (lane == 0 && (b == 0 || b == 5))
         printf("resolve b0: init %lld stage %lld loop %lld (gather %lld decide %lld fallback %lld) final %lld total %lld "
                "n1 %d n2 %d act %d fall %d match %d batches %d\n",
                t_init - t_begin, tStage, tLoop, tA, tB, tFall, clock64() - t_loopend, clock64() - t_begin, n1, n2, nAct, nFall,
@@ -746,7 +746,7 @@ __global__ __launch_bounds__(64) void k_resolve_sbp(const orb_keypoint* __restri
                                                     int checkOri, const uint32_t* __restrict__ cand,
                                                     const int* __restrict__ ncand, int32_t* __restrict__ curMp,
                                                     int32_t* __restrict__ nmatches_out, int32_t* __restrict__ histIdx,
-                                                    uint8_t* __restrict__ histBin) {
+                                                    uint8_t* __restrict__ histBin, int thDist) {
     extern __shared__ __attribute__((aligned(16))) int sm[];
     const int lane = threadIdx.x;
     int* ckey = sm;              // [ncur]
@@ -775,7 +775,7 @@ __global__ __launch_bounds__(64) void k_resolve_sbp(const orb_keypoint* __restri
         }
         if (accKey == ~0ull) continue;
         const int bestDist = (int)(accKey >> 40), bestIdx2 = (int)(accKey & 0xFFFFFull);
-        if (bestDist <= kThHigh) {
+        if (bestDist <= thDist) {   // TH_HIGH (:1671), ORBdist for the relocalisation form (:1789)
             if (lane == 0) {
                 curMp[bestIdx2] = i;
                 if (checkOri) {
@@ -811,6 +811,79 @@ __global__ __launch_bounds__(64) void k_resolve_sbp(const orb_keypoint* __restri
         nmatches -= wave_reduce_sum_i32(removed);
     }
     if (lane == 0) *nmatches_out = nmatches;
+}
+
+// ---------------------------------------------------------------- SearchByProjection(Frame, KeyFrame, set, th, ORBdist)
+
+struct SbkParams {
+    float Tcw[12];
+    float Ow[3];
+    float fx, fy, cx, cy;
+    float logsf;
+    int nlev;
+    float sf[32];
+    float th;
+};
+
+// One wave per keyframe map point (Tracking::Relocalization's projection search,
+// R/src/ORBmatcher.cpp:1719-1800): Rcw x + tcw (double-accumulated rows rounded to float),
+// invzc = 1.0 / z with no depth test, the frame-bounds test, cv::norm(PO) against 0.8 / 1.2 x the
+// point's min / max distance, PredictScale on the frame, GetFeaturesInArea(level-1, level+1) and
+// the Hamming distances; k_resolve_sbp then replays the keyframe order with the occupancy skip.
+__global__ __launch_bounds__(256) void k_cand_sbk(const orb_keypoint* __restrict__ kc, const uint8_t* __restrict__ dc,
+                                                  int nc_, int nmp, const uint8_t* __restrict__ valid,
+                                                  const float* __restrict__ xyz, const float* __restrict__ mind,
+                                                  const float* __restrict__ maxd, const uint8_t* __restrict__ mdesc,
+                                                  SbkParams P, GridParams g, uint32_t* __restrict__ cand,
+                                                  int* __restrict__ ncand, int* __restrict__ status) {
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int i = blockIdx.x * 4 + wid;
+    if (i >= nmp) return;
+    int* ncount = ncand + i;
+    if (!valid[i]) { if (lane == 0) *ncount = 0; return; }
+    const float* X = xyz + 3 * (size_t)i;
+    float x3[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        const double s = (double)P.Tcw[4 * r] * X[0] + (double)P.Tcw[4 * r + 1] * X[1] + (double)P.Tcw[4 * r + 2] * X[2];
+        x3[r] = (float)(s + (double)P.Tcw[4 * r + 3]);
+    }
+    const float invzc = (float)(1.0 / (double)x3[2]);
+    const float u = P.fx * x3[0] * invzc + P.cx;
+    const float v = P.fy * x3[1] * invzc + P.cy;
+    if (u < g.min_x || u > g.max_x || v < g.min_y || v > g.max_y) { if (lane == 0) *ncount = 0; return; }
+    const float PO[3] = {X[0] - P.Ow[0], X[1] - P.Ow[1], X[2] - P.Ow[2]};
+    const float ss = (PO[0] * PO[0] + PO[1] * PO[1]) + PO[2] * PO[2];
+    const float dist3D = (float)sqrt((double)ss);
+    const float maxDistance = 1.2f * maxd[i], minDistance = 0.8f * mind[i];
+    if (dist3D < minDistance || dist3D > maxDistance) { if (lane == 0) *ncount = 0; return; }
+    const float ratio = maxd[i] / dist3D;
+    int lev = (int)ceil(log((double)ratio) / (double)P.logsf);
+    if (lev < 0) lev = 0;
+    else if (lev >= P.nlev) lev = P.nlev - 1;
+    const float radius = P.th * P.sf[lev];
+    const AreaQuery q = make_area(g, u, v, radius, lev - 1, lev + 1);
+    uint32_t* out = cand + (size_t)i * kMaxCand;
+    const uint8_t* dq = mdesc + (size_t)i * 32;
+    int n = 0;
+    for (int j0 = 0; j0 < nc_; j0 += 64) {
+        const int j = j0 + lane;
+        bool ok = false;
+        int d = 0;
+        if (j < nc_ && q.cx0 <= q.cx1) {
+            const orb_keypoint k2 = kc[j];
+            ok = in_area(q, grid_cell(g, k2.x, k2.y), k2.octave, k2.x, k2.y);
+            if (ok) d = hamming32(dq, dc + (size_t)j * 32);
+        }
+        const uint64_t m = __ballot(ok);
+        const int pos = n + __popcll(m & ((1ull << lane) - 1ull));
+        if (ok && pos < kMaxCand) out[pos] = (uint32_t)j | ((uint32_t)d << 20);
+        n += __popcll(m);
+    }
+    if (lane == 0) {
+        if (n > kMaxCand) { atomicOr(status, 1); n = kMaxCand; }
+        *ncount = n;
+    }
 }
 
 // ---------------------------------------------------------------- SearchByProjection(Frame, local map points)
@@ -1592,7 +1665,84 @@ int orb_search_by_projection_frame(orb_matcher* m, const orb_frame_view* cur, co
     }
     const size_t lds = ((size_t)cur->n + kHisto + 4) * 4;
     hipLaunchKernelGGL(k_resolve_sbp, dim3(1), dim3(64), lds, s, m->d_k2, cur->n, m->d_k1, last->n, g, m->checkOri,
-                       m->d_cand, m->d_ncand, m->d_m12, m->d_nm, m->d_hI, m->d_hB);
+                       m->d_cand, m->d_ncand, m->d_m12, m->d_nm, m->d_hI, m->d_hB, kThHigh);
+    ORB_HIP_TRY(hipGetLastError());
+    ORB_HIP_TRY(hipMemcpyAsync(hcm, m->d_m12, (size_t)cur->n * 4, hipMemcpyDeviceToHost, s));
+    ORB_HIP_TRY(hipMemcpyAsync(hn, m->d_nm, 4, hipMemcpyDeviceToHost, s));
+    ORB_HIP_TRY(hipMemcpyAsync(hn + 1, m->d_status, 4, hipMemcpyDeviceToHost, s));
+    ORB_HIP_TRY(hipStreamSynchronize(s));
+    if (hn[1]) return ORB_EOVERFLOW;
+    std::memcpy(cur_mp, hcm, (size_t)cur->n * 4);
+    return hn[0];
+}
+
+int orb_search_by_projection_kf(orb_matcher* m, const orb_frame_view* cur, const float* Tcw_cur, const float Ow[3],
+                                const orb_frame_view* kf, const uint8_t* mp_valid, const float* mp_xyz,
+                                const float* mp_min_dist, const float* mp_max_dist, const uint8_t* mp_desc,
+                                const float cam[4], float log_scale_factor, int n_levels, const float* scale_factors,
+                                float th, int orb_dist, int32_t* cur_mp) {
+    if (!m || !cur || !Tcw_cur || !Ow || !kf || !mp_valid || !mp_xyz || !mp_min_dist || !mp_max_dist || !mp_desc ||
+        !cam || !scale_factors || !cur_mp || n_levels < 1 || n_levels > 32)
+        return ORB_EINVAL;
+    if (cur->n >= (1 << 20)) return ORB_EINVAL;
+    ORB_HIP_TRY(hipSetDevice(m->device));
+    const int nmp = kf->n;
+    const int cap = std::max(std::max(cur->n, nmp), 1);
+    int st = mensure(m, 1, cap);
+    if (st) return st;
+    SbkParams P;
+    std::memcpy(P.Tcw, Tcw_cur, sizeof(P.Tcw));
+    std::memcpy(P.Ow, Ow, sizeof(P.Ow));
+    P.fx = cam[0]; P.fy = cam[1]; P.cx = cam[2]; P.cy = cam[3];
+    P.logsf = log_scale_factor;
+    P.nlev = n_levels;
+    for (int l = 0; l < 32; l++) P.sf[l] = l < n_levels ? scale_factors[l] : 0.f;
+    P.th = th;
+    const size_t bytes = (size_t)cap * (2 * sizeof(orb_keypoint) + 32 + 32 + 4 + 12 + 4 + 4 + 1) + 1024;
+    st = mpin(m, bytes);
+    if (st) return st;
+    char* h = (char*)m->h_pin;
+    orb_keypoint* hkc = (orb_keypoint*)h;
+    orb_keypoint* hkl = hkc + cap;
+    uint8_t* hdc = (uint8_t*)(hkl + cap);
+    uint8_t* hmd = hdc + (size_t)cap * 32;
+    int32_t* hcm = (int32_t*)(hmd + (size_t)cap * 32);
+    float* hxyz = (float*)(hcm + cap);
+    float* hmin = hxyz + 3 * (size_t)cap;
+    float* hmax = hmin + cap;
+    uint8_t* hval = (uint8_t*)(hmax + cap);
+    int32_t* hn = (int32_t*)(((uintptr_t)(hval + cap) + 15) & ~(uintptr_t)15);
+    pack_view(cur, hkc);
+    pack_view(kf, hkl);
+    std::memcpy(hdc, cur->desc, (size_t)cur->n * 32);
+    std::memcpy(hmd, mp_desc, (size_t)nmp * 32);
+    std::memcpy(hcm, cur_mp, (size_t)cur->n * 4);
+    std::memcpy(hxyz, mp_xyz, (size_t)nmp * 12);
+    std::memcpy(hmin, mp_min_dist, (size_t)nmp * 4);
+    std::memcpy(hmax, mp_max_dist, (size_t)nmp * 4);
+    std::memcpy(hval, mp_valid, (size_t)nmp);
+    // scratch: the keyframe-side buffers of the frame-to-frame form (xyz, outlier = valid,
+    // hasMp = min distance, ur = max distance), all sized for cap entries by mensure
+    hipStream_t s = m->stream;
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_k2, hkc, (size_t)cur->n * sizeof(orb_keypoint), hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_k1, hkl, (size_t)nmp * sizeof(orb_keypoint), hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_d2, hdc, (size_t)cur->n * 32, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_mpd, hmd, (size_t)nmp * 32, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_m12, hcm, (size_t)cur->n * 4, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_xyz, hxyz, (size_t)nmp * 12, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_hasMp, hmin, (size_t)nmp * 4, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_ur, hmax, (size_t)nmp * 4, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_outl, hval, (size_t)nmp, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemsetAsync(m->d_status, 0, 4, s));
+    const GridParams g = grid_of(cur);
+    if (nmp > 0) {
+        hipLaunchKernelGGL(k_cand_sbk, dim3((nmp + 3) / 4), dim3(256), 0, s, m->d_k2, m->d_d2, cur->n, nmp, m->d_outl,
+                           m->d_xyz, (const float*)m->d_hasMp, (const float*)m->d_ur, m->d_mpd, P, g, m->d_cand,
+                           m->d_ncand, m->d_status);
+    }
+    const size_t lds = ((size_t)cur->n + kHisto + 4) * 4;
+    hipLaunchKernelGGL(k_resolve_sbp, dim3(1), dim3(64), lds, s, m->d_k2, cur->n, m->d_k1, nmp, g, m->checkOri,
+                       m->d_cand, m->d_ncand, m->d_m12, m->d_nm, m->d_hI, m->d_hB, orb_dist);
     ORB_HIP_TRY(hipGetLastError());
     ORB_HIP_TRY(hipMemcpyAsync(hcm, m->d_m12, (size_t)cur->n * 4, hipMemcpyDeviceToHost, s));
     ORB_HIP_TRY(hipMemcpyAsync(hn, m->d_nm, 4, hipMemcpyDeviceToHost, s));

@@ -145,6 +145,34 @@ class ORBmatcher:
             _abi.ptr(cur_mp)))
         return n, cur_mp
 
+    def SearchByProjectionKF(self, CurrentFrame: Frame, pKF: Frame, mp_valid, mp_xyz, mp_min_dist, mp_max_dist,
+                             mp_desc, cam, Ow, log_scale_factor, th: float, ORBdist: int, cur_mp=None):
+        """SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const set<MapPoint*>& sAlreadyFound,
+        th, ORBdist) (R/src/ORBmatcher.cpp:1719-1800).  Keyframe map points per keyframe keypoint
+        (mp_valid = set, not bad, not in sAlreadyFound; mfMinDistance / mfMaxDistance); cam =
+        (fx, fy, cx, cy); Ow = the frame's camera centre.  cur_mp: -1 empty, -2 already set.
+        Returns (nmatches, cur_mp) with cur_mp[i2] = the keyframe map point index assigned."""
+        if cur_mp is None:
+            cur_mp = np.full(CurrentFrame.N, -1, np.int32)
+        cur_mp = np.ascontiguousarray(cur_mp, np.int32).copy()
+        vc, vk = CurrentFrame.view(), pKF.view()
+        Tc = np.ascontiguousarray(np.asarray(CurrentFrame.mTcw, np.float32)[:3, :4])
+        a = [np.ascontiguousarray(x, t) for x, t in ((mp_valid, np.uint8), (mp_xyz, np.float32),
+                                                      (mp_min_dist, np.float32), (mp_max_dist, np.float32),
+                                                      (mp_desc, np.uint8))]
+        sf = np.ascontiguousarray(CurrentFrame.mvScaleFactors, np.float32)
+        camv = np.ascontiguousarray(np.asarray(cam, np.float32)[:4])
+        ow = np.ascontiguousarray(Ow, np.float32)
+        lib = _abi.lib()
+        vp = C.c_void_p
+        lib.orb_search_by_projection_kf.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, C.c_float, C.c_int, vp,
+                                                    C.c_float, C.c_int, vp]
+        lib.orb_search_by_projection_kf.restype = C.c_int
+        n = _abi.check("orb_search_by_projection_kf", lib.orb_search_by_projection_kf(
+            self._h, C.byref(vc), _abi.ptr(Tc), _abi.ptr(ow), C.byref(vk), *[_abi.ptr(x) for x in a], _abi.ptr(camv),
+            float(np.float32(log_scale_factor)), len(sf), _abi.ptr(sf), float(th), int(ORBdist), _abi.ptr(cur_mp)))
+        return n, cur_mp
+
     def SearchByProjectionLocal(self, F: Frame, vpMapPoints: LocalMapPoints, th: float = 3.0, cur_mp=None):
         """SearchByProjection(Frame&, const vector<MapPoint*>&, th).  cur_mp mirrors
         F.mvpMapPoints (-1 empty, -2 map point with observations, -3 without); returns

@@ -477,3 +477,16 @@ def featvec_arrays(fv):
     start[1:] = np.cumsum([len(fv[k]) for k in keys])
     idx = np.array([i for k in keys for i in fv[k]], np.int32)
     return np.array(keys, np.uint32), start, idx
+
+
+def search_by_projection_kf(cur, Tcw, Ow, kf, mp_valid, mp_xyz, mp_min, mp_max, mp_desc, cam4, log_sf, scale_factors,
+                            th, orb_dist, check_ori=True, cur_mp=None):
+    """oracle_search_by_projection_kf (Relocalization's projection search)."""
+    cur_mp = np.full(cur.s.n, -1, np.int32) if cur_mp is None else np.ascontiguousarray(cur_mp, np.int32).copy()
+    a = [np.ascontiguousarray(x, t) for x, t in ((Tcw, np.float32), (Ow, np.float32), (mp_valid, np.uint8),
+                                                  (mp_xyz, np.float32), (mp_min, np.float32), (mp_max, np.float32),
+                                                  (mp_desc, np.uint8), (cam4, np.float32), (scale_factors, np.float32))]
+    n = lib().oracle_search_by_projection_kf(C.byref(cur.s), P(a[0]), P(a[1]), C.byref(kf.s), *[P(x) for x in a[2:8]],
+                                             C.c_float(log_sf), len(a[8]), P(a[8]), C.c_float(th), int(orb_dist),
+                                             int(check_ori), P(cur_mp))
+    return n, cur_mp

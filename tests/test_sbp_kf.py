@@ -1,0 +1,70 @@
+"""ORBmatcher::SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, th, ORBdist)
+(R/src/ORBmatcher.cpp:1719-1800, Tracking::Relocalization): the oracle finds the planted
+correspondences (CPU); the gfx950 candidate kernel + sequential replay bit-exact against the oracle
+(GPU), with pre-occupied frame slots, both orientation settings and two ORBdist values."""
+import numpy as np
+import pytest
+
+import oracle_ref as O
+
+
+def _problem(seed=3, **kw):
+    from orb_slam2_amd import synth
+    p = synth.fuse_problem(seed=seed, **kw)
+    rng = np.random.default_rng(seed + 100)
+    kf = p["kf"]
+    kf["angle"] = rng.uniform(0, 360, len(kf["x"])).astype(np.float32)
+    n_mp = len(p["mp_xyz"])
+    kfs = {"x": rng.uniform(0, 640, n_mp).astype(np.float32), "y": rng.uniform(0, 480, n_mp).astype(np.float32),
+           "octave": np.zeros(n_mp, np.int32), "desc": np.zeros((n_mp, 32), np.uint8),
+           "angle": ((rng.uniform(0, 360, n_mp) if seed % 2 else 40.0 + rng.normal(0, 2, n_mp)) % 360).astype(np.float32),
+           "W": 640, "H": 480}
+    if seed % 2 == 0:   # a dominant rotation: current-frame angles = keyframe angles - 40 deg for most
+        kf["angle"] = (rng.normal(0, 2, len(kf["x"])) % 360).astype(np.float32)
+    occ = np.full(len(kf["x"]), -1, np.int32)
+    occ[rng.random(len(occ)) < 0.1] = -2
+    return p, kf, kfs, occ
+
+
+def _oracle(p, kf, kfs, occ, th, orb_dist, check_ori):
+    cur = O.FrameView(kf, kf["desc"], kf["W"], kf["H"])
+    kv = O.FrameView(kfs, kfs["desc"], kfs["W"], kfs["H"])
+    kp = p["kp"]
+    return O.search_by_projection_kf(cur, kp["Tcw"][:3, :4], kp["Ow"], kv, p["mp_valid"], p["mp_xyz"], p["mp_min_dist"],
+                                     p["mp_max_dist"], p["mp_desc"], kp["cam"][:4], kp["log_scale_factor"],
+                                     kp["scale_factors"], th, orb_dist, check_ori, occ)
+
+
+def test_oracle_finds_planted_points():
+    p, kf, kfs, occ = _problem()
+    n, m = _oracle(p, kf, kfs, np.full(len(kf["x"]), -1, np.int32), 10.0, 100, False)
+    assert n > 0.3 * len(p["mp_xyz"])
+    assert len(set(m[m >= 0].tolist())) == n                  # one frame slot per map point
+
+
+def _frame(k, kp):
+    from orb_slam2_amd import Frame
+    a = np.zeros(len(k["x"]), dtype=[("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+    a["x"], a["y"], a["angle"], a["octave"] = k["x"], k["y"], k["angle"], k["octave"]
+    T = np.eye(4, dtype=np.float32)
+    if kp is not None:
+        T[:3, :4] = np.asarray(kp["Tcw"], np.float32)[:3, :4]
+    return Frame(a, k["desc"], k["W"], k["H"], mTcw=T,
+                 mvScaleFactors=None if kp is None else np.asarray(kp["scale_factors"], np.float32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,th,orb_dist,ori", [(3, 10.0, 100, True), (4, 10.0, 100, True), (5, 5.0, 64, False),
+                                                  (6, 3.0, 50, True)])
+def test_search_by_projection_kf_gpu(amd, seed, th, orb_dist, ori):
+    p, kf, kfs, occ = _problem(seed)
+    rn, rm = _oracle(p, kf, kfs, occ, th, orb_dist, ori)
+    kp = p["kp"]
+    m = amd.ORBmatcher(0.75, ori)
+    n, gm = m.SearchByProjectionKF(_frame(kf, kp), _frame(kfs, None), p["mp_valid"], p["mp_xyz"], p["mp_min_dist"],
+                                   p["mp_max_dist"], p["mp_desc"], kp["cam"][:4], kp["Ow"], kp["log_scale_factor"],
+                                   th, orb_dist, occ)
+    assert n == rn and np.array_equal(gm, rm)
+    assert n > 0
+    m.close()
