@@ -299,6 +299,19 @@ int orb_search_by_projection_frame(orb_matcher* m, const orb_frame_view* cur, co
                                    const float* scale_factors, const float cam[6], float th,
                                    int mono, int32_t* cur_mp);
 
+/* ORBmatcher::SearchByProjection(KeyFrame* pKF, cv::Mat Scw, const vector<MapPoint*>& vpPoints,
+ * vector<MapPoint*>& vpMatched, int th) — R/src/ORBmatcher.cpp:370-497 (LoopClosing::ComputeSim3).
+ *   kf: the keyframe as a frame view (mvKeysUn, mDescriptors, bounds, grid); kp: Tcw = rows of
+ *   [Rcw | tcw] with the scale removed and Ow = -Rcw^T tcw as the reference computes them from Scw,
+ *   fx .. cy, mfLogScaleFactor, mnScaleLevels, mvScaleFactors (bf, inv_level_sigma2 unused);
+ *   mp_valid[i] != 0 when vpPoints[i] is not bad and not already in vpMatched; mp_* as for orb_fuse.
+ * matched (in/out, kf->n ints): -1 = vpMatched[idx] empty, any other negative value = set before the
+ * call, >= 0 on return = the vpPoints index assigned.  Returns nmatches. */
+int orb_search_by_projection_sim3(orb_matcher* m, const orb_frame_view* kf, const orb_kf_params* kp, int n_mp,
+                                  const uint8_t* mp_valid, const float* mp_xyz, const float* mp_normal,
+                                  const float* mp_min_dist, const float* mp_max_dist, const uint8_t* mp_desc, float th,
+                                  int32_t* matched);
+
 /* ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const set<MapPoint*>&
  * sAlreadyFound, float th, int ORBdist) — R/src/ORBmatcher.cpp:1719-1800 (Tracking::Relocalization).
  *   cur: the frame (mvKeysUn, mDescriptors, bounds, grid); Tcw_cur: rows 0..2 of mTcw; Ow: its

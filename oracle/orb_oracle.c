@@ -1797,3 +1797,58 @@ int oracle_search_by_projection_kf(const oracle_frame* cur, const float* Tcw, co
     free_grid(&g);
     return nmatches;
 }
+
+/* R/src/ORBmatcher.cpp:370-497, literally (float products restated as in oracle_fuse). */
+int oracle_search_by_projection_sim3(const oracle_frame* kf, const oracle_kf_params* kp, int n_mp,
+                                     const uint8_t* mp_valid, const float* mp_xyz, const float* mp_normal,
+                                     const float* mp_min_dist, const float* mp_max_dist, const uint8_t* mp_desc,
+                                     float th, int32_t* matched)
+{
+    ogrid g;
+    build_grid(kf, &g);
+    int* cand = (int*)malloc(sizeof(int) * (kf->n + 1));
+    int nmatches = 0;
+    for (int i = 0; i < n_mp; i++) {
+        if (!mp_valid[i]) continue;
+        const float* X = mp_xyz + 3 * (size_t)i;
+        float p3[3];
+        mat34_apply(kp->Tcw, X, p3);
+        if (p3[2] < 0.0f) continue;
+        const float invz = 1 / p3[2];
+        const float x = p3[0] * invz, y = p3[1] * invz;
+        const float u = kp->fx * x + kp->cx, v = kp->fy * y + kp->cy;
+        if (!(u >= kf->min_x && u < kf->max_x && v >= kf->min_y && v < kf->max_y)) continue;   /* IsInImage */
+        const float maxDistance = 1.2f * mp_max_dist[i], minDistance = 0.8f * mp_min_dist[i];
+        const float PO[3] = {X[0] - kp->Ow[0], X[1] - kp->Ow[1], X[2] - kp->Ow[2]};
+        const float ss = (PO[0] * PO[0] + PO[1] * PO[1]) + PO[2] * PO[2];
+        const float dist = (float)sqrt((double)ss);
+        if (dist < minDistance || dist > maxDistance) continue;
+        const float* Pn = mp_normal + 3 * (size_t)i;
+        const float dot = (PO[0] * Pn[0] + PO[1] * Pn[1]) + PO[2] * Pn[2];
+        if ((double)dot < 0.5 * dist) continue;
+        const float ratio = mp_max_dist[i] / dist;
+        int lev = (int)ceil(log((double)ratio) / (double)kp->log_scale_factor);
+        if (lev < 0) lev = 0;
+        else if (lev >= kp->n_levels) lev = kp->n_levels - 1;
+        const float radius = th * kp->scale_factors[lev];
+        const int nc = features_in_area(kf, &g, u, v, radius, -1, -1, cand, kf->n);
+        if (nc == 0) continue;
+        const uint8_t* dMP = mp_desc + (size_t)i * 32;
+        int bestDist = 256, bestIdx = -1;
+        for (int q = 0; q < nc; q++) {
+            const int idx = cand[q];
+            if (matched[idx] != -1) continue;
+            const int kpLevel = kf->octave[idx];
+            if (kpLevel < lev - 1 || kpLevel > lev) continue;
+            const int d = oracle_descriptor_distance(dMP, kf->desc + (size_t)idx * 32);
+            if (d < bestDist) { bestDist = d; bestIdx = idx; }
+        }
+        if (bestDist <= TH_LOW) {
+            matched[bestIdx] = i;
+            nmatches++;
+        }
+    }
+    free(cand);
+    free_grid(&g);
+    return nmatches;
+}

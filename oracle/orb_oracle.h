@@ -248,6 +248,15 @@ int oracle_search_by_projection_kf(const oracle_frame* cur, const float* Tcw, co
                                    float log_scale_factor, int n_levels, const float* scale_factors, float th,
                                    int orb_dist, int check_ori, int32_t* cur_mp);
 
+/* ORBmatcher::SearchByProjection(KeyFrame*, cv::Mat Scw, vpPoints, vpMatched, th)
+ * (R/src/ORBmatcher.cpp:370-497): kp as for oracle_fuse (Tcw with the scale removed, Ow);
+ * matched (in/out): -1 empty, other negatives pre-set, >= 0 the point index assigned.  Returns
+ * nmatches. */
+int oracle_search_by_projection_sim3(const oracle_frame* kf, const oracle_kf_params* kp, int n_mp,
+                                     const uint8_t* mp_valid, const float* mp_xyz, const float* mp_normal,
+                                     const float* mp_min_dist, const float* mp_max_dist, const uint8_t* mp_desc,
+                                     float th, int32_t* matched);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1246,6 +1246,79 @@ __global__ __launch_bounds__(256) void k_fuse(const orb_keypoint* __restrict__ k
     }
 }
 
+// ------------------------------------------------------------------ SearchByProjection(KeyFrame, Scw, points, matched, th)
+// LoopClosing's projection search (R/src/ORBmatcher.cpp:370-497): one wave per candidate map
+// point with Fuse's gates minus the reprojection test — depth >= 0, KeyFrame::IsInImage, 0.8 / 1.2 x
+// the min / max distance, the viewing-angle test, PredictScale on the keyframe, GetFeaturesInArea
+// with octaves level-1 .. level — and every candidate's distance; k_resolve_sbp replays the point
+// order with the vpMatched skip (first window entry on ties, bestDist <= TH_LOW, no rotation test).
+__global__ __launch_bounds__(256) void k_cand_sbs(const orb_keypoint* __restrict__ kk, const uint8_t* __restrict__ kd,
+                                                  int nk, GridParams g, FuseKf K, int n_mp,
+                                                  const uint8_t* __restrict__ valid, const float* __restrict__ xyz,
+                                                  const float* __restrict__ nrm, const float* __restrict__ mind,
+                                                  const float* __restrict__ maxd, const uint8_t* __restrict__ mdesc,
+                                                  float th, uint32_t* __restrict__ cand, int* __restrict__ ncand,
+                                                  int* __restrict__ status) {
+    const int lane = threadIdx.x & 63;
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n_mp) return;
+    bool go = valid[i] != 0;
+    const float* X = xyz + 3 * (size_t)i;
+    float u = 0, v = 0, radius = 0;
+    int lev = 0;
+    if (go) {
+        float p3[3];
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            const double s = (double)K.Tcw[4 * r] * X[0] + (double)K.Tcw[4 * r + 1] * X[1] + (double)K.Tcw[4 * r + 2] * X[2];
+            p3[r] = (float)(s + (double)K.Tcw[4 * r + 3]);
+        }
+        go = !(p3[2] < 0.0f);
+        const float invz = 1 / p3[2];
+        const float x = p3[0] * invz, y = p3[1] * invz;
+        u = K.fx * x + K.cx;
+        v = K.fy * y + K.cy;
+        go = go && u >= g.min_x && u < g.max_x && v >= g.min_y && v < g.max_y;   // KeyFrame::IsInImage
+        const float maxDistance = 1.2f * maxd[i], minDistance = 0.8f * mind[i];
+        const float PO[3] = {X[0] - K.Ow[0], X[1] - K.Ow[1], X[2] - K.Ow[2]};
+        const float ss = (PO[0] * PO[0] + PO[1] * PO[1]) + PO[2] * PO[2];
+        const float dist = (float)sqrt((double)ss);
+        go = go && !(dist < minDistance || dist > maxDistance);
+        const float* Pn = nrm + 3 * (size_t)i;
+        const float dot = (PO[0] * Pn[0] + PO[1] * Pn[1]) + PO[2] * Pn[2];
+        go = go && !((double)dot < 0.5 * dist);
+        const float ratio = maxd[i] / dist;
+        lev = (int)ceil(log((double)ratio) / (double)K.logsf);
+        if (lev < 0) lev = 0;
+        else if (lev >= K.nlev) lev = K.nlev - 1;
+        radius = th * K.sf[lev];
+    }
+    int n = 0;
+    if (go) {
+        const AreaQuery q = make_area(g, u, v, radius, -1, -1);
+        const uint8_t* dq = mdesc + (size_t)i * 32;
+        uint32_t* out = cand + (size_t)i * kMaxCand;
+        for (int j0 = 0; j0 < nk && q.cx0 <= q.cx1; j0 += 64) {
+            const int j = j0 + lane;
+            bool ok = false;
+            int d = 0;
+            if (j < nk) {
+                const orb_keypoint k2 = kk[j];
+                ok = in_area(q, grid_cell(g, k2.x, k2.y), k2.octave, k2.x, k2.y) && !(k2.octave < lev - 1 || k2.octave > lev);
+                if (ok) d = hamming32(dq, kd + (size_t)j * 32);
+            }
+            const uint64_t m = __ballot(ok);
+            const int pos = n + __popcll(m & ((1ull << lane) - 1ull));
+            if (ok && pos < kMaxCand) out[pos] = (uint32_t)j | ((uint32_t)d << 20);
+            n += __popcll(m);
+        }
+    }
+    if (lane == 0) {
+        if (n > kMaxCand) { atomicOr(status, 1); n = kMaxCand; }
+        ncand[i] = n;
+    }
+}
+
 // ------------------------------------------------------------------ SearchForTriangulation
 // ORBmatcher::SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo)
 // (R/src/ORBmatcher.cpp:785-983).  Keypoints only meet inside a common vocabulary node, and a
@@ -1750,6 +1823,81 @@ int orb_search_by_projection_kf(orb_matcher* m, const orb_frame_view* cur, const
     ORB_HIP_TRY(hipStreamSynchronize(s));
     if (hn[1]) return ORB_EOVERFLOW;
     std::memcpy(cur_mp, hcm, (size_t)cur->n * 4);
+    return hn[0];
+}
+
+int orb_search_by_projection_sim3(orb_matcher* m, const orb_frame_view* kf, const orb_kf_params* kp, int n_mp,
+                                  const uint8_t* mp_valid, const float* mp_xyz, const float* mp_normal,
+                                  const float* mp_min_dist, const float* mp_max_dist, const uint8_t* mp_desc, float th,
+                                  int32_t* matched) {
+    if (!m || !kf || !kp || !matched || n_mp < 0 || (n_mp > 0 && (!mp_valid || !mp_xyz || !mp_normal || !mp_min_dist ||
+                                                                   !mp_max_dist || !mp_desc)))
+        return ORB_EINVAL;
+    if (kp->n_levels < 1 || kp->n_levels > 32 || !kp->scale_factors || kf->n >= (1 << 20)) return ORB_EINVAL;
+    ORB_HIP_TRY(hipSetDevice(m->device));
+    const int cap = std::max(std::max(kf->n, n_mp), 1);
+    int st = mensure(m, 1, cap);
+    if (st) return st;
+    FuseKf K;
+    std::memcpy(K.Tcw, kp->Tcw, sizeof(K.Tcw));
+    std::memcpy(K.Ow, kp->Ow, sizeof(K.Ow));
+    K.fx = kp->fx; K.fy = kp->fy; K.cx = kp->cx; K.cy = kp->cy; K.bf = kp->bf; K.logsf = kp->log_scale_factor;
+    K.nlev = kp->n_levels;
+    for (int l = 0; l < 32; l++) {
+        K.sf[l] = l < kp->n_levels ? kp->scale_factors[l] : 0.f;
+        K.isig2[l] = 0.f;
+    }
+    const size_t bytes = (size_t)cap * (sizeof(orb_keypoint) + 32 + 32 + 4 + 12 + 12 + 4 + 4 + 1) + 1024;
+    st = mpin(m, bytes);
+    if (st) return st;
+    char* h = (char*)m->h_pin;
+    orb_keypoint* hk = (orb_keypoint*)h;
+    uint8_t* hd = (uint8_t*)(hk + cap);
+    uint8_t* hmd = hd + (size_t)cap * 32;
+    int32_t* hm = (int32_t*)(hmd + (size_t)cap * 32);
+    float* hxyz = (float*)(hm + cap);
+    float* hnrm = hxyz + 3 * (size_t)cap;
+    float* hmin = hnrm + 3 * (size_t)cap;
+    float* hmax = hmin + cap;
+    uint8_t* hval = (uint8_t*)(hmax + cap);
+    int32_t* hn = (int32_t*)(((uintptr_t)(hval + cap) + 15) & ~(uintptr_t)15);
+    pack_view(kf, hk);
+    std::memcpy(hd, kf->desc, (size_t)kf->n * 32);
+    std::memcpy(hmd, mp_desc, (size_t)n_mp * 32);
+    std::memcpy(hm, matched, (size_t)kf->n * 4);
+    std::memcpy(hxyz, mp_xyz, (size_t)n_mp * 12);
+    std::memcpy(hnrm, mp_normal, (size_t)n_mp * 12);
+    std::memcpy(hmin, mp_min_dist, (size_t)n_mp * 4);
+    std::memcpy(hmax, mp_max_dist, (size_t)n_mp * 4);
+    std::memcpy(hval, mp_valid, (size_t)n_mp);
+    // scratch: d_d1 (32 B per entry) holds the normals, d_hasMp / d_ur the min / max distances
+    hipStream_t s = m->stream;
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_k2, hk, (size_t)kf->n * sizeof(orb_keypoint), hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_d2, hd, (size_t)kf->n * 32, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_mpd, hmd, (size_t)n_mp * 32, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_m12, hm, (size_t)kf->n * 4, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_xyz, hxyz, (size_t)n_mp * 12, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_d1, hnrm, (size_t)n_mp * 12, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_hasMp, hmin, (size_t)n_mp * 4, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_ur, hmax, (size_t)n_mp * 4, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(m->d_outl, hval, (size_t)n_mp, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemsetAsync(m->d_status, 0, 4, s));
+    const GridParams g = grid_of(kf);
+    if (n_mp > 0) {
+        hipLaunchKernelGGL(k_cand_sbs, dim3((n_mp + 3) / 4), dim3(256), 0, s, m->d_k2, m->d_d2, kf->n, g, K, n_mp,
+                           m->d_outl, m->d_xyz, (const float*)m->d_d1, (const float*)m->d_hasMp,
+                           (const float*)m->d_ur, m->d_mpd, th, m->d_cand, m->d_ncand, m->d_status);
+    }
+    const size_t lds = ((size_t)kf->n + kHisto + 4) * 4;
+    hipLaunchKernelGGL(k_resolve_sbp, dim3(1), dim3(64), lds, s, m->d_k2, kf->n, m->d_k2, n_mp, g, 0, m->d_cand,
+                       m->d_ncand, m->d_m12, m->d_nm, m->d_hI, m->d_hB, kThLow);
+    ORB_HIP_TRY(hipGetLastError());
+    ORB_HIP_TRY(hipMemcpyAsync(hm, m->d_m12, (size_t)kf->n * 4, hipMemcpyDeviceToHost, s));
+    ORB_HIP_TRY(hipMemcpyAsync(hn, m->d_nm, 4, hipMemcpyDeviceToHost, s));
+    ORB_HIP_TRY(hipMemcpyAsync(hn + 1, m->d_status, 4, hipMemcpyDeviceToHost, s));
+    ORB_HIP_TRY(hipStreamSynchronize(s));
+    if (hn[1]) return ORB_EOVERFLOW;
+    std::memcpy(matched, hm, (size_t)kf->n * 4);
     return hn[0];
 }
 

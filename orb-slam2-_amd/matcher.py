@@ -173,6 +173,30 @@ class ORBmatcher:
             float(np.float32(log_scale_factor)), len(sf), _abi.ptr(sf), float(th), int(ORBdist), _abi.ptr(cur_mp)))
         return n, cur_mp
 
+    def SearchByProjectionSim3(self, pKF: Frame, Tcw, Ow, cam, log_scale_factor, scale_factors, mp_valid, mp_xyz,
+                               mp_normal, mp_min_dist, mp_max_dist, mp_desc, th: float, matched=None):
+        """SearchByProjection(KeyFrame* pKF, cv::Mat Scw, vpPoints, vpMatched, th)
+        (R/src/ORBmatcher.cpp:370-497).  Tcw = [Rcw | tcw] with the Sim3 scale removed and Ow =
+        -Rcw^T tcw as the reference derives them from Scw; cam = (fx, fy, cx, cy); points as for
+        Fuse (mp_valid = not bad and not already matched).  matched: -1 empty, -2 set before.
+        Returns (nmatches, matched) with matched[idx] = the vpPoints index assigned."""
+        matched = np.full(pKF.N, -1, np.int32) if matched is None else np.ascontiguousarray(matched, np.int32).copy()
+        sf = np.ascontiguousarray(scale_factors, np.float32)
+        kp = KfParams((C.c_float * 12)(*np.asarray(Tcw, np.float32).reshape(-1)[:12]),
+                      (C.c_float * 3)(*np.asarray(Ow, np.float32)), *[float(np.float32(v)) for v in cam[:4]], 0.0,
+                      float(np.float32(log_scale_factor)), len(sf), _abi.ptr(sf), None)
+        a = [np.ascontiguousarray(x, t) for x, t in ((mp_valid, np.uint8), (mp_xyz, np.float32), (mp_normal, np.float32),
+                                                      (mp_min_dist, np.float32), (mp_max_dist, np.float32),
+                                                      (mp_desc, np.uint8))]
+        v = pKF.view()
+        lib = _abi.lib()
+        vp = C.c_void_p
+        lib.orb_search_by_projection_sim3.argtypes = [vp, vp, vp, C.c_int, vp, vp, vp, vp, vp, vp, C.c_float, vp]
+        lib.orb_search_by_projection_sim3.restype = C.c_int
+        n = _abi.check("orb_search_by_projection_sim3", lib.orb_search_by_projection_sim3(
+            self._h, C.byref(v), C.byref(kp), len(a[0]), *[_abi.ptr(x) for x in a], float(th), _abi.ptr(matched)))
+        return n, matched
+
     def SearchByProjectionLocal(self, F: Frame, vpMapPoints: LocalMapPoints, th: float = 3.0, cur_mp=None):
         """SearchByProjection(Frame&, const vector<MapPoint*>&, th).  cur_mp mirrors
         F.mvpMapPoints (-1 empty, -2 map point with observations, -3 without); returns

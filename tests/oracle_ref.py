@@ -490,3 +490,19 @@ def search_by_projection_kf(cur, Tcw, Ow, kf, mp_valid, mp_xyz, mp_min, mp_max, 
                                              C.c_float(log_sf), len(a[8]), P(a[8]), C.c_float(th), int(orb_dist),
                                              int(check_ori), P(cur_mp))
     return n, cur_mp
+
+
+def search_by_projection_sim3(prob, th=10.0, matched=None):
+    """oracle_search_by_projection_sim3 on a synth.fuse_problem (the keyframe and its pose with
+    the Sim3 scale already removed): (nmatches, matched)."""
+    kf = prob["kf"]
+    fv = FrameView(kf, kf["desc"], kf["W"], kf["H"], kf["uright"])
+    kp = kf_params(prob["kp"])
+    n = len(prob["mp_valid"])
+    a = {k: np.ascontiguousarray(prob[k]) for k in ("mp_valid", "mp_xyz", "mp_normal", "mp_min_dist", "mp_max_dist",
+                                                    "mp_desc")}
+    m = np.full(len(kf["x"]), -1, np.int32) if matched is None else np.ascontiguousarray(matched, np.int32).copy()
+    nm = lib().oracle_search_by_projection_sim3(C.byref(fv.s), C.byref(kp), n, P(a["mp_valid"]), P(a["mp_xyz"]),
+                                                P(a["mp_normal"]), P(a["mp_min_dist"]), P(a["mp_max_dist"]),
+                                                P(a["mp_desc"]), C.c_float(th), P(m))
+    return nm, m
