@@ -189,6 +189,49 @@ int orb_fuse(int device, const orb_frame_view* kf, const orb_kf_params* kp, int 
              const float* mp_xyz, const float* mp_normal, const float* mp_min_dist, const float* mp_max_dist,
              const uint8_t* mp_desc, float th, int32_t* best_idx, int32_t* best_dist);
 
+/* ORBmatcher::Fuse(KeyFrame* pKF, cv::Mat Scw, const vector<MapPoint*>& vpPoints, float th,
+ * vector<MapPoint*>& vpReplacePoint) — the matching step of R/src/ORBmatcher.cpp:1164-1290
+ * (LoopClosing::SearchAndFuse): kp->Tcw / Ow = [Rcw | tcw] with the Sim3 scale removed and
+ * -Rcw^T tcw as the reference derives them from Scw (bf, inv_level_sigma2 unused); mp_valid[i] =
+ * !isBad() && the point is not among pKF->GetMapPoints().  No reprojection-error gate.  best_idx /
+ * best_dist as for orb_fuse; the replace / add step (:1263-1283) stays with the caller, in vector
+ * order.  Host buffers. */
+int orb_fuse_sim3(int device, const orb_frame_view* kf, const orb_kf_params* kp, int n_mp, const uint8_t* mp_valid,
+                  const float* mp_xyz, const float* mp_normal, const float* mp_min_dist, const float* mp_max_dist,
+                  const uint8_t* mp_desc, float th, int32_t* best_idx, int32_t* best_dist);
+
+/* One keyframe's side of ORBmatcher::SearchBySim3: Tcw = [R|t] world -> this camera
+ * (GetRotation / GetTranslation); S = [sR|t] this camera -> the other camera (keyframe 1: sR21 =
+ * (1/s12) R12^T, t21 = -sR21 t12; keyframe 2: sR12 = s12 R12, t12 — as the reference computes them);
+ * per keypoint i (n = the keyframe's N): valid[i] != 0 when GetMapPointMatches()[i] is set, not bad
+ * and not already matched (vbAlreadyMatched1 / 2); xyz, min_dist / max_dist (mfMinDistance /
+ * mfMaxDistance) and desc of that map point. */
+typedef struct {
+    float Tcw[12];
+    float S[12];
+    int n;
+    const uint8_t* valid;
+    const float* xyz;
+    const float* min_dist;
+    const float* max_dist;
+    const uint8_t* desc;
+} orb_sim3_points;
+/* mfLogScaleFactor, mnScaleLevels, mvScaleFactors of a keyframe. */
+typedef struct {
+    float log_scale_factor;
+    int n_levels;
+    const float* scale_factors;
+} orb_scale_params;
+
+/* ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th) — R/src/ORBmatcher.cpp:
+ * 1305-1503 (LoopClosing::ComputeSim3): both projection directions on the GPU (pKF1's fx, fy, cx,
+ * cy = cam1 for both, as the reference), the mutual check on the host.  matches12 (kf1->n ints)
+ * receives the keyframe-2 index whose map point becomes vpMatches12[i1] (pairs found by this call
+ * only), or -1.  Returns nFound.  Host buffers. */
+int orb_search_by_sim3(int device, const orb_frame_view* kf1, const orb_frame_view* kf2, const orb_sim3_points* p1,
+                       const orb_sim3_points* p2, const float cam1[4], const orb_scale_params* sc1,
+                       const orb_scale_params* sc2, float th, int32_t* matches12);
+
 /* ORBmatcher::SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo) —
  * R/src/ORBmatcher.cpp:785-983 (LocalMapping::CreateNewMapPoints, R/src/LocalMapping.cpp:374).
  *   kf1 / kf2: the keyframes as frame views (mvKeysUn incl. angle and octave, mDescriptors,

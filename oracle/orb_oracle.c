@@ -1324,9 +1324,9 @@ int oracle_distinctive_descriptor(const uint8_t* desc, int N)
  * cv::norm(PO) = sqrt of the float sum ((x*x + y*y) + z*z) in double, PO.dot(Pn) = the float sum
  * ((px*nx + py*ny) + pz*nz) widened to double — OpenCV-version dependent, parity unpinned there;
  * PredictScale's log(ratio) in double (MapPoint.cpp:500, R/src/MapPoint.cpp:489-507). */
-void oracle_fuse(const oracle_frame* kf, const oracle_kf_params* kp, int n_mp, const uint8_t* mp_valid,
-                 const float* mp_xyz, const float* mp_normal, const float* mp_min_dist, const float* mp_max_dist,
-                 const uint8_t* mp_desc, float th, int32_t* best_idx, int32_t* best_dist)
+static void fuse_core(const oracle_frame* kf, const oracle_kf_params* kp, int n_mp, const uint8_t* mp_valid,
+                      const float* mp_xyz, const float* mp_normal, const float* mp_min_dist, const float* mp_max_dist,
+                      const uint8_t* mp_desc, float th, int32_t* best_idx, int32_t* best_dist, int sim3)
 {
     ogrid g;
     build_grid(kf, &g);
@@ -1342,7 +1342,8 @@ void oracle_fuse(const oracle_frame* kf, const oracle_kf_params* kp, int n_mp, c
             p3[r] = (float)(s + (double)kp->Tcw[4 * r + 3]);
         }
         if (p3[2] < 0.0f) continue;
-        const float invz = 1 / p3[2];
+        /* Fuse(pKF, vpMapPoints) divides in float (:1042), Fuse(pKF, Scw, ..) in double (:1194) */
+        const float invz = sim3 ? (float)(1.0 / (double)p3[2]) : 1 / p3[2];
         const float x = p3[0] * invz, y = p3[1] * invz;
         const float u = kp->fx * x + kp->cx, v = kp->fy * y + kp->cy;
         if (!(u >= kf->min_x && u < kf->max_x && v >= kf->min_y && v < kf->max_y)) continue;   /* IsInImage */
@@ -1367,7 +1368,9 @@ void oracle_fuse(const oracle_frame* kf, const oracle_kf_params* kp, int n_mp, c
             const int kpLevel = kf->octave[idx];
             if (kpLevel < nPredictedLevel - 1 || kpLevel > nPredictedLevel) continue;
             const float ex = u - kf->x[idx], ey = v - kf->y[idx];
-            if (kf->uright && kf->uright[idx] >= 0) {
+            if (sim3) {
+                /* no reprojection-error gate in the Scw form (:1232-1249) */
+            } else if (kf->uright && kf->uright[idx] >= 0) {
                 const float er = ur - kf->uright[idx];
                 const float e2 = ex * ex + ey * ey + er * er;
                 if ((double)(e2 * kp->inv_level_sigma2[kpLevel]) > 7.8) continue;
@@ -1386,6 +1389,22 @@ void oracle_fuse(const oracle_frame* kf, const oracle_kf_params* kp, int n_mp, c
     }
     free(cand);
     free_grid(&g);
+}
+
+void oracle_fuse(const oracle_frame* kf, const oracle_kf_params* kp, int n_mp, const uint8_t* mp_valid,
+                 const float* mp_xyz, const float* mp_normal, const float* mp_min_dist, const float* mp_max_dist,
+                 const uint8_t* mp_desc, float th, int32_t* best_idx, int32_t* best_dist)
+{
+    fuse_core(kf, kp, n_mp, mp_valid, mp_xyz, mp_normal, mp_min_dist, mp_max_dist, mp_desc, th, best_idx, best_dist, 0);
+}
+
+/* ORBmatcher::Fuse(KeyFrame*, cv::Mat Scw, vpPoints, th, vpReplacePoint), the matching step of
+ * R/src/ORBmatcher.cpp:1164-1261: Fuse's gates without the reprojection test, 1.0/z in double. */
+void oracle_fuse_sim3(const oracle_frame* kf, const oracle_kf_params* kp, int n_mp, const uint8_t* mp_valid,
+                      const float* mp_xyz, const float* mp_normal, const float* mp_min_dist, const float* mp_max_dist,
+                      const uint8_t* mp_desc, float th, int32_t* best_idx, int32_t* best_dist)
+{
+    fuse_core(kf, kp, n_mp, mp_valid, mp_xyz, mp_normal, mp_min_dist, mp_max_dist, mp_desc, th, best_idx, best_dist, 1);
 }
 
 /* ORBmatcher::SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo)
@@ -1851,4 +1870,67 @@ int oracle_search_by_projection_sim3(const oracle_frame* kf, const oracle_kf_par
     free(cand);
     free_grid(&g);
     return nmatches;
+}
+
+/* One direction of R/src/ORBmatcher.cpp:1335-1438: the points of `p` (keyframe A) into keyframe B. */
+static void sim3_direction(const oracle_sim3_points* p, const oracle_frame* kb, const float* cam, float lsf, int nlev,
+                           const float* sf, float th, int* vnMatch)
+{
+    ogrid g;
+    build_grid(kb, &g);
+    int* cand = (int*)malloc(sizeof(int) * (size_t)(kb->n + 1));
+    for (int i = 0; i < p->n; i++) {
+        vnMatch[i] = -1;
+        if (!p->valid[i]) continue;
+        float c1[3], c2[3];
+        mat34_apply(p->Tcw, p->xyz + 3 * (size_t)i, c1);   /* R1w * p3Dw + t1w */
+        mat34_apply(p->S, c1, c2);                         /* sR21 * p3Dc1 + t21 */
+        if (c2[2] < 0.0f) continue;
+        const float invz = (float)(1.0 / (double)c2[2]);
+        const float x = c2[0] * invz, y = c2[1] * invz;
+        const float u = cam[0] * x + cam[2], v = cam[1] * y + cam[3];
+        if (!(u >= kb->min_x && u < kb->max_x && v >= kb->min_y && v < kb->max_y)) continue;   /* IsInImage */
+        const float maxDistance = 1.2f * p->max_dist[i], minDistance = 0.8f * p->min_dist[i];
+        const float ss = (c2[0] * c2[0] + c2[1] * c2[1]) + c2[2] * c2[2];
+        const float dist3D = (float)sqrt((double)ss);
+        if (dist3D < minDistance || dist3D > maxDistance) continue;
+        const float ratio = p->max_dist[i] / dist3D;
+        int lev = (int)ceil(log((double)ratio) / (double)lsf);
+        if (lev < 0) lev = 0;
+        else if (lev >= nlev) lev = nlev - 1;
+        const float radius = th * sf[lev];
+        const int nc = features_in_area(kb, &g, u, v, radius, -1, -1, cand, kb->n);
+        int bestDist = INT_MAX, bestIdx = -1;
+        for (int q = 0; q < nc; q++) {
+            const int idx = cand[q];
+            if (kb->octave[idx] < lev - 1 || kb->octave[idx] > lev) continue;
+            const int d = oracle_descriptor_distance(p->desc + (size_t)i * 32, kb->desc + (size_t)idx * 32);
+            if (d < bestDist) { bestDist = d; bestIdx = idx; }
+        }
+        if (bestDist <= TH_HIGH) vnMatch[i] = bestIdx;
+    }
+    free(cand);
+    free_grid(&g);
+}
+
+int oracle_search_by_sim3(const oracle_frame* kf1, const oracle_frame* kf2, const oracle_sim3_points* p1,
+                          const oracle_sim3_points* p2, const float* cam1, float lsf1, int nlev1, const float* sf1,
+                          float lsf2, int nlev2, const float* sf2, float th, int32_t* matches12)
+{
+    int* m1 = (int*)malloc(sizeof(int) * (size_t)(p1->n + 1));
+    int* m2 = (int*)malloc(sizeof(int) * (size_t)(p2->n + 1));
+    sim3_direction(p1, kf2, cam1, lsf2, nlev2, sf2, th, m1);
+    sim3_direction(p2, kf1, cam1, lsf1, nlev1, sf1, th, m2);
+    int nFound = 0;
+    for (int i1 = 0; i1 < p1->n; i1++) {
+        matches12[i1] = -1;
+        const int idx2 = m1[i1];
+        if (idx2 >= 0 && m2[idx2] == i1) {
+            matches12[i1] = idx2;
+            nFound++;
+        }
+    }
+    free(m1);
+    free(m2);
+    return nFound;
 }

@@ -257,6 +257,31 @@ int oracle_search_by_projection_sim3(const oracle_frame* kf, const oracle_kf_par
                                      const float* mp_min_dist, const float* mp_max_dist, const uint8_t* mp_desc,
                                      float th, int32_t* matched);
 
+/* ORBmatcher::Fuse(KeyFrame*, cv::Mat Scw, vpPoints, th, vpReplacePoint) matching step
+ * (R/src/ORBmatcher.cpp:1164-1261): as oracle_fuse without the reprojection-error gate. */
+void oracle_fuse_sim3(const oracle_frame* kf, const oracle_kf_params* kp, int n_mp, const uint8_t* mp_valid,
+                      const float* mp_xyz, const float* mp_normal, const float* mp_min_dist, const float* mp_max_dist,
+                      const uint8_t* mp_desc, float th, int32_t* best_idx, int32_t* best_dist);
+
+/* One keyframe's side of ORBmatcher::SearchBySim3 (see orb_sim3_points in the C-ABI). */
+typedef struct {
+    float Tcw[12];
+    float S[12];
+    int n;
+    const uint8_t* valid;
+    const float* xyz;
+    const float* min_dist;
+    const float* max_dist;
+    const uint8_t* desc;
+} oracle_sim3_points;
+
+/* ORBmatcher::SearchBySim3 (R/src/ORBmatcher.cpp:1305-1503) for the map points of this call
+ * (valid = set, not bad, not already matched): matches12[i1] = idx2 of the mutual pairs or -1.
+ * cam1 = pKF1's fx, fy, cx, cy; lsf / nlev / sf per keyframe.  Returns nFound. */
+int oracle_search_by_sim3(const oracle_frame* kf1, const oracle_frame* kf2, const oracle_sim3_points* p1,
+                          const oracle_sim3_points* p2, const float* cam1, float lsf1, int nlev1, const float* sf1,
+                          float lsf2, int nlev2, const float* sf2, float th, int32_t* matches12);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1172,7 +1172,8 @@ __global__ __launch_bounds__(256) void k_fuse(const orb_keypoint* __restrict__ k
                                               const uint8_t* __restrict__ valid, const float* __restrict__ xyz,
                                               const float* __restrict__ nrm, const float* __restrict__ mind,
                                               const float* __restrict__ maxd, const uint8_t* __restrict__ mdesc,
-                                              float th, int32_t* __restrict__ best_idx, int32_t* __restrict__ best_dist) {
+                                              float th, int32_t* __restrict__ best_idx, int32_t* __restrict__ best_dist,
+                                              int sim3) {
     const int lane = threadIdx.x & 63;
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= n_mp) return;
@@ -1189,7 +1190,8 @@ __global__ __launch_bounds__(256) void k_fuse(const orb_keypoint* __restrict__ k
             p3[r] = (float)(s + (double)K.Tcw[4 * r + 3]);
         }
         go = !(p3[2] < 0.0f);
-        const float invz = 1 / p3[2];
+        // Fuse(pKF, vpMapPoints) divides in float (:1042), Fuse(pKF, Scw, ..) in double (:1194)
+        const float invz = sim3 ? (float)(1.0 / (double)p3[2]) : 1 / p3[2];
         const float x = p3[0] * invz, y = p3[1] * invz;
         u = K.fx * x + K.cx;
         v = K.fy * y + K.cy;
@@ -1220,7 +1222,9 @@ __global__ __launch_bounds__(256) void k_fuse(const orb_keypoint* __restrict__ k
             const int kl = k2.octave;
             if (kl < lev - 1 || kl > lev) continue;
             const float ex = u - k2.x, ey = v - k2.y;
-            if (kur && kur[j] >= 0) {
+            if (sim3) {
+                // the Scw form has no reprojection-error gate (:1232-1249)
+            } else if (kur && kur[j] >= 0) {
                 const float er = ur - kur[j];
                 const float e2 = ex * ex + ey * ey + er * er;
                 if ((double)(e2 * K.isig2[kl]) > 7.8) continue;
@@ -1317,6 +1321,86 @@ __global__ __launch_bounds__(256) void k_cand_sbs(const orb_keypoint* __restrict
         if (n > kMaxCand) { atomicOr(status, 1); n = kMaxCand; }
         ncand[i] = n;
     }
+}
+
+// ------------------------------------------------------------------ SearchBySim3
+// ORBmatcher::SearchBySim3 (R/src/ORBmatcher.cpp:1305-1503): one direction per launch — each
+// eligible map point of one keyframe goes through [R|t] (world -> its camera) and [sR|t] (its
+// camera -> the other camera; double-accumulated rows rounded to float), is projected with
+// pKF1's intrinsics, tested with the other keyframe's IsInImage and the 0.8 / 1.2 x distance
+// range on |p3Dc| (the reference's cv::norm of the camera-frame point), PredictScale on the other
+// keyframe, and takes the least-distance keypoint of the window at octaves level-1 .. level
+// (first window entry on ties) if <= TH_HIGH.  The mutual check runs on the host.
+struct Sim3Side {
+    float T[12], S[12];
+    float fx, fy, cx, cy;
+    float logsf;
+    int nlev;
+    float sf[32];
+    float th;
+};
+
+__global__ __launch_bounds__(256) void k_sim3_match(const orb_keypoint* __restrict__ kk, const uint8_t* __restrict__ kd,
+                                                    int nk, GridParams g, Sim3Side P, int n_mp,
+                                                    const uint8_t* __restrict__ valid, const float* __restrict__ xyz,
+                                                    const float* __restrict__ mind, const float* __restrict__ maxd,
+                                                    const uint8_t* __restrict__ mdesc, int32_t* __restrict__ match) {
+    const int lane = threadIdx.x & 63;
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n_mp) return;
+    int out = -1;
+    bool go = valid[i] != 0;
+    float u = 0, v = 0, radius = 0;
+    int lev = 0;
+    if (go) {
+        const float* X = xyz + 3 * (size_t)i;
+        float c1[3], c2[3];
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            const double s = (double)P.T[4 * r] * X[0] + (double)P.T[4 * r + 1] * X[1] + (double)P.T[4 * r + 2] * X[2];
+            c1[r] = (float)(s + (double)P.T[4 * r + 3]);
+        }
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            const double s = (double)P.S[4 * r] * c1[0] + (double)P.S[4 * r + 1] * c1[1] + (double)P.S[4 * r + 2] * c1[2];
+            c2[r] = (float)(s + (double)P.S[4 * r + 3]);
+        }
+        go = !(c2[2] < 0.0f);
+        const float invz = (float)(1.0 / (double)c2[2]);
+        u = P.fx * (c2[0] * invz) + P.cx;
+        v = P.fy * (c2[1] * invz) + P.cy;
+        go = go && u >= g.min_x && u < g.max_x && v >= g.min_y && v < g.max_y;   // KeyFrame::IsInImage
+        const float maxDistance = 1.2f * maxd[i], minDistance = 0.8f * mind[i];
+        const float ss = (c2[0] * c2[0] + c2[1] * c2[1]) + c2[2] * c2[2];
+        const float dist3D = (float)sqrt((double)ss);
+        go = go && !(dist3D < minDistance || dist3D > maxDistance);
+        const float ratio = maxd[i] / dist3D;
+        lev = (int)ceil(log((double)ratio) / (double)P.logsf);
+        if (lev < 0) lev = 0;
+        else if (lev >= P.nlev) lev = P.nlev - 1;
+        radius = P.th * P.sf[lev];
+    }
+    if (go) {
+        const AreaQuery q = make_area(g, u, v, radius, -1, -1);
+        const uint8_t* dq = mdesc + (size_t)i * 32;
+        int bd = 0x7fffffff, bk = 0x7fffffff;
+        for (int j = lane; j < nk && q.cx0 <= q.cx1; j += 64) {
+            const orb_keypoint k2 = kk[j];
+            const int cell = grid_cell(g, k2.x, k2.y);
+            if (!in_area(q, cell, k2.octave, k2.x, k2.y)) continue;
+            if (k2.octave < lev - 1 || k2.octave > lev) continue;
+            const int d = hamming32(dq, kd + (size_t)j * 32);
+            const int key = (cell << 16) | j;
+            if (d < bd || (d == bd && key < bk)) { bd = d; bk = key; }
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            const int od = __shfl_xor(bd, o, 64), ok = __shfl_xor(bk, o, 64);
+            if (od < bd || (od == bd && ok < bk)) { bd = od; bk = ok; }
+        }
+        if (bd <= kThHigh) out = bk & 0xffff;
+    }
+    if (lane == 0) match[i] = out;
 }
 
 // ------------------------------------------------------------------ SearchForTriangulation
@@ -2081,14 +2165,15 @@ int orb_distinctive_descriptors(int device, const uint8_t* desc, const int32_t* 
     return rc;
 }
 
-int orb_fuse(int device, const orb_frame_view* kf, const orb_kf_params* kp, int n_mp, const uint8_t* mp_valid,
-             const float* mp_xyz, const float* mp_normal, const float* mp_min_dist, const float* mp_max_dist,
-             const uint8_t* mp_desc, float th, int32_t* best_idx, int32_t* best_dist) {
+static int fuse_impl(int device, const orb_frame_view* kf, const orb_kf_params* kp, int n_mp, const uint8_t* mp_valid,
+                     const float* mp_xyz, const float* mp_normal, const float* mp_min_dist, const float* mp_max_dist,
+                     const uint8_t* mp_desc, float th, int32_t* best_idx, int32_t* best_dist, int sim3) {
     if (!kf || !kp || n_mp < 0 || kf->n < 0 || kf->n >= (1 << 16)) return ORB_EINVAL;
     if (n_mp > 0 && (!mp_valid || !mp_xyz || !mp_normal || !mp_min_dist || !mp_max_dist || !mp_desc || !best_idx ||
                      !best_dist))
         return ORB_EINVAL;
-    if (kp->n_levels < 1 || kp->n_levels > 32 || !kp->scale_factors || !kp->inv_level_sigma2) return ORB_EINVAL;
+    if (kp->n_levels < 1 || kp->n_levels > 32 || !kp->scale_factors || (!sim3 && !kp->inv_level_sigma2))
+        return ORB_EINVAL;
     int st = check_device(device);
     if (st) return st;
     if (n_mp == 0) return ORB_OK;
@@ -2102,7 +2187,7 @@ int orb_fuse(int device, const orb_frame_view* kf, const orb_kf_params* kp, int 
     K.nlev = kp->n_levels;
     for (int l = 0; l < 32; l++) {
         K.sf[l] = l < kp->n_levels ? kp->scale_factors[l] : 0.f;
-        K.isig2[l] = l < kp->n_levels ? kp->inv_level_sigma2[l] : 0.f;
+        K.isig2[l] = (l < kp->n_levels && kp->inv_level_sigma2) ? kp->inv_level_sigma2[l] : 0.f;
     }
     const int nk = kf->n;
     std::vector<orb_keypoint> hk((size_t)std::max(nk, 1));
@@ -2141,7 +2226,7 @@ int orb_fuse(int device, const orb_frame_view* kf, const orb_kf_params* kp, int 
     (void)hipMemcpyAsync(dMD, mp_desc, (size_t)n_mp * 32, hipMemcpyHostToDevice, s);
     const GridParams g = grid_of(kf);
     hipLaunchKernelGGL(k_fuse, dim3((n_mp + 3) / 4), dim3(256), 0, s, dK, dD, kf->uright ? (const float*)dU : nullptr,
-                       nk, g, K, n_mp, dV, dX, dN, dMin, dMax, dMD, th, dBI, dBD);
+                       nk, g, K, n_mp, dV, dX, dN, dMin, dMax, dMD, th, dBI, dBD, sim3);
     int rc = hipGetLastError() == hipSuccess ? ORB_OK : ORB_EGPU;
     if (rc == ORB_OK) {
         (void)hipMemcpyAsync(best_idx, dBI, (size_t)n_mp * 4, hipMemcpyDeviceToHost, s);
@@ -2151,6 +2236,108 @@ int orb_fuse(int device, const orb_frame_view* kf, const orb_kf_params* kp, int 
     (void)hipStreamDestroy(s);
     (void)hipFree(base);
     return rc;
+}
+
+int orb_fuse(int device, const orb_frame_view* kf, const orb_kf_params* kp, int n_mp, const uint8_t* mp_valid,
+             const float* mp_xyz, const float* mp_normal, const float* mp_min_dist, const float* mp_max_dist,
+             const uint8_t* mp_desc, float th, int32_t* best_idx, int32_t* best_dist) {
+    return fuse_impl(device, kf, kp, n_mp, mp_valid, mp_xyz, mp_normal, mp_min_dist, mp_max_dist, mp_desc, th, best_idx,
+                     best_dist, 0);
+}
+
+int orb_fuse_sim3(int device, const orb_frame_view* kf, const orb_kf_params* kp, int n_mp, const uint8_t* mp_valid,
+                  const float* mp_xyz, const float* mp_normal, const float* mp_min_dist, const float* mp_max_dist,
+                  const uint8_t* mp_desc, float th, int32_t* best_idx, int32_t* best_dist) {
+    return fuse_impl(device, kf, kp, n_mp, mp_valid, mp_xyz, mp_normal, mp_min_dist, mp_max_dist, mp_desc, th, best_idx,
+                     best_dist, 1);
+}
+
+int orb_search_by_sim3(int device, const orb_frame_view* kf1, const orb_frame_view* kf2, const orb_sim3_points* p1,
+                       const orb_sim3_points* p2, const float cam1[4], const orb_scale_params* sc1,
+                       const orb_scale_params* sc2, float th, int32_t* matches12) {
+    if (!kf1 || !kf2 || !p1 || !p2 || !cam1 || !sc1 || !sc2 || !matches12) return ORB_EINVAL;
+    if (kf1->n < 0 || kf2->n < 0 || kf1->n >= (1 << 16) || kf2->n >= (1 << 16) || p1->n != kf1->n || p2->n != kf2->n)
+        return ORB_EINVAL;
+    if (sc1->n_levels < 1 || sc1->n_levels > 32 || sc2->n_levels < 1 || sc2->n_levels > 32 || !sc1->scale_factors ||
+        !sc2->scale_factors)
+        return ORB_EINVAL;
+    int st = check_device(device);
+    if (st) return st;
+    const int n1 = kf1->n, n2 = kf2->n;
+    for (int i = 0; i < n1; i++) matches12[i] = -1;
+    if (n1 == 0 || n2 == 0) return 0;
+    ORB_HIP_TRY(hipSetDevice(device));
+    auto side = [&](const orb_sim3_points* p, const orb_scale_params* sc) {
+        Sim3Side S;
+        std::memcpy(S.T, p->Tcw, sizeof(S.T));
+        std::memcpy(S.S, p->S, sizeof(S.S));
+        S.fx = cam1[0]; S.fy = cam1[1]; S.cx = cam1[2]; S.cy = cam1[3];
+        S.logsf = sc->log_scale_factor;
+        S.nlev = sc->n_levels;
+        for (int l = 0; l < 32; l++) S.sf[l] = l < sc->n_levels ? sc->scale_factors[l] : 0.f;
+        S.th = th;
+        return S;
+    };
+    // points of keyframe 1 project into keyframe 2 (its scale table) and vice versa
+    const Sim3Side S12 = side(p1, sc2), S21 = side(p2, sc1);
+    std::vector<orb_keypoint> hk1((size_t)n1), hk2((size_t)n2);
+    pack_view(kf1, hk1.data());
+    pack_view(kf2, hk2.data());
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t per1 = al((size_t)n1 * sizeof(orb_keypoint)) + al((size_t)n1 * 32) + al(n1) + al((size_t)n1 * 12) +
+                        2 * al((size_t)n1 * 4) + al((size_t)n1 * 32) + al((size_t)n1 * 4);
+    const size_t per2 = al((size_t)n2 * sizeof(orb_keypoint)) + al((size_t)n2 * 32) + al(n2) + al((size_t)n2 * 12) +
+                        2 * al((size_t)n2 * 4) + al((size_t)n2 * 32) + al((size_t)n2 * 4);
+    char* base = nullptr;
+    ORB_HIP_TRY(hipMalloc(&base, per1 + per2));
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) { (void)hipFree(base); return ORB_EGPU; }
+    char* c = base;
+    auto put = [&](const void* src, size_t bytes) {
+        char* r = c;
+        c += al(bytes);
+        if (src && bytes) (void)hipMemcpyAsync(r, src, bytes, hipMemcpyHostToDevice, s);
+        return r;
+    };
+    auto* dK1 = (orb_keypoint*)put(hk1.data(), (size_t)n1 * sizeof(orb_keypoint));
+    auto* dD1 = (uint8_t*)put(kf1->desc, (size_t)n1 * 32);
+    auto* dV1 = (uint8_t*)put(p1->valid, n1);
+    auto* dX1 = (float*)put(p1->xyz, (size_t)n1 * 12);
+    auto* dMin1 = (float*)put(p1->min_dist, (size_t)n1 * 4);
+    auto* dMax1 = (float*)put(p1->max_dist, (size_t)n1 * 4);
+    auto* dMD1 = (uint8_t*)put(p1->desc, (size_t)n1 * 32);
+    auto* dM1 = (int32_t*)put(nullptr, (size_t)n1 * 4);
+    auto* dK2 = (orb_keypoint*)put(hk2.data(), (size_t)n2 * sizeof(orb_keypoint));
+    auto* dD2 = (uint8_t*)put(kf2->desc, (size_t)n2 * 32);
+    auto* dV2 = (uint8_t*)put(p2->valid, n2);
+    auto* dX2 = (float*)put(p2->xyz, (size_t)n2 * 12);
+    auto* dMin2 = (float*)put(p2->min_dist, (size_t)n2 * 4);
+    auto* dMax2 = (float*)put(p2->max_dist, (size_t)n2 * 4);
+    auto* dMD2 = (uint8_t*)put(p2->desc, (size_t)n2 * 32);
+    auto* dM2 = (int32_t*)put(nullptr, (size_t)n2 * 4);
+    hipLaunchKernelGGL(k_sim3_match, dim3((n1 + 3) / 4), dim3(256), 0, s, dK2, dD2, n2, grid_of(kf2), S12, n1, dV1, dX1,
+                       dMin1, dMax1, dMD1, dM1);
+    hipLaunchKernelGGL(k_sim3_match, dim3((n2 + 3) / 4), dim3(256), 0, s, dK1, dD1, n1, grid_of(kf1), S21, n2, dV2, dX2,
+                       dMin2, dMax2, dMD2, dM2);
+    std::vector<int32_t> m1((size_t)n1), m2((size_t)n2);
+    int rc = hipGetLastError() == hipSuccess ? ORB_OK : ORB_EGPU;
+    if (rc == ORB_OK) {
+        (void)hipMemcpyAsync(m1.data(), dM1, (size_t)n1 * 4, hipMemcpyDeviceToHost, s);
+        (void)hipMemcpyAsync(m2.data(), dM2, (size_t)n2 * 4, hipMemcpyDeviceToHost, s);
+        if (hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
+    }
+    (void)hipStreamDestroy(s);
+    (void)hipFree(base);
+    if (rc) return rc;
+    int nFound = 0;   // R :1490-1503: keep the pairs both directions agree on
+    for (int i1 = 0; i1 < n1; i1++) {
+        const int idx2 = m1[i1];
+        if (idx2 >= 0 && m2[idx2] == i1) {
+            matches12[i1] = idx2;
+            nFound++;
+        }
+    }
+    return nFound;
 }
 
 int orb_search_for_triangulation(int device, const orb_frame_view* kf1, const orb_frame_view* kf2,

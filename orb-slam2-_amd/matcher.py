@@ -289,14 +289,30 @@ class KfParams(C.Structure):
                 ("n_levels", C.c_int), ("scale_factors", C.c_void_p), ("inv_level_sigma2", C.c_void_p)]
 
 
+def FuseSim3(kf: Frame, Tcw, Ow, cam, log_scale_factor, scale_factors, mp_valid, mp_xyz, mp_normal, mp_min_dist,
+             mp_max_dist, mp_desc, th=4.0, device=0):
+    """ORBmatcher::Fuse(KeyFrame* pKF, cv::Mat Scw, vpPoints, th, vpReplacePoint) matching step
+    (R/src/ORBmatcher.cpp:1164-1261) on the GPU: Tcw = [Rcw | tcw] with the Sim3 scale removed,
+    Ow = -Rcw^T tcw, cam = (fx, fy, cx, cy); mp_valid = not bad and not among the keyframe's map
+    points.  Returns (best_idx, best_dist) per point; the replace / add step stays with the caller."""
+    return _fuse("orb_fuse_sim3", kf, Tcw, Ow, tuple(cam[:4]) + (0.0,), log_scale_factor, scale_factors, None, mp_valid,
+                 mp_xyz, mp_normal, mp_min_dist, mp_max_dist, mp_desc, th, device)
+
+
 def Fuse(kf: Frame, Tcw, Ow, cam, log_scale_factor, scale_factors, inv_level_sigma2, mp_valid, mp_xyz, mp_normal,
          mp_min_dist, mp_max_dist, mp_desc, th=3.0, device=0):
     """ORBmatcher::Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, float th) matching step
     (R/src/ORBmatcher.cpp:995-1121) on the GPU: per map point the keyframe keypoint it fuses into
     (-1 = none) and the distance.  kf: the keyframe as a Frame (mvKeysUn, mDescriptors, mvuRight,
     bounds); Tcw 3x4 float, Ow = camera centre, cam = (fx, fy, cx, cy, mbf)."""
+    return _fuse("orb_fuse", kf, Tcw, Ow, cam, log_scale_factor, scale_factors, inv_level_sigma2, mp_valid, mp_xyz,
+                 mp_normal, mp_min_dist, mp_max_dist, mp_desc, th, device)
+
+
+def _fuse(entry, kf, Tcw, Ow, cam, log_scale_factor, scale_factors, inv_level_sigma2, mp_valid, mp_xyz, mp_normal,
+          mp_min_dist, mp_max_dist, mp_desc, th, device):
     sf = np.ascontiguousarray(scale_factors, np.float32)
-    isg = np.ascontiguousarray(inv_level_sigma2, np.float32)
+    isg = None if inv_level_sigma2 is None else np.ascontiguousarray(inv_level_sigma2, np.float32)
     kp = KfParams((C.c_float * 12)(*np.asarray(Tcw, np.float32).reshape(-1)[:12]),
                   (C.c_float * 3)(*np.asarray(Ow, np.float32)), *[float(np.float32(v)) for v in cam],
                   float(np.float32(log_scale_factor)), len(sf), _abi.ptr(sf), _abi.ptr(isg))
@@ -307,12 +323,57 @@ def Fuse(kf: Frame, Tcw, Ow, cam, log_scale_factor, scale_factors, inv_level_sig
     bi, bd = np.zeros(n, np.int32), np.zeros(n, np.int32)
     v = kf.view()
     lib = _abi.lib()
-    lib.orb_fuse.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int] + [C.c_void_p] * 6 + [C.c_float, C.c_void_p,
-                                                                                           C.c_void_p]
-    lib.orb_fuse.restype = C.c_int
-    _abi.check("orb_fuse", lib.orb_fuse(device, C.byref(v), C.byref(kp), n, *[_abi.ptr(x) for x in a], th,
-                                        _abi.ptr(bi), _abi.ptr(bd)))
+    fn = getattr(lib, entry)
+    fn.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int] + [C.c_void_p] * 6 + [C.c_float, C.c_void_p, C.c_void_p]
+    fn.restype = C.c_int
+    _abi.check(entry, fn(device, C.byref(v), C.byref(kp), n, *[_abi.ptr(x) for x in a], th, _abi.ptr(bi),
+                         _abi.ptr(bd)))
     return bi, bd
+
+
+class Sim3Points(C.Structure):
+    _fields_ = [("Tcw", C.c_float * 12), ("S", C.c_float * 12), ("n", C.c_int), ("valid", C.c_void_p),
+                ("xyz", C.c_void_p), ("min_dist", C.c_void_p), ("max_dist", C.c_void_p), ("desc", C.c_void_p)]
+
+
+class ScaleParams(C.Structure):
+    _fields_ = [("log_scale_factor", C.c_float), ("n_levels", C.c_int), ("scale_factors", C.c_void_p)]
+
+
+def SearchBySim3(kf1: Frame, kf2: Frame, pts1, pts2, cam1, scale1, scale2, th=7.5, device=0):
+    """ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th)
+    (R/src/ORBmatcher.cpp:1305-1503) on the GPU.  ptsN: dict with Tcw ([R|t] world -> camera N),
+    S ([sR|t] camera N -> the other camera, as the reference computes sR21 / t21 and sR12 / t12) and
+    per keypoint valid / xyz / min_dist / max_dist / desc of its map point; cam1 = pKF1's (fx, fy,
+    cx, cy); scaleN = (mfLogScaleFactor, mvScaleFactors).  Returns (nFound, matches12)."""
+    keep = []
+
+    def side(p):
+        a = [np.ascontiguousarray(p[f], t) for f, t in (("valid", np.uint8), ("xyz", np.float32),
+                                                        ("min_dist", np.float32), ("max_dist", np.float32),
+                                                        ("desc", np.uint8))]
+        keep.extend(a)
+        return Sim3Points((C.c_float * 12)(*np.asarray(p["Tcw"], np.float32).reshape(-1)[:12]),
+                          (C.c_float * 12)(*np.asarray(p["S"], np.float32).reshape(-1)[:12]), len(a[0]),
+                          *[_abi.ptr(x) for x in a])
+
+    def scale(sc):
+        sf = np.ascontiguousarray(sc[1], np.float32)
+        keep.append(sf)
+        return ScaleParams(float(np.float32(sc[0])), len(sf), _abi.ptr(sf))
+    p1, p2 = side(pts1), side(pts2)
+    s1, s2 = scale(scale1), scale(scale2)
+    cam = np.ascontiguousarray(np.asarray(cam1, np.float32)[:4])
+    m = np.zeros(kf1.N, np.int32)
+    v1, v2 = kf1.view(), kf2.view()
+    lib = _abi.lib()
+    vp = C.c_void_p
+    lib.orb_search_by_sim3.argtypes = [C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_float, vp]
+    lib.orb_search_by_sim3.restype = C.c_int
+    n = _abi.check("orb_search_by_sim3", lib.orb_search_by_sim3(
+        device, C.byref(v1), C.byref(v2), C.byref(p1), C.byref(p2), _abi.ptr(cam), C.byref(s1), C.byref(s2),
+        float(th), _abi.ptr(m)))
+    return n, m
 
 
 def SearchForTriangulation(kf1: Frame, kf2: Frame, has_mp1, has_mp2, featvec1, featvec2, F12, epipole,

@@ -427,3 +427,74 @@ def bow_match_problem(voc, seed=9, n_land=900, keep=0.8, extra=200, mp_frac=0.75
                 "desc": np.ascontiguousarray(d[perm]), "uright": None,
                 "has_mp": (rng.random(n) < mp_frac).astype(np.uint8), "W": W, "H": H}
     return view(0.0), view(rot_deg)
+
+
+def sim3_problem(seed=6, n_points=700, keep=0.85, extra=120, mp_frac=0.85, s12=1.0, W=640, H=480, nlevels=8):
+    """Synthetic ORBmatcher::SearchBySim3 input: two keyframes 0.4 m apart viewing n_points
+    3-D points; keypoint = projection + N(0, 0.7 px), octave = the point's level, descriptor = the
+    point's with U{0..25} bits flipped; mp_frac of the point keypoints carry the map point (xyz,
+    mfMinDistance / mfMaxDistance from the distance to camera 1, descriptor = the point's); the
+    Sim3 is (s12, R12 = R1 R2^T, t12 = t1 - s12 R12 t2).  Returns per keyframe the keypoints, the
+    map-point arrays (per keypoint) and [R|t]; plus s12, R12, t12 and the camera."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    fx, fy, cx, cy = TUM1
+    sf = np.array([np.float32(1.2) ** l for l in range(nlevels)], np.float32)
+    R1, t1 = np.eye(3), np.zeros(3)
+    R2 = _rot(np.array([0.02, 0.08, -0.01]))
+    t2 = np.array([-0.4, 0.03, 0.02])
+    pts = np.stack([rng.uniform(-2, 2, n_points), rng.uniform(-1.5, 1.5, n_points), rng.uniform(2, 8, n_points)], 1)
+    base = rng.integers(0, 256, (n_points, 32), dtype=np.uint8)
+    lvl = rng.integers(0, nlevels, n_points)
+    dist1 = np.linalg.norm(pts, axis=1)
+    maxd = (dist1 * sf[lvl]).astype(np.float32)
+    mind = (maxd / sf[nlevels - 1]).astype(np.float32)
+
+    def kf(R, t):
+        xs, ys, os, ds, an, mp = [], [], [], [], [], []
+        for i in np.flatnonzero(rng.random(n_points) < keep):
+            Xc = R @ pts[i] + t
+            u, v = fx * Xc[0] / Xc[2] + cx + rng.normal(0, 0.7), fy * Xc[1] / Xc[2] + cy + rng.normal(0, 0.7)
+            if not (0 <= u < W and 0 <= v < H):
+                continue
+            bits = np.unpackbits(base[i])
+            bits[rng.choice(256, int(rng.integers(0, 26)), replace=False)] ^= 1
+            xs.append(u); ys.append(v); os.append(int(lvl[i])); ds.append(np.packbits(bits)); an.append(0.0)
+            mp.append(i if rng.random() < mp_frac else -1)
+        for _ in range(extra):
+            xs.append(rng.uniform(0, W)); ys.append(rng.uniform(0, H)); os.append(int(rng.integers(0, nlevels)))
+            ds.append(rng.integers(0, 256, 32, dtype=np.uint8)); an.append(0.0); mp.append(-1)
+        mp = np.array(mp)
+        has = mp >= 0
+        n = len(xs)
+        xyz = np.zeros((n, 3), np.float32)
+        xyz[has] = pts[mp[has]].astype(np.float32)
+        md = np.zeros((n, 32), np.uint8)
+        md[has] = base[mp[has]]
+        mn, mx = np.zeros(n, np.float32), np.zeros(n, np.float32)
+        mn[has], mx[has] = mind[mp[has]], maxd[mp[has]]
+        T = np.zeros((3, 4), np.float32)
+        T[:, :3], T[:, 3] = R, t
+        return {"x": np.array(xs, np.float32), "y": np.array(ys, np.float32), "octave": np.array(os, np.int32),
+                "angle": np.array(an, np.float32), "desc": np.array(ds, np.uint8), "uright": None, "W": W, "H": H,
+                "mp_valid": has.astype(np.uint8), "mp_xyz": xyz, "mp_min_dist": mn, "mp_max_dist": mx, "mp_desc": md,
+                "Tcw": T, "point": mp}
+    k1, k2 = kf(R1, t1), kf(R2, t2)
+    R12 = (R1 @ R2.T).astype(np.float32)
+    t12 = (t1 - s12 * R12.astype(np.float64) @ t2).astype(np.float32)
+    return {"kf1": k1, "kf2": k2, "s12": np.float32(s12), "R12": R12, "t12": t12, "cam": (fx, fy, cx, cy),
+            "scale_factors": sf, "log_scale_factor": float(np.log(np.float32(1.2))), "n_levels": nlevels}
+
+
+def sim3_side_transforms(p):
+    """sR21 = (1/s12) R12^T, t21 = -sR21 t12 and sR12 = s12 R12 as R/src/ORBmatcher.cpp:1315-1318
+    compute them (float Mats: scaled elements rounded to float, the product accumulated in double)."""
+    s12 = float(p["s12"])
+    R12 = np.asarray(p["R12"], np.float32)
+    sR12 = (R12.astype(np.float64) * s12).astype(np.float32)
+    sR21 = (R12.T.astype(np.float64) * (1.0 / s12)).astype(np.float32)
+    t21 = (-(sR21.astype(np.float64) @ np.asarray(p["t12"], np.float32).astype(np.float64))).astype(np.float32)
+    S1 = np.zeros((3, 4), np.float32)
+    S1[:, :3], S1[:, 3] = sR21, t21
+    S2 = np.zeros((3, 4), np.float32)
+    S2[:, :3], S2[:, 3] = sR12, p["t12"]
+    return S1, S2

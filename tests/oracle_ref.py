@@ -357,8 +357,9 @@ def kf_params(kp):
     return s
 
 
-def fuse(prob, th=3.0):
-    """oracle_fuse on a synth.fuse_problem: (best_idx, best_dist) per map point."""
+def fuse(prob, th=3.0, sim3=False):
+    """oracle_fuse (or oracle_fuse_sim3) on a synth.fuse_problem: (best_idx, best_dist) per map
+    point."""
     kf = prob["kf"]
     fv = FrameView(kf, kf["desc"], kf["W"], kf["H"], kf["uright"])
     kp = kf_params(prob["kp"])
@@ -366,8 +367,9 @@ def fuse(prob, th=3.0):
     a = {k: np.ascontiguousarray(prob[k]) for k in ("mp_valid", "mp_xyz", "mp_normal", "mp_min_dist", "mp_max_dist",
                                                     "mp_desc")}
     bi, bd = np.zeros(n, np.int32), np.zeros(n, np.int32)
-    lib().oracle_fuse(C.byref(fv.s), C.byref(kp), n, P(a["mp_valid"]), P(a["mp_xyz"]), P(a["mp_normal"]),
-                      P(a["mp_min_dist"]), P(a["mp_max_dist"]), P(a["mp_desc"]), C.c_float(th), P(bi), P(bd))
+    fn = lib().oracle_fuse_sim3 if sim3 else lib().oracle_fuse
+    fn(C.byref(fv.s), C.byref(kp), n, P(a["mp_valid"]), P(a["mp_xyz"]), P(a["mp_normal"]),
+       P(a["mp_min_dist"]), P(a["mp_max_dist"]), P(a["mp_desc"]), C.c_float(th), P(bi), P(bd))
     return bi, bd
 
 
@@ -506,3 +508,35 @@ def search_by_projection_sim3(prob, th=10.0, matched=None):
                                                 P(a["mp_normal"]), P(a["mp_min_dist"]), P(a["mp_max_dist"]),
                                                 P(a["mp_desc"]), C.c_float(th), P(m))
     return nm, m
+
+
+class Sim3Points(C.Structure):
+    _fields_ = [("Tcw", C.c_float * 12), ("S", C.c_float * 12), ("n", C.c_int), ("valid", C.c_void_p),
+                ("xyz", C.c_void_p), ("min_dist", C.c_void_p), ("max_dist", C.c_void_p), ("desc", C.c_void_p)]
+
+
+def sim3_points(k, S, keep):
+    a = [np.ascontiguousarray(k[f], t) for f, t in (("mp_valid", np.uint8), ("mp_xyz", np.float32),
+                                                    ("mp_min_dist", np.float32), ("mp_max_dist", np.float32),
+                                                    ("mp_desc", np.uint8))]
+    keep.extend(a)
+    return Sim3Points((C.c_float * 12)(*np.asarray(k["Tcw"], np.float32).reshape(-1)),
+                      (C.c_float * 12)(*np.asarray(S, np.float32).reshape(-1)), len(a[0]), *[P(x) for x in a])
+
+
+def search_by_sim3(p, th=7.5):
+    """oracle_search_by_sim3 on a synth.sim3_problem: (nFound, matches12)."""
+    from_synth = __import__("orb_slam2_amd.synth", fromlist=["sim3_side_transforms"])
+    S1, S2 = from_synth.sim3_side_transforms(p)
+    k1, k2 = p["kf1"], p["kf2"]
+    f1 = FrameView(k1, k1["desc"], k1["W"], k1["H"])
+    f2 = FrameView(k2, k2["desc"], k2["W"], k2["H"])
+    keep = []
+    p1, p2 = sim3_points(k1, S1, keep), sim3_points(k2, S2, keep)
+    cam = np.ascontiguousarray(p["cam"], np.float32)
+    sf = np.ascontiguousarray(p["scale_factors"], np.float32)
+    m = np.zeros(len(k1["x"]), np.int32)
+    n = lib().oracle_search_by_sim3(C.byref(f1.s), C.byref(f2.s), C.byref(p1), C.byref(p2), P(cam),
+                                    C.c_float(p["log_scale_factor"]), p["n_levels"], P(sf),
+                                    C.c_float(p["log_scale_factor"]), p["n_levels"], P(sf), C.c_float(th), P(m))
+    return n, m

@@ -125,3 +125,30 @@ def test_fuse_oracle_vs_python_restatement():
     bi, bd = O.fuse(p)
     pi, pd = _py_fuse(p)
     assert np.array_equal(bi, pi) and np.array_equal(bd, pd)
+
+
+def test_fuse_sim3_oracle_drops_only_the_reprojection_gate():
+    """The Scw form (R/src/ORBmatcher.cpp:1164-1261) keeps every Fuse gate but the reprojection
+    test, so it matches at least the points Fuse matches at the same radius."""
+    p = _prob(seed=5)
+    bi, _ = O.fuse(p, 4.0)
+    si, _ = O.fuse(p, 4.0, sim3=True)
+    assert np.all(si[bi >= 0] >= 0) and (si >= 0).sum() >= (bi >= 0).sum()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw,th", [(dict(), 4.0), (dict(seed=9, n_kps=3000, n_mp=2000, true_frac=0.8), 4.0),
+                                   (dict(seed=13, stereo_frac=0.5), 8.0)])
+def test_fuse_sim3_gpu_matches_oracle(amd, kw, th):
+    from orb_slam2_amd import Frame
+    p = _prob(**kw)
+    bi, bd = O.fuse(p, th, sim3=True)
+    kf, kp = p["kf"], p["kp"]
+    k = np.zeros(len(kf["x"]), dtype=[("x", "f4"), ("y", "f4"), ("size", "f4"), ("angle", "f4"), ("response", "f4"),
+                                     ("octave", "i4"), ("class_id", "i4")])
+    k["x"], k["y"], k["octave"] = kf["x"], kf["y"], kf["octave"]
+    fr = Frame(k, kf["desc"], kf["W"], kf["H"])
+    gi, gd = amd.FuseSim3(fr, kp["Tcw"], kp["Ow"], kp["cam"], kp["log_scale_factor"], kp["scale_factors"],
+                          p["mp_valid"], p["mp_xyz"], p["mp_normal"], p["mp_min_dist"], p["mp_max_dist"], p["mp_desc"],
+                          th)
+    assert np.array_equal(gi, bi) and np.array_equal(gd, bd)
