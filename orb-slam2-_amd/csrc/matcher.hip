@@ -407,10 +407,8 @@ __global__ __launch_bounds__(64) void k_resolve_sfi(const orb_keypoint* __restri
     int* qidx = hcount + 32;                       // [kRange]
     int* qnc = qidx + kRange;                      // [kRange]
     uint32_t* qtk = (uint32_t*)(qnc + kRange);     // [kRange * kTopK]
-    int* bq = (int*)(qtk + kRange * kTopK);        // [8] per-batch decisions: keypoint (or -1)
-    int* dq = bq + 8;                              // [8] and distance
 #ifdef ORB_TIMING
-    int* nMatchL = dq + 8;
+    int* nMatchL = (int*)(qtk + kRange * kTopK);
     if (lane == 0) nMatchL[0] = 0;
 #endif
     const int myK = lane & (kTopK - 1);
@@ -489,11 +487,14 @@ __global__ __launch_bounds__(64) void k_resolve_sfi(const orb_keypoint* __restri
             const bool match = a < na && !fallback && mk != 0 && bestd <= kThLow &&
                                (float)bestd < (float)best2 * nnratio;
             // publish every query's decision (bi, dist; -1 = none) to its 8 lanes' peers via LDS
-            if (myK == 0) { bq[q] = match ? bi : -1; dq[q] = bestd; }
-            wave_lds_sync();
+            // (lane 8u holds query u's decision: eight v_readlane broadcasts, no LDS round trip)
+            const int myb = match ? bi : -1;
             int qbi[8], qbd[8];
 #pragma unroll
-            for (int u = 0; u < 8; u++) { qbi[u] = bq[u]; qbd[u] = dq[u]; }
+            for (int u = 0; u < 8; u++) {
+                qbi[u] = __builtin_amdgcn_readlane(myb, 8 * u);
+                qbd[u] = __builtin_amdgcn_readlane(bestd, 8 * u);
+            }
             // conflicts: an earlier match of the batch on one of my candidates up to my second
             // survivor, at a distance <= mine (it would now be skipped)
             const int lim = mk2 ? f2 : kTopK - 1;
