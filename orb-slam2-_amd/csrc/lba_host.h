@@ -36,16 +36,23 @@ inline void build_structure(const lba_problem* p, const std::vector<uint8_t>& le
         ptAct[p->edge_point[e]] = 1;
     }
     s.act.clear();
+    s.act.reserve(NE);
     for (int e = 0; e < NE; e++) {
         if (level[e] != lvl) continue;
         const int pt = p->edge_point[e];
         if (pt < own0 || pt >= own1) continue;
         s.act.push_back(e);
     }
+    // g2o orders the Hessian blocks by vertex id; callers usually pass ids ascending already
+    auto by_id = [](std::vector<int>& o, const int64_t* id) {
+        if (std::is_sorted(o.begin(), o.end(), [&](int a, int b) { return id[a] < id[b]; })) return;
+        std::stable_sort(o.begin(), o.end(), [&](int a, int b) { return id[a] < id[b]; });
+    };
     std::vector<int> order;
+    order.reserve(std::max(NP, NM));
     for (int i = 0; i < NP; i++)
         if (poseAct[i] && !p->pose_fixed[i]) order.push_back(i);
-    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return p->pose_id[a] < p->pose_id[b]; });
+    by_id(order, p->pose_id);
     s.poseIdx.assign(NP, -1);
     for (size_t k = 0; k < order.size(); k++) s.poseIdx[order[k]] = (int)k;
     s.freePoses = order;
@@ -53,7 +60,7 @@ inline void build_structure(const lba_problem* p, const std::vector<uint8_t>& le
     order.clear();
     for (int i = own0; i < own1; i++)
         if (ptAct[i]) order.push_back(i);
-    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return p->point_id[a] < p->point_id[b]; });
+    by_id(order, p->point_id);
     s.ptLocal.assign(NM, -1);
     for (size_t k = 0; k < order.size(); k++) s.ptLocal[order[k]] = (int)k;
     s.ptGlob = order;
