@@ -672,11 +672,37 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_solve(const double* __restrict__
     __syncthreads();
     TSTAMP(t_f0);
     const int T = np / kNB;
+    // One 16 x 16 tile of the trailing update: A(I, K) -= W(I, panel) L(K, panel)^T, four
+    // v_mfma_f64_16x16x4_f64 per tile
+    auto trail_tile = [&](int jb, int I0, int K0) {
+        const int li = lane & 15, lk = lane >> 4;
+        double a[kNB / 4], bb[kNB / 4];
+        dbl4 acc;
+#pragma unroll
+        for (int s = 0; s < kNB / 4; s++) {
+            const int p = jb + 4 * s + lk;
+            a[s] = -A[(size_t)p * ld + I0 + li];        // -W(I0 + li, p)
+            bb[s] = A[(size_t)(K0 + li) * ld + p];      //  L(K0 + li, p)
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) acc[q] = A[(size_t)(I0 + lk + 4 * q) * ld + K0 + li];
+#pragma unroll
+        for (int s = 0; s < kNB / 4; s++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], bb[s], acc, 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 4; q++) A[(size_t)(I0 + lk + 4 * q) * ld + K0 + li] = acc[q];
+    };
+    auto tri = [](int t, int& ti, int& tk) {   // t -> (ti, tk), tk <= ti, row-major lower triangle
+        ti = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
+        while ((ti + 1) * (ti + 2) / 2 <= t) ti++;
+        while (ti * (ti + 1) / 2 > t) ti--;
+        tk = t - ti * (ti + 1) / 2;
+    };
+    bool factored = false;   // panel kb already factored during the previous step (look-ahead)
     for (int kb = 0; kb < T; kb++) {
         const int jb = kb * kNB;
         TSTAMP(t_d0);
         // ---- 1. panel: rows [jb, jb + 192) in wave 0's registers
-        if (wave == 0) {
+        if (wave == 0 && !factored) {
             const int ns = min(np - jb, kPanelRows);
             bool okp;
             if (ns <= 64) okp = ldlt_panel<1>(A, ld, jb + ns, jb, dg, rdg, y, dummy, lane);
@@ -721,35 +747,41 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_solve(const double* __restrict__
         }
         TACC(tRows, t_r0);
         TSTAMP(t_t0);
-        // ---- 2. trailing lower triangle, 16 x 16 tiles (I >= K > kb) on the MFMA units:
-        //         A(I, K) -= W(I, panel) L(K, panel)^T, four v_mfma_f64_16x16x4_f64 per tile
-        {
-            const int m = T - kb - 1, nt = m * (m + 1) / 2;
-            const int li = lane & 15, lk = lane >> 4;
-            for (int t = wave; t < nt; t += kLdlT / 64) {
-                int ti = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
-                while ((ti + 1) * (ti + 2) / 2 <= t) ti++;
-                while (ti * (ti + 1) / 2 > t) ti--;
-                const int tk = t - ti * (ti + 1) / 2;
-                const int I0 = (kb + 1 + ti) * kNB, K0 = (kb + 1 + tk) * kNB;
-                double a[kNB / 4], bb[kNB / 4];
-                dbl4 acc;
-#pragma unroll
-                for (int s = 0; s < kNB / 4; s++) {
-                    const int p = jb + 4 * s + lk;
-                    a[s] = -A[(size_t)p * ld + I0 + li];        // -W(I0 + li, p)
-                    bb[s] = A[(size_t)(K0 + li) * ld + p];      //  L(K0 + li, p)
+        // ---- 2. trailing lower triangle, 16 x 16 tiles (I >= K > kb) on the MFMA units.
+        //         LDS image (np <= 128): look-ahead — the tiles of column block kb+1 first (all
+        //         waves), then wave 0 factors panel kb+1 while waves 1..7 update the other tiles
+        //         (disjoint addresses; every tile still sees its panel updates in panel order, so
+        //         the result is bitwise that of the plain order)
+        const int m = T - kb - 1;
+        if (kLds && m > 0) {
+            for (int ti = wave; ti < m; ti += kLdlT / 64) trail_tile(jb, (kb + 1 + ti) * kNB, (kb + 1) * kNB);
+            __syncthreads();
+            if (wave == 0) {
+                const int jn = jb + kNB, ns = min(np - jn, kPanelRows);
+                const bool okp = ns <= 64 ? ldlt_panel<1>(A, ld, jn + ns, jn, dg, rdg, y, dummy, lane)
+                                          : ldlt_panel<2>(A, ld, jn + ns, jn, dg, rdg, y, dummy, lane);
+                if (!okp && lane == 0) failS = 1;
+            } else {
+                const int nt = m * (m - 1) / 2;   // tiles with K > kb + 1
+                for (int t = wave - 1; t < nt; t += kLdlT / 64 - 1) {
+                    int ti, tk;
+                    tri(t, ti, tk);
+                    trail_tile(jb, (kb + 2 + ti) * kNB, (kb + 2 + tk) * kNB);
                 }
-#pragma unroll
-                for (int q = 0; q < 4; q++) acc[q] = A[(size_t)(I0 + lk + 4 * q) * ld + K0 + li];
-#pragma unroll
-                for (int s = 0; s < kNB / 4; s++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], bb[s], acc, 0, 0, 0);
-#pragma unroll
-                for (int q = 0; q < 4; q++) A[(size_t)(I0 + lk + 4 * q) * ld + K0 + li] = acc[q];
             }
+            factored = true;
+        } else {
+            const int nt = m * (m + 1) / 2;
+            for (int t = wave; t < nt; t += kLdlT / 64) {
+                int ti, tk;
+                tri(t, ti, tk);
+                trail_tile(jb, (kb + 1 + ti) * kNB, (kb + 1 + tk) * kNB);
+            }
+            factored = false;
         }
         __syncthreads();
         TACC(tTrail, t_t0);
+        if (failS) break;
     }
     TSTAMP(t_s0);
     if (failS) {
