@@ -70,6 +70,9 @@ def parse():
     ap.add_argument("--lba-solves", type=int, default=5, help="timed LocalBundleAdjustment calls")
     ap.add_argument("--lba-points", type=int, default=3000)
     ap.add_argument("--lba-kf", type=int, default=20)
+    ap.add_argument("--no-stereo", action="store_true", help="skip the config-5 sharded stereo leg")
+    ap.add_argument("--stereo-batches", type=int, default=16,
+                    help="8-frame EuRoC stereo batches per step of the config-5 leg")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the secondary legs (brute-force 2-NN, stereo config 5, KITTI config 3)")
     return ap.parse_args()
@@ -89,13 +92,34 @@ def algorithmic_bytes(stage, lw, lh, n_pre, n_out):
     raise KeyError(stage)
 
 
+def host_threads():
+    """Host threads this process may run on (the lease's CPU share: sched affinity, not the
+    machine's os.cpu_count())."""
+    try:
+        return max(1, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        return max(1, os.cpu_count() or 1)
+
+
+def host_info():
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"nproc": host_threads(), "machine_cpus": os.cpu_count(), "cpu_model": model}
+
+
 def cpu_baseline(frames, nfeatures, budget_s):
     """Oracle (C restatement of the reference, -O2, 1 thread per frame) on a bounded sample."""
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_ref as O
     p = O.params(nfeatures)
     W, H = frames.shape[2], frames.shape[1]
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads = host_threads()
 
     def one(i):
         a = O.extract(p, frames[i])
@@ -120,7 +144,7 @@ def cpu_baseline(frames, nfeatures, budget_s):
 
         list(pool.map(match, range(n)))
     dt = time.perf_counter() - t0
-    return {"value": round(n / dt, 2), "unit": "frames/s", "cores": threads, "kind": "port",
+    return {"value": round(n / dt, 2), "unit": "frames/s", "cores": threads, "kind": "port", "host": host_info(),
             "sample": f"{n + 1} frames extracted + {n} SearchForInitialization pairs, {W}x{H}, "
                       f"{nfeatures} feat, oracle C restatement, {threads} host threads (1 frame per thread)"}
 
@@ -209,6 +233,10 @@ def bench_lba(args, amd, dev, local, rank, world):
     st = ctx.stats()
     ctx.profile(False)
     tot = sum(times)
+    er = torch.tensor([float(np.count_nonzero(r["edge_erase"]))], dtype=torch.float64, device=dev)
+    if world > 1:      # each rank flags the edges of its own landmark shard
+        torch.distributed.all_reduce(er)
+    erased = int(er.item())
     if world > 1:
         t = torch.tensor([tot], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -220,7 +248,12 @@ def bench_lba(args, amd, dev, local, rank, world):
            "iterations_per_solve": iters / args.lba_solves, "trials": st["trials"] / args.lba_solves,
            "stage_ms_per_solve": {k: round(st[k] / args.lba_solves, 4) for k in
                                   ("linearize_ms", "schur_ms", "solve_ms", "update_ms")},
-           "n_gpus": world}
+           "n_gpus": world,
+           # LM decisions of the last timed solve: identical for every world size (landmark shards
+           # only reorder the f64 sums; tests/test_bench_ranks.py compares N=1 with N=2)
+           "decisions": {"iterations": [int(x) for x in r["iterations"]], "trials": int(r["trials"]),
+                         "chi2_trace": [float(x) for x in r["trace"][:, 1]],
+                         "erased_edges": erased}}
     out["roofline"] = lba_roofline(pb, out, world)
     if rank == 0 and not args.no_cpu:
         sys.path.insert(0, str(ROOT / "tests"))
@@ -274,6 +307,151 @@ def _extract_leg(amd, dev, frames, nf, steps, warmup, pairs_fn=None):
     return (time.perf_counter() - t0) / steps, buf
 
 
+EUROC_MBF = 47.9   # R/Examples/Stereo/EuRoC.yaml Camera.bf (435.2 fx x 0.11 m)
+
+
+def _timed_ranks(fn, steps, warmup, dev, world):
+    """warmup untimed calls, then `steps` timed ones bracketed by barrier + synchronize on both
+    sides; returns the max over ranks of the elapsed seconds."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt
+
+
+def bench_config5(args, amd, dev, rank, world):
+    """BASELINE config 5: EuRoC-geometry stereo (752x480, 1200 feat, 8 levels), 8-frame batches
+    sharded over the ranks (rank r takes its contiguous share of each batch's 8 stereo pairs; no
+    data-path collective).  Per pair: ORBextractor on the left and the right image (both kept in
+    the two-extractor roles of R/src/Frame.cpp:86-89) and Frame::ComputeStereoMatches
+    (R/src/Frame.cpp:551-770) on the device pyramids.  Two timings:
+      * throughput: `--stereo-batches` batches per step (strong scaling: the total is fixed);
+      * latency: one 8-frame batch per step, sharded the same way (ms per batch, max over ranks)."""
+    from orb_slam2_amd import synth, _abi
+    lib = _abi.lib()
+    W, H, NF, PB = 752, 480, 1200, 8
+    shard = np.array_split(np.arange(PB), world)[rank]
+    cv = synth.canvas(0x5EED0005, W, H)
+    out = {"config": f"synthetic EuRoC MH_01 geometry {W}x{H} stereo (smooth integer disparity 5..60 px), {NF} feat, "
+                     f"8 levels, mbf {EUROC_MBF}, mb 0 (reference call order); {PB}-frame batches sharded over "
+                     f"{world} rank(s)", "pairs_per_batch": PB, "scaling": "strong"}
+    for tag, nb in (("throughput", args.stereo_batches), ("latency_one_batch", 1)):
+        pairs = [b * PB + int(j) for b in range(nb) for j in shard]
+        P = len(pairs)
+        if P == 0:       # more ranks than pairs: this rank idles in the timed region
+            fr = None
+        else:
+            fr = np.stack([im for t in pairs for im in synth.stereo_pair(cv, W, H, t)])
+        ex = amd.ORBextractor(NF, 1.2, 8, 20, 7, device=dev.index or 0, max_w=W, max_h=H, max_batch=max(2 * P, 1))
+        cap = C.c_int()
+        _abi.check("geom", lib.orb_extractor_geometry(ex._h, W, H, None, None, None, C.byref(cap)))
+        cap = cap.value
+        st = torch.cuda.current_stream(dev).cuda_stream
+        if P:
+            imgs = torch.from_numpy(fr).to(dev)
+            kps = torch.zeros((2 * P, cap, 7), dtype=torch.int32, device=dev)
+            desc = torch.zeros((2 * P, cap, 32), dtype=torch.uint8, device=dev)
+            cnt = torch.zeros(2 * P, dtype=torch.int32, device=dev)
+            ur = torch.zeros((P, cap), dtype=torch.float32, device=dev)
+            dep = torch.zeros_like(ur)
+            ns = torch.zeros(P, dtype=torch.int32, device=dev)
+
+        def step():
+            if not P:
+                return
+            _abi.check("x", lib.orb_extract_batch_device(ex._h, C.c_void_p(imgs.data_ptr()), H * W, 2 * P, W, H,
+                                                          C.c_void_p(kps.data_ptr()), C.c_void_p(desc.data_ptr()),
+                                                          cap, C.c_void_p(cnt.data_ptr()), C.c_void_p(st)))
+            _abi.check("stereo", lib.orb_compute_stereo_matches_batch_device(
+                ex._h, C.c_void_p(kps.data_ptr()), C.c_void_p(desc.data_ptr()), C.c_void_p(cnt.data_ptr()), cap, P,
+                C.c_float(EUROC_MBF), C.c_float(0.0), C.c_void_p(ur.data_ptr()), C.c_void_p(dep.data_ptr()),
+                C.c_void_p(ns.data_ptr()), C.c_void_p(st)))
+        steps = max(args.steps, 5)
+        dt = _timed_ranks(step, steps, 3, dev, world)
+        tot = torch.tensor([float(ns.sum()) if P else 0.0, float(P)], dtype=torch.float64, device=dev)
+        if world > 1:
+            torch.distributed.all_reduce(tot)
+        total_pairs = nb * PB
+        assert int(tot[1]) == total_pairs, "every pair of every batch processed exactly once"
+        out[tag] = {"stereo_frames_per_s": round(total_pairs * steps / dt, 1), "ms_per_step": round(dt / steps * 1e3, 4),
+                    "batches_per_step": nb, "pairs_per_rank": P,
+                    "stereo_matches_per_pair": round(float(tot[0]) / total_pairs, 1)}
+        del ex
+    if rank == 0 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline_stereo(cv, W, H, NF, EUROC_MBF, 8)
+    return out
+
+
+def cpu_baseline_stereo(cv, W, H, NF, mbf, n_pairs):
+    """Oracle: both images of each pair extracted (1 pair per host thread) + ComputeStereoMatches."""
+    from orb_slam2_amd import synth
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_ref as O
+    p = O.params(NF)
+    threads = host_threads()
+    prs = [synth.stereo_pair(cv, W, H, t) for t in range(n_pairs)]
+
+    def one(lr):
+        a = O.extract(p, lr[0], want_pyramid=True)
+        b = O.extract(p, lr[1], want_pyramid=True)
+        return O.compute_stereo_matches(p, a, b, mbf)[0]
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(threads) as pool:
+        list(pool.map(one, prs))
+    dt = time.perf_counter() - t0
+    return {"stereo_frames_per_s": round(n_pairs / dt, 2), "cores": threads, "kind": "port",
+            "sample": f"{n_pairs} stereo pairs {W}x{H}, {NF} feat: both images extracted + ComputeStereoMatches, "
+                      f"oracle C restatement, 1 pair per host thread"}
+
+
+KITTI_MBF = 386.1448   # R/Examples/Stereo/KITTI00-02.yaml Camera.bf
+
+
+def bench_stereo_kitti(args, amd, dev, P=32):
+    """BASELINE config 3, stereo: KITTI 00 geometry 1241x376, 2000 feat; per pair both images
+    extracted + Frame::ComputeStereoMatches with the KITTI bf, HBM-resident, one GPU."""
+    from orb_slam2_amd import synth, _abi
+    lib = _abi.lib()
+    W, H, NF = 1241, 376, 2000
+    cv = synth.canvas(0x5EED0003, W, H)
+    fr = np.stack([im for t in range(P) for im in synth.stereo_pair(cv, W, H, t)])
+    ns = torch.zeros(P, dtype=torch.int32, device=dev)
+    o = {}
+
+    def stereo(b):
+        if "ur" not in o:     # [P][cap] outputs at the extractor's keypoint capacity stride
+            o["ur"] = torch.zeros((P, b["cap"]), dtype=torch.float32, device=dev)
+            o["dep"] = torch.zeros_like(o["ur"])
+        _abi.check("stereo", lib.orb_compute_stereo_matches_batch_device(
+            b["ex"]._h, C.c_void_p(b["kps"].data_ptr()), C.c_void_p(b["desc"].data_ptr()),
+            C.c_void_p(b["cnt"].data_ptr()), b["cap"], P, C.c_float(KITTI_MBF), C.c_float(0.0),
+            C.c_void_p(o["ur"].data_ptr()), C.c_void_p(o["dep"].data_ptr()), C.c_void_p(ns.data_ptr()),
+            C.c_void_p(b["stream"])))
+    dt, b = _extract_leg(amd, dev, fr, NF, 10, 3, stereo)
+    out = {"stereo_frames_per_s": round(P / dt, 1), "ms_per_step": round(dt * 1e3, 4), "pairs_per_step": P,
+           "keypoints_per_image": float(b["cnt"].float().mean()),
+           "stereo_matches_per_pair": float(ns.float().mean()),
+           "config": f"synthetic KITTI 00 geometry {W}x{H} stereo (smooth integer disparity 5..60 px), {NF} feat, "
+                     f"mbf {KITTI_MBF}, mb 0 (reference call order)"}
+    if not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline_stereo(cv, W, H, NF, KITTI_MBF, 8)
+    return out
+
+
 def bench_extras(args, amd, dev):
     """Secondary legs of SURVEY §8d: (ii) all-pairs 2-NN Hamming throughput (integer-VALU
     roofline: 16 lane-ops per 256-bit pair), config 5 stereo (EuRoC 752x480, 1200 feat,
@@ -316,24 +494,8 @@ def bench_extras(args, amd, dev):
     out["knn2_bruteforce"] = {"pairs_per_s": round(pairs / dt, 1), "ms_per_batch": round(dt * 1e3, 4),
                               "frame_pairs": B, "roofline": {"bound": "valu", "unit": "pairs/s",
                                                              "peak": peak_pairs, "frac": round(pairs / dt / peak_pairs, 4)}}
-    # ---- config 5: stereo pairs (left frames 2p, right 2p+1), extraction + ComputeStereoMatches
-    W, H, P = 752, 480, 32
-    cv = synth.canvas(0x5EED0005, W, H)
-    fr = np.stack([im for t in range(P) for im in synth.stereo_pair(cv, W, H, t)])
-    ur = torch.zeros((P, 4096), dtype=torch.float32, device=dev)
-    dep = torch.zeros_like(ur)
-    ns = torch.zeros(P, dtype=torch.int32, device=dev)
-
-    def stereo(b):
-        _abi.check("stereo", lib.orb_compute_stereo_matches_batch_device(
-            b["ex"]._h, C.c_void_p(b["kps"].data_ptr()), C.c_void_p(b["desc"].data_ptr()),
-            C.c_void_p(b["cnt"].data_ptr()), b["cap"], P, C.c_float(47.9), C.c_float(0.0), C.c_void_p(ur.data_ptr()),
-            C.c_void_p(dep.data_ptr()), C.c_void_p(ns.data_ptr()), C.c_void_p(b["stream"])))
-    dt, b = _extract_leg(amd, dev, fr, 1200, 10, 3, stereo)
-    out["stereo_euroc_752x480"] = {"stereo_frames_per_s": round(P / dt, 1), "ms_per_step": round(dt * 1e3, 4),
-                                   "pairs_per_step": P, "stereo_matches_per_frame": float(ns.float().mean()),
-                                   "config": "synthetic stereo pairs (smooth disparity 5..60 px), 1200 feat, mb=0 "
-                                             "(reference call order), both images extracted + ComputeStereoMatches"}
+    # ---- config 3 stereo: KITTI 00 geometry pairs, extraction of both images + ComputeStereoMatches
+    out["stereo_kitti_1241x376"] = bench_stereo_kitti(args, amd, dev)
     # ---- config 3: KITTI geometry, 2000 features, extract + SearchForInitialization
     W, H, B = 1241, 376, 64
     cv = synth.canvas(0x5EED0003, W, H)
@@ -403,7 +565,7 @@ def bench_pose(args, amd, dev, n_frames=256, n_points=600):
         sys.path.insert(0, str(ROOT / "tests"))
         import oracle_ref as O
         sample = frames[:64]
-        threads = max(1, min(16, os.cpu_count() or 1))
+        threads = host_threads()
         t0 = time.perf_counter()
         with cf.ThreadPoolExecutor(threads) as ex:
             list(ex.map(O.pose_optimization, sample))
@@ -575,13 +737,56 @@ def batch_sweep(amd, dev, m):
     return res
 
 
-def main():
-    args = parse()
+def spawn_ranks(n):
+    """`bench.py --gpus N` without a launcher: start N worker processes of this script (one per
+    GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set) before this parent process makes any GPU
+    call, forward their output and exit with the first non-zero return code."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(pathlib.Path(__file__).resolve()), *sys.argv[1:]], env=env))
+    rcs = [p.wait() for p in procs]
+    return next((rc for rc in rcs if rc != 0), 0)
+
+
+def init_ranks(args):
+    """Rank / device / backend of this process.  One process per GPU over RCCL ("nccl") when
+    every local rank has its own device; when ranks outnumber the visible devices (a rehearsal of
+    N ranks on a one-GPU lease) ranks share devices round-robin and the collectives run over gloo,
+    since RCCL refuses two ranks on one device."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if args.gpus > 1 and world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch with torch.distributed.run "
+                         f"--nproc-per-node {args.gpus}, or without a launcher (bench.py spawns the ranks)")
+    ndev = torch.cuda.device_count()
+    if ndev < 1:
+        raise SystemExit("no GPU visible")
+    dev_idx = local % ndev
+    backend = None
     if world > 1:
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = "nccl" if ndev >= local_world else "gloo"
+        kw = {"device_id": torch.device("cuda", dev_idx)} if backend == "nccl" else {}
+        torch.distributed.init_process_group(backend, **kw)
+        world = torch.distributed.get_world_size()
+        rank = torch.distributed.get_rank()
+    return world, rank, dev_idx, backend, min(ndev, local_world)
+
+
+def main():
+    args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    world, rank, local, backend, n_devices = init_ranks(args)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     # all work (torch copies, HIP kernels, collectives) on one explicit non-default stream
@@ -693,6 +898,9 @@ def main():
         "value": round(value, 2),
         "unit": "frames/s",
         "n_gpus": world,
+        "world_size": world,
+        "collective_backend": backend,
+        "distinct_devices": n_devices if world > 1 else 1,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(1000 * dt / args.steps, 4),
@@ -737,6 +945,8 @@ def main():
                                    "peak_gbs": HBM_PEAK_GBS, "frac": round(b_ext * value / 1e9 / HBM_PEAK_GBS, 5)}
     if not args.no_lba:
         result["lba"] = bench_lba(args, amd, dev, local, rank, world)
+    if not args.no_stereo:
+        result["config5_stereo_sharded"] = bench_config5(args, amd, dev, rank, world)
     if world == 1 and not args.no_extras:
         result["extras"] = bench_extras(args, amd, dev)
     if rank == 0 and not args.no_cpu:

@@ -85,6 +85,14 @@ int orb_extract_batch_device(orb_extractor* ex, const uint8_t* d_imgs, size_t im
                              int B, int w, int h, orb_keypoint* d_kps, uint8_t* d_desc, int cap,
                              int32_t* d_counts, void* stream);
 
+/* Status of the handle's last extraction (orb_extract or orb_extract_batch_device), after waiting
+ * for the stream it ran on: *status = 0 when every internal table held, else a bit set —
+ * 1 a FAST cell window wider than the kernel's limit, 2 a cell's keypoint list truncated,
+ * 4 the octree iteration bound hit, 8 an octree node table full during a split phase,
+ * 16 a level's node list truncated.  Returns ORB_EOVERFLOW when *status != 0 (then some
+ * frame's keypoints of that batch may be incomplete), 0 otherwise. */
+int orb_extractor_batch_status(orb_extractor* ex, int32_t* status);
+
 /* Public `std::vector<cv::Mat> mvImagePyramid` (R/include/ORBextractor.h:88),
  * read by Frame::ComputeStereoMatches (R/src/Frame.cpp:558,675,689,695): returns a
  * host pointer to level `level` of frame `frame` of the last extraction
@@ -487,9 +495,13 @@ int lba_set_comm(lba_context* c, int rank, int world, double* d_workspace, size_
 
 /* Optimizer::LocalBundleAdjustment's optimisation (R/src/Optimizer.cpp:784-880):
  * optimize(5) with Huber kernels, chi2/depth outlier pass, optimize(10) on the
- * inliers without kernels, final chi2/depth check.  *stop (mbAbortBA) is polled
- * like SparseOptimizer::terminate().  The caller applies the results under
- * Map::mMutexMapUpdate exactly as R :883-917 do. */
+ * inliers without kernels, final chi2/depth check.  *stop (mbAbortBA) is read like
+ * SparseOptimizer::terminate(): on entry, after every LM trial (the device's decision
+ * kernel reads a host-mapped mirror of it, refreshed while the host waits) and between
+ * the two optimize() calls; with a communicator the ranks' flags are summed so every rank
+ * stops at the same point.  Every edge index must lie in [0, n_points) / [0, n_poses) and
+ * every array of a non-empty set must be non-NULL (ORB_EINVAL otherwise).  The caller
+ * applies the results under Map::mMutexMapUpdate exactly as R :883-917 do. */
 int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const volatile uint8_t* stop,
               lba_result* r);
 
@@ -511,6 +523,15 @@ int lba_solve_global(lba_context* c, const lba_problem* p, const lba_options* o,
  * zero or non-finite (the factorisation failure g2o turns into chi2 = inf). */
 int lba_dense_solve(lba_context* c, const double* S, const double* b, int n, double* x);
 int lba_profile(lba_context* c, int enable);
+/* Test hook for the stop semantics: the LM loop behaves as if *stop became set the moment the
+ * solve's trial count reached n_trials (sampled where g2o calls terminate(): after every trial,
+ * G/core/optimization_algorithm_levenberg.cpp:149, and before every iteration,
+ * G/core/sparse_optimizer.cpp:376), so a stop point is reproducible; n_trials < 0 turns it off. */
+int lba_debug_stop_after_trials(lba_context* c, int n_trials);
+/* Diagnostics: copies n doubles of a device buffer of the last solve's final LM state (0 the reduced
+ * matrix S, 1 b_s, 2 x, 3 Hpp blocks, 4 b_p, 5 Hll blocks, 6 b_l, 7 D^-1 blocks) to out; returns
+ * the buffer's length in doubles. */
+int lba_debug_buffer(lba_context* c, int which, double* out, size_t n);
 int lba_stats(lba_context* c, double* ms4, int* iters, int* trials);
 
 /* Converter::toSE3Quat(const cv::Mat& Tcw) / Converter::toCvMat(const SE3Quat&)

@@ -147,6 +147,7 @@ typedef struct {
     int rank, world, own0, own1;
     oracle_allreduce_fn ar;
     void* ar_user;
+    int stop_after;   /* terminate() once this many trials ran (-1: off) */
 } lba_ctx;
 
 static void allreduce(lba_ctx* c, double* v, int n, int op)
@@ -565,6 +566,12 @@ static void compute_active_errors(lba_ctx* c)
 enum { LM_OK = 0, LM_TERMINATE = 1 };
 
 /* OptimizationAlgorithmLevenberg::solve (G/core/optimization_algorithm_levenberg.cpp:61-164) */
+/* SparseOptimizer::terminate(): the caller's flag, or the test hook's trial count */
+static int terminated(const lba_ctx* c, const volatile uint8_t* stop, const lba_result_t* r)
+{
+    return (stop && *stop) || (c->stop_after >= 0 && r->trials >= c->stop_after);
+}
+
 static int lm_iteration(lba_ctx* c, int iteration, const volatile uint8_t* stop, lba_result_t* r)
 {
     compute_active_errors(c);
@@ -612,7 +619,7 @@ static int lm_iteration(lba_ctx* c, int iteration, const volatile uint8_t* stop,
         }
         qmax++;
         r->trials++;
-    } while (rho < 0 && qmax < c->o->max_trials && !(stop && *stop));
+    } while (rho < 0 && qmax < c->o->max_trials && !terminated(c, stop, r));
     if (r->trace && r->n_trace < 64) {
         double* t = r->trace + 4 * r->n_trace++;
         t[0] = iniChi; t[1] = currentChi; t[2] = c->lambda; t[3] = qmax;
@@ -629,7 +636,7 @@ static int optimize(lba_ctx* c, int iterations, const volatile uint8_t* stop, lb
 {
     if (c->P + c->M == 0 && c->world == 1) return 0;
     int it = 0, ok = 1;
-    for (int i = 0; i < iterations && !(stop && *stop) && ok; i++) {
+    for (int i = 0; i < iterations && !terminated(c, stop, r) && ok; i++) {
         ok = lm_iteration(c, i, stop, r) == LM_OK;
         it++;
     }
@@ -637,17 +644,23 @@ static int optimize(lba_ctx* c, int iterations, const volatile uint8_t* stop, lb
 }
 
 static int lba_run(const lba_problem_t* p, const lba_options_t* o, const volatile uint8_t* stop, lba_result_t* r,
-                   int rank, int world, oracle_allreduce_fn ar, void* user, int global, int robust);
+                   int rank, int world, oracle_allreduce_fn ar, void* user, int global, int robust, int stop_after);
 
 int oracle_lba_solve(const lba_problem_t* p, const lba_options_t* o, const volatile uint8_t* stop, lba_result_t* r)
 {
-    return lba_run(p, o, stop, r, 0, 1, NULL, NULL, 0, 1);
+    return lba_run(p, o, stop, r, 0, 1, NULL, NULL, 0, 1, -1);
+}
+
+int oracle_lba_solve_stop_after(const lba_problem_t* p, const lba_options_t* o, int stop_after_trials,
+                                lba_result_t* r)
+{
+    return lba_run(p, o, NULL, r, 0, 1, NULL, NULL, 0, 1, stop_after_trials < 0 ? -1 : stop_after_trials);
 }
 
 int oracle_lba_solve_dist(const lba_problem_t* p, const lba_options_t* o, const volatile uint8_t* stop,
                           lba_result_t* r, int rank, int world, oracle_allreduce_fn ar, void* user)
 {
-    return lba_run(p, o, stop, r, rank, world, ar, user, 0, 1);
+    return lba_run(p, o, stop, r, rank, world, ar, user, 0, 1, -1);
 }
 
 /* Optimizer::BundleAdjustment (R/src/Optimizer.cpp:78-277): one optimize(nIterations) = iters1
@@ -656,11 +669,11 @@ int oracle_lba_solve_dist(const lba_problem_t* p, const lba_options_t* o, const 
 int oracle_global_ba(const lba_problem_t* p, const lba_options_t* o, int robust, const volatile uint8_t* stop,
                      lba_result_t* r)
 {
-    return lba_run(p, o, stop, r, 0, 1, NULL, NULL, 1, robust);
+    return lba_run(p, o, stop, r, 0, 1, NULL, NULL, 1, robust, -1);
 }
 
 static int lba_run(const lba_problem_t* p, const lba_options_t* o, const volatile uint8_t* stop, lba_result_t* r,
-                   int rank, int world, oracle_allreduce_fn ar, void* user, int global, int robust)
+                   int rank, int world, oracle_allreduce_fn ar, void* user, int global, int robust, int stop_after)
 {
     lba_ctx c;
     memset(&c, 0, sizeof(c));
@@ -670,6 +683,7 @@ static int lba_run(const lba_problem_t* p, const lba_options_t* o, const volatil
     c.world = world;
     c.ar = ar;
     c.ar_user = user;
+    c.stop_after = stop_after;
     c.own0 = (int)((long long)p->n_points * rank / world);
     c.own1 = (int)((long long)p->n_points * (rank + 1) / world);
     const int NP = p->n_poses, NM = p->n_points, NE = p->n_edges;
@@ -711,7 +725,7 @@ static int lba_run(const lba_problem_t* p, const lba_options_t* o, const volatil
      * optimize(nIterations), R/src/Optimizer.cpp:230-231 */
     init_optimization(&c, 0);
     r->iterations[0] = optimize(&c, o->iters1, stop, r);
-    int bDoMore = !global && !(stop && *stop);
+    int bDoMore = !global && !terminated(&c, stop, r);
     if (bDoMore) {
         /* outlier pass (R/src/Optimizer.cpp:805-836) */
         for (int e = 0; e < NE; e++) {

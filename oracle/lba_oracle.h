@@ -66,6 +66,13 @@ typedef struct {
 int oracle_lba_solve(const lba_problem_t* p, const lba_options_t* o, const volatile uint8_t* stop,
                      lba_result_t* r);
 
+/* Same, with the stop flag treated as set once the solve's LM trial count reaches stop_after_trials
+ * (the test hook lba_debug_stop_after_trials of the library): terminate() is sampled after every
+ * trial (G/core/optimization_algorithm_levenberg.cpp:149), before every iteration
+ * (G/core/sparse_optimizer.cpp:376) and before the second optimize() (R/src/Optimizer.cpp:792-796). */
+int oracle_lba_solve_stop_after(const lba_problem_t* p, const lba_options_t* o, int stop_after_trials,
+                                lba_result_t* r);
+
 /* Landmark-sharded variant (the multi-GPU algorithm of liborbslam2_amd): rank
  * `rank` of `world` owns points [rank*M/world, (rank+1)*M/world); `ar` all-reduces
  * n doubles in place across ranks (op 0 sum, 1 max). */

@@ -63,6 +63,7 @@ def lib() -> C.CDLL:
             "orb_extractor_stage_times": [vp, vp, i32, vp],
             "orb_extractor_geometry": [vp, i32, i32, vp, vp, vp, vp],
             "orb_extractor_last_counts": [vp, i32, vp, vp],
+            "orb_extractor_batch_status": [vp, vp],
             "orb_matcher_create": [i32, f32, i32, vp],
             "orb_matcher_destroy": [vp],
             "orb_descriptor_distance": [vp, vp],

@@ -2114,6 +2114,19 @@ int orb_extract_batch_device(orb_extractor* ex, const uint8_t* d_imgs, size_t im
     return run_pipeline(ex, B, d_kps, d_desc, cap, d_counts, s);
 }
 
+int orb_extractor_batch_status(orb_extractor* ex, int32_t* status) {
+    if (!ex || !status) return ORB_EINVAL;
+    ORB_HIP_TRY(hipSetDevice(ex->device));
+    hipStream_t st = ex->lastStream ? ex->lastStream : ex->stream;
+    int32_t* h = nullptr;
+    if (ensure_pinned(&ex->h_out, &ex->h_out_bytes, 64)) return ORB_ENOMEM;
+    h = (int32_t*)ex->h_out + 15;   // the last word of the 64-byte header (orb_extract uses words 0-1)
+    ORB_HIP_TRY(hipMemcpyAsync(h, ex->d_status, 4, hipMemcpyDeviceToHost, st));
+    ORB_HIP_TRY(hipStreamSynchronize(st));
+    *status = *h;
+    return *h ? ORB_EOVERFLOW : ORB_OK;
+}
+
 int orb_pyramid_level(orb_extractor* ex, int frame, int level, const uint8_t** host, int* w, int* h, size_t* stride) {
     if (!ex || level < 0 || level >= ex->p.nlevels || frame < 0 || frame >= ex->lastB || ex->gw < 0) return ORB_EINVAL;
     ORB_HIP_TRY(hipSetDevice(ex->device));
@@ -2124,9 +2137,11 @@ int orb_pyramid_level(orb_extractor* ex, int frame, int level, const uint8_t** h
     const LevelGeom& L = g.lv[level];
     uint8_t* dst = ex->h_levels.data() + per * frame + L.off;
     char& valid = ex->h_level_valid[(size_t)frame * g.nlevels + level];
-    if (!valid) {
-        ORB_HIP_TRY(hipStreamSynchronize(ex->stream));
-        ORB_HIP_TRY(hipMemcpy(dst, ex->d_pyr + per * frame + L.off, (size_t)L.pitch * L.h, hipMemcpyDeviceToHost));
+    if (!valid) {   // ordered after the extraction on the stream it ran on (a caller stream for the batch path)
+        hipStream_t st = ex->lastStream ? ex->lastStream : ex->stream;
+        ORB_HIP_TRY(hipMemcpyAsync(dst, ex->d_pyr + per * frame + L.off, (size_t)L.pitch * L.h, hipMemcpyDeviceToHost,
+                                   st));
+        ORB_HIP_TRY(hipStreamSynchronize(st));
         valid = 1;
     }
     if (host) *host = dst;
@@ -2206,8 +2221,7 @@ int orb_extractor_last_counts(orb_extractor* ex, int frame, int* pre_counts, int
     ORB_HIP_TRY(hipSetDevice(ex->device));
     const Geom& g = ex->g;
     std::vector<int> cc(g.cellsPerFrame), lc(g.nlevels);
-    ORB_HIP_TRY(hipStreamSynchronize(ex->stream));
-    ORB_HIP_TRY(hipDeviceSynchronize());
+    ORB_HIP_TRY(hipStreamSynchronize(ex->lastStream ? ex->lastStream : ex->stream));
     ORB_HIP_TRY(hipMemcpy(cc.data(), ex->d_cellCount + (size_t)frame * g.cellsPerFrame, cc.size() * 4,
                           hipMemcpyDeviceToHost));
     ORB_HIP_TRY(hipMemcpy(lc.data(), ex->d_levelCount + (size_t)frame * g.nlevels, lc.size() * 4,

@@ -58,6 +58,12 @@ struct LmState {
     int phase;      // 0: linearise next, 1: trial next, 2: done
     int it, qmax, nBad, itersDone, trials, pop;
     int traceBase;  // first trace row of this optimize() call
+    // SparseOptimizer::terminate() (the mbAbortBA flag, G/core/sparse_optimizer.h:189): sampled
+    // after every trial, where g2o tests it in the trial loop (optimization_algorithm_levenberg.cpp:149)
+    // and right after in the iteration loop (sparse_optimizer.cpp:376)
+    int stopAfter;  // test hook: stop once trialBase + trials reaches it (-1: off)
+    int trialBase;  // trials of this solve before this optimize() call
+    int stopped;    // 1 once the stop was observed
 };
 
 // Kernels of the LM loop run only in their phase (`want`): 0 linearisation, 1 trial,
@@ -96,7 +102,16 @@ struct LbaDev {
     double *partChi, *partScale, *partMax;   // per-workgroup partials (single-process LM kernels)
     int* flags;                 // [0] LDLT failure
     LmState* lm;                // LM control state (device)
+    const uint32_t* stopWord;   // host-mapped mirror of the caller's stop flag (lba_wait copies it)
 };
+
+// terminate() as the device sees it after a trial: the test hook's trial count, else the stop word
+// (single process: the host-mapped word itself; with a communicator: the ranks' all-reduced sample)
+__device__ __forceinline__ bool lm_stop_now(const LmState* st, const uint32_t* word, double shared) {
+    if (st->stopAfter >= 0 && st->trialBase + st->trials >= st->stopAfter) return true;
+    if (word) return __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
+    return shared > 0.0;
+}
 
 __device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
@@ -465,7 +480,10 @@ __global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag) {
     }
     sum += __shfl_xor(sum, 1, 64);
     sum += __shfl_xor(sum, 2, 64);
-    if (v < nv && q == 0) {
+    // a diagonal block's product (Hpl D^-1) Hpl^T is not bitwise symmetric: only its upper
+    // triangle (r <= qq) is stored, mirrored, as g2o fills S from the upper blocks (the lower
+    // entries written by both threads of a pair would race)
+    if (v < nv && q == 0 && !(diag && v < 36 && v / 6 > v % 6)) {
         const int n = 6 * d.P;
         if (v < 36) {
             const int r = v / 6, qq = v % 6;
@@ -1007,7 +1025,8 @@ __global__ void k_lm_begin(LmState* st, const double* __restrict__ red) {
 // SparseOptimizer::optimize / OptimizationAlgorithmLevenberg (termination on qmax == max
 // trials, rho == 0 or three iterations without 1e-3 relative progress).
 __device__ void lm_decide(LmState* st, double chiSum, double scaleSum, int fail, int maxTrials, int iterations,
-                          int fixedIterations, double* __restrict__ trace) {
+                          int fixedIterations, double* __restrict__ trace, const uint32_t* stopWord,
+                          double sharedStop) {
     const double tempChi = fail ? DBL_MAX : chiSum;
     double rho = st->currentChi - tempChi;
     const double scale = scaleSum + 1e-3;
@@ -1027,7 +1046,8 @@ __device__ void lm_decide(LmState* st, double chiSum, double scaleSum, int fail,
     st->rho = rho;
     st->qmax++;
     st->trials++;
-    if (rho < 0 && st->qmax < maxTrials) return;   // next trial of this iteration
+    const bool stopNow = lm_stop_now(st, stopWord, sharedStop);
+    if (rho < 0 && st->qmax < maxTrials && !stopNow) return;   // next trial of this iteration
     const int row = st->traceBase + st->itersDone;
     if (trace && row < 64) {
         trace[4 * row] = st->iniChi;
@@ -1047,14 +1067,22 @@ __device__ void lm_decide(LmState* st, double chiSum, double scaleSum, int fail,
             if (st->nBad >= 3) go = false;
         }
     }
-    st->phase = (go && st->it < iterations) ? 0 : 2;
+    if (stopNow) st->stopped = 1;   // the iteration loop ends as well (sparse_optimizer.cpp:376)
+    st->phase = (go && st->it < iterations && !stopNow) ? 0 : 2;
 }
 __global__ void k_lm_decide(LmState* st, const double* __restrict__ red, const int* __restrict__ flags, int maxTrials,
                             int iterations, int fixedIterations, double* __restrict__ trace) {
     if (threadIdx.x != 0) return;
     st->pop = 0;
     if (st->phase != 1) return;
-    lm_decide(st, red[0], red[2], flags[0], maxTrials, iterations, fixedIterations, trace);
+    lm_decide(st, red[0], red[2], flags[0], maxTrials, iterations, fixedIterations, trace, nullptr, red[3]);
+}
+
+// Communicator path: this rank's stop sample into red[3], summed over the ranks with the scale
+// term (red[2..3]) so every rank takes the same terminate() decision.
+__global__ void k_stop_sample(const LmState* st, const uint32_t* __restrict__ word, double* __restrict__ red) {
+    if (threadIdx.x != 0 || st->phase != 1) return;
+    red[3] = (word && __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) ? 1.0 : 0.0;
 }
 
 // Single process: the start of an LM iteration in one wave — the linearisation's robust chi2
@@ -1095,7 +1123,7 @@ __global__ __launch_bounds__(1024) void k_lm_decide_fused(LbaDev d, const int32_
         c = wave_sum_d(c);
         sc = wave_sum_d(sc);
         if (tid == 0) {
-            lm_decide(st, c, sc, d.flags[0], maxTrials, iterations, fixedIterations, trace);
+            lm_decide(st, c, sc, d.flags[0], maxTrials, iterations, fixedIterations, trace, d.stopWord, 0.0);
             pop = st->pop;
         }
     }
@@ -1151,6 +1179,13 @@ struct lba_context {
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};   // stage timing
     hipEvent_t evSync = nullptr;                               // LM decision hand-off
     double* h_scal = nullptr;                                  // pinned LM scalars / state (4 KB)
+    // terminate(): the caller's stop flag (mbAbortBA) mirrored into a host-mapped word the LM
+    // decision kernels read after every trial; lba_wait copies it while the host waits
+    uint32_t* h_stop = nullptr;
+    uint32_t* d_stop = nullptr;
+    const volatile uint8_t* stopSrc = nullptr;
+    int stopAfter = -1;                                        // test hook (lba_debug_stop_after_trials)
+    orbamd::LbaDev last{};                                     // device buffers of the last solve (lba_debug_buffer)
     std::vector<hipEvent_t> slotEv;                            // per-slot stage timing
     // grow-only pinned staging: [0] problem upload, [1] per-optimize() structure, [2] downloads
     char* stage[3] = {nullptr, nullptr, nullptr};
@@ -1255,11 +1290,14 @@ static UpItem up(T** dst, const T* src, size_t n) {
 
 // Waits for the stream by spinning on an event (a blocking hipStreamSynchronize sleeps and
 // adds tens of microseconds per LM trial).
+static inline void mirror_stop(lba_context* c) {
+    if (c->stopSrc && *c->stopSrc && c->h_stop && !__atomic_load_n(c->h_stop, __ATOMIC_RELAXED))
+        __atomic_store_n(c->h_stop, 1u, __ATOMIC_RELEASE);
+}
 static int lba_wait(lba_context* c) {
     if (hipEventRecord(c->evSync, c->stream) != hipSuccess) return ORB_EGPU;
     hipError_t e;
-    while ((e = hipEventQuery(c->evSync)) == hipErrorNotReady) {
-    }
+    while ((e = hipEventQuery(c->evSync)) == hipErrorNotReady) mirror_stop(c);
     return e == hipSuccess ? ORB_OK : ORB_EGPU;
 }
 
@@ -1300,7 +1338,10 @@ int lba_create(int device, lba_context** out) {
     c->device = device;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return ORB_EGPU; }
     bool ok = hipEventCreateWithFlags(&c->evSync, hipEventDisableTiming) == hipSuccess &&
-              hipHostMalloc((void**)&c->h_scal, 4096, hipHostMallocDefault) == hipSuccess;
+              hipHostMalloc((void**)&c->h_scal, 4096, hipHostMallocDefault) == hipSuccess &&
+              hipHostMalloc((void**)&c->h_stop, 64, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
+              hipHostGetDevicePointer((void**)&c->d_stop, c->h_stop, 0) == hipSuccess;
+    if (c->h_stop) *c->h_stop = 0;
     for (auto& e : c->ev) ok = ok && hipEventCreate(&e) == hipSuccess;
     if (!ok) { lba_destroy(c); return ORB_EGPU; }
     *out = c;
@@ -1317,6 +1358,7 @@ void lba_destroy(lba_context* c) {
     if (c->evSync) (void)hipEventDestroy(c->evSync);
     for (auto e : c->slotEv) (void)hipEventDestroy(e);
     if (c->h_scal) (void)hipHostFree(c->h_scal);
+    if (c->h_stop) (void)hipHostFree(c->h_stop);
     for (auto p : c->stage)
         if (p) (void)hipHostFree(p);
     for (auto& g : c->graphs) (void)hipGraphExecDestroy(g.exec);
@@ -1388,6 +1430,36 @@ int lba_dense_solve(lba_context* c, const double* S, const double* b, int n, dou
     return fail ? ORB_EINVAL : ORB_OK;
 }
 
+int lba_debug_stop_after_trials(lba_context* c, int n_trials) {
+    if (!c) return ORB_EINVAL;
+    c->stopAfter = n_trials < 0 ? -1 : n_trials;
+    return ORB_OK;
+}
+
+int lba_debug_buffer(lba_context* c, int which, double* out, size_t n) {
+    if (!c || !out) return ORB_EINVAL;
+    const LbaDev& d = c->last;
+    const double* src = nullptr;
+    size_t avail = 0;
+    const size_t P = (size_t)d.P, M = (size_t)d.M;
+    switch (which) {
+        case 0: src = d.S; avail = 36 * P * P; break;
+        case 1: src = d.bs; avail = 6 * P; break;
+        case 2: src = d.x; avail = 6 * P + 3 * M; break;
+        case 3: src = d.Hpp; avail = 36 * P; break;
+        case 4: src = d.bp; avail = 6 * P; break;
+        case 5: src = d.Hll; avail = 9 * M; break;
+        case 6: src = d.bl; avail = 3 * M; break;
+        case 7: src = d.Dinv; avail = 9 * M; break;
+        default: return ORB_EINVAL;
+    }
+    if (!src || n > avail) return ORB_EINVAL;
+    ORB_HIP_TRY(hipSetDevice(c->device));
+    ORB_HIP_TRY(hipStreamSynchronize(c->stream));
+    ORB_HIP_TRY(hipMemcpy(out, src, 8 * n, hipMemcpyDeviceToHost));
+    return (int)avail;
+}
+
 int lba_profile(lba_context* c, int enable) {
     if (!c) return ORB_EINVAL;
     c->profile = enable != 0;
@@ -1444,14 +1516,47 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
     const auto hEntry = std::chrono::steady_clock::now();
 #endif
     if (!c || !p || !o || !r || p->n_poses < 0 || p->n_points < 0 || p->n_edges < 0) return ORB_EINVAL;
+    const int NP = p->n_poses, NM = p->n_points, NE = p->n_edges;
+    if ((NP > 0 && (!p->pose_q || !p->pose_t || !p->pose_fixed || !p->pose_id)) ||
+        (NM > 0 && (!p->point_xyz || !p->point_id)) ||
+        (NE > 0 && (!p->edge_point || !p->edge_pose || !p->edge_stereo || !p->edge_obs || !p->edge_info ||
+                    !p->edge_cam)))
+        return ORB_EINVAL;
+    for (int e = 0; e < NE; e++)   // every index the structure build and the kernels dereference
+        if (p->edge_point[e] < 0 || p->edge_point[e] >= NM || p->edge_pose[e] < 0 || p->edge_pose[e] >= NP)
+            return ORB_EINVAL;
     ORB_HIP_TRY(hipSetDevice(c->device));
     hipStream_t s = c->stream;
-    const int NP = p->n_poses, NM = p->n_points, NE = p->n_edges;
     r->iterations[0] = r->iterations[1] = 0;
     r->trials = 0;
     r->n_trace = 0;
     r->aborted = 0;
-    if (!global && stop && *stop) {   // R/src/Optimizer.cpp:784-786: return before optimizing, no write-back
+    struct StopScope {   // the stop mirror is live for this call only
+        lba_context* c;
+        ~StopScope() { c->stopSrc = nullptr; }
+    } stopScope{c};
+    c->stopSrc = stop;
+    __atomic_store_n(c->h_stop, (stop && *stop) ? 1u : 0u, __ATOMIC_RELEASE);
+    auto stopped = [&]() { return (stop && *stop) || (c->stopAfter >= 0 && r->trials >= c->stopAfter); };
+    // with a communicator every rank must take the same stop decision: a rank's flag is summed
+    // over the ranks (the decision points are rare: entry, after each optimize())
+    auto agreed = [&](bool mine, bool* out) -> int {
+        *out = mine;
+        if (c->world <= 1) return ORB_OK;
+        if (!c->allreduce || !c->ws || c->wsDoubles < 1) return ORB_EINVAL;
+        double* h = c->h_scal + 256;
+        h[0] = mine ? 1.0 : 0.0;
+        ORB_HIP_TRY(hipMemcpyAsync(c->ws, h, 8, hipMemcpyHostToDevice, s));
+        TRY(lba_wait(c));
+        if (c->allreduce(c->commUser, 0, 1, 0) != 0) return ORB_EGPU;
+        ORB_HIP_TRY(hipMemcpyAsync(h, c->ws, 8, hipMemcpyDeviceToHost, s));
+        TRY(lba_wait(c));
+        *out = h[0] > 0.5;
+        return ORB_OK;
+    };
+    bool stopEntry = false;
+    TRY(agreed(!global && stop && *stop, &stopEntry));
+    if (stopEntry) {   // R/src/Optimizer.cpp:784-786: return before optimizing, no write-back
         r->aborted = 1;
         return ORB_OK;
     }
@@ -1471,6 +1576,7 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
     ORB_HIP_TRY(hipMemsetAsync(d.err, 0, 24 * (size_t)NE, s));
     d.q = q; d.t = t; d.X = X; d.fixed = fixed; d.ept = ept; d.eps = eps; d.est = est; d.obs = obs; d.info = info;
     d.cam = cam; d.robust = robust;
+    d.stopWord = c->d_stop;
     // per-edge / per-vertex scratch sized for the full problem
     TRY(dalloc(c, &d.Hll_e, 6 * (size_t)NE)); TRY(dalloc(c, &d.Hpp_e, 21 * (size_t)NE));
     TRY(dalloc(c, &d.Hpl_e, 18 * (size_t)NE)); TRY(dalloc(c, &d.bl_e, 3 * (size_t)NE));
@@ -1504,7 +1610,7 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
     std::vector<uint8_t> level(NE, 0), robustH(NE, robustKernels ? 1 : 0);
     const double hm = o->huber_mono, hsv = o->huber_stereo;
     const int maxTrials = o->max_trials > 0 ? o->max_trials : 10;
-    auto stopped = [&]() { return stop && *stop; };
+    bool devStopped = false;   // the LM kernels observed terminate()
 
     auto elapsed = [&](hipEvent_t a, hipEvent_t b) {
         float ms = 0;
@@ -1590,7 +1696,8 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
             const int nx = 6 * d.P + 3 * d.M;
             hipLaunchKernelGGL(k_scale_terms, grid(nx), dim3(256), 0, s, d, root ? 1 : 0, d.echi);
             hipLaunchKernelGGL(k_sum, dim3(1), dim3(1024), 0, s, d.echi, nx, d.red + 2, d.lm, 1);
-            TRY(comm_allreduce_g(c, d.red + 2, 1, 0, d.lm, 1));
+            hipLaunchKernelGGL(k_stop_sample, dim3(1), dim3(64), 0, s, d.lm, d.stopWord, d.red);
+            TRY(comm_allreduce_g(c, d.red + 2, 2, 0, d.lm, 1));
             hipLaunchKernelGGL(k_lm_decide, dim3(1), dim3(64), 0, s, d.lm, d.red, d.flags, maxTrials, iterations,
                                o->fixed_iterations ? 1 : 0, d_trace);
             hipLaunchKernelGGL(k_pop, grid(std::max(d.M, d.P)), dim3(256), 0, s, d, d.P, d_freePoses);
@@ -1605,11 +1712,15 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
     auto optimize = [&](int iterations, int& itersDone) -> int {
         itersDone = 0;
         if (hs.P + hs.M == 0 && c->world == 1) return ORB_OK;
-        if (iterations <= 0 || stopped()) return ORB_OK;
+        bool stopNow = false;
+        TRY(agreed(stopped(), &stopNow));
+        if (iterations <= 0 || stopNow) return ORB_OK;   // sparse_optimizer.cpp:376 before iteration 0
         LmState* hst = reinterpret_cast<LmState*>(reinterpret_cast<char*>(c->h_scal) + 512);
         std::memset(hst, 0, sizeof(LmState));
         hst->ni = 2;
         hst->traceBase = r->trace ? r->n_trace : 64;
+        hst->stopAfter = c->stopAfter;
+        hst->trialBase = r->trials;
         ORB_HIP_TRY(hipMemcpyAsync(d.lm, hst, sizeof(LmState), hipMemcpyHostToDevice, s));
         // Single process, no stage events: the slots are captured into HIP graphs and
         // replayed, so the LM loop pays one graph launch per group of slots instead of a host
@@ -1684,8 +1795,12 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
                 }
             }
             known = hst->itersDone;
-            if (hst->phase == 2 || stopped()) break;
+            if (hst->phase == 2) break;
+            // single process: a stop seen by the host between iterations ends the loop where
+            // g2o's iteration loop would test terminate(); mid-iteration the device decides
+            if (c->world == 1 && hst->phase == 0 && stopped()) { devStopped = true; break; }
         }
+        if (hst->stopped) devStopped = true;
         itersDone = hst->itersDone;
         r->trials += hst->trials;
         c->n_trials += hst->trials;
@@ -1711,7 +1826,9 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
     HSTAMP(1);
     TRY(optimize(o->iters1, r->iterations[0]));
     HSTAMP(2);
-    const bool bDoMore = !global && !stopped();   // global BA: one optimize(nIterations), R :230-231
+    bool stopAfter1 = false;
+    TRY(agreed(stopped() || devStopped, &stopAfter1));
+    const bool bDoMore = !global && !stopAfter1;   // global BA: one optimize(nIterations), R :230-231
     auto edge_check = [&](std::vector<double>& chi, std::vector<uint8_t>& dep) -> int {
         if (NE > 0) hipLaunchKernelGGL(k_edge_check, grid(NE), dim3(256), 0, s, d, NE, d_chi2, d_depth);
         chi.resize(NE);
@@ -1785,6 +1902,7 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         if (r->pose_t) std::memcpy(r->pose_t, h + bq, 24 * (size_t)NP);
         if (r->point_xyz) std::memcpy(r->point_xyz, h + bq + bt, 24 * (size_t)NM);
     }
+    c->last = d;
 #ifdef ORB_TIMING
     HSTAMP(6);
     auto us = [&](int a, int b) { return std::chrono::duration<double, std::micro>(hT[b] - hT[a]).count(); };

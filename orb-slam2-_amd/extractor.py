@@ -110,3 +110,12 @@ class ORBextractor:
         _abi.check("orb_extract_batch_device", _abi.lib().orb_extract_batch_device(
             self._h, _abi.ptr(imgs), H * W, B, W, H, _abi.ptr(kps_out), _abi.ptr(desc_out), cap,
             _abi.ptr(counts_out), C.c_void_p(stream) if stream else None))
+
+    def batch_status(self):
+        """Status bits of the last extraction (include/orbslam2_amd.h orb_extractor_batch_status):
+        0 when no internal table overflowed."""
+        st = C.c_int32(0)
+        rc = _abi.lib().orb_extractor_batch_status(self._h, C.byref(st))
+        if rc not in (0, -75):
+            _abi.check("orb_extractor_batch_status", rc)
+        return int(st.value)

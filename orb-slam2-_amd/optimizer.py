@@ -34,6 +34,11 @@ class LbaResult(C.Structure):
                 ("trials", C.c_int), ("trace", C.c_void_p), ("n_trace", C.c_int), ("aborted", C.c_int)]
 
 
+# lba_problem's field types (include/orbslam2_amd.h); Tcw is converted separately
+PROBLEM_DTYPES = {"pose_fixed": np.uint8, "pose_id": np.int64, "point_xyz": np.float64, "point_id": np.int64,
+                  "point_bad": np.uint8, "edge_point": np.int32, "edge_pose": np.int32, "edge_stereo": np.uint8,
+                  "edge_obs": np.float64, "edge_info": np.float64, "edge_cam": np.float64}
+
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_size_t, C.c_size_t, C.c_int)
 
 
@@ -61,6 +66,8 @@ def _sig():
                             ("lba_solve", [vp, vp, vp, vp, vp], C.c_int), ("lba_profile", [vp, i32], C.c_int),
                             ("lba_solve_global", [vp, vp, vp, i32, vp, vp], C.c_int),
                             ("lba_stats", [vp, vp, vp, vp], C.c_int),
+                            ("lba_debug_stop_after_trials", [vp, i32], C.c_int),
+                            ("lba_debug_buffer", [vp, i32, vp, sz], C.c_int),
                             ("lba_dense_solve", [vp, vp, vp, i32, vp], C.c_int), ("lba_pose_from_Tcw", [vp, vp, vp], None),
                             ("lba_pose_to_Tcw", [vp, vp, vp], None),
                             ("lba_poses_from_Tcw", [vp, i32, vp, vp], None)]:
@@ -133,6 +140,21 @@ class LocalBA:
     def profile(self, enable=True):
         _sig().lba_profile(self._h, int(enable))
 
+    def debug_buffer(self, which):
+        """A device buffer of the last solve (lba_debug_buffer: 0 S, 1 b_s, 2 x, 3 Hpp, 4 b_p, 5 Hll,
+        6 b_l, 7 D^-1) as a float64 array."""
+        n = _sig().lba_debug_buffer(self._h, which, _abi.ptr(np.zeros(1)), 0)
+        _abi.check("lba_debug_buffer", n)
+        out = np.zeros(n)
+        _abi.check("lba_debug_buffer", _sig().lba_debug_buffer(self._h, which, _abi.ptr(out), n))
+        return out
+
+    def debug_stop_after_trials(self, n):
+        """Test hook: behave as if the stop flag became set when the solve's trial count reached n
+        (None / negative: off)."""
+        _abi.check("lba_debug_stop_after_trials",
+                   _sig().lba_debug_stop_after_trials(self._h, -1 if n is None else int(n)))
+
     def stats(self):
         ms = np.zeros(4)
         it, tr = C.c_int(), C.c_int()
@@ -150,7 +172,9 @@ class LocalBA:
         Tcw = np.ascontiguousarray(prob["Tcw"], np.float32)
         q, t = np.zeros((nk, 4)), np.zeros((nk, 3))
         _sig().lba_poses_from_Tcw(_abi.ptr(Tcw), nk, _abi.ptr(q), _abi.ptr(t))   # Converter::toSE3Quat
-        a = {k: np.ascontiguousarray(v) for k, v in prob.items()}
+        # each field coerced to the C type lba_problem declares (include/orbslam2_amd.h)
+        a = {k: np.ascontiguousarray(v, PROBLEM_DTYPES[k]) if k in PROBLEM_DTYPES and v is not None else v
+             for k, v in prob.items()}
         P = _abi.ptr
         pr = LbaProblem(nk, P(q), P(t), P(a["pose_fixed"]), P(a["pose_id"]), len(a["point_xyz"]), P(a["point_xyz"]),
                         P(a["point_id"]), P(a.get("point_bad")), len(a["edge_point"]), P(a["edge_point"]),

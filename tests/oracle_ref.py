@@ -279,7 +279,7 @@ def global_ba(prob, n_iterations=10, robust=True, stop=False, fixed_iterations=F
     return lba_solve(prob, global_ba_options(n_iterations, fixed_iterations), stop, global_robust=int(robust))
 
 
-def lba_solve(prob, options=None, stop=False, global_robust=None):
+def lba_solve(prob, options=None, stop=False, global_robust=None, stop_after_trials=None):
     options = options or lba_options()
     nk = len(prob["Tcw"])
     qs, ts = zip(*[quat_from_Tcw(T) for T in prob["Tcw"]])
@@ -295,7 +295,9 @@ def lba_solve(prob, options=None, stop=False, global_robust=None):
     r = LbaResult(P(out["pose_q"]), P(out["pose_t"]), P(out["point_xyz"]), P(out["edge_erase"]),
                   P(out["edge_chi2"]), (C.c_int * 2)(0, 0), 0, P(out["trace"]), 0)
     flag = (C.c_uint8 * 1)(1 if stop else 0)
-    if global_robust is None:
+    if stop_after_trials is not None:
+        st = lib().oracle_lba_solve_stop_after(C.byref(pr), C.byref(options), int(stop_after_trials), C.byref(r))
+    elif global_robust is None:
         st = lib().oracle_lba_solve(C.byref(pr), C.byref(options), flag, C.byref(r))
     else:
         st = lib().oracle_global_ba(C.byref(pr), C.byref(options), global_robust, flag, C.byref(r))

@@ -105,10 +105,12 @@ def test_noise_image_retry_threshold(amd):
     _compare(ref, kps, desc)
 
 
-@pytest.mark.parametrize("W,H,nf,seed,mbf", [(752, 480, 1200, 0x5EED0005, 47.9), (640, 480, 1000, 0x5EED0006, 40.0)])
+@pytest.mark.parametrize("W,H,nf,seed,mbf", [(752, 480, 1200, 0x5EED0005, 47.9), (640, 480, 1000, 0x5EED0006, 40.0),
+                                             (1241, 376, 2000, 0x5EED0003, 386.1448)])
 def test_compute_stereo_matches(amd, W, H, nf, seed, mbf):
     """Frame::ComputeStereoMatches on the GPU (pyramids read in place) vs the oracle on a
-    synthetic stereo pair with a smooth disparity field."""
+    synthetic stereo pair with a smooth disparity field: EuRoC geometry,
+    TUM geometry, and KITTI 00 geometry with the KITTI bf (config 3, R/Examples/Stereo/KITTI00-02.yaml)."""
     from orb_slam2_amd import synth
     cv = synth.canvas(seed, W, H)
     left, right = synth.stereo_pair(cv, W, H, 0)
@@ -169,3 +171,40 @@ def test_compute_stereo_matches_batch_device(amd):
         assert int(ns[i]) == n_ref
         assert np.array_equal(ur[i, :nl].cpu().numpy(), ur_ref)
         assert np.array_equal(dep[i, :nl].cpu().numpy(), dep_ref)
+
+
+def test_batch_device_status_dense_octree_hbm_path(amd):
+    """Throughput path with a frame whose levels hold far more FAST keys than the octree's LDS
+    key buffers (uniform noise: ~27,700 keys on level 0, so k_octree runs on its HBM key
+    arrays): keypoints / descriptors bit-exact vs the oracle and the batch status (cell /
+    octree table overflow bits, orb_extractor_batch_status) reads 0."""
+    import torch
+    from orb_slam2_amd import synth, _abi
+    import ctypes as C
+    W, H, nf = 640, 480, 1000
+    noise = np.random.default_rng(5).integers(0, 256, (H, W)).astype(np.uint8)
+    frame = synth.frame(synth.canvas(0x5EED0001, W, H), W, H, 0)
+    imgs = np.stack([noise, frame, noise[::-1].copy()])
+    B = len(imgs)
+    dev = torch.device("cuda", 0)
+    ex = amd.ORBextractor(nf, 1.2, 8, 20, 7, max_w=W, max_h=H, max_batch=B)
+    cap = C.c_int()
+    _abi.check("geom", _abi.lib().orb_extractor_geometry(ex._h, W, H, None, None, None, C.byref(cap)))
+    cap = cap.value
+    ti = torch.from_numpy(imgs).to(dev)
+    kps = torch.zeros((B, cap, 7), dtype=torch.int32, device=dev)
+    desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(B, dtype=torch.int32, device=dev)
+    ex.extract_batch_device(ti, kps, desc, cnt, torch.cuda.current_stream(dev).cuda_stream)
+    assert ex.batch_status() == 0
+    pre = np.zeros(8, np.int32)
+    _abi.check("counts", _abi.lib().orb_extractor_last_counts(ex._h, 0, _abi.ptr(pre), None))
+    assert pre[0] > 20000
+    p = O.params(nf)
+    for b in range(B):
+        ref = O.extract(p, imgs[b])
+        n = int(cnt[b])
+        assert n == len(ref["kps"])
+        got_k = kps[b, :n].cpu().numpy().view(amd._abi.KEYPOINT_DTYPE).reshape(-1)
+        assert got_k.tobytes() == ref["kps"].tobytes()
+        assert np.array_equal(desc[b, :n].cpu().numpy(), ref["desc"])

@@ -85,3 +85,112 @@ def test_dense_solve_zero_pivot_fails(amd):
     S[7, 7] = 0.0
     with pytest.raises(amd._abi.OrbError):
         amd.LocalBA().dense_solve(S, np.ones(20))
+
+
+@pytest.mark.parametrize("stop_after", [0, 1, 3, 4, 7, 10, 13, 18])
+def test_stop_after_trials_matches_oracle(amd, stop_after):
+    """mbAbortBA raised at a reproducible point: terminate() true once the solve has run
+    `stop_after` LM trials.  g2o samples it after every trial (levenberg.cpp:149), before every
+    iteration (sparse_optimizer.cpp:376) and before the second optimize (Optimizer.cpp:792-796);
+    the device's decision kernel samples at the same points, so decisions, estimates and the
+    erase set equal the oracle stopped at the same trial."""
+    pb = _problem(amd, n_local=12, n_fixed=2, n_points=1200, seed=31, outlier_frac=0.2)
+    ref = O.lba_solve(pb, stop_after_trials=stop_after)
+    ctx = amd.LocalBA()
+    ctx.debug_stop_after_trials(stop_after)
+    got = ctx.solve(pb)
+    assert not got["aborted"]
+    _compare(ref, got)
+    assert got["trials"] == min(ref["trials"], got["trials"])
+    full = O.lba_solve(pb)
+    if stop_after < full["trials"]:
+        assert sum(got["iterations"]) < sum(full["iterations"]) or got["trials"] < full["trials"]
+
+
+def test_stop_flag_raised_mid_solve_by_host_thread(amd):
+    """The Tracking thread's InterruptBA (R/src/Tracking.cpp:1411) arrives while the solve runs:
+    the LM loop stops at the next trial boundary, skips the second optimize() and still writes
+    back; the result equals the oracle stopped after the same number of trials."""
+    import threading
+    import time
+    pb = _problem(amd, n_local=30, n_fixed=4, n_points=12000, seed=33, outlier_frac=0.1)
+    ctx = amd.LocalBA()
+    ctx.solve(pb)                                    # warm-up (code objects, arena)
+    t0 = time.perf_counter()
+    full = ctx.solve(pb)
+    t_full = time.perf_counter() - t0
+    flag = (C.c_uint8 * 1)(0)
+    timer = threading.Timer(t_full / 4, lambda: C.memset(flag, 1, 1))
+    timer.start()
+    got = ctx.solve(pb, stop=flag)
+    timer.join()
+    assert not got["aborted"]
+    assert got["trials"] <= full["trials"]
+    ref = O.lba_solve(pb, stop_after_trials=got["trials"])
+    _compare(ref, got)
+
+
+def test_lba_rejects_out_of_range_edges(amd):
+    """lba_solve validates every edge index before touching host or device memory."""
+    pb = _problem(amd, n_points=200, seed=4)
+    bad = dict(pb)
+    bad["edge_point"] = pb["edge_point"].copy()
+    bad["edge_point"][5] = len(pb["point_xyz"])
+    with pytest.raises(amd._abi.OrbError):
+        amd.LocalBA().solve(bad)
+    bad = dict(pb)
+    bad["edge_pose"] = pb["edge_pose"].copy()
+    bad["edge_pose"][0] = -1
+    with pytest.raises(amd._abi.OrbError):
+        amd.LocalBA().solve(bad)
+
+
+def test_lba_coerces_field_dtypes(amd):
+    """int64 edge indices and float32 observations are converted to the header's C types."""
+    pb = _problem(amd, n_points=300, seed=6)
+    ref = amd.LocalBA().solve(pb)
+    alt = dict(pb)
+    alt["edge_point"] = pb["edge_point"].astype(np.int64)
+    alt["edge_pose"] = pb["edge_pose"].astype(np.int64)
+    got = amd.LocalBA().solve(alt)
+    assert got["iterations"] == ref["iterations"] and got["trials"] == ref["trials"]
+    assert np.array_equal(got["point_xyz"], ref["point_xyz"]) and np.array_equal(got["pose_q"], ref["pose_q"])
+
+
+def test_stop_after_rejected_trial(amd):
+    """A stop inside a trial loop that is still open (its first trial was rejected, rho < 0).
+    Near convergence the sign of rho is decided by the last bits of the chi2 sums, so such
+    rejections do not line up with the oracle's; the semantics are therefore
+    checked against the GPU's own bitwise-reproducible runs: stopped after the rejected trial,
+    the solve counts that iteration, records lambda * ni and qmax 1 for it, keeps the popped
+    estimates — bitwise those of the solve that ends just before the iteration — and the
+    earlier trace rows equal the unstopped solve's."""
+    from orb_slam2_amd import optimizer
+    pb = _problem(amd, n_local=12, n_fixed=2, n_points=1200, seed=31, outlier_frac=0.2)
+    full = amd.LocalBA().solve(pb, optimizer.options(5, 40, fixed_iterations=True))
+    qmax = full["trace"][:, 3].astype(int)
+    ks = [k for k in range(5, len(qmax)) if qmax[k] >= 2]
+    assert ks, "this problem has rejected trials in the second round"
+    k = ks[0]
+    before = int(qmax[:k].sum())
+    ctx = amd.LocalBA()
+    ctx.debug_stop_after_trials(before + 1)
+    got = ctx.solve(pb, optimizer.options(5, 40, fixed_iterations=True))
+    assert got["iterations"] == (5, k - 5 + 1) and got["trials"] == before + 1
+    assert np.array_equal(got["trace"][:k], full["trace"][:k])
+    assert got["trace"][k, 0] == full["trace"][k, 0] and got["trace"][k, 1] == full["trace"][k, 0]
+    assert got["trace"][k, 3] == 1 and got["trace"][k, 2] > full["trace"][k - 1, 2]
+    upto = amd.LocalBA().solve(pb, optimizer.options(5, k - 5, fixed_iterations=True))
+    assert np.array_equal(got["pose_q"], upto["pose_q"]) and np.array_equal(got["point_xyz"], upto["point_xyz"])
+
+
+def test_local_ba_bitwise_reproducible(amd):
+    """Every reduction of the LM pipeline has a fixed order and no two threads store the same
+    element (k_schur_pairs keeps a diagonal block's upper triangle only): repeated solves on one
+    context and on fresh contexts give bitwise identical estimates, traces and chi2."""
+    pb = _problem(amd, n_points=600, seed=6, stereo_frac=0.3)
+    ctx = amd.LocalBA()
+    runs = [ctx.solve(pb) for _ in range(3)] + [amd.LocalBA().solve(pb) for _ in range(2)]
+    for r in runs[1:]:
+        for k in ("pose_q", "pose_t", "point_xyz", "edge_chi2", "trace", "edge_erase"):
+            assert np.array_equal(r[k], runs[0][k]), k
