@@ -148,7 +148,18 @@ typedef struct {
     oracle_allreduce_fn ar;
     void* ar_user;
     int stop_after;   /* terminate() once this many trials ran (-1: off) */
+    /* OpenMP variant (oracle_lba_solve_omp): threads > 1 parallelises the loops g2o's
+     * G2O_OPENMP build parallelises (G/core/sparse_optimizer.cpp:70-71 computeActiveErrors,
+     * G/core/block_solver.hpp:528 buildSystem's edge loop, :379-380 the Schur landmark loop) plus
+     * the landmark back-substitution and point updates.  Unlike g2o (vertex locks: arrival-order sums) every sum keeps the
+     * serial order, so the variant is bitwise identical to the single-thread oracle. */
+    int threads;
+    double* eprod;    /* [n_edges][72] per-edge quadratic-form terms of the parallel buildSystem */
+    double* dbl;      /* [M][3] Dinv b_l of the parallel Schur */
+    int *pose_a_start, *pose_a;   /* per free pose index: its pt_edges positions, landmark-ascending */
 } lba_ctx;
+
+#define OMP_IF(c) if ((c)->threads > 1) num_threads((c)->threads)
 
 static void allreduce(lba_ctx* c, double* v, int n, int op)
 {
@@ -297,7 +308,7 @@ static void init_optimization(lba_ctx* c, int level)
     memset(c->pt_edge_start, 0, sizeof(int) * (c->M + 1));
     for (int k = 0; k < c->n_act; k++) c->pt_edge_start[c->point_idx[p->edge_point[c->act_edges[k]]] + 1]++;
     for (int i = 0; i < c->M; i++) c->pt_edge_start[i + 1] += c->pt_edge_start[i];
-    int* fill = (int*)malloc(sizeof(int) * (c->M + 1));
+    int* fill = (int*)malloc(sizeof(int) * (c->M + c->P + 2));
     memcpy(fill, c->pt_edge_start, sizeof(int) * (c->M + 1));
     for (int k = 0; k < c->n_act; k++) {
         const int e = c->act_edges[k];
@@ -319,6 +330,19 @@ static void init_optimization(lba_ctx* c, int level)
             a[j + 1] = v;
         }
     }
+    if (c->threads > 1) {   /* per pose row: its edge positions in landmark order (parallel Schur) */
+        memset(c->pose_a_start, 0, sizeof(int) * (c->P + 1));
+        for (int a = 0; a < c->n_act; a++) {
+            const int i1 = c->pose_idx[p->edge_pose[c->pt_edges[a]]];
+            if (i1 >= 0) c->pose_a_start[i1 + 1]++;
+        }
+        for (int i = 0; i < c->P; i++) c->pose_a_start[i + 1] += c->pose_a_start[i];
+        memcpy(fill, c->pose_a_start, sizeof(int) * (c->P + 1));
+        for (int a = 0; a < c->n_act; a++) {
+            const int i1 = c->pose_idx[p->edge_pose[c->pt_edges[a]]];
+            if (i1 >= 0) c->pose_a[fill[i1]++] = a;
+        }
+    }
     free(fill);
     free(order);
     free(pose_act);
@@ -326,6 +350,76 @@ static void init_optimization(lba_ctx* c, int level)
 }
 
 /* ------------------------------------------------------------ buildSystem */
+
+/* OpenMP buildSystem: the per-edge linearisation and quadratic-form terms in parallel
+ * (G/core/block_solver.hpp:528), then the block sums in edge order, term by term as the serial
+ * loop adds them (so every accumulator sees the same sequence of additions). */
+static void build_system_omp(lba_ctx* c)
+{
+    const lba_problem_t* p = c->p;
+#pragma omp parallel for schedule(static) OMP_IF(c)
+    for (int k = 0; k < c->n_act; k++) {
+        const int e = c->act_edges[k];
+        double A[9], B[18];
+        const int D = linearize(c, e, A, B);
+        const double w = p->edge_info[e];
+        const double* er = c->err + 3 * e;
+        double rho1 = 1.0;
+        if (c->robust[e]) {
+            const double chi = edge_chi2(c, e), d = huber_delta(c, e);
+            if (chi > d * d) rho1 = d / sqrt(chi);
+        }
+        const double W = rho1 * w;
+        double om_r[3] = {0, 0, 0};
+        for (int r = 0; r < D; r++) om_r[r] = -(w * er[r]) * rho1;
+        double* t = c->eprod + 72 * (size_t)k;   /* hl 9 | bl 3x3 | hp 36 | bp 6x3 */
+        for (int i = 0; i < 3; i++) {
+            for (int r = 0; r < 3; r++) t[9 + i * 3 + r] = r < D ? A[r * 3 + i] * om_r[r] : 0.0;
+            for (int j = 0; j < 3; j++) {
+                double s = 0;
+                for (int r = 0; r < D; r++) s += A[r * 3 + i] * W * A[r * 3 + j];
+                t[i * 3 + j] = s;
+            }
+        }
+        if (c->pose_idx[p->edge_pose[e]] >= 0) {
+            double* hpl = c->Hpl + 18 * e;
+            for (int i = 0; i < 6; i++) {
+                for (int r = 0; r < 3; r++) t[54 + i * 3 + r] = r < D ? B[r * 6 + i] * om_r[r] : 0.0;
+                for (int j = 0; j < 6; j++) {
+                    double s = 0;
+                    for (int r = 0; r < D; r++) s += B[r * 6 + i] * W * B[r * 6 + j];
+                    t[18 + i * 6 + j] = s;
+                }
+                for (int j = 0; j < 3; j++) {
+                    double s = 0;
+                    for (int r = 0; r < D; r++) s += B[r * 6 + i] * W * A[r * 3 + j];
+                    hpl[i * 3 + j] = s;
+                }
+            }
+        }
+    }
+    for (int k = 0; k < c->n_act; k++) {
+        const int e = c->act_edges[k];
+        const int D = p->edge_stereo[e] ? 3 : 2;
+        const double* t = c->eprod + 72 * (size_t)k;
+        const int li = c->point_idx[p->edge_point[e]];
+        const int pi = c->pose_idx[p->edge_pose[e]];
+        double* hl = c->Hll + 9 * li;
+        double* bl = c->bl + 3 * li;
+        for (int i = 0; i < 3; i++) {
+            for (int r = 0; r < D; r++) bl[i] += t[9 + i * 3 + r];
+            for (int j = 0; j < 3; j++) hl[i * 3 + j] += t[i * 3 + j];
+        }
+        if (pi >= 0) {
+            double* hp = c->Hpp + 36 * pi;
+            double* bp = c->bp + 6 * pi;
+            for (int i = 0; i < 6; i++) {
+                for (int r = 0; r < D; r++) bp[i] += t[54 + i * 3 + r];
+                for (int j = 0; j < 6; j++) hp[i * 6 + j] += t[18 + i * 6 + j];
+            }
+        }
+    }
+}
 
 static void build_system(lba_ctx* c)
 {
@@ -336,6 +430,10 @@ static void build_system(lba_ctx* c)
     memset(c->Hll, 0, sizeof(double) * 9 * c->M);
     memset(c->bl, 0, sizeof(double) * 3 * c->M);
     memset(c->S, 0, sizeof(double) * np * np);     /* off-diagonal pose blocks stay zero in Hpp */
+    if (c->threads > 1) {
+        build_system_omp(c);
+        return;
+    }
     for (int k = 0; k < c->n_act; k++) {
         const int e = c->act_edges[k];
         double A[9], B[18];
@@ -426,7 +524,55 @@ static int schur_solve(lba_ctx* c, double lambda)
         for (int r = 0; r < 6; r++)
             for (int q = 0; q < 6; q++) S[(6 * i + r) * np + 6 * i + q] = c->Hpp[36 * i + r * 6 + q] + (r == q ? lambda : 0.);
     double* coef = (double*)calloc(np + 1, sizeof(double));
-    for (int l = 0; l < c->M; l++) {
+    if (c->threads > 1) {
+        /* Dinv and Dinv b_l per landmark in parallel (G/core/block_solver.hpp:379-380), then the
+         * S blocks and coef by pose row i1 in parallel: each row walks the landmarks in ascending
+         * order, so every block receives its products in the serial loop's order. */
+#pragma omp parallel for schedule(static) OMP_IF(c)
+        for (int l = 0; l < c->M; l++) {
+            double D[9];
+            memcpy(D, c->Hll + 9 * l, sizeof(D));
+            D[0] += lambda; D[4] += lambda; D[8] += lambda;
+            double* Di = c->Dinv + 9 * l;
+            inv3(D, Di);
+            const double* b = c->bl + 3 * l;
+            for (int i = 0; i < 3; i++) c->dbl[3 * l + i] = Di[i * 3] * b[0] + Di[i * 3 + 1] * b[1] + Di[i * 3 + 2] * b[2];
+        }
+#pragma omp parallel for schedule(dynamic, 1) OMP_IF(c)
+        for (int row = 0; row < c->P; row++) {
+            for (int ka = c->pose_a_start[row]; ka < c->pose_a_start[row + 1]; ka++) {
+                const int a = c->pose_a[ka];
+                const int l = c->point_idx[p->edge_point[c->pt_edges[a]]];
+                const double* Di = c->Dinv + 9 * l;
+                const double* db = c->dbl + 3 * l;
+                const int s1 = c->pt_edge_start[l + 1];
+                {
+                    const int e1 = c->pt_edges[a];
+                    const int i1 = row;
+                    const double* Bi = c->Hpl + 18 * e1;
+                    double BD[18];
+                    for (int r = 0; r < 6; r++)
+                        for (int q = 0; q < 3; q++)
+                            BD[r * 3 + q] = Bi[r * 3] * Di[q] + Bi[r * 3 + 1] * Di[3 + q] + Bi[r * 3 + 2] * Di[6 + q];
+                    for (int r = 0; r < 6; r++)
+                        coef[6 * i1 + r] += Bi[r * 3] * db[0] + Bi[r * 3 + 1] * db[1] + Bi[r * 3 + 2] * db[2];
+                    for (int bb = a; bb < s1; bb++) {
+                        const int e2 = c->pt_edges[bb];
+                        const int i2 = c->pose_idx[p->edge_pose[e2]];
+                        if (i2 < 0) continue;
+                        const double* Bj = c->Hpl + 18 * e2;
+                        for (int r = 0; r < 6; r++)
+                            for (int q = 0; q < 6; q++) {
+                                const double v = BD[r * 3] * Bj[q * 3] + BD[r * 3 + 1] * Bj[q * 3 + 1] +
+                                                 BD[r * 3 + 2] * Bj[q * 3 + 2];
+                                S[(6 * i1 + r) * np + 6 * i2 + q] -= v;
+                            }
+                    }
+                }
+            }
+        }
+    }
+    for (int l = 0; l < c->M && c->threads <= 1; l++) {
         double D[9];
         memcpy(D, c->Hll + 9 * l, sizeof(D));
         D[0] += lambda; D[4] += lambda; D[8] += lambda;
@@ -499,6 +645,7 @@ static int schur_solve(lba_ctx* c, double lambda)
         for (int k = np - 1; k >= 0; k--)
             for (int i = 0; i < k; i++) xp[i] = fma(-S[k * np + i], xp[k], xp[i]);
         /* landmarks: x_l = Dinv (b_l - Hpl^T x_p) */
+#pragma omp parallel for schedule(static) OMP_IF(c)
         for (int l = 0; l < c->M; l++) {
             double cl[3] = {c->bl[3 * l], c->bl[3 * l + 1], c->bl[3 * l + 2]};
             for (int a = c->pt_edge_start[l]; a < c->pt_edge_start[l + 1]; a++) {
@@ -544,6 +691,7 @@ static void update(lba_ctx* c)
         memcpy(c->pq + 4 * i, q, sizeof(q));
         memcpy(c->pt + 3 * i, t, sizeof(t));
     }
+#pragma omp parallel for schedule(static) OMP_IF(c)
     for (int i = 0; i < p->n_points; i++) {
         const int k = c->point_idx[i];
         if (k < 0) continue;
@@ -560,6 +708,7 @@ static double active_robust_chi2(lba_ctx* c)
 }
 static void compute_active_errors(lba_ctx* c)
 {
+#pragma omp parallel for schedule(static) OMP_IF(c)
     for (int k = 0; k < c->n_act; k++) compute_error(c, c->act_edges[k]);
 }
 
@@ -644,23 +793,32 @@ static int optimize(lba_ctx* c, int iterations, const volatile uint8_t* stop, lb
 }
 
 static int lba_run(const lba_problem_t* p, const lba_options_t* o, const volatile uint8_t* stop, lba_result_t* r,
-                   int rank, int world, oracle_allreduce_fn ar, void* user, int global, int robust, int stop_after);
+                   int rank, int world, oracle_allreduce_fn ar, void* user, int global, int robust, int stop_after,
+                   int threads);
 
 int oracle_lba_solve(const lba_problem_t* p, const lba_options_t* o, const volatile uint8_t* stop, lba_result_t* r)
 {
-    return lba_run(p, o, stop, r, 0, 1, NULL, NULL, 0, 1, -1);
+    return lba_run(p, o, stop, r, 0, 1, NULL, NULL, 0, 1, -1, 1);
+}
+
+/* The OpenMP CPU path of SURVEY 8d(b): the same solve with the g2o G2O_OPENMP loops run on
+ * `threads` host threads; bitwise identical results to oracle_lba_solve. */
+int oracle_lba_solve_omp(const lba_problem_t* p, const lba_options_t* o, const volatile uint8_t* stop,
+                         lba_result_t* r, int threads)
+{
+    return lba_run(p, o, stop, r, 0, 1, NULL, NULL, 0, 1, -1, threads < 1 ? 1 : threads);
 }
 
 int oracle_lba_solve_stop_after(const lba_problem_t* p, const lba_options_t* o, int stop_after_trials,
                                 lba_result_t* r)
 {
-    return lba_run(p, o, NULL, r, 0, 1, NULL, NULL, 0, 1, stop_after_trials < 0 ? -1 : stop_after_trials);
+    return lba_run(p, o, NULL, r, 0, 1, NULL, NULL, 0, 1, stop_after_trials < 0 ? -1 : stop_after_trials, 1);
 }
 
 int oracle_lba_solve_dist(const lba_problem_t* p, const lba_options_t* o, const volatile uint8_t* stop,
                           lba_result_t* r, int rank, int world, oracle_allreduce_fn ar, void* user)
 {
-    return lba_run(p, o, stop, r, rank, world, ar, user, 0, 1, -1);
+    return lba_run(p, o, stop, r, rank, world, ar, user, 0, 1, -1, 1);
 }
 
 /* Optimizer::BundleAdjustment (R/src/Optimizer.cpp:78-277): one optimize(nIterations) = iters1
@@ -669,11 +827,12 @@ int oracle_lba_solve_dist(const lba_problem_t* p, const lba_options_t* o, const 
 int oracle_global_ba(const lba_problem_t* p, const lba_options_t* o, int robust, const volatile uint8_t* stop,
                      lba_result_t* r)
 {
-    return lba_run(p, o, stop, r, 0, 1, NULL, NULL, 1, robust, -1);
+    return lba_run(p, o, stop, r, 0, 1, NULL, NULL, 1, robust, -1, 1);
 }
 
 static int lba_run(const lba_problem_t* p, const lba_options_t* o, const volatile uint8_t* stop, lba_result_t* r,
-                   int rank, int world, oracle_allreduce_fn ar, void* user, int global, int robust, int stop_after)
+                   int rank, int world, oracle_allreduce_fn ar, void* user, int global, int robust, int stop_after,
+                   int threads)
 {
     lba_ctx c;
     memset(&c, 0, sizeof(c));
@@ -684,6 +843,7 @@ static int lba_run(const lba_problem_t* p, const lba_options_t* o, const volatil
     c.ar = ar;
     c.ar_user = user;
     c.stop_after = stop_after;
+    c.threads = threads;
     c.own0 = (int)((long long)p->n_points * rank / world);
     c.own1 = (int)((long long)p->n_points * (rank + 1) / world);
     const int NP = p->n_poses, NM = p->n_points, NE = p->n_edges;
@@ -710,6 +870,12 @@ static int lba_run(const lba_problem_t* p, const lba_options_t* o, const volatil
     c.Dinv = (double*)malloc(sizeof(double) * 9 * (NM + 1));
     c.pt_edge_start = (int*)malloc(sizeof(int) * (NM + 2));
     c.pt_edges = (int*)malloc(sizeof(int) * (NE + 1));
+    if (threads > 1) {
+        c.eprod = (double*)malloc(sizeof(double) * 72 * (NE + 1));
+        c.dbl = (double*)malloc(sizeof(double) * 3 * (NM + 1));
+        c.pose_a_start = (int*)malloc(sizeof(int) * (NP + 2));
+        c.pose_a = (int*)malloc(sizeof(int) * (NE + 1));
+    }
     memcpy(c.pq, p->pose_q, sizeof(double) * 4 * NP);
     memcpy(c.pt, p->pose_t, sizeof(double) * 3 * NP);
     memcpy(c.X, p->point_xyz, sizeof(double) * 3 * NM);
@@ -766,7 +932,8 @@ done:
     free(c.pq); free(c.pt); free(c.X); free(c.bq); free(c.bt); free(c.bX); free(c.err);
     free(c.level); free(c.robust); free(c.act_edges); free(c.pose_idx); free(c.point_idx);
     free(c.Hpp); free(c.S); free(c.bp); free(c.Hll); free(c.bl); free(c.Hpl); free(c.x); free(c.Dinv);
-    free(c.pt_edge_start); free(c.pt_edges);
+    free(c.pt_edge_start); free(c.pt_edges); free(c.eprod); free(c.dbl);
+    free(c.pose_a_start); free(c.pose_a);
     (void)cmp_i64_idx_base;
     return status;
 }

@@ -65,6 +65,10 @@ typedef struct {
  * reference returns without writing back, R/src/Optimizer.cpp:784-786). */
 int oracle_lba_solve(const lba_problem_t* p, const lba_options_t* o, const volatile uint8_t* stop,
                      lba_result_t* r);
+/* OpenMP CPU path: g2o's G2O_OPENMP loops on `threads` host threads, serial sum
+ * order kept, so the result is bitwise identical to oracle_lba_solve. */
+int oracle_lba_solve_omp(const lba_problem_t* p, const lba_options_t* o, const volatile uint8_t* stop,
+                         lba_result_t* r, int threads);
 
 /* Same, with the stop flag treated as set once the solve's LM trial count reaches stop_after_trials
  * (the test hook lba_debug_stop_after_trials of the library): terminate() is sampled after every

@@ -279,7 +279,8 @@ def global_ba(prob, n_iterations=10, robust=True, stop=False, fixed_iterations=F
     return lba_solve(prob, global_ba_options(n_iterations, fixed_iterations), stop, global_robust=int(robust))
 
 
-def lba_solve(prob, options=None, stop=False, global_robust=None, stop_after_trials=None):
+def lba_solve(prob, options=None, stop=False, global_robust=None, stop_after_trials=None, threads=None):
+    """Oracle local BA; threads=N runs the OpenMP variant (oracle_lba_solve_omp)."""
     options = options or lba_options()
     nk = len(prob["Tcw"])
     qs, ts = zip(*[quat_from_Tcw(T) for T in prob["Tcw"]])
@@ -295,7 +296,9 @@ def lba_solve(prob, options=None, stop=False, global_robust=None, stop_after_tri
     r = LbaResult(P(out["pose_q"]), P(out["pose_t"]), P(out["point_xyz"]), P(out["edge_erase"]),
                   P(out["edge_chi2"]), (C.c_int * 2)(0, 0), 0, P(out["trace"]), 0)
     flag = (C.c_uint8 * 1)(1 if stop else 0)
-    if stop_after_trials is not None:
+    if threads is not None:
+        st = lib().oracle_lba_solve_omp(C.byref(pr), C.byref(options), flag, C.byref(r), int(threads))
+    elif stop_after_trials is not None:
         st = lib().oracle_lba_solve_stop_after(C.byref(pr), C.byref(options), int(stop_after_trials), C.byref(r))
     elif global_robust is None:
         st = lib().oracle_lba_solve(C.byref(pr), C.byref(options), flag, C.byref(r))

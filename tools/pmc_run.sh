@@ -8,6 +8,6 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=$1; shift
 export TMPDIR=/tmp
 cd /tmp
-timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-trace --output-format csv -d $R/gpurun_out/pmc_$TAG -o run -- \
-    python3 $R/bench.py --no-cpu --no-lba --no-extras --steps 5 --warmup 2 $PMC_BENCH_ARGS > $R/gpurun_out/pmc_$TAG.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-trace --output-format csv -d $R/gpurun_out/pmc_$TAG -o run -- \
+    python3 $R/bench.py --no-cpu --no-lba --no-extras --no-stereo --steps 5 --warmup 2 $PMC_BENCH_ARGS > $R/gpurun_out/pmc_$TAG.log 2>&1
 echo pmc done
