@@ -623,8 +623,6 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
 // ------------------------------------------------------------------ A4: octree
 
 constexpr int OT_T = 256;
-constexpr int OT_V = 8;
-constexpr int OT_TILE = OT_T * OT_V;
 
 __device__ __forceinline__ int kx_of(uint32_t k) { return (int)(k & 0xFFFu); }
 __device__ __forceinline__ int ky_of(uint32_t k) { return (int)((k >> 12) & 0xFFFu); }
@@ -697,38 +695,16 @@ __device__ __forceinline__ int node_of(const int* start, int m, int k) {
     return lo;
 }
 
-// Packed 4 x 16-bit counters (quadrant histograms) for an intra-tile scan.
-__device__ __forceinline__ uint64_t qbit(int q) { return 1ull << (16 * q); }
-__device__ __forceinline__ int qfield(uint64_t v, int q) { return (int)((v >> (16 * q)) & 0xFFFFull); }
-
-// One tile pass of the segmented quadrant scan: returns this thread's exclusive prefix
-// (packed, tile-local) of its first key; fills tile total into *tot (all threads).
-__device__ __forceinline__ uint64_t tile_scan(uint64_t local, uint64_t* wtot, uint64_t& total) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint64_t incl = wave_incl_scan_u64(local);
-    if (lane == 63) wtot[wid] = incl;
-    __syncthreads();
-    uint64_t wofs = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < OT_T / 64; w++) {
-        const uint64_t v = wtot[w];
-        if (w < wid) wofs += v;
-        tot += v;
-    }
-    total = tot;
-    __syncthreads();
-    return wofs + incl - local;
-}
-
 struct OctScratch {
-    uint4* P0;      // [cap+1] prefix of active-key quadrant counts at node starts
-    int* ne;        // nonempty children of a processed node
+    uint4* qc;      // [cap+1] per node: key counts of the four children (n1, n2, n3, n4)
+    int* ne;        // nonempty children of a processed node (-1: not split this pass)
     int* push;      // push base of a processed node
     int* newpos;    // new list position of an unprocessed node
-    int* rank;      // processing rank
+    int* rank;      // processing rank (final phase)
     int* order;     // node at rank
     int* proc;      // processed flag
     int* tmp;       // scan scratch
+    long long* rk;  // [cap] final-phase sort key (count, creation sequence); -1 = not a candidate
 };
 
 struct OctCtx {          // LDS carve-up shared by both key-storage variants
@@ -750,148 +726,118 @@ struct OctCtx {          // LDS carve-up shared by both key-storage variants
 };
 
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) unsigned long long lds_u64;
 
-// DistributeOctTree on n keys held in kA (kB: scratch of the same size); KP is the key
-// storage: LDS (lds_u32, the common case) or global memory for very dense levels.
+__device__ __forceinline__ int quad_field(const uint4& c, int q) {
+    return q == 0 ? (int)c.x : q == 1 ? (int)c.y : q == 2 ? (int)c.z : (int)c.w;
+}
+__device__ __forceinline__ unsigned nonempty_mask(const uint4& c) {
+    return (unsigned)(c.x != 0) | ((unsigned)(c.y != 0) << 1) | ((unsigned)(c.z != 0) << 2) | ((unsigned)(c.w != 0) << 3);
+}
+
+// DistributeOctTree (R/src/ORBextractor.cpp:571-817) on n keys held in kA, in place: keys never
+// move; each key carries the list index of the node that holds it (nid, same storage as kA: LDS
+// for the common levels, global memory for very dense ones).  The std::list is emulated at node
+// level (ping-pong SoA tables in list order); a pass is
+//   1. each key of an active node adds itself to its child quadrant's count (LDS atomics),
+//   2. per node: nonempty children, processing order (list order in the breadth-wise passes;
+//      (count, creation sequence) descending in the final size-ordered phase, :736), push_front
+//      positions, new positions of the nodes left in place,
+//   3. each key takes its new node index (child of its node, or the node's new position).
+// Within a node the reference keeps vToDistributeKeys order (every DivideNode partition is
+// stable), so "first maximum wins" (:796-814) is the maximum response at the smallest original
+// index: one 64-bit LDS atomicMax of (response, ~index) per node.
 template <typename KP>
-__device__ __forceinline__ void octree_run(const Geom& g, const LevelGeom& L, int l, int b, int n, KP* kA, KP* kB, const OctCtx& C_,
-                           OctScratch& S, uint64_t* wtot, int* wsum, int* sc, uint4* carry_s, uint32_t* outK,
-                           int* outCount, int* status) {
+__device__ __forceinline__ void octree_run(const Geom& g, const LevelGeom& L, int l, int b, int n, const KP* kA, KP* nid,
+                                           const OctCtx& C_, OctScratch& S, int* wsum, int* sc, lds_u64* best,
+                                           uint32_t* outK, int* outCount, int* status) {
     const int tid = threadIdx.x;
     const int cap = C_.cap;
-    (void)cap;
     TSTAMP(t_begin);
-    long long tB = 0, tN = 0, tO0 = 0, tO1 = 0, tF = 0, tC = 0;
+    long long tK = 0, tN = 0, tO0 = 0, tO1 = 0, tF = 0, tU = 0;
     int np0 = 0, np1 = 0;
-    (void)tB; (void)tN; (void)tO0; (void)tO1; (void)tF; (void)tC; (void)np0; (void)np1;
-    // ---- initial nodes (R/src/ORBextractor.cpp:577-627): stable partition by x / hX
+    (void)tK; (void)tN; (void)tO0; (void)tO1; (void)tF; (void)tU; (void)np0; (void)np1; (void)l; (void)b;
+    // ---- initial nodes (:577-627): part = x / hX; nodes pushed back in part order, empty ones erased
     const int nIni = L.nIni;
     const float hX = L.hX;
     const int H = L.maxBY - kMinBorder;
-    if (tid == 0) sc[0] = 0;
+    for (int i = tid; i < nIni; i += OT_T) S.tmp[i] = 0;
     __syncthreads();
-    {
+    for (int k = tid; k < n; k += OT_T) atomicAdd(&S.tmp[min((int)((float)kx_of(kA[k]) / hX), nIni - 1)], 1);
+    __syncthreads();
+    if (tid == 0) {
         const NodeTab T0 = C_.tab(0);
-        int base = 0;
+        int idx = 0;
         for (int part = 0; part < nIni; part++) {
-            int partCount = 0;
-            for (int t0 = 0; t0 < n; t0 += OT_TILE) {
-                const int k0 = t0 + tid * OT_V;
-                int local = 0;
-                uint32_t kk[OT_V];
-#pragma unroll
-                for (int v = 0; v < OT_V; v++) {
-                    const int k = k0 + v;
-                    kk[v] = k < n ? kA[k] : 0u;
-                    if (k < n && (int)((float)kx_of(kk[v]) / hX) == part) local++;
-                }
-                uint64_t tot;
-                int run = base + partCount + (int)tile_scan((uint64_t)local, wtot, tot);
-#pragma unroll
-                for (int v = 0; v < OT_V; v++) {
-                    const int k = k0 + v;
-                    if (k < n && (int)((float)kx_of(kk[v]) / hX) == part) kB[run++] = kk[v];
-                }
-                partCount += (int)tot;
-            }
-            // nodes are pushed back in part order; empty initial nodes are erased
-            if (partCount > 0 && tid == 0) {
-                const int idx = sc[0];
-                T0.start[idx] = base;
-                T0.cnt[idx] = partCount;
-                const int x0 = (int)(hX * (float)part), x1 = (int)(hX * (float)(part + 1));
-                T0.b0[idx] = (uint32_t)x0;
-                T0.b1[idx] = (uint32_t)x1 | ((uint32_t)H << 16);
-                T0.seq[idx] = idx;
-                T0.flag[idx] = partCount == 1 ? 1 : 0;
-                sc[0] = idx + 1;
-            }
-            base += partCount;
-            __syncthreads();
+            const int c = S.tmp[part];
+            S.newpos[part] = idx;
+            if (c == 0) continue;
+            T0.cnt[idx] = c;
+            T0.b0[idx] = (uint32_t)(int)(hX * (float)part);
+            T0.b1[idx] = (uint32_t)(int)(hX * (float)(part + 1)) | ((uint32_t)H << 16);
+            T0.seq[idx] = idx;
+            T0.flag[idx] = c == 1 ? 1 : 0;
+            idx++;
         }
+        sc[0] = idx;
     }
-    TSTAMP(t_init);
-    int m = sc[0];  // list size (uniform)
     __syncthreads();
-    {   // keys now live in kB
-        KP* t = kA; kA = kB; kB = t;
-    }
-    int cur = 0;            // table holding the current list
-    int phase = 0;          // 0 = outer pass, 1 = inner (size-ordered) pass
+    for (int k = tid; k < n; k += OT_T) nid[k] = (uint32_t)S.newpos[min((int)((float)kx_of(kA[k]) / hX), nIni - 1)];
+    TSTAMP(t_init);
+    int m = sc[0];   // list size (uniform)
+    __syncthreads();
+    int cur = 0;     // table holding the current list
+    int phase = 0;   // 0 = breadth-wise passes, 1 = size-ordered passes
     int nIter = 0;
+    constexpr int KV = 8;   // keys per thread whose (node, quadrant) stay in registers across a pass
     while (true) {
         if (++nIter > 4096) { if (tid == 0) atomicOr(status, 4); break; }
         const NodeTab O = C_.tab(cur);
         const NodeTab Nw = C_.tab(cur ^ 1);
         const int prevSize = m;
-        // active flags: outer -> every node with >1 keys (== !bNoMore); inner -> candidates
-        // Pass B: quadrant prefix at node starts
-        TSTAMP(t_pb);
 #ifdef ORB_TIMING
         if (phase == 0) np0++; else np1++;
 #endif
-        if (tid == 0) *carry_s = make_uint4(0, 0, 0, 0);
+        TSTAMP(t_k);
+        // 1. child counts of the active nodes (outer pass: every node with > 1 keys, i.e.
+        //    !bNoMore; final phase: the candidates, i.e. children created with > 1 keys)
+        for (int i = tid; i < m; i += OT_T) S.qc[i] = make_uint4(0, 0, 0, 0);
         __syncthreads();
-        for (int t0 = 0; t0 < n; t0 += OT_TILE) {
-            const int k0 = t0 + tid * OT_V;
-            uint64_t local = 0;
-            int qv[OT_V];
-            int nd = k0 < n ? node_of(O.start, m, k0) : 0;
-            int ndv[OT_V];
+        int ndr[KV];
+        uint32_t qr = 0;   // 2 bits per cached key; bit 16 + v: active
 #pragma unroll
-            for (int v = 0; v < OT_V; v++) {
-                const int k = k0 + v;
-                qv[v] = -1;
-                ndv[v] = nd;
-                if (k < n) {
-                    while (nd + 1 < m && O.start[nd + 1] <= k) nd++;
-                    ndv[v] = nd;
-                    const bool act = phase == 0 ? (O.cnt[nd] > 1) : ((O.flag[nd] & 2) != 0);
-                    if (act) {
-                        int mx, my;
-                        node_split(O.b0[nd], O.b1[nd], mx, my);
-                        qv[v] = key_quadrant(kA[k], mx, my);
-                        local += qbit(qv[v]);
-                    }
+        for (int v = 0; v < KV; v++) {
+            const int k = v * OT_T + tid;
+            ndr[v] = 0;
+            if (k < n) {
+                const int nd = (int)nid[k];
+                ndr[v] = nd;
+                const bool act = phase == 0 ? (O.cnt[nd] > 1) : ((O.flag[nd] & 2) != 0);
+                if (act) {
+                    int mx, my;
+                    node_split(O.b0[nd], O.b1[nd], mx, my);
+                    const int q = key_quadrant(kA[k], mx, my);
+                    qr |= ((uint32_t)q << (2 * v)) | (1u << (16 + v));
+                    atomicAdd(reinterpret_cast<unsigned*>(&S.qc[nd]) + q, 1u);
                 }
             }
-            uint64_t tot;
-            const uint64_t ex = tile_scan(local, wtot, tot);
-            const uint4 carry = *carry_s;
-            uint4 R = make_uint4(carry.x + qfield(ex, 0), carry.y + qfield(ex, 1), carry.z + qfield(ex, 2),
-                                 carry.w + qfield(ex, 3));
-#pragma unroll
-            for (int v = 0; v < OT_V; v++) {
-                const int k = k0 + v;
-                if (k < n) {
-                    if (O.start[ndv[v]] == k) S.P0[ndv[v]] = R;
-                    if (qv[v] == 0) R.x++;
-                    else if (qv[v] == 1) R.y++;
-                    else if (qv[v] == 2) R.z++;
-                    else if (qv[v] == 3) R.w++;
-                }
-            }
-            __syncthreads();
-            if (tid == 0) {
-                uint4 c2 = carry;
-                c2.x += qfield(tot, 0); c2.y += qfield(tot, 1); c2.z += qfield(tot, 2); c2.w += qfield(tot, 3);
-                *carry_s = c2;
-            }
-            __syncthreads();
         }
-        if (tid == 0) S.P0[m] = *carry_s;
+        for (int k = KV * OT_T + tid; k < n; k += OT_T) {
+            const int nd = (int)nid[k];
+            const bool act = phase == 0 ? (O.cnt[nd] > 1) : ((O.flag[nd] & 2) != 0);
+            if (act) {
+                int mx, my;
+                node_split(O.b0[nd], O.b1[nd], mx, my);
+                atomicAdd(reinterpret_cast<unsigned*>(&S.qc[nd]) + key_quadrant(kA[k], mx, my), 1u);
+            }
+        }
         __syncthreads();
-        TACC(tB, t_pb);
+        TACC(tK, t_k);
         TSTAMP(t_nl);
-        // node level: child counts, ne, active
+        // 2. node level: nonempty children of the active nodes
         for (int i = tid; i < m; i += OT_T) {
             const bool act = phase == 0 ? (O.cnt[i] > 1) : ((O.flag[i] & 2) != 0);
-            int ne = 0;
-            if (act) {
-                const uint4 a = S.P0[i], c = S.P0[i + 1];
-                ne = (c.x != a.x) + (c.y != a.y) + (c.z != a.z) + (c.w != a.w);
-            }
-            S.ne[i] = act ? ne : -1;
+            S.ne[i] = act ? __popc(nonempty_mask(S.qc[i])) : -1;
         }
         __syncthreads();
         TACC(tN, t_nl);
@@ -908,22 +854,25 @@ __device__ __forceinline__ void octree_run(const Geom& g, const LevelGeom& L, in
             if (tid == 0) sc[1] = C;
             __syncthreads();
         } else {
-            // rank = number of candidates ordered after (count, seq) descending
-            for (int i = tid; i < m; i += OT_T) {
-                if (S.ne[i] < 0) { S.rank[i] = -1; continue; }
-                const int ci = O.cnt[i], si = O.seq[i];
-                int r = 0;
-                for (int j2 = 0; j2 < m; j2++) {
-                    if (S.ne[j2] < 0) continue;
-                    const int cj = O.cnt[j2], sj = O.seq[j2];
-                    if (cj > ci || (cj == ci && sj > si)) r++;
-                }
-                S.rank[i] = r;
-                S.order[r] = i;
-            }
+            // candidates sorted by (size, pointer) ascending and split from the back (:736-739):
+            // rank = number of candidates with a larger (count, creation sequence)
+            for (int i = tid; i < m; i += OT_T)
+                S.rk[i] = S.ne[i] < 0 ? -1ll : (((long long)O.cnt[i] << 24) | (long long)O.seq[i]);
             if (tid == 0) sc[2] = 0;
             __syncthreads();
-            for (int i = tid; i < m; i += OT_T) if (S.ne[i] >= 0) atomicAdd(&sc[2], 1);
+            for (int i = tid; i < m; i += OT_T) {
+                const long long ki = S.rk[i];
+                if (ki < 0) { S.rank[i] = -1; continue; }
+                int r = 0, j2 = 0;
+                for (; j2 + 8 <= m; j2 += 8) {
+#pragma unroll
+                    for (int u = 0; u < 8; u++) r += S.rk[j2 + u] > ki ? 1 : 0;
+                }
+                for (; j2 < m; j2++) r += S.rk[j2] > ki ? 1 : 0;
+                S.rank[i] = r;
+                S.order[r] = i;
+                atomicAdd(&sc[2], 1);
+            }
             __syncthreads();
             const int nc = sc[2];
             for (int r = tid; r < nc; r += OT_T) S.tmp[r] = S.ne[S.order[r]];
@@ -931,6 +880,7 @@ __device__ __forceinline__ void octree_run(const Geom& g, const LevelGeom& L, in
             block_scan_lds(S.tmp, nc, wsum);
             if (tid == 0) sc[3] = 0x7fffffff;
             __syncthreads();
+            // the loop stops after the first split that brings the list to N nodes (:783-784)
             for (int r = tid; r < nc; r += OT_T) {
                 const int i = S.order[r];
                 S.push[i] = S.tmp[r];
@@ -956,7 +906,7 @@ __device__ __forceinline__ void octree_run(const Geom& g, const LevelGeom& L, in
         if (phase == 0) { TACC(tO0, t_or); } else { TACC(tO1, t_or); }
         TSTAMP(t_fi);
         const int C = sc[1];
-        // new positions of unprocessed nodes
+        // new positions of the nodes left in place (they follow the C pushed children)
         for (int i = tid; i < m; i += OT_T) S.tmp[i] = S.proc[i] ? 0 : 1;
         __syncthreads();
         const int nUnproc = block_scan_lds(S.tmp, m, wsum);
@@ -966,10 +916,9 @@ __device__ __forceinline__ void octree_run(const Geom& g, const LevelGeom& L, in
             break;
         }
         for (int i = tid; i < m; i += OT_T) S.newpos[i] = S.proc[i] ? -1 : C + S.tmp[i];
-        __syncthreads();
-        // fill the new table
         if (tid == 0) sc[4] = 0;
         __syncthreads();
+        // fill the new table: children of a processed node at C-1-(push + r) (push_front order)
         for (int i = tid; i < m; i += OT_T) {
             if (!S.proc[i]) {
                 const int j2 = S.newpos[i];
@@ -979,99 +928,61 @@ __device__ __forceinline__ void octree_run(const Geom& g, const LevelGeom& L, in
                 Nw.seq[j2] = 0;
                 Nw.flag[j2] = O.cnt[i] == 1 ? 1 : 0;
             } else {
-                const uint4 a = S.P0[i], c = S.P0[i + 1];
-                const int cc[4] = {(int)(c.x - a.x), (int)(c.y - a.y), (int)(c.z - a.z), (int)(c.w - a.w)};
+                const uint4 cq = S.qc[i];
                 int r = 0;
                 for (int q = 0; q < 4; q++) {
-                    if (cc[q] == 0) continue;
+                    const int cc = quad_field(cq, q);
+                    if (cc == 0) continue;
                     const int push = S.push[i] + r;
                     const int j2 = C - 1 - push;
                     uint32_t c0, c1;
                     child_bounds(O.b0[i], O.b1[i], q, c0, c1);
-                    Nw.cnt[j2] = cc[q];
+                    Nw.cnt[j2] = cc;
                     Nw.b0[j2] = c0;
                     Nw.b1[j2] = c1;
                     Nw.seq[j2] = push;
-                    Nw.flag[j2] = cc[q] == 1 ? 1 : 2;
-                    if (cc[q] > 1) atomicAdd(&sc[4], 1);
+                    Nw.flag[j2] = cc == 1 ? 1 : 2;
+                    if (cc > 1) atomicAdd(&sc[4], 1);
                     r++;
                 }
             }
         }
-        __syncthreads();
-        const int nToExpand = sc[4];
-        for (int i = tid; i < newM; i += OT_T) Nw.start[i] = Nw.cnt[i];
-        __syncthreads();
-        block_scan_lds(Nw.start, newM, wsum);
-        if (tid == 0) Nw.start[newM] = n;
-        __syncthreads();
         TACC(tF, t_fi);
-        TSTAMP(t_pc);
-        // Pass C: move keys (stable within every child / unprocessed node)
-        if (tid == 0) *carry_s = make_uint4(0, 0, 0, 0);
-        __syncthreads();
-        for (int t0 = 0; t0 < n; t0 += OT_TILE) {
-            const int k0 = t0 + tid * OT_V;
-            uint64_t local = 0;
-            int qv[OT_V], ndv[OT_V];
-            uint32_t kk[OT_V];
-            int nd = k0 < n ? node_of(O.start, m, k0) : 0;
+        TSTAMP(t_u);
+        // 3. every key takes its node's new index
 #pragma unroll
-            for (int v = 0; v < OT_V; v++) {
-                const int k = k0 + v;
-                qv[v] = -1;
-                ndv[v] = nd;
-                kk[v] = 0;
-                if (k < n) {
-                    while (nd + 1 < m && O.start[nd + 1] <= k) nd++;
-                    ndv[v] = nd;
-                    kk[v] = kA[k];
-                    if (S.ne[nd] >= 0) {
-                        int mx, my;
-                        node_split(O.b0[nd], O.b1[nd], mx, my);
-                        qv[v] = key_quadrant(kk[v], mx, my);
-                        local += qbit(qv[v]);
-                    }
-                }
-            }
-            uint64_t tot;
-            const uint64_t ex = tile_scan(local, wtot, tot);
-            const uint4 carry = *carry_s;
-            uint4 R = make_uint4(carry.x + qfield(ex, 0), carry.y + qfield(ex, 1), carry.z + qfield(ex, 2),
-                                 carry.w + qfield(ex, 3));
-#pragma unroll
-            for (int v = 0; v < OT_V; v++) {
-                const int k = k0 + v;
-                if (k >= n) continue;
-                const int i = ndv[v];
-                const int q = qv[v];
-                if (S.proc[i]) {
-                    const uint4 a = S.P0[i], c = S.P0[i + 1];
-                    // rank of child q among the non-empty children (n1..n4 order)
-                    const unsigned ne = (unsigned)(c.x != a.x) | ((unsigned)(c.y != a.y) << 1) |
-                                        ((unsigned)(c.z != a.z) << 2) | ((unsigned)(c.w != a.w) << 3);
-                    const unsigned rq = q == 0 ? R.x - a.x : q == 1 ? R.y - a.y : q == 2 ? R.z - a.z : R.w - a.w;
-                    const int r = __popc(ne & ((1u << q) - 1u));
-                    const int j2 = C - 1 - (S.push[i] + r);
-                    kB[Nw.start[j2] + (int)rq] = kk[v];
+        for (int v = 0; v < KV; v++) {
+            const int k = v * OT_T + tid;
+            if (k < n) {
+                const int nd = ndr[v];
+                int nn;
+                if (S.proc[nd] && ((qr >> (16 + v)) & 1u)) {
+                    const int q = (int)((qr >> (2 * v)) & 3u);
+                    const int r = __popc(nonempty_mask(S.qc[nd]) & ((1u << q) - 1u));
+                    nn = C - 1 - (S.push[nd] + r);
                 } else {
-                    kB[Nw.start[S.newpos[i]] + (k - O.start[i])] = kk[v];
+                    nn = S.newpos[nd];
                 }
-                if (q == 0) R.x++;
-                else if (q == 1) R.y++;
-                else if (q == 2) R.z++;
-                else if (q == 3) R.w++;
+                nid[k] = (uint32_t)nn;
             }
-            __syncthreads();
-            if (tid == 0) {
-                uint4 c2 = carry;
-                c2.x += qfield(tot, 0); c2.y += qfield(tot, 1); c2.z += qfield(tot, 2); c2.w += qfield(tot, 3);
-                *carry_s = c2;
-            }
-            __syncthreads();
         }
-        TACC(tC, t_pc);
-        { KP* t = kA; kA = kB; kB = t; }
+        for (int k = KV * OT_T + tid; k < n; k += OT_T) {
+            const int nd = (int)nid[k];
+            int nn;
+            if (S.proc[nd]) {
+                int mx, my;
+                node_split(O.b0[nd], O.b1[nd], mx, my);
+                const int q = key_quadrant(kA[k], mx, my);
+                const int r = __popc(nonempty_mask(S.qc[nd]) & ((1u << q) - 1u));
+                nn = C - 1 - (S.push[nd] + r);
+            } else {
+                nn = S.newpos[nd];
+            }
+            nid[k] = (uint32_t)nn;
+        }
+        __syncthreads();
+        TACC(tU, t_u);
+        const int nToExpand = sc[4];
         cur ^= 1;
         m = newM;
         // termination logic of R/src/ORBextractor.cpp:722-791
@@ -1083,15 +994,16 @@ __device__ __forceinline__ void octree_run(const Geom& g, const LevelGeom& L, in
     }
     __syncthreads();
     // retain the best point in each node (first max wins, R/src/ORBextractor.cpp:796-814)
-    const NodeTab F = C_.tab(cur);
+    for (int i = tid; i < m; i += OT_T) best[i] = 0ull;
+    __syncthreads();
+    for (int k = tid; k < n; k += OT_T) {
+        const unsigned long long v = ((unsigned long long)kr_of(kA[k]) << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)k);
+        __hip_atomic_fetch_max(&best[(int)nid[k]], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __syncthreads();
     for (int i = tid; i < m; i += OT_T) {
-        const int s0 = F.start[i], s1 = s0 + F.cnt[i];
-        uint32_t best = kA[s0];
-        for (int k = s0 + 1; k < s1; k++) {
-            const uint32_t v = kA[k];
-            if (kr_of(v) > kr_of(best)) best = v;
-        }
-        if (i < L.nodeCap) outK[i] = best;
+        const uint32_t k = 0xFFFFFFFFu - (uint32_t)(best[i] & 0xFFFFFFFFull);
+        if (i < L.nodeCap) outK[i] = kA[k];
     }
     if (tid == 0) {
         if (m > L.nodeCap) atomicOr(status, 16);
@@ -1099,8 +1011,8 @@ __device__ __forceinline__ void octree_run(const Geom& g, const LevelGeom& L, in
     }
 #ifdef ORB_TIMING
     if (tid == 0 && b == 0 && (l == 0 || l == 7))
-        printf("octree l%d n %d m %d: init %lld passes %d+%d B %lld N %lld O0 %lld O1 %lld F %lld C %lld total %lld\n", l, n, m,
-               t_init - t_begin, np0, np1, tB, tN, tO0, tO1, tF, tC, clock64() - t_begin);
+        printf("octree l%d n %d m %d: init %lld passes %d+%d K %lld N %lld O0 %lld O1 %lld F %lld U %lld total %lld\n", l, n,
+               m, t_init - t_begin, np0, np1, tK, tN, tO0, tO1, tF, tU, clock64() - t_begin);
 #endif
 }
 
@@ -1117,7 +1029,7 @@ __global__ __launch_bounds__(OT_T) void k_octree(Geom g, const uint32_t* __restr
     unsigned char* p = smem;
     auto carve = [&](size_t bytes) { unsigned char* r = p; p += (bytes + 15) & ~(size_t)15; return r; };
     OctScratch S;
-    S.P0 = (uint4*)carve(sizeof(uint4) * (cap + 1));
+    S.qc = (uint4*)carve(sizeof(uint4) * (cap + 1));
     OctCtx C_;
     C_.cap = cap;
     C_.tabStride = ((4 * (size_t)(cap + 1) + 15) & ~(size_t)15) + 5 * ((4 * (size_t)cap + 15) & ~(size_t)15);
@@ -1129,12 +1041,12 @@ __global__ __launch_bounds__(OT_T) void k_octree(Geom g, const uint32_t* __restr
     S.order = (int*)carve(sizeof(int) * cap);
     S.proc = (int*)carve(sizeof(int) * cap);
     S.tmp = (int*)carve(sizeof(int) * (cap + 1));
+    S.rk = (long long*)carve(sizeof(long long) * cap);
+    lds_u64* best = (lds_u64*)carve(sizeof(unsigned long long) * cap);
     int* cellOff = (int*)carve(sizeof(int) * (L.nCols * L.nRows + 1 + 64));
-    uint64_t* wtot = (uint64_t*)carve(sizeof(uint64_t) * 8);
     int* wsum = (int*)carve(sizeof(int) * 8);
     int* sc = (int*)carve(sizeof(int) * 32);    // uniform scalars
-    uint4* carry_s = (uint4*)carve(sizeof(uint4));
-    lds_u32* keysL = (lds_u32*)carve(sizeof(uint32_t) * ldsKeyCap);   // LDS ping-pong key buffers
+    lds_u32* keysL = (lds_u32*)carve(sizeof(uint32_t) * ldsKeyCap);   // LDS keys + node ids
 
     const size_t kbase = (size_t)b * g.slotsPerFrame + L.slotBase;
     const int ncell = L.nCols * L.nRows;
@@ -1183,10 +1095,9 @@ __global__ __launch_bounds__(OT_T) void k_octree(Geom g, const uint32_t* __restr
     }
     __syncthreads();
     if (inLds)
-        octree_run<lds_u32>(g, L, l, b, n, keysL, keysL + n, C_, S, wtot, wsum, sc, carry_s, outK, outCount, status);
+        octree_run<lds_u32>(g, L, l, b, n, keysL, keysL + n, C_, S, wsum, sc, best, outK, outCount, status);
     else
-        octree_run<uint32_t>(g, L, l, b, n, keyA + kbase, keyB + kbase, C_, S, wtot, wsum, sc, carry_s, outK,
-                             outCount, status);
+        octree_run<uint32_t>(g, L, l, b, n, keyA + kbase, keyB + kbase, C_, S, wsum, sc, best, outK, outCount, status);
 }
 
 // ------------------------------------------------------------------ A6: blur
@@ -1879,10 +1790,11 @@ static size_t octree_lds_bytes(const Geom& g) {
     size_t s = r16(sizeof(uint4) * (cap + 1));
     s += 2 * (r16(4 * (cap + 1)) + 5 * r16(4 * cap));
     s += 6 * r16(4 * cap) + r16(4 * (cap + 1));
+    s += 2 * r16(8 * cap);
     int maxCells = 0;
     for (int l = 0; l < g.nlevels; l++) maxCells = std::max(maxCells, g.lv[l].nCols * g.lv[l].nRows);
     s += r16(4 * (maxCells + 1 + 64));
-    s += r16(8 * 8) + r16(4 * 8) + r16(4 * 32) + r16(16);
+    s += r16(4 * 8) + r16(4 * 32);
     return s;
 }
 
