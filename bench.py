@@ -59,6 +59,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=128, help="frames per step per GPU")
     ap.add_argument("--streams", type=int, default=2,
                     help="independent frame sequences per GPU, each on its own HIP stream (batch split)")
+    ap.add_argument("--match-stream", action="store_true",
+                    help="SearchForInitialization on a second stream per sequence, overlapping the next step's "
+                         "extraction (measured slower than the single-stream chain on MI355X)")
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--nfeatures", type=int, default=1000)
@@ -826,40 +829,66 @@ def main():
     Bs = B // S
 
     class Pipe:
-        """One frame sequence: its own extractor / matcher handles, buffers and HIP stream, so
-        the latency-bound stages of one sequence overlap the others on the GPU."""
+        """One frame sequence: its own extractor / matcher handles, buffers and HIP streams, so
+        the latency-bound stages of one sequence overlap the others on the GPU.  Extraction and
+        matching run on two streams of their own (a two-stage software pipeline over steps):
+        SearchForInitialization of step s (match stream) overlaps the extraction of step s+1
+        (extract stream).  Keypoint buffers are double-buffered by step parity; row 0 of a buffer
+        holds the previous step's last frame (pair t-1, t across step boundaries), copied on the
+        match stream, and the extraction that next overwrites the other buffer waits for that
+        copy."""
 
         def __init__(self, k):
             self.k = k
             self.ts = torch.cuda.Stream(dev)
-            self.stream = self.ts.cuda_stream
+            self.tm = torch.cuda.Stream(dev) if args.match_stream else self.ts
+            self.stream, self.mstream = self.ts.cuda_stream, self.tm.cuda_stream
             self.ex = amd.ORBextractor(NF, 1.2, 8, 20, 7, device=local, max_w=W, max_h=H, max_batch=Bs)
             self.m = amd.ORBmatcher(0.9, True, device=local)
-            # frame slot 0 holds the previous step's last frame (pair t-1, t across step boundaries)
-            self.kps = torch.zeros((Bs + 1, cap, 7), dtype=torch.int32, device=dev)
-            self.desc = torch.zeros((Bs + 1, cap, 32), dtype=torch.uint8, device=dev)
-            self.counts = torch.zeros(Bs + 1, dtype=torch.int32, device=dev)
+            nb = 2 if args.match_stream else 1
+            self.kps = [torch.zeros((Bs + 1, cap, 7), dtype=torch.int32, device=dev) for _ in range(nb)]
+            self.desc = [torch.zeros((Bs + 1, cap, 32), dtype=torch.uint8, device=dev) for _ in range(nb)]
+            self.counts = [torch.zeros(Bs + 1, dtype=torch.int32, device=dev) for _ in range(nb)]
             self.m12 = torch.zeros((Bs, cap), dtype=torch.int32, device=dev)
             self.nm = torch.zeros(Bs, dtype=torch.int32, device=dev)
+            self.ev_ext = [torch.cuda.Event() for _ in range(2)]
+            self.ev_copy = [torch.cuda.Event() for _ in range(2)]
+            self.copy_pending = None
+            self.last = 0
 
         def step(self, s):
             n_pool = pool.shape[0]
             start = (s * B + self.k * Bs) % (n_pool - Bs + 1)
             imgs = pool[start:start + Bs]
-            with torch.cuda.stream(self.ts):
-                self.kps[0].copy_(self.kps[Bs])
-                self.desc[0].copy_(self.desc[Bs])
-                self.counts[0:1].copy_(self.counts[Bs:Bs + 1])
-            kps, desc, counts = self.kps, self.desc, self.counts
+            nb = len(self.kps)
+            cur, prv = s % nb, (s - 1) % nb
+            kps, desc, counts = self.kps[cur], self.desc[cur], self.counts[cur]
+            if nb == 1:                            # one buffer: carry the last frame before overwriting
+                with torch.cuda.stream(self.ts):
+                    kps[0].copy_(kps[Bs])
+                    desc[0].copy_(desc[Bs])
+                    counts[0:1].copy_(counts[Bs:Bs + 1])
+            if self.copy_pending is not None:      # the previous step's match stream copied row Bs out
+                self.ts.wait_event(self.copy_pending)
             _abi.check("orb_extract_batch_device", lib.orb_extract_batch_device(
                 self.ex._h, C.c_void_p(imgs.data_ptr()), H * W, Bs, W, H, C.c_void_p(kps.data_ptr() + row_kp),
                 C.c_void_p(desc.data_ptr() + row_d), cap, C.c_void_p(counts.data_ptr() + 4),
                 C.c_void_p(self.stream)))
+            if nb == 2:
+                self.ev_ext[s % 2].record(self.ts)
+                self.tm.wait_event(self.ev_ext[s % 2])
+                with torch.cuda.stream(self.tm):
+                    kps[0].copy_(self.kps[prv][Bs])
+                    desc[0].copy_(self.desc[prv][Bs])
+                    counts[0:1].copy_(self.counts[prv][Bs:Bs + 1])
+                self.ev_copy[s % 2].record(self.tm)
+                self.copy_pending = self.ev_copy[s % 2]
             _abi.check("orb_search_for_initialization_batch_device", lib.orb_search_for_initialization_batch_device(
                 self.m._h, C.c_void_p(kps.data_ptr()), C.c_void_p(desc.data_ptr()), C.c_void_p(counts.data_ptr()),
                 C.c_void_p(kps.data_ptr() + row_kp), C.c_void_p(desc.data_ptr() + row_d),
                 C.c_void_p(counts.data_ptr() + 4), Bs, cap, W, H, 100, C.c_void_p(self.m12.data_ptr()),
-                C.c_void_p(self.nm.data_ptr()), C.c_void_p(self.stream)))
+                C.c_void_p(self.nm.data_ptr()), C.c_void_p(self.mstream)))
+            self.last = cur
 
     ex0 = amd.ORBextractor(NF, 1.2, 8, 20, 7, device=local, max_w=W, max_h=H, max_batch=1)
     lw, lh, cells = (np.zeros(8, np.int32) for _ in range(3))
@@ -912,7 +941,7 @@ def main():
             ncalls.value += nc.value
     frames_total = B * args.steps * world
     value = frames_total / dt
-    cnt = torch.cat([p.counts[1:] for p in pipes]).cpu().numpy()
+    cnt = torch.cat([p.counts[p.last][1:] for p in pipes]).cpu().numpy()
     nmatch = torch.cat([p.nm for p in pipes]).cpu().numpy()
 
     result = {
@@ -934,7 +963,9 @@ def main():
         "config": {"workload": f"synthetic {W}x{H} grayscale stream, {NF} feat/frame, 8 levels, scale 1.2, "
                                f"FAST 20/7; extract + SearchForInitialization(t-1,t; window 100, nnratio 0.9, "
                                f"checkOri) per frame; {B} frames per step per GPU as {S} independent "
-                               f"sequences on {S} HIP streams, HBM-resident",
+                               f"sequences, each on an extraction and a matching HIP stream"
+                               f"{' (matching of step s overlaps extraction of step s+1)' if args.match_stream else ''}"
+                               f", HBM-resident",
                    "batch_per_gpu": B, "streams_per_gpu": S, "width": W, "height": H, "nfeatures": NF,
                    "parallelism": f"frame-sharded x{world}"},
         "keypoints_per_frame": float(np.mean(cnt)),

@@ -27,6 +27,7 @@ constexpr int kGridRows = 48;    // FRAME_GRID_ROWS
 constexpr int kHisto = 30;       // HISTO_LENGTH
 constexpr int kThLow = 50;       // TH_LOW
 constexpr int kThHigh = 100;     // TH_HIGH
+constexpr size_t kMaxLds = 160 * 1024;   // LDS of one gfx950 workgroup
 constexpr int kMaxCand = 1024;   // per-query candidate list capacity (overflow -> status)
 
 struct GridParams {
@@ -132,7 +133,6 @@ __device__ __forceinline__ Best2 wave_best2(int d, unsigned order, int idx, bool
 // ---------------------------------------------------------------- SearchForInitialization
 
 constexpr int kTopK = 8;   // candidates kept per query, in the reference's preference order
-constexpr int kRange = 256;  // queries staged in LDS at a time by k_resolve_sfi
 
 #ifdef ORB_TIMING   // instrumented variant (tools/build_variant.py): per-phase clocks of one wave
 #define TSTAMP(v) const long long v = clock64()
@@ -347,273 +347,190 @@ __global__ __launch_bounds__(256) void k_cand_sfi(const orb_keypoint* __restrict
     }
 }
 
-// Sequential replay of R/src/ORBmatcher.cpp:512-616 for one frame pair per workgroup (one
-// wave).  Active queries (non-empty window) are staged in LDS with their top-K lists; one
-// query then costs one LDS probe of vMatchedDistance by K lanes and a ballot.  Only when
-// fewer than two of the K survive the skip test and more candidates exist does the wave
-// rescan the query's full list.
-// vnMatches12 is rebuilt at the end: a query keeps its match iff vnMatches21 still points
-// back to it (a later query that stole the keypoint overwrote vnMatches21), and every query
-// that ever matched sits in the rotation histogram, as rotHist[bin].push_back(i1) does.
-__global__ __launch_bounds__(64) void k_resolve_sfi(const orb_keypoint* __restrict__ kps1, const int32_t* __restrict__ n1s,
-                                                    const orb_keypoint* __restrict__ kps2, const int32_t* __restrict__ n2s,
-                                                    int cap, GridParams g, float nnratio, int checkOri,
-                                                    const uint32_t* __restrict__ cand, const int* __restrict__ ncand,
-                                                    const uint32_t* __restrict__ topk, float* __restrict__ prev,
-                                                    int32_t* __restrict__ matches12, int32_t* __restrict__ nmatches_out) {
-    TSTAMP(t_begin);
-    long long tStage = 0, tLoop = 0;
-    int nFall = 0, nAct = 0, nMatch = 0, nBatch = 0;
-    long long tFall = 0, tA = 0, tB = 0;
-    (void)tStage; (void)tLoop; (void)nFall; (void)nAct; (void)nMatch; (void)nBatch; (void)tFall; (void)tA; (void)tB;
+// SearchForInitialization's sequential loop (R/src/ORBmatcher.cpp:512-566) for one frame pair per
+// 256-thread workgroup, as the fixpoint of a parallel iteration.  A query's decision (bestIdx2,
+// bestDist or none) depends on the state vMatchedDistance has when the loop reaches it, and that
+// state is fixed by the decisions of the earlier queries alone: vMatchedDistance[i2] is the
+// smallest bestDist among the earlier queries that matched i2 (a later match of i2 passed the
+// `vMatchedDistance[i2] <= dist` skip test, so it is strictly smaller), INT_MAX if none did.
+// Iteration t recomputes every query's decision from the decisions of iteration t-1 (Jacobi
+// sweep; iteration 0 assumes no match).  Query k is exact from iteration k on, so the sweeps
+// reach a fixpoint, and at a fixpoint every query sees the sequential state (induction over the
+// query order): the fixpoint is the sequential result.  Conflicts between nearby queries are
+// rare, so a pair takes a few sweeps.
+//   sweep = (A) claim lists: every matched query links itself into the list of its keypoint
+//           (LDS head stamped with the sweep number, so no reset); (B) per query: its top-K
+//           candidates (distance, visiting order) probe the state through the lists, the first
+//           survivor is bestIdx2 and the second carries bestDist2; a query with fewer than two
+//           survivors among the top-K and a longer list is (F) rescanned over its whole list by
+//           a wave.
+// vnMatches12 follows: a query keeps its match iff it is the last query that matched the keypoint
+// (a later one stole it), and every query that ever matched sits in the rotation histogram, as
+// rotHist[bin].push_back(i1) does; then ComputeThreeMaxima (:1854-1895) filters.
+constexpr int kRsT = 256;
+__global__ __launch_bounds__(kRsT) void k_resolve_sfi(const orb_keypoint* __restrict__ kps1, const int32_t* __restrict__ n1s,
+                                                      const orb_keypoint* __restrict__ kps2, const int32_t* __restrict__ n2s,
+                                                      int cap, float nnratio, int checkOri,
+                                                      const uint32_t* __restrict__ cand, const int* __restrict__ ncand,
+                                                      const uint32_t* __restrict__ topk, float* __restrict__ prev,
+                                                      int32_t* __restrict__ matches12, int32_t* __restrict__ nmatches_out,
+                                                      int* __restrict__ status) {
     extern __shared__ __attribute__((aligned(16))) int sm[];
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int b = blockIdx.x;
     const int n1 = min((int)n1s[b], cap), n2 = min((int)n2s[b], cap);
-    int* vMD = sm;                   // vMatchedDistance [n2]
-    int* v21 = sm + cap;             // vnMatches21 [n2]
-    int* ckey = sm + 2 * cap;        // grid cell key per F2 keypoint (full-rescan order)
-    int* mt = sm + 3 * cap;          // i2 each query matched when it was processed, or -1
-    int* hcount = sm + 4 * cap;      // [kHisto]
+    int* qidx = sm;                  // [cap] i1 of the active query of rank q (ascending i1)
+    int* qnc = qidx + cap;           // [cap] its candidate count
+    int* dec0 = qnc + cap;           // [cap] decision per rank, ping-pong: i2 | bestDist << 20, -1 = none
+    int* dec1 = dec0 + cap;
+    int* nxt = dec1 + cap;           // [cap] claim list link
+    int* fbq = nxt + cap;            // [cap] queries rescanned this sweep; later i1 -> rank
+    int* head = fbq + cap;           // [cap] per F2 keypoint: claim list head (sweep << 16 | rank); later last claimant
+    int* qrank = head + cap;         // [cap] rank of query i1, -1 if inactive
+    int* hcount = qrank + cap;       // [32]
+    int* sc = hcount + 32;           // [16] uniform scalars
     const orb_keypoint* K1 = kps1 + (size_t)b * cap;
     const orb_keypoint* K2 = kps2 + (size_t)b * cap;
-    int32_t* m12 = matches12 + (size_t)b * cap;
     const uint32_t* TK = topk + (size_t)b * cap * kTopK;
     const int* NC = ncand + (size_t)b * cap;
-    for (int j0 = 0; j0 < n2; j0 += 256) {
-        float kx[4], ky[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int j = j0 + u * 64 + lane;
-            kx[u] = j < n2 ? K2[j].x : 0.f;
-            ky[u] = j < n2 ? K2[j].y : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int j = j0 + u * 64 + lane;
-            if (j < n2) {
-                vMD[j] = INT_MAX;
-                v21[j] = -1;
-                ckey[j] = grid_cell(g, kx[u], ky[u]);
-            }
+    const uint32_t* CAND = cand + (size_t)b * cap * kMaxCand;
+    // ---- active queries (non-empty window) compacted in i1 order: contiguous chunk per thread
+    const int chunk = (n1 + kRsT - 1) / kRsT;
+    const int c0 = min(tid * chunk, n1), c1 = min(c0 + chunk, n1);
+    int loc = 0;
+    for (int i = c0; i < c1; i++) loc += NC[i] > 0 ? 1 : 0;
+    {
+        const int incl = wave_incl_scan_i32(loc);
+        if (lane == 63) sc[8 + wid] = incl;
+        for (int j = tid; j < n2; j += kRsT) head[j] = -1;
+        if (tid < 32) hcount[tid] = 0;
+        if (tid < 4) sc[tid] = 0;
+        __syncthreads();
+        int run = incl - loc;
+        for (int w = 0; w < wid; w++) run += sc[8 + w];
+        for (int i = c0; i < c1; i++) {
+            const int nc = NC[i];
+            qrank[i] = -1;
+            if (nc > 0) { qidx[run] = i; qnc[run] = nc; dec0[run] = -1; qrank[i] = run; run++; }
         }
     }
-    for (int i = lane; i < n1; i += 64) mt[i] = -1;
-    if (lane < kHisto) hcount[lane] = 0;
+    const int na = sc[8] + sc[9] + sc[10] + sc[11];
     __syncthreads();
-    // Queries are taken in ranges of kRange: the active ones (a non-empty window) are
-    // compacted and their top-K lists bulk-loaded into LDS, so the serial replay below
-    // touches only LDS.
-    int* qidx = hcount + 32;                       // [kRange]
-    int* qnc = qidx + kRange;                      // [kRange]
-    uint32_t* qtk = (uint32_t*)(qnc + kRange);     // [kRange * kTopK]
-#ifdef ORB_TIMING
-    int* nMatchL = (int*)(qtk + kRange * kTopK);
-    if (lane == 0) nMatchL[0] = 0;
-#endif
-    const int myK = lane & (kTopK - 1);
-    TSTAMP(t_init);
-    for (int r0 = 0; r0 < n1; r0 += kRange) {
-        TSTAMP(t_r0);
-        const int rEnd = min(n1, r0 + kRange);
-        int na = 0;
-        // all loads of a stage are issued before any is consumed (global latency paid once)
-        int ncv[kRange / 64];
-#pragma unroll
-        for (int u = 0; u < kRange / 64; u++) {
-            const int i = r0 + u * 64 + lane;
-            ncv[u] = i < rEnd ? NC[i] : 0;
+    int* dcur = dec0;
+    int* dnew = dec1;
+    int it = 0;
+    for (;; it++) {
+        if (it > na + 1) { if (tid == 0) atomicOr(status, 2); break; }   // unreachable: converges by sweep na
+        // (A) claim lists of the current decisions
+        for (int q = tid; q < na; q += kRsT) {
+            const int dq = dcur[q];
+            if (dq < 0) continue;
+            const int old = atomicExch(&head[dq & 0xFFFFF], (it << 16) | q);
+            nxt[q] = (old >> 16) == it ? (old & 0xFFFF) : -1;
         }
-#pragma unroll
-        for (int u = 0; u < kRange / 64; u++) {
-            const int i = r0 + u * 64 + lane;
-            const uint64_t m = __ballot(ncv[u] > 0);
-            if (ncv[u] > 0) {
-                const int pos = na + __popcll(m & ((1ull << lane) - 1ull));
-                qidx[pos] = i;
-                qnc[pos] = ncv[u];
+        if (tid == 0) { sc[(it + 1) & 1] = 0; sc[2 + ((it + 1) & 1)] = 0; }
+        __syncthreads();
+        // state seen by query q at keypoint j: smallest bestDist of an earlier query that matched j
+        auto seen = [&](int j, int q) {
+            int s = INT_MAX;
+            const int h = head[j];
+            int u = (h >> 16) == it ? (h & 0xFFFF) : -1;
+            while (u >= 0) {
+                if (u < q) s = min(s, dcur[u] >> 20);
+                u = nxt[u];
             }
-            na += __popcll(m);
-        }
-        wave_lds_sync();
-        for (int t0 = 0; t0 < na * kTopK; t0 += 64 * 8) {
-            uint32_t tv[8];
+            return s;
+        };
+        // (B) decisions from the top-K lists
+        for (int q = tid; q < na; q += kRsT) {
+            const int nc = qnc[q];
+            const uint4* t4 = reinterpret_cast<const uint4*>(TK + (size_t)qidx[q] * kTopK);
+            const uint4 ta = t4[0], tb = t4[1];
+            const uint32_t e[kTopK] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
+            const int kn = min(nc, kTopK);
+            int f = -1, f2 = -1;
 #pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const int t = t0 + u * 64 + lane;
-                tv[u] = t < na * kTopK ? TK[(size_t)qidx[t / kTopK] * kTopK + (t % kTopK)] : 0u;
-            }
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const int t = t0 + u * 64 + lane;
-                if (t < na * kTopK) qtk[t] = tv[u];
-            }
-        }
-        wave_lds_sync();
-        TACC(tStage, t_r0);
-        TSTAMP(t_l0);
-        // Eight queries at a time, decided in parallel: lane 8q+k probes vMatchedDistance for
-        // the k-th preferred candidate of query a0+q (one LDS gather), every query takes its
-        // first / second surviving candidate from the ballot.  A decision stands unless an
-        // earlier query of the same batch matched one of its candidates up to its second
-        // survivor at a distance <= its own (that candidate would now be skipped); the batch
-        // commits up to the first such query (or the first needing a full-list rescan) and
-        // the next batch starts there, so every commit sees exactly the sequential state.
-        int a0 = 0;
-        while (a0 < na) {
-            TSTAMP(t_b0);
-#ifdef ORB_TIMING
-            nBatch++;
-#endif
-            const int q = lane >> 3;
-            const int a = a0 + q;
-            uint32_t e = ~0u;
-            int nc = 0, qi = -1;
-            if (a < na) { nc = qnc[a]; e = qtk[a * kTopK + myK]; qi = qidx[a]; }
-            const int j = (int)(e & 0xFFFFFu), d = (int)(e >> 20);
-            bool valid = false;
-            if (a < na && myK < min(nc, kTopK)) valid = vMD[j] > d;   // `if(vMatchedDistance[i2]<=dist) continue;`
-            const uint64_t vm = __ballot(valid);
-            TACC(tA, t_b0);
-            TSTAMP(t_b1);
-            const uint32_t mk = (uint32_t)(vm >> (q * 8)) & 0xFFu;
-            const uint32_t mk2 = mk & (mk - 1u);
-            const int f = mk ? __ffs(mk) - 1 : 0, f2 = mk2 ? __ffs(mk2) - 1 : 0;
-            uint32_t e1 = 0u, e2 = 0u;
-            if (a < na) { e1 = qtk[a * kTopK + f]; e2 = qtk[a * kTopK + f2]; }
-            const int bestd = (int)(e1 >> 20), bi = (int)(e1 & 0xFFFFFu);
-            const int best2 = mk2 ? (int)(e2 >> 20) : INT_MAX;
-            const bool fallback = a < na && __popc(mk) < 2 && nc > kTopK;
-            const bool match = a < na && !fallback && mk != 0 && bestd <= kThLow &&
-                               (float)bestd < (float)best2 * nnratio;
-            // publish every query's decision (bi, dist; -1 = none) to its 8 lanes' peers via LDS
-            // (lane 8u holds query u's decision: eight v_readlane broadcasts, no LDS round trip)
-            const int myb = match ? bi : -1;
-            int qbi[8], qbd[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                qbi[u] = __builtin_amdgcn_readlane(myb, 8 * u);
-                qbd[u] = __builtin_amdgcn_readlane(bestd, 8 * u);
-            }
-            // conflicts: an earlier match of the batch on one of my candidates up to my second
-            // survivor, at a distance <= mine (it would now be skipped)
-            const int lim = mk2 ? f2 : kTopK - 1;
-            bool hit = false;
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                hit |= u < q && valid && myK <= lim && qbi[u] == j && qbd[u] <= d;
-            }
-            const uint64_t stop = __ballot(hit) | __ballot(fallback && myK == 0);
-            const int qEnd = min(8, na - a0);
-            const int qs = stop ? min(qEnd, (__ffsll((unsigned long long)stop) - 1) >> 3) : qEnd;
-#ifdef ORB_TIMING
-            nAct += qs;
-#endif
-            // commit queries < qs: every match records mt; vnMatches21 / vMatchedDistance take the
-            // last committed match of each keypoint (stealing within the batch)
-            if (myK == 0 && q < qs && match) {
-#ifdef ORB_TIMING
-                atomicAdd(&nMatchL[0], 1);
-#endif
-                mt[qi] = bi;
-                bool sup = false;
-#pragma unroll
-                for (int u = 0; u < 8; u++) sup |= u > q && u < qs && qbi[u] == bi;
-                if (!sup) {
-                    v21[bi] = qi;
-                    vMD[bi] = bestd;
-                }
-            }
-            wave_lds_sync();
-            TACC(tB, t_b1);
-            if (qs < qEnd && ((stop >> (qs * 8)) & 1ull) && __builtin_amdgcn_readlane((int)fallback, qs * 8)) {
-                TSTAMP(t_f0);
-#ifdef ORB_TIMING
-                nFall++; nAct++;
-#endif
-                // fewer than two of the top-K survive: rescan the query's whole list
-                const int ncq = __builtin_amdgcn_readlane(nc, qs * 8);
-                const int iq = __builtin_amdgcn_readlane(qi, qs * 8);
-                const uint32_t* C = cand + ((size_t)b * cap + iq) * kMaxCand;
-                Best2 acc;
-                acc.best = INT_MAX; acc.best2 = INT_MAX; acc.idx = -1;
-                unsigned accOrder = 0xFFFFFu;
-                for (int c0 = 0; c0 < ncq; c0 += 64) {
-                    const int c = c0 + lane;
-                    bool ok = false;
-                    int dd = 0, jj = 0;
-                    unsigned order = 0;
-                    if (c < ncq) {
-                        const uint32_t ce = C[c];
-                        jj = (int)(ce & 0xFFFFFu);
-                        dd = (int)(ce >> 20);
-                        ok = vMD[jj] > dd;
-                        order = (unsigned)ckey[jj];
-                    }
-                    const Best2 r = wave_best2(dd, order, jj, ok);
-                    if (r.idx >= 0) {
-                        const unsigned rOrder = (unsigned)ckey[r.idx];
-                        const bool rFirst = (r.best < acc.best) ||
-                                            (r.best == acc.best && (rOrder < accOrder || (rOrder == accOrder && r.idx < acc.idx)));
-                        if (rFirst) {
-                            acc.best2 = min(acc.best, r.best2);
-                            acc.idx = r.idx;
-                            accOrder = rOrder;
-                            acc.best = r.best;
-                        } else {
-                            acc.best2 = min(acc.best2, r.best);
-                        }
+            for (int k = 0; k < kTopK; k++) {
+                if (k < kn && f2 < 0) {
+                    const int j = (int)(e[k] & 0xFFFFFu), d = (int)(e[k] >> 20);
+                    if (seen(j, q) > d) {
+                        if (f < 0) f = k; else f2 = k;
                     }
                 }
-                const int fbi = __builtin_amdgcn_readfirstlane(acc.idx);
-                const int fbd = __builtin_amdgcn_readfirstlane(acc.best);
-                const int fb2 = __builtin_amdgcn_readfirstlane(acc.best2);
-                if (fbi >= 0 && fbd <= kThLow && (float)fbd < (float)fb2 * nnratio) {
-#ifdef ORB_TIMING
-                    nMatch++;
-#endif
-                    if (lane == 0) {
-                        v21[fbi] = iq;
-                        vMD[fbi] = fbd;
-                        mt[iq] = fbi;
+            }
+            if (f2 < 0 && nc > kTopK) {      // fewer than two survivors among the top-K
+                fbq[atomicAdd(&sc[2 + (it & 1)], 1)] = q;
+                continue;
+            }
+            int nd = -1;
+            if (f >= 0) {
+                const int bd = (int)(e[f] >> 20);
+                const int b2 = f2 >= 0 ? (int)(e[f2] >> 20) : INT_MAX;
+                if (bd <= kThLow && (float)bd < (float)b2 * nnratio) nd = (int)e[f];
+            }
+            dnew[q] = nd;
+            if (nd != dcur[q]) sc[it & 1] = 1;
+        }
+        __syncthreads();
+        // (F) whole-list rescans, one wave per query: best = smallest (dist, visiting position) among
+        //     the survivors, bestDist2 = the multiset second smallest (the reference's running pair)
+        const int nfb = sc[2 + (it & 1)];
+        for (int f = wid; f < nfb; f += kRsT / 64) {
+            const int q = fbq[f];
+            const int nc = min(qnc[q], kMaxCand);
+            const uint32_t* L = CAND + (size_t)qidx[q] * kMaxCand;
+            unsigned long long bestKey = ~0ull;   // dist << 32 | position << 20 | i2
+            int best2 = INT_MAX;
+            for (int cb = 0; cb < nc; cb += 64) {
+                const int c = cb + lane;
+                bool ok = false;
+                int d = 0, j = 0;
+                if (c < nc) {
+                    const uint32_t ce = L[c];
+                    j = (int)(ce & 0xFFFFFu);
+                    d = (int)(ce >> 20);
+                    ok = seen(j, q) > d;
+                }
+                const unsigned long long key = ok ? (((unsigned long long)d << 32) | ((unsigned long long)c << 20) | (unsigned)j) : ~0ull;
+                const unsigned long long mk = wave_min_u64(key);
+                // second: the chunk's other survivors and the previous running pair
+                const int d2 = (ok && key != mk) ? d : INT_MAX;
+                const int cb2 = wave_min_i32(d2);
+                if (mk != ~0ull) {
+                    const int mkd = (int)(mk >> 32);
+                    if (mk < bestKey) {
+                        best2 = min(bestKey == ~0ull ? INT_MAX : (int)(bestKey >> 32), min(best2, cb2));
+                        bestKey = mk;
+                    } else {
+                        best2 = min(best2, min(mkd, cb2));
                     }
                 }
-                wave_lds_sync();
-                TACC(tFall, t_f0);
-                a0 += qs + 1;
-            } else {
-                a0 += qs;
+            }
+            if (lane == 0) {
+                int nd = -1;
+                if (bestKey != ~0ull) {
+                    const int bd = (int)(bestKey >> 32);
+                    if (bd <= kThLow && (float)bd < (float)best2 * nnratio) nd = (int)(bestKey & 0xFFFFFull) | (bd << 20);
+                }
+                dnew[q] = nd;
+                if (nd != dcur[q]) sc[it & 1] = 1;
             }
         }
-        wave_lds_sync();
-        TACC(tLoop, t_l0);
+        __syncthreads();
+        const bool again = sc[it & 1] != 0;
+        int* t = dcur; dcur = dnew; dnew = t;
+        if (!again) break;
     }
-    TSTAMP(t_loopend);
     __syncthreads();
-    // rotation bin of every query that ever matched (stolen ones included); a query keeps its
-    // match iff vnMatches21 still points back to it
-    for (int i0 = 0; i0 < n1; i0 += 256) {
-        int jv[4];
-        float a1[4], a2[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int i = i0 + u * 64 + lane;
-            jv[u] = i < n1 ? mt[i] : -1;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int i = i0 + u * 64 + lane;
-            a1[u] = jv[u] >= 0 ? K1[i].angle : 0.f;
-            a2[u] = jv[u] >= 0 ? K2[jv[u]].angle : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int i = i0 + u * 64 + lane;
-            if (jv[u] < 0) continue;
-            const int bin = rot_bin(a1[u] - a2[u]);
-            if (checkOri) atomicAdd(&hcount[bin], 1);
-            mt[i] = v21[jv[u]] == i ? (jv[u] | (bin << 24)) : -1;
-        }
+    // ---- last claimant per keypoint (vnMatches21), rotation histogram of every match
+    for (int j = tid; j < n2; j += kRsT) head[j] = -1;
+    __syncthreads();
+    for (int q = tid; q < na; q += kRsT) {
+        const int dq = dcur[q];
+        if (dq < 0) continue;
+        const int j = dq & 0xFFFFF;
+        atomicMax(&head[j], q);
+        if (checkOri) atomicAdd(&hcount[rot_bin(K1[qidx[q]].angle - K2[j].angle)], 1);
     }
     __syncthreads();
     int ind1 = -1, ind2 = -1, ind3 = -1;
@@ -629,52 +546,38 @@ __global__ __launch_bounds__(64) void k_resolve_sfi(const orb_keypoint* __restri
         if ((float)max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
         else if ((float)max3 < 0.1f * (float)max1) { ind3 = -1; }
     }
+    int32_t* m12 = matches12 + (size_t)b * cap;
     int kept = 0;
-    for (int i0 = 0; i0 < n1; i0 += 256) {
-        int jv[4];
-        float px[4], py[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int i = i0 + u * 64 + lane;
-            int j = i < n1 ? mt[i] : -1;
-            if (j >= 0) {
-                const int bin = j >> 24;
-                j &= 0xFFFFFF;
-                if (checkOri && bin != ind1 && bin != ind2 && bin != ind3) j = -1;
-            }
-            jv[u] = j;
-        }
-        if (prev) {
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                px[u] = jv[u] >= 0 ? K2[jv[u]].x : 0.f;
-                py[u] = jv[u] >= 0 ? K2[jv[u]].y : 0.f;
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int i = i0 + u * 64 + lane;
-            if (i >= n1) continue;
-            m12[i] = jv[u];
-            if (jv[u] >= 0) {
-                kept++;
-                if (prev) {
-                    prev[((size_t)b * cap + i) * 2] = px[u];
-                    prev[((size_t)b * cap + i) * 2 + 1] = py[u];
+    for (int i = tid; i < n1; i += kRsT) {
+        const int q = qrank[i];
+        int j = -1;
+        if (q >= 0) {
+            const int dq = dcur[q];
+            if (dq >= 0 && head[dq & 0xFFFFF] == q) {
+                j = dq & 0xFFFFF;
+                if (checkOri) {
+                    const int bin = rot_bin(K1[i].angle - K2[j].angle);
+                    if (bin != ind1 && bin != ind2 && bin != ind3) j = -1;
                 }
+            }
+        }
+        m12[i] = j;
+        if (j >= 0) {
+            kept++;
+            if (prev) {
+                const orb_keypoint k2 = K2[j];
+                prev[((size_t)b * cap + i) * 2] = k2.x;
+                prev[((size_t)b * cap + i) * 2 + 1] = k2.y;
             }
         }
     }
     kept = wave_reduce_sum_i32(kept);
-    if (lane == 0) nmatches_out[b] = kept;
-#ifdef ORB_TIMING
-    if (lane == 0 && (b == 0 || b == 5))
-        printf("resolve b0: init %lld stage %lld loop %lld (gather %lld decide %lld fallback %lld) final %lld total %lld "
-               "n1 %d n2 %d act %d fall %d match %d batches %d\n",
-               t_init - t_begin, tStage, tLoop, tA, tB, tFall, clock64() - t_loopend, clock64() - t_begin, n1, n2, nAct, nFall,
-               nMatch + nMatchL[0], nBatch);
-#endif
+    if (lane == 0) sc[12 + wid] = kept;
+    __syncthreads();
+    if (tid == 0) nmatches_out[b] = sc[12] + sc[13] + sc[14] + sc[15];
 }
+
+static size_t resolve_sfi_lds(int cap) { return (8 * (size_t)cap + 32 + 16) * 4; }
 
 // ---------------------------------------------------------------- SearchByProjection(Frame, Frame)
 
@@ -1702,10 +1605,11 @@ int orb_search_for_initialization(orb_matcher* m, const orb_frame_view* f1, cons
     hipLaunchKernelGGL(k_cand_sfi, dim3((cap + 3) / 4, 1), dim3(256), 0, s, m->d_k1, m->d_d1, m->d_n, m->d_d2, m->d_cs,
                        m->d_gj, m->d_gxy, m->d_prev, cap, g, (float)window, m->d_cand, m->d_ncand, m->d_topk,
                        m->d_status);
-    const size_t lds = (4 * (size_t)cap + 32 + (2 + kTopK) * kRange + 32) * 4;
-    if (lds > 65536) return ORB_E2BIG;
-    hipLaunchKernelGGL(k_resolve_sfi, dim3(1), dim3(64), lds, s, m->d_k1, m->d_n, m->d_k2, m->d_n + 1, cap, g,
-                       m->nnratio, m->checkOri, m->d_cand, m->d_ncand, m->d_topk, m->d_prev, m->d_m12, m->d_nm);
+    const size_t lds = resolve_sfi_lds(cap);
+    if (lds > kMaxLds || cap > 32767) return ORB_E2BIG;
+    hipLaunchKernelGGL(k_resolve_sfi, dim3(1), dim3(kRsT), lds, s, m->d_k1, m->d_n, m->d_k2, m->d_n + 1, cap,
+                       m->nnratio, m->checkOri, m->d_cand, m->d_ncand, m->d_topk, m->d_prev, m->d_m12, m->d_nm,
+                       m->d_status);
     ORB_HIP_TRY(hipGetLastError());
     int32_t* hm = (int32_t*)hd1;   // reuse pinned space
     ORB_HIP_TRY(hipMemcpyAsync(hm, m->d_m12, (size_t)f1->n * 4, hipMemcpyDeviceToHost, s));
@@ -1736,10 +1640,11 @@ int orb_search_for_initialization_batch_device(orb_matcher* m, const orb_keypoin
     hipLaunchKernelGGL(k_cand_sfi, dim3((cap + 3) / 4, nb), dim3(256), 0, s, d_kps1, d_desc1, d_n1, d_desc2, m->d_cs,
                        m->d_gj, m->d_gxy, (const float*)nullptr, cap, g, (float)window, m->d_cand, m->d_ncand,
                        m->d_topk, m->d_status);
-    const size_t lds = (4 * (size_t)cap + 32 + (2 + kTopK) * kRange + 32) * 4;
-    if (lds > 65536) return ORB_E2BIG;
-    hipLaunchKernelGGL(k_resolve_sfi, dim3(nb), dim3(64), lds, s, d_kps1, d_n1, d_kps2, d_n2, cap, g, m->nnratio,
-                       m->checkOri, m->d_cand, m->d_ncand, m->d_topk, (float*)nullptr, d_matches12, d_nmatches);
+    const size_t lds = resolve_sfi_lds(cap);
+    if (lds > kMaxLds || cap > 32767) return ORB_E2BIG;
+    hipLaunchKernelGGL(k_resolve_sfi, dim3(nb), dim3(kRsT), lds, s, d_kps1, d_n1, d_kps2, d_n2, cap, m->nnratio,
+                       m->checkOri, m->d_cand, m->d_ncand, m->d_topk, (float*)nullptr, d_matches12, d_nmatches,
+                       m->d_status);
     ORB_HIP_TRY(hipGetLastError());
     return ORB_OK;
 }
