@@ -384,7 +384,9 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
                                                    int* __restrict__ status, int maxW, int maxH) {
     TSTAMP(t_fc0);
     extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // the wave index is uniform: readfirstlane keeps it (and the level / cell / geometry derived
+    // from it) in SGPRs, so g.lv[l] fields are scalar loads instead of per-lane flat loads
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     int bx, b;
     xcd_block_2d(bx, b);
     const int c = bx * 4 + wid;
@@ -433,13 +435,15 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
         const int NW1 = NW + 1;                     // aligned source dwords per row
         const int R = 64 / NW1, k = lane % NW1, r0 = lane / NW1;
         const int rows = rh + 6;
+        const int pitch = L.pitch;
         for (int rb = 0; rb < rows; rb += 8 * R) {
             uint32_t a[8];
+            // every lane loads (row clamped into the window, so the address is always inside the
+            // level): no exec-masked branch, all eight loads in flight together
 #pragma unroll
             for (int u = 0; u < 8; u++) {
-                const int r = rb + u * R + r0;
-                a[u] = (r0 < R && r < rows) ? *reinterpret_cast<const uint32_t*>(img + (size_t)(ry0 - 3 + r) * L.pitch + ga + 4 * k)
-                                            : 0u;
+                const int r = min(rb + u * R + min(r0, R - 1), rows - 1);
+                a[u] = *reinterpret_cast<const uint32_t*>(img + (ry0 - 3 + r) * pitch + ga + 4 * min(k, NW));
             }
 #pragma unroll
             for (int u = 0; u < 8; u++) {
@@ -1280,7 +1284,9 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
                                                      uint8_t* __restrict__ desc, int cap, int32_t* __restrict__ counts,
                                                      uint32_t kA, uint32_t kB) {
     __shared__ __attribute__((aligned(16))) unsigned char od_sm[4][kOdWaveBytes];
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // the wave index is uniform: readfirstlane keeps it (and the level / cell / geometry derived
+    // from it) in SGPRs, so g.lv[l] fields are scalar loads instead of per-lane flat loads
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     int bx, b;
     xcd_block_2d(bx, b);
     const int q = bx * 4 + wid;
@@ -1308,17 +1314,17 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
     // 1. patch
     if (x - 24 >= 0 && x + 24 <= L.w && y - 21 >= 0 && y + 21 < L.h) {
         const int gx0 = x - 24, sh = gx0 & 3, ga = gx0 - sh;
+        const int pitch = L.pitch;
+        const uint8_t* src0 = img + (y - 21) * pitch + ga;
         for (int t0 = 0; t0 < kOdRows * 12; t0 += 64 * 4) {
             uint32_t a0[4], a1[4];
+            // unconditional loads (index clamped into the window): all in flight together
 #pragma unroll
             for (int u = 0; u < 4; u++) {
-                const int t = t0 + u * 64 + lane;
-                a0[u] = a1[u] = 0;
-                if (t < kOdRows * 12) {
-                    const uint8_t* src = img + (size_t)(y - 21 + t / 12) * L.pitch + ga + 4 * (t % 12);
-                    a0[u] = *reinterpret_cast<const uint32_t*>(src);
-                    a1[u] = *reinterpret_cast<const uint32_t*>(src + 4);
-                }
+                const int t = min(t0 + u * 64 + lane, kOdRows * 12 - 1);
+                const uint8_t* src = src0 + (t / 12) * pitch + 4 * (t % 12);
+                a0[u] = *reinterpret_cast<const uint32_t*>(src);
+                a1[u] = *reinterpret_cast<const uint32_t*>(src + 4);
             }
 #pragma unroll
             for (int u = 0; u < 4; u++) {
@@ -1473,7 +1479,9 @@ __global__ __launch_bounds__(256) void k_stereo_match(Geom g, StereoTabs tb, con
                                                       float* __restrict__ ur, float* __restrict__ depth,
                                                       int32_t* __restrict__ sad, int outStride) {
     __shared__ int rowsad[4][128];
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // the wave index is uniform: readfirstlane keeps it (and the level / cell / geometry derived
+    // from it) in SGPRs, so g.lv[l] fields are scalar loads instead of per-lane flat loads
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int p = blockIdx.y;
     const int iL = blockIdx.x * 4 + wid;
     const int nl = nLs[(size_t)p * cntStride], nr = nRs[(size_t)p * cntStride];
