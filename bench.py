@@ -29,9 +29,12 @@ import torch  # noqa: E402
 import pkgload  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md)
+VALU_PEAK_TOPS = 78.6            # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md)
+VALU_MEASURED_TOPS = 39.3        # tools/micro/valu_peak.hip: 4 cycles per wave64 VALU op (profiles/r02_valu_peak.txt)
 STAGES = ["resize", "fast_detect", "reserved", "octree", "reserved2", "orient_blur_desc"]
 KERNELS = ["k_resize", "k_fast_cell", None, "k_octree", None, "k_orient_desc"]
-PMC_TRAFFIC = ROOT / "profiles" / "r01_pmc_traffic.json"   # tools/pmc_run.sh + tools/pmc_traffic.py
+PMC_TRAFFIC = ROOT / "profiles" / "r02_pmc_traffic.json"   # tools/pmc_run.sh + tools/pmc_traffic.py
+PMC_VALU = ROOT / "profiles" / "r02_valu_pmc.json"         # tools/gpu_valu_pmc.sh + tools/pmc_valu.py
 
 
 def pmc_traffic(kernel, W, H, NF, Bs):
@@ -47,6 +50,20 @@ def pmc_traffic(kernel, W, H, NF, Bs):
                 != (W, H, NF, Bs):
             return None
         return int(doc["kernels"][kernel]["traffic_bytes_per_batch"])
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def pmc_valu_ops(kernel, W, H, NF, Bs):
+    """VALU lane-ops (SQ_INSTS_VALU x 64) per launch of `kernel` from the committed PMC pass of
+    this configuration; None when that pass does not match it."""
+    try:
+        doc = json.loads(PMC_VALU.read_text())
+        cfg = doc["config"]
+        if (int(cfg["width"]), int(cfg["height"]), int(cfg["nfeatures"]), int(cfg["frames_per_launch"])) \
+                != (W, H, NF, Bs):
+            return None
+        return float(doc["kernels"][kernel]["valu_lane_ops"])
     except (OSError, KeyError, ValueError):
         return None
 
@@ -910,11 +927,14 @@ def main():
         step(s)
     torch.cuda.synchronize(dev)
     if not args.no_profile:
-        # every stream's extractor records its stage events: with S streams sharing the chip a
-        # launch overlapped by another stream's kernels runs longer than one that is alone, and the
-        # rocprofv3 per-kernel average (profiles/) is over all of them
+        # every stream's extractor records two HIP events around its k_fast_cell launch (the
+        # dominant kernel) inside the timed region: with S streams sharing the chip a launch
+        # overlapped by another stream's kernels runs longer than one that is alone, and the
+        # rocprofv3 per-kernel average (profiles/) is over all of them.  The per-stage split is
+        # taken in a separate profiled pass after the timed region (events at every stage
+        # boundary add dispatch bubbles).
         for p in pipes:
-            lib.orb_extractor_profile(p.ex._h, 1)
+            lib.orb_extractor_profile(p.ex._h, 2)
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
@@ -929,16 +949,25 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
-    # stage times (HIP events recorded on the launch stream during the timed region)
-    stage_ms = np.zeros(6)
-    ncalls = C.c_int(0)
-    if not args.no_profile:
+    # k_fast_cell launch times (HIP events recorded on the launch stream during the timed region)
+    def stage_times():
+        tot, calls = np.zeros(6), 0
         for p in pipes:
             sm, nc = np.zeros(6), C.c_int(0)
             lib.orb_extractor_stage_times(p.ex._h, _abi.ptr(sm), 6, C.byref(nc))
             lib.orb_extractor_profile(p.ex._h, 0)
-            stage_ms += sm
-            ncalls.value += nc.value
+            tot += sm
+            calls += nc.value
+        return tot, calls
+    fast_ms, ncalls = stage_times() if not args.no_profile else (np.zeros(6), 0)
+    stage_ms, nstage = np.zeros(6), 0
+    if not args.no_profile:      # the stage split: a separate pass with every stage boundary recorded
+        for p in pipes:
+            lib.orb_extractor_profile(p.ex._h, 1)
+        for s in range(min(args.steps, 10)):
+            step(args.warmup + args.steps + s)
+        torch.cuda.synchronize(dev)
+        stage_ms, nstage = stage_times()
     frames_total = B * args.steps * world
     value = frames_total / dt
     cnt = torch.cat([p.counts[p.last][1:] for p in pipes]).cpu().numpy()
@@ -971,26 +1000,43 @@ def main():
         "keypoints_per_frame": float(np.mean(cnt)),
         "matches_per_pair": float(np.mean(nmatch)),
     }
-    if not args.no_profile and ncalls.value > 0:
-        per_launch_ms = stage_ms / ncalls.value
-        dom = int(np.argmax(per_launch_ms))
+    if not args.no_profile and ncalls > 0:
+        fast_launch_ms = float(fast_ms[1]) / ncalls       # live, timed region, launch streams
         n_out = float(np.mean(cnt))
         pre = np.zeros(8, np.int32)
         lib.orb_extractor_last_counts(ex._h, 0, _abi.ptr(pre), None)
         n_pre = float(pre.sum())
-        bytes_per_launch = algorithmic_bytes(STAGES[dom], lw, lh, n_pre, n_out) * Bs
-        achieved = bytes_per_launch / (per_launch_ms[dom] * 1e-3) / 1e9
-        result["roofline"] = {"bound": "hbm", "kernel": KERNELS[dom], "achieved": round(achieved, 2),
-                              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                              "traffic": None,
-                              "launch_ms": round(float(per_launch_ms[dom]), 4)}
-        tr = pmc_traffic(KERNELS[dom], W, H, NF, Bs)
+        # k_fast_cell is VALU-issue-bound (profiles/r02_valu_pmc.json: SQ_ACTIVE_INST_VALU ~ the
+        # VALU instruction count x 4 cycles keeps the SIMDs >80 % busy), so its roofline is the
+        # vector ALU: achieved = VALU lane-ops per launch (SQ_INSTS_VALU x 64 from the committed
+        # PMC pass of this configuration) / the live launch time; peak = 78.6 T lane-ops/s
+        # (256 CU x 128 lanes x 2.4 GHz, MI355X_MICROARCH.md) and, beside it, the issue rate
+        # measured by tools/micro/valu_peak.hip (4 cycles per wave64 VALU instruction:
+        # 6.1e11 wave-instructions/s = 39.3 T lane-ops/s).  The HBM figure stays as secondary.
+        hbm_bytes = algorithmic_bytes("fast_detect", lw, lh, n_pre, n_out) * Bs
+        hbm = {"bound": "hbm", "achieved": round(hbm_bytes / (fast_launch_ms * 1e-3) / 1e9, 2), "peak": HBM_PEAK_GBS,
+               "unit": "GB/s", "algorithmic_bytes_per_launch": int(hbm_bytes), "traffic": None}
+        hbm["frac"] = round(hbm["achieved"] / HBM_PEAK_GBS, 5)
+        tr = pmc_traffic("k_fast_cell", W, H, NF, Bs)
         if tr is not None:
-            result["roofline"]["traffic"] = tr
-            result["roofline"]["traffic_unit"] = "bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)"
-            result["roofline"]["traffic_source"] = PMC_TRAFFIC.name
-        result["stage_ms_per_batch"] = {k: round(float(v), 4) for k, v in zip(STAGES, per_launch_ms)
+            hbm["traffic"] = tr
+            hbm["traffic_unit"] = "bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)"
+            hbm["traffic_source"] = PMC_TRAFFIC.name
+        roof = {"bound": "valu", "kernel": "k_fast_cell", "achieved": None, "peak": VALU_PEAK_TOPS, "unit": "TOP/s",
+                "frac": None, "traffic": hbm["traffic"], "launch_ms": round(fast_launch_ms, 4),
+                "frames_per_launch": Bs, "hbm": hbm}
+        ops = pmc_valu_ops("k_fast_cell", W, H, NF, Bs)
+        if ops is not None:
+            ach = ops / (fast_launch_ms * 1e-3) / 1e12
+            roof.update(achieved=round(ach, 3), frac=round(ach / VALU_PEAK_TOPS, 4),
+                        valu_lane_ops_per_launch=ops, valu_ops_source=PMC_VALU.name,
+                        measured_issue_peak=VALU_MEASURED_TOPS,
+                        frac_of_measured_issue_peak=round(ach / VALU_MEASURED_TOPS, 4))
+        result["roofline"] = roof
+    if nstage > 0:
+        result["stage_ms_per_batch"] = {k: round(float(v) / nstage, 4) for k, v in zip(STAGES, stage_ms)
                                         if not k.startswith("reserved")}
+        result["stage_ms_source"] = "separate profiled pass after the timed region (events at every stage boundary)"
     # whole-pipeline roofline of SURVEY §8d: B_ext = P0 + 2 sum_{l>=1} P_l + N_kp (28 + 32) per frame
     P = (lw.astype(np.int64) * lh)
     b_ext = float(P[0] + 2 * P[1:].sum()) + float(np.mean(cnt)) * 60.0

@@ -112,7 +112,9 @@ int orb_pyramid_level_device(orb_extractor* ex, int frame, int level, int blurre
  * 4 reserved (always 0), 5 orientation + Gaussian + descriptor).  orb_extractor_stage_times
  * waits for them, writes the summed milliseconds per stage to ms[0..n_stages)
  * and the number of profiled calls to *n_calls, then resets; returns the number
- * of stages. */
+ * of stages.  enable = 2 records only the two events bracketing stage 1
+ * (k_fast_cell), so a timed run pays two event records per call; the other
+ * stages then read 0. */
 int orb_extractor_profile(orb_extractor* ex, int enable);
 int orb_extractor_stage_times(orb_extractor* ex, double* ms, int n_stages, int* n_calls);
 

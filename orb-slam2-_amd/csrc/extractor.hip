@@ -268,7 +268,8 @@ __global__ __launch_bounds__(256) void k_resize(Geom g, int l, uint8_t* __restri
             for (int u = 0; u < 8; u++) {
                 rr[u] = r;
                 ww[u] = wq;
-                v[u] = r < rows ? *reinterpret_cast<const uint32_t*>(src + (size_t)(yLo + r) * S.pitch + cA + 4 * wq) : 0u;
+                // unconditional (row clamped into the window): the eight loads stay in flight together
+                v[u] = *reinterpret_cast<const uint32_t*>(src + (yLo + min(r, rows - 1)) * S.pitch + cA + 4 * wq);
                 r += dq;
                 wq += dr;
                 if (wq >= words) { wq -= words; r++; }
@@ -1699,7 +1700,7 @@ struct orb_extractor {
     std::vector<char> h_level_valid;
     int lastB = 0;
     // stage profiling (HIP events on the launch stream)
-    bool profile = false;
+    int profile = 0;   // 0 off, 1 every stage boundary, 2 only around k_fast_cell (stage 1)
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::array<hipEvent_t, kStages + 1>> ev_sets;
     double stage_ms[kStages] = {0};
@@ -1823,15 +1824,16 @@ static int run_pipeline(orb_extractor* ex, int B, orb_keypoint* d_kps, uint8_t* 
                         hipStream_t st) {
     const Geom& g = ex->g;
     std::array<hipEvent_t, kStages + 1> ev{};
-    const bool prof = ex->profile;
+    const int prof = ex->profile;
     if (prof) {
-        for (auto& e : ev) {
-            e = ev_get(ex);
-            if (!e) return ORB_EGPU;
+        for (int i = 0; i <= kStages; i++) {
+            if (prof == 2 && i != 1 && i != 2) continue;   // two events bracketing k_fast_cell only
+            ev[i] = ev_get(ex);
+            if (!ev[i]) return ORB_EGPU;
         }
     }
     auto mark = [&](int i) {
-        if (prof) (void)hipEventRecord(ev[i], st);
+        if (prof && ev[i]) (void)hipEventRecord(ev[i], st);
     };
     ORB_HIP_TRY(hipMemsetAsync(ex->d_status, 0, 4, st));
     mark(0);
@@ -2096,7 +2098,8 @@ int orb_pyramid_level_device(orb_extractor* ex, int frame, int level, int blurre
 
 int orb_extractor_profile(orb_extractor* ex, int enable) {
     if (!ex) return ORB_EINVAL;
-    ex->profile = enable != 0;
+    if (enable < 0 || enable > 2) return ORB_EINVAL;
+    ex->profile = enable;
     return ORB_OK;
 }
 
@@ -2104,14 +2107,17 @@ int orb_extractor_stage_times(orb_extractor* ex, double* ms, int n_stages, int* 
     if (!ex || (n_stages > 0 && !ms)) return ORB_EINVAL;
     ORB_HIP_TRY(hipSetDevice(ex->device));
     for (auto& set : ex->ev_sets) {
-        ORB_HIP_TRY(hipEventSynchronize(set[kStages]));
+        for (int i = kStages; i >= 0; i--)
+            if (set[i]) { ORB_HIP_TRY(hipEventSynchronize(set[i])); break; }
         for (int i = 0; i < kStages; i++) {
+            if (!set[i] || !set[i + 1]) continue;   // mode 2 records stage 1 only
             float t = 0.f;
             ORB_HIP_TRY(hipEventElapsedTime(&t, set[i], set[i + 1]));
             ex->stage_ms[i] += t;
         }
         ex->stage_calls++;
-        for (auto e : set) ex->ev_pool.push_back(e);
+        for (auto e : set)
+            if (e) ex->ev_pool.push_back(e);
     }
     ex->ev_sets.clear();
     for (int i = 0; i < n_stages && i < kStages; i++) ms[i] = ex->stage_ms[i];
