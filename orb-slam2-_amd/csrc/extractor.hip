@@ -322,6 +322,198 @@ __global__ __launch_bounds__(256) void k_resize(Geom g, int l, uint8_t* __restri
     }
 }
 
+// ------------------------------------------------------------------ A2: whole pyramid in one launch
+//
+// ComputePyramid (R/src/ORBextractor.cpp:1197-1229) for all levels in one launch: a workgroup owns
+// one band of one frame.  Bands partition the rows of the last level; going down the pyramid, a
+// band's range at level l-1 is exactly the source rows its level-l range reads (cv::resize's row
+// pair of the first and last row), so a workgroup computes every level of its band from its own
+// LDS copy of the level below.  Neighbouring bands recompute the few rows where their ranges
+// overlap (the same arithmetic on the same source bytes, so both write identical values), and the
+// ranges of all bands cover every row of every level (checked on the host; otherwise the per-level
+// k_resize launches are used).  Level 0 is staged from the caller's frames (written into the
+// pitched slab on the way when they are not already there, replacing a separate copy kernel).
+struct PyrBand {
+    int s0, n;   // rows [s0, s0 + n) of a level computed by a band
+};
+
+__global__ __launch_bounds__(256) void k_pyramid(Geom g, const uint8_t* __restrict__ src, long long srcFrameStride,
+                                                 int srcRowStride, int writeL0, uint8_t* __restrict__ pyr,
+                                                 const uint2* __restrict__ rztab, const PyrBand* __restrict__ bands,
+                                                 int nBands, int bufABytes, int bufBBytes, int* __restrict__ status) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t pyr_sm[];
+    const int tid = threadIdx.x;
+    int k, b;
+    xcd_block_2d(k, b);
+    uint8_t* bufA = reinterpret_cast<uint8_t*>(pyr_sm);
+    uint8_t* bufB = bufA + bufABytes;   // even levels in A, odd levels in B
+    uint2* tabL = reinterpret_cast<uint2*>(bufB + bufBBytes);   // this level's column then row coefficients
+    uint8_t* slab = pyr + (size_t)b * g.frameBytes;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) *status = 0;   // this call's status word
+#ifdef ORB_TIMING
+    long long tl[9];
+    tl[0] = clock64();
+#endif
+    // ---- level 0 rows of this band -> LDS (row pitch rounded to a dword), and into the slab
+    {
+        const LevelGeom& L = g.lv[0];
+        const PyrBand bd = bands[k];
+        const int wq = (L.w + 3) >> 2;   // dwords per LDS row
+        const uint8_t* s = src + (size_t)b * srcFrameStride;
+        uint32_t* dst32 = reinterpret_cast<uint32_t*>(bufA);
+        if ((L.w & 15) == 0 && ((srcRowStride | (int)((uintptr_t)s & 15)) & 15) == 0) {
+            // 16-byte rows: eight uint4 loads in flight per thread
+            const int w16 = L.w >> 4, items = bd.n * w16;
+            for (int t0 = 0; t0 < items; t0 += 256 * 8) {
+                uint4 v[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int t = min(t0 + u * 256 + tid, items - 1);
+                    const int r = t / w16, q = t - r * w16;
+                    v[u] = *reinterpret_cast<const uint4*>(s + (size_t)(bd.s0 + r) * srcRowStride + 16 * q);
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int t = t0 + u * 256 + tid;
+                    if (t < items) {
+                        const int r = t / w16, q = t - r * w16;
+                        *reinterpret_cast<uint4*>(bufA + r * (wq * 4) + 16 * q) = v[u];
+                        if (writeL0) *reinterpret_cast<uint4*>(slab + L.off + (size_t)(bd.s0 + r) * L.pitch + 16 * q) = v[u];
+                    }
+                }
+            }
+        } else {
+        const int items = bd.n * wq;
+        for (int t0 = 0; t0 < items; t0 += 256 * 4) {
+            uint32_t v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                // unconditional: item clamped into the band (all loads in flight together)
+                const int t = min(t0 + u * 256 + tid, items - 1);
+                const int r = t / wq, q = t - r * wq;
+                const uint8_t* row = s + (size_t)(bd.s0 + r) * srcRowStride;
+                const int x = 4 * q;
+                if (x + 4 <= L.w && ((srcRowStride | (int)(uintptr_t)s) & 3) == 0) {
+                    v[u] = *reinterpret_cast<const uint32_t*>(row + x);
+                } else {
+                    uint32_t w = 0;
+                    for (int j = 0; j < 4; j++)
+                        if (x + j < L.w) w |= (uint32_t)row[x + j] << (8 * j);
+                    v[u] = w;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int t = t0 + u * 256 + tid;
+                if (t < items) {
+                    dst32[t] = v[u];
+                    if (writeL0) {
+                        const int r = t / wq, q = t - r * wq;
+                        *reinterpret_cast<uint32_t*>(slab + L.off + (size_t)(bd.s0 + r) * L.pitch + 4 * q) = v[u];
+                    }
+                }
+            }
+        }
+        }
+    }
+    __syncthreads();
+#ifdef ORB_TIMING
+    tl[1] = clock64();
+#endif
+    // ---- levels 1 .. nlevels-1: task = (row, group of 4 output columns), columns fastest (the
+    //      dword stores of a wave are contiguous); the column / row coefficient tables are L1-hot
+    uint8_t* cur = bufA;
+    uint8_t* nxt = bufB;
+    for (int l = 1; l < g.nlevels; l++) {
+        const LevelGeom& D = g.lv[l];
+        const LevelGeom& S = g.lv[l - 1];
+        const PyrBand sb = bands[(l - 1) * nBands + k], db = bands[l * nBands + k];
+        const int sp = ((S.w + 3) >> 2) << 2, dp = ((D.w + 3) >> 2) << 2;   // LDS row pitches
+        const int G = (D.w + 3) >> 2;   // column groups
+        uint8_t* out = slab + D.off;
+        // the level's column coefficients and the band's row coefficients -> LDS
+        uint2* XT = tabL;
+        uint2* YT = tabL + D.w;
+        for (int i = tid; i < D.w + db.n; i += 256)
+            tabL[i] = i < D.w ? rztab[D.rzX + i] : rztab[D.rzY + db.s0 + (i - D.w)];
+        __syncthreads();
+        // thread = (column group cg, row phase rp): the group's column coefficients stay in
+        // registers while the thread walks rows rp, rp + 4, ... two at a time
+        for (int pr = tid; pr < 4 * G; pr += 256) {
+            const int rp = pr / G, cg = pr - rp * G;
+            const int dx0 = 4 * cg;
+            // the group's source bytes x0[j], x1[j] lie in an 8-byte window starting at x0[0]
+            // (host-checked span): per row three aligned dwords, two alignbytes re-base the window
+            // at x0[0] and two v_perm gather the four x0 and the four x1 bytes; the weights stay
+            // in registers and SDWA byte selects feed the 24-bit multiplies
+            uint32_t a0[4], a1[4], sel0 = 0, sel1 = 0;
+            const int xb = (int)(XT[min(dx0, D.w - 1)].x & 0xFFFF);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint2 c = XT[min(dx0 + j, D.w - 1)];
+                sel0 |= (uint32_t)((int)(c.x & 0xFFFF) - xb) << (8 * j);
+                sel1 |= (uint32_t)((int)(c.x >> 16) - xb) << (8 * j);
+                a0[j] = c.y & 0xFFFF;
+                a1[j] = c.y >> 16;
+            }
+            const int dw = xb >> 2;
+            const uint32_t sh = (uint32_t)(xb & 3);
+            const int valid = D.w - dx0;   // pitch padding stays 0
+            const uint32_t keep = valid < 4 ? (1u << (8 * valid)) - 1u : 0xFFFFFFFFu;
+            for (int r = rp; r < db.n; r += 8) {
+                const int rr[2] = {r, min(r + 4, db.n - 1)};
+                uint2 cy[2];
+#pragma unroll
+                for (int u = 0; u < 2; u++) cy[u] = YT[rr[u]];
+                uint32_t g0[2][2], g1[2][2];   // [row pair u][source row 0/1]: x0 bytes, x1 bytes
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const uint32_t sy = h ? (cy[u].x >> 16) : (cy[u].x & 0xFFFF);
+                        const uint32_t* R = reinterpret_cast<const uint32_t*>(cur + __umul24(sy - (uint32_t)sb.s0, (uint32_t)sp)) + dw;
+                        const uint32_t d0 = R[0], d1 = R[1], d2 = R[2];
+                        const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh), w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+                        g0[u][h] = __builtin_amdgcn_perm(w1, w0, sel0);
+                        g1[u][h] = __builtin_amdgcn_perm(w1, w0, sel1);
+                    }
+                }
+                uint32_t packed[2] = {0u, 0u};
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    const uint32_t b0 = cy[u].y & 0xFFFF, b1 = cy[u].y >> 16;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        // every product fits 24 x 24 -> 32 bits (bytes x 11-bit weights, 19-bit sums
+                        // x 11-bit weights): v_mad_u32_u24, not the quarter-rate v_mul_lo_u32
+                        const uint32_t v0 = __umul24((g0[u][0] >> (8 * j)) & 0xFFu, a0[j]) + __umul24((g1[u][0] >> (8 * j)) & 0xFFu, a1[j]);
+                        const uint32_t v1 = __umul24((g0[u][1] >> (8 * j)) & 0xFFu, a0[j]) + __umul24((g1[u][1] >> (8 * j)) & 0xFFu, a1[j]);
+                        const uint32_t v = min((__umul24(v0, b0) + __umul24(v1, b1) + (1u << 21)) >> 22, 255u);
+                        packed[u] |= v << (8 * j);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    if (u == 1 && r + 4 >= db.n) break;
+                    const uint32_t pv = packed[u] & keep;
+                    *reinterpret_cast<uint32_t*>(nxt + rr[u] * dp + dx0) = pv;
+                    *reinterpret_cast<uint32_t*>(out + (size_t)(db.s0 + rr[u]) * D.pitch + dx0) = pv;
+                }
+            }
+        }
+        __syncthreads();   // (also: the coefficient tables are rewritten by the next level)
+        uint8_t* t = cur; cur = nxt; nxt = t;
+#ifdef ORB_TIMING
+        tl[l + 1] = clock64();
+#endif
+    }
+#ifdef ORB_TIMING
+    if (tid == 0 && b == 0 && (k == 0 || k == 7))
+        printf("pyramid band %d: L0 %lld L1 %lld L2 %lld L3 %lld L4 %lld L5 %lld L6 %lld L7 %lld\n", k, tl[1] - tl[0],
+               tl[2] - tl[1], tl[3] - tl[2], tl[4] - tl[3], tl[5] - tl[4], tl[6] - tl[5], tl[7] - tl[6], tl[8] - tl[7]);
+#endif
+}
+
 // ------------------------------------------------------------------ A3: FAST score
 
 // S = max over the 16 circular 9-arcs of min(v - p) (dark) or min(p - v) (bright), minus 1.
@@ -1675,6 +1867,8 @@ struct orb_extractor {
     int gw = -1, gh = -1;
     int blurK[4];
     uint2* d_rztab = nullptr;        // resize coefficient tables of the current geometry
+    PyrBand* d_bands = nullptr;      // k_pyramid band table [level][band] (nullptr: per-level k_resize)
+    int nBands = 0, pyrBufA = 0, pyrBufB = 0, pyrTab = 0;
     // stereo scratch (orb_compute_stereo_matches*)
     void* d_st = nullptr;
     size_t st_bytes = 0;
@@ -1748,9 +1942,79 @@ static int ensure_geom(orb_extractor* ex, int w, int h) {
     }
     ORB_HIP_TRY(hipSetDevice(ex->device));
     if (ex->d_rztab) (void)hipFree(ex->d_rztab);
+    if (ex->d_bands) (void)hipFree(ex->d_bands);
     ex->d_rztab = nullptr;
     if (hipMalloc((void**)&ex->d_rztab, std::max<size_t>(tab.size(), 1) * sizeof(uint2)) != hipSuccess) return ORB_ENOMEM;
     ORB_HIP_TRY(hipMemcpy(ex->d_rztab, tab.data(), tab.size() * sizeof(uint2), hipMemcpyHostToDevice));
+    // k_pyramid bands: the fewest bands whose two LDS level buffers fit 52 KB (three workgroups
+    // per CU), with every row of every level covered; none -> the per-level k_resize launches
+    if (ex->d_bands) (void)hipFree(ex->d_bands);
+    ex->d_bands = nullptr;
+    ex->nBands = 0;
+    {
+        const int nl = g.nlevels, Hl = g.lv[nl - 1].h;
+        std::vector<PyrBand> best;
+        int bestK = 0, bestA = 0, bestB = 0, bestT = 0;
+        // k_pyramid gathers a 4-column group's source bytes from an 8-byte window at its first
+        // column (scale factors up to ~1.9); wider spans keep the per-level launches
+        bool spanOk = true;
+        for (int l = 1; l < nl; l++) {
+            const uint2* XT = tab.data() + g.lv[l].rzX;
+            for (int x = 0; x < g.lv[l].w; x += 4) {
+                const int xb = (int)(XT[x].x & 0xFFFF);
+                for (int j = 0; j < 4; j++) {
+                    const uint2 c = XT[std::min(x + j, g.lv[l].w - 1)];
+                    if ((int)(c.x & 0xFFFF) - xb > 7 || (int)(c.x >> 16) - xb > 7 || (int)(c.x & 0xFFFF) < xb) spanOk = false;
+                }
+            }
+        }
+        for (int K = 8; spanOk && K <= std::min(64, Hl) && bestK == 0; K++) {
+            std::vector<PyrBand> bt((size_t)nl * K);
+            for (int k = 0; k < K; k++) {
+                int a = (int)((long long)k * Hl / K), e = (int)((long long)(k + 1) * Hl / K);
+                bt[(size_t)(nl - 1) * K + k] = {a, e - a};
+                for (int l = nl - 1; l >= 1; l--) {   // source rows of [a, e) at level l
+                    const uint2* YT = tab.data() + g.lv[l].rzY;
+                    const int lo = (int)(YT[a].x & 0xFFFF), hi = (int)(YT[e - 1].x >> 16);
+                    a = lo;
+                    e = hi + 1;
+                    bt[(size_t)(l - 1) * K + k] = {a, e - a};
+                }
+            }
+            bool ok = true;
+            int bufA = 0, bufB = 0;
+            for (int l = 0; l < nl && ok; l++) {
+                int end = 0;
+                for (int k = 0; k < K; k++) {
+                    const PyrBand& p = bt[(size_t)l * K + k];
+                    if (p.n <= 0 || p.s0 > end) ok = false;
+                    end = std::max(end, p.s0 + p.n);
+                    const int bytes = p.n * (((g.lv[l].w + 3) >> 2) << 2);
+                    if (l % 2 == 0) bufA = std::max(bufA, bytes); else bufB = std::max(bufB, bytes);
+                }
+                if (end != g.lv[l].h || bt[(size_t)l * K].s0 != 0) ok = false;
+            }
+            bufA = (bufA + 15 + 16) & ~15;   // +16: the last row's third dword read may pass the row
+            bufB = (bufB + 15 + 16) & ~15;
+            int tabBytes = 0;   // per-level coefficient tables staged next to the buffers
+            for (int l = 1; l < nl; l++) {
+                int maxN = 0;
+                for (int k = 0; k < K; k++) maxN = std::max(maxN, bt[(size_t)l * K + k].n);
+                tabBytes = std::max(tabBytes, 8 * (g.lv[l].w + maxN));
+            }
+            if (ok && bufA + bufB + tabBytes <= 52 * 1024) {
+                best = bt; bestK = K; bestA = bufA; bestB = bufB; bestT = tabBytes;
+            }
+        }
+        if (bestK > 0) {
+            if (hipMalloc((void**)&ex->d_bands, best.size() * sizeof(PyrBand)) != hipSuccess) return ORB_ENOMEM;
+            ORB_HIP_TRY(hipMemcpy(ex->d_bands, best.data(), best.size() * sizeof(PyrBand), hipMemcpyHostToDevice));
+            ex->nBands = bestK;
+            ex->pyrBufA = bestA;
+            ex->pyrBufB = bestB;
+            ex->pyrTab = bestT;
+        }
+    }
     ex->g = g;
     ex->gw = w;
     ex->gh = h;
@@ -1820,8 +2084,10 @@ static hipEvent_t ev_get(orb_extractor* ex) {
 }
 
 // Enqueues the full pipeline for B frames already resident in d_pyr level 0.
-static int run_pipeline(orb_extractor* ex, int B, orb_keypoint* d_kps, uint8_t* d_desc, int cap, int32_t* d_counts,
-                        hipStream_t st) {
+// Level 0 of frame b is read from src + b * srcFrameStride (rows srcRowStride bytes apart); when it
+// is not the slab itself (writeL0) it is also written into the slab's pitched level 0.
+static int run_pipeline(orb_extractor* ex, int B, const uint8_t* src, long long srcFrameStride, int srcRowStride,
+                        int writeL0, orb_keypoint* d_kps, uint8_t* d_desc, int cap, int32_t* d_counts, hipStream_t st) {
     const Geom& g = ex->g;
     std::array<hipEvent_t, kStages + 1> ev{};
     const int prof = ex->profile;
@@ -1835,17 +2101,32 @@ static int run_pipeline(orb_extractor* ex, int B, orb_keypoint* d_kps, uint8_t* 
     auto mark = [&](int i) {
         if (prof && ev[i]) (void)hipEventRecord(ev[i], st);
     };
-    ORB_HIP_TRY(hipMemsetAsync(ex->d_status, 0, 4, st));
     mark(0);
-    for (int l = 1; l < g.nlevels; l++) {
-        const LevelGeom& L = g.lv[l];
-        // source window bound of one 256 x 16 block: ceil(256 * rsx) + 2 columns (+3 for dword
-        // alignment), ceil(16 * rsy) + 2 rows
-        const int srcW32 = (int)std::ceil(kRzCols * L.rsx) / 4 + 3;
-        const int srcRows = (int)std::ceil(kRzRows * L.rsy) + 3;
-        dim3 grid((L.w + kRzCols - 1) / kRzCols, (L.h + kRzRows - 1) / kRzRows, B);
-        hipLaunchKernelGGL(k_resize, grid, dim3(256), (size_t)srcW32 * srcRows * 4, st, g, l, ex->d_pyr, ex->d_rztab,
-                           srcW32, srcRows);
+    if (ex->d_bands) {
+        // whole pyramid (and the level-0 copy) in one launch; it also clears the status word
+        hipLaunchKernelGGL(k_pyramid, dim3(ex->nBands, B), dim3(256), (size_t)(ex->pyrBufA + ex->pyrBufB + ex->pyrTab),
+                           st, g, src, srcFrameStride, srcRowStride, writeL0, ex->d_pyr, ex->d_rztab, ex->d_bands,
+                           ex->nBands, ex->pyrBufA, ex->pyrBufB, ex->d_status);
+    } else {
+        ORB_HIP_TRY(hipMemsetAsync(ex->d_status, 0, 4, st));
+        if (writeL0) {
+            const int w = g.lv[0].w, h = g.lv[0].h;
+            const int vec16 = (w % 16 == 0) && (srcRowStride == w) && (srcFrameStride % 16 == 0) &&
+                              ((uintptr_t)src % 16 == 0);
+            const int items = vec16 ? (w / 16) * h : ((w + 3) / 4) * h;
+            hipLaunchKernelGGL(k_load_frames, dim3((items + 255) / 256, B), dim3(256), 0, st, g, src,
+                               (size_t)srcFrameStride, ex->d_pyr, vec16);
+        }
+        for (int l = 1; l < g.nlevels; l++) {
+            const LevelGeom& L = g.lv[l];
+            // source window bound of one 256 x 16 block: ceil(256 * rsx) + 2 columns (+3 for dword
+            // alignment), ceil(16 * rsy) + 2 rows
+            const int srcW32 = (int)std::ceil(kRzCols * L.rsx) / 4 + 3;
+            const int srcRows = (int)std::ceil(kRzRows * L.rsy) + 3;
+            dim3 grid((L.w + kRzCols - 1) / kRzCols, (L.h + kRzRows - 1) / kRzRows, B);
+            hipLaunchKernelGGL(k_resize, grid, dim3(256), (size_t)srcW32 * srcRows * 4, st, g, l, ex->d_pyr,
+                               ex->d_rztab, srcW32, srcRows);
+        }
     }
     mark(1);
     {
@@ -1932,6 +2213,7 @@ void orb_extractor_destroy(orb_extractor* ex) {
     if (ex->stream) (void)hipStreamSynchronize(ex->stream);
     release_buffers(ex);
     if (ex->d_rztab) (void)hipFree(ex->d_rztab);
+    if (ex->d_bands) (void)hipFree(ex->d_bands);
     if (ex->d_st) (void)hipFree(ex->d_st);
     if (ex->h_st) (void)hipHostFree(ex->h_st);
     for (auto& set : ex->ev_sets)
@@ -1986,7 +2268,8 @@ int orb_extract(orb_extractor* ex, const uint8_t* img, int w, int h, size_t stri
     for (int y = 0; y < h; y++) std::memcpy(ex->h_stage + (size_t)y * L0.pitch, img + (size_t)y * stride, (size_t)w);
     ORB_HIP_TRY(hipMemcpyAsync(ex->d_pyr + L0.off, ex->h_stage, imgBytes, hipMemcpyHostToDevice, ex->stream));
     const int cap = (int)ex->capHostOut;
-    st = run_pipeline(ex, 1, ex->d_kps, ex->d_desc, cap, ex->d_counts, ex->stream);
+    st = run_pipeline(ex, 1, ex->d_pyr + L0.off, g.frameBytes, L0.pitch, 0, ex->d_kps, ex->d_desc, cap, ex->d_counts,
+                      ex->stream);
     if (st) return st;
     st = ensure_pinned(&ex->h_out, &ex->h_out_bytes, 64 + (size_t)cap * (sizeof(orb_keypoint) + 32));
     if (st) return st;
@@ -2026,14 +2309,9 @@ int orb_extract_batch_device(orb_extractor* ex, const uint8_t* d_imgs, size_t im
     if (st) return st;
     hipStream_t s = stream ? (hipStream_t)stream : ex->stream;
     const Geom& g = ex->g;
-    const int vec16 = (w % 16 == 0) && (img_stride_frame % 16 == 0) && ((uintptr_t)d_imgs % 16 == 0);
-    const int items = vec16 ? (w / 16) * h : ((w + 3) / 4) * h;
-    hipLaunchKernelGGL(k_load_frames, dim3((items + 255) / 256, B), dim3(256), 0, s, g, d_imgs, img_stride_frame,
-                       ex->d_pyr, vec16);
-    ORB_HIP_TRY(hipGetLastError());
     ex->lastB = B;
     ex->h_level_valid.assign((size_t)B * g.nlevels, 0);
-    return run_pipeline(ex, B, d_kps, d_desc, cap, d_counts, s);
+    return run_pipeline(ex, B, d_imgs, (long long)img_stride_frame, w, 1, d_kps, d_desc, cap, d_counts, s);
 }
 
 int orb_extractor_batch_status(orb_extractor* ex, int32_t* status) {
