@@ -637,6 +637,64 @@ static void orb_descriptor(const oracle_keypoint* kpt, const uint8_t* img, size_
 
 typedef struct { float x, y, resp; } okey;
 
+/* ComputeKeyPointsOctTree's cell loop for one level (R/src/ORBextractor.cpp:819-896): FAST per
+ * 30-px cell window at iniThFAST, minThFAST when the cell yields none; keys in vToDistributeKeys
+ * order (cell rows, then cells, then cv::FAST's raster order), coordinates relative to the
+ * 16-px border.  *out is malloc'ed; returns the count. */
+static int level_fast_keys(const oracle_orb_params* p, const uint8_t* img, int cols, int rows, okey** out)
+{
+    const float W = 30;
+    const int minBorderX = EDGE_THRESHOLD - 3, minBorderY = minBorderX;
+    const int maxBorderX = cols - EDGE_THRESHOLD + 3, maxBorderY = rows - EDGE_THRESHOLD + 3;
+    int capk = 4096, nk = 0;
+    okey* keys = (okey*)malloc(sizeof(okey) * capk);
+    const float width = (float)(maxBorderX - minBorderX);
+    const float height = (float)(maxBorderY - minBorderY);
+    const int nCols = (int)(width / W);
+    const int nRows = (int)(height / W);
+    const int wCell = (int)ceilf(width / (float)nCols);
+    const int hCell = (int)ceilf(height / (float)nRows);
+    int cellbuf_cap = 64 * 64 * 3;
+    int* cellbuf = (int*)malloc(sizeof(int) * cellbuf_cap);
+    for (int i = 0; i < nRows; i++) {
+        const float iniY = (float)(minBorderY + i * hCell);
+        float maxY = iniY + (float)hCell + 6;
+        if (iniY >= (float)(maxBorderY - 3)) continue;
+        if (maxY > (float)maxBorderY) maxY = (float)maxBorderY;
+        for (int j = 0; j < nCols; j++) {
+            const float iniX = (float)(minBorderX + j * wCell);
+            float maxX = iniX + (float)wCell + 6;
+            if (iniX >= (float)(maxBorderX - 6)) continue;
+            if (maxX > (float)maxBorderX) maxX = (float)maxBorderX;
+            const int rx0 = (int)iniX, ry0 = (int)iniY;
+            const int rw = (int)maxX - rx0, rh = (int)maxY - ry0;
+            int nc = oracle_fast_roi(img, (size_t)cols, rx0, ry0, rw, rh, p->iniThFAST, cellbuf, cellbuf_cap / 3);
+            if (nc == 0)
+                nc = oracle_fast_roi(img, (size_t)cols, rx0, ry0, rw, rh, p->minThFAST, cellbuf, cellbuf_cap / 3);
+            for (int q = 0; q < nc; q++) {
+                if (nk == capk) { capk *= 2; keys = (okey*)realloc(keys, sizeof(okey) * capk); }
+                keys[nk].x = (float)cellbuf[3 * q] + (float)(j * wCell);
+                keys[nk].y = (float)cellbuf[3 * q + 1] + (float)(i * hCell);
+                keys[nk].resp = (float)cellbuf[3 * q + 2];
+                nk++;
+            }
+        }
+    }
+    free(cellbuf);
+    *out = keys;
+    return nk;
+}
+
+int oracle_level_keys(const oracle_orb_params* p, const uint8_t* img, int cols, int rows, float* kx, float* ky,
+                      float* kr, int cap)
+{
+    okey* keys = NULL;
+    const int nk = level_fast_keys(p, img, cols, rows, &keys);
+    for (int q = 0; q < nk && q < cap; q++) { kx[q] = keys[q].x; ky[q] = keys[q].y; kr[q] = keys[q].resp; }
+    free(keys);
+    return nk;
+}
+
 int oracle_orb_extract(const oracle_orb_params* p, const uint8_t* img, int w, int h, size_t stride,
                        oracle_keypoint* kps, uint8_t* desc, int capacity, int* n_out,
                        int* level_counts, int* pre_counts, uint8_t* pyramid, uint8_t* blurred)
@@ -663,46 +721,12 @@ int oracle_orb_extract(const oracle_orb_params* p, const uint8_t* img, int w, in
     /* A3/A4 per level */
     oracle_keypoint* all[MAX_LEVELS];
     int nall[MAX_LEVELS];
-    const float W = 30;
     for (int l = 0; l < nl; l++) {
         const int cols = lw[l], rows = lh[l];
         const int minBorderX = EDGE_THRESHOLD - 3, minBorderY = minBorderX;
         const int maxBorderX = cols - EDGE_THRESHOLD + 3, maxBorderY = rows - EDGE_THRESHOLD + 3;
-        int capk = 4096, nk = 0;
-        okey* keys = (okey*)malloc(sizeof(okey) * capk);
-        const float width = (float)(maxBorderX - minBorderX);
-        const float height = (float)(maxBorderY - minBorderY);
-        const int nCols = (int)(width / W);
-        const int nRows = (int)(height / W);
-        const int wCell = (int)ceilf(width / (float)nCols);
-        const int hCell = (int)ceilf(height / (float)nRows);
-        int cellbuf_cap = 64 * 64 * 3;
-        int* cellbuf = (int*)malloc(sizeof(int) * cellbuf_cap);
-        for (int i = 0; i < nRows; i++) {
-            const float iniY = (float)(minBorderY + i * hCell);
-            float maxY = iniY + (float)hCell + 6;
-            if (iniY >= (float)(maxBorderY - 3)) continue;
-            if (maxY > (float)maxBorderY) maxY = (float)maxBorderY;
-            for (int j = 0; j < nCols; j++) {
-                const float iniX = (float)(minBorderX + j * wCell);
-                float maxX = iniX + (float)wCell + 6;
-                if (iniX >= (float)(maxBorderX - 6)) continue;
-                if (maxX > (float)maxBorderX) maxX = (float)maxBorderX;
-                const int rx0 = (int)iniX, ry0 = (int)iniY;
-                const int rw = (int)maxX - rx0, rh = (int)maxY - ry0;
-                int nc = oracle_fast_roi(lvl[l], (size_t)cols, rx0, ry0, rw, rh, p->iniThFAST, cellbuf, cellbuf_cap / 3);
-                if (nc == 0)
-                    nc = oracle_fast_roi(lvl[l], (size_t)cols, rx0, ry0, rw, rh, p->minThFAST, cellbuf, cellbuf_cap / 3);
-                for (int q = 0; q < nc; q++) {
-                    if (nk == capk) { capk *= 2; keys = (okey*)realloc(keys, sizeof(okey) * capk); }
-                    keys[nk].x = (float)cellbuf[3 * q] + (float)(j * wCell);
-                    keys[nk].y = (float)cellbuf[3 * q + 1] + (float)(i * hCell);
-                    keys[nk].resp = (float)cellbuf[3 * q + 2];
-                    nk++;
-                }
-            }
-        }
-        free(cellbuf);
+        okey* keys = NULL;
+        const int nk = level_fast_keys(p, lvl[l], cols, rows, &keys);
         if (pre_counts) pre_counts[l] = nk;
         float* kx = (float*)malloc(sizeof(float) * (nk + 1));
         float* ky = (float*)malloc(sizeof(float) * (nk + 1));

@@ -84,6 +84,11 @@ int oracle_orb_extract(const oracle_orb_params* p, const uint8_t* img, int w, in
                        oracle_keypoint* kps, uint8_t* desc, int capacity, int* n_out,
                        int* level_counts, int* pre_counts, uint8_t* pyramid, uint8_t* blurred);
 
+/* One level's FAST keys before DistributeOctTree (the cell loop of R/src/ORBextractor.cpp:819-896),
+ * in vToDistributeKeys order, border-relative; returns the count (only the first cap written). */
+int oracle_level_keys(const oracle_orb_params* p, const uint8_t* img, int cols, int rows, float* kx, float* ky,
+                      float* kr, int cap);
+
 /* DistributeOctTree on explicit inputs (for unit tests): keys are (x,y,response)
  * triples in level-interior coordinates; writes the indices of the retained keys
  * (into the input array) in output order; returns count. */
