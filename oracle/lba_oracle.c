@@ -958,6 +958,7 @@ typedef struct {
     double H[36], b[6], x[6];
     double lambda, ni;
     int nBad;
+    int g2o_order;         /* 1: every sum in edge order, as g2o accumulates (no GPU reduction shape) */
 } pose_ctx;
 
 static void pose_compute_error(pose_ctx* c, int e)
@@ -1031,6 +1032,15 @@ static double pose_block_sum(double* th /* [256] per-thread partials */)
 
 static double pose_active_errors(pose_ctx* c)
 {   /* computeActiveErrors + activeRobustChi2 */
+    if (c->g2o_order) {   /* G/core/sparse_optimizer.cpp activeRobustChi2: edges in order */
+        double s = 0;
+        for (int e = 0; e < c->p->n; e++) {
+            if (c->level[e]) continue;
+            pose_compute_error(c, e);
+            s += pose_robust_chi2(c, e);
+        }
+        return s;
+    }
     double th[POSE_T] = {0};
     for (int e = 0; e < c->p->n; e++) {
         if (c->level[e]) continue;
@@ -1048,10 +1058,13 @@ static void pose_build_system(pose_ctx* c)
     const pose_problem_t* p = c->p;
     double part[27][POSE_T];   /* 55 KB on the stack: the oracle runs one frame per thread in bench.py */
     memset(part, 0, sizeof(part));
+    double seqsum[27] = {0};   /* g2o order: each edge's 6x6 / 6 terms added to the vertex in edge order */
     for (int e = 0; e < p->n; e++) {
         if (c->level[e]) continue;
         double* acc = NULL;
         const int th = e % POSE_T;
+        double* col[27];
+        for (int v = 0; v < 27; v++) col[v] = c->g2o_order ? &seqsum[v] : &part[v][th];
         const double* X = p->xw + 3 * e;
         double Xc[3];
         quat_rot(c->q, X, Xc);
@@ -1083,16 +1096,17 @@ static void pose_build_system(pose_ctx* c)
         for (int i = 0; i < 6; i++) {   /* all three rows: a mono edge's third row adds exact zeros */
             double sb = 0;
             for (int r = 0; r < 3; r++) sb += J[r * 6 + i] * om[r];
-            part[21 + i][th] += sb;
+            *col[21 + i] += sb;
             for (int j = i; j < 6; j++) {
                 double h = 0;
                 for (int r = 0; r < 3; r++) h += J[r * 6 + i] * W * J[r * 6 + j];
-                part[o++][th] += h;
+                *col[o++] += h;
             }
         }
     }
     double res[27];
-    for (int v = 0; v < 27; v++) {
+    for (int v = 0; v < 27 && c->g2o_order; v++) res[v] = seqsum[v];
+    for (int v = 0; v < 27 && !c->g2o_order; v++) {
         double g[8];
         for (int k = 0; k < 8; k++) {
             double sg = 0.0;
@@ -1201,7 +1215,16 @@ static int pose_lm_iteration(pose_ctx* c, int iteration, pose_result_t* r)
     return LM_OK;
 }
 
-int oracle_pose_optimization(const pose_problem_t* p, pose_result_t* r)
+static int pose_optimization(const pose_problem_t* p, pose_result_t* r, int g2o_order);
+
+int oracle_pose_optimization(const pose_problem_t* p, pose_result_t* r) { return pose_optimization(p, r, 0); }
+
+/* The same with g2o's summation order (edges accumulated in order, G/core/sparse_optimizer.cpp
+ * activeRobustChi2 and BlockSolver::buildSystem over the unary edges): the reference's own order,
+ * against which the GPU's (reduction-shaped) decisions are compared in tests/test_pose_gpu.py. */
+int oracle_pose_optimization_g2o_order(const pose_problem_t* p, pose_result_t* r) { return pose_optimization(p, r, 1); }
+
+static int pose_optimization(const pose_problem_t* p, pose_result_t* r, int g2o_order)
 {
     const int n = p->n;
     memcpy(r->pose_q, p->pose_q, sizeof(r->pose_q));
@@ -1214,6 +1237,7 @@ int oracle_pose_optimization(const pose_problem_t* p, pose_result_t* r)
     pose_ctx c;
     memset(&c, 0, sizeof(c));
     c.p = p;
+    c.g2o_order = g2o_order;
     c.level = (uint8_t*)calloc(n, 1);
     c.robust = (uint8_t*)malloc(n);
     c.err = (double*)calloc(3 * (size_t)n, sizeof(double));

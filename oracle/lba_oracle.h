@@ -113,6 +113,8 @@ typedef struct {
 } pose_result_t;
 
 int oracle_pose_optimization(const pose_problem_t* p, pose_result_t* r);
+/* g2o's summation order (edges in order) instead of the GPU kernel's reduction shape. */
+int oracle_pose_optimization_g2o_order(const pose_problem_t* p, pose_result_t* r);
 
 /* Helpers shared with tests: Converter::toSE3Quat / SE3Quat::exp semantics. */
 void oracle_quat_from_matrix(const double R[9], double q[4]);

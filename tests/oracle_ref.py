@@ -323,9 +323,10 @@ class PoseResult(C.Structure):
                 ("n_inliers", C.c_int), ("iterations", C.c_int * 4), ("trials", C.c_int)]
 
 
-def pose_optimization(frame):
+def pose_optimization(frame, g2o_order=False):
     """oracle_pose_optimization on one frame of synth.pose_problems: the optimised pose, the
-    mvbOutlier flags, the return value and per-round LM iterations."""
+    mvbOutlier flags, the return value and per-round LM iterations.  g2o_order: every sum in edge
+    order (oracle_pose_optimization_g2o_order) instead of the GPU kernel's reduction shape."""
     q, t = quat_from_Tcw(frame["Tcw"])
     obs = np.ascontiguousarray(frame["obs"], np.float64)
     xw = np.ascontiguousarray(frame["xw"], np.float64)
@@ -335,7 +336,7 @@ def pose_optimization(frame):
     out = np.zeros(n, np.uint8)
     r = PoseResult()
     r.outlier = P(out)
-    lib().oracle_pose_optimization(C.byref(pr), C.byref(r))
+    (lib().oracle_pose_optimization_g2o_order if g2o_order else lib().oracle_pose_optimization)(C.byref(pr), C.byref(r))
     return dict(pose_q=np.array(r.pose_q[:]), pose_t=np.array(r.pose_t[:]), outlier=out, n_inliers=r.n_inliers,
                 iterations=tuple(r.iterations), trials=r.trials)
 

@@ -54,3 +54,21 @@ def test_pose_optimization_large_batch(amd):
     for a, b in zip(all_[100:103], part):
         assert np.array_equal(a["pose_q"], b["pose_q"]) and np.array_equal(a["outlier"], b["outlier"])
     _check(amd, frames[::50])
+
+
+def test_pose_optimization_vs_g2o_summation_order(amd):
+    """The GPU against the oracle in g2o's own summation order (edges in order): the outcome
+    (outlier flags, inlier count) identical and poses within 1e-5 (north_star); LM trial counts
+    may differ where rho changes sign on a near-zero step (tests/test_pose_oracle_cpu.py), so
+    they are reported, not asserted."""
+    from orb_slam2_amd import synth
+    frames = synth.pose_problems(n_frames=64, n_points=600, stereo_frac=0.3, seed=21)
+    got = amd.PoseOptimization(frames)
+    same = 0
+    for f, g in zip(frames, got):
+        ref = O.pose_optimization(f, g2o_order=True)
+        assert np.array_equal(g["outlier"], ref["outlier"]) and g["n_inliers"] == ref["n_inliers"]
+        assert np.abs(g["pose_q"] - ref["pose_q"]).max() < 1e-5
+        assert np.abs(g["pose_t"] - ref["pose_t"]).max() < 1e-5
+        same += g["trials"] == ref["trials"] and g["iterations"] == ref["iterations"]
+    print(f"GPU vs g2o-order oracle: identical LM iterations and trials on {same}/{len(frames)} frames")
