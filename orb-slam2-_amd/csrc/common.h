@@ -2,8 +2,10 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <vector>
 
 #include "../../include/orbslam2_amd.h"
 
@@ -24,6 +26,43 @@ constexpr int kWave = 64;
 
 // Returns ORB_OK when a gfx950 device `dev` is usable, else ORB_ENODEV.
 int check_device(int dev);
+
+// Per-thread, per-device scratch of the handle-less host entry points (the LocalMapping,
+// LoopClosing and Tracking threads call the matchers and PoseOptimization concurrently): one
+// non-blocking stream and one grow-only device buffer per (host thread, device), so a call
+// allocates nothing, never hipFree-synchronises the device, and two threads never share a
+// buffer.  Kept for the thread's lifetime (no HIP calls from thread-exit destructors).
+struct HostScratch {
+    int device = -1;
+    hipStream_t stream = nullptr;
+    char* base = nullptr;
+    size_t cap = 0;
+};
+inline int host_scratch(int device, size_t bytes, HostScratch** out) {
+    thread_local std::vector<HostScratch*> pool;
+    HostScratch* h = nullptr;
+    for (HostScratch* p : pool)
+        if (p->device == device) h = p;
+    if (!h) {
+        h = new HostScratch();
+        h->device = device;
+        if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+            delete h;
+            return ORB_EGPU;
+        }
+        pool.push_back(h);
+    }
+    if (h->cap < bytes) {   // grow (rare): the stream is idle between calls of this thread
+        if (h->base) (void)hipFree(h->base);
+        h->base = nullptr;
+        h->cap = 0;
+        const size_t cap = std::max(bytes + bytes / 2, (size_t)1 << 20);
+        if (hipMalloc((void**)&h->base, cap) != hipSuccess) return ORB_ENOMEM;
+        h->cap = cap;
+    }
+    *out = h;
+    return ORB_OK;
+}
 
 // 8-bit row pitch used for every device image (multiple of 64 bytes).
 inline int pitch_of(int w) { return (w + 63) & ~63; }

@@ -2048,9 +2048,10 @@ int orb_distinctive_descriptors(int device, const uint8_t* desc, const int32_t* 
     char* base = nullptr;
     const size_t bD = ((T * 32 + 255) & ~(size_t)255), bS = (((size_t)n_points + 1) * 4 + 255) & ~(size_t)255,
                  bI = ((size_t)n_points * 4 + 255) & ~(size_t)255;
-    ORB_HIP_TRY(hipMalloc(&base, bD + bS + bI + (size_t)n_points * 32 + 256));
-    hipStream_t s = nullptr;
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) { (void)hipFree(base); return ORB_EGPU; }
+    HostScratch* hsc = nullptr;
+    if (int e_ = host_scratch(device, bD + bS + bI + (size_t)n_points * 32 + 256, &hsc)) return e_;
+    base = hsc->base;
+    hipStream_t s = hsc->stream;
     uint8_t* dD = (uint8_t*)base;
     int32_t* dS = (int32_t*)(base + bD);
     int32_t* dI = (int32_t*)(base + bD + bS);
@@ -2058,16 +2059,14 @@ int orb_distinctive_descriptors(int device, const uint8_t* desc, const int32_t* 
     std::vector<int32_t> rel((size_t)n_points + 1);
     for (int m = 0; m <= n_points; m++) rel[m] = start[m] - start[0];
     int rc = ORB_OK;
-    if (T) (void)hipMemcpyAsync(dD, desc + (size_t)start[0] * 32, T * 32, hipMemcpyHostToDevice, s);
-    (void)hipMemcpyAsync(dS, rel.data(), rel.size() * 4, hipMemcpyHostToDevice, s);
+    if (T) ORB_HIP_TRY(hipMemcpyAsync(dD, desc + (size_t)start[0] * 32, T * 32, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(dS, rel.data(), rel.size() * 4, hipMemcpyHostToDevice, s));
     rc = orb_distinctive_descriptors_device(dD, dS, n_points, dI, best_desc ? dB : nullptr, s);
     if (rc == ORB_OK) {
-        (void)hipMemcpyAsync(best_idx, dI, (size_t)n_points * 4, hipMemcpyDeviceToHost, s);
-        if (best_desc) (void)hipMemcpyAsync(best_desc, dB, (size_t)n_points * 32, hipMemcpyDeviceToHost, s);
+        ORB_HIP_TRY(hipMemcpyAsync(best_idx, dI, (size_t)n_points * 4, hipMemcpyDeviceToHost, s));
+        if (best_desc) ORB_HIP_TRY(hipMemcpyAsync(best_desc, dB, (size_t)n_points * 32, hipMemcpyDeviceToHost, s));
         if (hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
     }
-    (void)hipStreamDestroy(s);
-    (void)hipFree(base);
     return rc;
 }
 
@@ -2103,9 +2102,10 @@ static int fuse_impl(int device, const orb_frame_view* kf, const orb_kf_params* 
                  bV = al((size_t)n_mp), bX = al((size_t)n_mp * 12), bM = al((size_t)n_mp * 4), bMD = al((size_t)n_mp * 32),
                  bO = al((size_t)n_mp * 4);
     char* base = nullptr;
-    ORB_HIP_TRY(hipMalloc(&base, bK + bD + bU + bV + 2 * bX + 2 * bM + bMD + 2 * bO));
-    hipStream_t s = nullptr;
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) { (void)hipFree(base); return ORB_EGPU; }
+    HostScratch* hsc = nullptr;
+    if (int e_ = host_scratch(device, bK + bD + bU + bV + 2 * bX + 2 * bM + bMD + 2 * bO, &hsc)) return e_;
+    base = hsc->base;
+    hipStream_t s = hsc->stream;
     char* c = base;
     auto take = [&](size_t b) { char* r = c; c += b; return r; };
     orb_keypoint* dK = (orb_keypoint*)take(bK);
@@ -2120,27 +2120,25 @@ static int fuse_impl(int device, const orb_frame_view* kf, const orb_kf_params* 
     int32_t* dBI = (int32_t*)take(bO);
     int32_t* dBD = (int32_t*)take(bO);
     if (nk) {
-        (void)hipMemcpyAsync(dK, hk.data(), (size_t)nk * sizeof(orb_keypoint), hipMemcpyHostToDevice, s);
-        (void)hipMemcpyAsync(dD, kf->desc, (size_t)nk * 32, hipMemcpyHostToDevice, s);
-        if (kf->uright) (void)hipMemcpyAsync(dU, kf->uright, (size_t)nk * 4, hipMemcpyHostToDevice, s);
+        ORB_HIP_TRY(hipMemcpyAsync(dK, hk.data(), (size_t)nk * sizeof(orb_keypoint), hipMemcpyHostToDevice, s));
+        ORB_HIP_TRY(hipMemcpyAsync(dD, kf->desc, (size_t)nk * 32, hipMemcpyHostToDevice, s));
+        if (kf->uright) ORB_HIP_TRY(hipMemcpyAsync(dU, kf->uright, (size_t)nk * 4, hipMemcpyHostToDevice, s));
     }
-    (void)hipMemcpyAsync(dV, mp_valid, (size_t)n_mp, hipMemcpyHostToDevice, s);
-    (void)hipMemcpyAsync(dX, mp_xyz, (size_t)n_mp * 12, hipMemcpyHostToDevice, s);
-    (void)hipMemcpyAsync(dN, mp_normal, (size_t)n_mp * 12, hipMemcpyHostToDevice, s);
-    (void)hipMemcpyAsync(dMin, mp_min_dist, (size_t)n_mp * 4, hipMemcpyHostToDevice, s);
-    (void)hipMemcpyAsync(dMax, mp_max_dist, (size_t)n_mp * 4, hipMemcpyHostToDevice, s);
-    (void)hipMemcpyAsync(dMD, mp_desc, (size_t)n_mp * 32, hipMemcpyHostToDevice, s);
+    ORB_HIP_TRY(hipMemcpyAsync(dV, mp_valid, (size_t)n_mp, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(dX, mp_xyz, (size_t)n_mp * 12, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(dN, mp_normal, (size_t)n_mp * 12, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(dMin, mp_min_dist, (size_t)n_mp * 4, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(dMax, mp_max_dist, (size_t)n_mp * 4, hipMemcpyHostToDevice, s));
+    ORB_HIP_TRY(hipMemcpyAsync(dMD, mp_desc, (size_t)n_mp * 32, hipMemcpyHostToDevice, s));
     const GridParams g = grid_of(kf);
     hipLaunchKernelGGL(k_fuse, dim3((n_mp + 3) / 4), dim3(256), 0, s, dK, dD, kf->uright ? (const float*)dU : nullptr,
                        nk, g, K, n_mp, dV, dX, dN, dMin, dMax, dMD, th, dBI, dBD, sim3);
     int rc = hipGetLastError() == hipSuccess ? ORB_OK : ORB_EGPU;
     if (rc == ORB_OK) {
-        (void)hipMemcpyAsync(best_idx, dBI, (size_t)n_mp * 4, hipMemcpyDeviceToHost, s);
-        (void)hipMemcpyAsync(best_dist, dBD, (size_t)n_mp * 4, hipMemcpyDeviceToHost, s);
+        ORB_HIP_TRY(hipMemcpyAsync(best_idx, dBI, (size_t)n_mp * 4, hipMemcpyDeviceToHost, s));
+        ORB_HIP_TRY(hipMemcpyAsync(best_dist, dBD, (size_t)n_mp * 4, hipMemcpyDeviceToHost, s));
         if (hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
     }
-    (void)hipStreamDestroy(s);
-    (void)hipFree(base);
     return rc;
 }
 
@@ -2195,14 +2193,19 @@ int orb_search_by_sim3(int device, const orb_frame_view* kf1, const orb_frame_vi
     const size_t per2 = al((size_t)n2 * sizeof(orb_keypoint)) + al((size_t)n2 * 32) + al(n2) + al((size_t)n2 * 12) +
                         2 * al((size_t)n2 * 4) + al((size_t)n2 * 32) + al((size_t)n2 * 4);
     char* base = nullptr;
-    ORB_HIP_TRY(hipMalloc(&base, per1 + per2));
-    hipStream_t s = nullptr;
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) { (void)hipFree(base); return ORB_EGPU; }
+    HostScratch* hsc = nullptr;
+    if (int e_ = host_scratch(device, per1 + per2, &hsc)) return e_;
+    base = hsc->base;
+    hipStream_t s = hsc->stream;
     char* c = base;
+    hipError_t cpErr = hipSuccess;   // first failed upload, checked before the launch
     auto put = [&](const void* src, size_t bytes) {
         char* r = c;
         c += al(bytes);
-        if (src && bytes) (void)hipMemcpyAsync(r, src, bytes, hipMemcpyHostToDevice, s);
+        if (src && bytes) {
+            const hipError_t e = hipMemcpyAsync(r, src, bytes, hipMemcpyHostToDevice, s);
+            if (e != hipSuccess && cpErr == hipSuccess) cpErr = e;
+        }
         return r;
     };
     auto* dK1 = (orb_keypoint*)put(hk1.data(), (size_t)n1 * sizeof(orb_keypoint));
@@ -2221,6 +2224,7 @@ int orb_search_by_sim3(int device, const orb_frame_view* kf1, const orb_frame_vi
     auto* dMax2 = (float*)put(p2->max_dist, (size_t)n2 * 4);
     auto* dMD2 = (uint8_t*)put(p2->desc, (size_t)n2 * 32);
     auto* dM2 = (int32_t*)put(nullptr, (size_t)n2 * 4);
+    if (cpErr != hipSuccess) return ORB_EGPU;
     hipLaunchKernelGGL(k_sim3_match, dim3((n1 + 3) / 4), dim3(256), 0, s, dK2, dD2, n2, grid_of(kf2), S12, n1, dV1, dX1,
                        dMin1, dMax1, dMD1, dM1);
     hipLaunchKernelGGL(k_sim3_match, dim3((n2 + 3) / 4), dim3(256), 0, s, dK1, dD1, n1, grid_of(kf1), S21, n2, dV2, dX2,
@@ -2228,12 +2232,10 @@ int orb_search_by_sim3(int device, const orb_frame_view* kf1, const orb_frame_vi
     std::vector<int32_t> m1((size_t)n1), m2((size_t)n2);
     int rc = hipGetLastError() == hipSuccess ? ORB_OK : ORB_EGPU;
     if (rc == ORB_OK) {
-        (void)hipMemcpyAsync(m1.data(), dM1, (size_t)n1 * 4, hipMemcpyDeviceToHost, s);
-        (void)hipMemcpyAsync(m2.data(), dM2, (size_t)n2 * 4, hipMemcpyDeviceToHost, s);
+        ORB_HIP_TRY(hipMemcpyAsync(m1.data(), dM1, (size_t)n1 * 4, hipMemcpyDeviceToHost, s));
+        ORB_HIP_TRY(hipMemcpyAsync(m2.data(), dM2, (size_t)n2 * 4, hipMemcpyDeviceToHost, s));
         if (hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
     }
-    (void)hipStreamDestroy(s);
-    (void)hipFree(base);
     if (rc) return rc;
     int nFound = 0;   // R :1490-1503: keep the pairs both directions agree on
     for (int i1 = 0; i1 < n1; i1++) {
@@ -2298,14 +2300,19 @@ int orb_search_for_triangulation(int device, const orb_frame_view* kf1, const or
                        al((size_t)n1) + al((size_t)n2 + 1) + al(common.size() * 16) + al((size_t)L1 * 4 + 1) +
                        al((size_t)L2 * 4 + 1) + al(4) + 4096;
     char* base = nullptr;
-    ORB_HIP_TRY(hipMalloc(&base, tot));
-    hipStream_t s = nullptr;
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) { (void)hipFree(base); return ORB_EGPU; }
+    HostScratch* hsc = nullptr;
+    if (int e_ = host_scratch(device, tot, &hsc)) return e_;
+    base = hsc->base;
+    hipStream_t s = hsc->stream;
     char* c = base;
+    hipError_t cpErr = hipSuccess;   // first failed upload, checked before the launch
     auto put = [&](const void* src, size_t bytes) {
         char* r = c;
         c += al(bytes + 1);
-        if (src && bytes) (void)hipMemcpyAsync(r, src, bytes, hipMemcpyHostToDevice, s);
+        if (src && bytes) {
+            const hipError_t e = hipMemcpyAsync(r, src, bytes, hipMemcpyHostToDevice, s);
+            if (e != hipSuccess && cpErr == hipSuccess) cpErr = e;
+        }
         return r;
     };
     auto* dK1 = (orb_keypoint*)put(hk1.data(), (size_t)n1 * sizeof(orb_keypoint));
@@ -2321,18 +2328,17 @@ int orb_search_for_triangulation(int device, const orb_frame_view* kf1, const or
     auto* dI2 = (int32_t*)put(fidx2, (size_t)L2 * 4);
     auto* dMt = (int32_t*)put(matches12, (size_t)n1 * 4);
     auto* dNm = (int32_t*)put(nullptr, 4);
+    if (cpErr != hipSuccess) return ORB_EGPU;
     hipLaunchKernelGGL(k_sft, dim3((unsigned)common.size()), dim3(64), 0, s, dK1, dD1, kf1->uright ? dU1 : nullptr, dM1,
                        dK2, dD2, kf2->uright ? dU2 : nullptr, dM2, dN, dI1, dI2, P, dMt);
     hipLaunchKernelGGL(k_sft_rot, dim3(1), dim3(256), 0, s, dK1, dK2, n1, check_ori ? 1 : 0, dMt, dNm);
     int rc = hipGetLastError() == hipSuccess ? ORB_OK : ORB_EGPU;
     int nm = 0;
     if (rc == ORB_OK) {
-        (void)hipMemcpyAsync(matches12, dMt, (size_t)n1 * 4, hipMemcpyDeviceToHost, s);
-        (void)hipMemcpyAsync(&nm, dNm, 4, hipMemcpyDeviceToHost, s);
+        ORB_HIP_TRY(hipMemcpyAsync(matches12, dMt, (size_t)n1 * 4, hipMemcpyDeviceToHost, s));
+        ORB_HIP_TRY(hipMemcpyAsync(&nm, dNm, 4, hipMemcpyDeviceToHost, s));
         if (hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
     }
-    (void)hipStreamDestroy(s);
-    (void)hipFree(base);
     return rc == ORB_OK ? nm : rc;
 }
 
@@ -2380,14 +2386,19 @@ static int search_by_bow(int device, const orb_frame_view* v1, const uint8_t* ok
                        al(common.size() * 16 + 1) + al((size_t)L1 * 4 + 1) + al((size_t)L2 * 4 + 1) +
                        al((size_t)n1 * 4 + 1) + al(4 + 1) + 4096;
     char* base = nullptr;
-    ORB_HIP_TRY(hipMalloc(&base, tot));
-    hipStream_t s = nullptr;
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) { (void)hipFree(base); return ORB_EGPU; }
+    HostScratch* hsc = nullptr;
+    if (int e_ = host_scratch(device, tot, &hsc)) return e_;
+    base = hsc->base;
+    hipStream_t s = hsc->stream;
     char* c = base;
+    hipError_t cpErr = hipSuccess;   // first failed upload, checked before the launch
     auto put = [&](const void* src, size_t bytes) {
         char* r = c;
         c += al(bytes + 1);
-        if (src && bytes) (void)hipMemcpyAsync(r, src, bytes, hipMemcpyHostToDevice, s);
+        if (src && bytes) {
+            const hipError_t e = hipMemcpyAsync(r, src, bytes, hipMemcpyHostToDevice, s);
+            if (e != hipSuccess && cpErr == hipSuccess) cpErr = e;
+        }
         return r;
     };
     auto* dK1 = (orb_keypoint*)put(hk1.data(), (size_t)n1 * sizeof(orb_keypoint));
@@ -2401,18 +2412,17 @@ static int search_by_bow(int device, const orb_frame_view* v1, const uint8_t* ok
     auto* dI2 = (int32_t*)put(fidx2, (size_t)L2 * 4);
     auto* dMt = (int32_t*)put(matches12, (size_t)n1 * 4);
     auto* dNm = (int32_t*)put(nullptr, 4);
+    if (cpErr != hipSuccess) return ORB_EGPU;
     hipLaunchKernelGGL(k_sbb, dim3((unsigned)common.size()), dim3(64), 0, s, dD1, dO1, dD2, ok2 ? dO2 : nullptr, dN,
                        dI1, dI2, thIncl, ratio, dMt);
     hipLaunchKernelGGL(k_sft_rot, dim3(1), dim3(256), 0, s, dK1, dK2, n1, check_ori ? 1 : 0, dMt, dNm);
     int rc = hipGetLastError() == hipSuccess ? ORB_OK : ORB_EGPU;
     int nm = 0;
     if (rc == ORB_OK) {
-        (void)hipMemcpyAsync(matches12, dMt, (size_t)n1 * 4, hipMemcpyDeviceToHost, s);
-        (void)hipMemcpyAsync(&nm, dNm, 4, hipMemcpyDeviceToHost, s);
+        ORB_HIP_TRY(hipMemcpyAsync(matches12, dMt, (size_t)n1 * 4, hipMemcpyDeviceToHost, s));
+        ORB_HIP_TRY(hipMemcpyAsync(&nm, dNm, 4, hipMemcpyDeviceToHost, s));
         if (hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
     }
-    (void)hipStreamDestroy(s);
-    (void)hipFree(base);
     return rc == ORB_OK ? nm : rc;
 }
 

@@ -375,15 +375,20 @@ int pose_optimize_batch(int device, const pose_batch* p, pose_batch_result* r, i
     const size_t szOut = (size_t)B * 7 * 8 + (size_t)B * 4 + (size_t)B * 5 * 4 + (size_t)E;
     const size_t szWork = (size_t)E * 3 * 8 + 2 * (size_t)E;
     char* base = nullptr;
-    ORB_HIP_TRY(hipMalloc(&base, szIn + szOut + szWork + 1024));
-    hipStream_t s = nullptr;
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) { (void)hipFree(base); return ORB_EGPU; }
+    HostScratch* hsc = nullptr;
+    if (int e_ = host_scratch(device, szIn + szOut + szWork + 1024, &hsc)) return e_;
+    base = hsc->base;
+    hipStream_t s = hsc->stream;
     char* cur = base;
     auto take = [&](size_t bytes) { char* r0 = cur; cur += (bytes + 15) & ~(size_t)15; return r0; };
     pose_batch dp = *p;
+    hipError_t cpErr = hipSuccess;   // first failed upload, checked before the launch
     auto up = [&](const void* src, size_t bytes) -> const void* {
         char* dst = take(bytes);
-        if (bytes) (void)hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
+        if (bytes) {
+            const hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
+            if (e != hipSuccess && cpErr == hipSuccess) cpErr = e;
+        }
         return dst;
     };
     dp.pose_q = (const double*)up(p->pose_q, (size_t)B * 32);
@@ -401,17 +406,16 @@ int pose_optimize_batch(int device, const pose_batch* p, pose_batch_result* r, i
     int32_t* dIters = (int32_t*)take((size_t)B * 20);
     double* dWork = (double*)take((size_t)E * 24 + 8);
     uint8_t* dFlags = (uint8_t*)take(2 * (size_t)E + 2);
+    if (cpErr != hipSuccess) return ORB_EGPU;
     int rc = pose_optimize_batch_device(&dp, &dr, dWork, dFlags, dIters, s);
     if (rc == ORB_OK) {
-        (void)hipMemcpyAsync(r->pose_q, dr.pose_q, (size_t)B * 32, hipMemcpyDeviceToHost, s);
-        (void)hipMemcpyAsync(r->pose_t, dr.pose_t, (size_t)B * 24, hipMemcpyDeviceToHost, s);
-        (void)hipMemcpyAsync(r->n_inliers, dr.n_inliers, (size_t)B * 4, hipMemcpyDeviceToHost, s);
-        if (E) (void)hipMemcpyAsync(r->outlier, dr.outlier, (size_t)E, hipMemcpyDeviceToHost, s);
-        if (iters) (void)hipMemcpyAsync(iters, dIters, (size_t)B * 20, hipMemcpyDeviceToHost, s);
+        ORB_HIP_TRY(hipMemcpyAsync(r->pose_q, dr.pose_q, (size_t)B * 32, hipMemcpyDeviceToHost, s));
+        ORB_HIP_TRY(hipMemcpyAsync(r->pose_t, dr.pose_t, (size_t)B * 24, hipMemcpyDeviceToHost, s));
+        ORB_HIP_TRY(hipMemcpyAsync(r->n_inliers, dr.n_inliers, (size_t)B * 4, hipMemcpyDeviceToHost, s));
+        if (E) ORB_HIP_TRY(hipMemcpyAsync(r->outlier, dr.outlier, (size_t)E, hipMemcpyDeviceToHost, s));
+        if (iters) ORB_HIP_TRY(hipMemcpyAsync(iters, dIters, (size_t)B * 20, hipMemcpyDeviceToHost, s));
         if (hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
     }
-    (void)hipStreamDestroy(s);
-    (void)hipFree(base);
     return rc;
 }
 
