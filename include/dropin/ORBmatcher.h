@@ -1,0 +1,73 @@
+// Drop-in replacement for R/include/ORBmatcher.h: the same class declaration.  The constructor
+// (R/src/ORBmatcher.cpp:46-48), DescriptorDistance (:1901-1917) and SearchForInitialization
+// (:499-617) are defined here over liborbslam2_amd through include/orbslam2_amd_shim.hpp; delete
+// those three definitions from R/src/ORBmatcher.cpp and keep the rest.  Compiles inside the
+// reference tree only (OpenCV, Frame.h); the shim is compiled and tested here with mock types.
+#ifndef ORBMATCHER_H
+#define ORBMATCHER_H
+
+#include <vector>
+#include <opencv2/core/core.hpp>
+#include <opencv2/features2d/features2d.hpp>
+
+#include "Frame.h"
+#include "KeyFrame.h"
+#include "MapPoint.h"
+#include "orbslam2_amd_shim.hpp"
+
+namespace ORB_SLAM2 {
+
+class ORBmatcher {
+public:
+    ORBmatcher(float nnratio = 0.6, bool checkOri = true)
+        : mfNNratio(nnratio), mbCheckOrientation(checkOri), mDev(nnratio, checkOri) {}
+
+    // 256-bit Hamming distance of two 32-byte rows (R :1901-1917)
+    static int DescriptorDistance(const cv::Mat& a, const cv::Mat& b) {
+        return orbslam2_amd::Matcher::DescriptorDistance(a.ptr<uint8_t>(), b.ptr<uint8_t>());
+    }
+
+    int SearchByProjection(Frame& F, const std::vector<MapPoint*>& vpMapPoints, const float th = 3);
+    int SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, const float th, const bool bMono);
+    int SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const std::set<MapPoint*>& sAlreadyFound,
+                           const float th, const int ORBdist);
+    int SearchByProjection(KeyFrame* pKF, cv::Mat Scw, const std::vector<MapPoint*>& vpPoints,
+                           std::vector<MapPoint*>& vpMatched, int th);
+    int SearchByBoW(KeyFrame* pKF, Frame& F, std::vector<MapPoint*>& vpMapPointMatches);
+    int SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoint*>& vpMatches12);
+
+    // monocular initialisation matching on the GPU (R :499-617): same outputs, same order
+    int SearchForInitialization(Frame& F1, Frame& F2, std::vector<cv::Point2f>& vbPrevMatched,
+                                std::vector<int>& vnMatches12, int windowSize = 10) {
+        return mDev.SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize);
+    }
+
+    int SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, cv::Mat F12,
+                               std::vector<std::pair<size_t, size_t> >& vMatchedPairs, const bool bOnlyStereo);
+    int SearchBySim3(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoint*>& vpMatches12, const float& s12,
+                     const cv::Mat& R12, const cv::Mat& t12, const float th);
+    int Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, const float th = 3.0);
+    int Fuse(KeyFrame* pKF, cv::Mat Scw, const std::vector<MapPoint*>& vpPoints, float th,
+             vector<MapPoint*>& vpReplacePoint);
+
+public:
+    static const int TH_LOW;
+    static const int TH_HIGH;
+    static const int HISTO_LENGTH;
+
+protected:
+    bool CheckDistEpipolarLine(const cv::KeyPoint& kp1, const cv::KeyPoint& kp2, const cv::Mat& F12,
+                               const KeyFrame* pKF);
+    float RadiusByViewingCos(const float& viewCos);
+    void ComputeThreeMaxima(std::vector<int>* histo, const int L, int& ind1, int& ind2, int& ind3);
+
+    float mfNNratio;
+    bool mbCheckOrientation;
+
+private:
+    orbslam2_amd::Matcher mDev;
+};
+
+}  // namespace ORB_SLAM2
+
+#endif  // ORBMATCHER_H
