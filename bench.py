@@ -532,10 +532,14 @@ def bench_extras(args, amd, dev):
     dt = (time.perf_counter() - t0) / reps
     c = buf["cnt"].cpu().numpy().astype(np.int64)
     pairs = float((c[:-1] * c[1:]).sum())
-    peak_pairs = 256 * 64 * 2.4e9 / 16
+    # 16 lane-ops per pair (8 xor + 8 bcnt on dword pairs); 78.6 T lane-ops/s nominal (4 SIMD x 32
+    # lanes per CU per clock), 39.3 T measured for wave64 issue (profiles/r02_valu_peak.txt)
+    peak_pairs = VALU_PEAK_TOPS * 1e12 / 16
     out["knn2_bruteforce"] = {"pairs_per_s": round(pairs / dt, 1), "ms_per_batch": round(dt * 1e3, 4),
                               "frame_pairs": B, "roofline": {"bound": "valu", "unit": "pairs/s",
-                                                             "peak": peak_pairs, "frac": round(pairs / dt / peak_pairs, 4)}}
+                                                             "peak": peak_pairs, "frac": round(pairs / dt / peak_pairs, 4),
+                                                             "frac_of_measured_issue_peak":
+                                                                 round(pairs / dt / (VALU_MEASURED_TOPS * 1e12 / 16), 4)}}
     # ---- config 3 stereo: KITTI 00 geometry pairs, extraction of both images + ComputeStereoMatches
     out["stereo_kitti_1241x376"] = bench_stereo_kitti(args, amd, dev)
     # ---- config 3: KITTI geometry, 2000 features, extract + SearchForInitialization

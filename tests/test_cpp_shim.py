@@ -134,13 +134,20 @@ def test_shim_local_bundle_adjustment(shim, tmp_path, amd, stereo):
                    np.int32, np.uint8, np.float64, np.float64, np.float64, np.uint8, np.float64, np.float64,
                    np.float64, np.int32, np.float32, np.float32, np.int32, np.int32)
     NP, NE = len(pfix), len(ept)
-    # the gathered graph: every keyframe (local first, then the fixed cameras), every point and
-    # every observation of the synthetic problem, ids as the reference assigns them
-    assert NP == nk and NE == len(pb["edge_point"]) and len(xid) == len(pb["point_id"])
-    local = np.nonzero(np.asarray(pb["pose_fixed"]) == 0)[0]
+    # the gathered graph (R :567-668): the local points are those a local keyframe observes; every
+    # observation of a local point is an edge; the fixed cameras are the other keyframes observing
+    # one; ids as the reference assigns them (points: mnId + maxKFid + 1)
+    e_pt, e_kf = np.asarray(pb["edge_point"]), np.asarray(pb["edge_pose"])
+    fixed_in = np.asarray(pb["pose_fixed"])
+    local_pts = np.unique(e_pt[fixed_in[e_kf] == 0])
+    local_edge = np.isin(e_pt, local_pts)
+    fixed_cams = np.unique(e_kf[local_edge & (fixed_in[e_kf] == 1)])
+    local = np.nonzero(fixed_in == 0)[0]
+    assert NP == len(local) + len(fixed_cams) and NE == int(local_edge.sum()) and len(xid) == len(local_pts)
     assert np.array_equal(pid[:len(local)], np.asarray(pb["pose_id"])[local])
+    assert np.array_equal(np.sort(pid[len(local):]), np.sort(np.asarray(pb["pose_id"])[fixed_cams]))
     assert np.array_equal(pfix[len(local):], np.ones(NP - len(local), np.uint8))
-    assert np.array_equal(np.sort(xid - (pid.max() + 1)), np.sort(np.asarray(pb["point_id"])))   # mnId+maxKFid+1
+    assert np.array_equal(np.sort(xid - (pid.max() + 1)), np.sort(np.asarray(pb["point_id"])[local_pts]))
     # the same arrays through the Python binding of lba_solve: bitwise the same solve
     kf_of_pose = {int(i): k for k, i in enumerate(np.asarray(pb["pose_id"]))}
     Tcw = np.stack([np.asarray(pb["Tcw"], np.float32)[kf_of_pose[int(i)]] for i in pid])
@@ -157,5 +164,9 @@ def test_shim_local_bundle_adjustment(shim, tmp_path, amd, stereo):
     for k in range(len(local)):
         assert np.array_equal(Tout.reshape(nk, 4, 4)[kf_of_pose[int(pid[k])]],
                               opt.pose_to_Tcw(ref["pose_q"][k], ref["pose_t"][k]))
-    assert np.array_equal(upd, np.ones(len(xid), np.int32))
-    assert int(nobs.sum()) == NE - int(erase.sum())
+    is_local = np.zeros(len(pb["point_id"]), bool)
+    is_local[local_pts] = True
+    assert np.array_equal(upd, is_local.astype(np.int32))    # points outside the window untouched
+    nobs0 = np.bincount(e_pt, minlength=len(is_local))
+    assert int(nobs.sum()) == int(nobs0.sum()) - int(erase.sum())
+    assert np.array_equal(nobs[~is_local], nobs0[~is_local])
