@@ -1,0 +1,6 @@
+set -e
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+ORB_SLAM2_AMD_LIB=orb-slam2-_amd/lib/variant/timing/liborbslam2_amd.so timeout -k 10 120 python -u tools/lba_timing.py > gpurun_out/lba_timing.log 2>&1
+timeout -k 10 120 python -u tools/lba_timing.py > gpurun_out/lba_plain.log 2>&1
+echo ok
