@@ -64,6 +64,7 @@ struct LmState {
     int stopAfter;  // test hook: stop once trialBase + trials reaches it (-1: off)
     int trialBase;  // trials of this solve before this optimize() call
     int stopped;    // 1 once the stop was observed
+    int pending;    // single process, fused slots: a trial's decision is still to be taken
 };
 
 // Kernels of the LM loop run only in their phase (`want`): 0 linearisation, 1 trial,
@@ -100,8 +101,11 @@ struct LbaDev {
     double *S, *bs, *x;         // x: [6P + 3M]
     double* red;                // reduction scratch
     double *partChi, *partScale, *partMax;   // per-workgroup partials (single-process LM kernels)
+    double* partLin;            // fused slots: k_edge_lin's chi2 partials (partChi holds the trial's)
     int* flags;                 // [0] LDLT failure
     LmState* lm;                // LM control state (device)
+    LmState* lmMid;             // fused slots: the state between k_edge_lin and k_point_schur (never
+                                // written by a kernel whose other workgroups read it)
     const uint32_t* stopWord;   // host-mapped mirror of the caller's stop flag (lba_wait copies it)
 };
 
@@ -170,13 +174,70 @@ __device__ __forceinline__ double edge_error(const LbaDev& d, int k, double hmon
     return chi;
 }
 
+__device__ void lm_begin(LmState* st, double chi, double maxDiag);
+__device__ void lm_decide(LmState* st, double chiSum, double scaleSum, int fail, int maxTrials, int iterations,
+                          int fixedIterations, double* __restrict__ trace, const uint32_t* stopWord, double sharedStop);
+
+// Fused LM bookkeeping (single process).  A trial's decision and an iteration's start are not
+// separate launches: every workgroup of the next kernel that needs them recomputes them from
+// the producers' partials — the same loads in the same order, so the same bits — and
+// workgroup 0 alone writes the result (and the trace row).  A kernel never writes the state
+// copy its own workgroups read: k_edge_lin reads `lm` and writes `lmMid`, k_vertex_reduce
+// reads `lmMid`, k_point_schur reads `lmMid` and writes `lm`, the trial kernels read `lm`.
+struct LmFuse {
+    int nChi, nScale, maxTrials, iterations, fixedIterations;
+    const int32_t* freePoses;
+    double* trace;
+};
+// The pending trial decision (lm_decide on the trial's chi2 and scale partials and the stop
+// sample k_edge_errors took), as k_lm_decide_fused takes it.  Returns the state after it.
+// (The partial sums are loaded whether or not a decision is pending, with the state, so a
+// caller pays one memory round trip.)
+__device__ __forceinline__ LmState lm_decide_local(const LbaDev& d, const LmFuse& f, int lane, bool writer) {
+    LmState ls = *d.lm;
+    double c = 0.0, sc = 0.0;
+    for (int i = lane; i < f.nChi; i += 64) c += d.partChi[i];
+    for (int i = lane; i < f.nScale; i += 64) sc += d.partScale[i];
+    const int fail = d.flags[0];
+    const double stop = d.red[4];
+    c = wave_sum_d(c);
+    sc = wave_sum_d(sc);
+    ls.pop = 0;
+    if (ls.pending) {
+        lm_decide(&ls, c, sc, fail, f.maxTrials, f.iterations, f.fixedIterations, writer ? f.trace : nullptr, nullptr,
+                  stop);
+        ls.pending = 0;
+    }
+    return ls;
+}
+// pop() of the slice [g0, g0 + stride) ... of points and free poses after a rejected trial
+__device__ __forceinline__ void lm_pop_slice(const LbaDev& d, const int32_t* freePoses, int g0, int stride) {
+    for (int i = g0; i < d.M; i += stride) {
+        const int g = d.ptGlob[i];
+        for (int j = 0; j < 3; j++) d.X[3 * (size_t)g + j] = d.bX[3 * (size_t)g + j];
+    }
+    for (int i = g0; i < d.P; i += stride) {
+        const int p = freePoses[i];
+        for (int j = 0; j < 4; j++) d.q[4 * p + j] = d.bq[4 * p + j];
+        for (int j = 0; j < 3; j++) d.t[3 * p + j] = d.bt[3 * p + j];
+    }
+}
+
 // Trial errors (one wave per 64 edges); partChi[block] = the wave's robust chi2 sum.
-__global__ __launch_bounds__(64) void k_edge_errors(LbaDev d, double hmono, double hstereo, int want) {
+// Fused slots (`fuse`): workgroup 0 marks the decision pending and samples terminate() (the
+// host-mapped stop word) once into red[4], so every decider sees the same sample.
+__global__ __launch_bounds__(64) void k_edge_errors(LbaDev d, double hmono, double hstereo, int want, int fuse) {
     if (lm_off(d.lm, want)) return;
     const int k = blockIdx.x * 64 + threadIdx.x;
     const double chi = k < d.nact ? edge_error(d, k, hmono, hstereo) : 0.0;
     const double sum = wave_sum_d(chi);
-    if (threadIdx.x == 0) d.partChi[blockIdx.x] = sum;
+    if (threadIdx.x == 0) {
+        d.partChi[blockIdx.x] = sum;
+        if (fuse && blockIdx.x == 0) {
+            d.lm->pending = 1;
+            d.red[4] = lm_stop_now(d.lm, d.stopWord, 0.0) ? 1.0 : 0.0;
+        }
+    }
 }
 
 // Jacobians + Huber-weighted quadratic-form blocks per active edge.
@@ -270,8 +331,18 @@ __device__ __forceinline__ void edge_linearize(const LbaDev& d, int k, double hm
 // Phase-0 linearisation of active edge k (computeActiveErrors + linearizeOplus +
 // constructQuadraticForm, G/core/sparse_optimizer.cpp:384-394, block_solver.hpp:502-561).
 // One wave per 64 edges (a launch wide enough to reach every CU); partChi[block] as above.
-__global__ __launch_bounds__(64) void k_edge_lin(LbaDev d, double hmono, double hstereo) {
-    if (lm_off(d.lm, 0)) return;
+// Fused slots: first takes the previous trial's pending decision (lm_decide_local; workgroup
+// 0 writes it back) and, after a rejection, restores this workgroup's slice of the estimates.
+__global__ __launch_bounds__(64) void k_edge_lin(LbaDev d, double hmono, double hstereo, int fuse, LmFuse f) {
+    if (fuse) {
+        const LmState ls = lm_decide_local(d, f, threadIdx.x, blockIdx.x == 0 && threadIdx.x == 0);
+        if (blockIdx.x == 0 && threadIdx.x == 0) *d.lmMid = ls;
+        const int phase = ls.phase, pop = ls.pop;
+        if (pop) lm_pop_slice(d, f.freePoses, blockIdx.x * 64 + threadIdx.x, (int)gridDim.x * 64);
+        if (phase != 0) return;
+    } else if (lm_off(d.lm, 0)) {
+        return;
+    }
     const int k = blockIdx.x * 64 + threadIdx.x;
     double chi = 0.0;
     if (k < d.nact) {
@@ -279,7 +350,7 @@ __global__ __launch_bounds__(64) void k_edge_lin(LbaDev d, double hmono, double 
         edge_linearize(d, k, hmono, hstereo);
     }
     const double sum = wave_sum_d(chi);
-    if (threadIdx.x == 0) d.partChi[blockIdx.x] = sum;
+    if (threadIdx.x == 0) (fuse ? d.partLin : d.partChi)[blockIdx.x] = sum;
 }
 
 // Vertex blocks (256 threads): workgroups [0, P) reduce Hpp, b_p of one free pose over its
@@ -372,13 +443,33 @@ __global__ __launch_bounds__(256) void k_vertex_reduce(LbaDev d) {
 
 // Per landmark with lambda (G/core/block_solver.hpp:380-398): D^-1 = (Hll + lambda I)^-1
 // (Eigen's 3x3 cofactor inverse) and D^-1 b_l.
-__global__ __launch_bounds__(64) void k_point_schur(LbaDev d) {
-    if (lm_off(d.lm, 1)) return;
-    const double lambda = d.lm->lambda;
-    const int l = blockIdx.x * 64 + threadIdx.x;
+// Fused slots: an iteration that was just linearised (phase 0) starts here — lm_begin from
+// k_edge_lin's chi2 partials and k_vertex_reduce's maxima (workgroup 0 writes the state).
+__global__ __launch_bounds__(64) void k_point_schur(LbaDev d, int fuse, int nChi, int nMax) {
+    // every load of the workgroup is issued before the state is known (one memory round trip):
+    // the landmark's Hll, b_l and, fused, the state and the partials
+    const int l = blockIdx.x * 64 + threadIdx.x, lc = min(l, d.M - 1);
+    double m[9], blv[3];
+    for (int i = 0; i < 9; i++) m[i] = d.Hll[9 * (size_t)lc + i];
+    for (int i = 0; i < 3; i++) blv[i] = d.bl[3 * (size_t)lc + i];
+    double lambda;
+    if (fuse) {
+        LmState ls = *d.lmMid;
+        const int lane = threadIdx.x;
+        double c = 0.0, mx = 0.0;
+        for (int i = lane; i < nChi; i += 64) c += d.partLin[i];
+        for (int i = lane; i < nMax; i += 64) mx = fmax(mx, d.partMax[i]);
+        c = wave_sum_d(c);
+        mx = wave_max_d(mx);
+        if (ls.phase == 0) lm_begin(&ls, c, mx);
+        if (blockIdx.x == 0 && lane == 0) *d.lm = ls;
+        if (ls.phase != 1) return;
+        lambda = ls.lambda;
+    } else {
+        if (lm_off(d.lm, 1)) return;
+        lambda = d.lm->lambda;
+    }
     if (l >= d.M) return;
-    double m[9];
-    for (int i = 0; i < 9; i++) m[i] = d.Hll[9 * (size_t)l + i];
     m[0] += lambda; m[4] += lambda; m[8] += lambda;
     double c[9];
     for (int i = 0; i < 3; i++)
@@ -392,8 +483,7 @@ __global__ __launch_bounds__(64) void k_point_schur(LbaDev d) {
     for (int i = 0; i < 3; i++)
         for (int j = 0; j < 3; j++) Di[j * 3 + i] = c[i * 3 + j] * invdet;
     for (int i = 0; i < 9; i++) d.Dinv[9 * (size_t)l + i] = Di[i];
-    const double* bl = d.bl + 3 * (size_t)l;
-    for (int i = 0; i < 3; i++) d.db[3 * (size_t)l + i] = Di[i * 3] * bl[0] + Di[i * 3 + 1] * bl[1] + Di[i * 3 + 2] * bl[2];
+    for (int i = 0; i < 3; i++) d.db[3 * (size_t)l + i] = Di[i * 3] * blv[0] + Di[i * 3 + 1] * blv[1] + Di[i * 3 + 2] * blv[2];
 }
 
 // Reduced camera system (G/core/block_solver.hpp:408-440): one workgroup per pose-pair block
@@ -528,7 +618,7 @@ __device__ __forceinline__ double shfl_d(double v, int src) {
 // two agree to rounding (tests compare the LM traces to 1e-9 relative).
 constexpr int kNB = 16;
 constexpr int kLdlT = 512;
-constexpr int kLdlLdsMaxN = 128;   // padded order held in LDS: (128 * 129 + 3 * 128 + 64) * 8 B = 133 KB
+constexpr int kLdlLdsMaxN = 128;   // padded order held in LDS: (128 * 129 + 3 * 128 + 128) * 8 B = 133 KB
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ double rcp_nr(double d) {
@@ -637,7 +727,90 @@ __device__ __forceinline__ bool ldlt_panel(double* __restrict__ A, int ld, int n
     return ok;
 }
 
-constexpr int kPanelRows = 192;   // rows of a panel factored in wave 0's registers (3 per lane)
+// The LDS-image panel split over waves: group g (wave g) holds the panel's 16 diagonal rows in
+// lanes 0..15 and rows jb + 16 + 48 g + (lane - 16) in lanes 16..63, so every group computes
+// the pivots, 1/d_j and W(jb+k, j) itself (v_readlane within the wave; the W row of the
+// diagonal block through the group's own 16-double LDS scratch) and no wave waits on another
+// inside the column loop.  The diagonal rows are computed identically by every group (same
+// operations in the same order); group 0 alone stores them, d and 1/d.  Groups only write rows
+// they own, after every group has read its inputs (arrival counter `arrive`, group 0 waits
+// for `target`).  Per-column work as ldlt_panel<1>.
+__device__ __forceinline__ bool ldlt_panel_grp(double* __restrict__ A, int ld, int np, int jb, double* __restrict__ dg,
+                                               double* __restrict__ rdg, double* __restrict__ y, double* dummy,
+                                               double* __restrict__ wsc, int lane, int g, int* arrive, int target) {
+    const int r = lane < kNB ? jb + lane : jb + kNB + 48 * g + (lane - kNB);
+    const bool live = r < np, own = live && (g == 0 || lane >= kNB);
+    const int rc = min(r, np - 1);
+    double P[kNB];
+    double Y = y[rc];
+#pragma unroll
+    for (int c = 0; c < kNB; c++) P[c] = A[(size_t)rc * ld + jb + c];
+    // inputs read (this wave's LDS operations complete in order): arrive; group 0 then waits
+    // for every group before its first store
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (g == 0)
+        while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    double* const Lrow = own ? A + (size_t)r * ld + jb : dummy + lane;
+    double* const Wcol = own ? A + (size_t)jb * ld + r : dummy + lane;
+    double* const dsink = dummy + lane;
+    double dj = shfl_d(P[0], 0);
+    bool ok = dj != 0.0 && isfinite(dj);
+    double rd = rcp_nr(dj);
+#pragma unroll
+    for (int c = 0; c < kNB; c++) {
+        const int j = jb + c;
+        const double yj = shfl_d(Y, c);   // final: every k < j has been applied
+        const double w = P[c];
+        const double l = w * rd;
+        P[c] = l;
+        const bool below = r > j;
+        *(below ? Wcol + (size_t)c * ld : dsink) = w;   // W(r, j)
+        *(below ? Lrow + c : dsink) = l;                // L(r, j)
+        *(g == 0 && lane == 0 ? dg + j : dsink) = dj;
+        *(g == 0 && lane == 0 ? rdg + j : dsink) = rd;
+        *(lane < kNB ? wsc + lane : dsink) = w;         // the diagonal block's W(jb+k, j), this group only
+        double wk[kNB];
+#pragma unroll
+        for (int k = c + 2; k < kNB; k++) wk[k] = wsc[k];
+        double djn = 1.0, r0 = 1.0, e0 = 0.0, r1 = 1.0, e1 = 0.0;
+        if (c + 1 < kNB) {
+            const double w1 = shfl_d(w, c + 1);   // W(j+1, j)
+            P[c + 1] = __builtin_fma(-l, w1, P[c + 1]);
+            djn = shfl_d(P[c + 1], c + 1);
+            r0 = __builtin_amdgcn_rcp(djn);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const int nk = kNB - 2 - c > 0 ? kNB - 2 - c : 0;
+        const int g1 = c + 2 + (nk + 2) / 3, g2 = c + 2 + 2 * (nk + 2) / 3;
+#pragma unroll
+        for (int k = c + 2; k < kNB && k < g1; k++) P[k] = __builtin_fma(-l, wk[k], P[k]);
+        if (c + 1 < kNB) { e0 = __builtin_fma(-djn, r0, 1.0); r1 = __builtin_fma(r0, e0, r0); }
+        if (below) Y = __builtin_fma(-l, yj, Y);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = g1; k < kNB && k < g2; k++) P[k] = __builtin_fma(-l, wk[k], P[k]);
+        if (c + 1 < kNB) { e1 = __builtin_fma(-djn, r1, 1.0); r1 = __builtin_fma(r1, e1, r1); }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = g2; k < kNB; k++) P[k] = __builtin_fma(-l, wk[k], P[k]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (c + 1 < kNB) {
+            ok = ok && djn != 0.0 && isfinite(djn);
+            dj = djn;
+            rd = r1;
+        }
+    }
+    if (own) y[r] = Y;
+    return ok;
+}
+// groups for the panel at jb: the 16 diagonal rows plus 48 rows below per group
+__device__ __forceinline__ int panel_groups(int np, int jb) { return max(1, (np - jb - kNB + 47) / 48); }
+
+// rows of a panel factored in registers: all of them with the LDS image (ldlt_panel_grp), 192
+// (three per lane of wave 0) with the global image, the rest one per thread (step 1b)
+constexpr int kPanelRowsLds = 128, kPanelRowsGlobal = 192;
 
 template <bool kLds>
 __global__ __launch_bounds__(kLdlT) void k_ldlt_solve(const double* __restrict__ Sg, const double* __restrict__ b,
@@ -653,40 +826,75 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_solve(const double* __restrict__
 #endif
     const int np = (n + kNB - 1) & ~(kNB - 1);
     const int ld = np + 1;   // odd: column-strided lanes spread over the LDS banks
+    constexpr int kPanelRows = kLds ? kPanelRowsLds : kPanelRowsGlobal;
     double* A = kLds ? sh : work;
     double* dg = sh + (kLds ? (size_t)np * ld : 0);
     double* rdg = dg + np;
     double* y = rdg + np;
     double* dummy = y + np;   // 64 per-lane sinks for masked-off panel stores
-    __shared__ int failS;
+    double* wsc = dummy + 64; // per-group W-row scratch of the grouped panel (4 x 16)
+    __shared__ int failS, arriveS;
+    int arriveTarget = 0;     // the grouped panels' cumulative arrivals (uniform over the workgroup)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // ---- stage S (n x n, row-major) into the padded np x np image (identity padding);
-    //      wave w copies rows w, w + 8, ... in 64-column chunks, 16 unconditional loads
-    //      (clamped addresses) in flight per lane, no integer division
+    // ---- stage S (n x n, row-major, n = 6P even) into the padded np x np image (identity
+    //      padding).  In LDS: wave w copies rows w, w + 8, ... with lane c moving the column pair
+    //      (2c, 2c+1) by one 16-byte load — every load of the wave in flight at once (one round
+    //      trip; out-of-range rows read 0 through the buffer resource).  Global image: 8-byte loads.
     {
         constexpr int kW = kLdlT / 64;
         const __amdgpu_buffer_rsrc_t rs = buf_rsrc(Sg, (uint32_t)n * n * 8);
-        for (int j0 = 0; j0 < np; j0 += 64) {
-            const int j = j0 + lane;
-            for (int i0 = wave; i0 < np; i0 += kW * 16) {
-                double v[16];
+        if (kLds && (n & 1) == 0 && np <= 128) {
+            constexpr int kRows = 128 / kW;   // rows per wave at np = 128
+            const int cp = n >> 1, c = lane;
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            u32x4 v[kRows];
 #pragma unroll
-                for (int u = 0; u < 16; u++) {   // padding: offset out of range -> 0, plus identity
-                    const int i = i0 + kW * u;
-                    const bool in = i < n && j < n;
-                    v[u] = buf_ld_f64(rs, in ? (i * n + j) * 8 : kBufOob) + ((!in && i == j) ? 1.0 : 0.0);
+            for (int u = 0; u < kRows; u++) {
+                const int i = wave + kW * u;
+                const bool in = i < n && c < cp;
+                v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, in ? (i * n + 2 * c) * 8 : kBufOob, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < kRows; u++) {
+                const int i = wave + kW * u;
+                if (i < n && c < cp) {
+                    A[(size_t)i * ld + 2 * c] = __longlong_as_double((long long)(((unsigned long long)v[u].y << 32) | v[u].x));
+                    A[(size_t)i * ld + 2 * c + 1] =
+                        __longlong_as_double((long long)(((unsigned long long)v[u].w << 32) | v[u].z));
                 }
+            }
+            // identity padding: rows n..np-1 (all columns) and columns n..np-1 of rows < n
+            for (int t = tid; t < (np - n) * np; t += kLdlT) {
+                const int i = n + t / np, j = t % np;
+                A[(size_t)i * ld + j] = i == j ? 1.0 : 0.0;
+            }
+            for (int t = tid; t < n * (np - n); t += kLdlT) {
+                const int i = t / (np - n), j = n + t % (np - n);
+                A[(size_t)i * ld + j] = 0.0;
+            }
+        } else {
+            for (int j0 = 0; j0 < np; j0 += 64) {
+                const int j = j0 + lane;
+                for (int i0 = wave; i0 < np; i0 += kW * 16) {
+                    double v[16];
 #pragma unroll
-                for (int u = 0; u < 16; u++) {
-                    const int i = i0 + kW * u;
-                    if (i < np && j < np) A[(size_t)i * ld + j] = v[u];
+                    for (int u = 0; u < 16; u++) {   // padding: offset out of range -> 0, plus identity
+                        const int i = i0 + kW * u;
+                        const bool in = i < n && j < n;
+                        v[u] = buf_ld_f64(rs, in ? (i * n + j) * 8 : kBufOob) + ((!in && i == j) ? 1.0 : 0.0);
+                    }
+#pragma unroll
+                    for (int u = 0; u < 16; u++) {
+                        const int i = i0 + kW * u;
+                        if (i < np && j < np) A[(size_t)i * ld + j] = v[u];
+                    }
                 }
             }
         }
         for (int t = tid; t < np; t += kLdlT) y[t] = t < n ? b[t] : 0.0;
     }
     TSTAMP(t_sa);
-    if (tid == 0) failS = 0;
+    if (tid == 0) { failS = 0; arriveS = 0; }
     __syncthreads();
     TSTAMP(t_f0);
     const int T = np / kNB;
@@ -720,7 +928,15 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_solve(const double* __restrict__
         const int jb = kb * kNB;
         TSTAMP(t_d0);
         // ---- 1. panel: rows [jb, jb + 192) in wave 0's registers
-        if (wave == 0 && !factored) {
+        if (kLds && !factored) {
+            const int ng = panel_groups(np, jb);
+            arriveTarget += ng;
+            if (wave < ng) {
+                const bool okp = ldlt_panel_grp(A, ld, np, jb, dg, rdg, y, dummy, wsc + 16 * wave, lane, wave, &arriveS,
+                                                arriveTarget);
+                if (!okp && wave == 0 && lane == 0) failS = 1;
+            }
+        } else if (wave == 0 && !factored) {
             const int ns = min(np - jb, kPanelRows);
             bool okp;
             if (ns <= 64) okp = ldlt_panel<1>(A, ld, jb + ns, jb, dg, rdg, y, dummy, lane);
@@ -774,14 +990,15 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_solve(const double* __restrict__
         if (kLds && m > 0) {
             for (int ti = wave; ti < m; ti += kLdlT / 64) trail_tile(jb, (kb + 1 + ti) * kNB, (kb + 1) * kNB);
             __syncthreads();
-            if (wave == 0) {
-                const int jn = jb + kNB, ns = min(np - jn, kPanelRows);
-                const bool okp = ns <= 64 ? ldlt_panel<1>(A, ld, jn + ns, jn, dg, rdg, y, dummy, lane)
-                                          : ldlt_panel<2>(A, ld, jn + ns, jn, dg, rdg, y, dummy, lane);
-                if (!okp && lane == 0) failS = 1;
+            const int jn = jb + kNB, ng = panel_groups(np, jn);
+            arriveTarget += ng;
+            if (wave < ng) {
+                const bool okp = ldlt_panel_grp(A, ld, np, jn, dg, rdg, y, dummy, wsc + 16 * wave, lane, wave, &arriveS,
+                                                arriveTarget);
+                if (!okp && wave == 0 && lane == 0) failS = 1;
             } else {
                 const int nt = m * (m - 1) / 2;   // tiles with K > kb + 1
-                for (int t = wave - 1; t < nt; t += kLdlT / 64 - 1) {
+                for (int t = wave - ng; t < nt; t += kLdlT / 64 - ng) {
                     int ti, tk;
                     tri(t, ti, tk);
                     trail_tile(jb, (kb + 2 + ti) * kNB, (kb + 2 + tk) * kNB);
@@ -806,48 +1023,37 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_solve(const double* __restrict__
         if (tid == 0) flags[0] = 1;
         return;
     }
-    if (wave != 0) return;
-    for (int i = lane; i < np; i += 64) y[i] = y[i] * rdg[i];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+    for (int i = tid; i < np; i += kLdlT) y[i] = y[i] * rdg[i];
+    __syncthreads();
     // ---- backward substitution with L^T: x_i = y_i - sum_{k > i} L(k, i) x_k, k descending,
-    //      in 16-row blocks from the bottom on wave 0
+    //      in 16-row blocks from the bottom: wave 0 solves the block's 16 x 16 triangle
+    //      (v_readlane chain), then every thread takes one row above the block (the block's x
+    //      read back from LDS as broadcasts, its column of L conflict-free)
     for (int kb = np - kNB; kb >= 0; kb -= kNB) {
-        const int r = lane & 15;
-        double Ab[kNB];
+        if (wave == 0) {
+            const int r = lane & 15;
+            double Ab[kNB];
 #pragma unroll
-        for (int c = 0; c < kNB; c++) Ab[c] = A[(size_t)(kb + c) * ld + kb + r];   // L(kb+c, kb+r), used for r < c
-        double xb = y[kb + r];
+            for (int c = 0; c < kNB; c++) Ab[c] = A[(size_t)(kb + c) * ld + kb + r];   // L(kb+c, kb+r), used for r < c
+            double xb = y[kb + r];
 #pragma unroll
-        for (int c = kNB - 1; c > 0; c--) {
-            const double xc = shfl_d(xb, c);
-            xb = r < c ? __builtin_fma(-Ab[c], xc, xb) : xb;
-        }
-        double xs[kNB];
-#pragma unroll
-        for (int c = 0; c < kNB; c++) xs[c] = shfl_d(xb, c);
-        if (lane < kNB) y[kb + r] = xb;
-        for (int i0 = 0; i0 < kb; i0 += 128) {   // two rows per lane per pass
-            const int i1 = i0 + lane, i2 = i0 + 64 + lane;
-            const int c1 = min(i1, kb - 1), c2 = min(i2, kb - 1);   // clamped reads, guarded stores
-            double v1 = y[c1], v2 = y[c2];
-            double l1[kNB], l2[kNB];
-#pragma unroll
-            for (int c = 0; c < kNB; c++) {
-                l1[c] = A[(size_t)(kb + c) * ld + c1];
-                l2[c] = A[(size_t)(kb + c) * ld + c2];
+            for (int c = kNB - 1; c > 0; c--) {
+                const double xc = shfl_d(xb, c);
+                xb = r < c ? __builtin_fma(-Ab[c], xc, xb) : xb;
             }
-#pragma unroll
-            for (int c = kNB - 1; c >= 0; c--) {
-                v1 = __builtin_fma(-l1[c], xs[c], v1);
-                v2 = __builtin_fma(-l2[c], xs[c], v2);
-            }
-            if (i1 < kb) y[i1] = v1;
-            if (i2 < kb) y[i2] = v2;
+            if (lane < kNB) y[kb + r] = xb;
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
+        __syncthreads();
+        if (kb == 0) break;
+        for (int i = tid; i < kb; i += kLdlT) {
+            double v = y[i];
+#pragma unroll
+            for (int c = kNB - 1; c >= 0; c--) v = __builtin_fma(-A[(size_t)(kb + c) * ld + i], y[kb + c], v);
+            y[i] = v;
+        }
+        __syncthreads();
     }
+    if (wave != 0) return;
     for (int i = lane; i < n; i += 64) x[i] = y[i];
     if (lane == 0) flags[0] = 0;
 #ifdef ORB_TIMING
@@ -1103,12 +1309,28 @@ __global__ __launch_bounds__(64) void k_lm_begin_fused(LbaDev d, int nChi, int n
 // Single process: the end of an LM trial in one workgroup — the trial's robust chi2 and the
 // scale x^T (lambda x + b) from the producers' partials, the rho decision (lm_decide) and,
 // after a rejected trial, pop() of every free pose and owned point.
+// With fused slots (`fuse`) it closes a group of slots: the last trial's pending decision.
 __global__ __launch_bounds__(1024) void k_lm_decide_fused(LbaDev d, const int32_t* __restrict__ freePoses,
                                                           int maxTrials, int iterations, int fixedIterations,
-                                                          double* __restrict__ trace, int nChi, int nScale) {
+                                                          double* __restrict__ trace, int nChi, int nScale, int fuse) {
     __shared__ int go, pop;
     LmState* st = d.lm;
     const int tid = threadIdx.x;
+    if (fuse) {
+        if (tid < 64 && st->pending) {
+            const LmFuse f{nChi, nScale, maxTrials, iterations, fixedIterations, freePoses, trace};
+            const LmState ls = lm_decide_local(d, f, tid, tid == 0);
+            if (tid == 0) {
+                *st = ls;
+                pop = ls.pop;
+            }
+        } else if (tid == 0) {
+            pop = 0;
+        }
+        __syncthreads();
+        if (pop) lm_pop_slice(d, freePoses, tid, 1024);
+        return;
+    }
     if (tid == 0) {
         st->pop = 0;
         go = st->phase == 1;
@@ -1417,7 +1639,7 @@ int lba_dense_solve(lba_context* c, const double* S, const double* b, int n, dou
     ORB_HIP_TRY(hipMemcpyAsync(dS, S, 8 * (size_t)n * n, hipMemcpyHostToDevice, s));
     ORB_HIP_TRY(hipMemcpyAsync(db, b, 8 * (size_t)n, hipMemcpyHostToDevice, s));
     if (np <= kLdlLdsMaxN)
-        hipLaunchKernelGGL(k_ldlt_solve<true>, dim3(1), dim3(kLdlT), ((size_t)np * (np + 1) + 3 * (size_t)np + 64) * 8, s,
+        hipLaunchKernelGGL(k_ldlt_solve<true>, dim3(1), dim3(kLdlT), ((size_t)np * (np + 1) + 3 * (size_t)np + 128) * 8, s,
                            dS, db, n, nullptr, dx, df, nullptr);
     else
         hipLaunchKernelGGL(k_ldlt_solve<false>, dim3(1), dim3(kLdlT), (3 * (size_t)np + 64) * 8, s, dS, db, n, dw, dx, df,
@@ -1591,10 +1813,12 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
     TRY(dalloc(c, &d.x, 6 * (size_t)NP + 3 * (size_t)NM));
     TRY(dalloc(c, &d.red, 16));
     TRY(dalloc(c, &d.partChi, (size_t)NE / 64 + 2));
+    TRY(dalloc(c, &d.partLin, (size_t)NE / 64 + 2));
     TRY(dalloc(c, &d.partScale, (size_t)NM / 64 + 3));
     TRY(dalloc(c, &d.partMax, (size_t)NP + (size_t)NM / 64 + 2));
     TRY(dalloc(c, &d.flags, 4));
     TRY(dalloc(c, &d.lm, 1));
+    TRY(dalloc(c, &d.lmMid, 1));
     double* d_trace = nullptr;
     TRY(dalloc(c, &d_trace, 4 * 64));
     double* d_ldlw = nullptr;   // global image of the padded reduced matrix when it exceeds LDS
@@ -1642,6 +1866,15 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
     auto grid = [](int n) { return dim3((unsigned)std::max(1, (n + 255) / 256)); };
 
 
+    auto fuse_slots = [&]() { return c->world == 1 && d.nact > 0 && d.M > 0; };
+    // fused slots: the decision of a group's last trial (k_edge_lin takes the others)
+    auto enqueue_close = [&](int iterations) {
+        if (!fuse_slots()) return;
+        const int nbE = (d.nact + 63) / 64, nbB = (d.M + 63) / 64 + 1;
+        hipLaunchKernelGGL(k_lm_decide_fused, dim3(1), dim3(1024), 0, s, d, d_freePoses, maxTrials, iterations,
+                           o->fixed_iterations ? 1 : 0, d_trace, nbE, nbB, 1);
+    };
+
     // One LM "slot": the linearisation of an iteration (runs only when the device state says a
     // new iteration starts) followed by one trial (runs only while the iteration's trial loop
     // is open) and its decision.  Slots are enqueued back to back without host round trips.
@@ -1651,10 +1884,16 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         if (prof) (void)hipEventRecord(ev[0], s);
         // ---- linearisation (G/core/sparse_optimizer.cpp:384-394, block_solver.hpp:502-561)
         const int nbE = (d.nact + 63) / 64, nbV = d.P + (d.M + 63) / 64, nbB = (d.M + 63) / 64 + 1;
-        if (d.nact > 0) hipLaunchKernelGGL(k_edge_lin, dim3(nbE), dim3(64), 0, s, d, hm, hsv);
-        if (nbV > 0) hipLaunchKernelGGL(k_vertex_reduce, dim3(nbV), dim3(256), 0, s, d);
+        // single process with edges and points: the decision and the iteration start ride in
+        // k_edge_lin and k_point_schur (LmFuse), the group of slots ends with one decision kernel
+        const bool fuse = fuse_slots();
+        const LmFuse f{nbE, nbB, maxTrials, iterations, o->fixed_iterations ? 1 : 0, d_freePoses, d_trace};
+        if (d.nact > 0) hipLaunchKernelGGL(k_edge_lin, dim3(nbE), dim3(64), 0, s, d, hm, hsv, fuse ? 1 : 0, f);
+        LbaDev dv = d;
+        if (fuse) dv.lm = d.lmMid;
+        if (nbV > 0) hipLaunchKernelGGL(k_vertex_reduce, dim3(nbV), dim3(256), 0, s, dv);
         if (single) {
-            hipLaunchKernelGGL(k_lm_begin_fused, dim3(1), dim3(64), 0, s, d, nbE, nbV);
+            if (!fuse) hipLaunchKernelGGL(k_lm_begin_fused, dim3(1), dim3(64), 0, s, d, nbE, nbV);
         } else {
             hipLaunchKernelGGL(k_sum, dim3(1), dim3(1024), 0, s, d.echi, d.nact, d.red, d.lm, 0);
             TRY(comm_allreduce_g(c, d.red, 1, 0, d.lm, 0));
@@ -1668,7 +1907,7 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         }
         if (prof) (void)hipEventRecord(ev[1], s);
         // ---- trial: Schur complement, reduced solve, back-substitution + update, new chi2
-        if (d.M > 0) hipLaunchKernelGGL(k_point_schur, dim3((d.M + 63) / 64), dim3(64), 0, s, d);
+        if (d.M > 0) hipLaunchKernelGGL(k_point_schur, dim3((d.M + 63) / 64), dim3(64), 0, s, d, fuse ? 1 : 0, nbE, nbV);
         const int npairs = d.P * (d.P + 1) / 2;
         if (npairs > 0) hipLaunchKernelGGL(k_schur_pairs, dim3(npairs), dim3(kSpT), 0, s, d, root ? 1 : 0);
         if (d.P > 0) TRY(comm_allreduce_g(c, d.S, (size_t)36 * d.P * d.P + 6 * (size_t)d.P, 0, d.lm, 1));
@@ -1676,7 +1915,7 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         if (d.P > 0) {
             const int n = 6 * d.P, np = (n + kNB - 1) & ~(kNB - 1);
             if (np <= kLdlLdsMaxN)
-                hipLaunchKernelGGL(k_ldlt_solve<true>, dim3(1), dim3(kLdlT), ((size_t)np * (np + 1) + 3 * (size_t)np + 64) * 8,
+                hipLaunchKernelGGL(k_ldlt_solve<true>, dim3(1), dim3(kLdlT), ((size_t)np * (np + 1) + 3 * (size_t)np + 128) * 8,
                                    s, d.S, d.bs, n, nullptr, d.x, d.flags, d.lm);
             else
                 hipLaunchKernelGGL(k_ldlt_solve<false>, dim3(1), dim3(kLdlT), (3 * (size_t)np + 64) * 8, s, d.S, d.bs, n,
@@ -1686,10 +1925,11 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         }
         if (prof) (void)hipEventRecord(ev[3], s);
         hipLaunchKernelGGL(k_backsub_update, dim3(nbB), dim3(256), 0, s, d, d_freePoses);
-        if (d.nact > 0) hipLaunchKernelGGL(k_edge_errors, dim3(nbE), dim3(64), 0, s, d, hm, hsv, 1);
+        if (d.nact > 0) hipLaunchKernelGGL(k_edge_errors, dim3(nbE), dim3(64), 0, s, d, hm, hsv, 1, fuse ? 1 : 0);
         if (single) {
-            hipLaunchKernelGGL(k_lm_decide_fused, dim3(1), dim3(1024), 0, s, d, d_freePoses, maxTrials, iterations,
-                               o->fixed_iterations ? 1 : 0, d_trace, nbE, nbB);
+            if (!fuse)
+                hipLaunchKernelGGL(k_lm_decide_fused, dim3(1), dim3(1024), 0, s, d, d_freePoses, maxTrials, iterations,
+                                   o->fixed_iterations ? 1 : 0, d_trace, nbE, nbB, 0);
         } else {
             hipLaunchKernelGGL(k_sum, dim3(1), dim3(1024), 0, s, d.echi, d.nact, d.red, d.lm, 1);
             TRY(comm_allreduce_g(c, d.red, 1, 0, d.lm, 1));
@@ -1749,6 +1989,7 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
             ORB_HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
             int st = ORB_OK;
             for (int i = 0; i < nslots && !st; i++) st = enqueue_slot(iterations, nullptr);
+            if (!st) enqueue_close(iterations);
             const hipError_t ce = hipStreamEndCapture(s, &g);
             if (st) { if (g) (void)hipGraphDestroy(g); return st; }
             if (ce != hipSuccess) return ORB_EGPU;
@@ -1782,6 +2023,7 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
                     if (gOne) ORB_HIP_TRY(hipGraphLaunch(gOne, s));
                     else TRY(enqueue_slot(iterations, c->profile ? &c->slotEv[5 * (size_t)g] : nullptr));
                 }
+                if (!gOne) enqueue_close(iterations);
             }
             ORB_HIP_TRY(hipMemcpyAsync(hst, d.lm, sizeof(LmState), hipMemcpyDeviceToHost, s));
             TRY(lba_wait(c));
