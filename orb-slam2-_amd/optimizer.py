@@ -162,6 +162,35 @@ class LocalBA:
         return dict(linearize_ms=ms[0], schur_ms=ms[1], solve_ms=ms[2], update_ms=ms[3], iterations=it.value,
                     trials=tr.value)
 
+    def prepared(self, prob, opts=None):
+        """The lba_solve call of solve(prob) with its arguments marshalled once: returns a
+        zero-argument callable that runs only the C-ABI call (the benchmark's timed region) and
+        returns (iterations, trials)."""
+        opts = opts or options()
+        nk = len(prob["Tcw"])
+        Tcw = np.ascontiguousarray(prob["Tcw"], np.float32)
+        q, t = np.zeros((nk, 4)), np.zeros((nk, 3))
+        _sig().lba_poses_from_Tcw(_abi.ptr(Tcw), nk, _abi.ptr(q), _abi.ptr(t))
+        a = {k: np.ascontiguousarray(v, PROBLEM_DTYPES[k]) if k in PROBLEM_DTYPES and v is not None else v
+             for k, v in prob.items()}
+        P = _abi.ptr
+        pr = LbaProblem(nk, P(q), P(t), P(a["pose_fixed"]), P(a["pose_id"]), len(a["point_xyz"]), P(a["point_xyz"]),
+                        P(a["point_id"]), P(a.get("point_bad")), len(a["edge_point"]), P(a["edge_point"]),
+                        P(a["edge_pose"]), P(a["edge_stereo"]), P(a["edge_obs"]), P(a["edge_info"]), P(a["edge_cam"]))
+        ne = len(a["edge_point"])
+        out = dict(pose_q=np.zeros((nk, 4)), pose_t=np.zeros((nk, 3)), point_xyz=a["point_xyz"].copy(),
+                   edge_erase=np.zeros(ne, np.uint8), edge_chi2=np.zeros(ne), trace=np.zeros((64, 4)))
+        r = LbaResult(P(out["pose_q"]), P(out["pose_t"]), P(out["point_xyz"]), P(out["edge_erase"]),
+                      P(out["edge_chi2"]), (C.c_int * 2)(0, 0), 0, P(out["trace"]), 0, 0)
+        flag = (C.c_uint8 * 1)(0)
+        keep = (q, t, a, out, Tcw)   # the arrays the structs point into stay alive with the closure
+        fn, h, rp, op, rr = _sig().lba_solve, self._h, C.byref(pr), C.byref(opts), C.byref(r)
+
+        def call():
+            _abi.check("lba_solve", fn(h, rp, op, flag, rr))
+            return (r.iterations[0], r.iterations[1]), r.trials, keep
+        return call
+
     def solve(self, prob, opts=None, stop=None, global_ba=False, robust=True):
         """prob: dict of arrays (synth.ba_problem layout).  stop: a 1-byte ctypes array
         polled like mbAbortBA.  global_ba: Optimizer::BundleAdjustment instead of the local BA
