@@ -567,8 +567,54 @@ def bench_extras(args, amd, dev):
                              "matches_per_pair": float(nm.float().mean())}
     out["batch_sweep_640x480"] = batch_sweep(amd, dev, m)
     out["pose_optimization"] = bench_pose(args, amd, dev)
+    out["single_call_latency"] = bench_single_calls(args, amd, dev)
     out["bow_transform"] = bench_bow(args, amd, dev)
     out["global_ba"] = bench_gba(args, amd, dev)
+    return out
+
+
+def bench_single_calls(args, amd, dev, reps=50):
+    """The host-buffer entry points the C++ shims call once per frame / keyframe, timed one call
+    at a time (median of `reps`, after warm-up; PCIe both ways included): ORBextractor::operator()
+    on one 640x480 image (orb_extract: image in, keypoints + descriptors out), SearchForInitialization
+    on one pair of those frames (orb_search_for_initialization), PoseOptimization of one frame
+    (pose_optimize_batch, B = 1: frame in, pose + outlier flags out).  lba_solve's host path is
+    the `lba` leg."""
+    from orb_slam2_amd import synth, _abi, optimizer as opt
+    import ctypes as C
+
+    def med(fn):
+        for _ in range(5):
+            fn()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return round(1e6 * float(np.median(ts)), 1)
+    cv = synth.canvas(0x5EED0002, 640, 480)
+    img0, img1 = (np.ascontiguousarray(synth.frame(cv, 640, 480, t)) for t in (0, 1))
+    ex = amd.ORBextractor(1000, 1.2, 8, 20, 7, device=dev.index or 0)
+    out = {"orb_extract_640x480_us": med(lambda: ex(img0))}
+    k0, d0 = ex(img0)
+    k1, d1 = ex(img1)
+    m = amd.ORBmatcher(0.9, True, device=dev.index or 0)
+    f0, f1 = amd.Frame(k0, d0, 640, 480), amd.Frame(k1, d1, 640, 480)
+    prev = np.stack([k0["x"], k0["y"]], 1).astype(np.float32)
+    out["search_for_initialization_us"] = med(lambda: m.SearchForInitialization(f0, f1, prev.copy(), 100))
+    fr = synth.pose_problems(n_frames=1, n_points=600, stereo_frac=0.3, seed=21)
+    a = opt.pack_pose_frames(fr)
+    E = int(a["edge_start"][-1])
+    pb = opt.PoseBatch(1, E, _abi.ptr(a["pose_q"]), _abi.ptr(a["pose_t"]), _abi.ptr(a["cam"]), _abi.ptr(a["edge_start"]),
+                       _abi.ptr(a["edge_obs"]), _abi.ptr(a["edge_xw"]), _abi.ptr(a["edge_info"]))
+    q, t = np.zeros((1, 4)), np.zeros((1, 3))
+    outl, ninl, iters = np.zeros(E, np.uint8), np.zeros(1, np.int32), np.zeros((1, 5), np.int32)
+    r = opt.PoseBatchResult(_abi.ptr(q), _abi.ptr(t), _abi.ptr(outl), _abi.ptr(ninl))
+    lib, devi = opt._pose_sig(), dev.index or 0
+    out["pose_optimization_one_frame_us"] = med(
+        lambda: _abi.check("pose", lib.pose_optimize_batch(devi, C.byref(pb), C.byref(r), _abi.ptr(iters))))
+    out["note"] = ("host buffers, PCIe both ways, one call at a time (median); each call is a chain of dependent "
+                   "launches + copies, so these are launch/transfer latencies, not throughput")
     return out
 
 

@@ -227,25 +227,13 @@ __global__ __launch_bounds__(256) void k_grid_sfi(const orb_keypoint* __restrict
 //   (0xFFFFFFFF past the end).  For the reference's loop (R/src/ORBmatcher.cpp:523-549)
 //   the first entry of this order not skipped by vMatchedDistance is bestIdx2 and the next
 //   one carries bestDist2, so the sequential replay reads only this prefix.
-__global__ __launch_bounds__(256) void k_cand_sfi(const orb_keypoint* __restrict__ kps1, const uint8_t* __restrict__ desc1,
-                                                  const int32_t* __restrict__ n1s, const uint8_t* __restrict__ desc2,
-                                                  const int* __restrict__ cellStart, const int* __restrict__ gj,
-                                                  const float2* __restrict__ gxy, const float* __restrict__ prev,
-                                                  int cap, GridParams g, float window, uint32_t* __restrict__ cand,
-                                                  int* __restrict__ ncand, uint32_t* __restrict__ topk,
-                                                  int* __restrict__ status) {
-    __shared__ int segOff[4][kGridCols + 1];
-    __shared__ uint32_t sj[4][kMaxCand];
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    int bx, b;
-    xcd_block_2d(bx, b);
-    const int i1 = bx * 4 + wid;
-    const int n1 = min((int)n1s[b], cap);
-    if (i1 >= n1) return;
-    const orb_keypoint* K1 = kps1 + (size_t)b * cap;
+__device__ __forceinline__ void cand_query(const orb_keypoint& kp1, int i1, int b, int lane, const uint8_t* __restrict__ desc1,
+                                           const uint8_t* __restrict__ desc2, const int* __restrict__ cellStart,
+                                           const int* __restrict__ gj, const float2* __restrict__ gxy,
+                                           const float* __restrict__ prev, int cap, const GridParams& g, float window,
+                                           uint32_t* __restrict__ cand, int* __restrict__ ncand,
+                                           uint32_t* __restrict__ topk, int* __restrict__ status, int* so, uint32_t* J) {
     int* nc = ncand + (size_t)b * cap + i1;
-    const orb_keypoint kp1 = K1[i1];
-    if (kp1.octave > 0) { if (lane == 0) *nc = 0; return; }
     float px, py;
     if (prev) { px = prev[((size_t)b * cap + i1) * 2]; py = prev[((size_t)b * cap + i1) * 2 + 1]; }
     else { px = kp1.x; py = kp1.y; }
@@ -256,8 +244,6 @@ __global__ __launch_bounds__(256) void k_cand_sfi(const orb_keypoint* __restrict
     const float2* GXY = gxy + (size_t)b * cap;
     const uint4* dq4 = reinterpret_cast<const uint4*>(desc1 + ((size_t)b * cap + i1) * 32);
     const uint4 qa = dq4[0], qb = dq4[1];
-    int* so = segOff[wid];
-    uint32_t* J = sj[wid];
     // one lane per grid column of the window: bucket range [cy0, cy1] of that column
     const int ncx = q.cx1 - q.cx0 + 1;   // <= 64
     int segS = 0, segL = 0;
@@ -344,6 +330,47 @@ __global__ __launch_bounds__(256) void k_cand_sfi(const orb_keypoint* __restrict
     if (lane < kTopK) {
         uint32_t* tk = topk + ((size_t)b * cap + i1) * kTopK;
         tk[lane] = run == ~0u ? ~0u : J[run & 0x7FFu];
+    }
+}
+
+
+// One wave per query would launch a wave for every keypoint slot of every frame although only
+// the level-0 queries (about a fifth, and the first ones: keypoints are concatenated by level)
+// do work.  Instead kCandWaves waves per frame: wave w owns queries w, w + kCandWaves, ...; it
+// reads their octaves in one load per lane, zeroes the candidate count of the others in
+// parallel, and runs cand_query on its level-0 ones.
+constexpr int kCandWaves = 128;
+__global__ __launch_bounds__(256) void k_cand_sfi(const orb_keypoint* __restrict__ kps1, const uint8_t* __restrict__ desc1,
+                                                  const int32_t* __restrict__ n1s, const uint8_t* __restrict__ desc2,
+                                                  const int* __restrict__ cellStart, const int* __restrict__ gj,
+                                                  const float2* __restrict__ gxy, const float* __restrict__ prev,
+                                                  int cap, GridParams g, float window, uint32_t* __restrict__ cand,
+                                                  int* __restrict__ ncand, uint32_t* __restrict__ topk,
+                                                  int* __restrict__ status) {
+    __shared__ int segOff[4][kGridCols + 1];
+    __shared__ uint32_t sj[4][kMaxCand];
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    int bx, b;
+    xcd_block_2d(bx, b);
+    const int w = bx * 4 + wid;
+    const int n1 = min((int)n1s[b], cap);
+    const orb_keypoint* K1 = kps1 + (size_t)b * cap;
+    int* NC = ncand + (size_t)b * cap;
+    for (int base = w; base < n1; base += kCandWaves * 64) {
+        const int iq = base + kCandWaves * lane;
+        const bool in = iq < n1;
+        const int oct = K1[in ? iq : 0].octave;
+        if (in && oct > 0) NC[iq] = 0;
+        uint64_t act = __ballot(in && oct == 0);
+        while (act) {
+            const int k = __builtin_ctzll(act);
+            act &= act - 1;
+            const int i1 = base + kCandWaves * k;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();   // the wave's LDS scratch is reused query after query
+            cand_query(K1[i1], i1, b, lane, desc1, desc2, cellStart, gj, gxy, prev, cap, g, window, cand, ncand, topk,
+                       status, segOff[wid], sj[wid]);
+        }
     }
 }
 
@@ -1602,7 +1629,7 @@ int orb_search_for_initialization(orb_matcher* m, const orb_frame_view* f1, cons
     ORB_HIP_TRY(hipMemsetAsync(m->d_status, 0, 4, s));
     const GridParams g = grid_of(f2);
     hipLaunchKernelGGL(k_grid_sfi, dim3(1), dim3(256), 0, s, m->d_k2, m->d_n + 1, cap, g, m->d_cs, m->d_gj, m->d_gxy);
-    hipLaunchKernelGGL(k_cand_sfi, dim3((cap + 3) / 4, 1), dim3(256), 0, s, m->d_k1, m->d_d1, m->d_n, m->d_d2, m->d_cs,
+    hipLaunchKernelGGL(k_cand_sfi, dim3(kCandWaves / 4, 1), dim3(256), 0, s, m->d_k1, m->d_d1, m->d_n, m->d_d2, m->d_cs,
                        m->d_gj, m->d_gxy, m->d_prev, cap, g, (float)window, m->d_cand, m->d_ncand, m->d_topk,
                        m->d_status);
     const size_t lds = resolve_sfi_lds(cap);
@@ -1637,7 +1664,7 @@ int orb_search_for_initialization_batch_device(orb_matcher* m, const orb_keypoin
     g.winv = (float)kGridCols / (float)width;
     g.hinv = (float)kGridRows / (float)height;
     hipLaunchKernelGGL(k_grid_sfi, dim3(nb), dim3(256), 0, s, d_kps2, d_n2, cap, g, m->d_cs, m->d_gj, m->d_gxy);
-    hipLaunchKernelGGL(k_cand_sfi, dim3((cap + 3) / 4, nb), dim3(256), 0, s, d_kps1, d_desc1, d_n1, d_desc2, m->d_cs,
+    hipLaunchKernelGGL(k_cand_sfi, dim3(kCandWaves / 4, nb), dim3(256), 0, s, d_kps1, d_desc1, d_n1, d_desc2, m->d_cs,
                        m->d_gj, m->d_gxy, (const float*)nullptr, cap, g, (float)window, m->d_cand, m->d_ncand,
                        m->d_topk, m->d_status);
     const size_t lds = resolve_sfi_lds(cap);
