@@ -30,6 +30,7 @@
 #include <cmath>
 #include <cstring>
 #include <numeric>
+#include <functional>
 #include <vector>
 
 #include "common.h"
@@ -1949,8 +1950,9 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
     // one optimize() call (G/core/sparse_optimizer.cpp:354-419).  The host enqueues as many
     // slots as iterations remain (one trial each), then reads the device state once: more
     // slots only when trials were rejected.  The stop flag is polled between those groups.
-    auto optimize = [&](int iterations, int& itersDone) -> int {
+    auto optimize = [&](int iterations, int& itersDone, const std::function<int()>& tail, bool& tailRan) -> int {
         itersDone = 0;
+        tailRan = false;
         if (hs.P + hs.M == 0 && c->world == 1) return ORB_OK;
         bool stopNow = false;
         TRY(agreed(stopped(), &stopNow));
@@ -2025,6 +2027,11 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
                 }
                 if (!gOne) enqueue_close(iterations);
             }
+            // speculative: what the host reads after optimize() (edge chi2 / depth, estimates)
+            // rides behind every group, so the last group's copy is already there when the LM
+            // state says the loop is over
+            TRY(tail());
+            tailRan = true;
             ORB_HIP_TRY(hipMemcpyAsync(hst, d.lm, sizeof(LmState), hipMemcpyDeviceToHost, s));
             TRY(lba_wait(c));
             if (c->profile) {
@@ -2062,37 +2069,42 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
 #ifdef ORB_TIMING
     std::chrono::steady_clock::time_point hT[10];
 #endif
+    // pinned staging of everything the host reads after an optimize(): chi2 (8 NE), depth flag
+    // (NE), then q, t, X (contiguous in the problem batch); reserved before any copy is queued
+    const size_t estOff = (9 * (size_t)NE + 255) & ~(size_t)255;
+    const size_t bq = ((32 * (size_t)NP + 255) & ~(size_t)255), bt = ((24 * (size_t)NP + 255) & ~(size_t)255);
+    const size_t estBytes = bq + bt + 24 * (size_t)NM;
+    TRY(stage_reserve(c, 2, estOff + estBytes));
+    char* const hStage = c->stage[2];
+    const std::function<int()> tail = [&]() -> int {
+        if (NE > 0) {
+            hipLaunchKernelGGL(k_edge_check, grid(NE), dim3(256), 0, s, d, NE, d_chi2, d_depth);
+            ORB_HIP_TRY(hipMemcpyAsync(hStage, d_chi2, 8 * (size_t)NE, hipMemcpyDeviceToHost, s));
+            ORB_HIP_TRY(hipMemcpyAsync(hStage + 8 * (size_t)NE, d_depth, NE, hipMemcpyDeviceToHost, s));
+        }
+        ORB_HIP_TRY(hipMemcpyAsync(hStage + estOff, q, estBytes, hipMemcpyDeviceToHost, s));
+        return ORB_OK;
+    };
+    auto ensure_tail = [&](bool ran) -> int {   // an optimize() that ran no group queued no tail
+        if (ran) return ORB_OK;
+        TRY(tail());
+        return lba_wait(c);
+    };
+    const double* chi = reinterpret_cast<const double*>(hStage);
+    const uint8_t* dep = reinterpret_cast<const uint8_t*>(hStage + 8 * (size_t)NE);
     HSTAMP(0);
     // ---- R/src/Optimizer.cpp:789-841
     TRY(init_opt(0));
     HSTAMP(1);
-    TRY(optimize(o->iters1, r->iterations[0]));
+    bool tailRan = false;
+    TRY(optimize(o->iters1, r->iterations[0], tail, tailRan));
     HSTAMP(2);
     bool stopAfter1 = false;
     TRY(agreed(stopped() || devStopped, &stopAfter1));
     const bool bDoMore = !global && !stopAfter1;   // global BA: one optimize(nIterations), R :230-231
-    auto edge_check = [&](std::vector<double>& chi, std::vector<uint8_t>& dep) -> int {
-        if (NE > 0) hipLaunchKernelGGL(k_edge_check, grid(NE), dim3(256), 0, s, d, NE, d_chi2, d_depth);
-        chi.resize(NE);
-        dep.resize(NE);
-        TRY(stage_reserve(c, 2, 9 * (size_t)NE + 64));   // pinned: one pageable D2H costs more than the kernel
-        char* h = c->stage[2];
-        if (NE > 0) {
-            ORB_HIP_TRY(hipMemcpyAsync(h, d_chi2, 8 * (size_t)NE, hipMemcpyDeviceToHost, s));
-            ORB_HIP_TRY(hipMemcpyAsync(h + 8 * (size_t)NE, d_depth, NE, hipMemcpyDeviceToHost, s));
-        }
-        TRY(lba_wait(c));
-        if (NE > 0) {
-            std::memcpy(chi.data(), h, 8 * (size_t)NE);
-            std::memcpy(dep.data(), h + 8 * (size_t)NE, NE);
-        }
-        return ORB_OK;
-    };
-    std::vector<double> chi;
-    std::vector<uint8_t> dep;
     const int own0 = (int)((long long)NM * c->rank / c->world), own1 = (int)((long long)NM * (c->rank + 1) / c->world);
     if (bDoMore) {
-        TRY(edge_check(chi, dep));
+        TRY(ensure_tail(tailRan));
         for (int e = 0; e < NE; e++) {
             if (p->point_bad && p->point_bad[p->edge_point[e]]) continue;
             const double thr = p->edge_stereo[e] ? o->chi2_stereo : o->chi2_mono;
@@ -2117,11 +2129,11 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         HSTAMP(3);
         TRY(init_opt(0));
         HSTAMP(4);
-        TRY(optimize(o->iters2, r->iterations[1]));
+        TRY(optimize(o->iters2, r->iterations[1], tail, tailRan));
     }
     HSTAMP(5);
     // ---- final check (R/src/Optimizer.cpp:850-880) and write-back data
-    TRY(edge_check(chi, dep));
+    TRY(ensure_tail(tailRan));
     for (int e = 0; e < NE; e++) {
         const int pt = p->edge_point[e];
         const bool mine = pt >= own0 && pt < own1;
@@ -2133,13 +2145,8 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         }
         if (r->edge_erase) r->edge_erase[e] = er;
     }
-    {   // estimates back through pinned staging (q, t, X are contiguous in the problem batch)
-        const size_t bq = ((32 * (size_t)NP + 255) & ~(size_t)255), bt = ((24 * (size_t)NP + 255) & ~(size_t)255);
-        const size_t tot = bq + bt + 24 * (size_t)NM;
-        TRY(stage_reserve(c, 2, tot));
-        char* h = c->stage[2];
-        ORB_HIP_TRY(hipMemcpyAsync(h, q, tot, hipMemcpyDeviceToHost, s));
-        TRY(lba_wait(c));
+    {   // estimates (q, t, X)
+        const char* h = hStage + estOff;
         if (r->pose_q) std::memcpy(r->pose_q, h, 32 * (size_t)NP);
         if (r->pose_t) std::memcpy(r->pose_t, h + bq, 24 * (size_t)NP);
         if (r->point_xyz) std::memcpy(r->point_xyz, h + bq + bt, 24 * (size_t)NM);

@@ -17,8 +17,14 @@ for a in sys.argv[1:]:
     kw[k] = int(v)
 pb = synth.ba_problem(**kw)
 ba = amd.LocalBA()
-for i in range(4):
+n = 12
+call = ba.prepared(pb)
+ts = []
+for i in range(n):
     t0 = time.perf_counter()
-    r = ba.solve(pb)
+    its, trials, _ = call()
     dt = time.perf_counter() - t0
-    print(f"solve {i}: {dt * 1e3:.3f} ms, iterations {r['iterations']}, trials {r['trials']}", flush=True)
+    ts.append(dt)
+    print(f"solve {i}: {dt * 1e3:.3f} ms, iterations {its}, trials {trials}", flush=True)
+import statistics  # noqa: E402
+print(f"median of solves 4..{n - 1}: {1e3 * statistics.median(ts[4:]):.3f} ms", flush=True)
