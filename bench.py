@@ -73,8 +73,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=256, help="frames per step per GPU")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--batch", type=int, default=384, help="frames per step per GPU")
+    ap.add_argument("--streams", type=int, default=3,
                     help="independent frame sequences per GPU, each on its own HIP stream (batch split)")
     ap.add_argument("--match-stream", action="store_true",
                     help="SearchForInitialization on a second stream per sequence, overlapping the next step's "
@@ -1047,8 +1047,8 @@ def main():
         "config": {"workload": f"synthetic {W}x{H} grayscale stream, {NF} feat/frame, 8 levels, scale 1.2, "
                                f"FAST 20/7; extract + SearchForInitialization(t-1,t; window 100, nnratio 0.9, "
                                f"checkOri) per frame; {B} frames per step per GPU as {S} independent "
-                               f"sequences, each on an extraction and a matching HIP stream"
-                               f"{' (matching of step s overlaps extraction of step s+1)' if args.match_stream else ''}"
+                               f"sequences, each on its own HIP stream"
+                               f"{' plus a matching stream (matching of step s overlaps extraction of step s+1)' if args.match_stream else ' (extraction then matching)'}"
                                f", HBM-resident",
                    "batch_per_gpu": B, "streams_per_gpu": S, "width": W, "height": H, "nfeatures": NF,
                    "parallelism": f"frame-sharded x{world}"},
