@@ -1097,6 +1097,18 @@ def main():
     b_ext = float(P[0] + 2 * P[1:].sum()) + float(np.mean(cnt)) * 60.0
     result["pipeline_roofline"] = {"bytes_per_frame": b_ext, "achieved_gbs": round(b_ext * value / 1e9, 2),
                                    "peak_gbs": HBM_PEAK_GBS, "frac": round(b_ext * value / 1e9 / HBM_PEAK_GBS, 5)}
+    # the whole step against the VALU bound: every extraction + matching kernel's lane-ops per
+    # frame (committed PMC pass of this configuration) x frames/s
+    kern = ("k_pyramid", "k_fast_cell", "k_octree", "k_orient_desc", "k_grid_sfi", "k_cand_sfi", "k_resolve_sfi")
+    ops = [pmc_valu_ops(k, W, H, NF, Bs) for k in kern]
+    if all(o is not None for o in ops):
+        per_frame = sum(ops) / Bs
+        ach = per_frame * value / 1e12
+        result["pipeline_valu"] = {"lane_ops_per_frame": round(per_frame), "kernels": list(kern),
+                                   "achieved": round(ach, 3), "unit": "TOP/s", "peak": VALU_PEAK_TOPS,
+                                   "frac": round(ach / VALU_PEAK_TOPS, 4), "measured_issue_peak": VALU_MEASURED_TOPS,
+                                   "frac_of_measured_issue_peak": round(ach / VALU_MEASURED_TOPS, 4),
+                                   "ops_source": PMC_VALU.name}
     if not args.no_lba:
         result["lba"] = bench_lba(args, amd, dev, local, rank, world)
     if not args.no_stereo:
