@@ -290,7 +290,7 @@ def bench_lba(args, amd, dev, local, rank, world):
                          "chi2_trace": [float(x) for x in r["trace"][:, 1]],
                          "erased_edges": erased}}
     out["roofline"] = lba_roofline(pb, out, world)
-    if rank == 0 and not args.no_cpu:
+    if world == 1 and not args.no_cpu:   # the CPU baseline is an N=1 figure
         sys.path.insert(0, str(ROOT / "tests"))
         import oracle_ref as O
 
@@ -438,7 +438,7 @@ def bench_config5(args, amd, dev, rank, world):
                     "batches_per_step": nb, "pairs_per_rank": P,
                     "stereo_matches_per_pair": round(float(tot[0]) / total_pairs, 1)}
         del ex
-    if rank == 0 and not args.no_cpu:
+    if world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline_stereo(cv, W, H, NF, EUROC_MBF, 8)
     return out
 
@@ -1115,7 +1115,7 @@ def main():
         result["config5_stereo_sharded"] = bench_config5(args, amd, dev, rank, world)
     if world == 1 and not args.no_extras:
         result["extras"] = bench_extras(args, amd, dev)
-    if rank == 0 and not args.no_cpu:
+    if world == 1 and not args.no_cpu:   # rank 0 at N=1 only
         result["cpu_baseline"] = cpu_baseline(pool_np[: min(len(pool_np), 512)], NF, args.cpu_seconds)
         result["speedup_vs_cpu_baseline"] = round(value / result["cpu_baseline"]["value"], 1)
     if rank == 0:
