@@ -547,15 +547,15 @@ constexpr int kTileW = 64, kTileH = 16;   // blur tiles
 __host__ __device__ inline int fc_patch_stride(int maxW) { return ((maxW + 8 + 3) & ~3) + 4; }
 __host__ __device__ inline int fc_score_stride(int maxW) { return (maxW + 3) & ~3; }
 // patch (window bytes; after scoring it holds the u8 suppressed score per survivor), score map,
-// u16 y*64+x list of the pre-test survivors.  ~5.9 KB per wave for 36 x 36 regions: six
-// 4-wave workgroups per CU.
+// u16 y*64+x list of the pre-test survivors, 64 u16 sinks.  ~6.0 KB per wave for 36 x 36
+// regions: six 4-wave workgroups per CU.
 __host__ __device__ inline int fc_wave_bytes(int maxW, int maxH) {
     int patch = ((maxH + 6) * fc_patch_stride(maxW) + 15) & ~15;
     const int keep = (maxW * maxH + 15) & ~15;
     if (patch < keep) patch = keep;
-    const int sc = (maxH * fc_score_stride(maxW) + 15) & ~15;
+    const int sc = ((maxH + 2) * fc_score_stride(maxW + 2) + 15) & ~15;   // 1-px zero border
     const int list = (maxW * maxH * 2 + 15) & ~15;
-    return patch + sc + list;
+    return patch + sc + list + 128;   // + one u16 sink per lane (branch-free list emission)
 }
 
 // One wave per FAST cell (R/src/ORBextractor.cpp:851-896): cv::FAST on the cell's window,
@@ -608,13 +608,14 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
         if (lane == 0) { *cnt_out = 0; atomicOr(status, 1); }
         return;
     }
-    const int PWS = fc_patch_stride(maxW), W32 = PWS >> 2, SCS = fc_score_stride(maxW);
+    const int PWS = fc_patch_stride(maxW), W32 = PWS >> 2, SCS = fc_score_stride(maxW + 2);
     unsigned char* base = dsm + (size_t)wid * fc_wave_bytes(maxW, maxH);
     uint32_t* patch32 = reinterpret_cast<uint32_t*>(base);
     const uint8_t* patch = base;
     const int patchBytes = max(((maxH + 6) * PWS + 15) & ~15, (maxW * maxH + 15) & ~15);
     uint8_t* sc = base + patchBytes;
-    uint16_t* list = reinterpret_cast<uint16_t*>(sc + ((maxH * SCS + 15) & ~15));
+    uint16_t* list = reinterpret_cast<uint16_t*>(sc + (((maxH + 2) * SCS + 15) & ~15));
+    uint16_t* const lsink = list + (((maxW * maxH * 2 + 15) & ~15) >> 1) + lane;
     uint8_t* kp = base;   // the window is dead once every survivor is scored (phase 3)
     const uint8_t* img = pyr + (size_t)b * g.frameBytes + L.off;
     const int rx0 = iniX + 3, ry0 = iniY + 3;
@@ -629,23 +630,27 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
         const int R = 64 / NW1, k = lane % NW1, r0 = lane / NW1;
         const int rows = rh + 6;
         const int pitch = L.pitch;
+        // buffer loads over the rest of the frame slab: a row past the window (or past the slab:
+        // reads 0) is loaded but never stored, so no clamp and no exec mask; the row step is a
+        // scalar offset, the lane's part one 24-bit multiply-add
+        const __amdgpu_buffer_rsrc_t rs = buf_rsrc(img, (uint32_t)(g.frameBytes - L.off));
+        const uint32_t laneOff = __umul24((uint32_t)(ry0 - 3 + r0), (uint32_t)pitch) + (uint32_t)(ga + 4 * k);
+        uint32_t* const sink = reinterpret_cast<uint32_t*>(list) + lane;   // the list is written only later
         for (int rb = 0; rb < rows; rb += 8 * R) {
             uint32_t a[8];
-            // every lane loads (row clamped into the window, so the address is always inside the
-            // level): no exec-masked branch, all eight loads in flight together
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                a[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)laneOff, (rb + u * R) * pitch, 0);
 #pragma unroll
             for (int u = 0; u < 8; u++) {
-                const int r = min(rb + u * R + min(r0, R - 1), rows - 1);
-                a[u] = *reinterpret_cast<const uint32_t*>(img + (ry0 - 3 + r) * pitch + ga + 4 * min(k, NW));
-            }
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const uint32_t nx = __shfl_down(a[u], 1, 64);
+                // the next dword of the row sits in the next lane (DPP wave_shl:1, no LDS round trip)
+                const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a[u], 0x130, 0xF, 0xF, false);
                 const int r = rb + u * R + r0;
-                if (r0 < R && r < rows && k < NW) patch32[r * W32 + k] = __builtin_amdgcn_alignbyte(nx, a[u], sh);
+                const bool st = r0 < R && r < rows && k < NW;
+                *(st ? patch32 + r * W32 + k : sink) = __builtin_amdgcn_alignbyte(nx, a[u], sh);
             }
         }
-        for (int q = lane; q < rh * SCS / 4; q += 64) reinterpret_cast<uint32_t*>(sc)[q] = 0u;
+        for (int q = lane; q < (rh + 2) * SCS / 4; q += 64) reinterpret_cast<uint32_t*>(sc)[q] = 0u;
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -692,10 +697,16 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
             }
             const int cntW = __popc(want);
             const int incl = wave_incl_scan_dpp(cntW);
-            int pos = n + incl - cntW;
+            const int pos = n + incl - cntW;
+            // branch-free emission: entry kk at pos + (survivors below kk); the others go to the
+            // lane's sink past the list
+            const uint16_t e0 = (uint16_t)(y * 64 + 4 * gq);
 #pragma unroll
-            for (int kk = 0; kk < 4; kk++)
-                if (want & (1u << kk)) list[pos++] = (uint16_t)(y * 64 + 4 * gq + kk);
+            for (int kk = 0; kk < 4; kk++) {
+                const bool on = (want >> kk) & 1u;
+                const int at = pos + __popc(want & ((1u << kk) - 1u));
+                *(on ? list + at : lsink) = (uint16_t)(e0 + kk);
+            }
             n += __shfl(incl, 63, 64);
         }
     }
@@ -753,7 +764,7 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
         q[12] = patch[cc - 3];           q[13] = patch[cc + PWS - 3];
         q[14] = patch[cc + 2 * PWS - 2]; q[15] = patch[cc + 3 * PWS - 1];
         const int S = fast_score(patch[cc], q);
-        if (S >= g.tmin && S > 0) sc[y * SCS + x] = (uint8_t)S;
+        if (S >= g.tmin && S > 0) sc[(y + 1) * SCS + x + 1] = (uint8_t)S;
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -764,22 +775,18 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
     for (int k = lane; k < n; k += 64) {
         const int p = list[k];
         const int y = p >> 6, x = p & 63;
-        const int si = y * SCS + x;
+        const int si = (y + 1) * SCS + x + 1;   // the zero border stands for "outside the region"
         const int s = sc[si];
-        int keep = 0;
-        if (s > 0) {
-            int nb = 0;
+        int nb = 0;
 #pragma unroll
-            for (int dy = -1; dy <= 1; dy++) {
+        for (int dy = -1; dy <= 1; dy++) {
 #pragma unroll
-                for (int dx = -1; dx <= 1; dx++) {
-                    if (dx == 0 && dy == 0) continue;
-                    const int xx = x + dx, yy = y + dy;
-                    if (xx >= 0 && xx < rw && yy >= 0 && yy < rh) nb = max(nb, (int)sc[si + dy * SCS + dx]);
-                }
+            for (int dx = -1; dx <= 1; dx++) {
+                if (dx == 0 && dy == 0) continue;
+                nb = max(nb, (int)sc[si + dy * SCS + dx]);
             }
-            keep = s > nb ? s : 0;
         }
+        const int keep = s > 0 && s > nb ? s : 0;
         kp[k] = (uint8_t)keep;
         anyIni |= keep > 0 && keep >= g.iniTh;
     }
