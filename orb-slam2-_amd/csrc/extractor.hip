@@ -1513,24 +1513,25 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
 
     // 1. patch
     if (x - 24 >= 0 && x + 24 <= L.w && y - 21 >= 0 && y + 21 < L.h) {
+        // lane = (row r0 of 4 per pass, aligned source dword k of 13): one buffer load per pass
+        // at a scalar row offset (rows past the window, or past the slab, read harmlessly and are
+        // never stored), the next dword of the row from the next lane by DPP wave_shl:1, the
+        // realigned dword stored (lanes with no patch dword write into the row-sum area, which
+        // step 3a overwrites)
         const int gx0 = x - 24, sh = gx0 & 3, ga = gx0 - sh;
         const int pitch = L.pitch;
-        const uint8_t* src0 = img + (y - 21) * pitch + ga;
-        for (int t0 = 0; t0 < kOdRows * 12; t0 += 64 * 4) {
-            uint32_t a0[4], a1[4];
-            // unconditional loads (index clamped into the window): all in flight together
+        const long long winOff = (long long)L.off + (long long)(y - 21) * pitch + ga;
+        const __amdgpu_buffer_rsrc_t rs = buf_rsrc(img + (winOff - L.off), (uint32_t)(g.frameBytes - winOff));
+        const int r0 = lane / 13, k = lane - 13 * r0;
+        const uint32_t laneOff = __umul24((uint32_t)r0, (uint32_t)pitch) + 4u * (uint32_t)k;
+        uint32_t* const sink = reinterpret_cast<uint32_t*>(RS) + lane;
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int t = min(t0 + u * 64 + lane, kOdRows * 12 - 1);
-                const uint8_t* src = src0 + (t / 12) * pitch + 4 * (t % 12);
-                a0[u] = *reinterpret_cast<const uint32_t*>(src);
-                a1[u] = *reinterpret_cast<const uint32_t*>(src + 4);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int t = t0 + u * 64 + lane;
-                if (t < kOdRows * 12) P32[t] = __builtin_amdgcn_alignbyte(a1[u], a0[u], sh);
-            }
+        for (int rb = 0; rb < kOdRows; rb += 4) {
+            const uint32_t a = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)laneOff, rb * pitch, 0);
+            const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a, 0x130, 0xF, 0xF, false);
+            const int r = rb + r0;
+            const bool st = r0 < 4 && k < 12 && r < kOdRows;
+            *(st ? P32 + r * 12 + k : sink) = __builtin_amdgcn_alignbyte(nx, a, sh);
         }
     } else {
         uint8_t* P8w = od_sm[wid];
@@ -1550,15 +1551,11 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
             const int v = it * 8 + vr - 15;
             if (v > 15) continue;
             const int um = g.umax[abs(v)];
-            uint32_t wu = 0, w1 = 0;
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int u = 4 * d + j - 16;
-                if (abs(u) <= um) {
-                    wu |= (uint32_t)(u + 16) << (8 * j);
-                    w1 |= 1u << (8 * j);
-                }
-            }
+            // bytes j with |4d + j - 16| <= um, i.e. j in [16 - um - 4d, 16 + um - 4d] ∩ [0, 3]
+            const int ja = max(0, 16 - um - 4 * d), jb = min(3, 16 + um - 4 * d);
+            const uint32_t m = ja > jb ? 0u : (0xFFFFFFFFu << (8 * min(ja, 3))) & (0xFFFFFFFFu >> (8 * (3 - max(jb, 0))));
+            const uint32_t w1 = m & 0x01010101u;
+            const uint32_t wu = m & (0x03020100u + (uint32_t)(4 * d) * 0x01010101u);   // bytes u + 16 = 4d + j
             const uint32_t pw = P32[(21 + v) * 12 + 2 + d];
             const int s1 = (int)__builtin_amdgcn_udot4(pw, w1, 0u, false);
             m10 += (int)__builtin_amdgcn_udot4(pw, wu, 0u, false) - 16 * s1;
