@@ -85,6 +85,8 @@ struct LbaDev {
     const uint8_t* est;         // stereo flag
     const double *obs, *info, *cam;
     uint8_t* robust;
+    uint8_t* emask;             // [NE] 1 = the edge takes part (its level is the optimized one), 0 = outlier
+    const uint8_t* bad;         // [NM] MapPoint::isBad() at the call (kept out of the outlier pass)
     double* err;                // [NE][3] last computed error
     // active structure (per optimize())
     const int32_t* act;         // active edges
@@ -143,9 +145,16 @@ __device__ __forceinline__ double d_edge_chi2(const LbaDev& d, int e) {
     return s;
 }
 
-// computeError of active edge k; echi[k] = its robust chi2 (activeRobustChi2 term), returned
+// computeError of active edge k; echi[k] = its robust chi2 (activeRobustChi2 term), returned.
+// An edge the outlier pass moved to level 1 (emask 0) is not active in the second optimize():
+// chi2 0, and its stored error is left as the first round last computed it (g2o's chi2() of a
+// level-1 edge reads that stale error in the final check, R/src/Optimizer.cpp:850-880).
 __device__ __forceinline__ double edge_error(const LbaDev& d, int k, double hmono, double hstereo) {
     const int e = d.act[k];
+    if (!d.emask[e]) {
+        d.echi[k] = 0.0;
+        return 0.0;
+    }
     double Xc[3];
     d_transform(d, d.eps[e], d.ept[e], Xc);
     const double* cam = d.cam + 5 * e;
@@ -245,6 +254,16 @@ __global__ __launch_bounds__(64) void k_edge_errors(LbaDev d, double hmono, doub
 // Hll_e: 3x3 upper (00 01 02 11 12 22); Hpp_e: 6x6 upper row-major (21); Hpl_e: 6x3; bl_e: 3; bp_e: 6
 __device__ __forceinline__ void edge_linearize(const LbaDev& d, int k, double hmono, double hstereo) {
     const int e = d.act[k];
+    if (!d.emask[e]) {   // level-1 edge: its quadratic-form blocks are exact zeros
+        for (int i = 0; i < 6; i++) d.Hll_e[6 * (size_t)k + i] = 0.0;
+        for (int i = 0; i < 3; i++) d.bl_e[3 * (size_t)k + i] = 0.0;
+        if (d.poseIdx[d.eps[e]] >= 0) {
+            for (int i = 0; i < 21; i++) d.Hpp_e[21 * (size_t)k + i] = 0.0;
+            for (int i = 0; i < 6; i++) d.bp_e[6 * (size_t)k + i] = 0.0;
+            for (int i = 0; i < 18; i++) d.Hpl_e[18 * (size_t)k + i] = 0.0;
+        }
+        return;
+    }
     const int pose = d.eps[e];
     double R[9], Xc[3];
     d_quat_to_R(d.q + 4 * pose, R);
@@ -332,6 +351,7 @@ __device__ __forceinline__ void edge_linearize(const LbaDev& d, int k, double hm
 // Phase-0 linearisation of active edge k (computeActiveErrors + linearizeOplus +
 // constructQuadraticForm, G/core/sparse_optimizer.cpp:384-394, block_solver.hpp:502-561).
 // One wave per 64 edges (a launch wide enough to reach every CU); partChi[block] as above.
+__device__ __forceinline__ void edge_lin_body(const LbaDev& d, double hmono, double hstereo, int fuse);
 // Fused slots: first takes the previous trial's pending decision (lm_decide_local; workgroup
 // 0 writes it back) and, after a rejection, restores this workgroup's slice of the estimates.
 __global__ __launch_bounds__(64) void k_edge_lin(LbaDev d, double hmono, double hstereo, int fuse, LmFuse f) {
@@ -341,9 +361,25 @@ __global__ __launch_bounds__(64) void k_edge_lin(LbaDev d, double hmono, double 
         const int phase = ls.phase, pop = ls.pop;
         if (pop) lm_pop_slice(d, f.freePoses, blockIdx.x * 64 + threadIdx.x, (int)gridDim.x * 64);
         if (phase != 0) return;
+        if (pop) {
+            // a rejected trial that still ends the iteration (fixed-iteration mode, rho == 0 or a
+            // failed solve) is followed by the next linearisation in this same launch, while other
+            // workgroups are still restoring their slices: read the restored values from the push()
+            // backups instead (bX for every active point, bq / bt for every pose — fixed poses'
+            // backups are their never-changing estimates, copied at the solve's start)
+            LbaDev db = d;
+            db.X = d.bX;
+            db.q = d.bq;
+            db.t = d.bt;
+            edge_lin_body(db, hmono, hstereo, fuse);
+            return;
+        }
     } else if (lm_off(d.lm, 0)) {
         return;
     }
+    edge_lin_body(d, hmono, hstereo, fuse);
+}
+__device__ __forceinline__ void edge_lin_body(const LbaDev& d, double hmono, double hstereo, int fuse) {
     const int k = blockIdx.x * 64 + threadIdx.x;
     double chi = 0.0;
     if (k < d.nact) {
@@ -1363,6 +1399,24 @@ __global__ __launch_bounds__(1024) void k_lm_decide_fused(LbaDev d, const int32_
     }
 }
 
+// The outlier pass between the two optimize() rounds (R/src/Optimizer.cpp:805-836) on the
+// device: every active edge of a good point whose chi2 (k_edge_check) exceeds the threshold or
+// whose depth is not positive leaves the optimisation (level 1 -> emask 0), and every edge of a
+// good point loses its robust kernel.  The block structure is kept: a level-1 edge contributes
+// exact zeros, so a vertex left without active edges keeps a decoupled lambda-only block and
+// a zero step, as g2o leaves an inactive vertex untouched.
+__global__ __launch_bounds__(256) void k_outlier_mask(LbaDev d, const double* __restrict__ chi2,
+                                                      const uint8_t* __restrict__ depthPos, double thMono,
+                                                      double thStereo) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= d.nact) return;
+    const int e = d.act[k];
+    if (d.bad && d.bad[d.ept[e]]) return;
+    const double thr = d.est[e] ? thStereo : thMono;
+    if (chi2[e] > thr || !depthPos[e]) d.emask[e] = 0;
+    d.robust[e] = 0;
+}
+
 // chi2 / depth of every edge (final check and outlier pass): chi2() uses the stored error
 __global__ __launch_bounds__(256) void k_edge_check(LbaDev d, int ne, double* __restrict__ chi2,
                                                     uint8_t* __restrict__ depthPos) {
@@ -1791,14 +1845,28 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
     int32_t *ept, *eps;
     TRY(dalloc(c, &d.bq, 4 * (size_t)NP)); TRY(dalloc(c, &d.bt, 3 * (size_t)NP)); TRY(dalloc(c, &d.bX, 3 * (size_t)NM));
     TRY(dalloc(c, &d.err, 3 * (size_t)NE));
-    TRY(upload_batch(c, 0, {up(&q, p->pose_q, 4 * (size_t)NP), up(&t, p->pose_t, 3 * (size_t)NP),
-                            up(&X, p->point_xyz, 3 * (size_t)NM), up(&fixed, p->pose_fixed, NP),
-                            up(&ept, p->edge_point, NE), up(&eps, p->edge_pose, NE), up(&est, p->edge_stereo, NE),
-                            up(&obs, p->edge_obs, 3 * (size_t)NE), up(&info, p->edge_info, NE),
-                            up(&cam, p->edge_cam, 5 * (size_t)NE)}));
+    uint8_t* bad = nullptr;
+    {   // one pinned batch (q, t, X first and contiguous: the estimates come back the same way)
+        std::vector<UpItem> items{up(&q, p->pose_q, 4 * (size_t)NP), up(&t, p->pose_t, 3 * (size_t)NP),
+                                  up(&X, p->point_xyz, 3 * (size_t)NM), up(&fixed, p->pose_fixed, NP),
+                                  up(&ept, p->edge_point, NE), up(&eps, p->edge_pose, NE),
+                                  up(&est, p->edge_stereo, NE), up(&obs, p->edge_obs, 3 * (size_t)NE),
+                                  up(&info, p->edge_info, NE), up(&cam, p->edge_cam, 5 * (size_t)NE)};
+        if (p->point_bad && NM > 0) items.push_back(up(&bad, p->point_bad, NM));
+        TRY(upload_batch(c, 0, items));
+    }
     ORB_HIP_TRY(hipMemsetAsync(d.err, 0, 24 * (size_t)NE, s));
+    // push() backups start as the estimates: a fixed pose's backup then always equals its
+    // (never updated) estimate, which the fused linearisation after a pop reads (k_edge_lin)
+    if (NP > 0) {
+        ORB_HIP_TRY(hipMemcpyAsync(d.bq, q, 32 * (size_t)NP, hipMemcpyDeviceToDevice, s));
+        ORB_HIP_TRY(hipMemcpyAsync(d.bt, t, 24 * (size_t)NP, hipMemcpyDeviceToDevice, s));
+    }
     d.q = q; d.t = t; d.X = X; d.fixed = fixed; d.ept = ept; d.eps = eps; d.est = est; d.obs = obs; d.info = info;
     d.cam = cam; d.robust = robust;
+    TRY(dalloc(c, &d.emask, std::max(NE, 1)));   // every edge at level 0 for the first optimize()
+    ORB_HIP_TRY(hipMemsetAsync(d.emask, 1, std::max(NE, 1), s));
+    d.bad = bad;
     d.stopWord = c->d_stop;
     // per-edge / per-vertex scratch sized for the full problem
     TRY(dalloc(c, &d.Hll_e, 6 * (size_t)NE)); TRY(dalloc(c, &d.Hpp_e, 21 * (size_t)NE));
@@ -1867,7 +1935,11 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
     auto grid = [](int n) { return dim3((unsigned)std::max(1, (n + 255) / 256)); };
 
 
+#ifdef ORB_NO_FUSE
+    auto fuse_slots = [&]() { return false; };
+#else
     auto fuse_slots = [&]() { return c->world == 1 && d.nact > 0 && d.M > 0; };
+#endif
     // fused slots: the decision of a group's last trial (k_edge_lin takes the others)
     auto enqueue_close = [&](int iterations) {
         if (!fuse_slots()) return;
@@ -2104,30 +2176,13 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
     const bool bDoMore = !global && !stopAfter1;   // global BA: one optimize(nIterations), R :230-231
     const int own0 = (int)((long long)NM * c->rank / c->world), own1 = (int)((long long)NM * (c->rank + 1) / c->world);
     if (bDoMore) {
-        TRY(ensure_tail(tailRan));
-        for (int e = 0; e < NE; e++) {
-            if (p->point_bad && p->point_bad[p->edge_point[e]]) continue;
-            const double thr = p->edge_stereo[e] ? o->chi2_stereo : o->chi2_mono;
-            if (chi[e] > thr || !dep[e]) level[e] = 1;
-            robustH[e] = 0;
-        }
-        // every rank only knows the errors of its own edges: share the level decisions
-        if (c->world > 1) {
-            std::vector<double> lv(NE);
-            for (int e = 0; e < NE; e++) {
-                const int pt = p->edge_point[e];
-                lv[e] = (pt >= own0 && pt < own1) ? (double)level[e] : 0.0;
-            }
-            if (NE > (int)c->wsDoubles) return ORB_EINVAL;
-            ORB_HIP_TRY(hipMemcpyAsync(c->ws, lv.data(), 8 * (size_t)NE, hipMemcpyHostToDevice, s));
-            TRY(lba_wait(c));
-            if (c->allreduce(c->commUser, 0, NE, 0) != 0) return ORB_EGPU;
-            ORB_HIP_TRY(hipMemcpyAsync(lv.data(), c->ws, 8 * (size_t)NE, hipMemcpyDeviceToHost, s));
-            TRY(lba_wait(c));
-            for (int e = 0; e < NE; e++) level[e] = lv[e] > 0.5 ? 1 : 0;
-        }
+        // the outlier pass on the device (k_outlier_mask), behind the edge check the last group's
+        // tail queued: no host round trip and no second structure build between the rounds
+        if (!tailRan) TRY(tail());
+        if (hs.act.size() > 0)
+            hipLaunchKernelGGL(k_outlier_mask, grid((int)hs.act.size()), dim3(256), 0, s, d, d_chi2, d_depth,
+                               o->chi2_mono, o->chi2_stereo);
         HSTAMP(3);
-        TRY(init_opt(0));
         HSTAMP(4);
         TRY(optimize(o->iters2, r->iterations[1], tail, tailRan));
     }
