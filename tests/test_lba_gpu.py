@@ -194,3 +194,19 @@ def test_local_ba_bitwise_reproducible(amd):
     for r in runs[1:]:
         for k in ("pose_q", "pose_t", "point_xyz", "edge_chi2", "trace", "edge_erase"):
             assert np.array_equal(r[k], runs[0][k]), k
+
+
+def test_repeated_solves_bitwise_identical(amd):
+    """Every reduction of the LM loop has a fixed order, so repeated solves (fresh and reused
+    contexts, cached slot graphs) are bitwise identical — including fixed-iteration solves whose
+    rejected trials end iterations, where a pop and the next linearisation share one launch."""
+    from orb_slam2_amd import optimizer
+    pb = _problem(amd, n_local=12, n_fixed=2, n_points=1200, seed=31, outlier_frac=0.2)
+    opts = optimizer.options(5, 40, fixed_iterations=True)
+    ref = amd.LocalBA().solve(pb, opts)
+    assert (ref["trace"][:, 3] >= 2).any(), "the problem has rejected trials"
+    ctx = amd.LocalBA()
+    for r in [amd.LocalBA().solve(pb, opts)] + [ctx.solve(pb, opts) for _ in range(3)]:
+        assert np.array_equal(r["trace"], ref["trace"])
+        assert np.array_equal(r["pose_q"], ref["pose_q"]) and np.array_equal(r["point_xyz"], ref["point_xyz"])
+        assert np.array_equal(r["edge_erase"], ref["edge_erase"])
