@@ -6,15 +6,16 @@
 //   k_edge_lin        computeActiveErrors + EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ Jacobians
 //                     and Huber-weighted quadratic-form blocks per edge (base_binary_edge.hpp:54-120)
 //   k_vertex_reduce   Hpp, b_p per free pose and Hll, b_l per landmark
-//   k_lm_begin_fused  chi2, lambda init, LM bookkeeping (single workgroup)
+//   (LM iteration start: chi2, lambda init — inside k_point_schur in a single process)
 // Per LM trial (lambda):
-//   k_point_schur     D^-1 = (Hll + lambda I)^-1 per landmark, Hpl D^-1 and Hpl D^-1 b_l per edge
+//   k_point_schur     D^-1 = (Hll + lambda I)^-1 per landmark (and the LM iteration start, fused)
 //   k_schur_pairs     reduced camera matrix S = Hpp + lambda I - sum W D^-1 W^T and b_s, one
 //                     workgroup per 6x6 pose-pair block (G/core/block_solver.hpp:382-440)
 //   k_ldlt_solve      dense LDL^T of S in one workgroup, trailing updates on the f64 MFMA units
 //                     (LinearSolverEigen's SimplicialLDLT role)
 //   k_backsub_update  x_l, push + oplus (SE3Quat::exp * T, X += x_l)
-//   k_edge_errors / k_lm_decide_fused: trial chi2, scale, rho test, lambda, pop on rejection.
+//   k_edge_errors     trial chi2 (the rho test, lambda update and pop on rejection are taken by
+//                     the next slot's k_edge_lin, or by k_lm_decide_fused closing a group of slots)
 // The LM control state lives on the device: a "slot" (linearisation + one trial) is enqueued
 // without host round trips, its kernels run only in their phase, and in a single process the
 // slot is a HIP graph replayed per trial.  Every reduction has a fixed order, so results are
@@ -131,6 +132,39 @@ __device__ __forceinline__ double wave_max_d(double v) {
     return v;
 }
 
+// Lane `lane`'s share of a partial-sum vector, p[lane] + p[lane + 64] + ... in that order (then
+// a wave_sum_d): eight loads in flight per round trip instead of one dependent load per step.
+__device__ __forceinline__ double lane_sum(const double* __restrict__ p, int n, int lane) {
+    double c = 0.0;
+    for (int b = 0; b < n; b += 8 * 64) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int i = b + 64 * u + lane;
+            v[u] = p[i < n ? i : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+            if (b + 64 * u + lane < n) c += v[u];
+    }
+    return c;
+}
+__device__ __forceinline__ double lane_max(const double* __restrict__ p, int n, int lane) {
+    double m = 0.0;
+    for (int b = 0; b < n; b += 8 * 64) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int i = b + 64 * u + lane;
+            v[u] = p[i < n ? i : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+            if (b + 64 * u + lane < n) m = fmax(m, v[u]);
+    }
+    return m;
+}
+
 __device__ __forceinline__ void d_transform(const LbaDev& d, int pose, int pt, double Xc[3]) {
     double r[3];
     d_quat_rot(d.q + 4 * pose, d.X + 3 * pt, r);
@@ -205,9 +239,7 @@ struct LmFuse {
 // caller pays one memory round trip.)
 __device__ __forceinline__ LmState lm_decide_local(const LbaDev& d, const LmFuse& f, int lane, bool writer) {
     LmState ls = *d.lm;
-    double c = 0.0, sc = 0.0;
-    for (int i = lane; i < f.nChi; i += 64) c += d.partChi[i];
-    for (int i = lane; i < f.nScale; i += 64) sc += d.partScale[i];
+    double c = lane_sum(d.partChi, f.nChi, lane), sc = lane_sum(d.partScale, f.nScale, lane);
     const int fail = d.flags[0];
     const double stop = d.red[4];
     c = wave_sum_d(c);
@@ -493,12 +525,19 @@ __global__ __launch_bounds__(64) void k_point_schur(LbaDev d, int fuse, int nChi
     if (fuse) {
         LmState ls = *d.lmMid;
         const int lane = threadIdx.x;
-        double c = 0.0, mx = 0.0;
-        for (int i = lane; i < nChi; i += 64) c += d.partLin[i];
-        for (int i = lane; i < nMax; i += 64) mx = fmax(mx, d.partMax[i]);
-        c = wave_sum_d(c);
-        mx = wave_max_d(mx);
-        if (ls.phase == 0) lm_begin(&ls, c, mx);
+        if (ls.phase == 0) {
+            // lm_begin: only workgroup 0 (which writes the state) needs the chi2 sum; the others
+            // need the maximum diagonal only at iteration 0, where it sets lambda
+            if (blockIdx.x == 0 || ls.it == 0) {
+                double c = blockIdx.x == 0 ? lane_sum(d.partLin, nChi, lane) : 0.0;
+                double mx = ls.it == 0 ? lane_max(d.partMax, nMax, lane) : 0.0;
+                c = wave_sum_d(c);
+                mx = wave_max_d(mx);
+                lm_begin(&ls, c, mx);
+            } else {
+                ls.phase = 1;   // (lm_begin at it > 0 leaves lambda as it is)
+            }
+        }
         if (blockIdx.x == 0 && lane == 0) *d.lm = ls;
         if (ls.phase != 1) return;
         lambda = ls.lambda;
@@ -1335,9 +1374,7 @@ __global__ __launch_bounds__(64) void k_lm_begin_fused(LbaDev d, int nChi, int n
     LmState* st = d.lm;
     if (st->phase != 0) return;
     const int lane = threadIdx.x;
-    double c = 0.0, m = 0.0;
-    for (int i = lane; i < nChi; i += 64) c += d.partChi[i];
-    for (int i = lane; i < nMax; i += 64) m = fmax(m, d.partMax[i]);
+    double c = lane_sum(d.partChi, nChi, lane), m = lane_max(d.partMax, nMax, lane);
     c = wave_sum_d(c);
     m = wave_max_d(m);
     if (lane == 0) lm_begin(st, c, m);
@@ -1376,9 +1413,7 @@ __global__ __launch_bounds__(1024) void k_lm_decide_fused(LbaDev d, const int32_
     __syncthreads();
     if (!go) return;
     if (tid < 64) {
-        double c = 0.0, sc = 0.0;
-        for (int i = tid; i < nChi; i += 64) c += d.partChi[i];
-        for (int i = tid; i < nScale; i += 64) sc += d.partScale[i];
+        double c = lane_sum(d.partChi, nChi, tid), sc = lane_sum(d.partScale, nScale, tid);
         c = wave_sum_d(c);
         sc = wave_sum_d(sc);
         if (tid == 0) {
