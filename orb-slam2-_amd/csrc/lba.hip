@@ -427,61 +427,61 @@ __device__ __forceinline__ void edge_lin_body(const LbaDev& d, double hmono, dou
 // landmarks each, four lanes per landmark (edges in pose-index order, lanes combined by xor).
 // partMax[block] = the block's largest |diagonal| (computeLambdaInit).
 constexpr int kLanesPerPt = 4;
-__global__ __launch_bounds__(256) void k_vertex_reduce(LbaDev d) {
-    if (lm_off(d.lm, 0)) return;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    __shared__ double part[27][257];
-    __shared__ double wmax[4];
-    if ((int)blockIdx.x < d.P) {
-        const int p = blockIdx.x;
-        double acc[27];
+// Pose block p (256 threads): Hpp_p, b_p over its edges; returns the block's max |diagonal|
+// (valid in thread 0).
+__device__ __forceinline__ double pose_block_reduce(const LbaDev& d, int p, double (*part)[257]) {
+    const int tid = threadIdx.x;
+    double acc[27];
 #pragma unroll
-        for (int i = 0; i < 27; i++) acc[i] = 0;
-        for (int a = d.poStart[p] + tid; a < d.poStart[p + 1]; a += 256) {
-            const int k = d.poAct[a];
+    for (int i = 0; i < 27; i++) acc[i] = 0;
+    for (int a = d.poStart[p] + tid; a < d.poStart[p + 1]; a += 256) {
+        const int k = d.poAct[a];
 #pragma unroll
-            for (int i = 0; i < 21; i++) acc[i] += d.Hpp_e[21 * (size_t)k + i];
+        for (int i = 0; i < 21; i++) acc[i] += d.Hpp_e[21 * (size_t)k + i];
 #pragma unroll
-            for (int i = 0; i < 6; i++) acc[21 + i] += d.bp_e[6 * (size_t)k + i];
-        }
-#pragma unroll
-        for (int i = 0; i < 27; i++) part[i][tid] = acc[i];
-        __syncthreads();
-        // value v = t >> 3 (27 values x 8 eighths of 32 partials), eighths meet by xor
-        const int v = tid >> 3, e8 = tid & 7;
-        double sum = 0.0;
-        if (v < 27) {
-#pragma unroll 8
-            for (int i = 0; i < 32; i++) sum += part[v][32 * e8 + i];
-        }
-        sum += __shfl_xor(sum, 1, 64);
-        sum += __shfl_xor(sum, 2, 64);
-        sum += __shfl_xor(sum, 4, 64);
-        __syncthreads();
-        if (v < 27 && e8 == 0) part[v][0] = sum;
-        __syncthreads();
-        if (tid < 27) {
-            const double val = part[tid][0];
-            if (tid < 21) {
-                int i = 0, o = tid;
-                while (o >= 6 - i) { o -= 6 - i; i++; }
-                const int j = i + o;
-                d.Hpp[36 * (size_t)p + i * 6 + j] = val;
-                d.Hpp[36 * (size_t)p + j * 6 + i] = val;
-            } else {
-                d.bp[6 * (size_t)p + tid - 21] = val;
-            }
-        }
-        if (tid == 0) {   // diagonal entries sit at upper-row offsets 0, 6, 11, 15, 18, 20
-            double m = 0;
-            const int dia[6] = {0, 6, 11, 15, 18, 20};
-            for (int i = 0; i < 6; i++) m = fmax(m, fabs(part[dia[i]][0]));
-            d.partMax[blockIdx.x] = m;
-        }
-        return;
+        for (int i = 0; i < 6; i++) acc[21 + i] += d.bp_e[6 * (size_t)k + i];
     }
-    const int l = ((int)blockIdx.x - d.P) * (256 / kLanesPerPt) + (tid / kLanesPerPt), sub = tid % kLanesPerPt;
-    double h[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 27; i++) part[i][tid] = acc[i];
+    __syncthreads();
+    // value v = t >> 3 (27 values x 8 eighths of 32 partials), eighths meet by xor
+    const int v = tid >> 3, e8 = tid & 7;
+    double sum = 0.0;
+    if (v < 27) {
+#pragma unroll 8
+        for (int i = 0; i < 32; i++) sum += part[v][32 * e8 + i];
+    }
+    sum += __shfl_xor(sum, 1, 64);
+    sum += __shfl_xor(sum, 2, 64);
+    sum += __shfl_xor(sum, 4, 64);
+    __syncthreads();
+    if (v < 27 && e8 == 0) part[v][0] = sum;
+    __syncthreads();
+    if (tid < 27) {
+        const double val = part[tid][0];
+        if (tid < 21) {
+            int i = 0, o = tid;
+            while (o >= 6 - i) { o -= 6 - i; i++; }
+            const int j = i + o;
+            d.Hpp[36 * (size_t)p + i * 6 + j] = val;
+            d.Hpp[36 * (size_t)p + j * 6 + i] = val;
+        } else {
+            d.bp[6 * (size_t)p + tid - 21] = val;
+        }
+    }
+    double m = 0;
+    if (tid == 0) {   // diagonal entries sit at upper-row offsets 0, 6, 11, 15, 18, 20
+        const int dia[6] = {0, 6, 11, 15, 18, 20};
+        for (int i = 0; i < 6; i++) m = fmax(m, fabs(part[dia[i]][0]));
+    }
+    return m;
+}
+
+// Landmark l's Hll (6 upper entries) and b_l over its edges, kLanesPerPt lanes per landmark
+// (edges in pose-index order, lanes combined by xor); every lane of the group returns the sums.
+__device__ __forceinline__ void landmark_reduce(const LbaDev& d, int l, int sub, double h[6], double b[3]) {
+    for (int i = 0; i < 6; i++) h[i] = 0.0;
+    for (int i = 0; i < 3; i++) b[i] = 0.0;
     if (l < d.M) {
         for (int a = d.ptStart[l] + sub; a < d.ptStart[l + 1]; a += kLanesPerPt) {
             const int k = d.ptAct[a];
@@ -495,19 +495,55 @@ __global__ __launch_bounds__(256) void k_vertex_reduce(LbaDev d) {
     for (int i = 0; i < 6; i++) { h[i] += __shfl_xor(h[i], 1, 64); h[i] += __shfl_xor(h[i], 2, 64); }
 #pragma unroll
     for (int i = 0; i < 3; i++) { b[i] += __shfl_xor(b[i], 1, 64); b[i] += __shfl_xor(b[i], 2, 64); }
+}
+__device__ __forceinline__ void landmark_store(const LbaDev& d, int l, const double h[6], const double b[3]) {
+    double* H = d.Hll + 9 * (size_t)l;
+    H[0] = h[0]; H[1] = h[1]; H[2] = h[2];
+    H[3] = h[1]; H[4] = h[3]; H[5] = h[4];
+    H[6] = h[2]; H[7] = h[4]; H[8] = h[5];
+    for (int i = 0; i < 3; i++) d.bl[3 * (size_t)l + i] = b[i];
+}
+
+__global__ __launch_bounds__(256) void k_vertex_reduce(LbaDev d) {
+    if (lm_off(d.lm, 0)) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    __shared__ double part[27][257];
+    __shared__ double wmax[4];
+    if ((int)blockIdx.x < d.P) {
+        const double m = pose_block_reduce(d, blockIdx.x, part);
+        if (tid == 0) d.partMax[blockIdx.x] = m;
+        return;
+    }
+    const int l = ((int)blockIdx.x - d.P) * (256 / kLanesPerPt) + (tid / kLanesPerPt), sub = tid % kLanesPerPt;
+    double h[6], b[3];
+    landmark_reduce(d, l, sub, h, b);
     double m = 0.0;
     if (l < d.M && sub == 0) {
-        double* H = d.Hll + 9 * (size_t)l;
-        H[0] = h[0]; H[1] = h[1]; H[2] = h[2];
-        H[3] = h[1]; H[4] = h[3]; H[5] = h[4];
-        H[6] = h[2]; H[7] = h[4]; H[8] = h[5];
-        for (int i = 0; i < 3; i++) d.bl[3 * (size_t)l + i] = b[i];
+        landmark_store(d, l, h, b);
         m = fmax(fabs(h[0]), fmax(fabs(h[3]), fabs(h[5])));
     }
     m = wave_max_d(m);
     if (lane == 0) wmax[wave] = m;
     __syncthreads();
     if (tid == 0) d.partMax[blockIdx.x] = fmax(fmax(wmax[0], wmax[1]), fmax(wmax[2], wmax[3]));
+}
+
+// D^-1 = (Hll + lambda I)^-1 (Eigen's 3x3 cofactor inverse) and D^-1 b_l of landmark l.
+__device__ __forceinline__ void dinv_store(const LbaDev& d, int l, double m[9], const double blv[3], double lambda) {
+    m[0] += lambda; m[4] += lambda; m[8] += lambda;
+    double c[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+            c[i * 3 + j] = m[i1 * 3 + j1] * m[i2 * 3 + j2] - m[i1 * 3 + j2] * m[i2 * 3 + j1];
+        }
+    const double det = c[0] * m[0] + c[3] * m[3] + c[6] * m[6];
+    const double invdet = 1.0 / det;
+    double Di[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) Di[j * 3 + i] = c[i * 3 + j] * invdet;
+    for (int i = 0; i < 9; i++) d.Dinv[9 * (size_t)l + i] = Di[i];
+    for (int i = 0; i < 3; i++) d.db[3 * (size_t)l + i] = Di[i * 3] * blv[0] + Di[i * 3 + 1] * blv[1] + Di[i * 3 + 2] * blv[2];
 }
 
 // Per landmark with lambda (G/core/block_solver.hpp:380-398): D^-1 = (Hll + lambda I)^-1
@@ -546,20 +582,62 @@ __global__ __launch_bounds__(64) void k_point_schur(LbaDev d, int fuse, int nChi
         lambda = d.lm->lambda;
     }
     if (l >= d.M) return;
-    m[0] += lambda; m[4] += lambda; m[8] += lambda;
-    double c[9];
-    for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 3; j++) {
-            const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
-            c[i * 3 + j] = m[i1 * 3 + j1] * m[i2 * 3 + j2] - m[i1 * 3 + j2] * m[i2 * 3 + j1];
+    dinv_store(d, l, m, blv, lambda);
+}
+
+// Landmarks of the fused slots after an optimize()'s first (slots 2.., where the iteration
+// start never initialises lambda): k_vertex_reduce's reduction and k_point_schur's D^-1 in one
+// launch.  Workgroups [0, P) reduce the free poses' Hpp, b_p; the others reduce 64 landmarks'
+// Hll, b_l (phase 0) or read them back (a retrial, phase 1) and form D^-1, D^-1 b_l with the
+// trial's lambda.  Wave 0 of every workgroup reads the state from lmMid: a just-linearised
+// iteration starts here (lm_begin at it > 0 leaves lambda alone, so only workgroup 0, which
+// writes the state to lm, sums k_edge_lin's chi2 partials).
+__global__ __launch_bounds__(256) void k_vertex_schur(LbaDev d, int nChi) {
+    __shared__ double part[27][257];
+    __shared__ double lamS;
+    __shared__ int ph0S, phS;
+    const int tid = threadIdx.x, lane = tid & 63;
+    if (tid < 64) {
+        LmState ls = *d.lmMid;
+        const int ph0 = ls.phase;
+        if (ph0 == 0) {
+            if (blockIdx.x == 0) {
+                double c = lane_sum(d.partLin, nChi, lane);
+                c = wave_sum_d(c);
+                lm_begin(&ls, c, 0.0);   // (it > 0 here: the max diagonal is not used)
+            } else {
+                ls.phase = 1;
+            }
         }
-    const double det = c[0] * m[0] + c[3] * m[3] + c[6] * m[6];
-    const double invdet = 1.0 / det;
-    double Di[9];
-    for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 3; j++) Di[j * 3 + i] = c[i * 3 + j] * invdet;
-    for (int i = 0; i < 9; i++) d.Dinv[9 * (size_t)l + i] = Di[i];
-    for (int i = 0; i < 3; i++) d.db[3 * (size_t)l + i] = Di[i * 3] * blv[0] + Di[i * 3 + 1] * blv[1] + Di[i * 3 + 2] * blv[2];
+        if (blockIdx.x == 0 && lane == 0) *d.lm = ls;
+        if (lane == 0) {
+            lamS = ls.lambda;
+            ph0S = ph0;
+            phS = ls.phase;
+        }
+    }
+    __syncthreads();
+    if (phS != 1) return;
+    const int ph0 = ph0S;
+    const double lambda = lamS;
+    if ((int)blockIdx.x < d.P) {
+        if (ph0 == 0) (void)pose_block_reduce(d, blockIdx.x, part);
+        return;
+    }
+    const int l = ((int)blockIdx.x - d.P) * (256 / kLanesPerPt) + (tid / kLanesPerPt), sub = tid % kLanesPerPt;
+    double h[6], b[3];
+    if (ph0 == 0) landmark_reduce(d, l, sub, h, b);
+    if (l >= d.M || sub != 0) return;
+    double m[9], blv[3];
+    if (ph0 == 0) {
+        landmark_store(d, l, h, b);
+        m[0] = h[0]; m[1] = h[1]; m[2] = h[2]; m[3] = h[1]; m[4] = h[3]; m[5] = h[4]; m[6] = h[2]; m[7] = h[4]; m[8] = h[5];
+        blv[0] = b[0]; blv[1] = b[1]; blv[2] = b[2];
+    } else {
+        for (int i = 0; i < 9; i++) m[i] = d.Hll[9 * (size_t)l + i];
+        for (int i = 0; i < 3; i++) blv[i] = d.bl[3 * (size_t)l + i];
+    }
+    dinv_store(d, l, m, blv, lambda);
 }
 
 // Reduced camera system (G/core/block_solver.hpp:408-440): one workgroup per pose-pair block
@@ -1986,7 +2064,10 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
     // One LM "slot": the linearisation of an iteration (runs only when the device state says a
     // new iteration starts) followed by one trial (runs only while the iteration's trial loop
     // is open) and its decision.  Slots are enqueued back to back without host round trips.
-    auto enqueue_slot = [&](int iterations, hipEvent_t* ev) -> int {
+    // `first`: the first slot of an optimize() call (its iteration start initialises lambda from
+    // the maximum diagonal, so the fused slots keep k_vertex_reduce + k_point_schur there; the
+    // others merge them into k_vertex_schur)
+    auto enqueue_slot = [&](int iterations, hipEvent_t* ev, bool first) -> int {
         const bool prof = ev != nullptr;
         const bool single = c->world == 1;   // no collectives: the LM bookkeeping fuses into single kernels
         if (prof) (void)hipEventRecord(ev[0], s);
@@ -1999,7 +2080,9 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         if (d.nact > 0) hipLaunchKernelGGL(k_edge_lin, dim3(nbE), dim3(64), 0, s, d, hm, hsv, fuse ? 1 : 0, f);
         LbaDev dv = d;
         if (fuse) dv.lm = d.lmMid;
-        if (nbV > 0) hipLaunchKernelGGL(k_vertex_reduce, dim3(nbV), dim3(256), 0, s, dv);
+        const bool merged = fuse && !first && nbV > 0;
+        if (merged) hipLaunchKernelGGL(k_vertex_schur, dim3(nbV), dim3(256), 0, s, d, nbE);
+        else if (nbV > 0) hipLaunchKernelGGL(k_vertex_reduce, dim3(nbV), dim3(256), 0, s, dv);
         if (single) {
             if (!fuse) hipLaunchKernelGGL(k_lm_begin_fused, dim3(1), dim3(64), 0, s, d, nbE, nbV);
         } else {
@@ -2015,7 +2098,8 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         }
         if (prof) (void)hipEventRecord(ev[1], s);
         // ---- trial: Schur complement, reduced solve, back-substitution + update, new chi2
-        if (d.M > 0) hipLaunchKernelGGL(k_point_schur, dim3((d.M + 63) / 64), dim3(64), 0, s, d, fuse ? 1 : 0, nbE, nbV);
+        if (d.M > 0 && !merged)
+            hipLaunchKernelGGL(k_point_schur, dim3((d.M + 63) / 64), dim3(64), 0, s, d, fuse ? 1 : 0, nbE, nbV);
         const int npairs = d.P * (d.P + 1) / 2;
         if (npairs > 0) hipLaunchKernelGGL(k_schur_pairs, dim3(npairs), dim3(kSpT), 0, s, d, root ? 1 : 0);
         if (d.P > 0) TRY(comm_allreduce_g(c, d.S, (size_t)36 * d.P * d.P + 6 * (size_t)d.P, 0, d.lm, 1));
@@ -2077,27 +2161,28 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         // slot is enqueued kernel by kernel.)
         // graphs of `iterations` slots (the first group) and of one slot (the slots after
         // rejected trials), looked up by every captured launch parameter
-        auto slot_graph = [&](int nslots, hipGraphExec_t* out) -> int {
+        auto slot_graph = [&](int nslots, hipGraphExec_t* out, bool firstGroup) -> int {
             *out = nullptr;
             if (c->world != 1 || c->profile || s == nullptr) return ORB_OK;
             struct {
                 LbaDev d;
                 const void* ptrs[4];
                 double h[2];
-                int v[5];
+                int v[6];
             } k;
             std::memset(&k, 0, sizeof(k));
             k.d = d;
             k.ptrs[0] = d_freePoses; k.ptrs[1] = d_trace; k.ptrs[2] = d_ldlw; k.ptrs[3] = s;
             k.h[0] = hm; k.h[1] = hsv;
             k.v[0] = iterations; k.v[1] = maxTrials; k.v[2] = o->fixed_iterations; k.v[3] = root; k.v[4] = nslots;
+            k.v[5] = firstGroup ? 1 : 0;
             std::vector<char> key(reinterpret_cast<const char*>(&k), reinterpret_cast<const char*>(&k) + sizeof(k));
             for (auto& g : c->graphs)
                 if (g.key == key) { *out = g.exec; return ORB_OK; }
             hipGraph_t g = nullptr;
             ORB_HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
             int st = ORB_OK;
-            for (int i = 0; i < nslots && !st; i++) st = enqueue_slot(iterations, nullptr);
+            for (int i = 0; i < nslots && !st; i++) st = enqueue_slot(iterations, nullptr, firstGroup && i == 0);
             if (!st) enqueue_close(iterations);
             const hipError_t ce = hipStreamEndCapture(s, &g);
             if (st) { if (g) (void)hipGraphDestroy(g); return st; }
@@ -2113,7 +2198,7 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
             return ORB_OK;
         };
         hipGraphExec_t gAll = nullptr, gOne = nullptr;
-        TRY(slot_graph(iterations, &gAll));
+        TRY(slot_graph(iterations, &gAll, true));
         int known = 0;
         for (;;) {
             const int G = std::max(1, iterations - known);
@@ -2127,10 +2212,11 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
             if (gAll && G == iterations) {
                 ORB_HIP_TRY(hipGraphLaunch(gAll, s));
             } else {
-                if (gAll && !gOne) TRY(slot_graph(1, &gOne));
+                if (gAll && !gOne) TRY(slot_graph(1, &gOne, false));
                 for (int g = 0; g < G; g++) {
                     if (gOne) ORB_HIP_TRY(hipGraphLaunch(gOne, s));
-                    else TRY(enqueue_slot(iterations, c->profile ? &c->slotEv[5 * (size_t)g] : nullptr));
+                    else TRY(enqueue_slot(iterations, c->profile ? &c->slotEv[5 * (size_t)g] : nullptr,
+                                          known == 0 && g == 0));
                 }
                 if (!gOne) enqueue_close(iterations);
             }
