@@ -31,6 +31,7 @@
 #include <cmath>
 #include <cstring>
 #include <numeric>
+#include <type_traits>
 #include <functional>
 #include <vector>
 
@@ -754,6 +755,14 @@ __device__ __forceinline__ double shfl_d(double v, int src) {
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
+// the same with a wave-uniform lane index held in an SGPR
+__device__ __forceinline__ double shfl_d_dyn(double v, int src) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, src);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), src);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
 // ------------------------------------------------------------------ reduced camera solve
 // Dense LDL^T of S (no pivoting; fails only on a zero or non-finite pivot, like
 // SimplicialLDLT, G/solvers/linear_solver_eigen.h:94-120) + both triangular solves, one
@@ -772,7 +781,7 @@ __device__ __forceinline__ double shfl_d(double v, int src) {
 // two agree to rounding (tests compare the LM traces to 1e-9 relative).
 constexpr int kNB = 16;
 constexpr int kLdlT = 512;
-constexpr int kLdlLdsMaxN = 128;   // padded order held in LDS: (128 * 129 + 3 * 128 + 128) * 8 B = 133 KB
+constexpr int kLdlLdsMaxN = 128;   // padded order held in LDS: (128 * 129 + 3 * 128 + 256 + 16 * 129 + 64) * 8 B = 151 KB
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ double rcp_nr(double d) {
@@ -883,17 +892,31 @@ __device__ __forceinline__ bool ldlt_panel(double* __restrict__ A, int ld, int n
 
 // The LDS-image panel split over waves: group g (wave g) holds the panel's 16 diagonal rows in
 // lanes 0..15 and rows jb + 16 + 48 g + (lane - 16) in lanes 16..63, so every group computes
-// the pivots, 1/d_j and W(jb+k, j) itself (v_readlane within the wave; the W row of the
-// diagonal block through the group's own 16-double LDS scratch) and no wave waits on another
-// inside the column loop.  The diagonal rows are computed identically by every group (same
-// operations in the same order); group 0 alone stores them, d and 1/d.  Groups only write rows
-// they own, after every group has read its inputs (arrival counter `arrive`, group 0 waits
-// for `target`).  Per-column work as ldlt_panel<1>.
-__device__ __forceinline__ bool ldlt_panel_grp(double* __restrict__ A, int ld, int np, int jb, double* __restrict__ dg,
-                                               double* __restrict__ rdg, double* __restrict__ y, double* dummy,
-                                               double* __restrict__ wsc, int lane, int g, int* arrive, int target) {
+// the pivots, 1/d_j and W(jb+k, j) itself and no wave waits on another inside the column loop.
+// The diagonal rows are computed identically by every group (same operations in the same
+// order); group 0 alone stores them and 1/d.  Groups only write rows they own, after every
+// group has read its inputs (arrival counter `arrive`, group 0 waits for `target`).
+// Column j = jb + c: W(r, j) = A(r, j) goes to the upper triangle at (j, r), L(r, j) = W(r, j) / d_j
+// to the lower, and the later columns take A(r, k) = fma(-L(r, j), W(jb+k, j), A(r, k)), k > c,
+// in column order.  W(jb+k, j) reaches the lanes by v_readlane for k = c+1, c+2 (applied at
+// once: the next two pivots depend on them) and through the group's 16-double LDS row `wsc` for
+// k > c+2, read at column c and applied at the start of column c+1, so the LDS round trip
+// overlaps a column of work.  The pivot chain is one multiply-add per column: the next pivot
+//   d_{j+1} = A(j+1, j+1) - W(j+1, j)^2 / d_j = fma(-W(j+1, j)^2, 1/d_j, A(j+1, j+1))
+// takes A(j+1, j+1) and W(j+1, j) by v_readlane (final before column j), then v_rcp_f64 and two
+// Newton steps.  (Lane j+1's own A(j+1, j+1) rounds differently; it is never used: 1/d is the
+// broadcast value.)  Stores are unconditional at loop-invariant bases: the rows below the
+// diagonal block write their W and L in place, the diagonal lanes and rows past np write into
+// the `shadow` sink (kNB * ld + 64 doubles); group 0's diagonal lanes store their L row and 1/d
+// after the loop (the diagonal block's W, its upper triangle, is never read again).  A zero or
+// non-finite pivot only clears the returned flag.
+template <bool kTail>
+__device__ __forceinline__ bool ldlt_panel_grp(double* __restrict__ A, int ld, int np, int nr, int jb,
+                                               double* __restrict__ rdg, double* __restrict__ y,
+                                               double* __restrict__ shadow, double* __restrict__ wsc, int lane,
+                                               int g, int* arrive, int target) {
     const int r = lane < kNB ? jb + lane : jb + kNB + 48 * g + (lane - kNB);
-    const bool live = r < np, own = live && (g == 0 || lane >= kNB);
+    const bool live = r < np, inplace = live && lane >= kNB;
     const int rc = min(r, np - 1);
     double P[kNB];
     double Y = y[rc];
@@ -906,57 +929,67 @@ __device__ __forceinline__ bool ldlt_panel_grp(double* __restrict__ A, int ld, i
     if (g == 0)
         while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) __builtin_amdgcn_s_sleep(1);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    double* const Lrow = own ? A + (size_t)r * ld + jb : dummy + lane;
-    double* const Wcol = own ? A + (size_t)jb * ld + r : dummy + lane;
-    double* const dsink = dummy + lane;
+    double* const Lrow = inplace ? A + (size_t)r * ld + jb : shadow + (size_t)(lane & (kNB - 1)) * ld;
+    double* const Wcol = inplace ? A + (size_t)jb * ld + r : shadow + lane;
+    double* const wst = lane < kNB ? wsc + lane : shadow + lane;
     double dj = shfl_d(P[0], 0);
     bool ok = dj != 0.0 && isfinite(dj);
     double rd = rcp_nr(dj);
+    double myrd = 1.0;             // lane c keeps 1/d_{jb+c} (padding: 1)
+    double Wd[kNB], lprev = 0.0;   // column c-1's deferred W(jb+k, j-1), k > c+1, and L(r, j-1)
 #pragma unroll
     for (int c = 0; c < kNB; c++) {
         const int j = jb + c;
+        // the identity padding's columns (j >= nr, last panel only: kTail) stay as staged: their W
+        // and L entries are zero, 1/d = 1 (set with the staging), so the chain stops at the
+        // order.  (A full panel has no exit: a loop exit is a block boundary where the deferred
+        // LDS reads would be waited for.)
+        if (kTail && j >= nr) break;
+        const double w = P[c];   // final: column c-1 applied its update of column c at once
+        double djn = 1.0, rn = 1.0, w1 = 0.0, w2 = 0.0;
+        if (c + 1 < kNB) {   // the chain: W(j+1, j) and A(j+1, j+1) are final
+            w1 = shfl_d(w, c + 1);
+            const double a1 = shfl_d(P[c + 1], c + 1);
+            djn = __builtin_fma(-(w1 * w1), rd, a1);
+            rn = __builtin_amdgcn_rcp(djn);
+        }
+        if (c + 2 < kNB) w2 = shfl_d(w, c + 2);
         const double yj = shfl_d(Y, c);   // final: every k < j has been applied
-        const double w = P[c];
+        __builtin_amdgcn_sched_barrier(0);
+        // column c-1's deferred updates (its LDS reads were issued a column ago)
+        if (c >= 1) {
+#pragma unroll
+            for (int k = c + 2; k < kNB; k++) P[k] = __builtin_fma(-lprev, Wd[k], P[k]);
+        }
         const double l = w * rd;
         P[c] = l;
-        const bool below = r > j;
-        *(below ? Wcol + (size_t)c * ld : dsink) = w;   // W(r, j)
-        *(below ? Lrow + c : dsink) = l;                // L(r, j)
-        *(g == 0 && lane == 0 ? dg + j : dsink) = dj;
-        *(g == 0 && lane == 0 ? rdg + j : dsink) = rd;
-        *(lane < kNB ? wsc + lane : dsink) = w;         // the diagonal block's W(jb+k, j), this group only
-        double wk[kNB];
+        Wcol[(size_t)c * ld] = w;   // W(r, j)
+        Lrow[c] = l;                // L(r, j)
+        myrd = lane == c ? rd : myrd;
+        *wst = w;                   // the diagonal block's W(jb+k, j)
 #pragma unroll
-        for (int k = c + 2; k < kNB; k++) wk[k] = wsc[k];
-        double djn = 1.0, r0 = 1.0, e0 = 0.0, r1 = 1.0, e1 = 0.0;
+        for (int k = c + 3; k < kNB; k++) Wd[k] = wsc[k];     // consumed at column c+1
+        if (c + 1 < kNB) P[c + 1] = __builtin_fma(-l, w1, P[c + 1]);
+        if (c + 2 < kNB) P[c + 2] = __builtin_fma(-l, w2, P[c + 2]);
+        if (r > j) Y = __builtin_fma(-l, yj, Y);
+        lprev = l;
         if (c + 1 < kNB) {
-            const double w1 = shfl_d(w, c + 1);   // W(j+1, j)
-            P[c + 1] = __builtin_fma(-l, w1, P[c + 1]);
-            djn = shfl_d(P[c + 1], c + 1);
-            r0 = __builtin_amdgcn_rcp(djn);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        const int nk = kNB - 2 - c > 0 ? kNB - 2 - c : 0;
-        const int g1 = c + 2 + (nk + 2) / 3, g2 = c + 2 + 2 * (nk + 2) / 3;
-#pragma unroll
-        for (int k = c + 2; k < kNB && k < g1; k++) P[k] = __builtin_fma(-l, wk[k], P[k]);
-        if (c + 1 < kNB) { e0 = __builtin_fma(-djn, r0, 1.0); r1 = __builtin_fma(r0, e0, r0); }
-        if (below) Y = __builtin_fma(-l, yj, Y);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int k = g1; k < kNB && k < g2; k++) P[k] = __builtin_fma(-l, wk[k], P[k]);
-        if (c + 1 < kNB) { e1 = __builtin_fma(-djn, r1, 1.0); r1 = __builtin_fma(r1, e1, r1); }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int k = g2; k < kNB; k++) P[k] = __builtin_fma(-l, wk[k], P[k]);
-        __builtin_amdgcn_sched_barrier(0);
-        if (c + 1 < kNB) {
+            const double e0 = __builtin_fma(-djn, rn, 1.0);
+            const double r1 = __builtin_fma(rn, e0, rn);
+            const double e1 = __builtin_fma(-djn, r1, 1.0);
             ok = ok && djn != 0.0 && isfinite(djn);
             dj = djn;
-            rd = r1;
+            rd = __builtin_fma(r1, e1, r1);
         }
+        __builtin_amdgcn_sched_barrier(0);
     }
-    if (own) y[r] = Y;
+    if (g == 0 && lane < kNB) {   // the diagonal block's L row (entries past the diagonal: unread)
+        double* const Ld = A + (size_t)r * ld + jb;
+#pragma unroll
+        for (int c = 0; c < kNB; c++) Ld[c] = P[c];
+        rdg[r] = myrd;
+    }
+    if (live && (g == 0 || lane >= kNB)) y[r] = Y;
     return ok;
 }
 // groups for the panel at jb: the 16 diagonal rows plus 48 rows below per group
@@ -985,8 +1018,10 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_solve(const double* __restrict__
     double* dg = sh + (kLds ? (size_t)np * ld : 0);
     double* rdg = dg + np;
     double* y = rdg + np;
-    double* dummy = y + np;   // 64 per-lane sinks for masked-off panel stores
-    double* wsc = dummy + 64; // per-group W-row scratch of the grouped panel (4 x 16)
+    // 64 per-lane sinks for masked-off panel stores; with the LDS image the grouped panels' W-row
+    // scratch follows (16 doubles per group at dummy + 64), then their store sink
+    double* dummy = y + np;
+    double* shadow = dummy + 256;   // LDS image: the grouped panels' store sink (kNB * ld + 64)
     __shared__ int failS, arriveS;
     int arriveTarget = 0;     // the grouped panels' cumulative arrivals (uniform over the workgroup)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1046,6 +1081,7 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_solve(const double* __restrict__
             }
         }
         for (int t = tid; t < np; t += kLdlT) y[t] = t < n ? b[t] : 0.0;
+        for (int t = n + tid; t < np; t += kLdlT) dg[t] = rdg[t] = 1.0;   // padding pivots (not factored)
     }
     TSTAMP(t_sa);
     if (tid == 0) { failS = 0; arriveS = 0; }
@@ -1086,7 +1122,9 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_solve(const double* __restrict__
             const int ng = panel_groups(np, jb);
             arriveTarget += ng;
             if (wave < ng) {
-                const bool okp = ldlt_panel_grp(A, ld, np, jb, dg, rdg, y, dummy, wsc + 16 * wave, lane, wave, &arriveS,
+                const bool okp = jb + kNB > n ? ldlt_panel_grp<true>(A, ld, np, n, jb, rdg, y, shadow, dummy + 64 + 16 * wave, lane, wave, &arriveS,
+                                                arriveTarget)
+                                                 : ldlt_panel_grp<false>(A, ld, np, n, jb, rdg, y, shadow, dummy + 64 + 16 * wave, lane, wave, &arriveS,
                                                 arriveTarget);
                 if (!okp && wave == 0 && lane == 0) failS = 1;
             }
@@ -1147,7 +1185,9 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_solve(const double* __restrict__
             const int jn = jb + kNB, ng = panel_groups(np, jn);
             arriveTarget += ng;
             if (wave < ng) {
-                const bool okp = ldlt_panel_grp(A, ld, np, jn, dg, rdg, y, dummy, wsc + 16 * wave, lane, wave, &arriveS,
+                const bool okp = jn + kNB > n ? ldlt_panel_grp<true>(A, ld, np, n, jn, rdg, y, shadow, dummy + 64 + 16 * wave, lane, wave, &arriveS,
+                                                arriveTarget)
+                                                 : ldlt_panel_grp<false>(A, ld, np, n, jn, rdg, y, shadow, dummy + 64 + 16 * wave, lane, wave, &arriveS,
                                                 arriveTarget);
                 if (!okp && wave == 0 && lane == 0) failS = 1;
             } else {
@@ -1175,6 +1215,69 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_solve(const double* __restrict__
     TSTAMP(t_s0);
     if (failS) {
         if (tid == 0) flags[0] = 1;
+        return;
+    }
+    if (kLds) {
+        // ---- y /= d and the backward substitution with L^T on wave 0 alone, in registers (rows
+        //      lane and 64 + lane, np <= 128): for j descending, x_j is final (v_readlane) and every
+        //      row i < j takes x_i = fma(-L(j, i), x_j, x_i), L(j, i) read along row j of the lower
+        //      triangle (conflict-free, immediate offsets).  Each row subtracts its terms in
+        //      descending j, as the blocked form below does.  The diagonal and upper part of the
+        //      two 64-row diagonal blocks (W, unread after the factorisation) are zeroed first, so
+        //      the loads need no mask (a zero term adds -0 * x_j: x_i is unchanged but for the sign
+        //      of an exact zero).  The identity padding (j >= n) has x_j = 0 and is skipped.
+        {   // four threads per row j < 128: columns j + q, j + q + 4, ... up to the block's end
+            const int j = tid >> 2, q = tid & 3, end = min((j | 63) + 1, np);
+            if (j < np)
+                for (int i = j + q; i < end; i += 4) A[(size_t)j * ld + i] = 0.0;
+        }
+        __syncthreads();
+        if (wave != 0) return;
+        const int i1 = 64 + lane;
+        double X0 = lane < np ? y[lane] * rdg[lane] : 0.0;
+        double X1 = i1 < np ? y[i1] * rdg[i1] : 0.0;
+        TSTAMP(t_b0);
+        const int kTop = (n - 1) & ~(kNB - 1);
+        for (int kb = kTop; kb >= 0; kb -= kNB) {
+            const double* Lk = A + (size_t)kb * ld;
+            double La[kNB], Lb[kNB];
+            if (kb >= 64) {
+#pragma unroll
+                for (int t = 0; t < kNB; t++) { La[t] = Lk[(size_t)t * ld + lane]; Lb[t] = Lk[(size_t)t * ld + i1]; }
+                if (kb + kNB > n) {   // the top block: its padding rows skipped
+                    for (int j = n - 1; j >= kb; j--) {
+                        const double xj = shfl_d_dyn(X1, j - 64);
+                        X0 = __builtin_fma(-A[(size_t)j * ld + lane], xj, X0);
+                        X1 = __builtin_fma(-A[(size_t)j * ld + i1], xj, X1);
+                    }
+                    continue;
+                }
+#pragma unroll
+                for (int t = kNB - 1; t >= 0; t--) {
+                    const double xj = shfl_d_dyn(X1, kb + t - 64);
+                    X0 = __builtin_fma(-La[t], xj, X0);
+                    X1 = __builtin_fma(-Lb[t], xj, X1);
+                }
+            } else {
+#pragma unroll
+                for (int t = 0; t < kNB; t++) La[t] = Lk[(size_t)t * ld + lane];
+                if (kb + kNB > n) {
+                    for (int j = n - 1; j >= kb; j--) X0 = __builtin_fma(-A[(size_t)j * ld + lane], shfl_d_dyn(X0, j), X0);
+                    continue;
+                }
+#pragma unroll
+                for (int t = kNB - 1; t >= 0; t--) X0 = __builtin_fma(-La[t], shfl_d_dyn(X0, kb + t), X0);
+            }
+        }
+#ifdef ORB_TIMING
+        if (lane == 0) printf("ldlt backsolve: zero+init %lld chain %lld\n", t_b0 - t_s0, clock64() - t_b0);
+#endif
+        if (lane < n) x[lane] = X0;
+        if (i1 < n) x[i1] = X1;
+        if (lane == 0) flags[0] = 0;
+#ifdef ORB_TIMING
+        if (lane == 0) printf("ldlt n %d: stage %lld (own %lld) panel %lld rows %lld trailing %lld solve %lld | panels %lld %lld %lld %lld %lld %lld %lld %lld | bar %lld %lld\n", n, t_f0 - t_l0, t_sa - t_l0, tDiag, tRows, tTrail, clock64() - t_s0, tp[0], tp[1], tp[2], tp[3], tp[4], tp[5], tp[6], tp[7], tpb[0], tpb[1]);
+#endif
         return;
     }
     for (int i = tid; i < np; i += kLdlT) y[i] = y[i] * rdg[i];
@@ -1807,7 +1910,7 @@ int lba_dense_solve(lba_context* c, const double* S, const double* b, int n, dou
     ORB_HIP_TRY(hipMemcpyAsync(dS, S, 8 * (size_t)n * n, hipMemcpyHostToDevice, s));
     ORB_HIP_TRY(hipMemcpyAsync(db, b, 8 * (size_t)n, hipMemcpyHostToDevice, s));
     if (np <= kLdlLdsMaxN)
-        hipLaunchKernelGGL(k_ldlt_solve<true>, dim3(1), dim3(kLdlT), ((size_t)np * (np + 1) + 3 * (size_t)np + 128) * 8, s,
+        hipLaunchKernelGGL(k_ldlt_solve<true>, dim3(1), dim3(kLdlT), ((size_t)np * (np + 1) + 3 * (size_t)np + 256 + (size_t)kNB * (np + 1) + 64) * 8, s,
                            dS, db, n, nullptr, dx, df, nullptr);
     else
         hipLaunchKernelGGL(k_ldlt_solve<false>, dim3(1), dim3(kLdlT), (3 * (size_t)np + 64) * 8, s, dS, db, n, dw, dx, df,
@@ -2107,7 +2210,7 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         if (d.P > 0) {
             const int n = 6 * d.P, np = (n + kNB - 1) & ~(kNB - 1);
             if (np <= kLdlLdsMaxN)
-                hipLaunchKernelGGL(k_ldlt_solve<true>, dim3(1), dim3(kLdlT), ((size_t)np * (np + 1) + 3 * (size_t)np + 128) * 8,
+                hipLaunchKernelGGL(k_ldlt_solve<true>, dim3(1), dim3(kLdlT), ((size_t)np * (np + 1) + 3 * (size_t)np + 256 + (size_t)kNB * (np + 1) + 64) * 8,
                                    s, d.S, d.bs, n, nullptr, d.x, d.flags, d.lm);
             else
                 hipLaunchKernelGGL(k_ldlt_solve<false>, dim3(1), dim3(kLdlT), (3 * (size_t)np + 64) * 8, s, d.S, d.bs, n,
