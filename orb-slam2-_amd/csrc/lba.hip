@@ -184,14 +184,21 @@ __device__ __forceinline__ double d_edge_chi2(const LbaDev& d, int e) {
 // An edge the outlier pass moved to level 1 (emask 0) is not active in the second optimize():
 // chi2 0, and its stored error is left as the first round last computed it (g2o's chi2() of a
 // level-1 edge reads that stale error in the final check, R/src/Optimizer.cpp:850-880).
-__device__ __forceinline__ double edge_error(const LbaDev& d, int k, double hmono, double hstereo) {
+// (Xw: the edge's point, read from d.X unless the caller holds it)
+__device__ __forceinline__ double edge_error(const LbaDev& d, int k, double hmono, double hstereo,
+                                             const double* Xw = nullptr) {
     const int e = d.act[k];
     if (!d.emask[e]) {
         d.echi[k] = 0.0;
         return 0.0;
     }
     double Xc[3];
-    d_transform(d, d.eps[e], d.ept[e], Xc);
+    {
+        const int pose = d.eps[e];
+        double r[3];
+        d_quat_rot(d.q + 4 * pose, Xw ? Xw : d.X + 3 * d.ept[e], r);
+        for (int i = 0; i < 3; i++) Xc[i] = r[i] + d.t[3 * pose + i];
+    }
     const double* cam = d.cam + 5 * e;
     const double* obs = d.obs + 3 * e;
     double* er = d.err + 3 * e;
@@ -999,10 +1006,40 @@ __device__ __forceinline__ int panel_groups(int np, int jb) { return max(1, (np 
 // (three per lane of wave 0) with the global image, the rest one per thread (step 1b)
 constexpr int kPanelRowsLds = 128, kPanelRowsGlobal = 192;
 
+// The free poses' update after the reduced solve (the pose block of the back-substitution,
+// G/core/block_solver.hpp:462-484, sparse_optimizer.cpp:422-435): push() of T and
+// T <- exp(x_p) T, and the poses' share of x^T (lambda x + b) into *scaleOut.  Fused slots run it
+// on wave 0 of k_ldlt_solve, so the landmark blocks of k_backsub_errors see the new poses.
+struct PoseTail {
+    double *q, *t, *bq, *bt, *scaleOut;
+    const double* bp;
+    const int32_t *freePoses, *poseIdx;
+    int P;
+};
+__device__ __forceinline__ void pose_tail(const PoseTail& pt, const double* xs, double lambda, int lane) {
+    double sc = 0.0;
+    for (int i = lane; i < pt.P; i += 64) {
+        const int p = pt.freePoses[i];
+        const int k = pt.poseIdx[p];
+        double q[4], t[3], u[6];
+        for (int j = 0; j < 4; j++) { q[j] = pt.q[4 * p + j]; pt.bq[4 * p + j] = q[j]; }
+        for (int j = 0; j < 3; j++) { t[j] = pt.t[3 * p + j]; pt.bt[3 * p + j] = t[j]; }
+        for (int j = 0; j < 6; j++) {
+            u[j] = xs[6 * k + j];
+            sc += u[j] * (lambda * u[j] + pt.bp[6 * k + j]);
+        }
+        d_se3_exp_left(u, q, t);
+        for (int j = 0; j < 4; j++) pt.q[4 * p + j] = q[j];
+        for (int j = 0; j < 3; j++) pt.t[3 * p + j] = t[j];
+    }
+    sc = wave_sum_d(sc);
+    if (lane == 0) *pt.scaleOut = sc;
+}
+
 template <bool kLds>
 __global__ __launch_bounds__(kLdlT) void k_ldlt_solve(const double* __restrict__ Sg, const double* __restrict__ b,
                                                       int n, double* __restrict__ work, double* __restrict__ x,
-                                                      int* __restrict__ flags, const LmState* st) {
+                                                      int* __restrict__ flags, const LmState* st, PoseTail ptail) {
     if (lm_off(st, 1)) return;
     extern __shared__ __attribute__((aligned(16))) double sh[];
     TSTAMP(t_l0);
@@ -1215,6 +1252,9 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_solve(const double* __restrict__
     TSTAMP(t_s0);
     if (failS) {
         if (tid == 0) flags[0] = 1;
+        // the update still runs (with the previous x), as the separate pose block did: the
+        // failed trial is then rejected and popped
+        if (ptail.scaleOut && wave == 0) pose_tail(ptail, x, st->lambda, lane);
         return;
     }
     if (kLds) {
@@ -1275,6 +1315,14 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_solve(const double* __restrict__
         if (lane < n) x[lane] = X0;
         if (i1 < n) x[i1] = X1;
         if (lane == 0) flags[0] = 0;
+        if (ptail.scaleOut) {   // x through LDS to the pose lanes (this wave's LDS operations are in order)
+            y[lane] = X0;
+            if (i1 < np) y[i1] = X1;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            pose_tail(ptail, y, st->lambda, lane);
+        }
 #ifdef ORB_TIMING
         if (lane == 0) printf("ldlt n %d: stage %lld (own %lld) panel %lld rows %lld trailing %lld solve %lld | panels %lld %lld %lld %lld %lld %lld %lld %lld | bar %lld %lld\n", n, t_f0 - t_l0, t_sa - t_l0, tDiag, tRows, tTrail, clock64() - t_s0, tp[0], tp[1], tp[2], tp[3], tp[4], tp[5], tp[6], tp[7], tpb[0], tpb[1]);
 #endif
@@ -1385,6 +1433,72 @@ __global__ __launch_bounds__(256) void k_backsub_update(LbaDev d, const int32_t*
     if (lane == 0) wsum[wave] = sc;
     __syncthreads();
     if (tid == 0) d.partScale[blockIdx.x] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+}
+
+// Fused slots: the landmark blocks of k_backsub_update followed by the trial errors of each
+// landmark's edges (k_edge_errors' work, one launch fewer per slot).  k_ldlt_solve's tail has
+// already pushed and updated the free poses and written their share of the scale; here lane
+// sub of a landmark's four evaluates its edges sub, sub + 4, ... at the new X_l (broadcast from
+// lane 0 of the four), so partChi[block] holds the robust chi2 of the block's 64 landmarks'
+// edges.  Workgroup 0 marks the decision pending and samples terminate() as k_edge_errors did.
+__global__ __launch_bounds__(256) void k_backsub_errors(LbaDev d, double hmono, double hstereo) {
+    if (lm_off(d.lm, 1)) return;
+    const double lambda = d.lm->lambda;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    __shared__ double wsum[4], csum[4];
+    const int l = blockIdx.x * 64 + tid / kLanesPerPt, sub = tid % kLanesPerPt;
+    double cl[3] = {0.0, 0.0, 0.0};
+    if (l < d.M) {
+        for (int a = d.ptStart[l] + sub; a < d.ptStart[l + 1]; a += kLanesPerPt) {
+            const int k = d.ptAct[a];
+            const int pi = d.actPi[k];
+            if (pi < 0) break;   // fixed poses are last
+            const double* Bi = d.Hpl_e + 18 * (size_t)k;
+            const double* xp = d.x + 6 * pi;
+#pragma unroll
+            for (int q = 0; q < 3; q++)
+#pragma unroll
+                for (int r = 0; r < 6; r++) cl[q] += Bi[r * 3 + q] * (-xp[r]);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 3; q++) { cl[q] += __shfl_xor(cl[q], 1, 64); cl[q] += __shfl_xor(cl[q], 2, 64); }
+    double sc = 0.0, Xn[3] = {0.0, 0.0, 0.0};
+    if (l < d.M && sub == 0) {
+        const double* bl = d.bl + 3 * (size_t)l;
+        const double c0 = bl[0] + cl[0], c1 = bl[1] + cl[1], c2 = bl[2] + cl[2];
+        const double* Di = d.Dinv + 9 * (size_t)l;
+        double* xl = d.x + 6 * (size_t)d.P + 3 * (size_t)l;
+        const int g = d.ptGlob[l];
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+            const double v = Di[q * 3] * c0 + Di[q * 3 + 1] * c1 + Di[q * 3 + 2] * c2;
+            xl[q] = v;
+            const double X = d.X[3 * (size_t)g + q];
+            d.bX[3 * (size_t)g + q] = X;
+            Xn[q] = X + v;
+            d.X[3 * (size_t)g + q] = Xn[q];
+            sc += v * (lambda * v + bl[q]);
+        }
+    }
+    // the new X_l from lane 0 of the four (ds_swizzle-free: a 4-lane broadcast by shuffles)
+#pragma unroll
+    for (int q = 0; q < 3; q++) Xn[q] = __shfl(Xn[q], lane & ~(kLanesPerPt - 1), 64);
+    double chi = 0.0;
+    if (l < d.M)
+        for (int a = d.ptStart[l] + sub; a < d.ptStart[l + 1]; a += kLanesPerPt) chi += edge_error(d, d.ptAct[a], hmono, hstereo, Xn);
+    sc = wave_sum_d(sc);
+    chi = wave_sum_d(chi);
+    if (lane == 0) { wsum[wave] = sc; csum[wave] = chi; }
+    __syncthreads();
+    if (tid == 0) {
+        d.partScale[blockIdx.x] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+        d.partChi[blockIdx.x] = (csum[0] + csum[1]) + (csum[2] + csum[3]);
+        if (blockIdx.x == 0) {
+            d.lm->pending = 1;
+            d.red[4] = lm_stop_now(d.lm, d.stopWord, 0.0) ? 1.0 : 0.0;
+        }
+    }
 }
 
 // pop() after a rejected trial (communicator path; k_lm_decide_fused does it in one process)
@@ -1911,10 +2025,10 @@ int lba_dense_solve(lba_context* c, const double* S, const double* b, int n, dou
     ORB_HIP_TRY(hipMemcpyAsync(db, b, 8 * (size_t)n, hipMemcpyHostToDevice, s));
     if (np <= kLdlLdsMaxN)
         hipLaunchKernelGGL(k_ldlt_solve<true>, dim3(1), dim3(kLdlT), ((size_t)np * (np + 1) + 3 * (size_t)np + 256 + (size_t)kNB * (np + 1) + 64) * 8, s,
-                           dS, db, n, nullptr, dx, df, nullptr);
+                           dS, db, n, nullptr, dx, df, nullptr, PoseTail{});
     else
         hipLaunchKernelGGL(k_ldlt_solve<false>, dim3(1), dim3(kLdlT), (3 * (size_t)np + 64) * 8, s, dS, db, n, dw, dx, df,
-                           nullptr);
+                           nullptr, PoseTail{});
     ORB_HIP_TRY(hipGetLastError());
     int fail = 0;
     ORB_HIP_TRY(hipMemcpyAsync(x, dx, 8 * (size_t)n, hipMemcpyDeviceToHost, s));
@@ -2156,12 +2270,18 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
 #else
     auto fuse_slots = [&]() { return c->world == 1 && d.nact > 0 && d.M > 0; };
 #endif
+    // fused slots whose reduced system fits the LDS image: the pose update rides in
+    // k_ldlt_solve's tail and the trial errors in k_backsub_errors (no k_edge_errors launch)
+    auto merge_errors = [&]() {
+        const int np = (6 * d.P + kNB - 1) & ~(kNB - 1);
+        return fuse_slots() && d.P > 0 && np <= kLdlLdsMaxN;
+    };
     // fused slots: the decision of a group's last trial (k_edge_lin takes the others)
     auto enqueue_close = [&](int iterations) {
         if (!fuse_slots()) return;
         const int nbE = (d.nact + 63) / 64, nbB = (d.M + 63) / 64 + 1;
         hipLaunchKernelGGL(k_lm_decide_fused, dim3(1), dim3(1024), 0, s, d, d_freePoses, maxTrials, iterations,
-                           o->fixed_iterations ? 1 : 0, d_trace, nbE, nbB, 1);
+                           o->fixed_iterations ? 1 : 0, d_trace, merge_errors() ? nbB - 1 : nbE, nbB, 1);
     };
 
     // One LM "slot": the linearisation of an iteration (runs only when the device state says a
@@ -2179,7 +2299,9 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         // single process with edges and points: the decision and the iteration start ride in
         // k_edge_lin and k_point_schur (LmFuse), the group of slots ends with one decision kernel
         const bool fuse = fuse_slots();
-        const LmFuse f{nbE, nbB, maxTrials, iterations, o->fixed_iterations ? 1 : 0, d_freePoses, d_trace};
+        const bool merge = merge_errors();
+        const LmFuse f{merge ? nbB - 1 : nbE, nbB, maxTrials, iterations, o->fixed_iterations ? 1 : 0, d_freePoses,
+                       d_trace};
         if (d.nact > 0) hipLaunchKernelGGL(k_edge_lin, dim3(nbE), dim3(64), 0, s, d, hm, hsv, fuse ? 1 : 0, f);
         LbaDev dv = d;
         if (fuse) dv.lm = d.lmMid;
@@ -2209,18 +2331,25 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         if (prof) (void)hipEventRecord(ev[2], s);
         if (d.P > 0) {
             const int n = 6 * d.P, np = (n + kNB - 1) & ~(kNB - 1);
+            PoseTail pt{};
+            if (merge)
+                pt = PoseTail{d.q, d.t, d.bq, d.bt, d.partScale + (nbB - 1), d.bp, d_freePoses, d.poseIdx, d.P};
             if (np <= kLdlLdsMaxN)
                 hipLaunchKernelGGL(k_ldlt_solve<true>, dim3(1), dim3(kLdlT), ((size_t)np * (np + 1) + 3 * (size_t)np + 256 + (size_t)kNB * (np + 1) + 64) * 8,
-                                   s, d.S, d.bs, n, nullptr, d.x, d.flags, d.lm);
+                                   s, d.S, d.bs, n, nullptr, d.x, d.flags, d.lm, pt);
             else
                 hipLaunchKernelGGL(k_ldlt_solve<false>, dim3(1), dim3(kLdlT), (3 * (size_t)np + 64) * 8, s, d.S, d.bs, n,
-                                   d_ldlw, d.x, d.flags, d.lm);
+                                   d_ldlw, d.x, d.flags, d.lm, PoseTail{});
         } else {
             ORB_HIP_TRY(hipMemsetAsync(d.flags, 0, 4, s));
         }
         if (prof) (void)hipEventRecord(ev[3], s);
-        hipLaunchKernelGGL(k_backsub_update, dim3(nbB), dim3(256), 0, s, d, d_freePoses);
-        if (d.nact > 0) hipLaunchKernelGGL(k_edge_errors, dim3(nbE), dim3(64), 0, s, d, hm, hsv, 1, fuse ? 1 : 0);
+        if (merge) {
+            hipLaunchKernelGGL(k_backsub_errors, dim3(nbB - 1), dim3(256), 0, s, d, hm, hsv);
+        } else {
+            hipLaunchKernelGGL(k_backsub_update, dim3(nbB), dim3(256), 0, s, d, d_freePoses);
+            if (d.nact > 0) hipLaunchKernelGGL(k_edge_errors, dim3(nbE), dim3(64), 0, s, d, hm, hsv, 1, fuse ? 1 : 0);
+        }
         if (single) {
             if (!fuse)
                 hipLaunchKernelGGL(k_lm_decide_fused, dim3(1), dim3(1024), 0, s, d, d_freePoses, maxTrials, iterations,
