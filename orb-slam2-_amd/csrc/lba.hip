@@ -29,6 +29,8 @@
 #include <cfloat>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <type_traits>
@@ -1729,6 +1731,137 @@ __global__ __launch_bounds__(1024) void k_lm_decide_fused(LbaDev d, const int32_
     }
 }
 
+constexpr int kStructHistMax = 4096;   // k_struct_count's LDS key histogram (ints)
+
+// ---- The block structure of the first optimize() on the device (single process: every edge
+//      is active at level 0, so act is the identity), the arrays build_csr (lba_host.h) makes on
+//      the host from the vertex maps build_maps made: per edge its local landmark and pose index,
+//      the CSR by landmark (entries ordered by (pose key, edge); key P = fixed pose) and the CSR
+//      by free pose (entries in the landmark-major order of the first CSR).  Counts by atomics
+//      (order-free), exclusive scans on one workgroup, the landmark buckets filled by atomics and
+//      then sorted (a bucket holds one edge per observing keyframe), the pose buckets by one
+//      workgroup per pose ranking its entries along the landmark-major list: the same arrays,
+//      bit for bit, as the host build (checked by ORB_LBA_CHECK_STRUCT, tests/test_lba_gpu.py).
+__global__ __launch_bounds__(256) void k_struct_count(const int32_t* __restrict__ ept, const int32_t* __restrict__ eps,
+                                                      int ne, const int32_t* __restrict__ ptLocal,
+                                                      const int32_t* __restrict__ poseIdx, int P,
+                                                      int32_t* __restrict__ act, int32_t* __restrict__ actPt,
+                                                      int32_t* __restrict__ actPi, int32_t* __restrict__ ptCnt,
+                                                      int32_t* __restrict__ keyCnt, uint8_t* __restrict__ robust,
+                                                      int robustFlag) {
+    extern __shared__ int32_t hist[];   // P + 1 key counts when they fit (else global atomics)
+    const int tid = threadIdx.x, k = blockIdx.x * 256 + tid;
+    const bool lds = P + 1 <= kStructHistMax;
+    if (lds) {
+        for (int i = tid; i <= P; i += 256) hist[i] = 0;
+        __syncthreads();
+    }
+    if (k < ne) {
+        const int pt = ptLocal[ept[k]], pi = poseIdx[eps[k]];
+        act[k] = k;
+        actPt[k] = pt;
+        actPi[k] = pi;
+        robust[k] = (uint8_t)robustFlag;
+        atomicAdd(ptCnt + pt, 1);
+        if (lds) atomicAdd(hist + (pi < 0 ? P : pi), 1);
+        else atomicAdd(keyCnt + (pi < 0 ? P : pi), 1);
+    }
+    if (lds) {
+        __syncthreads();
+        for (int i = tid; i <= P; i += 256)
+            if (hist[i]) atomicAdd(keyCnt + i, hist[i]);
+    }
+}
+
+// exclusive scan of v over a 1024-thread workgroup; *total = the sum (uniform)
+__device__ __forceinline__ int blk_excl_scan(int v, int* wsum, int& total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int incl = wave_incl_scan_i32(v);
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int before = 0, all = 0;
+    for (int w = 0; w < 16; w++) {
+        const int t = wsum[w];
+        before += w < wave ? t : 0;
+        all += t;
+    }
+    __syncthreads();
+    total = all;
+    return before + incl - v;
+}
+
+// ptStart[0..M] and poStart[0..P] (kStart of the host build) by exclusive scans
+__global__ __launch_bounds__(1024) void k_struct_scan(const int32_t* __restrict__ ptCnt, int M,
+                                                      const int32_t* __restrict__ keyCnt, int P,
+                                                      int32_t* __restrict__ ptStart, int32_t* __restrict__ poStart) {
+    __shared__ int wsum[16];
+    const int tid = threadIdx.x;
+    int carry = 0;
+    for (int i0 = 0; i0 <= M; i0 += 1024) {
+        const int i = i0 + tid, v = i < M ? ptCnt[i] : 0;
+        int tot;
+        const int ex = blk_excl_scan(v, wsum, tot);
+        if (i <= M) ptStart[i] = carry + ex;
+        carry += tot;
+    }
+    carry = 0;
+    for (int i0 = 0; i0 <= P; i0 += 1024) {
+        const int i = i0 + tid, v = i < P ? keyCnt[i] : 0;
+        int tot;
+        const int ex = blk_excl_scan(v, wsum, tot);
+        if (i <= P) poStart[i] = carry + ex;
+        carry += tot;
+    }
+}
+
+// the landmark buckets: entries in arrival order, then each bucket sorted by (pose key, edge)
+__global__ __launch_bounds__(256) void k_struct_pt(int ne, const int32_t* __restrict__ actPt,
+                                                   const int32_t* __restrict__ ptStart, int32_t* __restrict__ ptFill,
+                                                   int32_t* __restrict__ ptAct) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= ne) return;
+    const int pt = actPt[k];
+    ptAct[ptStart[pt] + atomicAdd(ptFill + pt, 1)] = k;
+}
+__global__ __launch_bounds__(256) void k_struct_ptsort(int M, int P, const int32_t* __restrict__ ptStart,
+                                                       const int32_t* __restrict__ actPi, int32_t* __restrict__ ptAct) {
+    const int m = blockIdx.x * 256 + threadIdx.x;
+    if (m >= M) return;
+    const int b = ptStart[m], e = ptStart[m + 1];
+    auto key = [&](int k) { const int pi = actPi[k]; return ((long long)(pi < 0 ? P : pi) << 32) | (unsigned)k; };
+    for (int i = b + 1; i < e; i++) {
+        const int k = ptAct[i];
+        const long long kk = key(k);
+        int j = i - 1;
+        while (j >= b && key(ptAct[j]) > kk) {
+            ptAct[j + 1] = ptAct[j];
+            j--;
+        }
+        ptAct[j + 1] = k;
+    }
+}
+// the pose buckets: workgroup i ranks the entries of pose i along the landmark-major list
+__global__ __launch_bounds__(1024) void k_struct_po(int na, const int32_t* __restrict__ ptAct,
+                                                    const int32_t* __restrict__ actPi, const int32_t* __restrict__ actPt,
+                                                    const int32_t* __restrict__ poStart, int32_t* __restrict__ poAct,
+                                                    int32_t* __restrict__ poPt) {
+    __shared__ int wsum[16];
+    const int i = blockIdx.x, tid = threadIdx.x;
+    int at = poStart[i];
+    for (int t0 = 0; t0 < na; t0 += 1024) {
+        const int t = t0 + tid;
+        const int k = t < na ? ptAct[t] : 0;
+        const bool mine = t < na && actPi[k] == i;
+        int tot;
+        const int ex = blk_excl_scan(mine ? 1 : 0, wsum, tot);
+        if (mine) {
+            poAct[at + ex] = k;
+            poPt[at + ex] = actPt[k];
+        }
+        at += tot;
+    }
+}
+
 // The outlier pass between the two optimize() rounds (R/src/Optimizer.cpp:805-836) on the
 // device: every active edge of a good point whose chi2 (k_edge_check) exceeds the threshold or
 // whose depth is not positive leaves the optimisation (level 1 -> emask 0), and every edge of a
@@ -2105,6 +2238,9 @@ void lba_pose_to_Tcw(const double q[4], const double t[3], float Tcw[16]) {
     Tcw[15] = 1.f;
 }
 
+// slots per captured LM graph (see optimize())
+constexpr int kGraphSlots = 5;
+
 static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, const volatile uint8_t* stop,
                    lba_result* r, bool global, bool robustKernels);
 
@@ -2168,6 +2304,13 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         return ORB_OK;
     }
     lba_free_all(c);
+    // single process: the edge-level part of the block structure is built on the device
+    // (k_struct_*); with a communicator (owned landmark ranges) on the host
+    const bool devStruct = c->world == 1 && NE > 0 && !std::getenv("ORB_LBA_HOST_STRUCT");
+    std::vector<uint8_t> level(NE, 0);
+    HostStructure hs;
+    int32_t* d_freePoses = nullptr;
+    int32_t *d_poseIdx0 = nullptr, *d_ptLocal0 = nullptr, *d_ptGlob0 = nullptr;
     LbaDev d;
     std::memset(&d, 0, sizeof(d));
     double *q, *t, *X, *obs, *info, *cam;
@@ -2183,6 +2326,13 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
                                   up(&est, p->edge_stereo, NE), up(&obs, p->edge_obs, 3 * (size_t)NE),
                                   up(&info, p->edge_info, NE), up(&cam, p->edge_cam, 5 * (size_t)NE)};
         if (p->point_bad && NM > 0) items.push_back(up(&bad, p->point_bad, NM));
+        if (devStruct) {   // the vertex maps of the first optimize() (host, O(NE) flags + the id order)
+            build_maps(p, level, 0, 0, 1, hs, false);
+            items.push_back(up(&d_poseIdx0, hs.poseIdx));
+            items.push_back(up(&d_ptLocal0, hs.ptLocal));
+            items.push_back(up(&d_ptGlob0, hs.ptGlob));
+            items.push_back(up(&d_freePoses, hs.freePoses));
+        }
         TRY(upload_batch(c, 0, items));
     }
     ORB_HIP_TRY(hipMemsetAsync(d.err, 0, 24 * (size_t)NE, s));
@@ -2230,7 +2380,7 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
     TRY(dalloc(c, &d_chi2, NE));
     TRY(dalloc(c, &d_depth, NE));
 
-    std::vector<uint8_t> level(NE, 0), robustH(NE, robustKernels ? 1 : 0);
+    std::vector<uint8_t> robustH;
     const double hm = o->huber_mono, hsv = o->huber_stereo;
     const int maxTrials = o->max_trials > 0 ? o->max_trials : 10;
     bool devStopped = false;   // the LM kernels observed terminate()
@@ -2241,14 +2391,62 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         return (double)ms;
     };
 
-    HostStructure hs;
-    int32_t* d_freePoses = nullptr;
     const bool root = c->rank == 0;
 
     // global sum of the owned-point partials (and replicated pose part) of a scalar vector
 
+    auto grid = [](int n) { return dim3((unsigned)std::max(1, (n + 255) / 256)); };
+    auto init_opt_device = [&]() -> int {
+        const int P = hs.P, M = hs.M;
+        int32_t *act, *actPt, *actPi, *ptStart, *ptAct, *poStart, *poAct, *poPt, *cnt;
+        TRY(dalloc(c, &act, NE)); TRY(dalloc(c, &actPt, NE)); TRY(dalloc(c, &actPi, NE));
+        TRY(dalloc(c, &ptStart, (size_t)M + 1)); TRY(dalloc(c, &ptAct, NE));
+        TRY(dalloc(c, &poStart, (size_t)P + 1)); TRY(dalloc(c, &poAct, NE)); TRY(dalloc(c, &poPt, NE));
+        TRY(dalloc(c, &robust, NE));
+        TRY(dalloc(c, &cnt, 2 * (size_t)M + P + 1));   // ptCnt [M], ptFill [M], keyCnt [P + 1]
+        int32_t *ptCnt = cnt, *ptFill = cnt + M, *keyCnt = cnt + 2 * M;
+        ORB_HIP_TRY(hipMemsetAsync(cnt, 0, 4 * (2 * (size_t)M + P + 1), s));
+        const size_t hist = 4 * (size_t)(P + 1 <= kStructHistMax ? P + 1 : 0);
+        hipLaunchKernelGGL(k_struct_count, grid(NE), dim3(256), hist, s, d.ept, d.eps, NE, d_ptLocal0, d_poseIdx0, P,
+                           act, actPt, actPi, ptCnt, keyCnt, robust, robustKernels ? 1 : 0);
+        hipLaunchKernelGGL(k_struct_scan, dim3(1), dim3(1024), 0, s, ptCnt, M, keyCnt, P, ptStart, poStart);
+        hipLaunchKernelGGL(k_struct_pt, grid(NE), dim3(256), 0, s, NE, actPt, ptStart, ptFill, ptAct);
+        hipLaunchKernelGGL(k_struct_ptsort, grid(M), dim3(256), 0, s, M, P, ptStart, actPi, ptAct);
+        if (P > 0)
+            hipLaunchKernelGGL(k_struct_po, dim3(P), dim3(1024), 0, s, NE, ptAct, actPi, actPt, poStart, poAct, poPt);
+        ORB_HIP_TRY(hipGetLastError());
+        d.robust = robust;
+        d.act = act; d.nact = NE; d.poseIdx = d_poseIdx0; d.ptGlob = d_ptGlob0;
+        d.P = P; d.M = M; d.ptStart = ptStart; d.ptAct = ptAct; d.poStart = poStart; d.poAct = poAct; d.poPt = poPt;
+        d.actPt = actPt; d.actPi = actPi;
+        d.bs = d.S + (size_t)36 * d.P * d.P;
+        if (std::getenv("ORB_LBA_CHECK_STRUCT")) {   // test hook: the device arrays against the host build
+            HostStructure h;
+            build_structure(p, level, 0, 0, 1, h);
+            const int nPo = h.poStart.empty() ? 0 : h.poStart.back();
+            const std::pair<const int32_t*, const std::vector<int32_t>*> cmp[] = {
+                {act, &h.act}, {actPt, &h.actPt}, {actPi, &h.actPi}, {ptStart, &h.ptStart}, {ptAct, &h.ptAct},
+                {poStart, &h.poStart}, {poAct, &h.poAct}, {poPt, &h.poPt}};
+            if (h.P != P || h.M != M || (int)h.act.size() != NE || nPo > NE) return ORB_EGPU;
+            std::vector<int32_t> got;
+            for (const auto& pr : cmp) {
+                got.assign(pr.second->size(), 0);
+                if (!got.empty())
+                    ORB_HIP_TRY(hipMemcpyAsync(got.data(), pr.first, 4 * got.size(), hipMemcpyDeviceToHost, s));
+                TRY(lba_wait(c));
+                if (got != *pr.second) {
+                    std::fprintf(stderr, "lba: device structure differs from the host build (array %d)\n",
+                                 (int)(&pr - cmp));
+                    return ORB_EGPU;
+                }
+            }
+        }
+        return ORB_OK;
+    };
     auto init_opt = [&](int lvl) -> int {
+        if (devStruct && lvl == 0) return init_opt_device();
         build_structure(p, level, lvl, c->rank, c->world, hs);
+        robustH.assign(NE, robustKernels ? 1 : 0);
         int32_t *act, *poseIdx, *ptGlob, *actPt, *actPi, *ptStart, *ptAct, *poStart, *poAct, *poPt;
         TRY(upload_batch(c, 1, {up(&act, hs.act), up(&poseIdx, hs.poseIdx), up(&ptGlob, hs.ptGlob), up(&actPt, hs.actPt),
                                 up(&actPi, hs.actPi), up(&ptStart, hs.ptStart), up(&ptAct, hs.ptAct),
@@ -2262,7 +2460,6 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         return ORB_OK;
     };
 
-    auto grid = [](int n) { return dim3((unsigned)std::max(1, (n + 255) / 256)); };
 
 
 #ifdef ORB_NO_FUSE
@@ -2376,7 +2573,7 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
     auto optimize = [&](int iterations, int& itersDone, const std::function<int()>& tail, bool& tailRan) -> int {
         itersDone = 0;
         tailRan = false;
-        if (hs.P + hs.M == 0 && c->world == 1) return ORB_OK;
+        if (d.P + d.M == 0 && c->world == 1) return ORB_OK;
         bool stopNow = false;
         TRY(agreed(stopped(), &stopNow));
         if (iterations <= 0 || stopNow) return ORB_OK;   // sparse_optimizer.cpp:376 before iteration 0
@@ -2393,14 +2590,14 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         // slot is enqueued kernel by kernel.)
         // graphs of `iterations` slots (the first group) and of one slot (the slots after
         // rejected trials), looked up by every captured launch parameter
-        auto slot_graph = [&](int nslots, hipGraphExec_t* out, bool firstGroup) -> int {
+        auto slot_graph = [&](int nslots, hipGraphExec_t* out, bool firstGroup, bool close) -> int {
             *out = nullptr;
             if (c->world != 1 || c->profile || s == nullptr) return ORB_OK;
             struct {
                 LbaDev d;
                 const void* ptrs[4];
                 double h[2];
-                int v[6];
+                int v[7];
             } k;
             std::memset(&k, 0, sizeof(k));
             k.d = d;
@@ -2408,29 +2605,49 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
             k.h[0] = hm; k.h[1] = hsv;
             k.v[0] = iterations; k.v[1] = maxTrials; k.v[2] = o->fixed_iterations; k.v[3] = root; k.v[4] = nslots;
             k.v[5] = firstGroup ? 1 : 0;
+            k.v[6] = close ? 1 : 0;
             std::vector<char> key(reinterpret_cast<const char*>(&k), reinterpret_cast<const char*>(&k) + sizeof(k));
-            for (auto& g : c->graphs)
-                if (g.key == key) { *out = g.exec; return ORB_OK; }
+            for (size_t i = 0; i < c->graphs.size(); i++)
+                if (c->graphs[i].key == key) {   // most recently used last: eviction takes the front
+                    *out = c->graphs[i].exec;
+                    std::rotate(c->graphs.begin() + i, c->graphs.begin() + i + 1, c->graphs.end());
+                    return ORB_OK;
+                }
             hipGraph_t g = nullptr;
             ORB_HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
             int st = ORB_OK;
             for (int i = 0; i < nslots && !st; i++) st = enqueue_slot(iterations, nullptr, firstGroup && i == 0);
-            if (!st) enqueue_close(iterations);
+            if (!st && close) enqueue_close(iterations);
             const hipError_t ce = hipStreamEndCapture(s, &g);
             if (st) { if (g) (void)hipGraphDestroy(g); return st; }
             if (ce != hipSuccess) return ORB_EGPU;
             const hipError_t ie = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
             (void)hipGraphDestroy(g);
             if (ie != hipSuccess) return ORB_EGPU;
-            if (c->graphs.size() >= 8) {
+            if (c->graphs.size() >= 16) {
                 (void)hipGraphExecDestroy(c->graphs.front().exec);
                 c->graphs.erase(c->graphs.begin());
             }
             c->graphs.push_back({std::move(key), *out});
             return ORB_OK;
         };
-        hipGraphExec_t gAll = nullptr, gOne = nullptr;
-        TRY(slot_graph(iterations, &gAll, true));
+        // the first group as graphs of at most kGraphSlots slots each (the decision kernel closes
+        // the last): one long graph leaves the GPU idle for hundreds of microseconds partway
+        // through (rocprof trace of config 4: a 300-390 us hole after the 30th node of a
+        // 10-slot graph)
+        int chunk = kGraphSlots;
+        if (const char* e = std::getenv("ORB_LBA_GRAPH_SLOTS")) chunk = std::max(1, std::atoi(e));
+        chunk = std::max(chunk, (iterations + 7) / 8);   // at most 8 graphs: the cache (16) keeps them all
+        std::vector<hipGraphExec_t> gFirst;
+        for (int i0 = 0; i0 < iterations; i0 += chunk) {
+            hipGraphExec_t ge = nullptr;
+            const int ns = std::min(chunk, iterations - i0);
+            TRY(slot_graph(ns, &ge, i0 == 0, i0 + ns >= iterations));
+            if (!ge) { gFirst.clear(); break; }
+            gFirst.push_back(ge);
+        }
+        hipGraphExec_t gOne = nullptr;
+        const bool gAll = !gFirst.empty();
         int known = 0;
         for (;;) {
             const int G = std::max(1, iterations - known);
@@ -2442,9 +2659,9 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
                 }
             }
             if (gAll && G == iterations) {
-                ORB_HIP_TRY(hipGraphLaunch(gAll, s));
+                for (hipGraphExec_t ge : gFirst) ORB_HIP_TRY(hipGraphLaunch(ge, s));
             } else {
-                if (gAll && !gOne) TRY(slot_graph(1, &gOne, false));
+                if (gAll && !gOne) TRY(slot_graph(1, &gOne, false, true));
                 for (int g = 0; g < G; g++) {
                     if (gOne) ORB_HIP_TRY(hipGraphLaunch(gOne, s));
                     else TRY(enqueue_slot(iterations, c->profile ? &c->slotEv[5 * (size_t)g] : nullptr,
@@ -2532,8 +2749,8 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         // the outlier pass on the device (k_outlier_mask), behind the edge check the last group's
         // tail queued: no host round trip and no second structure build between the rounds
         if (!tailRan) TRY(tail());
-        if (hs.act.size() > 0)
-            hipLaunchKernelGGL(k_outlier_mask, grid((int)hs.act.size()), dim3(256), 0, s, d, d_chi2, d_depth,
+        if (d.nact > 0)
+            hipLaunchKernelGGL(k_outlier_mask, grid(d.nact), dim3(256), 0, s, d, d_chi2, d_depth,
                                o->chi2_mono, o->chi2_stereo);
         HSTAMP(3);
         HSTAMP(4);

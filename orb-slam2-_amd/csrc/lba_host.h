@@ -23,9 +23,12 @@ struct HostStructure {
 };
 
 // initializeOptimization(level) (G/core/sparse_optimizer.cpp:199-267) restricted to the
-// landmarks owned by this rank (contiguous range of point indices).
-inline void build_structure(const lba_problem* p, const std::vector<uint8_t>& level, int lvl, int rank, int world,
-                     HostStructure& s) {
+// landmarks owned by this rank (contiguous range of point indices), first half: the active
+// edges (unless `withAct` is false: the caller knows they are all of them) and the vertex
+// index maps (poseIdx / freePoses, ptLocal / ptGlob).  build_csr makes the rest; the single-
+// process solver builds that part on the device instead (k_struct_*, lba.hip).
+inline void build_maps(const lba_problem* p, const std::vector<uint8_t>& level, int lvl, int rank, int world,
+                       HostStructure& s, bool withAct = true) {
     const int NP = p->n_poses, NM = p->n_points, NE = p->n_edges;
     const int own0 = (int)((long long)NM * rank / world), own1 = (int)((long long)NM * (rank + 1) / world);
     std::vector<uint8_t> poseAct(NP, 0), ptAct(NM, 0);
@@ -36,8 +39,8 @@ inline void build_structure(const lba_problem* p, const std::vector<uint8_t>& le
         ptAct[p->edge_point[e]] = 1;
     }
     s.act.clear();
-    s.act.reserve(NE);
-    for (int e = 0; e < NE; e++) {
+    if (withAct) s.act.reserve(NE);
+    for (int e = 0; withAct && e < NE; e++) {
         if (level[e] != lvl) continue;
         const int pt = p->edge_point[e];
         if (pt < own0 || pt >= own1) continue;
@@ -65,6 +68,11 @@ inline void build_structure(const lba_problem* p, const std::vector<uint8_t>& le
     for (size_t k = 0; k < order.size(); k++) s.ptLocal[order[k]] = (int)k;
     s.ptGlob = order;
     s.M = (int)order.size();
+}
+
+// Second half: per active edge its local landmark and pose index, the CSR by landmark and the
+// CSR by free pose.
+inline void build_csr(const lba_problem* p, HostStructure& s) {
     const int NA = (int)s.act.size();
     s.actPt.resize(NA);
     s.actPi.resize(NA);
@@ -107,6 +115,12 @@ inline void build_structure(const lba_problem* p, const std::vector<uint8_t>& le
             s.poPt[at] = s.actPt[k];
         }
     }
+}
+
+inline void build_structure(const lba_problem* p, const std::vector<uint8_t>& level, int lvl, int rank, int world,
+                            HostStructure& s) {
+    build_maps(p, level, lvl, rank, world, s);
+    build_csr(p, s);
 }
 
 }  // namespace orbamd

@@ -210,3 +210,28 @@ def test_repeated_solves_bitwise_identical(amd):
         assert np.array_equal(r["trace"], ref["trace"])
         assert np.array_equal(r["pose_q"], ref["pose_q"]) and np.array_equal(r["point_xyz"], ref["point_xyz"])
         assert np.array_equal(r["edge_erase"], ref["edge_erase"])
+
+
+@pytest.mark.parametrize("kw,shuffle_ids,global_ba", [
+    (dict(), False, False),                                               # config 4
+    (dict(stereo_frac=0.5, seed=7), True, False),                         # ids out of index order
+    (dict(n_local=30, n_fixed=0, n_points=4000, seed=11), False, False),
+    (dict(n_local=8, n_fixed=2, n_points=500, seed=3), True, True),       # Optimizer::BundleAdjustment
+])
+def test_device_structure_matches_host_build(amd, monkeypatch, kw, shuffle_ids, global_ba):
+    """The single-process solver builds the edge-level block structure on the device
+    (k_struct_*): ORB_LBA_CHECK_STRUCT compares every array with the host build
+    (csrc/lba_host.h) inside the call, and the solve equals the host-built one bitwise."""
+    pb = _problem(amd, **kw)
+    if shuffle_ids:   # g2o orders the Hessian blocks by vertex id, not by index
+        rng = np.random.default_rng(1)
+        pb = dict(pb)
+        pb["pose_id"] = rng.permutation(len(pb["pose_id"])).astype(np.int64) * 3 + 1
+        pb["point_id"] = rng.permutation(len(pb["point_id"])).astype(np.int64) + 1000
+    monkeypatch.setenv("ORB_LBA_CHECK_STRUCT", "1")
+    dev = amd.LocalBA().solve(pb, global_ba=global_ba)
+    monkeypatch.delenv("ORB_LBA_CHECK_STRUCT")
+    monkeypatch.setenv("ORB_LBA_HOST_STRUCT", "1")
+    host = amd.LocalBA().solve(pb, global_ba=global_ba)
+    for k in ("pose_q", "pose_t", "point_xyz", "edge_chi2", "trace", "edge_erase"):
+        assert np.array_equal(dev[k], host[k]), k
