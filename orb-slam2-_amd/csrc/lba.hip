@@ -29,6 +29,7 @@
 #include <cfloat>
 #include <chrono>
 #include <cmath>
+#include <climits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1731,7 +1732,21 @@ __global__ __launch_bounds__(1024) void k_lm_decide_fused(LbaDev d, const int32_
     }
 }
 
+__global__ __launch_bounds__(256) void k_lba_init(double* __restrict__ err, uint8_t* __restrict__ emask, int ne,
+                                                  double* __restrict__ bq, const double* __restrict__ q,
+                                                  double* __restrict__ bt, const double* __restrict__ t, int np,
+                                                  int32_t* __restrict__ cnt, int ncnt) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < 3 * ne) err[i] = 0.0;
+    if (i < ne) emask[i] = 1;
+    if (i < 4 * np) bq[i] = q[i];
+    if (i < 3 * np) bt[i] = t[i];
+    if (i < ncnt) cnt[i] = 0;
+}
+
 constexpr int kStructHistMax = 4096;   // k_struct_count's LDS key histogram (ints)
+constexpr int kSortReg = 16;           // k_struct_ptsort: landmark buckets ranked in registers
+constexpr int kPoRun = 16;             // k_struct_po: consecutive entries per thread
 
 // ---- The block structure of the first optimize() on the device (single process: every edge
 //      is active at level 0, so act is the identity), the arrays build_csr (lba_host.h) makes on
@@ -1823,13 +1838,38 @@ __global__ __launch_bounds__(256) void k_struct_pt(int ne, const int32_t* __rest
     const int pt = actPt[k];
     ptAct[ptStart[pt] + atomicAdd(ptFill + pt, 1)] = k;
 }
+// ... and each landmark-major entry's pose key and landmark (piT, ptT) for k_struct_po
 __global__ __launch_bounds__(256) void k_struct_ptsort(int M, int P, const int32_t* __restrict__ ptStart,
-                                                       const int32_t* __restrict__ actPi, int32_t* __restrict__ ptAct) {
+                                                       const int32_t* __restrict__ actPi, int32_t* __restrict__ ptAct,
+                                                       int32_t* __restrict__ piT, int32_t* __restrict__ ptT) {
     const int m = blockIdx.x * 256 + threadIdx.x;
     if (m >= M) return;
-    const int b = ptStart[m], e = ptStart[m + 1];
+    const int b = ptStart[m], e = ptStart[m + 1], n = e - b;
+    if (n <= 0) return;
     auto key = [&](int k) { const int pi = actPi[k]; return ((long long)(pi < 0 ? P : pi) << 32) | (unsigned)k; };
-    for (int i = b + 1; i < e; i++) {
+    if (n <= kSortReg) {   // ranks in registers: every load in flight at once, keys are distinct
+        int kv[kSortReg];
+        long long kk[kSortReg];
+#pragma unroll
+        for (int i = 0; i < kSortReg; i++) kv[i] = ptAct[b + min(i, n - 1)];
+#pragma unroll
+        for (int i = 0; i < kSortReg; i++) kk[i] = key(kv[i]);   // unconditional (clamped index): no
+#pragma unroll                                                       // exec-masked load chain
+        for (int i = 0; i < kSortReg; i++) kk[i] = i < n ? kk[i] : LLONG_MAX;
+#pragma unroll
+        for (int i = 0; i < kSortReg; i++) {
+            int r = 0;
+#pragma unroll
+            for (int j = 0; j < kSortReg; j++) r += kk[j] < kk[i] ? 1 : 0;
+            if (i < n) {
+                ptAct[b + r] = kv[i];
+                piT[b + r] = (int)(kk[i] >> 32);
+                ptT[b + r] = m;
+            }
+        }
+        return;
+    }
+    for (int i = b + 1; i < e; i++) {   // a landmark seen by more keyframes: insertion sort
         const int k = ptAct[i];
         const long long kk = key(k);
         int j = i - 1;
@@ -1839,31 +1879,53 @@ __global__ __launch_bounds__(256) void k_struct_ptsort(int M, int P, const int32
         }
         ptAct[j + 1] = k;
     }
+    for (int i = b; i < e; i++) {
+        piT[i] = (int)(key(ptAct[i]) >> 32);
+        ptT[i] = m;
+    }
 }
-// the pose buckets: workgroup i ranks the entries of pose i along the landmark-major list
+// the pose buckets: workgroup i ranks the entries of pose i along the landmark-major list, each
+// thread a run of kPoRun consecutive entries (their pose keys and landmarks from
+// k_struct_ptsort: contiguous 16-byte loads, no gathers), one scan per pass
 __global__ __launch_bounds__(1024) void k_struct_po(int na, const int32_t* __restrict__ ptAct,
-                                                    const int32_t* __restrict__ actPi, const int32_t* __restrict__ actPt,
+                                                    const int32_t* __restrict__ piT, const int32_t* __restrict__ ptT,
                                                     const int32_t* __restrict__ poStart, int32_t* __restrict__ poAct,
                                                     int32_t* __restrict__ poPt) {
     __shared__ int wsum[16];
     const int i = blockIdx.x, tid = threadIdx.x;
+    const __amdgpu_buffer_rsrc_t rk = buf_rsrc(ptAct, (uint32_t)na * 4), rp = buf_rsrc(piT, (uint32_t)na * 4),
+                                 rl = buf_rsrc(ptT, (uint32_t)na * 4);
     int at = poStart[i];
-    for (int t0 = 0; t0 < na; t0 += 1024) {
-        const int t = t0 + tid;
-        const int k = t < na ? ptAct[t] : 0;
-        const bool mine = t < na && actPi[k] == i;
-        int tot;
-        const int ex = blk_excl_scan(mine ? 1 : 0, wsum, tot);
-        if (mine) {
-            poAct[at + ex] = k;
-            poPt[at + ex] = actPt[k];
+    for (int t0 = 0; t0 < na; t0 += 1024 * kPoRun) {
+        const int tb = t0 + tid * kPoRun;
+        int kv[kPoRun], pi[kPoRun], pt[kPoRun];
+        typedef int i32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int u = 0; u < kPoRun; u += 4) {   // past the end: the buffer resource reads 0
+            const i32x4 a = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, (tb + u) * 4, 0, 0));
+            const i32x4 b = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rp, (tb + u) * 4, 0, 0));
+            const i32x4 c = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rl, (tb + u) * 4, 0, 0));
+#pragma unroll
+            for (int q = 0; q < 4; q++) { kv[u + q] = a[q]; pi[u + q] = b[q]; pt[u + q] = c[q]; }
         }
+        unsigned mine = 0;
+#pragma unroll
+        for (int u = 0; u < kPoRun; u++) mine |= (tb + u < na && pi[u] == i) ? 1u << u : 0u;
+        int tot;
+        int pos = at + blk_excl_scan(__popc(mine), wsum, tot);
+#pragma unroll
+        for (int u = 0; u < kPoRun; u++)
+            if ((mine >> u) & 1u) {
+                poAct[pos] = kv[u];
+                poPt[pos] = pt[u];
+                pos++;
+            }
         at += tot;
     }
 }
 
 // The outlier pass between the two optimize() rounds (R/src/Optimizer.cpp:805-836) on the
-// device: every active edge of a good point whose chi2 (k_edge_check) exceeds the threshold or
+// device: every active edge of a good point whose chi2 (k_readback) exceeds the threshold or
 // whose depth is not positive leaves the optimisation (level 1 -> emask 0), and every edge of a
 // good point loses its robust kernel.  The block structure is kept: a level-1 edge contributes
 // exact zeros, so a vertex left without active edges keeps a decoupled lambda-only block and
@@ -1881,14 +1943,32 @@ __global__ __launch_bounds__(256) void k_outlier_mask(LbaDev d, const double* __
 }
 
 // chi2 / depth of every edge (final check and outlier pass): chi2() uses the stored error
-__global__ __launch_bounds__(256) void k_edge_check(LbaDev d, int ne, double* __restrict__ chi2,
-                                                    uint8_t* __restrict__ depthPos) {
-    const int e = blockIdx.x * 256 + threadIdx.x;
-    if (e >= ne) return;
-    chi2[e] = d_edge_chi2(d, e);
-    double Xc[3];
-    d_transform(d, d.eps[e], d.ept[e], Xc);
-    depthPos[e] = Xc[2] > 0.0 ? 1 : 0;
+
+// What the host reads after an optimize() (the final check, R/src/Optimizer.cpp:850-880, and the
+// write-back): per edge the chi2 and the depth test (kept on the device too, for
+// k_outlier_mask), the estimates q | t | X and the LM state, stored by the kernel straight into
+// host-coherent pinned memory: no copy commands.  Queued speculatively behind every group of LM
+// slots (the host reads it once the state says the loop is over).
+__global__ __launch_bounds__(256) void k_readback(LbaDev d, int ne, double* __restrict__ chi2,
+                                                  uint8_t* __restrict__ depthPos, char* __restrict__ h, size_t estOff,
+                                                  size_t offT, size_t offX, int np, int nm, size_t lmOff,
+                                                  const double* __restrict__ trace, size_t traceOff) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < 4 * 64) reinterpret_cast<double*>(h + traceOff)[i] = trace[i];
+    if (i < ne) {
+        const double c2 = d_edge_chi2(d, i);
+        double Xc[3];
+        d_transform(d, d.eps[i], d.ept[i], Xc);
+        const uint8_t dp = Xc[2] > 0.0 ? 1 : 0;
+        chi2[i] = c2;
+        depthPos[i] = dp;
+        reinterpret_cast<double*>(h)[i] = c2;
+        reinterpret_cast<uint8_t*>(h + 8 * (size_t)ne)[i] = dp;
+    }
+    if (i < 4 * np) reinterpret_cast<double*>(h + estOff)[i] = d.q[i];
+    if (i < 3 * np) reinterpret_cast<double*>(h + estOff + offT)[i] = d.t[i];
+    if (i < 3 * nm) reinterpret_cast<double*>(h + estOff + offX)[i] = d.X[i];
+    if (i < (int)(sizeof(LmState) / 4)) reinterpret_cast<int*>(h + lmOff)[i] = reinterpret_cast<const int*>(d.lm)[i];
 }
 
 }  // namespace orbamd
@@ -1929,6 +2009,7 @@ struct lba_context {
     std::vector<hipEvent_t> slotEv;                            // per-slot stage timing
     // grow-only pinned staging: [0] problem upload, [1] per-optimize() structure, [2] downloads
     char* stage[3] = {nullptr, nullptr, nullptr};
+    char* stageDev[3] = {nullptr, nullptr, nullptr};   // device address of a mapped (coherent) slot
     size_t stageCap[3] = {0, 0, 0};
     // instantiated LM-slot graphs keyed by every captured launch parameter: a solve of the same
     // shape reuses them (the arena hands out the same addresses in the same order)
@@ -1984,13 +2065,21 @@ static int dalloc(lba_context* c, T** p, size_t n) {
         if (s_) return s_;     \
     } while (0)
 
-static int stage_reserve(lba_context* c, int slot, size_t bytes) {
+// Pinned staging slot; `mapped`: host-coherent memory the kernels store into directly (slot 2,
+// the post-optimize read-back)
+static int stage_reserve(lba_context* c, int slot, size_t bytes, bool mapped = false) {
     if (c->stageCap[slot] >= bytes) return ORB_OK;
     if (c->stage[slot]) (void)hipHostFree(c->stage[slot]);
-    c->stage[slot] = nullptr;
+    c->stage[slot] = c->stageDev[slot] = nullptr;
     c->stageCap[slot] = 0;
     const size_t cap = std::max(bytes + bytes / 2, (size_t)1 << 16);
-    if (hipHostMalloc((void**)&c->stage[slot], cap, hipHostMallocDefault) != hipSuccess) return ORB_ENOMEM;
+    const unsigned flags = mapped ? hipHostMallocMapped | hipHostMallocCoherent : hipHostMallocDefault;
+    if (hipHostMalloc((void**)&c->stage[slot], cap, flags) != hipSuccess) return ORB_ENOMEM;
+    if (mapped && hipHostGetDevicePointer((void**)&c->stageDev[slot], c->stage[slot], 0) != hipSuccess) {
+        (void)hipHostFree(c->stage[slot]);
+        c->stage[slot] = nullptr;
+        return ORB_ENOMEM;
+    }
     c->stageCap[slot] = cap;
     return ORB_OK;
 }
@@ -2016,6 +2105,7 @@ static int upload_batch(lba_context* c, int slot, const std::vector<UpItem>& ite
         *it.dst = dbase + off;
         off += (it.bytes + 255) & ~(size_t)255;
     }
+    // (one copy: sending it in pieces as the staging fills measured no faster, 128-384 KB pieces)
     if (total) ORB_HIP_TRY(hipMemcpyAsync(dbase, c->stage[slot], total, hipMemcpyHostToDevice, c->stream));
     return ORB_OK;
 }
@@ -2239,7 +2329,7 @@ void lba_pose_to_Tcw(const double q[4], const double t[3], float Tcw[16]) {
 }
 
 // slots per captured LM graph (see optimize())
-constexpr int kGraphSlots = 5;
+constexpr int kGraphSlots = 16;
 
 static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, const volatile uint8_t* stop,
                    lba_result* r, bool global, bool robustKernels);
@@ -2335,17 +2425,19 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         }
         TRY(upload_batch(c, 0, items));
     }
-    ORB_HIP_TRY(hipMemsetAsync(d.err, 0, 24 * (size_t)NE, s));
-    // push() backups start as the estimates: a fixed pose's backup then always equals its
-    // (never updated) estimate, which the fused linearisation after a pop reads (k_edge_lin)
-    if (NP > 0) {
-        ORB_HIP_TRY(hipMemcpyAsync(d.bq, q, 32 * (size_t)NP, hipMemcpyDeviceToDevice, s));
-        ORB_HIP_TRY(hipMemcpyAsync(d.bt, t, 24 * (size_t)NP, hipMemcpyDeviceToDevice, s));
-    }
+    // one launch: the errors zeroed, every edge at level 0 for the first optimize(), the push()
+    // backups start as the estimates (a fixed pose's backup then always equals its never updated
+    // estimate, which the fused linearisation after a pop reads, k_edge_lin), and the device
+    // structure build's counters zeroed
+    TRY(dalloc(c, &d.emask, std::max(NE, 1)));
+    int32_t* d_structCnt = nullptr;   // k_struct_*: ptCnt [M], ptFill [M], keyCnt [P + 1]
+    const int nCnt = devStruct ? 2 * hs.M + hs.P + 1 : 0;
+    if (devStruct) TRY(dalloc(c, &d_structCnt, nCnt));
+    hipLaunchKernelGGL(k_lba_init, dim3(std::max(1, (std::max({3 * NE, 4 * NP, nCnt}) + 255) / 256)), dim3(256), 0, s,
+                       d.err, d.emask, NE, d.bq, q, d.bt, t, NP, d_structCnt, nCnt);
+    ORB_HIP_TRY(hipGetLastError());
     d.q = q; d.t = t; d.X = X; d.fixed = fixed; d.ept = ept; d.eps = eps; d.est = est; d.obs = obs; d.info = info;
     d.cam = cam; d.robust = robust;
-    TRY(dalloc(c, &d.emask, std::max(NE, 1)));   // every edge at level 0 for the first optimize()
-    ORB_HIP_TRY(hipMemsetAsync(d.emask, 1, std::max(NE, 1), s));
     d.bad = bad;
     d.stopWord = c->d_stop;
     // per-edge / per-vertex scratch sized for the full problem
@@ -2403,17 +2495,18 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         TRY(dalloc(c, &ptStart, (size_t)M + 1)); TRY(dalloc(c, &ptAct, NE));
         TRY(dalloc(c, &poStart, (size_t)P + 1)); TRY(dalloc(c, &poAct, NE)); TRY(dalloc(c, &poPt, NE));
         TRY(dalloc(c, &robust, NE));
-        TRY(dalloc(c, &cnt, 2 * (size_t)M + P + 1));   // ptCnt [M], ptFill [M], keyCnt [P + 1]
+        int32_t *piT, *ptT;   // per landmark-major entry: pose key, landmark
+        TRY(dalloc(c, &piT, NE)); TRY(dalloc(c, &ptT, NE));
+        cnt = d_structCnt;   // zeroed by k_lba_init
         int32_t *ptCnt = cnt, *ptFill = cnt + M, *keyCnt = cnt + 2 * M;
-        ORB_HIP_TRY(hipMemsetAsync(cnt, 0, 4 * (2 * (size_t)M + P + 1), s));
         const size_t hist = 4 * (size_t)(P + 1 <= kStructHistMax ? P + 1 : 0);
         hipLaunchKernelGGL(k_struct_count, grid(NE), dim3(256), hist, s, d.ept, d.eps, NE, d_ptLocal0, d_poseIdx0, P,
                            act, actPt, actPi, ptCnt, keyCnt, robust, robustKernels ? 1 : 0);
         hipLaunchKernelGGL(k_struct_scan, dim3(1), dim3(1024), 0, s, ptCnt, M, keyCnt, P, ptStart, poStart);
         hipLaunchKernelGGL(k_struct_pt, grid(NE), dim3(256), 0, s, NE, actPt, ptStart, ptFill, ptAct);
-        hipLaunchKernelGGL(k_struct_ptsort, grid(M), dim3(256), 0, s, M, P, ptStart, actPi, ptAct);
+        hipLaunchKernelGGL(k_struct_ptsort, grid(M), dim3(256), 0, s, M, P, ptStart, actPi, ptAct, piT, ptT);
         if (P > 0)
-            hipLaunchKernelGGL(k_struct_po, dim3(P), dim3(1024), 0, s, NE, ptAct, actPi, actPt, poStart, poAct, poPt);
+            hipLaunchKernelGGL(k_struct_po, dim3(P), dim3(1024), 0, s, NE, ptAct, piT, ptT, poStart, poAct, poPt);
         ORB_HIP_TRY(hipGetLastError());
         d.robust = robust;
         d.act = act; d.nact = NE; d.poseIdx = d_poseIdx0; d.ptGlob = d_ptGlob0;
@@ -2567,6 +2660,15 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         return ORB_OK;
     };
 
+    // pinned staging of everything the host reads after an optimize(): chi2 (8 NE), depth flag
+    // (NE), then q, t, X (contiguous in the problem batch); reserved before any copy is queued
+    const size_t estOff = (9 * (size_t)NE + 255) & ~(size_t)255;
+    const size_t bq = ((32 * (size_t)NP + 255) & ~(size_t)255), bt = ((24 * (size_t)NP + 255) & ~(size_t)255);
+    const size_t estBytes = bq + bt + 24 * (size_t)NM;
+    const size_t lmOff = (estOff + estBytes + 255) & ~(size_t)255;   // then the LM state
+    const size_t traceOff = (lmOff + sizeof(LmState) + 255) & ~(size_t)255;   // and the trace rows
+    TRY(stage_reserve(c, 2, traceOff + 32 * 64, true));
+    char* const hStage = c->stage[2];
     // one optimize() call (G/core/sparse_optimizer.cpp:354-419).  The host enqueues as many
     // slots as iterations remain (one trial each), then reads the device state once: more
     // slots only when trials were rejected.  The stop flag is polled between those groups.
@@ -2632,9 +2734,9 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
             return ORB_OK;
         };
         // the first group as graphs of at most kGraphSlots slots each (the decision kernel closes
-        // the last): one long graph leaves the GPU idle for hundreds of microseconds partway
-        // through (rocprof trace of config 4: a 300-390 us hole after the 30th node of a
-        // 10-slot graph)
+        // the last; a graph boundary costs ~8 us).  Under rocprofv3 a 10-slot graph shows a
+        // 300-390 us hole after its 30th node (the profiler slows the dispatch of the nodes);
+        // without it one graph and chunks of 5 time the same (ORB_LBA_GRAPH_SLOTS sweep)
         int chunk = kGraphSlots;
         if (const char* e = std::getenv("ORB_LBA_GRAPH_SLOTS")) chunk = std::max(1, std::atoi(e));
         chunk = std::max(chunk, (iterations + 7) / 8);   // at most 8 graphs: the cache (16) keeps them all
@@ -2674,8 +2776,8 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
             // state says the loop is over
             TRY(tail());
             tailRan = true;
-            ORB_HIP_TRY(hipMemcpyAsync(hst, d.lm, sizeof(LmState), hipMemcpyDeviceToHost, s));
             TRY(lba_wait(c));
+            std::memcpy(hst, c->stage[2] + lmOff, sizeof(LmState));   // stored by k_readback
             if (c->profile) {
                 for (int g = 0; g < G; g++) {
                     hipEvent_t* ev = &c->slotEv[5 * (size_t)g];
@@ -2699,9 +2801,9 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         if (r->trace && r->n_trace < 64) {
             const int rows = std::min(64 - r->n_trace, itersDone);
             if (rows > 0) {
-                ORB_HIP_TRY(hipMemcpyAsync(r->trace + 4 * r->n_trace, d_trace + 4 * r->n_trace, 32 * (size_t)rows,
-                                           hipMemcpyDeviceToHost, s));
-                TRY(lba_wait(c));
+                // the last group's k_readback stored the rows (the loop above waited for it)
+                std::memcpy(r->trace + 4 * r->n_trace,
+                            reinterpret_cast<const double*>(c->stage[2] + traceOff) + 4 * r->n_trace, 32 * (size_t)rows);
                 r->n_trace += rows;
             }
         }
@@ -2711,20 +2813,11 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
 #ifdef ORB_TIMING
     std::chrono::steady_clock::time_point hT[10];
 #endif
-    // pinned staging of everything the host reads after an optimize(): chi2 (8 NE), depth flag
-    // (NE), then q, t, X (contiguous in the problem batch); reserved before any copy is queued
-    const size_t estOff = (9 * (size_t)NE + 255) & ~(size_t)255;
-    const size_t bq = ((32 * (size_t)NP + 255) & ~(size_t)255), bt = ((24 * (size_t)NP + 255) & ~(size_t)255);
-    const size_t estBytes = bq + bt + 24 * (size_t)NM;
-    TRY(stage_reserve(c, 2, estOff + estBytes));
-    char* const hStage = c->stage[2];
     const std::function<int()> tail = [&]() -> int {
-        if (NE > 0) {
-            hipLaunchKernelGGL(k_edge_check, grid(NE), dim3(256), 0, s, d, NE, d_chi2, d_depth);
-            ORB_HIP_TRY(hipMemcpyAsync(hStage, d_chi2, 8 * (size_t)NE, hipMemcpyDeviceToHost, s));
-            ORB_HIP_TRY(hipMemcpyAsync(hStage + 8 * (size_t)NE, d_depth, NE, hipMemcpyDeviceToHost, s));
-        }
-        ORB_HIP_TRY(hipMemcpyAsync(hStage + estOff, q, estBytes, hipMemcpyDeviceToHost, s));
+        const int n = std::max({NE, 4 * NP, 3 * NM, (int)(sizeof(LmState) / 4), 4 * 64});
+        hipLaunchKernelGGL(k_readback, grid(n), dim3(256), 0, s, d, NE, d_chi2, d_depth, c->stageDev[2], estOff, bq,
+                           bq + bt, NP, NM, lmOff, d_trace, traceOff);
+        ORB_HIP_TRY(hipGetLastError());
         return ORB_OK;
     };
     auto ensure_tail = [&](bool ran) -> int {   // an optimize() that ran no group queued no tail
