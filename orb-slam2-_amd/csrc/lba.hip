@@ -440,12 +440,44 @@ __device__ __forceinline__ void edge_lin_body(const LbaDev& d, double hmono, dou
 constexpr int kLanesPerPt = 4;
 // Pose block p (256 threads): Hpp_p, b_p over its edges; returns the block's max |diagonal|
 // (valid in thread 0).
-__device__ __forceinline__ double pose_block_reduce(const LbaDev& d, int p, double (*part)[257]) {
+// The first kPoseBatch edges of each thread (a, a + 256, ...) are fetched with every load in
+// flight at once (clamped indices; the caller may issue them before it knows whether the block
+// runs, k_vertex_schur), so the chain poStart -> poAct -> Hpp_e costs one round trip each
+// instead of one per edge; further edges (poses with more than 256 * kPoseBatch) follow in the
+// same order.  The per-thread summation order is the edge order either way.
+constexpr int kPoseBatch = 4;
+struct PosePrefetch {
+    int a0, a1;
+    double v[kPoseBatch][27];
+};
+__device__ __forceinline__ void pose_prefetch(const LbaDev& d, int p, PosePrefetch& f) {
+    const int tid = threadIdx.x;
+    f.a0 = d.poStart[p];
+    f.a1 = d.poStart[p + 1];
+    int k[kPoseBatch];
+#pragma unroll
+    for (int u = 0; u < kPoseBatch; u++) k[u] = d.poAct[min(f.a0 + tid + 256 * u, max(f.a1 - 1, 0))];
+#pragma unroll
+    for (int u = 0; u < kPoseBatch; u++) {
+#pragma unroll
+        for (int i = 0; i < 21; i++) f.v[u][i] = d.Hpp_e[21 * (size_t)k[u] + i];
+#pragma unroll
+        for (int i = 0; i < 6; i++) f.v[u][21 + i] = d.bp_e[6 * (size_t)k[u] + i];
+    }
+}
+__device__ __forceinline__ double pose_block_reduce(const LbaDev& d, int p, double (*part)[257],
+                                                    const PosePrefetch& f) {
     const int tid = threadIdx.x;
     double acc[27];
 #pragma unroll
     for (int i = 0; i < 27; i++) acc[i] = 0;
-    for (int a = d.poStart[p] + tid; a < d.poStart[p + 1]; a += 256) {
+#pragma unroll
+    for (int u = 0; u < kPoseBatch; u++) {
+        const bool in = f.a0 + tid + 256 * u < f.a1;
+#pragma unroll
+        for (int i = 0; i < 27; i++) acc[i] = in ? acc[i] + f.v[u][i] : acc[i];
+    }
+    for (int a = f.a0 + tid + 256 * kPoseBatch; a < f.a1; a += 256) {
         const int k = d.poAct[a];
 #pragma unroll
         for (int i = 0; i < 21; i++) acc[i] += d.Hpp_e[21 * (size_t)k + i];
@@ -490,11 +522,43 @@ __device__ __forceinline__ double pose_block_reduce(const LbaDev& d, int p, doub
 
 // Landmark l's Hll (6 upper entries) and b_l over its edges, kLanesPerPt lanes per landmark
 // (edges in pose-index order, lanes combined by xor); every lane of the group returns the sums.
-__device__ __forceinline__ void landmark_reduce(const LbaDev& d, int l, int sub, double h[6], double b[3]) {
+// The lane's first kPtBatch edges are fetched with all loads in flight (landmark_prefetch, which
+// k_vertex_schur issues before it reads the LM state); further edges follow in order.
+constexpr int kPtBatch = 2;
+struct PtPrefetch {
+    int a0, a1;
+    double v[kPtBatch][9];
+};
+__device__ __forceinline__ void landmark_prefetch(const LbaDev& d, int l, int sub, PtPrefetch& f) {
+    const int lc = min(l, d.M - 1);
+    f.a0 = d.ptStart[lc] + sub;
+    f.a1 = l < d.M ? d.ptStart[lc + 1] : f.a0;
+    const int last = max(d.ptStart[lc + 1] - 1, 0);
+    int k[kPtBatch];
+#pragma unroll
+    for (int u = 0; u < kPtBatch; u++) k[u] = d.ptAct[min(f.a0 + kLanesPerPt * u, last)];
+#pragma unroll
+    for (int u = 0; u < kPtBatch; u++) {
+#pragma unroll
+        for (int i = 0; i < 6; i++) f.v[u][i] = d.Hll_e[6 * (size_t)k[u] + i];
+#pragma unroll
+        for (int i = 0; i < 3; i++) f.v[u][6 + i] = d.bl_e[3 * (size_t)k[u] + i];
+    }
+}
+__device__ __forceinline__ void landmark_reduce(const LbaDev& d, int l, int sub, double h[6], double b[3],
+                                                const PtPrefetch& f) {
     for (int i = 0; i < 6; i++) h[i] = 0.0;
     for (int i = 0; i < 3; i++) b[i] = 0.0;
     if (l < d.M) {
-        for (int a = d.ptStart[l] + sub; a < d.ptStart[l + 1]; a += kLanesPerPt) {
+#pragma unroll
+        for (int u = 0; u < kPtBatch; u++) {
+            const bool in = f.a0 + kLanesPerPt * u < f.a1;
+#pragma unroll
+            for (int i = 0; i < 6; i++) h[i] = in ? h[i] + f.v[u][i] : h[i];
+#pragma unroll
+            for (int i = 0; i < 3; i++) b[i] = in ? b[i] + f.v[u][6 + i] : b[i];
+        }
+        for (int a = f.a0 + kLanesPerPt * kPtBatch; a < f.a1; a += kLanesPerPt) {
             const int k = d.ptAct[a];
 #pragma unroll
             for (int i = 0; i < 6; i++) h[i] += d.Hll_e[6 * (size_t)k + i];
@@ -521,13 +585,17 @@ __global__ __launch_bounds__(256) void k_vertex_reduce(LbaDev d) {
     __shared__ double part[27][257];
     __shared__ double wmax[4];
     if ((int)blockIdx.x < d.P) {
-        const double m = pose_block_reduce(d, blockIdx.x, part);
+        PosePrefetch pf;
+        pose_prefetch(d, blockIdx.x, pf);
+        const double m = pose_block_reduce(d, blockIdx.x, part, pf);
         if (tid == 0) d.partMax[blockIdx.x] = m;
         return;
     }
     const int l = ((int)blockIdx.x - d.P) * (256 / kLanesPerPt) + (tid / kLanesPerPt), sub = tid % kLanesPerPt;
     double h[6], b[3];
-    landmark_reduce(d, l, sub, h, b);
+    PtPrefetch pf;
+    landmark_prefetch(d, l, sub, pf);
+    landmark_reduce(d, l, sub, h, b, pf);
     double m = 0.0;
     if (l < d.M && sub == 0) {
         landmark_store(d, l, h, b);
@@ -608,6 +676,13 @@ __global__ __launch_bounds__(256) void k_vertex_schur(LbaDev d, int nChi) {
     __shared__ double lamS;
     __shared__ int ph0S, phS;
     const int tid = threadIdx.x, lane = tid & 63;
+    // a pose block's edge data is fetched before the state is known (wasted on a retrial, where
+    // the reduction is not redone): the two load chains overlap
+    PosePrefetch pf;
+    PtPrefetch lf;
+    const int l = ((int)blockIdx.x - d.P) * (256 / kLanesPerPt) + (tid / kLanesPerPt), sub = tid % kLanesPerPt;
+    if ((int)blockIdx.x < d.P) pose_prefetch(d, blockIdx.x, pf);
+    else landmark_prefetch(d, l, sub, lf);
     if (tid < 64) {
         LmState ls = *d.lmMid;
         const int ph0 = ls.phase;
@@ -632,12 +707,11 @@ __global__ __launch_bounds__(256) void k_vertex_schur(LbaDev d, int nChi) {
     const int ph0 = ph0S;
     const double lambda = lamS;
     if ((int)blockIdx.x < d.P) {
-        if (ph0 == 0) (void)pose_block_reduce(d, blockIdx.x, part);
+        if (ph0 == 0) (void)pose_block_reduce(d, blockIdx.x, part, pf);
         return;
     }
-    const int l = ((int)blockIdx.x - d.P) * (256 / kLanesPerPt) + (tid / kLanesPerPt), sub = tid % kLanesPerPt;
     double h[6], b[3];
-    if (ph0 == 0) landmark_reduce(d, l, sub, h, b);
+    if (ph0 == 0) landmark_reduce(d, l, sub, h, b, lf);
     if (l >= d.M || sub != 0) return;
     double m[9], blv[3];
     if (ph0 == 0) {
