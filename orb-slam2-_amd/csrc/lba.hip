@@ -1519,43 +1519,82 @@ __global__ __launch_bounds__(256) void k_backsub_update(LbaDev d, const int32_t*
 // lane 0 of the four), so partChi[block] holds the robust chi2 of the block's 64 landmarks'
 // edges.  Workgroup 0 marks the decision pending and samples terminate() as k_edge_errors did.
 __global__ __launch_bounds__(256) void k_backsub_errors(LbaDev d, double hmono, double hstereo) {
-    if (lm_off(d.lm, 1)) return;
-    const double lambda = d.lm->lambda;
+    // Every load that does not depend on another is issued before the phase guard and the
+    // first use (clamped indices, unconditional): the state, the landmark's CSR range, its
+    // first kPtBatch edges (act position, pose index, Hpl block, the pose's x) and its bl,
+    // D^-1, X, so the chain is ptStart -> ptAct -> (actPi, Hpl) -> x instead of one round
+    // trip per dependent load per edge.  The summation order is the original's.
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     __shared__ double wsum[4], csum[4];
     const int l = blockIdx.x * 64 + tid / kLanesPerPt, sub = tid % kLanesPerPt;
+    const int lc = min(l, d.M - 1);
+    const int phase = d.lm->phase;
+    const double lambda = d.lm->lambda;
+    const int a0 = d.ptStart[lc] + sub, a1 = l < d.M ? d.ptStart[lc + 1] : a0;
+    const int g = d.ptGlob[lc];
+    double blv[3], Di[9], Xo[3];
+#pragma unroll
+    for (int q = 0; q < 3; q++) blv[q] = d.bl[3 * (size_t)lc + q];
+#pragma unroll
+    for (int q = 0; q < 9; q++) Di[q] = d.Dinv[9 * (size_t)lc + q];
+#pragma unroll
+    for (int q = 0; q < 3; q++) Xo[q] = d.X[3 * (size_t)g + q];
+    const int last = max(d.ptStart[lc + 1] - 1, 0);
+    int kk[kPtBatch], pi[kPtBatch];
+    double B[kPtBatch][18], xp[kPtBatch][6];
+#pragma unroll
+    for (int u = 0; u < kPtBatch; u++) kk[u] = d.ptAct[min(a0 + kLanesPerPt * u, last)];
+#pragma unroll
+    for (int u = 0; u < kPtBatch; u++) {
+        pi[u] = d.actPi[kk[u]];
+#pragma unroll
+        for (int i = 0; i < 18; i++) B[u][i] = d.Hpl_e[18 * (size_t)kk[u] + i];
+    }
+#pragma unroll
+    for (int u = 0; u < kPtBatch; u++)
+#pragma unroll
+        for (int r = 0; r < 6; r++) xp[u][r] = d.x[6 * max(pi[u], 0) + r];
+    if (phase != 1) return;   // lm_off(d.lm, 1)
     double cl[3] = {0.0, 0.0, 0.0};
-    if (l < d.M) {
-        for (int a = d.ptStart[l] + sub; a < d.ptStart[l + 1]; a += kLanesPerPt) {
-            const int k = d.ptAct[a];
-            const int pi = d.actPi[k];
-            if (pi < 0) break;   // fixed poses are last
-            const double* Bi = d.Hpl_e + 18 * (size_t)k;
-            const double* xp = d.x + 6 * pi;
+    bool open = true;   // fixed poses are last: the first one ends the landmark's sum
+#pragma unroll
+    for (int u = 0; u < kPtBatch; u++) {
+        open = open && a0 + kLanesPerPt * u < a1 && pi[u] >= 0;
+        if (open) {
 #pragma unroll
             for (int q = 0; q < 3; q++)
 #pragma unroll
-                for (int r = 0; r < 6; r++) cl[q] += Bi[r * 3 + q] * (-xp[r]);
+                for (int r = 0; r < 6; r++) cl[q] += B[u][r * 3 + q] * (-xp[u][r]);
+        }
+    }
+    if (open) {
+        for (int a = a0 + kLanesPerPt * kPtBatch; a < a1; a += kLanesPerPt) {
+            const int k = d.ptAct[a];
+            const int pik = d.actPi[k];
+            if (pik < 0) break;
+            const double* Bi = d.Hpl_e + 18 * (size_t)k;
+            const double* xq = d.x + 6 * pik;
+#pragma unroll
+            for (int q = 0; q < 3; q++)
+#pragma unroll
+                for (int r = 0; r < 6; r++) cl[q] += Bi[r * 3 + q] * (-xq[r]);
         }
     }
 #pragma unroll
     for (int q = 0; q < 3; q++) { cl[q] += __shfl_xor(cl[q], 1, 64); cl[q] += __shfl_xor(cl[q], 2, 64); }
     double sc = 0.0, Xn[3] = {0.0, 0.0, 0.0};
     if (l < d.M && sub == 0) {
-        const double* bl = d.bl + 3 * (size_t)l;
-        const double c0 = bl[0] + cl[0], c1 = bl[1] + cl[1], c2 = bl[2] + cl[2];
-        const double* Di = d.Dinv + 9 * (size_t)l;
+        const double c0 = blv[0] + cl[0], c1 = blv[1] + cl[1], c2 = blv[2] + cl[2];
         double* xl = d.x + 6 * (size_t)d.P + 3 * (size_t)l;
-        const int g = d.ptGlob[l];
 #pragma unroll
         for (int q = 0; q < 3; q++) {
             const double v = Di[q * 3] * c0 + Di[q * 3 + 1] * c1 + Di[q * 3 + 2] * c2;
             xl[q] = v;
-            const double X = d.X[3 * (size_t)g + q];
+            const double X = Xo[q];
             d.bX[3 * (size_t)g + q] = X;
             Xn[q] = X + v;
             d.X[3 * (size_t)g + q] = Xn[q];
-            sc += v * (lambda * v + bl[q]);
+            sc += v * (lambda * v + blv[q]);
         }
     }
     // the new X_l from lane 0 of the four (ds_swizzle-free: a 4-lane broadcast by shuffles)
