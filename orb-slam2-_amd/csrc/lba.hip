@@ -293,28 +293,88 @@ __global__ __launch_bounds__(64) void k_edge_errors(LbaDev d, double hmono, doub
     }
 }
 
-// Jacobians + Huber-weighted quadratic-form blocks per active edge.
-// Hll_e: 3x3 upper (00 01 02 11 12 22); Hpp_e: 6x6 upper row-major (21); Hpl_e: 6x3; bl_e: 3; bp_e: 6
-__device__ __forceinline__ void edge_linearize(const LbaDev& d, int k, double hmono, double hstereo) {
+// The read-only inputs of active edge k (k_edge_lin loads them before it reads the LM state,
+// so the two load chains overlap).
+struct EdgeStatic {
+    int e, pose, pt;
+    bool on, st, rob;
+    double info, obs[3], cam[5];
+};
+__device__ __forceinline__ EdgeStatic edge_static(const LbaDev& d, int k) {
+    EdgeStatic s;
     const int e = d.act[k];
-    if (!d.emask[e]) {   // level-1 edge: its quadratic-form blocks are exact zeros
+    s.e = e;
+    s.on = d.emask[e] != 0;
+    s.pose = d.eps[e];
+    s.pt = d.ept[e];
+    s.st = d.est[e] != 0;
+    s.rob = d.robust[e] != 0;
+    s.info = d.info[e];
+#pragma unroll
+    for (int i = 0; i < 3; i++) s.obs[i] = d.obs[3 * (size_t)e + i];
+#pragma unroll
+    for (int i = 0; i < 5; i++) s.cam[i] = d.cam[5 * (size_t)e + i];
+    return s;
+}
+
+// computeError (edge_error's arithmetic) then the Jacobians and Huber-weighted quadratic-form
+// blocks of active edge k from the error just computed (no reload).  Returns the robust chi2.
+// Hll_e: 3x3 upper (00 01 02 11 12 22); Hpp_e: 6x6 upper row-major (21); Hpl_e: 6x3; bl_e: 3; bp_e: 6
+__device__ __forceinline__ double edge_error_lin(const LbaDev& d, int k, const EdgeStatic& s, double hmono,
+                                                 double hstereo) {
+    const int e = s.e, pose = s.pose;
+    const bool freePose = d.poseIdx[pose] >= 0;
+    if (!s.on) {   // level-1 edge: chi2 0, its stored error stays, its blocks are exact zeros
+        d.echi[k] = 0.0;
         for (int i = 0; i < 6; i++) d.Hll_e[6 * (size_t)k + i] = 0.0;
         for (int i = 0; i < 3; i++) d.bl_e[3 * (size_t)k + i] = 0.0;
-        if (d.poseIdx[d.eps[e]] >= 0) {
+        if (freePose) {
             for (int i = 0; i < 21; i++) d.Hpp_e[21 * (size_t)k + i] = 0.0;
             for (int i = 0; i < 6; i++) d.bp_e[6 * (size_t)k + i] = 0.0;
             for (int i = 0; i < 18; i++) d.Hpl_e[18 * (size_t)k + i] = 0.0;
         }
-        return;
+        return 0.0;
     }
-    const int pose = d.eps[e];
-    double R[9], Xc[3];
+    double Xc[3];
+    {
+        double r[3];
+        d_quat_rot(d.q + 4 * pose, d.X + 3 * s.pt, r);
+        for (int i = 0; i < 3; i++) Xc[i] = r[i] + d.t[3 * pose + i];
+    }
+    const double* cam = s.cam;
+    const double* obs = s.obs;
+    double er[3];
+    if (!s.st) {
+        const double u = Xc[0] / Xc[2], v = Xc[1] / Xc[2];
+        er[0] = obs[0] - (u * cam[0] + cam[2]);
+        er[1] = obs[1] - (v * cam[1] + cam[3]);
+        er[2] = 0;
+    } else {
+        const float invz = (float)(1.0f / Xc[2]);
+        const double r0 = Xc[0] * invz * cam[0] + cam[2];
+        const double r1 = Xc[1] * invz * cam[1] + cam[3];
+        const float bff = (float)cam[4];
+        const double r2 = r0 - (double)(bff * invz);
+        er[0] = obs[0] - r0;
+        er[1] = obs[1] - r1;
+        er[2] = obs[2] - r2;
+    }
+    for (int i = 0; i < 3; i++) d.err[3 * (size_t)e + i] = er[i];
+    const double w = s.info;
+    double chi2 = er[0] * (w * er[0]) + er[1] * (w * er[1]);   // d_edge_chi2
+    if (s.st) chi2 += er[2] * (w * er[2]);
+    double chi = chi2;
+    if (s.rob) {
+        const double delta = s.st ? hstereo : hmono, dsqr = delta * delta;
+        if (chi > dsqr) chi = 2 * sqrt(chi) * delta - dsqr;
+    }
+    d.echi[k] = chi;
+    // linearizeOplus + constructQuadraticForm at the same estimate (Xc as d_transform gives it)
+    double R[9];
     d_quat_to_R(d.q + 4 * pose, R);
-    d_transform(d, pose, d.ept[e], Xc);
     const double x = Xc[0], y = Xc[1], z = Xc[2], z_2 = z * z;
-    const double* cam = d.cam + 5 * e;
     const double fx = cam[0], fy = cam[1], bf = cam[4];
-    const bool st = d.est[e] != 0;
+    const bool st = s.st;
     const int D = st ? 3 : 2;
     double A[9], B[18];
     if (!st) {
@@ -340,13 +400,10 @@ __device__ __forceinline__ void edge_linearize(const LbaDev& d, int k, double hm
     } else {
         for (int i = 12; i < 18; i++) B[i] = 0;
     }
-    const double w = d.info[e];
-    const double* er = d.err + 3 * e;
     double rho1 = 1.0;
-    if (d.robust[e]) {
-        const double chi = d_edge_chi2(d, e);
+    if (s.rob) {
         const double delta = st ? hstereo : hmono;
-        if (chi > delta * delta) rho1 = delta / sqrt(chi);
+        if (chi2 > delta * delta) rho1 = delta / sqrt(chi2);
     }
     const double W = rho1 * w;
     double om[3];
@@ -358,9 +415,9 @@ __device__ __forceinline__ void edge_linearize(const LbaDev& d, int k, double hm
     {
         int o = 0;
         for (int i = 0; i < 3; i++) {
-            double s = 0;
-            for (int r = 0; r < 3; r++) s += A[r * 3 + i] * om[r];
-            bl[i] = s;
+            double sm = 0;
+            for (int r = 0; r < 3; r++) sm += A[r * 3 + i] * om[r];
+            bl[i] = sm;
             for (int j = i; j < 3; j++) {
                 double h = 0;
                 for (int r = 0; r < 3; r++) h += A[r * 3 + i] * W * A[r * 3 + j];
@@ -368,15 +425,15 @@ __device__ __forceinline__ void edge_linearize(const LbaDev& d, int k, double hm
             }
         }
     }
-    if (d.poseIdx[pose] >= 0) {
+    if (freePose) {
         double* hp = d.Hpp_e + 21 * (size_t)k;
         double* bp = d.bp_e + 6 * (size_t)k;
         double* hpl = d.Hpl_e + 18 * (size_t)k;
         int o = 0;
         for (int i = 0; i < 6; i++) {
-            double s = 0;
-            for (int r = 0; r < 3; r++) s += B[r * 6 + i] * om[r];
-            bp[i] = s;
+            double sm = 0;
+            for (int r = 0; r < 3; r++) sm += B[r * 6 + i] * om[r];
+            bp[i] = sm;
             for (int j = i; j < 6; j++) {
                 double h = 0;
                 for (int r = 0; r < 3; r++) h += B[r * 6 + i] * W * B[r * 6 + j];
@@ -389,15 +446,18 @@ __device__ __forceinline__ void edge_linearize(const LbaDev& d, int k, double hm
             }
         }
     }
+    return chi;
 }
 
 // Phase-0 linearisation of active edge k (computeActiveErrors + linearizeOplus +
 // constructQuadraticForm, G/core/sparse_optimizer.cpp:384-394, block_solver.hpp:502-561).
 // One wave per 64 edges (a launch wide enough to reach every CU); partChi[block] as above.
-__device__ __forceinline__ void edge_lin_body(const LbaDev& d, double hmono, double hstereo, int fuse);
+__device__ __forceinline__ void edge_lin_body(const LbaDev& d, const EdgeStatic& es, double hmono, double hstereo,
+                                              int fuse);
 // Fused slots: first takes the previous trial's pending decision (lm_decide_local; workgroup
 // 0 writes it back) and, after a rejection, restores this workgroup's slice of the estimates.
 __global__ __launch_bounds__(64) void k_edge_lin(LbaDev d, double hmono, double hstereo, int fuse, LmFuse f) {
+    const EdgeStatic es = edge_static(d, max(min((int)(blockIdx.x * 64 + threadIdx.x), d.nact - 1), 0));
     if (fuse) {
         const LmState ls = lm_decide_local(d, f, threadIdx.x, blockIdx.x == 0 && threadIdx.x == 0);
         if (blockIdx.x == 0 && threadIdx.x == 0) *d.lmMid = ls;
@@ -414,21 +474,19 @@ __global__ __launch_bounds__(64) void k_edge_lin(LbaDev d, double hmono, double 
             db.X = d.bX;
             db.q = d.bq;
             db.t = d.bt;
-            edge_lin_body(db, hmono, hstereo, fuse);
+            edge_lin_body(db, es, hmono, hstereo, fuse);
             return;
         }
     } else if (lm_off(d.lm, 0)) {
         return;
     }
-    edge_lin_body(d, hmono, hstereo, fuse);
+    edge_lin_body(d, es, hmono, hstereo, fuse);
 }
-__device__ __forceinline__ void edge_lin_body(const LbaDev& d, double hmono, double hstereo, int fuse) {
+__device__ __forceinline__ void edge_lin_body(const LbaDev& d, const EdgeStatic& es, double hmono, double hstereo,
+                                              int fuse) {
     const int k = blockIdx.x * 64 + threadIdx.x;
     double chi = 0.0;
-    if (k < d.nact) {
-        chi = edge_error(d, k, hmono, hstereo);
-        edge_linearize(d, k, hmono, hstereo);
-    }
+    if (k < d.nact) chi = edge_error_lin(d, k, es, hmono, hstereo);
     const double sum = wave_sum_d(chi);
     if (threadIdx.x == 0) (fuse ? d.partLin : d.partChi)[blockIdx.x] = sum;
 }
@@ -737,7 +795,7 @@ __global__ __launch_bounds__(256) void k_vertex_schur(LbaDev d, int nChi) {
 constexpr int kSpT = 256;
 constexpr int kSpList = 4096;   // pose j's landmark list held in LDS up to this length
 __global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag) {
-    if (lm_off(d.lm, 1)) return;
+    const int phase = d.lm->phase;   // loaded with the pair's CSR ranges (one round trip)
     __shared__ double part[42][kSpT + 1];
     __shared__ int32_t listJ[kSpList];
     const int tid = threadIdx.x;
@@ -746,6 +804,7 @@ __global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag) {
     const int bj = bi + rem;
     const bool diag = bi == bj;
     const int a0 = d.poStart[bi], a1 = d.poStart[bi + 1], b0 = d.poStart[bj], nb = d.poStart[bj + 1] - b0;
+    if (phase != 1) return;   // lm_off(d.lm, 1)
     const bool inLds = nb <= kSpList;
     if (!diag && inLds)
         for (int t = tid; t < nb; t += kSpT) listJ[t] = d.poPt[b0 + t];
