@@ -498,68 +498,54 @@ __device__ __forceinline__ void edge_lin_body(const LbaDev& d, const EdgeStatic&
 constexpr int kLanesPerPt = 4;
 // Pose block p (256 threads): Hpp_p, b_p over its edges; returns the block's max |diagonal|
 // (valid in thread 0).
-// The first kPoseBatch edges of each thread (a, a + 256, ...) are fetched with every load in
-// flight at once (clamped indices; the caller may issue them before it knows whether the block
-// runs, k_vertex_schur), so the chain poStart -> poAct -> Hpp_e costs one round trip each
-// instead of one per edge; further edges (poses with more than 256 * kPoseBatch) follow in the
-// same order.  The per-thread summation order is the edge order either way.
-constexpr int kPoseBatch = 4;
+// Pose block p (256 threads): Hpp_p (21 upper entries) and b_p over its edges.  The 27 values
+// of an edge are read by 27 lanes of a 32-lane group (one edge's Hpp_e and bp_e rows are
+// contiguous: a few cache lines per load instruction, where a lane reading a whole 27-value row
+// makes every instruction touch 64 lines); group g of the 8 takes edges g, g + 8, ... of the
+// pose's list.  The list's first kPoseIdx act positions are fetched by the block in one round
+// trip (pose_prefetch, which k_vertex_schur issues before it reads the LM state) and shared
+// through LDS; the value loads go out kPoseBatch per lane at a time.  The 8 group partials meet
+// in LDS in group order.  Returns the block's max |diagonal| (thread 0).
+constexpr int kPoseIdx = 1024, kPoseBatch = 32;
 struct PosePrefetch {
     int a0, a1;
-    double v[kPoseBatch][27];
+    int k[kPoseIdx / 256];
 };
+__device__ __forceinline__ const double* pose_val_ptr(const LbaDev& d, int k, int v) {
+    return v < 21 ? d.Hpp_e + 21 * (size_t)k + v : d.bp_e + 6 * (size_t)k + (v - 21);
+}
 __device__ __forceinline__ void pose_prefetch(const LbaDev& d, int p, PosePrefetch& f) {
     const int tid = threadIdx.x;
     f.a0 = d.poStart[p];
     f.a1 = d.poStart[p + 1];
-    int k[kPoseBatch];
+    const int last = max(f.a1 - 1, 0);
 #pragma unroll
-    for (int u = 0; u < kPoseBatch; u++) k[u] = d.poAct[min(f.a0 + tid + 256 * u, max(f.a1 - 1, 0))];
-#pragma unroll
-    for (int u = 0; u < kPoseBatch; u++) {
-#pragma unroll
-        for (int i = 0; i < 21; i++) f.v[u][i] = d.Hpp_e[21 * (size_t)k[u] + i];
-#pragma unroll
-        for (int i = 0; i < 6; i++) f.v[u][21 + i] = d.bp_e[6 * (size_t)k[u] + i];
-    }
+    for (int u = 0; u < kPoseIdx / 256; u++) f.k[u] = d.poAct[min(f.a0 + tid + 256 * u, last)];
 }
 __device__ __forceinline__ double pose_block_reduce(const LbaDev& d, int p, double (*part)[257],
                                                     const PosePrefetch& f) {
-    const int tid = threadIdx.x;
-    double acc[27];
+    const int tid = threadIdx.x, g = tid >> 5, v = min(tid & 31, 26);
+    int* idx = reinterpret_cast<int*>(&part[0][0]);   // (27 * 257 doubles hold kPoseIdx ints)
 #pragma unroll
-    for (int i = 0; i < 27; i++) acc[i] = 0;
-#pragma unroll
-    for (int u = 0; u < kPoseBatch; u++) {
-        const bool in = f.a0 + tid + 256 * u < f.a1;
-#pragma unroll
-        for (int i = 0; i < 27; i++) acc[i] = in ? acc[i] + f.v[u][i] : acc[i];
-    }
-    for (int a = f.a0 + tid + 256 * kPoseBatch; a < f.a1; a += 256) {
-        const int k = d.poAct[a];
-#pragma unroll
-        for (int i = 0; i < 21; i++) acc[i] += d.Hpp_e[21 * (size_t)k + i];
-#pragma unroll
-        for (int i = 0; i < 6; i++) acc[21 + i] += d.bp_e[6 * (size_t)k + i];
-    }
-#pragma unroll
-    for (int i = 0; i < 27; i++) part[i][tid] = acc[i];
+    for (int u = 0; u < kPoseIdx / 256; u++) idx[tid + 256 * u] = f.k[u];
     __syncthreads();
-    // value v = t >> 3 (27 values x 8 eighths of 32 partials), eighths meet by xor
-    const int v = tid >> 3, e8 = tid & 7;
-    double sum = 0.0;
-    if (v < 27) {
-#pragma unroll 8
-        for (int i = 0; i < 32; i++) sum += part[v][32 * e8 + i];
+    const int n = f.a1 - f.a0, nl = min(n, kPoseIdx);
+    double acc = 0.0;
+    for (int jb = g; jb < nl; jb += 8 * kPoseBatch) {   // edges jb, jb + 8, ... of this group
+        double x[kPoseBatch];
+#pragma unroll
+        for (int u = 0; u < kPoseBatch; u++) x[u] = *pose_val_ptr(d, idx[min(jb + 8 * u, nl - 1)], v);
+#pragma unroll
+        for (int u = 0; u < kPoseBatch; u++) acc = jb + 8 * u < nl ? acc + x[u] : acc;
     }
-    sum += __shfl_xor(sum, 1, 64);
-    sum += __shfl_xor(sum, 2, 64);
-    sum += __shfl_xor(sum, 4, 64);
-    __syncthreads();
-    if (v < 27 && e8 == 0) part[v][0] = sum;
+    for (int j = kPoseIdx + g; j < n; j += 8) acc += *pose_val_ptr(d, d.poAct[f.a0 + j], v);   // long lists
+    __syncthreads();   // idx aliases part
+    if ((tid & 31) < 27) part[g][tid & 31] = acc;
     __syncthreads();
     if (tid < 27) {
-        const double val = part[tid][0];
+        double val = 0.0;
+#pragma unroll
+        for (int q = 0; q < 8; q++) val += part[q][tid];
         if (tid < 21) {
             int i = 0, o = tid;
             while (o >= 6 - i) { o -= 6 - i; i++; }
@@ -569,11 +555,13 @@ __device__ __forceinline__ double pose_block_reduce(const LbaDev& d, int p, doub
         } else {
             d.bp[6 * (size_t)p + tid - 21] = val;
         }
+        part[8][tid] = val;
     }
+    __syncthreads();
     double m = 0;
     if (tid == 0) {   // diagonal entries sit at upper-row offsets 0, 6, 11, 15, 18, 20
         const int dia[6] = {0, 6, 11, 15, 18, 20};
-        for (int i = 0; i < 6; i++) m = fmax(m, fabs(part[dia[i]][0]));
+        for (int i = 0; i < 6; i++) m = fmax(m, fabs(part[8][dia[i]]));
     }
     return m;
 }
