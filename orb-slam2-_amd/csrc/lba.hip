@@ -317,6 +317,50 @@ __device__ __forceinline__ EdgeStatic edge_static(const LbaDev& d, int k) {
     return s;
 }
 
+// edge_error of active edge k from its prefetched read-only inputs, at the point Xw
+__device__ __forceinline__ double edge_error_s(const LbaDev& d, int k, const EdgeStatic& s, double hmono,
+                                               double hstereo, const double* Xw) {
+    if (!s.on) {
+        d.echi[k] = 0.0;
+        return 0.0;
+    }
+    const int e = s.e, pose = s.pose;
+    double Xc[3];
+    {
+        double r[3];
+        d_quat_rot(d.q + 4 * pose, Xw, r);
+        for (int i = 0; i < 3; i++) Xc[i] = r[i] + d.t[3 * pose + i];
+    }
+    const double* cam = s.cam;
+    const double* obs = s.obs;
+    double er[3];
+    if (!s.st) {
+        const double u = Xc[0] / Xc[2], v = Xc[1] / Xc[2];
+        er[0] = obs[0] - (u * cam[0] + cam[2]);
+        er[1] = obs[1] - (v * cam[1] + cam[3]);
+        er[2] = 0;
+    } else {
+        const float invz = (float)(1.0f / Xc[2]);
+        const double r0 = Xc[0] * invz * cam[0] + cam[2];
+        const double r1 = Xc[1] * invz * cam[1] + cam[3];
+        const float bff = (float)cam[4];
+        const double r2 = r0 - (double)(bff * invz);
+        er[0] = obs[0] - r0;
+        er[1] = obs[1] - r1;
+        er[2] = obs[2] - r2;
+    }
+    for (int i = 0; i < 3; i++) d.err[3 * (size_t)e + i] = er[i];
+    const double w = s.info;
+    double chi = er[0] * (w * er[0]) + er[1] * (w * er[1]);   // d_edge_chi2
+    if (s.st) chi += er[2] * (w * er[2]);
+    if (s.rob) {
+        const double delta = s.st ? hstereo : hmono, dsqr = delta * delta;
+        if (chi > dsqr) chi = 2 * sqrt(chi) * delta - dsqr;
+    }
+    d.echi[k] = chi;
+    return chi;
+}
+
 // computeError (edge_error's arithmetic) then the Jacobians and Huber-weighted quadratic-form
 // blocks of active edge k from the error just computed (no reload).  Returns the robust chi2.
 // Hll_e: 3x3 upper (00 01 02 11 12 22); Hpp_e: 6x6 upper row-major (21); Hpl_e: 6x3; bl_e: 3; bp_e: 6
@@ -1601,6 +1645,9 @@ __global__ __launch_bounds__(256) void k_backsub_errors(LbaDev d, double hmono, 
     for (int u = 0; u < kPtBatch; u++)
 #pragma unroll
         for (int r = 0; r < 6; r++) xp[u][r] = d.x[6 * max(pi[u], 0) + r];
+    EdgeStatic es[kPtBatch];   // the same edges' inputs for the trial errors below
+#pragma unroll
+    for (int u = 0; u < kPtBatch; u++) es[u] = edge_static(d, kk[u]);
     if (phase != 1) return;   // lm_off(d.lm, 1)
     double cl[3] = {0.0, 0.0, 0.0};
     bool open = true;   // fixed poses are last: the first one ends the landmark's sum
@@ -1648,8 +1695,12 @@ __global__ __launch_bounds__(256) void k_backsub_errors(LbaDev d, double hmono, 
 #pragma unroll
     for (int q = 0; q < 3; q++) Xn[q] = __shfl(Xn[q], lane & ~(kLanesPerPt - 1), 64);
     double chi = 0.0;
-    if (l < d.M)
-        for (int a = d.ptStart[l] + sub; a < d.ptStart[l + 1]; a += kLanesPerPt) chi += edge_error(d, d.ptAct[a], hmono, hstereo, Xn);
+    if (l < d.M) {
+#pragma unroll
+        for (int u = 0; u < kPtBatch; u++)
+            if (a0 + kLanesPerPt * u < a1) chi += edge_error_s(d, kk[u], es[u], hmono, hstereo, Xn);
+        for (int a = a0 + kLanesPerPt * kPtBatch; a < a1; a += kLanesPerPt) chi += edge_error(d, d.ptAct[a], hmono, hstereo, Xn);
+    }
     sc = wave_sum_d(sc);
     chi = wave_sum_d(chi);
     if (lane == 0) { wsum[wave] = sc; csum[wave] = chi; }
