@@ -838,6 +838,10 @@ __global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag) {
     const int a0 = d.poStart[bi], a1 = d.poStart[bi + 1], b0 = d.poStart[bj], nb = d.poStart[bj + 1] - b0;
     if (phase != 1) return;   // lm_off(d.lm, 1)
     const bool inLds = nb <= kSpList;
+    // the next edge's act position and landmark are loaded one iteration ahead (the first ones
+    // with pose j's list), so each edge's chain is the search, pose j's act position and the blocks
+    const int aLast = max(a1 - 1, 0);
+    int e1n = d.poAct[min(a0 + tid, aLast)], ln = d.poPt[min(a0 + tid, aLast)];
     if (!diag && inLds)
         for (int t = tid; t < nb; t += kSpT) listJ[t] = d.poPt[b0 + t];
     __syncthreads();
@@ -846,7 +850,9 @@ __global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag) {
 #pragma unroll
     for (int i = 0; i < 42; i++) acc[i] = 0.0;
     for (int a = a0 + tid; a < a1; a += kSpT) {
-        const int e1 = d.poAct[a], l = d.poPt[a];
+        const int e1 = e1n, l = ln;
+        e1n = d.poAct[min(a + kSpT, aLast)];
+        ln = d.poPt[min(a + kSpT, aLast)];
         int e2 = e1;
         if (!diag) {   // lower_bound of l in pose j's sorted landmark list
             int lo = 0, hi = nb;
