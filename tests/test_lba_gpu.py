@@ -217,12 +217,20 @@ def test_repeated_solves_bitwise_identical(amd):
     (dict(stereo_frac=0.5, seed=7), True, False),                         # ids out of index order
     (dict(n_local=30, n_fixed=0, n_points=4000, seed=11), False, False),
     (dict(n_local=8, n_fixed=2, n_points=500, seed=3), True, True),       # Optimizer::BundleAdjustment
+    # landmarks seen by 17-30 keyframes (k_struct_ptsort's insertion-sort path), edges shuffled
+    (dict(n_local=30, n_fixed=4, n_points=400, seed=13, k_range=(17, 30), shuffle_edges=True), True, False),
 ])
 def test_device_structure_matches_host_build(amd, monkeypatch, kw, shuffle_ids, global_ba):
     """The single-process solver builds the edge-level block structure on the device
     (k_struct_*): ORB_LBA_CHECK_STRUCT compares every array with the host build
     (csrc/lba_host.h) inside the call, and the solve equals the host-built one bitwise."""
+    kw = dict(kw)
+    shuffle_edges = kw.pop("shuffle_edges", False)
     pb = _problem(amd, **kw)
+    if shuffle_edges:   # the edge order is the caller's: no grouping by landmark
+        perm = np.random.default_rng(2).permutation(len(pb["edge_point"]))
+        pb = {k: (v[perm] if k.startswith("edge_") else v) for k, v in pb.items()}
+        assert np.bincount(pb["edge_point"]).max() > 16
     if shuffle_ids:   # g2o orders the Hessian blocks by vertex id, not by index
         rng = np.random.default_rng(1)
         pb = dict(pb)
