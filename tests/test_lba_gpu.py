@@ -33,6 +33,7 @@ def _compare(ref, got, tol=1e-5):
     dict(stereo_frac=0.5, seed=7),                            # mixed mono / stereo edges
     dict(n_local=8, n_fixed=2, n_points=500, seed=3),
     dict(n_local=30, n_fixed=0, n_points=4000, seed=11, outlier_frac=0.15),
+    dict(n_local=30, n_fixed=4, n_points=400, seed=13, k_range=(17, 30)),   # landmarks seen by 17-30 KFs
 ])
 def test_local_ba_matches_oracle(amd, kw):
     pb = _problem(amd, **kw)
