@@ -365,7 +365,7 @@ __device__ __forceinline__ double edge_error_s(const LbaDev& d, int k, const Edg
 // blocks of active edge k from the error just computed (no reload).  Returns the robust chi2.
 // Hll_e: 3x3 upper (00 01 02 11 12 22); Hpp_e: 6x6 upper row-major (21); Hpl_e: 6x3; bl_e: 3; bp_e: 6
 __device__ __forceinline__ double edge_error_lin(const LbaDev& d, int k, const EdgeStatic& s, double hmono,
-                                                 double hstereo) {
+                                                 double hstereo, const double* qp, const double* tp, const double* Xp) {
     const int e = s.e, pose = s.pose;
     const bool freePose = d.poseIdx[pose] >= 0;
     if (!s.on) {   // level-1 edge: chi2 0, its stored error stays, its blocks are exact zeros
@@ -382,8 +382,8 @@ __device__ __forceinline__ double edge_error_lin(const LbaDev& d, int k, const E
     double Xc[3];
     {
         double r[3];
-        d_quat_rot(d.q + 4 * pose, d.X + 3 * s.pt, r);
-        for (int i = 0; i < 3; i++) Xc[i] = r[i] + d.t[3 * pose + i];
+        d_quat_rot(qp, Xp, r);
+        for (int i = 0; i < 3; i++) Xc[i] = r[i] + tp[i];
     }
     const double* cam = s.cam;
     const double* obs = s.obs;
@@ -415,7 +415,7 @@ __device__ __forceinline__ double edge_error_lin(const LbaDev& d, int k, const E
     d.echi[k] = chi;
     // linearizeOplus + constructQuadraticForm at the same estimate (Xc as d_transform gives it)
     double R[9];
-    d_quat_to_R(d.q + 4 * pose, R);
+    d_quat_to_R(qp, R);
     const double x = Xc[0], y = Xc[1], z = Xc[2], z_2 = z * z;
     const double fx = cam[0], fy = cam[1], bf = cam[4];
     const bool st = s.st;
@@ -496,12 +496,27 @@ __device__ __forceinline__ double edge_error_lin(const LbaDev& d, int k, const E
 // Phase-0 linearisation of active edge k (computeActiveErrors + linearizeOplus +
 // constructQuadraticForm, G/core/sparse_optimizer.cpp:384-394, block_solver.hpp:502-561).
 // One wave per 64 edges (a launch wide enough to reach every CU); partChi[block] as above.
-__device__ __forceinline__ void edge_lin_body(const LbaDev& d, const EdgeStatic& es, double hmono, double hstereo,
-                                              int fuse);
+struct EdgeVars {   // the edge's pose and point estimates, loaded with its static inputs
+    double q[4], t[3], X[3];
+};
+__device__ __forceinline__ void edge_vars(const LbaDev& d, const EdgeStatic& es, EdgeVars& v) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) v.q[i] = d.q[4 * es.pose + i];
+#pragma unroll
+    for (int i = 0; i < 3; i++) v.t[i] = d.t[3 * es.pose + i];
+#pragma unroll
+    for (int i = 0; i < 3; i++) v.X[i] = d.X[3 * (size_t)es.pt + i];
+}
+__device__ __forceinline__ void edge_lin_body(const LbaDev& d, const EdgeStatic& es, const EdgeVars& ev, double hmono,
+                                              double hstereo, int fuse);
 // Fused slots: first takes the previous trial's pending decision (lm_decide_local; workgroup
 // 0 writes it back) and, after a rejection, restores this workgroup's slice of the estimates.
 __global__ __launch_bounds__(64) void k_edge_lin(LbaDev d, double hmono, double hstereo, int fuse, LmFuse f) {
     const EdgeStatic es = edge_static(d, max(min((int)(blockIdx.x * 64 + threadIdx.x), d.nact - 1), 0));
+    // the estimates as they stand: what the linearisation reads unless the decision below pops
+    // (then the push() backups are read instead and these are dropped)
+    EdgeVars ev;
+    edge_vars(d, es, ev);
     if (fuse) {
         const LmState ls = lm_decide_local(d, f, threadIdx.x, blockIdx.x == 0 && threadIdx.x == 0);
         if (blockIdx.x == 0 && threadIdx.x == 0) *d.lmMid = ls;
@@ -518,19 +533,21 @@ __global__ __launch_bounds__(64) void k_edge_lin(LbaDev d, double hmono, double 
             db.X = d.bX;
             db.q = d.bq;
             db.t = d.bt;
-            edge_lin_body(db, es, hmono, hstereo, fuse);
+            EdgeVars evb;
+            edge_vars(db, es, evb);
+            edge_lin_body(db, es, evb, hmono, hstereo, fuse);
             return;
         }
     } else if (lm_off(d.lm, 0)) {
         return;
     }
-    edge_lin_body(d, es, hmono, hstereo, fuse);
+    edge_lin_body(d, es, ev, hmono, hstereo, fuse);
 }
-__device__ __forceinline__ void edge_lin_body(const LbaDev& d, const EdgeStatic& es, double hmono, double hstereo,
-                                              int fuse) {
+__device__ __forceinline__ void edge_lin_body(const LbaDev& d, const EdgeStatic& es, const EdgeVars& ev, double hmono,
+                                              double hstereo, int fuse) {
     const int k = blockIdx.x * 64 + threadIdx.x;
     double chi = 0.0;
-    if (k < d.nact) chi = edge_error_lin(d, k, es, hmono, hstereo);
+    if (k < d.nact) chi = edge_error_lin(d, k, es, hmono, hstereo, ev.q, ev.t, ev.X);
     const double sum = wave_sum_d(chi);
     if (threadIdx.x == 0) (fuse ? d.partLin : d.partChi)[blockIdx.x] = sum;
 }
