@@ -13,6 +13,7 @@ Prints ONE JSON line on rank 0.
 """
 import argparse
 import concurrent.futures as cf
+import hashlib
 import ctypes as C
 import json
 import os
@@ -434,9 +435,24 @@ def bench_config5(args, amd, dev, rank, world):
             torch.distributed.all_reduce(tot)
         total_pairs = nb * PB
         assert int(tot[1]) == total_pairs, "every pair of every batch processed exactly once"
+        # per-pair digest of mvuRight / mvDepth over the left keypoints, gathered in pair order, so
+        # a sharded run can be compared with one rank array for array (tests/test_bench_ranks.py)
+        local = {}
+        if P:
+            ur_h, dep_h, cnt_h = ur.cpu().numpy(), dep.cpu().numpy(), cnt.cpu().numpy()
+            for j, t in enumerate(pairs):
+                n = min(int(cnt_h[2 * j]), cap)
+                local[t] = hashlib.sha256(ur_h[j, :n].tobytes() + dep_h[j, :n].tobytes()).hexdigest()
+        if world > 1:
+            parts = [None] * world
+            torch.distributed.all_gather_object(parts, local)
+            for d in parts:
+                local.update(d)
+        digest = hashlib.sha256("".join(local[t] for t in sorted(local)).encode()).hexdigest()[:16]
         out[tag] = {"stereo_frames_per_s": round(total_pairs * steps / dt, 1), "ms_per_step": round(dt / steps * 1e3, 4),
                     "batches_per_step": nb, "pairs_per_rank": P,
-                    "stereo_matches_per_pair": round(float(tot[0]) / total_pairs, 1)}
+                    "stereo_matches_per_pair": round(float(tot[0]) / total_pairs, 1),
+                    "uright_depth_sha16": digest}
         del ex
     if world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline_stereo(cv, W, H, NF, EUROC_MBF, 8)
@@ -834,6 +850,105 @@ def batch_sweep(amd, dev, m):
     return res
 
 
+class Pipe:
+    """One frame sequence of the bench step: its own extractor / matcher handles, buffers and HIP
+    streams, so the latency-bound stages of one sequence overlap the others on the GPU.  With
+    `match_stream`, extraction and matching run on two streams of their own (a two-stage software
+    pipeline over steps): SearchForInitialization of step s (match stream) overlaps the extraction
+    of step s+1 (extract stream); keypoint buffers are then double-buffered by step parity, row 0
+    of a buffer holding the previous step's last frame (pair t-1, t across step boundaries), copied
+    on the match stream, and the extraction that next overwrites the other buffer waits for that
+    copy.  tests/test_bench_pipeline.py drives this same class against the oracle."""
+
+    def __init__(self, k, amd, dev, local, pool, W, H, NF, B, Bs, cap, match_stream=False):
+        from orb_slam2_amd import _abi
+        self._abi, self.lib = _abi, _abi.lib()
+        self.k, self.pool, self.W, self.H, self.B, self.Bs, self.cap = k, pool, W, H, B, Bs, cap
+        self.row_kp, self.row_d = cap * 28, cap * 32
+        self.ts = torch.cuda.Stream(dev)
+        self.tm = torch.cuda.Stream(dev) if match_stream else self.ts
+        self.stream, self.mstream = self.ts.cuda_stream, self.tm.cuda_stream
+        self.ex = amd.ORBextractor(NF, 1.2, 8, 20, 7, device=local, max_w=W, max_h=H, max_batch=Bs)
+        self.m = amd.ORBmatcher(0.9, True, device=local)
+        nb = 2 if match_stream else 1
+        self.kps = [torch.zeros((Bs + 1, cap, 7), dtype=torch.int32, device=dev) for _ in range(nb)]
+        self.desc = [torch.zeros((Bs + 1, cap, 32), dtype=torch.uint8, device=dev) for _ in range(nb)]
+        self.counts = [torch.zeros(Bs + 1, dtype=torch.int32, device=dev) for _ in range(nb)]
+        self.m12 = torch.zeros((Bs, cap), dtype=torch.int32, device=dev)
+        self.nm = torch.zeros(Bs, dtype=torch.int32, device=dev)
+        self.ev_ext = [torch.cuda.Event() for _ in range(2)]
+        self.ev_copy = [torch.cuda.Event() for _ in range(2)]
+        self.copy_pending = None
+        self.last = 0
+
+    def frame_range(self, s):
+        """Pool indices of the frames step s extracts on this sequence."""
+        start = (s * self.B + self.k * self.Bs) % (self.pool.shape[0] - self.Bs + 1)
+        return start, start + self.Bs
+
+    def step(self, s):
+        lib, Bs, cap = self.lib, self.Bs, self.cap
+        start, stop = self.frame_range(s)
+        imgs = self.pool[start:stop]
+        nb = len(self.kps)
+        cur, prv = s % nb, (s - 1) % nb
+        kps, desc, counts = self.kps[cur], self.desc[cur], self.counts[cur]
+        if nb == 1:                            # one buffer: carry the last frame before overwriting
+            with torch.cuda.stream(self.ts):
+                kps[0].copy_(kps[Bs])
+                desc[0].copy_(desc[Bs])
+                counts[0:1].copy_(counts[Bs:Bs + 1])
+        if self.copy_pending is not None:      # the previous step's match stream copied row Bs out
+            self.ts.wait_event(self.copy_pending)
+        self._abi.check("orb_extract_batch_device", lib.orb_extract_batch_device(
+            self.ex._h, C.c_void_p(imgs.data_ptr()), self.H * self.W, Bs, self.W, self.H,
+            C.c_void_p(kps.data_ptr() + self.row_kp), C.c_void_p(desc.data_ptr() + self.row_d), cap,
+            C.c_void_p(counts.data_ptr() + 4), C.c_void_p(self.stream)))
+        if nb == 2:
+            self.ev_ext[s % 2].record(self.ts)
+            self.tm.wait_event(self.ev_ext[s % 2])
+            with torch.cuda.stream(self.tm):
+                kps[0].copy_(self.kps[prv][Bs])
+                desc[0].copy_(self.desc[prv][Bs])
+                counts[0:1].copy_(self.counts[prv][Bs:Bs + 1])
+            self.ev_copy[s % 2].record(self.tm)
+            self.copy_pending = self.ev_copy[s % 2]
+        self._abi.check("orb_search_for_initialization_batch_device", lib.orb_search_for_initialization_batch_device(
+            self.m._h, C.c_void_p(kps.data_ptr()), C.c_void_p(desc.data_ptr()), C.c_void_p(counts.data_ptr()),
+            C.c_void_p(kps.data_ptr() + self.row_kp), C.c_void_p(desc.data_ptr() + self.row_d),
+            C.c_void_p(counts.data_ptr() + 4), Bs, cap, self.W, self.H, 100, C.c_void_p(self.m12.data_ptr()),
+            C.c_void_p(self.nm.data_ptr()), C.c_void_p(self.mstream)))
+        self.last = cur
+
+    def status(self):
+        """(extractor, matcher) overflow bits accumulated on this sequence's handles (waits for
+        their streams; reading the matcher's clears it)."""
+        es, ms = C.c_int32(0), C.c_int32(0)
+        self.lib.orb_extractor_batch_status(self.ex._h, C.byref(es))
+        self.lib.orb_matcher_batch_status(self.m._h, C.byref(ms))
+        return es.value, ms.value
+
+    def snapshot(self):
+        """Host copies of the last step's outputs (call after synchronising): per extracted frame
+        its keypoints / descriptors (rows 1..Bs), per pair (t-1, t) matches12 and nmatches."""
+        cur = self.last
+        cnt = self.counts[cur].cpu().numpy()
+        kps = self.kps[cur].cpu().numpy()
+        desc = self.desc[cur].cpu().numpy()
+        return {"counts": cnt, "kps": kps, "desc": desc, "m12": self.m12.cpu().numpy(), "nm": self.nm.cpu().numpy()}
+
+
+def bench_capacity(amd, local, W, H, NF):
+    """Per-frame keypoint capacity the device batch path needs at this geometry (never truncates)."""
+    from orb_slam2_amd import _abi
+    ex0 = amd.ORBextractor(NF, 1.2, 8, 20, 7, device=local, max_w=W, max_h=H, max_batch=1)
+    lw, lh, cells = (np.zeros(8, np.int32) for _ in range(3))
+    cap = C.c_int()
+    _abi.check("orb_extractor_geometry", _abi.lib().orb_extractor_geometry(
+        ex0._h, W, H, _abi.ptr(lw), _abi.ptr(lh), _abi.ptr(cells), C.byref(cap)))
+    return cap.value, lw, lh
+
+
 def spawn_ranks(n):
     """`bench.py --gpus N` without a launcher: start N worker processes of this script (one per
     GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set) before this parent process makes any GPU
@@ -900,78 +1015,10 @@ def main():
     assert B % S == 0, "--batch must be a multiple of --streams"
     Bs = B // S
 
-    class Pipe:
-        """One frame sequence: its own extractor / matcher handles, buffers and HIP streams, so
-        the latency-bound stages of one sequence overlap the others on the GPU.  Extraction and
-        matching run on two streams of their own (a two-stage software pipeline over steps):
-        SearchForInitialization of step s (match stream) overlaps the extraction of step s+1
-        (extract stream).  Keypoint buffers are double-buffered by step parity; row 0 of a buffer
-        holds the previous step's last frame (pair t-1, t across step boundaries), copied on the
-        match stream, and the extraction that next overwrites the other buffer waits for that
-        copy."""
-
-        def __init__(self, k):
-            self.k = k
-            self.ts = torch.cuda.Stream(dev)
-            self.tm = torch.cuda.Stream(dev) if args.match_stream else self.ts
-            self.stream, self.mstream = self.ts.cuda_stream, self.tm.cuda_stream
-            self.ex = amd.ORBextractor(NF, 1.2, 8, 20, 7, device=local, max_w=W, max_h=H, max_batch=Bs)
-            self.m = amd.ORBmatcher(0.9, True, device=local)
-            nb = 2 if args.match_stream else 1
-            self.kps = [torch.zeros((Bs + 1, cap, 7), dtype=torch.int32, device=dev) for _ in range(nb)]
-            self.desc = [torch.zeros((Bs + 1, cap, 32), dtype=torch.uint8, device=dev) for _ in range(nb)]
-            self.counts = [torch.zeros(Bs + 1, dtype=torch.int32, device=dev) for _ in range(nb)]
-            self.m12 = torch.zeros((Bs, cap), dtype=torch.int32, device=dev)
-            self.nm = torch.zeros(Bs, dtype=torch.int32, device=dev)
-            self.ev_ext = [torch.cuda.Event() for _ in range(2)]
-            self.ev_copy = [torch.cuda.Event() for _ in range(2)]
-            self.copy_pending = None
-            self.last = 0
-
-        def step(self, s):
-            n_pool = pool.shape[0]
-            start = (s * B + self.k * Bs) % (n_pool - Bs + 1)
-            imgs = pool[start:start + Bs]
-            nb = len(self.kps)
-            cur, prv = s % nb, (s - 1) % nb
-            kps, desc, counts = self.kps[cur], self.desc[cur], self.counts[cur]
-            if nb == 1:                            # one buffer: carry the last frame before overwriting
-                with torch.cuda.stream(self.ts):
-                    kps[0].copy_(kps[Bs])
-                    desc[0].copy_(desc[Bs])
-                    counts[0:1].copy_(counts[Bs:Bs + 1])
-            if self.copy_pending is not None:      # the previous step's match stream copied row Bs out
-                self.ts.wait_event(self.copy_pending)
-            _abi.check("orb_extract_batch_device", lib.orb_extract_batch_device(
-                self.ex._h, C.c_void_p(imgs.data_ptr()), H * W, Bs, W, H, C.c_void_p(kps.data_ptr() + row_kp),
-                C.c_void_p(desc.data_ptr() + row_d), cap, C.c_void_p(counts.data_ptr() + 4),
-                C.c_void_p(self.stream)))
-            if nb == 2:
-                self.ev_ext[s % 2].record(self.ts)
-                self.tm.wait_event(self.ev_ext[s % 2])
-                with torch.cuda.stream(self.tm):
-                    kps[0].copy_(self.kps[prv][Bs])
-                    desc[0].copy_(self.desc[prv][Bs])
-                    counts[0:1].copy_(self.counts[prv][Bs:Bs + 1])
-                self.ev_copy[s % 2].record(self.tm)
-                self.copy_pending = self.ev_copy[s % 2]
-            _abi.check("orb_search_for_initialization_batch_device", lib.orb_search_for_initialization_batch_device(
-                self.m._h, C.c_void_p(kps.data_ptr()), C.c_void_p(desc.data_ptr()), C.c_void_p(counts.data_ptr()),
-                C.c_void_p(kps.data_ptr() + row_kp), C.c_void_p(desc.data_ptr() + row_d),
-                C.c_void_p(counts.data_ptr() + 4), Bs, cap, W, H, 100, C.c_void_p(self.m12.data_ptr()),
-                C.c_void_p(self.nm.data_ptr()), C.c_void_p(self.mstream)))
-            self.last = cur
-
-    ex0 = amd.ORBextractor(NF, 1.2, 8, 20, 7, device=local, max_w=W, max_h=H, max_batch=1)
-    lw, lh, cells = (np.zeros(8, np.int32) for _ in range(3))
-    cap = C.c_int()
-    _abi.check("orb_extractor_geometry", _abi.lib().orb_extractor_geometry(
-        ex0._h, W, H, _abi.ptr(lw), _abi.ptr(lh), _abi.ptr(cells), C.byref(cap)))
-    cap = cap.value
+    cap, lw, lh = bench_capacity(amd, local, W, H, NF)
     lib = _abi.lib()
-    row_kp, row_d = cap * 28, cap * 32
     torch.cuda.synchronize(dev)
-    pipes = [Pipe(k) for k in range(S)]
+    pipes = [Pipe(k, amd, dev, local, pool, W, H, NF, B, Bs, cap, args.match_stream) for k in range(S)]
     ex = pipes[0].ex
 
     def step(s):
@@ -1004,6 +1051,15 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
+    # overflow bits of every sequence's extractor and matcher over warm-up + timed steps: a set bit
+    # means some frame's keypoints or some pair's candidate list were truncated (not the reference)
+    ext_status = mat_status = 0
+    for p in pipes:
+        e, m = p.status()
+        ext_status |= e
+        mat_status |= m
+    if ext_status or mat_status:
+        raise SystemExit(f"bench: overflow status extractor={ext_status} matcher={mat_status}")
     # k_fast_cell launch times (HIP events recorded on the launch stream during the timed region)
     def stage_times():
         tot, calls = np.zeros(6), 0
@@ -1052,6 +1108,7 @@ def main():
                                f", HBM-resident",
                    "batch_per_gpu": B, "streams_per_gpu": S, "width": W, "height": H, "nfeatures": NF,
                    "parallelism": f"frame-sharded x{world}"},
+        "status": {"extractor": ext_status, "matcher": mat_status},
         "keypoints_per_frame": float(np.mean(cnt)),
         "matches_per_pair": float(np.mean(nmatch)),
     }

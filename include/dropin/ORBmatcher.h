@@ -1,7 +1,8 @@
 // Drop-in replacement for R/include/ORBmatcher.h: the same class declaration.  The constructor
-// (R/src/ORBmatcher.cpp:46-48), DescriptorDistance (:1901-1917) and SearchForInitialization
-// (:499-617) are defined here over liborbslam2_amd through include/orbslam2_amd_shim.hpp; delete
-// those three definitions from R/src/ORBmatcher.cpp and keep the rest.  Compiles inside the
+// (R/src/ORBmatcher.cpp:46-48), DescriptorDistance (:1901-1917), SearchForInitialization
+// (:499-617) and the two tracking forms of SearchByProjection (:63-163, :1564-1718) are defined
+// here over liborbslam2_amd through include/orbslam2_amd_shim.hpp; delete those five definitions
+// from R/src/ORBmatcher.cpp and keep the rest.  Compiles inside the
 // reference tree only (OpenCV, Frame.h); the shim is compiled and tested here with mock types.
 #ifndef ORBMATCHER_H
 #define ORBMATCHER_H
@@ -27,8 +28,13 @@ public:
         return orbslam2_amd::Matcher::DescriptorDistance(a.ptr<uint8_t>(), b.ptr<uint8_t>());
     }
 
-    int SearchByProjection(Frame& F, const std::vector<MapPoint*>& vpMapPoints, const float th = 3);
-    int SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, const float th, const bool bMono);
+    // tracking matchers on the GPU: the local map (R :63-163) and the motion model (R :1564-1718)
+    int SearchByProjection(Frame& F, const std::vector<MapPoint*>& vpMapPoints, const float th = 3) {
+        return mDev.SearchByProjection(F, vpMapPoints, th);
+    }
+    int SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, const float th, const bool bMono) {
+        return mDev.SearchByProjection(CurrentFrame, LastFrame, th, bMono);
+    }
     int SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const std::set<MapPoint*>& sAlreadyFound,
                            const float th, const int ORBdist);
     int SearchByProjection(KeyFrame* pKF, cv::Mat Scw, const std::vector<MapPoint*>& vpPoints,

@@ -338,12 +338,18 @@ int orb_search_for_initialization(orb_matcher* m, const orb_frame_view* f1, cons
 /* ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame,
  * float th, bool bMono) — R/src/ORBmatcher.cpp:1564-1718.
  *   Tcw_cur / Tcw_last: row-major 3x4 float poses (mTcw rows 0..2).
- *   last_has_mp[i] != 0 when LastFrame.mvpMapPoints[i] is set, last_outlier[i] =
- *   mvbOutlier[i]; last_mp_xyz (3 floats) / last_mp_desc (32 B) per last keypoint
- *   (GetWorldPos / GetDescriptor).  scale_factors = CurrentFrame.mvScaleFactors.
+ *   last_has_mp[i]: 0 when LastFrame.mvpMapPoints[i] is NULL, 1 when it is set to a map point
+ *   with observations, 2 when set to one with Observations() == 0 (the temporal points
+ *   Tracking::UpdateLastFrame creates for stereo / RGB-D, R/src/Tracking.cpp:1132-1137, with
+ *   nObs(0), R/src/MapPoint.cpp:65: a current slot given such a point stays open to later
+ *   last-frame points, R :1649-1651);
+ *   last_outlier[i] = mvbOutlier[i]; last_mp_xyz (3 floats) / last_mp_desc (32 B) per last
+ *   keypoint (GetWorldPos / GetDescriptor).  scale_factors = CurrentFrame.mvScaleFactors.
  *   cam = {fx, fy, cx, cy, mbf, mb}.
- *   cur_mp (in/out, cur.n ints): -1 empty slot, -2 occupied by a map point with
- *   observations, >= 0 the last-frame keypoint index whose map point was assigned.
+ *   cur_mp (in/out, cur.n ints) is CurrentFrame.mvpMapPoints: -1 empty slot, -2 occupied by a
+ *   map point with observations (skipped), -3 occupied by one without (a candidate; returned as
+ *   -3 when untouched); on return >= 0 = the last-frame keypoint index whose map point this call
+ *   assigned, -1 = empty (including a slot the rotation check cleared).
  * Returns nmatches. */
 int orb_search_by_projection_frame(orb_matcher* m, const orb_frame_view* cur, const float* Tcw_cur,
                                    const orb_frame_view* last, const float* Tcw_last,
@@ -424,6 +430,13 @@ int orb_search_for_initialization_batch_device(orb_matcher* m, const orb_keypoin
                                                const int32_t* d_n2, int nb, int cap, int width,
                                                int height, int window, int32_t* d_matches12,
                                                int32_t* d_nmatches, void* stream);
+
+/* Overflow bits of the batched SearchForInitialization calls since the last query (waits for the
+ * stream of the last batch call, then clears them): 1 a query's candidate list (the
+ * GetFeaturesInArea result, R/src/ORBmatcher.cpp:523) was longer than the kernel's 1024-entry
+ * capacity and was truncated, 2 the resolution sweeps did not converge.  Returns ORB_EOVERFLOW
+ * when *status != 0 (then some pair's matches12 may differ from the reference's), 0 otherwise. */
+int orb_matcher_batch_status(orb_matcher* m, int32_t* status);
 
 /* ------------------------------------------------------------ local BA */
 

@@ -10,7 +10,9 @@
 //   Extractor                 ORBextractor (R/include/ORBextractor.h:45-123): ctor, operator()
 //                             (R/src/ORBextractor.cpp:1120-1188), the inline getters, mvImagePyramid
 //   Matcher                   ORBmatcher (R/include/ORBmatcher.h:37-143): DescriptorDistance
-//                             (R/src/ORBmatcher.cpp:1901-1917), SearchForInitialization (:499-617)
+//                             (R/src/ORBmatcher.cpp:1901-1917), SearchForInitialization (:499-617),
+//                             SearchByProjection(Frame&, const Frame&, th, bMono) (:1564-1718) and
+//                             SearchByProjection(Frame&, const vector<MapPoint*>&, th) (:63-163)
 //   LocalBundleAdjustment     Optimizer::LocalBundleAdjustment (R/include/Optimizer.h:45,
 //                             R/src/Optimizer.cpp:564-918): graph gathering, lba_solve, write-back
 //
@@ -28,6 +30,7 @@
 #include <stdexcept>
 #include <string>
 #include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "orbslam2_amd.h"
@@ -173,7 +176,86 @@ public:
                      "orb_search_for_initialization");
     }
 
+    // SearchByProjection(CurrentFrame, LastFrame, th, bMono) (R :1564-1718, Tracking::TrackWithMotionModel):
+    // reads both frames' mTcw, the last frame's mvpMapPoints / mvbOutlier and their GetWorldPos /
+    // GetDescriptor / Observations, the current frame's fx..cy, mbf, mb, mvScaleFactors, mvuRight and
+    // mvpMapPoints; writes CurrentFrame.mvpMapPoints as the reference does (a slot holding a point
+    // without observations may be taken over; the rotation check clears the slots it rejects).
+    template <class FrameT>
+    int SearchByProjection(FrameT& CurrentFrame, const FrameT& LastFrame, float th, bool bMono) {
+        FrameView<FrameT> cur(CurrentFrame), last(LastFrame);
+        const size_t nc = CurrentFrame.mvKeysUn.size(), nl = LastFrame.mvKeysUn.size();
+        float Tc[12], Tl[12];
+        detail_read_T34(CurrentFrame.mTcw, Tc);
+        detail_read_T34(LastFrame.mTcw, Tl);
+        std::vector<int32_t> has(nl, 0), slots(nc, -1);
+        std::vector<uint8_t> outl(nl, 0), desc(nl * 32, 0);
+        std::vector<float> xyz(nl * 3, 0.f);
+        for (size_t i = 0; i < nl; i++) {
+            auto mp = LastFrame.mvpMapPoints[i];   // MapPoint* (the vector is const, the points are not)
+            if (!mp) continue;
+            has[i] = mp->Observations() > 0 ? 1 : 2;
+            outl[i] = LastFrame.mvbOutlier[i] ? 1 : 0;
+            const auto X = mp->GetWorldPos();
+            for (int k = 0; k < 3; k++) xyz[3 * i + (size_t)k] = X.template at<float>(k, 0);
+            const auto d = mp->GetDescriptor();
+            std::memcpy(&desc[32 * i], d.data, 32);
+        }
+        for (size_t i = 0; i < nc; i++)
+            if (CurrentFrame.mvpMapPoints[i]) slots[i] = CurrentFrame.mvpMapPoints[i]->Observations() > 0 ? -2 : -3;
+        const float cam[6] = {FrameT::fx, FrameT::fy, FrameT::cx, FrameT::cy, CurrentFrame.mbf, CurrentFrame.mb};
+        const int n = check(orb_search_by_projection_frame(h_, &cur.v, Tc, &last.v, Tl, has.data(), outl.data(), xyz.data(),
+                                                           desc.data(), CurrentFrame.mvScaleFactors.data(), cam, th,
+                                                           bMono ? 1 : 0, slots.data()),
+                            "orb_search_by_projection_frame");
+        for (size_t i = 0; i < nc; i++) {
+            if (slots[i] >= 0) CurrentFrame.mvpMapPoints[i] = LastFrame.mvpMapPoints[(size_t)slots[i]];
+            else if (slots[i] == -1) CurrentFrame.mvpMapPoints[i] = nullptr;
+        }
+        return n;
+    }
+
+    // SearchByProjection(F, vpMapPoints, th) (R :63-163, Tracking::SearchLocalPoints): reads every
+    // point's mbTrackInView / isBad / mTrackProjX / mTrackProjY / mTrackProjXR / mnTrackScaleLevel /
+    // mTrackViewCos / GetDescriptor / Observations and F's mvScaleFactors, mvuRight, mvpMapPoints;
+    // writes F.mvpMapPoints (later points overwrite earlier ones, as in the reference).
+    template <class FrameT, class MapPointT>
+    int SearchByProjection(FrameT& F, const std::vector<MapPointT*>& vpMapPoints, float th = 3) {
+        FrameView<FrameT> f(F);
+        const size_t nm = vpMapPoints.size(), nf = F.mvKeysUn.size();
+        std::vector<uint8_t> inView(nm, 0), hasObs(nm, 0), desc(nm * 32, 0);
+        std::vector<float> proj(nm * 3, 0.f), vcos(nm, 0.f);
+        std::vector<int32_t> level(nm, 0), slots(nf, -1);
+        for (size_t i = 0; i < nm; i++) {
+            MapPointT* pMP = vpMapPoints[i];
+            if (!pMP->mbTrackInView || pMP->isBad()) continue;
+            inView[i] = 1;
+            proj[3 * i] = pMP->mTrackProjX;
+            proj[3 * i + 1] = pMP->mTrackProjY;
+            proj[3 * i + 2] = pMP->mTrackProjXR;
+            level[i] = pMP->mnTrackScaleLevel;
+            vcos[i] = pMP->mTrackViewCos;
+            hasObs[i] = pMP->Observations() > 0 ? 1 : 0;
+            const auto d = pMP->GetDescriptor();
+            std::memcpy(&desc[32 * i], d.data, 32);
+        }
+        for (size_t i = 0; i < nf; i++)
+            if (F.mvpMapPoints[i]) slots[i] = F.mvpMapPoints[i]->Observations() > 0 ? -2 : -3;
+        const int n = check(orb_search_by_projection_local(h_, &f.v, (int)nm, inView.data(), proj.data(), level.data(),
+                                                           vcos.data(), desc.data(), hasObs.data(),
+                                                           F.mvScaleFactors.data(), th, slots.data()),
+                            "orb_search_by_projection_local");
+        for (size_t i = 0; i < nf; i++)
+            if (slots[i] >= 0) F.mvpMapPoints[i] = vpMapPoints[(size_t)slots[i]];
+        return n;
+    }
+
 private:
+    template <class MatT>
+    static void detail_read_T34(const MatT& T, float out[12]) {   // rows 0..2 of a 4x4 float cv::Mat
+        for (int r = 0; r < 3; r++)
+            for (int k = 0; k < 4; k++) out[4 * r + k] = T.template at<float>(r, k);
+    }
     orb_matcher* h_ = nullptr;
 };
 
@@ -313,13 +395,23 @@ void LocalBundleAdjustment(KeyFrameT* pKF, bool* pbStopFlag, MapT* pMap, LbaDump
     D.trials = r.trials;
     D.aborted = r.aborted;
     if (r.aborted) return;   // R :784-786: stopped before optimizing, nothing written back
+    // ---- vToErase (R :850-880): the mono edges in insertion order, then the stereo edges, each
+    //      skipping a point that became bad while the solve ran (isBad() read now, as R :855/:872
+    //      do after optimize); the order matters to EraseObservation's choice of mpRefKF / SetBadFlag
+    std::vector<std::pair<KeyFrameT*, MapPointT*>> vToErase;
+    for (int pass = 0; pass < 2; pass++)
+        for (int e = 0; e < NE; e++) {
+            if ((int)D.edge_stereo[(size_t)e] != pass || !D.edge_erase[(size_t)e]) continue;
+            MapPointT* pMP = vpMP[(size_t)D.edge_point[(size_t)e]];
+            if (pMP->isBad()) continue;
+            vToErase.emplace_back(vpEdgeKF[(size_t)e], pMP);
+        }
     // ---- write-back (R :883-917)
     std::unique_lock<std::mutex> lock(pMap->mMutexMapUpdate);
-    for (int e = 0; e < NE; e++)
-        if (D.edge_erase[(size_t)e]) {
-            vpEdgeKF[(size_t)e]->EraseMapPointMatch(vpMP[(size_t)D.edge_point[(size_t)e]]);
-            vpMP[(size_t)D.edge_point[(size_t)e]]->EraseObservation(vpEdgeKF[(size_t)e]);
-        }
+    for (auto& ke : vToErase) {
+        ke.first->EraseMapPointMatch(ke.second);
+        ke.second->EraseObservation(ke.first);
+    }
     int i = 0;
     for (KeyFrameT* k : lLocalKeyFrames) {   // Converter::toCvMat(SE3Quat): 4x4 float
         float T[16];

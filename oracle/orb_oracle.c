@@ -1050,7 +1050,11 @@ int oracle_search_by_projection_ff(const oracle_frame* cur, const float* Tcw,
         int bestDist = 256, bestIdx2 = -1;
         for (int q = 0; q < nc; q++) {
             const int i2 = cand[q];
-            if (cur_mp[i2] != -1) continue;          /* occupied by a map point with observations */
+            /* R :1649-1651: skip a slot whose map point has observations.  cur_mp[i2] == -3 holds a
+             * point without any on entry; a slot this call gave last point j holds one without any
+             * when last_has_mp[j] == 2 (Tracking::UpdateLastFrame's temporal points) */
+            const int cm = cur_mp[i2];
+            if (!(cm == -1 || cm == -3 || (cm >= 0 && last_has_mp[cm] == 2))) continue;
             if (cur->uright && cur->uright[i2] > 0) {
                 const float ur = u - cam->mbf * invzc;
                 const float er = fabsf(ur - cur->uright[i2]);

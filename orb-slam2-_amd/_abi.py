@@ -76,6 +76,7 @@ def lib() -> C.CDLL:
             "orb_hamming_knn2_batch_device": [vp, vp, vp, vp, vp, i32, i32, i32, vp, vp, vp, vp],
             "orb_search_for_initialization_batch_device": [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32,
                                                            vp, vp, vp],
+            "orb_matcher_batch_status": [vp, vp],
         }
         for name, args in sig.items():
             fn = getattr(_lib, name)

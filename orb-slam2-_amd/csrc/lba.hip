@@ -2628,6 +2628,7 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         return ORB_OK;
     }
     lba_free_all(c);
+    std::memset(&c->last, 0, sizeof(c->last));   // lba_debug_buffer: no pointers into a freed arena
     // single process: the edge-level part of the block structure is built on the device
     // (k_struct_*); with a communicator (owned landmark ranges) on the host
     const bool devStruct = c->world == 1 && NE > 0 && !std::getenv("ORB_LBA_HOST_STRUCT");

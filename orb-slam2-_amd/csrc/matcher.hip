@@ -431,7 +431,7 @@ __global__ __launch_bounds__(kRsT) void k_resolve_sfi(const orb_keypoint* __rest
         if (lane == 63) sc[8 + wid] = incl;
         for (int j = tid; j < n2; j += kRsT) head[j] = -1;
         if (tid < 32) hcount[tid] = 0;
-        if (tid < 4) sc[tid] = 0;
+        if (tid < 6) sc[tid] = 0;
         __syncthreads();
         int run = incl - loc;
         for (int w = 0; w < wid; w++) run += sc[8 + w];
@@ -455,7 +455,9 @@ __global__ __launch_bounds__(kRsT) void k_resolve_sfi(const orb_keypoint* __rest
             const int old = atomicExch(&head[dq & 0xFFFFF], (it << 16) | q);
             nxt[q] = (old >> 16) == it ? (old & 0xFFFF) : -1;
         }
-        if (tid == 0) { sc[(it + 1) & 1] = 0; sc[2 + ((it + 1) & 1)] = 0; }
+        // convergence flags rotate through three slots: the slot cleared here (the next sweep's) is
+        // neither this sweep's nor the previous one, which a slower wave may still be reading below
+        if (tid == 0) { sc[(it + 1) % 3] = 0; sc[4 + ((it + 1) & 1)] = 0; }
         __syncthreads();
         // state seen by query q at keypoint j: smallest bestDist of an earlier query that matched j
         auto seen = [&](int j, int q) {
@@ -486,7 +488,7 @@ __global__ __launch_bounds__(kRsT) void k_resolve_sfi(const orb_keypoint* __rest
                 }
             }
             if (f2 < 0 && nc > kTopK) {      // fewer than two survivors among the top-K
-                fbq[atomicAdd(&sc[2 + (it & 1)], 1)] = q;
+                fbq[atomicAdd(&sc[4 + (it & 1)], 1)] = q;
                 continue;
             }
             int nd = -1;
@@ -496,12 +498,12 @@ __global__ __launch_bounds__(kRsT) void k_resolve_sfi(const orb_keypoint* __rest
                 if (bd <= kThLow && (float)bd < (float)b2 * nnratio) nd = (int)e[f];
             }
             dnew[q] = nd;
-            if (nd != dcur[q]) sc[it & 1] = 1;
+            if (nd != dcur[q]) sc[it % 3] = 1;
         }
         __syncthreads();
         // (F) whole-list rescans, one wave per query: best = smallest (dist, visiting position) among
         //     the survivors, bestDist2 = the multiset second smallest (the reference's running pair)
-        const int nfb = sc[2 + (it & 1)];
+        const int nfb = sc[4 + (it & 1)];
         for (int f = wid; f < nfb; f += kRsT / 64) {
             const int q = fbq[f];
             const int nc = min(qnc[q], kMaxCand);
@@ -540,11 +542,11 @@ __global__ __launch_bounds__(kRsT) void k_resolve_sfi(const orb_keypoint* __rest
                     if (bd <= kThLow && (float)bd < (float)best2 * nnratio) nd = (int)(bestKey & 0xFFFFFull) | (bd << 20);
                 }
                 dnew[q] = nd;
-                if (nd != dcur[q]) sc[it & 1] = 1;
+                if (nd != dcur[q]) sc[it % 3] = 1;
             }
         }
         __syncthreads();
-        const bool again = sc[it & 1] != 0;
+        const bool again = sc[it % 3] != 0;
         int* t = dcur; dcur = dnew; dnew = t;
         if (!again) break;
     }
@@ -677,7 +679,8 @@ __global__ __launch_bounds__(64) void k_resolve_sbp(const orb_keypoint* __restri
                                                     int checkOri, const uint32_t* __restrict__ cand,
                                                     const int* __restrict__ ncand, int32_t* __restrict__ curMp,
                                                     int32_t* __restrict__ nmatches_out, int32_t* __restrict__ histIdx,
-                                                    uint8_t* __restrict__ histBin, int thDist) {
+                                                    uint8_t* __restrict__ histBin, int thDist,
+                                                    const int32_t* __restrict__ lastHas) {
     extern __shared__ __attribute__((aligned(16))) int sm[];
     const int lane = threadIdx.x;
     int* ckey = sm;              // [ncur]
@@ -697,7 +700,12 @@ __global__ __launch_bounds__(64) void k_resolve_sbp(const orb_keypoint* __restri
             if (c < nc) {
                 const uint32_t e = C[c];
                 const int j = (int)(e & 0xFFFFFu), d = (int)(e >> 20);
-                if (curMp[j] == -1)     // occupied slots are skipped (R :1649-1651)
+                // occupied slots are skipped (R :1649-1651), but only when the slot's map point has
+                // observations: with lastHas (the Frame form) a slot holding a point without any
+                // (-3 on entry, or one this call assigned from a last-frame point marked 2: the
+                // temporal visual-odometry points of Tracking::UpdateLastFrame) stays a candidate
+                const int cm = curMp[j];
+                if (cm == -1 || (lastHas && (cm == -3 || (cm >= 0 && lastHas[cm] == 2))))
                     key = ((unsigned long long)(unsigned)d << 40) | ((unsigned long long)(unsigned)ckey[j] << 20) |
                           (unsigned long long)(unsigned)j;
             }
@@ -995,6 +1003,7 @@ struct orb_matcher {
     int *d_cs = nullptr, *d_gj = nullptr;   // SFI grid buckets
     float2* d_gxy = nullptr;
     int *d_ncand = nullptr, *d_status = nullptr;
+    hipStream_t batch_stream = nullptr;   // stream of the last orb_search_for_initialization_batch_device
     // SBP extras
     int32_t* d_hasMp = nullptr;
     uint8_t* d_outl = nullptr;
@@ -1052,6 +1061,9 @@ static int mensure(orb_matcher* m, size_t pairs, size_t pts) {
     MALLOC(m->d_sf, 64 * 4);
     MALLOC(m->d_mpd, P * 32);
 #undef MALLOC
+    // the batch path accumulates overflow bits until orb_matcher_batch_status reads them
+    ORB_HIP_TRY(hipMemsetAsync(m->d_status, 0, 64, m->stream));
+    ORB_HIP_TRY(hipStreamSynchronize(m->stream));
     m->capPairs = pairs;
     m->capPts = pts;
     return ORB_OK;
@@ -1659,6 +1671,8 @@ int orb_search_for_initialization_batch_device(orb_matcher* m, const orb_keypoin
     int st = mensure(m, nb, cap);
     if (st) return st;
     hipStream_t s = stream ? (hipStream_t)stream : m->stream;
+    if (m->batch_stream && m->batch_stream != s) ORB_HIP_TRY(hipStreamSynchronize(m->batch_stream));
+    m->batch_stream = s;
     GridParams g;
     g.min_x = 0.f; g.min_y = 0.f; g.max_x = (float)width; g.max_y = (float)height;
     g.winv = (float)kGridCols / (float)width;
@@ -1674,6 +1688,20 @@ int orb_search_for_initialization_batch_device(orb_matcher* m, const orb_keypoin
                        m->d_status);
     ORB_HIP_TRY(hipGetLastError());
     return ORB_OK;
+}
+
+int orb_matcher_batch_status(orb_matcher* m, int32_t* status) {
+    if (!m || !status) return ORB_EINVAL;
+    *status = 0;
+    if (!m->d_status) return ORB_OK;
+    ORB_HIP_TRY(hipSetDevice(m->device));
+    if (m->batch_stream) ORB_HIP_TRY(hipStreamSynchronize(m->batch_stream));
+    int32_t v = 0;
+    ORB_HIP_TRY(hipMemcpyAsync(&v, m->d_status, 4, hipMemcpyDeviceToHost, m->stream));
+    ORB_HIP_TRY(hipMemsetAsync(m->d_status, 0, 4, m->stream));
+    ORB_HIP_TRY(hipStreamSynchronize(m->stream));
+    *status = v;
+    return v ? ORB_EOVERFLOW : ORB_OK;
 }
 
 int orb_search_by_projection_frame(orb_matcher* m, const orb_frame_view* cur, const float* Tcw_cur,
@@ -1755,7 +1783,8 @@ int orb_search_by_projection_frame(orb_matcher* m, const orb_frame_view* cur, co
     }
     const size_t lds = ((size_t)cur->n + kHisto + 4) * 4;
     hipLaunchKernelGGL(k_resolve_sbp, dim3(1), dim3(64), lds, s, m->d_k2, cur->n, m->d_k1, last->n, g, m->checkOri,
-                       m->d_cand, m->d_ncand, m->d_m12, m->d_nm, m->d_hI, m->d_hB, kThHigh);
+                       m->d_cand, m->d_ncand, m->d_m12, m->d_nm, m->d_hI, m->d_hB, kThHigh,
+                       (const int32_t*)m->d_hasMp);
     ORB_HIP_TRY(hipGetLastError());
     ORB_HIP_TRY(hipMemcpyAsync(hcm, m->d_m12, (size_t)cur->n * 4, hipMemcpyDeviceToHost, s));
     ORB_HIP_TRY(hipMemcpyAsync(hn, m->d_nm, 4, hipMemcpyDeviceToHost, s));
@@ -1832,7 +1861,7 @@ int orb_search_by_projection_kf(orb_matcher* m, const orb_frame_view* cur, const
     }
     const size_t lds = ((size_t)cur->n + kHisto + 4) * 4;
     hipLaunchKernelGGL(k_resolve_sbp, dim3(1), dim3(64), lds, s, m->d_k2, cur->n, m->d_k1, nmp, g, m->checkOri,
-                       m->d_cand, m->d_ncand, m->d_m12, m->d_nm, m->d_hI, m->d_hB, orb_dist);
+                       m->d_cand, m->d_ncand, m->d_m12, m->d_nm, m->d_hI, m->d_hB, orb_dist, (const int32_t*)nullptr);
     ORB_HIP_TRY(hipGetLastError());
     ORB_HIP_TRY(hipMemcpyAsync(hcm, m->d_m12, (size_t)cur->n * 4, hipMemcpyDeviceToHost, s));
     ORB_HIP_TRY(hipMemcpyAsync(hn, m->d_nm, 4, hipMemcpyDeviceToHost, s));
@@ -1907,7 +1936,7 @@ int orb_search_by_projection_sim3(orb_matcher* m, const orb_frame_view* kf, cons
     }
     const size_t lds = ((size_t)kf->n + kHisto + 4) * 4;
     hipLaunchKernelGGL(k_resolve_sbp, dim3(1), dim3(64), lds, s, m->d_k2, kf->n, m->d_k2, n_mp, g, 0, m->d_cand,
-                       m->d_ncand, m->d_m12, m->d_nm, m->d_hI, m->d_hB, kThLow);
+                       m->d_ncand, m->d_m12, m->d_nm, m->d_hI, m->d_hB, kThLow, (const int32_t*)nullptr);
     ORB_HIP_TRY(hipGetLastError());
     ORB_HIP_TRY(hipMemcpyAsync(hm, m->d_m12, (size_t)kf->n * 4, hipMemcpyDeviceToHost, s));
     ORB_HIP_TRY(hipMemcpyAsync(hn, m->d_nm, 4, hipMemcpyDeviceToHost, s));

@@ -4,6 +4,8 @@
 // tests/test_cpp_shim.py:
 //   shim_caller extract IN OUT   ORBextractor::operator() on one image
 //   shim_caller sfi IN OUT       ORBmatcher::SearchForInitialization on two frames
+//   shim_caller sbp IN OUT       ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono)
+//   shim_caller sbl IN OUT       ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th)
 //   shim_caller lba IN OUT       Optimizer::LocalBundleAdjustment on a mock keyframe / map-point graph
 // IN / OUT: little-endian arrays, each written as int64 element count + raw elements.
 // Exit status: 0 ok, 3 the library reported an error (e.g. no gfx950 device), 2 bad usage.
@@ -11,6 +13,8 @@
 #include <cstdlib>
 #include <map>
 #include <mutex>
+#include <string>
+#include <utility>
 #include <stdexcept>
 #include <vector>
 
@@ -46,16 +50,24 @@ struct Mat {   // the cv::Mat members the shim uses
 struct Point2f { float x, y; };
 struct KeyPoint { Point2f pt; float size, angle, response; int octave, class_id; };
 
+struct MapPoint;
 struct Frame {
     std::vector<KeyPoint> mvKeysUn;
     Mat mDescriptors;
     std::vector<float> mvuRight;
+    std::vector<MapPoint*> mvpMapPoints;
+    std::vector<bool> mvbOutlier;
+    std::vector<float> mvScaleFactors;
+    Mat mTcw;
+    float mbf = 0, mb = 0;
     static float mnMinX, mnMinY, mnMaxX, mnMaxY, mfGridElementWidthInv, mfGridElementHeightInv;
+    static float fx, fy, cx, cy;
 };
 float Frame::mnMinX, Frame::mnMinY, Frame::mnMaxX, Frame::mnMaxY, Frame::mfGridElementWidthInv,
-    Frame::mfGridElementHeightInv;
+    Frame::mfGridElementHeightInv, Frame::fx, Frame::fy, Frame::cx, Frame::cy;
 
-struct MapPoint;
+// the order of KeyFrame::EraseMapPointMatch calls (keyframe mnId, map point mnId)
+std::vector<std::pair<unsigned long, unsigned long>> g_erase_log;
 struct KeyFrame {
     unsigned long mnId = 0, mnBALocalForKF = 0, mnBAFixedForKF = 0;
     bool bad = false;
@@ -70,10 +82,7 @@ struct KeyFrame {
     bool isBad() const { return bad; }
     Mat GetPose() { return Tcw; }
     void SetPose(const Mat& T) { Tcw = T; }
-    void EraseMapPointMatch(MapPoint* p) {
-        for (auto& m : matches)
-            if (m == p) m = nullptr;
-    }
+    void EraseMapPointMatch(MapPoint* p);
 };
 struct MapPoint {
     unsigned long mnId = 0, mnBALocalForKF = 0;
@@ -87,7 +96,20 @@ struct MapPoint {
     std::map<KeyFrame*, size_t> GetObservations() { return obs; }
     void EraseObservation(KeyFrame* k) { obs.erase(k); }
     void UpdateNormalAndDepth() { updates++; }
+    // tracking members read by SearchByProjection
+    int extraObs = 0;   // observations beyond `obs` (the matcher tests keep `obs` empty)
+    int Observations() { return (int)obs.size() + extraObs; }
+    Mat desc;
+    Mat GetDescriptor() { return desc; }
+    bool mbTrackInView = false;
+    float mTrackProjX = 0, mTrackProjY = 0, mTrackProjXR = 0, mTrackViewCos = 0;
+    int mnTrackScaleLevel = 0;
 };
+inline void KeyFrame::EraseMapPointMatch(MapPoint* p) {
+    g_erase_log.emplace_back(mnId, p->mnId);
+    for (auto& m : matches)
+        if (m == p) m = nullptr;
+}
 struct Map {
     std::mutex mMutexMapUpdate;
 };
@@ -162,6 +184,117 @@ static void run_sfi(FILE* in, FILE* out) {
     wr(out, &d01, 1);
 }
 
+static void set_grid(const std::vector<float>& g) {
+    mock::Frame::mnMinX = g[0]; mock::Frame::mnMinY = g[1]; mock::Frame::mnMaxX = g[2]; mock::Frame::mnMaxY = g[3];
+    mock::Frame::mfGridElementWidthInv = g[4]; mock::Frame::mfGridElementHeightInv = g[5];
+}
+
+// current-frame slots on entry: -1 NULL, -2 a point with observations, -3 one without; on exit the
+// index of the point a slot holds in `pts`, or the same codes
+static void init_slots(mock::Frame& F, const std::vector<int32_t>& init, mock::MapPoint& withObs, mock::MapPoint& noObs) {
+    F.mvpMapPoints.assign(init.size(), nullptr);
+    for (size_t i = 0; i < init.size(); i++)
+        F.mvpMapPoints[i] = init[i] == -2 ? &withObs : init[i] == -3 ? &noObs : nullptr;
+}
+static std::vector<int32_t> read_slots(const mock::Frame& F, const std::vector<mock::MapPoint*>& pts,
+                                       const mock::MapPoint& withObs, const mock::MapPoint& noObs) {
+    std::map<const mock::MapPoint*, int32_t> idx;
+    for (size_t i = 0; i < pts.size(); i++) idx[pts[i]] = (int32_t)i;
+    std::vector<int32_t> o(F.mvpMapPoints.size(), -1);
+    for (size_t i = 0; i < o.size(); i++) {
+        const mock::MapPoint* p = F.mvpMapPoints[i];
+        o[i] = !p ? -1 : p == &withObs ? -2 : p == &noObs ? -3 : idx.at(p);
+    }
+    return o;
+}
+
+static void run_sbp(FILE* in, FILE* out) {
+    mock::Frame C, L;
+    load_frame(in, C);
+    C.mvuRight = rd<float>(in);
+    load_frame(in, L);
+    L.mvuRight.assign(L.mvKeysUn.size(), -1.f);
+    set_grid(rd<float>(in));
+    const auto Tc = rd<float>(in), Tl = rd<float>(in);
+    const auto has = rd<int32_t>(in);
+    const auto outl = rd<uint8_t>(in);
+    const auto xyz = rd<float>(in);
+    const auto mpd = rd<uint8_t>(in);
+    C.mvScaleFactors = rd<float>(in);
+    const auto cam = rd<float>(in);
+    const auto th = rd<float>(in);
+    const auto mono = rd<int32_t>(in);
+    const auto init = rd<int32_t>(in);
+    C.mTcw.create(4, 4, orbslam2_amd::kCV_32F);
+    L.mTcw.create(4, 4, orbslam2_amd::kCV_32F);
+    for (int i = 0; i < 16; i++) {
+        C.mTcw.at<float>(i / 4, i % 4) = Tc[(size_t)i];
+        L.mTcw.at<float>(i / 4, i % 4) = Tl[(size_t)i];
+    }
+    mock::Frame::fx = cam[0]; mock::Frame::fy = cam[1]; mock::Frame::cx = cam[2]; mock::Frame::cy = cam[3];
+    C.mbf = cam[4]; C.mb = cam[5];
+    const size_t nl = L.mvKeysUn.size();
+    std::vector<mock::MapPoint> pts(nl);
+    std::vector<mock::MapPoint*> ptr(nl, nullptr);
+    L.mvpMapPoints.assign(nl, nullptr);
+    L.mvbOutlier.assign(nl, false);
+    for (size_t i = 0; i < nl; i++) {
+        ptr[i] = &pts[i];
+        pts[i].X.create(3, 1, orbslam2_amd::kCV_32F);
+        for (int k = 0; k < 3; k++) pts[i].X.at<float>(k, 0) = xyz[3 * i + (size_t)k];
+        pts[i].desc.create(1, 32, orbslam2_amd::kCV_8U);
+        std::copy(mpd.begin() + 32 * (long)i, mpd.begin() + 32 * (long)(i + 1), pts[i].desc.data);
+        pts[i].extraObs = has[i] == 1 ? 1 : 0;   // 2: a point without observations (temporal)
+        if (has[i]) L.mvpMapPoints[i] = &pts[i];
+        L.mvbOutlier[i] = outl[i] != 0;
+    }
+    mock::MapPoint withObs, noObs;
+    withObs.extraObs = 1;
+    init_slots(C, init, withObs, noObs);
+    orbslam2_amd::Matcher matcher(0.9f, true);
+    const int32_t n = matcher.SearchByProjection(C, L, th[0], mono[0] != 0);
+    wr(out, &n, 1);
+    wr(out, read_slots(C, ptr, withObs, noObs));
+}
+
+static void run_sbl(FILE* in, FILE* out) {
+    mock::Frame F;
+    load_frame(in, F);
+    F.mvuRight = rd<float>(in);
+    set_grid(rd<float>(in));
+    const auto inView = rd<uint8_t>(in), bad = rd<uint8_t>(in);
+    const auto proj = rd<float>(in);
+    const auto level = rd<int32_t>(in);
+    const auto vcos = rd<float>(in);
+    const auto mpd = rd<uint8_t>(in);
+    const auto hasObs = rd<uint8_t>(in);
+    F.mvScaleFactors = rd<float>(in);
+    const auto th = rd<float>(in), nn = rd<float>(in);
+    const auto init = rd<int32_t>(in);
+    const size_t nm = inView.size();
+    std::vector<mock::MapPoint> pts(nm);
+    std::vector<mock::MapPoint*> ptr(nm);
+    for (size_t i = 0; i < nm; i++) {
+        mock::MapPoint& p = pts[i];
+        ptr[i] = &p;
+        p.bad = bad[i] != 0;
+        p.mbTrackInView = inView[i] != 0;
+        p.mTrackProjX = proj[3 * i]; p.mTrackProjY = proj[3 * i + 1]; p.mTrackProjXR = proj[3 * i + 2];
+        p.mnTrackScaleLevel = level[i];
+        p.mTrackViewCos = vcos[i];
+        p.extraObs = hasObs[i] ? 1 : 0;
+        p.desc.create(1, 32, orbslam2_amd::kCV_8U);
+        std::copy(mpd.begin() + 32 * (long)i, mpd.begin() + 32 * (long)(i + 1), p.desc.data);
+    }
+    mock::MapPoint withObs, noObs;
+    withObs.extraObs = 1;
+    init_slots(F, init, withObs, noObs);
+    orbslam2_amd::Matcher matcher(nn[0], true);
+    const int32_t n = matcher.SearchByProjection(F, ptr, th[0]);
+    wr(out, &n, 1);
+    wr(out, read_slots(F, ptr, withObs, noObs));
+}
+
 static void run_lba(FILE* in, FILE* out) {
     const auto Tcw = rd<float>(in);
     const auto fixedCam = rd<uint8_t>(in);
@@ -230,11 +363,14 @@ static void run_lba(FILE* in, FILE* out) {
         nobs.push_back((int32_t)M.obs.size());
     }
     wr(out, Tout); wr(out, Xout); wr(out, upd); wr(out, nobs);
+    std::vector<int64_t> elog;   // EraseMapPointMatch calls in order: keyframe mnId, map point mnId
+    for (const auto& e : mock::g_erase_log) { elog.push_back((int64_t)e.first); elog.push_back((int64_t)e.second); }
+    wr(out, elog);
 }
 
 int main(int argc, char** argv) {
     if (argc != 4) {
-        std::fprintf(stderr, "usage: %s extract|sfi|lba IN OUT\n", argv[0]);
+        std::fprintf(stderr, "usage: %s extract|sfi|sbp|sbl|lba IN OUT\n", argv[0]);
         return 2;
     }
     FILE* in = std::fopen(argv[2], "rb");
@@ -244,6 +380,8 @@ int main(int argc, char** argv) {
     try {
         if (mode == "extract") run_extract(in, out);
         else if (mode == "sfi") run_sfi(in, out);
+        else if (mode == "sbp") run_sbp(in, out);
+        else if (mode == "sbl") run_sbl(in, out);
         else if (mode == "lba") run_lba(in, out);
         else return 2;
     } catch (const std::exception& e) {

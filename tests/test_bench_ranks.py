@@ -38,3 +38,7 @@ def test_bench_two_ranks_report_world_and_agree_with_one():
     c1, c2 = one["config5_stereo_sharded"], two["config5_stereo_sharded"]
     for tag in ("throughput", "latency_one_batch"):
         assert c1[tag]["stereo_matches_per_pair"] == c2[tag]["stereo_matches_per_pair"]
+        # mvuRight / mvDepth of every pair identical whether one rank or two computed it
+        assert c1[tag]["uright_depth_sha16"] == c2[tag]["uright_depth_sha16"]
+    # frame shards: both ranks' sequences carried no truncation
+    assert one["status"] == {"extractor": 0, "matcher": 0} and two["status"] == {"extractor": 0, "matcher": 0}

@@ -3,10 +3,12 @@ shim include/orbslam2_amd_shim.hpp, with mock cv::Mat / KeyPoint / Frame / KeyFr
 Map types carrying the member names the reference's own types have:
   * CPU: the program compiles with -Wall -Wextra -Werror, links the library through the header,
     and without a GPU fails cleanly (exit 3, the ORB_ENODEV message) instead of falling back;
-  * GPU: ORBextractor::operator() and ORBmatcher::SearchForInitialization through the shim are
-    bit-exact against the oracle; Optimizer::LocalBundleAdjustment through the shim gathers the
-    reference's graph (R/src/Optimizer.cpp:567-782) from the mock keyframes, solves, and writes
-    back (:883-917) exactly what lba_solve returns for the gathered arrays."""
+  * GPU: ORBextractor::operator(), ORBmatcher::SearchForInitialization and both tracking forms of
+    ORBmatcher::SearchByProjection through the shim are bit-exact against the oracle;
+    Optimizer::LocalBundleAdjustment through the shim gathers the reference's graph
+    (R/src/Optimizer.cpp:567-782) from the mock keyframes, solves within the oracle's tolerances
+    (identical LM decisions and erase set, poses / points to 1e-5), and writes back (:850-917)
+    exactly what lba_solve returns, erasing mono observations before stereo ones."""
 import pathlib
 import shutil
 import subprocess
@@ -15,6 +17,7 @@ import numpy as np
 import pytest
 
 import oracle_ref as O
+from test_matcher_gpu import _sbp_setup
 
 ROOT = pathlib.Path(__file__).resolve().parents[1]
 LIB_DIR = ROOT / "orb-slam2-_amd" / "lib"
@@ -113,6 +116,65 @@ def test_shim_search_for_initialization_matches_oracle(shim, tmp_path):
     assert int(d01[0]) == O.descriptor_distance(a["desc"][0], b["desc"][0])
 
 
+def _frame_arrays(kps, desc):
+    return (np.ascontiguousarray(kps["x"], np.float32), np.ascontiguousarray(kps["y"], np.float32),
+            np.ascontiguousarray(kps["angle"], np.float32), np.ascontiguousarray(kps["octave"], np.int32),
+            np.ascontiguousarray(desc, np.uint8))
+
+
+GRID = np.array([0, 0, 640, 480, np.float32(64) / np.float32(640), np.float32(48) / np.float32(480)], np.float32)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stereo,th,temporal", [(False, 15.0, False), (True, 7.0, True)])
+def test_shim_search_by_projection_frame_matches_oracle(shim, tmp_path, stereo, th, temporal):
+    """Tracking::TrackWithMotionModel's call through the shim: the mock frames' mTcw, mvpMapPoints
+    (with and without observations), mvbOutlier, mvuRight and the static intrinsics are gathered by
+    the shim; CurrentFrame.mvpMapPoints comes back as the oracle's R :1564-1718 leaves it."""
+    a, b, cam, xyz, Tl, Tc, has, outl, mpd, ur, sf = _sbp_setup(stereo=stereo)
+    init = np.full(len(b["kps"]), -1, np.int32)
+    init[::17] = -2
+    if temporal:
+        rng = np.random.default_rng(12)
+        has = np.where((has > 0) & (rng.random(len(has)) < 0.4), 2, has).astype(np.int32)
+        init[5::19] = -3
+    cur = O.FrameView(b["kps"], b["desc"], 640, 480, uright=ur)
+    last = O.FrameView(a["kps"], a["desc"], 640, 480)
+    n_ref, mp_ref = O.search_by_projection_ff(cur, Tc[:3], last, Tl[:3], has, outl, xyz, mpd, sf,
+                                              O.Camera(*[float(v) for v in cam]), th, not stereo, True, init)
+    urc = ur if ur is not None else np.full(len(b["kps"]), -1, np.float32)
+    r, outp = _run(shim, "sbp", tmp_path, *_frame_arrays(b["kps"], b["desc"]), urc,
+                   *_frame_arrays(a["kps"], a["desc"]), GRID, np.asarray(Tc, np.float32).reshape(-1),
+                   np.asarray(Tl, np.float32).reshape(-1), has.astype(np.int32), outl.astype(np.uint8),
+                   xyz.astype(np.float32).reshape(-1), mpd, sf.astype(np.float32), cam.astype(np.float32),
+                   np.array([th], np.float32), np.array([0 if stereo else 1], np.int32), init)
+    assert r.returncode == 0, r.stderr
+    n, slots = _read(outp, np.int32, np.int32)
+    assert int(n[0]) == n_ref and np.array_equal(slots, mp_ref)
+    assert n_ref > 100
+
+
+@pytest.mark.gpu
+def test_shim_search_by_projection_local_matches_oracle(shim, tmp_path):
+    """Tracking::SearchLocalPoints's call through the shim: mbTrackInView / isBad / mTrackProj* /
+    mnTrackScaleLevel / mTrackViewCos / GetDescriptor / Observations read from mock map points."""
+    from test_matcher_gpu import _sbl_setup
+    b, in_view, proj, level, vcos, md, has_obs, ur, init, sf = _sbl_setup(stereo=True)
+    f = O.FrameView(b["kps"], b["desc"], 640, 480, uright=ur)
+    th = 3.0
+    rng = np.random.default_rng(4)
+    bad = (rng.random(len(in_view)) < 0.05) & in_view
+    n_ref, mp_ref = O.search_by_projection_local(f, in_view & ~bad, proj, level, vcos, md, has_obs, sf, 0.8, th, init)
+    r, outp = _run(shim, "sbl", tmp_path, *_frame_arrays(b["kps"], b["desc"]), ur, GRID,
+                   in_view.astype(np.uint8), bad.astype(np.uint8), proj.astype(np.float32).reshape(-1),
+                   level.astype(np.int32), vcos.astype(np.float32), md, has_obs.astype(np.uint8), sf.astype(np.float32),
+                   np.array([th], np.float32), np.array([0.8], np.float32), init)
+    assert r.returncode == 0, r.stderr
+    n, slots = _read(outp, np.int32, np.int32)
+    assert int(n[0]) == n_ref and np.array_equal(slots, mp_ref)
+    assert n_ref > 50
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("stereo", [0.0, 0.4])
 def test_shim_local_bundle_adjustment(shim, tmp_path, amd, stereo):
@@ -130,9 +192,9 @@ def test_shim_local_bundle_adjustment(shim, tmp_path, amd, stereo):
                    np.zeros(1, np.uint8))
     assert r.returncode == 0, r.stderr
     (pq, pt, pfix, pid, X, xid, xbad, ept, eps, est, eobs, einfo, ecam, erase, oq, ot, ox, st, Tout, Xout, upd,
-     nobs) = _read(outp, np.float64, np.float64, np.uint8, np.int64, np.float64, np.int64, np.uint8, np.int32,
-                   np.int32, np.uint8, np.float64, np.float64, np.float64, np.uint8, np.float64, np.float64,
-                   np.float64, np.int32, np.float32, np.float32, np.int32, np.int32)
+     nobs, elog) = _read(outp, np.float64, np.float64, np.uint8, np.int64, np.float64, np.int64, np.uint8, np.int32,
+                         np.int32, np.uint8, np.float64, np.float64, np.float64, np.uint8, np.float64, np.float64,
+                         np.float64, np.int32, np.float32, np.float32, np.int32, np.int32, np.int64)
     NP, NE = len(pfix), len(ept)
     # the gathered graph (R :567-668): the local points are those a local keyframe observes; every
     # observation of a local point is an edge; the fixed cameras are the other keyframes observing
@@ -156,6 +218,19 @@ def test_shim_local_bundle_adjustment(shim, tmp_path, amd, stereo):
                 edge_cam=ecam.reshape(-1, 5))
     ref = amd.LocalBA().solve(prob)
     assert tuple(st[:2]) == ref["iterations"] and int(st[2]) == ref["trials"] and int(st[3]) == 0
+    # ... and within the oracle's tolerances (tests/test_lba_gpu.py): same LM decisions, same erase set
+    orc = O.lba_solve(prob)
+    assert tuple(st[:2]) == orc["iterations"] and int(st[2]) == orc["trials"]
+    assert np.array_equal(erase, orc["edge_erase"])
+    assert np.abs(oq.reshape(-1, 4) - orc["pose_q"]).max() < 1e-5 and np.abs(ot.reshape(-1, 3) - orc["pose_t"]).max() < 1e-5
+    assert np.abs(ox.reshape(-1, 3) - orc["point_xyz"]).max() < 1e-5
+    # vToErase order (R :850-880): every erased mono edge in edge order, then every erased stereo edge
+    mp_mnid = xid - (pid.max() + 1)
+    want = [(int(pid[eps[e]]), int(mp_mnid[ept[e]])) for pas in (0, 1) for e in range(NE)
+            if erase[e] and int(est[e]) == pas]
+    assert [tuple(x) for x in elog.reshape(-1, 2)] == want
+    if stereo:
+        assert erase[est == 1].any() and erase[est == 0].any()
     assert np.array_equal(oq.reshape(-1, 4), ref["pose_q"]) and np.array_equal(ot.reshape(-1, 3), ref["pose_t"])
     assert np.array_equal(ox.reshape(-1, 3), ref["point_xyz"]) and np.array_equal(erase, ref["edge_erase"])
     # write-back (R :883-917): local keyframes' Tcw = Converter::toCvMat of the estimate, fixed

@@ -96,14 +96,22 @@ def _sbp_setup(W=640, H=480, nf=1000, seed=0x5EED0001, stereo=False):
     return a, b, cam, xyz, Tl, Tc, has, outl, mpd, ur, sf
 
 
-@pytest.mark.parametrize("stereo,th", [(False, 15.0), (True, 7.0), (True, 15.0)])
-def test_search_by_projection_frame(amd, stereo, th):
+@pytest.mark.parametrize("stereo,th,temporal", [(False, 15.0, False), (True, 7.0, False), (True, 15.0, False),
+                                                (True, 7.0, True), (True, 15.0, True)])
+def test_search_by_projection_frame(amd, stereo, th, temporal):
+    """temporal: 40 % of the last frame's map points have no observations (Tracking::UpdateLastFrame's
+    temporal points, R/src/Tracking.cpp:1132-1137) and some current slots hold such a point on entry
+    (-3): those slots stay candidates (R/src/ORBmatcher.cpp:1649-1651)."""
     a, b, cam, xyz, Tl, Tc, has, outl, mpd, ur, sf = _sbp_setup(stereo=stereo)
     cur = O.FrameView(b["kps"], b["desc"], 640, 480, uright=ur)
     last = O.FrameView(a["kps"], a["desc"], 640, 480)
     camo = O.Camera(*[float(v) for v in cam])
     init = np.full(len(b["kps"]), -1, np.int32)
     init[::17] = -2
+    if temporal:
+        rng = np.random.default_rng(12)
+        has = np.where((has > 0) & (rng.random(len(has)) < 0.4), 2, has).astype(np.int32)
+        init[5::19] = -3
     n_ref, mp_ref = O.search_by_projection_ff(cur, Tc[:3], last, Tl[:3], has, outl, xyz, mpd, sf, camo, th,
                                               not stereo, True, init)
     m = amd.ORBmatcher(0.9, True)

@@ -266,6 +266,131 @@ def test_search_by_projection_local_oracle_vs_python():
     assert nm > 30
 
 
+def test_search_by_projection_frame_oracle_vs_python():
+    """The C oracle of SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, th, bMono)
+    against a literal Python restatement of R/src/ORBmatcher.cpp:1564-1718, with the last frame's
+    map points as objects that do or do not have observations (Tracking::UpdateLastFrame's temporal
+    points have none, R/src/Tracking.cpp:1132-1137) and current slots pre-set to points with and
+    without observations: a slot whose point has no observations stays a candidate, so a later last
+    point can take it over, and the rotation histogram then lists the slot twice."""
+    from orb_slam2_amd import _abi
+    rng = np.random.default_rng(5)
+    W, H, n, nl = 640, 480, 300, 260
+    kc = np.zeros(n, _abi.KEYPOINT_DTYPE)
+    kc["x"] = rng.uniform(20, 620, n).astype(np.float32)
+    kc["y"] = rng.uniform(20, 460, n).astype(np.float32)
+    kc["octave"] = rng.integers(0, 3, n)
+    kc["angle"] = rng.uniform(0, 360, n).astype(np.float32)
+    dc = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    urc = np.where(rng.random(n) < 0.5, kc["x"] - 12, -1).astype(np.float32)
+    src = rng.integers(0, n, nl)                       # last keypoints near current ones (crowded)
+    kl = np.zeros(nl, _abi.KEYPOINT_DTYPE)
+    kl["x"] = (kc["x"][src] + rng.normal(0, 1.5, nl)).astype(np.float32)
+    kl["y"] = (kc["y"][src] + rng.normal(0, 1.5, nl)).astype(np.float32)
+    kl["octave"] = np.clip(kc["octave"][src] + rng.integers(-1, 2, nl), 0, 2)
+    kl["angle"] = np.where(rng.random(nl) < 0.8, kc["angle"][src] + rng.normal(0, 3, nl),
+                           rng.uniform(0, 360, nl)).astype(np.float32) % np.float32(360)
+    dl = rng.integers(0, 256, (nl, 32), dtype=np.uint8)
+    fx, fy, cx, cy, mbf = 500.0, 500.0, 320.0, 240.0, 40.0
+    cam = np.array([fx, fy, cx, cy, mbf, mbf / fx], np.float32)
+    z = rng.uniform(2.0, 4.0, nl).astype(np.float32)
+    xyz = np.stack([(kl["x"] - cx) * z / fx, (kl["y"] - cy) * z / fy, z], 1).astype(np.float32)
+    md = dc[src].copy()
+    md[np.arange(nl), rng.integers(0, 32, nl)] ^= 0x07
+    md[rng.random(nl) < 0.2] = dc[rng.integers(0, n)]          # near-ties
+    has = rng.choice([0, 1, 2], nl, p=[0.15, 0.45, 0.4]).astype(np.int32)
+    outl = (rng.random(nl) < 0.05).astype(np.uint8)
+    Tl = np.eye(4, dtype=np.float32)[:3].copy()
+    Tc = np.eye(4, dtype=np.float32)[:3].copy()
+    Tc[0, 3], Tc[2, 3] = np.float32(0.004), np.float32(0.02)
+    sf = (np.float32(1.2) ** np.arange(8)).astype(np.float32)
+    init = np.full(n, -1, np.int32)
+    init[::11] = -2
+    init[5::13] = -3
+    cur = O.FrameView(kc, dc, W, H, uright=urc)
+    last = O.FrameView(kl, dl, W, H)
+    retaken = 0
+    for th, mono in ((7.0, False), (15.0, True)):
+        n_c, mp_c = O.search_by_projection_ff(cur, Tc, last, Tl, has, outl, xyz, md, sf, O.Camera(*map(float, cam)),
+                                              th, mono, True, init)
+        # ---- literal restatement: slots hold ("pre", has_obs) or ("last", i)
+        slot = [None if v == -1 else ("pre", v == -2) for v in init]
+        obs = lambda s: s[1] if s[0] == "pre" else has[s[1]] == 1
+        f32 = np.float32
+        twc = [f32(-sum(float(Tc[r, c]) * float(Tc[r, 3]) for r in range(3))) for c in range(3)]
+        tlc2 = f32(sum(float(Tl[2, c]) * float(twc[c]) for c in range(3)) + float(Tl[2, 3]))
+        bF = tlc2 > cam[5] and not mono
+        bB = -tlc2 > cam[5] and not mono
+        hist = [[] for _ in range(30)]
+        nm = 0
+        pop = lambda a: bin(int(a)).count("1")
+        for i in range(nl):
+            if not has[i] or outl[i]:
+                continue
+            x3 = [f32(sum(float(Tc[r, c]) * float(xyz[i, c]) for c in range(3)) + float(Tc[r, 3])) for r in range(3)]
+            invz = f32(1.0 / float(x3[2]))
+            if invz < 0:
+                continue
+            u = f32(f32(f32(cam[0] * x3[0]) * invz) + cam[2])
+            v = f32(f32(f32(cam[1] * x3[1]) * invz) + cam[3])
+            if u < 0 or u > W or v < 0 or v > H:
+                continue
+            lo = int(kl["octave"][i])
+            rad = f32(f32(th) * sf[lo])
+            if bF:
+                cand = _py_features_in_area(kc["x"], kc["y"], kc["octave"], W, H, u, v, rad, lo, -1)
+            elif bB:
+                cand = _py_features_in_area(kc["x"], kc["y"], kc["octave"], W, H, u, v, rad, 0, lo)
+            else:
+                cand = _py_features_in_area(kc["x"], kc["y"], kc["octave"], W, H, u, v, rad, lo - 1, lo + 1)
+            if not cand:
+                continue
+            bd, bi = 256, -1
+            for i2 in cand:
+                if slot[i2] is not None and obs(slot[i2]):
+                    continue
+                if urc[i2] > 0:
+                    urp = f32(u - f32(cam[4] * invz))
+                    if abs(f32(urp - urc[i2])) > rad:
+                        continue
+                dist = sum(pop(a ^ b) for a, b in zip(md[i], dc[i2]))
+                if dist < bd:
+                    bd, bi = dist, i2
+            if bd <= 100:
+                slot[bi] = ("last", i)
+                nm += 1
+                rot = f32(kl["angle"][i] - kc["angle"][bi])
+                if rot < 0:
+                    rot = f32(rot + f32(360))
+                b = int(np.round(f32(rot * f32(f32(30) / f32(360)))))
+                hist[0 if b == 30 else b].append(bi)
+        sizes = [len(h) for h in hist]
+        m1 = m2 = m3 = 0
+        i1 = i2_ = i3 = -1
+        for b, c in enumerate(sizes):
+            if c > m1:
+                m3, m2, m1, i3, i2_, i1 = m2, m1, c, i2_, i1, b
+            elif c > m2:
+                m3, m2, i3, i2_ = m2, c, i2_, b
+            elif c > m3:
+                m3, i3 = c, b
+        if f32(m2) < f32(0.1) * f32(m1):
+            i2_ = i3 = -1
+        elif f32(m3) < f32(0.1) * f32(m1):
+            i3 = -1
+        for b in range(30):
+            if b not in (i1, i2_, i3):
+                for j in hist[b]:
+                    slot[j] = None
+                    nm -= 1
+        want = np.array([-1 if s is None else (s[1] if s[0] == "last" else (-2 if s[1] else -3)) for s in slot], np.int32)
+        assert nm == n_c and np.array_equal(want, mp_c), th
+        assert nm > 20
+        listed = [j for h in hist for j in h]
+        retaken += len(listed) - len(set(listed))     # slots taken over from a point without observations
+    assert retaken > 0
+
+
 def test_compute_stereo_matches_oracle_vs_python():
     """The C oracle of Frame::ComputeStereoMatches against a literal Python restatement of
     R/src/Frame.cpp:551-770 (with mb = 0 at call time) on a synthetic stereo pair."""
