@@ -157,6 +157,8 @@ typedef struct {
     double* eprod;    /* [n_edges][72] per-edge quadratic-form terms of the parallel buildSystem */
     double* dbl;      /* [M][3] Dinv b_l of the parallel Schur */
     int *pose_a_start, *pose_a;   /* per free pose index: its pt_edges positions, landmark-ascending */
+    int *pt_k_start, *pt_k;       /* per point index / free pose index: its act positions k, ascending */
+    int *po_k_start, *po_k;       /* (the parallel merge of buildSystem keeps the serial edge order) */
 } lba_ctx;
 
 #define OMP_IF(c) if ((c)->threads > 1) num_threads((c)->threads)
@@ -343,6 +345,28 @@ static void init_optimization(lba_ctx* c, int level)
             if (i1 >= 0) c->pose_a[fill[i1]++] = a;
         }
     }
+    if (c->threads > 1) {   /* per point / per free pose: act positions in ascending order */
+        memset(c->pt_k_start, 0, sizeof(int) * (c->M + 1));
+        memset(c->po_k_start, 0, sizeof(int) * (c->P + 1));
+        for (int k = 0; k < c->n_act; k++) {
+            const int e = c->act_edges[k];
+            c->pt_k_start[c->point_idx[p->edge_point[e]] + 1]++;
+            const int pi = c->pose_idx[p->edge_pose[e]];
+            if (pi >= 0) c->po_k_start[pi + 1]++;
+        }
+        for (int i = 0; i < c->M; i++) c->pt_k_start[i + 1] += c->pt_k_start[i];
+        for (int i = 0; i < c->P; i++) c->po_k_start[i + 1] += c->po_k_start[i];
+        int* f2 = (int*)malloc(sizeof(int) * (c->M + c->P + 2));
+        memcpy(f2, c->pt_k_start, sizeof(int) * (c->M + 1));
+        memcpy(f2 + c->M + 1, c->po_k_start, sizeof(int) * (c->P + 1));
+        for (int k = 0; k < c->n_act; k++) {
+            const int e = c->act_edges[k];
+            c->pt_k[f2[c->point_idx[p->edge_point[e]]]++] = k;
+            const int pi = c->pose_idx[p->edge_pose[e]];
+            if (pi >= 0) c->po_k[f2[c->M + 1 + pi]++] = k;
+        }
+        free(f2);
+    }
     free(fill);
     free(order);
     free(pose_act);
@@ -398,21 +422,31 @@ static void build_system_omp(lba_ctx* c)
             }
         }
     }
-    for (int k = 0; k < c->n_act; k++) {
-        const int e = c->act_edges[k];
-        const int D = p->edge_stereo[e] ? 3 : 2;
-        const double* t = c->eprod + 72 * (size_t)k;
-        const int li = c->point_idx[p->edge_point[e]];
-        const int pi = c->pose_idx[p->edge_pose[e]];
+    /* the block sums: every landmark block over its edges in act order (in parallel over
+     * landmarks), every pose block entry likewise (in parallel over pose x entry) — each
+     * accumulator sees the serial loop's sequence of additions */
+#pragma omp parallel for schedule(static) OMP_IF(c)
+    for (int li = 0; li < c->M; li++) {
         double* hl = c->Hll + 9 * li;
         double* bl = c->bl + 3 * li;
-        for (int i = 0; i < 3; i++) {
-            for (int r = 0; r < D; r++) bl[i] += t[9 + i * 3 + r];
-            for (int j = 0; j < 3; j++) hl[i * 3 + j] += t[i * 3 + j];
+        for (int a = c->pt_k_start[li]; a < c->pt_k_start[li + 1]; a++) {
+            const int k = c->pt_k[a];
+            const int D = p->edge_stereo[c->act_edges[k]] ? 3 : 2;
+            const double* t = c->eprod + 72 * (size_t)k;
+            for (int i = 0; i < 3; i++) {
+                for (int r = 0; r < D; r++) bl[i] += t[9 + i * 3 + r];
+                for (int j = 0; j < 3; j++) hl[i * 3 + j] += t[i * 3 + j];
+            }
         }
-        if (pi >= 0) {
-            double* hp = c->Hpp + 36 * pi;
-            double* bp = c->bp + 6 * pi;
+    }
+#pragma omp parallel for schedule(dynamic, 1) OMP_IF(c)
+    for (int pi = 0; pi < c->P; pi++) {
+        double* hp = c->Hpp + 36 * pi;
+        double* bp = c->bp + 6 * pi;
+        for (int a = c->po_k_start[pi]; a < c->po_k_start[pi + 1]; a++) {
+            const int k = c->po_k[a];
+            const int D = p->edge_stereo[c->act_edges[k]] ? 3 : 2;
+            const double* t = c->eprod + 72 * (size_t)k;
             for (int i = 0; i < 6; i++) {
                 for (int r = 0; r < D; r++) bp[i] += t[54 + i * 3 + r];
                 for (int j = 0; j < 6; j++) hp[i * 6 + j] += t[18 + i * 6 + j];
@@ -538,8 +572,16 @@ static int schur_solve(lba_ctx* c, double lambda)
             const double* b = c->bl + 3 * l;
             for (int i = 0; i < 3; i++) c->dbl[3 * l + i] = Di[i * 3] * b[0] + Di[i * 3 + 1] * b[1] + Di[i * 3 + 2] * b[2];
         }
+        /* work items = pose row x a range of block columns (the row's landmarks are walked by
+         * every item of the row, each forming the products of its own columns only), so a
+         * window with fewer rows than threads still spreads; coef by the first item of a row */
+        const int nq = c->P >= 4 * c->threads ? 1 : (4 * c->threads + c->P - 1) / (c->P > 0 ? c->P : 1);
 #pragma omp parallel for schedule(dynamic, 1) OMP_IF(c)
-        for (int row = 0; row < c->P; row++) {
+        for (int item = 0; item < c->P * nq; item++) {
+            const int row = item / nq, qc = item % nq;
+            const int col0 = row + (int)((long long)(c->P - row) * qc / nq);
+            const int col1 = row + (int)((long long)(c->P - row) * (qc + 1) / nq);
+            if (col0 >= col1 && qc > 0) continue;
             for (int ka = c->pose_a_start[row]; ka < c->pose_a_start[row + 1]; ka++) {
                 const int a = c->pose_a[ka];
                 const int l = c->point_idx[p->edge_point[c->pt_edges[a]]];
@@ -554,12 +596,13 @@ static int schur_solve(lba_ctx* c, double lambda)
                     for (int r = 0; r < 6; r++)
                         for (int q = 0; q < 3; q++)
                             BD[r * 3 + q] = Bi[r * 3] * Di[q] + Bi[r * 3 + 1] * Di[3 + q] + Bi[r * 3 + 2] * Di[6 + q];
-                    for (int r = 0; r < 6; r++)
-                        coef[6 * i1 + r] += Bi[r * 3] * db[0] + Bi[r * 3 + 1] * db[1] + Bi[r * 3 + 2] * db[2];
+                    if (qc == 0)
+                        for (int r = 0; r < 6; r++)
+                            coef[6 * i1 + r] += Bi[r * 3] * db[0] + Bi[r * 3 + 1] * db[1] + Bi[r * 3 + 2] * db[2];
                     for (int bb = a; bb < s1; bb++) {
                         const int e2 = c->pt_edges[bb];
                         const int i2 = c->pose_idx[p->edge_pose[e2]];
-                        if (i2 < 0) continue;
+                        if (i2 < col0 || i2 >= col1) continue;   /* (fixed poses: -1) */
                         const double* Bj = c->Hpl + 18 * e2;
                         for (int r = 0; r < 6; r++)
                             for (int q = 0; q < 6; q++) {
@@ -620,11 +663,20 @@ static int schur_solve(lba_ctx* c, double lambda)
      * GPU factorisation (k_ldlt_solve) follows element for element. */
     int ok = 1;
     double* d = (double*)malloc(sizeof(double) * (np + 1));
-    for (int j = 0; j < np && ok; j++) {
-        double dj = S[j * np + j];
-        for (int k = 0; k < j; k++) dj = fma(-S[k * np + j], S[j * np + k], dj);
-        if (dj == 0.0 || !isfinite(dj)) { ok = 0; break; }
-        d[j] = dj;
+    /* (OpenMP variant, large systems: the rows i > j of column j in parallel — each element is
+     * the same operation sequence, so the factor is bitwise the serial one) */
+#pragma omp parallel if (c->threads > 1 && np >= 96) num_threads(c->threads > 1 ? c->threads : 1)
+    for (int j = 0; j < np; j++) {
+#pragma omp single
+        {
+            double dj = S[j * np + j];
+            for (int k = 0; k < j; k++) dj = fma(-S[k * np + j], S[j * np + k], dj);
+            if (ok && (dj == 0.0 || !isfinite(dj))) ok = 0;
+            d[j] = dj;
+        }
+        if (!ok) continue;   /* (every thread reads ok after the single's barrier) */
+        const double dj = d[j];
+#pragma omp for schedule(static)
         for (int i = j + 1; i < np; i++) {
             double v = S[i * np + j];
             for (int k = 0; k < j; k++) v = fma(-S[k * np + i], S[j * np + k], v);
@@ -875,6 +927,10 @@ static int lba_run(const lba_problem_t* p, const lba_options_t* o, const volatil
         c.dbl = (double*)malloc(sizeof(double) * 3 * (NM + 1));
         c.pose_a_start = (int*)malloc(sizeof(int) * (NP + 2));
         c.pose_a = (int*)malloc(sizeof(int) * (NE + 1));
+        c.pt_k_start = (int*)malloc(sizeof(int) * (NM + 2));
+        c.pt_k = (int*)malloc(sizeof(int) * (NE + 1));
+        c.po_k_start = (int*)malloc(sizeof(int) * (NP + 2));
+        c.po_k = (int*)malloc(sizeof(int) * (NE + 1));
     }
     memcpy(c.pq, p->pose_q, sizeof(double) * 4 * NP);
     memcpy(c.pt, p->pose_t, sizeof(double) * 3 * NP);
@@ -934,6 +990,7 @@ done:
     free(c.Hpp); free(c.S); free(c.bp); free(c.Hll); free(c.bl); free(c.Hpl); free(c.x); free(c.Dinv);
     free(c.pt_edge_start); free(c.pt_edges); free(c.eprod); free(c.dbl);
     free(c.pose_a_start); free(c.pose_a);
+    free(c.pt_k_start); free(c.pt_k); free(c.po_k_start); free(c.po_k);
     (void)cmp_i64_idx_base;
     return status;
 }

@@ -106,6 +106,9 @@ struct LbaDev {
     double *Hll_e, *Hpp_e, *Hpl_e, *bl_e, *bp_e, *echi;
     // reduced per vertex
     double *Hll, *bl, *Dinv, *db, *Hpp, *bp;   // db = Dinv b_l
+    double* Ae;                 // [nact][18] Hpl_e D^-1 of the edge's landmark (per trial)
+    const int32_t* pairs;       // pose-pair blocks of S with shared landmarks, (bi << 16 | bj), bi <= bj
+    const int32_t* npairs;      // their count
     double *S, *bs, *x;         // x: [6P + 3M]
     double* red;                // reduction scratch
     double *partChi, *partScale, *partMax;   // per-workgroup partials (single-process LM kernels)
@@ -714,8 +717,8 @@ __global__ __launch_bounds__(256) void k_vertex_reduce(LbaDev d) {
     if (tid == 0) d.partMax[blockIdx.x] = fmax(fmax(wmax[0], wmax[1]), fmax(wmax[2], wmax[3]));
 }
 
-// D^-1 = (Hll + lambda I)^-1 (Eigen's 3x3 cofactor inverse) and D^-1 b_l of landmark l.
-__device__ __forceinline__ void dinv_store(const LbaDev& d, int l, double m[9], const double blv[3], double lambda) {
+// D^-1 = (Hll + lambda I)^-1 (Eigen's 3x3 cofactor inverse) of a landmark block m (row-major)
+__device__ __forceinline__ void dinv_of(double m[9], double lambda, double Di[9]) {
     m[0] += lambda; m[4] += lambda; m[8] += lambda;
     double c[9];
     for (int i = 0; i < 3; i++)
@@ -725,11 +728,39 @@ __device__ __forceinline__ void dinv_store(const LbaDev& d, int l, double m[9], 
         }
     const double det = c[0] * m[0] + c[3] * m[3] + c[6] * m[6];
     const double invdet = 1.0 / det;
-    double Di[9];
     for (int i = 0; i < 3; i++)
         for (int j = 0; j < 3; j++) Di[j * 3 + i] = c[i * 3 + j] * invdet;
+}
+// D^-1 and D^-1 b_l of landmark l
+__device__ __forceinline__ void dinv_store(const LbaDev& d, int l, const double Di[9], const double blv[3]) {
     for (int i = 0; i < 9; i++) d.Dinv[9 * (size_t)l + i] = Di[i];
     for (int i = 0; i < 3; i++) d.db[3 * (size_t)l + i] = Di[i * 3] * blv[0] + Di[i * 3 + 1] * blv[1] + Di[i * 3 + 2] * blv[2];
+}
+// Hpl_e D^-1 (the product of G/core/block_solver.hpp:419) of every free-pose edge of landmark l,
+// edges a0, a0 + stride, ... of its list: formed once per edge and trial here, where D^-1 is in
+// registers, instead of once per pose pair in k_schur_pairs
+__device__ __forceinline__ void hpl_dinv_edges(const LbaDev& d, int l, const double Di[9], int sub, int stride) {
+    const int a1 = d.ptStart[l + 1];
+    for (int a = d.ptStart[l] + sub; a < a1; a += stride) {
+        const int k = d.ptAct[a];
+        if (d.actPi[k] < 0) continue;   // fixed pose: no Hpl block
+        const double2* B = reinterpret_cast<const double2*>(d.Hpl_e + 18 * (size_t)k);
+        double w[18];
+#pragma unroll
+        for (int h = 0; h < 9; h++) {
+            const double2 x = B[h];
+            w[2 * h] = x.x; w[2 * h + 1] = x.y;
+        }
+        double u[18];
+#pragma unroll
+        for (int r = 0; r < 6; r++)
+#pragma unroll
+            for (int q = 0; q < 3; q++)
+                u[r * 3 + q] = w[r * 3] * Di[q] + w[r * 3 + 1] * Di[3 + q] + w[r * 3 + 2] * Di[6 + q];
+        double2* U = reinterpret_cast<double2*>(d.Ae + 18 * (size_t)k);
+#pragma unroll
+        for (int h = 0; h < 9; h++) U[h] = make_double2(u[2 * h], u[2 * h + 1]);
+    }
 }
 
 // Per landmark with lambda (G/core/block_solver.hpp:380-398): D^-1 = (Hll + lambda I)^-1
@@ -768,7 +799,10 @@ __global__ __launch_bounds__(64) void k_point_schur(LbaDev d, int fuse, int nChi
         lambda = d.lm->lambda;
     }
     if (l >= d.M) return;
-    dinv_store(d, l, m, blv, lambda);
+    double Di[9];
+    dinv_of(m, lambda, Di);
+    dinv_store(d, l, Di, blv);
+    hpl_dinv_edges(d, l, Di, 0, 1);
 }
 
 // Landmarks of the fused slots after an optimize()'s first (slots 2.., where the iteration
@@ -819,17 +853,22 @@ __global__ __launch_bounds__(256) void k_vertex_schur(LbaDev d, int nChi) {
     }
     double h[6], b[3];
     if (ph0 == 0) landmark_reduce(d, l, sub, h, b, lf);
-    if (l >= d.M || sub != 0) return;
+    if (l >= d.M) return;
+    // every lane of the landmark's group forms D^-1 (the reduced sums are in all four), lane 0
+    // stores it, and the four lanes split the landmark's Hpl D^-1 products
     double m[9], blv[3];
     if (ph0 == 0) {
-        landmark_store(d, l, h, b);
+        if (sub == 0) landmark_store(d, l, h, b);
         m[0] = h[0]; m[1] = h[1]; m[2] = h[2]; m[3] = h[1]; m[4] = h[3]; m[5] = h[4]; m[6] = h[2]; m[7] = h[4]; m[8] = h[5];
         blv[0] = b[0]; blv[1] = b[1]; blv[2] = b[2];
     } else {
         for (int i = 0; i < 9; i++) m[i] = d.Hll[9 * (size_t)l + i];
         for (int i = 0; i < 3; i++) blv[i] = d.bl[3 * (size_t)l + i];
     }
-    dinv_store(d, l, m, blv, lambda);
+    double Di[9];
+    dinv_of(m, lambda, Di);
+    if (sub == 0) dinv_store(d, l, Di, blv);
+    hpl_dinv_edges(d, l, Di, sub, kLanesPerPt);
 }
 
 // Reduced camera system (G/core/block_solver.hpp:408-440): one workgroup per pose-pair block
@@ -844,13 +883,13 @@ __global__ __launch_bounds__(256) void k_vertex_schur(LbaDev d, int nChi) {
 constexpr int kSpT = 256;
 constexpr int kSpList = 4096;   // pose j's landmark list held in LDS up to this length
 __global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag) {
+    if ((int)blockIdx.x >= *d.npairs) return;   // blocks with no shared landmark stay 0 (zeroed per solve)
+    const int pr = d.pairs[blockIdx.x];
     const int phase = d.lm->phase;   // loaded with the pair's CSR ranges (one round trip)
     __shared__ double part[42][kSpT + 1];
     __shared__ int32_t listJ[kSpList];
     const int tid = threadIdx.x;
-    int bi = 0, rem = blockIdx.x;
-    while (rem >= d.P - bi) { rem -= d.P - bi; bi++; }
-    const int bj = bi + rem;
+    const int bi = pr >> 16, bj = pr & 0xFFFF;
     const bool diag = bi == bj;
     const int a0 = d.poStart[bi], a1 = d.poStart[bi + 1], b0 = d.poStart[bj], nb = d.poStart[bj + 1] - b0;
     if (phase != 1) return;   // lm_off(d.lm, 1)
@@ -881,22 +920,17 @@ __global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag) {
             if (lo == nb || Lj[lo] != l) continue;
             e2 = d.poAct[b0 + lo];
         }
-        const double2* Bi = reinterpret_cast<const double2*>(d.Hpl_e + 18 * (size_t)e1);
+        // A_e1 = Hpl_e1 D^-1 (formed per edge by the landmark kernel) against Hpl_e2
+        const double2* Ui = reinterpret_cast<const double2*>(d.Ae + 18 * (size_t)e1);
         const double2* Bj = reinterpret_cast<const double2*>(d.Hpl_e + 18 * (size_t)e2);
-        const double* Dl = d.Dinv + 9 * (size_t)l;
-        double w[18], v[18], Di[9], u[18];
+        double v[18], u[18];
 #pragma unroll
         for (int h = 0; h < 9; h++) {
-            const double2 x = Bi[h], y = Bj[h];
-            w[2 * h] = x.x; w[2 * h + 1] = x.y;
+            const double2 x = Ui[h], y = Bj[h];
+            u[2 * h] = x.x; u[2 * h + 1] = x.y;
             v[2 * h] = y.x; v[2 * h + 1] = y.y;
-            Di[h] = Dl[h];
         }
-#pragma unroll
-        for (int r = 0; r < 6; r++)   // Hpl D^-1 (the product of block_solver.hpp:419)
-#pragma unroll
-            for (int q = 0; q < 3; q++)
-                u[r * 3 + q] = w[r * 3] * Di[q] + w[r * 3 + 1] * Di[3 + q] + w[r * 3 + 2] * Di[6 + q];
+        const double* w = v;   // diagonal blocks: e2 == e1, Hpl_e1 for b_s
 #pragma unroll
         for (int r = 0; r < 6; r++)
 #pragma unroll
@@ -942,6 +976,57 @@ __global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag) {
             d.bs[6 * bi + v - 36] = (addDiag ? d.bp[6 * bi + v - 36] : 0.0) - sum;
         }
     }
+}
+
+// The pose-pair blocks of S that receive a Schur term (G/core/block_solver.hpp:192-207 builds
+// the same set as the sparsity pattern of the reduced matrix): per landmark, every pair of its
+// free-pose edges marks block (i, j), i <= j, row-major upper-triangle index; all == 1 marks every
+// block (with a communicator a block may get its terms on another rank only).
+__global__ __launch_bounds__(256) void k_pair_mark(LbaDev d, int32_t* __restrict__ flag, int all) {
+    const int P = d.P;
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (all) {
+        if (t < P * (P + 1) / 2) flag[t] = 1;
+        return;
+    }
+    if (t < P) flag[t * P - t * (t - 1) / 2] = 1;   // every diagonal block (Hpp + lambda I)
+    if (t >= d.M) return;
+    const int a0 = d.ptStart[t], a1 = d.ptStart[t + 1];
+    for (int a = a0; a < a1; a++) {
+        const int pa = d.actPi[d.ptAct[a]];
+        if (pa < 0) continue;
+        for (int b = a; b < a1; b++) {
+            const int pb = d.actPi[d.ptAct[b]];
+            if (pb < 0) continue;
+            const int i = min(pa, pb), j = max(pa, pb);
+            flag[i * P - i * (i - 1) / 2 + (j - i)] = 1;
+        }
+    }
+}
+// the marked blocks compacted in index order (one workgroup): pairs[k] = bi << 16 | bj, *npairs
+__global__ __launch_bounds__(1024) void k_pair_list(const int32_t* __restrict__ flag, int P, int32_t* __restrict__ pairs,
+                                                    int32_t* __restrict__ npairs) {
+    __shared__ int wsum[16];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int N = P * (P + 1) / 2;
+    const int chunk = (N + 1023) / 1024, c0 = min(tid * chunk, N), c1 = min(c0 + chunk, N);
+    int loc = 0;
+    for (int i = c0; i < c1; i++) loc += flag[i] ? 1 : 0;
+    const int incl = wave_incl_scan_i32(loc);
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int run = incl - loc;
+    for (int w = 0; w < wave; w++) run += wsum[w];
+    if (c0 < c1) {
+        int bi = 0, rem = c0;   // index -> (bi, bj) of the first entry, then walk
+        while (rem >= P - bi) { rem -= P - bi; bi++; }
+        int bj = bi + rem;
+        for (int i = c0; i < c1; i++) {
+            if (flag[i]) pairs[run++] = (bi << 16) | bj;
+            if (++bj == P) { bi++; bj = bi; }
+        }
+    }
+    if (tid == 1023) *npairs = run;
 }
 
 // Broadcast of lane `src` (a compile-time constant at every call site) through two
@@ -1191,7 +1276,10 @@ __device__ __forceinline__ bool ldlt_panel_grp(double* __restrict__ A, int ld, i
     return ok;
 }
 // groups for the panel at jb: the 16 diagonal rows plus 48 rows below per group
-__device__ __forceinline__ int panel_groups(int np, int jb) { return max(1, (np - jb - kNB + 47) / 48); }
+__host__ __device__ __forceinline__ int panel_groups(int np, int jb) {
+    const int g = (np - jb - kNB + 47) / 48;
+    return g > 1 ? g : 1;
+}
 
 // rows of a panel factored in registers: all of them with the LDS image (ldlt_panel_grp), 192
 // (three per lane of wave 0) with the global image, the rest one per thread (step 1b)
@@ -1555,6 +1643,224 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_solve(const double* __restrict__
 #ifdef ORB_TIMING
     if (lane == 0) printf("ldlt n %d: stage %lld (own %lld) panel %lld rows %lld trailing %lld solve %lld | panels %lld %lld %lld %lld %lld %lld %lld %lld | bar %lld %lld\n", n, t_f0 - t_l0, t_sa - t_l0, tDiag, tRows, tTrail, clock64() - t_s0, tp[0], tp[1], tp[2], tp[3], tp[4], tp[5], tp[6], tp[7], tpb[0], tpb[1]);
 #endif
+}
+
+
+// ------------------------------------------------------------------ multi-workgroup reduced solve
+// Reduced systems beyond the LDS image (np > 128, more than 21 free keyframes: LocalMapping's
+// window is every covisible keyframe, unbounded, R/src/Optimizer.cpp:569-625).  The same blocked
+// right-looking LDL^T in 16-column panels as k_ldlt_solve, spread over the chip, two launches
+// per panel (a dependent kernel boundary, ~1.5 us, is the cheapest cross-XCD synchronisation):
+//   k_ldlt_mw_panel  the panel's rows split over waves, 48 below the diagonal block per wave; every
+//                    wave also holds the 16 diagonal rows and computes the pivots, 1/d and the
+//                    diagonal block's W itself (ldlt_panel_grp's scheme), so no wave waits on another
+//   k_ldlt_mw_trail  the trailing lower triangle, one 16 x 16 tile per wave, four v_mfma_f64_16x16x4
+// then k_ldlt_mw_back (one workgroup): y /= d and the backward substitution with L^T (and, in fused
+// slots, the free poses' update, as k_ldlt_solve's tail).  The work image is np x np (ld = np): W in
+// the upper triangle, L in the lower; a diagonal block's L rows go to Ldg[np][16] and its rows'
+// finished forward substitution to yfin (the diagonal rows are read by every wave of the panel
+// while it runs, so nothing writes them in place).
+struct MwLdl {
+    double *A, *rdg, *y, *yfin, *Ldg, *sink;
+    int* fail;
+    int n, np;
+};
+constexpr int kMwWaves = 4;   // waves per workgroup of the panel / trailing kernels
+
+__device__ __forceinline__ void tri_index(int t, int& ti, int& tk) {   // t -> (ti, tk), tk <= ti, row-major
+    ti = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
+    while ((ti + 1) * (ti + 2) / 2 <= t) ti++;
+    while (ti * (ti + 1) / 2 > t) ti--;
+    tk = t - ti * (ti + 1) / 2;
+}
+
+// S (n x n) -> the padded image (identity padding), y = b, the padding pivots' 1/d = 1
+__global__ __launch_bounds__(256) void k_ldlt_mw_stage(MwLdl m, const double* __restrict__ S, const double* __restrict__ b,
+                                                      const LmState* st) {
+    if (lm_off(st, 1)) return;
+    const int np = m.np, n = m.n;
+    const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (t == 0) *m.fail = 0;
+    if (t < (size_t)np * np) {
+        const int i = (int)(t / np), j = (int)(t % np);
+        m.A[t] = (i < n && j < n) ? S[(size_t)i * n + j] : (i == j ? 1.0 : 0.0);
+    }
+    if (t < (size_t)np) {
+        m.y[t] = (int)t < n ? b[t] : 0.0;
+        if ((int)t >= n) m.rdg[t] = 1.0;
+    }
+}
+
+template <bool kTail>
+__global__ __launch_bounds__(64 * kMwWaves) void k_ldlt_mw_panel(MwLdl m, int jb, const LmState* st) {
+    if (lm_off(st, 1)) return;
+    if (__builtin_amdgcn_readfirstlane(*m.fail)) return;
+    __shared__ double wscS[kMwWaves][kNB];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int g = __builtin_amdgcn_readfirstlane((int)blockIdx.x * kMwWaves + wv);
+    const int np = m.np, ld = np, nr = m.n;
+    if (g > 0 && jb + kNB + 48 * g >= np) return;   // no rows below for this group (group 0 always runs)
+    double* const A = m.A;
+    double* const wsc = wscS[wv];
+    const int r = lane < kNB ? jb + lane : jb + kNB + 48 * g + (lane - kNB);
+    const bool live = r < np, inplace = live && lane >= kNB;
+    const int rc = min(r, np - 1);
+    double P[kNB];
+    double Y = m.y[rc];
+#pragma unroll
+    for (int c = 0; c < kNB; c++) P[c] = A[(size_t)rc * ld + jb + c];
+    double* const Lrow = inplace ? A + (size_t)r * ld + jb : m.sink + (size_t)(lane & (kNB - 1)) * ld;
+    double* const Wcol = inplace ? A + (size_t)jb * ld + r : m.sink + lane;
+    double* const wst = lane < kNB ? wsc + lane : m.sink + lane;
+    double dj = shfl_d(P[0], 0);
+    bool ok = dj != 0.0 && isfinite(dj);
+    double rd = rcp_nr(dj);
+    double myrd = 1.0;
+    double Wd[kNB], lprev = 0.0;
+#pragma unroll
+    for (int c = 0; c < kNB; c++) {
+        const int j = jb + c;
+        if (kTail && j >= nr) break;
+        const double w = P[c];
+        double djn = 1.0, rn = 1.0, w1 = 0.0, w2 = 0.0;
+        if (c + 1 < kNB) {
+            w1 = shfl_d(w, c + 1);
+            const double a1 = shfl_d(P[c + 1], c + 1);
+            djn = __builtin_fma(-(w1 * w1), rd, a1);
+            rn = __builtin_amdgcn_rcp(djn);
+        }
+        if (c + 2 < kNB) w2 = shfl_d(w, c + 2);
+        const double yj = shfl_d(Y, c);
+        __builtin_amdgcn_sched_barrier(0);
+        if (c >= 1) {
+#pragma unroll
+            for (int k = c + 2; k < kNB; k++) P[k] = __builtin_fma(-lprev, Wd[k], P[k]);
+        }
+        const double l = w * rd;
+        P[c] = l;
+        Wcol[(size_t)c * ld] = w;
+        Lrow[c] = l;
+        myrd = lane == c ? rd : myrd;
+        *wst = w;
+#pragma unroll
+        for (int k = c + 3; k < kNB; k++) Wd[k] = wsc[k];
+        if (c + 1 < kNB) P[c + 1] = __builtin_fma(-l, w1, P[c + 1]);
+        if (c + 2 < kNB) P[c + 2] = __builtin_fma(-l, w2, P[c + 2]);
+        if (r > j) Y = __builtin_fma(-l, yj, Y);
+        lprev = l;
+        if (c + 1 < kNB) {
+            const double e0 = __builtin_fma(-djn, rn, 1.0);
+            const double r1 = __builtin_fma(rn, e0, rn);
+            const double e1 = __builtin_fma(-djn, r1, 1.0);
+            ok = ok && djn != 0.0 && isfinite(djn);
+            dj = djn;
+            rd = __builtin_fma(r1, e1, r1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (g == 0 && lane < kNB) {   // the diagonal block: L rows, 1/d, finished y
+#pragma unroll
+        for (int c = 0; c < kNB; c++) m.Ldg[(size_t)r * kNB + c] = P[c];
+        m.rdg[r] = myrd;
+        m.yfin[r] = Y;
+        if (lane == 0 && !ok) *m.fail = 1;
+    }
+    if (inplace) m.y[r] = Y;
+}
+
+// trailing update after panel kb: tiles (I, K), I >= K > kb, one per wave
+__global__ __launch_bounds__(64 * kMwWaves) void k_ldlt_mw_trail(MwLdl m, int kb, const LmState* st) {
+    if (lm_off(st, 1)) return;
+    if (__builtin_amdgcn_readfirstlane(*m.fail)) return;
+    const int lane = threadIdx.x & 63;
+    const int T = m.np / kNB, mm = T - kb - 1;
+    const int t = __builtin_amdgcn_readfirstlane((int)blockIdx.x * kMwWaves + (int)(threadIdx.x >> 6));
+    if (t >= mm * (mm + 1) / 2) return;
+    int ti, tk;
+    tri_index(t, ti, tk);
+    const int I0 = (kb + 1 + ti) * kNB, K0 = (kb + 1 + tk) * kNB, jb = kb * kNB, ld = m.np;
+    const double* __restrict__ A = m.A;
+    const int li = lane & 15, lk = lane >> 4;
+    double a[kNB / 4], bb[kNB / 4];
+    dbl4 acc;
+#pragma unroll
+    for (int s = 0; s < kNB / 4; s++) {
+        const int p = jb + 4 * s + lk;
+        a[s] = -A[(size_t)p * ld + I0 + li];        // -W(I0 + li, p)
+        bb[s] = A[(size_t)(K0 + li) * ld + p];      //  L(K0 + li, p)
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) acc[q] = A[(size_t)(I0 + lk + 4 * q) * ld + K0 + li];
+#pragma unroll
+    for (int s = 0; s < kNB / 4; s++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], bb[s], acc, 0, 0, 0);
+#pragma unroll
+    for (int q = 0; q < 4; q++) m.A[(size_t)(I0 + lk + 4 * q) * ld + K0 + li] = acc[q];
+}
+
+// y /= d and x = L^-T y in 16-row blocks from the bottom (wave 0 solves a block's triangle from
+// Ldg by a v_readlane chain, then every thread takes one row above it), y held in LDS; then
+// x out, and in fused slots the free poses' update (pose_tail) on wave 0.
+constexpr int kMwBackT = 1024;
+__global__ __launch_bounds__(kMwBackT) void k_ldlt_mw_back(MwLdl m, double* __restrict__ x, int* __restrict__ flags,
+                                                          const LmState* st, PoseTail ptail) {
+    if (lm_off(st, 1)) return;
+    extern __shared__ __attribute__((aligned(16))) double ys[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int np = m.np, n = m.n, ld = np;
+    if (__builtin_amdgcn_readfirstlane(*m.fail)) {
+        // as k_ldlt_solve: the update still runs (with the previous x) and the trial is rejected
+        if (tid == 0) flags[0] = 1;
+        if (ptail.scaleOut && wave == 0) pose_tail(ptail, x, st->lambda, lane);
+        return;
+    }
+    for (int i = tid; i < np; i += kMwBackT) ys[i] = m.yfin[i] * m.rdg[i];
+    __syncthreads();
+    for (int kb = np - kNB; kb >= 0; kb -= kNB) {
+        if (wave == 0) {
+            const int r = lane & 15;
+            double Ab[kNB];
+#pragma unroll
+            for (int c = 0; c < kNB; c++) Ab[c] = m.Ldg[(size_t)(kb + c) * kNB + r];   // L(kb+c, kb+r), used for r < c
+            double xb = ys[kb + r];
+#pragma unroll
+            for (int c = kNB - 1; c > 0; c--) {
+                const double xc = shfl_d(xb, c);
+                xb = r < c ? __builtin_fma(-Ab[c], xc, xb) : xb;
+            }
+            if (lane < kNB) ys[kb + r] = xb;
+        }
+        __syncthreads();
+        if (kb == 0) break;
+        for (int i = tid; i < kb; i += kMwBackT) {
+            double v = ys[i];
+#pragma unroll
+            for (int c = kNB - 1; c >= 0; c--) v = __builtin_fma(-m.A[(size_t)(kb + c) * ld + i], ys[kb + c], v);
+            ys[i] = v;
+        }
+        __syncthreads();
+    }
+    for (int i = tid; i < n; i += kMwBackT) x[i] = ys[i];
+    if (tid == 0) flags[0] = 0;
+    if (ptail.scaleOut && wave == 0) pose_tail(ptail, ys, st->lambda, lane);
+}
+
+// enqueue the multi-workgroup solve of S x = b (n = order of S) on s
+static void enqueue_ldlt_mw(hipStream_t s, const MwLdl& m, const double* S, const double* b, double* x, int* flags,
+                            const LmState* st, const PoseTail& pt) {
+    const int np = m.np, T = np / kNB;
+    const size_t tot = (size_t)np * np;
+    hipLaunchKernelGGL(k_ldlt_mw_stage, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, m, S, b, st);
+    for (int kb = 0; kb < T; kb++) {
+        const int jb = kb * kNB, groups = panel_groups(np, jb);
+        const dim3 gp((unsigned)((groups + kMwWaves - 1) / kMwWaves));
+        if (jb + kNB > m.n) hipLaunchKernelGGL(k_ldlt_mw_panel<true>, gp, dim3(64 * kMwWaves), 0, s, m, jb, st);
+        else hipLaunchKernelGGL(k_ldlt_mw_panel<false>, gp, dim3(64 * kMwWaves), 0, s, m, jb, st);
+        const int mm = T - kb - 1, tiles = mm * (mm + 1) / 2;
+        if (tiles > 0)
+            hipLaunchKernelGGL(k_ldlt_mw_trail, dim3((unsigned)((tiles + kMwWaves - 1) / kMwWaves)), dim3(64 * kMwWaves),
+                               0, s, m, kb, st);
+    }
+    hipLaunchKernelGGL(k_ldlt_mw_back, dim3(1), dim3(kMwBackT), (size_t)np * 8, s, m, x, flags, st, pt);
 }
 
 
@@ -2299,6 +2605,24 @@ static int dalloc(lba_context* c, T** p, size_t n) {
         if (s_) return s_;     \
     } while (0)
 
+// buffers of the multi-workgroup reduced solve for orders up to nMax (k_ldlt_mw_*); the order
+// itself is set per solve.  Used above the LDS image unless ORB_LBA_LDLT_SINGLE selects the
+// one-workgroup global-memory k_ldlt_solve<false> (kept for A/B runs).
+static bool use_mw(int np) { return np > kLdlLdsMaxN && !std::getenv("ORB_LBA_LDLT_SINGLE"); }
+static int mw_alloc(lba_context* c, int nMax, MwLdl* m) {
+    std::memset(m, 0, sizeof(*m));
+    const size_t np = ((size_t)nMax + kNB - 1) & ~(size_t)(kNB - 1);
+    TRY(dalloc(c, &m->A, np * np)); TRY(dalloc(c, &m->rdg, np)); TRY(dalloc(c, &m->y, np));
+    TRY(dalloc(c, &m->yfin, np)); TRY(dalloc(c, &m->Ldg, np * kNB)); TRY(dalloc(c, &m->sink, kNB * np + 64));
+    TRY(dalloc(c, &m->fail, 1));
+    return ORB_OK;
+}
+static MwLdl mw_order(MwLdl m, int n) {
+    m.n = n;
+    m.np = (n + kNB - 1) & ~(kNB - 1);
+    return m;
+}
+
 // Pinned staging slot; `mapped`: host-coherent memory the kernels store into directly (slot 2,
 // the post-optimize read-back)
 static int stage_reserve(lba_context* c, int slot, size_t bytes, bool mapped = false) {
@@ -2477,10 +2801,14 @@ int lba_dense_solve(lba_context* c, const double* S, const double* b, int n, dou
     double *dS, *db, *dx, *dw = nullptr;
     int* df;
     TRY(dalloc(c, &dS, (size_t)n * n)); TRY(dalloc(c, &db, n)); TRY(dalloc(c, &dx, n)); TRY(dalloc(c, &df, 1));
-    if (np > kLdlLdsMaxN) TRY(dalloc(c, &dw, (size_t)np * (np + 1)));
+    MwLdl mw{};
+    if (use_mw(np)) TRY(mw_alloc(c, n, &mw));
+    else if (np > kLdlLdsMaxN) TRY(dalloc(c, &dw, (size_t)np * (np + 1)));
     ORB_HIP_TRY(hipMemcpyAsync(dS, S, 8 * (size_t)n * n, hipMemcpyHostToDevice, s));
     ORB_HIP_TRY(hipMemcpyAsync(db, b, 8 * (size_t)n, hipMemcpyHostToDevice, s));
-    if (np <= kLdlLdsMaxN)
+    if (use_mw(np))
+        enqueue_ldlt_mw(s, mw_order(mw, n), dS, db, dx, df, nullptr, PoseTail{});
+    else if (np <= kLdlLdsMaxN)
         hipLaunchKernelGGL(k_ldlt_solve<true>, dim3(1), dim3(kLdlT), ((size_t)np * (np + 1) + 3 * (size_t)np + 256 + (size_t)kNB * (np + 1) + 64) * 8, s,
                            dS, db, n, nullptr, dx, df, nullptr, PoseTail{});
     else
@@ -2680,6 +3008,7 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
     TRY(dalloc(c, &d.Hpl_e, 18 * (size_t)NE)); TRY(dalloc(c, &d.bl_e, 3 * (size_t)NE));
     TRY(dalloc(c, &d.bp_e, 6 * (size_t)NE));
     TRY(dalloc(c, &d.echi, (size_t)NE + 6 * (size_t)NP + 3 * (size_t)NM));
+    TRY(dalloc(c, &d.Ae, 18 * (size_t)NE));
     TRY(dalloc(c, &d.Hll, 9 * (size_t)NM)); TRY(dalloc(c, &d.bl, 3 * (size_t)NM)); TRY(dalloc(c, &d.Dinv, 9 * (size_t)NM));
     TRY(dalloc(c, &d.db, 3 * (size_t)NM));
     TRY(dalloc(c, &d.Hpp, 36 * (size_t)NP)); TRY(dalloc(c, &d.bp, 6 * (size_t)NP));
@@ -2698,9 +3027,11 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
     double* d_trace = nullptr;
     TRY(dalloc(c, &d_trace, 4 * 64));
     double* d_ldlw = nullptr;   // global image of the padded reduced matrix when it exceeds LDS
+    MwLdl mwBase{};             // or the multi-workgroup solve's buffers
     {
         const size_t npMax = ((size_t)6 * NP + kNB - 1) & ~(size_t)(kNB - 1);
-        if (npMax > (size_t)kLdlLdsMaxN) TRY(dalloc(c, &d_ldlw, npMax * (npMax + 1)));
+        if (use_mw((int)npMax)) TRY(mw_alloc(c, 6 * NP, &mwBase));
+        else if (npMax > (size_t)kLdlLdsMaxN) TRY(dalloc(c, &d_ldlw, npMax * (npMax + 1)));
     }
     double* d_chi2 = nullptr;
     uint8_t* d_depth = nullptr;
@@ -2799,7 +3130,7 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
     // k_ldlt_solve's tail and the trial errors in k_backsub_errors (no k_edge_errors launch)
     auto merge_errors = [&]() {
         const int np = (6 * d.P + kNB - 1) & ~(kNB - 1);
-        return fuse_slots() && d.P > 0 && np <= kLdlLdsMaxN;
+        return fuse_slots() && d.P > 0 && (np <= kLdlLdsMaxN || use_mw(np));
     };
     // fused slots: the decision of a group's last trial (k_edge_lin takes the others)
     auto enqueue_close = [&](int iterations) {
@@ -2862,6 +3193,8 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
             if (np <= kLdlLdsMaxN)
                 hipLaunchKernelGGL(k_ldlt_solve<true>, dim3(1), dim3(kLdlT), ((size_t)np * (np + 1) + 3 * (size_t)np + 256 + (size_t)kNB * (np + 1) + 64) * 8,
                                    s, d.S, d.bs, n, nullptr, d.x, d.flags, d.lm, pt);
+            else if (use_mw(np))
+                enqueue_ldlt_mw(s, mw_order(mwBase, n), d.S, d.bs, d.x, d.flags, d.lm, pt);
             else
                 hipLaunchKernelGGL(k_ldlt_solve<false>, dim3(1), dim3(kLdlT), (3 * (size_t)np + 64) * 8, s, d.S, d.bs, n,
                                    d_ldlw, d.x, d.flags, d.lm, PoseTail{});
@@ -2929,7 +3262,7 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         // rejected trials), looked up by every captured launch parameter
         auto slot_graph = [&](int nslots, hipGraphExec_t* out, bool firstGroup, bool close) -> int {
             *out = nullptr;
-            if (c->world != 1 || c->profile || s == nullptr) return ORB_OK;
+            if (c->world != 1 || c->profile || s == nullptr || std::getenv("ORB_LBA_NO_GRAPH")) return ORB_OK;
             struct {
                 LbaDev d;
                 const void* ptrs[4];
@@ -2938,7 +3271,7 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
             } k;
             std::memset(&k, 0, sizeof(k));
             k.d = d;
-            k.ptrs[0] = d_freePoses; k.ptrs[1] = d_trace; k.ptrs[2] = d_ldlw; k.ptrs[3] = s;
+            k.ptrs[0] = d_freePoses; k.ptrs[1] = d_trace; k.ptrs[2] = d_ldlw ? (const void*)d_ldlw : (const void*)mwBase.A; k.ptrs[3] = s;
             k.h[0] = hm; k.h[1] = hsv;
             k.v[0] = iterations; k.v[1] = maxTrials; k.v[2] = o->fixed_iterations; k.v[3] = root; k.v[4] = nslots;
             k.v[5] = firstGroup ? 1 : 0;
@@ -3063,8 +3396,28 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
     const double* chi = reinterpret_cast<const double*>(hStage);
     const uint8_t* dep = reinterpret_cast<const uint8_t*>(hStage + 8 * (size_t)NE);
     HSTAMP(0);
+    // the pose-pair blocks of S with shared landmarks (k_schur_pairs runs only those; the
+    // others are zeroed here once and stay zero: the outlier pass keeps the block structure)
+    auto build_pairs = [&]() -> int {
+        const int P = d.P, np2 = P * (P + 1) / 2;
+        int32_t *flag, *pairs, *npairs;
+        TRY(dalloc(c, &flag, np2)); TRY(dalloc(c, &pairs, np2)); TRY(dalloc(c, &npairs, 1));
+        ORB_HIP_TRY(hipMemsetAsync(npairs, 0, 4, s));
+        if (P > 0) {
+            const int all = c->world > 1 ? 1 : 0;
+            ORB_HIP_TRY(hipMemsetAsync(flag, 0, 4 * (size_t)np2, s));
+            ORB_HIP_TRY(hipMemsetAsync(d.S, 0, 8 * (size_t)36 * P * P, s));
+            hipLaunchKernelGGL(k_pair_mark, grid(std::max({d.M, P, all ? np2 : 0})), dim3(256), 0, s, d, flag, all);
+            hipLaunchKernelGGL(k_pair_list, dim3(1), dim3(1024), 0, s, flag, P, pairs, npairs);
+            ORB_HIP_TRY(hipGetLastError());
+        }
+        d.pairs = pairs;
+        d.npairs = npairs;
+        return ORB_OK;
+    };
     // ---- R/src/Optimizer.cpp:789-841
     TRY(init_opt(0));
+    TRY(build_pairs());
     HSTAMP(1);
     bool tailRan = false;
     TRY(optimize(o->iters1, r->iterations[0], tail, tailRan));

@@ -174,6 +174,89 @@ def ba_problem(seed=42, n_local=20, n_fixed=4, n_points=3000, stereo_frac=0.0, W
     }
 
 
+def ba_problem_corridor(seed=42, n_local=60, n_fixed=4, n_points=8000, stereo_frac=0.0, W=640, H=480,
+                        k_range=(2, 8), outlier_frac=0.05, spacing=0.5):
+    """A scaled LocalBundleAdjustment window (SURVEY 8d's "scaled config"): n_local optimised
+    keyframes (id 0 fixed) and n_fixed fixed cameras (half before, half after the window) along a
+    straight path of `spacing`-metre steps, all looking at a wall of points 4-8 m ahead, so each
+    point is visible from a contiguous run of keyframes and the covisibility (the reduced camera
+    matrix's non-zero blocks) is banded, as along a real trajectory.  Each point is observed by
+    k ~ U{k_range} of the keyframes it projects into; octaves, noise, outliers, stereo and the
+    pose / point perturbations as ba_problem (vectorised: 100k points in seconds)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    fx, fy, cx, cy = TUM1
+    nk = n_local + n_fixed
+    nb = n_fixed // 2
+    xs = np.concatenate([np.arange(n_local) * spacing,
+                         -(np.arange(nb) + 1) * spacing,
+                         n_local * spacing + np.arange(n_fixed - nb) * spacing])
+    Rcw = np.stack([_rot(rng.normal(0, 0.01, 3)) for _ in range(nk)])
+    C = np.stack([xs, rng.normal(0, 0.05, nk), np.zeros(nk)], 1)
+    tcw = -np.einsum("kij,kj->ki", Rcw, C)
+    inv_sigma2 = (np.float32(1.0) / np.array([np.float32(1.2) ** (2 * l) for l in range(8)], np.float32))
+    x_lo, x_hi = xs.min() - 2.0, xs.max() + 2.0
+    pts, obs_kf, cnt = [], [], []
+    got = 0
+    while got < n_points:
+        B = 8192
+        X = np.stack([rng.uniform(x_lo, x_hi, B), rng.uniform(-1.5, 1.5, B), rng.uniform(4.0, 8.0, B)], 1)
+        Xc = np.einsum("kij,bj->bki", Rcw, X) + tcw[None]
+        u = fx * Xc[..., 0] / Xc[..., 2] + cx
+        v = fy * Xc[..., 1] / Xc[..., 2] + cy
+        vis = (Xc[..., 2] > 0.1) & (u >= 0) & (u < W) & (v >= 0) & (v < H)
+        nvis = vis.sum(1)
+        k = np.minimum(rng.integers(k_range[0], k_range[1] + 1, B), nvis)
+        keep = nvis >= 2
+        keys = np.where(vis, rng.random((B, nk)), 2.0)
+        order = np.argsort(keys, axis=1)
+        for b in np.nonzero(keep)[0]:
+            if got >= n_points:
+                break
+            sel = np.sort(order[b, :k[b]])
+            pts.append(X[b])
+            obs_kf.append(sel)
+            got += 1
+    pts = np.array(pts)
+    cnt = np.array([len(o) for o in obs_kf])
+    e_pt = np.repeat(np.arange(n_points), cnt).astype(np.int32)
+    e_kf = np.concatenate(obs_kf).astype(np.int32)
+    ne = len(e_pt)
+    Xc = np.einsum("eij,ej->ei", Rcw[e_kf], pts[e_pt]) + tcw[e_kf]
+    u = fx * Xc[:, 0] / Xc[:, 2] + cx
+    v = fy * Xc[:, 1] / Xc[:, 2] + cy
+    lvl = rng.integers(0, 8, ne)
+    sig = 1.2 ** lvl
+    uo = u + rng.normal(0, 1, ne) * sig
+    vo = v + rng.normal(0, 1, ne) * sig
+    uo = np.where(rng.random(ne) < outlier_frac, uo + 20.0, uo)
+    st = rng.random(ne) < stereo_frac
+    ur = np.where(st, uo - KITTI_BF / Xc[:, 2] + rng.normal(0, 1, ne) * sig, -1.0)
+    e_obs = np.stack([uo, vo, ur], 1).astype(np.float32).astype(np.float64)
+    Tcw = np.zeros((nk, 4, 4), np.float32)
+    for i in range(nk):
+        R, t = Rcw[i], tcw[i]
+        if 0 < i < n_local:
+            R = _rot(rng.normal(0, 0.01 / np.sqrt(3), 3)) @ R
+            t = t + rng.normal(0, 0.01 / np.sqrt(3), 3)
+        Tcw[i, :3, :3] = R
+        Tcw[i, :3, 3] = t
+        Tcw[i, 3, 3] = 1
+    Xp = (pts + rng.normal(0, 0.02 / np.sqrt(3), pts.shape)).astype(np.float32).astype(np.float64)
+    fixed = np.zeros(nk, np.uint8)
+    fixed[0] = 1
+    fixed[n_local:] = 1
+    cam = np.tile(np.array([fx, fy, cx, cy, np.float32(KITTI_BF)], np.float64), (ne, 1))
+    return {
+        "Tcw": Tcw, "pose_fixed": fixed, "pose_id": np.arange(nk, dtype=np.int64),
+        "point_xyz": Xp, "point_id": np.arange(n_points, dtype=np.int64) + nk,
+        "point_bad": np.zeros(n_points, np.uint8),
+        "edge_point": e_pt, "edge_pose": e_kf,
+        "edge_stereo": st.astype(np.uint8), "edge_obs": e_obs,
+        "edge_info": inv_sigma2[lvl].astype(np.float64), "edge_cam": cam,
+        "edge_octave": lvl.astype(np.int32),
+    }
+
+
 def pose_problems(n_frames=8, seed=5, n_points=600, stereo_frac=0.0, outlier_frac=0.1, W=640, H=480,
                   rot_noise=0.01, trans_noise=0.02):
     """Synthetic Optimizer::PoseOptimization inputs (Tracking's motion-model / local-map step):

@@ -67,10 +67,12 @@ def test_bad_points_skip_outlier_pass(amd):
     _compare(ref, got)
 
 
-@pytest.mark.parametrize("n,seed", [(6, 0), (114, 1), (120, 2), (128, 3), (130, 4), (180, 5), (301, 6)])
+@pytest.mark.parametrize("n,seed", [(6, 0), (114, 1), (120, 2), (128, 3), (130, 4), (180, 5), (301, 6), (600, 7),
+                                    (1194, 8)])
 def test_dense_solve_vs_numpy(amd, n, seed):
-    """Reduced camera system solve (blocked MFMA LDL^T, LDS and global images) against a
-    float64 numpy solve of the same SPD system: relative residual at f64 rounding level."""
+    """Reduced camera system solve (blocked MFMA LDL^T: the LDS image up to 128, the
+    multi-workgroup k_ldlt_mw_* beyond) against a float64 numpy solve of the same SPD system:
+    relative residual at f64 rounding level."""
     rng = np.random.default_rng(seed)
     G = rng.standard_normal((n, n + 8))
     S = G @ G.T + n * np.eye(n)
@@ -244,3 +246,31 @@ def test_device_structure_matches_host_build(amd, monkeypatch, kw, shuffle_ids, 
     host = amd.LocalBA().solve(pb, global_ba=global_ba)
     for k in ("pose_q", "pose_t", "point_xyz", "edge_chi2", "trace", "edge_erase"):
         assert np.array_equal(dev[k], host[k]), k
+
+
+@pytest.mark.parametrize("kw", [
+    dict(n_local=60, n_fixed=4, n_points=8000, seed=21),                     # 6P = 354: multi-workgroup LDL^T
+    dict(n_local=60, n_fixed=4, n_points=8000, seed=22, stereo_frac=0.5),
+    dict(n_local=200, n_fixed=4, n_points=100000, seed=23),                  # SURVEY 8d's scaled config: 6P = 1194
+])
+def test_scaled_local_ba_matches_oracle(amd, kw):
+    """Local BA windows beyond the LDS image (more than 21 free keyframes, R/src/Optimizer.cpp:569-625
+    bounds the window only by covisibility): a corridor of keyframes with banded covisibility,
+    the fused slots with the multi-workgroup reduced solve and the pair-list Schur complement,
+    within the oracle's tolerances (identical LM decisions, chi2 trace 1e-9, estimates 1e-5)."""
+    from orb_slam2_amd import synth
+    pb = synth.ba_problem_corridor(**kw)
+    ref = O.lba_solve(pb)
+    got = amd.LocalBA().solve(pb)
+    _compare(ref, got)
+
+
+def test_scaled_local_ba_bitwise_reproducible(amd):
+    """The multi-workgroup solve and the pair-list Schur keep every reduction order fixed."""
+    from orb_slam2_amd import synth
+    pb = synth.ba_problem_corridor(n_local=40, n_fixed=2, n_points=4000, seed=24, stereo_frac=0.3)
+    ctx = amd.LocalBA()
+    runs = [ctx.solve(pb) for _ in range(2)] + [amd.LocalBA().solve(pb)]
+    for r in runs[1:]:
+        for k in ("pose_q", "pose_t", "point_xyz", "edge_chi2", "trace", "edge_erase"):
+            assert np.array_equal(r[k], runs[0][k]), k

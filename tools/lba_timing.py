@@ -1,4 +1,5 @@
-"""Runs a few LocalBundleAdjustment solves of the config-4 problem and prints
+"""Runs a few LocalBundleAdjustment solves of the config-4 problem (corridor=1 n_local=200
+n_points=100000: the scaled window) and prints
 per-stage event times; with ORB_SLAM2_AMD_LIB pointing at an ORB_TIMING variant
 (tools/build_variant.py timing -DORB_TIMING) the kernels print their own clock splits."""
 import pathlib
@@ -14,8 +15,11 @@ from orb_slam2_amd import synth  # noqa: E402
 kw = {}
 for a in sys.argv[1:]:
     k, v = a.split("=")
-    kw[k] = int(v)
-pb = synth.ba_problem(**kw)
+    kw[k] = float(v) if "." in v else int(v)
+# corridor=1: the scaled window generator (synth.ba_problem_corridor, banded covisibility)
+gen = synth.ba_problem_corridor if kw.pop("corridor", 0) else synth.ba_problem
+pb = gen(**kw)
+print(f"problem: {len(pb['Tcw'])} keyframes, {len(pb['point_xyz'])} points, {len(pb['edge_point'])} edges", flush=True)
 ba = amd.LocalBA()
 n = 12
 call = ba.prepared(pb)
