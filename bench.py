@@ -29,6 +29,11 @@ import torch  # noqa: E402
 
 import pkgload  # noqa: E402
 
+# the OpenMP CPU baselines (oracle_lba_solve_omp, the extraction port) open and close a parallel
+# region per loop: keep the worker threads spinning between regions, as a production OpenMP
+# build of g2o would be run (read by the system libgomp when the oracle library loads)
+os.environ.setdefault("OMP_WAIT_POLICY", "active")
+
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md)
 VALU_PEAK_TOPS = 78.6            # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md)
 VALU_MEASURED_TOPS = 39.3        # tools/micro/valu_peak.hip: 4 cycles per wave64 VALU op (profiles/r02_valu_peak.txt)
@@ -91,6 +96,9 @@ def parse():
     ap.add_argument("--lba-solves", type=int, default=10, help="timed LocalBundleAdjustment calls")
     ap.add_argument("--lba-points", type=int, default=3000)
     ap.add_argument("--lba-kf", type=int, default=20)
+    ap.add_argument("--lba-comm", choices=["native", "torch"], default="native",
+                    help="N>1 local BA: the library's device group driven by rank 0 (native) or one rank per "
+                         "GPU with a torch.distributed all-reduce callback (torch)")
     ap.add_argument("--no-stereo", action="store_true", help="skip the config-5 sharded stereo leg")
     ap.add_argument("--stereo-batches", type=int, default=16,
                     help="8-frame EuRoC stereo batches per step of the config-5 leg")
@@ -233,12 +241,21 @@ def bench_lba(args, amd, dev, local, rank, world):
     from orb_slam2_amd import synth
     pb = synth.ba_problem(n_local=args.lba_kf, n_points=args.lba_points)
     nk, ne = len(pb["Tcw"]), len(pb["edge_point"])
-    ctx = amd.LocalBA(local)
-    # a dedicated stream (the legacy default stream cannot be captured into the LM slot graph);
-    # RCCL calls of the all-reduce callback are issued on the same stream
-    stream = torch.cuda.Stream(dev)
-    ctx.set_stream(stream.cuda_stream)
-    if world > 1:
+    native = world > 1 and args.lba_comm == "native"
+    if native:
+        # the drop-in's multi-GPU path: ONE process (rank 0, LocalMapping's thread) drives a group
+        # of contexts on all the ranks' devices; the library's peer-to-peer all-reduce over xGMI
+        # carries the exchange (lba_group_*); the other ranks wait at the barrier
+        ndev = torch.cuda.device_count()
+        devices = [r % ndev for r in range(world)]
+        ctx = amd.LocalBAGroup(devices) if rank == 0 else None
+    else:
+        ctx = amd.LocalBA(local)
+        # a dedicated stream (the legacy default stream cannot be captured into the LM slot graph);
+        # RCCL calls of the all-reduce callback are issued on the same stream
+        stream = torch.cuda.Stream(dev)
+        ctx.set_stream(stream.cuda_stream)
+    if world > 1 and not native:
         ws = torch.zeros(max(36 * nk * nk + 6 * nk, ne) + 64, dtype=torch.float64, device=dev)
 
         def ar(off, cnt, op):
@@ -246,6 +263,11 @@ def bench_lba(args, amd, dev, local, rank, world):
                 torch.distributed.all_reduce(ws[off:off + cnt], op=torch.distributed.ReduceOp.SUM if op == 0
                                              else torch.distributed.ReduceOp.MAX)
         ctx.set_comm(rank, world, ws, ar)
+    if native and rank != 0:   # rank 0 runs the sharded solves; its result is broadcast below
+        torch.distributed.barrier()
+        obj = [None]
+        torch.distributed.broadcast_object_list(obj, src=0)
+        return obj[0]
     # warm-up: allocations, code objects and the LM-slot graphs of both group shapes (the
     # first solves instantiate them); LocalMapping calls LocalBundleAdjustment once per keyframe,
     # so the steady state is what it sees
@@ -261,36 +283,50 @@ def bench_lba(args, amd, dev, local, rank, world):
         its, _, _ = call()
         times.append(time.perf_counter() - t0)
         iters += sum(its)
-    # stage split from a separate profiled pass (per-slot HIP events; kernels enqueued one by
-    # one, so these solves are slower than the timed ones above)
-    ctx.profile(True)
-    for _ in range(args.lba_solves):
-        r = ctx.solve(pb)      # (decisions below: the same in every solve of this problem)
-    st = ctx.stats()
-    ctx.profile(False)
     tot = sum(times)
-    er = torch.tensor([float(np.count_nonzero(r["edge_erase"]))], dtype=torch.float64, device=dev)
-    if world > 1:      # each rank flags the edges of its own landmark shard
-        torch.distributed.all_reduce(er)
-    erased = int(er.item())
-    if world > 1:
-        t = torch.tensor([tot], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        tot = float(t.item())
+    if native:
+        ex_ms, n_ex = ctx.stats()
+        r = ctx.solve(pb)
+        st = None
+        erased = int(np.count_nonzero(r["edge_erase"]))
+    else:
+        # stage split from a separate profiled pass (per-slot HIP events; kernels enqueued one by
+        # one, so these solves are slower than the timed ones above)
+        ctx.profile(True)
+        for _ in range(args.lba_solves):
+            r = ctx.solve(pb)      # (decisions below: the same in every solve of this problem)
+        st = ctx.stats()
+        ctx.profile(False)
+        er = torch.tensor([float(np.count_nonzero(r["edge_erase"]))], dtype=torch.float64, device=dev)
+        if world > 1:      # each rank flags the edges of its own landmark shard
+            torch.distributed.all_reduce(er)
+        erased = int(er.item())
+        if world > 1:
+            t = torch.tensor([tot], dtype=torch.float64, device=dev)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            tot = float(t.item())
     out = {"config": f"{args.lba_kf} KF (+4 fixed) x {args.lba_points} points, {ne} mono edges, "
                      f"landmarks sharded x{world}",
            "ms_per_iter": round(1000 * tot / max(iters, 1), 4),
            "solve_ms": round(1000 * tot / args.lba_solves, 3),
-           "iterations_per_solve": iters / args.lba_solves, "trials": st["trials"] / args.lba_solves,
-           "stage_ms_per_solve": {k: round(st[k] / args.lba_solves, 4) for k in
-                                  ("linearize_ms", "schur_ms", "solve_ms", "update_ms")},
+           "iterations_per_solve": iters / args.lba_solves, "trials": r["trials"],
            "n_gpus": world,
+           "collective": ("none" if world == 1 else
+                          "library peer-to-peer all-reduce over xGMI (lba_group, one process driving every device)"
+                          if native else "torch.distributed all_reduce callback (RCCL), one process per GPU"),
            # LM decisions of the last timed solve: identical for every world size (landmark shards
            # only reorder the f64 sums; tests/test_bench_ranks.py compares N=1 with N=2)
            "decisions": {"iterations": [int(x) for x in r["iterations"]], "trials": int(r["trials"]),
                          "chi2_trace": [float(x) for x in r["trace"][:, 1]],
                          "erased_edges": erased}}
-    out["roofline"] = lba_roofline(pb, out, world)
+    if st is not None:
+        out["stage_ms_per_solve"] = {k: round(st[k] / args.lba_solves, 4) for k in
+                                     ("linearize_ms", "schur_ms", "solve_ms", "update_ms")}
+    if native:
+        out["exchange_us_per_collective"] = round(1000 * ex_ms / max(n_ex, 1), 2)
+        out["collectives_per_trial"] = round(n_ex / max(1, (3 + args.lba_solves) * r["trials"]), 2)
+    if st is not None:   # (the native group's solves have no per-slot stage events)
+        out["roofline"] = lba_roofline(pb, out, world)
     if world == 1 and not args.no_cpu:   # the CPU baseline is an N=1 figure
         sys.path.insert(0, str(ROOT / "tests"))
         import oracle_ref as O
@@ -306,7 +342,7 @@ def bench_lba(args, amd, dev, local, rank, world):
             return dt, n, it
         dt, n, it = timed(None)
         out["cpu_baseline"] = {"ms_per_iter": round(1000 * dt / it, 4), "solve_ms": round(1000 * dt / n, 3),
-                               "cores": 1, "kind": "port",
+                               "cores": 1, "kind": "port", "cpu_model": host_info()["cpu_model"],
                                "sample": f"{n} LocalBundleAdjustment solves, oracle C restatement of g2o "
                                          f"LM+Schur (dense LDLT), 1 thread (reference builds g2o without OpenMP)"}
         th = host_threads()
@@ -318,6 +354,9 @@ def bench_lba(args, amd, dev, local, rank, world):
                       f"edges, Schur landmarks) on {th} threads, bitwise identical to the 1-thread oracle"}
         out["speedup_vs_cpu"] = round(out["cpu_baseline"]["ms_per_iter"] / out["ms_per_iter"], 2)
         out["speedup_vs_cpu_openmp"] = round(out["cpu_baseline_openmp"]["ms_per_iter"] / out["ms_per_iter"], 2)
+    if native:   # rank 0 -> the waiting ranks
+        torch.distributed.barrier()
+        torch.distributed.broadcast_object_list([out], src=0)
     return out
 
 
@@ -477,6 +516,7 @@ def cpu_baseline_stereo(cv, W, H, NF, mbf, n_pairs):
         list(pool.map(one, prs))
     dt = time.perf_counter() - t0
     return {"stereo_frames_per_s": round(n_pairs / dt, 2), "cores": threads, "kind": "port",
+            "cpu_model": host_info()["cpu_model"],
             "sample": f"{n_pairs} stereo pairs {W}x{H}, {NF} feat: both images extracted + ComputeStereoMatches, "
                       f"oracle C restatement, 1 pair per host thread"}
 

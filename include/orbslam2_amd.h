@@ -549,6 +549,25 @@ int lba_debug_stop_after_trials(lba_context* c, int n_trials);
 int lba_debug_buffer(lba_context* c, int which, double* out, size_t n);
 int lba_stats(lba_context* c, double* ms4, int* iters, int* trials);
 
+/* Multi-GPU Optimizer::LocalBundleAdjustment from ONE process — the drop-in's model: LocalMapping
+ * calls it on its own thread (R/src/LocalMapping.cpp:94-95, R/src/System.cpp:104-105).  A group
+ * holds one context per entry of devices[0..n) (n <= 16; a device may repeat: two contexts on one
+ * device rehearse the exchange on a one-GPU machine).  lba_group_solve shards the landmarks as
+ * lba_set_comm does (rank r owns [r M / n, (r+1) M / n)) and all-reduces the pose blocks, the
+ * reduced camera system S + b_s and the LM scalars with the library's own one-shot peer-to-peer
+ * kernel over xGMI (every rank reads every rank's slice through peer access and sums in rank
+ * order: all ranks take bitwise the same LM decisions); no caller callback.  Same arguments and
+ * results as lba_solve (points, edge chi2 and erase flags merged from their owners).  Returns
+ * ORB_ENODEV when two listed devices cannot access each other. */
+typedef struct lba_group lba_group;
+int lba_group_create(const int* devices, int n, lba_group** out);
+void lba_group_destroy(lba_group* g);
+int lba_group_solve(lba_group* g, const lba_problem* p, const lba_options* o, const volatile uint8_t* stop,
+                    lba_result* r);
+/* Cumulative exchange time measured on rank 0's stream (from its partial being ready to every
+ * rank having read it, per collective) and the number of collectives. */
+int lba_group_stats(lba_group* g, double* exchange_ms, long* n_exchanges);
+
 /* Converter::toSE3Quat(const cv::Mat& Tcw) / Converter::toCvMat(const SE3Quat&)
  * (R/src/Converter.cpp:47-57, 59-63): row-major 4x4 float <-> quaternion + t. */
 void lba_pose_from_Tcw(const float Tcw[16], double q[4], double t[3]);

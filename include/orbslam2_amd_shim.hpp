@@ -14,7 +14,8 @@
 //                             SearchByProjection(Frame&, const Frame&, th, bMono) (:1564-1718) and
 //                             SearchByProjection(Frame&, const vector<MapPoint*>&, th) (:63-163)
 //   LocalBundleAdjustment     Optimizer::LocalBundleAdjustment (R/include/Optimizer.h:45,
-//                             R/src/Optimizer.cpp:564-918): graph gathering, lba_solve, write-back
+//                             R/src/Optimizer.cpp:564-918): graph gathering, lba_solve (or, given a
+//                             device list, lba_group_solve over several GPUs), write-back
 //
 // Errors: the reference's methods have no error returns, so a negative ORB_E* status becomes a
 // std::runtime_error here (there is no CPU fallback: without a gfx950 device the constructors
@@ -297,9 +298,9 @@ struct LbaDump {
     int iterations[2] = {0, 0}, trials = 0, aborted = 0;
 };
 
-template <class KeyFrameT, class MapT>
-void LocalBundleAdjustment(KeyFrameT* pKF, bool* pbStopFlag, MapT* pMap, LbaDump* dump = nullptr,
-                           lba_context* ctx = nullptr) {
+namespace detail {
+template <class KeyFrameT, class MapT, class Solve>
+void local_ba(KeyFrameT* pKF, bool* pbStopFlag, MapT* pMap, LbaDump* dump, Solve&& solve) {
     using MapPointT = typename std::remove_pointer<typename decltype(pKF->GetMapPointMatches())::value_type>::type;
     using MatT = typename std::decay<decltype(pKF->GetPose())>::type;
     // ---- local keyframes, local map points, fixed cameras (R :567-625)
@@ -388,8 +389,7 @@ void LocalBundleAdjustment(KeyFrameT* pKF, bool* pbStopFlag, MapT* pMap, LbaDump
     lba_result r{D.out_q.data(), D.out_t.data(), D.out_xyz.data(), D.edge_erase.data(), nullptr, {0, 0}, 0,
                  nullptr, 0, 0};
     static_assert(sizeof(bool) == 1, "mbAbortBA is read as one byte");
-    check(lba_solve(ctx ? ctx : thread_lba(), &p, &o, reinterpret_cast<const volatile uint8_t*>(pbStopFlag), &r),
-          "lba_solve");
+    check(solve(&p, &o, reinterpret_cast<const volatile uint8_t*>(pbStopFlag), &r), "lba_solve");
     D.iterations[0] = r.iterations[0];
     D.iterations[1] = r.iterations[1];
     D.trials = r.trials;
@@ -425,6 +425,36 @@ void LocalBundleAdjustment(KeyFrameT* pKF, bool* pbStopFlag, MapT* pMap, LbaDump
         vpMP[(size_t)m]->SetWorldPos(detail::make_mat<MatT>(3, 1, X));
         vpMP[(size_t)m]->UpdateNormalAndDepth();
     }
+}
+}  // namespace detail
+
+template <class KeyFrameT, class MapT>
+void LocalBundleAdjustment(KeyFrameT* pKF, bool* pbStopFlag, MapT* pMap, LbaDump* dump = nullptr,
+                           lba_context* ctx = nullptr) {
+    lba_context* c = ctx ? ctx : thread_lba();
+    detail::local_ba(pKF, pbStopFlag, pMap, dump,
+                     [c](const lba_problem* p, const lba_options* o, const volatile uint8_t* st, lba_result* r) {
+                         return lba_solve(c, p, o, st, r);
+                     });
+}
+
+// The same window sharded over several GPUs of this process (lba_group_*: landmark shards, the
+// library's peer-to-peer all-reduce over xGMI, identical LM decisions on every device).  One group
+// per calling thread and device list, created on first use.
+inline lba_group* thread_lba_group(const std::vector<int>& devices) {
+    thread_local std::map<std::vector<int>, lba_group*> groups;
+    lba_group*& g = groups[devices];
+    if (!g) check(lba_group_create(devices.data(), (int)devices.size(), &g), "lba_group_create");
+    return g;
+}
+template <class KeyFrameT, class MapT>
+void LocalBundleAdjustment(KeyFrameT* pKF, bool* pbStopFlag, MapT* pMap, const std::vector<int>& devices,
+                           LbaDump* dump = nullptr) {
+    lba_group* g = thread_lba_group(devices);
+    detail::local_ba(pKF, pbStopFlag, pMap, dump,
+                     [g](const lba_problem* p, const lba_options* o, const volatile uint8_t* st, lba_result* r) {
+                         return lba_group_solve(g, p, o, st, r);
+                     });
 }
 
 }  // namespace orbslam2_amd

@@ -26,6 +26,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <thread>
 #include <cfloat>
 #include <chrono>
 #include <cmath>
@@ -882,6 +884,7 @@ __global__ __launch_bounds__(256) void k_vertex_schur(LbaDev d, int nChi) {
 // carries Hpp + lambda I and b_p).
 constexpr int kSpT = 256;
 constexpr int kSpList = 4096;   // pose j's landmark list held in LDS up to this length
+constexpr int kSpChunk = 1024;  // pose i's edges looked up per round (4 per thread)
 __global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag) {
     if ((int)blockIdx.x >= *d.npairs) return;   // blocks with no shared landmark stay 0 (zeroed per solve)
     const int pr = d.pairs[blockIdx.x];
@@ -894,10 +897,6 @@ __global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag) {
     const int a0 = d.poStart[bi], a1 = d.poStart[bi + 1], b0 = d.poStart[bj], nb = d.poStart[bj + 1] - b0;
     if (phase != 1) return;   // lm_off(d.lm, 1)
     const bool inLds = nb <= kSpList;
-    // the next edge's act position and landmark are loaded one iteration ahead (the first ones
-    // with pose j's list), so each edge's chain is the search, pose j's act position and the blocks
-    const int aLast = max(a1 - 1, 0);
-    int e1n = d.poAct[min(a0 + tid, aLast)], ln = d.poPt[min(a0 + tid, aLast)];
     if (!diag && inLds)
         for (int t = tid; t < nb; t += kSpT) listJ[t] = d.poPt[b0 + t];
     __syncthreads();
@@ -905,22 +904,9 @@ __global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag) {
     double acc[42];
 #pragma unroll
     for (int i = 0; i < 42; i++) acc[i] = 0.0;
-    for (int a = a0 + tid; a < a1; a += kSpT) {
-        const int e1 = e1n, l = ln;
-        e1n = d.poAct[min(a + kSpT, aLast)];
-        ln = d.poPt[min(a + kSpT, aLast)];
-        int e2 = e1;
-        if (!diag) {   // lower_bound of l in pose j's sorted landmark list
-            int lo = 0, hi = nb;
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (Lj[mid] < l) lo = mid + 1;
-                else hi = mid;
-            }
-            if (lo == nb || Lj[lo] != l) continue;
-            e2 = d.poAct[b0 + lo];
-        }
-        // A_e1 = Hpl_e1 D^-1 (formed per edge by the landmark kernel) against Hpl_e2
+    // the product of one shared landmark: A_e1 = Hpl_e1 D^-1 (formed per edge by the landmark
+    // kernel) against Hpl_e2; diagonal blocks (e2 == e1) also b_s's Hpl_e1 D^-1 b_l
+    auto product = [&](int e1, int e2, int l) {
         const double2* Ui = reinterpret_cast<const double2*>(d.Ae + 18 * (size_t)e1);
         const double2* Bj = reinterpret_cast<const double2*>(d.Hpl_e + 18 * (size_t)e2);
         double v[18], u[18];
@@ -930,7 +916,6 @@ __global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag) {
             u[2 * h] = x.x; u[2 * h + 1] = x.y;
             v[2 * h] = y.x; v[2 * h + 1] = y.y;
         }
-        const double* w = v;   // diagonal blocks: e2 == e1, Hpl_e1 for b_s
 #pragma unroll
         for (int r = 0; r < 6; r++)
 #pragma unroll
@@ -940,7 +925,64 @@ __global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag) {
             const double* db = d.db + 3 * (size_t)l;
             const double g0 = db[0], g1 = db[1], g2 = db[2];
 #pragma unroll
-            for (int i = 0; i < 6; i++) acc[36 + i] += w[i * 3] * g0 + w[i * 3 + 1] * g1 + w[i * 3 + 2] * g2;
+            for (int i = 0; i < 6; i++) acc[36 + i] += v[i * 3] * g0 + v[i * 3 + 1] * g1 + v[i * 3 + 2] * g2;
+        }
+    };
+    if (diag) {   // every edge of pose i pairs with itself: already a dense list
+        for (int a = a0 + tid; a < a1; a += kSpT) {
+            const int e1 = d.poAct[a];
+            product(e1, e1, d.poPt[a]);
+        }
+    } else {
+        // off-diagonal: chunks of 4 edges per thread of pose i are looked up in pose j's landmark
+        // list (lower_bound), the matches compacted in thread order (a workgroup scan) into `trip`,
+        // then the products run over the dense list: no lane idles through a product for an edge
+        // without a match
+        __shared__ int2 trip[kSpChunk];
+        __shared__ int wtot[kSpT / 64];
+        const int lane = tid & 63, wave = tid >> 6;
+        for (int base = a0; base < a1; base += kSpChunk) {
+            int m1[kSpChunk / kSpT], m2[kSpChunk / kSpT], lm[kSpChunk / kSpT];
+#pragma unroll
+            for (int u = 0; u < kSpChunk / kSpT; u++) {
+                const int a = min(base + tid + kSpT * u, a1 - 1);   // clamped: unconditional loads
+                m1[u] = d.poAct[a];
+                const int lv = d.poPt[a];
+                lm[u] = base + tid + kSpT * u < a1 ? lv : -1;
+            }
+            int cnt = 0;
+#pragma unroll
+            for (int u = 0; u < kSpChunk / kSpT; u++) {
+                const int l = lm[u];
+                int lo = 0, hi = nb;
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (Lj[mid] < l) lo = mid + 1;
+                    else hi = mid;
+                }
+                const bool hit = l >= 0 && lo < nb && Lj[lo] == l;
+                const int e2 = d.poAct[b0 + min(lo, nb - 1)];
+                m2[u] = hit ? e2 : -1;
+                cnt += hit ? 1 : 0;
+            }
+            const int incl = wave_incl_scan_i32(cnt);
+            if (lane == 63) wtot[wave] = incl;
+            __syncthreads();
+            int off = incl - cnt, total = 0;
+#pragma unroll
+            for (int w = 0; w < kSpT / 64; w++) {
+                off += w < wave ? wtot[w] : 0;
+                total += wtot[w];
+            }
+#pragma unroll
+            for (int u = 0; u < kSpChunk / kSpT; u++)
+                if (m2[u] >= 0) trip[off++] = make_int2(m1[u], m2[u]);
+            __syncthreads();
+            for (int m = tid; m < total; m += kSpT) {
+                const int2 tr = trip[m];
+                product(tr.x, tr.y, 0);
+            }
+            __syncthreads();   // trip and wtot are rewritten by the next chunk
         }
     }
     const int nv = diag ? 42 : 36;
@@ -1029,6 +1071,125 @@ __global__ __launch_bounds__(1024) void k_pair_list(const int32_t* __restrict__ 
     if (tid == 1023) *npairs = run;
 }
 
+// ---- The Schur complement as a dense f64 MFMA GEMM (A/B against k_schur_pairs; ORB_LBA_SCHUR_MFMA=1,
+// reduced systems in the LDS image).  SURVEY 8d's densified form of G/core/block_solver.hpp:382-433:
+// S = Hpp + lambda I - Y Y^T with Y = W L^-T, W the 6P x 3M matrix of the Hpl blocks and D_l = L L^T
+// the landmark's Cholesky factor (W D^-1 W^T = (W L^-T)(W L^-T)^T).  Y^T is built k-major
+// (k_schur_ymat), split over chunks of kYLm landmarks (48 k) each workgroup of k_schur_gemm multiplies
+// its chunk into all upper 16 x 16 tiles of S with v_mfma_f64_16x16x4 (partials in HBM), and
+// k_schur_msum adds the chunks in a fixed order (bitwise reproducible) with Hpp + lambda I and b_s.
+// Y is dense: a landmark's 3 columns are non-zero only in its observers' 6-row blocks, so the MFMA
+// units execute ~P / k_mean times the algorithmic flops (the measurement this mode exists for).
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+constexpr int kYLm = 16;   // landmarks per GEMM chunk
+constexpr int kYLmB = 8;   // landmarks per k_schur_ymat workgroup
+
+__global__ __launch_bounds__(256) void k_schur_ymat(LbaDev d, double* __restrict__ Yt, int np, double* __restrict__ ce) {
+    if (d.lm->phase != 1) return;
+    __shared__ double tile[3 * kYLmB][128];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < 3 * kYLmB * 128; i += 256) (&tile[0][0])[i] = 0.0;
+    __syncthreads();
+    const int l = blockIdx.x * kYLmB + tid;
+    if (tid < kYLmB && l < d.M) {
+        const double lambda = d.lm->lambda;
+        double D[9];
+        for (int i = 0; i < 9; i++) D[i] = d.Hll[9 * (size_t)l + i];
+        D[0] += lambda; D[4] += lambda; D[8] += lambda;
+        // D = L L^T; Li = L^-1 (lower)
+        const double l00 = sqrt(D[0]), l10 = D[3] / l00, l20 = D[6] / l00;
+        const double l11 = sqrt(D[4] - l10 * l10), l21 = (D[7] - l20 * l10) / l11;
+        const double l22 = sqrt(D[8] - l20 * l20 - l21 * l21);
+        const double m00 = 1.0 / l00, m11 = 1.0 / l11, m22 = 1.0 / l22;
+        const double m10 = -l10 * m00 * m11, m21 = -l21 * m11 * m22, m20 = -(l20 * m00 + l21 * m10) * m22;
+        const double Li[9] = {m00, 0.0, 0.0, m10, m11, 0.0, m20, m21, m22};
+        const double* db = d.db + 3 * (size_t)l;
+        for (int a = d.ptStart[l]; a < d.ptStart[l + 1]; a++) {
+            const int k = d.ptAct[a];
+            const int pi = d.actPi[k];
+            if (pi < 0) continue;
+            const double* W = d.Hpl_e + 18 * (size_t)k;
+            for (int r = 0; r < 6; r++) {
+                for (int q = 0; q < 3; q++) {   // Y_e = W L^-T: (W L^-T)[r][q] = sum_m W[r][m] Li[q][m]
+                    double y = 0.0;
+                    for (int m = 0; m <= q; m++) y += W[r * 3 + m] * Li[q * 3 + m];
+                    tile[3 * tid + q][6 * pi + r] = y;
+                }
+                ce[6 * (size_t)k + r] = W[r * 3] * db[0] + W[r * 3 + 1] * db[1] + W[r * 3 + 2] * db[2];
+            }
+        }
+    }
+    __syncthreads();
+    const int nl = min(kYLmB, d.M - (int)blockIdx.x * kYLmB);
+    for (int i = tid; i < 3 * nl * np; i += 256) {
+        const int c = i / np, r = i % np;
+        Yt[((size_t)blockIdx.x * 3 * kYLmB + c) * np + r] = tile[c][r];
+    }
+}
+
+// chunk c (kYLm landmarks = 48 rows of Y^T): every upper tile (I <= K) of Y Y^T, 12 MFMAs per tile
+__global__ __launch_bounds__(256) void k_schur_gemm(LbaDev d, const double* __restrict__ Yt, int np,
+                                                    double* __restrict__ part) {
+    if (d.lm->phase != 1) return;
+    __shared__ double ys[3 * kYLm][128];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int kr = min(3 * kYLm, 3 * d.M - (int)blockIdx.x * 3 * kYLm);   // rows of Y^T in this chunk
+    for (int i = tid; i < 3 * kYLm * np; i += 256) {
+        const int r = i / np, c = i % np;
+        ys[r][c] = r < kr ? Yt[((size_t)blockIdx.x * 3 * kYLm + r) * np + c] : 0.0;
+    }
+    __syncthreads();
+    const int T = np / 16, nt = T * (T + 1) / 2;
+    const int li = lane & 15, lk = lane >> 4;
+    for (int t = wave; t < nt; t += 4) {
+        int ti = 0, rem = t;   // row-major upper triangle: (ti, tk), ti <= tk
+        while (rem >= T - ti) { rem -= T - ti; ti++; }
+        const int tk = ti + rem;
+        dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s = 0; s < 3 * kYLm / 4; s++) {
+            const double a = ys[4 * s + lk][16 * ti + li], b = ys[4 * s + lk][16 * tk + li];
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+        }
+        double* o = part + ((size_t)blockIdx.x * nt + t) * 256;
+#pragma unroll
+        for (int q = 0; q < 4; q++) o[(lk + 4 * q) * 16 + li] = acc[q];
+    }
+}
+
+// S (upper, mirrored) = [root] Hpp + lambda I - sum over chunks (chunk order), b_s = [root] b_p - the
+// edges' Hpl D^-1 b_l (pose's edges in list order)
+__global__ __launch_bounds__(256) void k_schur_msum(LbaDev d, const double* __restrict__ part, int nchunks, int np,
+                                                    const double* __restrict__ ce, int addDiag) {
+    if (d.lm->phase != 1) return;
+    const int T = np / 16, nt = T * (T + 1) / 2, n = 6 * d.P;
+    const int g = blockIdx.x * 256 + threadIdx.x;
+    if (g < nt * 256) {
+        const int t = g >> 8, e = g & 255;
+        int ti = 0, rem = t;
+        while (rem >= T - ti) { rem -= T - ti; ti++; }
+        const int tk = ti + rem;
+        const int R = 16 * ti + (e >> 4), Cc = 16 * tk + (e & 15);
+        if (R < n && Cc < n && R <= Cc) {
+            double v = 0.0;
+            for (int c = 0; c < nchunks; c++) v += part[((size_t)c * nt + t) * 256 + e];
+            double val = 0.0;
+            if (addDiag && R / 6 == Cc / 6) {
+                val = d.Hpp[36 * (size_t)(R / 6) + (R % 6) * 6 + Cc % 6];
+                if (R == Cc) val += d.lm->lambda;
+            }
+            val -= v;
+            d.S[(size_t)R * n + Cc] = val;
+            d.S[(size_t)Cc * n + R] = val;
+        }
+    } else if (g < nt * 256 + n) {
+        const int i = g - nt * 256, p = i / 6, r = i % 6;
+        double v = 0.0;
+        for (int a = d.poStart[p]; a < d.poStart[p + 1]; a++) v += ce[6 * (size_t)d.poAct[a] + r];
+        d.bs[i] = (addDiag ? d.bp[i] : 0.0) - v;
+    }
+}
+
 // Broadcast of lane `src` (a compile-time constant at every call site) through two
 // v_readlane_b32 into SGPRs: a few cycles, against a ds_bpermute round trip for __shfl.
 __device__ __forceinline__ double shfl_d(double v, int src) {
@@ -1065,7 +1226,6 @@ __device__ __forceinline__ double shfl_d_dyn(double v, int src) {
 constexpr int kNB = 16;
 constexpr int kLdlT = 512;
 constexpr int kLdlLdsMaxN = 128;   // padded order held in LDS: (128 * 129 + 3 * 128 + 256 + 16 * 129 + 64) * 8 B = 151 KB
-typedef double dbl4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ double rcp_nr(double d) {
     double r = __builtin_amdgcn_rcp(d);
@@ -2272,6 +2432,11 @@ __global__ __launch_bounds__(1024) void k_lm_decide_fused(LbaDev d, const int32_
     }
 }
 
+// Measurement hook (ORB_LBA_EXTRA_BOUNDARY=1): one empty 256-workgroup launch after each kernel of
+// an LM slot, so the slot graph carries 5 more dependent kernel boundaries; the difference in solve
+// time / (5 x slots) is what one boundary costs inside this graph.
+__global__ __launch_bounds__(64) void k_nop() {}
+
 __global__ __launch_bounds__(256) void k_lba_init(double* __restrict__ err, uint8_t* __restrict__ emask, int ne,
                                                   double* __restrict__ bq, const double* __restrict__ q,
                                                   double* __restrict__ bt, const double* __restrict__ t, int np,
@@ -2525,6 +2690,7 @@ struct lba_context {
     // communicator
     int rank = 0, world = 1;
     double* ws = nullptr;          // caller-owned device workspace (doubles)
+    double* wsOut = nullptr;       // where a collective leaves its result (NULL: in place in ws)
     size_t wsDoubles = 0;
     lba_allreduce_fn allreduce = nullptr;
     void* commUser = nullptr;
@@ -2711,7 +2877,7 @@ static int comm_allreduce_g(lba_context* c, double* dbuf, size_t n, int op, cons
     const unsigned g = (unsigned)std::min<size_t>(1024, (n + 255) / 256);
     hipLaunchKernelGGL(k_pack, dim3(g), dim3(256), 0, c->stream, c->ws, dbuf, n, st, want);
     if (c->allreduce(c->commUser, 0, n, op) != 0) return ORB_EGPU;
-    hipLaunchKernelGGL(k_unpack, dim3(g), dim3(256), 0, c->stream, dbuf, c->ws, n, st, want);
+    hipLaunchKernelGGL(k_unpack, dim3(g), dim3(256), 0, c->stream, dbuf, c->wsOut ? c->wsOut : c->ws, n, st, want);
     return ORB_OK;
 }
 
@@ -2944,7 +3110,7 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         ORB_HIP_TRY(hipMemcpyAsync(c->ws, h, 8, hipMemcpyHostToDevice, s));
         TRY(lba_wait(c));
         if (c->allreduce(c->commUser, 0, 1, 0) != 0) return ORB_EGPU;
-        ORB_HIP_TRY(hipMemcpyAsync(h, c->ws, 8, hipMemcpyDeviceToHost, s));
+        ORB_HIP_TRY(hipMemcpyAsync(h, c->wsOut ? c->wsOut : c->ws, 8, hipMemcpyDeviceToHost, s));
         TRY(lba_wait(c));
         *out = h[0] > 0.5;
         return ORB_OK;
@@ -3028,6 +3194,17 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
     TRY(dalloc(c, &d_trace, 4 * 64));
     double* d_ldlw = nullptr;   // global image of the padded reduced matrix when it exceeds LDS
     MwLdl mwBase{};             // or the multi-workgroup solve's buffers
+    // the dense MFMA Schur (A/B): Y^T, per-chunk partial tiles, per-edge Hpl D^-1 b_l
+    const bool schurMfma = std::getenv("ORB_LBA_SCHUR_MFMA") != nullptr && c->world == 1 &&
+                           (((size_t)6 * NP + kNB - 1) & ~(size_t)(kNB - 1)) <= (size_t)kLdlLdsMaxN;
+    double *d_Yt = nullptr, *d_ypart = nullptr, *d_ce = nullptr;
+    if (schurMfma) {
+        const size_t npm = ((size_t)6 * NP + 15) & ~(size_t)15, T = npm / 16;
+        const size_t nch = ((size_t)NM + kYLm - 1) / kYLm;
+        TRY(dalloc(c, &d_Yt, ((size_t)NM + kYLmB) * 3 * npm));
+        TRY(dalloc(c, &d_ypart, nch * (T * (T + 1) / 2) * 256));
+        TRY(dalloc(c, &d_ce, 6 * (size_t)NE));
+    }
     {
         const size_t npMax = ((size_t)6 * NP + kNB - 1) & ~(size_t)(kNB - 1);
         if (use_mw((int)npMax)) TRY(mw_alloc(c, 6 * NP, &mwBase));
@@ -3158,11 +3335,14 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         const bool merge = merge_errors();
         const LmFuse f{merge ? nbB - 1 : nbE, nbB, maxTrials, iterations, o->fixed_iterations ? 1 : 0, d_freePoses,
                        d_trace};
+        const bool extraB = std::getenv("ORB_LBA_EXTRA_BOUNDARY") != nullptr;
+        auto boundary = [&]() { if (extraB) hipLaunchKernelGGL(k_nop, dim3(256), dim3(64), 0, s); };
         if (d.nact > 0) hipLaunchKernelGGL(k_edge_lin, dim3(nbE), dim3(64), 0, s, d, hm, hsv, fuse ? 1 : 0, f);
+        boundary();
         LbaDev dv = d;
         if (fuse) dv.lm = d.lmMid;
         const bool merged = fuse && !first && nbV > 0;
-        if (merged) hipLaunchKernelGGL(k_vertex_schur, dim3(nbV), dim3(256), 0, s, d, nbE);
+        if (merged) { hipLaunchKernelGGL(k_vertex_schur, dim3(nbV), dim3(256), 0, s, d, nbE); boundary(); }
         else if (nbV > 0) hipLaunchKernelGGL(k_vertex_reduce, dim3(nbV), dim3(256), 0, s, dv);
         if (single) {
             if (!fuse) hipLaunchKernelGGL(k_lm_begin_fused, dim3(1), dim3(64), 0, s, d, nbE, nbV);
@@ -3182,7 +3362,17 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         if (d.M > 0 && !merged)
             hipLaunchKernelGGL(k_point_schur, dim3((d.M + 63) / 64), dim3(64), 0, s, d, fuse ? 1 : 0, nbE, nbV);
         const int npairs = d.P * (d.P + 1) / 2;
-        if (npairs > 0) hipLaunchKernelGGL(k_schur_pairs, dim3(npairs), dim3(kSpT), 0, s, d, root ? 1 : 0);
+        if (schurMfma && d.P > 0 && d.M > 0) {
+            const int npm = (6 * d.P + 15) & ~15, T = npm / 16, nt = T * (T + 1) / 2;
+            const int nch = (d.M + kYLm - 1) / kYLm;
+            hipLaunchKernelGGL(k_schur_ymat, dim3((d.M + kYLmB - 1) / kYLmB), dim3(256), 0, s, d, d_Yt, npm, d_ce);
+            hipLaunchKernelGGL(k_schur_gemm, dim3(nch), dim3(256), 0, s, d, d_Yt, npm, d_ypart);
+            hipLaunchKernelGGL(k_schur_msum, dim3((nt * 256 + 6 * d.P + 255) / 256), dim3(256), 0, s, d, d_ypart, nch, npm,
+                               d_ce, root ? 1 : 0);
+        } else if (npairs > 0) {
+            hipLaunchKernelGGL(k_schur_pairs, dim3(npairs), dim3(kSpT), 0, s, d, root ? 1 : 0);
+            boundary();
+        }
         if (d.P > 0) TRY(comm_allreduce_g(c, d.S, (size_t)36 * d.P * d.P + 6 * (size_t)d.P, 0, d.lm, 1));
         if (prof) (void)hipEventRecord(ev[2], s);
         if (d.P > 0) {
@@ -3190,10 +3380,11 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
             PoseTail pt{};
             if (merge)
                 pt = PoseTail{d.q, d.t, d.bq, d.bt, d.partScale + (nbB - 1), d.bp, d_freePoses, d.poseIdx, d.P};
-            if (np <= kLdlLdsMaxN)
+            if (np <= kLdlLdsMaxN) {
                 hipLaunchKernelGGL(k_ldlt_solve<true>, dim3(1), dim3(kLdlT), ((size_t)np * (np + 1) + 3 * (size_t)np + 256 + (size_t)kNB * (np + 1) + 64) * 8,
                                    s, d.S, d.bs, n, nullptr, d.x, d.flags, d.lm, pt);
-            else if (use_mw(np))
+                boundary();
+            } else if (use_mw(np))
                 enqueue_ldlt_mw(s, mw_order(mwBase, n), d.S, d.bs, d.x, d.flags, d.lm, pt);
             else
                 hipLaunchKernelGGL(k_ldlt_solve<false>, dim3(1), dim3(kLdlT), (3 * (size_t)np + 64) * 8, s, d.S, d.bs, n,
@@ -3204,6 +3395,7 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         if (prof) (void)hipEventRecord(ev[3], s);
         if (merge) {
             hipLaunchKernelGGL(k_backsub_errors, dim3(nbB - 1), dim3(256), 0, s, d, hm, hsv);
+            boundary();
         } else {
             hipLaunchKernelGGL(k_backsub_update, dim3(nbB), dim3(256), 0, s, d, d_freePoses);
             if (d.nact > 0) hipLaunchKernelGGL(k_edge_errors, dim3(nbE), dim3(64), 0, s, d, hm, hsv, 1, fuse ? 1 : 0);
@@ -3267,7 +3459,7 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
                 LbaDev d;
                 const void* ptrs[4];
                 double h[2];
-                int v[7];
+                int v[8];
             } k;
             std::memset(&k, 0, sizeof(k));
             k.d = d;
@@ -3276,6 +3468,7 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
             k.v[0] = iterations; k.v[1] = maxTrials; k.v[2] = o->fixed_iterations; k.v[3] = root; k.v[4] = nslots;
             k.v[5] = firstGroup ? 1 : 0;
             k.v[6] = close ? 1 : 0;
+            k.v[7] = (schurMfma ? 1 : 0) | (std::getenv("ORB_LBA_EXTRA_BOUNDARY") ? 2 : 0);
             std::vector<char> key(reinterpret_cast<const char*>(&k), reinterpret_cast<const char*>(&k) + sizeof(k));
             for (size_t i = 0; i < c->graphs.size(); i++)
                 if (c->graphs[i].key == key) {   // most recently used last: eviction takes the front
@@ -3466,6 +3659,270 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
                 std::chrono::duration<double, std::micro>(hT[0] - hEntry).count());
 #endif
     ORB_HIP_TRY(hipGetLastError());
+    return ORB_OK;
+}
+
+
+// ------------------------------------------------------------------ device group (one process, N GPUs)
+// LocalBundleAdjustment sharded over the GPUs of one process, the drop-in's model (LocalMapping
+// runs the local BA on one thread, R/src/LocalMapping.cpp:94-95).  Rank r (context on devices[r])
+// owns the landmark range [r M / n, (r+1) M / n), as lba_set_comm; the collectives are the library's
+// own: a one-shot peer-to-peer all-reduce kernel (k_peer_allreduce) in which every rank reads every
+// rank's workspace slice through peer access over xGMI and sums it in rank order, so all ranks hold
+// bitwise the same reduced system and take the same LM decisions.  Each collective is ordered by
+// events between the ranks' streams: rank r records "ready", waits for its peers' ready events,
+// reduces into its own result buffer, records "read", and waits for its peers' read events before
+// anything may overwrite its workspace; a host spin barrier between the records makes sure every
+// event a stream waits on has been recorded.  One host thread per rank runs lba_solve.
+constexpr int kMaxGroup = 16;
+struct PeerPtrs {
+    const double* p[kMaxGroup];
+};
+__global__ __launch_bounds__(256) void k_peer_allreduce(PeerPtrs in, int nr, size_t n, int op, double* __restrict__ out) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        double v = in.p[0][i];
+        for (int r = 1; r < nr; r++) {
+            const double w = in.p[r][i];
+            v = op ? fmax(v, w) : v + w;
+        }
+        out[i] = v;
+    }
+}
+
+struct lba_group {
+    int n = 0;
+    std::vector<int> dev;
+    std::vector<lba_context*> ctx;
+    std::vector<double*> ws, res;
+    size_t wsDoubles = 0;
+    std::vector<hipEvent_t> evReady, evRead;
+    std::atomic<int> arrive{0};
+    std::atomic<unsigned> bgen{0};
+    std::atomic<bool> abort{false};
+    struct Rank {
+        lba_group* g;
+        int r;
+    } ranks[kMaxGroup];
+    // exchange timing on rank 0's stream: (before ready, after the peers' read) per collective
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;
+    size_t ntev = 0;
+    double exchangeMs = 0.0;
+    long exchanges = 0;
+};
+
+static bool group_barrier(lba_group* g) {
+    const unsigned gen = g->bgen.load(std::memory_order_acquire);
+    if (g->arrive.fetch_add(1, std::memory_order_acq_rel) + 1 == g->n) {
+        g->arrive.store(0, std::memory_order_relaxed);
+        g->bgen.fetch_add(1, std::memory_order_acq_rel);
+        return !g->abort.load();
+    }
+    for (int spins = 0; g->bgen.load(std::memory_order_acquire) == gen; spins++) {
+        if (g->abort.load()) return false;
+        if (spins > 256) std::this_thread::yield();
+    }
+    return !g->abort.load();
+}
+
+static int group_allreduce(void* user, size_t off, size_t cnt, int op) {
+    auto* rk = static_cast<lba_group::Rank*>(user);
+    lba_group* g = rk->g;
+    const int r = rk->r, n = g->n;
+    lba_context* c = g->ctx[r];
+    hipStream_t s = c->stream;
+    if (hipSetDevice(c->device) != hipSuccess) return 1;
+    hipEvent_t t0 = nullptr, t1 = nullptr;
+    if (r == 0) {
+        if (g->ntev == g->tev.size()) {
+            hipEvent_t a, b;
+            if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return 1;
+            g->tev.push_back({a, b});
+        }
+        t0 = g->tev[g->ntev].first;
+        t1 = g->tev[g->ntev].second;
+        g->ntev++;
+        if (hipEventRecord(t0, s) != hipSuccess) return 1;
+    }
+    if (hipEventRecord(g->evReady[r], s) != hipSuccess) return 1;
+    if (!group_barrier(g)) return 1;
+    for (int p = 0; p < n; p++)
+        if (p != r && hipStreamWaitEvent(s, g->evReady[p], 0) != hipSuccess) return 1;
+    PeerPtrs pp{};
+    for (int p = 0; p < n; p++) pp.p[p] = g->ws[p] + off;
+    const unsigned blocks = (unsigned)std::max<size_t>(1, std::min<size_t>(1024, (cnt + 255) / 256));
+    hipLaunchKernelGGL(k_peer_allreduce, dim3(blocks), dim3(256), 0, s, pp, n, cnt, op, g->res[r] + off);
+    if (hipGetLastError() != hipSuccess) return 1;
+    if (hipEventRecord(g->evRead[r], s) != hipSuccess) return 1;
+    if (!group_barrier(g)) return 1;
+    for (int p = 0; p < n; p++)
+        if (p != r && hipStreamWaitEvent(s, g->evRead[p], 0) != hipSuccess) return 1;
+    if (r == 0 && hipEventRecord(t1, s) != hipSuccess) return 1;
+    return 0;
+}
+
+static void group_free_ws(lba_group* g) {
+    for (int r = 0; r < g->n; r++) {
+        (void)hipSetDevice(g->dev[r]);
+        if (g->ws[r]) (void)hipFree(g->ws[r]);
+        if (g->res[r]) (void)hipFree(g->res[r]);
+        g->ws[r] = g->res[r] = nullptr;
+    }
+    g->wsDoubles = 0;
+}
+
+void lba_group_destroy(lba_group* g) {
+    if (!g) return;
+    for (int r = 0; r < g->n; r++)
+        if (g->ctx[r]) {
+            (void)hipSetDevice(g->dev[r]);
+            (void)hipStreamSynchronize(g->ctx[r]->stream);
+        }
+    group_free_ws(g);
+    for (int r = 0; r < g->n; r++) {
+        (void)hipSetDevice(g->dev[r]);
+        if (g->evReady[r]) (void)hipEventDestroy(g->evReady[r]);
+        if (g->evRead[r]) (void)hipEventDestroy(g->evRead[r]);
+        if (g->ctx[r]) lba_destroy(g->ctx[r]);
+    }
+    if (!g->dev.empty()) (void)hipSetDevice(g->dev[0]);
+    for (auto& e : g->tev) {
+        (void)hipEventDestroy(e.first);
+        (void)hipEventDestroy(e.second);
+    }
+    delete g;
+}
+
+int lba_group_create(const int* devices, int n, lba_group** out) {
+    if (!devices || !out || n < 1 || n > kMaxGroup) return ORB_EINVAL;
+    *out = nullptr;
+    lba_group* g = new lba_group();
+    g->n = n;
+    g->dev.assign(devices, devices + n);
+    g->ctx.assign(n, nullptr);
+    g->ws.assign(n, nullptr);
+    g->res.assign(n, nullptr);
+    g->evReady.assign(n, nullptr);
+    g->evRead.assign(n, nullptr);
+    for (int r = 0; r < n; r++) {
+        g->ranks[r] = {g, r};
+        int st = lba_create(devices[r], &g->ctx[r]);
+        if (st) { lba_group_destroy(g); return st; }
+        if (hipEventCreateWithFlags(&g->evReady[r], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&g->evRead[r], hipEventDisableTiming) != hipSuccess) {
+            lba_group_destroy(g);
+            return ORB_EGPU;
+        }
+    }
+    // peer access between every pair of distinct devices (xGMI)
+    for (int a = 0; a < n; a++)
+        for (int b = 0; b < n; b++) {
+            if (devices[a] == devices[b]) continue;
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, devices[a], devices[b]) != hipSuccess || !can) {
+                lba_group_destroy(g);
+                return ORB_ENODEV;
+            }
+            (void)hipSetDevice(devices[a]);
+            const hipError_t e = hipDeviceEnablePeerAccess(devices[b], 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+                lba_group_destroy(g);
+                return ORB_EGPU;
+            }
+            (void)hipGetLastError();
+        }
+    *out = g;
+    return ORB_OK;
+}
+
+int lba_group_solve(lba_group* g, const lba_problem* p, const lba_options* o, const volatile uint8_t* stop,
+                    lba_result* r) {
+    if (!g || !p || !o || !r || p->n_poses < 0 || p->n_points < 0 || p->n_edges < 0) return ORB_EINVAL;
+    const int n = g->n;
+    if (n == 1) return lba_solve(g->ctx[0], p, o, stop, r);
+    const size_t NP = (size_t)p->n_poses, NM = (size_t)p->n_points, NE = (size_t)p->n_edges;
+    const size_t need = std::max(36 * NP * NP + 6 * NP, NE) + 64;
+    if (need > g->wsDoubles) {
+        group_free_ws(g);
+        for (int q = 0; q < n; q++) {
+            ORB_HIP_TRY(hipSetDevice(g->dev[q]));
+            if (hipMalloc((void**)&g->ws[q], need * 8) != hipSuccess || hipMalloc((void**)&g->res[q], need * 8) != hipSuccess) {
+                group_free_ws(g);
+                return ORB_ENOMEM;
+            }
+        }
+        g->wsDoubles = need;
+    }
+    for (int q = 0; q < n; q++) {
+        TRY(lba_set_comm(g->ctx[q], q, n, g->ws[q], g->wsDoubles, group_allreduce, &g->ranks[q]));
+        g->ctx[q]->wsOut = g->res[q];
+    }
+    g->abort.store(false);
+    g->arrive.store(0);
+    g->ntev = 0;
+    // every rank writes its own copy of the outputs; the owners' slices are merged below
+    struct Out {
+        std::vector<double> q, t, X, chi, trace;
+        std::vector<uint8_t> er;
+        lba_result res{};
+    };
+    std::vector<Out> outs(n);
+    for (int q = 0; q < n; q++) {
+        Out& u = outs[q];
+        u.q.assign(4 * NP + 1, 0.0); u.t.assign(3 * NP + 1, 0.0); u.X.assign(3 * NM + 1, 0.0);
+        u.chi.assign(NE + 1, 0.0); u.er.assign(NE + 1, 0); u.trace.assign(4 * 64, 0.0);
+        u.res = lba_result{u.q.data(), u.t.data(), u.X.data(), u.er.data(), u.chi.data(), {0, 0}, 0,
+                           q == 0 && r->trace ? u.trace.data() : nullptr, 0, 0};
+    }
+    std::vector<int> st(n, ORB_OK);
+    auto run = [&](int q) {
+        st[q] = lba_solve(g->ctx[q], p, o, stop, &outs[q].res);
+        if (st[q] != ORB_OK) g->abort.store(true);
+    };
+    std::vector<std::thread> th;
+    for (int q = 1; q < n; q++) th.emplace_back(run, q);
+    run(0);
+    for (auto& t : th) t.join();
+    for (int q = 0; q < n; q++)
+        if (st[q] != ORB_OK) return st[q];
+    // rank 0's exchange timing (its stream is idle: lba_solve waited for its last group)
+    if (g->ntev) {
+        ORB_HIP_TRY(hipSetDevice(g->dev[0]));
+        for (size_t i = 0; i < g->ntev; i++) {
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, g->tev[i].first, g->tev[i].second) == hipSuccess) g->exchangeMs += ms;
+        }
+        g->exchanges += (long)g->ntev;
+    }
+    const lba_result& r0 = outs[0].res;
+    if (r->pose_q) std::memcpy(r->pose_q, outs[0].q.data(), 32 * NP);
+    if (r->pose_t) std::memcpy(r->pose_t, outs[0].t.data(), 24 * NP);
+    for (int q = 0; q < n; q++) {   // landmark shards: [q M / n, (q+1) M / n) from rank q
+        const size_t a = (size_t)((long long)NM * q / n), b = (size_t)((long long)NM * (q + 1) / n);
+        if (r->point_xyz && b > a) std::memcpy(r->point_xyz + 3 * a, outs[q].X.data() + 3 * a, 24 * (b - a));
+    }
+    for (size_t e = 0; e < NE; e++) {   // each edge's chi2 / erase flag from its landmark's owner (others 0)
+        double c2 = 0.0;
+        uint8_t er = 0;
+        for (int q = 0; q < n; q++) { c2 += outs[q].chi[e]; er |= outs[q].er[e]; }
+        if (r->edge_chi2) r->edge_chi2[e] = c2;
+        if (r->edge_erase) r->edge_erase[e] = er;
+    }
+    r->iterations[0] = r0.iterations[0];
+    r->iterations[1] = r0.iterations[1];
+    r->trials = r0.trials;
+    r->aborted = r0.aborted;
+    r->n_trace = 0;
+    if (r->trace && r0.n_trace > 0) {
+        std::memcpy(r->trace, outs[0].trace.data(), 32 * (size_t)r0.n_trace);
+        r->n_trace = r0.n_trace;
+    }
+    return ORB_OK;
+}
+
+int lba_group_stats(lba_group* g, double* exchange_ms, long* n_exchanges) {
+    if (!g) return ORB_EINVAL;
+    if (exchange_ms) *exchange_ms = g->exchangeMs;
+    if (n_exchanges) *n_exchanges = g->exchanges;
     return ORB_OK;
 }
 

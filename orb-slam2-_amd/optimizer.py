@@ -70,7 +70,10 @@ def _sig():
                             ("lba_debug_buffer", [vp, i32, vp, sz], C.c_int),
                             ("lba_dense_solve", [vp, vp, vp, i32, vp], C.c_int), ("lba_pose_from_Tcw", [vp, vp, vp], None),
                             ("lba_pose_to_Tcw", [vp, vp, vp], None),
-                            ("lba_poses_from_Tcw", [vp, i32, vp, vp], None)]:
+                            ("lba_poses_from_Tcw", [vp, i32, vp, vp], None),
+                            ("lba_group_create", [vp, i32, vp], C.c_int), ("lba_group_destroy", [vp], None),
+                            ("lba_group_solve", [vp, vp, vp, vp, vp], C.c_int),
+                            ("lba_group_stats", [vp, vp, vp], C.c_int)]:
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res
@@ -225,6 +228,76 @@ class LocalBA:
         out["aborted"] = bool(r.aborted)
         out["init_q"], out["init_t"] = q, t
         return out
+
+
+def _marshal(prob):
+    """lba_problem / lba_result structs over numpy copies of `prob` (kept alive in the tuple)."""
+    nk = len(prob["Tcw"])
+    Tcw = np.ascontiguousarray(prob["Tcw"], np.float32)
+    q, t = np.zeros((nk, 4)), np.zeros((nk, 3))
+    _sig().lba_poses_from_Tcw(_abi.ptr(Tcw), nk, _abi.ptr(q), _abi.ptr(t))   # Converter::toSE3Quat
+    a = {k: np.ascontiguousarray(v, PROBLEM_DTYPES[k]) if k in PROBLEM_DTYPES and v is not None else v
+         for k, v in prob.items()}
+    P = _abi.ptr
+    pr = LbaProblem(nk, P(q), P(t), P(a["pose_fixed"]), P(a["pose_id"]), len(a["point_xyz"]), P(a["point_xyz"]),
+                    P(a["point_id"]), P(a.get("point_bad")), len(a["edge_point"]), P(a["edge_point"]),
+                    P(a["edge_pose"]), P(a["edge_stereo"]), P(a["edge_obs"]), P(a["edge_info"]), P(a["edge_cam"]))
+    ne = len(a["edge_point"])
+    out = dict(pose_q=np.zeros((nk, 4)), pose_t=np.zeros((nk, 3)), point_xyz=a["point_xyz"].copy(),
+               edge_erase=np.zeros(ne, np.uint8), edge_chi2=np.zeros(ne), trace=np.zeros((64, 4)))
+    r = LbaResult(P(out["pose_q"]), P(out["pose_t"]), P(out["point_xyz"]), P(out["edge_erase"]),
+                  P(out["edge_chi2"]), (C.c_int * 2)(0, 0), 0, P(out["trace"]), 0, 0)
+    return pr, r, out, (q, t, a, Tcw)
+
+
+class LocalBAGroup:
+    """Multi-GPU LocalBundleAdjustment from one process (lba_group_*): one context per entry of
+    `devices` (a device may repeat), landmarks sharded over them, the reduced system all-reduced
+    by the library's peer-to-peer kernel over xGMI."""
+
+    def __init__(self, devices):
+        devs = (C.c_int * len(devices))(*[int(d) for d in devices])
+        h = C.c_void_p()
+        _abi.check("lba_group_create", _sig().lba_group_create(devs, len(devices), C.byref(h)))
+        self._h = h
+        self.devices = list(devices)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _sig().lba_group_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def prepared(self, prob, opts=None):
+        opts = opts or options()
+        pr, r, out, keep = _marshal(prob)
+        flag = (C.c_uint8 * 1)(0)
+        fn, h = _sig().lba_group_solve, self._h
+
+        def call():
+            _abi.check("lba_group_solve", fn(h, C.byref(pr), C.byref(opts), flag, C.byref(r)))
+            return (r.iterations[0], r.iterations[1]), r.trials, (keep, out)
+        return call
+
+    def solve(self, prob, opts=None, stop=None):
+        opts = opts or options()
+        pr, r, out, keep = _marshal(prob)
+        flag = stop if stop is not None else (C.c_uint8 * 1)(0)
+        _abi.check("lba_group_solve", _sig().lba_group_solve(self._h, C.byref(pr), C.byref(opts), flag, C.byref(r)))
+        out["iterations"] = (r.iterations[0], r.iterations[1])
+        out["trials"] = r.trials
+        out["trace"] = out["trace"][: r.n_trace]
+        out["aborted"] = bool(r.aborted)
+        out["init_q"], out["init_t"] = keep[0], keep[1]
+        return out
+
+    def stats(self):
+        """(total exchange ms on rank 0's stream, number of collectives) since creation."""
+        ms, n = C.c_double(), C.c_long()
+        _abi.check("lba_group_stats", _sig().lba_group_stats(self._h, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
 
 
 class Optimizer:

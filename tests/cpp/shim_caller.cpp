@@ -7,6 +7,7 @@
 //   shim_caller sbp IN OUT       ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono)
 //   shim_caller sbl IN OUT       ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th)
 //   shim_caller lba IN OUT       Optimizer::LocalBundleAdjustment on a mock keyframe / map-point graph
+//   shim_caller lbag IN OUT      the same through the device-list overload (lba_group, several GPUs)
 // IN / OUT: little-endian arrays, each written as int64 element count + raw elements.
 // Exit status: 0 ok, 3 the library reported an error (e.g. no gfx950 device), 2 bad usage.
 #include <cstdio>
@@ -295,7 +296,7 @@ static void run_sbl(FILE* in, FILE* out) {
     wr(out, read_slots(F, ptr, withObs, noObs));
 }
 
-static void run_lba(FILE* in, FILE* out) {
+static void run_lba(FILE* in, FILE* out, bool group) {
     const auto Tcw = rd<float>(in);
     const auto fixedCam = rd<uint8_t>(in);
     const auto kfId = rd<int64_t>(in);
@@ -307,6 +308,7 @@ static void run_lba(FILE* in, FILE* out) {
     const auto cam = rd<float>(in);
     const auto invSig2 = rd<float>(in);
     const auto stopFlag = rd<uint8_t>(in);
+    const std::vector<int32_t> devices = group ? rd<int32_t>(in) : std::vector<int32_t>();
     const size_t nk = fixedCam.size(), np = mpId.size(), ne = ePt.size();
     std::vector<mock::KeyFrame> kfs(nk);
     std::vector<mock::MapPoint> mps(np);
@@ -342,7 +344,10 @@ static void run_lba(FILE* in, FILE* out) {
     mock::Map map;
     bool stop = stopFlag[0] != 0;
     orbslam2_amd::LbaDump D;
-    orbslam2_amd::LocalBundleAdjustment(pKF, &stop, &map, &D);
+    if (group)   // the multi-GPU overload: landmarks sharded over the listed devices
+        orbslam2_amd::LocalBundleAdjustment(pKF, &stop, &map, std::vector<int>(devices.begin(), devices.end()), &D);
+    else
+        orbslam2_amd::LocalBundleAdjustment(pKF, &stop, &map, &D);
     wr(out, D.pose_q); wr(out, D.pose_t); wr(out, D.pose_fixed); wr(out, D.pose_id);
     wr(out, D.point_xyz); wr(out, D.point_id); wr(out, D.point_bad);
     wr(out, D.edge_point); wr(out, D.edge_pose); wr(out, D.edge_stereo); wr(out, D.edge_obs); wr(out, D.edge_info);
@@ -370,7 +375,7 @@ static void run_lba(FILE* in, FILE* out) {
 
 int main(int argc, char** argv) {
     if (argc != 4) {
-        std::fprintf(stderr, "usage: %s extract|sfi|sbp|sbl|lba IN OUT\n", argv[0]);
+        std::fprintf(stderr, "usage: %s extract|sfi|sbp|sbl|lba|lbag IN OUT\n", argv[0]);
         return 2;
     }
     FILE* in = std::fopen(argv[2], "rb");
@@ -382,7 +387,8 @@ int main(int argc, char** argv) {
         else if (mode == "sfi") run_sfi(in, out);
         else if (mode == "sbp") run_sbp(in, out);
         else if (mode == "sbl") run_sbl(in, out);
-        else if (mode == "lba") run_lba(in, out);
+        else if (mode == "lba") run_lba(in, out, false);
+        else if (mode == "lbag") run_lba(in, out, true);
         else return 2;
     } catch (const std::exception& e) {
         std::fprintf(stderr, "%s\n", e.what());

@@ -176,20 +176,26 @@ def test_shim_search_by_projection_local_matches_oracle(shim, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("stereo", [0.0, 0.4])
-def test_shim_local_bundle_adjustment(shim, tmp_path, amd, stereo):
+@pytest.mark.parametrize("stereo,group", [(0.0, None), (0.4, None), (0.4, 2)])
+def test_shim_local_bundle_adjustment(shim, tmp_path, amd, stereo, group):
+    """group: the device-list overload (lba_group over `group` contexts, sharing the device on a
+    one-GPU machine) — the same gathering and write-back, the same LM decisions."""
     from orb_slam2_amd import synth
     pb = synth.ba_problem(n_local=8, n_fixed=3, n_points=900, stereo_frac=stereo, seed=11)
     inv_sigma2 = (np.float32(1.0) / np.array([np.float32(1.2) ** (2 * l) for l in range(8)], np.float32))
     octave = np.array([int(np.argmin(np.abs(inv_sigma2.astype(np.float64) - i))) for i in pb["edge_info"]], np.int32)
     nk = len(pb["Tcw"])
     cam = np.asarray(pb["edge_cam"][0], np.float32)
-    r, outp = _run(shim, "lba", tmp_path, np.asarray(pb["Tcw"], np.float32).reshape(-1),
+    extra = []
+    if group:
+        import torch
+        extra = [np.array([r % torch.cuda.device_count() for r in range(group)], np.int32)]
+    r, outp = _run(shim, "lbag" if group else "lba", tmp_path, np.asarray(pb["Tcw"], np.float32).reshape(-1),
                    np.asarray(pb["pose_fixed"], np.uint8), np.asarray(pb["pose_id"], np.int64),
                    np.asarray(pb["point_xyz"], np.float32).reshape(-1), np.asarray(pb["point_id"], np.int64),
                    np.asarray(pb["edge_point"], np.int32), np.asarray(pb["edge_pose"], np.int32),
                    np.asarray(pb["edge_obs"], np.float32).reshape(-1), octave, cam, inv_sigma2,
-                   np.zeros(1, np.uint8))
+                   np.zeros(1, np.uint8), *extra)
     assert r.returncode == 0, r.stderr
     (pq, pt, pfix, pid, X, xid, xbad, ept, eps, est, eobs, einfo, ecam, erase, oq, ot, ox, st, Tout, Xout, upd,
      nobs, elog) = _read(outp, np.float64, np.float64, np.uint8, np.int64, np.float64, np.int64, np.uint8, np.int32,
@@ -218,6 +224,8 @@ def test_shim_local_bundle_adjustment(shim, tmp_path, amd, stereo):
                 edge_cam=ecam.reshape(-1, 5))
     ref = amd.LocalBA().solve(prob)
     assert tuple(st[:2]) == ref["iterations"] and int(st[2]) == ref["trials"] and int(st[3]) == 0
+    if group:   # sharded sums: the same decisions, estimates to rounding; compare with the group solve
+        ref = amd.LocalBAGroup(extra[0].tolist()).solve(prob)
     # ... and within the oracle's tolerances (tests/test_lba_gpu.py): same LM decisions, same erase set
     orc = O.lba_solve(prob)
     assert tuple(st[:2]) == orc["iterations"] and int(st[2]) == orc["trials"]

@@ -274,3 +274,16 @@ def test_scaled_local_ba_bitwise_reproducible(amd):
     for r in runs[1:]:
         for k in ("pose_q", "pose_t", "point_xyz", "edge_chi2", "trace", "edge_erase"):
             assert np.array_equal(r[k], runs[0][k]), k
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(stereo_frac=0.5, seed=7)])
+def test_schur_mfma_mode_matches_oracle(amd, monkeypatch, kw):
+    """ORB_LBA_SCHUR_MFMA=1: the Schur complement as the densified f64 MFMA GEMM S -= Y Y^T
+    (k_schur_ymat / k_schur_gemm / k_schur_msum, the A/B of SURVEY 8d) within the oracle's
+    tolerances, and bitwise reproducible."""
+    monkeypatch.setenv("ORB_LBA_SCHUR_MFMA", "1")
+    pb = _problem(amd, **kw)
+    got = amd.LocalBA().solve(pb)
+    _compare(O.lba_solve(pb), got)
+    again = amd.LocalBA().solve(pb)
+    assert np.array_equal(again["trace"], got["trace"]) and np.array_equal(again["point_xyz"], got["point_xyz"])

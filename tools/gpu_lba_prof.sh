@@ -6,8 +6,9 @@ cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
 prof() {   # name, env, args
-  timeout -k 10 300 env $2 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$1 -o run -- python3 $R/tools/lba_timing.py $3 > $R/gpurun_out/prof_$1.log 2>&1
+  timeout -k 10 300 env $2 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$1 -o run -- python3 $R/tools/lba_timing.py $3 > $R/gpurun_out/prof_$1.log 2>&1
   f=$(find $R/gpurun_out/prof_$1 -name "*kernel_stats.csv" | head -1)
+  [ -n "$f" ] || { tail -5 $R/gpurun_out/prof_$1.log; exit 1; }
   python3 $R/tools/stats_summary.py $f $R/gpurun_out/prof_$1_stats.txt "$4"
   grep median $R/gpurun_out/prof_$1.log
   head -14 $R/gpurun_out/prof_$1_stats.txt
