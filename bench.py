@@ -96,6 +96,7 @@ def parse():
     ap.add_argument("--lba-solves", type=int, default=10, help="timed LocalBundleAdjustment calls")
     ap.add_argument("--lba-points", type=int, default=3000)
     ap.add_argument("--lba-kf", type=int, default=20)
+    ap.add_argument("--no-lba-scaled", action="store_true", help="skip the 60 KF / 200 KF corridor windows")
     ap.add_argument("--lba-comm", choices=["native", "torch"], default="native",
                     help="N>1 local BA: the library's device group driven by rank 0 (native) or one rank per "
                          "GPU with a torch.distributed all-reduce callback (torch)")
@@ -242,14 +243,27 @@ def bench_lba(args, amd, dev, local, rank, world):
     pb = synth.ba_problem(n_local=args.lba_kf, n_points=args.lba_points)
     nk, ne = len(pb["Tcw"]), len(pb["edge_point"])
     native = world > 1 and args.lba_comm == "native"
+    fallback = None
     if native:
         # the drop-in's multi-GPU path: ONE process (rank 0, LocalMapping's thread) drives a group
         # of contexts on all the ranks' devices; the library's peer-to-peer all-reduce over xGMI
-        # carries the exchange (lba_group_*); the other ranks wait at the barrier
+        # carries the exchange (lba_group_*); the other ranks wait at the barrier.  Without peer
+        # access between the devices the group cannot form: every rank then takes the torch path.
         ndev = torch.cuda.device_count()
         devices = [r % ndev for r in range(world)]
-        ctx = amd.LocalBAGroup(devices) if rank == 0 else None
-    else:
+        ok = torch.ones(1, dtype=torch.float64, device=dev)
+        ctx = None
+        if rank == 0:
+            try:
+                ctx = amd.LocalBAGroup(devices)
+            except RuntimeError as exc:
+                fallback = str(exc)
+                ok.zero_()
+        torch.distributed.broadcast(ok, src=0)
+        if ok.item() == 0:
+            native = False
+            fallback = fallback or "lba_group_create failed on rank 0"
+    if not native:
         ctx = amd.LocalBA(local)
         # a dedicated stream (the legacy default stream cannot be captured into the LM slot graph);
         # RCCL calls of the all-reduce callback are issued on the same stream
@@ -311,6 +325,7 @@ def bench_lba(args, amd, dev, local, rank, world):
            "solve_ms": round(1000 * tot / args.lba_solves, 3),
            "iterations_per_solve": iters / args.lba_solves, "trials": r["trials"],
            "n_gpus": world,
+           "native_group_unavailable": fallback,
            "collective": ("none" if world == 1 else
                           "library peer-to-peer all-reduce over xGMI (lba_group, one process driving every device)"
                           if native else "torch.distributed all_reduce callback (RCCL), one process per GPU"),
@@ -355,6 +370,67 @@ def bench_lba(args, amd, dev, local, rank, world):
         out["speedup_vs_cpu"] = round(out["cpu_baseline"]["ms_per_iter"] / out["ms_per_iter"], 2)
         out["speedup_vs_cpu_openmp"] = round(out["cpu_baseline_openmp"]["ms_per_iter"] / out["ms_per_iter"], 2)
     if native:   # rank 0 -> the waiting ranks
+        torch.distributed.barrier()
+        torch.distributed.broadcast_object_list([out], src=0)
+    return out
+
+
+def bench_lba_scaled(args, amd, dev, rank, world):
+    """SURVEY 8d's scaled local-BA windows (the reduced system beyond the LDS image: the
+    multi-workgroup LDL^T and the pair-list Schur complement): corridor windows of 60 KF x 8,000
+    and 200 KF x 100,000 points with banded covisibility (synth.ba_problem_corridor).  N > 1:
+    rank 0 drives the device group (lba_group) over every rank's device, as bench_lba does.
+    At N = 1 the oracle's OpenMP variant is timed beside it on one solve."""
+    from orb_slam2_amd import synth
+    sizes = ((60, 8000), (200, 100000))
+    native = world > 1
+    if native and rank != 0:
+        torch.distributed.barrier()
+        obj = [None]
+        torch.distributed.broadcast_object_list(obj, src=0)
+        return obj[0]
+    out = {}
+    for nl, npts in sizes:
+        pb = synth.ba_problem_corridor(n_local=nl, n_fixed=4, n_points=npts)
+        if native:
+            ndev = torch.cuda.device_count()
+            ctx = amd.LocalBAGroup([r % ndev for r in range(world)])
+        else:
+            ctx = amd.LocalBA(dev.index or 0)
+        call = ctx.prepared(pb)
+        for _ in range(2):
+            call()
+        times, iters = [], 0
+        for _ in range(5):
+            t0 = time.perf_counter()
+            its, tr, _ = call()
+            times.append(time.perf_counter() - t0)
+            iters += sum(its)
+        fixed = pb["pose_fixed"].astype(bool)
+        P = int(np.count_nonzero(~fixed))
+        T = (6 * P + 15) // 16
+        tiles = sum((T - k - 1) * (T - k) // 2 for k in range(T))
+        key = f"{nl}kf_{npts // 1000}k"
+        out[key] = {"keyframes": nl, "fixed": 4, "points": npts, "edges": int(len(pb["edge_point"])),
+                    "reduced_order": 6 * P, "ms_per_iter": round(1000 * sum(times) / max(iters, 1), 4),
+                    "solve_ms": round(1000 * float(np.median(times)), 3), "iterations_per_solve": iters / 5,
+                    "trials_per_solve": tr, "ldlt_mfma_flops_per_trial": tiles * 8192}
+        if world == 1 and not args.no_cpu:
+            sys.path.insert(0, str(ROOT / "tests"))
+            import oracle_ref as O
+            th = host_threads()
+            t0 = time.perf_counter()
+            rr = O.lba_solve(pb, threads=th)
+            dt = time.perf_counter() - t0
+            out[key]["cpu_baseline_openmp"] = {"ms_per_iter": round(1000 * dt / sum(rr["iterations"]), 3),
+                                               "cores": th, "kind": "port", "cpu_model": host_info()["cpu_model"],
+                                               "sample": "one LocalBundleAdjustment solve, oracle_lba_solve_omp"}
+            out[key]["speedup_vs_cpu_openmp"] = round(out[key]["cpu_baseline_openmp"]["ms_per_iter"] /
+                                                      out[key]["ms_per_iter"], 1)
+        del ctx
+    out["note"] = ("corridor windows, banded covisibility; ms_per_iter = lba_solve wall / LM iterations"
+                   + (f"; landmarks sharded over {world} devices by one process (lba_group)" if native else ""))
+    if native:
         torch.distributed.barrier()
         torch.distributed.broadcast_object_list([out], src=0)
     return out
@@ -1208,6 +1284,8 @@ def main():
                                    "ops_source": PMC_VALU.name}
     if not args.no_lba:
         result["lba"] = bench_lba(args, amd, dev, local, rank, world)
+        if not args.no_lba_scaled:
+            result["lba_scaled"] = bench_lba_scaled(args, amd, dev, rank, world)
     if not args.no_stereo:
         result["config5_stereo_sharded"] = bench_config5(args, amd, dev, rank, world)
     if world == 1 and not args.no_extras:

@@ -111,6 +111,8 @@ struct LbaDev {
     double* Ae;                 // [nact][18] Hpl_e D^-1 of the edge's landmark (per trial)
     const int32_t* pairs;       // pose-pair blocks of S with shared landmarks, (bi << 16 | bj), bi <= bj
     const int32_t* npairs;      // their count
+    const int32_t* tripStart;   // per listed pair: first entry of its shared-landmark list, count at +1
+    const int2* trips;          // (act position of pose i's edge, of pose j's edge), landmark order
     double *S, *bs, *x;         // x: [6P + 3M]
     double* red;                // reduction scratch
     double *partChi, *partScale, *partMax;   // per-workgroup partials (single-process LM kernels)
@@ -595,16 +597,28 @@ __device__ __forceinline__ double pose_block_reduce(const LbaDev& d, int p, doub
 #pragma unroll
     for (int u = 0; u < kPoseIdx / 256; u++) idx[tid + 256 * u] = f.k[u];
     __syncthreads();
-    const int n = f.a1 - f.a0, nl = min(n, kPoseIdx);
+    const int n = f.a1 - f.a0;
     double acc = 0.0;
-    for (int jb = g; jb < nl; jb += 8 * kPoseBatch) {   // edges jb, jb + 8, ... of this group
-        double x[kPoseBatch];
+    // the list in chunks of kPoseIdx act positions: the first chunk came with pose_prefetch, the
+    // next ones (poses with more edges, the scaled windows) are staged the same way, so every
+    // value load of a chunk is issued without waiting on an index load
+    for (int c0 = 0; c0 < n; c0 += kPoseIdx) {
+        if (c0 > 0) {
+            __syncthreads();   // the previous chunk's indices are consumed
+            const int last = f.a1 - 1;
 #pragma unroll
-        for (int u = 0; u < kPoseBatch; u++) x[u] = *pose_val_ptr(d, idx[min(jb + 8 * u, nl - 1)], v);
+            for (int u = 0; u < kPoseIdx / 256; u++) idx[tid + 256 * u] = d.poAct[min(f.a0 + c0 + tid + 256 * u, last)];
+            __syncthreads();
+        }
+        const int nl = min(n - c0, kPoseIdx);
+        for (int jb = g; jb < nl; jb += 8 * kPoseBatch) {   // edges jb, jb + 8, ... of this group
+            double x[kPoseBatch];
 #pragma unroll
-        for (int u = 0; u < kPoseBatch; u++) acc = jb + 8 * u < nl ? acc + x[u] : acc;
+            for (int u = 0; u < kPoseBatch; u++) x[u] = *pose_val_ptr(d, idx[min(jb + 8 * u, nl - 1)], v);
+#pragma unroll
+            for (int u = 0; u < kPoseBatch; u++) acc = jb + 8 * u < nl ? acc + x[u] : acc;
+        }
     }
-    for (int j = kPoseIdx + g; j < n; j += 8) acc += *pose_val_ptr(d, d.poAct[f.a0 + j], v);   // long lists
     __syncthreads();   // idx aliases part
     if ((tid & 31) < 27) part[g][tid & 31] = acc;
     __syncthreads();
@@ -758,7 +772,7 @@ __device__ __forceinline__ void hpl_dinv_edges(const LbaDev& d, int l, const dou
         for (int r = 0; r < 6; r++)
 #pragma unroll
             for (int q = 0; q < 3; q++)
-                u[r * 3 + q] = w[r * 3] * Di[q] + w[r * 3 + 1] * Di[3 + q] + w[r * 3 + 2] * Di[6 + q];
+                u[r * 3 + q] = __builtin_fma(w[r * 3 + 2], Di[6 + q], __builtin_fma(w[r * 3 + 1], Di[3 + q], w[r * 3] * Di[q]));
         double2* U = reinterpret_cast<double2*>(d.Ae + 18 * (size_t)k);
 #pragma unroll
         for (int h = 0; h < 9; h++) U[h] = make_double2(u[2 * h], u[2 * h + 1]);
@@ -890,17 +904,11 @@ __global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag) {
     const int pr = d.pairs[blockIdx.x];
     const int phase = d.lm->phase;   // loaded with the pair's CSR ranges (one round trip)
     __shared__ double part[42][kSpT + 1];
-    __shared__ int32_t listJ[kSpList];
     const int tid = threadIdx.x;
     const int bi = pr >> 16, bj = pr & 0xFFFF;
     const bool diag = bi == bj;
-    const int a0 = d.poStart[bi], a1 = d.poStart[bi + 1], b0 = d.poStart[bj], nb = d.poStart[bj + 1] - b0;
+    const int a0 = d.poStart[bi], a1 = d.poStart[bi + 1];
     if (phase != 1) return;   // lm_off(d.lm, 1)
-    const bool inLds = nb <= kSpList;
-    if (!diag && inLds)
-        for (int t = tid; t < nb; t += kSpT) listJ[t] = d.poPt[b0 + t];
-    __syncthreads();
-    const int32_t* Lj = inLds ? listJ : d.poPt + b0;
     double acc[42];
 #pragma unroll
     for (int i = 0; i < 42; i++) acc[i] = 0.0;
@@ -916,16 +924,20 @@ __global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag) {
             u[2 * h] = x.x; u[2 * h + 1] = x.y;
             v[2 * h] = y.x; v[2 * h + 1] = y.y;
         }
+        // three fused multiply-adds per entry (the terms accumulate straight into the partial)
 #pragma unroll
         for (int r = 0; r < 6; r++)
 #pragma unroll
             for (int q = 0; q < 6; q++)
-                acc[r * 6 + q] += u[r * 3] * v[q * 3] + u[r * 3 + 1] * v[q * 3 + 1] + u[r * 3 + 2] * v[q * 3 + 2];
+                acc[r * 6 + q] = __builtin_fma(u[r * 3 + 2], v[q * 3 + 2],
+                                               __builtin_fma(u[r * 3 + 1], v[q * 3 + 1],
+                                                             __builtin_fma(u[r * 3], v[q * 3], acc[r * 6 + q])));
         if (diag) {
             const double* db = d.db + 3 * (size_t)l;
             const double g0 = db[0], g1 = db[1], g2 = db[2];
 #pragma unroll
-            for (int i = 0; i < 6; i++) acc[36 + i] += v[i * 3] * g0 + v[i * 3 + 1] * g1 + v[i * 3 + 2] * g2;
+            for (int i = 0; i < 6; i++)
+                acc[36 + i] = __builtin_fma(v[i * 3 + 2], g2, __builtin_fma(v[i * 3 + 1], g1, __builtin_fma(v[i * 3], g0, acc[36 + i])));
         }
     };
     if (diag) {   // every edge of pose i pairs with itself: already a dense list
@@ -934,55 +946,11 @@ __global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag) {
             product(e1, e1, d.poPt[a]);
         }
     } else {
-        // off-diagonal: chunks of 4 edges per thread of pose i are looked up in pose j's landmark
-        // list (lower_bound), the matches compacted in thread order (a workgroup scan) into `trip`,
-        // then the products run over the dense list: no lane idles through a product for an edge
-        // without a match
-        __shared__ int2 trip[kSpChunk];
-        __shared__ int wtot[kSpT / 64];
-        const int lane = tid & 63, wave = tid >> 6;
-        for (int base = a0; base < a1; base += kSpChunk) {
-            int m1[kSpChunk / kSpT], m2[kSpChunk / kSpT], lm[kSpChunk / kSpT];
-#pragma unroll
-            for (int u = 0; u < kSpChunk / kSpT; u++) {
-                const int a = min(base + tid + kSpT * u, a1 - 1);   // clamped: unconditional loads
-                m1[u] = d.poAct[a];
-                const int lv = d.poPt[a];
-                lm[u] = base + tid + kSpT * u < a1 ? lv : -1;
-            }
-            int cnt = 0;
-#pragma unroll
-            for (int u = 0; u < kSpChunk / kSpT; u++) {
-                const int l = lm[u];
-                int lo = 0, hi = nb;
-                while (lo < hi) {
-                    const int mid = (lo + hi) >> 1;
-                    if (Lj[mid] < l) lo = mid + 1;
-                    else hi = mid;
-                }
-                const bool hit = l >= 0 && lo < nb && Lj[lo] == l;
-                const int e2 = d.poAct[b0 + min(lo, nb - 1)];
-                m2[u] = hit ? e2 : -1;
-                cnt += hit ? 1 : 0;
-            }
-            const int incl = wave_incl_scan_i32(cnt);
-            if (lane == 63) wtot[wave] = incl;
-            __syncthreads();
-            int off = incl - cnt, total = 0;
-#pragma unroll
-            for (int w = 0; w < kSpT / 64; w++) {
-                off += w < wave ? wtot[w] : 0;
-                total += wtot[w];
-            }
-#pragma unroll
-            for (int u = 0; u < kSpChunk / kSpT; u++)
-                if (m2[u] >= 0) trip[off++] = make_int2(m1[u], m2[u]);
-            __syncthreads();
-            for (int m = tid; m < total; m += kSpT) {
-                const int2 tr = trip[m];
-                product(tr.x, tr.y, 0);
-            }
-            __syncthreads();   // trip and wtot are rewritten by the next chunk
+        // off-diagonal: the pair's shared landmarks, listed once per solve by k_pair_trip
+        const int t0 = d.tripStart[2 * blockIdx.x], tn = d.tripStart[2 * blockIdx.x + 1];
+        for (int m = tid; m < tn; m += kSpT) {
+            const int2 tr = d.trips[t0 + m];
+            product(tr.x, tr.y, 0);
         }
     }
     const int nv = diag ? 42 : 36;
@@ -1024,51 +992,139 @@ __global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag) {
 // the same set as the sparsity pattern of the reduced matrix): per landmark, every pair of its
 // free-pose edges marks block (i, j), i <= j, row-major upper-triangle index; all == 1 marks every
 // block (with a communicator a block may get its terms on another rank only).
-__global__ __launch_bounds__(256) void k_pair_mark(LbaDev d, int32_t* __restrict__ flag, int all) {
-    const int P = d.P;
+// (the per-pair landmark counts go through an LDS histogram when the pair table fits: a few
+// hundred global counters hit by every landmark serialise on their atomics)
+constexpr int kPairHist = 8192;
+__global__ __launch_bounds__(256) void k_pair_mark(LbaDev d, int32_t* __restrict__ flag, int32_t* __restrict__ cnt,
+                                                   int all) {
+    __shared__ int32_t hist[kPairHist];
+    const int P = d.P, np2 = P * (P + 1) / 2;
+    const bool lds = np2 <= kPairHist;
     const int t = blockIdx.x * 256 + threadIdx.x;
-    if (all) {
-        if (t < P * (P + 1) / 2) flag[t] = 1;
-        return;
+    if (lds) {
+        for (int i = threadIdx.x; i < np2; i += 256) hist[i] = 0;
+        __syncthreads();
     }
+    if (all && t < np2) flag[t] = 1;
     if (t < P) flag[t * P - t * (t - 1) / 2] = 1;   // every diagonal block (Hpp + lambda I)
-    if (t >= d.M) return;
-    const int a0 = d.ptStart[t], a1 = d.ptStart[t + 1];
-    for (int a = a0; a < a1; a++) {
-        const int pa = d.actPi[d.ptAct[a]];
-        if (pa < 0) continue;
-        for (int b = a; b < a1; b++) {
-            const int pb = d.actPi[d.ptAct[b]];
-            if (pb < 0) continue;
-            const int i = min(pa, pb), j = max(pa, pb);
-            flag[i * P - i * (i - 1) / 2 + (j - i)] = 1;
+    if (t < d.M) {
+        const int a0 = d.ptStart[t], a1 = d.ptStart[t + 1];
+        for (int a = a0; a < a1; a++) {
+            const int pa = d.actPi[d.ptAct[a]];
+            if (pa < 0) continue;
+            for (int b = a + 1; b < a1; b++) {
+                const int pb = d.actPi[d.ptAct[b]];
+                if (pb < 0 || pb == pa) continue;
+                const int i = min(pa, pb), j = max(pa, pb), k = i * P - i * (i - 1) / 2 + (j - i);
+                flag[k] = 1;
+                if (lds) atomicAdd(&hist[k], 1);   // this landmark is one of the pair's shared ones
+                else atomicAdd(&cnt[k], 1);
+            }
         }
+    }
+    if (lds) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < np2; i += 256)
+            if (hist[i]) atomicAdd(&cnt[i], hist[i]);
     }
 }
 // the marked blocks compacted in index order (one workgroup): pairs[k] = bi << 16 | bj, *npairs
-__global__ __launch_bounds__(1024) void k_pair_list(const int32_t* __restrict__ flag, int P, int32_t* __restrict__ pairs,
-                                                    int32_t* __restrict__ npairs) {
-    __shared__ int wsum[16];
+// ... and, per listed pair, where its shared-landmark list starts (tripStart[2k]) and its length
+// ([2k + 1]) in the trips buffer k_pair_trip fills (offsets in list order)
+__global__ __launch_bounds__(1024) void k_pair_list(const int32_t* __restrict__ flag, const int32_t* __restrict__ cnt,
+                                                    int P, int32_t* __restrict__ pairs, int32_t* __restrict__ npairs,
+                                                    int32_t* __restrict__ tripStart) {
+    __shared__ int wsum[16], tsum[16];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int N = P * (P + 1) / 2;
     const int chunk = (N + 1023) / 1024, c0 = min(tid * chunk, N), c1 = min(c0 + chunk, N);
-    int loc = 0;
-    for (int i = c0; i < c1; i++) loc += flag[i] ? 1 : 0;
-    const int incl = wave_incl_scan_i32(loc);
-    if (lane == 63) wsum[wave] = incl;
+    int loc = 0, tloc = 0;
+    for (int i = c0; i < c1; i++) {
+        loc += flag[i] ? 1 : 0;
+        tloc += flag[i] ? cnt[i] : 0;
+    }
+    const int incl = wave_incl_scan_i32(loc), tincl = wave_incl_scan_i32(tloc);
+    if (lane == 63) { wsum[wave] = incl; tsum[wave] = tincl; }
     __syncthreads();
-    int run = incl - loc;
-    for (int w = 0; w < wave; w++) run += wsum[w];
+    int run = incl - loc, trun = tincl - tloc;
+    for (int w = 0; w < wave; w++) { run += wsum[w]; trun += tsum[w]; }
     if (c0 < c1) {
         int bi = 0, rem = c0;   // index -> (bi, bj) of the first entry, then walk
         while (rem >= P - bi) { rem -= P - bi; bi++; }
         int bj = bi + rem;
         for (int i = c0; i < c1; i++) {
-            if (flag[i]) pairs[run++] = (bi << 16) | bj;
+            if (flag[i]) {
+                tripStart[2 * run] = trun;
+                tripStart[2 * run + 1] = cnt[i];
+                trun += cnt[i];
+                pairs[run++] = (bi << 16) | bj;
+            }
             if (++bj == P) { bi++; bj = bi; }
         }
     }
     if (tid == 1023) *npairs = run;
+}
+
+// Once per solve (the block structure is fixed for both optimize() rounds): every off-diagonal
+// pair's shared landmarks as (pose i's edge, pose j's edge) act positions in pose i's landmark
+// order.  Four edges of pose i per thread are looked up in pose j's sorted landmark list (LDS up
+// to kSpList entries) and the matches compacted in thread order (a workgroup scan).
+__global__ __launch_bounds__(kSpT) void k_pair_trip(LbaDev d, int2* __restrict__ trips) {
+    if ((int)blockIdx.x >= *d.npairs) return;
+    const int pr = d.pairs[blockIdx.x];
+    const int bi = pr >> 16, bj = pr & 0xFFFF;
+    if (bi == bj) return;
+    __shared__ int32_t listJ[kSpList];
+    __shared__ int wtot[kSpT / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int a0 = d.poStart[bi], a1 = d.poStart[bi + 1], b0 = d.poStart[bj], nb = d.poStart[bj + 1] - b0;
+    const bool inLds = nb <= kSpList;
+    if (inLds)
+        for (int t = tid; t < nb; t += kSpT) listJ[t] = d.poPt[b0 + t];
+    __syncthreads();
+    const int32_t* Lj = inLds ? listJ : d.poPt + b0;
+    int2* out = trips + d.tripStart[2 * blockIdx.x];
+    int written = 0;
+    for (int base = a0; base < a1; base += kSpChunk) {
+        int m1[kSpChunk / kSpT], m2[kSpChunk / kSpT], lm[kSpChunk / kSpT];
+#pragma unroll
+        for (int u = 0; u < kSpChunk / kSpT; u++) {
+            const int a = min(base + tid + kSpT * u, a1 - 1);   // clamped: unconditional loads
+            m1[u] = d.poAct[a];
+            const int lv = d.poPt[a];
+            lm[u] = base + tid + kSpT * u < a1 ? lv : -1;
+        }
+        int cnt = 0;
+#pragma unroll
+        for (int u = 0; u < kSpChunk / kSpT; u++) {
+            const int l = lm[u];
+            int lo = 0, hi = nb;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (Lj[mid] < l) lo = mid + 1;
+                else hi = mid;
+            }
+            const bool hit = l >= 0 && lo < nb && Lj[lo] == l;
+            const int e2 = d.poAct[b0 + min(lo, nb - 1)];
+            m2[u] = hit ? e2 : -1;
+            cnt += hit ? 1 : 0;
+        }
+        const int incl = wave_incl_scan_i32(cnt);
+        if (lane == 63) wtot[wave] = incl;
+        __syncthreads();
+        int off = written + incl - cnt, total = 0;
+#pragma unroll
+        for (int w = 0; w < kSpT / 64; w++) {
+            off += w < wave ? wtot[w] : 0;
+            total += wtot[w];
+        }
+#pragma unroll
+        for (int u = 0; u < kSpChunk / kSpT; u++)
+            if (m2[u] >= 0) out[off++] = make_int2(m1[u], m2[u]);
+        written += total;
+        __syncthreads();   // wtot is rewritten by the next chunk
+    }
+    if (tid == 0) const_cast<int32_t*>(d.tripStart)[2 * blockIdx.x + 1] = written;   // the listed length
 }
 
 // ---- The Schur complement as a dense f64 MFMA GEMM (A/B against k_schur_pairs; ORB_LBA_SCHUR_MFMA=1,
@@ -1815,13 +1871,13 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_solve(const double* __restrict__
 //                    wave also holds the 16 diagonal rows and computes the pivots, 1/d and the
 //                    diagonal block's W itself (ldlt_panel_grp's scheme), so no wave waits on another
 //   k_ldlt_mw_trail  the trailing lower triangle, one 16 x 16 tile per wave, four v_mfma_f64_16x16x4
-// then k_ldlt_mw_back (one workgroup): y /= d and the backward substitution with L^T (and, in fused
-// slots, the free poses' update, as k_ldlt_solve's tail).  The work image is np x np (ld = np): W in
+// then the backward substitution in 128-row super-blocks (k_ldlt_mw_bsolve / k_ldlt_mw_bupd, below;
+// in fused slots it ends with the free poses' update, as k_ldlt_solve's tail).  The work image is np x np (ld = np): W in
 // the upper triangle, L in the lower; a diagonal block's L rows go to Ldg[np][16] and its rows'
 // finished forward substitution to yfin (the diagonal rows are read by every wave of the panel
 // while it runs, so nothing writes them in place).
 struct MwLdl {
-    double *A, *rdg, *y, *yfin, *Ldg, *sink;
+    double *A, *rdg, *y, *yfin, *Ldg, *sink, *yb;   // yb: the backward substitution's working vector
     int* fail;
     int n, np;
 };
@@ -1851,50 +1907,60 @@ __global__ __launch_bounds__(256) void k_ldlt_mw_stage(MwLdl m, const double* __
     }
 }
 
+// Panel jb of the multi-workgroup factorisation, kMwNB columns wide (twice k_ldlt_solve's: half
+// the launches and half the passes of the trailing update over the matrix).  Lanes 0..kMwNB-1 of
+// every wave hold the panel's diagonal rows, lanes kMwNB..63 its own rows below (group g: rows
+// jb + kMwNB + (64 - kMwNB) g + ...); the column recurrence is ldlt_panel_grp's.
+constexpr int kMwNB = 32;
+__host__ __device__ __forceinline__ int mw_groups(int np, int jb) {
+    const int g = (np - jb - kMwNB + (64 - kMwNB) - 1) / (64 - kMwNB);
+    return g > 1 ? g : 1;
+}
 template <bool kTail>
 __global__ __launch_bounds__(64 * kMwWaves) void k_ldlt_mw_panel(MwLdl m, int jb, const LmState* st) {
+    constexpr int NB = kMwNB, RB = 64 - kMwNB;   // diagonal lanes, rows below per wave
     if (lm_off(st, 1)) return;
     if (__builtin_amdgcn_readfirstlane(*m.fail)) return;
-    __shared__ double wscS[kMwWaves][kNB];
+    __shared__ double wscS[kMwWaves][NB];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int g = __builtin_amdgcn_readfirstlane((int)blockIdx.x * kMwWaves + wv);
     const int np = m.np, ld = np, nr = m.n;
-    if (g > 0 && jb + kNB + 48 * g >= np) return;   // no rows below for this group (group 0 always runs)
+    if (g > 0 && jb + NB + RB * g >= np) return;   // no rows below for this group (group 0 always runs)
     double* const A = m.A;
     double* const wsc = wscS[wv];
-    const int r = lane < kNB ? jb + lane : jb + kNB + 48 * g + (lane - kNB);
-    const bool live = r < np, inplace = live && lane >= kNB;
+    const int r = lane < NB ? jb + lane : jb + NB + RB * g + (lane - NB);
+    const bool live = r < np, inplace = live && lane >= NB;
     const int rc = min(r, np - 1);
-    double P[kNB];
+    double P[NB];
     double Y = m.y[rc];
 #pragma unroll
-    for (int c = 0; c < kNB; c++) P[c] = A[(size_t)rc * ld + jb + c];
-    double* const Lrow = inplace ? A + (size_t)r * ld + jb : m.sink + (size_t)(lane & (kNB - 1)) * ld;
+    for (int c = 0; c < NB; c++) P[c] = A[(size_t)rc * ld + jb + c];
+    double* const Lrow = inplace ? A + (size_t)r * ld + jb : m.sink + (size_t)(lane & (NB - 1)) * ld;
     double* const Wcol = inplace ? A + (size_t)jb * ld + r : m.sink + lane;
-    double* const wst = lane < kNB ? wsc + lane : m.sink + lane;
+    double* const wst = lane < NB ? wsc + lane : m.sink + lane;
     double dj = shfl_d(P[0], 0);
     bool ok = dj != 0.0 && isfinite(dj);
     double rd = rcp_nr(dj);
     double myrd = 1.0;
-    double Wd[kNB], lprev = 0.0;
+    double Wd[NB], lprev = 0.0;
 #pragma unroll
-    for (int c = 0; c < kNB; c++) {
+    for (int c = 0; c < NB; c++) {
         const int j = jb + c;
         if (kTail && j >= nr) break;
         const double w = P[c];
         double djn = 1.0, rn = 1.0, w1 = 0.0, w2 = 0.0;
-        if (c + 1 < kNB) {
+        if (c + 1 < NB) {
             w1 = shfl_d(w, c + 1);
             const double a1 = shfl_d(P[c + 1], c + 1);
             djn = __builtin_fma(-(w1 * w1), rd, a1);
             rn = __builtin_amdgcn_rcp(djn);
         }
-        if (c + 2 < kNB) w2 = shfl_d(w, c + 2);
+        if (c + 2 < NB) w2 = shfl_d(w, c + 2);
         const double yj = shfl_d(Y, c);
         __builtin_amdgcn_sched_barrier(0);
         if (c >= 1) {
 #pragma unroll
-            for (int k = c + 2; k < kNB; k++) P[k] = __builtin_fma(-lprev, Wd[k], P[k]);
+            for (int k = c + 2; k < NB; k++) P[k] = __builtin_fma(-lprev, Wd[k], P[k]);
         }
         const double l = w * rd;
         P[c] = l;
@@ -1903,12 +1969,12 @@ __global__ __launch_bounds__(64 * kMwWaves) void k_ldlt_mw_panel(MwLdl m, int jb
         myrd = lane == c ? rd : myrd;
         *wst = w;
 #pragma unroll
-        for (int k = c + 3; k < kNB; k++) Wd[k] = wsc[k];
-        if (c + 1 < kNB) P[c + 1] = __builtin_fma(-l, w1, P[c + 1]);
-        if (c + 2 < kNB) P[c + 2] = __builtin_fma(-l, w2, P[c + 2]);
+        for (int k = c + 3; k < NB; k++) Wd[k] = wsc[k];
+        if (c + 1 < NB) P[c + 1] = __builtin_fma(-l, w1, P[c + 1]);
+        if (c + 2 < NB) P[c + 2] = __builtin_fma(-l, w2, P[c + 2]);
         if (r > j) Y = __builtin_fma(-l, yj, Y);
         lprev = l;
-        if (c + 1 < kNB) {
+        if (c + 1 < NB) {
             const double e0 = __builtin_fma(-djn, rn, 1.0);
             const double r1 = __builtin_fma(rn, e0, rn);
             const double e1 = __builtin_fma(-djn, r1, 1.0);
@@ -1918,9 +1984,9 @@ __global__ __launch_bounds__(64 * kMwWaves) void k_ldlt_mw_panel(MwLdl m, int jb
         }
         __builtin_amdgcn_sched_barrier(0);
     }
-    if (g == 0 && lane < kNB) {   // the diagonal block: L rows, 1/d, finished y
+    if (g == 0 && lane < NB) {   // the diagonal block: L rows, 1/d, finished y
 #pragma unroll
-        for (int c = 0; c < kNB; c++) m.Ldg[(size_t)r * kNB + c] = P[c];
+        for (int c = 0; c < NB; c++) m.Ldg[(size_t)r * NB + c] = P[c];
         m.rdg[r] = myrd;
         m.yfin[r] = Y;
         if (lane == 0 && !ok) *m.fail = 1;
@@ -1928,23 +1994,24 @@ __global__ __launch_bounds__(64 * kMwWaves) void k_ldlt_mw_panel(MwLdl m, int jb
     if (inplace) m.y[r] = Y;
 }
 
-// trailing update after panel kb: tiles (I, K), I >= K > kb, one per wave
+// trailing update after the panel at column block kb (kMwNB wide): 16 x 16 tiles (I, K) of the
+// lower triangle beyond it, one per wave, kMwNB / 4 v_mfma_f64_16x16x4 each
 __global__ __launch_bounds__(64 * kMwWaves) void k_ldlt_mw_trail(MwLdl m, int kb, const LmState* st) {
     if (lm_off(st, 1)) return;
     if (__builtin_amdgcn_readfirstlane(*m.fail)) return;
     const int lane = threadIdx.x & 63;
-    const int T = m.np / kNB, mm = T - kb - 1;
+    const int jb = kb * kMwNB, t0 = (jb + kMwNB) / 16, T = m.np / 16, mm = T - t0;
     const int t = __builtin_amdgcn_readfirstlane((int)blockIdx.x * kMwWaves + (int)(threadIdx.x >> 6));
     if (t >= mm * (mm + 1) / 2) return;
     int ti, tk;
     tri_index(t, ti, tk);
-    const int I0 = (kb + 1 + ti) * kNB, K0 = (kb + 1 + tk) * kNB, jb = kb * kNB, ld = m.np;
+    const int I0 = (t0 + ti) * 16, K0 = (t0 + tk) * 16, ld = m.np;
     const double* __restrict__ A = m.A;
     const int li = lane & 15, lk = lane >> 4;
-    double a[kNB / 4], bb[kNB / 4];
+    double a[kMwNB / 4], bb[kMwNB / 4];
     dbl4 acc;
 #pragma unroll
-    for (int s = 0; s < kNB / 4; s++) {
+    for (int s = 0; s < kMwNB / 4; s++) {
         const int p = jb + 4 * s + lk;
         a[s] = -A[(size_t)p * ld + I0 + li];        // -W(I0 + li, p)
         bb[s] = A[(size_t)(K0 + li) * ld + p];      //  L(K0 + li, p)
@@ -1952,75 +2019,143 @@ __global__ __launch_bounds__(64 * kMwWaves) void k_ldlt_mw_trail(MwLdl m, int kb
 #pragma unroll
     for (int q = 0; q < 4; q++) acc[q] = A[(size_t)(I0 + lk + 4 * q) * ld + K0 + li];
 #pragma unroll
-    for (int s = 0; s < kNB / 4; s++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], bb[s], acc, 0, 0, 0);
+    for (int s = 0; s < kMwNB / 4; s++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], bb[s], acc, 0, 0, 0);
 #pragma unroll
     for (int q = 0; q < 4; q++) m.A[(size_t)(I0 + lk + 4 * q) * ld + K0 + li] = acc[q];
 }
 
-// y /= d and x = L^-T y in 16-row blocks from the bottom (wave 0 solves a block's triangle from
-// Ldg by a v_readlane chain, then every thread takes one row above it), y held in LDS; then
-// x out, and in fused slots the free poses' update (pose_tail) on wave 0.
-constexpr int kMwBackT = 1024;
-__global__ __launch_bounds__(kMwBackT) void k_ldlt_mw_back(MwLdl m, double* __restrict__ x, int* __restrict__ flags,
-                                                          const LmState* st, PoseTail ptail) {
+// The backward substitution x = L^-T (y / d) in super-blocks of kSB rows from the bottom, two
+// launches each: k_ldlt_mw_bsolve (one workgroup) stages the super-block's lower triangle of L in
+// LDS and solves its 16-row blocks bottom-up there (the chain of 16-row triangles runs out of LDS,
+// not out of L2); k_ldlt_mw_bupd (every row above, one per thread, over the chip) subtracts the
+// super-block's contribution L(K0 + c, i) x_{K0 + c}.  The bottom super-block first forms y / d
+// for every row; the top one ends with the fused slots' pose update.
+constexpr int kSB = 128;
+__global__ __launch_bounds__(512) void k_ldlt_mw_bsolve(MwLdl m, int K0, double* __restrict__ x, int* __restrict__ flags,
+                                                        const LmState* st, PoseTail ptail, int first, int last) {
     if (lm_off(st, 1)) return;
-    extern __shared__ __attribute__((aligned(16))) double ys[];
+    extern __shared__ __attribute__((aligned(16))) double bsm[];
+    double* Ls = bsm;                        // [kSB][kSB + 1]: L(K0 + r, K0 + c), c < r
+    double* ysb = Ls + kSB * (kSB + 1);      // [kSB]
+    double* xfull = ysb + kSB;               // [np] (top super-block: x for the pose update)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int np = m.np, n = m.n, ld = np;
+    const int np = m.np, n = m.n, ld = np, nsb = min(kSB, np - K0);
     if (__builtin_amdgcn_readfirstlane(*m.fail)) {
-        // as k_ldlt_solve: the update still runs (with the previous x) and the trial is rejected
-        if (tid == 0) flags[0] = 1;
-        if (ptail.scaleOut && wave == 0) pose_tail(ptail, x, st->lambda, lane);
+        if (last) {   // as k_ldlt_solve: the update still runs (with the previous x), the trial is rejected
+            if (tid == 0) flags[0] = 1;
+            if (ptail.scaleOut && wave == 0) pose_tail(ptail, x, st->lambda, lane);
+        }
         return;
     }
-    for (int i = tid; i < np; i += kMwBackT) ys[i] = m.yfin[i] * m.rdg[i];
+    if (first)
+        for (int i = tid; i < np; i += 512) {
+            const double v = m.yfin[i] * m.rdg[i];
+            m.yb[i] = v;
+            if (i >= K0) ysb[i - K0] = v;
+        }
+    else
+        for (int r = tid; r < nsb; r += 512) ysb[r] = m.yb[K0 + r];
+    {   // all kSB^2 / 512 loads of a thread in flight at once (a load per iteration serialised on
+        // the memory latency: the rows were just written by trailing updates on other XCDs)
+        constexpr int kPer = kSB * kSB / 512;
+        double v[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const int t = tid + 512 * k, r = t / kSB, c = t % kSB;
+            const bool sameBlk = (K0 + r) / kMwNB == (K0 + c) / kMwNB;   // a panel's diagonal block: from Ldg
+            v[k] = c >= r || r >= nsb ? 0.0
+                   : sameBlk          ? m.Ldg[(size_t)(K0 + r) * kMwNB + (K0 + c) % kMwNB]
+                                      : m.A[(size_t)(K0 + r) * ld + K0 + c];
+        }
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const int t = tid + 512 * k;
+            Ls[(t / kSB) * (kSB + 1) + t % kSB] = v[k];
+        }
+    }
     __syncthreads();
-    for (int kb = np - kNB; kb >= 0; kb -= kNB) {
+    for (int jb = nsb - kNB; jb >= 0; jb -= kNB) {
         if (wave == 0) {
             const int r = lane & 15;
-            double Ab[kNB];
-#pragma unroll
-            for (int c = 0; c < kNB; c++) Ab[c] = m.Ldg[(size_t)(kb + c) * kNB + r];   // L(kb+c, kb+r), used for r < c
-            double xb = ys[kb + r];
+            double xb = ysb[jb + r];
 #pragma unroll
             for (int c = kNB - 1; c > 0; c--) {
                 const double xc = shfl_d(xb, c);
-                xb = r < c ? __builtin_fma(-Ab[c], xc, xb) : xb;
+                xb = r < c ? __builtin_fma(-Ls[(jb + c) * (kSB + 1) + jb + r], xc, xb) : xb;
             }
-            if (lane < kNB) ys[kb + r] = xb;
+            if (lane < kNB) ysb[jb + r] = xb;
         }
         __syncthreads();
-        if (kb == 0) break;
-        for (int i = tid; i < kb; i += kMwBackT) {
-            double v = ys[i];
+        for (int i = tid; i < jb; i += 512) {
+            double v = ysb[i];
 #pragma unroll
-            for (int c = kNB - 1; c >= 0; c--) v = __builtin_fma(-m.A[(size_t)(kb + c) * ld + i], ys[kb + c], v);
-            ys[i] = v;
+            for (int c = kNB - 1; c >= 0; c--) v = __builtin_fma(-Ls[(jb + c) * (kSB + 1) + i], ysb[jb + c], v);
+            ysb[i] = v;
         }
         __syncthreads();
     }
-    for (int i = tid; i < n; i += kMwBackT) x[i] = ys[i];
+    for (int r = tid; r < nsb; r += 512)
+        if (K0 + r < n) x[K0 + r] = ysb[r];
+    if (!last) return;
     if (tid == 0) flags[0] = 0;
-    if (ptail.scaleOut && wave == 0) pose_tail(ptail, ys, st->lambda, lane);
+    if (ptail.scaleOut) {   // x through LDS: this super-block's rows from ysb, the rest as stored
+        for (int i = tid; i < np; i += 512) xfull[i] = i < nsb ? ysb[i] : (i < n ? x[i] : 0.0);
+        __syncthreads();
+        if (wave == 0) pose_tail(ptail, xfull, st->lambda, lane);
+    }
+}
+// 64 rows per workgroup; wave w takes the super-block's columns [32 w, 32 w + 32) with all 32
+// loads in flight, the four partial sums are added in wave order (deterministic)
+__global__ __launch_bounds__(256) void k_ldlt_mw_bupd(MwLdl m, int K0, const double* __restrict__ x, const LmState* st) {
+    if (lm_off(st, 1)) return;
+    if (__builtin_amdgcn_readfirstlane(*m.fail)) return;
+    static_assert(kSB == 128, "four waves of 32 columns");
+    __shared__ double xs[kSB];
+    __shared__ double part[4][64];
+    const int np = m.np, n = m.n, ld = np, nsb = min(kSB, np - K0);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int c = threadIdx.x; c < kSB; c += 256) xs[c] = c < nsb && K0 + c < n ? x[K0 + c] : 0.0;
+    __syncthreads();
+    const int i = blockIdx.x * 64 + lane;
+    if (i < K0) {
+        double a[32];
+#pragma unroll
+        for (int k = 0; k < 32; k++) {
+            const int c = 32 * w + k;
+            a[k] = c < nsb ? m.A[(size_t)(K0 + c) * ld + i] : 0.0;
+        }
+        double v = 0.0;
+#pragma unroll
+        for (int k = 31; k >= 0; k--) v = __builtin_fma(-a[k], xs[32 * w + k], v);
+        part[w][lane] = v;
+    }
+    __syncthreads();
+    if (w == 0 && i < K0) m.yb[i] = m.yb[i] + ((part[3][lane] + part[2][lane]) + (part[1][lane] + part[0][lane]));
 }
 
 // enqueue the multi-workgroup solve of S x = b (n = order of S) on s
 static void enqueue_ldlt_mw(hipStream_t s, const MwLdl& m, const double* S, const double* b, double* x, int* flags,
                             const LmState* st, const PoseTail& pt) {
-    const int np = m.np, T = np / kNB;
+    const int np = m.np, T = np / kMwNB;
     const size_t tot = (size_t)np * np;
     hipLaunchKernelGGL(k_ldlt_mw_stage, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, m, S, b, st);
     for (int kb = 0; kb < T; kb++) {
-        const int jb = kb * kNB, groups = panel_groups(np, jb);
+        const int jb = kb * kMwNB, groups = mw_groups(np, jb);
         const dim3 gp((unsigned)((groups + kMwWaves - 1) / kMwWaves));
-        if (jb + kNB > m.n) hipLaunchKernelGGL(k_ldlt_mw_panel<true>, gp, dim3(64 * kMwWaves), 0, s, m, jb, st);
+        if (jb + kMwNB > m.n) hipLaunchKernelGGL(k_ldlt_mw_panel<true>, gp, dim3(64 * kMwWaves), 0, s, m, jb, st);
         else hipLaunchKernelGGL(k_ldlt_mw_panel<false>, gp, dim3(64 * kMwWaves), 0, s, m, jb, st);
-        const int mm = T - kb - 1, tiles = mm * (mm + 1) / 2;
+        const int mm = np / 16 - (jb + kMwNB) / 16, tiles = mm * (mm + 1) / 2;
         if (tiles > 0)
             hipLaunchKernelGGL(k_ldlt_mw_trail, dim3((unsigned)((tiles + kMwWaves - 1) / kMwWaves)), dim3(64 * kMwWaves),
                                0, s, m, kb, st);
     }
-    hipLaunchKernelGGL(k_ldlt_mw_back, dim3(1), dim3(kMwBackT), (size_t)np * 8, s, m, x, flags, st, pt);
+    const int nsbk = (np + kSB - 1) / kSB;
+    for (int q = nsbk - 1; q >= 0; q--) {
+        const int K0 = q * kSB;
+        hipLaunchKernelGGL(k_ldlt_mw_bsolve, dim3(1), dim3(512), ((size_t)kSB * (kSB + 1) + kSB + np) * 8, s, m, K0, x,
+                           flags, st, q == 0 ? pt : PoseTail{}, q == nsbk - 1 ? 1 : 0, q == 0 ? 1 : 0);
+        if (q > 0) hipLaunchKernelGGL(k_ldlt_mw_bupd, dim3((K0 + 63) / 64), dim3(256), 0, s, m, K0, x, st);
+    }
 }
 
 
@@ -2777,15 +2912,16 @@ static int dalloc(lba_context* c, T** p, size_t n) {
 static bool use_mw(int np) { return np > kLdlLdsMaxN && !std::getenv("ORB_LBA_LDLT_SINGLE"); }
 static int mw_alloc(lba_context* c, int nMax, MwLdl* m) {
     std::memset(m, 0, sizeof(*m));
-    const size_t np = ((size_t)nMax + kNB - 1) & ~(size_t)(kNB - 1);
+    const size_t np = ((size_t)nMax + kMwNB - 1) & ~(size_t)(kMwNB - 1);
     TRY(dalloc(c, &m->A, np * np)); TRY(dalloc(c, &m->rdg, np)); TRY(dalloc(c, &m->y, np));
-    TRY(dalloc(c, &m->yfin, np)); TRY(dalloc(c, &m->Ldg, np * kNB)); TRY(dalloc(c, &m->sink, kNB * np + 64));
+    TRY(dalloc(c, &m->yfin, np)); TRY(dalloc(c, &m->Ldg, np * kMwNB)); TRY(dalloc(c, &m->sink, kMwNB * np + 64));
+    TRY(dalloc(c, &m->yb, np));
     TRY(dalloc(c, &m->fail, 1));
     return ORB_OK;
 }
 static MwLdl mw_order(MwLdl m, int n) {
     m.n = n;
-    m.np = (n + kNB - 1) & ~(kNB - 1);
+    m.np = (n + kMwNB - 1) & ~(kMwNB - 1);
     return m;
 }
 
@@ -3593,19 +3729,34 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
     // others are zeroed here once and stay zero: the outlier pass keeps the block structure)
     auto build_pairs = [&]() -> int {
         const int P = d.P, np2 = P * (P + 1) / 2;
-        int32_t *flag, *pairs, *npairs;
-        TRY(dalloc(c, &flag, np2)); TRY(dalloc(c, &pairs, np2)); TRY(dalloc(c, &npairs, 1));
+        // the shared-landmark lists' total: sum over landmarks of C(k, 2), k = its free-pose edges
+        // (an upper bound with a communicator, where each rank lists its own landmarks only)
+        std::vector<int32_t> kf((size_t)NM, 0);
+        for (int e = 0; e < NE; e++) kf[(size_t)p->edge_point[e]] += p->pose_fixed[p->edge_pose[e]] ? 0 : 1;
+        size_t ntrip = 0;
+        for (int l = 0; l < NM; l++) ntrip += (size_t)kf[(size_t)l] * (kf[(size_t)l] - 1) / 2;
+        int32_t *flag, *cnt, *pairs, *npairs, *tripStart;
+        int2* trips;
+        TRY(dalloc(c, &flag, 2 * (size_t)np2)); TRY(dalloc(c, &pairs, np2)); TRY(dalloc(c, &npairs, 1));
+        TRY(dalloc(c, &tripStart, 2 * (size_t)np2)); TRY(dalloc(c, &trips, std::max<size_t>(ntrip, 1)));
+        cnt = flag + np2;
         ORB_HIP_TRY(hipMemsetAsync(npairs, 0, 4, s));
         if (P > 0) {
             const int all = c->world > 1 ? 1 : 0;
-            ORB_HIP_TRY(hipMemsetAsync(flag, 0, 4 * (size_t)np2, s));
+            ORB_HIP_TRY(hipMemsetAsync(flag, 0, 8 * (size_t)np2, s));
             ORB_HIP_TRY(hipMemsetAsync(d.S, 0, 8 * (size_t)36 * P * P, s));
-            hipLaunchKernelGGL(k_pair_mark, grid(std::max({d.M, P, all ? np2 : 0})), dim3(256), 0, s, d, flag, all);
-            hipLaunchKernelGGL(k_pair_list, dim3(1), dim3(1024), 0, s, flag, P, pairs, npairs);
+            hipLaunchKernelGGL(k_pair_mark, grid(std::max({d.M, P, all ? np2 : 0})), dim3(256), 0, s, d, flag, cnt, all);
+            hipLaunchKernelGGL(k_pair_list, dim3(1), dim3(1024), 0, s, flag, cnt, P, pairs, npairs, tripStart);
+            d.pairs = pairs;
+            d.npairs = npairs;
+            d.tripStart = tripStart;
+            hipLaunchKernelGGL(k_pair_trip, dim3(np2), dim3(kSpT), 0, s, d, trips);
             ORB_HIP_TRY(hipGetLastError());
         }
         d.pairs = pairs;
         d.npairs = npairs;
+        d.tripStart = tripStart;
+        d.trips = trips;
         return ORB_OK;
     };
     // ---- R/src/Optimizer.cpp:789-841

@@ -12,7 +12,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 ROOT = pathlib.Path(__file__).resolve().parents[1]
-ARGS = ["--steps", "2", "--warmup", "1", "--batch", "8", "--streams", "1", "--pool", "16", "--no-cpu",
+ARGS = ["--steps", "2", "--warmup", "1", "--batch", "8", "--streams", "1", "--pool", "16", "--no-cpu", "--no-lba-scaled",
         "--no-extras", "--no-profile", "--lba-solves", "1", "--lba-points", "1500", "--stereo-batches", "2"]
 
 
