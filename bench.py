@@ -74,6 +74,24 @@ def pmc_valu_ops(kernel, W, H, NF, Bs):
         return None
 
 
+PMC_LANES = ROOT / "profiles" / "r03_lanes_pmc.json"   # tools/pmc_run.sh lanes ... + tools/pmc_lanes.py
+
+
+def pmc_lane_util(kernel, W, H, NF, Bs):
+    """Active-lane fraction of `kernel`'s VALU instructions (rocprof's VALUUtilization:
+    SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU x 64)) from the committed PMC pass; None when
+    absent or for another configuration."""
+    try:
+        doc = json.loads(PMC_LANES.read_text())
+        cfg = doc["config"]
+        if (int(cfg["width"]), int(cfg["height"]), int(cfg["nfeatures"]), int(cfg["frames_per_launch"])) \
+                != (W, H, NF, Bs):
+            return None
+        return float(doc["kernels"][kernel]["active_lane_frac"])
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -119,6 +137,47 @@ def algorithmic_bytes(stage, lw, lh, n_pre, n_out):
         return 4 * (n_pre + n_out)
     if stage == "orient_blur_desc":
         return n_out * (43 * 43 + 28 + 32)   # raw 43x43 window per keypoint in, keypoint + descriptor out
+    raise KeyError(stage)
+
+
+# Algorithmic op counts ("algorithmic ops"): one op = one arithmetic,
+# compare or load on one pixel / sample, counted from the restated algorithm itself, so that
+# neither codegen (address arithmetic, compaction, staging) nor idle lanes count as work.
+# Packed forms count per pixel (a SWAR compare of 4 pixels = 4 ops, a dot4 = 4 MACs).
+ALG_OPS = {
+    # FAST pre-test per region pixel: ring 0/4/8/12 and centre loads (5), 4 dark + 4 bright
+    # compares, the adjacent-pair test (8 and/or, 1 combine)
+    "fast_pixel": 18,
+    # per emitted corner (lower bound: every pre-test survivor is scored, only corners counted):
+    # 17 loads + 16 differences + the 9-arc min/max (64 for the 3-arcs, 96 for the arcs, 3 final)
+    # + NMS (9 loads, 8 max, 2) + emission (5)
+    "fast_corner": 17 + 16 + 64 + 96 + 3 + 19 + 5,
+    # bilinear resize per output pixel of levels 1..7: 4 loads, 4 MAC, round
+    "resize_pixel": 9,
+    # octree per pre-octree key: bucket, compare, move (≈ 30)
+    "octree_key": 30,
+    # per retained keypoint: 43x48 window (516 dword loads, realign, store = 1548), IC_Angle
+    # moments (31 rows x 8 dwords x (load + 2 dot4 x 4 + 2) = 2728), horizontal 7-tap pass
+    # (43 x 37 outputs x 7 MAC + 4 loads / 4 outputs = 11739), 512 BRIEF samples (rotation 4,
+    # round 2, 7 loads, 7 MAC, clamp 2 = 22 each = 11264), 256 compares, atan + sincos (≈60)
+    "keypoint": 1548 + 2728 + 11739 + 11264 + 256 + 60,
+}
+
+
+def algorithmic_ops(stage, lw, lh, n_pre, n_out):
+    """Per-frame algorithmic ops of a stage (ALG_OPS; n_pre = corners emitted by k_fast_cell,
+    n_out = retained keypoints)."""
+    lw = lw.astype(np.int64)
+    lh = lh.astype(np.int64)
+    region = int(np.maximum(lw - 32, 0).dot(np.maximum(lh - 32, 0)))   # [minBorder, w - minBorder)
+    if stage == "fast_detect":
+        return ALG_OPS["fast_pixel"] * region + ALG_OPS["fast_corner"] * n_pre
+    if stage == "resize":
+        return ALG_OPS["resize_pixel"] * int((lw[1:] * lh[1:]).sum())
+    if stage == "octree":
+        return ALG_OPS["octree_key"] * n_pre
+    if stage == "orient_blur_desc":
+        return ALG_OPS["keypoint"] * n_out
     raise KeyError(stage)
 
 
@@ -288,7 +347,7 @@ def bench_lba(args, amd, dev, local, rank, world):
     call = ctx.prepared(pb)
     for _ in range(3):
         call()
-    if world > 1:
+    if world > 1 and not native:   # (native: the other ranks wait at the barrier below)
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
     iters, times = 0, []
@@ -1112,6 +1171,9 @@ def init_ranks(args):
 
 def main():
     args = parse()
+    if os.environ.get("BENCH_STACKS_AFTER"):   # debugging aid: every thread's stack to stderr, periodically
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["BENCH_STACKS_AFTER"]), repeat=True)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
     world, rank, local, backend, n_devices = init_ranks(args)
@@ -1228,12 +1290,13 @@ def main():
         "keypoints_per_frame": float(np.mean(cnt)),
         "matches_per_pair": float(np.mean(nmatch)),
     }
+    pre = np.zeros(8, np.int32)
+    lib.orb_extractor_last_counts(ex._h, 0, _abi.ptr(pre), None)
+    n_pre_frame = float(pre.sum())   # corners k_fast_cell emitted for frame 0 of the last batch
     if not args.no_profile and ncalls > 0:
         fast_launch_ms = float(fast_ms[1]) / ncalls       # live, timed region, launch streams
         n_out = float(np.mean(cnt))
-        pre = np.zeros(8, np.int32)
-        lib.orb_extractor_last_counts(ex._h, 0, _abi.ptr(pre), None)
-        n_pre = float(pre.sum())
+        n_pre = n_pre_frame
         # k_fast_cell is VALU-issue-bound (profiles/r02_valu_pmc.json: SQ_ACTIVE_INST_VALU ~ the
         # VALU instruction count x 4 cycles keeps the SIMDs >80 % busy), so its roofline is the
         # vector ALU: achieved = VALU lane-ops per launch (SQ_INSTS_VALU x 64 from the committed
@@ -1253,6 +1316,12 @@ def main():
         roof = {"bound": "valu", "kernel": "k_fast_cell", "achieved": None, "peak": VALU_PEAK_TOPS, "unit": "TOP/s",
                 "frac": None, "traffic": hbm["traffic"], "launch_ms": round(fast_launch_ms, 4),
                 "frames_per_launch": Bs, "hbm": hbm}
+        # algorithmic ops (codegen- and lane-idleness-independent, ALG_OPS) per launch / live time
+        alg = algorithmic_ops("fast_detect", lw, lh, n_pre, n_out) * Bs
+        roof["algorithmic"] = {"ops_per_launch": int(alg), "achieved": round(alg / (fast_launch_ms * 1e-3) / 1e12, 3),
+                               "unit": "TOP/s", "peak": VALU_PEAK_TOPS,
+                               "frac": round(alg / (fast_launch_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4),
+                               "model": "ALG_OPS in bench.py (DESIGN.md §Roofline)"}
         ops = pmc_valu_ops("k_fast_cell", W, H, NF, Bs)
         if ops is not None:
             ach = ops / (fast_launch_ms * 1e-3) / 1e12
@@ -1260,6 +1329,10 @@ def main():
                         valu_lane_ops_per_launch=ops, valu_ops_source=PMC_VALU.name,
                         measured_issue_peak=VALU_MEASURED_TOPS,
                         frac_of_measured_issue_peak=round(ach / VALU_MEASURED_TOPS, 4))
+            util = pmc_lane_util("k_fast_cell", W, H, NF, Bs)
+            if util is not None:   # the issued lane-ops whose lanes were active
+                roof["active_lane_frac"] = util
+                roof["active_frac"] = round(ach * util / VALU_PEAK_TOPS, 4)
         result["roofline"] = roof
     if nstage > 0:
         result["stage_ms_per_batch"] = {k: round(float(v) / nstage, 4) for k, v in zip(STAGES, stage_ms)
@@ -1277,6 +1350,13 @@ def main():
     if all(o is not None for o in ops):
         per_frame = sum(ops) / Bs
         ach = per_frame * value / 1e12
+        alg_frame = sum(algorithmic_ops(st, lw, lh, float(n_pre_frame), float(np.mean(cnt)))
+                        for st in ("resize", "fast_detect", "octree", "orient_blur_desc"))
+        result["pipeline_algorithmic"] = {"ops_per_frame": int(alg_frame), "achieved": round(alg_frame * value / 1e12, 3),
+                                          "unit": "TOP/s", "peak": VALU_PEAK_TOPS,
+                                          "frac": round(alg_frame * value / 1e12 / VALU_PEAK_TOPS, 4),
+                                          "issued_lane_ops_per_algorithmic_op": round(per_frame / max(alg_frame, 1), 2),
+                                          "model": "ALG_OPS in bench.py (extraction stages; the matcher not counted)"}
         result["pipeline_valu"] = {"lane_ops_per_frame": round(per_frame), "kernels": list(kern),
                                    "achieved": round(ach, 3), "unit": "TOP/s", "peak": VALU_PEAK_TOPS,
                                    "frac": round(ach / VALU_PEAK_TOPS, 4), "measured_issue_peak": VALU_MEASURED_TOPS,

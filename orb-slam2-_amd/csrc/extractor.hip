@@ -583,8 +583,13 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
     int bx, b;
     xcd_block_2d(bx, b);
     const int c = bx * 4 + wid;
-    if (c >= g.cellsPerFrame) return;
-    const int l = level_of_cell(g, c);
+    // the four cells' survivor counts (phases 3-4 are pooled over the workgroup) and their
+    // "a key at iniThFAST" flags
+    __shared__ int poolN[4], anyS[4];
+    // a wave without a cell (past the frame's cells, or an empty / oversized region) keeps n = 0
+    // and still takes part in the pooled phases' barriers
+    bool act = c < g.cellsPerFrame;
+    const int l = level_of_cell(g, act ? c : g.cellsPerFrame - 1);
     const LevelGeom& L = g.lv[l];
     const int ci = c - L.cellBase;
     const int i = ci / L.nCols, j = ci % L.nCols;
@@ -593,32 +598,36 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
     int maxY = iniY + L.hCell + 6;
     const int iniX = kMinBorder + j * L.wCell;
     int maxX = iniX + L.wCell + 6;
-    if (iniY >= L.maxBY - 3 || iniX >= L.maxBX - 6) {
+    if (act && (iniY >= L.maxBY - 3 || iniX >= L.maxBX - 6)) {
         if (lane == 0) *cnt_out = 0;
-        return;
+        act = false;
     }
     if (maxY > L.maxBY) maxY = L.maxBY;
     if (maxX > L.maxBX) maxX = L.maxBX;
     const int rw = maxX - iniX - 6, rh = maxY - iniY - 6;   // detection region
-    if (rw <= 0 || rh <= 0) {
+    if (act && (rw <= 0 || rh <= 0)) {
         if (lane == 0) *cnt_out = 0;
-        return;
+        act = false;
     }
-    if (rw > maxW || rh > maxH || rw > 64) {
+    if (act && (rw > maxW || rh > maxH || rw > 64)) {
         if (lane == 0) { *cnt_out = 0; atomicOr(status, 1); }
-        return;
+        act = false;
     }
     const int PWS = fc_patch_stride(maxW), W32 = PWS >> 2, SCS = fc_score_stride(maxW + 2);
-    unsigned char* base = dsm + (size_t)wid * fc_wave_bytes(maxW, maxH);
+    const int waveBytes = fc_wave_bytes(maxW, maxH);
+    const int patchBytes = max(((maxH + 6) * PWS + 15) & ~15, (maxW * maxH + 15) & ~15);
+    const int listOff = patchBytes + (((maxH + 2) * SCS + 15) & ~15);
+    unsigned char* base = dsm + (size_t)wid * waveBytes;
     uint32_t* patch32 = reinterpret_cast<uint32_t*>(base);
     const uint8_t* patch = base;
-    const int patchBytes = max(((maxH + 6) * PWS + 15) & ~15, (maxW * maxH + 15) & ~15);
     uint8_t* sc = base + patchBytes;
-    uint16_t* list = reinterpret_cast<uint16_t*>(sc + (((maxH + 2) * SCS + 15) & ~15));
+    uint16_t* list = reinterpret_cast<uint16_t*>(base + listOff);
     uint16_t* const lsink = list + (((maxW * maxH * 2 + 15) & ~15) >> 1) + lane;
     uint8_t* kp = base;   // the window is dead once every survivor is scored (phase 3)
     const uint8_t* img = pyr + (size_t)b * g.frameBytes + L.off;
     const int rx0 = iniX + 3, ry0 = iniY + 3;
+    int n = 0;
+    if (act) {
 
     // 1. window rows ry0-3 .. ry0+rh+2, columns from rx0-4 (patch column 4 = region column 0):
     //    lane (row r0 + R*u, dword k) loads one aligned dword, all loads in flight at once; the
@@ -659,7 +668,6 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
     // 2. SWAR pre-test: task (row y, column group gq) covers region columns 4gq .. 4gq+3
     const uint32_t tpre = (uint32_t)max(g.tmin, 1);
     const uint32_t T1 = (tpre + 1u) * 0x00010001u;
-    int n = 0;
     {
         const int NG = (rw + 3) >> 2;
         const int R = 64 / NG, gq = lane % NG, r0 = lane / NG;
@@ -731,9 +739,9 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
                               patch[cc - 3 * PWS], patch[cc - 2 * PWS - 2], patch[cc - 3], patch[cc + 2 * PWS - 2]};
             uint32_t dk = 0, br = 0;
 #pragma unroll
-            for (int i = 0; i < 8; i++) {
-                dk |= (uint32_t)(v - e[i] > tv) << i;
-                br |= (uint32_t)(e[i] - v > tv) << i;
+            for (int u = 0; u < 8; u++) {
+                dk |= (uint32_t)(v - e[u] > tv) << u;
+                br |= (uint32_t)(e[u] - v > tv) << u;
             }
             dk |= dk << 8;
             br |= br << 8;
@@ -748,51 +756,68 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 
+    }   // act
+    if (lane == 0) { poolN[wid] = n; anyS[wid] = 0; }
+    __syncthreads();
+    // Phases 3-4 run over the workgroup's pooled survivors (the four cells' lists back to back,
+    // thread k on entry k): a cell's ~70 survivors no longer leave most of a wave's second pass
+    // idle.  Entry k of cell w lives in wave w's LDS (same layout per wave).
+    const int o1 = poolN[0], o2 = o1 + poolN[1], o3 = o2 + poolN[2], tot = o3 + poolN[3];
+    auto cell_of = [&](int k, int& kk, int& w) -> unsigned char* {
+        w = (int)(k >= o1) + (int)(k >= o2) + (int)(k >= o3);
+        kk = k - (w == 0 ? 0 : w == 1 ? o1 : w == 2 ? o2 : o3);
+        return dsm + (size_t)w * waveBytes;
+    };
+
     // 3. full score of the survivors.  The list is in raster order: lanes are row-major over
     //    (row, column group) and each lane appends its group's columns in order.
-    for (int k = lane; k < n; k += 64) {
-        const int p = list[k];
+    for (int k = threadIdx.x; k < tot; k += 256) {
+        int kk, w;
+        unsigned char* bw = cell_of(k, kk, w);
+        const uint8_t* pw = bw;
+        const int p = reinterpret_cast<const uint16_t*>(bw + listOff)[kk];
         const int y = p >> 6, x = p & 63;
         const int cc = (y + 3) * PWS + x + 4;
         int q[16];
-        q[0] = patch[cc + 3 * PWS];      q[1] = patch[cc + 3 * PWS + 1];
-        q[2] = patch[cc + 2 * PWS + 2];  q[3] = patch[cc + PWS + 3];
-        q[4] = patch[cc + 3];            q[5] = patch[cc - PWS + 3];
-        q[6] = patch[cc - 2 * PWS + 2];  q[7] = patch[cc - 3 * PWS + 1];
-        q[8] = patch[cc - 3 * PWS];      q[9] = patch[cc - 3 * PWS - 1];
-        q[10] = patch[cc - 2 * PWS - 2]; q[11] = patch[cc - PWS - 3];
-        q[12] = patch[cc - 3];           q[13] = patch[cc + PWS - 3];
-        q[14] = patch[cc + 2 * PWS - 2]; q[15] = patch[cc + 3 * PWS - 1];
-        const int S = fast_score(patch[cc], q);
-        if (S >= g.tmin && S > 0) sc[(y + 1) * SCS + x + 1] = (uint8_t)S;
+        q[0] = pw[cc + 3 * PWS];      q[1] = pw[cc + 3 * PWS + 1];
+        q[2] = pw[cc + 2 * PWS + 2];  q[3] = pw[cc + PWS + 3];
+        q[4] = pw[cc + 3];            q[5] = pw[cc - PWS + 3];
+        q[6] = pw[cc - 2 * PWS + 2];  q[7] = pw[cc - 3 * PWS + 1];
+        q[8] = pw[cc - 3 * PWS];      q[9] = pw[cc - 3 * PWS - 1];
+        q[10] = pw[cc - 2 * PWS - 2]; q[11] = pw[cc - PWS - 3];
+        q[12] = pw[cc - 3];           q[13] = pw[cc + PWS - 3];
+        q[14] = pw[cc + 2 * PWS - 2]; q[15] = pw[cc + 3 * PWS - 1];
+        const int S = fast_score(pw[cc], q);
+        if (S >= g.tmin && S > 0) bw[patchBytes + (y + 1) * SCS + x + 1] = (uint8_t)S;
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __syncthreads();
 
     TSTAMP(t_fc3);
     // 4. local maxima among the scored pixels (neighbours outside the region count as 0)
-    bool anyIni = false;
-    for (int k = lane; k < n; k += 64) {
-        const int p = list[k];
+    for (int k = threadIdx.x; k < tot; k += 256) {
+        int kk, w;
+        unsigned char* bw = cell_of(k, kk, w);
+        const int p = reinterpret_cast<const uint16_t*>(bw + listOff)[kk];
         const int y = p >> 6, x = p & 63;
+        const uint8_t* scw = bw + patchBytes;
         const int si = (y + 1) * SCS + x + 1;   // the zero border stands for "outside the region"
-        const int s = sc[si];
+        const int s = scw[si];
         int nb = 0;
 #pragma unroll
         for (int dy = -1; dy <= 1; dy++) {
 #pragma unroll
             for (int dx = -1; dx <= 1; dx++) {
                 if (dx == 0 && dy == 0) continue;
-                nb = max(nb, (int)sc[si + dy * SCS + dx]);
+                nb = max(nb, (int)scw[si + dy * SCS + dx]);
             }
         }
         const int keep = s > 0 && s > nb ? s : 0;
-        kp[k] = (uint8_t)keep;
-        anyIni |= keep > 0 && keep >= g.iniTh;
+        bw[kk] = (uint8_t)keep;   // kp of cell w
+        if (keep > 0 && keep >= g.iniTh) anyS[w] = 1;
     }
-    anyIni = __ballot(anyIni) != 0;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __syncthreads();
+    if (!act) return;
+    const bool anyIni = anyS[wid] != 0;
 
     TSTAMP(t_fc4);
     // 5. keys at the cell's threshold, in raster order

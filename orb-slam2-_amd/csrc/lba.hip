@@ -3331,8 +3331,10 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
     double* d_ldlw = nullptr;   // global image of the padded reduced matrix when it exceeds LDS
     MwLdl mwBase{};             // or the multi-workgroup solve's buffers
     // the dense MFMA Schur (A/B): Y^T, per-chunk partial tiles, per-edge Hpl D^-1 b_l
+    int nFree = 0;   // the reduced system's order is 6 x the free poses
+    for (int i = 0; i < NP; i++) nFree += p->pose_fixed[i] ? 0 : 1;
     const bool schurMfma = std::getenv("ORB_LBA_SCHUR_MFMA") != nullptr && c->world == 1 &&
-                           (((size_t)6 * NP + kNB - 1) & ~(size_t)(kNB - 1)) <= (size_t)kLdlLdsMaxN;
+                           (((size_t)6 * nFree + kNB - 1) & ~(size_t)(kNB - 1)) <= (size_t)kLdlLdsMaxN;
     double *d_Yt = nullptr, *d_ypart = nullptr, *d_ce = nullptr;
     if (schurMfma) {
         const size_t npm = ((size_t)6 * NP + 15) & ~(size_t)15, T = npm / 16;

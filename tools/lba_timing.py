@@ -1,5 +1,6 @@
 """Runs a few LocalBundleAdjustment solves of the config-4 problem (corridor=1 n_local=200
-n_points=100000: the scaled window) and prints
+n_points=100000: the scaled window; group=N: through lba_group on N contexts of device 0, with the
+per-collective exchange time of the group's all-reduce) and prints
 per-stage event times; with ORB_SLAM2_AMD_LIB pointing at an ORB_TIMING variant
 (tools/build_variant.py timing -DORB_TIMING) the kernels print their own clock splits."""
 import pathlib
@@ -18,9 +19,10 @@ for a in sys.argv[1:]:
     kw[k] = float(v) if "." in v else int(v)
 # corridor=1: the scaled window generator (synth.ba_problem_corridor, banded covisibility)
 gen = synth.ba_problem_corridor if kw.pop("corridor", 0) else synth.ba_problem
+group = kw.pop("group", 0)
 pb = gen(**kw)
 print(f"problem: {len(pb['Tcw'])} keyframes, {len(pb['point_xyz'])} points, {len(pb['edge_point'])} edges", flush=True)
-ba = amd.LocalBA()
+ba = amd.LocalBAGroup([0] * group) if group else amd.LocalBA()
 n = 12
 call = ba.prepared(pb)
 ts = []
@@ -30,5 +32,12 @@ for i in range(n):
     dt = time.perf_counter() - t0
     ts.append(dt)
     print(f"solve {i}: {dt * 1e3:.3f} ms, iterations {its}, trials {trials}", flush=True)
+    if group and i == 3:
+        ex0 = ba.stats()
 import statistics  # noqa: E402
 print(f"median of solves 4..{n - 1}: {1e3 * statistics.median(ts[4:]):.3f} ms", flush=True)
+if group:
+    ex1 = ba.stats()
+    nc = ex1[1] - ex0[1]
+    print(f"group of {group}: {nc} collectives in solves 4..{n - 1}, exchange {1e3 * (ex1[0] - ex0[0]) / max(nc, 1):.2f} us "
+          f"per collective (rank 0's stream, events around the all-reduce)", flush=True)

@@ -5,7 +5,7 @@ MfmaFlopsF64 = SQ_INSTS_VALU_MFMA_MOPS_F64 x 512 (rocprofv3's derived-counter de
 SQ_VALU_MFMA_BUSY_CYCLES counts MFMA-busy cycles summed over SIMDs; GRBM_GUI_ACTIVE is the
 kernel's GPU-active cycles.  The MFMA-busy fraction of the kernel's own SIMD (one workgroup
 for k_ldlt_solve) is busy / GUI_ACTIVE; of the whole chip it is busy / (GUI_ACTIVE x 1024 SIMDs).
-usage: python tools/pmc_lba.py OUT.json gpurun_out/pmc_lba"""
+usage: python tools/pmc_lba.py OUT.json gpurun_out/pmc_lba_TAG [lba_timing.py args]"""
 import json
 import sys
 
@@ -16,7 +16,8 @@ out, d = sys.argv[1], sys.argv[2]
 t = per_kernel(d)
 res = {"source": "rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_INSTS_VALU_MFMA_F64 SQ_VALU_MFMA_BUSY_CYCLES "
                  "SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 GRBM_GUI_ACTIVE --kernel-trace "
-                 "-- python3 tools/lba_timing.py (config 4: 20 KF x 3000 points)",
+                 "-- python3 tools/lba_timing.py " + " ".join(sys.argv[3:]) + " (no args: config 4, 20 KF x 3000 points)",
+       "env": {k: v for k, v in __import__("os").environ.items() if k.startswith("ORB_LBA_")},
        "kernels": {}}
 for k, c in sorted(t.items()):
     e = {kk: round(v, 2) for kk, v in c.items()}
