@@ -663,7 +663,6 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    TSTAMP(t_fc1);
 
     // 2. SWAR pre-test: task (row y, column group gq) covers region columns 4gq .. 4gq+3
     const uint32_t tpre = (uint32_t)max(g.tmin, 1);
@@ -721,7 +720,6 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 
-    TSTAMP(t_fc2);
     // 2b. second necessary test on the survivors: any 9-arc holds four cyclically consecutive
     //     even ring pixels (0, 2, .., 14), so they must all be dark or all bright at the same
     //     strict threshold; the list is compacted in place (order kept: a chunk's entries are all
@@ -757,8 +755,10 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 
     }   // act
+    TSTAMP(t_fc1);
     if (lane == 0) { poolN[wid] = n; anyS[wid] = 0; }
     __syncthreads();
+    TSTAMP(t_fc2);
     // Phases 3-4 run over the workgroup's pooled survivors (the four cells' lists back to back,
     // thread k on entry k): a cell's ~70 survivors no longer leave most of a wave's second pass
     // idle.  Entry k of cell w lives in wave w's LDS (same layout per wave).
@@ -844,8 +844,8 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
     }
 #ifdef ORB_TIMING
     if (lane == 0 && b == 0 && (c == 0 || c == 100 || c == 500))
-        printf("fast_cell c%d rw %d rh %d n %d keys %d: load %lld pretest %lld score %lld nms %lld emit %lld\n", c, rw, rh,
-               n, nk, t_fc1 - t_fc0, t_fc2 - t_fc1, t_fc3 - t_fc2, t_fc4 - t_fc3, clock64() - t_fc4);
+        printf("fast_cell c%d rw %d rh %d n %d keys %d: load+pretest %lld barrier %lld score %lld nms %lld emit %lld\n", c,
+               rw, rh, n, nk, t_fc1 - t_fc0, t_fc2 - t_fc1, t_fc3 - t_fc2, t_fc4 - t_fc3, clock64() - t_fc4);
 #endif
 }
 

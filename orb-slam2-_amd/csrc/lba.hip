@@ -1183,33 +1183,57 @@ __global__ __launch_bounds__(256) void k_schur_ymat(LbaDev d, double* __restrict
     }
 }
 
-// chunk c (kYLm landmarks = 48 rows of Y^T): every upper tile (I <= K) of Y Y^T, 12 MFMAs per tile
+// workgroup w: chunks w * kYLmG .. w * kYLmG + kYLmG - 1 (kYLm landmarks = 48 rows of Y^T each) into
+// every upper tile (I <= K) of Y Y^T, 12 MFMAs per tile and chunk; wave v keeps the accumulators
+// of tiles v, v + 4, ... (up to kGemmTiles per wave) in registers across the chunks, so the
+// partial sums k_schur_msum adds are one set per workgroup
+constexpr int kYLmG = 1;         // chunks per k_schur_gemm workgroup (4: 47 workgroups, 49 us; 1: 188)
+constexpr int kGemmTiles = 9;    // upper tiles per wave: T (T + 1) / 2 <= 36 at np <= 128
 __global__ __launch_bounds__(256) void k_schur_gemm(LbaDev d, const double* __restrict__ Yt, int np,
                                                     double* __restrict__ part) {
     if (d.lm->phase != 1) return;
     __shared__ double ys[3 * kYLm][128];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int kr = min(3 * kYLm, 3 * d.M - (int)blockIdx.x * 3 * kYLm);   // rows of Y^T in this chunk
-    for (int i = tid; i < 3 * kYLm * np; i += 256) {
-        const int r = i / np, c = i % np;
-        ys[r][c] = r < kr ? Yt[((size_t)blockIdx.x * 3 * kYLm + r) * np + c] : 0.0;
-    }
-    __syncthreads();
     const int T = np / 16, nt = T * (T + 1) / 2;
     const int li = lane & 15, lk = lane >> 4;
-    for (int t = wave; t < nt; t += 4) {
-        int ti = 0, rem = t;   // row-major upper triangle: (ti, tk), ti <= tk
-        while (rem >= T - ti) { rem -= T - ti; ti++; }
-        const int tk = ti + rem;
-        dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+    int tI[kGemmTiles], tK[kGemmTiles];
 #pragma unroll
-        for (int s = 0; s < 3 * kYLm / 4; s++) {
-            const double a = ys[4 * s + lk][16 * ti + li], b = ys[4 * s + lk][16 * tk + li];
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+    for (int j = 0; j < kGemmTiles; j++) {
+        int ti = 0, rem = min(wave + 4 * j, nt - 1);   // row-major upper triangle: (ti, tk), ti <= tk
+        while (rem >= T - ti) { rem -= T - ti; ti++; }
+        tI[j] = ti;
+        tK[j] = ti + rem;
+    }
+    dbl4 acc[kGemmTiles];
+#pragma unroll
+    for (int j = 0; j < kGemmTiles; j++) acc[j] = dbl4{0.0, 0.0, 0.0, 0.0};
+    for (int g = 0; g < kYLmG; g++) {
+        const int ch = blockIdx.x * kYLmG + g;
+        const int kr = min(3 * kYLm, 3 * d.M - ch * 3 * kYLm);   // rows of Y^T in this chunk
+        if (kr <= 0) break;
+        __syncthreads();
+        for (int i = tid; i < 3 * kYLm * np; i += 256) {
+            const int r = i / np, c = i % np;
+            ys[r][c] = r < kr ? Yt[((size_t)ch * 3 * kYLm + r) * np + c] : 0.0;
         }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kGemmTiles; j++) {
+            if (wave + 4 * j >= nt) break;
+#pragma unroll
+            for (int s = 0; s < 3 * kYLm / 4; s++) {
+                const double a = ys[4 * s + lk][16 * tI[j] + li], b = ys[4 * s + lk][16 * tK[j] + li];
+                acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[j], 0, 0, 0);
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < kGemmTiles; j++) {
+        const int t = wave + 4 * j;
+        if (t >= nt) break;
         double* o = part + ((size_t)blockIdx.x * nt + t) * 256;
 #pragma unroll
-        for (int q = 0; q < 4; q++) o[(lk + 4 * q) * 16 + li] = acc[q];
+        for (int q = 0; q < 4; q++) o[(lk + 4 * q) * 16 + li] = acc[j][q];
     }
 }
 
@@ -1228,6 +1252,7 @@ __global__ __launch_bounds__(256) void k_schur_msum(LbaDev d, const double* __re
         const int R = 16 * ti + (e >> 4), Cc = 16 * tk + (e & 15);
         if (R < n && Cc < n && R <= Cc) {
             double v = 0.0;
+#pragma unroll 8
             for (int c = 0; c < nchunks; c++) v += part[((size_t)c * nt + t) * 256 + e];
             double val = 0.0;
             if (addDiag && R / 6 == Cc / 6) {
@@ -1238,11 +1263,22 @@ __global__ __launch_bounds__(256) void k_schur_msum(LbaDev d, const double* __re
             d.S[(size_t)R * n + Cc] = val;
             d.S[(size_t)Cc * n + R] = val;
         }
-    } else if (g < nt * 256 + n) {
-        const int i = g - nt * 256, p = i / 6, r = i % 6;
-        double v = 0.0;
-        for (int a = d.poStart[p]; a < d.poStart[p + 1]; a++) v += ce[6 * (size_t)d.poAct[a] + r];
-        d.bs[i] = (addDiag ? d.bp[i] : 0.0) - v;
+    } else {
+        // b_s: one wave per pose (the tile part fills whole workgroups), lanes strided over the
+        // pose's edges, then a fixed-order wave reduction
+        const int p = (g - nt * 256) >> 6, lane = threadIdx.x & 63;
+        if (p >= d.P) return;
+        double v[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+        for (int a = d.poStart[p] + lane; a < d.poStart[p + 1]; a += 64) {
+            const double* c = ce + 6 * (size_t)d.poAct[a];
+#pragma unroll
+            for (int r = 0; r < 6; r++) v[r] += c[r];
+        }
+#pragma unroll
+        for (int r = 0; r < 6; r++) {
+            const double t = wave_sum_d(v[r]);
+            if (lane == r) d.bs[6 * p + r] = (addDiag ? d.bp[6 * p + r] : 0.0) - t;
+        }
     }
 }
 
@@ -1565,33 +1601,23 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_solve(const double* __restrict__
         constexpr int kW = kLdlT / 64;
         const __amdgpu_buffer_rsrc_t rs = buf_rsrc(Sg, (uint32_t)n * n * 8);
         if (kLds && (n & 1) == 0 && np <= 128) {
-            constexpr int kRows = 128 / kW;   // rows per wave at np = 128
-            const int cp = n >> 1, c = lane;
-            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-            u32x4 v[kRows];
+            // phase 1 (here, every wave): column block 0 of every row, the padding included —
+            // panel 0's input.  The rest of the lower triangle (phase 2) is staged by the waves
+            // that do not factor panel 0, while it is factored (below).  Nothing reads S's upper
+            // triangle: the diagonal lanes of a panel load theirs but never consume it, the
+            // trailing tiles of the diagonal carry it along unread, and the W stores fill the rest
+            // before a trailing tile reads it.
+            const int col = tid & 15;
+            double v[4];
 #pragma unroll
-            for (int u = 0; u < kRows; u++) {
-                const int i = wave + kW * u;
-                const bool in = i < n && c < cp;
-                v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, in ? (i * n + 2 * c) * 8 : kBufOob, 0, 0);
+            for (int u = 0; u < 4; u++) {
+                const int i = (tid >> 4) + 32 * u;
+                v[u] = buf_ld_f64(rs, i < n && col < n ? (i * n + col) * 8 : kBufOob);
             }
 #pragma unroll
-            for (int u = 0; u < kRows; u++) {
-                const int i = wave + kW * u;
-                if (i < n && c < cp) {
-                    A[(size_t)i * ld + 2 * c] = __longlong_as_double((long long)(((unsigned long long)v[u].y << 32) | v[u].x));
-                    A[(size_t)i * ld + 2 * c + 1] =
-                        __longlong_as_double((long long)(((unsigned long long)v[u].w << 32) | v[u].z));
-                }
-            }
-            // identity padding: rows n..np-1 (all columns) and columns n..np-1 of rows < n
-            for (int t = tid; t < (np - n) * np; t += kLdlT) {
-                const int i = n + t / np, j = t % np;
-                A[(size_t)i * ld + j] = i == j ? 1.0 : 0.0;
-            }
-            for (int t = tid; t < n * (np - n); t += kLdlT) {
-                const int i = t / (np - n), j = n + t % (np - n);
-                A[(size_t)i * ld + j] = 0.0;
+            for (int u = 0; u < 4; u++) {
+                const int i = (tid >> 4) + 32 * u;
+                if (i < np) A[(size_t)i * ld + col] = v[u] + ((i >= n || col >= n) && i == col ? 1.0 : 0.0);
             }
         } else {
             for (int j0 = 0; j0 < np; j0 += 64) {
@@ -1659,6 +1685,41 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_solve(const double* __restrict__
                                                  : ldlt_panel_grp<false>(A, ld, np, n, jb, rdg, y, shadow, dummy + 64 + 16 * wave, lane, wave, &arriveS,
                                                 arriveTarget);
                 if (!okp && wave == 0 && lane == 0) failS = 1;
+            } else if (kb == 0 && kLds && (n & 1) == 0 && np <= 128) {
+                // staging phase 2: rows 16.., column pairs (2c, 2c+1) from column 16 up to the
+                // diagonal (identity padding beyond n).  Rows are folded (16 + f with np - 1 - f:
+                // together at most 58 pairs, one per lane), so one round of 16-byte loads covers
+                // the triangle: every load of a wave in flight at once
+                const __amdgpu_buffer_rsrc_t rs = buf_rsrc(Sg, (uint32_t)n * n * 8);
+                const int nw = kLdlT / 64 - ng, nf = (np - kNB + 1) >> 1;
+                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                constexpr int kFold = 12;   // ceil(56 folded row pairs / 5 staging waves) at np = 128
+                u32x4 v[kFold];
+                int ri[kFold], ci[kFold];
+#pragma unroll
+                for (int u = 0; u < kFold; u++) {
+                    const int f = (wave - ng) + nw * u;
+                    const int rA = kNB + f, rB = np - 1 - f, cntA = (rA >> 1) - 7;
+                    const bool onA = lane < cntA;
+                    int i = onA ? rA : rB;
+                    const int c = 8 + (onA ? lane : lane - cntA);
+                    if (f >= nf || 2 * c > i || (!onA && rB <= rA)) i = -1;   // no pair for this lane
+                    ri[u] = i;
+                    ci[u] = c;
+                    const bool in = i >= 0 && i < n;
+                    v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, in ? (i * n + 2 * c) * 8 : kBufOob, 0, 0);
+                }
+#pragma unroll
+                for (int u = 0; u < kFold; u++) {
+                    const int i = ri[u], c = ci[u];
+                    if (i >= 0) {
+                        double* const dst = A + (size_t)i * ld + 2 * c;
+                        dst[0] = __longlong_as_double((long long)(((unsigned long long)v[u].y << 32) | v[u].x)) +
+                                 (i >= n && i == 2 * c ? 1.0 : 0.0);
+                        dst[1] = __longlong_as_double((long long)(((unsigned long long)v[u].w << 32) | v[u].z)) +
+                                 (i >= n && i == 2 * c + 1 ? 1.0 : 0.0);
+                    }
+                }
             }
         } else if (wave == 0 && !factored) {
             const int ns = min(np - jb, kPanelRows);
@@ -3502,10 +3563,10 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         const int npairs = d.P * (d.P + 1) / 2;
         if (schurMfma && d.P > 0 && d.M > 0) {
             const int npm = (6 * d.P + 15) & ~15, T = npm / 16, nt = T * (T + 1) / 2;
-            const int nch = (d.M + kYLm - 1) / kYLm;
+            const int nch = ((d.M + kYLm - 1) / kYLm + kYLmG - 1) / kYLmG;   // gemm workgroups = partial sets
             hipLaunchKernelGGL(k_schur_ymat, dim3((d.M + kYLmB - 1) / kYLmB), dim3(256), 0, s, d, d_Yt, npm, d_ce);
             hipLaunchKernelGGL(k_schur_gemm, dim3(nch), dim3(256), 0, s, d, d_Yt, npm, d_ypart);
-            hipLaunchKernelGGL(k_schur_msum, dim3((nt * 256 + 6 * d.P + 255) / 256), dim3(256), 0, s, d, d_ypart, nch, npm,
+            hipLaunchKernelGGL(k_schur_msum, dim3(nt + (d.P + 3) / 4), dim3(256), 0, s, d, d_ypart, nch, npm,
                                d_ce, root ? 1 : 0);
         } else if (npairs > 0) {
             hipLaunchKernelGGL(k_schur_pairs, dim3(npairs), dim3(kSpT), 0, s, d, root ? 1 : 0);
