@@ -39,8 +39,8 @@ VALU_PEAK_TOPS = 78.6            # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (MI355X_
 VALU_MEASURED_TOPS = 39.3        # tools/micro/valu_peak.hip: 4 cycles per wave64 VALU op (profiles/r02_valu_peak.txt)
 STAGES = ["resize", "fast_detect", "reserved", "octree", "reserved2", "orient_blur_desc"]
 KERNELS = ["k_resize", "k_fast_cell", None, "k_octree", None, "k_orient_desc"]
-PMC_TRAFFIC = ROOT / "profiles" / "r02_pmc_traffic.json"   # tools/pmc_run.sh + tools/pmc_traffic.py
-PMC_VALU = ROOT / "profiles" / "r02_valu_pmc.json"         # tools/gpu_valu_pmc.sh + tools/pmc_valu.py
+PMC_TRAFFIC = ROOT / "profiles" / "r03_pmc_traffic.json"   # tools/pmc_run.sh + tools/pmc_traffic.py
+PMC_VALU = ROOT / "profiles" / "r03_valu_pmc.json"         # tools/gpu_valu_pmc.sh + tools/pmc_valu.py
 
 
 def pmc_traffic(kernel, W, H, NF, Bs):

@@ -1535,6 +1535,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
     const uint8_t* img = pyr + (size_t)b * g.frameBytes + L.off;
     uint32_t* P32 = reinterpret_cast<uint32_t*>(od_sm[wid]);
     uint16_t* RS = reinterpret_cast<uint16_t*>(od_sm[wid] + kOdRows * kOdPW);
+    TSTAMP(t_od0);
 
     // 1. patch
     if (x - 24 >= 0 && x + 24 <= L.w && y - 21 >= 0 && y + 21 < L.h) {
@@ -1568,6 +1569,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 
+    TSTAMP(t_od1);
     // 2. moments: lane = (row group vr, dword d); patch dword 2+d holds u = 4d-16 .. 4d-13
     int m10 = 0, m01 = 0;
     {
@@ -1591,6 +1593,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
     m01 = wave_reduce_sum_i32(m01);
     const float angle = fast_atan2_dev((float)m01, (float)m10);
 
+    TSTAMP(t_od2);
     // 3a. horizontal Gaussian pass: RS[r][c] = sum_q k_q * raw(y-21+r, x-18+c-3+q), c < 37.
     //     Task (r, group gq) computes columns 4gq .. 4gq+3 from patch dwords gq .. gq+3.
     for (int t = lane; t < kOdRows * 10; t += 64) {
@@ -1613,6 +1616,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 
+    TSTAMP(t_od3);
     // 3b + 4. steered BRIEF: blurred(y+Y, x+X) = (sum_q k_q RS[Y+18+q][X+18] + 2^15) >> 16
     float bs, ac;
     glibc_sincosf(angle * g.factorPI, bs, ac);
@@ -1634,6 +1638,11 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
         const float x1 = (float)c_pattern[4 * pi + 2], y1 = (float)c_pattern[4 * pi + 3];
         words[r] = __ballot(sample(x0, y0) < sample(x1, y1));
     }
+#ifdef ORB_TIMING
+    if (lane == 0 && b == 0 && (q == 0 || q == 300 || q == 700))
+        printf("orient_desc q%d: patch %lld moments %lld hpass %lld brief %lld\n", q, t_od1 - t_od0, t_od2 - t_od1,
+               t_od3 - t_od2, clock64() - t_od3);
+#endif
     if (lane < 4) {
         uint64_t wv = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
         reinterpret_cast<uint64_t*>(desc + ((size_t)b * cap + outIdx) * 32)[lane] = wv;

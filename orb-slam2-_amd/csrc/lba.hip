@@ -27,6 +27,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <initializer_list>
 #include <thread>
 #include <cfloat>
 #include <chrono>
@@ -2551,7 +2552,7 @@ __global__ void k_lm_decide(LmState* st, const double* __restrict__ red, const i
     if (threadIdx.x != 0) return;
     st->pop = 0;
     if (st->phase != 1) return;
-    lm_decide(st, red[0], red[2], flags[0], maxTrials, iterations, fixedIterations, trace, nullptr, red[3]);
+    lm_decide(st, red[4], red[2], flags[0], maxTrials, iterations, fixedIterations, trace, nullptr, red[3]);
 }
 
 // Communicator path: this rank's stop sample into red[3], summed over the ranks with the scale
@@ -3068,14 +3069,35 @@ int upload(lba_context* c, T** dst, const std::vector<T>& v) {
 
 // All-reduce of an LM-loop buffer: staged through the workspace by guarded kernels, so a
 // slot whose phase is skipped reduces zeros and leaves the buffer alone.
-static int comm_allreduce_g(lba_context* c, double* dbuf, size_t n, int op, const LmState* st, int want) {
+// Several buffers with the same op ride in one collective (packed back to back in the workspace):
+// a collective costs far more than the pack / unpack launches around it.
+struct CommSeg {
+    double* p;
+    size_t n;
+};
+static int comm_allreduce_segs(lba_context* c, std::initializer_list<CommSeg> segs, int op, const LmState* st, int want) {
     if (c->world <= 1) return ORB_OK;
-    if (!c->allreduce || !c->ws || n > c->wsDoubles) return ORB_EINVAL;
-    const unsigned g = (unsigned)std::min<size_t>(1024, (n + 255) / 256);
-    hipLaunchKernelGGL(k_pack, dim3(g), dim3(256), 0, c->stream, c->ws, dbuf, n, st, want);
-    if (c->allreduce(c->commUser, 0, n, op) != 0) return ORB_EGPU;
-    hipLaunchKernelGGL(k_unpack, dim3(g), dim3(256), 0, c->stream, dbuf, c->wsOut ? c->wsOut : c->ws, n, st, want);
+    size_t tot = 0;
+    for (const CommSeg& sg : segs) tot += sg.n;
+    if (!c->allreduce || !c->ws || tot > c->wsDoubles) return ORB_EINVAL;
+    size_t off = 0;
+    for (const CommSeg& sg : segs) {
+        const unsigned g = (unsigned)std::min<size_t>(1024, (sg.n + 255) / 256);
+        hipLaunchKernelGGL(k_pack, dim3(g), dim3(256), 0, c->stream, c->ws + off, sg.p, sg.n, st, want);
+        off += sg.n;
+    }
+    if (c->allreduce(c->commUser, 0, tot, op) != 0) return ORB_EGPU;
+    const double* res = c->wsOut ? c->wsOut : c->ws;
+    off = 0;
+    for (const CommSeg& sg : segs) {
+        const unsigned g = (unsigned)std::min<size_t>(1024, (sg.n + 255) / 256);
+        hipLaunchKernelGGL(k_unpack, dim3(g), dim3(256), 0, c->stream, sg.p, res + off, sg.n, st, want);
+        off += sg.n;
+    }
     return ORB_OK;
+}
+static int comm_allreduce_g(lba_context* c, double* dbuf, size_t n, int op, const LmState* st, int want) {
+    return comm_allreduce_segs(c, {CommSeg{dbuf, n}}, op, st, want);
 }
 
 extern "C" {
@@ -3547,11 +3569,12 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
             if (!fuse) hipLaunchKernelGGL(k_lm_begin_fused, dim3(1), dim3(64), 0, s, d, nbE, nbV);
         } else {
             hipLaunchKernelGGL(k_sum, dim3(1), dim3(1024), 0, s, d.echi, d.nact, d.red, d.lm, 0);
-            TRY(comm_allreduce_g(c, d.red, 1, 0, d.lm, 0));
-            if (d.P > 0) {
-                TRY(comm_allreduce_g(c, d.Hpp, 36 * (size_t)d.P, 0, d.lm, 0));
-                TRY(comm_allreduce_g(c, d.bp, 6 * (size_t)d.P, 0, d.lm, 0));
-            }
+            // the iteration's chi2 with the pose blocks: one collective
+            if (d.P > 0)
+                TRY(comm_allreduce_segs(c, {CommSeg{d.red, 1}, CommSeg{d.Hpp, 36 * (size_t)d.P}, CommSeg{d.bp, 6 * (size_t)d.P}}, 0,
+                                        d.lm, 0));
+            else
+                TRY(comm_allreduce_g(c, d.red, 1, 0, d.lm, 0));
             hipLaunchKernelGGL(k_maxdiag, dim3(1), dim3(1024), 0, s, d.Hpp, d.P, d.Hll, d.M, d.red + 1, d.lm);
             TRY(comm_allreduce_g(c, d.red + 1, 1, 1, d.lm, 3));
             hipLaunchKernelGGL(k_lm_begin, dim3(1), dim3(64), 0, s, d.lm, d.red);
@@ -3604,13 +3627,13 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
                 hipLaunchKernelGGL(k_lm_decide_fused, dim3(1), dim3(1024), 0, s, d, d_freePoses, maxTrials, iterations,
                                    o->fixed_iterations ? 1 : 0, d_trace, nbE, nbB, 0);
         } else {
-            hipLaunchKernelGGL(k_sum, dim3(1), dim3(1024), 0, s, d.echi, d.nact, d.red, d.lm, 1);
-            TRY(comm_allreduce_g(c, d.red, 1, 0, d.lm, 1));
+            // the trial's chi2 (red[4]), the scale term (red[2]) and the stop sample (red[3]): one collective
+            hipLaunchKernelGGL(k_sum, dim3(1), dim3(1024), 0, s, d.echi, d.nact, d.red + 4, d.lm, 1);
             const int nx = 6 * d.P + 3 * d.M;
             hipLaunchKernelGGL(k_scale_terms, grid(nx), dim3(256), 0, s, d, root ? 1 : 0, d.echi);
             hipLaunchKernelGGL(k_sum, dim3(1), dim3(1024), 0, s, d.echi, nx, d.red + 2, d.lm, 1);
             hipLaunchKernelGGL(k_stop_sample, dim3(1), dim3(64), 0, s, d.lm, d.stopWord, d.red);
-            TRY(comm_allreduce_g(c, d.red + 2, 2, 0, d.lm, 1));
+            TRY(comm_allreduce_g(c, d.red + 2, 3, 0, d.lm, 1));
             hipLaunchKernelGGL(k_lm_decide, dim3(1), dim3(64), 0, s, d.lm, d.red, d.flags, maxTrials, iterations,
                                o->fixed_iterations ? 1 : 0, d_trace);
             hipLaunchKernelGGL(k_pop, grid(std::max(d.M, d.P)), dim3(256), 0, s, d, d.P, d_freePoses);
