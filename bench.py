@@ -181,6 +181,12 @@ def algorithmic_ops(stage, lw, lh, n_pre, n_out):
     raise KeyError(stage)
 
 
+def progress(rank, msg):
+    """A progress line on stderr (rank 0): the timed line stays the only stdout output."""
+    if rank == 0:
+        print(f"[bench] {time.strftime('%H:%M:%S')} {msg}", file=sys.stderr, flush=True)
+
+
 def host_threads():
     """Host threads this process may run on: the lease's CPU share.  The GPU box exports
     OMP_NUM_THREADS (16 per GPU) while its affinity mask shows the whole machine (256 CPUs), so
@@ -1290,6 +1296,7 @@ def main():
         "keypoints_per_frame": float(np.mean(cnt)),
         "matches_per_pair": float(np.mean(nmatch)),
     }
+    progress(rank, f"extraction + matching timed: {value:.0f} frames/s")
     pre = np.zeros(8, np.int32)
     lib.orb_extractor_last_counts(ex._h, 0, _abi.ptr(pre), None)
     n_pre_frame = float(pre.sum())   # corners k_fast_cell emitted for frame 0 of the last batch
@@ -1363,14 +1370,19 @@ def main():
                                    "frac_of_measured_issue_peak": round(ach / VALU_MEASURED_TOPS, 4),
                                    "ops_source": PMC_VALU.name}
     if not args.no_lba:
+        progress(rank, "local BA (config 4)")
         result["lba"] = bench_lba(args, amd, dev, local, rank, world)
         if not args.no_lba_scaled:
+            progress(rank, "local BA, scaled windows")
             result["lba_scaled"] = bench_lba_scaled(args, amd, dev, rank, world)
     if not args.no_stereo:
+        progress(rank, "config 5 (stereo)")
         result["config5_stereo_sharded"] = bench_config5(args, amd, dev, rank, world)
     if world == 1 and not args.no_extras:
+        progress(rank, "extras")
         result["extras"] = bench_extras(args, amd, dev)
     if world == 1 and not args.no_cpu:   # rank 0 at N=1 only
+        progress(rank, "CPU baseline (extraction + matching)")
         result["cpu_baseline"] = cpu_baseline(pool_np[: min(len(pool_np), 512)], NF, args.cpu_seconds)
         result["speedup_vs_cpu_baseline"] = round(value / result["cpu_baseline"]["value"], 1)
     if rank == 0:

@@ -154,7 +154,8 @@ typedef struct {
      * the landmark back-substitution and point updates.  Unlike g2o (vertex locks: arrival-order sums) every sum keeps the
      * serial order, so the variant is bitwise identical to the single-thread oracle. */
     int threads;
-    double* eprod;    /* [n_edges][72] per-edge quadratic-form terms of the parallel buildSystem */
+    double* eprod;    /* [n_edges][54] per-edge pose terms of the parallel buildSystem */
+    double* BD;       /* [n_edges][18] Hpl_e Dinv of the parallel Schur */
     double* dbl;      /* [M][3] Dinv b_l of the parallel Schur */
     int *pose_a_start, *pose_a;   /* per free pose index: its pt_edges positions, landmark-ascending */
     int *pt_k_start, *pt_k;       /* per point index / free pose index: its act positions k, ascending */
@@ -375,83 +376,96 @@ static void init_optimization(lba_ctx* c, int level)
 
 /* ------------------------------------------------------------ buildSystem */
 
-/* OpenMP buildSystem: the per-edge linearisation and quadratic-form terms in parallel
- * (G/core/block_solver.hpp:528), then the block sums in edge order, term by term as the serial
- * loop adds them (so every accumulator sees the same sequence of additions). */
+#ifdef LBA_ORACLE_TIMING
+#include <time.h>
+static double g_tp[8];
+static double now_s(void) { struct timespec ts; clock_gettime(CLOCK_MONOTONIC, &ts); return ts.tv_sec + 1e-9 * ts.tv_nsec; }
+#define TP(i, stmt) do { const double t0_ = now_s(); stmt; g_tp[i] += now_s() - t0_; } while (0)
+void oracle_lba_phase_times(double* out)   /* errors, chi2, build, push, schur_solve, update (s); resets */
+{
+    for (int i = 0; i < 8; i++) { out[i] = g_tp[i]; g_tp[i] = 0; }
+}
+#else
+#define TP(i, stmt) stmt
+#endif
+/* OpenMP buildSystem (G/core/block_solver.hpp:528), bitwise the serial loop: every accumulator
+ * receives the serial loop's additions in the serial (act) order.
+ *  A. in parallel over landmarks: each landmark's edges in act order are linearised, the landmark
+ *     blocks Hll / b_l accumulated in place, Hpl written per edge, and the edge's pose terms
+ *     (Hpp_e 36 | b_p,e 6 per residual row) stored per act edge;
+ *  B. in parallel over (pose, row of the 6x6 block): the pose's edges in act order add their
+ *     stored terms — 6 P work items, so a window with fewer poses than threads still spreads. */
 static void build_system_omp(lba_ctx* c)
 {
     const lba_problem_t* p = c->p;
-#pragma omp parallel for schedule(static) OMP_IF(c)
-    for (int k = 0; k < c->n_act; k++) {
-        const int e = c->act_edges[k];
-        double A[9], B[18];
-        const int D = linearize(c, e, A, B);
-        const double w = p->edge_info[e];
-        const double* er = c->err + 3 * e;
-        double rho1 = 1.0;
-        if (c->robust[e]) {
-            const double chi = edge_chi2(c, e), d = huber_delta(c, e);
-            if (chi > d * d) rho1 = d / sqrt(chi);
-        }
-        const double W = rho1 * w;
-        double om_r[3] = {0, 0, 0};
-        for (int r = 0; r < D; r++) om_r[r] = -(w * er[r]) * rho1;
-        double* t = c->eprod + 72 * (size_t)k;   /* hl 9 | bl 3x3 | hp 36 | bp 6x3 */
-        for (int i = 0; i < 3; i++) {
-            for (int r = 0; r < 3; r++) t[9 + i * 3 + r] = r < D ? A[r * 3 + i] * om_r[r] : 0.0;
-            for (int j = 0; j < 3; j++) {
-                double s = 0;
-                for (int r = 0; r < D; r++) s += A[r * 3 + i] * W * A[r * 3 + j];
-                t[i * 3 + j] = s;
-            }
-        }
-        if (c->pose_idx[p->edge_pose[e]] >= 0) {
-            double* hpl = c->Hpl + 18 * e;
-            for (int i = 0; i < 6; i++) {
-                for (int r = 0; r < 3; r++) t[54 + i * 3 + r] = r < D ? B[r * 6 + i] * om_r[r] : 0.0;
-                for (int j = 0; j < 6; j++) {
-                    double s = 0;
-                    for (int r = 0; r < D; r++) s += B[r * 6 + i] * W * B[r * 6 + j];
-                    t[18 + i * 6 + j] = s;
-                }
-                for (int j = 0; j < 3; j++) {
-                    double s = 0;
-                    for (int r = 0; r < D; r++) s += B[r * 6 + i] * W * A[r * 3 + j];
-                    hpl[i * 3 + j] = s;
-                }
-            }
-        }
-    }
-    /* the block sums: every landmark block over its edges in act order (in parallel over
-     * landmarks), every pose block entry likewise (in parallel over pose x entry) — each
-     * accumulator sees the serial loop's sequence of additions */
-#pragma omp parallel for schedule(static) OMP_IF(c)
+#ifdef LBA_ORACLE_TIMING
+    const double tA = now_s();
+#endif
+#pragma omp parallel for schedule(dynamic, 16) OMP_IF(c)
     for (int li = 0; li < c->M; li++) {
-        double* hl = c->Hll + 9 * li;
-        double* bl = c->bl + 3 * li;
+        double hl[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, bl[3] = {0, 0, 0};   /* stored once, below */
         for (int a = c->pt_k_start[li]; a < c->pt_k_start[li + 1]; a++) {
             const int k = c->pt_k[a];
-            const int D = p->edge_stereo[c->act_edges[k]] ? 3 : 2;
-            const double* t = c->eprod + 72 * (size_t)k;
+            const int e = c->act_edges[k];
+            double A[9], B[18];
+            const int D = linearize(c, e, A, B);
+            const double w = p->edge_info[e];
+            const double* er = c->err + 3 * e;
+            double rho1 = 1.0;
+            if (c->robust[e]) {
+                const double chi = edge_chi2(c, e), d = huber_delta(c, e);
+                if (chi > d * d) rho1 = d / sqrt(chi);
+            }
+            const double W = rho1 * w;
+            double om_r[3] = {0, 0, 0};
+            for (int r = 0; r < D; r++) om_r[r] = -(w * er[r]) * rho1;
             for (int i = 0; i < 3; i++) {
-                for (int r = 0; r < D; r++) bl[i] += t[9 + i * 3 + r];
-                for (int j = 0; j < 3; j++) hl[i * 3 + j] += t[i * 3 + j];
+                for (int r = 0; r < D; r++) bl[i] += A[r * 3 + i] * om_r[r];
+                for (int j = 0; j < 3; j++) {
+                    double s = 0;
+                    for (int r = 0; r < D; r++) s += A[r * 3 + i] * W * A[r * 3 + j];
+                    hl[i * 3 + j] += s;
+                }
+            }
+            if (c->pose_idx[p->edge_pose[e]] >= 0) {
+                double* hpl = c->Hpl + 18 * e;
+                double* t = c->eprod + 54 * (size_t)k;   /* per block row i: hp 6 | bp terms 3 */
+                for (int i = 0; i < 6; i++) {
+                    for (int r = 0; r < 3; r++) t[9 * i + 6 + r] = r < D ? B[r * 6 + i] * om_r[r] : 0.0;
+                    for (int j = 0; j < 6; j++) {
+                        double s = 0;
+                        for (int r = 0; r < D; r++) s += B[r * 6 + i] * W * B[r * 6 + j];
+                        t[9 * i + j] = s;
+                    }
+                    for (int j = 0; j < 3; j++) {
+                        double s = 0;
+                        for (int r = 0; r < D; r++) s += B[r * 6 + i] * W * A[r * 3 + j];
+                        hpl[i * 3 + j] = s;
+                    }
+                }
             }
         }
+        memcpy(c->Hll + 9 * li, hl, sizeof(hl));
+        memcpy(c->bl + 3 * li, bl, sizeof(bl));
     }
+#ifdef LBA_ORACLE_TIMING
+    const double tB = now_s();
+    g_tp[6] += tB - tA;
+#endif
 #pragma omp parallel for schedule(dynamic, 1) OMP_IF(c)
-    for (int pi = 0; pi < c->P; pi++) {
-        double* hp = c->Hpp + 36 * pi;
-        double* bp = c->bp + 6 * pi;
+    for (int item = 0; item < 6 * c->P; item++) {
+        const int pi = item / 6, i = item % 6;
+        /* local accumulators (neighbouring items' rows share cache lines), stored once */
+        double hp[6] = {0, 0, 0, 0, 0, 0}, bp = 0.0;
         for (int a = c->po_k_start[pi]; a < c->po_k_start[pi + 1]; a++) {
             const int k = c->po_k[a];
             const int D = p->edge_stereo[c->act_edges[k]] ? 3 : 2;
-            const double* t = c->eprod + 72 * (size_t)k;
-            for (int i = 0; i < 6; i++) {
-                for (int r = 0; r < D; r++) bp[i] += t[54 + i * 3 + r];
-                for (int j = 0; j < 6; j++) hp[i * 6 + j] += t[18 + i * 6 + j];
-            }
+            const double* t = c->eprod + 54 * (size_t)k + 9 * i;
+            for (int r = 0; r < D; r++) bp += t[6 + r];
+            for (int j = 0; j < 6; j++) hp[j] += t[j];
         }
+        for (int j = 0; j < 6; j++) c->Hpp[36 * pi + 6 * i + j] = hp[j];
+        c->bp[6 * pi + i] = bp;
     }
 }
 
@@ -571,6 +585,15 @@ static int schur_solve(lba_ctx* c, double lambda)
             inv3(D, Di);
             const double* b = c->bl + 3 * l;
             for (int i = 0; i < 3; i++) c->dbl[3 * l + i] = Di[i * 3] * b[0] + Di[i * 3 + 1] * b[1] + Di[i * 3 + 2] * b[2];
+            for (int a = c->pt_edge_start[l]; a < c->pt_edge_start[l + 1]; a++) {   /* Hpl_e Dinv, once per edge */
+                const int e = c->pt_edges[a];
+                if (c->pose_idx[p->edge_pose[e]] < 0) continue;
+                const double* Bi = c->Hpl + 18 * e;
+                double* BD = c->BD + 18 * (size_t)e;
+                for (int r = 0; r < 6; r++)
+                    for (int q = 0; q < 3; q++)
+                        BD[r * 3 + q] = Bi[r * 3] * Di[q] + Bi[r * 3 + 1] * Di[3 + q] + Bi[r * 3 + 2] * Di[6 + q];
+            }
         }
         /* work items = pose row x a range of block columns (the row's landmarks are walked by
          * every item of the row, each forming the products of its own columns only), so a
@@ -582,37 +605,43 @@ static int schur_solve(lba_ctx* c, double lambda)
             const int col0 = row + (int)((long long)(c->P - row) * qc / nq);
             const int col1 = row + (int)((long long)(c->P - row) * (qc + 1) / nq);
             if (col0 >= col1 && qc > 0) continue;
+            /* the item's 6 x 6 (col1 - col0) blocks and the row's coef accumulate in locals (items
+             * of neighbouring rows / column ranges share cache lines), from S's current values,
+             * in the serial order; stored once */
+            const int nc = 6 * (col1 - col0);
+            double acc[6 * (nc > 0 ? nc : 1)];
+            double cf[6] = {0, 0, 0, 0, 0, 0};
+            for (int r = 0; r < 6; r++)
+                for (int q = 0; q < nc; q++) acc[r * nc + q] = S[(6 * row + r) * np + 6 * col0 + q];
+            if (qc == 0)
+                for (int r = 0; r < 6; r++) cf[r] = coef[6 * row + r];
             for (int ka = c->pose_a_start[row]; ka < c->pose_a_start[row + 1]; ka++) {
                 const int a = c->pose_a[ka];
                 const int l = c->point_idx[p->edge_point[c->pt_edges[a]]];
-                const double* Di = c->Dinv + 9 * l;
                 const double* db = c->dbl + 3 * l;
                 const int s1 = c->pt_edge_start[l + 1];
-                {
-                    const int e1 = c->pt_edges[a];
-                    const int i1 = row;
-                    const double* Bi = c->Hpl + 18 * e1;
-                    double BD[18];
+                const int e1 = c->pt_edges[a];
+                const double* Bi = c->Hpl + 18 * e1;
+                const double* BD = c->BD + 18 * (size_t)e1;
+                if (qc == 0)
+                    for (int r = 0; r < 6; r++) cf[r] += Bi[r * 3] * db[0] + Bi[r * 3 + 1] * db[1] + Bi[r * 3 + 2] * db[2];
+                for (int bb = a; bb < s1; bb++) {
+                    const int e2 = c->pt_edges[bb];
+                    const int i2 = c->pose_idx[p->edge_pose[e2]];
+                    if (i2 < col0 || i2 >= col1) continue;   /* (fixed poses: -1) */
+                    const double* Bj = c->Hpl + 18 * e2;
+                    double* blk = acc + 6 * (i2 - col0);
                     for (int r = 0; r < 6; r++)
-                        for (int q = 0; q < 3; q++)
-                            BD[r * 3 + q] = Bi[r * 3] * Di[q] + Bi[r * 3 + 1] * Di[3 + q] + Bi[r * 3 + 2] * Di[6 + q];
-                    if (qc == 0)
-                        for (int r = 0; r < 6; r++)
-                            coef[6 * i1 + r] += Bi[r * 3] * db[0] + Bi[r * 3 + 1] * db[1] + Bi[r * 3 + 2] * db[2];
-                    for (int bb = a; bb < s1; bb++) {
-                        const int e2 = c->pt_edges[bb];
-                        const int i2 = c->pose_idx[p->edge_pose[e2]];
-                        if (i2 < col0 || i2 >= col1) continue;   /* (fixed poses: -1) */
-                        const double* Bj = c->Hpl + 18 * e2;
-                        for (int r = 0; r < 6; r++)
-                            for (int q = 0; q < 6; q++) {
-                                const double v = BD[r * 3] * Bj[q * 3] + BD[r * 3 + 1] * Bj[q * 3 + 1] +
-                                                 BD[r * 3 + 2] * Bj[q * 3 + 2];
-                                S[(6 * i1 + r) * np + 6 * i2 + q] -= v;
-                            }
-                    }
+                        for (int q = 0; q < 6; q++) {
+                            const double v = BD[r * 3] * Bj[q * 3] + BD[r * 3 + 1] * Bj[q * 3 + 1] + BD[r * 3 + 2] * Bj[q * 3 + 2];
+                            blk[r * nc + q] -= v;
+                        }
                 }
             }
+            for (int r = 0; r < 6; r++)
+                for (int q = 0; q < nc; q++) S[(6 * row + r) * np + 6 * col0 + q] = acc[r * nc + q];
+            if (qc == 0)
+                for (int r = 0; r < 6; r++) coef[6 * row + r] = cf[r];
         }
     }
     for (int l = 0; l < c->M && c->threads <= 1; l++) {
@@ -662,10 +691,13 @@ static int schur_solve(lba_ctx* c, double lambda)
      * (AMD-permuted, sparse) is not reproducible without Eigen; this recurrence is the one the
      * GPU factorisation (k_ldlt_solve) follows element for element. */
     int ok = 1;
+#ifdef LBA_ORACLE_TIMING
+    const double tL = now_s();
+#endif
     double* d = (double*)malloc(sizeof(double) * (np + 1));
     /* (OpenMP variant, large systems: the rows i > j of column j in parallel — each element is
      * the same operation sequence, so the factor is bitwise the serial one) */
-#pragma omp parallel if (c->threads > 1 && np >= 96) num_threads(c->threads > 1 ? c->threads : 1)
+#pragma omp parallel if (c->threads > 1 && np >= 256) num_threads(c->threads > 1 ? c->threads : 1)
     for (int j = 0; j < np; j++) {
 #pragma omp single
         {
@@ -684,6 +716,9 @@ static int schur_solve(lba_ctx* c, double lambda)
             S[i * np + j] = v / dj;   /* L(i, j) */
         }
     }
+#ifdef LBA_ORACLE_TIMING
+    g_tp[7] += now_s() - tL;
+#endif
     double* xp = c->x;
     if (ok) {
         for (int i = 0; i < np; i++) {
@@ -775,11 +810,12 @@ static int terminated(const lba_ctx* c, const volatile uint8_t* stop, const lba_
 
 static int lm_iteration(lba_ctx* c, int iteration, const volatile uint8_t* stop, lba_result_t* r)
 {
-    compute_active_errors(c);
-    double currentChi = active_robust_chi2(c);
+    TP(0, compute_active_errors(c));
+    double currentChi;
+    TP(1, currentChi = active_robust_chi2(c));
     double tempChi = currentChi;
     const double iniChi = currentChi;
-    build_system(c);
+    TP(2, build_system(c));
     share_pose_system(c);
     if (iteration == 0) {
         c->lambda = lambda_init(c);
@@ -790,13 +826,14 @@ static int lm_iteration(lba_ctx* c, int iteration, const volatile uint8_t* stop,
     int qmax = 0;
     const int nx = 6 * c->P + 3 * c->M;
     do {
-        push_state(c);
+        TP(3, push_state(c));
         const double lam = c->lambda;
-        const int ok2 = schur_solve(c, lam);
+        int ok2;
+        TP(4, ok2 = schur_solve(c, lam));
         if (!ok2) memset(c->x, 0, sizeof(double) * nx);   /* _x is left unchanged on failure; update is harmless */
-        update(c);
-        compute_active_errors(c);
-        tempChi = active_robust_chi2(c);
+        TP(5, update(c));
+        TP(0, compute_active_errors(c));
+        TP(1, tempChi = active_robust_chi2(c));
         if (!ok2) tempChi = DBL_MAX;
         rho = currentChi - tempChi;
         double scale = 0.;
@@ -923,7 +960,8 @@ static int lba_run(const lba_problem_t* p, const lba_options_t* o, const volatil
     c.pt_edge_start = (int*)malloc(sizeof(int) * (NM + 2));
     c.pt_edges = (int*)malloc(sizeof(int) * (NE + 1));
     if (threads > 1) {
-        c.eprod = (double*)malloc(sizeof(double) * 72 * (NE + 1));
+        c.eprod = (double*)malloc(sizeof(double) * 54 * (NE + 1));
+        c.BD = (double*)malloc(sizeof(double) * 18 * (NE + 1));
         c.dbl = (double*)malloc(sizeof(double) * 3 * (NM + 1));
         c.pose_a_start = (int*)malloc(sizeof(int) * (NP + 2));
         c.pose_a = (int*)malloc(sizeof(int) * (NE + 1));
@@ -988,7 +1026,7 @@ done:
     free(c.pq); free(c.pt); free(c.X); free(c.bq); free(c.bt); free(c.bX); free(c.err);
     free(c.level); free(c.robust); free(c.act_edges); free(c.pose_idx); free(c.point_idx);
     free(c.Hpp); free(c.S); free(c.bp); free(c.Hll); free(c.bl); free(c.Hpl); free(c.x); free(c.Dinv);
-    free(c.pt_edge_start); free(c.pt_edges); free(c.eprod); free(c.dbl);
+    free(c.pt_edge_start); free(c.pt_edges); free(c.eprod); free(c.BD); free(c.dbl);
     free(c.pose_a_start); free(c.pose_a);
     free(c.pt_k_start); free(c.pt_k); free(c.po_k_start); free(c.po_k);
     (void)cmp_i64_idx_base;
