@@ -351,8 +351,21 @@ def bench_lba(args, amd, dev, local, rank, world):
     # first solves instantiate them); LocalMapping calls LocalBundleAdjustment once per keyframe,
     # so the steady state is what it sees
     call = ctx.prepared(pb)
-    for _ in range(3):
-        call()
+    grp_live = native   # the group's solves are the timed ones (False after a fallback)
+    try:
+        for _ in range(3):
+            call()
+    except RuntimeError as exc:
+        if not native:
+            raise
+        # the group failed on this node (e.g. a timed-out exchange): rank 0 times its own device
+        # alone and says so; the waiting ranks still get the broadcast below
+        fallback = f"lba_group_solve failed: {exc}; rank 0 alone"
+        grp_live = False
+        ctx = amd.LocalBA(local)
+        call = ctx.prepared(pb)
+        for _ in range(3):
+            call()
     if world > 1 and not native:   # (native: the other ranks wait at the barrier below)
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
@@ -363,8 +376,12 @@ def bench_lba(args, amd, dev, local, rank, world):
         times.append(time.perf_counter() - t0)
         iters += sum(its)
     tot = sum(times)
-    if native:
+    if grp_live:
         ex_ms, n_ex = ctx.stats()
+        r = ctx.solve(pb)
+        st = None
+        erased = int(np.count_nonzero(r["edge_erase"]))
+    elif native:   # (fallback: rank 0's own solve, no stage split)
         r = ctx.solve(pb)
         st = None
         erased = int(np.count_nonzero(r["edge_erase"]))
@@ -392,8 +409,10 @@ def bench_lba(args, amd, dev, local, rank, world):
            "n_gpus": world,
            "native_group_unavailable": fallback,
            "collective": ("none" if world == 1 else
-                          "library peer-to-peer all-reduce over xGMI (lba_group, one process driving every device)"
-                          if native else "torch.distributed all_reduce callback (RCCL), one process per GPU"),
+                          "library device-side exchange over xGMI (lba_group: flag words + peer reads, one process "
+                          "driving every device, slots in HIP graphs)" if grp_live else
+                          "none (the group failed; rank 0's device alone)" if native else
+                          "torch.distributed all_reduce callback (RCCL), one process per GPU"),
            # LM decisions of the last timed solve: identical for every world size (landmark shards
            # only reorder the f64 sums; tests/test_bench_ranks.py compares N=1 with N=2)
            "decisions": {"iterations": [int(x) for x in r["iterations"]], "trials": int(r["trials"]),
@@ -402,8 +421,10 @@ def bench_lba(args, amd, dev, local, rank, world):
     if st is not None:
         out["stage_ms_per_solve"] = {k: round(st[k] / args.lba_solves, 4) for k in
                                      ("linearize_ms", "schur_ms", "solve_ms", "update_ms")}
-    if native:
-        out["exchange_us_per_collective"] = round(1000 * ex_ms / max(n_ex, 1), 2)
+    if grp_live:
+        # (host-ordered exchange: events around each collective; the device-side default has
+        # none — its cost is in the kernel trace as k_grp_sync / k_grp_reduce)
+        out["exchange_us_per_collective"] = round(1000 * ex_ms / max(n_ex, 1), 2) if ex_ms > 0 else None
         out["collectives_per_trial"] = round(n_ex / max(1, (3 + args.lba_solves) * r["trials"]), 2)
     if st is not None:   # (the native group's solves have no per-slot stage events)
         out["roofline"] = lba_roofline(pb, out, world)

@@ -655,13 +655,15 @@ constexpr int kPtBatch = 2;
 struct PtPrefetch {
     int a0, a1;
     double v[kPtBatch][9];
+    int k[kPtBatch], pi[kPtBatch];   // the same edges' act positions, pose indices and Hpl blocks
+    double w[kPtBatch][18];          // (k_vertex_schur's Hpl D^-1 products)
 };
 __device__ __forceinline__ void landmark_prefetch(const LbaDev& d, int l, int sub, PtPrefetch& f) {
     const int lc = min(l, d.M - 1);
     f.a0 = d.ptStart[lc] + sub;
     f.a1 = l < d.M ? d.ptStart[lc + 1] : f.a0;
     const int last = max(d.ptStart[lc + 1] - 1, 0);
-    int k[kPtBatch];
+    int* const k = f.k;
 #pragma unroll
     for (int u = 0; u < kPtBatch; u++) k[u] = d.ptAct[min(f.a0 + kLanesPerPt * u, last)];
 #pragma unroll
@@ -670,6 +672,14 @@ __device__ __forceinline__ void landmark_prefetch(const LbaDev& d, int l, int su
         for (int i = 0; i < 6; i++) f.v[u][i] = d.Hll_e[6 * (size_t)k[u] + i];
 #pragma unroll
         for (int i = 0; i < 3; i++) f.v[u][6 + i] = d.bl_e[3 * (size_t)k[u] + i];
+        f.pi[u] = d.actPi[k[u]];
+        const double2* B = reinterpret_cast<const double2*>(d.Hpl_e + 18 * (size_t)k[u]);
+#pragma unroll
+        for (int h = 0; h < 9; h++) {   // (a fixed pose's edge reads its unused Hpl slot)
+            const double2 x = B[h];
+            f.w[u][2 * h] = x.x;
+            f.w[u][2 * h + 1] = x.y;
+        }
     }
 }
 __device__ __forceinline__ void landmark_reduce(const LbaDev& d, int l, int sub, double h[6], double b[3],
@@ -780,6 +790,25 @@ __device__ __forceinline__ void hpl_dinv_edges(const LbaDev& d, int l, const dou
     }
 }
 
+// hpl_dinv_edges for lane `sub` of a landmark's kLanesPerPt group with its first kPtBatch edges'
+// Hpl blocks already in registers (landmark_prefetch)
+__device__ __forceinline__ void hpl_dinv_prefetched(const LbaDev& d, const double Di[9], const PtPrefetch& f) {
+#pragma unroll
+    for (int u = 0; u < kPtBatch; u++) {
+        if (f.a0 + kLanesPerPt * u >= f.a1 || f.pi[u] < 0) continue;
+        double v[18];
+#pragma unroll
+        for (int r = 0; r < 6; r++)
+#pragma unroll
+            for (int q = 0; q < 3; q++)
+                v[r * 3 + q] = __builtin_fma(f.w[u][r * 3 + 2], Di[6 + q],
+                                             __builtin_fma(f.w[u][r * 3 + 1], Di[3 + q], f.w[u][r * 3] * Di[q]));
+        double2* U = reinterpret_cast<double2*>(d.Ae + 18 * (size_t)f.k[u]);
+#pragma unroll
+        for (int h = 0; h < 9; h++) U[h] = make_double2(v[2 * h], v[2 * h + 1]);
+    }
+}
+
 // Per landmark with lambda (G/core/block_solver.hpp:380-398): D^-1 = (Hll + lambda I)^-1
 // (Eigen's 3x3 cofactor inverse) and D^-1 b_l.
 // Fused slots: an iteration that was just linearised (phase 0) starts here — lm_begin from
@@ -885,7 +914,8 @@ __global__ __launch_bounds__(256) void k_vertex_schur(LbaDev d, int nChi) {
     double Di[9];
     dinv_of(m, lambda, Di);
     if (sub == 0) dinv_store(d, l, Di, blv);
-    hpl_dinv_edges(d, l, Di, sub, kLanesPerPt);
+    hpl_dinv_prefetched(d, Di, lf);   // the lane's first kPtBatch edges, their Hpl blocks prefetched
+    hpl_dinv_edges(d, l, Di, sub + kLanesPerPt * kPtBatch, kLanesPerPt);
 }
 
 // Reduced camera system (G/core/block_solver.hpp:408-440): one workgroup per pose-pair block
@@ -1776,6 +1806,9 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_solve(const double* __restrict__
         if (kLds && m > 0) {
             for (int ti = wave; ti < m; ti += kLdlT / 64) trail_tile(jb, (kb + 1 + ti) * kNB, (kb + 1) * kNB);
             __syncthreads();
+            // (tried: these tiles on the panel waves only, each its own rows, the diagonal one
+            // flagged by group 0 — no barrier, but the panel waves' 3-4 tile updates then sit on
+            // the pivot chain's critical path: 46.5 k -> 59 k cycles for the look-ahead steps)
             const int jn = jb + kNB, ng = panel_groups(np, jn);
             arriveTarget += ng;
             if (wave < ng) {
@@ -2478,6 +2511,64 @@ __global__ __launch_bounds__(256) void k_unpack(double* __restrict__ buf, const 
     for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) buf[i] = ws[i];
 }
 
+// ---- device-side exchange of a device group (lba_group): no host in the loop, so the slots of a
+// sharded solve are captured into HIP graphs like the single-process ones.  Every rank's
+// workspace and flag words live in fine-grained memory on its own device; a collective is
+//   k_pack_sys (system-scope stores of the rank's contribution)
+//   k_grp_sync(0): epoch e = ++epoch; ready[rank] = e (release, system scope); wait ready[p] >= e
+//   k_grp_reduce: every rank sums all ranks' slices in rank order (system-scope loads over xGMI)
+//   k_grp_sync(1): read[rank] = e; wait read[p] >= e (nobody packs into a workspace still read)
+// Every rank runs the same sequence of collectives (identical LM decisions), so epochs agree.
+// A wait that exceeds ~1 s (a peer gone) sets the rank's error word and gives up: the solve then
+// fails with ORB_EGPU instead of hanging the device.
+constexpr int kMaxGroupDev = 16;
+struct GrpDev {
+    uint32_t* flags[kMaxGroupDev];   // rank p's flag words: [0] ready epoch, [32] read epoch
+    const double* ws[kMaxGroupDev];  // rank p's workspace
+    uint32_t* epoch;                 // this rank's collective counter
+    int* err;                        // this rank's error word
+    int rank, n;
+};
+__global__ void k_grp_sync(GrpDev g, int which) {
+    if (threadIdx.x != 0) return;
+    const bool failed = __hip_atomic_load(g.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+    uint32_t e = *g.epoch;
+    if (which == 0) {
+        e += 1;
+        *g.epoch = e;
+    }
+    const int w = which ? 32 : 0;
+    __hip_atomic_store(g.flags[g.rank] + w, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (failed) return;   // after one timed-out wait the rest of the solve does not wait (it fails anyway)
+    int spins = 0;   // bounded by iterations, not by a clock: ~1 s
+    for (int q = 0; q < g.n; q++) {
+        if (q == g.rank) continue;
+        while (__hip_atomic_load(g.flags[q] + w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+            if (++spins > (1 << 19)) {   // (an iteration is a sleep plus a system-scope load: ~1-3 us)
+                __hip_atomic_store(g.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                return;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+}
+__global__ __launch_bounds__(256) void k_pack_sys(double* __restrict__ ws, const double* __restrict__ buf, size_t n,
+                                                  const LmState* st, int want) {
+    const bool off = lm_off(st, want);
+    for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+        __hip_atomic_store(ws + i, off ? 0.0 : buf[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__global__ __launch_bounds__(256) void k_grp_reduce(GrpDev g, size_t n, int op, double* __restrict__ out) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        double v = __hip_atomic_load(g.ws[0] + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (int r = 1; r < g.n; r++) {
+            const double w = __hip_atomic_load(g.ws[r] + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            v = op ? fmax(v, w) : v + w;
+        }
+        out[i] = v;
+    }
+}
+
 
 // Start of an LM iteration (G/core/optimization_algorithm_levenberg.cpp:61-90): currentChi
 // from the linearisation's robust chi2 (red[0]), lambda from computeLambdaInit (red[1]) at it 0.
@@ -2891,6 +2982,8 @@ struct lba_context {
     size_t wsDoubles = 0;
     lba_allreduce_fn allreduce = nullptr;
     void* commUser = nullptr;
+    const orbamd::GrpDev* grp = nullptr;   // device-side exchange (lba_group): replaces the callback
+    bool grpGraphs = false;                // ... and its slots may be graph-captured (every rank on its own device)
     // device buffers: a grow-only arena reused across solves (hipMalloc / hipFree per buffer
     // and per call cost more than a small LBA's whole LM loop; hipFree also synchronises)
     std::vector<std::pair<char*, size_t>> chunks;   // (base, size); the last one is bumped
@@ -3069,6 +3162,17 @@ int upload(lba_context* c, T** dst, const std::vector<T>& v) {
 
 // All-reduce of an LM-loop buffer: staged through the workspace by guarded kernels, so a
 // slot whose phase is skipped reduces zeros and leaves the buffer alone.
+// the device-side collective of a group over the first n doubles of the ranks' workspaces
+static int grp_exchange(lba_context* c, size_t n, int op) {
+    const orbamd::GrpDev& g = *c->grp;
+    const unsigned blocks = (unsigned)std::max<size_t>(1, std::min<size_t>(1024, (n + 255) / 256));
+    hipLaunchKernelGGL(k_grp_sync, dim3(1), dim3(64), 0, c->stream, g, 0);
+    hipLaunchKernelGGL(k_grp_reduce, dim3(blocks), dim3(256), 0, c->stream, g, n, op, c->wsOut);
+    hipLaunchKernelGGL(k_grp_sync, dim3(1), dim3(64), 0, c->stream, g, 1);
+    ORB_HIP_TRY(hipGetLastError());
+    return ORB_OK;
+}
+
 // Several buffers with the same op ride in one collective (packed back to back in the workspace):
 // a collective costs far more than the pack / unpack launches around it.
 struct CommSeg {
@@ -3079,14 +3183,19 @@ static int comm_allreduce_segs(lba_context* c, std::initializer_list<CommSeg> se
     if (c->world <= 1) return ORB_OK;
     size_t tot = 0;
     for (const CommSeg& sg : segs) tot += sg.n;
-    if (!c->allreduce || !c->ws || tot > c->wsDoubles) return ORB_EINVAL;
+    if ((!c->allreduce && !c->grp) || !c->ws || tot > c->wsDoubles) return ORB_EINVAL;
     size_t off = 0;
     for (const CommSeg& sg : segs) {
         const unsigned g = (unsigned)std::min<size_t>(1024, (sg.n + 255) / 256);
-        hipLaunchKernelGGL(k_pack, dim3(g), dim3(256), 0, c->stream, c->ws + off, sg.p, sg.n, st, want);
+        if (c->grp) hipLaunchKernelGGL(k_pack_sys, dim3(g), dim3(256), 0, c->stream, c->ws + off, sg.p, sg.n, st, want);
+        else hipLaunchKernelGGL(k_pack, dim3(g), dim3(256), 0, c->stream, c->ws + off, sg.p, sg.n, st, want);
         off += sg.n;
     }
-    if (c->allreduce(c->commUser, 0, tot, op) != 0) return ORB_EGPU;
+    if (c->grp) {
+        TRY(grp_exchange(c, tot, op));
+    } else if (c->allreduce(c->commUser, 0, tot, op) != 0) {
+        return ORB_EGPU;
+    }
     const double* res = c->wsOut ? c->wsOut : c->ws;
     off = 0;
     for (const CommSeg& sg : segs) {
@@ -3166,6 +3275,8 @@ int lba_set_comm(lba_context* c, int rank, int world, double* d_workspace, size_
     c->wsDoubles = ws_doubles;
     c->allreduce = fn;
     c->commUser = user;
+    c->grp = nullptr;   // (lba_group installs its device-side exchange after this call)
+    c->grpGraphs = false;
     return ORB_OK;
 }
 
@@ -3323,12 +3434,13 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
     auto agreed = [&](bool mine, bool* out) -> int {
         *out = mine;
         if (c->world <= 1) return ORB_OK;
-        if (!c->allreduce || !c->ws || c->wsDoubles < 1) return ORB_EINVAL;
+        if ((!c->allreduce && !c->grp) || !c->ws || c->wsDoubles < 1) return ORB_EINVAL;
         double* h = c->h_scal + 256;
         h[0] = mine ? 1.0 : 0.0;
         ORB_HIP_TRY(hipMemcpyAsync(c->ws, h, 8, hipMemcpyHostToDevice, s));
         TRY(lba_wait(c));
-        if (c->allreduce(c->commUser, 0, 1, 0) != 0) return ORB_EGPU;
+        if (c->grp) TRY(grp_exchange(c, 1, 0));
+        else if (c->allreduce(c->commUser, 0, 1, 0) != 0) return ORB_EGPU;
         ORB_HIP_TRY(hipMemcpyAsync(h, c->wsOut ? c->wsOut : c->ws, 8, hipMemcpyDeviceToHost, s));
         TRY(lba_wait(c));
         *out = h[0] > 0.5;
@@ -3676,15 +3788,18 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         // rejected trials), looked up by every captured launch parameter
         auto slot_graph = [&](int nslots, hipGraphExec_t* out, bool firstGroup, bool close) -> int {
             *out = nullptr;
-            if (c->world != 1 || c->profile || s == nullptr || std::getenv("ORB_LBA_NO_GRAPH")) return ORB_OK;
+            if ((c->world != 1 && !(c->grp && c->grpGraphs)) || c->profile || s == nullptr || std::getenv("ORB_LBA_NO_GRAPH"))
+                return ORB_OK;
             struct {
                 LbaDev d;
                 const void* ptrs[4];
                 double h[2];
                 int v[8];
+                orbamd::GrpDev grp;   // a group's exchange pointers (zero without one)
             } k;
             std::memset(&k, 0, sizeof(k));
             k.d = d;
+            if (c->grp) k.grp = *c->grp;
             k.ptrs[0] = d_freePoses; k.ptrs[1] = d_trace; k.ptrs[2] = d_ldlw ? (const void*)d_ldlw : (const void*)mwBase.A; k.ptrs[3] = s;
             k.h[0] = hm; k.h[1] = hsv;
             k.v[0] = iterations; k.v[1] = maxTrials; k.v[2] = o->fixed_iterations; k.v[3] = root; k.v[4] = nslots;
@@ -3933,6 +4048,11 @@ struct lba_group {
     std::vector<double*> ws, res;
     size_t wsDoubles = 0;
     std::vector<hipEvent_t> evReady, evRead;
+    // device-side exchange (default; ORB_LBA_GROUP_HOST=1 keeps the host-ordered callback above):
+    // per rank 256 B of fine-grained flag memory (ready / read epochs, epoch counter, error word)
+    bool hostPath = false;
+    std::vector<uint32_t*> sync;
+    orbamd::GrpDev gdev[kMaxGroup];
     std::atomic<int> arrive{0};
     std::atomic<unsigned> bgen{0};
     std::atomic<bool> abort{false};
@@ -3997,6 +4117,12 @@ static int group_allreduce(void* user, size_t off, size_t cnt, int op) {
     return 0;
 }
 
+static int group_alloc_fine(int dev, size_t bytes, void** p) {
+    *p = nullptr;
+    if (hipSetDevice(dev) != hipSuccess) return ORB_EGPU;
+    return hipExtMallocWithFlags(p, bytes, hipDeviceMallocFinegrained) == hipSuccess ? ORB_OK : ORB_ENOMEM;
+}
+
 static void group_free_ws(lba_group* g) {
     for (int r = 0; r < g->n; r++) {
         (void)hipSetDevice(g->dev[r]);
@@ -4017,6 +4143,7 @@ void lba_group_destroy(lba_group* g) {
     group_free_ws(g);
     for (int r = 0; r < g->n; r++) {
         (void)hipSetDevice(g->dev[r]);
+        if (r < (int)g->sync.size() && g->sync[r]) (void)hipFree(g->sync[r]);
         if (g->evReady[r]) (void)hipEventDestroy(g->evReady[r]);
         if (g->evRead[r]) (void)hipEventDestroy(g->evRead[r]);
         if (g->ctx[r]) lba_destroy(g->ctx[r]);
@@ -4040,6 +4167,8 @@ int lba_group_create(const int* devices, int n, lba_group** out) {
     g->res.assign(n, nullptr);
     g->evReady.assign(n, nullptr);
     g->evRead.assign(n, nullptr);
+    g->sync.assign(n, nullptr);
+    g->hostPath = std::getenv("ORB_LBA_GROUP_HOST") != nullptr;
     for (int r = 0; r < n; r++) {
         g->ranks[r] = {g, r};
         int st = lba_create(devices[r], &g->ctx[r]);
@@ -4067,6 +4196,11 @@ int lba_group_create(const int* devices, int n, lba_group** out) {
             }
             (void)hipGetLastError();
         }
+    if (!g->hostPath)
+        for (int r = 0; r < n; r++) {
+            int st = group_alloc_fine(devices[r], 256, reinterpret_cast<void**>(&g->sync[r]));
+            if (st) { lba_group_destroy(g); return st; }
+        }
     *out = g;
     return ORB_OK;
 }
@@ -4082,7 +4216,9 @@ int lba_group_solve(lba_group* g, const lba_problem* p, const lba_options* o, co
         group_free_ws(g);
         for (int q = 0; q < n; q++) {
             ORB_HIP_TRY(hipSetDevice(g->dev[q]));
-            if (hipMalloc((void**)&g->ws[q], need * 8) != hipSuccess || hipMalloc((void**)&g->res[q], need * 8) != hipSuccess) {
+            const bool wsOk = g->hostPath ? hipMalloc((void**)&g->ws[q], need * 8) == hipSuccess
+                                          : group_alloc_fine(g->dev[q], need * 8, reinterpret_cast<void**>(&g->ws[q])) == ORB_OK;
+            if (!wsOk || hipSetDevice(g->dev[q]) != hipSuccess || hipMalloc((void**)&g->res[q], need * 8) != hipSuccess) {
                 group_free_ws(g);
                 return ORB_ENOMEM;
             }
@@ -4092,6 +4228,36 @@ int lba_group_solve(lba_group* g, const lba_problem* p, const lba_options* o, co
     for (int q = 0; q < n; q++) {
         TRY(lba_set_comm(g->ctx[q], q, n, g->ws[q], g->wsDoubles, group_allreduce, &g->ranks[q]));
         g->ctx[q]->wsOut = g->res[q];
+    }
+    if (!g->hostPath) {   // fresh epochs: every rank's flags, counter and error word zeroed
+        for (int q = 0; q < n; q++) {   // (ordered before every rank's work: the streams are non-blocking)
+            ORB_HIP_TRY(hipSetDevice(g->dev[q]));
+            ORB_HIP_TRY(hipMemsetAsync(g->sync[q], 0, 256, g->ctx[q]->stream));
+        }
+        for (int q = 0; q < n; q++) {
+            ORB_HIP_TRY(hipSetDevice(g->dev[q]));
+            ORB_HIP_TRY(hipStreamSynchronize(g->ctx[q]->stream));
+        }
+        for (int q = 0; q < n; q++) {
+            orbamd::GrpDev& gd = g->gdev[q];
+            std::memset(&gd, 0, sizeof(gd));
+            for (int p2 = 0; p2 < n; p2++) {
+                gd.flags[p2] = g->sync[p2];
+                gd.ws[p2] = g->ws[p2];
+            }
+            gd.epoch = g->sync[q] + 48;
+            gd.err = reinterpret_cast<int*>(g->sync[q] + 56);
+            gd.rank = q;
+            gd.n = n;
+            g->ctx[q]->grp = &gd;
+        }
+        // Graph-captured slots only when every rank has a device of its own: two ranks on one
+        // device may see their graph launches share a hardware queue, where a rank's waiting
+        // k_grp_sync would block the peer it waits for (measured: a ~1 s stall, then the timeout)
+        bool distinct = true;
+        for (int a = 0; a < n; a++)
+            for (int b2 = a + 1; b2 < n; b2++) distinct = distinct && g->dev[a] != g->dev[b2];
+        for (int q = 0; q < n; q++) g->ctx[q]->grpGraphs = distinct;
     }
     g->abort.store(false);
     g->arrive.store(0);
@@ -4110,6 +4276,13 @@ int lba_group_solve(lba_group* g, const lba_problem* p, const lba_options* o, co
         u.res = lba_result{u.q.data(), u.t.data(), u.X.data(), u.er.data(), u.chi.data(), {0, 0}, 0,
                            q == 0 && r->trace ? u.trace.data() : nullptr, 0, 0};
     }
+    // the arenas consolidated here, one rank at a time: inside the solves a rank's hipFree (which
+    // waits for the whole device) must never run while a peer's exchange kernel waits for that rank
+    for (int q = 0; q < n; q++) {
+        ORB_HIP_TRY(hipSetDevice(g->dev[q]));
+        ORB_HIP_TRY(hipStreamSynchronize(g->ctx[q]->stream));
+        lba_free_all(g->ctx[q]);
+    }
     std::vector<int> st(n, ORB_OK);
     auto run = [&](int q) {
         st[q] = lba_solve(g->ctx[q], p, o, stop, &outs[q].res);
@@ -4119,8 +4292,27 @@ int lba_group_solve(lba_group* g, const lba_problem* p, const lba_options* o, co
     for (int q = 1; q < n; q++) th.emplace_back(run, q);
     run(0);
     for (auto& t : th) t.join();
+    if (std::getenv("ORB_LBA_GROUP_DEBUG"))
+        for (int q = 0; q < n; q++) {
+            uint32_t w[64] = {0};
+            if (!g->hostPath) {
+                (void)hipSetDevice(g->dev[q]);
+                (void)hipMemcpy(w, g->sync[q], 256, hipMemcpyDeviceToHost);
+            }
+            fprintf(stderr, "lba_group rank %d: status %d ready %u read %u epoch %u err %u\n", q, st[q], w[0], w[32], w[48],
+                    w[56]);
+        }
     for (int q = 0; q < n; q++)
         if (st[q] != ORB_OK) return st[q];
+    if (!g->hostPath) {   // a timed-out wait on any rank fails the solve; collectives counted from the epoch
+        for (int q = 0; q < n; q++) {
+            uint32_t w[64];
+            ORB_HIP_TRY(hipSetDevice(g->dev[q]));
+            ORB_HIP_TRY(hipMemcpy(w, g->sync[q], 256, hipMemcpyDeviceToHost));
+            if (w[56] != 0) return ORB_EGPU;
+            if (q == 0) g->exchanges += (long)w[48];
+        }
+    }
     // rank 0's exchange timing (its stream is idle: lba_solve waited for its last group)
     if (g->ntev) {
         ORB_HIP_TRY(hipSetDevice(g->dev[0]));

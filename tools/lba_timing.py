@@ -39,5 +39,9 @@ print(f"median of solves 4..{n - 1}: {1e3 * statistics.median(ts[4:]):.3f} ms", 
 if group:
     ex1 = ba.stats()
     nc = ex1[1] - ex0[1]
-    print(f"group of {group}: {nc} collectives in solves 4..{n - 1}, exchange {1e3 * (ex1[0] - ex0[0]) / max(nc, 1):.2f} us "
-          f"per collective (rank 0's stream, events around the all-reduce)", flush=True)
+    if ex1[0] > 0:
+        print(f"group of {group}: {nc} collectives in solves 4..{n - 1}, exchange {1e3 * (ex1[0] - ex0[0]) / max(nc, 1):.2f} us "
+              f"per collective (rank 0's stream, events around the all-reduce)", flush=True)
+    else:
+        print(f"group of {group}: {nc} collectives in solves 4..{n - 1} (device-side exchange: per-collective time "
+              f"from the kernel trace, k_grp_sync / k_grp_reduce)", flush=True)
