@@ -1,4 +1,4 @@
-# LBA iteration: lba + group tests, config-4 / 60 KF timing, k_ldlt_solve clock split, kernel stats.
+# LBA iteration loop: lba + group + global-BA tests, config-4 / 60 KF timing, k_ldlt_solve clock split (ORB_TIMING variant), config-4 kernel stats.
 set -e
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
