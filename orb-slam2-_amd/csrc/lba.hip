@@ -2540,11 +2540,13 @@ __global__ void k_grp_sync(GrpDev g, int which) {
     const int w = which ? 32 : 0;
     __hip_atomic_store(g.flags[g.rank] + w, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     if (failed) return;   // after one timed-out wait the rest of the solve does not wait (it fails anyway)
-    int spins = 0;   // bounded by iterations, not by a clock: ~1 s
+    // bounded by iterations, not by a clock: ~10-30 s — far above any legitimate wait (a peer's first
+    // launch loads its code objects: ~0.3 s measured as a spurious timeout with a 2^19 bound)
+    int spins = 0;
     for (int q = 0; q < g.n; q++) {
         if (q == g.rank) continue;
         while (__hip_atomic_load(g.flags[q] + w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
-            if (++spins > (1 << 19)) {   // (an iteration is a sleep plus a system-scope load: ~1-3 us)
+            if (++spins > (1 << 24)) {   // (an iteration is a sleep plus a system-scope load: ~0.5-3 us)
                 __hip_atomic_store(g.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 return;
             }
@@ -4051,6 +4053,7 @@ struct lba_group {
     // device-side exchange (default; ORB_LBA_GROUP_HOST=1 keeps the host-ordered callback above):
     // per rank 256 B of fine-grained flag memory (ready / read epochs, epoch counter, error word)
     bool hostPath = false;
+    size_t warmNP = 0, warmNM = 0, warmNE = 0;   // the largest problem the ranks' buffers were grown for
     std::vector<uint32_t*> sync;
     orbamd::GrpDev gdev[kMaxGroup];
     std::atomic<int> arrive{0};
@@ -4168,7 +4171,16 @@ int lba_group_create(const int* devices, int n, lba_group** out) {
     g->evReady.assign(n, nullptr);
     g->evRead.assign(n, nullptr);
     g->sync.assign(n, nullptr);
-    g->hostPath = std::getenv("ORB_LBA_GROUP_HOST") != nullptr;
+    // The device-side exchange needs every rank on a device of its own: ranks sharing a device
+    // may find their streams on one hardware queue, where a rank's waiting k_grp_sync blocks the
+    // peer it waits for (seen as timeouts in a long-lived process with many streams).  Ranks on one
+    // device therefore use the host-ordered exchange, unless ORB_LBA_GROUP_DEVICE=1 (the test hook:
+    // two ranks, the second on a high-priority stream, i.e. another hardware queue)
+    bool distinct = true;
+    for (int a = 0; a < n; a++)
+        for (int b2 = a + 1; b2 < n; b2++) distinct = distinct && devices[a] != devices[b2];
+    const bool forceDev = std::getenv("ORB_LBA_GROUP_DEVICE") != nullptr && n == 2;
+    g->hostPath = std::getenv("ORB_LBA_GROUP_HOST") != nullptr || (!distinct && !forceDev);
     for (int r = 0; r < n; r++) {
         g->ranks[r] = {g, r};
         int st = lba_create(devices[r], &g->ctx[r]);
@@ -4201,6 +4213,20 @@ int lba_group_create(const int* devices, int n, lba_group** out) {
             int st = group_alloc_fine(devices[r], 256, reinterpret_cast<void**>(&g->sync[r]));
             if (st) { lba_group_destroy(g); return st; }
         }
+    if (!g->hostPath && !distinct) {   // (the test hook) rank 1 on the device's high-priority queue
+        int lo = 0, hi = 0;
+        (void)hipSetDevice(devices[1]);
+        lba_context* c1 = g->ctx[1];
+        hipStream_t hs = nullptr;
+        if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+            hipStreamCreateWithPriority(&hs, hipStreamNonBlocking, hi) != hipSuccess) {
+            lba_group_destroy(g);
+            return ORB_EGPU;
+        }
+        if (c1->stream && c1->ownStream) (void)hipStreamDestroy(c1->stream);
+        c1->stream = hs;
+        c1->ownStream = true;
+    }
     *out = g;
     return ORB_OK;
 }
@@ -4276,8 +4302,30 @@ int lba_group_solve(lba_group* g, const lba_problem* p, const lba_options* o, co
         u.res = lba_result{u.q.data(), u.t.data(), u.X.data(), u.er.data(), u.chi.data(), {0, 0}, 0,
                            q == 0 && r->trace ? u.trace.data() : nullptr, 0, 0};
     }
-    // the arenas consolidated here, one rank at a time: inside the solves a rank's hipFree (which
-    // waits for the whole device) must never run while a peer's exchange kernel waits for that rank
+    // No rank may block in a device-synchronising host call (hipFree, and the first-use growth of
+    // the arena / pinned staging) while a peer's exchange kernel waits for it.  A problem larger
+    // than any this group has solved is first solved once per rank alone (world 1, one rank at a
+    // time), which grows every arena and staging buffer to what the sharded solve needs; then the
+    // arenas are consolidated, so inside the sharded solves nothing is allocated or freed.
+    if (!g->hostPath && (NP > g->warmNP || NM > g->warmNM || NE > g->warmNE)) {
+        for (int q = 0; q < n; q++) {
+            lba_context* c = g->ctx[q];
+            const orbamd::GrpDev* gp = c->grp;
+            const bool gg = c->grpGraphs;
+            TRY(lba_set_comm(c, 0, 1, nullptr, 0, nullptr, nullptr));
+            lba_result dry = outs[q].res;
+            dry.trace = nullptr;
+            const int st0 = lba_solve(c, p, o, nullptr, &dry);
+            TRY(lba_set_comm(c, q, n, g->ws[q], g->wsDoubles, group_allreduce, &g->ranks[q]));
+            c->wsOut = g->res[q];
+            c->grp = gp;
+            c->grpGraphs = gg;
+            if (st0 != ORB_OK) return st0;
+        }
+        g->warmNP = std::max(g->warmNP, NP);
+        g->warmNM = std::max(g->warmNM, NM);
+        g->warmNE = std::max(g->warmNE, NE);
+    }
     for (int q = 0; q < n; q++) {
         ORB_HIP_TRY(hipSetDevice(g->dev[q]));
         ORB_HIP_TRY(hipStreamSynchronize(g->ctx[q]->stream));
