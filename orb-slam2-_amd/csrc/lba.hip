@@ -2125,7 +2125,7 @@ __global__ __launch_bounds__(64 * kMwWaves) void k_ldlt_mw_trail(MwLdl m, int kb
 // not out of L2); k_ldlt_mw_bupd (every row above, one per thread, over the chip) subtracts the
 // super-block's contribution L(K0 + c, i) x_{K0 + c}.  The bottom super-block first forms y / d
 // for every row; the top one ends with the fused slots' pose update.
-constexpr int kSB = 128;
+constexpr int kSB = 128;   // (64 measured no faster at np = 1224: 24.1 vs 23.7-23.9 ms per solve)
 __global__ __launch_bounds__(512) void k_ldlt_mw_bsolve(MwLdl m, int K0, double* __restrict__ x, int* __restrict__ flags,
                                                         const LmState* st, PoseTail ptail, int first, int last) {
     if (lm_off(st, 1)) return;
@@ -2199,12 +2199,12 @@ __global__ __launch_bounds__(512) void k_ldlt_mw_bsolve(MwLdl m, int K0, double*
         if (wave == 0) pose_tail(ptail, xfull, st->lambda, lane);
     }
 }
-// 64 rows per workgroup; wave w takes the super-block's columns [32 w, 32 w + 32) with all 32
-// loads in flight, the four partial sums are added in wave order (deterministic)
+// 64 rows per workgroup; wave w takes the super-block's columns [kSB/4 w, kSB/4 (w + 1)) with all
+// its loads in flight, the four partial sums are added in wave order (deterministic)
 __global__ __launch_bounds__(256) void k_ldlt_mw_bupd(MwLdl m, int K0, const double* __restrict__ x, const LmState* st) {
     if (lm_off(st, 1)) return;
     if (__builtin_amdgcn_readfirstlane(*m.fail)) return;
-    static_assert(kSB == 128, "four waves of 32 columns");
+    constexpr int kC = kSB / 4;   // columns per wave
     __shared__ double xs[kSB];
     __shared__ double part[4][64];
     const int np = m.np, n = m.n, ld = np, nsb = min(kSB, np - K0);
@@ -2213,15 +2213,15 @@ __global__ __launch_bounds__(256) void k_ldlt_mw_bupd(MwLdl m, int K0, const dou
     __syncthreads();
     const int i = blockIdx.x * 64 + lane;
     if (i < K0) {
-        double a[32];
+        double a[kC];
 #pragma unroll
-        for (int k = 0; k < 32; k++) {
-            const int c = 32 * w + k;
+        for (int k = 0; k < kC; k++) {
+            const int c = kC * w + k;
             a[k] = c < nsb ? m.A[(size_t)(K0 + c) * ld + i] : 0.0;
         }
         double v = 0.0;
 #pragma unroll
-        for (int k = 31; k >= 0; k--) v = __builtin_fma(-a[k], xs[32 * w + k], v);
+        for (int k = kC - 1; k >= 0; k--) v = __builtin_fma(-a[k], xs[kC * w + k], v);
         part[w][lane] = v;
     }
     __syncthreads();
