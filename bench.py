@@ -501,6 +501,22 @@ def bench_lba_scaled(args, amd, dev, rank, world):
                     "reduced_order": 6 * P, "ms_per_iter": round(1000 * sum(times) / max(iters, 1), 4),
                     "solve_ms": round(1000 * float(np.median(times)), 3), "iterations_per_solve": iters / 5,
                     "trials_per_solve": tr, "ldlt_mfma_flops_per_trial": tiles * 8192}
+        if not native:
+            # the reduced solve's share from one profiled solve (per-slot events, kernels enqueued one
+            # by one): its f64 MFMA rate against the 78.6 TFLOP/s peak.  The MFMA flops are the
+            # trailing-update tiles' (16x16x16 per tile and 16-column step); the pivot
+            # chain's VALU work is not counted
+            ctx.profile(True)
+            rp = ctx.solve(pb)
+            stp = ctx.stats()
+            ctx.profile(False)
+            t_tr = stp["solve_ms"] / max(1, rp["trials"]) * 1e-3
+            if t_tr > 0:
+                ach = tiles * 8192 / t_tr / 1e12
+                out[key]["reduced_solve"] = {"bound": "mfma", "us_per_trial": round(t_tr * 1e6, 1),
+                                             "achieved_tflops": round(ach, 4), "peak": F64_PEAK_TFLOPS,
+                                             "frac": round(ach / F64_PEAK_TFLOPS, 5),
+                                             "source": "one profiled solve (stage events; kernels enqueued one by one)"}
         if world == 1 and not args.no_cpu:
             sys.path.insert(0, str(ROOT / "tests"))
             import oracle_ref as O
