@@ -554,18 +554,22 @@ int lba_stats(lba_context* c, double* ms4, int* iters, int* trials);
  * holds one context per entry of devices[0..n) (n <= 16; a device may repeat: two contexts on one
  * device rehearse the exchange on a one-GPU machine).  lba_group_solve shards the landmarks as
  * lba_set_comm does (rank r owns [r M / n, (r+1) M / n)) and all-reduces the pose blocks, the
- * reduced camera system S + b_s and the LM scalars with the library's own one-shot peer-to-peer
- * kernel over xGMI (every rank reads every rank's slice through peer access and sums in rank
- * order: all ranks take bitwise the same LM decisions); no caller callback.  Same arguments and
- * results as lba_solve (points, edge chi2 and erase flags merged from their owners).  Returns
- * ORB_ENODEV when two listed devices cannot access each other. */
+ * reduced camera system S + b_s and the LM scalars with the library's own exchange over xGMI
+ * (every rank reads every rank's slice through peer access and sums in rank order: all ranks take
+ * bitwise the same LM decisions); no caller callback.  With every rank on its own device the
+ * exchange is device-side (flag words in fine-grained memory, no host in the loop, the LM slots
+ * replayed from HIP graphs); ranks sharing a device are ordered from the host (cross-stream
+ * events).  Same arguments and results as lba_solve (points, edge chi2 and erase flags merged from
+ * their owners).  Returns ORB_ENODEV when two listed devices cannot access each other, ORB_EGPU
+ * when a device-side wait timed out (a rank that never arrived). */
 typedef struct lba_group lba_group;
 int lba_group_create(const int* devices, int n, lba_group** out);
 void lba_group_destroy(lba_group* g);
 int lba_group_solve(lba_group* g, const lba_problem* p, const lba_options* o, const volatile uint8_t* stop,
                     lba_result* r);
-/* Cumulative exchange time measured on rank 0's stream (from its partial being ready to every
- * rank having read it, per collective) and the number of collectives. */
+/* The number of collectives since creation and, for the host-ordered exchange only, their
+ * cumulative time on rank 0's stream (from its partial being ready to every rank having read it;
+ * 0 with the device-side exchange, whose cost is in a kernel trace as k_grp_sync / k_grp_reduce). */
 int lba_group_stats(lba_group* g, double* exchange_ms, long* n_exchanges);
 
 /* Converter::toSE3Quat(const cv::Mat& Tcw) / Converter::toCvMat(const SE3Quat&)
