@@ -1500,7 +1500,31 @@ __device__ void glibc_sincosf(float y, float& s, float& c) {
 //  4. steered BRIEF (R :113-155) with glibc sincosf, 4 ballots -> 32 bytes.
 constexpr int kOdPW = 48;                // patch row stride (bytes): columns x-24 .. x+23
 constexpr int kOdRows = 43;              // rows y-21 .. y+21
-constexpr int kOdRsW = 40;               // row-sum stride (u16): columns x-18 .. x+18 (37 used)
+constexpr int kOdRsW = 42;               // row-sum stride (u16): columns x-18 .. x+18 (37 used; 8-column tasks end at 41)
+// The horizontal pass's tasks: row r (<< 8) and the first of 8 output columns c0 (even), covering
+// per row the columns a rotated pattern sample can need: a sample (X, Y) = the rounded rotation of a
+// pattern point lies within R = max pattern radius (18.38) + 0.75 of the keypoint (rounding moves
+// each coordinate by <= 0.5), and RS row r feeds the samples with |Y - (r - 21)| <= 3, so row r needs
+// |X| <= sqrt(R^2 - max(0, |r - 21| - 3)^2).  189 tasks (3 per lane; the full 43 x 37 grid in 4-column
+// tasks was 430, 7 per lane); 0xffff pads.  Generated from orb_pattern.inc.
+__constant__ uint16_t c_htask[192] = {
+    0x000c, 0x0014, 0x010a, 0x0112, 0x011a, 0x0208, 0x0210, 0x0218, 0x0306, 0x030e, 0x0316, 0x0404,
+    0x040c, 0x0414, 0x041c, 0x0504, 0x050c, 0x0514, 0x051c, 0x0604, 0x060c, 0x0614, 0x061c, 0x0702,
+    0x070a, 0x0712, 0x071a, 0x0802, 0x080a, 0x0812, 0x081a, 0x0822, 0x0902, 0x090a, 0x0912, 0x091a,
+    0x0922, 0x0a00, 0x0a08, 0x0a10, 0x0a18, 0x0a20, 0x0b00, 0x0b08, 0x0b10, 0x0b18, 0x0b20, 0x0c00,
+    0x0c08, 0x0c10, 0x0c18, 0x0c20, 0x0d00, 0x0d08, 0x0d10, 0x0d18, 0x0d20, 0x0e00, 0x0e08, 0x0e10,
+    0x0e18, 0x0e20, 0x0f00, 0x0f08, 0x0f10, 0x0f18, 0x0f20, 0x1000, 0x1008, 0x1010, 0x1018, 0x1020,
+    0x1100, 0x1108, 0x1110, 0x1118, 0x1120, 0x1200, 0x1208, 0x1210, 0x1218, 0x1220, 0x1300, 0x1308,
+    0x1310, 0x1318, 0x1320, 0x1400, 0x1408, 0x1410, 0x1418, 0x1420, 0x1500, 0x1508, 0x1510, 0x1518,
+    0x1520, 0x1600, 0x1608, 0x1610, 0x1618, 0x1620, 0x1700, 0x1708, 0x1710, 0x1718, 0x1720, 0x1800,
+    0x1808, 0x1810, 0x1818, 0x1820, 0x1900, 0x1908, 0x1910, 0x1918, 0x1920, 0x1a00, 0x1a08, 0x1a10,
+    0x1a18, 0x1a20, 0x1b00, 0x1b08, 0x1b10, 0x1b18, 0x1b20, 0x1c00, 0x1c08, 0x1c10, 0x1c18, 0x1c20,
+    0x1d00, 0x1d08, 0x1d10, 0x1d18, 0x1d20, 0x1e00, 0x1e08, 0x1e10, 0x1e18, 0x1e20, 0x1f00, 0x1f08,
+    0x1f10, 0x1f18, 0x1f20, 0x2000, 0x2008, 0x2010, 0x2018, 0x2020, 0x2102, 0x210a, 0x2112, 0x211a,
+    0x2122, 0x2202, 0x220a, 0x2212, 0x221a, 0x2222, 0x2302, 0x230a, 0x2312, 0x231a, 0x2404, 0x240c,
+    0x2414, 0x241c, 0x2504, 0x250c, 0x2514, 0x251c, 0x2604, 0x260c, 0x2614, 0x261c, 0x2706, 0x270e,
+    0x2716, 0x2808, 0x2810, 0x2818, 0x290a, 0x2912, 0x291a, 0x2a0c, 0x2a14, 0xffff, 0xffff, 0xffff,
+};
 constexpr int kOdWaveBytes = kOdRows * kOdPW + kOdRows * kOdRsW * 2;
 
 __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __restrict__ pyr,
@@ -1594,24 +1618,40 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
     const float angle = fast_atan2_dev((float)m01, (float)m10);
 
     TSTAMP(t_od2);
-    // 3a. horizontal Gaussian pass: RS[r][c] = sum_q k_q * raw(y-21+r, x-18+c-3+q), c < 37.
-    //     Task (r, group gq) computes columns 4gq .. 4gq+3 from patch dwords gq .. gq+3.
-    for (int t = lane; t < kOdRows * 10; t += 64) {
-        const int r = t / 10, gq = t % 10;
-        const uint32_t* row = P32 + r * 12 + gq;
-        const uint32_t d0 = row[0], d1 = row[1], d2 = row[2], d3 = gq < 9 ? row[3] : 0u;
-        // output column 4gq+i reads patch bytes 4gq+i+3 .. 4gq+i+9
-        const uint32_t A0 = __builtin_amdgcn_alignbyte(d1, d0, 3), B0 = __builtin_amdgcn_alignbyte(d2, d1, 3);
-        const uint32_t A1 = d1, B1 = d2;
-        const uint32_t A2 = __builtin_amdgcn_alignbyte(d2, d1, 1), B2 = __builtin_amdgcn_alignbyte(d3, d2, 1);
-        const uint32_t A3 = __builtin_amdgcn_alignbyte(d2, d1, 2), B3 = __builtin_amdgcn_alignbyte(d3, d2, 2);
-        const uint32_t s0 = __builtin_amdgcn_udot4(B0, kB, __builtin_amdgcn_udot4(A0, kA, 0u, false), false);
-        const uint32_t s1 = __builtin_amdgcn_udot4(B1, kB, __builtin_amdgcn_udot4(A1, kA, 0u, false), false);
-        const uint32_t s2 = __builtin_amdgcn_udot4(B2, kB, __builtin_amdgcn_udot4(A2, kA, 0u, false), false);
-        const uint32_t s3 = __builtin_amdgcn_udot4(B3, kB, __builtin_amdgcn_udot4(A3, kA, 0u, false), false);
-        uint32_t* rs32 = reinterpret_cast<uint32_t*>(RS + r * kOdRsW + 4 * gq);
-        rs32[0] = s0 | (s1 << 16);
-        rs32[1] = s2 | (s3 << 16);
+    // 3a. horizontal Gaussian pass: RS[r][c] = sum_q k_q * raw(y-21+r, x-18+c-3+q) on the columns
+    //     the pattern can reach (c_htask).  Task (r, c0) computes columns c0 .. c0+7 from the 16
+    //     patch bytes c0+3 .. c0+18, re-based by four alignbytes at the task's byte offset; output i
+    //     takes bytes c0+3+i .. +6 (taps -3 .. 0, kA) and c0+7+i .. +10 (taps +1 .. +3, kB)
+    {
+        uint32_t task[3];
+#pragma unroll
+        for (int it = 0; it < 3; it++) task[it] = c_htask[lane + 64 * it];
+#pragma unroll
+        for (int it = 0; it < 3; it++) {
+            if (task[it] == 0xFFFFu) continue;
+            const int r = (int)(task[it] >> 8), c0 = (int)(task[it] & 0xFFu);
+            const int o = c0 + 3;
+            const uint32_t* row = P32 + r * 12 + (o >> 2);
+            const uint32_t sh = (uint32_t)(o & 3);
+            uint32_t d[5];
+#pragma unroll
+            for (int k = 0; k < 5; k++) d[k] = row[k];   // (past the row: bytes of unused columns)
+            uint32_t w[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+            uint32_t out[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const uint32_t A = (i & 3) == 0 ? w[i >> 2] : __builtin_amdgcn_alignbyte(w[(i >> 2) + 1], w[i >> 2], i & 3);
+                const int j = i + 4;
+                const uint32_t B = (j & 3) == 0 ? w[j >> 2] : __builtin_amdgcn_alignbyte(w[(j >> 2) + 1], w[j >> 2], j & 3);
+                const uint32_t sum = __builtin_amdgcn_udot4(B, kB, __builtin_amdgcn_udot4(A, kA, 0u, false), false);
+                out[i >> 1] |= sum << (16 * (i & 1));
+            }
+            uint32_t* rs32 = reinterpret_cast<uint32_t*>(RS + r * kOdRsW + c0);
+#pragma unroll
+            for (int k = 0; k < 4; k++) rs32[k] = out[k];
+        }
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
