@@ -664,52 +664,58 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 
-    // 2. SWAR pre-test: task (row y, column group gq) covers region columns 4gq .. 4gq+3
+    // 2. SWAR pre-test: task (row y, column group gq) covers region columns 8gq .. 8gq+7 (two dwords:
+    //    the loads, the scan and the index math shared by eight pixels)
     const uint32_t tpre = (uint32_t)max(g.tmin, 1);
     const uint32_t T1 = (tpre + 1u) * 0x00010001u;
     {
-        const int NG = (rw + 3) >> 2;
+        // the four compass tests of the four pixels in dword cC (its neighbours cL, cR; the rows
+        // three above / below pUp, pDn): bit k of the result = pixel k may be a corner
+        auto pretest4 = [&](uint32_t cL, uint32_t cC, uint32_t cR, uint32_t pUp, uint32_t pDn) -> uint32_t {
+            const uint32_t pRt = __builtin_amdgcn_alignbyte(cR, cC, 3);   // ring 4 (dx = +3)
+            const uint32_t pLt = __builtin_amdgcn_alignbyte(cC, cL, 1);   // ring 12 (dx = -3)
+            const uint32_t vE = __builtin_amdgcn_perm(0u, cC, 0x0c020c00u);
+            const uint32_t vO = __builtin_amdgcn_perm(0u, cC, 0x0c030c01u);
+            const uint32_t vEb = vE + 0x02000200u, vOb = vO + 0x02000200u;
+            const uint32_t vEt = vE + T1, vOt = vO + T1;
+            // dark: v > p + t <=> 512 + v - (p + t + 1) >= 512; bright: 512 + p - (v + t + 1) >= 512
+            auto flags = [&](uint32_t p, uint32_t& dk, uint32_t& br) {
+                const uint32_t pE = __builtin_amdgcn_perm(0u, p, 0x0c020c00u);
+                const uint32_t pO = __builtin_amdgcn_perm(0u, p, 0x0c030c01u);
+                dk = ((vEb - (pE + T1)) & 0x02000200u) | (((vOb - (pO + T1)) & 0x02000200u) << 1);
+                br = (((pE + 0x02000200u) - vEt) & 0x02000200u) | ((((pO + 0x02000200u) - vOt) & 0x02000200u) << 1);
+            };
+            uint32_t d0, b0, d4, b4, d8, b8, d12, b12;
+            flags(pDn, d0, b0);
+            flags(pRt, d4, b4);
+            flags(pUp, d8, b8);
+            flags(pLt, d12, b12);
+            const uint32_t pass = (d0 & d4) | (d4 & d8) | (d8 & d12) | (d12 & d0) | (b0 & b4) | (b4 & b8) |
+                                  (b8 & b12) | (b12 & b0);
+            return ((pass >> 9) & 3u) | ((pass >> 23) & 12u);   // bits 9, 10, 25, 26 = the dword's columns
+        };
+        const int NG = (rw + 7) >> 3;
         const int R = 64 / NG, gq = lane % NG, r0 = lane / NG;
         for (int yb = 0; yb < rh; yb += R) {
             const int y = yb + r0;
             uint32_t want = 0;
             if (r0 < R && y < rh) {
-                const int rowC = (y + 3) * W32 + gq + 1;   // dword holding region columns 4gq..4gq+3
-                const uint32_t cL = patch32[rowC - 1], cC = patch32[rowC], cR = patch32[rowC + 1];
-                const uint32_t pUp = patch32[rowC - 3 * W32], pDn = patch32[rowC + 3 * W32];
-                const uint32_t pRt = __builtin_amdgcn_alignbyte(cR, cC, 3);   // ring 4 (dx = +3)
-                const uint32_t pLt = __builtin_amdgcn_alignbyte(cC, cL, 1);   // ring 12 (dx = -3)
-                const uint32_t vE = __builtin_amdgcn_perm(0u, cC, 0x0c020c00u);
-                const uint32_t vO = __builtin_amdgcn_perm(0u, cC, 0x0c030c01u);
-                const uint32_t vEb = vE + 0x02000200u, vOb = vO + 0x02000200u;
-                const uint32_t vEt = vE + T1, vOt = vO + T1;
-                // dark: v > p + t <=> 512 + v - (p + t + 1) >= 512; bright: 512 + p - (v + t + 1) >= 512
-                auto flags = [&](uint32_t p, uint32_t& dk, uint32_t& br) {
-                    const uint32_t pE = __builtin_amdgcn_perm(0u, p, 0x0c020c00u);
-                    const uint32_t pO = __builtin_amdgcn_perm(0u, p, 0x0c030c01u);
-                    dk = ((vEb - (pE + T1)) & 0x02000200u) | (((vOb - (pO + T1)) & 0x02000200u) << 1);
-                    br = (((pE + 0x02000200u) - vEt) & 0x02000200u) | ((((pO + 0x02000200u) - vOt) & 0x02000200u) << 1);
-                };
-                uint32_t d0, b0, d4, b4, d8, b8, d12, b12;
-                flags(pDn, d0, b0);
-                flags(pRt, d4, b4);
-                flags(pUp, d8, b8);
-                flags(pLt, d12, b12);
-                const uint32_t pass = (d0 & d4) | (d4 & d8) | (d8 & d12) | (d12 & d0) | (b0 & b4) | (b4 & b8) |
-                                      (b8 & b12) | (b12 & b0);
-                // bits 9, 10, 25, 26 = columns 4gq .. 4gq+3
-                want = ((pass >> 9) & 3u) | ((pass >> 23) & 12u);
-                const int valid = rw - 4 * gq;   // columns of this group inside the region
-                if (valid < 4) want &= (1u << valid) - 1u;
+                const int rowC = (y + 3) * W32 + 2 * gq + 1;   // dwords holding region columns 8gq..8gq+7
+                const uint32_t cL = patch32[rowC - 1], c0 = patch32[rowC], c1 = patch32[rowC + 1], cR = patch32[rowC + 2];
+                const uint32_t u0 = patch32[rowC - 3 * W32], u1 = patch32[rowC - 3 * W32 + 1];
+                const uint32_t d0 = patch32[rowC + 3 * W32], d1 = patch32[rowC + 3 * W32 + 1];
+                want = pretest4(cL, c0, c1, u0, d0) | (pretest4(c0, c1, cR, u1, d1) << 4);
+                const int valid = rw - 8 * gq;   // columns of this group inside the region
+                if (valid < 8) want &= (1u << valid) - 1u;
             }
             const int cntW = __popc(want);
             const int incl = wave_incl_scan_dpp(cntW);
             const int pos = n + incl - cntW;
             // branch-free emission: entry kk at pos + (survivors below kk); the others go to the
             // lane's sink past the list
-            const uint16_t e0 = (uint16_t)(y * 64 + 4 * gq);
+            const uint16_t e0 = (uint16_t)(y * 64 + 8 * gq);
 #pragma unroll
-            for (int kk = 0; kk < 4; kk++) {
+            for (int kk = 0; kk < 8; kk++) {
                 const bool on = (want >> kk) & 1u;
                 const int at = pos + __popc(want & ((1u << kk) - 1u));
                 *(on ? list + at : lsink) = (uint16_t)(e0 + kk);
