@@ -619,10 +619,8 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
     const int listOff = patchBytes + (((maxH + 2) * SCS + 15) & ~15);
     unsigned char* base = dsm + (size_t)wid * waveBytes;
     uint32_t* patch32 = reinterpret_cast<uint32_t*>(base);
-    const uint8_t* patch = base;
     uint8_t* sc = base + patchBytes;
     uint16_t* list = reinterpret_cast<uint16_t*>(base + listOff);
-    uint16_t* const lsink = list + (((maxW * maxH * 2 + 15) & ~15) >> 1) + lane;
     uint8_t* kp = base;   // the window is dead once every survivor is scored (phase 3)
     const uint8_t* img = pyr + (size_t)b * g.frameBytes + L.off;
     const int rx0 = iniX + 3, ry0 = iniY + 3;
@@ -664,35 +662,58 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 
-    // 2. SWAR pre-test: task (row y, column group gq) covers region columns 8gq .. 8gq+7 (two dwords:
-    //    the loads, the scan and the index math shared by eight pixels)
+    // 2. pre-test, byte-SWAR over four pixels per dword: any 9-arc holds four cyclically
+    //    consecutive even ring pixels (0, 2, .., 14), so they must all be dark (p < v - t) or all
+    //    bright (p > v + t) at the strict threshold tmin — a necessary condition for both passes.
+    //    Per byte, x < y is the top bit of  (~x & y) | (~(x ^ y) & ~((x | 0x80) - (y & 0x7f)))
+    //    (the subtraction cannot borrow across bytes; one v_bitop3 after it), with the saturated
+    //    A = max(v - t, 0) and B = min(v + t, 255) of the centre bytes: dark = p < A, bright = B < p.
+    //    Task (row y, column group gq) covers region columns 8gq .. 8gq+7 (two dwords: the loads,
+    //    the scan and the index math shared by eight pixels); survivors (~8 % of the pixels) are
+    //    appended in raster order by a loop over the task's set bits.
     const uint32_t tpre = (uint32_t)max(g.tmin, 1);
-    const uint32_t T1 = (tpre + 1u) * 0x00010001u;
     {
-        // the four compass tests of the four pixels in dword cC (its neighbours cL, cR; the rows
-        // three above / below pUp, pDn): bit k of the result = pixel k may be a corner
-        auto pretest4 = [&](uint32_t cL, uint32_t cC, uint32_t cR, uint32_t pUp, uint32_t pDn) -> uint32_t {
-            const uint32_t pRt = __builtin_amdgcn_alignbyte(cR, cC, 3);   // ring 4 (dx = +3)
-            const uint32_t pLt = __builtin_amdgcn_alignbyte(cC, cL, 1);   // ring 12 (dx = -3)
-            const uint32_t vE = __builtin_amdgcn_perm(0u, cC, 0x0c020c00u);
-            const uint32_t vO = __builtin_amdgcn_perm(0u, cC, 0x0c030c01u);
-            const uint32_t vEb = vE + 0x02000200u, vOb = vO + 0x02000200u;
-            const uint32_t vEt = vE + T1, vOt = vO + T1;
-            // dark: v > p + t <=> 512 + v - (p + t + 1) >= 512; bright: 512 + p - (v + t + 1) >= 512
-            auto flags = [&](uint32_t p, uint32_t& dk, uint32_t& br) {
-                const uint32_t pE = __builtin_amdgcn_perm(0u, p, 0x0c020c00u);
-                const uint32_t pO = __builtin_amdgcn_perm(0u, p, 0x0c030c01u);
-                dk = ((vEb - (pE + T1)) & 0x02000200u) | (((vOb - (pO + T1)) & 0x02000200u) << 1);
-                br = (((pE + 0x02000200u) - vEt) & 0x02000200u) | ((((pO + 0x02000200u) - vOt) & 0x02000200u) << 1);
+        typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+        const u16x2 tt = {(unsigned short)tpre, (unsigned short)tpre};
+        const u16x2 m255 = {255, 255};
+        constexpr uint32_t H = 0x80808080u, L7 = 0x7f7f7f7fu;
+        auto pk = [](uint32_t u) { return __builtin_bit_cast(u16x2, u); };
+        auto upk = [](u16x2 u) { return __builtin_bit_cast(uint32_t, u); };
+        // bit k of the result = pixel k of dword cC may be a corner.  Ring pixels by (dy, dx):
+        // 0 (+3, 0), 2 (+2, +2), 4 (0, +3), 6 (-2, +2), 8 (-3, 0), 10 (-2, -2), 12 (0, -3), 14 (+2, -2);
+        // rows above / below as u3 / d3 (the dword itself) and u2L.. / d2L.. (with neighbours).
+        auto even_ring4 = [&](uint32_t cL, uint32_t cC, uint32_t cR, uint32_t u3, uint32_t d3, uint32_t u2L,
+                              uint32_t u2C, uint32_t u2R, uint32_t d2L, uint32_t d2C, uint32_t d2R) -> uint32_t {
+            const uint32_t vE = cC & 0x00ff00ffu, vO = (cC >> 8) & 0x00ff00ffu;
+            const uint32_t A = upk(__builtin_elementwise_sub_sat(pk(vE), tt)) |
+                               (upk(__builtin_elementwise_sub_sat(pk(vO), tt)) << 8);
+            const uint32_t B = upk(__builtin_elementwise_min(pk(vE) + tt, m255)) |
+                               (upk(__builtin_elementwise_min(pk(vO) + tt, m255)) << 8);
+            const uint32_t HmA = H - (A & L7), Bh = B | H;
+            uint32_t dk[8], br[8];
+            // (x | 0x80) - (y & 0x7f) per byte: p < A from (p & 0x7f) + (0x80 - (A & 0x7f)), B < p from
+            // (B | 0x80) - (p & 0x7f); the select is one v_bitop3, truth table
+            // (~x & y) | (~(x ^ y) & ~s) over (x, y, s) = (0xf0, 0xcc, 0xaa) -> 0x4d
+            auto flags = [&](uint32_t p, int u) {
+                const uint32_t pl = p & L7;
+                dk[u] = __builtin_amdgcn_bitop3_b32(p, A, pl + HmA, 0x4d);   // p < A
+                br[u] = __builtin_amdgcn_bitop3_b32(B, p, Bh - pl, 0x4d);    // B < p
             };
-            uint32_t d0, b0, d4, b4, d8, b8, d12, b12;
-            flags(pDn, d0, b0);
-            flags(pRt, d4, b4);
-            flags(pUp, d8, b8);
-            flags(pLt, d12, b12);
-            const uint32_t pass = (d0 & d4) | (d4 & d8) | (d8 & d12) | (d12 & d0) | (b0 & b4) | (b4 & b8) |
-                                  (b8 & b12) | (b12 & b0);
-            return ((pass >> 9) & 3u) | ((pass >> 23) & 12u);   // bits 9, 10, 25, 26 = the dword's columns
+            flags(d3, 0);
+            flags(__builtin_amdgcn_alignbyte(d2R, d2C, 2), 1);
+            flags(__builtin_amdgcn_alignbyte(cR, cC, 3), 2);
+            flags(__builtin_amdgcn_alignbyte(u2R, u2C, 2), 3);
+            flags(u3, 4);
+            flags(__builtin_amdgcn_alignbyte(u2C, u2L, 2), 5);
+            flags(__builtin_amdgcn_alignbyte(cC, cL, 1), 6);
+            flags(__builtin_amdgcn_alignbyte(d2C, d2L, 2), 7);
+            uint32_t pd[8], pb[8], run = 0;
+#pragma unroll
+            for (int u = 0; u < 8; u++) { pd[u] = dk[u] & dk[(u + 1) & 7]; pb[u] = br[u] & br[(u + 1) & 7]; }
+#pragma unroll
+            for (int u = 0; u < 8; u++) run |= (pd[u] & pd[(u + 2) & 7]) | (pb[u] & pb[(u + 2) & 7]);
+            // top bits 7, 15, 23, 31 -> bits 21..24 (no two partial products collide)
+            return ((((run & H) >> 7) * 0x00204081u) >> 21) & 15u;
         };
         const int NG = (rw + 7) >> 3;
         const int R = 64 / NG, gq = lane % NG, r0 = lane / NG;
@@ -702,60 +723,23 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
             if (r0 < R && y < rh) {
                 const int rowC = (y + 3) * W32 + 2 * gq + 1;   // dwords holding region columns 8gq..8gq+7
                 const uint32_t cL = patch32[rowC - 1], c0 = patch32[rowC], c1 = patch32[rowC + 1], cR = patch32[rowC + 2];
-                const uint32_t u0 = patch32[rowC - 3 * W32], u1 = patch32[rowC - 3 * W32 + 1];
-                const uint32_t d0 = patch32[rowC + 3 * W32], d1 = patch32[rowC + 3 * W32 + 1];
-                want = pretest4(cL, c0, c1, u0, d0) | (pretest4(c0, c1, cR, u1, d1) << 4);
+                const int ru = rowC - 2 * W32, rd = rowC + 2 * W32;
+                const uint32_t uL = patch32[ru - 1], uA = patch32[ru], uB = patch32[ru + 1], uR = patch32[ru + 2];
+                const uint32_t dL = patch32[rd - 1], dA = patch32[rd], dB = patch32[rd + 1], dR = patch32[rd + 2];
+                const uint32_t u30 = patch32[rowC - 3 * W32], u31 = patch32[rowC - 3 * W32 + 1];
+                const uint32_t d30 = patch32[rowC + 3 * W32], d31 = patch32[rowC + 3 * W32 + 1];
+                want = even_ring4(cL, c0, c1, u30, d30, uL, uA, uB, dL, dA, dB) |
+                       (even_ring4(c0, c1, cR, u31, d31, uA, uB, uR, dA, dB, dR) << 4);
                 const int valid = rw - 8 * gq;   // columns of this group inside the region
                 if (valid < 8) want &= (1u << valid) - 1u;
             }
             const int cntW = __popc(want);
             const int incl = wave_incl_scan_dpp(cntW);
-            const int pos = n + incl - cntW;
-            // branch-free emission: entry kk at pos + (survivors below kk); the others go to the
-            // lane's sink past the list
+            int at = n + incl - cntW;
             const uint16_t e0 = (uint16_t)(y * 64 + 8 * gq);
-#pragma unroll
-            for (int kk = 0; kk < 8; kk++) {
-                const bool on = (want >> kk) & 1u;
-                const int at = pos + __popc(want & ((1u << kk) - 1u));
-                *(on ? list + at : lsink) = (uint16_t)(e0 + kk);
-            }
+            for (uint32_t m = want; m != 0u; m &= m - 1u) list[at++] = (uint16_t)(e0 + __builtin_ctz(m));
             n += __shfl(incl, 63, 64);
         }
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-
-    // 2b. second necessary test on the survivors: any 9-arc holds four cyclically consecutive
-    //     even ring pixels (0, 2, .., 14), so they must all be dark or all bright at the same
-    //     strict threshold; the list is compacted in place (order kept: a chunk's entries are all
-    //     read before any is written, and every write lands at or below its source index).
-    {
-        const int tv = (int)tpre;
-        int n2 = 0;
-        for (int k0 = 0; k0 < n; k0 += 64) {
-            const int k = k0 + lane;
-            const int p = k < n ? (int)list[k] : 0;
-            const int y = p >> 6, x = p & 63;
-            const int cc = (y + 3) * PWS + x + 4;
-            const int v = patch[cc];
-            const int e[8] = {patch[cc + 3 * PWS], patch[cc + 2 * PWS + 2], patch[cc + 3], patch[cc - 2 * PWS + 2],
-                              patch[cc - 3 * PWS], patch[cc - 2 * PWS - 2], patch[cc - 3], patch[cc + 2 * PWS - 2]};
-            uint32_t dk = 0, br = 0;
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                dk |= (uint32_t)(v - e[u] > tv) << u;
-                br |= (uint32_t)(e[u] - v > tv) << u;
-            }
-            dk |= dk << 8;
-            br |= br << 8;
-            const uint32_t run = (dk & (dk >> 1) & (dk >> 2) & (dk >> 3)) | (br & (br >> 1) & (br >> 2) & (br >> 3));
-            const bool pass = k < n && (run & 0xffu) != 0;
-            const uint64_t m = __ballot(pass);
-            if (pass) list[n2 + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)p;
-            n2 += __popcll(m);
-        }
-        n = n2;
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
