@@ -37,7 +37,8 @@ constexpr int kMinBorder = kEdge - 3;
 constexpr int kPatch = 31;
 constexpr int kHalfPatch = 15;
 
-__constant__ int8_t c_pattern[256 * 4] = {
+// bit_pattern_31_ as floats (exact small integers), one 16-byte load per point pair in the descriptor loop
+__constant__ __attribute__((aligned(16))) float c_patternf[256 * 4] = {
 #include "orb_pattern.inc"
 };
 
@@ -45,6 +46,7 @@ struct LevelGeom {
     int w, h, pitch;
     long long off;        // byte offset of this level in a frame's pyramid slab
     int nCols, nRows, wCell, hCell;
+    uint32_t nColsMag;    // floor(2^32 / nCols) + 1 (nCols > 1): cell row = umulhi(cell, nColsMag)
     int maxBX, maxBY;     // maxBorderX / maxBorderY (minBorder = 16)
     int cellBase;         // first cell of this level in the frame's cell array
     int slotBase;         // first FAST key slot of this level in the frame's slot array
@@ -150,6 +152,7 @@ static int build_geom(const orb_extractor_params& p, int w, int h, Geom* g) {
         L.nCols = (int)(width / 30.f);
         L.nRows = (int)(height / 30.f);
         if (L.nCols < 1 || L.nRows < 1) return ORB_EINVAL;
+        L.nColsMag = L.nCols > 1 ? (uint32_t)((1ull << 32) / (unsigned)L.nCols + 1u) : 0u;
         L.wCell = (int)std::ceil(width / (float)L.nCols);
         L.hCell = (int)std::ceil(height / (float)L.nRows);
         L.cellBase = cells;
@@ -190,6 +193,16 @@ static int build_geom(const orb_extractor_params& p, int w, int h, Geom* g) {
 }
 
 // ------------------------------------------------------------------ device helpers
+
+// n / d for n <= 64 and 1 <= d <= 64 without a division: (n * ceil(2^16 / d)) >> 16 (exact, as
+// n * (ceil(2^16 / d) * d - 2^16) < 2^16); the table is read with a uniform index (scalar load)
+struct Rcp16Tab {
+    uint32_t v[65];
+    constexpr Rcp16Tab() : v() {
+        for (int d = 1; d <= 64; d++) v[d] = (65536u + (uint32_t)d - 1u) / (uint32_t)d;
+    }
+};
+__constant__ Rcp16Tab c_rcp16 = Rcp16Tab();
 
 __device__ __forceinline__ int level_of_tile(const Geom& g, int tile) {
     int l = 0;
@@ -592,7 +605,8 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
     const int l = level_of_cell(g, act ? c : g.cellsPerFrame - 1);
     const LevelGeom& L = g.lv[l];
     const int ci = c - L.cellBase;
-    const int i = ci / L.nCols, j = ci % L.nCols;
+    // ci / nCols by a multiply-high on the scalar unit (exact: ci * (nColsMag * nCols - 2^32) < 2^32)
+    const int i = L.nCols > 1 ? (int)__umulhi((uint32_t)ci, L.nColsMag) : ci, j = ci - i * L.nCols;
     int* cnt_out = cellCount + (size_t)b * g.cellsPerFrame + c;
     const int iniY = kMinBorder + i * L.hCell;
     int maxY = iniY + L.hCell + 6;
@@ -634,7 +648,8 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
         const int gx0 = rx0 - 4, sh = gx0 & 3, ga = gx0 - sh;
         const int NW = (rw + 8 + 3) >> 2;           // dwords per patch row
         const int NW1 = NW + 1;                     // aligned source dwords per row
-        const int R = 64 / NW1, k = lane % NW1, r0 = lane / NW1;
+        const uint32_t mW = c_rcp16.v[NW1];
+        const int r0 = (int)(((uint32_t)lane * mW) >> 16), k = lane - r0 * NW1, R = (int)((64u * mW) >> 16);
         const int rows = rh + 6;
         const int pitch = L.pitch;
         // buffer loads over the rest of the frame slab: a row past the window (or past the slab:
@@ -716,7 +731,8 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
             return ((((run & H) >> 7) * 0x00204081u) >> 21) & 15u;
         };
         const int NG = (rw + 7) >> 3;
-        const int R = 64 / NG, gq = lane % NG, r0 = lane / NG;
+        const uint32_t mG = c_rcp16.v[NG];
+        const int r0 = (int)(((uint32_t)lane * mG) >> 16), gq = lane - r0 * NG, R = (int)((64u * mG) >> 16);
         for (int yb = 0; yb < rh; yb += R) {
             const int y = yb + r0;
             uint32_t want = 0;
@@ -1664,9 +1680,8 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
 #pragma unroll
     for (int r = 0; r < 4; r++) {
         const int pi = r * 64 + lane;   // pair index: byte pi/8, bit pi%8
-        const float x0 = (float)c_pattern[4 * pi], y0 = (float)c_pattern[4 * pi + 1];
-        const float x1 = (float)c_pattern[4 * pi + 2], y1 = (float)c_pattern[4 * pi + 3];
-        words[r] = __ballot(sample(x0, y0) < sample(x1, y1));
+        const float4 pp = reinterpret_cast<const float4*>(c_patternf)[pi];
+        words[r] = __ballot(sample(pp.x, pp.y) < sample(pp.z, pp.w));
     }
 #ifdef ORB_TIMING
     if (lane == 0 && b == 0 && (q == 0 || q == 300 || q == 700))
