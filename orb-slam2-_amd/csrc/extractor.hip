@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <array>
 #include <mutex>
@@ -2051,6 +2052,9 @@ static int ensure_geom(orb_extractor* ex, int w, int h) {
                 }
             }
         }
+        // (ORB_PYR_LDS_KB: diagnostic override of the 52 KB budget)
+        const char* ev = std::getenv("ORB_PYR_LDS_KB");
+        const int budget = (ev && std::atoi(ev) >= 8 && std::atoi(ev) <= 160) ? std::atoi(ev) * 1024 : 52 * 1024;
         for (int K = 8; spanOk && K <= std::min(64, Hl) && bestK == 0; K++) {
             std::vector<PyrBand> bt((size_t)nl * K);
             for (int k = 0; k < K; k++) {
@@ -2085,7 +2089,7 @@ static int ensure_geom(orb_extractor* ex, int w, int h) {
                 for (int k = 0; k < K; k++) maxN = std::max(maxN, bt[(size_t)l * K + k].n);
                 tabBytes = std::max(tabBytes, 8 * (g.lv[l].w + maxN));
             }
-            if (ok && bufA + bufB + tabBytes <= 52 * 1024) {
+            if (ok && bufA + bufB + tabBytes <= budget) {
                 best = bt; bestK = K; bestA = bufA; bestB = bufB; bestT = tabBytes;
             }
         }
@@ -2221,10 +2225,21 @@ static int run_pipeline(orb_extractor* ex, int B, const uint8_t* src, long long 
     }
     mark(2);
     mark(3);
-    // LDS key buffers sized so that two workgroups still fit a CU (<= 80 KB each)
+    // LDS key buffers: small batches (latency) keep a level's keys in LDS when they fit, with the
+    // buffers sized so that two workgroups still fit a CU (<= 80 KB each); batches of 32 frames or
+    // more keep them in their HBM arrays (L2-resident) and the launch takes only the node tables'
+    // LDS — measured on the bench step (3 x 128 frames): 80 KB -> 248 k frames/s, node tables only
+    // -> 259 k, as the octree's low-VALU workgroups no longer hold LDS that the other streams'
+    // FAST / descriptor workgroups could use.  ORB_OT_LDS_KB overrides the budget (diagnostics).
     const size_t ldsBase = octree_lds_bytes(g);
+    static const int otEnvKb = [] {
+        const char* e = std::getenv("ORB_OT_LDS_KB");
+        const int kb = e ? std::atoi(e) : 0;
+        return kb >= 16 && kb <= 160 ? kb : 0;
+    }();
+    const long long otBudget = otEnvKb ? otEnvKb * 1024LL : B >= 32 ? 0LL : 80 * 1024LL;
     const int keyCap = (int)std::max<long long>(0, std::min<long long>(2LL * g.maxLevelSlots,
-                                                                          ((long long)81920 - (long long)ldsBase) / 4 - 8));
+                                                                          (otBudget - (long long)ldsBase) / 4 - 8));
     const size_t lds = ldsBase + 16 + 4 * (size_t)keyCap;
     hipLaunchKernelGGL(k_octree, dim3(g.nlevels, B), dim3(OT_T), lds, st, g, ex->d_slots, ex->d_cellCount,
                        ex->d_keyA, ex->d_keyB, ex->d_outKeys, ex->d_levelCount, ex->d_status, keyCap);
