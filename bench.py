@@ -97,8 +97,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=384, help="frames per step per GPU")
-    ap.add_argument("--streams", type=int, default=3,
+    ap.add_argument("--batch", type=int, default=512, help="frames per step per GPU")
+    ap.add_argument("--streams", type=int, default=4,
                     help="independent frame sequences per GPU, each on its own HIP stream (batch split)")
     ap.add_argument("--match-stream", action="store_true",
                     help="SearchForInitialization on a second stream per sequence, overlapping the next step's "
