@@ -458,18 +458,18 @@ __global__ __launch_bounds__(256) void k_pyramid(Geom g, const uint8_t* __restri
             const int dx0 = 4 * cg;
             // the group's source bytes x0[j], x1[j] lie in an 8-byte window starting at x0[0]
             // (host-checked span): per row three aligned dwords, two alignbytes re-base the window
-            // at x0[0] and two v_perm gather the four x0 and the four x1 bytes; the weights stay
-            // in registers and SDWA byte selects feed the 24-bit multiplies
-            uint32_t a0[4], a1[4], sel0 = 0, sel1 = 0;
+            // at x0[0], one v_perm per column places x0[j] and x1[j] in the two u16 halves, and one
+            // v_dot2_u32_u16 against (a0[j], a1[j]) gives the column's horizontal sum
+            // a0 x0 + a1 x1 (<= 255 * 2048, exact)
+            uint32_t sel[4], wt[4];
             const int xb = (int)(XT[min(dx0, D.w - 1)].x & 0xFFFF);
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const uint2 c = XT[min(dx0 + j, D.w - 1)];
-                sel0 |= (uint32_t)((int)(c.x & 0xFFFF) - xb) << (8 * j);
-                sel1 |= (uint32_t)((int)(c.x >> 16) - xb) << (8 * j);
-                a0[j] = c.y & 0xFFFF;
-                a1[j] = c.y >> 16;
+                sel[j] = (uint32_t)((int)(c.x & 0xFFFF) - xb) | 0x0c00u | ((uint32_t)((int)(c.x >> 16) - xb) << 16) | 0x0c000000u;
+                wt[j] = c.y;   // a0 | a1 << 16
             }
+            typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
             const int dw = xb >> 2;
             const uint32_t sh = (uint32_t)(xb & 3);
             const int valid = D.w - dx0;   // pitch padding stays 0
@@ -479,7 +479,7 @@ __global__ __launch_bounds__(256) void k_pyramid(Geom g, const uint8_t* __restri
                 uint2 cy[2];
 #pragma unroll
                 for (int u = 0; u < 2; u++) cy[u] = YT[rr[u]];
-                uint32_t g0[2][2], g1[2][2];   // [row pair u][source row 0/1]: x0 bytes, x1 bytes
+                uint32_t hs[2][2][4];   // [row pair u][source row 0/1][column]: horizontal sums
 #pragma unroll
                 for (int u = 0; u < 2; u++) {
 #pragma unroll
@@ -488,8 +488,10 @@ __global__ __launch_bounds__(256) void k_pyramid(Geom g, const uint8_t* __restri
                         const uint32_t* R = reinterpret_cast<const uint32_t*>(cur + __umul24(sy - (uint32_t)sb.s0, (uint32_t)sp)) + dw;
                         const uint32_t d0 = R[0], d1 = R[1], d2 = R[2];
                         const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh), w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-                        g0[u][h] = __builtin_amdgcn_perm(w1, w0, sel0);
-                        g1[u][h] = __builtin_amdgcn_perm(w1, w0, sel1);
+#pragma unroll
+                        for (int j = 0; j < 4; j++)
+                            hs[u][h][j] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(w1, w0, sel[j])),
+                                                                 __builtin_bit_cast(u16x2, wt[j]), 0u, false);
                     }
                 }
                 uint32_t packed[2] = {0u, 0u};
@@ -498,11 +500,9 @@ __global__ __launch_bounds__(256) void k_pyramid(Geom g, const uint8_t* __restri
                     const uint32_t b0 = cy[u].y & 0xFFFF, b1 = cy[u].y >> 16;
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
-                        // every product fits 24 x 24 -> 32 bits (bytes x 11-bit weights, 19-bit sums
-                        // x 11-bit weights): v_mad_u32_u24, not the quarter-rate v_mul_lo_u32
-                        const uint32_t v0 = __umul24((g0[u][0] >> (8 * j)) & 0xFFu, a0[j]) + __umul24((g1[u][0] >> (8 * j)) & 0xFFu, a1[j]);
-                        const uint32_t v1 = __umul24((g0[u][1] >> (8 * j)) & 0xFFu, a0[j]) + __umul24((g1[u][1] >> (8 * j)) & 0xFFu, a1[j]);
-                        const uint32_t v = min((__umul24(v0, b0) + __umul24(v1, b1) + (1u << 21)) >> 22, 255u);
+                        // 19-bit sums x 11-bit weights fit 24 x 24 -> 32 bits: v_mad_u32_u24, not
+                        // the quarter-rate v_mul_lo_u32
+                        const uint32_t v = min((__umul24(hs[u][0][j], b0) + __umul24(hs[u][1][j], b1) + (1u << 21)) >> 22, 255u);
                         packed[u] |= v << (8 * j);
                     }
                 }
