@@ -102,6 +102,12 @@ __device__ __forceinline__ int wave_incl_scan_i32(int v) {
     return v;
 }
 
+// Sum over a fully active wave: the DPP inclusive scan's total, read from lane 63 (no LDS
+// crossbar round trips, unlike the __shfl_xor butterfly below)
+__device__ __forceinline__ int wave_sum_dpp(int v) {
+    return __builtin_amdgcn_readlane(wave_incl_scan_dpp(v), 63);
+}
+
 __device__ __forceinline__ int wave_reduce_sum_i32(int v) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);

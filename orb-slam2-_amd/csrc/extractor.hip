@@ -1540,6 +1540,17 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
                                                      uint8_t* __restrict__ desc, int cap, int32_t* __restrict__ counts,
                                                      uint32_t kA, uint32_t kB) {
     __shared__ __attribute__((aligned(16))) unsigned char od_sm[4][kOdWaveBytes];
+    // IC_Angle's per-(row v, dword d) byte masks |4d + j - 16| <= umax[|v|] (step 2), built once
+    // per workgroup before any wave can leave
+    __shared__ uint32_t momMask[31 * 8];
+    if (threadIdx.x < 31 * 8) {
+        const int v = (int)(threadIdx.x >> 3) - 15, d = threadIdx.x & 7;
+        const int um = g.umax[abs(v)];
+        const int ja = max(0, 16 - um - 4 * d), jb = min(3, 16 + um - 4 * d);
+        momMask[threadIdx.x] =
+            ja > jb ? 0u : (0xFFFFFFFFu << (8 * min(ja, 3))) & (0xFFFFFFFFu >> (8 * (3 - max(jb, 0))));
+    }
+    __syncthreads();
     // the wave index is uniform: readfirstlane keeps it (and the level / cell / geometry derived
     // from it) in SGPRs, so g.lv[l] fields are scalar loads instead of per-lane flat loads
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -1608,10 +1619,8 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
         for (int it = 0; it < 4; it++) {
             const int v = it * 8 + vr - 15;
             if (v > 15) continue;
-            const int um = g.umax[abs(v)];
-            // bytes j with |4d + j - 16| <= um, i.e. j in [16 - um - 4d, 16 + um - 4d] ∩ [0, 3]
-            const int ja = max(0, 16 - um - 4 * d), jb = min(3, 16 + um - 4 * d);
-            const uint32_t m = ja > jb ? 0u : (0xFFFFFFFFu << (8 * min(ja, 3))) & (0xFFFFFFFFu >> (8 * (3 - max(jb, 0))));
+            // bytes j with |4d + j - 16| <= umax[|v|], i.e. j in [16 - um - 4d, 16 + um - 4d] ∩ [0, 3]
+            const uint32_t m = momMask[(v + 15) * 8 + d];
             const uint32_t w1 = m & 0x01010101u;
             const uint32_t wu = m & (0x03020100u + (uint32_t)(4 * d) * 0x01010101u);   // bytes u + 16 = 4d + j
             const uint32_t pw = P32[(21 + v) * 12 + 2 + d];
@@ -1620,8 +1629,8 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
             m01 += v * s1;
         }
     }
-    m10 = wave_reduce_sum_i32(m10);
-    m01 = wave_reduce_sum_i32(m01);
+    m10 = wave_sum_dpp(m10);
+    m01 = wave_sum_dpp(m01);
     const float angle = fast_atan2_dev((float)m01, (float)m10);
 
     TSTAMP(t_od2);
