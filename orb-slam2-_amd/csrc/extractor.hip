@@ -755,7 +755,7 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
             int at = n + incl - cntW;
             const uint16_t e0 = (uint16_t)(y * 64 + 8 * gq);
             for (uint32_t m = want; m != 0u; m &= m - 1u) list[at++] = (uint16_t)(e0 + __builtin_ctz(m));
-            n += __shfl(incl, 63, 64);
+            n += __builtin_amdgcn_readlane(incl, 63);   // the wave total (scalar)
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -880,7 +880,7 @@ __device__ int block_scan_lds(int* a, int m, int* wsum) {
     const int s0 = min(tid * chunk, m), s1 = min(s0 + chunk, m);
     int local = 0;
     for (int i = s0; i < s1; i++) local += a[i];
-    int incl = wave_incl_scan_i32(local);
+    int incl = wave_incl_scan_dpp(local);   // (every thread of the workgroup calls it)
     if (lane == 63) wsum[wid] = incl;
     __syncthreads();
     int wofs = 0, total = 0;

@@ -252,8 +252,8 @@ __device__ __forceinline__ void cand_query(const orb_keypoint& kp1, int i1, int 
         segS = CS[c0];
         segL = CS[c0 + (q.cy1 - q.cy0) + 1] - segS;
     }
-    const int incl = wave_incl_scan_i32(segL);
-    const int T = __shfl(incl, 63, 64);
+    const int incl = wave_incl_scan_dpp(segL);   // (the whole wave runs a query)
+    const int T = __builtin_amdgcn_readlane(incl, 63);
     if (lane < ncx) so[lane] = incl - segL;
     if (lane == 0) so[kGridCols] = T;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
