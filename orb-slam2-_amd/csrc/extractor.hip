@@ -347,6 +347,12 @@ __global__ __launch_bounds__(256) void k_resize(Geom g, int l, uint8_t* __restri
 // ranges of all bands cover every row of every level (checked on the host; otherwise the per-level
 // k_resize launches are used).  Level 0 is staged from the caller's frames (written into the
 // pitched slab on the way when they are not already there, replacing a separate copy kernel).
+// output rows per k_pyramid thread iteration (rows r, r + 4, ..: their source-row loads in flight together)
+#ifndef ORB_PYR_ROWS
+#define ORB_PYR_ROWS 2
+#endif
+constexpr int kPyrRows = ORB_PYR_ROWS;
+
 struct PyrBand {
     int s0, n;   // rows [s0, s0 + n) of a level computed by a band
 };
@@ -452,7 +458,8 @@ __global__ __launch_bounds__(256) void k_pyramid(Geom g, const uint8_t* __restri
             tabL[i] = i < D.w ? rztab[D.rzX + i] : rztab[D.rzY + db.s0 + (i - D.w)];
         __syncthreads();
         // thread = (column group cg, row phase rp): the group's column coefficients stay in
-        // registers while the thread walks rows rp, rp + 4, ... two at a time
+        // registers while the thread walks rows rp, rp + 4, ... kPyrRows at a time (2; 3 and 4 measured
+        // the same in a same-box A/B)
         for (int pr = tid; pr < 4 * G; pr += 256) {
             const int rp = pr / G, cg = pr - rp * G;
             const int dx0 = 4 * cg;
@@ -474,14 +481,17 @@ __global__ __launch_bounds__(256) void k_pyramid(Geom g, const uint8_t* __restri
             const uint32_t sh = (uint32_t)(xb & 3);
             const int valid = D.w - dx0;   // pitch padding stays 0
             const uint32_t keep = valid < 4 ? (1u << (8 * valid)) - 1u : 0xFFFFFFFFu;
-            for (int r = rp; r < db.n; r += 8) {
-                const int rr[2] = {r, min(r + 4, db.n - 1)};
-                uint2 cy[2];
+            for (int r = rp; r < db.n; r += 4 * kPyrRows) {
+                int rr[kPyrRows];
+                uint2 cy[kPyrRows];
 #pragma unroll
-                for (int u = 0; u < 2; u++) cy[u] = YT[rr[u]];
-                uint32_t hs[2][2][4];   // [row pair u][source row 0/1][column]: horizontal sums
+                for (int u = 0; u < kPyrRows; u++) {
+                    rr[u] = min(r + 4 * u, db.n - 1);
+                    cy[u] = YT[rr[u]];
+                }
+                uint32_t hs[kPyrRows][2][4];   // [row u][source row 0/1][column]: horizontal sums
 #pragma unroll
-                for (int u = 0; u < 2; u++) {
+                for (int u = 0; u < kPyrRows; u++) {
 #pragma unroll
                     for (int h = 0; h < 2; h++) {
                         const uint32_t sy = h ? (cy[u].x >> 16) : (cy[u].x & 0xFFFF);
@@ -494,22 +504,19 @@ __global__ __launch_bounds__(256) void k_pyramid(Geom g, const uint8_t* __restri
                                                                  __builtin_bit_cast(u16x2, wt[j]), 0u, false);
                     }
                 }
-                uint32_t packed[2] = {0u, 0u};
 #pragma unroll
-                for (int u = 0; u < 2; u++) {
+                for (int u = 0; u < kPyrRows; u++) {
                     const uint32_t b0 = cy[u].y & 0xFFFF, b1 = cy[u].y >> 16;
+                    uint32_t packed = 0u;
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
                         // 19-bit sums x 11-bit weights fit 24 x 24 -> 32 bits: v_mad_u32_u24, not
                         // the quarter-rate v_mul_lo_u32
                         const uint32_t v = min((__umul24(hs[u][0][j], b0) + __umul24(hs[u][1][j], b1) + (1u << 21)) >> 22, 255u);
-                        packed[u] |= v << (8 * j);
+                        packed |= v << (8 * j);
                     }
-                }
-#pragma unroll
-                for (int u = 0; u < 2; u++) {
-                    if (u == 1 && r + 4 >= db.n) break;
-                    const uint32_t pv = packed[u] & keep;
+                    if (u > 0 && r + 4 * u >= db.n) break;
+                    const uint32_t pv = packed & keep;
                     *reinterpret_cast<uint32_t*>(nxt + rr[u] * dp + dx0) = pv;
                     *reinterpret_cast<uint32_t*>(out + (size_t)(db.s0 + rr[u]) * D.pitch + dx0) = pv;
                 }
