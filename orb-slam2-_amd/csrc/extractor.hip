@@ -730,13 +730,15 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
             flags(__builtin_amdgcn_alignbyte(u2C, u2L, 2), 5);
             flags(__builtin_amdgcn_alignbyte(cC, cL, 1), 6);
             flags(__builtin_amdgcn_alignbyte(d2C, d2L, 2), 7);
-            uint32_t pd[8], pb[8], run = 0;
-#pragma unroll
-            for (int u = 0; u < 8; u++) { pd[u] = dk[u] & dk[(u + 1) & 7]; pb[u] = br[u] & br[(u + 1) & 7]; }
-#pragma unroll
-            for (int u = 0; u < 8; u++) run |= (pd[u] & pd[(u + 2) & 7]) | (pb[u] & pb[(u + 2) & 7]);
-            // top bits 7, 15, 23, 31 -> bits 21..24 (no two partial products collide)
-            return ((((run & H) >> 7) * 0x00204081u) >> 21) & 15u;
+            // a run of four at u is P_u & P_{u+2} with P_u = D_u & D_{u+1}; over the four even (odd)
+            // starts the OR of adjacent products on a 4-cycle factors as
+            // P0 P2 | P2 P4 | P4 P6 | P6 P0 = (P0 | P4) & (P2 | P6)   (ten operations per polarity)
+            auto runs = [](const uint32_t D[8]) {
+                const uint32_t ev = ((D[0] & D[1]) | (D[4] & D[5])) & ((D[2] & D[3]) | (D[6] & D[7]));
+                return (((D[1] & D[2]) | (D[5] & D[6])) & ((D[3] & D[4]) | (D[7] & D[0]))) | ev;
+            };
+            return (runs(dk) | runs(br)) & H;   // pixel k's flag in bit 8k + 7
+
         };
         const int NG = (rw + 7) >> 3;
         const uint32_t mG = c_rcp16.v[NG];
@@ -752,8 +754,11 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
                 const uint32_t dL = patch32[rd - 1], dA = patch32[rd], dB = patch32[rd + 1], dR = patch32[rd + 2];
                 const uint32_t u30 = patch32[rowC - 3 * W32], u31 = patch32[rowC - 3 * W32 + 1];
                 const uint32_t d30 = patch32[rowC + 3 * W32], d31 = patch32[rowC + 3 * W32 + 1];
-                want = even_ring4(cL, c0, c1, u30, d30, uL, uA, uB, dL, dA, dB) |
-                       (even_ring4(c0, c1, cR, u31, d31, uA, uB, uR, dA, dB, dR) << 4);
+                // flags of pixels 0-3 in bits 0, 8, 16, 24 and of pixels 4-7 in bits 4, 12, 20, 28;
+                // one multiply moves bit 8k (+4) to bit 21 + k (+4): no two partial products collide
+                const uint32_t f = (even_ring4(cL, c0, c1, u30, d30, uL, uA, uB, dL, dA, dB) >> 7) |
+                                   (even_ring4(c0, c1, cR, u31, d31, uA, uB, uR, dA, dB, dR) >> 3);
+                want = ((f * 0x00204081u) >> 21) & 0xFFu;
                 const int valid = rw - 8 * gq;   // columns of this group inside the region
                 if (valid < 8) want &= (1u << valid) - 1u;
             }
