@@ -1691,19 +1691,40 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
     const float a = ac, bb = bs;
     const int k0 = (int)(kA & 0xff), k1 = (int)((kA >> 8) & 0xff), k2 = (int)((kA >> 16) & 0xff),
               k3 = (int)(kA >> 24);   // taps 0..3 (3 = centre); taps 4..6 mirror 2..0
-    auto sample = [&](float px, float py) -> int {
-        const int X = __float2int_rn(px * a - py * bb), Y = __float2int_rn(px * bb + py * a);
-        const uint16_t* c0 = RS + (Y + 18) * kOdRsW + X + 18;
-        const uint32_t acc = (uint32_t)(k0 * (c0[0] + c0[6 * kOdRsW]) + k1 * (c0[kOdRsW] + c0[5 * kOdRsW]) +
-                                        k2 * (c0[2 * kOdRsW] + c0[4 * kOdRsW]) + k3 * c0[3 * kOdRsW]);
-        return (int)min((acc + (1u << 15)) >> 16, 255u);
+    // A sample's rotated offset: the products px a, py b (px b, py a) as one v_pk_mul_f32 each
+    // (the same IEEE products and sums as the scalar form), cvRound by the 1.5 * 2^23 magic add
+    // (round-half-even for |x| < 2^22), and the row-sum address from the magic-biased bit
+    // patterns directly: __umul24 reads Y + 2^22 from the low 24 bits and the biases fold into
+    // one constant (mod 2^32).  The vertical taps pair up (0, 6), (1, 5), (2, 4) for
+    // v_dot2_u32_u16; the integer sum is the same.
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    const f2 cs = {a, bb}, sc = {bb, a};
+    const uint32_t kk0 = (uint32_t)k0 * 0x10001u, kk1 = (uint32_t)k1 * 0x10001u, kk2 = (uint32_t)k2 * 0x10001u;
+    constexpr uint32_t kMagicBits = 0x4B400000u;   // bits of 1.5 * 2^23
+    constexpr uint32_t kRsOff = 2u * (18u * kOdRsW + 18u) - 2u * kOdRsW * (kMagicBits & 0xFFFFFFu) - 2u * kMagicBits;
+    auto sample = [&](f2 p) -> int {
+        const f2 u = p * cs, w = p * sc;
+        const float xf = u.x - u.y, yf = w.x + w.y;
+        const uint32_t xb = __float_as_uint(xf + 12582912.0f), yb = __float_as_uint(yf + 12582912.0f);
+        const uint32_t off = __umul24(yb, 2u * kOdRsW) + 2u * xb + kRsOff;   // 2 ((Y + 18) kOdRsW + X + 18)
+        const uint16_t* c0 = reinterpret_cast<const uint16_t*>(reinterpret_cast<const unsigned char*>(RS) + off);
+        const uint32_t p06 = (uint32_t)c0[0] | ((uint32_t)c0[6 * kOdRsW] << 16);
+        const uint32_t p15 = (uint32_t)c0[kOdRsW] | ((uint32_t)c0[5 * kOdRsW] << 16);
+        const uint32_t p24 = (uint32_t)c0[2 * kOdRsW] | ((uint32_t)c0[4 * kOdRsW] << 16);
+        uint32_t acc = __umul24((uint32_t)k3, (uint32_t)c0[3 * kOdRsW]) + (1u << 15);
+        acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, p06), __builtin_bit_cast(u16x2, kk0), acc, false);
+        acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, p15), __builtin_bit_cast(u16x2, kk1), acc, false);
+        acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, p24), __builtin_bit_cast(u16x2, kk2), acc, false);
+        return (int)min(acc >> 16, 255u);
     };
     uint64_t words[4];
 #pragma unroll
     for (int r = 0; r < 4; r++) {
         const int pi = r * 64 + lane;   // pair index: byte pi/8, bit pi%8
         const float4 pp = reinterpret_cast<const float4*>(c_patternf)[pi];
-        words[r] = __ballot(sample(pp.x, pp.y) < sample(pp.z, pp.w));
+        const f2 p0 = {pp.x, pp.y}, p1 = {pp.z, pp.w};
+        words[r] = __ballot(sample(p0) < sample(p1));
     }
 #ifdef ORB_TIMING
     if (lane == 0 && b == 0 && (q == 0 || q == 300 || q == 700))
