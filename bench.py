@@ -347,114 +347,125 @@ def bench_lba(args, amd, dev, local, rank, world):
         obj = [None]
         torch.distributed.broadcast_object_list(obj, src=0)
         return obj[0]
-    # warm-up: allocations, code objects and the LM-slot graphs of both group shapes (the
-    # first solves instantiate them); LocalMapping calls LocalBundleAdjustment once per keyframe,
-    # so the steady state is what it sees
-    call = ctx.prepared(pb)
-    grp_live = native   # the group's solves are the timed ones (False after a fallback)
+
+    def body():
+        nonlocal ctx, fallback
+        # warm-up: allocations, code objects and the LM-slot graphs of both group shapes (the
+        # first solves instantiate them); LocalMapping calls LocalBundleAdjustment once per keyframe,
+        # so the steady state is what it sees
+        call = ctx.prepared(pb)
+        grp_live = native   # the group's solves are the timed ones (False after a fallback)
+        try:
+            for _ in range(3):
+                call()
+        except RuntimeError as exc:
+            if not native:
+                raise
+            # the group failed on this node (e.g. a timed-out exchange): rank 0 times its own device
+            # alone and says so; the waiting ranks still get the broadcast below
+            fallback = f"lba_group_solve failed: {exc}; rank 0 alone"
+            grp_live = False
+            ctx = amd.LocalBA(local)
+            call = ctx.prepared(pb)
+            for _ in range(3):
+                call()
+        if world > 1 and not native:   # (native: the other ranks wait at the barrier below)
+            torch.distributed.barrier()
+        torch.cuda.synchronize(dev)
+        iters, times = 0, []
+        for _ in range(args.lba_solves):   # timed: the lba_solve C-ABI call (arguments marshalled once)
+            t0 = time.perf_counter()
+            its, _, _ = call()
+            times.append(time.perf_counter() - t0)
+            iters += sum(its)
+        tot = sum(times)
+        if grp_live:
+            ex_ms, n_ex = ctx.stats()
+            r = ctx.solve(pb)
+            st = None
+            erased = int(np.count_nonzero(r["edge_erase"]))
+        elif native:   # (fallback: rank 0's own solve, no stage split)
+            r = ctx.solve(pb)
+            st = None
+            erased = int(np.count_nonzero(r["edge_erase"]))
+        else:
+            # stage split from a separate profiled pass (per-slot HIP events; kernels enqueued one by
+            # one, so these solves are slower than the timed ones above)
+            ctx.profile(True)
+            for _ in range(args.lba_solves):
+                r = ctx.solve(pb)      # (decisions below: the same in every solve of this problem)
+            st = ctx.stats()
+            ctx.profile(False)
+            er = torch.tensor([float(np.count_nonzero(r["edge_erase"]))], dtype=torch.float64, device=dev)
+            if world > 1:      # each rank flags the edges of its own landmark shard
+                torch.distributed.all_reduce(er)
+            erased = int(er.item())
+            if world > 1:
+                t = torch.tensor([tot], dtype=torch.float64, device=dev)
+                torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+                tot = float(t.item())
+        out = {"config": f"{args.lba_kf} KF (+4 fixed) x {args.lba_points} points, {ne} mono edges, "
+                         f"landmarks sharded x{world}",
+               "ms_per_iter": round(1000 * tot / max(iters, 1), 4),
+               "solve_ms": round(1000 * tot / args.lba_solves, 3),
+               "iterations_per_solve": iters / args.lba_solves, "trials": r["trials"],
+               "n_gpus": world,
+               "native_group_unavailable": fallback,
+               "collective": ("none" if world == 1 else
+                              "library device-side exchange over xGMI (lba_group: flag words + peer reads, one process "
+                              "driving every device, slots in HIP graphs)" if grp_live else
+                              "none (the group failed; rank 0's device alone)" if native else
+                              "torch.distributed all_reduce callback (RCCL), one process per GPU"),
+               # LM decisions of the last timed solve: identical for every world size (landmark shards
+               # only reorder the f64 sums; tests/test_bench_ranks.py compares N=1 with N=2)
+               "decisions": {"iterations": [int(x) for x in r["iterations"]], "trials": int(r["trials"]),
+                             "chi2_trace": [float(x) for x in r["trace"][:, 1]],
+                             "erased_edges": erased}}
+        if st is not None:
+            out["stage_ms_per_solve"] = {k: round(st[k] / args.lba_solves, 4) for k in
+                                         ("linearize_ms", "schur_ms", "solve_ms", "update_ms")}
+        if grp_live:
+            # (host-ordered exchange: events around each collective; the device-side default has
+            # none — its cost is in the kernel trace as k_grp_sync / k_grp_reduce)
+            out["exchange_us_per_collective"] = round(1000 * ex_ms / max(n_ex, 1), 2) if ex_ms > 0 else None
+            out["collectives_per_trial"] = round(n_ex / max(1, (3 + args.lba_solves) * r["trials"]), 2)
+        if st is not None:   # (the native group's solves have no per-slot stage events)
+            out["roofline"] = lba_roofline(pb, out, world)
+        if world == 1 and not args.no_cpu:   # the CPU baseline is an N=1 figure
+            sys.path.insert(0, str(ROOT / "tests"))
+            import oracle_ref as O
+
+            def timed(threads, budget=3.0):
+                t0 = time.perf_counter()
+                n, it = 0, 0
+                while time.perf_counter() - t0 < budget or n < 2:
+                    rr = O.lba_solve(pb, threads=threads)
+                    it += sum(rr["iterations"])
+                    n += 1
+                dt = time.perf_counter() - t0
+                return dt, n, it
+            dt, n, it = timed(None)
+            out["cpu_baseline"] = {"ms_per_iter": round(1000 * dt / it, 4), "solve_ms": round(1000 * dt / n, 3),
+                                   "cores": 1, "kind": "port", "cpu_model": host_info()["cpu_model"],
+                                   "sample": f"{n} LocalBundleAdjustment solves, oracle C restatement of g2o "
+                                             f"LM+Schur (dense LDLT), 1 thread (reference builds g2o without OpenMP)"}
+            th = host_threads()
+            dt, n, it = timed(th)
+            out["cpu_baseline_openmp"] = {
+                "ms_per_iter": round(1000 * dt / it, 4), "solve_ms": round(1000 * dt / n, 3), "cores": th, "kind": "port",
+                "host": host_info(),
+                "sample": f"{n} solves, oracle_lba_solve_omp: g2o's G2O_OPENMP loops (computeActiveErrors, buildSystem "
+                          f"edges, Schur landmarks) on {th} threads, bitwise identical to the 1-thread oracle"}
+            out["speedup_vs_cpu"] = round(out["cpu_baseline"]["ms_per_iter"] / out["ms_per_iter"], 2)
+            out["speedup_vs_cpu_openmp"] = round(out["cpu_baseline_openmp"]["ms_per_iter"] / out["ms_per_iter"], 2)
+        return out
+
     try:
-        for _ in range(3):
-            call()
-    except RuntimeError as exc:
+        out = body()
+    except Exception as exc:   # rank 0 must still reach the ranks waiting at the barrier below
         if not native:
             raise
-        # the group failed on this node (e.g. a timed-out exchange): rank 0 times its own device
-        # alone and says so; the waiting ranks still get the broadcast below
-        fallback = f"lba_group_solve failed: {exc}; rank 0 alone"
-        grp_live = False
-        ctx = amd.LocalBA(local)
-        call = ctx.prepared(pb)
-        for _ in range(3):
-            call()
-    if world > 1 and not native:   # (native: the other ranks wait at the barrier below)
-        torch.distributed.barrier()
-    torch.cuda.synchronize(dev)
-    iters, times = 0, []
-    for _ in range(args.lba_solves):   # timed: the lba_solve C-ABI call (arguments marshalled once)
-        t0 = time.perf_counter()
-        its, _, _ = call()
-        times.append(time.perf_counter() - t0)
-        iters += sum(its)
-    tot = sum(times)
-    if grp_live:
-        ex_ms, n_ex = ctx.stats()
-        r = ctx.solve(pb)
-        st = None
-        erased = int(np.count_nonzero(r["edge_erase"]))
-    elif native:   # (fallback: rank 0's own solve, no stage split)
-        r = ctx.solve(pb)
-        st = None
-        erased = int(np.count_nonzero(r["edge_erase"]))
-    else:
-        # stage split from a separate profiled pass (per-slot HIP events; kernels enqueued one by
-        # one, so these solves are slower than the timed ones above)
-        ctx.profile(True)
-        for _ in range(args.lba_solves):
-            r = ctx.solve(pb)      # (decisions below: the same in every solve of this problem)
-        st = ctx.stats()
-        ctx.profile(False)
-        er = torch.tensor([float(np.count_nonzero(r["edge_erase"]))], dtype=torch.float64, device=dev)
-        if world > 1:      # each rank flags the edges of its own landmark shard
-            torch.distributed.all_reduce(er)
-        erased = int(er.item())
-        if world > 1:
-            t = torch.tensor([tot], dtype=torch.float64, device=dev)
-            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-            tot = float(t.item())
-    out = {"config": f"{args.lba_kf} KF (+4 fixed) x {args.lba_points} points, {ne} mono edges, "
-                     f"landmarks sharded x{world}",
-           "ms_per_iter": round(1000 * tot / max(iters, 1), 4),
-           "solve_ms": round(1000 * tot / args.lba_solves, 3),
-           "iterations_per_solve": iters / args.lba_solves, "trials": r["trials"],
-           "n_gpus": world,
-           "native_group_unavailable": fallback,
-           "collective": ("none" if world == 1 else
-                          "library device-side exchange over xGMI (lba_group: flag words + peer reads, one process "
-                          "driving every device, slots in HIP graphs)" if grp_live else
-                          "none (the group failed; rank 0's device alone)" if native else
-                          "torch.distributed all_reduce callback (RCCL), one process per GPU"),
-           # LM decisions of the last timed solve: identical for every world size (landmark shards
-           # only reorder the f64 sums; tests/test_bench_ranks.py compares N=1 with N=2)
-           "decisions": {"iterations": [int(x) for x in r["iterations"]], "trials": int(r["trials"]),
-                         "chi2_trace": [float(x) for x in r["trace"][:, 1]],
-                         "erased_edges": erased}}
-    if st is not None:
-        out["stage_ms_per_solve"] = {k: round(st[k] / args.lba_solves, 4) for k in
-                                     ("linearize_ms", "schur_ms", "solve_ms", "update_ms")}
-    if grp_live:
-        # (host-ordered exchange: events around each collective; the device-side default has
-        # none — its cost is in the kernel trace as k_grp_sync / k_grp_reduce)
-        out["exchange_us_per_collective"] = round(1000 * ex_ms / max(n_ex, 1), 2) if ex_ms > 0 else None
-        out["collectives_per_trial"] = round(n_ex / max(1, (3 + args.lba_solves) * r["trials"]), 2)
-    if st is not None:   # (the native group's solves have no per-slot stage events)
-        out["roofline"] = lba_roofline(pb, out, world)
-    if world == 1 and not args.no_cpu:   # the CPU baseline is an N=1 figure
-        sys.path.insert(0, str(ROOT / "tests"))
-        import oracle_ref as O
-
-        def timed(threads, budget=3.0):
-            t0 = time.perf_counter()
-            n, it = 0, 0
-            while time.perf_counter() - t0 < budget or n < 2:
-                rr = O.lba_solve(pb, threads=threads)
-                it += sum(rr["iterations"])
-                n += 1
-            dt = time.perf_counter() - t0
-            return dt, n, it
-        dt, n, it = timed(None)
-        out["cpu_baseline"] = {"ms_per_iter": round(1000 * dt / it, 4), "solve_ms": round(1000 * dt / n, 3),
-                               "cores": 1, "kind": "port", "cpu_model": host_info()["cpu_model"],
-                               "sample": f"{n} LocalBundleAdjustment solves, oracle C restatement of g2o "
-                                         f"LM+Schur (dense LDLT), 1 thread (reference builds g2o without OpenMP)"}
-        th = host_threads()
-        dt, n, it = timed(th)
-        out["cpu_baseline_openmp"] = {
-            "ms_per_iter": round(1000 * dt / it, 4), "solve_ms": round(1000 * dt / n, 3), "cores": th, "kind": "port",
-            "host": host_info(),
-            "sample": f"{n} solves, oracle_lba_solve_omp: g2o's G2O_OPENMP loops (computeActiveErrors, buildSystem "
-                      f"edges, Schur landmarks) on {th} threads, bitwise identical to the 1-thread oracle"}
-        out["speedup_vs_cpu"] = round(out["cpu_baseline"]["ms_per_iter"] / out["ms_per_iter"], 2)
-        out["speedup_vs_cpu_openmp"] = round(out["cpu_baseline_openmp"]["ms_per_iter"] / out["ms_per_iter"], 2)
+        out = {"error": f"{type(exc).__name__}: {exc}", "n_gpus": world}
     if native:   # rank 0 -> the waiting ranks
         torch.distributed.barrier()
         torch.distributed.broadcast_object_list([out], src=0)
@@ -476,16 +487,43 @@ def bench_lba_scaled(args, amd, dev, rank, world):
         torch.distributed.broadcast_object_list(obj, src=0)
         return obj[0]
     out = {}
+    try:
+        _lba_scaled_sizes(args, amd, dev, world, native, sizes, out)
+    except Exception as exc:   # rank 0 must still reach the ranks waiting at the barrier below
+        if not native:
+            raise
+        out["error"] = f"{type(exc).__name__}: {exc}"
+    out["note"] = ("corridor windows, banded covisibility; ms_per_iter = lba_solve wall / LM iterations"
+                   + (f"; landmarks sharded over {world} devices by one process (lba_group)" if native else ""))
+    if native:
+        torch.distributed.barrier()
+        torch.distributed.broadcast_object_list([out], src=0)
+    return out
+
+
+def _lba_scaled_sizes(args, amd, dev, world, native, sizes, out):
+    from orb_slam2_amd import synth
     for nl, npts in sizes:
         pb = synth.ba_problem_corridor(n_local=nl, n_fixed=4, n_points=npts)
+        group_error = None
         if native:
-            ndev = torch.cuda.device_count()
-            ctx = amd.LocalBAGroup([r % ndev for r in range(world)])
+            try:
+                ndev = torch.cuda.device_count()
+                ctx = amd.LocalBAGroup([r % ndev for r in range(world)])
+                call = ctx.prepared(pb)
+                for _ in range(2):
+                    call()
+            except RuntimeError as exc:   # the group cannot form or a sharded solve failed here:
+                group_error = str(exc)    # rank 0's device alone, and the line says so
+                ctx = amd.LocalBA(dev.index or 0)
+                call = ctx.prepared(pb)
+                for _ in range(2):
+                    call()
         else:
             ctx = amd.LocalBA(dev.index or 0)
-        call = ctx.prepared(pb)
-        for _ in range(2):
-            call()
+            call = ctx.prepared(pb)
+            for _ in range(2):
+                call()
         times, iters = [], 0
         for _ in range(5):
             t0 = time.perf_counter()
@@ -501,6 +539,8 @@ def bench_lba_scaled(args, amd, dev, rank, world):
                     "reduced_order": 6 * P, "ms_per_iter": round(1000 * sum(times) / max(iters, 1), 4),
                     "solve_ms": round(1000 * float(np.median(times)), 3), "iterations_per_solve": iters / 5,
                     "trials_per_solve": tr, "ldlt_mfma_flops_per_trial": tiles * 8192}
+        if group_error is not None:
+            out[key]["native_group_unavailable"] = group_error
         if not native:
             # the reduced solve's share from one profiled solve (per-slot events, kernels enqueued one
             # by one): its f64 MFMA rate against the 78.6 TFLOP/s peak.  The MFMA flops are the
@@ -530,12 +570,6 @@ def bench_lba_scaled(args, amd, dev, rank, world):
             out[key]["speedup_vs_cpu_openmp"] = round(out[key]["cpu_baseline_openmp"]["ms_per_iter"] /
                                                       out[key]["ms_per_iter"], 1)
         del ctx
-    out["note"] = ("corridor windows, banded covisibility; ms_per_iter = lba_solve wall / LM iterations"
-                   + (f"; landmarks sharded over {world} devices by one process (lba_group)" if native else ""))
-    if native:
-        torch.distributed.barrier()
-        torch.distributed.broadcast_object_list([out], src=0)
-    return out
 
 
 def _extract_leg(amd, dev, frames, nf, steps, warmup, pairs_fn=None):
