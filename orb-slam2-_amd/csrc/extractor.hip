@@ -688,9 +688,9 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
     // 2. pre-test, byte-SWAR over four pixels per dword: any 9-arc holds four cyclically
     //    consecutive even ring pixels (0, 2, .., 14), so they must all be dark (p < v - t) or all
     //    bright (p > v + t) at the strict threshold tmin — a necessary condition for both passes.
-    //    Per byte, x < y is the top bit of  (~x & y) | (~(x ^ y) & ~((x | 0x80) - (y & 0x7f)))
-    //    (the subtraction cannot borrow across bytes; one v_bitop3 after it), with the saturated
-    //    A = max(v - t, 0) and B = min(v + t, 255) of the centre bytes: dark = p < A, bright = B < p.
+    //    Per byte, x > y is the top bit of the carry-free byte average v_lerp_u8(x, ~y), with the
+    //    saturated A = max(v - t, 0) and B = min(v + t, 255) of the centre bytes: dark = A > p,
+    //    bright = p > B (three operations per ring dword).
     //    Task (row y, column group gq) covers region columns 8gq .. 8gq+7 (two dwords: the loads,
     //    the scan and the index math shared by eight pixels); survivors (~8 % of the pixels) are
     //    appended in raster order by a loop over the task's set bits.
@@ -699,7 +699,7 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
         typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
         const u16x2 tt = {(unsigned short)tpre, (unsigned short)tpre};
         const u16x2 m255 = {255, 255};
-        constexpr uint32_t H = 0x80808080u, L7 = 0x7f7f7f7fu;
+        constexpr uint32_t H = 0x80808080u;
         auto pk = [](uint32_t u) { return __builtin_bit_cast(u16x2, u); };
         auto upk = [](u16x2 u) { return __builtin_bit_cast(uint32_t, u); };
         // bit k of the result = pixel k of dword cC may be a corner.  Ring pixels by (dy, dx):
@@ -712,15 +712,13 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
                                (upk(__builtin_elementwise_sub_sat(pk(vO), tt)) << 8);
             const uint32_t B = upk(__builtin_elementwise_min(pk(vE) + tt, m255)) |
                                (upk(__builtin_elementwise_min(pk(vO) + tt, m255)) << 8);
-            const uint32_t HmA = H - (A & L7), Bh = B | H;
+            const uint32_t nB = ~B;
             uint32_t dk[8], br[8];
-            // (x | 0x80) - (y & 0x7f) per byte: p < A from (p & 0x7f) + (0x80 - (A & 0x7f)), B < p from
-            // (B | 0x80) - (p & 0x7f); the select is one v_bitop3, truth table
-            // (~x & y) | (~(x ^ y) & ~s) over (x, y, s) = (0xf0, 0xcc, 0xaa) -> 0x4d
+            // v_lerp_u8 averages bytes without carries between them: (x + ~y) >> 1 has its top bit
+            // set iff x + 255 - y >= 256, i.e. x > y
             auto flags = [&](uint32_t p, int u) {
-                const uint32_t pl = p & L7;
-                dk[u] = __builtin_amdgcn_bitop3_b32(p, A, pl + HmA, 0x4d);   // p < A
-                br[u] = __builtin_amdgcn_bitop3_b32(B, p, Bh - pl, 0x4d);    // B < p
+                dk[u] = __builtin_amdgcn_lerp(A, ~p, 0u);   // A > p: dark
+                br[u] = __builtin_amdgcn_lerp(p, nB, 0u);   // p > B: bright
             };
             flags(d3, 0);
             flags(__builtin_amdgcn_alignbyte(d2R, d2C, 2), 1);
