@@ -593,9 +593,14 @@ __host__ __device__ inline int fc_wave_bytes(int maxW, int maxH) {
 //     does not depend on t (a neighbour >= S is a corner at t whenever S is), so both passes
 //     (iniThFAST, then minThFAST if the cell is empty, :879-883) read the same maxima;
 //  5. keys emitted in raster order, as cv::FAST returns them.
+// MW > 0: the region width bound maxW is the compile-time MW (the host passes the same value), so
+// the window / score-map row strides are constants and every ring / neighbour load takes an
+// immediate offset from one address; MW = 0: strides at run time (any cell width).
+template <int MW>
 __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __restrict__ pyr,
                                                    uint32_t* __restrict__ slots, int* __restrict__ cellCount,
-                                                   int* __restrict__ status, int maxW, int maxH) {
+                                                   int* __restrict__ status, int maxWarg, int maxH) {
+    const int maxW = MW > 0 ? MW : maxWarg;
     TSTAMP(t_fc0);
     extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
     // the wave index is uniform: readfirstlane keeps it (and the level / cell / geometry derived
@@ -783,7 +788,7 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
     auto cell_of = [&](int k, int& kk, int& w) -> unsigned char* {
         w = (int)(k >= o1) + (int)(k >= o2) + (int)(k >= o3);
         kk = k - (w == 0 ? 0 : w == 1 ? o1 : w == 2 ? o2 : o3);
-        return dsm + (size_t)w * waveBytes;
+        return dsm + __umul24((uint32_t)w, (uint32_t)waveBytes);
     };
 
     // 3. full score of the survivors.  The list is in raster order: lanes are row-major over
@@ -2259,9 +2264,26 @@ static int run_pipeline(orb_extractor* ex, int B, const uint8_t* src, long long 
     {
         // FAST + NMS + cell retry fused per cell (stage 1); stage 2 (the former separate
         // cell pass) is empty
-        const size_t lds = 4 * (size_t)fc_wave_bytes(g.maxCellW, g.maxCellH);
-        hipLaunchKernelGGL(k_fast_cell, dim3((g.cellsPerFrame + 3) / 4, B), dim3(256), lds, st, g, ex->d_pyr,
-                           ex->d_slots, ex->d_cellCount, ex->d_status, g.maxCellW, g.maxCellH);
+        // the width bound rounded up to 4 (a layout with room for it); the common cell widths of
+        // ORB-SLAM2's 30-px grid get a compile-time instantiation
+        const int mw = (g.maxCellW + 3) & ~3;
+        const size_t lds = 4 * (size_t)fc_wave_bytes(mw, g.maxCellH);
+        const dim3 grid((g.cellsPerFrame + 3) / 4, B);
+        if (mw == 32)
+            hipLaunchKernelGGL(k_fast_cell<32>, grid, dim3(256), lds, st, g, ex->d_pyr, ex->d_slots, ex->d_cellCount,
+                               ex->d_status, mw, g.maxCellH);
+        else if (mw == 36)
+            hipLaunchKernelGGL(k_fast_cell<36>, grid, dim3(256), lds, st, g, ex->d_pyr, ex->d_slots, ex->d_cellCount,
+                               ex->d_status, mw, g.maxCellH);
+        else if (mw == 40)
+            hipLaunchKernelGGL(k_fast_cell<40>, grid, dim3(256), lds, st, g, ex->d_pyr, ex->d_slots, ex->d_cellCount,
+                               ex->d_status, mw, g.maxCellH);
+        else if (mw == 44)
+            hipLaunchKernelGGL(k_fast_cell<44>, grid, dim3(256), lds, st, g, ex->d_pyr, ex->d_slots, ex->d_cellCount,
+                               ex->d_status, mw, g.maxCellH);
+        else
+            hipLaunchKernelGGL(k_fast_cell<0>, grid, dim3(256), lds, st, g, ex->d_pyr, ex->d_slots, ex->d_cellCount,
+                               ex->d_status, mw, g.maxCellH);
     }
     mark(2);
     mark(3);
