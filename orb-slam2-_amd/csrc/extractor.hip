@@ -1594,6 +1594,15 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
     uint16_t* RS = reinterpret_cast<uint16_t*>(od_sm[wid] + kOdRows * kOdPW);
     TSTAMP(t_od0);
 
+    // the horizontal pass's task words and this lane's BRIEF point pairs: loaded first, so their
+    // latency hides under the window load and the moments (neither depends on the angle)
+    uint32_t task[3];
+#pragma unroll
+    for (int it = 0; it < 3; it++) task[it] = c_htask[lane + 64 * it];
+    float4 ppair[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) ppair[r] = reinterpret_cast<const float4*>(c_patternf)[r * 64 + lane];
+
     // 1. patch
     if (x - 24 >= 0 && x + 24 <= L.w && y - 21 >= 0 && y + 21 < L.h) {
         // lane = (row r0 of 4 per pass, aligned source dword k of 13): one buffer load per pass
@@ -1654,9 +1663,6 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
     //     patch bytes c0+3 .. c0+18, re-based by four alignbytes at the task's byte offset; output i
     //     takes bytes c0+3+i .. +6 (taps -3 .. 0, kA) and c0+7+i .. +10 (taps +1 .. +3, kB)
     {
-        uint32_t task[3];
-#pragma unroll
-        for (int it = 0; it < 3; it++) task[it] = c_htask[lane + 64 * it];
 #pragma unroll
         for (int it = 0; it < 3; it++) {
             if (task[it] == 0xFFFFu) continue;
@@ -1724,8 +1730,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
     uint64_t words[4];
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-        const int pi = r * 64 + lane;   // pair index: byte pi/8, bit pi%8
-        const float4 pp = reinterpret_cast<const float4*>(c_patternf)[pi];
+        const float4 pp = ppair[r];   // pair r * 64 + lane: byte pi/8, bit pi%8
         const f2 p0 = {pp.x, pp.y}, p1 = {pp.z, pp.w};
         words[r] = __ballot(sample(p0) < sample(p1));
     }
