@@ -195,15 +195,13 @@ static int build_geom(const orb_extractor_params& p, int w, int h, Geom* g) {
 
 // ------------------------------------------------------------------ device helpers
 
-// n / d for n <= 64 and 1 <= d <= 64 without a division: (n * ceil(2^16 / d)) >> 16 (exact, as
-// n * (ceil(2^16 / d) * d - 2^16) < 2^16); the table is read with a uniform index (scalar load)
-struct Rcp16Tab {
-    uint32_t v[65];
-    constexpr Rcp16Tab() : v() {
-        for (int d = 1; d <= 64; d++) v[d] = (65536u + (uint32_t)d - 1u) / (uint32_t)d;
-    }
-};
-__constant__ Rcp16Tab c_rcp16 = Rcp16Tab();
+// n / d for n <= 64 and 1 <= d <= 64 without a division: (n * m) >> 16 with m = floor(2^16 * rcp(d))
+// + 1, which lies in [2^16 / d, 2^16 / d + 2) (v_rcp_f32 is within 1 ulp, so 2^16 rcp(d) is within
+// 0.008 of 2^16 / d, itself an integer or at least 1/64 above one): e = m d - 2^16 < 2d and
+// n e < 2^13 < 2^16, so the quotient is exact.  No table load in the chain to the window loads.
+__device__ __forceinline__ uint32_t rcp16(int d) {
+    return (uint32_t)(65536.0f * __builtin_amdgcn_rcpf((float)d)) + 1u;
+}
 
 __device__ __forceinline__ int level_of_tile(const Geom& g, int tile) {
     int l = 0;
@@ -661,7 +659,7 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
         const int gx0 = rx0 - 4, sh = gx0 & 3, ga = gx0 - sh;
         const int NW = (rw + 8 + 3) >> 2;           // dwords per patch row
         const int NW1 = NW + 1;                     // aligned source dwords per row
-        const uint32_t mW = c_rcp16.v[NW1];
+        const uint32_t mW = rcp16(NW1);
         const int r0 = (int)(((uint32_t)lane * mW) >> 16), k = lane - r0 * NW1, R = (int)((64u * mW) >> 16);
         const int rows = rh + 6;
         const int pitch = L.pitch;
@@ -744,7 +742,7 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
 
         };
         const int NG = (rw + 7) >> 3;
-        const uint32_t mG = c_rcp16.v[NG];
+        const uint32_t mG = rcp16(NG);
         const int r0 = (int)(((uint32_t)lane * mG) >> 16), gq = lane - r0 * NG, R = (int)((64u * mG) >> 16);
         for (int yb = 0; yb < rh; yb += R) {
             const int y = yb + r0;
