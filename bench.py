@@ -572,9 +572,27 @@ def _lba_scaled_sizes(args, amd, dev, world, native, sizes, out):
         del ctx
 
 
-def _extract_leg(amd, dev, frames, nf, steps, warmup, pairs_fn=None):
+def batch_status(ex=None, m=None, what="leg"):
+    """The overflow bits of an extractor's / matcher's batched calls (orb_extractor_batch_status,
+    orb_matcher_batch_status; waits for their streams, reading the matcher's clears it).  A set
+    bit means some frame's keypoints or some pair's candidate list were truncated, i.e. the leg did
+    not compute the reference's result: fail loudly instead of reporting its rate."""
+    from orb_slam2_amd import _abi
+    lib = _abi.lib()
+    es, ms = C.c_int32(0), C.c_int32(0)
+    if ex is not None:
+        lib.orb_extractor_batch_status(ex._h, C.byref(es))
+    if m is not None:
+        lib.orb_matcher_batch_status(m._h, C.byref(ms))
+    if es.value or ms.value:
+        raise SystemExit(f"bench {what}: overflow status extractor={es.value} matcher={ms.value}")
+    return {"extractor": es.value, "matcher": ms.value}
+
+
+def _extract_leg(amd, dev, frames, nf, steps, warmup, pairs_fn=None, matcher=None):
     """Times batched extraction of an HBM-resident frame array (one step = all frames)
-    plus an optional per-step device function; returns (seconds per step, extractor, buffers)."""
+    plus an optional per-step device function; returns (seconds per step, buffers).  The
+    extractor's overflow bits are read after the timed steps (batch_status)."""
     from orb_slam2_amd import _abi
     B, H, W = frames.shape
     ex = amd.ORBextractor(nf, 1.2, 8, 20, 7, device=dev.index or 0, max_w=W, max_h=H, max_batch=B)
@@ -587,7 +605,7 @@ def _extract_leg(amd, dev, frames, nf, steps, warmup, pairs_fn=None):
     cnt = torch.zeros(B, dtype=torch.int32, device=dev)
     st = torch.cuda.current_stream(dev).cuda_stream
     lib = _abi.lib()
-    buf = dict(ex=ex, cap=cap, kps=kps, desc=desc, cnt=cnt, stream=st, lib=lib)
+    buf = dict(ex=ex, cap=cap, kps=kps, desc=desc, cnt=cnt, stream=st, lib=lib, matcher=matcher)
 
     def step():
         _abi.check("x", lib.orb_extract_batch_device(ex._h, C.c_void_p(imgs.data_ptr()), H * W, B, W, H,
@@ -603,7 +621,9 @@ def _extract_leg(amd, dev, frames, nf, steps, warmup, pairs_fn=None):
     for _ in range(steps):
         step()
     torch.cuda.synchronize(dev)
-    return (time.perf_counter() - t0) / steps, buf
+    dt = (time.perf_counter() - t0) / steps
+    buf["status"] = batch_status(ex, buf.get("matcher"), "extraction leg")
+    return dt, buf
 
 
 EUROC_MBF = 47.9   # R/Examples/Stereo/EuRoC.yaml Camera.bf (435.2 fx x 0.11 m)
@@ -640,8 +660,7 @@ def bench_config5(args, amd, dev, rank, world):
     (R/src/Frame.cpp:551-770) on the device pyramids.  Two timings:
       * throughput: `--stereo-batches` batches per step (strong scaling: the total is fixed);
       * latency: one 8-frame batch per step, sharded the same way (ms per batch, max over ranks)."""
-    from orb_slam2_amd import synth, _abi
-    lib = _abi.lib()
+    from orb_slam2_amd import synth
     W, H, NF, PB = 752, 480, 1200, 8
     shard = np.array_split(np.arange(PB), world)[rank]
     cv = synth.canvas(0x5EED0005, W, H)
@@ -651,36 +670,11 @@ def bench_config5(args, amd, dev, rank, world):
     for tag, nb in (("throughput", args.stereo_batches), ("latency_one_batch", 1)):
         pairs = [b * PB + int(j) for b in range(nb) for j in shard]
         P = len(pairs)
-        if P == 0:       # more ranks than pairs: this rank idles in the timed region
-            fr = None
-        else:
-            fr = np.stack([im for t in pairs for im in synth.stereo_pair(cv, W, H, t)])
-        ex = amd.ORBextractor(NF, 1.2, 8, 20, 7, device=dev.index or 0, max_w=W, max_h=H, max_batch=max(2 * P, 1))
-        cap = C.c_int()
-        _abi.check("geom", lib.orb_extractor_geometry(ex._h, W, H, None, None, None, C.byref(cap)))
-        cap = cap.value
-        st = torch.cuda.current_stream(dev).cuda_stream
-        if P:
-            imgs = torch.from_numpy(fr).to(dev)
-            kps = torch.zeros((2 * P, cap, 7), dtype=torch.int32, device=dev)
-            desc = torch.zeros((2 * P, cap, 32), dtype=torch.uint8, device=dev)
-            cnt = torch.zeros(2 * P, dtype=torch.int32, device=dev)
-            ur = torch.zeros((P, cap), dtype=torch.float32, device=dev)
-            dep = torch.zeros_like(ur)
-            ns = torch.zeros(P, dtype=torch.int32, device=dev)
-
-        def step():
-            if not P:
-                return
-            _abi.check("x", lib.orb_extract_batch_device(ex._h, C.c_void_p(imgs.data_ptr()), H * W, 2 * P, W, H,
-                                                          C.c_void_p(kps.data_ptr()), C.c_void_p(desc.data_ptr()),
-                                                          cap, C.c_void_p(cnt.data_ptr()), C.c_void_p(st)))
-            _abi.check("stereo", lib.orb_compute_stereo_matches_batch_device(
-                ex._h, C.c_void_p(kps.data_ptr()), C.c_void_p(desc.data_ptr()), C.c_void_p(cnt.data_ptr()), cap, P,
-                C.c_float(EUROC_MBF), C.c_float(0.0), C.c_void_p(ur.data_ptr()), C.c_void_p(dep.data_ptr()),
-                C.c_void_p(ns.data_ptr()), C.c_void_p(st)))
+        step, o = config5_shard(amd, dev, cv, pairs)
+        ur, dep, ns, cnt, cap, ex = o["ur"], o["dep"], o["ns"], o["cnt"], o["cap"], o["ex"]
         steps = max(args.steps, 5)
         dt = _timed_ranks(step, steps, 3, dev, world)
+        status = batch_status(ex, None, "config 5") if P else {"extractor": 0, "matcher": 0}
         tot = torch.tensor([float(ns.sum()) if P else 0.0, float(P)], dtype=torch.float64, device=dev)
         if world > 1:
             torch.distributed.all_reduce(tot)
@@ -703,11 +697,50 @@ def bench_config5(args, amd, dev, rank, world):
         out[tag] = {"stereo_frames_per_s": round(total_pairs * steps / dt, 1), "ms_per_step": round(dt / steps * 1e3, 4),
                     "batches_per_step": nb, "pairs_per_rank": P,
                     "stereo_matches_per_pair": round(float(tot[0]) / total_pairs, 1),
-                    "uright_depth_sha16": digest}
-        del ex
+                    "uright_depth_sha16": digest, "status": status}
+        del ex, o
     if world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline_stereo(cv, W, H, NF, EUROC_MBF, 8)
     return out
+
+
+def config5_shard(amd, dev, cv, pairs, W=752, H=480, NF=1200, mbf=EUROC_MBF):
+    """One rank's share of config 5: the stereo pairs `pairs` (indices into the synthetic EuRoC
+    stream of canvas `cv`) resident in HBM as frames (2j, 2j+1) = (left, right) of one batch.  The
+    returned step() runs orb_extract_batch_device over all 2P images (the two extractor roles of
+    R/src/Frame.cpp:86-89 in one launch) and orb_compute_stereo_matches_batch_device
+    (Frame::ComputeStereoMatches, R/src/Frame.cpp:551-770) on the device pyramids, on the current
+    stream.  Returns (step, buffers); tests/test_bench_pipeline.py runs it against the oracle."""
+    from orb_slam2_amd import synth, _abi
+    lib = _abi.lib()
+    P = len(pairs)
+    ex = amd.ORBextractor(NF, 1.2, 8, 20, 7, device=dev.index or 0, max_w=W, max_h=H, max_batch=max(2 * P, 1))
+    cap = C.c_int()
+    _abi.check("geom", lib.orb_extractor_geometry(ex._h, W, H, None, None, None, C.byref(cap)))
+    cap = cap.value
+    st = torch.cuda.current_stream(dev).cuda_stream
+    o = {"ex": ex, "cap": cap, "P": P, "ur": None, "dep": None, "ns": None, "cnt": None, "frames": None}
+    if P == 0:      # more ranks than pairs: this rank idles in the timed region
+        return (lambda: None), o
+    fr = np.stack([im for t in pairs for im in synth.stereo_pair(cv, W, H, t)])
+    imgs = torch.from_numpy(fr).to(dev)
+    kps = torch.zeros((2 * P, cap, 7), dtype=torch.int32, device=dev)
+    desc = torch.zeros((2 * P, cap, 32), dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(2 * P, dtype=torch.int32, device=dev)
+    ur = torch.zeros((P, cap), dtype=torch.float32, device=dev)
+    dep = torch.zeros_like(ur)
+    ns = torch.zeros(P, dtype=torch.int32, device=dev)
+    o.update(frames=fr, imgs=imgs, kps=kps, desc=desc, cnt=cnt, ur=ur, dep=dep, ns=ns)
+
+    def step():
+        _abi.check("x", lib.orb_extract_batch_device(ex._h, C.c_void_p(imgs.data_ptr()), H * W, 2 * P, W, H,
+                                                      C.c_void_p(kps.data_ptr()), C.c_void_p(desc.data_ptr()),
+                                                      cap, C.c_void_p(cnt.data_ptr()), C.c_void_p(st)))
+        _abi.check("stereo", lib.orb_compute_stereo_matches_batch_device(
+            ex._h, C.c_void_p(kps.data_ptr()), C.c_void_p(desc.data_ptr()), C.c_void_p(cnt.data_ptr()), cap, P,
+            C.c_float(mbf), C.c_float(0.0), C.c_void_p(ur.data_ptr()), C.c_void_p(dep.data_ptr()),
+            C.c_void_p(ns.data_ptr()), C.c_void_p(st)))
+    return step, o
 
 
 def cpu_baseline_stereo(cv, W, H, NF, mbf, n_pairs):
@@ -759,12 +792,41 @@ def bench_stereo_kitti(args, amd, dev, P=32):
     dt, b = _extract_leg(amd, dev, fr, NF, 10, 3, stereo)
     out = {"stereo_frames_per_s": round(P / dt, 1), "ms_per_step": round(dt * 1e3, 4), "pairs_per_step": P,
            "keypoints_per_image": float(b["cnt"].float().mean()),
-           "stereo_matches_per_pair": float(ns.float().mean()),
+           "stereo_matches_per_pair": float(ns.float().mean()), "status": b["status"],
            "config": f"synthetic KITTI 00 geometry {W}x{H} stereo (smooth integer disparity 5..60 px), {NF} feat, "
                      f"mbf {KITTI_MBF}, mb 0 (reference call order)"}
     if not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline_stereo(cv, W, H, NF, KITTI_MBF, 8)
     return out
+
+
+def kitti_sfi_leg(amd, dev, m, B=64, steps=10, warmup=3):
+    """BASELINE config 3 (KITTI 00 geometry 1241x376, 2000 feat, 8 levels): one step = B
+    HBM-resident synthetic frames through orb_extract_batch_device, then
+    orb_search_for_initialization_batch_device on the B-1 in-batch pairs (t-1, t) with window 100
+    (R/src/ORBmatcher.cpp:499-617, as R/src/Tracking.cpp:779-780 calls it).  Returns (seconds per
+    step, buffers incl. m12 / nm and both handles' status, the host frames);
+    tests/test_bench_pipeline.py runs this same leg against the oracle."""
+    from orb_slam2_amd import synth, _abi
+    lib = _abi.lib()
+    W, H = 1241, 376
+    cv = synth.canvas(0x5EED0003, W, H)
+    fr = np.stack([synth.frame(cv, W, H, t) for t in range(B)])
+    o = {}
+
+    def sfi(b):
+        cp = b["cap"]
+        if "m12" not in o:
+            o["m12"] = torch.zeros((B - 1, cp), dtype=torch.int32, device=dev)
+            o["nm"] = torch.zeros(B - 1, dtype=torch.int32, device=dev)
+        _abi.check("sfi", lib.orb_search_for_initialization_batch_device(
+            m._h, C.c_void_p(b["kps"].data_ptr()), C.c_void_p(b["desc"].data_ptr()), C.c_void_p(b["cnt"].data_ptr()),
+            C.c_void_p(b["kps"].data_ptr() + cp * 28), C.c_void_p(b["desc"].data_ptr() + cp * 32),
+            C.c_void_p(b["cnt"].data_ptr() + 4), B - 1, cp, W, H, 100, C.c_void_p(o["m12"].data_ptr()),
+            C.c_void_p(o["nm"].data_ptr()), C.c_void_p(b["stream"])))
+    dt, b = _extract_leg(amd, dev, fr, 2000, steps, warmup, sfi, matcher=m)
+    b.update(o)
+    return dt, b, fr
 
 
 def bench_extras(args, amd, dev):
@@ -816,23 +878,11 @@ def bench_extras(args, amd, dev):
     # ---- config 3 stereo: KITTI 00 geometry pairs, extraction of both images + ComputeStereoMatches
     out["stereo_kitti_1241x376"] = bench_stereo_kitti(args, amd, dev)
     # ---- config 3: KITTI geometry, 2000 features, extract + SearchForInitialization
-    W, H, B = 1241, 376, 64
-    cv = synth.canvas(0x5EED0003, W, H)
-    fr = np.stack([synth.frame(cv, W, H, t) for t in range(B)])
-    m12 = torch.zeros((B - 1, 8192), dtype=torch.int32, device=dev)
-    nm = torch.zeros(B - 1, dtype=torch.int32, device=dev)
-
-    def sfi(b):
-        cp = b["cap"]
-        _abi.check("sfi", lib.orb_search_for_initialization_batch_device(
-            m._h, C.c_void_p(b["kps"].data_ptr()), C.c_void_p(b["desc"].data_ptr()), C.c_void_p(b["cnt"].data_ptr()),
-            C.c_void_p(b["kps"].data_ptr() + cp * 28), C.c_void_p(b["desc"].data_ptr() + cp * 32),
-            C.c_void_p(b["cnt"].data_ptr() + 4), B - 1, cp, W, H, 100, C.c_void_p(m12.data_ptr()),
-            C.c_void_p(nm.data_ptr()), C.c_void_p(b["stream"])))
-    dt, b = _extract_leg(amd, dev, fr, 2000, 10, 3, sfi)
+    B = 64
+    dt, b, _ = kitti_sfi_leg(amd, dev, m, B, 10, 3)
     out["kitti_1241x376"] = {"frames_per_s": round(B / dt, 1), "ms_per_step": round(dt * 1e3, 4),
                              "keypoints_per_frame": float(b["cnt"].float().mean()),
-                             "matches_per_pair": float(nm.float().mean())}
+                             "matches_per_pair": float(b["nm"].float().mean()), "status": b["status"]}
     out["batch_sweep_640x480"] = batch_sweep(amd, dev, m)
     out["pose_optimization"] = bench_pose(args, amd, dev)
     out["single_call_latency"] = bench_single_calls(args, amd, dev)
@@ -1052,8 +1102,8 @@ def batch_sweep(amd, dev, m):
                 C.c_void_p(b["cnt"].data_ptr()), C.c_void_p(b["kps"].data_ptr() + cp * 28),
                 C.c_void_p(b["desc"].data_ptr() + cp * 32), C.c_void_p(b["cnt"].data_ptr() + 4), B - 1, cp, W, H,
                 100, C.c_void_p(m12.data_ptr()), C.c_void_p(nm.data_ptr()), C.c_void_p(b["stream"])))
-        dt, b = _extract_leg(amd, dev, fr, NF, 20 if B < 64 else 10, 3, sfi)
-        res[f"B{B}"] = {"frames_per_s": round(B / dt, 1), "ms_per_step": round(dt * 1e3, 4)}
+        dt, b = _extract_leg(amd, dev, fr, NF, 20 if B < 64 else 10, 3, sfi, matcher=m if B > 1 else None)
+        res[f"B{B}"] = {"frames_per_s": round(B / dt, 1), "ms_per_step": round(dt * 1e3, 4), "status": b["status"]}
     # PCIe-inclusive, B = 64: H2D of the frames, extraction + matching, D2H of the results
     B = 64
     fr = np.stack([synth.frame(cv, W, H, t) for t in range(B)])
@@ -1097,6 +1147,7 @@ def batch_sweep(amd, dev, m):
     torch.cuda.synchronize(dev)
     dt = (time.perf_counter() - t0) / reps
     res["B64_pcie_inclusive"] = {"frames_per_s": round(B / dt, 1), "ms_per_step": round(dt * 1e3, 4),
+                                 "status": batch_status(ex, m, "PCIe-inclusive leg"),
                                  "h2d_bytes": int(host_in.numel()),
                                  "d2h_bytes": int(kps.numel() * 4 + desc.numel() + m12.numel() * 4)}
     return res

@@ -98,3 +98,76 @@ def test_bench_pipeline_matches_oracle(amd, match_stream):
             prev_last[k] = idx[-1]
     steps = 3 if match_stream else 2
     assert checked_frames == steps * B and checked_pairs == steps * B - S
+
+
+def _check_frames(tag, frames, kps_t, desc_t, cnt_t, p, n_threads=16):
+    """Every frame's keypoints (all 7 fields) and descriptors bit-exact vs the oracle's
+    ORBextractor::operator(); returns the oracle outputs (want_pyramid for the stereo check)."""
+    from orb_slam2_amd import _abi
+    KP = _abi.KEYPOINT_DTYPE
+    with cf.ThreadPoolExecutor(min(n_threads, os.cpu_count() or 1)) as ex:
+        refs = list(ex.map(lambda im: O.extract(p, im, want_pyramid=True), frames))
+    cnt, kps, desc = cnt_t.cpu().numpy(), kps_t.cpu().numpy(), desc_t.cpu().numpy()
+    for i, ref in enumerate(refs):
+        n = int(cnt[i])
+        assert n == len(ref["kps"]), f"{tag} frame {i}: {n} vs {len(ref['kps'])} keypoints"
+        assert kps[i, :n].copy().view(KP).reshape(-1).tobytes() == ref["kps"].tobytes(), f"{tag} frame {i}: keypoints"
+        assert np.array_equal(desc[i, :n], ref["desc"]), f"{tag} frame {i}: descriptors"
+    return refs
+
+
+def test_bench_kitti_leg_matches_oracle(amd):
+    """BASELINE config 3 as bench.py's extras time it (kitti_sfi_leg: KITTI 00 geometry 1241x376,
+    2000 feat, B = 64 HBM-resident frames through orb_extract_batch_device, then
+    orb_search_for_initialization_batch_device over the 63 in-batch pairs): every frame and every
+    pair bit-exact vs the oracle (R/src/ORBextractor.cpp:1120-1188, R/src/ORBmatcher.cpp:499-617),
+    and both handles' overflow bits read 0 (the leg raises otherwise)."""
+    bench = _bench()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    m = amd.ORBmatcher(0.9, True, device=0)
+    W, H, B = 1241, 376, 64
+    _, b, frames = bench.kitti_sfi_leg(amd, dev, m, B, steps=2, warmup=1)
+    assert b["status"] == {"extractor": 0, "matcher": 0}
+    p = O.params(2000)
+    refs = _check_frames("kitti", frames, b["kps"], b["desc"], b["cnt"], p)
+    nm, m12 = b["nm"].cpu().numpy(), b["m12"].cpu().numpy()
+    for q in range(B - 1):
+        r1, r2 = refs[q], refs[q + 1]
+        fa, fb = O.FrameView(r1["kps"], r1["desc"], W, H), O.FrameView(r2["kps"], r2["desc"], W, H)
+        prev = np.stack([r1["kps"]["x"], r1["kps"]["y"]], 1).astype(np.float32).reshape(-1)
+        n_ref, m_ref, _ = O.search_for_initialization(fa, fb, prev, nnratio=0.9, window=100)
+        assert int(nm[q]) == n_ref, f"kitti pair {q}: nmatches"
+        assert np.array_equal(m12[q, :len(r1["kps"])], m_ref), f"kitti pair {q}: matches12"
+    assert float(nm.mean()) > 100
+
+
+@pytest.mark.parametrize("pairs", [list(range(8)), [13, 14, 15]])
+def test_bench_config5_batch_matches_oracle(amd, pairs):
+    """BASELINE config 5 as bench.py times it (config5_shard: EuRoC geometry 752x480, 1200 feat,
+    a full 8-pair stereo batch, and a 3-pair shard of the next batch as one rank of a sharded run
+    holds it): both images of every pair extracted in one orb_extract_batch_device call, then
+    orb_compute_stereo_matches_batch_device; every frame's keypoints / descriptors and every pair's
+    mvuRight / mvDepth / nstereo bit-exact vs the oracle (R/src/Frame.cpp:551-770), batch status 0."""
+    bench = _bench()
+    from orb_slam2_amd import synth
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    W, H, NF = 752, 480, 1200
+    cv = synth.canvas(0x5EED0005, W, H)
+    step, o = bench.config5_shard(amd, dev, cv, pairs)
+    step()
+    step()
+    torch.cuda.synchronize(dev)
+    assert bench.batch_status(o["ex"], None, "config 5 test") == {"extractor": 0, "matcher": 0}
+    p = O.params(NF)
+    refs = _check_frames("config5", o["frames"], o["kps"], o["desc"], o["cnt"], p)
+    ur, dep, ns = o["ur"].cpu().numpy(), o["dep"].cpu().numpy(), o["ns"].cpu().numpy()
+    for j in range(len(pairs)):
+        a, bb = refs[2 * j], refs[2 * j + 1]
+        n_ref, ur_ref, dep_ref = O.compute_stereo_matches(p, a, bb, bench.EUROC_MBF)
+        nl = len(a["kps"])
+        assert int(ns[j]) == n_ref, f"pair {pairs[j]}: nstereo"
+        assert np.array_equal(ur[j, :nl], ur_ref), f"pair {pairs[j]}: mvuRight"
+        assert np.array_equal(dep[j, :nl], dep_ref), f"pair {pairs[j]}: mvDepth"
+        assert n_ref > 300
