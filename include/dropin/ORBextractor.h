@@ -1,5 +1,6 @@
 // Drop-in replacement for R/include/ORBextractor.h (R = the reference's ORB-SLAM2 tree): the same
-// class surface (ctor, operator(), the inline getters, the public mvImagePyramid) implemented by
+// class surface (ctor, operator(), the inline getters, the public mvImagePyramid — filled on request,
+// see operator()) implemented by
 // liborbslam2_amd through include/orbslam2_amd_shim.hpp.  Compiles inside the reference tree only
 // (OpenCV); the shim it wraps is compiled and tested here with mock types (tests/test_cpp_shim.py).
 // R/src/ORBextractor.cpp drops out of the build.
@@ -32,12 +33,18 @@ public:
         mDev.extract(im, keypoints, d);
         if (d.empty()) descriptors.release();
         else d.copyTo(descriptors);
-        // mvImagePyramid (:88) as host views of the device pyramid (one download per call; the
-        // stereo matcher of include/dropin use the device copy and never read these)
+        // mvImagePyramid (:88): its only reader in the reference is Frame::ComputeStereoMatches
+        // (R/src/Frame.cpp:558, 675), which the drop-in runs on the device pyramids
+        // (include/dropin/Frame_ComputeStereoMatches.cc), so a call downloads nothing beyond the
+        // keypoints and descriptors.  A caller that reads the levels on the host opts in once with
+        // SetHostPyramid(true); each call then refreshes the host views (one download per call).
         mvImagePyramid.clear();
-        for (const auto& L : mDev.pyramid())
-            mvImagePyramid.push_back(cv::Mat(L.rows, L.cols, CV_8U, const_cast<uint8_t*>(L.data), L.step));
+        if (mbHostPyramid)
+            for (const auto& L : mDev.pyramid())
+                mvImagePyramid.push_back(cv::Mat(L.rows, L.cols, CV_8U, const_cast<uint8_t*>(L.data), L.step));
     }
+
+    void SetHostPyramid(bool on) { mbHostPyramid = on; }
 
     int inline GetLevels() { return mDev.GetLevels(); }
     float inline GetScaleFactor() { return mDev.GetScaleFactor(); }
@@ -51,6 +58,7 @@ public:
 
 private:
     orbslam2_amd::Extractor mDev;
+    bool mbHostPyramid = false;
 };
 
 }  // namespace ORB_SLAM2

@@ -1,9 +1,12 @@
-// Drop-in replacement for R/include/ORBmatcher.h: the same class declaration.  The constructor
-// (R/src/ORBmatcher.cpp:46-48), DescriptorDistance (:1901-1917), SearchForInitialization
-// (:499-617) and the two tracking forms of SearchByProjection (:63-163, :1564-1718) are defined
-// here over liborbslam2_amd through include/orbslam2_amd_shim.hpp; delete those five definitions
-// from R/src/ORBmatcher.cpp and keep the rest.  Compiles inside the
-// reference tree only (OpenCV, Frame.h); the shim is compiled and tested here with mock types.
+// Drop-in replacement for R/include/ORBmatcher.h: the same class declaration.  Defined here over
+// liborbslam2_amd through include/orbslam2_amd_shim.hpp: the constructor (R/src/ORBmatcher.cpp:46-48),
+// DescriptorDistance (:1901-1917), SearchForInitialization (:499-617), the two tracking forms of
+// SearchByProjection (:63-163, :1564-1718), both SearchByBoW overloads (:220-372, :632-760),
+// SearchForTriangulation (:785-983) and Fuse(pKF, vpMapPoints, th) (:995-1154); delete those
+// definitions from R/src/ORBmatcher.cpp and keep the rest.  Fuse reads a point's raw
+// mfMinDistance / mfMaxDistance through MapPoint::GetDistances (one accessor added
+// to R/include/MapPoint.h).  Compiles inside the reference tree only (OpenCV, Frame.h); the shim
+// is compiled and tested here with mock types (tests/test_cpp_shim*.py).
 #ifndef ORBMATCHER_H
 #define ORBMATCHER_H
 
@@ -39,8 +42,14 @@ public:
                            const float th, const int ORBdist);
     int SearchByProjection(KeyFrame* pKF, cv::Mat Scw, const std::vector<MapPoint*>& vpPoints,
                            std::vector<MapPoint*>& vpMatched, int th);
-    int SearchByBoW(KeyFrame* pKF, Frame& F, std::vector<MapPoint*>& vpMapPointMatches);
-    int SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoint*>& vpMatches12);
+    // BoW matchers on the GPU: tracking's reference keyframe / relocalisation (R :220-372) and
+    // loop closing (R :632-760)
+    int SearchByBoW(KeyFrame* pKF, Frame& F, std::vector<MapPoint*>& vpMapPointMatches) {
+        return mDev.SearchByBoW(pKF, F, vpMapPointMatches);
+    }
+    int SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoint*>& vpMatches12) {
+        return mDev.SearchByBoW(pKF1, pKF2, vpMatches12);
+    }
 
     // monocular initialisation matching on the GPU (R :499-617): same outputs, same order
     int SearchForInitialization(Frame& F1, Frame& F2, std::vector<cv::Point2f>& vbPrevMatched,
@@ -48,11 +57,16 @@ public:
         return mDev.SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize);
     }
 
+    // LocalMapping's matchers on the GPU: new map points (R :785-983) and fusion (R :995-1154)
     int SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, cv::Mat F12,
-                               std::vector<std::pair<size_t, size_t> >& vMatchedPairs, const bool bOnlyStereo);
+                               std::vector<std::pair<size_t, size_t> >& vMatchedPairs, const bool bOnlyStereo) {
+        return mDev.SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo);
+    }
     int SearchBySim3(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoint*>& vpMatches12, const float& s12,
                      const cv::Mat& R12, const cv::Mat& t12, const float th);
-    int Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, const float th = 3.0);
+    int Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, const float th = 3.0) {
+        return mDev.Fuse(pKF, vpMapPoints, th);
+    }
     int Fuse(KeyFrame* pKF, cv::Mat Scw, const std::vector<MapPoint*>& vpPoints, float th,
              vector<MapPoint*>& vpReplacePoint);
 

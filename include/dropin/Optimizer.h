@@ -29,7 +29,7 @@ public:
     void static LocalBundleAdjustment(KeyFrame* pKF, bool* pbStopFlag, Map* pMap) {
         orbslam2_amd::LocalBundleAdjustment(pKF, pbStopFlag, pMap);
     }
-    int static PoseOptimization(Frame* pFrame);
+    int static PoseOptimization(Frame* pFrame) { return orbslam2_amd::PoseOptimization(pFrame); }
     void static OptimizeEssentialGraph(Map* pMap, KeyFrame* pLoopKF, KeyFrame* pCurKF,
                                        const LoopClosing::KeyFrameAndPose& NonCorrectedSim3,
                                        const LoopClosing::KeyFrameAndPose& CorrectedSim3,

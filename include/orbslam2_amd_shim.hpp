@@ -12,7 +12,12 @@
 //   Matcher                   ORBmatcher (R/include/ORBmatcher.h:37-143): DescriptorDistance
 //                             (R/src/ORBmatcher.cpp:1901-1917), SearchForInitialization (:499-617),
 //                             SearchByProjection(Frame&, const Frame&, th, bMono) (:1564-1718) and
-//                             SearchByProjection(Frame&, const vector<MapPoint*>&, th) (:63-163)
+//                             SearchByProjection(Frame&, const vector<MapPoint*>&, th) (:63-163),
+//                             SearchForTriangulation (:785-983), Fuse(pKF, vpMapPoints, th)
+//                             (:995-1154), SearchByBoW(pKF, F, ...) (:220-372) and
+//                             SearchByBoW(pKF1, pKF2, ...) (:632-760)
+//   ComputeStereoMatches      Frame::ComputeStereoMatches (R/src/Frame.cpp:551-770)
+//   PoseOptimization          Optimizer::PoseOptimization (R/src/Optimizer.cpp:306-535)
 //   LocalBundleAdjustment     Optimizer::LocalBundleAdjustment (R/include/Optimizer.h:45,
 //                             R/src/Optimizer.cpp:564-918): graph gathering, lba_solve (or, given a
 //                             device list, lba_group_solve over several GPUs), write-back
@@ -128,8 +133,9 @@ private:
 };
 
 // ======================================================================= ORBmatcher
-// A Frame's matcher view: mvKeysUn split into arrays (built once per call), mDescriptors,
-// mvuRight and the static grid bounds (R/include/Frame.h: mnMinX .. mfGridElementHeightInv).
+// A Frame's (or KeyFrame's) matcher view: mvKeysUn split into arrays (built once per call),
+// mDescriptors, mvuRight and the grid bounds (R/include/Frame.h: mnMinX .. mfGridElementHeightInv;
+// R/include/KeyFrame.h:199-206 keeps the same names as const members).
 template <class FrameT>
 struct FrameView {
     std::vector<float> x, y, ang;
@@ -146,14 +152,83 @@ struct FrameView {
         v.x = x.data(); v.y = y.data(); v.angle = ang.data(); v.octave = oct.data();
         v.desc = F.mDescriptors.data;
         v.uright = F.mvuRight.empty() ? nullptr : F.mvuRight.data();
-        v.min_x = FrameT::mnMinX; v.min_y = FrameT::mnMinY; v.max_x = FrameT::mnMaxX; v.max_y = FrameT::mnMaxY;
-        v.grid_w_inv = FrameT::mfGridElementWidthInv; v.grid_h_inv = FrameT::mfGridElementHeightInv;
+        // static members of Frame, const members of KeyFrame: both read through the object
+        v.min_x = (float)F.mnMinX; v.min_y = (float)F.mnMinY; v.max_x = (float)F.mnMaxX; v.max_y = (float)F.mnMaxY;
+        v.grid_w_inv = F.mfGridElementWidthInv; v.grid_h_inv = F.mfGridElementHeightInv;
     }
 };
 
+// DBoW2::FeatureVector (std::map<NodeId, std::vector<unsigned int>>) as the C-ABI's arrays: node
+// ids ascending (map order), CSR starts, feature indices in insertion order.
+template <class FV>
+struct FeatVecArrays {
+    std::vector<uint32_t> nodes;
+    std::vector<int32_t> start{0}, fidx;
+    explicit FeatVecArrays(const FV& fv) {
+        for (const auto& kv : fv) {
+            nodes.push_back((uint32_t)kv.first);
+            for (const auto i : kv.second) fidx.push_back((int32_t)i);
+            start.push_back((int32_t)fidx.size());
+        }
+    }
+    int n() const { return (int)nodes.size(); }
+};
+
+namespace detail {
+template <class MatT>
+inline void read_Tcw(const MatT& T, float out[16]) {
+    for (int r = 0; r < 4; r++)
+        for (int k = 0; k < 4; k++) out[4 * r + k] = T.template at<float>(r, k);
+}
+template <class MatT>
+inline MatT make_mat(int rows, int cols, const float* v) {   // cv::Mat(rows, cols, CV_32F)
+    MatT m(rows, cols, kCV_32F);
+    for (int r = 0; r < rows; r++)
+        for (int k = 0; k < cols; k++) m.template at<float>(r, k) = v[cols * r + k];
+    return m;
+}
+// cv::Mat float products R*x + t (3x3 * 3x1 + 3x1) as OpenCV's GEMM evaluates CV_32F: dot products
+// accumulated in double, rounded to float once (the oracle's convention, oracle/orb_oracle.c)
+inline void rx_plus_t(const float R[9], const float x[3], const float t[3], float out[3]) {
+    for (int r = 0; r < 3; r++)
+        out[r] = (float)((double)R[3 * r] * x[0] + (double)R[3 * r + 1] * x[1] + (double)R[3 * r + 2] * x[2] +
+                         (double)t[r]);
+}
+template <class MatT>
+inline void read_vec3(const MatT& m, float out[3]) {
+    for (int k = 0; k < 3; k++) out[k] = m.template at<float>(k, 0);
+}
+template <class MatT>
+inline void read_mat33(const MatT& m, float out[9]) {
+    for (int r = 0; r < 3; r++)
+        for (int k = 0; k < 3; k++) out[3 * r + k] = m.template at<float>(r, k);
+}
+// orb_kf_params of a keyframe (ORBmatcher::Fuse reads GetPose, GetCameraCenter, the intrinsics
+// and the scale tables, R/src/ORBmatcher.cpp:997-1006)
+template <class KeyFrameT>
+struct KfParams {
+    orb_kf_params p{};
+    std::vector<float> sf, isg;
+    explicit KfParams(KeyFrameT* pKF) {
+        const auto T = pKF->GetPose();
+        for (int r = 0; r < 3; r++)
+            for (int k = 0; k < 4; k++) p.Tcw[4 * r + k] = T.template at<float>(r, k);
+        read_vec3(pKF->GetCameraCenter(), p.Ow);
+        p.fx = pKF->fx; p.fy = pKF->fy; p.cx = pKF->cx; p.cy = pKF->cy; p.bf = pKF->mbf;
+        p.log_scale_factor = pKF->mfLogScaleFactor;
+        p.n_levels = pKF->mnScaleLevels;
+        sf.assign(pKF->mvScaleFactors.begin(), pKF->mvScaleFactors.end());
+        isg.assign(pKF->mvInvLevelSigma2.begin(), pKF->mvInvLevelSigma2.end());
+        p.scale_factors = sf.data();
+        p.inv_level_sigma2 = isg.data();
+    }
+};
+}  // namespace detail
+
 class Matcher {
 public:
-    explicit Matcher(float nnratio = 0.6f, bool checkOri = true, int device = 0) {
+    explicit Matcher(float nnratio = 0.6f, bool checkOri = true, int device = 0)
+        : nnratio_(nnratio), checkOri_(checkOri), device_(device) {
         check(orb_matcher_create(device, nnratio, checkOri ? 1 : 0, &h_), "orb_matcher_create");
     }
     ~Matcher() { orb_matcher_destroy(h_); }
@@ -251,6 +326,138 @@ public:
         return n;
     }
 
+    // SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo) (R :785-983,
+    // LocalMapping::CreateNewMapPoints, R/src/LocalMapping.cpp:374): the epipole (:791-797) from
+    // pKF1->GetCameraCenter() and pKF2's GetRotation / GetTranslation / intrinsics, both keyframes'
+    // mFeatVec, GetMapPoint(i) occupancy, pKF2's mvScaleFactors / mvLevelSigma2; vMatchedPairs in
+    // KF1 index order (:975-981).
+    template <class KeyFrameT, class MatT>
+    int SearchForTriangulation(KeyFrameT* pKF1, KeyFrameT* pKF2, const MatT& F12,
+                               std::vector<std::pair<size_t, size_t>>& vMatchedPairs, bool bOnlyStereo) {
+        FrameView<KeyFrameT> a(*pKF1), b(*pKF2);
+        FeatVecArrays<decltype(pKF1->mFeatVec)> fv1(pKF1->mFeatVec), fv2(pKF2->mFeatVec);
+        const size_t n1 = pKF1->mvKeysUn.size(), n2 = pKF2->mvKeysUn.size();
+        std::vector<uint8_t> has1(n1), has2(n2);
+        for (size_t i = 0; i < n1; i++) has1[i] = pKF1->GetMapPoint(i) ? 1 : 0;
+        for (size_t i = 0; i < n2; i++) has2[i] = pKF2->GetMapPoint(i) ? 1 : 0;
+        float Cw[3], R2w[9], t2w[3], C2[3], F[9];
+        detail::read_vec3(pKF1->GetCameraCenter(), Cw);
+        detail::read_mat33(pKF2->GetRotation(), R2w);
+        detail::read_vec3(pKF2->GetTranslation(), t2w);
+        detail::rx_plus_t(R2w, Cw, t2w, C2);   // C2 = R2w*Cw + t2w
+        const float invz = 1.0f / C2[2];
+        const float ex = pKF2->fx * C2[0] * invz + pKF2->cx;
+        const float ey = pKF2->fy * C2[1] * invz + pKF2->cy;
+        detail::read_mat33(F12, F);
+        const std::vector<float> sf2(pKF2->mvScaleFactors.begin(), pKF2->mvScaleFactors.end());
+        const std::vector<float> s2(pKF2->mvLevelSigma2.begin(), pKF2->mvLevelSigma2.end());
+        std::vector<int32_t> m12(n1, -1);
+        const int n = check(orb_search_for_triangulation(device_, &a.v, &b.v, has1.data(), has2.data(), fv1.n(),
+                                                         fv1.nodes.data(), fv1.start.data(), fv1.fidx.data(), fv2.n(),
+                                                         fv2.nodes.data(), fv2.start.data(), fv2.fidx.data(), F, ex, ey,
+                                                         sf2.data(), s2.data(), (int)sf2.size(), bOnlyStereo ? 1 : 0,
+                                                         checkOri_ ? 1 : 0, m12.data()),
+                            "orb_search_for_triangulation");
+        vMatchedPairs.clear();
+        vMatchedPairs.reserve((size_t)n);
+        for (size_t i = 0; i < n1; i++)
+            if (m12[i] >= 0) vMatchedPairs.push_back(std::make_pair(i, (size_t)m12[i]));
+        return n;
+    }
+
+    // Fuse(pKF, vpMapPoints, th) (R :995-1154, LocalMapping::SearchInNeighbors): the matching step of
+    // every point on the GPU (orb_fuse), then the replace / add step in vector order on the host.  A
+    // point is re-checked there (isBad, IsInKeyFrame) because an earlier iteration of the reference
+    // loop may have replaced it or added it to pKF, which makes the reference skip it (:1011-1014);
+    // pKF->GetMapPoint(bestIdx) is likewise read at that point of the loop.  The distances are the
+    // raw mfMinDistance / mfMaxDistance, read through MapPoint::GetDistances (a
+    // one-line accessor the drop-in adds to MapPoint; the kernel applies the 0.8 / 1.2 invariance).
+    template <class KeyFrameT, class MapPointT>
+    int Fuse(KeyFrameT* pKF, const std::vector<MapPointT*>& vpMapPoints, const float th = 3.0f) {
+        FrameView<KeyFrameT> kv(*pKF);
+        detail::KfParams<KeyFrameT> kp(pKF);
+        const size_t n = vpMapPoints.size();
+        std::vector<uint8_t> valid(n, 0), desc(n * 32, 0);
+        std::vector<float> xyz(3 * n, 0.f), nrm(3 * n, 0.f), mind(n, 0.f), maxd(n, 0.f);
+        for (size_t i = 0; i < n; i++) {
+            MapPointT* pMP = vpMapPoints[i];
+            if (!pMP || pMP->isBad() || pMP->IsInKeyFrame(pKF)) continue;
+            valid[i] = 1;
+            detail::read_vec3(pMP->GetWorldPos(), &xyz[3 * i]);
+            detail::read_vec3(pMP->GetNormal(), &nrm[3 * i]);
+            pMP->GetDistances(mind[i], maxd[i]);
+            const auto d = pMP->GetDescriptor();
+            std::memcpy(&desc[32 * i], d.data, 32);
+        }
+        std::vector<int32_t> bi(n, -1), bd(n, 256);
+        if (n)
+            check(orb_fuse(device_, &kv.v, &kp.p, (int)n, valid.data(), xyz.data(), nrm.data(), mind.data(), maxd.data(),
+                           desc.data(), th, bi.data(), bd.data()),
+                  "orb_fuse");
+        int nFused = 0;
+        for (size_t i = 0; i < n; i++) {
+            if (bi[i] < 0) continue;   // bestDist > TH_LOW (or no candidate)
+            MapPointT* pMP = vpMapPoints[i];
+            if (pMP->isBad() || pMP->IsInKeyFrame(pKF)) continue;
+            const size_t bestIdx = (size_t)bi[i];
+            MapPointT* pMPinKF = pKF->GetMapPoint(bestIdx);
+            if (pMPinKF) {   // :1123-1136
+                if (!pMPinKF->isBad()) {
+                    if (pMPinKF->Observations() > pMP->Observations()) pMP->Replace(pMPinKF);
+                    else pMPinKF->Replace(pMP);
+                }
+            } else {         // :1137-1141
+                pMP->AddObservation(pKF, bestIdx);
+                pKF->AddMapPoint(pMP, bestIdx);
+            }
+            nFused++;
+        }
+        return nFused;
+    }
+
+    // SearchByBoW(pKF, F, vpMapPointMatches) (R :220-372, Tracking::TrackReferenceKeyFrame /
+    // Relocalization): vpMapPointMatches = F.N NULLs, then the keyframe's map point for every match.
+    template <class KeyFrameT, class FrameT, class MapPointT>
+    int SearchByBoW(KeyFrameT* pKF, FrameT& F, std::vector<MapPointT*>& vpMapPointMatches) {
+        const std::vector<MapPointT*> vpMapPointsKF = pKF->GetMapPointMatches();
+        FrameView<KeyFrameT> kv(*pKF);
+        FrameView<FrameT> fv(F);
+        FeatVecArrays<decltype(pKF->mFeatVec)> a(pKF->mFeatVec);
+        FeatVecArrays<decltype(F.mFeatVec)> b(F.mFeatVec);
+        std::vector<uint8_t> ok(vpMapPointsKF.size());
+        for (size_t i = 0; i < ok.size(); i++) ok[i] = vpMapPointsKF[i] && !vpMapPointsKF[i]->isBad() ? 1 : 0;
+        const size_t nf = F.mvKeysUn.size();
+        vpMapPointMatches = std::vector<MapPointT*>(nf, static_cast<MapPointT*>(nullptr));
+        std::vector<int32_t> mf(nf, -1);
+        const int n = check(orb_search_by_bow_frame(device_, &kv.v, ok.data(), a.n(), a.nodes.data(), a.start.data(),
+                                                    a.fidx.data(), &fv.v, b.n(), b.nodes.data(), b.start.data(),
+                                                    b.fidx.data(), nnratio_, checkOri_ ? 1 : 0, mf.data()),
+                            "orb_search_by_bow_frame");
+        for (size_t j = 0; j < nf; j++)
+            if (mf[j] >= 0) vpMapPointMatches[j] = vpMapPointsKF[(size_t)mf[j]];
+        return n;
+    }
+
+    // SearchByBoW(pKF1, pKF2, vpMatches12) (R :632-760, LoopClosing::ComputeSim3).
+    template <class KeyFrameT, class MapPointT>
+    int SearchByBoW(KeyFrameT* pKF1, KeyFrameT* pKF2, std::vector<MapPointT*>& vpMatches12) {
+        const std::vector<MapPointT*> vp1 = pKF1->GetMapPointMatches(), vp2 = pKF2->GetMapPointMatches();
+        FrameView<KeyFrameT> k1(*pKF1), k2(*pKF2);
+        FeatVecArrays<decltype(pKF1->mFeatVec)> a(pKF1->mFeatVec), b(pKF2->mFeatVec);
+        std::vector<uint8_t> ok1(vp1.size()), ok2(vp2.size());
+        for (size_t i = 0; i < vp1.size(); i++) ok1[i] = vp1[i] && !vp1[i]->isBad() ? 1 : 0;
+        for (size_t i = 0; i < vp2.size(); i++) ok2[i] = vp2[i] && !vp2[i]->isBad() ? 1 : 0;
+        vpMatches12 = std::vector<MapPointT*>(vp1.size(), static_cast<MapPointT*>(nullptr));
+        std::vector<int32_t> m12(vp1.size(), -1);
+        const int n = check(orb_search_by_bow_kf(device_, &k1.v, ok1.data(), a.n(), a.nodes.data(), a.start.data(),
+                                                 a.fidx.data(), &k2.v, ok2.data(), b.n(), b.nodes.data(), b.start.data(),
+                                                 b.fidx.data(), nnratio_, checkOri_ ? 1 : 0, m12.data()),
+                            "orb_search_by_bow_kf");
+        for (size_t i = 0; i < vp1.size(); i++)
+            if (m12[i] >= 0) vpMatches12[i] = vp2[(size_t)m12[i]];
+        return n;
+    }
+
 private:
     template <class MatT>
     static void detail_read_T34(const MatT& T, float out[12]) {   // rows 0..2 of a 4x4 float cv::Mat
@@ -258,7 +465,79 @@ private:
             for (int k = 0; k < 4; k++) out[4 * r + k] = T.template at<float>(r, k);
     }
     orb_matcher* h_ = nullptr;
+    float nnratio_;
+    bool checkOri_;
+    int device_;
 };
+
+// ======================================================================= Frame::ComputeStereoMatches
+// R/src/Frame.cpp:551-770 on the device: reads the two extractors' device pyramids in place (no
+// mvImagePyramid download) and F.mvKeys / mvKeysRight / mDescriptors / mDescriptorsRight / mbf /
+// mb; writes F.mvuRight and F.mvDepth (N entries, -1 = no stereo match) as :555-556 initialise them.
+// left / right = the handles that extracted this frame's images (their last call).
+template <class FrameT>
+void ComputeStereoMatches(FrameT& F, orb_extractor* left, orb_extractor* right) {
+    const size_t N = F.mvKeys.size(), Nr = F.mvKeysRight.size();
+    F.mvuRight = std::vector<float>(N, -1.0f);
+    F.mvDepth = std::vector<float>(N, -1.0f);
+    if (N == 0 || Nr == 0) return;
+    static_assert(sizeof(F.mvKeys[0]) == sizeof(orb_keypoint), "KeyPoint must have the cv::KeyPoint layout");
+    check(orb_compute_stereo_matches(left, right, reinterpret_cast<const orb_keypoint*>(F.mvKeys.data()),
+                                     F.mDescriptors.data, (int)N,
+                                     reinterpret_cast<const orb_keypoint*>(F.mvKeysRight.data()),
+                                     F.mDescriptorsRight.data, (int)Nr, F.mbf, F.mb, F.mvuRight.data(),
+                                     F.mvDepth.data()),
+          "orb_compute_stereo_matches");
+}
+
+// ======================================================================= Optimizer::PoseOptimization
+// R/src/Optimizer.cpp:306-535 (Tracking: every tracked frame, R/src/Tracking.cpp:1030, 1203, 1262,
+// 1908): one edge per keypoint with a map point, in keypoint order, gathered under
+// MapPoint::mGlobalMutex (:343-429; mvbOutlier[i] = false for each), the four optimize(10) rounds on
+// the GPU (pose_optimize_batch, one frame), then mvbOutlier, SetPose and the return value
+// nInitialCorrespondences - nBad.  Below 3 edges: return 0, pose untouched (:431-432).
+template <class FrameT>
+int PoseOptimization(FrameT* pFrame, int device = 0) {
+    using MapPointT = typename std::remove_pointer<typename std::decay<decltype(pFrame->mvpMapPoints[0])>::type>::type;
+    using MatT = typename std::decay<decltype(pFrame->mTcw)>::type;
+    const size_t N = pFrame->mvKeysUn.size();
+    std::vector<size_t> idx;
+    std::vector<double> obs, xw, info;
+    {
+        std::unique_lock<std::mutex> lock(MapPointT::mGlobalMutex);
+        for (size_t i = 0; i < N; i++) {
+            MapPointT* pMP = pFrame->mvpMapPoints[i];
+            if (!pMP) continue;
+            pFrame->mvbOutlier[i] = false;
+            const auto& kp = pFrame->mvKeysUn[i];
+            obs.push_back(kp.pt.x);
+            obs.push_back(kp.pt.y);
+            obs.push_back(pFrame->mvuRight[i]);   // < 0: monocular edge
+            float X[3];
+            detail::read_vec3(pMP->GetWorldPos(), X);
+            xw.insert(xw.end(), {(double)X[0], (double)X[1], (double)X[2]});
+            info.push_back((double)pFrame->mvInvLevelSigma2[(size_t)kp.octave]);
+            idx.push_back(i);
+        }
+    }
+    const int E = (int)idx.size();
+    if (E < 3) return 0;
+    float T[16];
+    detail::read_Tcw(pFrame->mTcw, T);
+    double q[4], t[3], oq[4], ot[3];
+    lba_pose_from_Tcw(T, q, t);   // Converter::toSE3Quat
+    const double cam[5] = {pFrame->fx, pFrame->fy, pFrame->cx, pFrame->cy, pFrame->mbf};
+    const int32_t start[2] = {0, E};
+    pose_batch b{1, E, q, t, cam, start, obs.data(), xw.data(), info.data()};
+    std::vector<uint8_t> outl((size_t)E, 0);
+    int32_t ninl = 0;
+    pose_batch_result r{oq, ot, outl.data(), &ninl};
+    check(pose_optimize_batch(device, &b, &r, nullptr), "pose_optimize_batch");
+    for (int e = 0; e < E; e++) pFrame->mvbOutlier[idx[(size_t)e]] = outl[(size_t)e] != 0;
+    lba_pose_to_Tcw(oq, ot, T);   // Converter::toCvMat
+    pFrame->SetPose(detail::make_mat<MatT>(4, 4, T));
+    return ninl;
+}
 
 // ======================================================================= LocalBundleAdjustment
 // Per-thread solver context (LocalMapping runs the local BA on its own thread).
@@ -267,21 +546,6 @@ inline lba_context* thread_lba(int device = 0) {
     if (!c) check(lba_create(device, &c), "lba_create");
     return c;
 }
-
-namespace detail {
-template <class MatT>
-inline void read_Tcw(const MatT& T, float out[16]) {
-    for (int r = 0; r < 4; r++)
-        for (int k = 0; k < 4; k++) out[4 * r + k] = T.template at<float>(r, k);
-}
-template <class MatT>
-inline MatT make_mat(int rows, int cols, const float* v) {   // cv::Mat(rows, cols, CV_32F)
-    MatT m(rows, cols, kCV_32F);
-    for (int r = 0; r < rows; r++)
-        for (int k = 0; k < cols; k++) m.template at<float>(r, k) = v[cols * r + k];
-    return m;
-}
-}  // namespace detail
 
 // Optimizer::LocalBundleAdjustment(pKF, pbStopFlag, pMap): the local window and its fixed
 // observers gathered exactly as R/src/Optimizer.cpp:567-625 does (covisible keyframes in

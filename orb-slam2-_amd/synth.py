@@ -420,7 +420,8 @@ def triangulation_problem(seed=4, n_points=800, extra=150, stereo_frac=0.3, mp_f
     C2 = R2 @ C1 + t2
     ex, ey = np.float32(fx * C2[0] / C2[2] + cx), np.float32(fy * C2[1] / C2[2] + cy)
     return {"kf1": k1, "kf2": k2, "F12": F12, "ex": float(ex), "ey": float(ey), "scale_factors": sf,
-            "level_sigma2": sig2}
+            "level_sigma2": sig2, "R1": R1.astype(np.float32), "t1": t1.astype(np.float32),
+            "R2": R2.astype(np.float32), "t2": t2.astype(np.float32)}
 
 
 def vocabulary(k=10, L=4, seed=7, early_leaf=0.08, stop_frac=0.05, dup_frac=0.03):

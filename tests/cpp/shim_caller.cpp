@@ -8,13 +8,28 @@
 //   shim_caller sbl IN OUT       ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th)
 //   shim_caller lba IN OUT       Optimizer::LocalBundleAdjustment on a mock keyframe / map-point graph
 //   shim_caller lbag IN OUT      the same through the device-list overload (lba_group, several GPUs)
+//   shim_caller pose IN OUT      Optimizer::PoseOptimization on a mock Frame
+//   shim_caller stereo IN OUT    ORBextractor on a left / right image (two handles), then
+//                                Frame::ComputeStereoMatches on the mock Frame
+//   shim_caller fuse IN OUT      ORBmatcher::Fuse(pKF, vpMapPoints, th), replace / add on mock points
+//   shim_caller sft IN OUT       ORBmatcher::SearchForTriangulation(pKF1, pKF2, F12, pairs, bOnlyStereo)
+//   shim_caller sbbf IN OUT      ORBmatcher::SearchByBoW(pKF, F, vpMapPointMatches)
+//   shim_caller sbbk IN OUT      ORBmatcher::SearchByBoW(pKF1, pKF2, vpMatches12)
+//   shim_caller threads IN OUT   the SURVEY 8b threading contract: two Extractor handles on two host
+//                                threads at once (stereo L/R, R/src/Frame.cpp:86-89), SearchForInitialization
+//                                and PoseOptimization on a third and fourth (Tracking), LocalBundleAdjustment
+//                                on a fifth (LocalMapping), each repeated; results must not change
 // IN / OUT: little-endian arrays, each written as int64 element count + raw elements.
 // Exit status: 0 ok, 3 the library reported an error (e.g. no gfx950 device), 2 bad usage.
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <utility>
 #include <stdexcept>
 #include <vector>
@@ -51,39 +66,65 @@ struct Mat {   // the cv::Mat members the shim uses
 struct Point2f { float x, y; };
 struct KeyPoint { Point2f pt; float size, angle, response; int octave, class_id; };
 
+using FeatureVector = std::map<unsigned int, std::vector<unsigned int>>;   // DBoW2::FeatureVector
+
 struct MapPoint;
 struct Frame {
-    std::vector<KeyPoint> mvKeysUn;
-    Mat mDescriptors;
-    std::vector<float> mvuRight;
+    std::vector<KeyPoint> mvKeys, mvKeysRight, mvKeysUn;
+    Mat mDescriptors, mDescriptorsRight;
+    std::vector<float> mvuRight, mvDepth;
     std::vector<MapPoint*> mvpMapPoints;
     std::vector<bool> mvbOutlier;
-    std::vector<float> mvScaleFactors;
+    std::vector<float> mvScaleFactors, mvInvLevelSigma2;
+    FeatureVector mFeatVec;
     Mat mTcw;
     float mbf = 0, mb = 0;
     static float mnMinX, mnMinY, mnMaxX, mnMaxY, mfGridElementWidthInv, mfGridElementHeightInv;
     static float fx, fy, cx, cy;
+    void SetPose(const Mat& T) { mTcw = T; }
 };
 float Frame::mnMinX, Frame::mnMinY, Frame::mnMaxX, Frame::mnMaxY, Frame::mfGridElementWidthInv,
     Frame::mfGridElementHeightInv, Frame::fx, Frame::fy, Frame::cx, Frame::cy;
 
 // the order of KeyFrame::EraseMapPointMatch calls (keyframe mnId, map point mnId)
-std::vector<std::pair<unsigned long, unsigned long>> g_erase_log;
+thread_local std::vector<std::pair<unsigned long, unsigned long>> g_erase_log;
 struct KeyFrame {
     unsigned long mnId = 0, mnBALocalForKF = 0, mnBAFixedForKF = 0;
     bool bad = false;
     std::vector<KeyFrame*> covis;
-    std::vector<MapPoint*> matches;
-    Mat Tcw;
+    std::vector<MapPoint*> matches;   // mvpMapPoints
+    Mat Tcw, Ow;
     std::vector<KeyPoint> mvKeysUn;
-    std::vector<float> mvuRight, mvInvLevelSigma2;
+    Mat mDescriptors;
+    std::vector<float> mvuRight, mvInvLevelSigma2, mvLevelSigma2, mvScaleFactors;
+    FeatureVector mFeatVec;
     float fx = 0, fy = 0, cx = 0, cy = 0, mbf = 0;
+    float mfLogScaleFactor = 0;
+    int mnScaleLevels = 8;
+    int mnMinX = 0, mnMinY = 0, mnMaxX = 640, mnMaxY = 480;   // const int members in the reference
+    float mfGridElementWidthInv = 0, mfGridElementHeightInv = 0;
     std::vector<KeyFrame*> GetVectorCovisibleKeyFrames() { return covis; }
     std::vector<MapPoint*> GetMapPointMatches() { return matches; }
+    MapPoint* GetMapPoint(size_t i) { return matches[i]; }
+    void AddMapPoint(MapPoint* p, size_t i) { matches[i] = p; }
+    void ReplaceMapPointMatch(size_t i, MapPoint* p) { matches[i] = p; }
     bool isBad() const { return bad; }
     Mat GetPose() { return Tcw; }
     void SetPose(const Mat& T) { Tcw = T; }
+    Mat GetCameraCenter() { return Ow; }
+    Mat GetRotation() {
+        Mat R(3, 3, orbslam2_amd::kCV_32F);
+        for (int r = 0; r < 3; r++)
+            for (int k = 0; k < 3; k++) R.at<float>(r, k) = Tcw.at<float>(r, k);
+        return R;
+    }
+    Mat GetTranslation() {
+        Mat t(3, 1, orbslam2_amd::kCV_32F);
+        for (int r = 0; r < 3; r++) t.at<float>(r, 0) = Tcw.at<float>(r, 3);
+        return t;
+    }
     void EraseMapPointMatch(MapPoint* p);
+    void EraseMapPointMatch(size_t i) { matches[i] = nullptr; }
 };
 struct MapPoint {
     unsigned long mnId = 0, mnBALocalForKF = 0;
@@ -105,7 +146,35 @@ struct MapPoint {
     bool mbTrackInView = false;
     float mTrackProjX = 0, mTrackProjY = 0, mTrackProjXR = 0, mTrackViewCos = 0;
     int mnTrackScaleLevel = 0;
+    // Fuse / PoseOptimization members
+    static std::mutex mGlobalMutex;
+    Mat normal;
+    float mfMinDistance = 0, mfMaxDistance = 0;
+    Mat GetNormal() { return normal; }
+    void GetDistances(float& mn, float& mx) { mn = mfMinDistance; mx = mfMaxDistance; }
+    bool IsInKeyFrame(KeyFrame* k) { return obs.count(k) > 0; }
+    void AddObservation(KeyFrame* k, size_t i) { obs[k] = i; }
+    MapPoint* replacedBy = nullptr;
+    // MapPoint::Replace (R/src/MapPoint.cpp:177-219): observations move to pMP unless it is in that
+    // keyframe already (then the keyframe's slot is erased); this point becomes bad
+    void Replace(MapPoint* p) {
+        if (p == this) return;
+        const auto o = obs;
+        obs.clear();
+        bad = true;
+        replacedBy = p;
+        for (const auto& kv : o) {
+            if (!p->IsInKeyFrame(kv.first)) {
+                kv.first->ReplaceMapPointMatch(kv.second, p);
+                p->AddObservation(kv.first, kv.second);
+            } else {
+                kv.first->EraseMapPointMatch(kv.second);
+            }
+        }
+        p->extraObs += extraObs;
+    }
 };
+std::mutex MapPoint::mGlobalMutex;
 inline void KeyFrame::EraseMapPointMatch(MapPoint* p) {
     g_erase_log.emplace_back(mnId, p->mnId);
     for (auto& m : matches)
@@ -297,6 +366,7 @@ static void run_sbl(FILE* in, FILE* out) {
 }
 
 static void run_lba(FILE* in, FILE* out, bool group) {
+    mock::g_erase_log.clear();
     const auto Tcw = rd<float>(in);
     const auto fixedCam = rd<uint8_t>(in);
     const auto kfId = rd<int64_t>(in);
@@ -373,9 +443,334 @@ static void run_lba(FILE* in, FILE* out, bool group) {
     wr(out, elog);
 }
 
+// ---------------------------------------------------------------- PoseOptimization
+// IN: Tcw (16), keypoint x, y, octave, uright, has_mp (uint8), map point xyz (3 per keypoint),
+//     mvInvLevelSigma2, cam (fx, fy, cx, cy, bf).  OUT: return value, mvbOutlier (uint8 per
+//     keypoint), Tcw after the call.
+static void run_pose(FILE* in, FILE* out) {
+    const auto T = rd<float>(in);
+    const auto x = rd<float>(in), y = rd<float>(in);
+    const auto oct = rd<int32_t>(in);
+    mock::Frame F;
+    F.mvuRight = rd<float>(in);
+    const auto has = rd<uint8_t>(in);
+    const auto xyz = rd<float>(in);
+    F.mvInvLevelSigma2 = rd<float>(in);
+    const auto cam = rd<float>(in);
+    const size_t n = x.size();
+    F.mvKeysUn.resize(n);
+    for (size_t i = 0; i < n; i++) F.mvKeysUn[i] = mock::KeyPoint{{x[i], y[i]}, 31.f, 0.f, 0.f, oct[i], -1};
+    std::vector<mock::MapPoint> pts(n);
+    F.mvpMapPoints.assign(n, nullptr);
+    F.mvbOutlier.assign(n, true);   // stale flags: the call resets every edge's
+    for (size_t i = 0; i < n; i++) {
+        pts[i].X.create(3, 1, orbslam2_amd::kCV_32F);
+        for (int k = 0; k < 3; k++) pts[i].X.at<float>(k, 0) = xyz[3 * i + (size_t)k];
+        if (has[i]) F.mvpMapPoints[i] = &pts[i];
+    }
+    F.mTcw.create(4, 4, orbslam2_amd::kCV_32F);
+    for (int i = 0; i < 16; i++) F.mTcw.at<float>(i / 4, i % 4) = T[(size_t)i];
+    mock::Frame::fx = cam[0]; mock::Frame::fy = cam[1]; mock::Frame::cx = cam[2]; mock::Frame::cy = cam[3];
+    F.mbf = cam[4];
+    const int32_t r = orbslam2_amd::PoseOptimization(&F);
+    wr(out, &r, 1);
+    std::vector<uint8_t> o(n);
+    for (size_t i = 0; i < n; i++) o[i] = F.mvbOutlier[i] ? 1 : 0;
+    wr(out, o);
+    std::vector<float> To(16);
+    for (int i = 0; i < 16; i++) To[(size_t)i] = F.mTcw.at<float>(i / 4, i % 4);
+    wr(out, To);
+}
+
+// ---------------------------------------------------------------- stereo Frame
+// IN: (w, h, nfeatures), left image, right image, (mbf, mb).  OUT: left keypoints (bytes), left
+// descriptors, right keypoints, right descriptors, mvuRight, mvDepth.  The two extractions run on
+// two host threads at once, as the stereo Frame constructor does (R/src/Frame.cpp:86-89); the
+// extractors persist per calling thread, as Tracking's mpORBextractorLeft / Right do.
+struct StereoExtractors {
+    int w = 0, h = 0, nf = 0;
+    std::unique_ptr<orbslam2_amd::Extractor> L, R;
+};
+static void run_stereo(FILE* in, FILE* out) {
+    const auto whn = rd<int32_t>(in);
+    const auto l = rd<uint8_t>(in), r = rd<uint8_t>(in);
+    const auto mb = rd<float>(in);
+    const int W = whn[0], H = whn[1], NF = whn[2];
+    thread_local StereoExtractors ex;
+    if (!ex.L || ex.w != W || ex.h != H || ex.nf != NF) {
+        ex.L.reset(new orbslam2_amd::Extractor(NF, 1.2f, 8, 20, 7, 0, W, H));
+        ex.R.reset(new orbslam2_amd::Extractor(NF, 1.2f, 8, 20, 7, 0, W, H));
+        ex.w = W; ex.h = H; ex.nf = NF;
+    }
+    mock::Mat iL(H, W, orbslam2_amd::kCV_8U), iR(H, W, orbslam2_amd::kCV_8U);
+    std::copy(l.begin(), l.end(), iL.data);
+    std::copy(r.begin(), r.end(), iR.data);
+    mock::Frame F;
+    std::string errL;
+    std::thread tl([&] {
+        try { ex.L->extract(iL, F.mvKeys, F.mDescriptors); } catch (const std::exception& e) { errL = e.what(); }
+    });
+    ex.R->extract(iR, F.mvKeysRight, F.mDescriptorsRight);
+    tl.join();
+    if (!errL.empty()) throw std::runtime_error(errL);
+    F.mbf = mb[0];
+    F.mb = mb[1];
+    orbslam2_amd::ComputeStereoMatches(F, ex.L->handle(), ex.R->handle());
+    wr(out, reinterpret_cast<const uint8_t*>(F.mvKeys.data()), F.mvKeys.size() * sizeof(mock::KeyPoint));
+    wr(out, F.mDescriptors.data, (size_t)F.mDescriptors.rows * 32);
+    wr(out, reinterpret_cast<const uint8_t*>(F.mvKeysRight.data()), F.mvKeysRight.size() * sizeof(mock::KeyPoint));
+    wr(out, F.mDescriptorsRight.data, (size_t)F.mDescriptorsRight.rows * 32);
+    wr(out, F.mvuRight);
+    wr(out, F.mvDepth);
+}
+
+// ---------------------------------------------------------------- keyframes for the LocalMapping /
+// LoopClosing matchers.  IN: keypoint x, y, angle, octave, descriptors, mvuRight, grid bounds
+// (minX, minY, maxX, maxY, 1/cell w, 1/cell h), Tcw (16), camera centre (3), (fx, fy, cx, cy, bf),
+// mfLogScaleFactor, mvScaleFactors, mvInvLevelSigma2, mvLevelSigma2, mFeatVec (node ids, CSR
+// starts, feature indices).
+static void load_kf(FILE* in, mock::KeyFrame& K) {
+    const auto x = rd<float>(in), y = rd<float>(in), a = rd<float>(in);
+    const auto o = rd<int32_t>(in);
+    const auto d = rd<uint8_t>(in);
+    K.mvuRight = rd<float>(in);
+    const auto g = rd<float>(in);
+    const auto T = rd<float>(in), Ow = rd<float>(in), cam = rd<float>(in), lsf = rd<float>(in);
+    K.mvScaleFactors = rd<float>(in);
+    K.mvInvLevelSigma2 = rd<float>(in);
+    K.mvLevelSigma2 = rd<float>(in);
+    const auto nodes = rd<uint32_t>(in);
+    const auto start = rd<int32_t>(in), fidx = rd<int32_t>(in);
+    const size_t n = x.size();
+    K.mvKeysUn.resize(n);
+    for (size_t i = 0; i < n; i++) K.mvKeysUn[i] = mock::KeyPoint{{x[i], y[i]}, 31.f, a[i], 0.f, o[i], -1};
+    K.mDescriptors.create((int)n, 32, orbslam2_amd::kCV_8U);
+    std::copy(d.begin(), d.end(), K.mDescriptors.data);
+    K.mnMinX = (int)g[0]; K.mnMinY = (int)g[1]; K.mnMaxX = (int)g[2]; K.mnMaxY = (int)g[3];
+    K.mfGridElementWidthInv = g[4]; K.mfGridElementHeightInv = g[5];
+    K.Tcw.create(4, 4, orbslam2_amd::kCV_32F);
+    for (int i = 0; i < 16; i++) K.Tcw.at<float>(i / 4, i % 4) = T[(size_t)i];
+    K.Ow.create(3, 1, orbslam2_amd::kCV_32F);
+    for (int i = 0; i < 3; i++) K.Ow.at<float>(i, 0) = Ow[(size_t)i];
+    K.fx = cam[0]; K.fy = cam[1]; K.cx = cam[2]; K.cy = cam[3]; K.mbf = cam[4];
+    K.mfLogScaleFactor = lsf[0];
+    K.mnScaleLevels = (int)K.mvScaleFactors.size();
+    for (size_t k = 0; k < nodes.size(); k++)
+        for (int j = start[k]; j < start[k + 1]; j++) K.mFeatVec[nodes[k]].push_back((unsigned)fidx[(size_t)j]);
+    K.matches.assign(n, nullptr);
+}
+
+// map points of a keyframe's slots: IN per keypoint -1 none, 0 a good point, 1 a bad point;
+// point i of `pts` sits in slot i (mnId = slot)
+static void attach_points(mock::KeyFrame& K, const std::vector<int32_t>& kind, std::vector<mock::MapPoint>& pts) {
+    pts.assign(kind.size(), mock::MapPoint());
+    for (size_t i = 0; i < kind.size(); i++) {
+        pts[i].mnId = i;
+        pts[i].bad = kind[i] == 1;
+        if (kind[i] >= 0) K.matches[i] = &pts[i];
+    }
+}
+
+// IN: the keyframe, then per map point xyz, normal, mfMinDistance, mfMaxDistance, descriptor,
+// bad flag, observations outside this keyframe, the keyframe slot it already occupies (-1: none),
+// then vpMapPoints (point index or -1 = NULL) and th.  Points in a slot are the keyframe's.
+// OUT: nFused, per keyframe slot the mnId of its point (-1), per point bad / replaced-by mnId (-1) /
+// its slot in the keyframe (-1) / Observations().
+static void run_fuse(FILE* in, FILE* out) {
+    mock::KeyFrame K;
+    load_kf(in, K);
+    const auto xyz = rd<float>(in), nrm = rd<float>(in), mind = rd<float>(in), maxd = rd<float>(in);
+    const auto desc = rd<uint8_t>(in);
+    const auto bad = rd<uint8_t>(in);
+    const auto extra = rd<int32_t>(in), slot = rd<int32_t>(in), vec = rd<int32_t>(in);
+    const auto th = rd<float>(in);
+    const size_t np = bad.size();
+    std::vector<mock::MapPoint> pts(np);
+    for (size_t i = 0; i < np; i++) {
+        mock::MapPoint& P = pts[i];
+        P.mnId = i;
+        P.X.create(3, 1, orbslam2_amd::kCV_32F);
+        P.normal.create(3, 1, orbslam2_amd::kCV_32F);
+        for (int k = 0; k < 3; k++) {
+            P.X.at<float>(k, 0) = xyz[3 * i + (size_t)k];
+            P.normal.at<float>(k, 0) = nrm[3 * i + (size_t)k];
+        }
+        P.mfMinDistance = mind[i];
+        P.mfMaxDistance = maxd[i];
+        P.desc.create(1, 32, orbslam2_amd::kCV_8U);
+        std::copy(desc.begin() + 32 * (long)i, desc.begin() + 32 * (long)(i + 1), P.desc.data);
+        P.bad = bad[i] != 0;
+        P.extraObs = extra[i];
+        if (slot[i] >= 0) {
+            P.obs[&K] = (size_t)slot[i];
+            K.matches[(size_t)slot[i]] = &P;
+        }
+    }
+    std::vector<mock::MapPoint*> vp;
+    for (const int32_t v : vec) vp.push_back(v < 0 ? nullptr : &pts[(size_t)v]);
+    orbslam2_amd::Matcher matcher(0.6f, true);
+    const int32_t n = matcher.Fuse(&K, vp, th[0]);
+    wr(out, &n, 1);
+    std::vector<int32_t> slots;
+    for (auto* p : K.matches) slots.push_back(p ? (int32_t)p->mnId : -1);
+    wr(out, slots);
+    std::vector<int32_t> st;
+    for (auto& P : pts) {
+        st.push_back(P.bad ? 1 : 0);
+        st.push_back(P.replacedBy ? (int32_t)P.replacedBy->mnId : -1);
+        st.push_back(P.obs.count(&K) ? (int32_t)P.obs[&K] : -1);
+        st.push_back(P.Observations());
+    }
+    wr(out, st);
+}
+
+// IN: keyframe 1, keyframe 2, each followed by its slot kinds (attach_points), then F12 (9),
+// bOnlyStereo, checkOri.  OUT: nmatches, vMatchedPairs flattened.
+static void run_sft(FILE* in, FILE* out) {
+    mock::KeyFrame K1, K2;
+    std::vector<mock::MapPoint> p1, p2;
+    load_kf(in, K1);
+    attach_points(K1, rd<int32_t>(in), p1);
+    load_kf(in, K2);
+    attach_points(K2, rd<int32_t>(in), p2);
+    const auto F = rd<float>(in);
+    const auto flags = rd<int32_t>(in);
+    mock::Mat F12(3, 3, orbslam2_amd::kCV_32F);
+    for (int i = 0; i < 9; i++) F12.at<float>(i / 3, i % 3) = F[(size_t)i];
+    orbslam2_amd::Matcher matcher(0.6f, flags[1] != 0);
+    std::vector<std::pair<size_t, size_t>> pairs;
+    const int32_t n = matcher.SearchForTriangulation(&K1, &K2, F12, pairs, flags[0] != 0);
+    wr(out, &n, 1);
+    std::vector<int32_t> pv;
+    for (const auto& pr : pairs) { pv.push_back((int32_t)pr.first); pv.push_back((int32_t)pr.second); }
+    wr(out, pv);
+}
+
+// IN: the keyframe + its slot kinds, then the frame's keypoint x, y, angle, octave, descriptors and
+// mFeatVec (nodes, starts, indices), then (nnratio, checkOri).  OUT: nmatches, per frame feature
+// the keyframe slot whose point it matched (-1).
+static void run_sbbf(FILE* in, FILE* out) {
+    mock::KeyFrame K;
+    std::vector<mock::MapPoint> pk;
+    load_kf(in, K);
+    attach_points(K, rd<int32_t>(in), pk);
+    mock::Frame F;
+    load_frame(in, F);
+    const auto nodes = rd<uint32_t>(in);
+    const auto start = rd<int32_t>(in), fidx = rd<int32_t>(in);
+    for (size_t k = 0; k < nodes.size(); k++)
+        for (int j = start[k]; j < start[k + 1]; j++) F.mFeatVec[nodes[k]].push_back((unsigned)fidx[(size_t)j]);
+    const auto par = rd<float>(in);
+    orbslam2_amd::Matcher matcher(par[0], par[1] != 0);
+    std::vector<mock::MapPoint*> vm;
+    const int32_t n = matcher.SearchByBoW(&K, F, vm);
+    wr(out, &n, 1);
+    std::vector<int32_t> o;
+    for (auto* p : vm) o.push_back(p ? (int32_t)p->mnId : -1);
+    wr(out, o);
+}
+
+// IN: keyframe 1 + slot kinds, keyframe 2 + slot kinds, (nnratio, checkOri).  OUT: nmatches, per
+// keyframe-1 slot the keyframe-2 slot of vpMatches12 (-1).
+static void run_sbbk(FILE* in, FILE* out) {
+    mock::KeyFrame K1, K2;
+    std::vector<mock::MapPoint> p1, p2;
+    load_kf(in, K1);
+    attach_points(K1, rd<int32_t>(in), p1);
+    load_kf(in, K2);
+    attach_points(K2, rd<int32_t>(in), p2);
+    const auto par = rd<float>(in);
+    orbslam2_amd::Matcher matcher(par[0], par[1] != 0);
+    std::vector<mock::MapPoint*> vm;
+    const int32_t n = matcher.SearchByBoW(&K1, &K2, vm);
+    wr(out, &n, 1);
+    std::vector<int32_t> o;
+    for (auto* p : vm) o.push_back(p ? (int32_t)p->mnId : -1);
+    wr(out, o);
+}
+
+static bool run_mode(const std::string& mode, FILE* in, FILE* out) {
+    if (mode == "extract") run_extract(in, out);
+    else if (mode == "sfi") run_sfi(in, out);
+    else if (mode == "sbp") run_sbp(in, out);
+    else if (mode == "sbl") run_sbl(in, out);
+    else if (mode == "lba") run_lba(in, out, false);
+    else if (mode == "lbag") run_lba(in, out, true);
+    else if (mode == "pose") run_pose(in, out);
+    else if (mode == "stereo") run_stereo(in, out);
+    else if (mode == "fuse") run_fuse(in, out);
+    else if (mode == "sft") run_sft(in, out);
+    else if (mode == "sbbf") run_sbbf(in, out);
+    else if (mode == "sbbk") run_sbbk(in, out);
+    else return false;
+    return true;
+}
+
+// threads OUT REPS MODE1 IN1 [MODE2 IN2 ...]: one host thread per job, released together; each
+// runs its job REPS times (inputs re-read, so a mutated mock map starts afresh) and every result
+// must equal its first; OUT.k receives job k's first result.  Exit 4 on a differing repetition.
+static int run_threads(int argc, char** argv) {
+    const std::string outp = argv[2];
+    const int reps = std::atoi(argv[3]);
+    struct Job {
+        std::string mode, in, err;
+        std::vector<uint8_t> first;
+        int mismatches = 0;
+    };
+    std::vector<Job> jobs;
+    for (int a = 4; a + 1 < argc; a += 2) jobs.push_back(Job{argv[a], argv[a + 1], "", {}, 0});
+    std::atomic<int> ready{0};
+    std::vector<std::thread> th;
+    for (auto& J : jobs) {
+        th.emplace_back([&J, &ready, reps, n = (int)jobs.size()] {
+            ready.fetch_add(1);
+            while (ready.load() < n) std::this_thread::yield();
+            for (int r = 0; r < reps && J.err.empty(); r++) {
+                FILE* in = std::fopen(J.in.c_str(), "rb");
+                char* buf = nullptr;
+                size_t len = 0;
+                FILE* mem = open_memstream(&buf, &len);
+                try {
+                    if (!in || !mem || !run_mode(J.mode, in, mem)) J.err = "bad job " + J.mode;
+                } catch (const std::exception& e) {
+                    J.err = e.what();
+                }
+                if (in) std::fclose(in);
+                if (mem) std::fclose(mem);
+                std::vector<uint8_t> v(buf, buf + len);
+                std::free(buf);
+                if (!J.err.empty()) break;
+                if (r == 0) J.first = v;
+                else if (v != J.first) J.mismatches++;
+            }
+        });
+    }
+    for (auto& t : th) t.join();
+    int rc = 0;
+    for (size_t k = 0; k < jobs.size(); k++) {
+        const Job& J = jobs[k];
+        if (!J.err.empty()) {
+            std::fprintf(stderr, "job %zu (%s): %s\n", k, J.mode.c_str(), J.err.c_str());
+            rc = 3;
+            continue;
+        }
+        if (J.mismatches) {
+            std::fprintf(stderr, "job %zu (%s): %d repetitions differ from the first\n", k, J.mode.c_str(), J.mismatches);
+            if (!rc) rc = 4;
+        }
+        FILE* f = std::fopen((outp + "." + std::to_string(k)).c_str(), "wb");
+        if (!f) return 2;
+        if (!J.first.empty()) std::fwrite(J.first.data(), 1, J.first.size(), f);
+        std::fclose(f);
+    }
+    return rc;
+}
+
 int main(int argc, char** argv) {
+    if (argc >= 6 && std::string(argv[1]) == "threads") return run_threads(argc, argv);
     if (argc != 4) {
-        std::fprintf(stderr, "usage: %s extract|sfi|sbp|sbl|lba|lbag IN OUT\n", argv[0]);
+        std::fprintf(stderr, "usage: %s extract|sfi|sbp|sbl|lba|lbag|pose|stereo|fuse|sft|sbbf|sbbk IN OUT\n"
+                             "       %s threads OUT REPS MODE IN [MODE IN ...]\n", argv[0], argv[0]);
         return 2;
     }
     FILE* in = std::fopen(argv[2], "rb");
@@ -383,13 +778,7 @@ int main(int argc, char** argv) {
     if (!in || !out) return 2;
     const std::string mode = argv[1];
     try {
-        if (mode == "extract") run_extract(in, out);
-        else if (mode == "sfi") run_sfi(in, out);
-        else if (mode == "sbp") run_sbp(in, out);
-        else if (mode == "sbl") run_sbl(in, out);
-        else if (mode == "lba") run_lba(in, out, false);
-        else if (mode == "lbag") run_lba(in, out, true);
-        else return 2;
+        if (!run_mode(mode, in, out)) return 2;
     } catch (const std::exception& e) {
         std::fprintf(stderr, "%s\n", e.what());
         std::fclose(out);

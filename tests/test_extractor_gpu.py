@@ -82,6 +82,52 @@ def test_blurred_pyramid_on_demand_matches_oracle(amd):
         assert np.array_equal(a, b), f"level {lvl}: {np.count_nonzero(a != b)} px differ"
 
 
+@pytest.mark.parametrize("W,H,nf", [(640, 480, 1000), (1241, 376, 2000)])
+def test_batch_pyramid_level0_is_the_input(amd, W, H, nf):
+    """Level 0 of a batched extraction is the caller's frame (R/src/ORBextractor.cpp:1223 rebinds
+    mvImagePyramid[0] to the input): dword-aligned frames (640 wide) are read in place — the raw
+    level-0 device pointer is the input frame itself — and odd widths (KITTI 1241) are read from
+    the slab's copy; either way the host level 0 equals the frame and every level equals the
+    oracle's pyramid, for a middle frame of the batch."""
+    import ctypes as C
+    import torch
+    from orb_slam2_amd import _abi
+    B = 3
+    frames = _frames(W, H, 0x5EED0007, B)
+    dev = torch.device("cuda", 0)
+    ex = amd.ORBextractor(nf, 1.2, 8, 20, 7, max_w=W, max_h=H, max_batch=B)
+    cap = C.c_int()
+    _abi.check("geom", _abi.lib().orb_extractor_geometry(ex._h, W, H, None, None, None, C.byref(cap)))
+    ti = torch.from_numpy(np.stack(frames)).to(dev)
+    kps = torch.zeros((B, cap.value, 7), dtype=torch.int32, device=dev)
+    desc = torch.zeros((B, cap.value, 32), dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(B, dtype=torch.int32, device=dev)
+    ex.extract_batch_device(ti, kps, desc, cnt, torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize(dev)
+    assert ex.batch_status() == 0
+    ref = O.extract(O.params(nf), frames[1], want_pyramid=True)
+    lw, lh = ref["sizes"]
+    off = 0
+    for lvl in range(8):
+        p = C.POINTER(C.c_uint8)()
+        w, h, st = C.c_int(), C.c_int(), C.c_size_t()
+        _abi.check("orb_pyramid_level", _abi.lib().orb_pyramid_level(ex._h, 1, lvl, C.byref(p), C.byref(w), C.byref(h),
+                                                                     C.byref(st)))
+        a = np.ctypeslib.as_array(p, shape=(h.value, st.value))[:, :w.value]
+        b = ref["pyramid"][off:off + lw[lvl] * lh[lvl]].reshape(lh[lvl], lw[lvl])
+        off += lw[lvl] * lh[lvl]
+        assert np.array_equal(a, b), f"level {lvl}: {np.count_nonzero(a != b)} px differ"
+        if lvl == 0:
+            assert np.array_equal(a, frames[1])
+    dp, w, h, st = C.c_void_p(), C.c_int(), C.c_int(), C.c_size_t()
+    _abi.check("orb_pyramid_level_device", _abi.lib().orb_pyramid_level_device(ex._h, 1, 0, 0, C.byref(dp), C.byref(w),
+                                                                               C.byref(h), C.byref(st)))
+    if W % 4 == 0:
+        assert dp.value == ti.data_ptr() + W * H and st.value == W   # in place: no level-0 copy
+    else:
+        assert dp.value != ti.data_ptr() + W * H
+
+
 def test_empty_image_leaves_outputs(amd):
     ex = amd.ORBextractor(1000, 1.2, 8, 20, 7, max_w=640, max_h=480)
     sentinel = (np.zeros(3, np.uint8), np.ones((3, 32), np.uint8))
