@@ -76,6 +76,20 @@ struct Geom {
     LevelGeom lv[kMaxLevels];
 };
 
+// Level 0 as every consumer reads it.  R/src/ORBextractor.cpp:1223 rebinds mvImagePyramid[0] to the
+// input image rather than copying it; so do the kernels: frame b's level 0 is the caller's frame
+// p + b * frameStride (rows `pitch` bytes apart) whenever its rows are dword-aligned, else (odd
+// widths, the k_resize fallback) the slab's pitched level 0 that a copy kernel fills.  `bytes` =
+// the readable bytes from a frame's start (the bound of the consumers' buffer loads).  The frames
+// must stay valid and unchanged while a later call reads level 0 (orb_pyramid_level*, the stereo
+// matcher), as the reference's Mat header keeps the caller's image.
+struct L0Src {
+    const uint8_t* p;
+    long long frameStride;
+    int pitch;
+    uint32_t bytes;
+};
+
 // ------------------------------------------------------------------ host geometry
 
 static void host_tables(const orb_extractor_params& p, float* scale, float* inv_scale, float* sigma2,
@@ -201,6 +215,20 @@ static int build_geom(const orb_extractor_params& p, int w, int h, Geom* g) {
 // n e < 2^13 < 2^16, so the quotient is exact.  No table load in the chain to the window loads.
 __device__ __forceinline__ uint32_t rcp16(int d) {
     return (uint32_t)(65536.0f * __builtin_amdgcn_rcpf((float)d)) + 1u;
+}
+
+// level l of frame b: base pointer, row pitch and readable bytes (level 0 per L0Src)
+__device__ __forceinline__ const uint8_t* level_img(const Geom& g, const L0Src& z, const uint8_t* pyr, int b, int l,
+                                                   int& pitch, uint32_t& bytes) {
+    if (l == 0) {
+        pitch = z.pitch;
+        bytes = z.bytes;
+        return z.p + (size_t)b * z.frameStride;
+    }
+    const LevelGeom& L = g.lv[l];
+    pitch = L.pitch;
+    bytes = (uint32_t)(g.frameBytes - L.off);
+    return pyr + (size_t)b * g.frameBytes + L.off;
 }
 
 __device__ __forceinline__ int level_of_tile(const Geom& g, int tile) {
@@ -343,185 +371,153 @@ __global__ __launch_bounds__(256) void k_resize(Geom g, int l, uint8_t* __restri
 // LDS copy of the level below.  Neighbouring bands recompute the few rows where their ranges
 // overlap (the same arithmetic on the same source bytes, so both write identical values), and the
 // ranges of all bands cover every row of every level (checked on the host; otherwise the per-level
-// k_resize launches are used).  Level 0 is staged from the caller's frames (written into the
-// pitched slab on the way when they are not already there, replacing a separate copy kernel).
+// k_resize launches are used).  Level 0 is not copied (the reference rebinds mvImagePyramid[0] to
+// the input, :1223): level 1 is computed straight from the caller's frame (L0Src, L2-resident
+// buffer loads), so the LDS holds levels 1..7 only — the odd levels in one buffer, the even ones in
+// the other.
 // output rows per k_pyramid thread iteration (rows r, r + 4, ..: their source-row loads in flight together)
 #ifndef ORB_PYR_ROWS
 #define ORB_PYR_ROWS 2
 #endif
 constexpr int kPyrRows = ORB_PYR_ROWS;
+// LDS budget of one k_pyramid workgroup (both level buffers + the coefficient tables)
+#ifndef ORB_PYR_LDS_BUDGET_KB
+#define ORB_PYR_LDS_BUDGET_KB 32
+#endif
+constexpr int kPyrLdsBudget = ORB_PYR_LDS_BUDGET_KB * 1024;
 
 struct PyrBand {
     int s0, n;   // rows [s0, s0 + n) of a level computed by a band
 };
 
-__global__ __launch_bounds__(256) void k_pyramid(Geom g, const uint8_t* __restrict__ src, long long srcFrameStride,
-                                                 int srcRowStride, int writeL0, uint8_t* __restrict__ pyr,
+// One level of a band: output rows db of level l (D) from source rows sb of level l-1 (S), read
+// from LDS (`cur`, row pitch sp) or, for level 1, from the caller's level 0 through `rs`.
+template <bool FromGlobal>
+__device__ __forceinline__ void pyr_band_level(const LevelGeom& D, const LevelGeom& S, const PyrBand sb, const PyrBand db,
+                                               const uint2* XT, const uint2* YT, const uint8_t* cur,
+                                               __amdgpu_buffer_rsrc_t rs, int srcPitch, uint8_t* nxt, uint8_t* out,
+                                               int tid) {
+    const int sp = ((S.w + 3) >> 2) << 2, dp = ((D.w + 3) >> 2) << 2;   // LDS row pitches
+    const int G = (D.w + 3) >> 2;   // column groups
+    // thread = (column group cg, row phase rp): the group's column coefficients stay in registers
+    // while the thread walks rows rp, rp + 4, ... kPyrRows at a time (2; 3 and 4 measured the same
+    // in a same-box A/B)
+    for (int pr = tid; pr < 4 * G; pr += 256) {
+        const int rp = pr / G, cg = pr - rp * G;
+        const int dx0 = 4 * cg;
+        // the group's source bytes x0[j], x1[j] lie in an 8-byte window starting at x0[0]
+        // (host-checked span): per row three aligned dwords, two alignbytes re-base the window at
+        // x0[0], one v_perm per column places x0[j] and x1[j] in the two u16 halves, and one
+        // v_dot2_u32_u16 against (a0[j], a1[j]) gives the column's horizontal sum a0 x0 + a1 x1
+        // (<= 255 * 2048, exact)
+        uint32_t sel[4], wt[4];
+        const int xb = (int)(XT[min(dx0, D.w - 1)].x & 0xFFFF);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint2 c = XT[min(dx0 + j, D.w - 1)];
+            sel[j] = (uint32_t)((int)(c.x & 0xFFFF) - xb) | 0x0c00u | ((uint32_t)((int)(c.x >> 16) - xb) << 16) | 0x0c000000u;
+            wt[j] = c.y;   // a0 | a1 << 16
+        }
+        typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+        const int dw = xb >> 2;
+        const uint32_t sh = (uint32_t)(xb & 3);
+        const int valid = D.w - dx0;   // pitch padding stays 0
+        const uint32_t keep = valid < 4 ? (1u << (8 * valid)) - 1u : 0xFFFFFFFFu;
+        for (int r = rp; r < db.n; r += 4 * kPyrRows) {
+            int rr[kPyrRows];
+            uint2 cy[kPyrRows];
+#pragma unroll
+            for (int u = 0; u < kPyrRows; u++) {
+                rr[u] = min(r + 4 * u, db.n - 1);
+                cy[u] = YT[rr[u]];
+            }
+            uint32_t hs[kPyrRows][2][4];   // [row u][source row 0/1][column]: horizontal sums
+            uint32_t dd[kPyrRows][2][3];
+#pragma unroll
+            for (int u = 0; u < kPyrRows; u++) {
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const uint32_t sy = h ? (cy[u].x >> 16) : (cy[u].x & 0xFFFF);
+                    if (FromGlobal) {   // dword-aligned rows: the three dwords of the window (a dword
+                                        // past the frame reads 0 and is never selected)
+                        const int off = (int)__umul24(sy, (uint32_t)srcPitch) + 4 * dw;
+                        dd[u][h][0] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
+                        dd[u][h][1] = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 4, 0, 0);
+                        dd[u][h][2] = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 8, 0, 0);
+                    } else {
+                        const uint32_t* R = reinterpret_cast<const uint32_t*>(cur + __umul24(sy - (uint32_t)sb.s0, (uint32_t)sp)) + dw;
+                        dd[u][h][0] = R[0];
+                        dd[u][h][1] = R[1];
+                        dd[u][h][2] = R[2];
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kPyrRows; u++) {
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const uint32_t w0 = __builtin_amdgcn_alignbyte(dd[u][h][1], dd[u][h][0], sh);
+                    const uint32_t w1 = __builtin_amdgcn_alignbyte(dd[u][h][2], dd[u][h][1], sh);
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        hs[u][h][j] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(w1, w0, sel[j])),
+                                                             __builtin_bit_cast(u16x2, wt[j]), 0u, false);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kPyrRows; u++) {
+                const uint32_t b0 = cy[u].y & 0xFFFF, b1 = cy[u].y >> 16;
+                uint32_t packed = 0u;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    // 19-bit sums x 11-bit weights fit 24 x 24 -> 32 bits: v_mad_u32_u24, not the
+                    // quarter-rate v_mul_lo_u32
+                    const uint32_t v = min((__umul24(hs[u][0][j], b0) + __umul24(hs[u][1][j], b1) + (1u << 21)) >> 22, 255u);
+                    packed |= v << (8 * j);
+                }
+                if (u > 0 && r + 4 * u >= db.n) break;
+                const uint32_t pv = packed & keep;
+                *reinterpret_cast<uint32_t*>(nxt + rr[u] * dp + dx0) = pv;
+                *reinterpret_cast<uint32_t*>(out + (size_t)(db.s0 + rr[u]) * D.pitch + dx0) = pv;
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_pyramid(Geom g, L0Src z, uint8_t* __restrict__ pyr,
                                                  const uint2* __restrict__ rztab, const PyrBand* __restrict__ bands,
                                                  int nBands, int bufABytes, int bufBBytes, int* __restrict__ status) {
     extern __shared__ __attribute__((aligned(16))) uint32_t pyr_sm[];
     const int tid = threadIdx.x;
     int k, b;
     xcd_block_2d(k, b);
-    uint8_t* bufA = reinterpret_cast<uint8_t*>(pyr_sm);
-    uint8_t* bufB = bufA + bufABytes;   // even levels in A, odd levels in B
-    uint2* tabL = reinterpret_cast<uint2*>(bufB + bufBBytes);   // this level's column then row coefficients
+    uint8_t* bufOdd = reinterpret_cast<uint8_t*>(pyr_sm);
+    uint8_t* bufEven = bufOdd + bufBBytes;   // odd levels (1, 3, 5, 7) in B, even (2, 4, 6) in A
+    uint2* tabL = reinterpret_cast<uint2*>(bufEven + bufABytes);   // this level's column then row coefficients
     uint8_t* slab = pyr + (size_t)b * g.frameBytes;
     if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) *status = 0;   // this call's status word
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(z.p + (size_t)b * z.frameStride, z.bytes);
 #ifdef ORB_TIMING
     long long tl[9];
-    tl[0] = clock64();
+    tl[0] = tl[1] = clock64();
 #endif
-    // ---- level 0 rows of this band -> LDS (row pitch rounded to a dword), and into the slab
-    {
-        const LevelGeom& L = g.lv[0];
-        const PyrBand bd = bands[k];
-        const int wq = (L.w + 3) >> 2;   // dwords per LDS row
-        const uint8_t* s = src + (size_t)b * srcFrameStride;
-        uint32_t* dst32 = reinterpret_cast<uint32_t*>(bufA);
-        if ((L.w & 15) == 0 && ((srcRowStride | (int)((uintptr_t)s & 15)) & 15) == 0) {
-            // 16-byte rows: eight uint4 loads in flight per thread
-            const int w16 = L.w >> 4, items = bd.n * w16;
-            for (int t0 = 0; t0 < items; t0 += 256 * 8) {
-                uint4 v[8];
-#pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    const int t = min(t0 + u * 256 + tid, items - 1);
-                    const int r = t / w16, q = t - r * w16;
-                    v[u] = *reinterpret_cast<const uint4*>(s + (size_t)(bd.s0 + r) * srcRowStride + 16 * q);
-                }
-#pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    const int t = t0 + u * 256 + tid;
-                    if (t < items) {
-                        const int r = t / w16, q = t - r * w16;
-                        *reinterpret_cast<uint4*>(bufA + r * (wq * 4) + 16 * q) = v[u];
-                        if (writeL0) *reinterpret_cast<uint4*>(slab + L.off + (size_t)(bd.s0 + r) * L.pitch + 16 * q) = v[u];
-                    }
-                }
-            }
-        } else {
-        const int items = bd.n * wq;
-        for (int t0 = 0; t0 < items; t0 += 256 * 4) {
-            uint32_t v[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                // unconditional: item clamped into the band (all loads in flight together)
-                const int t = min(t0 + u * 256 + tid, items - 1);
-                const int r = t / wq, q = t - r * wq;
-                const uint8_t* row = s + (size_t)(bd.s0 + r) * srcRowStride;
-                const int x = 4 * q;
-                if (x + 4 <= L.w && ((srcRowStride | (int)(uintptr_t)s) & 3) == 0) {
-                    v[u] = *reinterpret_cast<const uint32_t*>(row + x);
-                } else {
-                    uint32_t w = 0;
-                    for (int j = 0; j < 4; j++)
-                        if (x + j < L.w) w |= (uint32_t)row[x + j] << (8 * j);
-                    v[u] = w;
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int t = t0 + u * 256 + tid;
-                if (t < items) {
-                    dst32[t] = v[u];
-                    if (writeL0) {
-                        const int r = t / wq, q = t - r * wq;
-                        *reinterpret_cast<uint32_t*>(slab + L.off + (size_t)(bd.s0 + r) * L.pitch + 4 * q) = v[u];
-                    }
-                }
-            }
-        }
-        }
-    }
-    __syncthreads();
-#ifdef ORB_TIMING
-    tl[1] = clock64();
-#endif
-    // ---- levels 1 .. nlevels-1: task = (row, group of 4 output columns), columns fastest (the
-    //      dword stores of a wave are contiguous); the column / row coefficient tables are L1-hot
-    uint8_t* cur = bufA;
-    uint8_t* nxt = bufB;
     for (int l = 1; l < g.nlevels; l++) {
         const LevelGeom& D = g.lv[l];
         const LevelGeom& S = g.lv[l - 1];
         const PyrBand sb = bands[(l - 1) * nBands + k], db = bands[l * nBands + k];
-        const int sp = ((S.w + 3) >> 2) << 2, dp = ((D.w + 3) >> 2) << 2;   // LDS row pitches
-        const int G = (D.w + 3) >> 2;   // column groups
-        uint8_t* out = slab + D.off;
         // the level's column coefficients and the band's row coefficients -> LDS
         uint2* XT = tabL;
         uint2* YT = tabL + D.w;
         for (int i = tid; i < D.w + db.n; i += 256)
             tabL[i] = i < D.w ? rztab[D.rzX + i] : rztab[D.rzY + db.s0 + (i - D.w)];
         __syncthreads();
-        // thread = (column group cg, row phase rp): the group's column coefficients stay in
-        // registers while the thread walks rows rp, rp + 4, ... kPyrRows at a time (2; 3 and 4 measured
-        // the same in a same-box A/B)
-        for (int pr = tid; pr < 4 * G; pr += 256) {
-            const int rp = pr / G, cg = pr - rp * G;
-            const int dx0 = 4 * cg;
-            // the group's source bytes x0[j], x1[j] lie in an 8-byte window starting at x0[0]
-            // (host-checked span): per row three aligned dwords, two alignbytes re-base the window
-            // at x0[0], one v_perm per column places x0[j] and x1[j] in the two u16 halves, and one
-            // v_dot2_u32_u16 against (a0[j], a1[j]) gives the column's horizontal sum
-            // a0 x0 + a1 x1 (<= 255 * 2048, exact)
-            uint32_t sel[4], wt[4];
-            const int xb = (int)(XT[min(dx0, D.w - 1)].x & 0xFFFF);
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint2 c = XT[min(dx0 + j, D.w - 1)];
-                sel[j] = (uint32_t)((int)(c.x & 0xFFFF) - xb) | 0x0c00u | ((uint32_t)((int)(c.x >> 16) - xb) << 16) | 0x0c000000u;
-                wt[j] = c.y;   // a0 | a1 << 16
-            }
-            typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-            const int dw = xb >> 2;
-            const uint32_t sh = (uint32_t)(xb & 3);
-            const int valid = D.w - dx0;   // pitch padding stays 0
-            const uint32_t keep = valid < 4 ? (1u << (8 * valid)) - 1u : 0xFFFFFFFFu;
-            for (int r = rp; r < db.n; r += 4 * kPyrRows) {
-                int rr[kPyrRows];
-                uint2 cy[kPyrRows];
-#pragma unroll
-                for (int u = 0; u < kPyrRows; u++) {
-                    rr[u] = min(r + 4 * u, db.n - 1);
-                    cy[u] = YT[rr[u]];
-                }
-                uint32_t hs[kPyrRows][2][4];   // [row u][source row 0/1][column]: horizontal sums
-#pragma unroll
-                for (int u = 0; u < kPyrRows; u++) {
-#pragma unroll
-                    for (int h = 0; h < 2; h++) {
-                        const uint32_t sy = h ? (cy[u].x >> 16) : (cy[u].x & 0xFFFF);
-                        const uint32_t* R = reinterpret_cast<const uint32_t*>(cur + __umul24(sy - (uint32_t)sb.s0, (uint32_t)sp)) + dw;
-                        const uint32_t d0 = R[0], d1 = R[1], d2 = R[2];
-                        const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh), w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-#pragma unroll
-                        for (int j = 0; j < 4; j++)
-                            hs[u][h][j] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(w1, w0, sel[j])),
-                                                                 __builtin_bit_cast(u16x2, wt[j]), 0u, false);
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < kPyrRows; u++) {
-                    const uint32_t b0 = cy[u].y & 0xFFFF, b1 = cy[u].y >> 16;
-                    uint32_t packed = 0u;
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        // 19-bit sums x 11-bit weights fit 24 x 24 -> 32 bits: v_mad_u32_u24, not
-                        // the quarter-rate v_mul_lo_u32
-                        const uint32_t v = min((__umul24(hs[u][0][j], b0) + __umul24(hs[u][1][j], b1) + (1u << 21)) >> 22, 255u);
-                        packed |= v << (8 * j);
-                    }
-                    if (u > 0 && r + 4 * u >= db.n) break;
-                    const uint32_t pv = packed & keep;
-                    *reinterpret_cast<uint32_t*>(nxt + rr[u] * dp + dx0) = pv;
-                    *reinterpret_cast<uint32_t*>(out + (size_t)(db.s0 + rr[u]) * D.pitch + dx0) = pv;
-                }
-            }
-        }
+        uint8_t* nxt = (l & 1) ? bufOdd : bufEven;
+        const uint8_t* cur = (l & 1) ? bufEven : bufOdd;
+        if (l == 1)
+            pyr_band_level<true>(D, S, sb, db, XT, YT, nullptr, rs, z.pitch, nxt, slab + D.off, tid);
+        else
+            pyr_band_level<false>(D, S, sb, db, XT, YT, cur, rs, 0, nxt, slab + D.off, tid);
         __syncthreads();   // (also: the coefficient tables are rewritten by the next level)
-        uint8_t* t = cur; cur = nxt; nxt = t;
 #ifdef ORB_TIMING
         tl[l + 1] = clock64();
 #endif
@@ -595,7 +591,7 @@ __host__ __device__ inline int fc_wave_bytes(int maxW, int maxH) {
 // the window / score-map row strides are constants and every ring / neighbour load takes an
 // immediate offset from one address; MW = 0: strides at run time (any cell width).
 template <int MW>
-__global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __restrict__ pyr,
+__global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __restrict__ pyr, L0Src z,
                                                    uint32_t* __restrict__ slots, int* __restrict__ cellCount,
                                                    int* __restrict__ status, int maxWarg, int maxH) {
     const int maxW = MW > 0 ? MW : maxWarg;
@@ -647,7 +643,9 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
     uint8_t* sc = base + patchBytes;
     uint16_t* list = reinterpret_cast<uint16_t*>(base + listOff);
     uint8_t* kp = base;   // the window is dead once every survivor is scored (phase 3)
-    const uint8_t* img = pyr + (size_t)b * g.frameBytes + L.off;
+    int pitch;
+    uint32_t imgBytes;
+    const uint8_t* img = level_img(g, z, pyr, b, l, pitch, imgBytes);
     const int rx0 = iniX + 3, ry0 = iniY + 3;
     int n = 0;
     if (act) {
@@ -662,11 +660,10 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
         const uint32_t mW = rcp16(NW1);
         const int r0 = (int)(((uint32_t)lane * mW) >> 16), k = lane - r0 * NW1, R = (int)((64u * mW) >> 16);
         const int rows = rh + 6;
-        const int pitch = L.pitch;
-        // buffer loads over the rest of the frame slab: a row past the window (or past the slab:
-        // reads 0) is loaded but never stored, so no clamp and no exec mask; the row step is a
-        // scalar offset, the lane's part one 24-bit multiply-add
-        const __amdgpu_buffer_rsrc_t rs = buf_rsrc(img, (uint32_t)(g.frameBytes - L.off));
+        // buffer loads over the rest of the level image: a row past the window (or past the
+        // image: reads 0) is loaded but never stored, so no clamp and no exec mask; the row step
+        // is a scalar offset, the lane's part one 24-bit multiply-add
+        const __amdgpu_buffer_rsrc_t rs = buf_rsrc(img, imgBytes);
         const uint32_t laneOff = __umul24((uint32_t)(ry0 - 3 + r0), (uint32_t)pitch) + (uint32_t)(ga + 4 * k);
         uint32_t* const sink = reinterpret_cast<uint32_t*>(list) + lane;   // the list is written only later
         for (int rb = 0; rb < rows; rb += 8 * R) {
@@ -1356,8 +1353,8 @@ __global__ __launch_bounds__(OT_T) void k_octree(Geom g, const uint32_t* __restr
 constexpr int kHalo = 3;   // blur radius
 constexpr int kLdsW = kTileW + 2 * kHalo, kLdsH = kTileH + 2 * kHalo;
 constexpr int kRowSumW = kTileW + 4;
-__global__ __launch_bounds__(256) void k_blur(Geom g, const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blurred,
-                                              int k0, int k1, int k2, int k3) {
+__global__ __launch_bounds__(256) void k_blur(Geom g, const uint8_t* __restrict__ pyr, L0Src z,
+                                              uint8_t* __restrict__ blurred, int k0, int k1, int k2, int k3) {
     __shared__ __attribute__((aligned(16))) uint32_t tile32[kLdsH][(kLdsW + 2) / 4];
     __shared__ __attribute__((aligned(16))) int rowsum[kLdsH][kRowSumW];
     const int b = blockIdx.y;
@@ -1365,7 +1362,9 @@ __global__ __launch_bounds__(256) void k_blur(Geom g, const uint8_t* __restrict_
     const LevelGeom& L = g.lv[l];
     const int t = blockIdx.x - L.tileBase;
     const int tx0 = (t % L.tilesX) * kTileW, ty0 = (t / L.tilesX) * kTileH;
-    const uint8_t* img = pyr + (size_t)b * g.frameBytes + L.off;
+    int ipitch;
+    uint32_t ibytes;
+    const uint8_t* img = level_img(g, z, pyr, b, l, ipitch, ibytes);
     uint8_t* out = blurred + (size_t)b * g.frameBytes + L.off;
     const int tid = threadIdx.x;
     constexpr int kWords = (kLdsW + 2) / 4;   // 18 words = 72 bytes per row, from column tx0 - 4
@@ -1375,10 +1374,10 @@ __global__ __launch_bounds__(256) void k_blur(Geom g, const uint8_t* __restrict_
         const int r = i / kWords, wd = i % kWords;
         uint32_t v = 0;
         if (interior) {
-            v = *reinterpret_cast<const uint32_t*>(img + (size_t)(ty0 - kHalo + r) * L.pitch + tx0 - 4 + 4 * wd);
+            v = *reinterpret_cast<const uint32_t*>(img + (size_t)(ty0 - kHalo + r) * ipitch + tx0 - 4 + 4 * wd);
         } else {
             const int y = reflect101(ty0 - kHalo + r, L.h);
-            const uint8_t* row = img + (size_t)y * L.pitch;
+            const uint8_t* row = img + (size_t)y * ipitch;
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 const int x = reflect101(tx0 - 4 + 4 * wd + k, L.w);
@@ -1547,7 +1546,7 @@ __constant__ uint16_t c_htask[192] = {
 };
 constexpr int kOdWaveBytes = kOdRows * kOdPW + kOdRows * kOdRsW * 2;
 
-__global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __restrict__ pyr,
+__global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __restrict__ pyr, L0Src z,
                                                      const uint32_t* __restrict__ outKeys,
                                                      const int* __restrict__ levelCount, orb_keypoint* __restrict__ kps,
                                                      uint8_t* __restrict__ desc, int cap, int32_t* __restrict__ counts,
@@ -1587,7 +1586,9 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
     if (outIdx >= cap) return;
     const uint32_t key = outKeys[(size_t)b * g.outPerFrame + q];
     const int x = kx_of(key) + kMinBorder, y = ky_of(key) + kMinBorder, resp = kr_of(key);
-    const uint8_t* img = pyr + (size_t)b * g.frameBytes + L.off;
+    int pitch;
+    uint32_t imgBytes;
+    const uint8_t* img = level_img(g, z, pyr, b, l, pitch, imgBytes);
     uint32_t* P32 = reinterpret_cast<uint32_t*>(od_sm[wid]);
     uint16_t* RS = reinterpret_cast<uint16_t*>(od_sm[wid] + kOdRows * kOdPW);
     TSTAMP(t_od0);
@@ -1609,9 +1610,8 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
         // realigned dword stored (lanes with no patch dword write into the row-sum area, which
         // step 3a overwrites)
         const int gx0 = x - 24, sh = gx0 & 3, ga = gx0 - sh;
-        const int pitch = L.pitch;
-        const long long winOff = (long long)L.off + (long long)(y - 21) * pitch + ga;
-        const __amdgpu_buffer_rsrc_t rs = buf_rsrc(img + (winOff - L.off), (uint32_t)(g.frameBytes - winOff));
+        const uint32_t winOff = (uint32_t)(y - 21) * (uint32_t)pitch + (uint32_t)ga;
+        const __amdgpu_buffer_rsrc_t rs = buf_rsrc(img + winOff, imgBytes - winOff);
         const int r0 = lane / 13, k = lane - 13 * r0;
         const uint32_t laneOff = __umul24((uint32_t)r0, (uint32_t)pitch) + 4u * (uint32_t)k;
         uint32_t* const sink = reinterpret_cast<uint32_t*>(RS) + lane;
@@ -1627,7 +1627,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
         uint8_t* P8w = od_sm[wid];
         for (int t = lane; t < kOdRows * kOdPW; t += 64) {
             const int r = t / kOdPW, cc = t % kOdPW;
-            P8w[t] = img[(size_t)reflect101(y - 21 + r, L.h) * L.pitch + reflect101(x - 24 + cc, L.w)];
+            P8w[t] = img[(size_t)reflect101(y - 21 + r, L.h) * pitch + reflect101(x - 24 + cc, L.w)];
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -1796,7 +1796,8 @@ struct StereoTabs {
 // floats = exact integer sums) at 11 offsets on the keypoint's level, parabola fit and the
 // disparity gate.  Pair p's left / right data: kL + p*kStride etc.; pyramids pyrL + p*pyStride.
 __global__ __launch_bounds__(256) void k_stereo_match(Geom g, StereoTabs tb, const uint8_t* __restrict__ pyrL,
-                                                      const uint8_t* __restrict__ pyrR, size_t pyStride,
+                                                      const uint8_t* __restrict__ pyrR, size_t pyStride, L0Src zL,
+                                                      L0Src zR,
                                                       const orb_keypoint* __restrict__ kL, const uint8_t* __restrict__ dL,
                                                       const int32_t* __restrict__ nLs, const orb_keypoint* __restrict__ kR,
                                                       const uint8_t* __restrict__ dR, const int32_t* __restrict__ nRs,
@@ -1864,15 +1865,17 @@ __global__ __launch_bounds__(256) void k_stereo_match(Geom g, StereoTabs tb, con
         const bool ok = cr >= 0 && cr + 11 < Lg.w && cr - 10 >= 0 && cx - 5 >= 0 && cx + 5 < Lg.w && cy - 5 >= 0 &&
                         cy + 5 < Lg.h;
         if (ok) {
-            const uint8_t* IL = pyrL + (size_t)p * pyStride + Lg.off;
-            const uint8_t* IR = pyrR + (size_t)p * pyStride + Lg.off;
-            const int P = Lg.pitch;
+            // pair p's pyramids: pyrL / pyrR + p * pyStride (level 0 per zL / zR, pair p = frame p)
+            int P, P2;
+            uint32_t nb;
+            const uint8_t* IL = level_img(g, zL, pyrL + (size_t)p * pyStride - (size_t)p * g.frameBytes, p, levelL, P, nb);
+            const uint8_t* IR = level_img(g, zR, pyrR + (size_t)p * pyStride - (size_t)p * g.frameBytes, p, levelL, P2, nb);
             const int cL = IL[(size_t)cy * P + cx];
             for (int c = lane; c < 121; c += 64) {
                 const int inc = c / 11 - 5, dy = c % 11 - 5;
-                const int cR = IR[(size_t)cy * P + cr + inc];
+                const int cR = IR[(size_t)cy * P2 + cr + inc];
                 const uint8_t* rl = IL + (size_t)(cy + dy) * P + cx - 5;
-                const uint8_t* rr = IR + (size_t)(cy + dy) * P + cr + inc - 5;
+                const uint8_t* rr = IR + (size_t)(cy + dy) * P2 + cr + inc - 5;
                 int acc = 0;
 #pragma unroll
                 for (int dx = 0; dx < 11; dx++) acc += abs(((int)rl[dx] - cL) - ((int)rr[dx] - cR));
@@ -2008,6 +2011,9 @@ struct orb_extractor {
     size_t h_st_bytes = 0;
     bool blurValid = false;          // d_blur holds the blurred pyramid of the last extraction
     hipStream_t lastStream = nullptr;
+    L0Src l0{nullptr, 0, 0, 0};     // level 0 of the last extraction (the caller's frames or the slab)
+    // ORB_L0_COPY=1: copy level 0 into the slab even when it could be read in place (A/B only)
+    bool forceL0Copy = [] { const char* e = std::getenv("ORB_L0_COPY"); return e && e[0] == '1'; }();
     size_t capFrames = 0, capFrameBytes = 0, capSlots = 0, capOut = 0, capCells = 0;
     uint8_t *d_pyr = nullptr, *d_blur = nullptr;
     uint32_t *d_slots = nullptr, *d_keyA = nullptr, *d_keyB = nullptr, *d_outKeys = nullptr;
@@ -2078,8 +2084,9 @@ static int ensure_geom(orb_extractor* ex, int w, int h) {
     ex->d_rztab = nullptr;
     if (hipMalloc((void**)&ex->d_rztab, std::max<size_t>(tab.size(), 1) * sizeof(uint2)) != hipSuccess) return ORB_ENOMEM;
     ORB_HIP_TRY(hipMemcpy(ex->d_rztab, tab.data(), tab.size() * sizeof(uint2), hipMemcpyHostToDevice));
-    // k_pyramid bands: the fewest bands whose two LDS level buffers fit 52 KB (three workgroups
-    // per CU), with every row of every level covered; none -> the per-level k_resize launches
+    // k_pyramid bands: the fewest bands whose two LDS level buffers (levels 1..7; level 0 is read
+    // from the caller's frame) fit the budget, with every row of every level covered; none -> the
+    // per-level k_resize launches
     if (ex->d_bands) (void)hipFree(ex->d_bands);
     ex->d_bands = nullptr;
     ex->nBands = 0;
@@ -2100,9 +2107,9 @@ static int ensure_geom(orb_extractor* ex, int w, int h) {
                 }
             }
         }
-        // (ORB_PYR_LDS_KB: diagnostic override of the 52 KB budget)
+        // (ORB_PYR_LDS_KB: diagnostic override of the budget)
         const char* ev = std::getenv("ORB_PYR_LDS_KB");
-        const int budget = (ev && std::atoi(ev) >= 8 && std::atoi(ev) <= 160) ? std::atoi(ev) * 1024 : 52 * 1024;
+        const int budget = (ev && std::atoi(ev) >= 8 && std::atoi(ev) <= 160) ? std::atoi(ev) * 1024 : kPyrLdsBudget;
         for (int K = 8; spanOk && K <= std::min(64, Hl) && bestK == 0; K++) {
             std::vector<PyrBand> bt((size_t)nl * K);
             for (int k = 0; k < K; k++) {
@@ -2125,6 +2132,7 @@ static int ensure_geom(orb_extractor* ex, int w, int h) {
                     if (p.n <= 0 || p.s0 > end) ok = false;
                     end = std::max(end, p.s0 + p.n);
                     const int bytes = p.n * (((g.lv[l].w + 3) >> 2) << 2);
+                    if (l == 0) continue;   // level 0: the caller's frame, not staged
                     if (l % 2 == 0) bufA = std::max(bufA, bytes); else bufB = std::max(bufB, bytes);
                 }
                 if (end != g.lv[l].h || bt[(size_t)l * K].s0 != 0) ok = false;
@@ -2218,12 +2226,31 @@ static hipEvent_t ev_get(orb_extractor* ex) {
     return e;
 }
 
-// Enqueues the full pipeline for B frames already resident in d_pyr level 0.
-// Level 0 of frame b is read from src + b * srcFrameStride (rows srcRowStride bytes apart); when it
-// is not the slab itself (writeL0) it is also written into the slab's pitched level 0.
+// Enqueues the full pipeline for B frames.  Level 0 of frame b is src + b * srcFrameStride (dense
+// rows srcRowStride bytes apart); `inSlab` = it already is the slab's pitched level 0 (orb_extract's
+// upload).  Dword-aligned frames are read in place by every consumer (L0Src, no copy); other frames
+// (odd widths) and the per-level k_resize fallback are first copied into the slab.  The level-0
+// source is kept in ex->l0 for the later readers (orb_pyramid_level*, the stereo matchers).
 static int run_pipeline(orb_extractor* ex, int B, const uint8_t* src, long long srcFrameStride, int srcRowStride,
-                        int writeL0, orb_keypoint* d_kps, uint8_t* d_desc, int cap, int32_t* d_counts, hipStream_t st) {
+                        int inSlab, orb_keypoint* d_kps, uint8_t* d_desc, int cap, int32_t* d_counts, hipStream_t st) {
     const Geom& g = ex->g;
+    const LevelGeom& L0 = g.lv[0];
+    const bool inPlace = inSlab || (ex->d_bands && (srcRowStride & 3) == 0 && (srcFrameStride & 3) == 0 &&
+                                    ((uintptr_t)src & 3) == 0 && !ex->forceL0Copy);
+    const bool copyL0 = !inPlace;
+    L0Src z;
+    if (inPlace && !inSlab) {
+        z.p = src;
+        z.frameStride = srcFrameStride;
+        z.pitch = srcRowStride;
+        z.bytes = (uint32_t)((size_t)(L0.h - 1) * srcRowStride + L0.w);
+    } else {
+        z.p = ex->d_pyr + L0.off;
+        z.frameStride = g.frameBytes;
+        z.pitch = L0.pitch;
+        z.bytes = (uint32_t)(g.frameBytes - L0.off);
+    }
+    ex->l0 = z;
     std::array<hipEvent_t, kStages + 1> ev{};
     const int prof = ex->profile;
     if (prof) {
@@ -2237,21 +2264,20 @@ static int run_pipeline(orb_extractor* ex, int B, const uint8_t* src, long long 
         if (prof && ev[i]) (void)hipEventRecord(ev[i], st);
     };
     mark(0);
+    if (copyL0) {   // odd widths / the fallback: level 0 into the slab first
+        const int w = L0.w, h = L0.h;
+        const int vec16 = (w % 16 == 0) && (srcRowStride == w) && (srcFrameStride % 16 == 0) && ((uintptr_t)src % 16 == 0);
+        const int items = vec16 ? (w / 16) * h : ((w + 3) / 4) * h;
+        hipLaunchKernelGGL(k_load_frames, dim3((items + 255) / 256, B), dim3(256), 0, st, g, src, (size_t)srcFrameStride,
+                           ex->d_pyr, vec16);
+    }
     if (ex->d_bands) {
-        // whole pyramid (and the level-0 copy) in one launch; it also clears the status word
+        // levels 1..7 in one launch; it also clears the status word
         hipLaunchKernelGGL(k_pyramid, dim3(ex->nBands, B), dim3(256), (size_t)(ex->pyrBufA + ex->pyrBufB + ex->pyrTab),
-                           st, g, src, srcFrameStride, srcRowStride, writeL0, ex->d_pyr, ex->d_rztab, ex->d_bands,
-                           ex->nBands, ex->pyrBufA, ex->pyrBufB, ex->d_status);
+                           st, g, z, ex->d_pyr, ex->d_rztab, ex->d_bands, ex->nBands, ex->pyrBufA, ex->pyrBufB,
+                           ex->d_status);
     } else {
         ORB_HIP_TRY(hipMemsetAsync(ex->d_status, 0, 4, st));
-        if (writeL0) {
-            const int w = g.lv[0].w, h = g.lv[0].h;
-            const int vec16 = (w % 16 == 0) && (srcRowStride == w) && (srcFrameStride % 16 == 0) &&
-                              ((uintptr_t)src % 16 == 0);
-            const int items = vec16 ? (w / 16) * h : ((w + 3) / 4) * h;
-            hipLaunchKernelGGL(k_load_frames, dim3((items + 255) / 256, B), dim3(256), 0, st, g, src,
-                               (size_t)srcFrameStride, ex->d_pyr, vec16);
-        }
         for (int l = 1; l < g.nlevels; l++) {
             const LevelGeom& L = g.lv[l];
             // source window bound of one 256 x 16 block: ceil(256 * rsx) + 2 columns (+3 for dword
@@ -2273,19 +2299,19 @@ static int run_pipeline(orb_extractor* ex, int B, const uint8_t* src, long long 
         const size_t lds = 4 * (size_t)fc_wave_bytes(mw, g.maxCellH);
         const dim3 grid((g.cellsPerFrame + 3) / 4, B);
         if (mw == 32)
-            hipLaunchKernelGGL(k_fast_cell<32>, grid, dim3(256), lds, st, g, ex->d_pyr, ex->d_slots, ex->d_cellCount,
+            hipLaunchKernelGGL(k_fast_cell<32>, grid, dim3(256), lds, st, g, ex->d_pyr, z, ex->d_slots, ex->d_cellCount,
                                ex->d_status, mw, g.maxCellH);
         else if (mw == 36)
-            hipLaunchKernelGGL(k_fast_cell<36>, grid, dim3(256), lds, st, g, ex->d_pyr, ex->d_slots, ex->d_cellCount,
+            hipLaunchKernelGGL(k_fast_cell<36>, grid, dim3(256), lds, st, g, ex->d_pyr, z, ex->d_slots, ex->d_cellCount,
                                ex->d_status, mw, g.maxCellH);
         else if (mw == 40)
-            hipLaunchKernelGGL(k_fast_cell<40>, grid, dim3(256), lds, st, g, ex->d_pyr, ex->d_slots, ex->d_cellCount,
+            hipLaunchKernelGGL(k_fast_cell<40>, grid, dim3(256), lds, st, g, ex->d_pyr, z, ex->d_slots, ex->d_cellCount,
                                ex->d_status, mw, g.maxCellH);
         else if (mw == 44)
-            hipLaunchKernelGGL(k_fast_cell<44>, grid, dim3(256), lds, st, g, ex->d_pyr, ex->d_slots, ex->d_cellCount,
+            hipLaunchKernelGGL(k_fast_cell<44>, grid, dim3(256), lds, st, g, ex->d_pyr, z, ex->d_slots, ex->d_cellCount,
                                ex->d_status, mw, g.maxCellH);
         else
-            hipLaunchKernelGGL(k_fast_cell<0>, grid, dim3(256), lds, st, g, ex->d_pyr, ex->d_slots, ex->d_cellCount,
+            hipLaunchKernelGGL(k_fast_cell<0>, grid, dim3(256), lds, st, g, ex->d_pyr, z, ex->d_slots, ex->d_cellCount,
                                ex->d_status, mw, g.maxCellH);
     }
     mark(2);
@@ -2316,7 +2342,7 @@ static int run_pipeline(orb_extractor* ex, int B, const uint8_t* src, long long 
         const int* k = ex->blurK;   // centre, +-1, +-2, +-3
         const uint32_t kA = (uint32_t)k[3] | ((uint32_t)k[2] << 8) | ((uint32_t)k[1] << 16) | ((uint32_t)k[0] << 24);
         const uint32_t kB = (uint32_t)k[1] | ((uint32_t)k[2] << 8) | ((uint32_t)k[3] << 16);
-        hipLaunchKernelGGL(k_orient_desc, dim3((g.outPerFrame + 3) / 4, B), dim3(256), 0, st, g, ex->d_pyr,
+        hipLaunchKernelGGL(k_orient_desc, dim3((g.outPerFrame + 3) / 4, B), dim3(256), 0, st, g, ex->d_pyr, z,
                            ex->d_outKeys, ex->d_levelCount, d_kps, d_desc, cap, d_counts, kA, kB);
     }
     mark(6);
@@ -2431,7 +2457,7 @@ int orb_extract(orb_extractor* ex, const uint8_t* img, int w, int h, size_t stri
     for (int y = 0; y < h; y++) std::memcpy(ex->h_stage + (size_t)y * L0.pitch, img + (size_t)y * stride, (size_t)w);
     ORB_HIP_TRY(hipMemcpyAsync(ex->d_pyr + L0.off, ex->h_stage, imgBytes, hipMemcpyHostToDevice, ex->stream));
     const int cap = (int)ex->capHostOut;
-    st = run_pipeline(ex, 1, ex->d_pyr + L0.off, g.frameBytes, L0.pitch, 0, ex->d_kps, ex->d_desc, cap, ex->d_counts,
+    st = run_pipeline(ex, 1, ex->d_pyr + L0.off, g.frameBytes, L0.pitch, 1, ex->d_kps, ex->d_desc, cap, ex->d_counts,
                       ex->stream);
     if (st) return st;
     st = ensure_pinned(&ex->h_out, &ex->h_out_bytes, 64 + (size_t)cap * (sizeof(orb_keypoint) + 32));
@@ -2474,7 +2500,7 @@ int orb_extract_batch_device(orb_extractor* ex, const uint8_t* d_imgs, size_t im
     const Geom& g = ex->g;
     ex->lastB = B;
     ex->h_level_valid.assign((size_t)B * g.nlevels, 0);
-    return run_pipeline(ex, B, d_imgs, (long long)img_stride_frame, w, 1, d_kps, d_desc, cap, d_counts, s);
+    return run_pipeline(ex, B, d_imgs, (long long)img_stride_frame, w, 0, d_kps, d_desc, cap, d_counts, s);
 }
 
 int orb_extractor_batch_status(orb_extractor* ex, int32_t* status) {
@@ -2502,8 +2528,12 @@ int orb_pyramid_level(orb_extractor* ex, int frame, int level, const uint8_t** h
     char& valid = ex->h_level_valid[(size_t)frame * g.nlevels + level];
     if (!valid) {   // ordered after the extraction on the stream it ran on (a caller stream for the batch path)
         hipStream_t st = ex->lastStream ? ex->lastStream : ex->stream;
-        ORB_HIP_TRY(hipMemcpyAsync(dst, ex->d_pyr + per * frame + L.off, (size_t)L.pitch * L.h, hipMemcpyDeviceToHost,
-                                   st));
+        if (level == 0)   // the caller's frame (read in place) or the slab's copy
+            ORB_HIP_TRY(hipMemcpy2DAsync(dst, (size_t)L.pitch, ex->l0.p + (size_t)frame * ex->l0.frameStride,
+                                         (size_t)ex->l0.pitch, (size_t)L.w, (size_t)L.h, hipMemcpyDeviceToHost, st));
+        else
+            ORB_HIP_TRY(hipMemcpyAsync(dst, ex->d_pyr + per * frame + L.off, (size_t)L.pitch * L.h,
+                                       hipMemcpyDeviceToHost, st));
         ORB_HIP_TRY(hipStreamSynchronize(st));
         valid = 1;
     }
@@ -2523,17 +2553,18 @@ int orb_pyramid_level_device(orb_extractor* ex, int frame, int level, int blurre
     if (blurred && !ex->blurValid && ex->lastB > 0) {
         ORB_HIP_TRY(hipSetDevice(ex->device));
         hipStream_t st = ex->lastStream ? ex->lastStream : ex->stream;
-        hipLaunchKernelGGL(k_blur, dim3(g.tilesPerFrame, ex->lastB), dim3(256), 0, st, g, ex->d_pyr, ex->d_blur,
-                           ex->blurK[0], ex->blurK[1], ex->blurK[2], ex->blurK[3]);
+        hipLaunchKernelGGL(k_blur, dim3(g.tilesPerFrame, ex->lastB), dim3(256), 0, st, g, ex->d_pyr, ex->l0,
+                           ex->d_blur, ex->blurK[0], ex->blurK[1], ex->blurK[2], ex->blurK[3]);
         ORB_HIP_TRY(hipGetLastError());
         ORB_HIP_TRY(hipStreamSynchronize(st));
         ex->blurValid = true;
     }
     const uint8_t* base = blurred ? ex->d_blur : ex->d_pyr;
-    if (dptr) *dptr = base + (size_t)frame * g.frameBytes + L.off;
+    const bool raw0 = !blurred && level == 0;   // level 0 as the consumers read it (L0Src)
+    if (dptr) *dptr = raw0 ? ex->l0.p + (size_t)frame * ex->l0.frameStride : base + (size_t)frame * g.frameBytes + L.off;
     if (w) *w = L.w;
     if (h) *h = L.h;
-    if (pitch) *pitch = (size_t)L.pitch;
+    if (pitch) *pitch = raw0 ? (size_t)ex->l0.pitch : (size_t)L.pitch;
     return ORB_OK;
 }
 
@@ -2661,7 +2692,7 @@ int orb_compute_stereo_matches(orb_extractor* left, orb_extractor* right, const 
     ORB_HIP_TRY(hipMemcpyAsync(dn, hn, 8, hipMemcpyHostToDevice, s));
     const float maxD = mbf / mb;   // mb = 0 in the reference: +inf
     hipLaunchKernelGGL(k_stereo_match, dim3((n_l + 3) / 4, 1), dim3(256), 0, s, left->g, stereo_tabs(left),
-                       left->d_pyr, right->d_pyr, (size_t)0, dkl, ddl, dn, dkr, ddr, dn + 1, cap, 1, cap, mbf, maxD, dur,
+                       left->d_pyr, right->d_pyr, (size_t)0, left->l0, right->l0, dkl, ddl, dn, dkr, ddr, dn + 1, cap, 1, cap, mbf, maxD, dur,
                        ddp, dsd, cap);
     hipLaunchKernelGGL(k_stereo_median, dim3(1), dim3(1024), 0, s, dn, 1, cap, dur, ddp, dsd, cap, dn + 2, dkeys);
     ORB_HIP_TRY(hipGetLastError());
@@ -2691,8 +2722,12 @@ int orb_compute_stereo_matches_batch_device(orb_extractor* ex, const orb_keypoin
     hipStream_t s = stream ? (hipStream_t)stream : ex->stream;
     const Geom& g = ex->g;
     const float maxD = mbf / mb;
+    // frames 2p (left) and 2p + 1 (right) of the last batch: level 0 at twice the frame stride
+    L0Src zL = ex->l0, zR = ex->l0;
+    zL.frameStride = zR.frameStride = 2 * ex->l0.frameStride;
+    zR.p = ex->l0.p + ex->l0.frameStride;
     hipLaunchKernelGGL(k_stereo_match, dim3((cap + 3) / 4, n_pairs), dim3(256), 0, s, g, stereo_tabs(ex), ex->d_pyr,
-                       ex->d_pyr + g.frameBytes, (size_t)(2 * g.frameBytes), d_kps, d_desc, d_counts, d_kps + cap,
+                       ex->d_pyr + g.frameBytes, (size_t)(2 * g.frameBytes), zL, zR, d_kps, d_desc, d_counts, d_kps + cap,
                        d_desc + (size_t)cap * 32, d_counts + 1, 2 * cap, 2, cap, mbf, maxD, d_uright, d_depth, dsd, cap);
     hipLaunchKernelGGL(k_stereo_median, dim3(n_pairs), dim3(1024), 0, s, d_counts, 2, cap, d_uright, d_depth, dsd, cap,
                        d_nstereo, dkeys);
