@@ -115,9 +115,11 @@ def parse():
     ap.add_argument("--lba-points", type=int, default=3000)
     ap.add_argument("--lba-kf", type=int, default=20)
     ap.add_argument("--no-lba-scaled", action="store_true", help="skip the 60 KF / 200 KF corridor windows")
-    ap.add_argument("--lba-comm", choices=["native", "torch"], default="native",
-                    help="N>1 local BA: the library's device group driven by rank 0 (native) or one rank per "
-                         "GPU with a torch.distributed all-reduce callback (torch)")
+    ap.add_argument("--lba-comm", choices=["native", "torch"], default="torch",
+                    help="N>1 local BA: one rank per GPU with a torch.distributed (RCCL) all-reduce callback "
+                         "(torch, the default), or the library's device-side group driven by rank 0 over every "
+                         "rank's device (native: its peer exchange has run on two contexts of one device only, "
+                         "so the line marks it unverified on distinct devices)")
     ap.add_argument("--no-stereo", action="store_true", help="skip the config-5 sharded stereo leg")
     ap.add_argument("--stereo-batches", type=int, default=16,
                     help="8-frame EuRoC stereo batches per step of the config-5 leg")
@@ -129,8 +131,8 @@ def parse():
 def algorithmic_bytes(stage, lw, lh, n_pre, n_out):
     """Per-frame algorithmic HBM bytes of each stage."""
     P = (lw.astype(np.int64) * lh).tolist()
-    if stage == "resize":
-        return sum(P[l - 1] + P[l] for l in range(1, len(P)))
+    if stage == "resize":   # k_pyramid: level 0 read once, levels 1.. written once (fused, LDS-staged)
+        return P[0] + sum(P[1:])
     if stage == "fast_detect":
         return sum(P) + 4 * n_pre
     if stage == "octree":
@@ -179,6 +181,56 @@ def algorithmic_ops(stage, lw, lh, n_pre, n_out):
     if stage == "orient_blur_desc":
         return ALG_OPS["keypoint"] * n_out
     raise KeyError(stage)
+
+
+EXT_KERNELS = (("k_pyramid", "resize", 0), ("k_fast_cell", "fast_detect", 1), ("k_octree", "octree", 3),
+               ("k_orient_desc", "orient_blur_desc", 5))
+
+
+def extraction_roofline(stage_ms, ncalls, lw, lh, n_pre, n_out, W, H, NF, Bs):
+    """SURVEY §8d roofline of every extraction kernel of the timed region, and the dominant one
+    (largest average launch time) as the line's `roofline`.  achieved = the kernel's algorithmic
+    HBM bytes per launch (algorithmic_bytes x the frames of a launch) / its average launch time
+    (HIP events on its stream, timed region); peak 8 TB/s; traffic = PMC FETCH_SIZE x 2 +
+    WRITE_SIZE per launch from the committed pass of this configuration (None when absent).  Each
+    kernel also carries its VALU view (issued lane-ops from the committed PMC pass, against the
+    78.6 T nominal and the measured wave64 issue rate) and its algorithmic-op rate (ALG_OPS)."""
+    per = {}
+    for name, stage, i in EXT_KERNELS:
+        ms = float(stage_ms[i]) / ncalls
+        if ms <= 0:
+            continue
+        byts = algorithmic_bytes(stage, lw, lh, n_pre, n_out) * Bs
+        gbs = byts / (ms * 1e-3) / 1e9
+        k = {"launch_ms": round(ms, 4), "algorithmic_bytes_per_launch": int(byts), "achieved_gbs": round(gbs, 2),
+             "frac": round(gbs / HBM_PEAK_GBS, 5), "traffic": pmc_traffic(name, W, H, NF, Bs)}
+        if k["traffic"]:
+            k["traffic_over_algorithmic"] = round(k["traffic"] / byts, 3)
+        alg = algorithmic_ops(stage, lw, lh, n_pre, n_out) * Bs
+        k["algorithmic_ops"] = {"ops_per_launch": int(alg), "achieved_tops": round(alg / (ms * 1e-3) / 1e12, 3),
+                                "frac": round(alg / (ms * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4)}
+        ops = pmc_valu_ops(name, W, H, NF, Bs)
+        if ops is not None:
+            ach = ops / (ms * 1e-3) / 1e12
+            k["valu"] = {"lane_ops_per_launch": ops, "achieved_tops": round(ach, 3), "peak": VALU_PEAK_TOPS,
+                         "frac": round(ach / VALU_PEAK_TOPS, 4), "measured_issue_peak": VALU_MEASURED_TOPS,
+                         "frac_of_measured_issue_peak": round(ach / VALU_MEASURED_TOPS, 4)}
+            util = pmc_lane_util(name, W, H, NF, Bs)
+            if util is not None:
+                k["valu"]["active_lane_frac"] = util
+        per[name] = k
+    if not per:
+        return None
+    dom = max(per, key=lambda n: per[n]["launch_ms"])
+    d = per[dom]
+    return {"bound": "hbm", "kernel": dom, "achieved": d["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": d["frac"], "traffic": d["traffic"],
+            "traffic_unit": "bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE, profiles/)",
+            "launch_ms": d["launch_ms"], "frames_per_launch": Bs,
+            "algorithmic_bytes_per_launch": d["algorithmic_bytes_per_launch"],
+            "bytes_model": "SURVEY 8d per kernel: k_pyramid P0 + sum_{l>=1} P_l; k_fast_cell sum_l P_l + 4 N_pre; "
+                           "k_octree 4 (N_pre + N); k_orient_desc N (43^2 + 60)",
+            "kernels": per}
 
 
 def progress(rank, msg):
@@ -413,7 +465,8 @@ def bench_lba(args, amd, dev, local, rank, world):
                "native_group_unavailable": fallback,
                "collective": ("none" if world == 1 else
                               "library device-side exchange over xGMI (lba_group: flag words + peer reads, one process "
-                              "driving every device, slots in HIP graphs)" if grp_live else
+                              "driving every device, slots in HIP graphs; verified before this run on two contexts "
+                              "of one device only)" if grp_live else
                               "none (the group failed; rank 0's device alone)" if native else
                               "torch.distributed all_reduce callback (RCCL), one process per GPU"),
                # LM decisions of the last timed solve: identical for every world size (landmark shards
@@ -478,9 +531,8 @@ def bench_lba_scaled(args, amd, dev, rank, world):
     and 200 KF x 100,000 points with banded covisibility (synth.ba_problem_corridor).  N > 1:
     rank 0 drives the device group (lba_group) over every rank's device, as bench_lba does.
     At N = 1 the oracle's OpenMP variant is timed beside it on one solve."""
-    from orb_slam2_amd import synth
     sizes = ((60, 8000), (200, 100000))
-    native = world > 1
+    native = world > 1 and args.lba_comm == "native"
     if native and rank != 0:
         torch.distributed.barrier()
         obj = [None]
@@ -488,25 +540,51 @@ def bench_lba_scaled(args, amd, dev, rank, world):
         return obj[0]
     out = {}
     try:
-        _lba_scaled_sizes(args, amd, dev, world, native, sizes, out)
+        _lba_scaled_sizes(args, amd, dev, world, native, sizes, out, rank)
     except Exception as exc:   # rank 0 must still reach the ranks waiting at the barrier below
         if not native:
             raise
         out["error"] = f"{type(exc).__name__}: {exc}"
     out["note"] = ("corridor windows, banded covisibility; ms_per_iter = lba_solve wall / LM iterations"
-                   + (f"; landmarks sharded over {world} devices by one process (lba_group)" if native else ""))
+                   + (f"; landmarks sharded over {world} devices by one process (lba_group, unverified on "
+                      f"distinct devices before this run)" if native else
+                      f"; landmarks sharded over {world} ranks, torch.distributed all_reduce (RCCL) callback, "
+                      f"max over ranks" if world > 1 else ""))
     if native:
         torch.distributed.barrier()
         torch.distributed.broadcast_object_list([out], src=0)
     return out
 
 
-def _lba_scaled_sizes(args, amd, dev, world, native, sizes, out):
+def torch_comm_context(amd, dev, rank, world, nk, ne):
+    """A LocalBA context of this rank whose collectives are torch.distributed.all_reduce calls (RCCL
+    over xGMI with one process per GPU, gloo when ranks share a device) on its own stream."""
+    ctx = amd.LocalBA(dev.index or 0)
+    stream = torch.cuda.Stream(dev)
+    ctx.set_stream(stream.cuda_stream)
+    ws = torch.zeros(max(36 * nk * nk + 6 * nk, ne) + 64, dtype=torch.float64, device=dev)
+
+    def ar(off, cnt, op):
+        with torch.cuda.stream(stream):
+            torch.distributed.all_reduce(ws[off:off + cnt], op=torch.distributed.ReduceOp.SUM if op == 0
+                                         else torch.distributed.ReduceOp.MAX)
+    ctx.set_comm(rank, world, ws, ar)
+    ctx._keep = (stream, ws)
+    return ctx
+
+
+def _lba_scaled_sizes(args, amd, dev, world, native, sizes, out, rank=0):
     from orb_slam2_amd import synth
     for nl, npts in sizes:
         pb = synth.ba_problem_corridor(n_local=nl, n_fixed=4, n_points=npts)
         group_error = None
-        if native:
+        if world > 1 and not native:   # one rank per GPU, RCCL all-reduce callback
+            ctx = torch_comm_context(amd, dev, rank, world, len(pb["Tcw"]), len(pb["edge_point"]))
+            call = ctx.prepared(pb)
+            for _ in range(2):
+                call()
+            torch.distributed.barrier()
+        elif native:
             try:
                 ndev = torch.cuda.device_count()
                 ctx = amd.LocalBAGroup([r % ndev for r in range(world)])
@@ -530,6 +608,10 @@ def _lba_scaled_sizes(args, amd, dev, world, native, sizes, out):
             its, tr, _ = call()
             times.append(time.perf_counter() - t0)
             iters += sum(its)
+        if world > 1 and not native:   # the slowest rank's time
+            t = torch.tensor([sum(times)], dtype=torch.float64, device=dev)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            times = [float(t[0]) / 5] * 5
         fixed = pb["pose_fixed"].astype(bool)
         P = int(np.count_nonzero(~fixed))
         T = (6 * P + 15) // 16
@@ -541,7 +623,7 @@ def _lba_scaled_sizes(args, amd, dev, world, native, sizes, out):
                     "trials_per_solve": tr, "ldlt_mfma_flops_per_trial": tiles * 8192}
         if group_error is not None:
             out[key]["native_group_unavailable"] = group_error
-        if not native:
+        if world == 1:
             # the reduced solve's share from one profiled solve (per-slot events, kernels enqueued one
             # by one): its f64 MFMA rate against the 78.6 TFLOP/s peak.  The MFMA flops are the
             # trailing-update tiles' (16x16x16 per tile and 16-column step); the pivot
@@ -1335,14 +1417,13 @@ def main():
         step(s)
     torch.cuda.synchronize(dev)
     if not args.no_profile:
-        # every stream's extractor records two HIP events around its k_fast_cell launch (the
-        # dominant kernel) inside the timed region: with S streams sharing the chip a launch
-        # overlapped by another stream's kernels runs longer than one that is alone, and the
-        # rocprofv3 per-kernel average (profiles/) is over all of them.  The per-stage split is
-        # taken in a separate profiled pass after the timed region (events at every stage
-        # boundary add dispatch bubbles).
+        # every stream's extractor records HIP events at its four kernels' boundaries (k_pyramid,
+        # k_fast_cell, k_octree, k_orient_desc: five events per call, mode 3) on its launch stream
+        # inside the timed region: with S streams sharing the chip a launch overlapped by other
+        # streams' kernels runs longer than one alone, and the rocprofv3 per-kernel averages
+        # (profiles/) are over the same mix
         for p in pipes:
-            lib.orb_extractor_profile(p.ex._h, 2)
+            lib.orb_extractor_profile(p.ex._h, 3)
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
@@ -1366,7 +1447,7 @@ def main():
         mat_status |= m
     if ext_status or mat_status:
         raise SystemExit(f"bench: overflow status extractor={ext_status} matcher={mat_status}")
-    # k_fast_cell launch times (HIP events recorded on the launch stream during the timed region)
+    # per-kernel launch times (HIP events recorded on the launch streams during the timed region)
     def stage_times():
         tot, calls = np.zeros(6), 0
         for p in pipes:
@@ -1376,15 +1457,7 @@ def main():
             tot += sm
             calls += nc.value
         return tot, calls
-    fast_ms, ncalls = stage_times() if not args.no_profile else (np.zeros(6), 0)
-    stage_ms, nstage = np.zeros(6), 0
-    if not args.no_profile:      # the stage split: a separate pass with every stage boundary recorded
-        for p in pipes:
-            lib.orb_extractor_profile(p.ex._h, 1)
-        for s in range(min(args.steps, 10)):
-            step(args.warmup + args.steps + s)
-        torch.cuda.synchronize(dev)
-        stage_ms, nstage = stage_times()
+    stage_ms, nstage = stage_times() if not args.no_profile else (np.zeros(6), 0)
     frames_total = B * args.steps * world
     value = frames_total / dt
     cnt = torch.cat([p.counts[p.last][1:] for p in pipes]).cpu().numpy()
@@ -1422,51 +1495,14 @@ def main():
     pre = np.zeros(8, np.int32)
     lib.orb_extractor_last_counts(ex._h, 0, _abi.ptr(pre), None)
     n_pre_frame = float(pre.sum())   # corners k_fast_cell emitted for frame 0 of the last batch
-    if not args.no_profile and ncalls > 0:
-        fast_launch_ms = float(fast_ms[1]) / ncalls       # live, timed region, launch streams
-        n_out = float(np.mean(cnt))
-        n_pre = n_pre_frame
-        # k_fast_cell is VALU-issue-bound (profiles/r02_valu_pmc.json: SQ_ACTIVE_INST_VALU ~ the
-        # VALU instruction count x 4 cycles keeps the SIMDs >80 % busy), so its roofline is the
-        # vector ALU: achieved = VALU lane-ops per launch (SQ_INSTS_VALU x 64 from the committed
-        # PMC pass of this configuration) / the live launch time; peak = 78.6 T lane-ops/s
-        # (256 CU x 128 lanes x 2.4 GHz, MI355X_MICROARCH.md) and, beside it, the issue rate
-        # measured by tools/micro/valu_peak.hip (4 cycles per wave64 VALU instruction:
-        # 6.1e11 wave-instructions/s = 39.3 T lane-ops/s).  The HBM figure stays as secondary.
-        hbm_bytes = algorithmic_bytes("fast_detect", lw, lh, n_pre, n_out) * Bs
-        hbm = {"bound": "hbm", "achieved": round(hbm_bytes / (fast_launch_ms * 1e-3) / 1e9, 2), "peak": HBM_PEAK_GBS,
-               "unit": "GB/s", "algorithmic_bytes_per_launch": int(hbm_bytes), "traffic": None}
-        hbm["frac"] = round(hbm["achieved"] / HBM_PEAK_GBS, 5)
-        tr = pmc_traffic("k_fast_cell", W, H, NF, Bs)
-        if tr is not None:
-            hbm["traffic"] = tr
-            hbm["traffic_unit"] = "bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)"
-            hbm["traffic_source"] = PMC_TRAFFIC.name
-        roof = {"bound": "valu", "kernel": "k_fast_cell", "achieved": None, "peak": VALU_PEAK_TOPS, "unit": "TOP/s",
-                "frac": None, "traffic": hbm["traffic"], "launch_ms": round(fast_launch_ms, 4),
-                "frames_per_launch": Bs, "hbm": hbm}
-        # algorithmic ops (codegen- and lane-idleness-independent, ALG_OPS) per launch / live time
-        alg = algorithmic_ops("fast_detect", lw, lh, n_pre, n_out) * Bs
-        roof["algorithmic"] = {"ops_per_launch": int(alg), "achieved": round(alg / (fast_launch_ms * 1e-3) / 1e12, 3),
-                               "unit": "TOP/s", "peak": VALU_PEAK_TOPS,
-                               "frac": round(alg / (fast_launch_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4),
-                               "model": "ALG_OPS in bench.py (DESIGN.md §Roofline)"}
-        ops = pmc_valu_ops("k_fast_cell", W, H, NF, Bs)
-        if ops is not None:
-            ach = ops / (fast_launch_ms * 1e-3) / 1e12
-            roof.update(achieved=round(ach, 3), frac=round(ach / VALU_PEAK_TOPS, 4),
-                        valu_lane_ops_per_launch=ops, valu_ops_source=PMC_VALU.name,
-                        measured_issue_peak=VALU_MEASURED_TOPS,
-                        frac_of_measured_issue_peak=round(ach / VALU_MEASURED_TOPS, 4))
-            util = pmc_lane_util("k_fast_cell", W, H, NF, Bs)
-            if util is not None:   # the issued lane-ops whose lanes were active
-                roof["active_lane_frac"] = util
-                roof["active_frac"] = round(ach * util / VALU_PEAK_TOPS, 4)
-        result["roofline"] = roof
+    if nstage > 0:
+        result["roofline"] = extraction_roofline(stage_ms, nstage, lw, lh, n_pre_frame, float(np.mean(cnt)), W, H, NF,
+                                                 Bs)
     if nstage > 0:
         result["stage_ms_per_batch"] = {k: round(float(v) / nstage, 4) for k, v in zip(STAGES, stage_ms)
                                         if not k.startswith("reserved")}
-        result["stage_ms_source"] = "separate profiled pass after the timed region (events at every stage boundary)"
+        result["stage_ms_source"] = ("timed region: HIP events at the kernel boundaries on each stream, average "
+                                     "launch time under the streams' sharing")
     # whole-pipeline roofline of SURVEY §8d: B_ext = P0 + 2 sum_{l>=1} P_l + N_kp (28 + 32) per frame
     P = (lw.astype(np.int64) * lh)
     b_ext = float(P[0] + 2 * P[1:].sum()) + float(np.mean(cnt)) * 60.0

@@ -114,7 +114,8 @@ int orb_pyramid_level_device(orb_extractor* ex, int frame, int level, int blurre
  * and the number of profiled calls to *n_calls, then resets; returns the number
  * of stages.  enable = 2 records only the two events bracketing stage 1
  * (k_fast_cell), so a timed run pays two event records per call; the other
- * stages then read 0. */
+ * stages then read 0.  enable = 3 records the four kernels' boundaries only (five events per
+ * call: k_pyramid, k_fast_cell, k_octree, k_orient_desc in stages 0, 1, 3, 5). */
 int orb_extractor_profile(orb_extractor* ex, int enable);
 int orb_extractor_stage_times(orb_extractor* ex, double* ms, int n_stages, int* n_calls);
 

@@ -2256,6 +2256,7 @@ static int run_pipeline(orb_extractor* ex, int B, const uint8_t* src, long long 
     if (prof) {
         for (int i = 0; i <= kStages; i++) {
             if (prof == 2 && i != 1 && i != 2) continue;   // two events bracketing k_fast_cell only
+            if (prof == 3 && (i == 3 || i == 5)) continue;  // the four kernels' boundaries only
             ev[i] = ev_get(ex);
             if (!ev[i]) return ORB_EGPU;
         }
@@ -2570,7 +2571,7 @@ int orb_pyramid_level_device(orb_extractor* ex, int frame, int level, int blurre
 
 int orb_extractor_profile(orb_extractor* ex, int enable) {
     if (!ex) return ORB_EINVAL;
-    if (enable < 0 || enable > 2) return ORB_EINVAL;
+    if (enable < 0 || enable > 3) return ORB_EINVAL;
     ex->profile = enable;
     return ORB_OK;
 }
@@ -2581,11 +2582,18 @@ int orb_extractor_stage_times(orb_extractor* ex, double* ms, int n_stages, int* 
     for (auto& set : ex->ev_sets) {
         for (int i = kStages; i >= 0; i--)
             if (set[i]) { ORB_HIP_TRY(hipEventSynchronize(set[i])); break; }
-        for (int i = 0; i < kStages; i++) {
-            if (!set[i] || !set[i + 1]) continue;   // mode 2 records stage 1 only
+        // consecutive recorded events a < b bracket the kernel of stage b - 1 (the stages between
+        // them launch nothing): mode 1 records every boundary, 2 the two around stage 1, 3 the
+        // kernel boundaries 0, 1, 2, 4, 6
+        for (int a = 0; a < kStages; a++) {
+            if (!set[a]) continue;
+            int b = a + 1;
+            while (b <= kStages && !set[b]) b++;
+            if (b > kStages) break;
             float t = 0.f;
-            ORB_HIP_TRY(hipEventElapsedTime(&t, set[i], set[i + 1]));
-            ex->stage_ms[i] += t;
+            ORB_HIP_TRY(hipEventElapsedTime(&t, set[a], set[b]));
+            ex->stage_ms[b - 1] += t;
+            a = b - 1;
         }
         ex->stage_calls++;
         for (auto e : set)

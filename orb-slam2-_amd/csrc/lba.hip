@@ -2132,8 +2132,7 @@ __global__ __launch_bounds__(512) void k_ldlt_mw_bsolve(MwLdl m, int K0, double*
     if (lm_off(st, 1)) return;
     extern __shared__ __attribute__((aligned(16))) double bsm[];
     double* Ls = bsm;                        // [kSB][kSB + 1]: L(K0 + r, K0 + c), c < r
-    double* ysb = Ls + kSB * (kSB + 1);      // [kSB]
-    double* xfull = ysb + kSB;               // [np] (top super-block: x for the pose update)
+    double* ysb = Ls + kSB * (kSB + 1);      // [kSB]  (LDS independent of the order: any window size)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int np = m.np, n = m.n, ld = np, nsb = min(kSB, np - K0);
     if (__builtin_amdgcn_readfirstlane(*m.fail)) {
@@ -2194,10 +2193,10 @@ __global__ __launch_bounds__(512) void k_ldlt_mw_bsolve(MwLdl m, int K0, double*
         if (K0 + r < n) x[K0 + r] = ysb[r];
     if (!last) return;
     if (tid == 0) flags[0] = 0;
-    if (ptail.scaleOut) {   // x through LDS: this super-block's rows from ysb, the rest as stored
-        for (int i = tid; i < np; i += 512) xfull[i] = i < nsb ? ysb[i] : (i < n ? x[i] : 0.0);
+    if (ptail.scaleOut) {   // x as stored: this super-block's rows just now (visible to the workgroup
+                            // after the barrier), the rest by the earlier launches
         __syncthreads();
-        if (wave == 0) pose_tail(ptail, xfull, st->lambda, lane);
+        if (wave == 0) pose_tail(ptail, x, st->lambda, lane);
     }
 }
 // 64 rows per workgroup; wave w takes the super-block's columns [kSB/4 w, kSB/4 (w + 1)) with all
@@ -2248,7 +2247,7 @@ static void enqueue_ldlt_mw(hipStream_t s, const MwLdl& m, const double* S, cons
     const int nsbk = (np + kSB - 1) / kSB;
     for (int q = nsbk - 1; q >= 0; q--) {
         const int K0 = q * kSB;
-        hipLaunchKernelGGL(k_ldlt_mw_bsolve, dim3(1), dim3(512), ((size_t)kSB * (kSB + 1) + kSB + np) * 8, s, m, K0, x,
+        hipLaunchKernelGGL(k_ldlt_mw_bsolve, dim3(1), dim3(512), ((size_t)kSB * (kSB + 1) + kSB) * 8, s, m, K0, x,
                            flags, st, q == 0 ? pt : PoseTail{}, q == nsbk - 1 ? 1 : 0, q == 0 ? 1 : 0);
         if (q > 0) hipLaunchKernelGGL(k_ldlt_mw_bupd, dim3((K0 + 63) / 64), dim3(256), 0, s, m, K0, x, st);
     }
@@ -2520,8 +2519,9 @@ __global__ __launch_bounds__(256) void k_unpack(double* __restrict__ buf, const 
 //   k_grp_reduce: every rank sums all ranks' slices in rank order (system-scope loads over xGMI)
 //   k_grp_sync(1): read[rank] = e; wait read[p] >= e (nobody packs into a workspace still read)
 // Every rank runs the same sequence of collectives (identical LM decisions), so epochs agree.
-// A wait that exceeds ~1 s (a peer gone) sets the rank's error word and gives up: the solve then
-// fails with ORB_EGPU instead of hanging the device.
+// A wait longer than GrpDev::waitTicks of the constant-rate wall clock (2 s; a peer's first launch,
+// loading its code objects, takes ~0.3 s) sets the rank's error word and gives up: the solve then
+// fails with ORB_EGPU instead of hanging the device, and the rank's later waits are skipped.
 constexpr int kMaxGroupDev = 16;
 struct GrpDev {
     uint32_t* flags[kMaxGroupDev];   // rank p's flag words: [0] ready epoch, [32] read epoch
@@ -2529,6 +2529,7 @@ struct GrpDev {
     uint32_t* epoch;                 // this rank's collective counter
     int* err;                        // this rank's error word
     int rank, n;
+    uint64_t waitTicks;              // wait bound in wall_clock64() ticks (hipDeviceAttributeWallClockRate)
 };
 __global__ void k_grp_sync(GrpDev g, int which) {
     if (threadIdx.x != 0) return;
@@ -2541,13 +2542,13 @@ __global__ void k_grp_sync(GrpDev g, int which) {
     const int w = which ? 32 : 0;
     __hip_atomic_store(g.flags[g.rank] + w, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     if (failed) return;   // after one timed-out wait the rest of the solve does not wait (it fails anyway)
-    // bounded by iterations, not by a clock: ~10-30 s — far above any legitimate wait (a peer's first
-    // launch loads its code objects: ~0.3 s measured as a spurious timeout with a 2^19 bound)
-    int spins = 0;
+    // bounded by the constant-rate wall clock (not by an iteration count, whose duration depends on
+    // the load latency over xGMI)
+    const uint64_t t0 = wall_clock64();
     for (int q = 0; q < g.n; q++) {
         if (q == g.rank) continue;
         while (__hip_atomic_load(g.flags[q] + w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
-            if (++spins > (1 << 24)) {   // (an iteration is a sleep plus a system-scope load: ~0.5-3 us)
+            if (wall_clock64() - t0 > g.waitTicks) {
                 __hip_atomic_store(g.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 return;
             }
@@ -4276,6 +4277,10 @@ int lba_group_solve(lba_group* g, const lba_problem* p, const lba_options* o, co
             gd.err = reinterpret_cast<int*>(g->sync[q] + 56);
             gd.rank = q;
             gd.n = n;
+            int khz = 0;   // wall-clock rate (100 MHz on gfx9); a 2 s bound
+            if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, g->dev[q]) != hipSuccess || khz <= 0)
+                khz = 100000;
+            gd.waitTicks = (uint64_t)khz * 1000ull * 2ull;
             g->ctx[q]->grp = &gd;
         }
         // Graph-captured slots only when every rank has a device of its own: two ranks on one
