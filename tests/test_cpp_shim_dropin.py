@@ -59,6 +59,8 @@ def test_shim_pose_optimization(shim, tmp_path, amd, kw):
     from orb_slam2_amd import synth, optimizer as opt
     frames = synth.pose_problems(n_frames=2, **kw)
     for f, frame in enumerate(frames):
+        # the shim reads the intrinsics from the Frame's float members (e->fx = pFrame->fx, R :366-369)
+        frame = dict(frame, cam=tuple(float(np.float32(v)) for v in frame["cam"]))
         arrays, pos = _pose_inputs(frame, 100 + f)
         r, outp = _run(shim, "pose", tmp_path, *arrays)
         assert r.returncode == 0, r.stderr
@@ -336,6 +338,7 @@ def test_shim_threading_contract(shim, tmp_path, amd):
            np.array([100], np.int32))
     # PoseOptimization job
     frame = synth.pose_problems(n_frames=1, stereo_frac=0.3, seed=21)[0]
+    frame = dict(frame, cam=tuple(float(np.float32(v)) for v in frame["cam"]))
     pose_in, pos = _pose_inputs(frame, 8)
     _write(tmp_path / "pose.in", *pose_in)
     # LocalBundleAdjustment job (the layout of test_cpp_shim.test_shim_local_bundle_adjustment)
