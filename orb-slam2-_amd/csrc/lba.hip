@@ -2511,6 +2511,49 @@ __global__ __launch_bounds__(256) void k_unpack(double* __restrict__ buf, const 
     for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) buf[i] = ws[i];
 }
 
+// The reduced system's exchange with a communicator (the upper triangle only): the
+// pose-pair blocks of the global pair list (every pair some landmark couples, the diagonal
+// blocks, identical on every rank) and b_s, packed back to back — G 6x6 blocks + 6P doubles in
+// place of the dense 36 P^2 + 6P.  Unpacking writes each block and its mirror, as k_schur_pairs
+// stores them.  Guarded like k_pack: a skipped phase packs zeros and leaves S alone.
+template <bool kSys>
+__global__ __launch_bounds__(256) void k_pack_pairs(double* __restrict__ ws, const double* __restrict__ S,
+                                                    const double* __restrict__ bs, const int32_t* __restrict__ pairs,
+                                                    int G, int P, const LmState* st, int want) {
+    const bool off = lm_off(st, want);
+    const size_t n = 6 * (size_t)P, tot = 36 * (size_t)G + n;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < tot; i += (size_t)gridDim.x * 256) {
+        double v;
+        if (i < 36 * (size_t)G) {
+            const int pr = pairs[i / 36], e = (int)(i % 36);
+            const int bi = pr >> 16, bj = pr & 0xFFFF;
+            v = S[(size_t)(6 * bi + e / 6) * n + 6 * bj + e % 6];
+        } else {
+            v = bs[i - 36 * (size_t)G];
+        }
+        v = off ? 0.0 : v;
+        if (kSys) __hip_atomic_store(ws + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        else ws[i] = v;
+    }
+}
+__global__ __launch_bounds__(256) void k_unpack_pairs(double* __restrict__ S, double* __restrict__ bs,
+                                                      const double* __restrict__ ws, const int32_t* __restrict__ pairs,
+                                                      int G, int P, const LmState* st, int want) {
+    if (lm_off(st, want)) return;
+    const size_t n = 6 * (size_t)P, tot = 36 * (size_t)G + n;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < tot; i += (size_t)gridDim.x * 256) {
+        const double v = ws[i];
+        if (i < 36 * (size_t)G) {
+            const int pr = pairs[i / 36], e = (int)(i % 36);
+            const int bi = pr >> 16, bj = pr & 0xFFFF, r = e / 6, q = e % 6;
+            S[(size_t)(6 * bi + r) * n + 6 * bj + q] = v;
+            S[(size_t)(6 * bj + q) * n + 6 * bi + r] = v;   // (a diagonal block: the same value twice)
+        } else {
+            bs[i - 36 * (size_t)G] = v;
+        }
+    }
+}
+
 // ---- device-side exchange of a device group (lba_group): no host in the loop, so the slots of a
 // sharded solve are captured into HIP graphs like the single-process ones.  Every rank's
 // workspace and flag words live in fine-grained memory on its own device; a collective is
@@ -2988,6 +3031,7 @@ struct lba_context {
     void* commUser = nullptr;
     const orbamd::GrpDev* grp = nullptr;   // device-side exchange (lba_group): replaces the callback
     bool grpGraphs = false;                // ... and its slots may be graph-captured (every rank on its own device)
+    std::vector<int32_t> gflagStage;       // the global pair flags of the last solve (packed exchange)
     // device buffers: a grow-only arena reused across solves (hipMalloc / hipFree per buffer
     // and per call cost more than a small LBA's whole LM loop; hipFree also synchronises)
     std::vector<std::pair<char*, size_t>> chunks;   // (base, size); the last one is bumped
@@ -3211,6 +3255,25 @@ static int comm_allreduce_segs(lba_context* c, std::initializer_list<CommSeg> se
 }
 static int comm_allreduce_g(lba_context* c, double* dbuf, size_t n, int op, const LmState* st, int want) {
     return comm_allreduce_segs(c, {CommSeg{dbuf, n}}, op, st, want);
+}
+// S + b_s over the communicator as the G listed pair blocks + b_s (k_pack_pairs)
+static int comm_allreduce_schur(lba_context* c, double* S, double* bs, const int32_t* pairs, int G, int P,
+                                const LmState* st, int want) {
+    if (c->world <= 1) return ORB_OK;
+    const size_t tot = 36 * (size_t)G + 6 * (size_t)P;
+    if ((!c->allreduce && !c->grp) || !c->ws || tot > c->wsDoubles) return ORB_EINVAL;
+    const unsigned g = (unsigned)std::max<size_t>(1, std::min<size_t>(1024, (tot + 255) / 256));
+    if (c->grp) hipLaunchKernelGGL(k_pack_pairs<true>, dim3(g), dim3(256), 0, c->stream, c->ws, S, bs, pairs, G, P, st, want);
+    else hipLaunchKernelGGL(k_pack_pairs<false>, dim3(g), dim3(256), 0, c->stream, c->ws, S, bs, pairs, G, P, st, want);
+    if (c->grp) {
+        TRY(grp_exchange(c, tot, 0));
+    } else if (c->allreduce(c->commUser, 0, tot, 0) != 0) {
+        return ORB_EGPU;
+    }
+    const double* res = c->wsOut ? c->wsOut : c->ws;
+    hipLaunchKernelGGL(k_unpack_pairs, dim3(g), dim3(256), 0, c->stream, S, bs, res, pairs, G, P, st, want);
+    ORB_HIP_TRY(hipGetLastError());
+    return ORB_OK;
 }
 
 extern "C" {
@@ -3463,6 +3526,7 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
     const bool devStruct = c->world == 1 && NE > 0 && !std::getenv("ORB_LBA_HOST_STRUCT");
     std::vector<uint8_t> level(NE, 0);
     HostStructure hs;
+    int gPairs = 0;   // with a communicator: the global pair list's length (the packed exchange)
     int32_t* d_freePoses = nullptr;
     int32_t *d_poseIdx0 = nullptr, *d_ptLocal0 = nullptr, *d_ptGlob0 = nullptr;
     LbaDev d;
@@ -3711,7 +3775,7 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
             hipLaunchKernelGGL(k_schur_pairs, dim3(npairs), dim3(kSpT), 0, s, d, root ? 1 : 0);
             boundary();
         }
-        if (d.P > 0) TRY(comm_allreduce_g(c, d.S, (size_t)36 * d.P * d.P + 6 * (size_t)d.P, 0, d.lm, 1));
+        if (d.P > 0) TRY(comm_allreduce_schur(c, d.S, d.bs, d.pairs, gPairs, d.P, d.lm, 1));
         if (prof) (void)hipEventRecord(ev[2], s);
         if (d.P > 0) {
             const int n = 6 * d.P, np = (n + kNB - 1) & ~(kNB - 1);
@@ -3947,10 +4011,33 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         cnt = flag + np2;
         ORB_HIP_TRY(hipMemsetAsync(npairs, 0, 4, s));
         if (P > 0) {
-            const int all = c->world > 1 ? 1 : 0;
             ORB_HIP_TRY(hipMemsetAsync(flag, 0, 8 * (size_t)np2, s));
             ORB_HIP_TRY(hipMemsetAsync(d.S, 0, 8 * (size_t)36 * P * P, s));
-            hipLaunchKernelGGL(k_pair_mark, grid(std::max({d.M, P, all ? np2 : 0})), dim3(256), 0, s, d, flag, cnt, all);
+            if (c->world > 1) {
+                // with a communicator every rank lists the GLOBAL pair set (every pair some landmark of
+                // any rank couples, and the diagonal): the same list on every rank, so the exchange can
+                // pack exactly those blocks (k_pack_pairs); each rank's own landmarks still set the
+                // trip counts below.  Built on the host from the problem arrays every rank holds.
+                std::vector<int32_t> gflag((size_t)np2, 0);
+                std::vector<std::vector<int>> lp((size_t)NM);
+                for (int e = 0; e < NE; e++) {   // every edge, every rank's landmarks: a superset is harmless
+                    const int pi = hs.poseIdx[(size_t)p->edge_pose[e]];
+                    if (pi >= 0) lp[(size_t)p->edge_point[e]].push_back(pi);
+                }
+                for (int i = 0; i < P; i++) gflag[(size_t)(i * P - i * (i - 1) / 2)] = 1;
+                for (const auto& v : lp)
+                    for (size_t a = 0; a < v.size(); a++)
+                        for (size_t b = a + 1; b < v.size(); b++) {
+                            if (v[a] == v[b]) continue;
+                            const int i = std::min(v[a], v[b]), j = std::max(v[a], v[b]);
+                            gflag[(size_t)(i * P - i * (i - 1) / 2 + (j - i))] = 1;
+                        }
+                gPairs = 0;
+                for (int32_t f : gflag) gPairs += f;
+                c->gflagStage = gflag;   // (kept: the copy is asynchronous)
+                ORB_HIP_TRY(hipMemcpyAsync(flag, c->gflagStage.data(), 4 * (size_t)np2, hipMemcpyHostToDevice, s));
+            }
+            hipLaunchKernelGGL(k_pair_mark, grid(std::max(d.M, P)), dim3(256), 0, s, d, flag, cnt, 0);
             hipLaunchKernelGGL(k_pair_list, dim3(1), dim3(1024), 0, s, flag, cnt, P, pairs, npairs, tripStart);
             d.pairs = pairs;
             d.npairs = npairs;
