@@ -2109,8 +2109,11 @@ static int ensure_geom(orb_extractor* ex, int w, int h) {
         }
         // (ORB_PYR_LDS_KB: diagnostic override of the budget)
         const char* ev = std::getenv("ORB_PYR_LDS_KB");
-        const int budget = (ev && std::atoi(ev) >= 8 && std::atoi(ev) <= 160) ? std::atoi(ev) * 1024 : kPyrLdsBudget;
-        for (int K = 8; spanOk && K <= std::min(64, Hl) && bestK == 0; K++) {
+        const int budget0 = (ev && std::atoi(ev) >= 8 && std::atoi(ev) <= 160) ? std::atoi(ev) * 1024 : kPyrLdsBudget;
+        // the budget grows (to 96 KB) for geometries whose bands cannot fit it (wide levels:
+        // KITTI's 1034-column level 1), rather than falling back to the per-level launches
+        for (int budget = budget0; spanOk && bestK == 0 && budget <= 96 * 1024; budget += 8 * 1024)
+        for (int K = 8; K <= std::min(64, Hl) && bestK == 0; K++) {
             std::vector<PyrBand> bt((size_t)nl * K);
             for (int k = 0; k < K; k++) {
                 int a = (int)((long long)k * Hl / K), e = (int)((long long)(k + 1) * Hl / K);

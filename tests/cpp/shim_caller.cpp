@@ -496,7 +496,8 @@ static void run_stereo(FILE* in, FILE* out) {
     const auto l = rd<uint8_t>(in), r = rd<uint8_t>(in);
     const auto mb = rd<float>(in);
     const int W = whn[0], H = whn[1], NF = whn[2];
-    thread_local StereoExtractors ex;
+    thread_local StereoExtractors tls;
+    StereoExtractors& ex = tls;   // (a lambda on another thread must not name the thread_local itself)
     if (!ex.L || ex.w != W || ex.h != H || ex.nf != NF) {
         ex.L.reset(new orbslam2_amd::Extractor(NF, 1.2f, 8, 20, 7, 0, W, H));
         ex.R.reset(new orbslam2_amd::Extractor(NF, 1.2f, 8, 20, 7, 0, W, H));
