@@ -36,7 +36,14 @@ os.environ.setdefault("OMP_WAIT_POLICY", "active")
 
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md)
 VALU_PEAK_TOPS = 78.6            # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md)
-VALU_MEASURED_TOPS = 39.3        # tools/micro/valu_peak.hip: 4 cycles per wave64 VALU op (profiles/r02_valu_peak.txt)
+# chip-wide VALU issue rates measured by tools/micro/valu_issue.hip at 8 waves per SIMD (every
+# SIMD fed; profiles/r04_valu_issue.txt): v_fma_f32 1.78 cycles per wave64 instruction per SIMD
+# (MI355X_MICROARCH.md: 2 on a SIMD-32), 8.04e11 wave-instructions/s = 51.5 T lane-ops/s; an
+# integer VOP3 (v_xad_u32) 2.53 cycles, 5.30e11/s = 33.9 T lane-ops/s.  One wave alone on its SIMD
+# gets ~9 cycles per instruction.  The extraction kernels are integer-VOP3 code, so the integer
+# rate is their issue ceiling; the f32 rate is quoted beside it.
+VALU_MEASURED_TOPS = 33.9        # integer VOP3 issue ceiling (the extraction / matcher kernels' mix)
+VALU_MEASURED_F32_TOPS = 51.5    # v_fma_f32 issue ceiling
 STAGES = ["resize", "fast_detect", "reserved", "octree", "reserved2", "orient_blur_desc"]
 KERNELS = ["k_resize", "k_fast_cell", None, "k_octree", None, "k_orient_desc"]
 PMC_TRAFFIC = ROOT / "profiles" / "r03_pmc_traffic.json"   # tools/pmc_run.sh + tools/pmc_traffic.py
@@ -214,7 +221,9 @@ def extraction_roofline(stage_ms, ncalls, lw, lh, n_pre, n_out, W, H, NF, Bs):
             ach = ops / (ms * 1e-3) / 1e12
             k["valu"] = {"lane_ops_per_launch": ops, "achieved_tops": round(ach, 3), "peak": VALU_PEAK_TOPS,
                          "frac": round(ach / VALU_PEAK_TOPS, 4), "measured_issue_peak": VALU_MEASURED_TOPS,
-                         "frac_of_measured_issue_peak": round(ach / VALU_MEASURED_TOPS, 4)}
+                         "frac_of_measured_issue_peak": round(ach / VALU_MEASURED_TOPS, 4),
+                         "frac_of_measured_f32_issue_peak": round(ach / VALU_MEASURED_F32_TOPS, 4),
+                         "issue_peak_source": "profiles/r04_valu_issue.txt (8 waves/SIMD; int VOP3 / f32 FMA)"}
             util = pmc_lane_util(name, W, H, NF, Bs)
             if util is not None:
                 k["valu"]["active_lane_frac"] = util
@@ -950,7 +959,7 @@ def bench_extras(args, amd, dev):
     c = buf["cnt"].cpu().numpy().astype(np.int64)
     pairs = float((c[:-1] * c[1:]).sum())
     # 16 lane-ops per pair (8 xor + 8 bcnt on dword pairs); 78.6 T lane-ops/s nominal (4 SIMD x 32
-    # lanes per CU per clock), 39.3 T measured for wave64 issue (profiles/r02_valu_peak.txt)
+    # lanes per CU per clock), 33.9 T measured for integer VOP3 issue at 8 waves per SIMD (profiles/r04_valu_issue.txt)
     peak_pairs = VALU_PEAK_TOPS * 1e12 / 16
     out["knn2_bruteforce"] = {"pairs_per_s": round(pairs / dt, 1), "ms_per_batch": round(dt * 1e3, 4),
                               "frame_pairs": B, "roofline": {"bound": "valu", "unit": "pairs/s",
@@ -1526,6 +1535,7 @@ def main():
                                    "achieved": round(ach, 3), "unit": "TOP/s", "peak": VALU_PEAK_TOPS,
                                    "frac": round(ach / VALU_PEAK_TOPS, 4), "measured_issue_peak": VALU_MEASURED_TOPS,
                                    "frac_of_measured_issue_peak": round(ach / VALU_MEASURED_TOPS, 4),
+                                   "frac_of_measured_f32_issue_peak": round(ach / VALU_MEASURED_F32_TOPS, 4),
                                    "ops_source": PMC_VALU.name}
     if not args.no_lba:
         progress(rank, "local BA (config 4)")

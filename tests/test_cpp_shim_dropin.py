@@ -166,8 +166,7 @@ def _py_fuse_resolve(best, vec, n_slots, slot0, bad0, extra0):
                 in_kf[b] = s
             else:
                 slots[s] = -1
-        extra[b] += extra[a]
-        extra[a] = 0
+        extra[b] += extra[a]   # (the replaced point keeps its stale count, as the mock does)
 
     n_fused = 0
     for v in vec:
