@@ -272,7 +272,8 @@ def test_shim_search_for_triangulation(shim, tmp_path, only_stereo, check_ori):
     assert r.returncode == 0, r.stderr
     n, pairs = _read(outp, np.int32, np.int32)
     want = np.stack([np.flatnonzero(m_ref >= 0), m_ref[m_ref >= 0]], 1).astype(np.int32)
-    assert int(n[0]) == n_ref and np.array_equal(pairs.reshape(-1, 2), want) and n_ref > 50
+    assert int(n[0]) == n_ref and np.array_equal(pairs.reshape(-1, 2), want)
+    assert n_ref > (10 if only_stereo else 50)
 
 
 def _bow(levelsup=3, seed=12):
