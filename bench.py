@@ -46,8 +46,8 @@ VALU_MEASURED_TOPS = 33.9        # integer VOP3 issue ceiling (the extraction / 
 VALU_MEASURED_F32_TOPS = 51.5    # v_fma_f32 issue ceiling
 STAGES = ["resize", "fast_detect", "reserved", "octree", "reserved2", "orient_blur_desc"]
 KERNELS = ["k_resize", "k_fast_cell", None, "k_octree", None, "k_orient_desc"]
-PMC_TRAFFIC = ROOT / "profiles" / "r03_pmc_traffic.json"   # tools/pmc_run.sh + tools/pmc_traffic.py
-PMC_VALU = ROOT / "profiles" / "r03_valu_pmc.json"         # tools/gpu_valu_pmc.sh + tools/pmc_valu.py
+PMC_TRAFFIC = ROOT / "profiles" / "r04_pmc_traffic.json"   # tools/pmc_run.sh + tools/pmc_traffic.py
+PMC_VALU = ROOT / "profiles" / "r04_valu_pmc.json"         # tools/gpu_valu_pmc.sh + tools/pmc_valu.py
 
 
 def pmc_traffic(kernel, W, H, NF, Bs):
@@ -81,7 +81,7 @@ def pmc_valu_ops(kernel, W, H, NF, Bs):
         return None
 
 
-PMC_LANES = ROOT / "profiles" / "r03_lanes_pmc.json"   # tools/pmc_run.sh lanes ... + tools/pmc_lanes.py
+PMC_LANES = ROOT / "profiles" / "r04_lanes_pmc.json"   # tools/pmc_run.sh lanes ... + tools/pmc_lanes.py
 
 
 def pmc_lane_util(kernel, W, H, NF, Bs):
@@ -1439,6 +1439,7 @@ def main():
     t0 = time.perf_counter()
     for s in range(args.steps):
         step(args.warmup + s)
+    t_enq = time.perf_counter() - t0   # host time to enqueue the K steps (the GPU runs behind it)
     torch.cuda.synchronize(dev)
     if world > 1:
         torch.distributed.barrier()
@@ -1483,6 +1484,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(1000 * dt / args.steps, 4),
+        "host_enqueue_ms_per_step": round(1000 * t_enq / args.steps, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

@@ -4263,12 +4263,13 @@ int lba_group_create(const int* devices, int n, lba_group** out) {
     // The device-side exchange needs every rank on a device of its own: ranks sharing a device
     // may find their streams on one hardware queue, where a rank's waiting k_grp_sync blocks the
     // peer it waits for (seen as timeouts in a long-lived process with many streams).  Ranks on one
-    // device therefore use the host-ordered exchange, unless ORB_LBA_GROUP_DEVICE=1 (the test hook:
-    // two ranks, the second on a high-priority stream, i.e. another hardware queue)
+    // device therefore use the host-ordered exchange, unless ORB_LBA_GROUP_DEVICE=1 (the test hook
+    // that rehearses the device-side protocol of an N-GPU node on one device: every rank after the
+    // first on a CU-masked stream of its own, which the runtime gives a dedicated hardware queue)
     bool distinct = true;
     for (int a = 0; a < n; a++)
         for (int b2 = a + 1; b2 < n; b2++) distinct = distinct && devices[a] != devices[b2];
-    const bool forceDev = std::getenv("ORB_LBA_GROUP_DEVICE") != nullptr && n == 2;
+    const bool forceDev = std::getenv("ORB_LBA_GROUP_DEVICE") != nullptr;
     g->hostPath = std::getenv("ORB_LBA_GROUP_HOST") != nullptr || (!distinct && !forceDev);
     for (int r = 0; r < n; r++) {
         g->ranks[r] = {g, r};
@@ -4302,19 +4303,25 @@ int lba_group_create(const int* devices, int n, lba_group** out) {
             int st = group_alloc_fine(devices[r], 256, reinterpret_cast<void**>(&g->sync[r]));
             if (st) { lba_group_destroy(g); return st; }
         }
-    if (!g->hostPath && !distinct) {   // (the test hook) rank 1 on the device's high-priority queue
-        int lo = 0, hi = 0;
-        (void)hipSetDevice(devices[1]);
-        lba_context* c1 = g->ctx[1];
-        hipStream_t hs = nullptr;
-        if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
-            hipStreamCreateWithPriority(&hs, hipStreamNonBlocking, hi) != hipSuccess) {
-            lba_group_destroy(g);
-            return ORB_EGPU;
+    if (!g->hostPath && !distinct) {   // (the test hook) ranks 1.. each on a hardware queue of its own
+        for (int r = 1; r < n; r++) {
+            (void)hipSetDevice(devices[r]);
+            lba_context* cr = g->ctx[r];
+            int cus = 0;
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, devices[r]) != hipSuccess || cus <= 0) {
+                lba_group_destroy(g);
+                return ORB_EGPU;
+            }
+            std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0xFFFFFFFFu);   // every CU
+            hipStream_t hs = nullptr;
+            if (hipExtStreamCreateWithCUMask(&hs, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+                lba_group_destroy(g);
+                return ORB_EGPU;
+            }
+            if (cr->stream && cr->ownStream) (void)hipStreamDestroy(cr->stream);
+            cr->stream = hs;
+            cr->ownStream = true;
         }
-        if (c1->stream && c1->ownStream) (void)hipStreamDestroy(c1->stream);
-        c1->stream = hs;
-        c1->ownStream = true;
     }
     *out = g;
     return ORB_OK;

@@ -24,11 +24,14 @@ def _devices(n):
     (2, dict(), True),                                                                  # host-ordered exchange
     (3, dict(stereo_frac=0.5, seed=7, outlier_frac=0.15), True),
     (2, dict(corridor=True, n_local=60, n_fixed=4, n_points=8000, seed=21), False),     # multi-workgroup solve
+    (4, dict(), False),                                                                 # device-side, 4 ranks
+    (8, dict(n_points=1600, seed=5, stereo_frac=0.3), False),                           # device-side, 8 ranks
 ])
 def test_group_matches_single_context_and_oracle(amd, monkeypatch, n, kw, host):
     """host=False: the device-side exchange (flag words + peer reads; slots captured into graphs
     when the ranks have devices of their own) — on a one-GPU machine forced with
-    ORB_LBA_GROUP_DEVICE=1, which puts the second rank on the device's high-priority queue;
+    ORB_LBA_GROUP_DEVICE=1, which puts every rank after the first on a CU-masked stream (a hardware
+    queue of its own), so 4 and 8 ranks rehearse an 8-GPU node's epochs and rank-ordered sums;
     host=True: the host-ordered callback with cross-stream events (what ranks sharing a device
     use by default)."""
     from orb_slam2_amd import synth
@@ -49,7 +52,7 @@ def test_group_matches_single_context_and_oracle(amd, monkeypatch, n, kw, host):
     assert np.array_equal(got["edge_erase"], one["edge_erase"])
     _compare(O.lba_solve(pb), got)
     ms, nx = grp.stats()
-    host_path = host or (not distinct and n != 2)
+    host_path = host
     assert nx > 0 and (ms > 0.0 if host_path else ms == 0.0)   # (event timing only on the host-ordered path)
     # reused group: bitwise the same
     again = grp.solve(pb)
