@@ -5,9 +5,21 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <mutex>
 #include <vector>
 
 #include "../../include/orbslam2_amd.h"
+
+namespace orbamd {
+// One process-wide lock between a handle's legacy-stream setup calls (synchronous hipMemcpy /
+// hipMemset / hipMalloc / hipFree) and the local BA's HIP graph capture: a legacy-stream call that
+// meets another thread's capture fails the call and invalidates the capture (Tracking
+// and LocalMapping threads call into the library at once).  Steady-state launches do not take it.
+inline std::mutex& legacy_capture_mutex() {
+    static std::mutex m;
+    return m;
+}
+}   // namespace orbamd
 
 #define ORB_HIP_TRY(expr)                                                                   \
     do {                                                                                    \

@@ -38,10 +38,26 @@ constexpr int kMinBorder = kEdge - 3;
 constexpr int kPatch = 31;
 constexpr int kHalfPatch = 15;
 
-// bit_pattern_31_ as floats (exact small integers), one 16-byte load per point pair in the descriptor loop
-__constant__ __attribute__((aligned(16))) float c_patternf[256 * 4] = {
+// bit_pattern_31_ (x0, y0, x1, y1 per pair) as floats (exact small integers), stored per pair as
+// (x0, x1, y0, y1): one 16-byte load per point pair in the descriptor loop, and the two points'
+// x and y coordinates land in register pairs for the packed-f32 rotation
+constexpr int kPatternI[256 * 4] = {
 #include "orb_pattern.inc"
 };
+struct PatternF {
+    float v[256 * 4];
+};
+constexpr PatternF pattern_xxyy() {
+    PatternF p{};
+    for (int i = 0; i < 256; i++) {
+        p.v[4 * i] = (float)kPatternI[4 * i];
+        p.v[4 * i + 1] = (float)kPatternI[4 * i + 2];
+        p.v[4 * i + 2] = (float)kPatternI[4 * i + 1];
+        p.v[4 * i + 3] = (float)kPatternI[4 * i + 3];
+    }
+    return p;
+}
+__constant__ __attribute__((aligned(16))) PatternF c_patternf = pattern_xxyy();
 
 struct LevelGeom {
     int w, h, pitch;
@@ -375,16 +391,14 @@ __global__ __launch_bounds__(256) void k_resize(Geom g, int l, uint8_t* __restri
 // the input, :1223): level 1 is computed straight from the caller's frame (L0Src, L2-resident
 // buffer loads), so the LDS holds levels 1..7 only — the odd levels in one buffer, the even ones in
 // the other.
-// output rows per k_pyramid thread iteration (rows r, r + 4, ..: their source-row loads in flight together)
-#ifndef ORB_PYR_ROWS
-#define ORB_PYR_ROWS 2
-#endif
-constexpr int kPyrRows = ORB_PYR_ROWS;
 // LDS budget of one k_pyramid workgroup (both level buffers + the coefficient tables)
 #ifndef ORB_PYR_LDS_BUDGET_KB
 #define ORB_PYR_LDS_BUDGET_KB 32
 #endif
 constexpr int kPyrLdsBudget = ORB_PYR_LDS_BUDGET_KB * 1024;
+
+// output rows per k_pyramid thread iteration (rows r, r + 4, ..: their source-row loads in flight together)
+constexpr int kPyrRows = 2;
 
 struct PyrBand {
     int s0, n;   // rows [s0, s0 + n) of a level computed by a band
@@ -423,6 +437,10 @@ __device__ __forceinline__ void pyr_band_level(const LevelGeom& D, const LevelGe
         const uint32_t sh = (uint32_t)(xb & 3);
         const int valid = D.w - dx0;   // pitch padding stays 0
         const uint32_t keep = valid < 4 ? (1u << (8 * valid)) - 1u : 0xFFFFFFFFu;
+        // (tried: a thread walking its rows in order, reusing the horizontal sums of a source row
+        // shared with the previous output row — 1.2 source rows per output row instead of 2 — was
+        // slower: one row of loads in flight instead of two rows' four)
+        const __amdgpu_buffer_rsrc_t ro = buf_rsrc(out, (uint32_t)(D.pitch * (db.s0 + db.n)));
         for (int r = rp; r < db.n; r += 4 * kPyrRows) {
             int rr[kPyrRows];
             uint2 cy[kPyrRows];
@@ -466,19 +484,20 @@ __device__ __forceinline__ void pyr_band_level(const LevelGeom& D, const LevelGe
             }
 #pragma unroll
             for (int u = 0; u < kPyrRows; u++) {
+                // cv's (h0 b0 + h1 b1 + 2^21) >> 22 with the row weights scaled by 4 (the LDS table
+                // holds them so): the result is byte 3 of the 32-bit sum — h <= 255 * 2049 (19 bits)
+                // and 4 b <= 8196 fit v_mad_u32_u24, the sum stays below 2^32 (255 * 2049^2 * 4 + 2^23)
+                // and its top byte never exceeds 255, so no shift and no clamp; two v_perm + one or
+                // pack the four
                 const uint32_t b0 = cy[u].y & 0xFFFF, b1 = cy[u].y >> 16;
-                uint32_t packed = 0u;
+                uint32_t v[4];
 #pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    // 19-bit sums x 11-bit weights fit 24 x 24 -> 32 bits: v_mad_u32_u24, not the
-                    // quarter-rate v_mul_lo_u32
-                    const uint32_t v = min((__umul24(hs[u][0][j], b0) + __umul24(hs[u][1][j], b1) + (1u << 21)) >> 22, 255u);
-                    packed |= v << (8 * j);
-                }
+                for (int j = 0; j < 4; j++) v[j] = __umul24(hs[u][1][j], b1) + (__umul24(hs[u][0][j], b0) + (1u << 23));
                 if (u > 0 && r + 4 * u >= db.n) break;
-                const uint32_t pv = packed & keep;
+                const uint32_t pv = (__builtin_amdgcn_perm(v[1], v[0], 0x0c0c0703u) |
+                                     __builtin_amdgcn_perm(v[3], v[2], 0x07030c0cu)) & keep;
                 *reinterpret_cast<uint32_t*>(nxt + rr[u] * dp + dx0) = pv;
-                *reinterpret_cast<uint32_t*>(out + (size_t)(db.s0 + rr[u]) * D.pitch + dx0) = pv;
+                __builtin_amdgcn_raw_buffer_store_b32(pv, ro, (int)__umul24((uint32_t)(db.s0 + rr[u]), (uint32_t)D.pitch) + dx0, 0, 0);
             }
         }
     }
@@ -508,8 +527,12 @@ __global__ __launch_bounds__(256) void k_pyramid(Geom g, L0Src z, uint8_t* __res
         // the level's column coefficients and the band's row coefficients -> LDS
         uint2* XT = tabL;
         uint2* YT = tabL + D.w;
-        for (int i = tid; i < D.w + db.n; i += 256)
-            tabL[i] = i < D.w ? rztab[D.rzX + i] : rztab[D.rzY + db.s0 + (i - D.w)];
+        // (row weights scaled by 4 here: w0 <= 2049, so the shift carries nothing into w1's half)
+        for (int i = tid; i < D.w + db.n; i += 256) {
+            uint2 c = i < D.w ? rztab[D.rzX + i] : rztab[D.rzY + db.s0 + (i - D.w)];
+            if (i >= D.w) c.y <<= 2;
+            tabL[i] = c;
+        }
         __syncthreads();
         uint8_t* nxt = (l & 1) ? bufOdd : bufEven;
         const uint8_t* cur = (l & 1) ? bufEven : bufOdd;
@@ -534,24 +557,33 @@ __global__ __launch_bounds__(256) void k_pyramid(Geom g, L0Src z, uint8_t* __res
 // S = max over the 16 circular 9-arcs of min(v - p) (dark) or min(p - v) (bright), minus 1.
 // OpenCV's cornerScore<16>(threshold t) == S for every pixel that is a corner at t, and a
 // pixel is a corner at t iff S >= t.  Stored as S if S >= tmin else 0.
-__device__ __forceinline__ int fast_score(const int v, const int p[16]) {
-    // 9-arc minima / maxima as min3 / max3 of three 3-arcs (v_min3_i32 / v_max3_i32)
-    int d[16];
+// (Before gfx950's packed 3-input minimum: the 9-arc minima / maxima as min3 / max3 of three
+// 3-arcs in 32-bit integers, one chain per polarity — 114 VALU operations per survivor.)
+// Both polarities run in one packed-f16 register (gfx950 v_pk_minimum3_f16 /
+// v_pk_maximum3_f16): lane pair k = (v - p_k, p_k - v).  The low half runs the dark chain (max over
+// arcs of the arc minimum of v - p), the high half the bright one (max over arcs of the arc minimum
+// of p - v); S = max(lo, hi) - 1.  Integers up to
+// 2048 are exact in f16.  (1024 + x, -(1024 + x)) is one multiply-add on the f16 bit patterns
+// (x * 0x10001 + 0xE4006400: 0x6400 + x is 1024 + x for x < 1024, no carry between the halves), and
+// their difference gives each pair exactly.
+__device__ __forceinline__ int fast_score_pk(const int v, const int p[16]) {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const h2 vn = __builtin_bit_cast(h2, (uint32_t)v * 0x10001u + 0xE4006400u);
+    h2 d[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) d[k] = v - p[k];
-    int mn3[16], mx3[16];
+    for (int k = 0; k < 16; k++) d[k] = vn - __builtin_bit_cast(h2, (uint32_t)p[k] * 0x10001u + 0xE4006400u);
+    h2 m3[16], a9[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        mn3[k] = min(min(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
-        mx3[k] = max(max(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
-    }
-    int A = -1024, Bp = 1024;
+    for (int k = 0; k < 16; k++)
+        m3[k] = __builtin_elementwise_minimum(__builtin_elementwise_minimum(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        A = max(A, min(min(mn3[k], mn3[(k + 3) & 15]), mn3[(k + 6) & 15]));
-        Bp = min(Bp, max(max(mx3[k], mx3[(k + 3) & 15]), mx3[(k + 6) & 15]));
-    }
-    return max(A, -Bp) - 1;
+    for (int k = 0; k < 16; k++)
+        a9[k] = __builtin_elementwise_minimum(__builtin_elementwise_minimum(m3[k], m3[(k + 3) & 15]), m3[(k + 6) & 15]);
+    h2 s = __builtin_elementwise_maximum(__builtin_elementwise_maximum(a9[0], a9[1]), a9[2]);
+#pragma unroll
+    for (int k = 3; k < 15; k += 2) s = __builtin_elementwise_maximum(__builtin_elementwise_maximum(s, a9[k]), a9[k + 1]);
+    s = __builtin_elementwise_maximum(s, a9[15]);
+    return (int)(s.x > s.y ? s.x : s.y) - 1;
 }
 
 constexpr int kTileW = 64, kTileH = 16;   // blur tiles
@@ -804,7 +836,7 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
         q[10] = pw[cc - 2 * PWS - 2]; q[11] = pw[cc - PWS - 3];
         q[12] = pw[cc - 3];           q[13] = pw[cc + PWS - 3];
         q[14] = pw[cc + 2 * PWS - 2]; q[15] = pw[cc + 3 * PWS - 1];
-        const int S = fast_score(pw[cc], q);
+        const int S = fast_score_pk(pw[cc], q);
         if (S >= g.tmin && S > 0) bw[patchBytes + (y + 1) * SCS + x + 1] = (uint8_t)S;
     }
     __syncthreads();
@@ -1600,7 +1632,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
     for (int it = 0; it < 3; it++) task[it] = c_htask[lane + 64 * it];
     float4 ppair[4];
 #pragma unroll
-    for (int r = 0; r < 4; r++) ppair[r] = reinterpret_cast<const float4*>(c_patternf)[r * 64 + lane];
+    for (int r = 0; r < 4; r++) ppair[r] = reinterpret_cast<const float4*>(c_patternf.v)[r * 64 + lane];
 
     // 1. patch
     if (x - 24 >= 0 && x + 24 <= L.w && y - 21 >= 0 && y + 21 < L.h) {
@@ -1659,7 +1691,11 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
     // 3a. horizontal Gaussian pass: RS[r][c] = sum_q k_q * raw(y-21+r, x-18+c-3+q) on the columns
     //     the pattern can reach (c_htask).  Task (r, c0) computes columns c0 .. c0+7 from the 16
     //     patch bytes c0+3 .. c0+18, re-based by four alignbytes at the task's byte offset; output i
-    //     takes bytes c0+3+i .. +6 (taps -3 .. 0, kA) and c0+7+i .. +10 (taps +1 .. +3, kB)
+    //     takes bytes c0+3+i .. +6 (taps -3 .. 0, kA) and c0+7+i .. +10 (taps +1 .. +3, kB).
+    //     (Tried: the whole 43 x 37 pass on the matrix cores, RS^T = Gh^T P^T by nine
+    //     v_mfma_i32_16x16x64_i8 over the i8-biased window and a host-built banded tap matrix —
+    //     bit-exact, 17 % fewer VALU per keypoint, but the extraction step 3-5 % slower in
+    //     same-box A/B runs, with 16-bit or 8-byte row-sum stores alike; kept out.)
     {
 #pragma unroll
         for (int it = 0; it < 3; it++) {
@@ -1698,23 +1734,23 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
     const float a = ac, bb = bs;
     const int k0 = (int)(kA & 0xff), k1 = (int)((kA >> 8) & 0xff), k2 = (int)((kA >> 16) & 0xff),
               k3 = (int)(kA >> 24);   // taps 0..3 (3 = centre); taps 4..6 mirror 2..0
-    // A sample's rotated offset: the products px a, py b (px b, py a) as one v_pk_mul_f32 each
-    // (the same IEEE products and sums as the scalar form), cvRound by the 1.5 * 2^23 magic add
-    // (round-half-even for |x| < 2^22), and the row-sum address from the magic-biased bit
-    // patterns directly: __umul24 reads Y + 2^22 from the low 24 bits and the biases fold into
-    // one constant (mod 2^32).  The vertical taps pair up (0, 6), (1, 5), (2, 4) for
-    // v_dot2_u32_u16; the integer sum is the same.
+    // The rotated offsets of a pair's two points at once in packed f32 (v_pk_mul_f32 / v_pk_add_f32:
+    // the same IEEE products and sums as the scalar form x a - y b, x b + y a, fp-contract off),
+    // cvRound by the 1.5 * 2^23 magic add (round-half-even for |x| < 2^22), and the row-sum address
+    // from the magic-biased bit patterns directly: __umul24 reads Y + 2^22 from the low 24 bits and
+    // the biases fold into one constant (mod 2^32).  The vertical taps pair up (0, 6), (1, 5),
+    // (2, 4) for v_dot2_u32_u16; the integer sum is the same.
     typedef float f2 __attribute__((ext_vector_type(2)));
     typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-    const f2 cs = {a, bb}, sc = {bb, a};
+    const f2 av = {a, a}, bv = {bb, bb};
     const uint32_t kk0 = (uint32_t)k0 * 0x10001u, kk1 = (uint32_t)k1 * 0x10001u, kk2 = (uint32_t)k2 * 0x10001u;
     constexpr uint32_t kMagicBits = 0x4B400000u;   // bits of 1.5 * 2^23
     constexpr uint32_t kRsOff = 2u * (18u * kOdRsW + 18u) - 2u * kOdRsW * (kMagicBits & 0xFFFFFFu) - 2u * kMagicBits;
-    auto sample = [&](f2 p) -> int {
-        const f2 u = p * cs, w = p * sc;
-        const float xf = u.x - u.y, yf = w.x + w.y;
-        const uint32_t xb = __float_as_uint(xf + 12582912.0f), yb = __float_as_uint(yf + 12582912.0f);
-        const uint32_t off = __umul24(yb, 2u * kOdRsW) + 2u * xb + kRsOff;   // 2 ((Y + 18) kOdRsW + X + 18)
+    const f2 magic = {12582912.0f, 12582912.0f};
+    // acc of one point, clamped so that acc >> 16 is the saturated blurred value (the 8-bit taps
+    // sum to 257, so an unclamped sum can reach 257 << 16)
+    auto sample = [&](uint32_t xb, uint32_t yb) -> uint32_t {
+        const uint32_t off = __umul24(yb, 2u * kOdRsW) + (2u * xb + kRsOff);   // 2 ((Y + 18) kOdRsW + X + 18)
         const uint16_t* c0 = reinterpret_cast<const uint16_t*>(reinterpret_cast<const unsigned char*>(RS) + off);
         const uint32_t p06 = (uint32_t)c0[0] | ((uint32_t)c0[6 * kOdRsW] << 16);
         const uint32_t p15 = (uint32_t)c0[kOdRsW] | ((uint32_t)c0[5 * kOdRsW] << 16);
@@ -1723,14 +1759,19 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
         acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, p06), __builtin_bit_cast(u16x2, kk0), acc, false);
         acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, p15), __builtin_bit_cast(u16x2, kk1), acc, false);
         acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, p24), __builtin_bit_cast(u16x2, kk2), acc, false);
-        return (int)min(acc >> 16, 255u);
+        return min(acc, 0x00FFFFFFu);
     };
     uint64_t words[4];
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-        const float4 pp = ppair[r];   // pair r * 64 + lane: byte pi/8, bit pi%8
-        const f2 p0 = {pp.x, pp.y}, p1 = {pp.z, pp.w};
-        words[r] = __ballot(sample(p0) < sample(p1));
+        const float4 pp = ppair[r];   // pair r * 64 + lane (byte pi/8, bit pi%8): (x0, x1, y0, y1)
+        const f2 px = {pp.x, pp.y}, py = {pp.z, pp.w};
+        const f2 xf = px * av - py * bv, yf = px * bv + py * av;
+        const f2 xm = xf + magic, ym = yf + magic;
+        const uint32_t s0 = sample(__float_as_uint(xm.x), __float_as_uint(ym.x));
+        const uint32_t s1 = sample(__float_as_uint(xm.y), __float_as_uint(ym.y));
+        // blurred(p0) < blurred(p1) <=> acc0 < (acc1 with its low 16 bits cleared)
+        words[r] = __ballot(s0 < (s1 & 0xFFFF0000u));
     }
 #ifdef ORB_TIMING
     if (lane == 0 && b == 0 && (q == 0 || q == 300 || q == 700))
@@ -2057,6 +2098,7 @@ static void release_buffers(orb_extractor* ex) {
 
 static int ensure_geom(orb_extractor* ex, int w, int h) {
     if (w == ex->gw && h == ex->gh) return ORB_OK;
+    std::lock_guard<std::mutex> lk(legacy_capture_mutex());   // legacy-stream setup calls (common.h)
     Geom g;
     int st = build_geom(ex->p, w, h, &g);
     if (st) return st;
@@ -2174,6 +2216,7 @@ static int ensure_capacity(orb_extractor* ex, int B) {
     if ((size_t)B <= ex->capFrames && fb <= ex->capFrameBytes && sl <= ex->capSlots && ou <= ex->capOut &&
         ce <= ex->capCells)
         return ORB_OK;
+    std::lock_guard<std::mutex> lk(legacy_capture_mutex());   // legacy-stream setup calls (common.h)
     ORB_HIP_TRY(hipStreamSynchronize(ex->stream));
     release_buffers(ex);
     const size_t nb = std::max<size_t>(B, 1);
@@ -2392,7 +2435,10 @@ int orb_extractor_create(const orb_extractor_params* params, int device, int max
     int k[7];
     gauss7_int(k);
     ex->blurK[0] = k[3]; ex->blurK[1] = k[2]; ex->blurK[2] = k[1]; ex->blurK[3] = k[0];
-    if (hipStreamCreateWithFlags(&ex->stream, hipStreamNonBlocking) != hipSuccess) { delete ex; return ORB_EGPU; }
+    {
+        std::lock_guard<std::mutex> lk(legacy_capture_mutex());
+        if (hipStreamCreateWithFlags(&ex->stream, hipStreamNonBlocking) != hipSuccess) { delete ex; return ORB_EGPU; }
+    }
     st = ensure_geom(ex, max_w, max_h);
     if (!st) st = ensure_capacity(ex, max_batch);
     if (st) { orb_extractor_destroy(ex); return st; }
@@ -2402,6 +2448,7 @@ int orb_extractor_create(const orb_extractor_params* params, int device, int max
 
 void orb_extractor_destroy(orb_extractor* ex) {
     if (!ex) return;
+    std::lock_guard<std::mutex> lk(legacy_capture_mutex());   // hipFree (common.h)
     (void)hipSetDevice(ex->device);
     if (ex->stream) (void)hipStreamSynchronize(ex->stream);
     release_buffers(ex);
@@ -2631,6 +2678,7 @@ int orb_extractor_last_counts(orb_extractor* ex, int frame, int* pre_counts, int
     const Geom& g = ex->g;
     std::vector<int> cc(g.cellsPerFrame), lc(g.nlevels);
     ORB_HIP_TRY(hipStreamSynchronize(ex->lastStream ? ex->lastStream : ex->stream));
+    std::lock_guard<std::mutex> lk(legacy_capture_mutex());   // legacy-stream copies (common.h)
     ORB_HIP_TRY(hipMemcpy(cc.data(), ex->d_cellCount + (size_t)frame * g.cellsPerFrame, cc.size() * 4,
                           hipMemcpyDeviceToHost));
     ORB_HIP_TRY(hipMemcpy(lc.data(), ex->d_levelCount + (size_t)frame * g.nlevels, lc.size() * 4,

@@ -3410,8 +3410,8 @@ int lba_debug_buffer(lba_context* c, int which, double* out, size_t n) {
     }
     if (!src || n > avail) return ORB_EINVAL;
     ORB_HIP_TRY(hipSetDevice(c->device));
+    ORB_HIP_TRY(hipMemcpyAsync(out, src, 8 * n, hipMemcpyDeviceToHost, c->stream));   // own stream (§8b threading)
     ORB_HIP_TRY(hipStreamSynchronize(c->stream));
-    ORB_HIP_TRY(hipMemcpy(out, src, 8 * n, hipMemcpyDeviceToHost));
     return (int)avail;
 }
 
@@ -3882,11 +3882,15 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
                     return ORB_OK;
                 }
             hipGraph_t g = nullptr;
-            ORB_HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
             int st = ORB_OK;
-            for (int i = 0; i < nslots && !st; i++) st = enqueue_slot(iterations, nullptr, firstGroup && i == 0);
-            if (!st && close) enqueue_close(iterations);
-            const hipError_t ce = hipStreamEndCapture(s, &g);
+            hipError_t ce;
+            {   // no other thread's legacy-stream setup call inside the capture (common.h)
+                std::lock_guard<std::mutex> lk(legacy_capture_mutex());
+                ORB_HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+                for (int i = 0; i < nslots && !st; i++) st = enqueue_slot(iterations, nullptr, firstGroup && i == 0);
+                if (!st && close) enqueue_close(iterations);
+                ce = hipStreamEndCapture(s, &g);
+            }
             if (st) { if (g) (void)hipGraphDestroy(g); return st; }
             if (ce != hipSuccess) return ORB_EGPU;
             const hipError_t ie = hipGraphInstantiate(out, g, nullptr, nullptr, 0);

@@ -1029,6 +1029,7 @@ static void mfree(orb_matcher* m) {
 
 static int mensure(orb_matcher* m, size_t pairs, size_t pts) {
     if (pairs <= m->capPairs && pts <= m->capPts) return ORB_OK;
+    std::lock_guard<std::mutex> lk(legacy_capture_mutex());   // hipMalloc / hipFree (common.h)
     ORB_HIP_TRY(hipStreamSynchronize(m->stream));
     pairs = std::max(pairs, m->capPairs);
     pts = std::max(pts, m->capPts);
@@ -1071,6 +1072,7 @@ static int mensure(orb_matcher* m, size_t pairs, size_t pts) {
 
 static int mpin(orb_matcher* m, size_t bytes) {
     if (m->h_pin_bytes >= bytes) return ORB_OK;
+    std::lock_guard<std::mutex> lk(legacy_capture_mutex());   // (common.h)
     if (m->h_pin) (void)hipHostFree(m->h_pin);
     m->h_pin = nullptr;
     m->h_pin_bytes = 0;
@@ -1591,13 +1593,17 @@ int orb_matcher_create(int device, float nnratio, int check_ori, orb_matcher** o
     m->device = device;
     m->nnratio = nnratio;
     m->checkOri = check_ori ? 1 : 0;
-    if (hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess) { delete m; return ORB_EGPU; }
+    {
+        std::lock_guard<std::mutex> lk(legacy_capture_mutex());   // (common.h)
+        if (hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess) { delete m; return ORB_EGPU; }
+    }
     *out = m;
     return ORB_OK;
 }
 
 void orb_matcher_destroy(orb_matcher* m) {
     if (!m) return;
+    std::lock_guard<std::mutex> lk(legacy_capture_mutex());   // hipFree (common.h)
     (void)hipSetDevice(m->device);
     if (m->stream) (void)hipStreamSynchronize(m->stream);
     mfree(m);
