@@ -2122,7 +2122,6 @@ static int ensure_geom(orb_extractor* ex, int w, int h) {
     }
     ORB_HIP_TRY(hipSetDevice(ex->device));
     if (ex->d_rztab) (void)hipFree(ex->d_rztab);
-    if (ex->d_bands) (void)hipFree(ex->d_bands);
     ex->d_rztab = nullptr;
     if (hipMalloc((void**)&ex->d_rztab, std::max<size_t>(tab.size(), 1) * sizeof(uint2)) != hipSuccess) return ORB_ENOMEM;
     ORB_HIP_TRY(hipMemcpy(ex->d_rztab, tab.data(), tab.size() * sizeof(uint2), hipMemcpyHostToDevice));

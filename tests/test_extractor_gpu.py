@@ -42,6 +42,18 @@ def test_extract_matches_oracle(amd, W, H, nf, seed):
         _compare(ref, kps, desc)
 
 
+def test_extract_geometry_changes_on_one_handle(amd):
+    """One handle created for the default bound (1280 x 1024), then fed 640 x 480, KITTI and 640 x 480
+    again: every geometry change rebuilds the resize tables and the pyramid band table (which an
+    earlier build freed twice, leaving a sticky HIP error that failed the next call)."""
+    ex = amd.ORBextractor(1000, 1.2, 8, 20, 7)
+    p = O.params(1000)
+    for W, H, seed in ((640, 480, 0x5EED0001), (1241, 376, 0x5EED0003), (640, 480, 0x5EED0002)):
+        img = _frames(W, H, seed, 1)[0]
+        kps, desc = ex(img)
+        _compare(O.extract(p, img), kps, desc)
+
+
 def test_pyramid_matches_oracle(amd):
     W, H = 640, 480
     img = _frames(W, H, 0x5EED0001, 1)[0]
