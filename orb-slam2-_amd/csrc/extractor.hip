@@ -1577,6 +1577,12 @@ __constant__ uint16_t c_htask[192] = {
     0x2716, 0x2808, 0x2810, 0x2818, 0x290a, 0x2912, 0x291a, 0x2a0c, 0x2a14, 0xffff, 0xffff, 0xffff,
 };
 constexpr int kOdWaveBytes = kOdRows * kOdPW + kOdRows * kOdRsW * 2;
+#ifndef ORB_OD_KPW
+#define ORB_OD_KPW 2
+#endif
+// keypoint slots per wave (even): a slot's window loads overlap the previous slot's work
+constexpr int kOdKpw = ORB_OD_KPW;
+static_assert(kOdKpw % 2 == 0, "two register sets in turn");
 
 __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __restrict__ pyr, L0Src z,
                                                      const uint32_t* __restrict__ outKeys,
@@ -1600,33 +1606,20 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     int bx, b;
     xcd_block_2d(bx, b);
-    const int q = bx * 4 + wid;
+    const int q0 = (bx * 4 + wid) * kOdKpw;
     const int* lc = levelCount + (size_t)b * g.nlevels;
-    if (q == 0 && lane == 0) {
+    if (q0 == 0 && lane == 0) {
         int tot = 0;
         for (int l = 0; l < g.nlevels; l++) tot += lc[l];
         counts[b] = tot;
     }
-    if (q >= g.outPerFrame) return;
-    int l = 0;
-    while (l + 1 < g.nlevels && q >= g.lv[l + 1].outBase) l++;
-    const LevelGeom& L = g.lv[l];
-    const int local = q - L.outBase;
-    if (local >= lc[l]) return;
-    int outIdx = local;
-    for (int l2 = 0; l2 < l; l2++) outIdx += lc[l2];
-    if (outIdx >= cap) return;
-    const uint32_t key = outKeys[(size_t)b * g.outPerFrame + q];
-    const int x = kx_of(key) + kMinBorder, y = ky_of(key) + kMinBorder, resp = kr_of(key);
-    int pitch;
-    uint32_t imgBytes;
-    const uint8_t* img = level_img(g, z, pyr, b, l, pitch, imgBytes);
     uint32_t* P32 = reinterpret_cast<uint32_t*>(od_sm[wid]);
     uint16_t* RS = reinterpret_cast<uint16_t*>(od_sm[wid] + kOdRows * kOdPW);
     TSTAMP(t_od0);
 
     // the horizontal pass's task words and this lane's BRIEF point pairs: loaded first, so their
-    // latency hides under the window load and the moments (neither depends on the angle)
+    // latency hides under the window load and the moments (neither depends on the angle); both
+    // keypoints of the wave use them
     uint32_t task[3];
 #pragma unroll
     for (int it = 0; it < 3; it++) task[it] = c_htask[lane + 64 * it];
@@ -1634,168 +1627,225 @@ __global__ __launch_bounds__(256) void k_orient_desc(Geom g, const uint8_t* __re
 #pragma unroll
     for (int r = 0; r < 4; r++) ppair[r] = reinterpret_cast<const float4*>(c_patternf.v)[r * 64 + lane];
 
-    // 1. patch
-    if (x - 24 >= 0 && x + 24 <= L.w && y - 21 >= 0 && y + 21 < L.h) {
-        // lane = (row r0 of 4 per pass, aligned source dword k of 13): one buffer load per pass
-        // at a scalar row offset (rows past the window, or past the slab, read harmlessly and are
-        // never stored), the next dword of the row from the next lane by DPP wave_shl:1, the
-        // realigned dword stored (lanes with no patch dword write into the row-sum area, which
-        // step 3a overwrites)
-        const int gx0 = x - 24, sh = gx0 & 3, ga = gx0 - sh;
-        const uint32_t winOff = (uint32_t)(y - 21) * (uint32_t)pitch + (uint32_t)ga;
-        const __amdgpu_buffer_rsrc_t rs = buf_rsrc(img + winOff, imgBytes - winOff);
-        const int r0 = lane / 13, k = lane - 13 * r0;
-        const uint32_t laneOff = __umul24((uint32_t)r0, (uint32_t)pitch) + 4u * (uint32_t)k;
-        uint32_t* const sink = reinterpret_cast<uint32_t*>(RS) + lane;
-#pragma unroll
-        for (int rb = 0; rb < kOdRows; rb += 4) {
-            const uint32_t a = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)laneOff, rb * pitch, 0);
-            const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a, 0x130, 0xF, 0xF, false);
-            const int r = rb + r0;
-            const bool st = r0 < 4 && k < 12 && r < kOdRows;
-            *(st ? P32 + r * 12 + k : sink) = __builtin_amdgcn_alignbyte(nx, a, sh);
-        }
-    } else {
-        uint8_t* P8w = od_sm[wid];
-        for (int t = lane; t < kOdRows * kOdPW; t += 64) {
-            const int r = t / kOdPW, cc = t % kOdPW;
-            P8w[t] = img[(size_t)reflect101(y - 21 + r, L.h) * pitch + reflect101(x - 24 + cc, L.w)];
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-
-    TSTAMP(t_od1);
-    // 2. moments: lane = (row group vr, dword d); patch dword 2+d holds u = 4d-16 .. 4d-13
-    int m10 = 0, m01 = 0;
-    {
-        const int d = lane & 7, vr = lane >> 3;
-        for (int it = 0; it < 4; it++) {
-            const int v = it * 8 + vr - 15;
-            if (v > 15) continue;
-            // bytes j with |4d + j - 16| <= umax[|v|], i.e. j in [16 - um - 4d, 16 + um - 4d] ∩ [0, 3]
-            const uint32_t m = momMask[(v + 15) * 8 + d];
-            const uint32_t w1 = m & 0x01010101u;
-            const uint32_t wu = m & (0x03020100u + (uint32_t)(4 * d) * 0x01010101u);   // bytes u + 16 = 4d + j
-            const uint32_t pw = P32[(21 + v) * 12 + 2 + d];
-            const int s1 = (int)__builtin_amdgcn_udot4(pw, w1, 0u, false);
-            m10 += (int)__builtin_amdgcn_udot4(pw, wu, 0u, false) - 16 * s1;
-            m01 += v * s1;
-        }
-    }
-    m10 = wave_sum_dpp(m10);
-    m01 = wave_sum_dpp(m01);
-    const float angle = fast_atan2_dev((float)m01, (float)m10);
-
-    TSTAMP(t_od2);
-    // 3a. horizontal Gaussian pass: RS[r][c] = sum_q k_q * raw(y-21+r, x-18+c-3+q) on the columns
-    //     the pattern can reach (c_htask).  Task (r, c0) computes columns c0 .. c0+7 from the 16
-    //     patch bytes c0+3 .. c0+18, re-based by four alignbytes at the task's byte offset; output i
-    //     takes bytes c0+3+i .. +6 (taps -3 .. 0, kA) and c0+7+i .. +10 (taps +1 .. +3, kB).
-    //     (Tried: the whole 43 x 37 pass on the matrix cores, RS^T = Gh^T P^T by nine
-    //     v_mfma_i32_16x16x64_i8 over the i8-biased window and a host-built banded tap matrix —
-    //     bit-exact, 17 % fewer VALU per keypoint, but the extraction step 3-5 % slower in
-    //     same-box A/B runs, with 16-bit or 8-byte row-sum stores alike; kept out.)
-    {
-#pragma unroll
-        for (int it = 0; it < 3; it++) {
-            if (task[it] == 0xFFFFu) continue;
-            const int r = (int)(task[it] >> 8), c0 = (int)(task[it] & 0xFFu);
-            const int o = c0 + 3;
-            const uint32_t* row = P32 + r * 12 + (o >> 2);
-            const uint32_t sh = (uint32_t)(o & 3);
-            uint32_t d[5];
-#pragma unroll
-            for (int k = 0; k < 5; k++) d[k] = row[k];   // (past the row: bytes of unused columns)
-            uint32_t w[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
-            uint32_t out[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                const uint32_t A = (i & 3) == 0 ? w[i >> 2] : __builtin_amdgcn_alignbyte(w[(i >> 2) + 1], w[i >> 2], i & 3);
-                const int j = i + 4;
-                const uint32_t B = (j & 3) == 0 ? w[j >> 2] : __builtin_amdgcn_alignbyte(w[(j >> 2) + 1], w[j >> 2], j & 3);
-                const uint32_t sum = __builtin_amdgcn_udot4(B, kB, __builtin_amdgcn_udot4(A, kA, 0u, false), false);
-                out[i >> 1] |= sum << (16 * (i & 1));
-            }
-            uint32_t* rs32 = reinterpret_cast<uint32_t*>(RS + r * kOdRsW + c0);
-#pragma unroll
-            for (int k = 0; k < 4; k++) rs32[k] = out[k];
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-
-    TSTAMP(t_od3);
-    // 3b + 4. steered BRIEF: blurred(y+Y, x+X) = (sum_q k_q RS[Y+18+q][X+18] + 2^15) >> 16
-    float bs, ac;
-    glibc_sincosf(angle * g.factorPI, bs, ac);
-    const float a = ac, bb = bs;
-    const int k0 = (int)(kA & 0xff), k1 = (int)((kA >> 8) & 0xff), k2 = (int)((kA >> 16) & 0xff),
-              k3 = (int)(kA >> 24);   // taps 0..3 (3 = centre); taps 4..6 mirror 2..0
-    // The rotated offsets of a pair's two points at once in packed f32 (v_pk_mul_f32 / v_pk_add_f32:
-    // the same IEEE products and sums as the scalar form x a - y b, x b + y a, fp-contract off),
-    // cvRound by the 1.5 * 2^23 magic add (round-half-even for |x| < 2^22), and the row-sum address
-    // from the magic-biased bit patterns directly: __umul24 reads Y + 2^22 from the low 24 bits and
-    // the biases fold into one constant (mod 2^32).  The vertical taps pair up (0, 6), (1, 5),
-    // (2, 4) for v_dot2_u32_u16; the integer sum is the same.
-    typedef float f2 __attribute__((ext_vector_type(2)));
-    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-    const f2 av = {a, a}, bv = {bb, bb};
-    const uint32_t kk0 = (uint32_t)k0 * 0x10001u, kk1 = (uint32_t)k1 * 0x10001u, kk2 = (uint32_t)k2 * 0x10001u;
-    constexpr uint32_t kMagicBits = 0x4B400000u;   // bits of 1.5 * 2^23
-    constexpr uint32_t kRsOff = 2u * (18u * kOdRsW + 18u) - 2u * kOdRsW * (kMagicBits & 0xFFFFFFu) - 2u * kMagicBits;
-    const f2 magic = {12582912.0f, 12582912.0f};
-    // acc of one point, clamped so that acc >> 16 is the saturated blurred value (the 8-bit taps
-    // sum to 257, so an unclamped sum can reach 257 << 16)
-    auto sample = [&](uint32_t xb, uint32_t yb) -> uint32_t {
-        const uint32_t off = __umul24(yb, 2u * kOdRsW) + (2u * xb + kRsOff);   // 2 ((Y + 18) kOdRsW + X + 18)
-        const uint16_t* c0 = reinterpret_cast<const uint16_t*>(reinterpret_cast<const unsigned char*>(RS) + off);
-        const uint32_t p06 = (uint32_t)c0[0] | ((uint32_t)c0[6 * kOdRsW] << 16);
-        const uint32_t p15 = (uint32_t)c0[kOdRsW] | ((uint32_t)c0[5 * kOdRsW] << 16);
-        const uint32_t p24 = (uint32_t)c0[2 * kOdRsW] | ((uint32_t)c0[4 * kOdRsW] << 16);
-        uint32_t acc = __umul24((uint32_t)k3, (uint32_t)c0[3 * kOdRsW]) + (1u << 15);
-        acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, p06), __builtin_bit_cast(u16x2, kk0), acc, false);
-        acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, p15), __builtin_bit_cast(u16x2, kk1), acc, false);
-        acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, p24), __builtin_bit_cast(u16x2, kk2), acc, false);
-        return min(acc, 0x00FFFFFFu);
+    // A keypoint slot: its level, output index and position, and (interior windows) the lane's
+    // eleven window dwords, loaded as soon as the slot is known - the second keypoint's loads are
+    // in flight while the first one is processed
+    struct OdKey {
+        int valid, l, outIdx, x, y, resp, pitch, interior, sh;
+        uint32_t imgBytes;
+        const uint8_t* img;
+        uint32_t a[(kOdRows + 3) / 4];
     };
-    uint64_t words[4];
+    const int r0 = lane / 13, kd = lane - 13 * r0;   // lane = (row r0 of 4 per pass, source dword kd of 13)
+    auto setup = [&](int q, OdKey& k) {
+        k.valid = 0;
+        if (q >= g.outPerFrame) return;
+        int l = 0;
+        while (l + 1 < g.nlevels && q >= g.lv[l + 1].outBase) l++;
+        const LevelGeom& L = g.lv[l];
+        const int local = q - L.outBase;
+        if (local >= lc[l]) return;
+        int outIdx = local;
+        for (int l2 = 0; l2 < l; l2++) outIdx += lc[l2];
+        if (outIdx >= cap) return;
+        const uint32_t key = outKeys[(size_t)b * g.outPerFrame + q];
+        k.l = l;
+        k.outIdx = outIdx;
+        k.x = kx_of(key) + kMinBorder;
+        k.y = ky_of(key) + kMinBorder;
+        k.resp = kr_of(key);
+        k.img = level_img(g, z, pyr, b, l, k.pitch, k.imgBytes);
+        k.interior = k.x - 24 >= 0 && k.x + 24 <= L.w && k.y - 21 >= 0 && k.y + 21 < L.h;
+        k.sh = 0;
+        if (k.interior) {
+            // one buffer load per pass at a scalar row offset (rows past the window, or past the
+            // slab, read harmlessly and are never stored)
+            const int gx0 = k.x - 24, ga = gx0 & ~3;
+            k.sh = gx0 - ga;
+            const uint32_t winOff = (uint32_t)(k.y - 21) * (uint32_t)k.pitch + (uint32_t)ga;
+            const __amdgpu_buffer_rsrc_t rs = buf_rsrc(k.img + winOff, k.imgBytes - winOff);
+            const uint32_t laneOff = __umul24((uint32_t)r0, (uint32_t)k.pitch) + 4u * (uint32_t)kd;
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
-        const float4 pp = ppair[r];   // pair r * 64 + lane (byte pi/8, bit pi%8): (x0, x1, y0, y1)
-        const f2 px = {pp.x, pp.y}, py = {pp.z, pp.w};
-        const f2 xf = px * av - py * bv, yf = px * bv + py * av;
-        const f2 xm = xf + magic, ym = yf + magic;
-        const uint32_t s0 = sample(__float_as_uint(xm.x), __float_as_uint(ym.x));
-        const uint32_t s1 = sample(__float_as_uint(xm.y), __float_as_uint(ym.y));
-        // blurred(p0) < blurred(p1) <=> acc0 < (acc1 with its low 16 bits cleared)
-        words[r] = __ballot(s0 < (s1 & 0xFFFF0000u));
-    }
-#ifdef ORB_TIMING
-    if (lane == 0 && b == 0 && (q == 0 || q == 300 || q == 700))
-        printf("orient_desc q%d: patch %lld moments %lld hpass %lld brief %lld\n", q, t_od1 - t_od0, t_od2 - t_od1,
-               t_od3 - t_od2, clock64() - t_od3);
-#endif
-    if (lane < 4) {
-        uint64_t wv = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
-        reinterpret_cast<uint64_t*>(desc + ((size_t)b * cap + outIdx) * 32)[lane] = wv;
-    }
-    if (lane == 0) {
-        orb_keypoint kp;
-        kp.x = (float)x;
-        kp.y = (float)y;
-        if (l != 0) {
-            kp.x = kp.x * L.scale;
-            kp.y = kp.y * L.scale;
+            for (int u = 0; u < (kOdRows + 3) / 4; u++)
+                k.a[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)laneOff, 4 * u * k.pitch, 0);
         }
-        kp.size = L.size;
-        kp.angle = angle;
-        kp.response = (float)resp;
-        kp.octave = l;
-        kp.class_id = -1;
-        kps[(size_t)b * cap + outIdx] = kp;
+        k.valid = 1;
+    };
+    auto process = [&](const OdKey& k) {
+        if (!k.valid) return;
+        const int l = k.l, x = k.x, y = k.y, resp = k.resp, outIdx = k.outIdx, pitch = k.pitch;
+        const uint8_t* img = k.img;
+        const LevelGeom& L = g.lv[l];
+        // 1. patch: the next dword of the row from the next lane by DPP wave_shl:1, the realigned
+        //    dword stored (lanes with no patch dword write into the row-sum area, which step 3a
+        //    overwrites)
+        if (k.interior) {
+            uint32_t* const sink = reinterpret_cast<uint32_t*>(RS) + lane;
+    #pragma unroll
+            for (int u = 0; u < (kOdRows + 3) / 4; u++) {
+                const uint32_t a = k.a[u];
+                const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a, 0x130, 0xF, 0xF, false);
+                const int r = 4 * u + r0;
+                const bool st = r0 < 4 && kd < 12 && r < kOdRows;
+                *(st ? P32 + r * 12 + kd : sink) = __builtin_amdgcn_alignbyte(nx, a, (uint32_t)k.sh);
+            }
+        } else {   // within 21 / 24 px of an edge: BORDER_REFLECT_101 per byte
+            uint8_t* P8w = od_sm[wid];
+            for (int t = lane; t < kOdRows * kOdPW; t += 64) {
+                const int r = t / kOdPW, cc = t % kOdPW;
+                P8w[t] = img[(size_t)reflect101(y - 21 + r, L.h) * pitch + reflect101(x - 24 + cc, L.w)];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+
+        TSTAMP(t_od1);
+        // 2. moments: lane = (row group vr, dword d); patch dword 2+d holds u = 4d-16 .. 4d-13
+        int m10 = 0, m01 = 0;
+        {
+            const int d = lane & 7, vr = lane >> 3;
+            for (int it = 0; it < 4; it++) {
+                const int v = it * 8 + vr - 15;
+                if (v > 15) continue;
+                // bytes j with |4d + j - 16| <= umax[|v|], i.e. j in [16 - um - 4d, 16 + um - 4d] ∩ [0, 3]
+                const uint32_t m = momMask[(v + 15) * 8 + d];
+                const uint32_t w1 = m & 0x01010101u;
+                const uint32_t wu = m & (0x03020100u + (uint32_t)(4 * d) * 0x01010101u);   // bytes u + 16 = 4d + j
+                const uint32_t pw = P32[(21 + v) * 12 + 2 + d];
+                const int s1 = (int)__builtin_amdgcn_udot4(pw, w1, 0u, false);
+                m10 += (int)__builtin_amdgcn_udot4(pw, wu, 0u, false) - 16 * s1;
+                m01 += v * s1;
+            }
+        }
+        m10 = wave_sum_dpp(m10);
+        m01 = wave_sum_dpp(m01);
+        const float angle = fast_atan2_dev((float)m01, (float)m10);
+
+        TSTAMP(t_od2);
+        // 3a. horizontal Gaussian pass: RS[r][c] = sum_q k_q * raw(y-21+r, x-18+c-3+q) on the columns
+        //     the pattern can reach (c_htask).  Task (r, c0) computes columns c0 .. c0+7 from the 16
+        //     patch bytes c0+3 .. c0+18, re-based by four alignbytes at the task's byte offset; output i
+        //     takes bytes c0+3+i .. +6 (taps -3 .. 0, kA) and c0+7+i .. +10 (taps +1 .. +3, kB).
+        //     (Tried: the whole 43 x 37 pass on the matrix cores, RS^T = Gh^T P^T by nine
+        //     v_mfma_i32_16x16x64_i8 over the i8-biased window and a host-built banded tap matrix —
+        //     bit-exact, 17 % fewer VALU per keypoint, but the extraction step 3-5 % slower in
+        //     same-box A/B runs, with 16-bit or 8-byte row-sum stores alike; kept out.)
+        {
+    #pragma unroll
+            for (int it = 0; it < 3; it++) {
+                if (task[it] == 0xFFFFu) continue;
+                const int r = (int)(task[it] >> 8), c0 = (int)(task[it] & 0xFFu);
+                const int o = c0 + 3;
+                const uint32_t* row = P32 + r * 12 + (o >> 2);
+                const uint32_t sh = (uint32_t)(o & 3);
+                uint32_t d[5];
+    #pragma unroll
+                for (int k = 0; k < 5; k++) d[k] = row[k];   // (past the row: bytes of unused columns)
+                uint32_t w[4];
+    #pragma unroll
+                for (int k = 0; k < 4; k++) w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+                uint32_t out[4] = {0u, 0u, 0u, 0u};
+    #pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    const uint32_t A = (i & 3) == 0 ? w[i >> 2] : __builtin_amdgcn_alignbyte(w[(i >> 2) + 1], w[i >> 2], i & 3);
+                    const int j = i + 4;
+                    const uint32_t B = (j & 3) == 0 ? w[j >> 2] : __builtin_amdgcn_alignbyte(w[(j >> 2) + 1], w[j >> 2], j & 3);
+                    const uint32_t sum = __builtin_amdgcn_udot4(B, kB, __builtin_amdgcn_udot4(A, kA, 0u, false), false);
+                    out[i >> 1] |= sum << (16 * (i & 1));
+                }
+                uint32_t* rs32 = reinterpret_cast<uint32_t*>(RS + r * kOdRsW + c0);
+    #pragma unroll
+                for (int k = 0; k < 4; k++) rs32[k] = out[k];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+
+        TSTAMP(t_od3);
+        // 3b + 4. steered BRIEF: blurred(y+Y, x+X) = (sum_q k_q RS[Y+18+q][X+18] + 2^15) >> 16
+        float bs, ac;
+        glibc_sincosf(angle * g.factorPI, bs, ac);
+        const float a = ac, bb = bs;
+        const int k0 = (int)(kA & 0xff), k1 = (int)((kA >> 8) & 0xff), k2 = (int)((kA >> 16) & 0xff),
+                  k3 = (int)(kA >> 24);   // taps 0..3 (3 = centre); taps 4..6 mirror 2..0
+        // The rotated offsets of a pair's two points at once in packed f32 (v_pk_mul_f32 / v_pk_add_f32:
+        // the same IEEE products and sums as the scalar form x a - y b, x b + y a, fp-contract off),
+        // cvRound by the 1.5 * 2^23 magic add (round-half-even for |x| < 2^22), and the row-sum address
+        // from the magic-biased bit patterns directly: __umul24 reads Y + 2^22 from the low 24 bits and
+        // the biases fold into one constant (mod 2^32).  The vertical taps pair up (0, 6), (1, 5),
+        // (2, 4) for v_dot2_u32_u16; the integer sum is the same.
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+        const f2 av = {a, a}, bv = {bb, bb};
+        const uint32_t kk0 = (uint32_t)k0 * 0x10001u, kk1 = (uint32_t)k1 * 0x10001u, kk2 = (uint32_t)k2 * 0x10001u;
+        constexpr uint32_t kMagicBits = 0x4B400000u;   // bits of 1.5 * 2^23
+        constexpr uint32_t kRsOff = 2u * (18u * kOdRsW + 18u) - 2u * kOdRsW * (kMagicBits & 0xFFFFFFu) - 2u * kMagicBits;
+        const f2 magic = {12582912.0f, 12582912.0f};
+        // acc of one point, clamped so that acc >> 16 is the saturated blurred value (the 8-bit taps
+        // sum to 257, so an unclamped sum can reach 257 << 16)
+        auto sample = [&](uint32_t xb, uint32_t yb) -> uint32_t {
+            const uint32_t off = __umul24(yb, 2u * kOdRsW) + (2u * xb + kRsOff);   // 2 ((Y + 18) kOdRsW + X + 18)
+            const uint16_t* c0 = reinterpret_cast<const uint16_t*>(reinterpret_cast<const unsigned char*>(RS) + off);
+            const uint32_t p06 = (uint32_t)c0[0] | ((uint32_t)c0[6 * kOdRsW] << 16);
+            const uint32_t p15 = (uint32_t)c0[kOdRsW] | ((uint32_t)c0[5 * kOdRsW] << 16);
+            const uint32_t p24 = (uint32_t)c0[2 * kOdRsW] | ((uint32_t)c0[4 * kOdRsW] << 16);
+            uint32_t acc = __umul24((uint32_t)k3, (uint32_t)c0[3 * kOdRsW]) + (1u << 15);
+            acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, p06), __builtin_bit_cast(u16x2, kk0), acc, false);
+            acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, p15), __builtin_bit_cast(u16x2, kk1), acc, false);
+            acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, p24), __builtin_bit_cast(u16x2, kk2), acc, false);
+            return min(acc, 0x00FFFFFFu);
+        };
+        uint64_t words[4];
+    #pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const float4 pp = ppair[r];   // pair r * 64 + lane (byte pi/8, bit pi%8): (x0, x1, y0, y1)
+            const f2 px = {pp.x, pp.y}, py = {pp.z, pp.w};
+            const f2 xf = px * av - py * bv, yf = px * bv + py * av;
+            const f2 xm = xf + magic, ym = yf + magic;
+            const uint32_t s0 = sample(__float_as_uint(xm.x), __float_as_uint(ym.x));
+            const uint32_t s1 = sample(__float_as_uint(xm.y), __float_as_uint(ym.y));
+            // blurred(p0) < blurred(p1) <=> acc0 < (acc1 with its low 16 bits cleared)
+            words[r] = __ballot(s0 < (s1 & 0xFFFF0000u));
+        }
+    #ifdef ORB_TIMING
+        if (lane == 0 && b == 0 && (k.outIdx == 0 || k.outIdx == 300 || k.outIdx == 700))
+            printf("orient_desc q%d: patch %lld moments %lld hpass %lld brief %lld\n", k.outIdx, t_od1 - t_od0, t_od2 - t_od1,
+                   t_od3 - t_od2, clock64() - t_od3);
+    #endif
+        if (lane < 4) {
+            uint64_t wv = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
+            reinterpret_cast<uint64_t*>(desc + ((size_t)b * cap + outIdx) * 32)[lane] = wv;
+        }
+        if (lane == 0) {
+            orb_keypoint kp;
+            kp.x = (float)x;
+            kp.y = (float)y;
+            if (l != 0) {
+                kp.x = kp.x * L.scale;
+                kp.y = kp.y * L.scale;
+            }
+            kp.size = L.size;
+            kp.angle = angle;
+            kp.response = (float)resp;
+            kp.octave = l;
+            kp.class_id = -1;
+            kps[(size_t)b * cap + outIdx] = kp;
+        }
+    };
+    // two register sets in turn: a slot's window loads are issued one slot ahead; each slot
+    // reuses the wave's LDS (its window stores follow the previous slot's reads)
+    OdKey k0, k1;
+    setup(__builtin_amdgcn_readfirstlane(q0), k0);
+    setup(__builtin_amdgcn_readfirstlane(q0 + 1), k1);
+    for (int t = 0; t < kOdKpw; t += 2) {
+        process(k0);
+        if (t + 2 < kOdKpw) setup(__builtin_amdgcn_readfirstlane(q0 + t + 2), k0);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        process(k1);
+        if (t + 3 < kOdKpw) setup(__builtin_amdgcn_readfirstlane(q0 + t + 3), k1);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -2388,7 +2438,7 @@ static int run_pipeline(orb_extractor* ex, int B, const uint8_t* src, long long 
         const int* k = ex->blurK;   // centre, +-1, +-2, +-3
         const uint32_t kA = (uint32_t)k[3] | ((uint32_t)k[2] << 8) | ((uint32_t)k[1] << 16) | ((uint32_t)k[0] << 24);
         const uint32_t kB = (uint32_t)k[1] | ((uint32_t)k[2] << 8) | ((uint32_t)k[3] << 16);
-        hipLaunchKernelGGL(k_orient_desc, dim3((g.outPerFrame + 3) / 4, B), dim3(256), 0, st, g, ex->d_pyr, z,
+        hipLaunchKernelGGL(k_orient_desc, dim3((g.outPerFrame + 4 * kOdKpw - 1) / (4 * kOdKpw), B), dim3(256), 0, st, g, ex->d_pyr, z,
                            ex->d_outKeys, ex->d_levelCount, d_kps, d_desc, cap, d_counts, kA, kB);
     }
     mark(6);
