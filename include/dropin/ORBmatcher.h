@@ -2,14 +2,17 @@
 // liborbslam2_amd through include/orbslam2_amd_shim.hpp: the constructor (R/src/ORBmatcher.cpp:46-48),
 // DescriptorDistance (:1901-1917), SearchForInitialization (:499-617), the two tracking forms of
 // SearchByProjection (:63-163, :1564-1718), both SearchByBoW overloads (:220-372, :632-760),
-// SearchForTriangulation (:785-983) and Fuse(pKF, vpMapPoints, th) (:995-1154); delete those
-// definitions from R/src/ORBmatcher.cpp and keep the rest.  Fuse reads a point's raw
+// SearchForTriangulation (:785-983), both Fuse overloads (:995-1154, :1164-1290), the
+// relocalisation and Sim3 forms of SearchByProjection (:1719-1800, :370-497) and SearchBySim3
+// (:1305-1503) — every matcher the reference defines; R/src/ORBmatcher.cpp then keeps only
+// TH_LOW / TH_HIGH / HISTO_LENGTH and the protected helpers.  The matchers read a point's raw
 // mfMinDistance / mfMaxDistance through MapPoint::GetDistances (one accessor added
 // to R/include/MapPoint.h).  Compiles inside the reference tree only (OpenCV, Frame.h); the shim
 // is compiled and tested here with mock types (tests/test_cpp_shim*.py).
 #ifndef ORBMATCHER_H
 #define ORBMATCHER_H
 
+#include <set>
 #include <vector>
 #include <opencv2/core/core.hpp>
 #include <opencv2/features2d/features2d.hpp>
@@ -38,10 +41,15 @@ public:
     int SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, const float th, const bool bMono) {
         return mDev.SearchByProjection(CurrentFrame, LastFrame, th, bMono);
     }
+    // relocalisation (R :1719-1800) and loop closing's Sim3 projection (R :370-497) on the GPU
     int SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const std::set<MapPoint*>& sAlreadyFound,
-                           const float th, const int ORBdist);
+                           const float th, const int ORBdist) {
+        return mDev.SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist);
+    }
     int SearchByProjection(KeyFrame* pKF, cv::Mat Scw, const std::vector<MapPoint*>& vpPoints,
-                           std::vector<MapPoint*>& vpMatched, int th);
+                           std::vector<MapPoint*>& vpMatched, int th) {
+        return mDev.SearchByProjection(pKF, Scw, vpPoints, vpMatched, th);
+    }
     // BoW matchers on the GPU: tracking's reference keyframe / relocalisation (R :220-372) and
     // loop closing (R :632-760)
     int SearchByBoW(KeyFrame* pKF, Frame& F, std::vector<MapPoint*>& vpMapPointMatches) {
@@ -62,13 +70,18 @@ public:
                                std::vector<std::pair<size_t, size_t> >& vMatchedPairs, const bool bOnlyStereo) {
         return mDev.SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo);
     }
+    // loop closing: both Sim3 projection directions plus the mutual check (R :1305-1503)
     int SearchBySim3(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoint*>& vpMatches12, const float& s12,
-                     const cv::Mat& R12, const cv::Mat& t12, const float th);
+                     const cv::Mat& R12, const cv::Mat& t12, const float th) {
+        return mDev.SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th);
+    }
     int Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, const float th = 3.0) {
         return mDev.Fuse(pKF, vpMapPoints, th);
     }
     int Fuse(KeyFrame* pKF, cv::Mat Scw, const std::vector<MapPoint*>& vpPoints, float th,
-             vector<MapPoint*>& vpReplacePoint);
+             vector<MapPoint*>& vpReplacePoint) {
+        return mDev.Fuse(pKF, Scw, vpPoints, th, vpReplacePoint);
+    }
 
 public:
     static const int TH_LOW;

@@ -33,6 +33,7 @@
 #include <list>
 #include <map>
 #include <mutex>
+#include <set>
 #include <stdexcept>
 #include <string>
 #include <type_traits>
@@ -202,6 +203,27 @@ template <class MatT>
 inline void read_mat33(const MatT& m, float out[9]) {
     for (int r = 0; r < 3; r++)
         for (int k = 0; k < 3; k++) out[3 * r + k] = m.template at<float>(r, k);
+}
+// Ow = -Rcw^T tcw of rows 0..2 of a pose (OpenCV float GEMM: double accumulation, one rounding)
+inline void camera_center(const float T[12], float Ow[3]) {
+    for (int k = 0; k < 3; k++)
+        Ow[k] = (float)(-((double)T[k] * T[3] + (double)T[4 + k] * T[7] + (double)T[8 + k] * T[11]));
+}
+// Scw = [sR | st] -> Tcw = [R | t] and Ow = -R^T t as R/src/ORBmatcher.cpp:382-386 / :1172-1176 derive
+// them: scw = sqrt(row 0 . row 0) (dot accumulated in double, the root rounded to float), every
+// element x / scw as x * (1.0 / scw) rounded once, then the camera centre
+template <class MatT>
+inline void decompose_scw(const MatT& Scw, float Tcw[12], float Ow[3]) {
+    double ss = 0.0;
+    for (int k = 0; k < 3; k++) {
+        const double v = Scw.template at<float>(0, k);
+        ss += v * v;
+    }
+    const float scw = (float)std::sqrt(ss);
+    const double inv = 1.0 / (double)scw;
+    for (int r = 0; r < 3; r++)
+        for (int k = 0; k < 4; k++) Tcw[4 * r + k] = (float)((double)Scw.template at<float>(r, k) * inv);
+    camera_center(Tcw, Ow);
 }
 // orb_kf_params of a keyframe (ORBmatcher::Fuse reads GetPose, GetCameraCenter, the intrinsics
 // and the scale tables, R/src/ORBmatcher.cpp:997-1006)
@@ -458,7 +480,205 @@ public:
         return n;
     }
 
+    // SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist) (R :1719-1800,
+    // Tracking::Relocalization): pKF->GetMapPointMatches() minus NULL, bad and sAlreadyFound points;
+    // the frame's mTcw (Ow = -Rcw^T tcw, :1723-1725), fx .. cy, mfLogScaleFactor, mnScaleLevels,
+    // mvScaleFactors; CurrentFrame.mvpMapPoints gains the keyframe's point in every slot this call
+    // matched (slots already set are never taken; the rotation check's rejects stay NULL).
+    template <class FrameT, class KeyFrameT, class MapPointT>
+    int SearchByProjection(FrameT& CurrentFrame, KeyFrameT* pKF, const std::set<MapPointT*>& sAlreadyFound,
+                           const float th, const int ORBdist) {
+        const std::vector<MapPointT*> vpMPs = pKF->GetMapPointMatches();
+        FrameView<FrameT> cur(CurrentFrame);
+        FrameView<KeyFrameT> kv(*pKF);
+        const size_t n = vpMPs.size(), nc = CurrentFrame.mvKeysUn.size();
+        std::vector<uint8_t> valid(n, 0), desc(n * 32, 0);
+        std::vector<float> xyz(3 * n, 0.f), mind(n, 0.f), maxd(n, 0.f);
+        for (size_t i = 0; i < n; i++) {
+            MapPointT* pMP = vpMPs[i];
+            if (!pMP || pMP->isBad() || sAlreadyFound.count(pMP)) continue;
+            valid[i] = 1;
+            detail::read_vec3(pMP->GetWorldPos(), &xyz[3 * i]);
+            pMP->GetDistances(mind[i], maxd[i]);
+            const auto d = pMP->GetDescriptor();
+            std::memcpy(&desc[32 * i], d.data, 32);
+        }
+        float Tc[12], Ow[3];
+        detail_read_T34(CurrentFrame.mTcw, Tc);
+        detail::camera_center(Tc, Ow);
+        std::vector<int32_t> slots(nc, -1);
+        for (size_t i = 0; i < nc; i++)
+            if (CurrentFrame.mvpMapPoints[i]) slots[i] = -2;
+        const float cam[4] = {CurrentFrame.fx, CurrentFrame.fy, CurrentFrame.cx, CurrentFrame.cy};
+        const int nm = check(orb_search_by_projection_kf(h_, &cur.v, Tc, Ow, &kv.v, valid.data(), xyz.data(), mind.data(),
+                                                         maxd.data(), desc.data(), cam, CurrentFrame.mfLogScaleFactor,
+                                                         CurrentFrame.mnScaleLevels, CurrentFrame.mvScaleFactors.data(),
+                                                         th, ORBdist, slots.data()),
+                             "orb_search_by_projection_kf");
+        for (size_t i = 0; i < nc; i++)
+            if (slots[i] >= 0) CurrentFrame.mvpMapPoints[i] = vpMPs[(size_t)slots[i]];
+        return nm;
+    }
+
+    // SearchByProjection(pKF, Scw, vpPoints, vpMatched, th) (R :370-497, LoopClosing::ComputeSim3):
+    // Tcw / Ow from Scw as :382-386 (detail::decompose_scw); a point is skipped when bad or already
+    // in vpMatched (:390-391); vpMatched[bestIdx] = vpPoints[iMP] for every match (:488-492).
+    template <class KeyFrameT, class MatT, class MapPointT>
+    int SearchByProjection(KeyFrameT* pKF, const MatT& Scw, const std::vector<MapPointT*>& vpPoints,
+                           std::vector<MapPointT*>& vpMatched, int th) {
+        FrameView<KeyFrameT> kv(*pKF);
+        detail::KfParams<KeyFrameT> kp(pKF);
+        detail::decompose_scw(Scw, kp.p.Tcw, kp.p.Ow);
+        std::set<MapPointT*> found(vpMatched.begin(), vpMatched.end());
+        found.erase(static_cast<MapPointT*>(nullptr));
+        const size_t n = vpPoints.size(), nk = vpMatched.size();
+        std::vector<uint8_t> valid(n, 0), desc(n * 32, 0);
+        std::vector<float> xyz(3 * n, 0.f), nrm(3 * n, 0.f), mind(n, 0.f), maxd(n, 0.f);
+        read_points(vpPoints, found, valid, xyz, nrm, mind, maxd, desc);
+        std::vector<int32_t> matched(nk, -1);
+        for (size_t i = 0; i < nk; i++)
+            if (vpMatched[i]) matched[i] = -2;
+        const int nm = check(orb_search_by_projection_sim3(h_, &kv.v, &kp.p, (int)n, valid.data(), xyz.data(), nrm.data(),
+                                                           mind.data(), maxd.data(), desc.data(), (float)th,
+                                                           matched.data()),
+                             "orb_search_by_projection_sim3");
+        for (size_t i = 0; i < nk; i++)
+            if (matched[i] >= 0) vpMatched[i] = vpPoints[(size_t)matched[i]];
+        return nm;
+    }
+
+    // SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th) (R :1305-1503): sR12 = s12 R12,
+    // sR21 = (1/s12) R12^T, t21 = -sR21 t12 (:1315-1318; scaled elements rounded to float, the product
+    // accumulated in double); vbAlreadyMatched1 / 2 from vpMatches12 and GetIndexInKeyFrame(pKF2)
+    // (:1327-1349); both keyframes' GetRotation / GetTranslation, scale tables and pKF1's intrinsics;
+    // vpMatches12[i1] = pKF2's point for every mutual pair found (:1525-1540).
+    template <class KeyFrameT, class MapPointT, class MatT>
+    int SearchBySim3(KeyFrameT* pKF1, KeyFrameT* pKF2, std::vector<MapPointT*>& vpMatches12, const float& s12,
+                     const MatT& R12, const MatT& t12, const float th) {
+        const std::vector<MapPointT*> vp1 = pKF1->GetMapPointMatches(), vp2 = pKF2->GetMapPointMatches();
+        const size_t N1 = vp1.size(), N2 = vp2.size();
+        std::vector<uint8_t> am1(N1, 0), am2(N2, 0);
+        for (size_t i = 0; i < N1; i++) {
+            MapPointT* pMP = vpMatches12[i];
+            if (!pMP) continue;
+            am1[i] = 1;
+            const int idx2 = pMP->GetIndexInKeyFrame(pKF2);
+            if (idx2 >= 0 && idx2 < (int)N2) am2[(size_t)idx2] = 1;
+        }
+        float R[9], t[3];
+        detail::read_mat33(R12, R);
+        detail::read_vec3(t12, t);
+        orb_sim3_points p1{}, p2{};
+        for (int r = 0; r < 3; r++) {
+            double acc = 0.0;
+            for (int k = 0; k < 3; k++) {
+                const float sr21 = (float)((double)R[3 * k + r] * (1.0 / (double)s12));
+                p1.S[4 * r + k] = sr21;
+                p2.S[4 * r + k] = (float)((double)R[3 * r + k] * (double)s12);
+                acc += (double)sr21 * t[k];
+            }
+            p1.S[4 * r + 3] = (float)(-acc);
+            p2.S[4 * r + 3] = t[r];
+        }
+        Sim3Side s1(pKF1, vp1, am1, p1), s2(pKF2, vp2, am2, p2);
+        FrameView<KeyFrameT> k1(*pKF1), k2(*pKF2);
+        const float cam1[4] = {pKF1->fx, pKF1->fy, pKF1->cx, pKF1->cy};
+        const orb_scale_params sc1{pKF1->mfLogScaleFactor, pKF1->mnScaleLevels, pKF1->mvScaleFactors.data()};
+        const orb_scale_params sc2{pKF2->mfLogScaleFactor, pKF2->mnScaleLevels, pKF2->mvScaleFactors.data()};
+        std::vector<int32_t> m12(N1, -1);
+        const int n = check(orb_search_by_sim3(device_, &k1.v, &k2.v, &p1, &p2, cam1, &sc1, &sc2, th, m12.data()),
+                            "orb_search_by_sim3");
+        for (size_t i = 0; i < N1; i++)
+            if (m12[i] >= 0) vpMatches12[i] = vp2[(size_t)m12[i]];
+        return n;
+    }
+
+    // Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) (R :1164-1290, LoopClosing::SearchAndFuse): Tcw /
+    // Ow from Scw (:1172-1176); a point is skipped when bad or among pKF->GetMapPoints() at entry
+    // (:1178, :1190); the matching step on the GPU (orb_fuse_sim3), then in vector order: the
+    // keyframe's point in the matched slot, read at that point of the loop, becomes
+    // vpReplacePoint[iMP] unless bad, an empty slot receives the point (AddObservation /
+    // AddMapPoint); nFused counts both (:1270-1283).
+    template <class KeyFrameT, class MatT, class MapPointT>
+    int Fuse(KeyFrameT* pKF, const MatT& Scw, const std::vector<MapPointT*>& vpPoints, float th,
+             std::vector<MapPointT*>& vpReplacePoint) {
+        FrameView<KeyFrameT> kv(*pKF);
+        detail::KfParams<KeyFrameT> kp(pKF);
+        detail::decompose_scw(Scw, kp.p.Tcw, kp.p.Ow);
+        const std::set<MapPointT*> spAlreadyFound = pKF->GetMapPoints();
+        const size_t n = vpPoints.size();
+        std::vector<uint8_t> valid(n, 0), desc(n * 32, 0);
+        std::vector<float> xyz(3 * n, 0.f), nrm(3 * n, 0.f), mind(n, 0.f), maxd(n, 0.f);
+        read_points(vpPoints, spAlreadyFound, valid, xyz, nrm, mind, maxd, desc);
+        std::vector<int32_t> bi(n, -1), bd(n, 256);
+        if (n)
+            check(orb_fuse_sim3(device_, &kv.v, &kp.p, (int)n, valid.data(), xyz.data(), nrm.data(), mind.data(),
+                                maxd.data(), desc.data(), th, bi.data(), bd.data()),
+                  "orb_fuse_sim3");
+        int nFused = 0;
+        for (size_t i = 0; i < n; i++) {
+            if (bi[i] < 0) continue;
+            MapPointT* pMP = vpPoints[i];
+            const size_t bestIdx = (size_t)bi[i];
+            MapPointT* pMPinKF = pKF->GetMapPoint(bestIdx);
+            if (pMPinKF) {
+                if (!pMPinKF->isBad()) vpReplacePoint[i] = pMPinKF;
+            } else {
+                pMP->AddObservation(pKF, bestIdx);
+                pKF->AddMapPoint(pMP, bestIdx);
+            }
+            nFused++;
+        }
+        return nFused;
+    }
+
 private:
+    // the per-point arrays of the Scw forms: valid = set, not bad, not in `skip`
+    template <class MapPointT>
+    static void read_points(const std::vector<MapPointT*>& vp, const std::set<MapPointT*>& skip, std::vector<uint8_t>& valid,
+                            std::vector<float>& xyz, std::vector<float>& nrm, std::vector<float>& mind,
+                            std::vector<float>& maxd, std::vector<uint8_t>& desc) {
+        for (size_t i = 0; i < vp.size(); i++) {
+            MapPointT* pMP = vp[i];
+            if (!pMP || pMP->isBad() || skip.count(pMP)) continue;
+            valid[i] = 1;
+            detail::read_vec3(pMP->GetWorldPos(), &xyz[3 * i]);
+            detail::read_vec3(pMP->GetNormal(), &nrm[3 * i]);
+            pMP->GetDistances(mind[i], maxd[i]);
+            const auto d = pMP->GetDescriptor();
+            std::memcpy(&desc[32 * i], d.data, 32);
+        }
+    }
+    // one keyframe's side of SearchBySim3 (orb_sim3_points): Tcw, and per slot the point's arrays
+    // when set, not bad and not already matched (:1355-1361, :1430-1436)
+    struct Sim3Side {
+        std::vector<uint8_t> valid, desc;
+        std::vector<float> xyz, mind, maxd;
+        template <class KeyFrameT, class MapPointT>
+        Sim3Side(KeyFrameT* pKF, const std::vector<MapPointT*>& vp, const std::vector<uint8_t>& already, orb_sim3_points& p)
+            : valid(vp.size(), 0), desc(vp.size() * 32, 0), xyz(vp.size() * 3, 0.f), mind(vp.size(), 0.f),
+              maxd(vp.size(), 0.f) {
+            float R[9], t[3];
+            detail::read_mat33(pKF->GetRotation(), R);
+            detail::read_vec3(pKF->GetTranslation(), t);
+            for (int r = 0; r < 3; r++) {
+                for (int k = 0; k < 3; k++) p.Tcw[4 * r + k] = R[3 * r + k];
+                p.Tcw[4 * r + 3] = t[r];
+            }
+            for (size_t i = 0; i < vp.size(); i++) {
+                MapPointT* pMP = vp[i];
+                if (!pMP || already[i] || pMP->isBad()) continue;
+                valid[i] = 1;
+                detail::read_vec3(pMP->GetWorldPos(), &xyz[3 * i]);
+                pMP->GetDistances(mind[i], maxd[i]);
+                const auto d = pMP->GetDescriptor();
+                std::memcpy(&desc[32 * i], d.data, 32);
+            }
+            p.n = (int)vp.size();
+            p.valid = valid.data(); p.xyz = xyz.data(); p.min_dist = mind.data(); p.max_dist = maxd.data();
+            p.desc = desc.data();
+        }
+    };
     template <class MatT>
     static void detail_read_T34(const MatT& T, float out[12]) {   // rows 0..2 of a 4x4 float cv::Mat
         for (int r = 0; r < 3; r++)

@@ -15,6 +15,10 @@
 //   shim_caller sft IN OUT       ORBmatcher::SearchForTriangulation(pKF1, pKF2, F12, pairs, bOnlyStereo)
 //   shim_caller sbbf IN OUT      ORBmatcher::SearchByBoW(pKF, F, vpMapPointMatches)
 //   shim_caller sbbk IN OUT      ORBmatcher::SearchByBoW(pKF1, pKF2, vpMatches12)
+//   shim_caller sbpk IN OUT      ORBmatcher::SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist)
+//   shim_caller sbps IN OUT      ORBmatcher::SearchByProjection(pKF, Scw, vpPoints, vpMatched, th)
+//   shim_caller sbs IN OUT       ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th)
+//   shim_caller fuses IN OUT     ORBmatcher::Fuse(pKF, Scw, vpPoints, th, vpReplacePoint)
 //   shim_caller threads IN OUT   the SURVEY 8b threading contract: two Extractor handles on two host
 //                                threads at once (stereo L/R, R/src/Frame.cpp:86-89), SearchForInitialization
 //                                and PoseOptimization on a third and fourth (Tracking), LocalBundleAdjustment
@@ -28,6 +32,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <utility>
@@ -76,6 +81,8 @@ struct Frame {
     std::vector<MapPoint*> mvpMapPoints;
     std::vector<bool> mvbOutlier;
     std::vector<float> mvScaleFactors, mvInvLevelSigma2;
+    float mfLogScaleFactor = 0;
+    int mnScaleLevels = 8;
     FeatureVector mFeatVec;
     Mat mTcw;
     float mbf = 0, mb = 0;
@@ -106,6 +113,7 @@ struct KeyFrame {
     std::vector<KeyFrame*> GetVectorCovisibleKeyFrames() { return covis; }
     std::vector<MapPoint*> GetMapPointMatches() { return matches; }
     MapPoint* GetMapPoint(size_t i) { return matches[i]; }
+    std::set<MapPoint*> GetMapPoints();
     void AddMapPoint(MapPoint* p, size_t i) { matches[i] = p; }
     void ReplaceMapPointMatch(size_t i, MapPoint* p) { matches[i] = p; }
     bool isBad() const { return bad; }
@@ -153,6 +161,10 @@ struct MapPoint {
     Mat GetNormal() { return normal; }
     void GetDistances(float& mn, float& mx) { mn = mfMinDistance; mx = mfMaxDistance; }
     bool IsInKeyFrame(KeyFrame* k) { return obs.count(k) > 0; }
+    int GetIndexInKeyFrame(KeyFrame* k) {
+        const auto it = obs.find(k);
+        return it == obs.end() ? -1 : (int)it->second;
+    }
     void AddObservation(KeyFrame* k, size_t i) { obs[k] = i; }
     MapPoint* replacedBy = nullptr;
     // MapPoint::Replace (R/src/MapPoint.cpp:177-219): observations move to pMP unless it is in that
@@ -179,6 +191,12 @@ inline void KeyFrame::EraseMapPointMatch(MapPoint* p) {
     g_erase_log.emplace_back(mnId, p->mnId);
     for (auto& m : matches)
         if (m == p) m = nullptr;
+}
+inline std::set<MapPoint*> KeyFrame::GetMapPoints() {   // R/src/KeyFrame.cpp: set, not bad
+    std::set<MapPoint*> s;
+    for (MapPoint* p : matches)
+        if (p && !p->isBad()) s.insert(p);
+    return s;
 }
 struct Map {
     std::mutex mMutexMapUpdate;
@@ -690,6 +708,165 @@ static void run_sbbk(FILE* in, FILE* out) {
     wr(out, o);
 }
 
+// map points of a keyframe's slots with their data: IN per slot xyz, normal, mfMinDistance,
+// mfMaxDistance, descriptor; point i sits in slot i (mnId = i), observed there
+static void point_data(FILE* in, mock::KeyFrame& K, std::vector<mock::MapPoint>& pts) {
+    const auto xyz = rd<float>(in), nrm = rd<float>(in), mind = rd<float>(in), maxd = rd<float>(in);
+    const auto desc = rd<uint8_t>(in);
+    for (size_t i = 0; i < pts.size(); i++) {
+        mock::MapPoint& P = pts[i];
+        P.mnId = i;
+        P.X.create(3, 1, orbslam2_amd::kCV_32F);
+        P.normal.create(3, 1, orbslam2_amd::kCV_32F);
+        for (int k = 0; k < 3; k++) {
+            P.X.at<float>(k, 0) = xyz[3 * i + (size_t)k];
+            P.normal.at<float>(k, 0) = nrm.empty() ? 0.f : nrm[3 * i + (size_t)k];
+        }
+        P.mfMinDistance = mind[i];
+        P.mfMaxDistance = maxd[i];
+        P.desc.create(1, 32, orbslam2_amd::kCV_8U);
+        std::copy(desc.begin() + 32 * (long)i, desc.begin() + 32 * (long)(i + 1), P.desc.data);
+        if (K.matches[i] == &P) P.obs[&K] = i;
+    }
+}
+static mock::Mat read_mat(FILE* in, int rows, int cols) {
+    const auto v = rd<float>(in);
+    if (v.size() != (size_t)(rows * cols)) throw std::runtime_error("bad matrix size");
+    mock::Mat m(rows, cols, orbslam2_amd::kCV_32F);
+    for (int i = 0; i < rows * cols; i++) m.at<float>(i / cols, i % cols) = v[(size_t)i];
+    return m;
+}
+
+// IN: the frame (keypoints, descriptors), grid, mTcw (16), (fx, fy, cx, cy), mfLogScaleFactor,
+// mvScaleFactors, slot codes (-1 NULL, -2 set), then the keyframe, its slot kinds (-1 none, 0 good,
+// 1 bad, 2 good but in sAlreadyFound), the points' data, (th, ORBdist, checkOri).
+// OUT: nmatches, per frame slot the keyframe slot of its point (-2 set before, -1 NULL).
+static void run_sbpk(FILE* in, FILE* out) {
+    mock::Frame F;
+    load_frame(in, F);
+    set_grid(rd<float>(in));
+    F.mTcw = read_mat(in, 4, 4);
+    const auto cam = rd<float>(in), lsf = rd<float>(in);
+    mock::Frame::fx = cam[0]; mock::Frame::fy = cam[1]; mock::Frame::cx = cam[2]; mock::Frame::cy = cam[3];
+    F.mfLogScaleFactor = lsf[0];
+    F.mvScaleFactors = rd<float>(in);
+    F.mnScaleLevels = (int)F.mvScaleFactors.size();
+    const auto init = rd<int32_t>(in);
+    mock::KeyFrame K;
+    load_kf(in, K);
+    auto kind = rd<int32_t>(in);
+    std::vector<mock::MapPoint> pts;
+    std::vector<int32_t> k01(kind);
+    for (auto& k : k01) if (k == 2) k = 0;
+    attach_points(K, k01, pts);
+    point_data(in, K, pts);
+    std::set<mock::MapPoint*> found;
+    for (size_t i = 0; i < kind.size(); i++)
+        if (kind[i] == 2) found.insert(&pts[i]);
+    const auto par = rd<float>(in);
+    mock::MapPoint preset;
+    F.mvpMapPoints.assign(init.size(), nullptr);
+    for (size_t i = 0; i < init.size(); i++)
+        if (init[i] == -2) F.mvpMapPoints[i] = &preset;
+    orbslam2_amd::Matcher matcher(0.6f, par[2] != 0);
+    const int32_t n = matcher.SearchByProjection(F, &K, found, par[0], (int)par[1]);
+    wr(out, &n, 1);
+    std::vector<int32_t> o;
+    for (auto* p : F.mvpMapPoints) o.push_back(!p ? -1 : p == &preset ? -2 : (int32_t)p->mnId);
+    wr(out, o);
+}
+
+// IN: the keyframe, Scw (16), the points' data (one per vpPoints entry), their bad flags, vpMatched
+// on entry per keyframe slot (-1 NULL, -2 a point outside vpPoints, else a vpPoints index), th.
+// OUT: nmatches, vpMatched per slot in the same codes.
+static void run_sbps(FILE* in, FILE* out) {
+    mock::KeyFrame K;
+    load_kf(in, K);
+    const mock::Mat Scw = read_mat(in, 4, 4);
+    const auto bad = rd<uint8_t>(in);
+    std::vector<mock::MapPoint> pts(bad.size());
+    mock::KeyFrame none;   // the points' data loader attaches nothing to an empty keyframe
+    none.matches.assign(pts.size(), nullptr);
+    point_data(in, none, pts);
+    for (size_t i = 0; i < pts.size(); i++) pts[i].bad = bad[i] != 0;
+    const auto pre = rd<int32_t>(in);
+    const auto th = rd<int32_t>(in);
+    std::vector<mock::MapPoint*> vp;
+    for (auto& P : pts) vp.push_back(&P);
+    mock::MapPoint foreign;
+    std::vector<mock::MapPoint*> vm(pre.size(), nullptr);
+    for (size_t i = 0; i < pre.size(); i++) vm[i] = pre[i] == -2 ? &foreign : pre[i] >= 0 ? vp[(size_t)pre[i]] : nullptr;
+    orbslam2_amd::Matcher matcher(0.75f, true);
+    const int32_t n = matcher.SearchByProjection(&K, Scw, vp, vm, th[0]);
+    wr(out, &n, 1);
+    std::vector<int32_t> o;
+    for (auto* p : vm) o.push_back(!p ? -1 : p == &foreign ? -2 : (int32_t)p->mnId);
+    wr(out, o);
+}
+
+// IN: keyframe 1, its slot kinds (-1 none, 0 good, 1 bad), its points' data; the same for keyframe 2;
+// vpMatches12 on entry per keyframe-1 slot (-1 NULL, -2 a point not in keyframe 2, else the
+// keyframe-2 slot whose point it is); s12, R12 (9), t12 (3), th.
+// OUT: nFound, vpMatches12 per keyframe-1 slot in the same codes.
+static void run_sbs(FILE* in, FILE* out) {
+    mock::KeyFrame K1, K2;
+    std::vector<mock::MapPoint> p1, p2;
+    load_kf(in, K1);
+    attach_points(K1, rd<int32_t>(in), p1);
+    point_data(in, K1, p1);
+    load_kf(in, K2);
+    attach_points(K2, rd<int32_t>(in), p2);
+    point_data(in, K2, p2);
+    const auto pre = rd<int32_t>(in);
+    const auto s12 = rd<float>(in);
+    const mock::Mat R12 = read_mat(in, 3, 3), t12 = read_mat(in, 3, 1);
+    const auto th = rd<float>(in);
+    mock::MapPoint foreign;
+    std::vector<mock::MapPoint*> vm(pre.size(), nullptr);
+    for (size_t i = 0; i < pre.size(); i++) vm[i] = pre[i] == -2 ? &foreign : pre[i] >= 0 ? &p2[(size_t)pre[i]] : nullptr;
+    orbslam2_amd::Matcher matcher(0.75f, true);
+    const int32_t n = matcher.SearchBySim3(&K1, &K2, vm, s12[0], R12, t12, th[0]);
+    wr(out, &n, 1);
+    std::vector<int32_t> o;
+    for (auto* p : vm) o.push_back(!p ? -1 : p == &foreign ? -2 : (int32_t)p->mnId);
+    wr(out, o);
+}
+
+// IN: the keyframe, Scw (16), the points' data, bad flags, the keyframe slot each point occupies on
+// entry (-1 none; such points are the keyframe's), vpPoints (point indices), th.
+// OUT: nFused, per keyframe slot the mnId of its point (-1), vpReplacePoint per vpPoints entry (mnId
+// or -1), per point its slot in the keyframe (-1).
+static void run_fuses(FILE* in, FILE* out) {
+    mock::KeyFrame K;
+    load_kf(in, K);
+    const mock::Mat Scw = read_mat(in, 4, 4);
+    const auto bad = rd<uint8_t>(in);
+    std::vector<mock::MapPoint> pts(bad.size());
+    mock::KeyFrame none;
+    none.matches.assign(pts.size(), nullptr);
+    point_data(in, none, pts);
+    const auto slot = rd<int32_t>(in), vec = rd<int32_t>(in);
+    const auto th = rd<float>(in);
+    for (size_t i = 0; i < pts.size(); i++) {
+        pts[i].bad = bad[i] != 0;
+        if (slot[i] >= 0) {
+            pts[i].obs[&K] = (size_t)slot[i];
+            K.matches[(size_t)slot[i]] = &pts[i];
+        }
+    }
+    std::vector<mock::MapPoint*> vp;
+    for (const int32_t v : vec) vp.push_back(&pts[(size_t)v]);
+    std::vector<mock::MapPoint*> repl(vp.size(), nullptr);
+    orbslam2_amd::Matcher matcher(0.6f, true);
+    const int32_t n = matcher.Fuse(&K, Scw, vp, th[0], repl);
+    wr(out, &n, 1);
+    std::vector<int32_t> slots, ro, po;
+    for (auto* p : K.matches) slots.push_back(p ? (int32_t)p->mnId : -1);
+    for (auto* p : repl) ro.push_back(p ? (int32_t)p->mnId : -1);
+    for (auto& P : pts) po.push_back(P.obs.count(&K) ? (int32_t)P.obs[&K] : -1);
+    wr(out, slots); wr(out, ro); wr(out, po);
+}
+
 static bool run_mode(const std::string& mode, FILE* in, FILE* out) {
     if (mode == "extract") run_extract(in, out);
     else if (mode == "sfi") run_sfi(in, out);
@@ -703,6 +880,10 @@ static bool run_mode(const std::string& mode, FILE* in, FILE* out) {
     else if (mode == "sft") run_sft(in, out);
     else if (mode == "sbbf") run_sbbf(in, out);
     else if (mode == "sbbk") run_sbbk(in, out);
+    else if (mode == "sbpk") run_sbpk(in, out);
+    else if (mode == "sbps") run_sbps(in, out);
+    else if (mode == "sbs") run_sbs(in, out);
+    else if (mode == "fuses") run_fuses(in, out);
     else return false;
     return true;
 }
@@ -770,7 +951,7 @@ static int run_threads(int argc, char** argv) {
 int main(int argc, char** argv) {
     if (argc >= 6 && std::string(argv[1]) == "threads") return run_threads(argc, argv);
     if (argc != 4) {
-        std::fprintf(stderr, "usage: %s extract|sfi|sbp|sbl|lba|lbag|pose|stereo|fuse|sft|sbbf|sbbk IN OUT\n"
+        std::fprintf(stderr, "usage: %s extract|sfi|sbp|sbl|lba|lbag|pose|stereo|fuse|sft|sbbf|sbbk|sbpk|sbps|sbs|fuses IN OUT\n"
                              "       %s threads OUT REPS MODE IN [MODE IN ...]\n", argv[0], argv[0]);
         return 2;
     }
