@@ -10,7 +10,7 @@
 // Per LM trial (lambda):
 //   k_point_schur     D^-1 = (Hll + lambda I)^-1 per landmark (and the LM iteration start, fused)
 //   k_schur_pairs     reduced camera matrix S = Hpp + lambda I - sum W D^-1 W^T and b_s, one
-//                     workgroup per 6x6 pose-pair block (G/core/block_solver.hpp:382-440)
+//                     wave per 6x6 pose-pair block (G/core/block_solver.hpp:382-440)
 //   k_ldlt_solve      dense LDL^T of S in one workgroup, trailing updates on the f64 MFMA units
 //                     (LinearSolverEigen's SimplicialLDLT role)
 //   k_backsub_update  x_l, push + oplus (SE3Quat::exp * T, X += x_l)
@@ -109,11 +109,13 @@ struct LbaDev {
     double *Hll_e, *Hpp_e, *Hpl_e, *bl_e, *bp_e, *echi;
     // reduced per vertex
     double *Hll, *bl, *Dinv, *db, *Hpp, *bp;   // db = Dinv b_l
-    double* Ae;                 // [nact][18] Hpl_e D^-1 of the edge's landmark (per trial)
+    double* Ae;                 // [pose-major position][18] Hpl_e D^-1 of the edge's landmark (per trial)
+    double* HplP;               // [pose-major position][18] Hpl_e (per trial, written with Ae)
+    const int32_t* poPos;       // per act position: its index in the pose-major lists (-1: fixed pose)
     const int32_t* pairs;       // pose-pair blocks of S with shared landmarks, (bi << 16 | bj), bi <= bj
     const int32_t* npairs;      // their count
     const int32_t* tripStart;   // per listed pair: first entry of its shared-landmark list, count at +1
-    const int2* trips;          // (act position of pose i's edge, of pose j's edge), landmark order
+    const int2* trips;          // (pose-major position of pose i's edge, of pose j's edge), landmark order
     double *S, *bs, *x;         // x: [6P + 3M]
     double* red;                // reduction scratch
     double *partChi, *partScale, *partMax;   // per-workgroup partials (single-process LM kernels)
@@ -765,7 +767,8 @@ __device__ __forceinline__ void dinv_store(const LbaDev& d, int l, const double 
 }
 // Hpl_e D^-1 (the product of G/core/block_solver.hpp:419) of every free-pose edge of landmark l,
 // edges a0, a0 + stride, ... of its list: formed once per edge and trial here, where D^-1 is in
-// registers, instead of once per pose pair in k_schur_pairs
+// registers, instead of once per pose pair in k_schur_pairs.  It and a copy of Hpl_e go to the
+// edge's pose-major position, so k_schur_pairs reads each pose's blocks as one contiguous run
 __device__ __forceinline__ void hpl_dinv_edges(const LbaDev& d, int l, const double Di[9], int sub, int stride) {
     const int a1 = d.ptStart[l + 1];
     for (int a = d.ptStart[l] + sub; a < a1; a += stride) {
@@ -784,9 +787,14 @@ __device__ __forceinline__ void hpl_dinv_edges(const LbaDev& d, int l, const dou
 #pragma unroll
             for (int q = 0; q < 3; q++)
                 u[r * 3 + q] = __builtin_fma(w[r * 3 + 2], Di[6 + q], __builtin_fma(w[r * 3 + 1], Di[3 + q], w[r * 3] * Di[q]));
-        double2* U = reinterpret_cast<double2*>(d.Ae + 18 * (size_t)k);
+        const size_t o = 18 * (size_t)d.poPos[k];
+        double2* U = reinterpret_cast<double2*>(d.Ae + o);
+        double2* H = reinterpret_cast<double2*>(d.HplP + o);
 #pragma unroll
-        for (int h = 0; h < 9; h++) U[h] = make_double2(u[2 * h], u[2 * h + 1]);
+        for (int h = 0; h < 9; h++) {
+            U[h] = make_double2(u[2 * h], u[2 * h + 1]);
+            H[h] = make_double2(w[2 * h], w[2 * h + 1]);
+        }
     }
 }
 
@@ -803,9 +811,14 @@ __device__ __forceinline__ void hpl_dinv_prefetched(const LbaDev& d, const doubl
             for (int q = 0; q < 3; q++)
                 v[r * 3 + q] = __builtin_fma(f.w[u][r * 3 + 2], Di[6 + q],
                                              __builtin_fma(f.w[u][r * 3 + 1], Di[3 + q], f.w[u][r * 3] * Di[q]));
-        double2* U = reinterpret_cast<double2*>(d.Ae + 18 * (size_t)f.k[u]);
+        const size_t o = 18 * (size_t)d.poPos[f.k[u]];
+        double2* U = reinterpret_cast<double2*>(d.Ae + o);
+        double2* H = reinterpret_cast<double2*>(d.HplP + o);
 #pragma unroll
-        for (int h = 0; h < 9; h++) U[h] = make_double2(v[2 * h], v[2 * h + 1]);
+        for (int h = 0; h < 9; h++) {
+            U[h] = make_double2(v[2 * h], v[2 * h + 1]);
+            H[h] = make_double2(f.w[u][2 * h], f.w[u][2 * h + 1]);
+        }
     }
 }
 
@@ -919,102 +932,123 @@ __global__ __launch_bounds__(256) void k_vertex_schur(LbaDev d, int nChi) {
 }
 
 // Reduced camera system (G/core/block_solver.hpp:408-440): one workgroup per pose-pair block
-// (i <= j, row-major triangular order), S_ij = [i == j](Hpp_i + lambda I) - sum_l (Hpl_il
-// D_l^-1) Hpl_jl^T over the landmarks l seen by both.  The landmarks shared by poses i and j
-// are found by intersecting their landmark-sorted edge lists (pose j's list staged in LDS,
-// one binary search per edge of pose i).  Thread t accumulates the whole 6 x 6 product of
-// pose i's edges t, t + 256, ... in registers (Hpl D^-1 formed on the fly); the 256 partials
-// meet in LDS in a fixed order, so the result is reproducible run to run.  The diagonal
-// blocks also form b_s,i = b_p,i - sum_e Hpl_e D_l^-1 b_l over pose i's edges (rank 0
-// carries Hpp + lambda I and b_p).
+// (i <= j, row-major triangular order; workgroups stride over the listed pairs), S_ij = [i == j]
+// (Hpp_i + lambda I) - sum_l (Hpl_il D_l^-1) Hpl_jl^T over the landmarks l seen by both
+// (k_pair_trip's list).  Thread t accumulates the whole 6 x 6 product of the pair's landmarks
+// t, t + 256, ... in registers (A_e = Hpl_e D^-1 from the landmark kernel); each wave's 64
+// partials of the 36 (42) values meet by recursive halving across the wave (reduce_halve, lane v
+// then holds value v) and the four waves' sums in 2 KB of LDS, in a fixed order, so the result is
+// reproducible run to run.  (The former form reduced 256 partials through 86 KB of LDS: one
+// workgroup per CU.)  The diagonal blocks also form b_s,i = b_p,i - sum_e Hpl_e D_l^-1 b_l over
+// pose i's edges (rank 0 carries Hpp + lambda I and b_p).
 constexpr int kSpT = 256;
 constexpr int kSpList = 4096;   // pose j's landmark list held in LDS up to this length
 constexpr int kSpChunk = 1024;  // pose i's edges looked up per round (4 per thread)
+constexpr int kSpW = kSpT / 64;   // k_schur_pairs: waves per workgroup
+constexpr int kSpMaxWg = 4096;    // k_schur_pairs: workgroups at most (they stride over the pairs; a multiple of 8)
+
+// cur[0 .. 2W) of every lane -> cur[0 .. W): lanes with bit W set keep the upper half, the others
+// the lower, each adding its xor-W partner's copy of the half it keeps
+template <int W>
+__device__ __forceinline__ void reduce_halve(double* cur, int lane) {
+    const bool up = (lane & W) != 0;
+#pragma unroll
+    for (int k = 0; k < W; k++) {
+        const double keep = up ? cur[W + k] : cur[k];
+        const double send = up ? cur[k] : cur[W + k];
+        cur[k] = keep + __shfl_xor(send, W, 64);
+    }
+}
+
 __global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag) {
-    if ((int)blockIdx.x >= *d.npairs) return;   // blocks with no shared landmark stay 0 (zeroed per solve)
-    const int pr = d.pairs[blockIdx.x];
-    const int phase = d.lm->phase;   // loaded with the pair's CSR ranges (one round trip)
-    __shared__ double part[42][kSpT + 1];
-    const int tid = threadIdx.x;
-    const int bi = pr >> 16, bj = pr & 0xFFFF;
-    const bool diag = bi == bj;
-    const int a0 = d.poStart[bi], a1 = d.poStart[bi + 1];
-    if (phase != 1) return;   // lm_off(d.lm, 1)
-    double acc[42];
+    const int np = *d.npairs;   // blocks with no shared landmark stay 0 (zeroed per solve)
+    const int phase = d.lm->phase;
+    if (phase != 1) return;     // lm_off(d.lm, 1)
+    __shared__ double wsum[kSpW][64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // XCD-aware: workgroup b runs on XCD b % 8 (gridDim.x is a multiple of 8), and each XCD takes
+    // one contiguous eighth of the pair list, so a pose's blocks are reused from that XCD's L2
+    const int chunk = (np + 7) >> 3;
+    for (int vb = blockIdx.x; (vb >> 3) < chunk; vb += gridDim.x) {
+        const int k = (vb & 7) * chunk + (vb >> 3);
+        if (k >= np) continue;
+        const int pr = __builtin_amdgcn_readfirstlane(d.pairs[k]);
+        const int bi = pr >> 16, bj = pr & 0xFFFF;
+        const bool diag = bi == bj;
+        double acc[64];
 #pragma unroll
-    for (int i = 0; i < 42; i++) acc[i] = 0.0;
-    // the product of one shared landmark: A_e1 = Hpl_e1 D^-1 (formed per edge by the landmark
-    // kernel) against Hpl_e2; diagonal blocks (e2 == e1) also b_s's Hpl_e1 D^-1 b_l
-    auto product = [&](int e1, int e2, int l) {
-        const double2* Ui = reinterpret_cast<const double2*>(d.Ae + 18 * (size_t)e1);
-        const double2* Bj = reinterpret_cast<const double2*>(d.Hpl_e + 18 * (size_t)e2);
-        double v[18], u[18];
+        for (int i = 0; i < 64; i++) acc[i] = 0.0;
+        // the product of one shared landmark: A_e1 against Hpl_e2; diagonal blocks (e2 == e1) also
+        // b_s's Hpl_e1 D^-1 b_l
+        auto product = [&](int e1, int e2, int l) {
+            const double2* Ui = reinterpret_cast<const double2*>(d.Ae + 18 * (size_t)e1);
+            const double2* Bj = reinterpret_cast<const double2*>(d.HplP + 18 * (size_t)e2);
+            double v[18], u[18];
 #pragma unroll
-        for (int h = 0; h < 9; h++) {
-            const double2 x = Ui[h], y = Bj[h];
-            u[2 * h] = x.x; u[2 * h + 1] = x.y;
-            v[2 * h] = y.x; v[2 * h + 1] = y.y;
-        }
-        // three fused multiply-adds per entry (the terms accumulate straight into the partial)
-#pragma unroll
-        for (int r = 0; r < 6; r++)
-#pragma unroll
-            for (int q = 0; q < 6; q++)
-                acc[r * 6 + q] = __builtin_fma(u[r * 3 + 2], v[q * 3 + 2],
-                                               __builtin_fma(u[r * 3 + 1], v[q * 3 + 1],
-                                                             __builtin_fma(u[r * 3], v[q * 3], acc[r * 6 + q])));
-        if (diag) {
-            const double* db = d.db + 3 * (size_t)l;
-            const double g0 = db[0], g1 = db[1], g2 = db[2];
-#pragma unroll
-            for (int i = 0; i < 6; i++)
-                acc[36 + i] = __builtin_fma(v[i * 3 + 2], g2, __builtin_fma(v[i * 3 + 1], g1, __builtin_fma(v[i * 3], g0, acc[36 + i])));
-        }
-    };
-    if (diag) {   // every edge of pose i pairs with itself: already a dense list
-        for (int a = a0 + tid; a < a1; a += kSpT) {
-            const int e1 = d.poAct[a];
-            product(e1, e1, d.poPt[a]);
-        }
-    } else {
-        // off-diagonal: the pair's shared landmarks, listed once per solve by k_pair_trip
-        const int t0 = d.tripStart[2 * blockIdx.x], tn = d.tripStart[2 * blockIdx.x + 1];
-        for (int m = tid; m < tn; m += kSpT) {
-            const int2 tr = d.trips[t0 + m];
-            product(tr.x, tr.y, 0);
-        }
-    }
-    const int nv = diag ? 42 : 36;
-#pragma unroll
-    for (int i = 0; i < 42; i++)
-        if (i < nv) part[i][tid] = acc[i];
-    __syncthreads();
-    // value v = t >> 2, quarter q = t & 3 sums part[v][64q .. 64q + 63]; quarters meet by xor
-    const int v = tid >> 2, q = tid & 3;
-    double sum = 0.0;
-    if (v < nv) {
-#pragma unroll 8
-        for (int i = 0; i < 64; i++) sum += part[v][64 * q + i];
-    }
-    sum += __shfl_xor(sum, 1, 64);
-    sum += __shfl_xor(sum, 2, 64);
-    // a diagonal block's product (Hpl D^-1) Hpl^T is not bitwise symmetric: only its upper
-    // triangle (r <= qq) is stored, mirrored, as g2o fills S from the upper blocks (the lower
-    // entries written by both threads of a pair would race)
-    if (v < nv && q == 0 && !(diag && v < 36 && v / 6 > v % 6)) {
-        const int n = 6 * d.P;
-        if (v < 36) {
-            const int r = v / 6, qq = v % 6;
-            double val = 0.0;
-            if (diag && addDiag) {
-                val = d.Hpp[36 * (size_t)bi + v];
-                if (r == qq) val += d.lm->lambda;
+            for (int h = 0; h < 9; h++) {
+                const double2 x = Ui[h], y = Bj[h];
+                u[2 * h] = x.x; u[2 * h + 1] = x.y;
+                v[2 * h] = y.x; v[2 * h + 1] = y.y;
             }
-            val -= sum;
-            d.S[(size_t)(6 * bi + r) * n + 6 * bj + qq] = val;
-            d.S[(size_t)(6 * bj + qq) * n + 6 * bi + r] = val;
+            // three fused multiply-adds per entry (the terms accumulate straight into the partial)
+#pragma unroll
+            for (int r = 0; r < 6; r++)
+#pragma unroll
+                for (int q = 0; q < 6; q++)
+                    acc[r * 6 + q] = __builtin_fma(u[r * 3 + 2], v[q * 3 + 2],
+                                                   __builtin_fma(u[r * 3 + 1], v[q * 3 + 1],
+                                                                 __builtin_fma(u[r * 3], v[q * 3], acc[r * 6 + q])));
+            if (diag) {
+                const double* db = d.db + 3 * (size_t)l;
+                const double g0 = db[0], g1 = db[1], g2 = db[2];
+#pragma unroll
+                for (int i = 0; i < 6; i++)
+                    acc[36 + i] = __builtin_fma(v[i * 3 + 2], g2, __builtin_fma(v[i * 3 + 1], g1, __builtin_fma(v[i * 3], g0, acc[36 + i])));
+            }
+        };
+        if (diag) {   // every edge of pose i pairs with itself: already a dense list
+            const int a0 = d.poStart[bi], a1 = d.poStart[bi + 1];
+            for (int a = a0 + tid; a < a1; a += kSpT) product(a, a, d.poPt[a]);
         } else {
-            d.bs[6 * bi + v - 36] = (addDiag ? d.bp[6 * bi + v - 36] : 0.0) - sum;
+            // off-diagonal: the pair's shared landmarks, listed once per solve by k_pair_trip
+            const int t0 = d.tripStart[2 * k], tn = d.tripStart[2 * k + 1];
+            for (int m = tid; m < tn; m += kSpT) {
+                const int2 tr = d.trips[t0 + m];
+                product(tr.x, tr.y, 0);
+            }
+        }
+        reduce_halve<32>(acc, lane);
+        reduce_halve<16>(acc, lane);
+        reduce_halve<8>(acc, lane);
+        reduce_halve<4>(acc, lane);
+        reduce_halve<2>(acc, lane);
+        reduce_halve<1>(acc, lane);
+        wsum[wave][lane] = acc[0];   // value v = lane
+        __syncthreads();
+        const int v = lane, nv = diag ? 42 : 36;
+        double sum = 0.0;
+        if (wave == 0) {
+#pragma unroll
+            for (int w = 0; w < kSpW; w++) sum += wsum[w][v];
+        }
+        __syncthreads();   // wsum is rewritten by the next pair
+        // a diagonal block's product (Hpl D^-1) Hpl^T is not bitwise symmetric: only its upper
+        // triangle (r <= qq) is stored, mirrored, as g2o fills S from the upper blocks
+        if (wave == 0 && v < nv && !(diag && v < 36 && v / 6 > v % 6)) {
+            const int n = 6 * d.P;
+            if (v < 36) {
+                const int r = v / 6, qq = v % 6;
+                double val = 0.0;
+                if (diag && addDiag) {
+                    val = d.Hpp[36 * (size_t)bi + v];
+                    if (r == qq) val += d.lm->lambda;
+                }
+                val -= sum;
+                d.S[(size_t)(6 * bi + r) * n + 6 * bj + qq] = val;
+                d.S[(size_t)(6 * bj + qq) * n + 6 * bi + r] = val;
+            } else {
+                d.bs[6 * bi + v - 36] = (addDiag ? d.bp[6 * bi + v - 36] : 0.0) - sum;
+            }
         }
     }
 }
@@ -1096,9 +1130,15 @@ __global__ __launch_bounds__(1024) void k_pair_list(const int32_t* __restrict__ 
     if (tid == 1023) *npairs = run;
 }
 
+// the inverse of the pose-major lists: poPos[poAct[a]] = a
+__global__ __launch_bounds__(256) void k_po_pos(LbaDev d, int32_t* __restrict__ poPos) {
+    const int a = blockIdx.x * 256 + threadIdx.x;
+    if (a < d.poStart[d.P]) poPos[d.poAct[a]] = a;
+}
+
 // Once per solve (the block structure is fixed for both optimize() rounds): every off-diagonal
-// pair's shared landmarks as (pose i's edge, pose j's edge) act positions in pose i's landmark
-// order.  Four edges of pose i per thread are looked up in pose j's sorted landmark list (LDS up
+// pair's shared landmarks as (pose i's edge, pose j's edge) pose-major positions in pose i's
+// landmark order.  Four edges of pose i per thread are looked up in pose j's sorted landmark list (LDS up
 // to kSpList entries) and the matches compacted in thread order (a workgroup scan).
 __global__ __launch_bounds__(kSpT) void k_pair_trip(LbaDev d, int2* __restrict__ trips) {
     if ((int)blockIdx.x >= *d.npairs) return;
@@ -1121,7 +1161,7 @@ __global__ __launch_bounds__(kSpT) void k_pair_trip(LbaDev d, int2* __restrict__
 #pragma unroll
         for (int u = 0; u < kSpChunk / kSpT; u++) {
             const int a = min(base + tid + kSpT * u, a1 - 1);   // clamped: unconditional loads
-            m1[u] = d.poAct[a];
+            m1[u] = a;
             const int lv = d.poPt[a];
             lm[u] = base + tid + kSpT * u < a1 ? lv : -1;
         }
@@ -1136,8 +1176,7 @@ __global__ __launch_bounds__(kSpT) void k_pair_trip(LbaDev d, int2* __restrict__
                 else hi = mid;
             }
             const bool hit = l >= 0 && lo < nb && Lj[lo] == l;
-            const int e2 = d.poAct[b0 + min(lo, nb - 1)];
-            m2[u] = hit ? e2 : -1;
+            m2[u] = hit ? b0 + lo : -1;
             cnt += hit ? 1 : 0;
         }
         const int incl = wave_incl_scan_i32(cnt);
@@ -3573,7 +3612,7 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
     TRY(dalloc(c, &d.Hpl_e, 18 * (size_t)NE)); TRY(dalloc(c, &d.bl_e, 3 * (size_t)NE));
     TRY(dalloc(c, &d.bp_e, 6 * (size_t)NE));
     TRY(dalloc(c, &d.echi, (size_t)NE + 6 * (size_t)NP + 3 * (size_t)NM));
-    TRY(dalloc(c, &d.Ae, 18 * (size_t)NE));
+    TRY(dalloc(c, &d.Ae, 18 * (size_t)NE)); TRY(dalloc(c, &d.HplP, 18 * (size_t)NE));
     TRY(dalloc(c, &d.Hll, 9 * (size_t)NM)); TRY(dalloc(c, &d.bl, 3 * (size_t)NM)); TRY(dalloc(c, &d.Dinv, 9 * (size_t)NM));
     TRY(dalloc(c, &d.db, 3 * (size_t)NM));
     TRY(dalloc(c, &d.Hpp, 36 * (size_t)NP)); TRY(dalloc(c, &d.bp, 6 * (size_t)NP));
@@ -3772,7 +3811,8 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
             hipLaunchKernelGGL(k_schur_msum, dim3(nt + (d.P + 3) / 4), dim3(256), 0, s, d, d_ypart, nch, npm,
                                d_ce, root ? 1 : 0);
         } else if (npairs > 0) {
-            hipLaunchKernelGGL(k_schur_pairs, dim3(npairs), dim3(kSpT), 0, s, d, root ? 1 : 0);
+            hipLaunchKernelGGL(k_schur_pairs, dim3(std::min((npairs + 7) & ~7, kSpMaxWg)), dim3(kSpT), 0, s, d,
+                               root ? 1 : 0);
             boundary();
         }
         if (d.P > 0) TRY(comm_allreduce_schur(c, d.S, d.bs, d.pairs, gPairs, d.P, d.lm, 1));
@@ -4008,8 +4048,12 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         for (int e = 0; e < NE; e++) kf[(size_t)p->edge_point[e]] += p->pose_fixed[p->edge_pose[e]] ? 0 : 1;
         size_t ntrip = 0;
         for (int l = 0; l < NM; l++) ntrip += (size_t)kf[(size_t)l] * (kf[(size_t)l] - 1) / 2;
-        int32_t *flag, *cnt, *pairs, *npairs, *tripStart;
+        int32_t *flag, *cnt, *pairs, *npairs, *tripStart, *poPos;
         int2* trips;
+        TRY(dalloc(c, &poPos, std::max(NE, 1)));
+        ORB_HIP_TRY(hipMemsetAsync(poPos, 0xFF, 4 * (size_t)std::max(NE, 1), s));   // -1: fixed-pose edges
+        if (P > 0) hipLaunchKernelGGL(k_po_pos, grid(NE), dim3(256), 0, s, d, poPos);
+        d.poPos = poPos;
         TRY(dalloc(c, &flag, 2 * (size_t)np2)); TRY(dalloc(c, &pairs, np2)); TRY(dalloc(c, &npairs, 1));
         TRY(dalloc(c, &tripStart, 2 * (size_t)np2)); TRY(dalloc(c, &trips, std::max<size_t>(ntrip, 1)));
         cnt = flag + np2;

@@ -20,10 +20,10 @@ for a in sys.argv[1:]:
 # corridor=1: the scaled window generator (synth.ba_problem_corridor, banded covisibility)
 gen = synth.ba_problem_corridor if kw.pop("corridor", 0) else synth.ba_problem
 group = kw.pop("group", 0)
+n = kw.pop("solves", 12)   # (under rocprofv3's kernel trace, 200 KF runs keep to a few solves)
 pb = gen(**kw)
 print(f"problem: {len(pb['Tcw'])} keyframes, {len(pb['point_xyz'])} points, {len(pb['edge_point'])} edges", flush=True)
 ba = amd.LocalBAGroup([0] * group) if group else amd.LocalBA()
-n = 12
 call = ba.prepared(pb)
 ts = []
 for i in range(n):
@@ -35,7 +35,7 @@ for i in range(n):
     if group and i == 3:
         ex0 = ba.stats()
 import statistics  # noqa: E402
-print(f"median of solves 4..{n - 1}: {1e3 * statistics.median(ts[4:]):.3f} ms", flush=True)
+print(f"median of solves {min(4, n - 1)}..{n - 1}: {1e3 * statistics.median(ts[min(4, n - 1):]):.3f} ms", flush=True)
 if group:
     ex1 = ba.stats()
     nc = ex1[1] - ex0[1]
