@@ -2169,6 +2169,7 @@ constexpr int kSB = 128;   // (64 measured no faster at np = 1224: 24.1 vs 23.7-
 __global__ __launch_bounds__(512) void k_ldlt_mw_bsolve(MwLdl m, int K0, double* __restrict__ x, int* __restrict__ flags,
                                                         const LmState* st, PoseTail ptail, int first, int last) {
     if (lm_off(st, 1)) return;
+    TSTAMP(t_b0);
     extern __shared__ __attribute__((aligned(16))) double bsm[];
     double* Ls = bsm;                        // [kSB][kSB + 1]: L(K0 + r, K0 + c), c < r
     double* ysb = Ls + kSB * (kSB + 1);      // [kSB]  (LDS independent of the order: any window size)
@@ -2189,47 +2190,60 @@ __global__ __launch_bounds__(512) void k_ldlt_mw_bsolve(MwLdl m, int K0, double*
         }
     else
         for (int r = tid; r < nsb; r += 512) ysb[r] = m.yb[K0 + r];
-    {   // all kSB^2 / 512 loads of a thread in flight at once (a load per iteration serialised on
-        // the memory latency: the rows were just written by trailing updates on other XCDs)
-        constexpr int kPer = kSB * kSB / 512;
+    {   // the strict lower triangle only (the chain and the updates read nothing else), row-major
+        // triangle order (coalesced rows); every load unconditional at a clamped index, all of a
+        // thread's in flight at once (the rows were just written by trailing updates on other XCDs)
+        constexpr int kPer = (kSB * (kSB - 1) / 2 + 511) / 512;
+        const int ntri = nsb * (nsb - 1) / 2;
         double v[kPer];
+        int at[kPer];
 #pragma unroll
         for (int k = 0; k < kPer; k++) {
-            const int t = tid + 512 * k, r = t / kSB, c = t % kSB;
+            int r, c;
+            tri_index(min(tid + 512 * k, max(ntri - 1, 0)), r, c);   // (r, c), c <= r
+            r += 1;                                                   // strict: c < r
             const bool sameBlk = (K0 + r) / kMwNB == (K0 + c) / kMwNB;   // a panel's diagonal block: from Ldg
-            v[k] = c >= r || r >= nsb ? 0.0
-                   : sameBlk          ? m.Ldg[(size_t)(K0 + r) * kMwNB + (K0 + c) % kMwNB]
-                                      : m.A[(size_t)(K0 + r) * ld + K0 + c];
+            v[k] = sameBlk ? m.Ldg[(size_t)(K0 + r) * kMwNB + (K0 + c) % kMwNB] : m.A[(size_t)(K0 + r) * ld + K0 + c];
+            at[k] = r * (kSB + 1) + c;
         }
 #pragma unroll
-        for (int k = 0; k < kPer; k++) {
-            const int t = tid + 512 * k;
-            Ls[(t / kSB) * (kSB + 1) + t % kSB] = v[k];
-        }
+        for (int k = 0; k < kPer; k++)
+            if (tid + 512 * k < ntri) Ls[at[k]] = v[k];
     }
     __syncthreads();
-    for (int jb = nsb - kNB; jb >= 0; jb -= kNB) {
+    TSTAMP(t_b1);
+    // kBB-row blocks bottom-up: wave 0 solves the block's triangle (its L entries read from LDS
+    // first, then the v_readlane chain), then every thread takes one row above the block
+    constexpr int kBB = 32;
+    for (int jb = nsb - kBB; jb >= 0; jb -= kBB) {
         if (wave == 0) {
-            const int r = lane & 15;
+            const int r = lane & (kBB - 1);
+            double Lb[kBB];
+#pragma unroll
+            for (int c = 1; c < kBB; c++) Lb[c] = Ls[(jb + c) * (kSB + 1) + jb + min(r, c - 1)];
             double xb = ysb[jb + r];
 #pragma unroll
-            for (int c = kNB - 1; c > 0; c--) {
+            for (int c = kBB - 1; c > 0; c--) {
                 const double xc = shfl_d(xb, c);
-                xb = r < c ? __builtin_fma(-Ls[(jb + c) * (kSB + 1) + jb + r], xc, xb) : xb;
+                xb = r < c ? __builtin_fma(-Lb[c], xc, xb) : xb;
             }
-            if (lane < kNB) ysb[jb + r] = xb;
+            if (lane < kBB) ysb[jb + r] = xb;
         }
         __syncthreads();
-        for (int i = tid; i < jb; i += 512) {
-            double v = ysb[i];
+        for (int i = tid; i < jb; i += 512) {   // four partial sums: a quarter of the dependent chain
+            double v[4] = {ysb[i], 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int c = kNB - 1; c >= 0; c--) v = __builtin_fma(-Ls[(jb + c) * (kSB + 1) + i], ysb[jb + c], v);
-            ysb[i] = v;
+            for (int c = kBB - 1; c >= 0; c--)
+                v[c & 3] = __builtin_fma(-Ls[(jb + c) * (kSB + 1) + i], ysb[jb + c], v[c & 3]);
+            ysb[i] = (v[0] + v[1]) + (v[2] + v[3]);
         }
         __syncthreads();
     }
     for (int r = tid; r < nsb; r += 512)
         if (K0 + r < n) x[K0 + r] = ysb[r];
+#ifdef ORB_TIMING
+    if (tid == 0) printf("mw bsolve K0 %d: stage %lld chain %lld\n", K0, t_b1 - t_b0, clock64() - t_b1);
+#endif
     if (!last) return;
     if (tid == 0) flags[0] = 0;
     if (ptail.scaleOut) {   // x as stored: this super-block's rows just now (visible to the workgroup
