@@ -374,18 +374,29 @@ __device__ __forceinline__ double edge_error_s(const LbaDev& d, int k, const Edg
 // computeError (edge_error's arithmetic) then the Jacobians and Huber-weighted quadratic-form
 // blocks of active edge k from the error just computed (no reload).  Returns the robust chi2.
 // Hll_e: 3x3 upper (00 01 02 11 12 22); Hpp_e: 6x6 upper row-major (21); Hpl_e: 6x3; bl_e: 3; bp_e: 6
+// (formed in registers; edge_lin_body stores them coalesced through LDS)
+struct EdgeBlocks {
+    double hl[6], bl[3], hp[21], bp[6], hpl[18];
+};
+constexpr int kEdgeStageMin = 100000;   // k_edge_lin<true> (stores through LDS) from this many active edges
+// kStage: the blocks go to `ob` (zeroed by the caller) for edge_lin_body's coalesced stores;
+// otherwise each lane stores its own rows (free-pose edges only for the pose blocks)
+template <bool kStage>
 __device__ __forceinline__ double edge_error_lin(const LbaDev& d, int k, const EdgeStatic& s, double hmono,
-                                                 double hstereo, const double* qp, const double* tp, const double* Xp) {
+                                                 double hstereo, const double* qp, const double* tp, const double* Xp,
+                                                 EdgeBlocks& ob) {
     const int e = s.e, pose = s.pose;
     const bool freePose = d.poseIdx[pose] >= 0;
     if (!s.on) {   // level-1 edge: chi2 0, its stored error stays, its blocks are exact zeros
         d.echi[k] = 0.0;
-        for (int i = 0; i < 6; i++) d.Hll_e[6 * (size_t)k + i] = 0.0;
-        for (int i = 0; i < 3; i++) d.bl_e[3 * (size_t)k + i] = 0.0;
-        if (freePose) {
-            for (int i = 0; i < 21; i++) d.Hpp_e[21 * (size_t)k + i] = 0.0;
-            for (int i = 0; i < 6; i++) d.bp_e[6 * (size_t)k + i] = 0.0;
-            for (int i = 0; i < 18; i++) d.Hpl_e[18 * (size_t)k + i] = 0.0;
+        if (!kStage) {
+            for (int i = 0; i < 6; i++) d.Hll_e[6 * (size_t)k + i] = 0.0;
+            for (int i = 0; i < 3; i++) d.bl_e[3 * (size_t)k + i] = 0.0;
+            if (freePose) {
+                for (int i = 0; i < 21; i++) d.Hpp_e[21 * (size_t)k + i] = 0.0;
+                for (int i = 0; i < 6; i++) d.bp_e[6 * (size_t)k + i] = 0.0;
+                for (int i = 0; i < 18; i++) d.Hpl_e[18 * (size_t)k + i] = 0.0;
+            }
         }
         return 0.0;
     }
@@ -464,8 +475,8 @@ __device__ __forceinline__ double edge_error_lin(const LbaDev& d, int k, const E
     for (int r = 0; r < 3; r++) om[r] = r < D ? -(w * er[r]) * rho1 : 0.0;
     // the products below run over all 3 rows: a mono edge's third Jacobian row and om[2] are
     // zero, so the extra terms add exact zeros (constant trip counts keep A, B in registers)
-    double* hl = d.Hll_e + 6 * (size_t)k;
-    double* bl = d.bl_e + 3 * (size_t)k;
+    double* hl = kStage ? ob.hl : d.Hll_e + 6 * (size_t)k;
+    double* bl = kStage ? ob.bl : d.bl_e + 3 * (size_t)k;
     {
         int o = 0;
         for (int i = 0; i < 3; i++) {
@@ -479,10 +490,10 @@ __device__ __forceinline__ double edge_error_lin(const LbaDev& d, int k, const E
             }
         }
     }
-    if (freePose) {
-        double* hp = d.Hpp_e + 21 * (size_t)k;
-        double* bp = d.bp_e + 6 * (size_t)k;
-        double* hpl = d.Hpl_e + 18 * (size_t)k;
+    if (kStage || freePose) {   // (staged, a fixed pose's edge fills its unused slots: nothing reads them)
+        double* hp = kStage ? ob.hp : d.Hpp_e + 21 * (size_t)k;
+        double* bp = kStage ? ob.bp : d.bp_e + 6 * (size_t)k;
+        double* hpl = kStage ? ob.hpl : d.Hpl_e + 18 * (size_t)k;
         int o = 0;
         for (int i = 0; i < 6; i++) {
             double sm = 0;
@@ -517,10 +528,12 @@ __device__ __forceinline__ void edge_vars(const LbaDev& d, const EdgeStatic& es,
 #pragma unroll
     for (int i = 0; i < 3; i++) v.X[i] = d.X[3 * (size_t)es.pt + i];
 }
+template <bool kStage>
 __device__ __forceinline__ void edge_lin_body(const LbaDev& d, const EdgeStatic& es, const EdgeVars& ev, double hmono,
                                               double hstereo, int fuse);
 // Fused slots: first takes the previous trial's pending decision (lm_decide_local; workgroup
 // 0 writes it back) and, after a rejection, restores this workgroup's slice of the estimates.
+template <bool kStage>
 __global__ __launch_bounds__(64) void k_edge_lin(LbaDev d, double hmono, double hstereo, int fuse, LmFuse f) {
     const EdgeStatic es = edge_static(d, max(min((int)(blockIdx.x * 64 + threadIdx.x), d.nact - 1), 0));
     // the estimates as they stand: what the linearisation reads unless the decision below pops
@@ -545,21 +558,53 @@ __global__ __launch_bounds__(64) void k_edge_lin(LbaDev d, double hmono, double 
             db.t = d.bt;
             EdgeVars evb;
             edge_vars(db, es, evb);
-            edge_lin_body(db, es, evb, hmono, hstereo, fuse);
+            edge_lin_body<kStage>(db, es, evb, hmono, hstereo, fuse);
             return;
         }
     } else if (lm_off(d.lm, 0)) {
         return;
     }
-    edge_lin_body(d, es, ev, hmono, hstereo, fuse);
+    edge_lin_body<kStage>(d, es, ev, hmono, hstereo, fuse);
 }
+template <bool kStage>
 __device__ __forceinline__ void edge_lin_body(const LbaDev& d, const EdgeStatic& es, const EdgeVars& ev, double hmono,
                                               double hstereo, int fuse) {
     const int k = blockIdx.x * 64 + threadIdx.x;
     double chi = 0.0;
-    if (k < d.nact) chi = edge_error_lin(d, k, es, hmono, hstereo, ev.q, ev.t, ev.X);
+    EdgeBlocks ob;
+    if (kStage) {
+#pragma unroll
+        for (int i = 0; i < 6; i++) ob.hl[i] = 0.0;
+#pragma unroll
+        for (int i = 0; i < 3; i++) ob.bl[i] = 0.0;
+#pragma unroll
+        for (int i = 0; i < 21; i++) ob.hp[i] = 0.0;
+#pragma unroll
+        for (int i = 0; i < 6; i++) ob.bp[i] = 0.0;
+#pragma unroll
+        for (int i = 0; i < 18; i++) ob.hpl[i] = 0.0;
+    }
+    if (k < d.nact) chi = edge_error_lin<kStage>(d, k, es, hmono, hstereo, ev.q, ev.t, ev.X, ob);
     const double sum = wave_sum_d(chi);
     if (threadIdx.x == 0) (fuse ? d.partLin : d.partChi)[blockIdx.x] = sum;
+    if (!kStage) return;
+    // the wave's 64 edges' blocks, each array through LDS, then stored as one contiguous run (a
+    // lane writing its own 168-byte row makes every store instruction touch 64 lines: 1.9x the
+    // bytes below L2 at 200 KF, PMC).  Small problems take k_edge_lin<false> (latency-bound there:
+    // the LDS round trips cost more than the lines).
+    __shared__ double stg[64 * 21];
+    const int base = blockIdx.x * 64, nk = min(d.nact - base, 64), lane = threadIdx.x;
+    auto put = [&](double* dst, const double* v, int W) {
+        for (int i = 0; i < W; i++) stg[lane * W + i] = v[i];
+        __syncthreads();
+        for (int t = lane; t < nk * W; t += 64) dst[(size_t)base * W + t] = stg[t];
+        __syncthreads();
+    };
+    put(d.Hpp_e, ob.hp, 21);
+    put(d.Hpl_e, ob.hpl, 18);
+    put(d.bp_e, ob.bp, 6);
+    put(d.Hll_e, ob.hl, 6);
+    put(d.bl_e, ob.bl, 3);
 }
 
 // Vertex blocks (256 threads): workgroups [0, P) reduce Hpp, b_p of one free pose over its
@@ -3791,7 +3836,10 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
                        d_trace};
         const bool extraB = std::getenv("ORB_LBA_EXTRA_BOUNDARY") != nullptr;
         auto boundary = [&]() { if (extraB) hipLaunchKernelGGL(k_nop, dim3(256), dim3(64), 0, s); };
-        if (d.nact > 0) hipLaunchKernelGGL(k_edge_lin, dim3(nbE), dim3(64), 0, s, d, hm, hsv, fuse ? 1 : 0, f);
+        if (d.nact >= kEdgeStageMin)
+            hipLaunchKernelGGL(k_edge_lin<true>, dim3(nbE), dim3(64), 0, s, d, hm, hsv, fuse ? 1 : 0, f);
+        else if (d.nact > 0)
+            hipLaunchKernelGGL(k_edge_lin<false>, dim3(nbE), dim3(64), 0, s, d, hm, hsv, fuse ? 1 : 0, f);
         boundary();
         LbaDev dv = d;
         if (fuse) dv.lm = d.lmMid;
