@@ -1104,10 +1104,12 @@ __global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag) {
 // block (with a communicator a block may get its terms on another rank only).
 // (the per-pair landmark counts go through an LDS histogram when the pair table fits: a few
 // hundred global counters hit by every landmark serialise on their atomics)
-constexpr int kPairHist = 8192;
+// (dynamic LDS of np2 counters up to kPairHist: 144 KB, 268 poses; 200 KF's 20,100 pairs through
+// global atomics took 270 us per solve)
+constexpr int kPairHist = 36864;
 __global__ __launch_bounds__(256) void k_pair_mark(LbaDev d, int32_t* __restrict__ flag, int32_t* __restrict__ cnt,
                                                    int all) {
-    __shared__ int32_t hist[kPairHist];
+    extern __shared__ int32_t hist[];
     const int P = d.P, np2 = P * (P + 1) / 2;
     const bool lds = np2 <= kPairHist;
     const int t = blockIdx.x * 256 + threadIdx.x;
@@ -4147,7 +4149,8 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
                 c->gflagStage = gflag;   // (kept: the copy is asynchronous)
                 ORB_HIP_TRY(hipMemcpyAsync(flag, c->gflagStage.data(), 4 * (size_t)np2, hipMemcpyHostToDevice, s));
             }
-            hipLaunchKernelGGL(k_pair_mark, grid(std::max(d.M, P)), dim3(256), 0, s, d, flag, cnt, 0);
+            hipLaunchKernelGGL(k_pair_mark, grid(std::max(d.M, P)), dim3(256), np2 <= kPairHist ? 4 * (size_t)np2 : 0, s, d,
+                               flag, cnt, 0);
             hipLaunchKernelGGL(k_pair_list, dim3(1), dim3(1024), 0, s, flag, cnt, P, pairs, npairs, tripStart);
             d.pairs = pairs;
             d.npairs = npairs;
