@@ -641,7 +641,7 @@ __device__ __forceinline__ void pose_prefetch(const LbaDev& d, int p, PosePrefet
 __device__ __forceinline__ double pose_block_reduce(const LbaDev& d, int p, double (*part)[257],
                                                     const PosePrefetch& f) {
     const int tid = threadIdx.x, g = tid >> 5, v = min(tid & 31, 26);
-    int* idx = reinterpret_cast<int*>(&part[0][0]);   // (27 * 257 doubles hold kPoseIdx ints)
+    int* idx = reinterpret_cast<int*>(&part[0][0]);   // (9 * 257 doubles hold kPoseIdx ints)
 #pragma unroll
     for (int u = 0; u < kPoseIdx / 256; u++) idx[tid + 256 * u] = f.k[u];
     __syncthreads();
@@ -766,7 +766,7 @@ __device__ __forceinline__ void landmark_store(const LbaDev& d, int l, const dou
 __global__ __launch_bounds__(256) void k_vertex_reduce(LbaDev d) {
     if (lm_off(d.lm, 0)) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    __shared__ double part[27][257];
+    __shared__ double part[9][257];   // (the pose blocks' 8 group partials + the sums; kPoseIdx ints alias it)
     __shared__ double wmax[4];
     if ((int)blockIdx.x < d.P) {
         PosePrefetch pf;
@@ -917,7 +917,7 @@ __global__ __launch_bounds__(64) void k_point_schur(LbaDev d, int fuse, int nChi
 // iteration starts here (lm_begin at it > 0 leaves lambda alone, so only workgroup 0, which
 // writes the state to lm, sums k_edge_lin's chi2 partials).
 __global__ __launch_bounds__(256) void k_vertex_schur(LbaDev d, int nChi) {
-    __shared__ double part[27][257];
+    __shared__ double part[9][257];   // (the pose blocks' 8 group partials + the sums; kPoseIdx ints alias it)
     __shared__ double lamS;
     __shared__ int ph0S, phS;
     const int tid = threadIdx.x, lane = tid & 63;
