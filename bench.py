@@ -717,7 +717,18 @@ def _extract_leg(amd, dev, frames, nf, steps, warmup, pairs_fn=None, matcher=Non
     return dt, buf
 
 
-EUROC_MBF = 47.9   # R/Examples/Stereo/EuRoC.yaml Camera.bf (435.2 fx x 0.11 m)
+def _camera(name):
+    """The reference's YAML camera settings (synth.CAMERAS, pinned to the YAMLs by
+    tests/test_reference_data.py); synth.py is loaded on its own, so no HIP library loads here."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("_orb_synth_cams", ROOT / "orb-slam2-_amd" / "synth.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.CAMERAS[name]
+
+
+# Camera.bf as Tracking reads it into the float mbf (R/Examples/Stereo/EuRoC.yaml:25, R/src/Tracking.cpp:95)
+EUROC_MBF = float(np.float32(_camera("EUROC")["bf"]))
 
 
 def _timed_ranks(fn, steps, warmup, dev, world):
@@ -857,7 +868,7 @@ def cpu_baseline_stereo(cv, W, H, NF, mbf, n_pairs):
                       f"oracle C restatement, 1 pair per host thread"}
 
 
-KITTI_MBF = 386.1448   # R/Examples/Stereo/KITTI00-02.yaml Camera.bf
+KITTI_MBF = float(np.float32(_camera("KITTI00")["bf"]))   # R/Examples/Stereo/KITTI00-02.yaml Camera.bf
 
 
 def bench_stereo_kitti(args, amd, dev, P=32):

@@ -76,8 +76,26 @@ def stream(seed: int, W: int, H: int, n: int) -> np.ndarray:
 
 # ---------------------------------------------------------------- local-BA problem
 
-TUM1 = (517.306408, 516.469215, 318.643040, 255.313989)
-KITTI_BF = 386.1448
+# The reference's camera / extractor settings for the BASELINE configs, as the example YAMLs hold
+# them (data values; tests/test_reference_data.py parses the YAMLs and pins every entry):
+#   TUM1      R/Examples/Monocular/TUM1.yaml       (config 1; configs 2 and 4 use its intrinsics)
+#   KITTI00   R/Examples/Stereo/KITTI00-02.yaml    (config 3)
+#   EUROC     R/Examples/Stereo/EuRoC.yaml         (config 5)
+# bf is the YAML's Camera.bf (Frame::mbf, a float: the stereo Frame reads it through cv::FileStorage
+# into the float Tracking::mbf, R/src/Tracking.cpp:95, include/Tracking.h:194); 0 for the monocular
+# camera.
+CAMERAS = {
+    "TUM1": dict(fx=517.306408, fy=516.469215, cx=318.643040, cy=255.313989, bf=0.0, width=640, height=480,
+                 nFeatures=1000, scaleFactor=1.2, nLevels=8, iniThFAST=20, minThFAST=7),
+    "KITTI00": dict(fx=718.856, fy=718.856, cx=607.1928, cy=185.2157, bf=386.1448, width=1241, height=376,
+                    nFeatures=2000, scaleFactor=1.2, nLevels=8, iniThFAST=20, minThFAST=7, ThDepth=35),
+    "EUROC": dict(fx=435.2046959714599, fy=435.2046959714599, cx=367.4517211914062, cy=252.2008514404297,
+                  bf=47.90639384423901, width=752, height=480,
+                  nFeatures=1200, scaleFactor=1.2, nLevels=8, iniThFAST=20, minThFAST=7, ThDepth=35),
+}
+TUM1 = tuple(CAMERAS["TUM1"][k] for k in ("fx", "fy", "cx", "cy"))
+KITTI_BF = CAMERAS["KITTI00"]["bf"]
+EUROC_BF = CAMERAS["EUROC"]["bf"]
 
 
 def _rot(axis_angle):

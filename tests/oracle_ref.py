@@ -4,13 +4,16 @@ TEST INFRASTRUCTURE: used only by tests/, __graft_entry__.smoke() and bench.py's
 cpu_baseline leg, as the checker.  Never imported by the product package.
 """
 import ctypes as C
+import os
 import pathlib
 import subprocess
 
 import numpy as np
 
 ROOT = pathlib.Path(__file__).resolve().parents[1]
-LIB_PATH = ROOT / "oracle" / "build" / "liborb_oracle.so"
+# ORB_ORACLE_LIB: another build of the same sources (tools/sanitize_cpu.sh points it at the
+# ASan/UBSan build, oracle/build/asan/liborb_oracle.so)
+LIB_PATH = pathlib.Path(os.environ.get("ORB_ORACLE_LIB", ROOT / "oracle" / "build" / "liborb_oracle.so"))
 
 
 class KeyPoint(C.Structure):

@@ -9,6 +9,7 @@ Map types carrying the member names the reference's own types have:
     (R/src/Optimizer.cpp:567-782) from the mock keyframes, solves within the oracle's tolerances
     (identical LM decisions and erase set, poses / points to 1e-5), and writes back (:850-917)
     exactly what lba_solve returns, erasing mono observations before stereo ones."""
+import os
 import pathlib
 import shutil
 import subprocess
@@ -25,6 +26,8 @@ LIB_DIR = ROOT / "orb-slam2-_amd" / "lib"
 
 @pytest.fixture(scope="module")
 def shim(tmp_path_factory):
+    if os.environ.get("ORB_SHIM_CALLER"):   # a prebuilt caller (tools/sanitize_cpu.sh: the ASan/UBSan build)
+        return pathlib.Path(os.environ["ORB_SHIM_CALLER"])
     gxx = shutil.which("g++")
     if gxx is None or not (LIB_DIR / "liborbslam2_amd.so").exists():
         pytest.skip("g++ or the built library is missing")

@@ -22,10 +22,13 @@ import numpy as np
 import pytest
 
 import oracle_ref as O
+from orb_slam2_amd import synth
 from test_cpp_shim import GRID, _frame_arrays, _read, _run, _write, shim  # noqa: F401  (fixture)
 
 pytestmark = pytest.mark.gpu
 F32 = np.float32
+# Camera.bf of R/Examples/Stereo/EuRoC.yaml / KITTI00-02.yaml as the float Frame::mbf
+EUROC_BF, KITTI_BF = (float(F32(synth.CAMERAS[k]["bf"])) for k in ("EUROC", "KITTI00"))
 
 
 # ------------------------------------------------------------------ PoseOptimization
@@ -107,7 +110,7 @@ def _check_stereo(outp, imgs, NF, mbf):
     assert int((ur >= 0).sum()) == n_ref and n_ref > 300
 
 
-@pytest.mark.parametrize("W,H,NF,seed,mbf", [(752, 480, 1200, 0x5EED0005, 47.9), (1241, 376, 2000, 0x5EED0003, 386.1448)])
+@pytest.mark.parametrize("W,H,NF,seed,mbf", [(752, 480, 1200, 0x5EED0005, EUROC_BF), (1241, 376, 2000, 0x5EED0003, KITTI_BF)])
 def test_shim_stereo_frame(shim, tmp_path, W, H, NF, seed, mbf):
     arrays, imgs = _stereo_inputs(W, H, NF, seed, 2, mbf)
     r, outp = _run(shim, "stereo", tmp_path, *arrays)
@@ -325,8 +328,8 @@ def test_shim_threading_contract(shim, tmp_path, amd):
     import subprocess
     from orb_slam2_amd import synth
     # stereo jobs
-    st_a, imgs_a = _stereo_inputs(752, 480, 1200, 0x5EED0005, 4, 47.9)
-    st_b, imgs_b = _stereo_inputs(1241, 376, 2000, 0x5EED0003, 1, 386.1448)
+    st_a, imgs_a = _stereo_inputs(752, 480, 1200, 0x5EED0005, 4, EUROC_BF)
+    st_b, imgs_b = _stereo_inputs(1241, 376, 2000, 0x5EED0003, 1, KITTI_BF)
     _write(tmp_path / "st_a.in", *st_a)
     _write(tmp_path / "st_b.in", *st_b)
     # SearchForInitialization job
@@ -354,8 +357,8 @@ def test_shim_threading_contract(shim, tmp_path, amd):
     argv = [str(shim), "threads", str(out), "6"] + [x for m, f in jobs for x in (m, str(tmp_path / f))]
     r = subprocess.run(argv, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, (r.returncode, r.stderr)
-    _check_stereo(f"{out}.0", imgs_a, 1200, 47.9)
-    _check_stereo(f"{out}.4", imgs_b, 2000, 386.1448)
+    _check_stereo(f"{out}.0", imgs_a, 1200, EUROC_BF)
+    _check_stereo(f"{out}.4", imgs_b, 2000, KITTI_BF)
     n, m12, _, _ = _read(f"{out}.1", np.int32, np.int32, F32, np.int32)
     fa, fb = O.FrameView(a["kps"], a["desc"], 640, 480), O.FrameView(b["kps"], b["desc"], 640, 480)
     n_ref, m_ref, _ = O.search_for_initialization(fa, fb, prev.copy(), nnratio=0.9, window=100)

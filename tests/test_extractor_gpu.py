@@ -4,8 +4,11 @@ import numpy as np
 import pytest
 
 import oracle_ref as O
+from orb_slam2_amd import synth
 
 pytestmark = pytest.mark.gpu
+# Camera.bf of R/Examples/Stereo/EuRoC.yaml / KITTI00-02.yaml as the float Frame::mbf
+EUROC_BF, KITTI_BF = (float(np.float32(synth.CAMERAS[k]["bf"])) for k in ("EUROC", "KITTI00"))
 
 CONFIGS = [
     # (W, H, nfeatures, seed)
@@ -163,8 +166,8 @@ def test_noise_image_retry_threshold(amd):
     _compare(ref, kps, desc)
 
 
-@pytest.mark.parametrize("W,H,nf,seed,mbf", [(752, 480, 1200, 0x5EED0005, 47.9), (640, 480, 1000, 0x5EED0006, 40.0),
-                                             (1241, 376, 2000, 0x5EED0003, 386.1448)])
+@pytest.mark.parametrize("W,H,nf,seed,mbf", [(752, 480, 1200, 0x5EED0005, EUROC_BF), (640, 480, 1000, 0x5EED0006, 40.0),
+                                             (1241, 376, 2000, 0x5EED0003, KITTI_BF)])
 def test_compute_stereo_matches(amd, W, H, nf, seed, mbf):
     """Frame::ComputeStereoMatches on the GPU (pyramids read in place) vs the oracle on a
     synthetic stereo pair with a smooth disparity field: EuRoC geometry,
@@ -193,7 +196,7 @@ def test_compute_stereo_matches_batch_device(amd):
     import torch
     from orb_slam2_amd import synth, _abi
     import ctypes as C
-    W, H, nf, mbf = 752, 480, 1200, 47.9
+    W, H, nf, mbf = 752, 480, 1200, EUROC_BF
     cv = synth.canvas(0x5EED0005, W, H)
     pairs = [synth.stereo_pair(cv, W, H, t) for t in range(3)]
     imgs = np.stack([im for pr in pairs for im in pr])

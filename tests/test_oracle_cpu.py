@@ -401,7 +401,7 @@ def test_compute_stereo_matches_oracle_vs_python():
     p = O.params(1200)
     a = O.extract(p, left, want_pyramid=True)
     b = O.extract(p, right, want_pyramid=True)
-    mbf = 47.9
+    mbf = float(np.float32(synth.CAMERAS["EUROC"]["bf"]))   # R/Examples/Stereo/EuRoC.yaml:25
     n_c, ur_c, dep_c = O.compute_stereo_matches(p, a, b, mbf)
     t = O.tables(p)
     lw, lh = a["sizes"]
