@@ -33,6 +33,10 @@ extern "C" {
 #define ORB_ENODEV (-19)   /* no usable gfx950 device */
 #define ORB_EGPU (-5)      /* a HIP call or kernel failed */
 #define ORB_EOVERFLOW (-75) /* an internal fixed-capacity table overflowed */
+#define ORB_EINTERNAL (-131) /* an internal consistency check failed (a library bug; the call did nothing useful) */
+/* No C++ exception crosses this ABI: every entry point is a function-try-block, std::bad_alloc
+ * returns ORB_ENOMEM and any other exception ORB_EINTERNAL (the void destroy / conversion
+ * functions swallow them). */
 
 /* cv::KeyPoint memory layout (pt.x, pt.y, size, angle, response, octave, class_id). */
 typedef struct {
@@ -80,10 +84,28 @@ int orb_extract(orb_extractor* ex, const uint8_t* img, int w, int h, size_t stri
  * memory.  Results stay on the device: frame b's keypoints at d_kps + b*cap,
  * descriptors at d_desc + b*cap*32, count at d_counts[b] (may exceed cap; then
  * only the first cap are written).  Asynchronous on `stream` (hipStream_t; NULL =
- * the handle's own stream).  Returns 0 when the work was enqueued. */
+ * the handle's own stream).  Returns 0 when the work was enqueued.
+ *
+ * LEVEL-0 LIFETIME.  As R/src/ORBextractor.cpp:1223 rebinds mvImagePyramid[0] to the input
+ * image instead of copying it, level 0 of this call IS d_imgs whenever its rows are
+ * dword-aligned (w, img_stride_frame and d_imgs multiples of 4): the extraction reads it in
+ * place, and so do the later readers of this handle's last extraction — orb_pyramid_level
+ * (level 0), orb_pyramid_level_device (raw level 0 is returned as a pointer into d_imgs, and
+ * the on-demand blurred pyramid is computed from it) and orb_compute_stereo_matches(_batch_device).
+ * d_imgs must therefore stay allocated and unchanged until the last of those reads has
+ * completed on its stream (or the next extraction of the handle is enqueued).  A caller that
+ * refills or frees d_imgs earlier (e.g. uploads the next batch into the same buffer) calls
+ * orb_extractor_set_level0_copy(ex, 1) first: level 0 is then copied into the handle's own
+ * pyramid slab and d_imgs is free once this call's work has run.  Unaligned frames are
+ * always copied. */
 int orb_extract_batch_device(orb_extractor* ex, const uint8_t* d_imgs, size_t img_stride_frame,
                              int B, int w, int h, orb_keypoint* d_kps, uint8_t* d_desc, int cap,
                              int32_t* d_counts, void* stream);
+
+/* copy = 1: every later extraction of `ex` copies level 0 into the handle's pyramid slab, so
+ * no later call reads the caller's frames (see LEVEL-0 LIFETIME above; one extra read + write
+ * of the frame per extraction).  copy = 0 (default): level 0 is read in place when aligned. */
+int orb_extractor_set_level0_copy(orb_extractor* ex, int copy);
 
 /* Status of the handle's last extraction (orb_extract or orb_extract_batch_device), after waiting
  * for the stream it ran on: *status = 0 when every internal table held, else a bit set —
@@ -96,13 +118,16 @@ int orb_extractor_batch_status(orb_extractor* ex, int32_t* status);
 /* Public `std::vector<cv::Mat> mvImagePyramid` (R/include/ORBextractor.h:88),
  * read by Frame::ComputeStereoMatches (R/src/Frame.cpp:558,675,689,695): returns a
  * host pointer to level `level` of frame `frame` of the last extraction
- * (downloaded lazily, valid until the next extraction). */
+ * (downloaded lazily, valid until the next extraction).  After orb_extract_batch_device,
+ * level 0 is downloaded from the caller's d_imgs unless level-0 copy is on (LEVEL-0 LIFETIME). */
 int orb_pyramid_level(orb_extractor* ex, int frame, int level, const uint8_t** host, int* w,
                       int* h, size_t* stride);
 
 /* Device pointer of the blurred or raw level (for on-device consumers).  The
  * blurred pyramid is computed on the first such request after an extraction
- * (the extraction itself evaluates the Gaussian only where descriptors sample). */
+ * (the extraction itself evaluates the Gaussian only where descriptors sample).
+ * Raw level 0 after orb_extract_batch_device points into the caller's d_imgs, and the
+ * blurred pyramid's level 0 is computed from it, unless level-0 copy is on (LEVEL-0 LIFETIME). */
 int orb_pyramid_level_device(orb_extractor* ex, int frame, int level, int blurred,
                              const uint8_t** dptr, int* w, int* h, size_t* pitch);
 
@@ -143,7 +168,9 @@ int orb_compute_stereo_matches(orb_extractor* left, orb_extractor* right, const 
 /* Batched device form for stereo streams: the last orb_extract_batch_device call of `ex`
  * held frames 2p (left) and 2p+1 (right) of n_pairs stereo pairs, with outputs d_kps /
  * d_desc / d_counts as that call wrote them (cap keypoints per frame).  Writes
- * d_uright / d_depth ([n_pairs][cap]) and d_nstereo[p].  Asynchronous on `stream`. */
+ * d_uright / d_depth ([n_pairs][cap]) and d_nstereo[p].  Asynchronous on `stream`.
+ * The SAD search reads level 0 of both images: the extraction's d_imgs must still hold
+ * those frames when this runs, unless level-0 copy is on (LEVEL-0 LIFETIME). */
 int orb_compute_stereo_matches_batch_device(orb_extractor* ex, const orb_keypoint* d_kps, const uint8_t* d_desc,
                                             const int32_t* d_counts, int cap, int n_pairs, float mbf, float mb,
                                             float* d_uright, float* d_depth, int32_t* d_nstereo, void* stream);

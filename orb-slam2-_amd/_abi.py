@@ -60,6 +60,7 @@ def lib() -> C.CDLL:
             "orb_pyramid_level": [vp, i32, i32, vp, vp, vp, vp],
             "orb_pyramid_level_device": [vp, i32, i32, i32, vp, vp, vp, vp],
             "orb_extractor_profile": [vp, i32],
+            "orb_extractor_set_level0_copy": [vp, i32],
             "orb_extractor_stage_times": [vp, vp, i32, vp],
             "orb_extractor_geometry": [vp, i32, i32, vp, vp, vp, vp],
             "orb_extractor_last_counts": [vp, i32, vp, vp],

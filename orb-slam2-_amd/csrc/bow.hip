@@ -89,7 +89,7 @@ struct orb_vocab {
 
 extern "C" {
 
-int orb_vocabulary_create(int device, const orb_vocabulary* voc, orb_vocab** out) {
+int orb_vocabulary_create(int device, const orb_vocabulary* voc, orb_vocab** out) try {
     if (!voc || !out || voc->n_nodes < 1 || !voc->desc || !voc->child_start || !voc->word_id || !voc->weight ||
         voc->L < 1)
         return ORB_EINVAL;
@@ -157,9 +157,9 @@ int orb_vocabulary_create(int device, const orb_vocabulary* voc, orb_vocab** out
     if (hipStreamSynchronize(h->stream) != hipSuccess) { orb_vocabulary_destroy(h); return ORB_EGPU; }
     *out = h;
     return ORB_OK;
-}
+} ORB_ABI_CATCH
 
-void orb_vocabulary_destroy(orb_vocab* h) {
+void orb_vocabulary_destroy(orb_vocab* h) try {
     if (!h) return;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
@@ -167,10 +167,10 @@ void orb_vocabulary_destroy(orb_vocab* h) {
     if (h->scratch) (void)hipFree(h->scratch);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
-}
+} ORB_ABI_CATCH_VOID
 
 int orb_vocabulary_transform_device(orb_vocab* h, const uint8_t* d_desc, int n, int levelsup, int32_t* d_word_id,
-                                    double* d_weight, int32_t* d_node_id, void* stream) {
+                                    double* d_weight, int32_t* d_node_id, void* stream) try {
     if (!h || n < 0 || (n > 0 && (!d_desc || !d_word_id || !d_weight || !d_node_id))) return ORB_EINVAL;
     if (n == 0) return ORB_OK;
     ORB_HIP_TRY(hipSetDevice(h->device));
@@ -178,10 +178,10 @@ int orb_vocabulary_transform_device(orb_vocab* h, const uint8_t* d_desc, int n, 
                        h->v, reinterpret_cast<const uint4*>(d_desc), n, levelsup, d_word_id, d_weight, d_node_id);
     ORB_HIP_TRY(hipGetLastError());
     return ORB_OK;
-}
+} ORB_ABI_CATCH
 
 int orb_vocabulary_transform(orb_vocab* h, const uint8_t* desc, int n, int levelsup, int32_t* word_id, double* weight,
-                             int32_t* node_id) {
+                             int32_t* node_id) try {
     if (!h || n < 0 || (n > 0 && (!desc || !word_id || !weight || !node_id))) return ORB_EINVAL;
     if (n == 0) return ORB_OK;
     ORB_HIP_TRY(hipSetDevice(h->device));
@@ -206,6 +206,6 @@ int orb_vocabulary_transform(orb_vocab* h, const uint8_t* desc, int n, int level
     ORB_HIP_TRY(hipMemcpyAsync(node_id, dN, (size_t)n * 4, hipMemcpyDeviceToHost, s));
     ORB_HIP_TRY(hipStreamSynchronize(s));
     return ORB_OK;
-}
+} ORB_ABI_CATCH
 
 }  // extern "C"

@@ -6,6 +6,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <mutex>
+#include <new>
 #include <vector>
 
 #include "../../include/orbslam2_amd.h"
@@ -20,6 +21,24 @@ inline std::mutex& legacy_capture_mutex() {
     return m;
 }
 }   // namespace orbamd
+
+// The C-ABI's exception barrier (include/orbslam2_amd.h: no C++ exception crosses it): every
+// extern "C" definition is a function-try-block ending in one of these handlers.
+namespace orbamd {
+inline int abi_exception_status() noexcept {   // called inside a catch (...) handler
+    try {
+        throw;
+    } catch (const std::bad_alloc&) {
+        return ORB_ENOMEM;
+    } catch (...) {
+        return ORB_EINTERNAL;
+    }
+}
+}   // namespace orbamd
+#define ORB_ABI_CATCH \
+    catch (...) { return orbamd::abi_exception_status(); }
+#define ORB_ABI_CATCH_VOID \
+    catch (...) {}
 
 #define ORB_HIP_TRY(expr)                                                                   \
     do {                                                                                    \
@@ -55,7 +74,10 @@ inline int host_scratch(int device, size_t bytes, HostScratch** out) {
     HostScratch* h = nullptr;
     for (HostScratch* p : pool)
         if (p->device == device) h = p;
+    // creation and growth (first use, a larger call) take the capture lock: they may run on the
+    // Tracking / LoopClosing threads while LocalMapping captures its LM graph
     if (!h) {
+        std::lock_guard<std::mutex> lk(legacy_capture_mutex());
         h = new HostScratch();
         h->device = device;
         if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -65,6 +87,7 @@ inline int host_scratch(int device, size_t bytes, HostScratch** out) {
         pool.push_back(h);
     }
     if (h->cap < bytes) {   // grow (rare): the stream is idle between calls of this thread
+        std::lock_guard<std::mutex> lk(legacy_capture_mutex());
         if (h->base) (void)hipFree(h->base);
         h->base = nullptr;
         h->cap = 0;

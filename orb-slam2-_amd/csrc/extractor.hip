@@ -2105,7 +2105,8 @@ struct orb_extractor {
     bool blurValid = false;          // d_blur holds the blurred pyramid of the last extraction
     hipStream_t lastStream = nullptr;
     L0Src l0{nullptr, 0, 0, 0};     // level 0 of the last extraction (the caller's frames or the slab)
-    // ORB_L0_COPY=1: copy level 0 into the slab even when it could be read in place (A/B only)
+    // copy level 0 into the slab even when it could be read in place: orb_extractor_set_level0_copy
+    // (the caller refills its frames before the later level-0 readers run), or ORB_L0_COPY=1 (A/B)
     bool forceL0Copy = [] { const char* e = std::getenv("ORB_L0_COPY"); return e && e[0] == '1'; }();
     size_t capFrames = 0, capFrameBytes = 0, capSlots = 0, capOut = 0, capCells = 0;
     uint8_t *d_pyr = nullptr, *d_blur = nullptr;
@@ -2470,7 +2471,7 @@ static void gauss7_int(int k[7]) {
 extern "C" {
 
 int orb_extractor_create(const orb_extractor_params* params, int device, int max_w, int max_h, int max_batch,
-                         orb_extractor** out) {
+                         orb_extractor** out) try {
     if (!params || !out || max_w <= 0 || max_h <= 0 || max_batch <= 0) return ORB_EINVAL;
     if (params->nlevels < 1 || params->nlevels > kMaxLevels || params->nfeatures < 0 || !(params->scaleFactor > 1.0f))
         return ORB_EINVAL;
@@ -2495,9 +2496,9 @@ int orb_extractor_create(const orb_extractor_params* params, int device, int max
     if (st) { orb_extractor_destroy(ex); return st; }
     *out = ex;
     return ORB_OK;
-}
+} ORB_ABI_CATCH
 
-void orb_extractor_destroy(orb_extractor* ex) {
+void orb_extractor_destroy(orb_extractor* ex) try {
     if (!ex) return;
     std::lock_guard<std::mutex> lk(legacy_capture_mutex());   // hipFree (common.h)
     (void)hipSetDevice(ex->device);
@@ -2514,25 +2515,28 @@ void orb_extractor_destroy(orb_extractor* ex) {
     if (ex->h_out) (void)hipHostFree(ex->h_out);
     if (ex->stream) (void)hipStreamDestroy(ex->stream);
     delete ex;
-}
+} ORB_ABI_CATCH_VOID
 
-int orb_extractor_levels(const orb_extractor* ex) { return ex ? ex->p.nlevels : ORB_EINVAL; }
+int orb_extractor_levels(const orb_extractor* ex) try { return ex ? ex->p.nlevels : ORB_EINVAL; } ORB_ABI_CATCH
 
 int orb_extractor_scale_tables(const orb_extractor* ex, float* scale, float* inv_scale, float* sigma2,
-                               float* inv_sigma2) {
+                               float* inv_sigma2) try {
     if (!ex) return ORB_EINVAL;
     host_tables(ex->p, scale, inv_scale, sigma2, inv_sigma2, nullptr);
     return ORB_OK;
-}
+} ORB_ABI_CATCH
 
-int orb_extractor_features_per_level(const orb_extractor* ex, int* per_level) {
+int orb_extractor_features_per_level(const orb_extractor* ex, int* per_level) try {
     if (!ex || !per_level) return ORB_EINVAL;
     host_tables(ex->p, nullptr, nullptr, nullptr, nullptr, per_level);
     return ORB_OK;
-}
+} ORB_ABI_CATCH
 
 static int ensure_pinned(void** p, size_t* cur, size_t need) {
     if (*cur >= need) return ORB_OK;
+    // growth (first use, a larger frame) frees and allocates pinned memory: under the capture lock,
+    // as the matcher's pinned staging does (common.h) — never called with the lock held
+    std::lock_guard<std::mutex> lk(legacy_capture_mutex());
     if (*p) (void)hipHostFree(*p);
     *p = nullptr;
     *cur = 0;
@@ -2542,7 +2546,7 @@ static int ensure_pinned(void** p, size_t* cur, size_t need) {
 }
 
 int orb_extract(orb_extractor* ex, const uint8_t* img, int w, int h, size_t stride, orb_keypoint* kps, uint8_t* desc,
-                int capacity, int* n_out) {
+                int capacity, int* n_out) try {
     if (!ex) return ORB_EINVAL;
     if (!img || w <= 0 || h <= 0) return ORB_OK;   // R/src/ORBextractor.cpp:1123-1124
     if (stride < (size_t)w || capacity < 0) return ORB_EINVAL;
@@ -2587,10 +2591,10 @@ int orb_extract(orb_extractor* ex, const uint8_t* img, int w, int h, size_t stri
         if (desc) std::memcpy(desc, hd, (size_t)N * 32);
     }
     return N;
-}
+} ORB_ABI_CATCH
 
 int orb_extract_batch_device(orb_extractor* ex, const uint8_t* d_imgs, size_t img_stride_frame, int B, int w, int h,
-                             orb_keypoint* d_kps, uint8_t* d_desc, int cap, int32_t* d_counts, void* stream) {
+                             orb_keypoint* d_kps, uint8_t* d_desc, int cap, int32_t* d_counts, void* stream) try {
     if (!ex || !d_imgs || B <= 0 || w <= 0 || h <= 0 || !d_kps || !d_desc || !d_counts || cap < 0) return ORB_EINVAL;
     if (img_stride_frame < (size_t)w * h) return ORB_EINVAL;
     ORB_HIP_TRY(hipSetDevice(ex->device));
@@ -2603,9 +2607,15 @@ int orb_extract_batch_device(orb_extractor* ex, const uint8_t* d_imgs, size_t im
     ex->lastB = B;
     ex->h_level_valid.assign((size_t)B * g.nlevels, 0);
     return run_pipeline(ex, B, d_imgs, (long long)img_stride_frame, w, 0, d_kps, d_desc, cap, d_counts, s);
-}
+} ORB_ABI_CATCH
 
-int orb_extractor_batch_status(orb_extractor* ex, int32_t* status) {
+int orb_extractor_set_level0_copy(orb_extractor* ex, int copy) try {
+    if (!ex || (copy != 0 && copy != 1)) return ORB_EINVAL;
+    ex->forceL0Copy = copy != 0;
+    return ORB_OK;
+} ORB_ABI_CATCH
+
+int orb_extractor_batch_status(orb_extractor* ex, int32_t* status) try {
     if (!ex || !status) return ORB_EINVAL;
     ORB_HIP_TRY(hipSetDevice(ex->device));
     hipStream_t st = ex->lastStream ? ex->lastStream : ex->stream;
@@ -2616,9 +2626,9 @@ int orb_extractor_batch_status(orb_extractor* ex, int32_t* status) {
     ORB_HIP_TRY(hipStreamSynchronize(st));
     *status = *h;
     return *h ? ORB_EOVERFLOW : ORB_OK;
-}
+} ORB_ABI_CATCH
 
-int orb_pyramid_level(orb_extractor* ex, int frame, int level, const uint8_t** host, int* w, int* h, size_t* stride) {
+int orb_pyramid_level(orb_extractor* ex, int frame, int level, const uint8_t** host, int* w, int* h, size_t* stride) try {
     if (!ex || level < 0 || level >= ex->p.nlevels || frame < 0 || frame >= ex->lastB || ex->gw < 0) return ORB_EINVAL;
     ORB_HIP_TRY(hipSetDevice(ex->device));
     const Geom& g = ex->g;
@@ -2644,10 +2654,10 @@ int orb_pyramid_level(orb_extractor* ex, int frame, int level, const uint8_t** h
     if (h) *h = L.h;
     if (stride) *stride = (size_t)L.pitch;
     return ORB_OK;
-}
+} ORB_ABI_CATCH
 
 int orb_pyramid_level_device(orb_extractor* ex, int frame, int level, int blurred, const uint8_t** dptr, int* w,
-                             int* h, size_t* pitch) {
+                             int* h, size_t* pitch) try {
     if (!ex || level < 0 || level >= ex->p.nlevels || frame < 0 || frame >= (int)ex->capFrames || ex->gw < 0)
         return ORB_EINVAL;
     const Geom& g = ex->g;
@@ -2668,16 +2678,16 @@ int orb_pyramid_level_device(orb_extractor* ex, int frame, int level, int blurre
     if (h) *h = L.h;
     if (pitch) *pitch = raw0 ? (size_t)ex->l0.pitch : (size_t)L.pitch;
     return ORB_OK;
-}
+} ORB_ABI_CATCH
 
-int orb_extractor_profile(orb_extractor* ex, int enable) {
+int orb_extractor_profile(orb_extractor* ex, int enable) try {
     if (!ex) return ORB_EINVAL;
     if (enable < 0 || enable > 3) return ORB_EINVAL;
     ex->profile = enable;
     return ORB_OK;
-}
+} ORB_ABI_CATCH
 
-int orb_extractor_stage_times(orb_extractor* ex, double* ms, int n_stages, int* n_calls) {
+int orb_extractor_stage_times(orb_extractor* ex, double* ms, int n_stages, int* n_calls) try {
     if (!ex || (n_stages > 0 && !ms)) return ORB_EINVAL;
     ORB_HIP_TRY(hipSetDevice(ex->device));
     for (auto& set : ex->ev_sets) {
@@ -2706,10 +2716,10 @@ int orb_extractor_stage_times(orb_extractor* ex, double* ms, int n_stages, int* 
     for (int i = 0; i < kStages; i++) ex->stage_ms[i] = 0;
     ex->stage_calls = 0;
     return kStages;
-}
+} ORB_ABI_CATCH
 
 int orb_extractor_geometry(orb_extractor* ex, int w, int h, int* level_w, int* level_h, int* cells_per_level,
-                           int* max_keypoints_per_frame) {
+                           int* max_keypoints_per_frame) try {
     if (!ex || w <= 0 || h <= 0) return ORB_EINVAL;
     int st = ensure_geom(ex, w, h);
     if (st) return st;
@@ -2721,9 +2731,9 @@ int orb_extractor_geometry(orb_extractor* ex, int w, int h, int* level_w, int* l
     }
     if (max_keypoints_per_frame) *max_keypoints_per_frame = g.outPerFrame;
     return ORB_OK;
-}
+} ORB_ABI_CATCH
 
-int orb_extractor_last_counts(orb_extractor* ex, int frame, int* pre_counts, int* level_counts) {
+int orb_extractor_last_counts(orb_extractor* ex, int frame, int* pre_counts, int* level_counts) try {
     if (!ex || frame < 0 || frame >= ex->lastB || ex->gw < 0) return ORB_EINVAL;
     ORB_HIP_TRY(hipSetDevice(ex->device));
     const Geom& g = ex->g;
@@ -2741,7 +2751,7 @@ int orb_extractor_last_counts(orb_extractor* ex, int frame, int* pre_counts, int
         if (level_counts) level_counts[l] = lc[l];
     }
     return ORB_OK;
-}
+} ORB_ABI_CATCH
 
 static int stereo_scratch(orb_extractor* ex, size_t bytes) {
     if (ex->st_bytes >= bytes) return ORB_OK;
@@ -2762,7 +2772,7 @@ static StereoTabs stereo_tabs(const orb_extractor* ex) {
 
 int orb_compute_stereo_matches(orb_extractor* left, orb_extractor* right, const orb_keypoint* kps_l,
                                const uint8_t* desc_l, int n_l, const orb_keypoint* kps_r, const uint8_t* desc_r,
-                               int n_r, float mbf, float mb, float* uright, float* depth) {
+                               int n_r, float mbf, float mb, float* uright, float* depth) try {
     if (!left || !right || n_l < 0 || n_r < 0 || (n_l && (!kps_l || !desc_l || !uright || !depth)) || (n_r && (!kps_r || !desc_r)))
         return ORB_EINVAL;
     for (int i = 0; i < n_l; i++) { uright[i] = -1.0f; depth[i] = -1.0f; }
@@ -2815,11 +2825,11 @@ int orb_compute_stereo_matches(orb_extractor* left, orb_extractor* right, const 
     std::memcpy(uright, hur, (size_t)n_l * 4);
     std::memcpy(depth, hdp, (size_t)n_l * 4);
     return hn[2];
-}
+} ORB_ABI_CATCH
 
 int orb_compute_stereo_matches_batch_device(orb_extractor* ex, const orb_keypoint* d_kps, const uint8_t* d_desc,
                                             const int32_t* d_counts, int cap, int n_pairs, float mbf, float mb,
-                                            float* d_uright, float* d_depth, int32_t* d_nstereo, void* stream) {
+                                            float* d_uright, float* d_depth, int32_t* d_nstereo, void* stream) try {
     if (!ex || !d_kps || !d_desc || !d_counts || cap <= 0 || n_pairs <= 0 || !d_uright || !d_depth || !d_nstereo)
         return ORB_EINVAL;
     if (ex->gw < 0 || ex->lastB < 2 * n_pairs) return ORB_EINVAL;   // frames 2p (left), 2p+1 (right)
@@ -2843,6 +2853,6 @@ int orb_compute_stereo_matches_batch_device(orb_extractor* ex, const orb_keypoin
                        d_nstereo, dkeys);
     ORB_HIP_TRY(hipGetLastError());
     return ORB_OK;
-}
+} ORB_ABI_CATCH
 
 }  // extern "C"

@@ -3378,7 +3378,7 @@ static int comm_allreduce_schur(lba_context* c, double* S, double* bs, const int
 
 extern "C" {
 
-int lba_create(int device, lba_context** out) {
+int lba_create(int device, lba_context** out) try {
     if (!out) return ORB_EINVAL;
     int st = check_device(device);
     if (st) return st;
@@ -3395,9 +3395,9 @@ int lba_create(int device, lba_context** out) {
     if (!ok) { lba_destroy(c); return ORB_EGPU; }
     *out = c;
     return ORB_OK;
-}
+} ORB_ABI_CATCH
 
-void lba_destroy(lba_context* c) {
+void lba_destroy(lba_context* c) try {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
@@ -3413,9 +3413,9 @@ void lba_destroy(lba_context* c) {
     for (auto& g : c->graphs) (void)hipGraphExecDestroy(g.exec);
     if (c->stream && c->ownStream) (void)hipStreamDestroy(c->stream);
     delete c;
-}
+} ORB_ABI_CATCH_VOID
 
-int lba_set_stream(lba_context* c, void* stream, int use_given) {
+int lba_set_stream(lba_context* c, void* stream, int use_given) try {
     if (!c) return ORB_EINVAL;
     if (c->stream && c->ownStream) {
         (void)hipStreamSynchronize(c->stream);
@@ -3430,10 +3430,10 @@ int lba_set_stream(lba_context* c, void* stream, int use_given) {
         c->ownStream = true;
     }
     return ORB_OK;
-}
+} ORB_ABI_CATCH
 
 int lba_set_comm(lba_context* c, int rank, int world, double* d_workspace, size_t ws_doubles, lba_allreduce_fn fn,
-                 void* user) {
+                 void* user) try {
     if (!c || world < 1 || rank < 0 || rank >= world) return ORB_EINVAL;
     if (world > 1 && (!d_workspace || !fn)) return ORB_EINVAL;
     c->rank = rank;
@@ -3445,17 +3445,17 @@ int lba_set_comm(lba_context* c, int rank, int world, double* d_workspace, size_
     c->grp = nullptr;   // (lba_group installs its device-side exchange after this call)
     c->grpGraphs = false;
     return ORB_OK;
-}
+} ORB_ABI_CATCH
 
-int lba_stats(lba_context* c, double* ms4, int* iters, int* trials) {
+int lba_stats(lba_context* c, double* ms4, int* iters, int* trials) try {
     if (!c) return ORB_EINVAL;
     if (ms4) { ms4[0] = c->ms_linearize; ms4[1] = c->ms_schur; ms4[2] = c->ms_solve; ms4[3] = c->ms_update; }
     if (iters) *iters = c->n_iters;
     if (trials) *trials = c->n_trials;
     return ORB_OK;
-}
+} ORB_ABI_CATCH
 
-int lba_dense_solve(lba_context* c, const double* S, const double* b, int n, double* x) {
+int lba_dense_solve(lba_context* c, const double* S, const double* b, int n, double* x) try {
     if (!c || !S || !b || !x || n <= 0) return ORB_EINVAL;
     ORB_HIP_TRY(hipSetDevice(c->device));
     lba_free_all(c);
@@ -3483,15 +3483,15 @@ int lba_dense_solve(lba_context* c, const double* S, const double* b, int n, dou
     ORB_HIP_TRY(hipMemcpyAsync(&fail, df, 4, hipMemcpyDeviceToHost, s));
     ORB_HIP_TRY(hipStreamSynchronize(s));
     return fail ? ORB_EINVAL : ORB_OK;
-}
+} ORB_ABI_CATCH
 
-int lba_debug_stop_after_trials(lba_context* c, int n_trials) {
+int lba_debug_stop_after_trials(lba_context* c, int n_trials) try {
     if (!c) return ORB_EINVAL;
     c->stopAfter = n_trials < 0 ? -1 : n_trials;
     return ORB_OK;
-}
+} ORB_ABI_CATCH
 
-int lba_debug_buffer(lba_context* c, int which, double* out, size_t n) {
+int lba_debug_buffer(lba_context* c, int which, double* out, size_t n) try {
     if (!c || !out) return ORB_EINVAL;
     const LbaDev& d = c->last;
     const double* src = nullptr;
@@ -3513,30 +3513,30 @@ int lba_debug_buffer(lba_context* c, int which, double* out, size_t n) {
     ORB_HIP_TRY(hipMemcpyAsync(out, src, 8 * n, hipMemcpyDeviceToHost, c->stream));   // own stream (§8b threading)
     ORB_HIP_TRY(hipStreamSynchronize(c->stream));
     return (int)avail;
-}
+} ORB_ABI_CATCH
 
-int lba_profile(lba_context* c, int enable) {
+int lba_profile(lba_context* c, int enable) try {
     if (!c) return ORB_EINVAL;
     c->profile = enable != 0;
     c->ms_linearize = c->ms_schur = c->ms_solve = c->ms_update = 0;
     c->n_iters = c->n_trials = 0;
     return ORB_OK;
-}
+} ORB_ABI_CATCH
 
-void lba_pose_from_Tcw(const float Tcw[16], double q[4], double t[3]) {
+void lba_pose_from_Tcw(const float Tcw[16], double q[4], double t[3]) try {
     // Converter::toSE3Quat (R/src/Converter.cpp:47-57): float Mat -> Matrix3d -> SE3Quat
     double R[9];
     for (int i = 0; i < 3; i++)
         for (int j = 0; j < 3; j++) R[i * 3 + j] = (double)Tcw[i * 4 + j];
     hd_quat_from_matrix(R, q);
     for (int i = 0; i < 3; i++) t[i] = (double)Tcw[i * 4 + 3];
-}
+} ORB_ABI_CATCH_VOID
 
-void lba_poses_from_Tcw(const float* Tcw, int n, double* q, double* t) {
+void lba_poses_from_Tcw(const float* Tcw, int n, double* q, double* t) try {
     for (int i = 0; i < n; i++) lba_pose_from_Tcw(Tcw + 16 * (size_t)i, q + 4 * (size_t)i, t + 3 * (size_t)i);
-}
+} ORB_ABI_CATCH_VOID
 
-void lba_pose_to_Tcw(const double q[4], const double t[3], float Tcw[16]) {
+void lba_pose_to_Tcw(const double q[4], const double t[3], float Tcw[16]) try {
     // Converter::toCvMat(SE3Quat): to_homogeneous_matrix() cast to float
     const double x = q[0], y = q[1], z = q[2], w = q[3];
     const double tx = 2 * x, ty = 2 * y, tz = 2 * z;
@@ -3551,7 +3551,7 @@ void lba_pose_to_Tcw(const double q[4], const double t[3], float Tcw[16]) {
     }
     Tcw[12] = Tcw[13] = Tcw[14] = 0.f;
     Tcw[15] = 1.f;
-}
+} ORB_ABI_CATCH_VOID
 
 // slots per captured LM graph (see optimize())
 constexpr int kGraphSlots = 16;
@@ -3559,14 +3559,14 @@ constexpr int kGraphSlots = 16;
 static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, const volatile uint8_t* stop,
                    lba_result* r, bool global, bool robustKernels);
 
-int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const volatile uint8_t* stop, lba_result* r) {
+int lba_solve(lba_context* c, const lba_problem* p, const lba_options* o, const volatile uint8_t* stop, lba_result* r) try {
     return lba_run(c, p, o, stop, r, false, true);
-}
+} ORB_ABI_CATCH
 
 int lba_solve_global(lba_context* c, const lba_problem* p, const lba_options* o, int robust,
-                     const volatile uint8_t* stop, lba_result* r) {
+                     const volatile uint8_t* stop, lba_result* r) try {
     return lba_run(c, p, o, stop, r, true, robust != 0);
-}
+} ORB_ABI_CATCH
 
 static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, const volatile uint8_t* stop,
                    lba_result* r, bool global, bool robustKernels) {
@@ -4157,6 +4157,19 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
             d.tripStart = tripStart;
             hipLaunchKernelGGL(k_pair_trip, dim3(np2), dim3(kSpT), 0, s, d, trips);
             ORB_HIP_TRY(hipGetLastError());
+            if (c->world > 1) {
+                // the packed exchange carries the first gPairs blocks of d.pairs: the device's list
+                // (gflag plus k_pair_mark's own marks) must be exactly the host's global set, or the
+                // all-reduced S would silently miss blocks.  Once per solve.
+                int32_t devPairs = -1;
+                ORB_HIP_TRY(hipMemcpyAsync(&devPairs, npairs, 4, hipMemcpyDeviceToHost, s));
+                ORB_HIP_TRY(hipStreamSynchronize(s));
+                if (devPairs != gPairs) {
+                    std::fprintf(stderr, "[orbslam2_amd] lba: rank %d lists %d pose pairs, the global set has %d\n",
+                                 c->rank, devPairs, gPairs);
+                    return ORB_EINTERNAL;
+                }
+            }
         }
         d.pairs = pairs;
         d.npairs = npairs;
@@ -4338,7 +4351,7 @@ static void group_free_ws(lba_group* g) {
     g->wsDoubles = 0;
 }
 
-void lba_group_destroy(lba_group* g) {
+void lba_group_destroy(lba_group* g) try {
     if (!g) return;
     for (int r = 0; r < g->n; r++)
         if (g->ctx[r]) {
@@ -4359,9 +4372,9 @@ void lba_group_destroy(lba_group* g) {
         (void)hipEventDestroy(e.second);
     }
     delete g;
-}
+} ORB_ABI_CATCH_VOID
 
-int lba_group_create(const int* devices, int n, lba_group** out) {
+int lba_group_create(const int* devices, int n, lba_group** out) try {
     if (!devices || !out || n < 1 || n > kMaxGroup) return ORB_EINVAL;
     *out = nullptr;
     lba_group* g = new lba_group();
@@ -4438,10 +4451,10 @@ int lba_group_create(const int* devices, int n, lba_group** out) {
     }
     *out = g;
     return ORB_OK;
-}
+} ORB_ABI_CATCH
 
 int lba_group_solve(lba_group* g, const lba_problem* p, const lba_options* o, const volatile uint8_t* stop,
-                    lba_result* r) {
+                    lba_result* r) try {
     if (!g || !p || !o || !r || p->n_poses < 0 || p->n_points < 0 || p->n_edges < 0) return ORB_EINVAL;
     const int n = g->n;
     if (n == 1) return lba_solve(g->ctx[0], p, o, stop, r);
@@ -4607,13 +4620,13 @@ int lba_group_solve(lba_group* g, const lba_problem* p, const lba_options* o, co
         r->n_trace = r0.n_trace;
     }
     return ORB_OK;
-}
+} ORB_ABI_CATCH
 
-int lba_group_stats(lba_group* g, double* exchange_ms, long* n_exchanges) {
+int lba_group_stats(lba_group* g, double* exchange_ms, long* n_exchanges) try {
     if (!g) return ORB_EINVAL;
     if (exchange_ms) *exchange_ms = g->exchangeMs;
     if (n_exchanges) *n_exchanges = g->exchanges;
     return ORB_OK;
-}
+} ORB_ABI_CATCH
 
 }  // extern "C"

@@ -1572,7 +1572,7 @@ __global__ __launch_bounds__(64) void k_distinctive(const uint8_t* __restrict__ 
 
 extern "C" {
 
-int orb_descriptor_distance(const uint8_t* a, const uint8_t* b) {
+int orb_descriptor_distance(const uint8_t* a, const uint8_t* b) try {
     if (!a || !b) return ORB_EINVAL;
     int dist = 0;
     for (int i = 0; i < 8; i++) {
@@ -1582,9 +1582,9 @@ int orb_descriptor_distance(const uint8_t* a, const uint8_t* b) {
         dist += __builtin_popcount(pa ^ pb);
     }
     return dist;
-}
+} ORB_ABI_CATCH
 
-int orb_matcher_create(int device, float nnratio, int check_ori, orb_matcher** out) {
+int orb_matcher_create(int device, float nnratio, int check_ori, orb_matcher** out) try {
     if (!out) return ORB_EINVAL;
     int st = check_device(device);
     if (st) return st;
@@ -1599,9 +1599,9 @@ int orb_matcher_create(int device, float nnratio, int check_ori, orb_matcher** o
     }
     *out = m;
     return ORB_OK;
-}
+} ORB_ABI_CATCH
 
-void orb_matcher_destroy(orb_matcher* m) {
+void orb_matcher_destroy(orb_matcher* m) try {
     if (!m) return;
     std::lock_guard<std::mutex> lk(legacy_capture_mutex());   // hipFree (common.h)
     (void)hipSetDevice(m->device);
@@ -1610,10 +1610,10 @@ void orb_matcher_destroy(orb_matcher* m) {
     if (m->h_pin) (void)hipHostFree(m->h_pin);
     if (m->stream) (void)hipStreamDestroy(m->stream);
     delete m;
-}
+} ORB_ABI_CATCH_VOID
 
 int orb_search_for_initialization(orb_matcher* m, const orb_frame_view* f1, const orb_frame_view* f2, float* prev_xy,
-                                  int32_t* matches12, int window) {
+                                  int32_t* matches12, int window) try {
     if (!m || !f1 || !f2 || !prev_xy || !matches12 || f1->n < 0 || f2->n < 0) return ORB_EINVAL;
     if (f2->n >= (1 << 20)) return ORB_EINVAL;
     ORB_HIP_TRY(hipSetDevice(m->device));
@@ -1666,12 +1666,12 @@ int orb_search_for_initialization(orb_matcher* m, const orb_frame_view* f1, cons
     std::memcpy(matches12, hm, (size_t)f1->n * 4);
     std::memcpy(prev_xy, hprev, (size_t)f1->n * 8);
     return hn[0];
-}
+} ORB_ABI_CATCH
 
 int orb_search_for_initialization_batch_device(orb_matcher* m, const orb_keypoint* d_kps1, const uint8_t* d_desc1,
                                                const int32_t* d_n1, const orb_keypoint* d_kps2, const uint8_t* d_desc2,
                                                const int32_t* d_n2, int nb, int cap, int width, int height, int window,
-                                               int32_t* d_matches12, int32_t* d_nmatches, void* stream) {
+                                               int32_t* d_matches12, int32_t* d_nmatches, void* stream) try {
     if (!m || nb <= 0 || cap <= 0 || width <= 0 || height <= 0) return ORB_EINVAL;
     ORB_HIP_TRY(hipSetDevice(m->device));
     int st = mensure(m, nb, cap);
@@ -1694,9 +1694,9 @@ int orb_search_for_initialization_batch_device(orb_matcher* m, const orb_keypoin
                        m->d_status);
     ORB_HIP_TRY(hipGetLastError());
     return ORB_OK;
-}
+} ORB_ABI_CATCH
 
-int orb_matcher_batch_status(orb_matcher* m, int32_t* status) {
+int orb_matcher_batch_status(orb_matcher* m, int32_t* status) try {
     if (!m || !status) return ORB_EINVAL;
     *status = 0;
     if (!m->d_status) return ORB_OK;
@@ -1708,12 +1708,12 @@ int orb_matcher_batch_status(orb_matcher* m, int32_t* status) {
     ORB_HIP_TRY(hipStreamSynchronize(m->stream));
     *status = v;
     return v ? ORB_EOVERFLOW : ORB_OK;
-}
+} ORB_ABI_CATCH
 
 int orb_search_by_projection_frame(orb_matcher* m, const orb_frame_view* cur, const float* Tcw_cur,
                                    const orb_frame_view* last, const float* Tcw_last, const int32_t* last_has_mp,
                                    const uint8_t* last_outlier, const float* last_mp_xyz, const uint8_t* last_mp_desc,
-                                   const float* scale_factors, const float cam[6], float th, int mono, int32_t* cur_mp) {
+                                   const float* scale_factors, const float cam[6], float th, int mono, int32_t* cur_mp) try {
     if (!m || !cur || !last || !Tcw_cur || !Tcw_last || !last_has_mp || !last_outlier || !last_mp_xyz ||
         !last_mp_desc || !scale_factors || !cam || !cur_mp)
         return ORB_EINVAL;
@@ -1799,13 +1799,13 @@ int orb_search_by_projection_frame(orb_matcher* m, const orb_frame_view* cur, co
     if (hn[1]) return ORB_EOVERFLOW;
     std::memcpy(cur_mp, hcm, (size_t)cur->n * 4);
     return hn[0];
-}
+} ORB_ABI_CATCH
 
 int orb_search_by_projection_kf(orb_matcher* m, const orb_frame_view* cur, const float* Tcw_cur, const float Ow[3],
                                 const orb_frame_view* kf, const uint8_t* mp_valid, const float* mp_xyz,
                                 const float* mp_min_dist, const float* mp_max_dist, const uint8_t* mp_desc,
                                 const float cam[4], float log_scale_factor, int n_levels, const float* scale_factors,
-                                float th, int orb_dist, int32_t* cur_mp) {
+                                float th, int orb_dist, int32_t* cur_mp) try {
     if (!m || !cur || !Tcw_cur || !Ow || !kf || !mp_valid || !mp_xyz || !mp_min_dist || !mp_max_dist || !mp_desc ||
         !cam || !scale_factors || !cur_mp || n_levels < 1 || n_levels > 32)
         return ORB_EINVAL;
@@ -1876,12 +1876,12 @@ int orb_search_by_projection_kf(orb_matcher* m, const orb_frame_view* cur, const
     if (hn[1]) return ORB_EOVERFLOW;
     std::memcpy(cur_mp, hcm, (size_t)cur->n * 4);
     return hn[0];
-}
+} ORB_ABI_CATCH
 
 int orb_search_by_projection_sim3(orb_matcher* m, const orb_frame_view* kf, const orb_kf_params* kp, int n_mp,
                                   const uint8_t* mp_valid, const float* mp_xyz, const float* mp_normal,
                                   const float* mp_min_dist, const float* mp_max_dist, const uint8_t* mp_desc, float th,
-                                  int32_t* matched) {
+                                  int32_t* matched) try {
     if (!m || !kf || !kp || !matched || n_mp < 0 || (n_mp > 0 && (!mp_valid || !mp_xyz || !mp_normal || !mp_min_dist ||
                                                                    !mp_max_dist || !mp_desc)))
         return ORB_EINVAL;
@@ -1951,12 +1951,12 @@ int orb_search_by_projection_sim3(orb_matcher* m, const orb_frame_view* kf, cons
     if (hn[1]) return ORB_EOVERFLOW;
     std::memcpy(matched, hm, (size_t)kf->n * 4);
     return hn[0];
-}
+} ORB_ABI_CATCH
 
 int orb_search_by_projection_local(orb_matcher* m, const orb_frame_view* f, int n_mp, const uint8_t* mp_in_view,
                                    const float* mp_proj, const int32_t* mp_level, const float* mp_view_cos,
                                    const uint8_t* mp_desc, const uint8_t* mp_has_obs, const float* scale_factors,
-                                   float th, int32_t* cur_mp) {
+                                   float th, int32_t* cur_mp) try {
     if (!m || !f || n_mp < 0 || !cur_mp || !scale_factors || f->n < 0) return ORB_EINVAL;
     if (n_mp > 0 && (!mp_in_view || !mp_proj || !mp_level || !mp_view_cos || !mp_desc || !mp_has_obs)) return ORB_EINVAL;
     if (f->n >= (1 << 20)) return ORB_EINVAL;
@@ -2034,10 +2034,10 @@ int orb_search_by_projection_local(orb_matcher* m, const orb_frame_view* f, int 
     if (hn[1]) return ORB_EOVERFLOW;
     std::memcpy(cur_mp, hcm, (size_t)f->n * 4);
     return hn[0];
-}
+} ORB_ABI_CATCH
 
 int orb_hamming_knn2(orb_matcher* m, const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* best_idx,
-                     int32_t* best_d, int32_t* second_d) {
+                     int32_t* best_d, int32_t* second_d) try {
     if (!m || nq < 0 || nt < 0 || (nq && (!q || !best_idx || !best_d || !second_d)) || (nt && !t)) return ORB_EINVAL;
     if (nq == 0) return ORB_OK;
     ORB_HIP_TRY(hipSetDevice(m->device));
@@ -2072,11 +2072,11 @@ int orb_hamming_knn2(orb_matcher* m, const uint8_t* q, int nq, const uint8_t* t,
     std::memcpy(best_d, hout + nq, (size_t)nq * 4);
     std::memcpy(second_d, hout + 2 * (size_t)nq, (size_t)nq * 4);
     return ORB_OK;
-}
+} ORB_ABI_CATCH
 
 int orb_hamming_knn2_batch_device(orb_matcher* m, const uint8_t* d_q, const int32_t* d_nq, const uint8_t* d_t,
                                   const int32_t* d_nt, int nb, int q_stride_rows, int t_stride_rows, int32_t* d_best_idx,
-                                  int32_t* d_best_d, int32_t* d_second_d, void* stream) {
+                                  int32_t* d_best_d, int32_t* d_second_d, void* stream) try {
     if (!m || !d_q || !d_nq || !d_t || !d_nt || nb <= 0 || q_stride_rows <= 0 || t_stride_rows <= 0) return ORB_EINVAL;
     ORB_HIP_TRY(hipSetDevice(m->device));
     hipStream_t s = stream ? (hipStream_t)stream : m->stream;
@@ -2084,21 +2084,21 @@ int orb_hamming_knn2_batch_device(orb_matcher* m, const uint8_t* d_q, const int3
                        t_stride_rows, d_best_idx, d_best_d, d_second_d);
     ORB_HIP_TRY(hipGetLastError());
     return ORB_OK;
-}
+} ORB_ABI_CATCH
 
 // MapPoint::ComputeDistinctiveDescriptors over a batch (device-resident, asynchronous).
 int orb_distinctive_descriptors_device(const uint8_t* d_desc, const int32_t* d_start, int n_points,
-                                       int32_t* d_best_idx, uint8_t* d_best_desc, void* stream) {
+                                       int32_t* d_best_idx, uint8_t* d_best_desc, void* stream) try {
     if (n_points < 0 || (n_points > 0 && (!d_desc || !d_start || !d_best_idx))) return ORB_EINVAL;
     if (n_points == 0) return ORB_OK;
     hipLaunchKernelGGL(k_distinctive, dim3(n_points), dim3(64), 0, (hipStream_t)stream, d_desc, d_start, d_best_idx,
                        d_best_desc);
     ORB_HIP_TRY(hipGetLastError());
     return ORB_OK;
-}
+} ORB_ABI_CATCH
 
 int orb_distinctive_descriptors(int device, const uint8_t* desc, const int32_t* start, int n_points, int32_t* best_idx,
-                                uint8_t* best_desc) {
+                                uint8_t* best_desc) try {
     if (n_points < 0 || (n_points > 0 && (!desc || !start || !best_idx))) return ORB_EINVAL;
     int st = check_device(device);
     if (st) return st;
@@ -2130,7 +2130,7 @@ int orb_distinctive_descriptors(int device, const uint8_t* desc, const int32_t* 
         if (hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
     }
     return rc;
-}
+} ORB_ABI_CATCH
 
 static int fuse_impl(int device, const orb_frame_view* kf, const orb_kf_params* kp, int n_mp, const uint8_t* mp_valid,
                      const float* mp_xyz, const float* mp_normal, const float* mp_min_dist, const float* mp_max_dist,
@@ -2206,21 +2206,21 @@ static int fuse_impl(int device, const orb_frame_view* kf, const orb_kf_params* 
 
 int orb_fuse(int device, const orb_frame_view* kf, const orb_kf_params* kp, int n_mp, const uint8_t* mp_valid,
              const float* mp_xyz, const float* mp_normal, const float* mp_min_dist, const float* mp_max_dist,
-             const uint8_t* mp_desc, float th, int32_t* best_idx, int32_t* best_dist) {
+             const uint8_t* mp_desc, float th, int32_t* best_idx, int32_t* best_dist) try {
     return fuse_impl(device, kf, kp, n_mp, mp_valid, mp_xyz, mp_normal, mp_min_dist, mp_max_dist, mp_desc, th, best_idx,
                      best_dist, 0);
-}
+} ORB_ABI_CATCH
 
 int orb_fuse_sim3(int device, const orb_frame_view* kf, const orb_kf_params* kp, int n_mp, const uint8_t* mp_valid,
                   const float* mp_xyz, const float* mp_normal, const float* mp_min_dist, const float* mp_max_dist,
-                  const uint8_t* mp_desc, float th, int32_t* best_idx, int32_t* best_dist) {
+                  const uint8_t* mp_desc, float th, int32_t* best_idx, int32_t* best_dist) try {
     return fuse_impl(device, kf, kp, n_mp, mp_valid, mp_xyz, mp_normal, mp_min_dist, mp_max_dist, mp_desc, th, best_idx,
                      best_dist, 1);
-}
+} ORB_ABI_CATCH
 
 int orb_search_by_sim3(int device, const orb_frame_view* kf1, const orb_frame_view* kf2, const orb_sim3_points* p1,
                        const orb_sim3_points* p2, const float cam1[4], const orb_scale_params* sc1,
-                       const orb_scale_params* sc2, float th, int32_t* matches12) {
+                       const orb_scale_params* sc2, float th, int32_t* matches12) try {
     if (!kf1 || !kf2 || !p1 || !p2 || !cam1 || !sc1 || !sc2 || !matches12) return ORB_EINVAL;
     if (kf1->n < 0 || kf2->n < 0 || kf1->n >= (1 << 16) || kf2->n >= (1 << 16) || p1->n != kf1->n || p2->n != kf2->n)
         return ORB_EINVAL;
@@ -2308,14 +2308,14 @@ int orb_search_by_sim3(int device, const orb_frame_view* kf1, const orb_frame_vi
         }
     }
     return nFound;
-}
+} ORB_ABI_CATCH
 
 int orb_search_for_triangulation(int device, const orb_frame_view* kf1, const orb_frame_view* kf2,
                                  const uint8_t* has_mp1, const uint8_t* has_mp2, int n_nodes1, const uint32_t* nodes1,
                                  const int32_t* start1, const int32_t* fidx1, int n_nodes2, const uint32_t* nodes2,
                                  const int32_t* start2, const int32_t* fidx2, const float F12[9], float ex, float ey,
                                  const float* scale_factors2, const float* level_sigma2, int n_levels2, int only_stereo,
-                                 int check_ori, int32_t* matches12) {
+                                 int check_ori, int32_t* matches12) try {
     if (!kf1 || !kf2 || !has_mp1 || !has_mp2 || !F12 || !scale_factors2 || !level_sigma2 || !matches12) return ORB_EINVAL;
     if (n_nodes1 < 0 || n_nodes2 < 0 || kf1->n < 0 || kf2->n < 0 || n_levels2 < 1 || n_levels2 > 32) return ORB_EINVAL;
     int st = check_device(device);
@@ -2402,7 +2402,7 @@ int orb_search_for_triangulation(int device, const orb_frame_view* kf1, const or
         if (hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
     }
     return rc == ORB_OK ? nm : rc;
-}
+} ORB_ABI_CATCH
 
 }  // extern "C"
 
@@ -2493,7 +2493,7 @@ extern "C" {
 int orb_search_by_bow_frame(int device, const orb_frame_view* kf, const uint8_t* kf_ok, int n_nodes_kf,
                             const uint32_t* nodes_kf, const int32_t* start_kf, const int32_t* fidx_kf,
                             const orb_frame_view* f, int n_nodes_f, const uint32_t* nodes_f, const int32_t* start_f,
-                            const int32_t* fidx_f, float nn_ratio, int check_ori, int32_t* matches_f) {
+                            const int32_t* fidx_f, float nn_ratio, int check_ori, int32_t* matches_f) try {
     if (!kf || !f || !matches_f || f->n < 0) return ORB_EINVAL;
     std::vector<int32_t> m12((size_t)std::max(kf->n, 1));
     const int n = search_by_bow(device, kf, kf_ok, n_nodes_kf, nodes_kf, start_kf, fidx_kf, f, nullptr, n_nodes_f,
@@ -2503,16 +2503,16 @@ int orb_search_by_bow_frame(int device, const orb_frame_view* kf, const uint8_t*
     for (int i = 0; i < kf->n; i++)
         if (m12[i] >= 0) matches_f[m12[i]] = i;
     return n;
-}
+} ORB_ABI_CATCH
 
 int orb_search_by_bow_kf(int device, const orb_frame_view* kf1, const uint8_t* ok1, int n_nodes1,
                          const uint32_t* nodes1, const int32_t* start1, const int32_t* fidx1,
                          const orb_frame_view* kf2, const uint8_t* ok2, int n_nodes2, const uint32_t* nodes2,
                          const int32_t* start2, const int32_t* fidx2, float nn_ratio, int check_ori,
-                         int32_t* matches12) {
+                         int32_t* matches12) try {
     if (!ok2) return ORB_EINVAL;
     return search_by_bow(device, kf1, ok1, n_nodes1, nodes1, start1, fidx1, kf2, ok2, n_nodes2, nodes2, start2, fidx2,
                          49 /* bestDist1 < TH_LOW */, nn_ratio, check_ori, matches12);
-}
+} ORB_ABI_CATCH
 
 }  // extern "C"

@@ -345,7 +345,7 @@ using namespace orbamd;
 extern "C" {
 
 int pose_optimize_batch_device(const pose_batch* p, const pose_batch_result* r, double* d_work, uint8_t* d_flags,
-                               int32_t* d_iters, void* stream) {
+                               int32_t* d_iters, void* stream) try {
     if (!p || !r || p->n_frames < 0 || !d_work || !d_flags) return ORB_EINVAL;
     if (p->n_frames == 0) return ORB_OK;
     PoseDev d;
@@ -358,9 +358,9 @@ int pose_optimize_batch_device(const pose_batch* p, const pose_batch_result* r, 
     hipLaunchKernelGGL(k_pose_opt, dim3(p->n_frames), dim3(kPoT), 0, (hipStream_t)stream, d);
     ORB_HIP_TRY(hipGetLastError());
     return ORB_OK;
-}
+} ORB_ABI_CATCH
 
-int pose_optimize_batch(int device, const pose_batch* p, pose_batch_result* r, int32_t* iters) {
+int pose_optimize_batch(int device, const pose_batch* p, pose_batch_result* r, int32_t* iters) try {
     if (!p || !r || p->n_frames < 0 || p->n_edges < 0) return ORB_EINVAL;
     int st = check_device(device);
     if (st) return st;
@@ -417,6 +417,6 @@ int pose_optimize_batch(int device, const pose_batch* p, pose_batch_result* r, i
         if (hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
     }
     return rc;
-}
+} ORB_ABI_CATCH
 
 }  // extern "C"

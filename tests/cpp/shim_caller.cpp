@@ -891,6 +891,9 @@ static bool run_mode(const std::string& mode, FILE* in, FILE* out) {
 // threads OUT REPS MODE1 IN1 [MODE2 IN2 ...]: one host thread per job, released together; each
 // runs its job REPS times (inputs re-read, so a mutated mock map starts afresh) and every result
 // must equal its first; OUT.k receives job k's first result.  Exit 4 on a differing repetition.
+// A mode written "fresh:MODE" runs every repetition on a new host thread, so each call of a
+// handle-less entry point creates its per-thread scratch (stream + device buffer, common.h
+// host_scratch) while the other jobs — the local BA's graph capture among them — are running.
 static int run_threads(int argc, char** argv) {
     const std::string outp = argv[2];
     const int reps = std::atoi(argv[3]);
@@ -907,16 +910,22 @@ static int run_threads(int argc, char** argv) {
         th.emplace_back([&J, &ready, reps, n = (int)jobs.size()] {
             ready.fetch_add(1);
             while (ready.load() < n) std::this_thread::yield();
+            const bool fresh = J.mode.rfind("fresh:", 0) == 0;
+            const std::string mode = fresh ? J.mode.substr(6) : J.mode;
             for (int r = 0; r < reps && J.err.empty(); r++) {
                 FILE* in = std::fopen(J.in.c_str(), "rb");
                 char* buf = nullptr;
                 size_t len = 0;
                 FILE* mem = open_memstream(&buf, &len);
-                try {
-                    if (!in || !mem || !run_mode(J.mode, in, mem)) J.err = "bad job " + J.mode;
-                } catch (const std::exception& e) {
-                    J.err = e.what();
-                }
+                auto call = [&] {
+                    try {
+                        if (!in || !mem || !run_mode(mode, in, mem)) J.err = "bad job " + J.mode;
+                    } catch (const std::exception& e) {
+                        J.err = e.what();
+                    }
+                };
+                if (fresh) std::thread(call).join();
+                else call();
                 if (in) std::fclose(in);
                 if (mem) std::fclose(mem);
                 std::vector<uint8_t> v(buf, buf + len);

@@ -42,3 +42,32 @@ def test_no_gpu_is_an_error_not_a_fallback(amd):
     with pytest.raises(amd._abi.OrbError) as e:
         amd.ORBextractor(1000, 1.2, 8, 20, 7)
     assert e.value.code == -19   # ORB_ENODEV
+
+
+def test_no_exception_crosses_the_abi():
+    """no C++ exception crosses the C-ABI.  Every definition of a declared entry point
+    in orb-slam2-_amd/csrc/*.hip is a function-try-block whose handler is ORB_ABI_CATCH
+    (std::bad_alloc -> ORB_ENOMEM, anything else -> ORB_EINTERNAL) or, for the void functions,
+    ORB_ABI_CATCH_VOID."""
+    names = set(declared())
+    seen = {}
+    for f in sorted((ROOT / "orb-slam2-_amd" / "csrc").glob("*.hip")):
+        src = f.read_text()
+        for m in re.finditer(r"^(int|void)\s+(\w+)\(", src, re.M):
+            if m.group(2) not in names:
+                continue
+            brace = src.index("{", m.start())
+            head = src[m.start(): brace]
+            if ";" in head:
+                continue   # a forward declaration
+            assert head.rstrip().endswith("try"), (f.name, m.group(2))
+            want = "ORB_ABI_CATCH_VOID" if m.group(1) == "void" else "ORB_ABI_CATCH"
+            first_line = src[m.start(): src.index("\n", m.start())].rstrip()
+            if first_line.endswith("}" + " " + want):
+                end = first_line   # a one-line definition
+            else:
+                close = re.compile(r"^}.*$", re.M).search(src, brace)   # the body's closing brace (column 0)
+                end = close.group(0).rstrip()
+            assert end.split()[-1] == want, (f.name, m.group(2), end)
+            seen[m.group(2)] = f.name
+    assert set(seen) == names, sorted(names - set(seen))

@@ -352,7 +352,11 @@ def test_shim_threading_contract(shim, tmp_path, amd):
            np.asarray(pb["point_id"], np.int64), np.asarray(pb["edge_point"], np.int32),
            np.asarray(pb["edge_pose"], np.int32), np.asarray(pb["edge_obs"], F32).reshape(-1), octave,
            np.asarray(pb["edge_cam"][0], F32), INV_SIGMA2, np.zeros(1, np.uint8))
-    jobs = [("stereo", "st_a.in"), ("sfi", "sfi.in"), ("pose", "pose.in"), ("lba", "lba.in"), ("stereo", "st_b.in")]
+    # fresh:pose — every PoseOptimization repetition on a new host thread, so its per-thread scratch
+    # (stream + device buffer) is created while the LocalMapping job may be capturing its LM graph
+    # (the creation takes the capture lock, common.h host_scratch)
+    jobs = [("stereo", "st_a.in"), ("sfi", "sfi.in"), ("pose", "pose.in"), ("lba", "lba.in"), ("stereo", "st_b.in"),
+            ("fresh:pose", "pose.in")]
     out = tmp_path / "thr.out"
     argv = [str(shim), "threads", str(out), "6"] + [x for m, f in jobs for x in (m, str(tmp_path / f))]
     r = subprocess.run(argv, capture_output=True, text=True, timeout=300)
@@ -366,6 +370,7 @@ def test_shim_threading_contract(shim, tmp_path, amd):
     n, outl, T = _read(f"{out}.2", np.int32, np.uint8, F32)
     ref = O.pose_optimization(frame)
     assert int(n[0]) == ref["n_inliers"] and np.array_equal(outl[pos], ref["outlier"])
+    assert (tmp_path / "thr.out.5").read_bytes() == (tmp_path / "thr.out.2").read_bytes()   # fresh-thread scratch
     res = _read(f"{out}.3", np.float64, np.float64, np.uint8, np.int64, np.float64, np.int64, np.uint8, np.int32,
                 np.int32, np.uint8, np.float64, np.float64, np.float64, np.uint8, np.float64, np.float64, np.float64,
                 np.int32)

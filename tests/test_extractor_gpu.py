@@ -191,8 +191,12 @@ def test_compute_stereo_matches(amd, W, H, nf, seed, mbf):
     assert n > 300
 
 
-def test_compute_stereo_matches_batch_device(amd):
-    """Device batch form: 3 stereo pairs extracted as frames (2p, 2p+1) of one batch."""
+@pytest.mark.parametrize("refill", [False, True])
+def test_compute_stereo_matches_batch_device(amd, refill):
+    """Device batch form: 3 stereo pairs extracted as frames (2p, 2p+1) of one batch.  refill:
+    level-0 copy on (orb_extractor_set_level0_copy), and the caller's frame buffer zeroed on the
+    stream right after the extraction is enqueued — the stereo matcher (which reads level 0) must
+    still see the extracted frames (include/orbslam2_amd.h, LEVEL-0 LIFETIME)."""
     import torch
     from orb_slam2_amd import synth, _abi
     import ctypes as C
@@ -212,11 +216,18 @@ def test_compute_stereo_matches_batch_device(amd):
     ur = torch.zeros((3, cap), dtype=torch.float32, device=dev)
     dep = torch.zeros((3, cap), dtype=torch.float32, device=dev)
     ns = torch.zeros(3, dtype=torch.int32, device=dev)
-    s = torch.cuda.current_stream(dev).cuda_stream
+    ts = torch.cuda.Stream(dev)   # an explicit stream: 0 (the legacy default) would select the handle's own
+    torch.cuda.synchronize(dev)
+    s = ts.cuda_stream
     lib = _abi.lib()
+    if refill:
+        _abi.check("l0copy", lib.orb_extractor_set_level0_copy(ex._h, 1))
     _abi.check("x", lib.orb_extract_batch_device(ex._h, C.c_void_p(ti.data_ptr()), H * W, 6, W, H,
                                                   C.c_void_p(kps.data_ptr()), C.c_void_p(desc.data_ptr()), cap,
                                                   C.c_void_p(cnt.data_ptr()), C.c_void_p(s)))
+    if refill:
+        with torch.cuda.stream(ts):
+            ti.zero_()   # the caller's next upload into the same buffer, same stream
     _abi.check("s", lib.orb_compute_stereo_matches_batch_device(
         ex._h, C.c_void_p(kps.data_ptr()), C.c_void_p(desc.data_ptr()), C.c_void_p(cnt.data_ptr()), cap, 3,
         C.c_float(mbf), C.c_float(0.0), C.c_void_p(ur.data_ptr()), C.c_void_p(dep.data_ptr()),
@@ -268,4 +279,55 @@ def test_batch_device_status_dense_octree_hbm_path(amd):
         assert n == len(ref["kps"])
         got_k = kps[b, :n].cpu().numpy().view(amd._abi.KEYPOINT_DTYPE).reshape(-1)
         assert got_k.tobytes() == ref["kps"].tobytes()
+        assert np.array_equal(desc[b, :n].cpu().numpy(), ref["desc"])
+
+
+@pytest.mark.parametrize("copy", [0, 1])
+def test_level0_lifetime_contract(amd, copy):
+    """LEVEL-0 LIFETIME (include/orbslam2_amd.h): without level-0 copy, raw level 0 of a device
+    batch IS the caller's frame (orb_pyramid_level_device returns a pointer into d_imgs, so a refill
+    of d_imgs is what a later level-0 read sees, as the reference's Mat header rebinding does);
+    with copy on, level 0 lives in the handle's slab and survives the refill.  Keypoints and
+    descriptors are identical either way."""
+    import torch
+    from orb_slam2_amd import synth, _abi
+    import ctypes as C
+    W, H, nf, B = 640, 480, 1000, 2
+    cv = synth.canvas(0x5EED0001, W, H)
+    imgs = np.stack([synth.frame(cv, W, H, t) for t in range(B)])
+    dev = torch.device("cuda", 0)
+    ex = amd.ORBextractor(nf, 1.2, 8, 20, 7, max_w=W, max_h=H, max_batch=B)
+    lib = _abi.lib()
+    _abi.check("l0copy", lib.orb_extractor_set_level0_copy(ex._h, copy))
+    assert lib.orb_extractor_set_level0_copy(ex._h, 2) == -22   # ORB_EINVAL
+    cap = C.c_int()
+    _abi.check("geom", lib.orb_extractor_geometry(ex._h, W, H, None, None, None, C.byref(cap)))
+    cap = cap.value
+    ti = torch.from_numpy(imgs).to(dev)
+    kps = torch.zeros((B, cap, 7), dtype=torch.int32, device=dev)
+    desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(B, dtype=torch.int32, device=dev)
+    ts = torch.cuda.Stream(dev)   # an explicit stream: 0 (the legacy default) would select the handle's own
+    torch.cuda.synchronize(dev)
+    ex.extract_batch_device(ti, kps, desc, cnt, ts.cuda_stream)
+    with torch.cuda.stream(ts):
+        ti.fill_(7)   # the caller refills its buffer on the extraction's stream
+    torch.cuda.synchronize(dev)
+    dp, w, h, pitch = C.c_void_p(), C.c_int(), C.c_int(), C.c_size_t()
+    _abi.check("lvl", lib.orb_pyramid_level_device(ex._h, 1, 0, 0, C.byref(dp), C.byref(w), C.byref(h), C.byref(pitch)))
+    hp = C.POINTER(C.c_uint8)()
+    _abi.check("lvlh", lib.orb_pyramid_level(ex._h, 1, 0, C.byref(hp), None, None, C.byref(pitch)))
+    l0 = np.ctypeslib.as_array(hp, shape=(H, pitch.value))[:, :W]
+    if copy:
+        assert dp.value != ti.data_ptr() + H * W
+        assert np.array_equal(l0, imgs[1])
+    else:
+        assert dp.value == ti.data_ptr() + H * W
+        assert (l0 == 7).all()
+    p = O.params(nf)
+    for b in range(B):
+        ref = O.extract(p, imgs[b])
+        n = int(cnt[b])
+        assert n == len(ref["kps"])
+        assert kps[b, :n].cpu().numpy().view(amd._abi.KEYPOINT_DTYPE).reshape(-1).tobytes() == ref["kps"].tobytes()
         assert np.array_equal(desc[b, :n].cpu().numpy(), ref["desc"])
