@@ -395,13 +395,25 @@ def bench_lba(args, amd, dev, local, rank, world):
         # RCCL calls of the all-reduce callback are issued on the same stream
         stream = torch.cuda.Stream(dev)
         ctx.set_stream(stream.cuda_stream)
+    # per-collective cost of the RCCL callback during the timed solves (HIP events on the LM stream
+    # around each all_reduce; DESIGN §5's cost model is checked against these at N > 1)
+    coll = {"on": False, "ev": [], "calls": 0, "bytes": 0}
     if world > 1 and not native:
         ws = torch.zeros(max(36 * nk * nk + 6 * nk, ne) + 64, dtype=torch.float64, device=dev)
 
         def ar(off, cnt, op):
             with torch.cuda.stream(stream):
+                if coll["on"]:
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
                 torch.distributed.all_reduce(ws[off:off + cnt], op=torch.distributed.ReduceOp.SUM if op == 0
                                              else torch.distributed.ReduceOp.MAX)
+                if coll["on"]:
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e1.record(stream)
+                    coll["ev"].append((e0, e1))
+                    coll["calls"] += 1
+                    coll["bytes"] += 8 * cnt
         ctx.set_comm(rank, world, ws, ar)
     if native and rank != 0:   # rank 0 runs the sharded solves; its result is broadcast below
         torch.distributed.barrier()
@@ -434,11 +446,13 @@ def bench_lba(args, amd, dev, local, rank, world):
             torch.distributed.barrier()
         torch.cuda.synchronize(dev)
         iters, times = 0, []
+        coll["on"] = True
         for _ in range(args.lba_solves):   # timed: the lba_solve C-ABI call (arguments marshalled once)
             t0 = time.perf_counter()
             its, _, _ = call()
             times.append(time.perf_counter() - t0)
             iters += sum(its)
+        coll["on"] = False
         tot = sum(times)
         if grp_live:
             ex_ms, n_ex = ctx.stats()
@@ -486,6 +500,17 @@ def bench_lba(args, amd, dev, local, rank, world):
         if st is not None:
             out["stage_ms_per_solve"] = {k: round(st[k] / args.lba_solves, 4) for k in
                                          ("linearize_ms", "schur_ms", "solve_ms", "update_ms")}
+        if coll["calls"]:
+            torch.cuda.synchronize(dev)
+            us = [1000.0 * a.elapsed_time(b) for a, b in coll["ev"]]
+            out["rccl_callback"] = {
+                "collectives_per_solve": round(coll["calls"] / args.lba_solves, 2),
+                "us_per_collective_mean": round(float(np.mean(us)), 2),
+                "us_per_collective_median": round(float(np.median(us)), 2),
+                "bytes_per_collective_mean": round(coll["bytes"] / coll["calls"], 1),
+                "collective_share_of_solve": round(sum(us) / 1e6 / max(tot, 1e-12), 4),
+                "note": "HIP events on the LM stream around each torch.distributed.all_reduce (RCCL) issued by "
+                        "the library's host callback, rank-local, timed solves only"}
         if grp_live:
             # (host-ordered exchange: events around each collective; the device-side default has
             # none — its cost is in the kernel trace as k_grp_sync / k_grp_reduce)
@@ -1035,7 +1060,169 @@ def bench_single_calls(args, amd, dev, reps=50):
         lambda: _abi.check("pose", lib.pose_optimize_batch(devi, C.byref(pb), C.byref(r), _abi.ptr(iters))))
     out["note"] = ("host buffers, PCIe both ways, one call at a time (median); each call is a chain of dependent "
                    "launches + copies, so these are launch/transfer latencies, not throughput")
+    out["routed_calls"] = bench_routed_calls(args, amd, dev, med)
     return out
+
+
+def bench_routed_calls(args, amd, dev, med, creps=9):
+    """Every other matcher / optimizer call the drop-in routes to the library, one call at
+    a time through its host-buffer entry point at the reference's call size (~1000 keypoints per
+    keyframe, TUM), against the oracle's restatement of the same call on one host thread (median of
+    `creps`; the reference runs these single-threaded on the LocalMapping / Tracking / LoopClosing
+    threads).  Each row: gpu_us, cpu_1thread_us, the reference call site.  LocalBundleAdjustment is
+    timed through the compiled C++ shim (graph gather R/src/Optimizer.cpp:569-625 + solve +
+    write-back :883-917, orb-slam2-_amd/lib/shim_caller timeit) on the config-4 window."""
+    from orb_slam2_amd import synth, Frame
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_ref as O
+    rows = {}
+
+    def cmed(fn):
+        fn()
+        ts = []
+        for _ in range(creps):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return round(1e6 * float(np.median(ts)), 1)
+
+    def row(name, gpu_fn, cpu_fn, site, size):
+        g = med(gpu_fn)
+        c = None if args.no_cpu else cmed(cpu_fn)
+        rows[name] = {"gpu_us": g, "cpu_1thread_us": c, "gpu_over_cpu": None if c is None else round(c / g, 2),
+                      "call_site": site, "size": size}
+
+    def kp_of(k, angle=True):
+        a = np.zeros(len(k["x"]), dtype=[("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                                         ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+        a["x"], a["y"], a["octave"] = k["x"], k["y"], k["octave"]
+        if angle and "angle" in k:
+            a["angle"] = k["angle"]
+        return a
+    # SearchByBoW(KF, Frame) and (KF, KF)
+    voc = synth.vocabulary(k=10, L=4, seed=5, early_leaf=0.05, stop_frac=0.03)
+    ov = O.OracleVocabulary(*voc, 4)
+    k1, k2 = synth.bow_match_problem(voc, seed=11)
+    fv1, fv2 = O.bow_transform(ov, k1["desc"], 4)[1], O.bow_transform(ov, k2["desc"], 4)[1]
+    a1, a2 = O.featvec_arrays(fv1), O.featvec_arrays(fv2)
+    f1, f2 = Frame(kp_of(k1), k1["desc"], k1["W"], k1["H"]), Frame(kp_of(k2), k2["desc"], k2["W"], k2["H"])
+    m = amd.ORBmatcher(0.7, True, device=dev.index or 0)
+    size = f"{len(k1['x'])} x {len(k2['x'])} features, levelsup 4"
+    row("search_by_bow_kf_frame", lambda: m.SearchByBoW(f1, k1["has_mp"], fv1, f2, a2),
+        lambda: O.search_by_bow_frame(k1, k1["has_mp"], a1, k2, a2, 0.7, True), "R/src/Tracking.cpp:1020, 1840", size)
+    row("search_by_bow_kf_kf", lambda: m.SearchByBoWKF(f1, k1["has_mp"], a1, f2, k2["has_mp"], fv2),
+        lambda: O.search_by_bow_kf(k1, k1["has_mp"], a1, k2, k2["has_mp"], a2, 0.7, True), "R/src/LoopClosing.cpp:327", size)
+    # SearchForTriangulation
+    tp = synth.triangulation_problem()
+    t1, t2 = tp["kf1"], tp["kf2"]
+    tf1 = Frame(kp_of(t1), t1["desc"], t1["W"], t1["H"], mvuRight=t1["uright"])
+    tf2 = Frame(kp_of(t2), t2["desc"], t2["W"], t2["H"], mvuRight=t2["uright"])
+    row("search_for_triangulation",
+        lambda: amd.SearchForTriangulation(tf1, tf2, t1["has_mp"], t2["has_mp"], (t1["nodes"], t1["start"], t1["fidx"]),
+                                           (t2["nodes"], t2["start"], t2["fidx"]), tp["F12"], (tp["ex"], tp["ey"]),
+                                           tp["scale_factors"], tp["level_sigma2"], False, True),
+        lambda: O.search_for_triangulation(tp, False, True), "R/src/LocalMapping.cpp:374",
+        f"{len(t1['x'])} x {len(t2['x'])} keypoints")
+    # Fuse (keyframe, map points) and the Scw form; SearchByProjection(KF, Scw)
+    fp = synth.fuse_problem()
+    kf, kp = fp["kf"], fp["kp"]
+    ff = Frame(kp_of(kf, False), kf["desc"], kf["W"], kf["H"], mvuRight=kf["uright"])
+    fargs = (fp["mp_valid"], fp["mp_xyz"], fp["mp_normal"], fp["mp_min_dist"], fp["mp_max_dist"], fp["mp_desc"])
+    fsize = f"{len(kf['x'])} keypoints, {len(fp['mp_xyz'])} map points"
+    row("fuse", lambda: amd.Fuse(ff, kp["Tcw"], kp["Ow"], kp["cam"], kp["log_scale_factor"], kp["scale_factors"],
+                                 kp["inv_level_sigma2"], *fargs, 3.0),
+        lambda: O.fuse(fp, 3.0), "R/src/LocalMapping.cpp:654, 688", fsize)
+    pre = np.full(len(kf["x"]), -1, np.int32)
+    row("search_by_projection_sim3",
+        lambda: m.SearchByProjectionSim3(ff, np.asarray(kp["Tcw"], np.float32)[:3, :4], kp["Ow"], kp["cam"],
+                                         kp["log_scale_factor"], kp["scale_factors"], *fargs, 10.0, pre.copy()),
+        lambda: O.search_by_projection_sim3(fp, 10.0, pre.copy()), "R/src/LoopClosing.cpp:474", fsize)
+    # SearchByProjection(Frame, KF, set, th, ORBdist) (relocalisation)
+    rng = np.random.default_rng(103)
+    n_mp = len(fp["mp_xyz"])
+    kfs = {"x": rng.uniform(0, 640, n_mp).astype(np.float32), "y": rng.uniform(0, 480, n_mp).astype(np.float32),
+           "octave": np.zeros(n_mp, np.int32), "desc": np.zeros((n_mp, 32), np.uint8),
+           "angle": rng.uniform(0, 360, n_mp).astype(np.float32), "W": 640, "H": 480}
+    kfa = dict(kf, angle=rng.uniform(0, 360, len(kf["x"])).astype(np.float32))
+    T = np.eye(4, dtype=np.float32)
+    T[:3, :4] = np.asarray(kp["Tcw"], np.float32)[:3, :4]
+    fcur = Frame(kp_of(kfa), kfa["desc"], kfa["W"], kfa["H"], mTcw=T, mvScaleFactors=np.asarray(kp["scale_factors"], np.float32))
+    fks = Frame(kp_of(kfs), kfs["desc"], 640, 480)
+    occ = np.full(len(kf["x"]), -1, np.int32)
+    cur_v, kf_v = O.FrameView(kfa, kfa["desc"], 640, 480), O.FrameView(kfs, kfs["desc"], 640, 480)
+    row("search_by_projection_kf",
+        lambda: m.SearchByProjectionKF(fcur, fks, fp["mp_valid"], fp["mp_xyz"], fp["mp_min_dist"], fp["mp_max_dist"],
+                                       fp["mp_desc"], kp["cam"][:4], kp["Ow"], kp["log_scale_factor"], 10.0, 100, occ.copy()),
+        lambda: O.search_by_projection_kf(cur_v, kp["Tcw"][:3, :4], kp["Ow"], kf_v, fp["mp_valid"], fp["mp_xyz"],
+                                          fp["mp_min_dist"], fp["mp_max_dist"], fp["mp_desc"], kp["cam"][:4],
+                                          kp["log_scale_factor"], kp["scale_factors"], 10.0, 100, True, occ.copy()),
+        "R/src/Tracking.cpp:1921", fsize)
+    # SearchBySim3
+    sp = synth.sim3_problem()
+    S1, S2 = synth.sim3_side_transforms(sp)
+    sides = [dict(Tcw=k["Tcw"], S=S, valid=k["mp_valid"], xyz=k["mp_xyz"], min_dist=k["mp_min_dist"],
+                  max_dist=k["mp_max_dist"], desc=k["mp_desc"]) for k, S in ((sp["kf1"], S1), (sp["kf2"], S2))]
+    sc = (sp["log_scale_factor"], sp["scale_factors"])
+    sf1 = Frame(kp_of(sp["kf1"], False), sp["kf1"]["desc"], 640, 480)
+    sf2 = Frame(kp_of(sp["kf2"], False), sp["kf2"]["desc"], 640, 480)
+    row("search_by_sim3", lambda: amd.SearchBySim3(sf1, sf2, sides[0], sides[1], sp["cam"], sc, sc, 7.5),
+        lambda: O.search_by_sim3(sp, 7.5), "R/src/LoopClosing.cpp:402",
+        f"{len(sp['kf1']['x'])} x {len(sp['kf2']['x'])} keypoints")
+    # ComputeDistinctiveDescriptors (per new map point: its observations' descriptors)
+    drng = np.random.default_rng(5)
+    lists = [drng.integers(0, 256, (int(drng.integers(2, 9)), 32), dtype=np.uint8) for _ in range(300)]
+    row("compute_distinctive_descriptors_300_points", lambda: amd.ComputeDistinctiveDescriptors(lists, device=dev.index or 0),
+        lambda: [O.distinctive_descriptor(l) for l in lists], "R/src/LocalMapping.cpp:467 (one call per point)",
+        "300 map points x 2-8 observations")
+    # Frame::ComputeStereoMatches (EuRoC geometry) after the two extractions
+    W, H, NF = 752, 480, 1200
+    left, right = synth.stereo_pair(synth.canvas(0x5EED0005, W, H), W, H, 0)
+    exL = amd.ORBextractor(NF, 1.2, 8, 20, 7, device=dev.index or 0, max_w=W, max_h=H)
+    exR = amd.ORBextractor(NF, 1.2, 8, 20, 7, device=dev.index or 0, max_w=W, max_h=H)
+    kl, dl = exL(left)
+    kr, dr = exR(right)
+    pp = O.params(NF)
+    ea, eb = O.extract(pp, left, want_pyramid=True), O.extract(pp, right, want_pyramid=True)
+    row("compute_stereo_matches_euroc", lambda: amd.ComputeStereoMatches(exL, exR, kl, dl, kr, dr, EUROC_MBF),
+        lambda: O.compute_stereo_matches(pp, ea, eb, EUROC_MBF), "R/src/Frame.cpp:101",
+        f"{len(kl)} x {len(kr)} keypoints, 752x480")
+    m.close()
+    # LocalBundleAdjustment through the compiled shim (config 4 window)
+    exe = ROOT / "orb-slam2-_amd" / "lib" / "shim_caller"
+    if exe.exists():
+        import subprocess
+        import tempfile
+        pb = synth.ba_problem(n_local=args.lba_kf, n_points=args.lba_points)
+        inv_sigma2 = (np.float32(1.0) / np.array([np.float32(1.2) ** (2 * lv) for lv in range(8)], np.float32))
+        octave = np.array([int(np.argmin(np.abs(inv_sigma2.astype(np.float64) - i))) for i in pb["edge_info"]], np.int32)
+        arrays = [np.asarray(pb["Tcw"], np.float32).reshape(-1), np.asarray(pb["pose_fixed"], np.uint8),
+                  np.asarray(pb["pose_id"], np.int64), np.asarray(pb["point_xyz"], np.float32).reshape(-1),
+                  np.asarray(pb["point_id"], np.int64), np.asarray(pb["edge_point"], np.int32),
+                  np.asarray(pb["edge_pose"], np.int32), np.asarray(pb["edge_obs"], np.float32).reshape(-1), octave,
+                  np.asarray(pb["edge_cam"][0], np.float32), inv_sigma2, np.zeros(1, np.uint8)]
+        with tempfile.TemporaryDirectory() as td:
+            inp = pathlib.Path(td) / "lba.in"
+            with open(inp, "wb") as f:
+                for a in arrays:
+                    a = np.ascontiguousarray(a)
+                    np.array([a.size], np.int64).tofile(f)
+                    a.tofile(f)
+            res = subprocess.run([str(exe), "timeit", "20", "lba", str(inp)], capture_output=True, text=True,
+                                 timeout=300)
+        g = None
+        if res.returncode == 0 and res.stdout.startswith("median_us"):
+            g = float(res.stdout.split()[1])
+        c = None
+        if not args.no_cpu:
+            t0 = time.perf_counter()
+            O.lba_solve(pb)
+            c = round(1e6 * (time.perf_counter() - t0), 1)
+        rows["local_bundle_adjustment_shim"] = {
+            "gpu_us": g, "cpu_1thread_us": c, "gpu_over_cpu": None if (c is None or not g) else round(c / g, 2),
+            "call_site": "R/src/LocalMapping.cpp:95", "size": f"{args.lba_kf} KF + 4 fixed x {args.lba_points} points",
+            "note": "whole call: graph gather from the (mock) map, lba_solve, write-back; cpu = the oracle's solve "
+                    "alone (no gather), 1 thread", "stderr_tail": None if res.returncode == 0 else res.stderr[-300:]}
+    return rows
 
 
 def bench_pose(args, amd, dev, n_frames=256, n_points=600):

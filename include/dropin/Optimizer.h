@@ -1,9 +1,9 @@
-// Drop-in replacement for R/include/Optimizer.h: the same static interface; LocalBundleAdjustment
-// (R/src/Optimizer.cpp:564-918) runs on liborbslam2_amd through include/orbslam2_amd_shim.hpp
-// (graph gathering and write-back as the reference does them, the solve on the GPU).  The other
-// methods keep their reference definitions in R/src/Optimizer.cpp (delete its
-// LocalBundleAdjustment definition).  PoseOptimization / BundleAdjustment over the same library:
-// INTEGRATION.md.  Compiles inside the reference tree only (OpenCV, g2o headers).
+// Drop-in replacement for R/include/Optimizer.h: the same static interface.  LocalBundleAdjustment
+// (R/src/Optimizer.cpp:564-918) and PoseOptimization (:306-535) run on liborbslam2_amd through
+// include/orbslam2_amd_shim.hpp (graph gathering and write-back as the reference does them, the
+// solve on the GPU); delete those two definitions from R/src/Optimizer.cpp.  The other methods keep
+// their reference definitions; BundleAdjustment over the same library (lba_solve_global) is wired
+// as INTEGRATION.md shows.  Compiles inside the reference tree only (OpenCV, g2o headers).
 #ifndef OPTIMIZER_H
 #define OPTIMIZER_H
 

@@ -187,6 +187,7 @@ int orb_vocabulary_transform(orb_vocab* h, const uint8_t* desc, int n, int level
     ORB_HIP_TRY(hipSetDevice(h->device));
     const size_t need = (size_t)n * (32 + 4 + 8 + 4) + 1024;
     if (h->scratchCap < need) {
+        std::lock_guard<std::mutex> lk(legacy_capture_mutex());   // hipFree / hipMalloc (common.h)
         if (h->scratch) (void)hipFree(h->scratch);
         h->scratch = nullptr;
         h->scratchCap = 0;

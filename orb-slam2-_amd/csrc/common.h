@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <cstring>
 #include <mutex>
 #include <new>
 #include <vector>
@@ -66,7 +67,8 @@ int check_device(int dev);
 struct HostScratch {
     int device = -1;
     hipStream_t stream = nullptr;
-    char* base = nullptr;
+    char* base = nullptr;   // device
+    char* pin = nullptr;    // pinned host staging of the same size (Staging below)
     size_t cap = 0;
 };
 inline int host_scratch(int device, size_t bytes, HostScratch** out) {
@@ -89,15 +91,60 @@ inline int host_scratch(int device, size_t bytes, HostScratch** out) {
     if (h->cap < bytes) {   // grow (rare): the stream is idle between calls of this thread
         std::lock_guard<std::mutex> lk(legacy_capture_mutex());
         if (h->base) (void)hipFree(h->base);
-        h->base = nullptr;
+        if (h->pin) (void)hipHostFree(h->pin);
+        h->base = h->pin = nullptr;
         h->cap = 0;
         const size_t cap = std::max(bytes + bytes / 2, (size_t)1 << 20);
         if (hipMalloc((void**)&h->base, cap) != hipSuccess) return ORB_ENOMEM;
+        if (hipHostMalloc((void**)&h->pin, cap, hipHostMallocDefault) != hipSuccess) return ORB_ENOMEM;
         h->cap = cap;
     }
     *out = h;
     return ORB_OK;
 }
+
+// One PCIe crossing each way for a handle-less host call: its host inputs are packed into the
+// thread's pinned staging at the offsets they take in the device scratch and go over in ONE copy
+// (a pageable hipMemcpyAsync per array costs ~10 us each); outputs are reserved after them in one
+// contiguous range that comes back in one copy, and the host reads them from the staging after
+// the stream sync.  Offsets advance in 256-byte steps; running past the scratch is an error.
+struct Staging {
+    HostScratch* h;
+    size_t off = 0, inEnd = 0;
+    bool over = false;
+    explicit Staging(HostScratch* hs) : h(hs) {}
+    static size_t al(size_t b) { return (b + 255) & ~(size_t)255; }
+    char* take(size_t bytes) {
+        const size_t a = al(bytes + 1);
+        if (off + a > h->cap) { over = true; return h->base; }
+        char* d = h->base + off;
+        off += a;
+        return d;
+    }
+    // an input: copied into the staging now, on the device after upload()
+    char* in(const void* src, size_t bytes) {
+        const size_t at = off;
+        char* d = take(bytes);
+        if (!over && src && bytes) std::memcpy(h->pin + at, src, bytes);
+        return d;
+    }
+    int upload(hipStream_t s) {
+        if (over) return ORB_EINTERNAL;
+        inEnd = off;
+        if (off && hipMemcpyAsync(h->base, h->pin, off, hipMemcpyHostToDevice, s) != hipSuccess) return ORB_EGPU;
+        return ORB_OK;
+    }
+    // device space after the inputs (outputs, work); `from` .. the end comes back in download()
+    char* out(size_t bytes) { return take(bytes); }
+    int download(hipStream_t s, const void* from) {
+        if (over) return ORB_EINTERNAL;
+        const size_t a = (size_t)((const char*)from - h->base);
+        if (a < off && hipMemcpyAsync(h->pin + a, from, off - a, hipMemcpyDeviceToHost, s) != hipSuccess) return ORB_EGPU;
+        return ORB_OK;
+    }
+    template <class T>
+    T* host(T* dptr) const { return (T*)(h->pin + ((const char*)dptr - h->base)); }
+};
 
 // 8-bit row pitch used for every device image (multiple of 64 bytes).
 inline int pitch_of(int w) { return (w + 63) & ~63; }

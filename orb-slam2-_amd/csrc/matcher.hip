@@ -2107,27 +2107,27 @@ int orb_distinctive_descriptors(int device, const uint8_t* desc, const int32_t* 
         if (start[m + 1] < start[m]) return ORB_EINVAL;
     ORB_HIP_TRY(hipSetDevice(device));
     const size_t T = (size_t)start[n_points] - (size_t)start[0];
-    char* base = nullptr;
     const size_t bD = ((T * 32 + 255) & ~(size_t)255), bS = (((size_t)n_points + 1) * 4 + 255) & ~(size_t)255,
                  bI = ((size_t)n_points * 4 + 255) & ~(size_t)255;
     HostScratch* hsc = nullptr;
-    if (int e_ = host_scratch(device, bD + bS + bI + (size_t)n_points * 32 + 256, &hsc)) return e_;
-    base = hsc->base;
+    if (int e_ = host_scratch(device, bD + bS + bI + (size_t)n_points * 32 + 8 * 256, &hsc)) return e_;
     hipStream_t s = hsc->stream;
-    uint8_t* dD = (uint8_t*)base;
-    int32_t* dS = (int32_t*)(base + bD);
-    int32_t* dI = (int32_t*)(base + bD + bS);
-    uint8_t* dB = (uint8_t*)(base + bD + bS + bI);
-    std::vector<int32_t> rel((size_t)n_points + 1);
-    for (int m = 0; m <= n_points; m++) rel[m] = start[m] - start[0];
-    int rc = ORB_OK;
-    if (T) ORB_HIP_TRY(hipMemcpyAsync(dD, desc + (size_t)start[0] * 32, T * 32, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(dS, rel.data(), rel.size() * 4, hipMemcpyHostToDevice, s));
-    rc = orb_distinctive_descriptors_device(dD, dS, n_points, dI, best_desc ? dB : nullptr, s);
+    Staging sg(hsc);   // one H2D (descriptors + relative starts), one D2H (index + descriptor)
+    uint8_t* dD = (uint8_t*)sg.in(T ? desc + (size_t)start[0] * 32 : nullptr, T * 32);
+    int32_t* dS = (int32_t*)sg.in(nullptr, ((size_t)n_points + 1) * 4);
+    int32_t* hrel = sg.host(dS);
+    for (int m = 0; m <= n_points; m++) hrel[m] = start[m] - start[0];
+    if (int e_ = sg.upload(s)) return e_;
+    int32_t* dI = (int32_t*)sg.out((size_t)n_points * 4);
+    uint8_t* dB = (uint8_t*)sg.out((size_t)n_points * 32);
+    int rc = orb_distinctive_descriptors_device(dD, dS, n_points, dI, best_desc ? dB : nullptr, s);
     if (rc == ORB_OK) {
-        ORB_HIP_TRY(hipMemcpyAsync(best_idx, dI, (size_t)n_points * 4, hipMemcpyDeviceToHost, s));
-        if (best_desc) ORB_HIP_TRY(hipMemcpyAsync(best_desc, dB, (size_t)n_points * 32, hipMemcpyDeviceToHost, s));
-        if (hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
+        rc = sg.download(s, dI);
+        if (rc == ORB_OK && hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
+        if (rc == ORB_OK) {
+            std::memcpy(best_idx, sg.host(dI), (size_t)n_points * 4);
+            if (best_desc) std::memcpy(best_desc, sg.host(dB), (size_t)n_points * 32);
+        }
     }
     return rc;
 } ORB_ABI_CATCH
@@ -2163,43 +2163,33 @@ static int fuse_impl(int device, const orb_frame_view* kf, const orb_kf_params* 
     const size_t bK = al((size_t)nk * sizeof(orb_keypoint) + 1), bD = al((size_t)nk * 32 + 1), bU = al((size_t)nk * 4 + 1),
                  bV = al((size_t)n_mp), bX = al((size_t)n_mp * 12), bM = al((size_t)n_mp * 4), bMD = al((size_t)n_mp * 32),
                  bO = al((size_t)n_mp * 4);
-    char* base = nullptr;
     HostScratch* hsc = nullptr;
-    if (int e_ = host_scratch(device, bK + bD + bU + bV + 2 * bX + 2 * bM + bMD + 2 * bO, &hsc)) return e_;
-    base = hsc->base;
+    if (int e_ = host_scratch(device, bK + bD + bU + bV + 2 * bX + 2 * bM + bMD + 2 * bO + 12 * 256, &hsc)) return e_;
     hipStream_t s = hsc->stream;
-    char* c = base;
-    auto take = [&](size_t b) { char* r = c; c += b; return r; };
-    orb_keypoint* dK = (orb_keypoint*)take(bK);
-    uint8_t* dD = (uint8_t*)take(bD);
-    float* dU = (float*)take(bU);
-    uint8_t* dV = (uint8_t*)take(bV);
-    float* dX = (float*)take(bX);
-    float* dN = (float*)take(bX);
-    float* dMin = (float*)take(bM);
-    float* dMax = (float*)take(bM);
-    uint8_t* dMD = (uint8_t*)take(bMD);
-    int32_t* dBI = (int32_t*)take(bO);
-    int32_t* dBD = (int32_t*)take(bO);
-    if (nk) {
-        ORB_HIP_TRY(hipMemcpyAsync(dK, hk.data(), (size_t)nk * sizeof(orb_keypoint), hipMemcpyHostToDevice, s));
-        ORB_HIP_TRY(hipMemcpyAsync(dD, kf->desc, (size_t)nk * 32, hipMemcpyHostToDevice, s));
-        if (kf->uright) ORB_HIP_TRY(hipMemcpyAsync(dU, kf->uright, (size_t)nk * 4, hipMemcpyHostToDevice, s));
-    }
-    ORB_HIP_TRY(hipMemcpyAsync(dV, mp_valid, (size_t)n_mp, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(dX, mp_xyz, (size_t)n_mp * 12, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(dN, mp_normal, (size_t)n_mp * 12, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(dMin, mp_min_dist, (size_t)n_mp * 4, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(dMax, mp_max_dist, (size_t)n_mp * 4, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(dMD, mp_desc, (size_t)n_mp * 32, hipMemcpyHostToDevice, s));
+    Staging sg(hsc);   // one H2D of every input, one D2H of both outputs
+    orb_keypoint* dK = (orb_keypoint*)sg.in(hk.data(), (size_t)nk * sizeof(orb_keypoint));
+    uint8_t* dD = (uint8_t*)sg.in(kf->desc, (size_t)nk * 32);
+    float* dU = (float*)sg.in(kf->uright, kf->uright ? (size_t)nk * 4 : 0);
+    uint8_t* dV = (uint8_t*)sg.in(mp_valid, (size_t)n_mp);
+    float* dX = (float*)sg.in(mp_xyz, (size_t)n_mp * 12);
+    float* dN = (float*)sg.in(mp_normal, (size_t)n_mp * 12);
+    float* dMin = (float*)sg.in(mp_min_dist, (size_t)n_mp * 4);
+    float* dMax = (float*)sg.in(mp_max_dist, (size_t)n_mp * 4);
+    uint8_t* dMD = (uint8_t*)sg.in(mp_desc, (size_t)n_mp * 32);
+    if (int e_ = sg.upload(s)) return e_;
+    int32_t* dBI = (int32_t*)sg.out((size_t)n_mp * 4);
+    int32_t* dBD = (int32_t*)sg.out((size_t)n_mp * 4);
     const GridParams g = grid_of(kf);
     hipLaunchKernelGGL(k_fuse, dim3((n_mp + 3) / 4), dim3(256), 0, s, dK, dD, kf->uright ? (const float*)dU : nullptr,
                        nk, g, K, n_mp, dV, dX, dN, dMin, dMax, dMD, th, dBI, dBD, sim3);
     int rc = hipGetLastError() == hipSuccess ? ORB_OK : ORB_EGPU;
     if (rc == ORB_OK) {
-        ORB_HIP_TRY(hipMemcpyAsync(best_idx, dBI, (size_t)n_mp * 4, hipMemcpyDeviceToHost, s));
-        ORB_HIP_TRY(hipMemcpyAsync(best_dist, dBD, (size_t)n_mp * 4, hipMemcpyDeviceToHost, s));
-        if (hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
+        rc = sg.download(s, dBI);
+        if (rc == ORB_OK && hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
+        if (rc == ORB_OK) {
+            std::memcpy(best_idx, sg.host(dBI), (size_t)n_mp * 4);
+            std::memcpy(best_dist, sg.host(dBD), (size_t)n_mp * 4);
+        }
     }
     return rc;
 }
@@ -2254,50 +2244,38 @@ int orb_search_by_sim3(int device, const orb_frame_view* kf1, const orb_frame_vi
                         2 * al((size_t)n1 * 4) + al((size_t)n1 * 32) + al((size_t)n1 * 4);
     const size_t per2 = al((size_t)n2 * sizeof(orb_keypoint)) + al((size_t)n2 * 32) + al(n2) + al((size_t)n2 * 12) +
                         2 * al((size_t)n2 * 4) + al((size_t)n2 * 32) + al((size_t)n2 * 4);
-    char* base = nullptr;
     HostScratch* hsc = nullptr;
-    if (int e_ = host_scratch(device, per1 + per2, &hsc)) return e_;
-    base = hsc->base;
+    if (int e_ = host_scratch(device, per1 + per2 + 16 * 256, &hsc)) return e_;
     hipStream_t s = hsc->stream;
-    char* c = base;
-    hipError_t cpErr = hipSuccess;   // first failed upload, checked before the launch
-    auto put = [&](const void* src, size_t bytes) {
-        char* r = c;
-        c += al(bytes);
-        if (src && bytes) {
-            const hipError_t e = hipMemcpyAsync(r, src, bytes, hipMemcpyHostToDevice, s);
-            if (e != hipSuccess && cpErr == hipSuccess) cpErr = e;
-        }
-        return r;
-    };
-    auto* dK1 = (orb_keypoint*)put(hk1.data(), (size_t)n1 * sizeof(orb_keypoint));
-    auto* dD1 = (uint8_t*)put(kf1->desc, (size_t)n1 * 32);
-    auto* dV1 = (uint8_t*)put(p1->valid, n1);
-    auto* dX1 = (float*)put(p1->xyz, (size_t)n1 * 12);
-    auto* dMin1 = (float*)put(p1->min_dist, (size_t)n1 * 4);
-    auto* dMax1 = (float*)put(p1->max_dist, (size_t)n1 * 4);
-    auto* dMD1 = (uint8_t*)put(p1->desc, (size_t)n1 * 32);
-    auto* dM1 = (int32_t*)put(nullptr, (size_t)n1 * 4);
-    auto* dK2 = (orb_keypoint*)put(hk2.data(), (size_t)n2 * sizeof(orb_keypoint));
-    auto* dD2 = (uint8_t*)put(kf2->desc, (size_t)n2 * 32);
-    auto* dV2 = (uint8_t*)put(p2->valid, n2);
-    auto* dX2 = (float*)put(p2->xyz, (size_t)n2 * 12);
-    auto* dMin2 = (float*)put(p2->min_dist, (size_t)n2 * 4);
-    auto* dMax2 = (float*)put(p2->max_dist, (size_t)n2 * 4);
-    auto* dMD2 = (uint8_t*)put(p2->desc, (size_t)n2 * 32);
-    auto* dM2 = (int32_t*)put(nullptr, (size_t)n2 * 4);
-    if (cpErr != hipSuccess) return ORB_EGPU;
+    Staging sg(hsc);   // one H2D of both sides' inputs, one D2H of both directions' matches
+    auto* dK1 = (orb_keypoint*)sg.in(hk1.data(), (size_t)n1 * sizeof(orb_keypoint));
+    auto* dD1 = (uint8_t*)sg.in(kf1->desc, (size_t)n1 * 32);
+    auto* dV1 = (uint8_t*)sg.in(p1->valid, n1);
+    auto* dX1 = (float*)sg.in(p1->xyz, (size_t)n1 * 12);
+    auto* dMin1 = (float*)sg.in(p1->min_dist, (size_t)n1 * 4);
+    auto* dMax1 = (float*)sg.in(p1->max_dist, (size_t)n1 * 4);
+    auto* dMD1 = (uint8_t*)sg.in(p1->desc, (size_t)n1 * 32);
+    auto* dK2 = (orb_keypoint*)sg.in(hk2.data(), (size_t)n2 * sizeof(orb_keypoint));
+    auto* dD2 = (uint8_t*)sg.in(kf2->desc, (size_t)n2 * 32);
+    auto* dV2 = (uint8_t*)sg.in(p2->valid, n2);
+    auto* dX2 = (float*)sg.in(p2->xyz, (size_t)n2 * 12);
+    auto* dMin2 = (float*)sg.in(p2->min_dist, (size_t)n2 * 4);
+    auto* dMax2 = (float*)sg.in(p2->max_dist, (size_t)n2 * 4);
+    auto* dMD2 = (uint8_t*)sg.in(p2->desc, (size_t)n2 * 32);
+    if (int e_ = sg.upload(s)) return e_;
+    auto* dM1 = (int32_t*)sg.out((size_t)n1 * 4);
+    auto* dM2 = (int32_t*)sg.out((size_t)n2 * 4);
     hipLaunchKernelGGL(k_sim3_match, dim3((n1 + 3) / 4), dim3(256), 0, s, dK2, dD2, n2, grid_of(kf2), S12, n1, dV1, dX1,
                        dMin1, dMax1, dMD1, dM1);
     hipLaunchKernelGGL(k_sim3_match, dim3((n2 + 3) / 4), dim3(256), 0, s, dK1, dD1, n1, grid_of(kf1), S21, n2, dV2, dX2,
                        dMin2, dMax2, dMD2, dM2);
-    std::vector<int32_t> m1((size_t)n1), m2((size_t)n2);
     int rc = hipGetLastError() == hipSuccess ? ORB_OK : ORB_EGPU;
     if (rc == ORB_OK) {
-        ORB_HIP_TRY(hipMemcpyAsync(m1.data(), dM1, (size_t)n1 * 4, hipMemcpyDeviceToHost, s));
-        ORB_HIP_TRY(hipMemcpyAsync(m2.data(), dM2, (size_t)n2 * 4, hipMemcpyDeviceToHost, s));
-        if (hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
+        rc = sg.download(s, dM1);
+        if (rc == ORB_OK && hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
     }
+    const int32_t* m1 = sg.host(dM1);
+    const int32_t* m2 = sg.host(dM2);
     if (rc) return rc;
     int nFound = 0;   // R :1490-1503: keep the pairs both directions agree on
     for (int i1 = 0; i1 < n1; i1++) {
@@ -2361,45 +2339,36 @@ int orb_search_for_triangulation(int device, const orb_frame_view* kf1, const or
                        al((size_t)n1 * 32) + al((size_t)n2 * 32 + 1) + 2 * al((size_t)n1 * 4) + 2 * al((size_t)n2 * 4 + 1) +
                        al((size_t)n1) + al((size_t)n2 + 1) + al(common.size() * 16) + al((size_t)L1 * 4 + 1) +
                        al((size_t)L2 * 4 + 1) + al(4) + 4096;
-    char* base = nullptr;
     HostScratch* hsc = nullptr;
     if (int e_ = host_scratch(device, tot, &hsc)) return e_;
-    base = hsc->base;
     hipStream_t s = hsc->stream;
-    char* c = base;
-    hipError_t cpErr = hipSuccess;   // first failed upload, checked before the launch
-    auto put = [&](const void* src, size_t bytes) {
-        char* r = c;
-        c += al(bytes + 1);
-        if (src && bytes) {
-            const hipError_t e = hipMemcpyAsync(r, src, bytes, hipMemcpyHostToDevice, s);
-            if (e != hipSuccess && cpErr == hipSuccess) cpErr = e;
-        }
-        return r;
-    };
-    auto* dK1 = (orb_keypoint*)put(hk1.data(), (size_t)n1 * sizeof(orb_keypoint));
-    auto* dK2 = (orb_keypoint*)put(hk2.data(), (size_t)n2 * sizeof(orb_keypoint));
-    auto* dD1 = (uint8_t*)put(kf1->desc, (size_t)n1 * 32);
-    auto* dD2 = (uint8_t*)put(kf2->desc, (size_t)n2 * 32);
-    auto* dU1 = (float*)put(kf1->uright, kf1->uright ? (size_t)n1 * 4 : 0);
-    auto* dU2 = (float*)put(kf2->uright, kf2->uright ? (size_t)n2 * 4 : 0);
-    auto* dM1 = (uint8_t*)put(has_mp1, (size_t)n1);
-    auto* dM2 = (uint8_t*)put(has_mp2, (size_t)n2);
-    auto* dN = (int4*)put(common.data(), common.size() * 16);
-    auto* dI1 = (int32_t*)put(fidx1, (size_t)L1 * 4);
-    auto* dI2 = (int32_t*)put(fidx2, (size_t)L2 * 4);
-    auto* dMt = (int32_t*)put(matches12, (size_t)n1 * 4);
-    auto* dNm = (int32_t*)put(nullptr, 4);
-    if (cpErr != hipSuccess) return ORB_EGPU;
+    Staging sg(hsc);   // one H2D of every input, one D2H of the matches and their count
+    auto* dK1 = (orb_keypoint*)sg.in(hk1.data(), (size_t)n1 * sizeof(orb_keypoint));
+    auto* dK2 = (orb_keypoint*)sg.in(hk2.data(), (size_t)n2 * sizeof(orb_keypoint));
+    auto* dD1 = (uint8_t*)sg.in(kf1->desc, (size_t)n1 * 32);
+    auto* dD2 = (uint8_t*)sg.in(kf2->desc, (size_t)n2 * 32);
+    auto* dU1 = (float*)sg.in(kf1->uright, kf1->uright ? (size_t)n1 * 4 : 0);
+    auto* dU2 = (float*)sg.in(kf2->uright, kf2->uright ? (size_t)n2 * 4 : 0);
+    auto* dM1 = (uint8_t*)sg.in(has_mp1, (size_t)n1);
+    auto* dM2 = (uint8_t*)sg.in(has_mp2, (size_t)n2);
+    auto* dN = (int4*)sg.in(common.data(), common.size() * 16);
+    auto* dI1 = (int32_t*)sg.in(fidx1, (size_t)L1 * 4);
+    auto* dI2 = (int32_t*)sg.in(fidx2, (size_t)L2 * 4);
+    auto* dMt = (int32_t*)sg.in(matches12, (size_t)n1 * 4);
+    auto* dNm = (int32_t*)sg.out(4);
+    if (int e_ = sg.upload(s)) return e_;
     hipLaunchKernelGGL(k_sft, dim3((unsigned)common.size()), dim3(64), 0, s, dK1, dD1, kf1->uright ? dU1 : nullptr, dM1,
                        dK2, dD2, kf2->uright ? dU2 : nullptr, dM2, dN, dI1, dI2, P, dMt);
     hipLaunchKernelGGL(k_sft_rot, dim3(1), dim3(256), 0, s, dK1, dK2, n1, check_ori ? 1 : 0, dMt, dNm);
     int rc = hipGetLastError() == hipSuccess ? ORB_OK : ORB_EGPU;
     int nm = 0;
     if (rc == ORB_OK) {
-        ORB_HIP_TRY(hipMemcpyAsync(matches12, dMt, (size_t)n1 * 4, hipMemcpyDeviceToHost, s));
-        ORB_HIP_TRY(hipMemcpyAsync(&nm, dNm, 4, hipMemcpyDeviceToHost, s));
-        if (hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
+        rc = sg.download(s, dMt);
+        if (rc == ORB_OK && hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
+        if (rc == ORB_OK) {
+            std::memcpy(matches12, sg.host(dMt), (size_t)n1 * 4);
+            nm = *sg.host(dNm);
+        }
     }
     return rc == ORB_OK ? nm : rc;
 } ORB_ABI_CATCH
@@ -2447,43 +2416,34 @@ static int search_by_bow(int device, const orb_frame_view* v1, const uint8_t* ok
                        al((size_t)n1 * 32 + 1) + al((size_t)n2 * 32 + 1) + al((size_t)n1 + 1) + al((size_t)n2 + 1) +
                        al(common.size() * 16 + 1) + al((size_t)L1 * 4 + 1) + al((size_t)L2 * 4 + 1) +
                        al((size_t)n1 * 4 + 1) + al(4 + 1) + 4096;
-    char* base = nullptr;
     HostScratch* hsc = nullptr;
     if (int e_ = host_scratch(device, tot, &hsc)) return e_;
-    base = hsc->base;
     hipStream_t s = hsc->stream;
-    char* c = base;
-    hipError_t cpErr = hipSuccess;   // first failed upload, checked before the launch
-    auto put = [&](const void* src, size_t bytes) {
-        char* r = c;
-        c += al(bytes + 1);
-        if (src && bytes) {
-            const hipError_t e = hipMemcpyAsync(r, src, bytes, hipMemcpyHostToDevice, s);
-            if (e != hipSuccess && cpErr == hipSuccess) cpErr = e;
-        }
-        return r;
-    };
-    auto* dK1 = (orb_keypoint*)put(hk1.data(), (size_t)n1 * sizeof(orb_keypoint));
-    auto* dK2 = (orb_keypoint*)put(hk2.data(), (size_t)n2 * sizeof(orb_keypoint));
-    auto* dD1 = (uint8_t*)put(v1->desc, (size_t)n1 * 32);
-    auto* dD2 = (uint8_t*)put(v2->desc, (size_t)n2 * 32);
-    auto* dO1 = (uint8_t*)put(ok1, (size_t)n1);
-    auto* dO2 = (uint8_t*)put(ok2, ok2 ? (size_t)n2 : 0);
-    auto* dN = (int4*)put(common.data(), common.size() * 16);
-    auto* dI1 = (int32_t*)put(fidx1, (size_t)L1 * 4);
-    auto* dI2 = (int32_t*)put(fidx2, (size_t)L2 * 4);
-    auto* dMt = (int32_t*)put(matches12, (size_t)n1 * 4);
-    auto* dNm = (int32_t*)put(nullptr, 4);
-    if (cpErr != hipSuccess) return ORB_EGPU;
+    Staging sg(hsc);   // one H2D of every input, one D2H of the matches and their count
+    auto* dK1 = (orb_keypoint*)sg.in(hk1.data(), (size_t)n1 * sizeof(orb_keypoint));
+    auto* dK2 = (orb_keypoint*)sg.in(hk2.data(), (size_t)n2 * sizeof(orb_keypoint));
+    auto* dD1 = (uint8_t*)sg.in(v1->desc, (size_t)n1 * 32);
+    auto* dD2 = (uint8_t*)sg.in(v2->desc, (size_t)n2 * 32);
+    auto* dO1 = (uint8_t*)sg.in(ok1, (size_t)n1);
+    auto* dO2 = (uint8_t*)sg.in(ok2, ok2 ? (size_t)n2 : 0);
+    auto* dN = (int4*)sg.in(common.data(), common.size() * 16);
+    auto* dI1 = (int32_t*)sg.in(fidx1, (size_t)L1 * 4);
+    auto* dI2 = (int32_t*)sg.in(fidx2, (size_t)L2 * 4);
+    auto* dMt = (int32_t*)sg.in(matches12, (size_t)n1 * 4);
+    auto* dNm = (int32_t*)sg.out(4);
+    if (int e_ = sg.upload(s)) return e_;
     hipLaunchKernelGGL(k_sbb, dim3((unsigned)common.size()), dim3(64), 0, s, dD1, dO1, dD2, ok2 ? dO2 : nullptr, dN,
                        dI1, dI2, thIncl, ratio, dMt);
     hipLaunchKernelGGL(k_sft_rot, dim3(1), dim3(256), 0, s, dK1, dK2, n1, check_ori ? 1 : 0, dMt, dNm);
     int rc = hipGetLastError() == hipSuccess ? ORB_OK : ORB_EGPU;
     int nm = 0;
     if (rc == ORB_OK) {
-        ORB_HIP_TRY(hipMemcpyAsync(matches12, dMt, (size_t)n1 * 4, hipMemcpyDeviceToHost, s));
-        ORB_HIP_TRY(hipMemcpyAsync(&nm, dNm, 4, hipMemcpyDeviceToHost, s));
-        if (hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
+        rc = sg.download(s, dMt);
+        if (rc == ORB_OK && hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
+        if (rc == ORB_OK) {
+            std::memcpy(matches12, sg.host(dMt), (size_t)n1 * 4);
+            nm = *sg.host(dNm);
+        }
     }
     return rc == ORB_OK ? nm : rc;
 }

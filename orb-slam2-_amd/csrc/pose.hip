@@ -374,47 +374,38 @@ int pose_optimize_batch(int device, const pose_batch* p, pose_batch_result* r, i
     const size_t szIn = (size_t)B * (4 + 3 + 5) * 8 + (size_t)(B + 1) * 4 + (size_t)E * 7 * 8;
     const size_t szOut = (size_t)B * 7 * 8 + (size_t)B * 4 + (size_t)B * 5 * 4 + (size_t)E;
     const size_t szWork = (size_t)E * 3 * 8 + 2 * (size_t)E;
-    char* base = nullptr;
     HostScratch* hsc = nullptr;
-    if (int e_ = host_scratch(device, szIn + szOut + szWork + 1024, &hsc)) return e_;
-    base = hsc->base;
+    if (int e_ = host_scratch(device, szIn + szOut + szWork + 16 * 256, &hsc)) return e_;
     hipStream_t s = hsc->stream;
-    char* cur = base;
-    auto take = [&](size_t bytes) { char* r0 = cur; cur += (bytes + 15) & ~(size_t)15; return r0; };
+    Staging sg(hsc);   // one H2D of the batch, one D2H of the results
     pose_batch dp = *p;
-    hipError_t cpErr = hipSuccess;   // first failed upload, checked before the launch
-    auto up = [&](const void* src, size_t bytes) -> const void* {
-        char* dst = take(bytes);
-        if (bytes) {
-            const hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
-            if (e != hipSuccess && cpErr == hipSuccess) cpErr = e;
-        }
-        return dst;
-    };
-    dp.pose_q = (const double*)up(p->pose_q, (size_t)B * 32);
-    dp.pose_t = (const double*)up(p->pose_t, (size_t)B * 24);
-    dp.cam = (const double*)up(p->cam, (size_t)B * 40);
-    dp.edge_start = (const int32_t*)up(p->edge_start, (size_t)(B + 1) * 4);
-    dp.edge_obs = (const double*)up(p->edge_obs, (size_t)E * 24);
-    dp.edge_xw = (const double*)up(p->edge_xw, (size_t)E * 24);
-    dp.edge_info = (const double*)up(p->edge_info, (size_t)E * 8);
+    dp.pose_q = (const double*)sg.in(p->pose_q, (size_t)B * 32);
+    dp.pose_t = (const double*)sg.in(p->pose_t, (size_t)B * 24);
+    dp.cam = (const double*)sg.in(p->cam, (size_t)B * 40);
+    dp.edge_start = (const int32_t*)sg.in(p->edge_start, (size_t)(B + 1) * 4);
+    dp.edge_obs = (const double*)sg.in(p->edge_obs, (size_t)E * 24);
+    dp.edge_xw = (const double*)sg.in(p->edge_xw, (size_t)E * 24);
+    dp.edge_info = (const double*)sg.in(p->edge_info, (size_t)E * 8);
+    if (int e_ = sg.upload(s)) return e_;
+    double* dWork = (double*)sg.out((size_t)E * 24 + 8);
+    uint8_t* dFlags = (uint8_t*)sg.out(2 * (size_t)E + 2);
     pose_batch_result dr;
-    dr.pose_q = (double*)take((size_t)B * 32);
-    dr.pose_t = (double*)take((size_t)B * 24);
-    dr.n_inliers = (int32_t*)take((size_t)B * 4);
-    dr.outlier = (uint8_t*)take((size_t)E + 1);
-    int32_t* dIters = (int32_t*)take((size_t)B * 20);
-    double* dWork = (double*)take((size_t)E * 24 + 8);
-    uint8_t* dFlags = (uint8_t*)take(2 * (size_t)E + 2);
-    if (cpErr != hipSuccess) return ORB_EGPU;
+    dr.pose_q = (double*)sg.out((size_t)B * 32);
+    dr.pose_t = (double*)sg.out((size_t)B * 24);
+    dr.n_inliers = (int32_t*)sg.out((size_t)B * 4);
+    dr.outlier = (uint8_t*)sg.out((size_t)E + 1);
+    int32_t* dIters = (int32_t*)sg.out((size_t)B * 20);
     int rc = pose_optimize_batch_device(&dp, &dr, dWork, dFlags, dIters, s);
     if (rc == ORB_OK) {
-        ORB_HIP_TRY(hipMemcpyAsync(r->pose_q, dr.pose_q, (size_t)B * 32, hipMemcpyDeviceToHost, s));
-        ORB_HIP_TRY(hipMemcpyAsync(r->pose_t, dr.pose_t, (size_t)B * 24, hipMemcpyDeviceToHost, s));
-        ORB_HIP_TRY(hipMemcpyAsync(r->n_inliers, dr.n_inliers, (size_t)B * 4, hipMemcpyDeviceToHost, s));
-        if (E) ORB_HIP_TRY(hipMemcpyAsync(r->outlier, dr.outlier, (size_t)E, hipMemcpyDeviceToHost, s));
-        if (iters) ORB_HIP_TRY(hipMemcpyAsync(iters, dIters, (size_t)B * 20, hipMemcpyDeviceToHost, s));
-        if (hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
+        rc = sg.download(s, dr.pose_q);
+        if (rc == ORB_OK && hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
+        if (rc == ORB_OK) {
+            std::memcpy(r->pose_q, sg.host(dr.pose_q), (size_t)B * 32);
+            std::memcpy(r->pose_t, sg.host(dr.pose_t), (size_t)B * 24);
+            std::memcpy(r->n_inliers, sg.host(dr.n_inliers), (size_t)B * 4);
+            if (E) std::memcpy(r->outlier, sg.host(dr.outlier), (size_t)E);
+            if (iters) std::memcpy(iters, sg.host(dIters), (size_t)B * 20);
+        }
     }
     return rc;
 } ORB_ABI_CATCH

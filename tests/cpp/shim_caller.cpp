@@ -19,13 +19,18 @@
 //   shim_caller sbps IN OUT      ORBmatcher::SearchByProjection(pKF, Scw, vpPoints, vpMatched, th)
 //   shim_caller sbs IN OUT       ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th)
 //   shim_caller fuses IN OUT     ORBmatcher::Fuse(pKF, Scw, vpPoints, th, vpReplacePoint)
+//   shim_caller timeit REPS lba IN   per-call wall time of Optimizer::LocalBundleAdjustment through the
+//                                shim (graph gather + solve + write-back, the mock map rebuilt from IN
+//                                before each call and not timed): prints "median_us N min_us M"
 //   shim_caller threads IN OUT   the SURVEY 8b threading contract: two Extractor handles on two host
 //                                threads at once (stereo L/R, R/src/Frame.cpp:86-89), SearchForInitialization
 //                                and PoseOptimization on a third and fourth (Tracking), LocalBundleAdjustment
 //                                on a fifth (LocalMapping), each repeated; results must not change
 // IN / OUT: little-endian arrays, each written as int64 element count + raw elements.
 // Exit status: 0 ok, 3 the library reported an error (e.g. no gfx950 device), 2 bad usage.
+#include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -383,6 +388,8 @@ static void run_sbl(FILE* in, FILE* out) {
     wr(out, read_slots(F, ptr, withObs, noObs));
 }
 
+static double g_call_us = 0.0;   // wall time of the last timed shim call (timeit mode)
+
 static void run_lba(FILE* in, FILE* out, bool group) {
     mock::g_erase_log.clear();
     const auto Tcw = rd<float>(in);
@@ -432,10 +439,12 @@ static void run_lba(FILE* in, FILE* out, bool group) {
     mock::Map map;
     bool stop = stopFlag[0] != 0;
     orbslam2_amd::LbaDump D;
+    const auto t0 = std::chrono::steady_clock::now();
     if (group)   // the multi-GPU overload: landmarks sharded over the listed devices
         orbslam2_amd::LocalBundleAdjustment(pKF, &stop, &map, std::vector<int>(devices.begin(), devices.end()), &D);
     else
         orbslam2_amd::LocalBundleAdjustment(pKF, &stop, &map, &D);
+    g_call_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
     wr(out, D.pose_q); wr(out, D.pose_t); wr(out, D.pose_fixed); wr(out, D.pose_id);
     wr(out, D.point_xyz); wr(out, D.point_id); wr(out, D.point_bad);
     wr(out, D.edge_point); wr(out, D.edge_pose); wr(out, D.edge_stereo); wr(out, D.edge_obs); wr(out, D.edge_info);
@@ -957,7 +966,39 @@ static int run_threads(int argc, char** argv) {
     return rc;
 }
 
+// timeit REPS MODE IN: the mode REPS times (after 3 untimed calls), output discarded; the median and
+// minimum of the per-call times the mode recorded
+static int run_timeit(int argc, char** argv) {
+    if (argc != 5) return 2;
+    const int reps = std::atoi(argv[2]);
+    const std::string mode = argv[3];
+    std::vector<double> ts;
+    for (int r = 0; r < reps + 3; r++) {
+        FILE* in = std::fopen(argv[4], "rb");
+        char* buf = nullptr;
+        size_t len = 0;
+        FILE* mem = open_memstream(&buf, &len);
+        if (!in || !mem) return 2;
+        g_call_us = -1.0;
+        try {
+            if (!run_mode(mode, in, mem)) return 2;
+        } catch (const std::exception& e) {
+            std::fprintf(stderr, "%s\n", e.what());
+            return 3;
+        }
+        std::fclose(in);
+        std::fclose(mem);
+        std::free(buf);
+        if (g_call_us < 0) return 2;   // the mode records no call time
+        if (r >= 3) ts.push_back(g_call_us);
+    }
+    std::sort(ts.begin(), ts.end());
+    std::printf("median_us %.1f min_us %.1f\n", ts[ts.size() / 2], ts[0]);
+    return 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc >= 2 && std::string(argv[1]) == "timeit") return run_timeit(argc, argv);
     if (argc >= 6 && std::string(argv[1]) == "threads") return run_threads(argc, argv);
     if (argc != 4) {
         std::fprintf(stderr, "usage: %s extract|sfi|sbp|sbl|lba|lbag|pose|stereo|fuse|sft|sbbf|sbbk|sbpk|sbps|sbs|fuses IN OUT\n"
