@@ -1060,14 +1060,25 @@ __device__ __forceinline__ void octree_run(const Geom& g, const LevelGeom& L, in
         sc[0] = idx;
     }
     __syncthreads();
-    for (int k = tid; k < n; k += OT_T) nid[k] = (uint32_t)S.newpos[min((int)((float)kx_of(kA[k]) / hX), nIni - 1)];
+    // keys k = v * OT_T + tid, v < KV (2,048: most levels' every key) keep the key and its node index
+    // in registers for the whole distribution (keys never move): a pass touches memory only for the
+    // keys beyond them, where nid / kA live in LDS or, for batches, HBM (L2)
+    constexpr int KV = 8;
+    uint32_t keyr[KV];
+    int nidr[KV];
+#pragma unroll
+    for (int v = 0; v < KV; v++) {
+        const int k = v * OT_T + tid;
+        keyr[v] = k < n ? (uint32_t)kA[k] : 0u;
+        nidr[v] = k < n ? S.newpos[min((int)((float)kx_of(keyr[v]) / hX), nIni - 1)] : 0;
+    }
+    for (int k = KV * OT_T + tid; k < n; k += OT_T) nid[k] = (uint32_t)S.newpos[min((int)((float)kx_of(kA[k]) / hX), nIni - 1)];
     TSTAMP(t_init);
     int m = sc[0];   // list size (uniform)
     __syncthreads();
     int cur = 0;     // table holding the current list
     int phase = 0;   // 0 = breadth-wise passes, 1 = size-ordered passes
     int nIter = 0;
-    constexpr int KV = 8;   // keys per thread whose (node, quadrant) stay in registers across a pass
     while (true) {
         if (++nIter > 4096) { if (tid == 0) atomicOr(status, 4); break; }
         const NodeTab O = C_.tab(cur);
@@ -1088,13 +1099,13 @@ __device__ __forceinline__ void octree_run(const Geom& g, const LevelGeom& L, in
             const int k = v * OT_T + tid;
             ndr[v] = 0;
             if (k < n) {
-                const int nd = (int)nid[k];
+                const int nd = nidr[v];
                 ndr[v] = nd;
                 const bool act = phase == 0 ? (O.cnt[nd] > 1) : ((O.flag[nd] & 2) != 0);
                 if (act) {
                     int mx, my;
                     node_split(O.b0[nd], O.b1[nd], mx, my);
-                    const int q = key_quadrant(kA[k], mx, my);
+                    const int q = key_quadrant(keyr[v], mx, my);
                     qr |= ((uint32_t)q << (2 * v)) | (1u << (16 + v));
                     atomicAdd(reinterpret_cast<unsigned*>(&S.qc[nd]) + q, 1u);
                 }
@@ -1241,7 +1252,7 @@ __device__ __forceinline__ void octree_run(const Geom& g, const LevelGeom& L, in
                 } else {
                     nn = S.newpos[nd];
                 }
-                nid[k] = (uint32_t)nn;
+                nidr[v] = nn;
             }
         }
         for (int k = KV * OT_T + tid; k < n; k += OT_T) {
@@ -1274,7 +1285,15 @@ __device__ __forceinline__ void octree_run(const Geom& g, const LevelGeom& L, in
     // retain the best point in each node (first max wins, R/src/ORBextractor.cpp:796-814)
     for (int i = tid; i < m; i += OT_T) best[i] = 0ull;
     __syncthreads();
-    for (int k = tid; k < n; k += OT_T) {
+#pragma unroll
+    for (int v = 0; v < KV; v++) {
+        const int k = v * OT_T + tid;
+        if (k < n) {
+            const unsigned long long bv = ((unsigned long long)kr_of(keyr[v]) << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)k);
+            __hip_atomic_fetch_max(&best[nidr[v]], bv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+    for (int k = KV * OT_T + tid; k < n; k += OT_T) {
         const unsigned long long v = ((unsigned long long)kr_of(kA[k]) << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)k);
         __hip_atomic_fetch_max(&best[(int)nid[k]], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }

@@ -1,13 +1,29 @@
-// VALU issue rate vs waves per SIMD: every lane runs 8 independent v_fma_f32
-// chains (or v_pk_fma_f32 / v_xad_u32 chains), k workgroups of 256 threads per CU = k waves per
-// SIMD.  Each workgroup's wave 0 stamps s_memtime (shader clock) and s_memrealtime (100 MHz
-// constant) around its loop, so the run reports the clock the SIMDs actually ran at and the
-// cycles per wave64 instruction per SIMD, next to MI355X_MICROARCH.md's "2 cycles (SIMD-32),
-// one wave alone 4".  Usage: valu_issue [iters]
+// VALU issue rate per instruction kind vs waves per SIMD: every lane
+// runs 8 independent chains of ONE instruction (inline asm, so exactly that instruction), k
+// workgroups of 256 threads per CU = k waves per SIMD.  Each workgroup's wave 0 stamps s_memtime
+// (shader clock) and s_memrealtime (100 MHz constant) at its start and end and reads HW_ID (the CU
+// it ran on), so the run can check what the wall clock alone cannot:
+//   * co-residency: per CU, the largest number of its workgroups whose [start, end] overlap at one
+//     instant (k means all k ran together);
+//   * the all-running window [max start, min end] over every workgroup of the launch: inside it
+//     every workgroup runs, so the chip's rate there is the sum of the workgroups' own rates
+//     (instructions / their own loop time) — the steady-state issue rate without dispatch ramp and
+//     tail;
+//   * the wall-clock rate (instructions / event time) beside it; the two agree when the kernel is
+//     long enough and the workgroups are co-resident.
+// The ops are the extraction kernels' integer mix (v_perm, v_alignbyte, v_lerp_u8, v_dot4_u32_u8,
+// v_bcnt, v_pk_minimum3_f16, v_xad_u32) and the f32 references (v_fma_f32, v_pk_fma_f32).
+// Usage: valu_issue [iters]   (default 65536: ~8x round 4's loop, >= 4 ms per launch at 8 waves/SIMD)
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
+
+constexpr int kOps = 9;
+static const char* kNames[kOps] = {"v_fma_f32",      "v_pk_fma_f32",  "v_xad_u32",       "v_perm_b32",        "v_alignbyte_b32",
+                                   "v_lerp_u8",      "v_dot4_u32_u8", "v_bcnt_u32_b32",  "v_pk_minimum3_f16"};
 
 template <int OP>
 __global__ __launch_bounds__(256) void k_issue(const float* in, float* out, unsigned long long* stamps, int iters) {
@@ -20,26 +36,40 @@ __global__ __launch_bounds__(256) void k_issue(const float* in, float* out, unsi
     for (int k = 0; k < 8; k++) {
         a[k] = in[(t + k) & 1023];
         p[k] = f2{a[k], a[k] + 1.0f};
-        u[k] = __float_as_uint(a[k]);
+        u[k] = __float_as_uint(a[k]) + k;
     }
     const float c = in[1000], d = in[1001];
     const f2 pc = {c, c}, pd = {d, d};
-    const unsigned uc = __float_as_uint(c), ud = __float_as_uint(d);
+    const unsigned uc = __float_as_uint(c), ud = __float_as_uint(d) | 0x0c0c0c0cu;
     unsigned long long t0 = 0, r0 = 0;
-    if (threadIdx.x == 0) { t0 = __builtin_amdgcn_s_memtime(); r0 = __builtin_amdgcn_s_memrealtime(); }
+    if (threadIdx.x == 0) {
+        t0 = __builtin_amdgcn_s_memtime();
+        r0 = __builtin_amdgcn_s_memrealtime();
+    }
     for (int i = 0; i < iters; i++) {
 #pragma unroll
         for (int k = 0; k < 8; k++) {
-            // inline asm: exactly one instruction of the measured kind per step (the compiler would
-            // otherwise SLP-pack the f32 chains or split the xad)
             if (OP == 0) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(a[k]) : "v"(c), "v"(d));
             if (OP == 1) asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(p[k]) : "v"(pc), "v"(pd));
             if (OP == 2) asm volatile("v_xad_u32 %0, %0, %1, %2" : "+v"(u[k]) : "v"(uc), "v"(ud));
+            if (OP == 3) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(u[k]) : "v"(uc), "v"(ud));
+            if (OP == 4) asm volatile("v_alignbyte_b32 %0, %0, %1, %2" : "+v"(u[k]) : "v"(uc), "v"(ud));
+            if (OP == 5) asm volatile("v_lerp_u8 %0, %0, %1, %2" : "+v"(u[k]) : "v"(uc), "v"(ud));
+            if (OP == 6) asm volatile("v_dot4_u32_u8 %0, %0, %1, %2" : "+v"(u[k]) : "v"(uc), "v"(ud));
+            if (OP == 7) asm volatile("v_bcnt_u32_b32 %0, %0, %1" : "+v"(u[k]) : "v"(uc));
+            if (OP == 8) asm volatile("v_pk_minimum3_f16 %0, %0, %1, %2" : "+v"(u[k]) : "v"(uc), "v"(ud));
         }
     }
     if (threadIdx.x == 0) {
-        stamps[4 * blockIdx.x + 0] = __builtin_amdgcn_s_memtime() - t0;
-        stamps[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - r0;
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        unsigned hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        stamps[6 * blockIdx.x + 0] = t0;
+        stamps[6 * blockIdx.x + 1] = t1;
+        stamps[6 * blockIdx.x + 2] = r0;
+        stamps[6 * blockIdx.x + 3] = r1;
+        stamps[6 * blockIdx.x + 4] = hw;
+        stamps[6 * blockIdx.x + 5] = 0;
     }
     float s = 0.f;
 #pragma unroll
@@ -47,51 +77,92 @@ __global__ __launch_bounds__(256) void k_issue(const float* in, float* out, unsi
     out[t] = s;
 }
 
+typedef void (*KFn)(const float*, float*, unsigned long long*, int);
+static KFn kfn(int op) {
+    switch (op) {
+        case 0: return k_issue<0>;
+        case 1: return k_issue<1>;
+        case 2: return k_issue<2>;
+        case 3: return k_issue<3>;
+        case 4: return k_issue<4>;
+        case 5: return k_issue<5>;
+        case 6: return k_issue<6>;
+        case 7: return k_issue<7>;
+        default: return k_issue<8>;
+    }
+}
+
 int main(int argc, char** argv) {
-    const int iters = argc > 1 ? std::atoi(argv[1]) : 8192;
+    const int iters = argc > 1 ? std::atoi(argv[1]) : 65536;
     int cus = 0;
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
     float *in, *out;
     unsigned long long* st;
-    hipMalloc(&in, 4096 * 4);
-    hipMalloc(&out, (size_t)cus * 8 * 256 * 4);
-    hipMalloc(&st, (size_t)cus * 8 * 4 * 8);
+    (void)hipMalloc(&in, 4096 * 4);
+    (void)hipMalloc(&out, (size_t)cus * 8 * 256 * 4);
+    (void)hipMalloc(&st, (size_t)cus * 8 * 6 * 8);
     std::vector<float> h(4096, 1.0f);
     h[1000] = 0.999f;
     h[1001] = 0.001f;
-    hipMemcpy(in, h.data(), 4096 * 4, hipMemcpyHostToDevice);
+    (void)hipMemcpy(in, h.data(), 4096 * 4, hipMemcpyHostToDevice);
     hipEvent_t e0, e1;
-    hipEventCreate(&e0);
-    hipEventCreate(&e1);
-    const char* names[] = {"v_fma_f32", "v_pk_fma_f32", "v_xad_u32"};
-    printf("CUs %d, iters %d, 8 independent chains per lane\n", cus, iters);
-    printf("%-13s %5s %10s %12s %10s %14s %12s\n", "op", "w/SIMD", "ms", "wave-inst/s", "clock GHz", "cyc/inst/SIMD",
-           "lane-ops/s");
-    for (int op = 0; op < 3; op++)
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    std::printf("CUs %d, iters %d, 8 independent chains per lane; rates in wave64 instructions\n", cus, iters);
+    std::printf("%-18s %3s %8s %7s %9s | %9s %9s %6s | %11s %11s %6s | %12s %12s\n", "op", "w/S", "wall ms", "GHz",
+                "coresid", "win ms", "loop ms", "win%", "wall inst/s", "win inst/s", "ratio", "cyc/inst/SIMD",
+                "lane-ops/s");
+    for (int op = 0; op < kOps; op++)
         for (int k : {1, 2, 4, 8}) {
             const int blocks = cus * k;
             float ms = 0.f;
-            for (int rep = 0; rep < 3; rep++) {
-                hipEventRecord(e0);
-                if (op == 0) hipLaunchKernelGGL(k_issue<0>, dim3(blocks), dim3(256), 0, 0, in, out, st, iters);
-                if (op == 1) hipLaunchKernelGGL(k_issue<1>, dim3(blocks), dim3(256), 0, 0, in, out, st, iters);
-                if (op == 2) hipLaunchKernelGGL(k_issue<2>, dim3(blocks), dim3(256), 0, 0, in, out, st, iters);
-                hipEventRecord(e1);
-                hipEventSynchronize(e1);
-                hipEventElapsedTime(&ms, e0, e1);
+            for (int rep = 0; rep < 2; rep++) {
+                (void)hipEventRecord(e0);
+                hipLaunchKernelGGL(kfn(op), dim3(blocks), dim3(256), 0, 0, in, out, st, iters);
+                (void)hipEventRecord(e1);
+                (void)hipEventSynchronize(e1);
+                (void)hipEventElapsedTime(&ms, e0, e1);
             }
-            std::vector<unsigned long long> s((size_t)blocks * 4);
-            hipMemcpy(s.data(), st, s.size() * 8, hipMemcpyDeviceToHost);
-            double cyc = 0, rt = 0;
-            for (int b = 0; b < blocks; b++) { cyc += (double)s[4 * b]; rt += (double)s[4 * b + 1]; }
-            const double ghz = cyc / (rt / 100e6) / 1e9;           // shader cycles per second of realtime
-            const double winst = (double)blocks * 4 * iters * 8;   // wave-instructions of the loop
-            const double perSimd = winst / (cus * 4.0);
-            const double loopSec = rt / blocks / 100e6;            // a workgroup's loop time (realtime)
-            const double cycPerInst = loopSec * ghz * 1e9 / perSimd;
-            const double lanes = op == 1 ? 128.0 : 64.0;           // a packed f32 instruction does two per lane
-            printf("%-13s %5d %10.3f %12.4g %10.3f %14.3f %12.4g\n", names[op], k, ms, winst / (ms * 1e-3), ghz,
-                   cycPerInst, winst * lanes / (ms * 1e-3));
+            std::vector<unsigned long long> s((size_t)blocks * 6);
+            (void)hipMemcpy(s.data(), st, s.size() * 8, hipMemcpyDeviceToHost);
+            // co-residency per CU (HW_ID: CU_ID bits 11:8, SH_ID 12, SE_ID 15:13 on gfx9; XCC from the
+            // dispatch order is not in HW_ID, so CUs are keyed by (block % 8 XCD, SE, SH, CU))
+            std::vector<std::vector<std::pair<unsigned long long, int>>> ev(8 * 256);
+            unsigned long long winStart = 0, winEnd = ~0ull;
+            double cyc = 0, rt = 0, rateSum = 0;
+            for (int b = 0; b < blocks; b++) {
+                const unsigned long long t0 = s[6 * b], t1 = s[6 * b + 1], r0 = s[6 * b + 2], r1 = s[6 * b + 3];
+                const unsigned hw = (unsigned)s[6 * b + 4];
+                const int cu = (hw >> 8) & 15, sh = (hw >> 12) & 1, se = (hw >> 13) & 7;
+                const int key = ((b % 8) * 8 + se) * 32 + sh * 16 + cu;
+                ev[(size_t)key % ev.size()].push_back({r0, +1});
+                ev[(size_t)key % ev.size()].push_back({r1, -1});
+                winStart = std::max(winStart, r0);
+                winEnd = std::min(winEnd, r1);
+                cyc += (double)(t1 - t0);
+                rt += (double)(r1 - r0);
+                rateSum += 4.0 * iters * 8 / ((double)(r1 - r0) / 100e6);   // this workgroup's wave-inst/s
+            }
+            int minPeak = 1 << 30, used = 0;
+            for (auto& e : ev) {
+                if (e.empty()) continue;
+                std::sort(e.begin(), e.end(), [](auto& x, auto& y) { return x.first != y.first ? x.first < y.first : x.second < y.second; });
+                int cur = 0, peak = 0;
+                for (auto& x : e) { cur += x.second; peak = std::max(peak, cur); }
+                minPeak = std::min(minPeak, peak);
+                used++;
+            }
+            const double ghz = cyc / (rt / 100e6) / 1e9;
+            const double winst = (double)blocks * 4 * iters * 8;
+            const double wallRate = winst / (ms * 1e-3);
+            const double winMs = winEnd > winStart ? (double)(winEnd - winStart) / 1e5 : 0.0;
+            const double loopMs = rt / blocks / 1e5;
+            const double winRate = winEnd > winStart ? rateSum : 0.0;   // every workgroup runs inside the window
+            const double cycPerInst = winRate > 0 ? cus * 4.0 * ghz * 1e9 / winRate : 0.0;
+            const double lanes = op == 1 ? 128.0 : 64.0;
+            std::printf("%-18s %3d %8.3f %7.3f %4d/%-4d | %9.3f %9.3f %5.1f%% | %11.4g %11.4g %6.3f | %12.3f %12.4g\n",
+                        kNames[op], k, ms, ghz, minPeak, used, winMs, loopMs, 100.0 * winMs / ms, wallRate, winRate,
+                        winRate > 0 ? wallRate / winRate : 0.0, cycPerInst, winRate * lanes);
         }
     return 0;
 }
