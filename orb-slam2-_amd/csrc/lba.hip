@@ -2044,6 +2044,410 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_solve(const double* __restrict__
 }
 
 
+// ------------------------------------------------------------------ reduced camera solve, dataflow form
+// k_ldlt_df: the same blocked right-looking LDL^T with the forward substitution folded in, and the same
+// backward substitution, as k_ldlt_solve<true> (S in LDS, even n, np <= 128), organised so the 16-column
+// pivot chain is the only sequential work and no workgroup barrier sits between panels:
+//  * wave 0 (PivotCols) factors every panel's 16 x 16 diagonal block E (the current Schur complement,
+//    both triangles) with lane (k, q) = k + 16 q holding column k, rows q, q+4, q+8, q+12.  Column c:
+//    u(k) = E(c, k) / d_c for k > c (0 otherwise) is L(k, c) and every lane takes X -= E(row, c) u(k),
+//    E(., c) broadcast within its 16-lane row by v_mov_b64_dpp row_newbcast (no v_readlane: ~24 cycles
+//    of issue each, profiles/r03_lat_micro.txt).  The next pivot comes one column ahead,
+//    d_{c+1} = E(c+1, c+1) - E(c+1, c)^2 / d_c from row c+1 before column c's update, so 1/d_{c+1}
+//    (v_rcp_f64 + Newton) overlaps the update; row c+1 replicated over the four lane rows comes from an
+//    LDS round trip issued a column earlier and corrected by the missing column (no cross-row
+//    permutation on the chain).  Per column the wave publishes u (16 doubles), 1/d_c and y_c/d_c, then a
+//    sequence counter, into per-panel LDS buffers (a late reader never sees them overwritten);
+//  * wave I (1..T-1) owns row block I (FollowCols): for each panel kb < I it follows the pivot's columns
+//    over its 16 rows (the same update with the published u; its y rides along), stores their W
+//    (upper triangle, the tiles' left operand) and L, then applies panel kb's trailing update to its own
+//    tiles (I, K), K = kb+1..I, with f64 MFMA (the diagonal tile last);
+//  * LDS flags (monotonic; one wave's LDS operations complete in order): rowDone[I] = kb+1 once row block
+//    I's panel-kb L is stored (the owners of lower blocks wait for it before a tile (., I)), diagReady =
+//    I once tile (I, I) holds every earlier panel's update and y of block I is stored (the pivot's input
+//    for panel I).  Waves 1 and 4 swap blocks so the pivot's SIMD partner (wave 4) owns the lightest one.
+// The elimination is the unblocked recurrence's, reassociated per panel (agreement to rounding with
+// oracle/lba_oracle.c: tests compare LM traces to 1e-9 and decisions exactly).
+template <int L>
+__device__ __forceinline__ double rbc16(double v) {   // lane L of each 16-lane row to the whole row
+    return __longlong_as_double(__builtin_amdgcn_mov_dpp(__double_as_longlong(v), 0x150 + L, 0xf, 0xf, true));
+}
+template <int R>
+__device__ __forceinline__ unsigned xrow32(unsigned v) {   // lane row R to all four rows (permlane swaps)
+    const auto a = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    const unsigned t = (R & 1) ? a[1] : a[0];
+    const auto b = __builtin_amdgcn_permlane32_swap(t, t, false, false);
+    return (R & 2) ? b[1] : b[0];
+}
+template <int R>
+__device__ __forceinline__ double xrow(double v) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    return __longlong_as_double((long long)(((unsigned long long)xrow32<R>((unsigned)(u >> 32)) << 32) |
+                                            xrow32<R>((unsigned)u)));
+}
+template <int C, int N>
+struct ColUnroll {
+    template <class F>
+    __device__ __forceinline__ static void run(F& f) {
+        f.template col<C>();
+        ColUnroll<C + 1, N>::run(f);
+    }
+};
+template <int N>
+struct ColUnroll<N, N> {
+    template <class F>
+    __device__ __forceinline__ static void run(F&) {}
+};
+template <int C, int N>
+struct ColUnrollTo {   // the last panel: columns past the order are identity padding, one uniform exit test each
+    template <class F>
+    __device__ __forceinline__ static void run(F& f, int nc) {
+        if (C >= nc) return;
+        f.template col<C>();
+        ColUnrollTo<C + 1, N>::run(f, nc);
+    }
+};
+template <int N>
+struct ColUnrollTo<N, N> {
+    template <class F>
+    __device__ __forceinline__ static void run(F&, int) {}
+};
+typedef __attribute__((address_space(3))) double lds_f64;
+typedef __attribute__((address_space(3))) int lds_i32;
+
+struct DfPivot {
+    // entering column C: X = E^(C-1), R = row C of E^(C-1) (replicated), rd = 1/d_C, Q = row C+1 of
+    // E^(C-2) (replicated), up = u_(C-1)
+    double X[4], Y, rd, R, Q, up;
+    int k, seq;
+    volatile lds_f64 *pubU, *pubRG, *sinkD, *rowbuf;
+    volatile lds_i32 *cnt, *sinkI;
+    bool qz, l0;
+    template <int C>
+    __device__ __forceinline__ void col() {
+        double P1 = 0.0, w = 0.0, rdn = 1.0;
+        if constexpr (C + 1 < kNB) {   // row C+1 of E^(C-1), then the next pivot's reciprocal
+            P1 = C == 0 ? Q : __builtin_fma(-rbc16<(C > 0 ? C - 1 : 0)>(Q), up, Q);
+            const double a = rbc16<C + 1>(P1);
+            w = rbc16<C>(P1);
+            rdn = rcp_nr(__builtin_fma(-(w * w), rd, a));
+        }
+        double Qn = 0.0;   // row C+2 of E^(C-1) through LDS, consumed at the next column's start
+        if constexpr (C + 2 < kNB) {
+            *((C + 2) % 4 == (int)(threadIdx.x & 63) >> 4 ? rowbuf + k : sinkD) = X[(C + 2) >> 2];
+            Qn = rowbuf[k];
+        }
+        const double u = R * (k > C ? rd : 0.0);
+#pragma unroll
+        for (int s = 0; s < 4; s++) X[s] = __builtin_fma(-rbc16<C>(X[s]), u, X[s]);
+        const double yc = rbc16<C>(Y);
+        Y = __builtin_fma(-u, yc, Y);
+        *(qz ? pubU + C * kNB + k : sinkD) = u;
+        *(l0 ? pubRG + 2 * C : sinkD) = rd;
+        *(l0 ? pubRG + 2 * C + 1 : sinkD) = rd * yc;
+        *(l0 ? cnt : sinkI) = seq + C + 1;
+        if constexpr (C + 1 < kNB) {
+            R = __builtin_fma(-w, u, P1);
+            rd = rdn;
+            up = u;
+            Q = Qn;
+        }
+    }
+};
+
+// kDiag: this row block is the next panel's diagonal block.  Its panel W / L go to LDS and its
+// diagonal tile takes the panel's update (one f64 MFMA per 4 columns) as the columns become final
+// (column k is frozen from column k on), so only the last MFMA is left when the loop ends and the pivot
+// waits ~1 k cycles less for the next panel.
+template <bool kDiag>
+struct DfFollow {
+    double X[4], Y[4];
+    dbl4 T;                  // kDiag: the diagonal tile, MFMA output layout
+    int k, seq, seen, jb, rb, ld;
+    const volatile lds_f64 *pubU, *pubRG;
+    const volatile lds_i32* cnt;
+    lds_f64 *A, *sinkD;
+    template <int C>
+    __device__ __forceinline__ void col() {
+        if (seen <= seq + C) {   // wave-uniform poll of the pivot's sequence counter
+            int v;
+            while ((v = __builtin_amdgcn_readfirstlane(*cnt)) <= seq + C) __builtin_amdgcn_s_sleep(1);
+            seen = v;
+        }
+        const double u = pubU[C * kNB + k];
+        const double g = pubRG[2 * C + 1];
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            const double wi = rbc16<C>(X[s]);
+            X[s] = __builtin_fma(-wi, u, X[s]);
+            Y[s] = __builtin_fma(-wi, g, Y[s]);
+        }
+        if constexpr (kDiag && (C & 3) == 3) {
+            // columns C-3..C are final: their W (upper triangle) and L (lower) out, then the tile's MFMA
+            const bool mine = k >= C - 3 && k <= C;
+            const double rdk = pubRG[2 * (k & 15)];
+            const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                const int r = rb + (lane >> 4) + 4 * s;
+                *(mine ? A + (size_t)(jb + k) * ld + r : sinkD) = X[s];
+                *(mine ? A + (size_t)r * ld + jb + k : sinkD) = X[s] * rdk;
+            }
+            const int pc = jb + (C - 3) + lk;
+            const double a = -A[(size_t)pc * ld + rb + li];
+            const double bb = A[(size_t)(rb + li) * ld + pc];
+            T = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, T, 0, 0, 0);
+        }
+    }
+};
+
+__host__ __device__ inline size_t ldlt_df_lds_bytes(int n) {
+    const int np = (n + kNB - 1) & ~(kNB - 1);
+    return 8 * ((size_t)np * (np + 1) + 2 * (size_t)np + (size_t)(np / kNB) * (kNB * kNB + 2 * kNB) + 64 + kNB + 64 + 32);
+}
+
+__global__ __launch_bounds__(kLdlT) void k_ldlt_df(const double* __restrict__ Sg, const double* __restrict__ b, int n,
+                                                  double* __restrict__ x, int* __restrict__ flags, const LmState* st,
+                                                  PoseTail ptail) {
+    if (lm_off(st, 1)) return;
+    extern __shared__ __attribute__((aligned(16))) double sh[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int np = (n + kNB - 1) & ~(kNB - 1), ld = np + 1, T = np / kNB;
+    const int k = lane & 15, q = lane >> 4;
+    double* A = sh;
+    double* rdg = A + (size_t)np * ld;
+    double* y = rdg + np;
+    double* pubU = y + np;                           // [T][16][16]
+    double* pubRG = pubU + (size_t)T * kNB * kNB;     // [T][16][2]
+    double* sinkD = pubRG + (size_t)T * 2 * kNB;      // 64 per-lane sinks
+    double* rowbuf = sinkD + 64;                      // 16
+    int* cnt = (int*)(rowbuf + kNB);
+    int* sinkI = cnt + 2;                             // 64
+    volatile lds_i32* rowDone = (volatile lds_i32*)(sinkI + 64);   // [8]
+    volatile lds_i32* diagReady = rowDone + 8;
+    __shared__ int failS;
+    if (tid == 0) { failS = 0; *cnt = 0; }
+    if (tid < 9) rowDone[tid] = 0;
+    __syncthreads();
+    // ---- staging, per owner, no barrier: the wave of row block I loads its rows' columns
+    //      [0, 16(I+1)) (its lower tiles and the whole diagonal tile) and their b, one 16-byte load per
+    //      (row, column pair), all in flight; identity padding past n (n even: no pair straddles it)
+    const __amdgpu_buffer_rsrc_t rsS = buf_rsrc(Sg, (uint32_t)n * n * 8);
+    auto stage_rows = [&](int I) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const int rbs = kNB * I, ncp = 8 * (I + 1);
+        u32x4 v[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+            const int idx = lane + 64 * u, i = rbs + (idx & 15), c2 = 2 * (idx >> 4);
+            v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsS, (idx >> 4) < ncp && i < n && c2 < n ? (i * n + c2) * 8 : kBufOob,
+                                                         0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+            const int idx = lane + 64 * u, i = rbs + (idx & 15), c2 = 2 * (idx >> 4);
+            if ((idx >> 4) < ncp) {
+                double* dst = A + (size_t)i * ld + c2;
+                dst[0] = __longlong_as_double((long long)(((unsigned long long)v[u].y << 32) | v[u].x)) +
+                         (i >= n && i == c2 ? 1.0 : 0.0);
+                dst[1] = __longlong_as_double((long long)(((unsigned long long)v[u].w << 32) | v[u].z)) +
+                         (i >= n && i == c2 + 1 ? 1.0 : 0.0);
+            }
+        }
+        if (lane < kNB) y[rbs + lane] = rbs + lane < n ? b[rbs + lane] : 0.0;
+    };
+    auto wait_ge = [&](volatile lds_i32* f, int v) {
+        while (__builtin_amdgcn_readfirstlane(*f) < v) __builtin_amdgcn_s_sleep(1);
+    };
+    auto tile = [&](int jb, int I0, int K0) {   // A(I, K) -= W(I, panel) L(K, panel)^T, four f64 MFMA
+        const int li = lane & 15, lk = lane >> 4;
+        double a[kNB / 4], bb[kNB / 4];
+        dbl4 acc;
+#pragma unroll
+        for (int s = 0; s < kNB / 4; s++) {
+            const int p = jb + 4 * s + lk;
+            a[s] = -A[(size_t)p * ld + I0 + li];
+            bb[s] = A[(size_t)(K0 + li) * ld + p];
+        }
+#pragma unroll
+        for (int s = 0; s < 4; s++) acc[s] = A[(size_t)(I0 + lk + 4 * s) * ld + K0 + li];
+#pragma unroll
+        for (int s = 0; s < kNB / 4; s++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], bb[s], acc, 0, 0, 0);
+#pragma unroll
+        for (int s = 0; s < 4; s++) A[(size_t)(I0 + lk + 4 * s) * ld + K0 + li] = acc[s];
+    };
+    if (wave == 0) {
+        stage_rows(0);
+        for (int kb = 0; kb < T; kb++) {
+            const int jb = kb * kNB;
+            if (kb > 0) wait_ge(diagReady, kb);
+            DfPivot P;
+            P.k = k;
+            P.seq = kNB * kb;
+            P.pubU = (volatile lds_f64*)(pubU + (size_t)kb * kNB * kNB);
+            P.pubRG = (volatile lds_f64*)(pubRG + (size_t)kb * 2 * kNB);
+            P.sinkD = (volatile lds_f64*)(sinkD + lane);
+            P.rowbuf = (volatile lds_f64*)rowbuf;
+            P.cnt = (volatile lds_i32*)cnt;
+            P.sinkI = (volatile lds_i32*)(sinkI + lane);
+            P.qz = q == 0;
+            P.l0 = lane == 0;
+#pragma unroll
+            for (int s = 0; s < 4; s++) P.X[s] = A[(size_t)(jb + q + 4 * s) * ld + jb + k];
+            P.Y = y[jb + k];
+            P.R = xrow<0>(P.X[0]);
+            P.Q = xrow<1>(P.X[0]);
+            P.up = 0.0;
+            P.rd = rcp_nr(rbc16<0>(P.R));
+            const int nc = n - jb;
+            if (nc >= kNB) ColUnroll<0, kNB>::run(P);
+            else ColUnrollTo<0, kNB>::run(P, nc);
+            // the diagonal block's L (strict lower), 1/d and its finished y; a zero or non-finite pivot
+            // (1/d zero or non-finite) flags the solve
+            const double rdk = jb + k < n ? pubRG[(size_t)kb * 2 * kNB + 2 * k] : 1.0;
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                const int i = q + 4 * s;
+                *(i > k ? A + (size_t)(jb + i) * ld + jb + k : sinkD + lane) = P.X[s] * rdk;
+            }
+            if (q == 0) { rdg[jb + k] = rdk; y[jb + k] = P.Y; }
+            const bool bad = !(rdk != 0.0 && isfinite(rdk));
+            if (__builtin_amdgcn_ballot_w64(bad) != 0 && lane == 0) failS = 1;
+        }
+    } else if (wave < T) {
+        const int I = wave == 4 ? 1 : (wave == 1 && T > 4) ? 4 : wave, rb = kNB * I;
+        stage_rows(I);
+        double Yr[4];
+#pragma unroll
+        for (int s = 0; s < 4; s++) Yr[s] = y[rb + q + 4 * s];
+        int seen = 0;
+        for (int kb = 0; kb < I; kb++) {
+            const int jb = kb * kNB;
+            const bool diagNext = kb == I - 1;
+            auto follow = [&](auto& F) {
+                F.k = k;
+                F.seq = kNB * kb;
+                F.seen = seen;
+                F.jb = jb;
+                F.rb = rb;
+                F.ld = ld;
+                F.pubU = (const volatile lds_f64*)(pubU + (size_t)kb * kNB * kNB);
+                F.pubRG = (const volatile lds_f64*)(pubRG + (size_t)kb * 2 * kNB);
+                F.cnt = (const volatile lds_i32*)cnt;
+                F.A = (lds_f64*)A;
+                F.sinkD = (lds_f64*)(sinkD + lane);
+#pragma unroll
+                for (int s = 0; s < 4; s++) {
+                    F.X[s] = A[(size_t)(rb + q + 4 * s) * ld + jb + k];
+                    F.Y[s] = Yr[s];
+                }
+                ColUnroll<0, kNB>::run(F);
+                seen = F.seen;
+#pragma unroll
+                for (int s = 0; s < 4; s++) Yr[s] = F.Y[s];
+            };
+            if (diagNext) {
+                DfFollow<true> F;
+                const int li = lane & 15, lk = lane >> 4;
+#pragma unroll
+                for (int s = 0; s < 4; s++) F.T[s] = A[(size_t)(rb + lk + 4 * s) * ld + rb + li];
+                follow(F);
+#pragma unroll
+                for (int s = 0; s < 4; s++) A[(size_t)(rb + lk + 4 * s) * ld + rb + li] = F.T[s];
+#pragma unroll
+                for (int s = 0; s < 4; s++)
+                    if (k == 0) y[rb + q + 4 * s] = Yr[s];
+                // tile (I, I) complete: the pivot's panel I may start
+                *(lane == 0 ? diagReady : (volatile lds_i32*)(sinkI + lane)) = I;
+                *(lane == 0 ? rowDone + I : (volatile lds_i32*)(sinkI + lane)) = kb + 1;
+            } else {
+                DfFollow<false> F;
+                follow(F);
+                const double rdk = pubRG[(size_t)kb * 2 * kNB + 2 * k];
+#pragma unroll
+                for (int s = 0; s < 4; s++) {
+                    const int r = rb + q + 4 * s;
+                    A[(size_t)(jb + k) * ld + r] = F.X[s];          // W(r, jb + k): the tiles' left operand
+                    A[(size_t)r * ld + jb + k] = F.X[s] * rdk;      // L(r, jb + k)
+                }
+                *(lane == 0 ? rowDone + I : (volatile lds_i32*)(sinkI + lane)) = kb + 1;
+                for (int K = kb + 1; K <= I; K++) {   // panel kb's trailing update of this row block's tiles
+                    if (K != I) wait_ge(rowDone + K, kb + 1);
+                    tile(jb, rb, kNB * K);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (failS) {
+        if (tid == 0) flags[0] = 1;
+        // the update still runs (with the previous x), as in k_ldlt_solve: the trial is then rejected
+        if (ptail.scaleOut && wave == 0) pose_tail(ptail, x, st->lambda, lane);
+        return;
+    }
+    // ---- y /= d and the backward substitution with L^T on wave 0 (k_ldlt_solve<true>'s register form)
+    {
+        const int j = tid >> 2, qq = tid & 3, end = min((j | 63) + 1, np);
+        if (j < np)
+            for (int i = j + qq; i < end; i += 4) A[(size_t)j * ld + i] = 0.0;
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    const int i1 = 64 + lane;
+    double X0 = lane < np ? y[lane] * rdg[lane] : 0.0;
+    double X1 = i1 < np ? y[i1] * rdg[i1] : 0.0;
+    const int kTop = (n - 1) & ~(kNB - 1);
+    for (int kb = kTop; kb >= 0; kb -= kNB) {
+        const double* Lk = A + (size_t)kb * ld;
+        double La[kNB], Lb[kNB];
+        if (kb >= 64) {
+#pragma unroll
+            for (int t = 0; t < kNB; t++) { La[t] = Lk[(size_t)t * ld + lane]; Lb[t] = Lk[(size_t)t * ld + i1]; }
+            if (kb + kNB > n) {
+                for (int jj = n - 1; jj >= kb; jj--) {
+                    const double xj = shfl_d_dyn(X1, jj - 64);
+                    X0 = __builtin_fma(-A[(size_t)jj * ld + lane], xj, X0);
+                    X1 = __builtin_fma(-A[(size_t)jj * ld + i1], xj, X1);
+                }
+                continue;
+            }
+#pragma unroll
+            for (int t = kNB - 1; t >= 0; t--) {
+                const double xj = shfl_d_dyn(X1, kb + t - 64);
+                X0 = __builtin_fma(-La[t], xj, X0);
+                X1 = __builtin_fma(-Lb[t], xj, X1);
+            }
+        } else {
+#pragma unroll
+            for (int t = 0; t < kNB; t++) La[t] = Lk[(size_t)t * ld + lane];
+            if (kb + kNB > n) {
+                for (int jj = n - 1; jj >= kb; jj--) X0 = __builtin_fma(-A[(size_t)jj * ld + lane], shfl_d_dyn(X0, jj), X0);
+                continue;
+            }
+#pragma unroll
+            for (int t = kNB - 1; t >= 0; t--) X0 = __builtin_fma(-La[t], shfl_d_dyn(X0, kb + t), X0);
+        }
+    }
+    if (lane < n) x[lane] = X0;
+    if (i1 < n) x[i1] = X1;
+    if (lane == 0) flags[0] = 0;
+    if (ptail.scaleOut) {   // x through LDS to the pose lanes (this wave's LDS operations are in order)
+        y[lane] = X0;
+        if (i1 < np) y[i1] = X1;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        pose_tail(ptail, y, st->lambda, lane);
+    }
+}
+// the dataflow solve applies to even orders that fit the LDS image (every local-BA system: n = 6P);
+// ORB_LBA_LDLT_OLD=1 keeps k_ldlt_solve<true> (A/B runs)
+static bool use_ldlt_df(int n) {
+    static const bool old = [] { const char* e = std::getenv("ORB_LBA_LDLT_OLD"); return e && e[0] == '1'; }();
+    const int np = (n + kNB - 1) & ~(kNB - 1);
+    return !old && (n & 1) == 0 && np <= kLdlLdsMaxN;
+}
+
 // ------------------------------------------------------------------ multi-workgroup reduced solve
 // Reduced systems beyond the LDS image (np > 128, more than 21 free keyframes: LocalMapping's
 // window is every covisible keyframe, unbounded, R/src/Optimizer.cpp:569-625).  The same blocked
@@ -3471,6 +3875,8 @@ int lba_dense_solve(lba_context* c, const double* S, const double* b, int n, dou
     ORB_HIP_TRY(hipMemcpyAsync(db, b, 8 * (size_t)n, hipMemcpyHostToDevice, s));
     if (use_mw(np))
         enqueue_ldlt_mw(s, mw_order(mw, n), dS, db, dx, df, nullptr, PoseTail{});
+    else if (use_ldlt_df(n))
+        hipLaunchKernelGGL(k_ldlt_df, dim3(1), dim3(kLdlT), ldlt_df_lds_bytes(n), s, dS, db, n, dx, df, nullptr, PoseTail{});
     else if (np <= kLdlLdsMaxN)
         hipLaunchKernelGGL(k_ldlt_solve<true>, dim3(1), dim3(kLdlT), ((size_t)np * (np + 1) + 3 * (size_t)np + 256 + (size_t)kNB * (np + 1) + 64) * 8, s,
                            dS, db, n, nullptr, dx, df, nullptr, PoseTail{});
@@ -3886,7 +4292,11 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
             PoseTail pt{};
             if (merge)
                 pt = PoseTail{d.q, d.t, d.bq, d.bt, d.partScale + (nbB - 1), d.bp, d_freePoses, d.poseIdx, d.P};
-            if (np <= kLdlLdsMaxN) {
+            if (use_ldlt_df(n)) {
+                hipLaunchKernelGGL(k_ldlt_df, dim3(1), dim3(kLdlT), ldlt_df_lds_bytes(n), s, d.S, d.bs, n, d.x, d.flags,
+                                   d.lm, pt);
+                boundary();
+            } else if (np <= kLdlLdsMaxN) {
                 hipLaunchKernelGGL(k_ldlt_solve<true>, dim3(1), dim3(kLdlT), ((size_t)np * (np + 1) + 3 * (size_t)np + 256 + (size_t)kNB * (np + 1) + 64) * 8,
                                    s, d.S, d.bs, n, nullptr, d.x, d.flags, d.lm, pt);
                 boundary();

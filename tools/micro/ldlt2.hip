@@ -99,6 +99,7 @@ int main(int argc, char** argv) {
     CHK(hipMalloc(&dx, 8 * (size_t)n));
     CHK(hipMalloc(&df, 4));
     CHK(hipMalloc(&dt, 8 * 64));
+    CHK(hipMemset(dt, 0, 8 * 64));
     CHK(hipMemcpy(dS, S.data(), 8 * (size_t)n * n, hipMemcpyHostToDevice));
     CHK(hipMemcpy(db, b.data(), 8 * (size_t)n, hipMemcpyHostToDevice));
     const size_t lds = ldlt2_lds_bytes(n);
@@ -141,6 +142,10 @@ int main(int argc, char** argv) {
     if (mode == 1) std::printf(" (tri-inv %lld, P tiles %lld, bsolve %lld)", t[4] - t[2], t[5] - t[4], t[3] - t[5]);
     std::printf(" | panel/trailing:");
     for (int i = 0; i < 8 && 16 * i < n; i++) std::printf(" %lld/%lld", t[8 + i] - (i ? t[16 + i - 1] : t[1]), t[16 + i] - t[8 + i]);
+    std::printf("\n  pivot: epilogue(kb-1) / wait / prologue:");
+    for (int i = 1; i < 8 && 16 * i < n; i++) std::printf(" %lld/%lld/%lld", t[40 + i] - t[8 + i - 1], t[48 + i] - t[40 + i], t[56 + i] - t[48 + i]);
+    std::printf("\n  pivot loop / last follower loop:");
+    for (int i = 0; i < 8 && 16 * i < n; i++) std::printf(" %lld/%lld", t[24 + i], t[32 + i]);
     std::printf("\n");
     return 0;
 }
