@@ -1773,7 +1773,7 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_solve(const double* __restrict__
 #pragma unroll
         for (int s = 0; s < kNB / 4; s++) {
             const int p = jb + 4 * s + lk;
-            a[s] = -A[(size_t)p * ld + I0 + li];        // -W(I0 + li, p)
+            a[s] = A[(size_t)p * ld + I0 + li];   // -W        // -W(I0 + li, p)
             bb[s] = A[(size_t)(K0 + li) * ld + p];      //  L(K0 + li, p)
         }
 #pragma unroll
@@ -2118,11 +2118,12 @@ typedef __attribute__((address_space(3))) int lds_i32;
 struct DfPivot {
     // entering column C: X = E^(C-1), R = row C of E^(C-1) (replicated), rd = 1/d_C, Q = row C+1 of
     // E^(C-2) (replicated), up = u_(C-1)
+    // stores go through per-lane bases fixed for the panel (the publishing lanes' records, the other
+    // lanes' private sinks), so a column's stores carry only immediate offsets
     double X[4], Y, rd, R, Q, up;
     int k, seq;
-    volatile lds_f64 *pubU, *pubRG, *sinkD, *rowbuf;
-    volatile lds_i32 *cnt, *sinkI;
-    bool qz, l0;
+    volatile lds_f64 *pU, *pRG, *rowW, *rowR;
+    volatile lds_i32* pC;
     template <int C>
     __device__ __forceinline__ void col() {
         double P1 = 0.0, w = 0.0, rdn = 1.0;
@@ -2133,19 +2134,19 @@ struct DfPivot {
             rdn = rcp_nr(__builtin_fma(-(w * w), rd, a));
         }
         double Qn = 0.0;   // row C+2 of E^(C-1) through LDS, consumed at the next column's start
-        if constexpr (C + 2 < kNB) {
-            *((C + 2) % 4 == (int)(threadIdx.x & 63) >> 4 ? rowbuf + k : sinkD) = X[(C + 2) >> 2];
-            Qn = rowbuf[k];
+        if constexpr (C + 2 < kNB) {   // every lane writes its own slot, all read lane row (C+2) % 4's
+            *rowW = X[(C + 2) >> 2];
+            Qn = rowR[((C + 2) & 3) * kNB];
         }
         const double u = R * (k > C ? rd : 0.0);
 #pragma unroll
         for (int s = 0; s < 4; s++) X[s] = __builtin_fma(-rbc16<C>(X[s]), u, X[s]);
         const double yc = rbc16<C>(Y);
         Y = __builtin_fma(-u, yc, Y);
-        *(qz ? pubU + C * kNB + k : sinkD) = u;
-        *(l0 ? pubRG + 2 * C : sinkD) = rd;
-        *(l0 ? pubRG + 2 * C + 1 : sinkD) = rd * yc;
-        *(l0 ? cnt : sinkI) = seq + C + 1;
+        pU[C * kNB] = u;
+        pRG[2 * C] = rd;
+        pRG[2 * C + 1] = rd * yc;
+        *pC = seq + C + 1;
         if constexpr (C + 1 < kNB) {
             R = __builtin_fma(-w, u, P1);
             rd = rdn;
@@ -2162,20 +2163,34 @@ struct DfPivot {
 template <bool kDiag>
 struct DfFollow {
     double X[4], Y[4];
+    double uq[4], gq[4];     // the current group of four published columns
     dbl4 T;                  // kDiag: the diagonal tile, MFMA output layout
+    double pa, pb;           // kDiag: the last group's MFMA operands, applied one group later
     int k, seq, seen, jb, rb, ld;
     const volatile lds_f64 *pubU, *pubRG;
     const volatile lds_i32* cnt;
     lds_f64 *A, *sinkD;
     template <int C>
     __device__ __forceinline__ void col() {
-        if (seen <= seq + C) {   // wave-uniform poll of the pivot's sequence counter
-            int v;
-            while ((v = __builtin_amdgcn_readfirstlane(*cnt)) <= seq + C) __builtin_amdgcn_s_sleep(1);
-            seen = v;
+        // the follower trails the pivot, so it takes the pivot's columns four at a time: one poll of the
+        // sequence counter (wave-uniform) and one LDS round trip for the group's u and y_c / d_c instead
+        // of one per column
+        if constexpr ((C & 3) == 0) {
+            if (__builtin_amdgcn_readfirstlane(seen) < seq + C + 4) {
+                int v;
+                while ((v = __builtin_amdgcn_readfirstlane(*cnt)) < seq + C + 4) __builtin_amdgcn_s_sleep(1);
+                seen = v;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                uq[j] = pubU[(C + j) * kNB + k];
+                gq[j] = pubRG[2 * (C + j) + 1];
+            }
+            // the previous group's MFMA, its operands' LDS round trip hidden behind this group's
+            if constexpr (kDiag && C > 0) T = __builtin_amdgcn_mfma_f64_16x16x4f64(pa, pb, T, 0, 0, 0);
         }
-        const double u = pubU[C * kNB + k];
-        const double g = pubRG[2 * C + 1];
+        const double u = uq[C & 3];
+        const double g = gq[C & 3];
 #pragma unroll
         for (int s = 0; s < 4; s++) {
             const double wi = rbc16<C>(X[s]);
@@ -2183,27 +2198,28 @@ struct DfFollow {
             Y[s] = __builtin_fma(-wi, g, Y[s]);
         }
         if constexpr (kDiag && (C & 3) == 3) {
-            // columns C-3..C are final: their W (upper triangle) and L (lower) out, then the tile's MFMA
-            const bool mine = k >= C - 3 && k <= C;
-            const double rdk = pubRG[2 * (k & 15)];
+            // columns C-3..C are final: their -W (upper triangle) and L (lower) out, and the tile's MFMA
+            // operands read back (the MFMA itself waits for the next group, or the caller)
             const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+            if ((k >> 2) == (C >> 2)) {
+                const double rdk = pubRG[2 * k];
 #pragma unroll
-            for (int s = 0; s < 4; s++) {
-                const int r = rb + (lane >> 4) + 4 * s;
-                *(mine ? A + (size_t)(jb + k) * ld + r : sinkD) = X[s];
-                *(mine ? A + (size_t)r * ld + jb + k : sinkD) = X[s] * rdk;
+                for (int s = 0; s < 4; s++) {
+                    const int r = rb + lk + 4 * s;
+                    A[(size_t)(jb + k) * ld + r] = -X[s];
+                    A[(size_t)r * ld + jb + k] = X[s] * rdk;
+                }
             }
             const int pc = jb + (C - 3) + lk;
-            const double a = -A[(size_t)pc * ld + rb + li];
-            const double bb = A[(size_t)(rb + li) * ld + pc];
-            T = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, T, 0, 0, 0);
+            pa = A[(size_t)pc * ld + rb + li];
+            pb = A[(size_t)(rb + li) * ld + pc];
         }
     }
 };
 
 __host__ __device__ inline size_t ldlt_df_lds_bytes(int n) {
     const int np = (n + kNB - 1) & ~(kNB - 1);
-    return 8 * ((size_t)np * (np + 1) + 2 * (size_t)np + (size_t)(np / kNB) * (kNB * kNB + 2 * kNB) + 64 + kNB + 64 + 32);
+    return 8 * ((size_t)np * (np + 1) + 2 * (size_t)np + (size_t)(np / kNB) * (kNB * kNB + 2 * kNB) + 64 + kNB * kNB + 4 * kNB + 64 + 32);
 }
 
 __global__ __launch_bounds__(kLdlT) void k_ldlt_df(const double* __restrict__ Sg, const double* __restrict__ b, int n,
@@ -2214,21 +2230,31 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_df(const double* __restrict__ Sg
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int np = (n + kNB - 1) & ~(kNB - 1), ld = np + 1, T = np / kNB;
     const int k = lane & 15, q = lane >> 4;
+#ifdef ORB_TIMING
+    long long tdf[40] = {0};
+    tdf[0] = clock64();
+#endif
     double* A = sh;
     double* rdg = A + (size_t)np * ld;
     double* y = rdg + np;
     double* pubU = y + np;                           // [T][16][16]
     double* pubRG = pubU + (size_t)T * kNB * kNB;     // [T][16][2]
-    double* sinkD = pubRG + (size_t)T * 2 * kNB;      // 64 per-lane sinks
-    double* rowbuf = sinkD + 64;                      // 16
-    int* cnt = (int*)(rowbuf + kNB);
+    double* sinkD = pubRG + (size_t)T * 2 * kNB;      // per-lane sinks: lane + up to 15 columns x 16
+    double* rowbuf = sinkD + 64 + kNB * kNB;          // [4][16]: the pivot's next-row exchange
+    int* cnt = (int*)(rowbuf + 4 * kNB);
     int* sinkI = cnt + 2;                             // 64
     volatile lds_i32* rowDone = (volatile lds_i32*)(sinkI + 64);   // [8]
     volatile lds_i32* diagReady = rowDone + 8;
     __shared__ int failS;
+#ifdef ORB_TIMING
+    __shared__ long long dbgT[32];
+#endif
     if (tid == 0) { failS = 0; *cnt = 0; }
     if (tid < 9) rowDone[tid] = 0;
     __syncthreads();
+#ifdef ORB_TIMING
+    tdf[35] = clock64();
+#endif
     // ---- staging, per owner, no barrier: the wave of row block I loads its rows' columns
     //      [0, 16(I+1)) (its lower tiles and the whole diagonal tile) and their b, one 16-byte load per
     //      (row, column pair), all in flight; identity padding past n (n even: no pair straddles it)
@@ -2266,7 +2292,7 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_df(const double* __restrict__ Sg
 #pragma unroll
         for (int s = 0; s < kNB / 4; s++) {
             const int p = jb + 4 * s + lk;
-            a[s] = -A[(size_t)p * ld + I0 + li];
+            a[s] = A[(size_t)p * ld + I0 + li];   // -W
             bb[s] = A[(size_t)(K0 + li) * ld + p];
         }
 #pragma unroll
@@ -2278,20 +2304,26 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_df(const double* __restrict__ Sg
     };
     if (wave == 0) {
         stage_rows(0);
+#ifdef ORB_TIMING
+        tdf[36] = clock64();
+#endif
         for (int kb = 0; kb < T; kb++) {
             const int jb = kb * kNB;
+#ifdef ORB_TIMING
+            if (kb < 8) tdf[1 + 4 * kb] = clock64();
+#endif
             if (kb > 0) wait_ge(diagReady, kb);
+#ifdef ORB_TIMING
+            if (kb < 8) tdf[2 + 4 * kb] = clock64();
+#endif
             DfPivot P;
             P.k = k;
             P.seq = kNB * kb;
-            P.pubU = (volatile lds_f64*)(pubU + (size_t)kb * kNB * kNB);
-            P.pubRG = (volatile lds_f64*)(pubRG + (size_t)kb * 2 * kNB);
-            P.sinkD = (volatile lds_f64*)(sinkD + lane);
-            P.rowbuf = (volatile lds_f64*)rowbuf;
-            P.cnt = (volatile lds_i32*)cnt;
-            P.sinkI = (volatile lds_i32*)(sinkI + lane);
-            P.qz = q == 0;
-            P.l0 = lane == 0;
+            P.pU = (volatile lds_f64*)(q == 0 ? pubU + (size_t)kb * kNB * kNB + k : sinkD + lane);
+            P.pRG = (volatile lds_f64*)(lane == 0 ? pubRG + (size_t)kb * 2 * kNB : sinkD + lane);
+            P.pC = (volatile lds_i32*)(lane == 0 ? cnt : sinkI + lane);
+            P.rowW = (volatile lds_f64*)(rowbuf + lane);
+            P.rowR = (volatile lds_f64*)(rowbuf + k);
 #pragma unroll
             for (int s = 0; s < 4; s++) P.X[s] = A[(size_t)(jb + q + 4 * s) * ld + jb + k];
             P.Y = y[jb + k];
@@ -2300,8 +2332,14 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_df(const double* __restrict__ Sg
             P.up = 0.0;
             P.rd = rcp_nr(rbc16<0>(P.R));
             const int nc = n - jb;
+#ifdef ORB_TIMING
+            if (kb < 8) tdf[3 + 4 * kb] = clock64();
+#endif
             if (nc >= kNB) ColUnroll<0, kNB>::run(P);
             else ColUnrollTo<0, kNB>::run(P, nc);
+#ifdef ORB_TIMING
+            if (kb < 8) tdf[4 + 4 * kb] = clock64();
+#endif
             // the diagonal block's L (strict lower), 1/d and its finished y; a zero or non-finite pivot
             // (1/d zero or non-finite) flags the solve
             const double rdk = jb + k < n ? pubRG[(size_t)kb * 2 * kNB + 2 * k] : 1.0;
@@ -2351,13 +2389,32 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_df(const double* __restrict__ Sg
                 const int li = lane & 15, lk = lane >> 4;
 #pragma unroll
                 for (int s = 0; s < 4; s++) F.T[s] = A[(size_t)(rb + lk + 4 * s) * ld + rb + li];
+#ifdef ORB_TIMING
+                const long long tfs = clock64();
+#endif
                 follow(F);
+#ifdef ORB_TIMING
+                if (lane == 0 && kb < 8) { dbgT[2 * kb] = tfs; dbgT[2 * kb + 1] = clock64(); }
+#endif
+                F.T = __builtin_amdgcn_mfma_f64_16x16x4f64(F.pa, F.pb, F.T, 0, 0, 0);
+                if (kb >= 1) {   // the previous panel's update of this tile, deferred (see below)
+                    const int jp = jb - kNB;
+#pragma unroll
+                    for (int s = 0; s < kNB / 4; s++) {
+                        const int pp = jp + 4 * s + lk;
+                        F.T = __builtin_amdgcn_mfma_f64_16x16x4f64(A[(size_t)pp * ld + rb + li], A[(size_t)(rb + li) * ld + pp],
+                                                                   F.T, 0, 0, 0);
+                    }
+                }
 #pragma unroll
                 for (int s = 0; s < 4; s++) A[(size_t)(rb + lk + 4 * s) * ld + rb + li] = F.T[s];
 #pragma unroll
                 for (int s = 0; s < 4; s++)
                     if (k == 0) y[rb + q + 4 * s] = Yr[s];
                 // tile (I, I) complete: the pivot's panel I may start
+#ifdef ORB_TIMING
+                if (lane == 0 && kb < 8) dbgT[16 + kb] = clock64();
+#endif
                 *(lane == 0 ? diagReady : (volatile lds_i32*)(sinkI + lane)) = I;
                 *(lane == 0 ? rowDone + I : (volatile lds_i32*)(sinkI + lane)) = kb + 1;
             } else {
@@ -2367,11 +2424,15 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_df(const double* __restrict__ Sg
 #pragma unroll
                 for (int s = 0; s < 4; s++) {
                     const int r = rb + q + 4 * s;
-                    A[(size_t)(jb + k) * ld + r] = F.X[s];          // W(r, jb + k): the tiles' left operand
+                    A[(size_t)(jb + k) * ld + r] = -F.X[s];         // -W(r, jb + k): the tiles' left operand
                     A[(size_t)r * ld + jb + k] = F.X[s] * rdk;      // L(r, jb + k)
                 }
                 *(lane == 0 ? rowDone + I : (volatile lds_i32*)(sinkI + lane)) = kb + 1;
-                for (int K = kb + 1; K <= I; K++) {   // panel kb's trailing update of this row block's tiles
+                // panel kb's trailing update of this row block's tiles; in the panel before the one where
+                // this block is the next diagonal block, the diagonal tile's update is deferred to after
+                // that panel's columns (above), so this wave starts following it one tile earlier
+                const int Kend = kb == I - 2 ? I - 1 : I;
+                for (int K = kb + 1; K <= Kend; K++) {
                     if (K != I) wait_ge(rowDone + K, kb + 1);
                     tile(jb, rb, kNB * K);
                 }
@@ -2379,6 +2440,9 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_df(const double* __restrict__ Sg
         }
     }
     __syncthreads();
+#ifdef ORB_TIMING
+    tdf[33] = clock64();
+#endif
     if (failS) {
         if (tid == 0) flags[0] = 1;
         // the update still runs (with the previous x), as in k_ldlt_solve: the trial is then rejected
@@ -2431,6 +2495,9 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_df(const double* __restrict__ Sg
     if (lane < n) x[lane] = X0;
     if (i1 < n) x[i1] = X1;
     if (lane == 0) flags[0] = 0;
+#ifdef ORB_TIMING
+    tdf[34] = clock64();
+#endif
     if (ptail.scaleOut) {   // x through LDS to the pose lanes (this wave's LDS operations are in order)
         y[lane] = X0;
         if (i1 < np) y[i1] = X1;
@@ -2439,6 +2506,19 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_df(const double* __restrict__ Sg
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         pose_tail(ptail, y, st->lambda, lane);
     }
+#ifdef ORB_TIMING
+    if (lane == 0) {
+        printf("ldlt_df n %d: to-factor-end %lld bsolve %lld tail %lld | per panel wait/prologue/loop/epilogue:", n,
+               tdf[33] - tdf[0], tdf[34] - tdf[33], clock64() - tdf[34]);
+        for (int kb = 0; kb < T && kb < 8; kb++)
+            printf(" %lld/%lld/%lld/%lld", tdf[2 + 4 * kb] - tdf[1 + 4 * kb], tdf[3 + 4 * kb] - tdf[2 + 4 * kb],
+                   tdf[4 + 4 * kb] - tdf[3 + 4 * kb], (kb + 1 < T && kb < 7 ? tdf[5 + 4 * kb] : tdf[33]) - tdf[4 + 4 * kb]);
+        printf(" | stage0 %lld (barrier %lld, stage_rows %lld) | diag follower start/loop-end/flag vs pivot loop start/end:", tdf[1] - tdf[0], tdf[35] - tdf[0], tdf[36] - tdf[35]);
+        for (int kb = 0; kb + 1 < T && kb < 7; kb++)
+            printf(" %lld/%lld/%lld", dbgT[2 * kb] - tdf[3 + 4 * kb], dbgT[2 * kb + 1] - tdf[4 + 4 * kb], dbgT[16 + kb] - tdf[4 + 4 * kb]);
+        printf("\n");
+    }
+#endif
 }
 // the dataflow solve applies to even orders that fit the LDS image (every local-BA system: n = 6P);
 // ORB_LBA_LDLT_OLD=1 keeps k_ldlt_solve<true> (A/B runs)

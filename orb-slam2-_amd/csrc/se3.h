@@ -76,8 +76,14 @@ __device__ inline void d_se3_exp_left(const double upd[6], double q[4], double t
     if (theta < 0.00001) {
         for (int i = 0; i < 9; i++) { R[i] = (i % 4 == 0 ? 1.0 : 0.0) + O[i] + O2[i]; V[i] = R[i]; }
     } else {
-        const double a = sin(theta) / theta, b = (1 - cos(theta)) / (theta * theta);
-        const double c = (theta - sin(theta)) / pow(theta, 3);
+        // (g2o's pow(theta, 3) as two products: the same value to an ulp, where theta - sin(theta)
+        // already carries the cancellation error; ocml's f64 pow was the longest link of the pose
+        // update that ends every reduced solve)
+        double sn, cs;
+        sincos(theta, &sn, &cs);
+        const double t2 = theta * theta;
+        const double a = sn / theta, b = (1 - cs) / t2;
+        const double c = (theta - sn) / (t2 * theta);
         for (int i = 0; i < 9; i++) {
             const double I = (i % 4 == 0 ? 1.0 : 0.0);
             R[i] = I + a * O[i] + b * O2[i];

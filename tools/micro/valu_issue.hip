@@ -6,9 +6,10 @@
 //   * co-residency: per CU, the largest number of its workgroups whose [start, end] overlap at one
 //     instant (k means all k ran together);
 //   * the all-running window [max start, min end] over every workgroup of the launch: inside it
-//     every workgroup runs, so the chip's rate there is the sum of the workgroups' own rates
-//     (instructions / their own loop time) — the steady-state issue rate without dispatch ramp and
-//     tail;
+//     every workgroup runs; each workgroup stamps s_memrealtime at 17 checkpoints (every 1/16 of its
+//     loop), so the instructions it executed inside the window are interpolated from its own
+//     checkpoints and the chip's steady-state rate is their sum over the window (no dispatch ramp or
+//     tail, and no workgroup credited for time it ran with fewer neighbours);
 //   * the wall-clock rate (instructions / event time) beside it; the two agree when the kernel is
 //     long enough and the workgroups are co-resident.
 // The ops are the extraction kernels' integer mix (v_perm, v_alignbyte, v_lerp_u8, v_dot4_u32_u8,
@@ -22,6 +23,7 @@
 #include <vector>
 
 constexpr int kOps = 9;
+constexpr int kStride = 24;   // per workgroup: memtime start / end, realtime start / end, HW_ID, -, 17 checkpoints
 static const char* kNames[kOps] = {"v_fma_f32",      "v_pk_fma_f32",  "v_xad_u32",       "v_perm_b32",        "v_alignbyte_b32",
                                    "v_lerp_u8",      "v_dot4_u32_u8", "v_bcnt_u32_b32",  "v_pk_minimum3_f16"};
 
@@ -45,8 +47,12 @@ __global__ __launch_bounds__(256) void k_issue(const float* in, float* out, unsi
     if (threadIdx.x == 0) {
         t0 = __builtin_amdgcn_s_memtime();
         r0 = __builtin_amdgcn_s_memrealtime();
+        stamps[kStride * blockIdx.x + 6] = r0;
     }
+    const int chunk = iters / 16;
     for (int i = 0; i < iters; i++) {
+        if (threadIdx.x == 0 && i > 0 && i % chunk == 0 && i / chunk < 16)
+            stamps[kStride * blockIdx.x + 6 + i / chunk] = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
         for (int k = 0; k < 8; k++) {
             if (OP == 0) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(a[k]) : "v"(c), "v"(d));
@@ -64,12 +70,13 @@ __global__ __launch_bounds__(256) void k_issue(const float* in, float* out, unsi
         const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
         unsigned hw;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        stamps[6 * blockIdx.x + 0] = t0;
-        stamps[6 * blockIdx.x + 1] = t1;
-        stamps[6 * blockIdx.x + 2] = r0;
-        stamps[6 * blockIdx.x + 3] = r1;
-        stamps[6 * blockIdx.x + 4] = hw;
-        stamps[6 * blockIdx.x + 5] = 0;
+        stamps[kStride * blockIdx.x + 0] = t0;
+        stamps[kStride * blockIdx.x + 1] = t1;
+        stamps[kStride * blockIdx.x + 2] = r0;
+        stamps[kStride * blockIdx.x + 3] = r1;
+        stamps[kStride * blockIdx.x + 4] = hw;
+        stamps[kStride * blockIdx.x + 5] = 0;
+        stamps[kStride * blockIdx.x + 22] = r1;
     }
     float s = 0.f;
 #pragma unroll
@@ -100,7 +107,7 @@ int main(int argc, char** argv) {
     unsigned long long* st;
     (void)hipMalloc(&in, 4096 * 4);
     (void)hipMalloc(&out, (size_t)cus * 8 * 256 * 4);
-    (void)hipMalloc(&st, (size_t)cus * 8 * 6 * 8);
+    (void)hipMalloc(&st, (size_t)cus * 8 * kStride * 8);
     std::vector<float> h(4096, 1.0f);
     h[1000] = 0.999f;
     h[1001] = 0.001f;
@@ -123,7 +130,7 @@ int main(int argc, char** argv) {
                 (void)hipEventSynchronize(e1);
                 (void)hipEventElapsedTime(&ms, e0, e1);
             }
-            std::vector<unsigned long long> s((size_t)blocks * 6);
+            std::vector<unsigned long long> s((size_t)blocks * kStride);
             (void)hipMemcpy(s.data(), st, s.size() * 8, hipMemcpyDeviceToHost);
             // co-residency per CU (HW_ID: CU_ID bits 11:8, SH_ID 12, SE_ID 15:13 on gfx9; XCC from the
             // dispatch order is not in HW_ID, so CUs are keyed by (block % 8 XCD, SE, SH, CU))
@@ -131,8 +138,8 @@ int main(int argc, char** argv) {
             unsigned long long winStart = 0, winEnd = ~0ull;
             double cyc = 0, rt = 0, rateSum = 0;
             for (int b = 0; b < blocks; b++) {
-                const unsigned long long t0 = s[6 * b], t1 = s[6 * b + 1], r0 = s[6 * b + 2], r1 = s[6 * b + 3];
-                const unsigned hw = (unsigned)s[6 * b + 4];
+                const unsigned long long t0 = s[kStride * b], t1 = s[kStride * b + 1], r0 = s[kStride * b + 2], r1 = s[kStride * b + 3];
+                const unsigned hw = (unsigned)s[kStride * b + 4];
                 const int cu = (hw >> 8) & 15, sh = (hw >> 12) & 1, se = (hw >> 13) & 7;
                 const int key = ((b % 8) * 8 + se) * 32 + sh * 16 + cu;
                 ev[(size_t)key % ev.size()].push_back({r0, +1});
@@ -157,7 +164,22 @@ int main(int argc, char** argv) {
             const double wallRate = winst / (ms * 1e-3);
             const double winMs = winEnd > winStart ? (double)(winEnd - winStart) / 1e5 : 0.0;
             const double loopMs = rt / blocks / 1e5;
-            const double winRate = winEnd > winStart ? rateSum : 0.0;   // every workgroup runs inside the window
+            // instructions each workgroup executed inside the all-running window, interpolated from its
+            // 17 checkpoints (1/16 of its loop apart)
+            double winInst = 0.0;
+            if (winEnd > winStart)
+                for (int b = 0; b < blocks; b++) {
+                    const unsigned long long* c = &s[(size_t)kStride * b + 6];
+                    auto progress = [&](unsigned long long t) {   // fraction of the loop done at realtime t
+                        if (t <= c[0]) return 0.0;
+                        for (int j = 0; j < 16; j++)
+                            if (t <= c[j + 1]) return (j + (double)(t - c[j]) / (double)(c[j + 1] - c[j] ? c[j + 1] - c[j] : 1)) / 16.0;
+                        return 1.0;
+                    };
+                    winInst += (progress(winEnd) - progress(winStart)) * 4.0 * iters * 8;
+                }
+            const double winRate = winEnd > winStart ? winInst / ((double)(winEnd - winStart) / 100e6) : 0.0;
+            (void)rateSum;
             const double cycPerInst = winRate > 0 ? cus * 4.0 * ghz * 1e9 / winRate : 0.0;
             const double lanes = op == 1 ? 128.0 : 64.0;
             std::printf("%-18s %3d %8.3f %7.3f %4d/%-4d | %9.3f %9.3f %5.1f%% | %11.4g %11.4g %6.3f | %12.3f %12.4g\n",
