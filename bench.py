@@ -1103,11 +1103,15 @@ def bench_routed_calls(args, amd, dev, med, creps=9):
     voc = synth.vocabulary(k=10, L=4, seed=5, early_leaf=0.05, stop_frac=0.03)
     ov = O.OracleVocabulary(*voc, 4)
     k1, k2 = synth.bow_match_problem(voc, seed=11)
-    fv1, fv2 = O.bow_transform(ov, k1["desc"], 4)[1], O.bow_transform(ov, k2["desc"], 4)[1]
+    # FeatureVector at level L - levelsup = 2 (this 4-level vocabulary, levelsup 2): the node granularity of
+    # the reference's ORBvoc (L = 6) with its levelsup 4 (R/src/Frame.cpp:465, R/src/KeyFrame.cpp:72), ~100
+    # nodes of ~10 features per side.  (levelsup 4 here would put every feature in the root node: one
+    # 900 x 900 node, one workgroup — not a call the reference makes.)
+    fv1, fv2 = O.bow_transform(ov, k1["desc"], 2)[1], O.bow_transform(ov, k2["desc"], 2)[1]
     a1, a2 = O.featvec_arrays(fv1), O.featvec_arrays(fv2)
     f1, f2 = Frame(kp_of(k1), k1["desc"], k1["W"], k1["H"]), Frame(kp_of(k2), k2["desc"], k2["W"], k2["H"])
     m = amd.ORBmatcher(0.7, True, device=dev.index or 0)
-    size = f"{len(k1['x'])} x {len(k2['x'])} features, levelsup 4"
+    size = f"{len(k1['x'])} x {len(k2['x'])} features, {len(fv1)} / {len(fv2)} level-2 nodes"
     row("search_by_bow_kf_frame", lambda: m.SearchByBoW(f1, k1["has_mp"], fv1, f2, a2),
         lambda: O.search_by_bow_frame(k1, k1["has_mp"], a1, k2, a2, 0.7, True), "R/src/Tracking.cpp:1020, 1840", size)
     row("search_by_bow_kf_kf", lambda: m.SearchByBoWKF(f1, k1["has_mp"], a1, f2, k2["has_mp"], fv2),

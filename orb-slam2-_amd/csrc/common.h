@@ -6,6 +6,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <initializer_list>
 #include <mutex>
 #include <new>
 #include <vector>
@@ -71,6 +72,20 @@ struct HostScratch {
     char* pin = nullptr;    // pinned host staging of the same size (Staging below)
     size_t cap = 0;
 };
+// grow-only (rare; the caller's stream is idle between its calls), under the capture lock
+inline int grow_scratch(HostScratch* h, size_t bytes) {
+    if (h->cap >= bytes) return ORB_OK;
+    std::lock_guard<std::mutex> lk(legacy_capture_mutex());
+    if (h->base) (void)hipFree(h->base);
+    if (h->pin) (void)hipHostFree(h->pin);
+    h->base = h->pin = nullptr;
+    h->cap = 0;
+    const size_t cap = std::max(bytes + bytes / 2, (size_t)1 << 20);
+    if (hipMalloc((void**)&h->base, cap) != hipSuccess) return ORB_ENOMEM;
+    if (hipHostMalloc((void**)&h->pin, cap, hipHostMallocDefault) != hipSuccess) return ORB_ENOMEM;
+    h->cap = cap;
+    return ORB_OK;
+}
 inline int host_scratch(int device, size_t bytes, HostScratch** out) {
     thread_local std::vector<HostScratch*> pool;
     HostScratch* h = nullptr;
@@ -88,17 +103,7 @@ inline int host_scratch(int device, size_t bytes, HostScratch** out) {
         }
         pool.push_back(h);
     }
-    if (h->cap < bytes) {   // grow (rare): the stream is idle between calls of this thread
-        std::lock_guard<std::mutex> lk(legacy_capture_mutex());
-        if (h->base) (void)hipFree(h->base);
-        if (h->pin) (void)hipHostFree(h->pin);
-        h->base = h->pin = nullptr;
-        h->cap = 0;
-        const size_t cap = std::max(bytes + bytes / 2, (size_t)1 << 20);
-        if (hipMalloc((void**)&h->base, cap) != hipSuccess) return ORB_ENOMEM;
-        if (hipHostMalloc((void**)&h->pin, cap, hipHostMallocDefault) != hipSuccess) return ORB_ENOMEM;
-        h->cap = cap;
-    }
+    if (int e = grow_scratch(h, bytes)) return e;
     *out = h;
     return ORB_OK;
 }
@@ -127,6 +132,19 @@ struct Staging {
         char* d = take(bytes);
         if (!over && src && bytes) std::memcpy(h->pin + at, src, bytes);
         return d;
+    }
+    // an input the caller writes into the staging itself (*hostp; nullptr once the staging overflowed)
+    char* in_place(size_t bytes, char** hostp) {
+        const size_t at = off;
+        char* d = take(bytes);
+        *hostp = over ? nullptr : h->pin + at;
+        return d;
+    }
+    // staging bytes for arrays of these sizes (256-byte steps, one guard byte each)
+    static size_t bytes_for(std::initializer_list<size_t> sizes) {
+        size_t t = 4096;
+        for (size_t b : sizes) t += al(b + 1);
+        return t;
     }
     int upload(hipStream_t s) {
         if (over) return ORB_EINTERNAL;

@@ -1011,6 +1011,8 @@ struct orb_matcher {
     uint8_t* d_mpd = nullptr;
     void* h_pin = nullptr;
     size_t h_pin_bytes = 0;
+    // the per-call host entry points' staging: inputs cross PCIe in one copy, outputs in one (common.h)
+    HostScratch hs;
 };
 
 static void mfree(orb_matcher* m) {
@@ -1079,6 +1081,12 @@ static int mpin(orb_matcher* m, size_t bytes) {
     if (hipHostMalloc(&m->h_pin, bytes, hipHostMallocDefault) != hipSuccess) return ORB_ENOMEM;
     m->h_pin_bytes = bytes;
     return ORB_OK;
+}
+
+static int mstage(orb_matcher* m, size_t bytes) {
+    m->hs.device = m->device;
+    m->hs.stream = m->stream;
+    return grow_scratch(&m->hs, bytes);
 }
 
 static GridParams grid_of(const orb_frame_view* f) {
@@ -1608,6 +1616,8 @@ void orb_matcher_destroy(orb_matcher* m) try {
     if (m->stream) (void)hipStreamSynchronize(m->stream);
     mfree(m);
     if (m->h_pin) (void)hipHostFree(m->h_pin);
+    if (m->hs.base) (void)hipFree(m->hs.base);
+    if (m->hs.pin) (void)hipHostFree(m->hs.pin);
     if (m->stream) (void)hipStreamDestroy(m->stream);
     delete m;
 } ORB_ABI_CATCH_VOID
@@ -1620,52 +1630,41 @@ int orb_search_for_initialization(orb_matcher* m, const orb_frame_view* f1, cons
     const int cap = std::max(std::max(f1->n, f2->n), 1);
     int st = mensure(m, 1, cap);
     if (st) return st;
-    const size_t bytes = (size_t)cap * (2 * sizeof(orb_keypoint) + 64 + 8 + 4) + 64;
-    st = mpin(m, bytes);
+    const size_t n1 = (size_t)f1->n, n2 = (size_t)f2->n;
+    st = mstage(m, Staging::bytes_for({n1 * sizeof(orb_keypoint), n2 * sizeof(orb_keypoint), n1 * 32, n2 * 32, 8, n1 * 8,
+                                       8, n1 * 4, 4}));
     if (st) return st;
-    char* h = (char*)m->h_pin;
-    orb_keypoint* hk1 = (orb_keypoint*)h;
-    orb_keypoint* hk2 = hk1 + cap;
-    uint8_t* hd1 = (uint8_t*)(hk2 + cap);
-    uint8_t* hd2 = hd1 + (size_t)cap * 32;
-    float* hprev = (float*)(hd2 + (size_t)cap * 32);
-    int32_t* hn = (int32_t*)(hprev + 2 * (size_t)cap);
-    pack_view(f1, hk1);
-    pack_view(f2, hk2);
-    std::memcpy(hd1, f1->desc, (size_t)f1->n * 32);
-    std::memcpy(hd2, f2->desc, (size_t)f2->n * 32);
-    std::memcpy(hprev, prev_xy, (size_t)f1->n * 8);
-    hn[0] = f1->n;
-    hn[1] = f2->n;
     hipStream_t s = m->stream;
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_k1, hk1, (size_t)f1->n * sizeof(orb_keypoint), hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_k2, hk2, (size_t)f2->n * sizeof(orb_keypoint), hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_d1, hd1, (size_t)f1->n * 32, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_d2, hd2, (size_t)f2->n * 32, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_prev, hprev, (size_t)f1->n * 8, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_n, hn, 8, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemsetAsync(m->d_status, 0, 4, s));
+    Staging sg(&m->hs);   // one H2D of the inputs, one D2H of prev / status / matches / count
+    char* hp;
+    auto* dK1 = (orb_keypoint*)sg.in_place(n1 * sizeof(orb_keypoint), &hp);
+    if (hp) pack_view(f1, (orb_keypoint*)hp);
+    auto* dK2 = (orb_keypoint*)sg.in_place(n2 * sizeof(orb_keypoint), &hp);
+    if (hp) pack_view(f2, (orb_keypoint*)hp);
+    auto* dD1 = (uint8_t*)sg.in(f1->desc, n1 * 32);
+    auto* dD2 = (uint8_t*)sg.in(f2->desc, n2 * 32);
+    const int32_t nn[2] = {f1->n, f2->n}, zero[2] = {0, 0};
+    auto* dN = (int32_t*)sg.in(nn, 8);
+    auto* dPrev = (float*)sg.in(prev_xy, n1 * 8);
+    auto* dSt = (int32_t*)sg.in(zero, 8);
+    auto* dM12 = (int32_t*)sg.out(n1 * 4);
+    auto* dNm = (int32_t*)sg.out(4);
+    if (int e_ = sg.upload(s)) return e_;
     const GridParams g = grid_of(f2);
-    hipLaunchKernelGGL(k_grid_sfi, dim3(1), dim3(256), 0, s, m->d_k2, m->d_n + 1, cap, g, m->d_cs, m->d_gj, m->d_gxy);
-    hipLaunchKernelGGL(k_cand_sfi, dim3(kCandWaves / 4, 1), dim3(256), 0, s, m->d_k1, m->d_d1, m->d_n, m->d_d2, m->d_cs,
-                       m->d_gj, m->d_gxy, m->d_prev, cap, g, (float)window, m->d_cand, m->d_ncand, m->d_topk,
-                       m->d_status);
+    hipLaunchKernelGGL(k_grid_sfi, dim3(1), dim3(256), 0, s, dK2, dN + 1, cap, g, m->d_cs, m->d_gj, m->d_gxy);
+    hipLaunchKernelGGL(k_cand_sfi, dim3(kCandWaves / 4, 1), dim3(256), 0, s, dK1, dD1, dN, dD2, m->d_cs, m->d_gj,
+                       m->d_gxy, dPrev, cap, g, (float)window, m->d_cand, m->d_ncand, m->d_topk, dSt);
     const size_t lds = resolve_sfi_lds(cap);
     if (lds > kMaxLds || cap > 32767) return ORB_E2BIG;
-    hipLaunchKernelGGL(k_resolve_sfi, dim3(1), dim3(kRsT), lds, s, m->d_k1, m->d_n, m->d_k2, m->d_n + 1, cap,
-                       m->nnratio, m->checkOri, m->d_cand, m->d_ncand, m->d_topk, m->d_prev, m->d_m12, m->d_nm,
-                       m->d_status);
+    hipLaunchKernelGGL(k_resolve_sfi, dim3(1), dim3(kRsT), lds, s, dK1, dN, dK2, dN + 1, cap, m->nnratio, m->checkOri,
+                       m->d_cand, m->d_ncand, m->d_topk, dPrev, dM12, dNm, dSt);
     ORB_HIP_TRY(hipGetLastError());
-    int32_t* hm = (int32_t*)hd1;   // reuse pinned space
-    ORB_HIP_TRY(hipMemcpyAsync(hm, m->d_m12, (size_t)f1->n * 4, hipMemcpyDeviceToHost, s));
-    ORB_HIP_TRY(hipMemcpyAsync(hprev, m->d_prev, (size_t)f1->n * 8, hipMemcpyDeviceToHost, s));
-    ORB_HIP_TRY(hipMemcpyAsync(hn, m->d_nm, 4, hipMemcpyDeviceToHost, s));
-    ORB_HIP_TRY(hipMemcpyAsync(hn + 1, m->d_status, 4, hipMemcpyDeviceToHost, s));
+    if (int e_ = sg.download(s, dPrev)) return e_;
     ORB_HIP_TRY(hipStreamSynchronize(s));
-    if (hn[1]) return ORB_EOVERFLOW;
-    std::memcpy(matches12, hm, (size_t)f1->n * 4);
-    std::memcpy(prev_xy, hprev, (size_t)f1->n * 8);
-    return hn[0];
+    if (*sg.host(dSt)) return ORB_EOVERFLOW;
+    std::memcpy(matches12, sg.host(dM12), n1 * 4);
+    std::memcpy(prev_xy, sg.host(dPrev), n1 * 8);
+    return *sg.host(dNm);
 } ORB_ABI_CATCH
 
 int orb_search_for_initialization_batch_device(orb_matcher* m, const orb_keypoint* d_kps1, const uint8_t* d_desc1,
@@ -1738,67 +1737,51 @@ int orb_search_by_projection_frame(orb_matcher* m, const orb_frame_view* cur, co
     c.fx = cam[0]; c.fy = cam[1]; c.cx = cam[2]; c.cy = cam[3]; c.mbf = cam[4]; c.mb = cam[5];
     const int bForward = tlc[2] > c.mb && !mono;
     const int bBackward = -tlc[2] > c.mb && !mono;
-    const size_t bytes = (size_t)cap * (2 * sizeof(orb_keypoint) + 32 + 32 + 4 + 4 + 1 + 12 + 4) + 1024;
-    st = mpin(m, bytes);
+    const size_t nc = (size_t)cur->n, nl = (size_t)last->n;
+    st = mstage(m, Staging::bytes_for({nc * sizeof(orb_keypoint), nl * sizeof(orb_keypoint), nc * 32, nl * 32, nc * 4,
+                                       nl * 12, nl * 4, nl, 48, 128, nc * 4, 8, 4}));
     if (st) return st;
-    char* h = (char*)m->h_pin;
-    orb_keypoint* hkc = (orb_keypoint*)h;
-    orb_keypoint* hkl = hkc + cap;
-    uint8_t* hdc = (uint8_t*)(hkl + cap);
-    uint8_t* hmd = hdc + (size_t)cap * 32;
-    float* hur = (float*)(hmd + (size_t)cap * 32);
-    int32_t* hcm = (int32_t*)(hur + cap);
-    float* hxyz = (float*)(hcm + cap);
-    int32_t* hhas = (int32_t*)(hxyz + 3 * (size_t)cap);
-    uint8_t* hout = (uint8_t*)(hhas + cap);
-    float* hT = (float*)(((uintptr_t)(hout + cap) + 15) & ~(uintptr_t)15);
-    float* hsf = hT + 16;
-    int32_t* hn = (int32_t*)(hsf + 32);
-    pack_view(cur, hkc);
-    pack_view(last, hkl);
-    std::memcpy(hdc, cur->desc, (size_t)cur->n * 32);
-    std::memcpy(hmd, last_mp_desc, (size_t)last->n * 32);
-    for (int i = 0; i < cur->n; i++) hur[i] = cur->uright ? cur->uright[i] : -1.f;
-    std::memcpy(hcm, cur_mp, (size_t)cur->n * 4);
-    std::memcpy(hxyz, last_mp_xyz, (size_t)last->n * 12);
-    std::memcpy(hhas, last_has_mp, (size_t)last->n * 4);
-    std::memcpy(hout, last_outlier, (size_t)last->n);
-    std::memcpy(hT, Tcw_cur, 12 * 4);
+    hipStream_t s = m->stream;
+    Staging sg(&m->hs);   // one H2D of the inputs, one D2H of matches / status / count
+    char* hp;
+    auto* dKc = (orb_keypoint*)sg.in_place(nc * sizeof(orb_keypoint), &hp);
+    if (hp) pack_view(cur, (orb_keypoint*)hp);
+    auto* dKl = (orb_keypoint*)sg.in_place(nl * sizeof(orb_keypoint), &hp);
+    if (hp) pack_view(last, (orb_keypoint*)hp);
+    auto* dDc = (uint8_t*)sg.in(cur->desc, nc * 32);
+    auto* dMd = (uint8_t*)sg.in(last_mp_desc, nl * 32);
+    auto* dUr = (float*)sg.in_place(nc * 4, &hp);
+    if (hp)
+        for (size_t i = 0; i < nc; i++) ((float*)hp)[i] = cur->uright ? cur->uright[i] : -1.f;
+    auto* dXyz = (float*)sg.in(last_mp_xyz, nl * 12);
+    auto* dHas = (int32_t*)sg.in(last_has_mp, nl * 4);
+    auto* dOut = (uint8_t*)sg.in(last_outlier, nl);
+    auto* dT = (float*)sg.in(Tcw_cur, 48);
     int maxOct = 0;
     for (int i = 0; i < last->n; i++) maxOct = std::max(maxOct, (int)last->octave[i]);
-    for (int i = 0; i <= maxOct && i < 32; i++) hsf[i] = scale_factors[i];
-    hipStream_t s = m->stream;
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_k2, hkc, (size_t)cur->n * sizeof(orb_keypoint), hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_k1, hkl, (size_t)last->n * sizeof(orb_keypoint), hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_d2, hdc, (size_t)cur->n * 32, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_mpd, hmd, (size_t)last->n * 32, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_ur, hur, (size_t)cur->n * 4, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_m12, hcm, (size_t)cur->n * 4, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_xyz, hxyz, (size_t)last->n * 12, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_hasMp, hhas, (size_t)last->n * 4, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_outl, hout, (size_t)last->n, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_T, hT, 12 * 4, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_sf, hsf, 32 * 4, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemsetAsync(m->d_status, 0, 4, s));
+    float sf[32] = {0.f};
+    for (int i = 0; i <= maxOct && i < 32; i++) sf[i] = scale_factors[i];
+    auto* dSf = (float*)sg.in(sf, 128);
+    auto* dM12 = (int32_t*)sg.in(cur_mp, nc * 4);
+    const int32_t zero[2] = {0, 0};
+    auto* dSt = (int32_t*)sg.in(zero, 8);
+    auto* dNm = (int32_t*)sg.out(4);
+    if (int e_ = sg.upload(s)) return e_;
     const GridParams g = grid_of(cur);
     if (last->n > 0) {
-        hipLaunchKernelGGL(k_cand_sbp, dim3((last->n + 3) / 4), dim3(256), 0, s, m->d_k2, m->d_d2,
-                           cur->uright ? (const float*)m->d_ur : (const float*)nullptr, cur->n, m->d_k1, last->n,
-                           m->d_hasMp, m->d_outl, m->d_xyz, m->d_mpd, m->d_T, m->d_sf, c, g, th, bForward, bBackward,
-                           m->d_cand, m->d_ncand, m->d_status);
+        hipLaunchKernelGGL(k_cand_sbp, dim3((last->n + 3) / 4), dim3(256), 0, s, dKc, dDc,
+                           cur->uright ? (const float*)dUr : (const float*)nullptr, cur->n, dKl, last->n, dHas, dOut,
+                           dXyz, dMd, dT, dSf, c, g, th, bForward, bBackward, m->d_cand, m->d_ncand, dSt);
     }
     const size_t lds = ((size_t)cur->n + kHisto + 4) * 4;
-    hipLaunchKernelGGL(k_resolve_sbp, dim3(1), dim3(64), lds, s, m->d_k2, cur->n, m->d_k1, last->n, g, m->checkOri,
-                       m->d_cand, m->d_ncand, m->d_m12, m->d_nm, m->d_hI, m->d_hB, kThHigh,
-                       (const int32_t*)m->d_hasMp);
+    hipLaunchKernelGGL(k_resolve_sbp, dim3(1), dim3(64), lds, s, dKc, cur->n, dKl, last->n, g, m->checkOri, m->d_cand,
+                       m->d_ncand, dM12, dNm, m->d_hI, m->d_hB, kThHigh, (const int32_t*)dHas);
     ORB_HIP_TRY(hipGetLastError());
-    ORB_HIP_TRY(hipMemcpyAsync(hcm, m->d_m12, (size_t)cur->n * 4, hipMemcpyDeviceToHost, s));
-    ORB_HIP_TRY(hipMemcpyAsync(hn, m->d_nm, 4, hipMemcpyDeviceToHost, s));
-    ORB_HIP_TRY(hipMemcpyAsync(hn + 1, m->d_status, 4, hipMemcpyDeviceToHost, s));
+    if (int e_ = sg.download(s, dM12)) return e_;
     ORB_HIP_TRY(hipStreamSynchronize(s));
-    if (hn[1]) return ORB_EOVERFLOW;
-    std::memcpy(cur_mp, hcm, (size_t)cur->n * 4);
-    return hn[0];
+    if (*sg.host(dSt)) return ORB_EOVERFLOW;
+    std::memcpy(cur_mp, sg.host(dM12), nc * 4);
+    return *sg.host(dNm);
 } ORB_ABI_CATCH
 
 int orb_search_by_projection_kf(orb_matcher* m, const orb_frame_view* cur, const float* Tcw_cur, const float Ow[3],
@@ -1823,59 +1806,42 @@ int orb_search_by_projection_kf(orb_matcher* m, const orb_frame_view* cur, const
     P.nlev = n_levels;
     for (int l = 0; l < 32; l++) P.sf[l] = l < n_levels ? scale_factors[l] : 0.f;
     P.th = th;
-    const size_t bytes = (size_t)cap * (2 * sizeof(orb_keypoint) + 32 + 32 + 4 + 12 + 4 + 4 + 1) + 1024;
-    st = mpin(m, bytes);
+    const size_t nc = (size_t)cur->n, nk = (size_t)nmp;
+    st = mstage(m, Staging::bytes_for({nc * sizeof(orb_keypoint), nk * sizeof(orb_keypoint), nc * 32, nk * 32, nk * 12,
+                                       nk * 4, nk * 4, nk, nc * 4, 8, 4}));
     if (st) return st;
-    char* h = (char*)m->h_pin;
-    orb_keypoint* hkc = (orb_keypoint*)h;
-    orb_keypoint* hkl = hkc + cap;
-    uint8_t* hdc = (uint8_t*)(hkl + cap);
-    uint8_t* hmd = hdc + (size_t)cap * 32;
-    int32_t* hcm = (int32_t*)(hmd + (size_t)cap * 32);
-    float* hxyz = (float*)(hcm + cap);
-    float* hmin = hxyz + 3 * (size_t)cap;
-    float* hmax = hmin + cap;
-    uint8_t* hval = (uint8_t*)(hmax + cap);
-    int32_t* hn = (int32_t*)(((uintptr_t)(hval + cap) + 15) & ~(uintptr_t)15);
-    pack_view(cur, hkc);
-    pack_view(kf, hkl);
-    std::memcpy(hdc, cur->desc, (size_t)cur->n * 32);
-    std::memcpy(hmd, mp_desc, (size_t)nmp * 32);
-    std::memcpy(hcm, cur_mp, (size_t)cur->n * 4);
-    std::memcpy(hxyz, mp_xyz, (size_t)nmp * 12);
-    std::memcpy(hmin, mp_min_dist, (size_t)nmp * 4);
-    std::memcpy(hmax, mp_max_dist, (size_t)nmp * 4);
-    std::memcpy(hval, mp_valid, (size_t)nmp);
-    // scratch: the keyframe-side buffers of the frame-to-frame form (xyz, outlier = valid,
-    // hasMp = min distance, ur = max distance), all sized for cap entries by mensure
     hipStream_t s = m->stream;
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_k2, hkc, (size_t)cur->n * sizeof(orb_keypoint), hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_k1, hkl, (size_t)nmp * sizeof(orb_keypoint), hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_d2, hdc, (size_t)cur->n * 32, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_mpd, hmd, (size_t)nmp * 32, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_m12, hcm, (size_t)cur->n * 4, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_xyz, hxyz, (size_t)nmp * 12, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_hasMp, hmin, (size_t)nmp * 4, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_ur, hmax, (size_t)nmp * 4, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_outl, hval, (size_t)nmp, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemsetAsync(m->d_status, 0, 4, s));
+    Staging sg(&m->hs);   // one H2D of the inputs, one D2H of matches / status / count
+    char* hp;
+    auto* dKc = (orb_keypoint*)sg.in_place(nc * sizeof(orb_keypoint), &hp);
+    if (hp) pack_view(cur, (orb_keypoint*)hp);
+    auto* dKk = (orb_keypoint*)sg.in_place(nk * sizeof(orb_keypoint), &hp);
+    if (hp) pack_view(kf, (orb_keypoint*)hp);
+    auto* dDc = (uint8_t*)sg.in(cur->desc, nc * 32);
+    auto* dMd = (uint8_t*)sg.in(mp_desc, nk * 32);
+    auto* dXyz = (float*)sg.in(mp_xyz, nk * 12);
+    auto* dMin = (float*)sg.in(mp_min_dist, nk * 4);
+    auto* dMax = (float*)sg.in(mp_max_dist, nk * 4);
+    auto* dVal = (uint8_t*)sg.in(mp_valid, nk);
+    auto* dM12 = (int32_t*)sg.in(cur_mp, nc * 4);
+    const int32_t zero[2] = {0, 0};
+    auto* dSt = (int32_t*)sg.in(zero, 8);
+    auto* dNm = (int32_t*)sg.out(4);
+    if (int e_ = sg.upload(s)) return e_;
     const GridParams g = grid_of(cur);
     if (nmp > 0) {
-        hipLaunchKernelGGL(k_cand_sbk, dim3((nmp + 3) / 4), dim3(256), 0, s, m->d_k2, m->d_d2, cur->n, nmp, m->d_outl,
-                           m->d_xyz, (const float*)m->d_hasMp, (const float*)m->d_ur, m->d_mpd, P, g, m->d_cand,
-                           m->d_ncand, m->d_status);
+        hipLaunchKernelGGL(k_cand_sbk, dim3((nmp + 3) / 4), dim3(256), 0, s, dKc, dDc, cur->n, nmp, dVal, dXyz,
+                           (const float*)dMin, (const float*)dMax, dMd, P, g, m->d_cand, m->d_ncand, dSt);
     }
     const size_t lds = ((size_t)cur->n + kHisto + 4) * 4;
-    hipLaunchKernelGGL(k_resolve_sbp, dim3(1), dim3(64), lds, s, m->d_k2, cur->n, m->d_k1, nmp, g, m->checkOri,
-                       m->d_cand, m->d_ncand, m->d_m12, m->d_nm, m->d_hI, m->d_hB, orb_dist, (const int32_t*)nullptr);
+    hipLaunchKernelGGL(k_resolve_sbp, dim3(1), dim3(64), lds, s, dKc, cur->n, dKk, nmp, g, m->checkOri, m->d_cand,
+                       m->d_ncand, dM12, dNm, m->d_hI, m->d_hB, orb_dist, (const int32_t*)nullptr);
     ORB_HIP_TRY(hipGetLastError());
-    ORB_HIP_TRY(hipMemcpyAsync(hcm, m->d_m12, (size_t)cur->n * 4, hipMemcpyDeviceToHost, s));
-    ORB_HIP_TRY(hipMemcpyAsync(hn, m->d_nm, 4, hipMemcpyDeviceToHost, s));
-    ORB_HIP_TRY(hipMemcpyAsync(hn + 1, m->d_status, 4, hipMemcpyDeviceToHost, s));
+    if (int e_ = sg.download(s, dM12)) return e_;
     ORB_HIP_TRY(hipStreamSynchronize(s));
-    if (hn[1]) return ORB_EOVERFLOW;
-    std::memcpy(cur_mp, hcm, (size_t)cur->n * 4);
-    return hn[0];
+    if (*sg.host(dSt)) return ORB_EOVERFLOW;
+    std::memcpy(cur_mp, sg.host(dM12), nc * 4);
+    return *sg.host(dNm);
 } ORB_ABI_CATCH
 
 int orb_search_by_projection_sim3(orb_matcher* m, const orb_frame_view* kf, const orb_kf_params* kp, int n_mp,
@@ -1899,58 +1865,42 @@ int orb_search_by_projection_sim3(orb_matcher* m, const orb_frame_view* kf, cons
         K.sf[l] = l < kp->n_levels ? kp->scale_factors[l] : 0.f;
         K.isig2[l] = 0.f;
     }
-    const size_t bytes = (size_t)cap * (sizeof(orb_keypoint) + 32 + 32 + 4 + 12 + 12 + 4 + 4 + 1) + 1024;
-    st = mpin(m, bytes);
+    const size_t nk = (size_t)kf->n, np = (size_t)n_mp;
+    st = mstage(m, Staging::bytes_for({nk * sizeof(orb_keypoint), nk * 32, np * 32, np * 12, np * 12, np * 4, np * 4, np,
+                                       nk * 4, 8, 4}));
     if (st) return st;
-    char* h = (char*)m->h_pin;
-    orb_keypoint* hk = (orb_keypoint*)h;
-    uint8_t* hd = (uint8_t*)(hk + cap);
-    uint8_t* hmd = hd + (size_t)cap * 32;
-    int32_t* hm = (int32_t*)(hmd + (size_t)cap * 32);
-    float* hxyz = (float*)(hm + cap);
-    float* hnrm = hxyz + 3 * (size_t)cap;
-    float* hmin = hnrm + 3 * (size_t)cap;
-    float* hmax = hmin + cap;
-    uint8_t* hval = (uint8_t*)(hmax + cap);
-    int32_t* hn = (int32_t*)(((uintptr_t)(hval + cap) + 15) & ~(uintptr_t)15);
-    pack_view(kf, hk);
-    std::memcpy(hd, kf->desc, (size_t)kf->n * 32);
-    std::memcpy(hmd, mp_desc, (size_t)n_mp * 32);
-    std::memcpy(hm, matched, (size_t)kf->n * 4);
-    std::memcpy(hxyz, mp_xyz, (size_t)n_mp * 12);
-    std::memcpy(hnrm, mp_normal, (size_t)n_mp * 12);
-    std::memcpy(hmin, mp_min_dist, (size_t)n_mp * 4);
-    std::memcpy(hmax, mp_max_dist, (size_t)n_mp * 4);
-    std::memcpy(hval, mp_valid, (size_t)n_mp);
-    // scratch: d_d1 (32 B per entry) holds the normals, d_hasMp / d_ur the min / max distances
     hipStream_t s = m->stream;
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_k2, hk, (size_t)kf->n * sizeof(orb_keypoint), hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_d2, hd, (size_t)kf->n * 32, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_mpd, hmd, (size_t)n_mp * 32, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_m12, hm, (size_t)kf->n * 4, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_xyz, hxyz, (size_t)n_mp * 12, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_d1, hnrm, (size_t)n_mp * 12, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_hasMp, hmin, (size_t)n_mp * 4, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_ur, hmax, (size_t)n_mp * 4, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_outl, hval, (size_t)n_mp, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemsetAsync(m->d_status, 0, 4, s));
+    Staging sg(&m->hs);   // one H2D of the inputs, one D2H of matches / status / count
+    char* hp;
+    auto* dK = (orb_keypoint*)sg.in_place(nk * sizeof(orb_keypoint), &hp);
+    if (hp) pack_view(kf, (orb_keypoint*)hp);
+    auto* dD = (uint8_t*)sg.in(kf->desc, nk * 32);
+    auto* dMd = (uint8_t*)sg.in(mp_desc, np * 32);
+    auto* dXyz = (float*)sg.in(mp_xyz, np * 12);
+    auto* dNrm = (float*)sg.in(mp_normal, np * 12);
+    auto* dMin = (float*)sg.in(mp_min_dist, np * 4);
+    auto* dMax = (float*)sg.in(mp_max_dist, np * 4);
+    auto* dVal = (uint8_t*)sg.in(mp_valid, np);
+    auto* dM = (int32_t*)sg.in(matched, nk * 4);
+    const int32_t zero[2] = {0, 0};
+    auto* dSt = (int32_t*)sg.in(zero, 8);
+    auto* dNm = (int32_t*)sg.out(4);
+    if (int e_ = sg.upload(s)) return e_;
     const GridParams g = grid_of(kf);
     if (n_mp > 0) {
-        hipLaunchKernelGGL(k_cand_sbs, dim3((n_mp + 3) / 4), dim3(256), 0, s, m->d_k2, m->d_d2, kf->n, g, K, n_mp,
-                           m->d_outl, m->d_xyz, (const float*)m->d_d1, (const float*)m->d_hasMp,
-                           (const float*)m->d_ur, m->d_mpd, th, m->d_cand, m->d_ncand, m->d_status);
+        hipLaunchKernelGGL(k_cand_sbs, dim3((n_mp + 3) / 4), dim3(256), 0, s, dK, dD, kf->n, g, K, n_mp, dVal, dXyz,
+                           (const float*)dNrm, (const float*)dMin, (const float*)dMax, dMd, th, m->d_cand, m->d_ncand,
+                           dSt);
     }
     const size_t lds = ((size_t)kf->n + kHisto + 4) * 4;
-    hipLaunchKernelGGL(k_resolve_sbp, dim3(1), dim3(64), lds, s, m->d_k2, kf->n, m->d_k2, n_mp, g, 0, m->d_cand,
-                       m->d_ncand, m->d_m12, m->d_nm, m->d_hI, m->d_hB, kThLow, (const int32_t*)nullptr);
+    hipLaunchKernelGGL(k_resolve_sbp, dim3(1), dim3(64), lds, s, dK, kf->n, dK, n_mp, g, 0, m->d_cand, m->d_ncand, dM,
+                       dNm, m->d_hI, m->d_hB, kThLow, (const int32_t*)nullptr);
     ORB_HIP_TRY(hipGetLastError());
-    ORB_HIP_TRY(hipMemcpyAsync(hm, m->d_m12, (size_t)kf->n * 4, hipMemcpyDeviceToHost, s));
-    ORB_HIP_TRY(hipMemcpyAsync(hn, m->d_nm, 4, hipMemcpyDeviceToHost, s));
-    ORB_HIP_TRY(hipMemcpyAsync(hn + 1, m->d_status, 4, hipMemcpyDeviceToHost, s));
+    if (int e_ = sg.download(s, dM)) return e_;
     ORB_HIP_TRY(hipStreamSynchronize(s));
-    if (hn[1]) return ORB_EOVERFLOW;
-    std::memcpy(matched, hm, (size_t)kf->n * 4);
-    return hn[0];
+    if (*sg.host(dSt)) return ORB_EOVERFLOW;
+    std::memcpy(matched, sg.host(dM), nk * 4);
+    return *sg.host(dNm);
 } ORB_ABI_CATCH
 
 int orb_search_by_projection_local(orb_matcher* m, const orb_frame_view* f, int n_mp, const uint8_t* mp_in_view,
@@ -1974,66 +1924,45 @@ int orb_search_by_projection_local(orb_matcher* m, const orb_frame_view* f, int 
     if (st) return st;
     const size_t lds = (size_t)2 * f->n * 4;
     if (lds > 65536) return ORB_E2BIG;
-    const size_t bytes = (size_t)f->n * (sizeof(orb_keypoint) + 32 + 4 + 4) + (size_t)n_mp * (1 + 12 + 4 + 4 + 32 + 1) +
-                         32 * 4 + 1024;
-    st = mpin(m, bytes);
+    const size_t nf = (size_t)f->n, np = (size_t)n_mp;
+    st = mstage(m, Staging::bytes_for({nf * sizeof(orb_keypoint), nf * 32, nf * 4, np * 12, np * 4, np * 4, 128, np * 32,
+                                       np, np, nf * 4, 8, 4}));
     if (st) return st;
-    char* h = (char*)m->h_pin;
-    orb_keypoint* hk = (orb_keypoint*)h;
-    uint8_t* hd = (uint8_t*)(hk + f->n);
-    float* hur = (float*)(hd + (size_t)f->n * 32);
-    int32_t* hcm = (int32_t*)(hur + f->n);
-    float* hproj = (float*)(hcm + f->n);
-    int32_t* hlvl = (int32_t*)(hproj + 3 * (size_t)n_mp);
-    float* hcos = (float*)(hlvl + n_mp);
-    float* hsf = hcos + n_mp;
-    int32_t* hn = (int32_t*)(hsf + 32);
-    uint8_t* hmd = (uint8_t*)(hn + 4);
-    uint8_t* hin = hmd + (size_t)n_mp * 32;
-    uint8_t* hobs = hin + n_mp;
-    pack_view(f, hk);
-    std::memcpy(hd, f->desc, (size_t)f->n * 32);
-    for (int i = 0; i < f->n; i++) hur[i] = f->uright ? f->uright[i] : -1.f;
-    std::memcpy(hcm, cur_mp, (size_t)f->n * 4);
-    std::memcpy(hproj, mp_proj, (size_t)n_mp * 12);
-    std::memcpy(hlvl, mp_level, (size_t)n_mp * 4);
-    std::memcpy(hcos, mp_view_cos, (size_t)n_mp * 4);
-    for (int i = 0; i <= maxLevel && i < 32; i++) hsf[i] = scale_factors[i];
-    std::memcpy(hmd, mp_desc, (size_t)n_mp * 32);
-    std::memcpy(hin, mp_in_view, (size_t)n_mp);
-    std::memcpy(hobs, mp_has_obs, (size_t)n_mp);
     hipStream_t s = m->stream;
-    // device layout reuses the matcher scratch: current frame in k2 / d2 / ur / m12, map points in
-    // xyz (projections), hasMp (levels), T (view cos, when it fits) and mpd (descriptors)
-    float* d_cos = (float*)m->d_prev;   // >= 8 bytes per slot
-    uint8_t* d_in = m->d_outl;
-    uint8_t* d_obs = m->d_hB;
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_k2, hk, (size_t)f->n * sizeof(orb_keypoint), hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_d2, hd, (size_t)f->n * 32, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_ur, hur, (size_t)f->n * 4, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_m12, hcm, (size_t)f->n * 4, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_xyz, hproj, (size_t)n_mp * 12, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_hasMp, hlvl, (size_t)n_mp * 4, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(d_cos, hcos, (size_t)n_mp * 4, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_sf, hsf, 32 * 4, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_mpd, hmd, (size_t)n_mp * 32, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(d_in, hin, (size_t)n_mp, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(d_obs, hobs, (size_t)n_mp, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemsetAsync(m->d_status, 0, 4, s));
+    Staging sg(&m->hs);   // one H2D of the inputs, one D2H of matches / status / count
+    char* hp;
+    auto* dK = (orb_keypoint*)sg.in_place(nf * sizeof(orb_keypoint), &hp);
+    if (hp) pack_view(f, (orb_keypoint*)hp);
+    auto* dD = (uint8_t*)sg.in(f->desc, nf * 32);
+    auto* dUr = (float*)sg.in_place(nf * 4, &hp);
+    if (hp)
+        for (size_t i = 0; i < nf; i++) ((float*)hp)[i] = f->uright ? f->uright[i] : -1.f;
+    auto* dProj = (float*)sg.in(mp_proj, np * 12);
+    auto* dLvl = (int32_t*)sg.in(mp_level, np * 4);
+    auto* dCos = (float*)sg.in(mp_view_cos, np * 4);
+    float sf[32] = {0.f};
+    for (int i = 0; i <= maxLevel && i < 32; i++) sf[i] = scale_factors[i];
+    auto* dSf = (float*)sg.in(sf, 128);
+    auto* dMd = (uint8_t*)sg.in(mp_desc, np * 32);
+    auto* dIn = (uint8_t*)sg.in(mp_in_view, np);
+    auto* dObs = (uint8_t*)sg.in(mp_has_obs, np);
+    auto* dM12 = (int32_t*)sg.in(cur_mp, nf * 4);
+    const int32_t zero[2] = {0, 0};
+    auto* dSt = (int32_t*)sg.in(zero, 8);
+    auto* dNm = (int32_t*)sg.out(4);
+    if (int e_ = sg.upload(s)) return e_;
     const GridParams g = grid_of(f);
-    hipLaunchKernelGGL(k_cand_sbl, dim3((n_mp + 3) / 4), dim3(256), 0, s, m->d_k2, m->d_d2,
-                       f->uright ? (const float*)m->d_ur : (const float*)nullptr, f->n, n_mp, d_in, m->d_xyz,
-                       m->d_hasMp, d_cos, m->d_mpd, m->d_sf, g, th, m->d_cand, m->d_ncand, m->d_status);
-    hipLaunchKernelGGL(k_resolve_sbl, dim3(1), dim3(64), lds, s, m->d_k2, f->n, n_mp, g, m->nnratio, d_obs, m->d_cand,
-                       m->d_ncand, m->d_m12, m->d_nm);
+    hipLaunchKernelGGL(k_cand_sbl, dim3((n_mp + 3) / 4), dim3(256), 0, s, dK, dD,
+                       f->uright ? (const float*)dUr : (const float*)nullptr, f->n, n_mp, dIn, dProj, dLvl, dCos, dMd,
+                       dSf, g, th, m->d_cand, m->d_ncand, dSt);
+    hipLaunchKernelGGL(k_resolve_sbl, dim3(1), dim3(64), lds, s, dK, f->n, n_mp, g, m->nnratio, dObs, m->d_cand,
+                       m->d_ncand, dM12, dNm);
     ORB_HIP_TRY(hipGetLastError());
-    ORB_HIP_TRY(hipMemcpyAsync(hcm, m->d_m12, (size_t)f->n * 4, hipMemcpyDeviceToHost, s));
-    ORB_HIP_TRY(hipMemcpyAsync(hn, m->d_nm, 4, hipMemcpyDeviceToHost, s));
-    ORB_HIP_TRY(hipMemcpyAsync(hn + 1, m->d_status, 4, hipMemcpyDeviceToHost, s));
+    if (int e_ = sg.download(s, dM12)) return e_;
     ORB_HIP_TRY(hipStreamSynchronize(s));
-    if (hn[1]) return ORB_EOVERFLOW;
-    std::memcpy(cur_mp, hcm, (size_t)f->n * 4);
-    return hn[0];
+    if (*sg.host(dSt)) return ORB_EOVERFLOW;
+    std::memcpy(cur_mp, sg.host(dM12), nf * 4);
+    return *sg.host(dNm);
 } ORB_ABI_CATCH
 
 int orb_hamming_knn2(orb_matcher* m, const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* best_idx,
@@ -2042,35 +1971,26 @@ int orb_hamming_knn2(orb_matcher* m, const uint8_t* q, int nq, const uint8_t* t,
     if (nq == 0) return ORB_OK;
     ORB_HIP_TRY(hipSetDevice(m->device));
     const int cap = std::max(std::max(nq, nt), 1);
-    int st = mensure(m, 1, cap);
+    const size_t bq = (size_t)nq * 4;
+    int st = mstage(m, Staging::bytes_for({(size_t)nq * 32, (size_t)nt * 32, 8, bq, bq, bq}));
     if (st) return st;
-    st = mpin(m, (size_t)cap * 64 + (size_t)nq * 12 + 64);
-    if (st) return st;
-    uint8_t* hq = (uint8_t*)m->h_pin;
-    uint8_t* ht = hq + (size_t)cap * 32;
-    int32_t* hn = (int32_t*)(ht + (size_t)cap * 32);
-    int32_t* hout = hn + 4;
-    std::memcpy(hq, q, (size_t)nq * 32);
-    if (nt) std::memcpy(ht, t, (size_t)nt * 32);
-    hn[0] = nq;
-    hn[1] = nt;
     hipStream_t s = m->stream;
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_d1, hq, (size_t)nq * 32, hipMemcpyHostToDevice, s));
-    if (nt) ORB_HIP_TRY(hipMemcpyAsync(m->d_d2, ht, (size_t)nt * 32, hipMemcpyHostToDevice, s));
-    ORB_HIP_TRY(hipMemcpyAsync(m->d_n, hn, 8, hipMemcpyHostToDevice, s));
-    int32_t* d_bi = m->d_m12;
-    int32_t* d_bd = m->d_hI;
-    int32_t* d_sd = (int32_t*)m->d_ncand;
-    hipLaunchKernelGGL(k_knn2, dim3((nq + 3) / 4, 1), dim3(256), 0, s, m->d_d1, m->d_n, m->d_d2, m->d_n + 1, cap, cap,
-                       d_bi, d_bd, d_sd);
+    Staging sg(&m->hs);   // one H2D of both descriptor sets, one D2H of the three outputs
+    auto* dQ = (uint8_t*)sg.in(q, (size_t)nq * 32);
+    auto* dT = (uint8_t*)sg.in(t, (size_t)nt * 32);
+    const int32_t nn[2] = {nq, nt};
+    auto* dN = (int32_t*)sg.in(nn, 8);
+    auto* dBi = (int32_t*)sg.out(bq);
+    auto* dBd = (int32_t*)sg.out(bq);
+    auto* dSd = (int32_t*)sg.out(bq);
+    if (int e_ = sg.upload(s)) return e_;
+    hipLaunchKernelGGL(k_knn2, dim3((nq + 3) / 4, 1), dim3(256), 0, s, dQ, dN, dT, dN + 1, cap, cap, dBi, dBd, dSd);
     ORB_HIP_TRY(hipGetLastError());
-    ORB_HIP_TRY(hipMemcpyAsync(hout, d_bi, (size_t)nq * 4, hipMemcpyDeviceToHost, s));
-    ORB_HIP_TRY(hipMemcpyAsync(hout + nq, d_bd, (size_t)nq * 4, hipMemcpyDeviceToHost, s));
-    ORB_HIP_TRY(hipMemcpyAsync(hout + 2 * (size_t)nq, d_sd, (size_t)nq * 4, hipMemcpyDeviceToHost, s));
+    if (int e_ = sg.download(s, dBi)) return e_;
     ORB_HIP_TRY(hipStreamSynchronize(s));
-    std::memcpy(best_idx, hout, (size_t)nq * 4);
-    std::memcpy(best_d, hout + nq, (size_t)nq * 4);
-    std::memcpy(second_d, hout + 2 * (size_t)nq, (size_t)nq * 4);
+    std::memcpy(best_idx, sg.host(dBi), bq);
+    std::memcpy(best_d, sg.host(dBd), bq);
+    std::memcpy(second_d, sg.host(dSd), bq);
     return ORB_OK;
 } ORB_ABI_CATCH
 

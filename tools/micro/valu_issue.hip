@@ -14,6 +14,8 @@
 //     long enough and the workgroups are co-resident.
 // The ops are the extraction kernels' integer mix (v_perm, v_alignbyte, v_lerp_u8, v_dot4_u32_u8,
 // v_bcnt, v_pk_minimum3_f16, v_xad_u32) and the f32 references (v_fma_f32, v_pk_fma_f32).
+// Each op runs with 8 U instructions per loop trip, U = 1, 4, 16 (64 / 256 / 1024 bytes of VOP3 per
+// trip): a rate that falls with U is bound by instruction fetch, not by the SIMD's issue.
 // Usage: valu_issue [iters]   (default 65536: ~8x round 4's loop, >= 4 ms per launch at 8 waves/SIMD)
 #include <hip/hip_runtime.h>
 
@@ -27,7 +29,7 @@ constexpr int kStride = 24;   // per workgroup: memtime start / end, realtime st
 static const char* kNames[kOps] = {"v_fma_f32",      "v_pk_fma_f32",  "v_xad_u32",       "v_perm_b32",        "v_alignbyte_b32",
                                    "v_lerp_u8",      "v_dot4_u32_u8", "v_bcnt_u32_b32",  "v_pk_minimum3_f16"};
 
-template <int OP>
+template <int OP, int U>
 __global__ __launch_bounds__(256) void k_issue(const float* in, float* out, unsigned long long* stamps, int iters) {
     float a[8];
     typedef float f2 __attribute__((ext_vector_type(2)));
@@ -49,12 +51,13 @@ __global__ __launch_bounds__(256) void k_issue(const float* in, float* out, unsi
         r0 = __builtin_amdgcn_s_memrealtime();
         stamps[kStride * blockIdx.x + 6] = r0;
     }
-    const int chunk = iters / 16;
-    for (int i = 0; i < iters; i++) {
-        if (threadIdx.x == 0 && i > 0 && i % chunk == 0 && i / chunk < 16)
-            stamps[kStride * blockIdx.x + 6 + i / chunk] = __builtin_amdgcn_s_memrealtime();
+    const int chunk = iters / 16;   // iters is a multiple of 64
+    for (int c = 0; c < 16; c++) {
+        if (c > 0 && threadIdx.x == 0) stamps[kStride * blockIdx.x + 6 + c] = __builtin_amdgcn_s_memrealtime();
+    for (int i = 0; i < chunk; i += U) {   // 8 U instructions of the op per trip, 3 loop SALU
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
+        for (int kk = 0; kk < 8 * U; kk++) {
+            const int k = kk & 7;
             if (OP == 0) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(a[k]) : "v"(c), "v"(d));
             if (OP == 1) asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(p[k]) : "v"(pc), "v"(pd));
             if (OP == 2) asm volatile("v_xad_u32 %0, %0, %1, %2" : "+v"(u[k]) : "v"(uc), "v"(ud));
@@ -65,6 +68,7 @@ __global__ __launch_bounds__(256) void k_issue(const float* in, float* out, unsi
             if (OP == 7) asm volatile("v_bcnt_u32_b32 %0, %0, %1" : "+v"(u[k]) : "v"(uc));
             if (OP == 8) asm volatile("v_pk_minimum3_f16 %0, %0, %1, %2" : "+v"(u[k]) : "v"(uc), "v"(ud));
         }
+    }
     }
     if (threadIdx.x == 0) {
         const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
@@ -85,22 +89,24 @@ __global__ __launch_bounds__(256) void k_issue(const float* in, float* out, unsi
 }
 
 typedef void (*KFn)(const float*, float*, unsigned long long*, int);
-static KFn kfn(int op) {
+template <int U>
+static KFn kfn_u(int op) {
     switch (op) {
-        case 0: return k_issue<0>;
-        case 1: return k_issue<1>;
-        case 2: return k_issue<2>;
-        case 3: return k_issue<3>;
-        case 4: return k_issue<4>;
-        case 5: return k_issue<5>;
-        case 6: return k_issue<6>;
-        case 7: return k_issue<7>;
-        default: return k_issue<8>;
+        case 0: return k_issue<0, U>;
+        case 1: return k_issue<1, U>;
+        case 2: return k_issue<2, U>;
+        case 3: return k_issue<3, U>;
+        case 4: return k_issue<4, U>;
+        case 5: return k_issue<5, U>;
+        case 6: return k_issue<6, U>;
+        case 7: return k_issue<7, U>;
+        default: return k_issue<8, U>;
     }
 }
+static KFn kfn(int op, int u) { return u == 1 ? kfn_u<1>(op) : u == 4 ? kfn_u<4>(op) : kfn_u<16>(op); }
 
 int main(int argc, char** argv) {
-    const int iters = argc > 1 ? std::atoi(argv[1]) : 65536;
+    const int iters = (argc > 1 ? std::atoi(argv[1]) : 65536) & ~255;
     int cus = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
     float *in, *out;
@@ -116,16 +122,17 @@ int main(int argc, char** argv) {
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     std::printf("CUs %d, iters %d, 8 independent chains per lane; rates in wave64 instructions\n", cus, iters);
-    std::printf("%-18s %3s %8s %7s %9s | %9s %9s %6s | %11s %11s %6s | %12s %12s\n", "op", "w/S", "wall ms", "GHz",
+    std::printf("%-18s %3s %3s %8s %7s %9s | %9s %9s %6s | %11s %11s %6s | %12s %12s\n", "op", "U", "w/S", "wall ms", "GHz",
                 "coresid", "win ms", "loop ms", "win%", "wall inst/s", "win inst/s", "ratio", "cyc/inst/SIMD",
                 "lane-ops/s");
     for (int op = 0; op < kOps; op++)
+        for (int u : {1, 4, 16})
         for (int k : {1, 2, 4, 8}) {
             const int blocks = cus * k;
             float ms = 0.f;
             for (int rep = 0; rep < 2; rep++) {
                 (void)hipEventRecord(e0);
-                hipLaunchKernelGGL(kfn(op), dim3(blocks), dim3(256), 0, 0, in, out, st, iters);
+                hipLaunchKernelGGL(kfn(op, u), dim3(blocks), dim3(256), 0, 0, in, out, st, iters);
                 (void)hipEventRecord(e1);
                 (void)hipEventSynchronize(e1);
                 (void)hipEventElapsedTime(&ms, e0, e1);
@@ -182,8 +189,8 @@ int main(int argc, char** argv) {
             (void)rateSum;
             const double cycPerInst = winRate > 0 ? cus * 4.0 * ghz * 1e9 / winRate : 0.0;
             const double lanes = op == 1 ? 128.0 : 64.0;
-            std::printf("%-18s %3d %8.3f %7.3f %4d/%-4d | %9.3f %9.3f %5.1f%% | %11.4g %11.4g %6.3f | %12.3f %12.4g\n",
-                        kNames[op], k, ms, ghz, minPeak, used, winMs, loopMs, 100.0 * winMs / ms, wallRate, winRate,
+            std::printf("%-18s %3d %3d %8.3f %7.3f %4d/%-4d | %9.3f %9.3f %5.1f%% | %11.4g %11.4g %6.3f | %12.3f %12.4g\n",
+                        kNames[op], u, k, ms, ghz, minPeak, used, winMs, loopMs, 100.0 * winMs / ms, wallRate, winRate,
                         winRate > 0 ? wallRate / winRate : 0.0, cycPerInst, winRate * lanes);
         }
     return 0;
