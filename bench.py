@@ -1112,9 +1112,9 @@ def bench_routed_calls(args, amd, dev, med, creps=9):
     f1, f2 = Frame(kp_of(k1), k1["desc"], k1["W"], k1["H"]), Frame(kp_of(k2), k2["desc"], k2["W"], k2["H"])
     m = amd.ORBmatcher(0.7, True, device=dev.index or 0)
     size = f"{len(k1['x'])} x {len(k2['x'])} features, {len(fv1)} / {len(fv2)} level-2 nodes"
-    row("search_by_bow_kf_frame", lambda: m.SearchByBoW(f1, k1["has_mp"], fv1, f2, a2),
+    row("search_by_bow_kf_frame", lambda: m.SearchByBoW(f1, k1["has_mp"], a1, f2, a2),
         lambda: O.search_by_bow_frame(k1, k1["has_mp"], a1, k2, a2, 0.7, True), "R/src/Tracking.cpp:1020, 1840", size)
-    row("search_by_bow_kf_kf", lambda: m.SearchByBoWKF(f1, k1["has_mp"], a1, f2, k2["has_mp"], fv2),
+    row("search_by_bow_kf_kf", lambda: m.SearchByBoWKF(f1, k1["has_mp"], a1, f2, k2["has_mp"], a2),
         lambda: O.search_by_bow_kf(k1, k1["has_mp"], a1, k2, k2["has_mp"], a2, 0.7, True), "R/src/LoopClosing.cpp:327", size)
     # SearchForTriangulation
     tp = synth.triangulation_problem()

@@ -752,6 +752,185 @@ __global__ __launch_bounds__(64) void k_resolve_sbp(const orb_keypoint* __restri
     if (lane == 0) *nmatches_out = nmatches;
 }
 
+// The replay above is one wave walking the points in order, three dependent global round trips each
+// (~0.7 us per point: 550-700 us for 800 points).  Its fast form: k_best_sbp finds every point's best
+// candidate against the slot occupancy at entry, all points in parallel (one wave each), and
+// k_resolve_sbp_lds replays with the occupancy, the grid-cell keys and those bests in LDS.  A slot's
+// eligibility only ever goes from true to false during the replay (an assignment makes it ineligible
+// unless the assigned point is a visual-odometry one, lastHas == 2), so a point whose entry-time best
+// slot is still eligible keeps it: the reference's scan over its candidates (R/src/ORBmatcher.cpp:
+// 1640-1671) would pick the same minimum; only a point whose best slot was taken re-scans its list.
+__global__ __launch_bounds__(256) void k_best_sbp(const orb_keypoint* __restrict__ kc, const orb_keypoint* __restrict__ kl,
+                                                  int nl, GridParams g, int checkOri, const uint32_t* __restrict__ cand,
+                                                  const int* __restrict__ ncand, const int32_t* __restrict__ curMp,
+                                                  const int32_t* __restrict__ lastHas,
+                                                  unsigned long long* __restrict__ best) {
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int i = blockIdx.x * 4 + wid;
+    if (i >= nl) return;
+    const int nc = ncand[i];
+    const uint32_t* C = cand + (size_t)i * kMaxCand;
+    unsigned long long acc = ~0ull;
+    for (int c0 = 0; c0 < nc; c0 += 64) {
+        const int c = c0 + lane;
+        unsigned long long key = ~0ull;
+        if (c < nc) {
+            const uint32_t e = C[c];
+            const int j = (int)(e & 0xFFFFFu), d = (int)(e >> 20);
+            const int cm = curMp[j];
+            if (cm == -1 || (lastHas && (cm == -3 || (cm >= 0 && lastHas[cm] == 2)))) {
+                const orb_keypoint k = kc[j];
+                key = ((unsigned long long)(unsigned)d << 40) | ((unsigned long long)(unsigned)grid_cell(g, k.x, k.y) << 20) |
+                      (unsigned long long)(unsigned)j;
+            }
+        }
+        const unsigned long long m = wave_min_u64(key);
+        acc = m < acc ? m : acc;
+    }
+    if (lane == 0) {
+        if (acc != ~0ull && checkOri)   // the rotation bin of this pair rides in bits 56..60
+            acc |= (unsigned long long)rot_bin(kl[i].angle - kc[(int)(acc & 0xFFFFFull)].angle) << 56;
+        best[i] = acc;
+    }
+}
+
+static size_t resolve_sbp_lds_bytes(int ncur, int nl) {
+    return (size_t)nl * (8 + 4 + 1 + 1) + (size_t)ncur * 12 + (kHisto + 8) * 4 + 64;
+}
+
+// The replay, 64 points at a time.  A point whose entry-time best is within the threshold claims its
+// slot; the lowest-indexed claimant of each slot is "clean": no earlier point takes that slot through
+// its own entry-time best, so the clean point keeps it unless an earlier point re-scans onto it.
+// Every other claimant is "dirty" and replays the reference's scan in order against the occupancy so
+// far.  Per batch: the clean points before the next dirty one are applied together (one store each),
+// the dirty one re-scans (wave-parallel over its list); if it lands on a slot whose clean claimant
+// comes later, that claimant turns dirty.  Every point sees exactly the occupancy of the sequential
+// replay (R/src/ORBmatcher.cpp:1640-1671 in point order).  Points whose entry-time best is over the
+// threshold never assign (a re-scan could only find a worse one) and are skipped.
+__global__ __launch_bounds__(64) void k_resolve_sbp_lds(const orb_keypoint* __restrict__ kc, int ncur,
+                                                        const orb_keypoint* __restrict__ kl, int nl, GridParams g,
+                                                        int checkOri, const uint32_t* __restrict__ cand,
+                                                        const int* __restrict__ ncand,
+                                                        const unsigned long long* __restrict__ best,
+                                                        int32_t* __restrict__ curMp, int32_t* __restrict__ nmatches_out,
+                                                        int thDist, const int32_t* __restrict__ lastHas) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long smq[];
+    unsigned long long* bestL = smq;                 // [nl]
+    int* histIdx = (int*)(bestL + nl);               // [nl]
+    int* ckey = histIdx + nl;                        // [ncur]
+    int* cmL = ckey + ncur;                          // [ncur]
+    int* firstL = cmL + ncur;                        // [ncur]
+    int* hcount = firstL + ncur;                     // [kHisto]
+    uint8_t* histBin = (uint8_t*)(hcount + kHisto + 8);   // [nl]
+    uint8_t* dem = histBin + nl;                     // [nl]
+    const int lane = threadIdx.x;
+    for (int j = lane; j < ncur; j += 64) {
+        const orb_keypoint k = kc[j];
+        ckey[j] = grid_cell(g, k.x, k.y);
+        cmL[j] = curMp[j];
+        firstL[j] = 0x7fffffff;
+    }
+    for (int i = lane; i < nl; i += 64) {
+        bestL[i] = best[i];
+        dem[i] = 0;
+    }
+    if (lane < kHisto) hcount[lane] = 0;
+    __syncthreads();
+    auto claims = [&](unsigned long long key) { return key != ~0ull && (int)((key >> 40) & 0xFFFF) <= thDist; };
+    for (int i = lane; i < nl; i += 64) {
+        const unsigned long long key = bestL[i];
+        if (claims(key)) atomicMin(&firstL[(int)(key & 0xFFFFFull)], i);
+    }
+    __syncthreads();
+    auto elig = [&](int cm) { return cm == -1 || (lastHas && (cm == -3 || (cm >= 0 && lastHas[cm] == 2))); };
+    int nmatches = 0, nh = 0;
+    for (int base = 0; base < nl; base += 64) {
+        const int i = base + lane;
+        const unsigned long long key = i < nl ? bestL[i] : ~0ull;
+        const bool cl = claims(key);
+        const int j = (int)(key & 0xFFFFFull);
+        const bool first = cl && firstL[j] == i;
+        int pos = 0;
+        for (;;) {
+            const bool dirty = cl && (!first || dem[i] != 0);
+            const uint64_t D = __ballot(dirty && lane >= pos);
+            const int nd = D ? (int)__builtin_ctzll(D) : 64;
+            // the clean claims in [pos, nd) in one step
+            const bool apply = cl && !dirty && lane >= pos && lane < nd;
+            const uint64_t A = __ballot(apply);
+            if (apply) {
+                cmL[j] = i;
+                if (checkOri) {
+                    const int at = nh + __popcll(A & ((1ull << lane) - 1ull));
+                    histIdx[at] = j;
+                    histBin[at] = (uint8_t)((key >> 56) & 31);
+                }
+            }
+            nmatches += __popcll(A);
+            if (checkOri) nh += __popcll(A);
+            if (nd == 64) break;
+            // the dirty point at lane nd: the reference's scan against the occupancy so far
+            const int id = base + nd;
+            const int nc = ncand[id];
+            const uint32_t* C = cand + (size_t)id * kMaxCand;
+            unsigned long long acc = ~0ull;
+            for (int c0 = 0; c0 < nc; c0 += 64) {
+                const int c = c0 + lane;
+                unsigned long long k2 = ~0ull;
+                if (c < nc) {
+                    const uint32_t e = C[c];
+                    const int jj = (int)(e & 0xFFFFFu), d = (int)(e >> 20);
+                    if (elig(cmL[jj]))
+                        k2 = ((unsigned long long)(unsigned)d << 40) | ((unsigned long long)(unsigned)ckey[jj] << 20) |
+                             (unsigned long long)(unsigned)jj;
+                }
+                const unsigned long long m = wave_min_u64(k2);
+                acc = m < acc ? m : acc;
+            }
+            if (acc != ~0ull && (int)(acc >> 40) <= thDist) {
+                const int js = (int)(acc & 0xFFFFFull);
+                const int fc = firstL[js];   // a later clean claimant of this slot loses it
+                if (lane == 0) {
+                    cmL[js] = id;
+                    if (fc > id && fc < nl) dem[fc] = 1;
+                    if (checkOri) {
+                        histIdx[nh] = js;
+                        histBin[nh] = (uint8_t)rot_bin(kl[id].angle - kc[js].angle);
+                    }
+                }
+                nmatches++;
+                if (checkOri) nh++;
+            }
+            pos = nd + 1;
+        }
+    }
+    __syncthreads();
+    if (checkOri) {
+        for (int e = lane; e < nh; e += 64) atomicAdd(&hcount[histBin[e]], 1);
+        __syncthreads();
+        int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+        for (int b = 0; b < kHisto; b++) {
+            const int c = hcount[b];
+            if (c > max1) { max3 = max2; max2 = max1; max1 = c; ind3 = ind2; ind2 = ind1; ind1 = b; }
+            else if (c > max2) { max3 = max2; max2 = c; ind3 = ind2; ind2 = b; }
+            else if (c > max3) { max3 = c; ind3 = b; }
+        }
+        if ((float)max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+        else if ((float)max3 < 0.1f * (float)max1) { ind3 = -1; }
+        int removed = 0;
+        for (int e = lane; e < nh; e += 64) {
+            const int bin = histBin[e];
+            if (bin == ind1 || bin == ind2 || bin == ind3) continue;
+            cmL[histIdx[e]] = -1;
+            removed++;
+        }
+        nmatches -= wave_reduce_sum_i32(removed);
+        __syncthreads();
+    }
+    for (int j = lane; j < ncur; j += 64) curMp[j] = cmL[j];
+    if (lane == 0) *nmatches_out = nmatches;
+}
+
 // ---------------------------------------------------------------- SearchByProjection(Frame, KeyFrame, set, th, ORBdist)
 
 struct SbkParams {
@@ -1000,6 +1179,7 @@ struct orb_matcher {
     uint8_t* d_hB = nullptr;
     uint32_t* d_cand = nullptr;
     uint32_t* d_topk = nullptr;
+    unsigned long long* d_best = nullptr;   // SBP: each point's best candidate at entry
     int *d_cs = nullptr, *d_gj = nullptr;   // SFI grid buckets
     float2* d_gxy = nullptr;
     int *d_ncand = nullptr, *d_status = nullptr;
@@ -1017,12 +1197,12 @@ struct orb_matcher {
 
 static void mfree(orb_matcher* m) {
     void* ptrs[] = {m->d_k1, m->d_k2, m->d_d1, m->d_d2, m->d_prev, m->d_ur, m->d_n, m->d_m12, m->d_nm, m->d_hI,
-                    m->d_hB, m->d_cand, m->d_topk, m->d_cs, m->d_gj, m->d_gxy, m->d_ncand, m->d_status, m->d_hasMp, m->d_outl, m->d_xyz, m->d_T,
+                    m->d_hB, m->d_cand, m->d_topk, m->d_best, m->d_cs, m->d_gj, m->d_gxy, m->d_ncand, m->d_status, m->d_hasMp, m->d_outl, m->d_xyz, m->d_T,
                     m->d_sf, m->d_mpd};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     m->d_k1 = m->d_k2 = nullptr; m->d_d1 = m->d_d2 = nullptr; m->d_prev = m->d_ur = nullptr;
-    m->d_n = m->d_m12 = m->d_nm = m->d_hI = nullptr; m->d_hB = nullptr; m->d_cand = nullptr; m->d_topk = nullptr;
+    m->d_n = m->d_m12 = m->d_nm = m->d_hI = nullptr; m->d_hB = nullptr; m->d_cand = nullptr; m->d_topk = nullptr; m->d_best = nullptr;
     m->d_cs = m->d_gj = nullptr; m->d_gxy = nullptr;
     m->d_ncand = m->d_status = nullptr; m->d_hasMp = nullptr; m->d_outl = nullptr;
     m->d_xyz = m->d_T = m->d_sf = nullptr; m->d_mpd = nullptr;
@@ -1052,6 +1232,7 @@ static int mensure(orb_matcher* m, size_t pairs, size_t pts) {
     MALLOC(m->d_hB, P);
     MALLOC(m->d_cand, P * kMaxCand * 4);
     MALLOC(m->d_topk, P * kTopK * 4);
+    MALLOC(m->d_best, P * 8);
     MALLOC(m->d_cs, pairs * (kCells + 1) * 4);
     MALLOC(m->d_gj, P * 4);
     MALLOC(m->d_gxy, P * 8);
@@ -1087,6 +1268,23 @@ static int mstage(orb_matcher* m, size_t bytes) {
     m->hs.device = m->device;
     m->hs.stream = m->stream;
     return grow_scratch(&m->hs, bytes);
+}
+
+// Launches the candidate replay: the LDS form when its state fits, else k_resolve_sbp.
+static void launch_resolve_sbp(orb_matcher* m, hipStream_t s, const orb_keypoint* kc, int ncur, const orb_keypoint* kl,
+                               int nl, GridParams g, int checkOri, int32_t* curMp, int32_t* nm, int thDist,
+                               const int32_t* lastHas) {
+    const size_t lds = resolve_sbp_lds_bytes(ncur, nl);
+    static const bool seqOnly = std::getenv("ORB_SBP_SEQ_RESOLVE") != nullptr;   // A/B of the two replays
+    if (nl > 0 && lds <= 65536 && !seqOnly) {
+        hipLaunchKernelGGL(k_best_sbp, dim3((nl + 3) / 4), dim3(256), 0, s, kc, kl, nl, g, checkOri, m->d_cand,
+                           m->d_ncand, curMp, lastHas, m->d_best);
+        hipLaunchKernelGGL(k_resolve_sbp_lds, dim3(1), dim3(64), lds, s, kc, ncur, kl, nl, g, checkOri, m->d_cand,
+                           m->d_ncand, m->d_best, curMp, nm, thDist, lastHas);
+        return;
+    }
+    hipLaunchKernelGGL(k_resolve_sbp, dim3(1), dim3(64), ((size_t)ncur + kHisto + 4) * 4, s, kc, ncur, kl, nl, g,
+                       checkOri, m->d_cand, m->d_ncand, curMp, nm, m->d_hI, m->d_hB, thDist, lastHas);
 }
 
 static GridParams grid_of(const orb_frame_view* f) {
@@ -1773,9 +1971,7 @@ int orb_search_by_projection_frame(orb_matcher* m, const orb_frame_view* cur, co
                            cur->uright ? (const float*)dUr : (const float*)nullptr, cur->n, dKl, last->n, dHas, dOut,
                            dXyz, dMd, dT, dSf, c, g, th, bForward, bBackward, m->d_cand, m->d_ncand, dSt);
     }
-    const size_t lds = ((size_t)cur->n + kHisto + 4) * 4;
-    hipLaunchKernelGGL(k_resolve_sbp, dim3(1), dim3(64), lds, s, dKc, cur->n, dKl, last->n, g, m->checkOri, m->d_cand,
-                       m->d_ncand, dM12, dNm, m->d_hI, m->d_hB, kThHigh, (const int32_t*)dHas);
+    launch_resolve_sbp(m, s, dKc, cur->n, dKl, last->n, g, m->checkOri, dM12, dNm, kThHigh, (const int32_t*)dHas);
     ORB_HIP_TRY(hipGetLastError());
     if (int e_ = sg.download(s, dM12)) return e_;
     ORB_HIP_TRY(hipStreamSynchronize(s));
@@ -1833,9 +2029,7 @@ int orb_search_by_projection_kf(orb_matcher* m, const orb_frame_view* cur, const
         hipLaunchKernelGGL(k_cand_sbk, dim3((nmp + 3) / 4), dim3(256), 0, s, dKc, dDc, cur->n, nmp, dVal, dXyz,
                            (const float*)dMin, (const float*)dMax, dMd, P, g, m->d_cand, m->d_ncand, dSt);
     }
-    const size_t lds = ((size_t)cur->n + kHisto + 4) * 4;
-    hipLaunchKernelGGL(k_resolve_sbp, dim3(1), dim3(64), lds, s, dKc, cur->n, dKk, nmp, g, m->checkOri, m->d_cand,
-                       m->d_ncand, dM12, dNm, m->d_hI, m->d_hB, orb_dist, (const int32_t*)nullptr);
+    launch_resolve_sbp(m, s, dKc, cur->n, dKk, nmp, g, m->checkOri, dM12, dNm, orb_dist, (const int32_t*)nullptr);
     ORB_HIP_TRY(hipGetLastError());
     if (int e_ = sg.download(s, dM12)) return e_;
     ORB_HIP_TRY(hipStreamSynchronize(s));
@@ -1892,9 +2086,7 @@ int orb_search_by_projection_sim3(orb_matcher* m, const orb_frame_view* kf, cons
                            (const float*)dNrm, (const float*)dMin, (const float*)dMax, dMd, th, m->d_cand, m->d_ncand,
                            dSt);
     }
-    const size_t lds = ((size_t)kf->n + kHisto + 4) * 4;
-    hipLaunchKernelGGL(k_resolve_sbp, dim3(1), dim3(64), lds, s, dK, kf->n, dK, n_mp, g, 0, m->d_cand, m->d_ncand, dM,
-                       dNm, m->d_hI, m->d_hB, kThLow, (const int32_t*)nullptr);
+    launch_resolve_sbp(m, s, dK, kf->n, dK, n_mp, g, 0, dM, dNm, kThLow, (const int32_t*)nullptr);
     ORB_HIP_TRY(hipGetLastError());
     if (int e_ = sg.download(s, dM)) return e_;
     ORB_HIP_TRY(hipStreamSynchronize(s));

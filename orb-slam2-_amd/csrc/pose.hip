@@ -12,8 +12,10 @@
 // in a fixed-order workgroup reduction, and every thread then takes the same LM decision on
 // the broadcast sums (the 6x6 LDL^T is solved redundantly per thread).  A batch of frames is
 // one launch (frames of several cameras or sequences); nothing returns to the host between LM
-// trials.  Per-edge state (last error, level, robust flag) lives in the caller-sized device
-// arena, so the stale-error semantics of g2o's e->chi2() after a rejected trial carry over.
+// trials.  Per-edge state (inputs, last error, level, robust flag) stays in registers for frames of
+// up to 1,024 edges (PoEdgesReg: the LM passes touch no memory) and in the caller-sized device
+// arena beyond; either way the stale-error semantics of g2o's e->chi2() after a rejected trial
+// carry over.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -101,77 +103,11 @@ __device__ __forceinline__ double po_block_sum(double v, double* sh) {
     return (sh[0] + sh[1]) + (sh[2] + sh[3]);
 }
 
-// errors + robust chi2 of the active edges at (q, t) (computeActiveErrors + activeRobustChi2)
-__device__ double po_active_chi2(const PoseDev& d, const FrameCam& k, int e0, int e1, const double q[4],
-                                 const double t[3], double* sh) {
-    double s = 0.0;
-    for (int e = e0 + (int)threadIdx.x; e < e1; e += kPoT) {
-        if (d.level[e]) continue;
-        po_error(d, k, e, q, t);
-        double chi = po_chi2(d, e);
-        if (d.robust[e]) {
-            const double delta = po_delta(d, e), dsqr = delta * delta;
-            if (chi > dsqr) chi = 2 * sqrt(chi) * delta - dsqr;
-        }
-        s += chi;
-    }
-    return po_block_sum(s, sh);
-}
-
-// linearizeOplus + BaseUnaryEdge::constructQuadraticForm over the active edges; H (21 upper
-// entries) and b reduced over the workgroup through LDS in a fixed order.
-__device__ void po_build(const PoseDev& d, const FrameCam& k, int e0, int e1, const double q[4], const double t[3],
-                         double (*part)[kPoT + 1], double* res, double H[36], double b[6]) {
-    double acc[27];
-#pragma unroll
-    for (int i = 0; i < 27; i++) acc[i] = 0.0;
+// The 27 per-thread sums (21 upper H entries, 6 of b) reduced over the workgroup through LDS in a
+// fixed order; every thread gets H (full) and b.
+__device__ __forceinline__ void po_reduce27(const double acc[27], double (*part)[kPoT + 1], double* res, double H[36],
+                                            double b[6]) {
     const int tid = threadIdx.x;
-    for (int e = e0 + tid; e < e1; e += kPoT) {
-        if (d.level[e]) continue;
-        double Xc[3];
-        po_transform(q, t, d.xw + 3 * (size_t)e, Xc);
-        const double x = Xc[0], y = Xc[1], invz = 1.0 / Xc[2], invz_2 = invz * invz;
-        const bool st = d.obs[3 * (size_t)e + 2] >= 0;
-        double J[18];
-        J[0] = x * y * invz_2 * k.fx;       J[1] = -(1 + (x * x * invz_2)) * k.fx; J[2] = y * invz * k.fx;
-        J[3] = -invz * k.fx;                J[4] = 0;                              J[5] = x * invz_2 * k.fx;
-        J[6] = (1 + y * y * invz_2) * k.fy; J[7] = -x * y * invz_2 * k.fy;         J[8] = -x * invz * k.fy;
-        J[9] = 0;                           J[10] = -invz * k.fy;                  J[11] = y * invz_2 * k.fy;
-        if (st) {
-            J[12] = J[0] - k.bf * y * invz_2; J[13] = J[1] + k.bf * x * invz_2; J[14] = J[2];
-            J[15] = J[3];                     J[16] = 0;                        J[17] = J[5] - k.bf * invz_2;
-        } else {
-#pragma unroll
-            for (int i = 12; i < 18; i++) J[i] = 0.0;
-        }
-        const double w = d.info[e];
-        const double* er = d.err + 3 * (size_t)e;
-        double rho1 = 1.0;
-        if (d.robust[e]) {
-            const double chi = po_chi2(d, e), delta = po_delta(d, e);
-            if (chi > delta * delta) rho1 = delta / sqrt(chi);
-        }
-        const double W = rho1 * w;
-        double om[3];
-#pragma unroll
-        for (int r = 0; r < 3; r++) om[r] = (r < 2 || st) ? -(w * er[r]) * rho1 : 0.0;
-        // all 3 rows: a monocular edge's third row and om[2] are zero (exact zeros added)
-        int o = 0;
-#pragma unroll
-        for (int i = 0; i < 6; i++) {
-            double s = 0;
-#pragma unroll
-            for (int r = 0; r < 3; r++) s += J[r * 6 + i] * om[r];
-            acc[21 + i] += s;
-#pragma unroll
-            for (int j = i; j < 6; j++) {
-                double h = 0;
-#pragma unroll
-                for (int r = 0; r < 3; r++) h += J[r * 6 + i] * W * J[r * 6 + j];
-                acc[o++] += h;
-            }
-        }
-    }
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < 27; i++) part[i][tid] = acc[i];
@@ -195,6 +131,47 @@ __device__ void po_build(const PoseDev& d, const FrameCam& k, int e0, int e1, co
             o++;
         }
     for (int i = 0; i < 6; i++) b[i] = res[21 + i];
+}
+
+// One active edge's linearizeOplus + constructQuadraticForm added to acc (Xc = the point in the
+// camera, er = its last computed error).
+__device__ __forceinline__ void po_accum_edge(const FrameCam& k, const double Xc[3], bool st, double w, bool robust,
+                                              double chi2, double delta, const double er[3], double acc[27]) {
+    const double x = Xc[0], y = Xc[1], invz = 1.0 / Xc[2], invz_2 = invz * invz;
+    double J[18];
+    J[0] = x * y * invz_2 * k.fx;       J[1] = -(1 + (x * x * invz_2)) * k.fx; J[2] = y * invz * k.fx;
+    J[3] = -invz * k.fx;                J[4] = 0;                              J[5] = x * invz_2 * k.fx;
+    J[6] = (1 + y * y * invz_2) * k.fy; J[7] = -x * y * invz_2 * k.fy;         J[8] = -x * invz * k.fy;
+    J[9] = 0;                           J[10] = -invz * k.fy;                  J[11] = y * invz_2 * k.fy;
+    if (st) {
+        J[12] = J[0] - k.bf * y * invz_2; J[13] = J[1] + k.bf * x * invz_2; J[14] = J[2];
+        J[15] = J[3];                     J[16] = 0;                        J[17] = J[5] - k.bf * invz_2;
+    } else {
+#pragma unroll
+        for (int i = 12; i < 18; i++) J[i] = 0.0;
+    }
+    double rho1 = 1.0;
+    if (robust && chi2 > delta * delta) rho1 = delta / sqrt(chi2);
+    const double W = rho1 * w;
+    double om[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) om[r] = (r < 2 || st) ? -(w * er[r]) * rho1 : 0.0;
+    // all 3 rows: a monocular edge's third row and om[2] are zero (exact zeros added)
+    int o = 0;
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        double s = 0;
+#pragma unroll
+        for (int r = 0; r < 3; r++) s += J[r * 6 + i] * om[r];
+        acc[21 + i] += s;
+#pragma unroll
+        for (int j = i; j < 6; j++) {
+            double h = 0;
+#pragma unroll
+            for (int r = 0; r < 3; r++) h += J[r * 6 + i] * W * J[r * 6 + j];
+            acc[o++] += h;
+        }
+    }
 }
 
 // (H + lambda I) x = b by LDL^T without pivoting (the oracle's recurrence); false when a pivot
@@ -227,42 +204,223 @@ __device__ bool po_solve(const double H[36], const double b[6], double lambda, d
     return true;
 }
 
-__global__ __launch_bounds__(kPoT) void k_pose_opt(PoseDev d) {
-    __shared__ double part[27][kPoT + 1];
-    __shared__ double res[32];
-    __shared__ double sh[8];
-    const int f = blockIdx.x, tid = threadIdx.x;
-    const int e0 = d.start[f], e1 = d.start[f + 1], n = e1 - e0;
-    const FrameCam k{d.cam[5 * f], d.cam[5 * f + 1], d.cam[5 * f + 2], d.cam[5 * f + 3], d.cam[5 * f + 4]};
+// Per-edge state in the device arena (any edge count): the frame's edges strided over the threads.
+struct PoEdgesGlobal {
+    const PoseDev& d;
+    FrameCam k;
+    int e0, e1;
+    __device__ void init() {
+        for (int e = e0 + (int)threadIdx.x; e < e1; e += kPoT) {
+            d.level[e] = 0;
+            d.robust[e] = 1;
+            d.outlier[e] = 0;
+        }
+    }
+    __device__ double active_count() const {
+        double cnt = 0.0;
+        for (int e = e0 + (int)threadIdx.x; e < e1; e += kPoT) cnt += d.level[e] ? 0.0 : 1.0;
+        return cnt;
+    }
+    __device__ double chi2(const double q[4], const double t[3]) const {
+        double s = 0.0;
+        for (int e = e0 + (int)threadIdx.x; e < e1; e += kPoT) {
+            if (d.level[e]) continue;
+            po_error(d, k, e, q, t);
+            double chi = po_chi2(d, e);
+            if (d.robust[e]) {
+                const double delta = po_delta(d, e), dsqr = delta * delta;
+                if (chi > dsqr) chi = 2 * sqrt(chi) * delta - dsqr;
+            }
+            s += chi;
+        }
+        return s;
+    }
+    __device__ void accum(const double q[4], const double t[3], double acc[27]) const {
+        for (int e = e0 + (int)threadIdx.x; e < e1; e += kPoT) {
+            if (d.level[e]) continue;
+            double Xc[3];
+            po_transform(q, t, d.xw + 3 * (size_t)e, Xc);
+            const bool st = d.obs[3 * (size_t)e + 2] >= 0;
+            const double* er = d.err + 3 * (size_t)e;
+            const double ev[3] = {er[0], er[1], er[2]};
+            po_accum_edge(k, Xc, st, d.info[e], d.robust[e] != 0, d.robust[e] ? po_chi2(d, e) : 0.0, po_delta(d, e), ev,
+                          acc);
+        }
+    }
+    // classification (R/src/Optimizer.cpp:461-520): inactive edges get their error at the final
+    // estimate, active ones keep the last computed one (e->chi2())
+    __device__ double classify(int it, const double q[4], const double t[3]) {
+        double bad = 0.0;
+        for (int e = e0 + (int)threadIdx.x; e < e1; e += kPoT) {
+            if (d.level[e]) po_error(d, k, e, q, t);
+            const float chi2 = (float)po_chi2(d, e);
+            const float thr = d.obs[3 * (size_t)e + 2] >= 0 ? 7.815f : 5.991f;
+            const uint8_t o = chi2 > thr ? 1 : 0;
+            d.outlier[e] = o;
+            d.level[e] = o;
+            bad += o;
+            if (it == 2) d.robust[e] = 0;
+        }
+        return bad;
+    }
+};
+
+// The same state in registers for frames of at most kPoT * EPT edges: edge tid + kPoT s in slot s
+// (the strided order above), loaded once; the LM passes touch no memory but the reductions' LDS.
+// Arithmetic and summation order are PoEdgesGlobal's, so results are bit-identical.
+template <int EPT>
+struct PoEdgesReg {
+    FrameCam k;
+    double obs[EPT][3], xw[EPT][3], info[EPT], er[EPT][3];
+    bool valid[EPT], st[EPT], level[EPT], robust[EPT];
+    uint8_t* outlier;
+    int e0;
+    __device__ void load(const PoseDev& d, int e0_, int e1) {
+        e0 = e0_;
+        outlier = d.outlier;
+#pragma unroll
+        for (int s = 0; s < EPT; s++) {
+            const int e = e0 + (int)threadIdx.x + kPoT * s;
+            valid[s] = e < e1;
+            const int ec = valid[s] ? e : e0;
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                obs[s][c] = d.obs[3 * (size_t)ec + c];
+                xw[s][c] = d.xw[3 * (size_t)ec + c];
+                er[s][c] = 0.0;
+            }
+            info[s] = d.info[ec];
+            st[s] = obs[s][2] >= 0;
+        }
+    }
+    __device__ void init() {
+#pragma unroll
+        for (int s = 0; s < EPT; s++) {
+            level[s] = false;
+            robust[s] = true;
+            if (valid[s]) outlier[e0 + (int)threadIdx.x + kPoT * s] = 0;
+        }
+    }
+    __device__ double active_count() const {
+        double cnt = 0.0;
+#pragma unroll
+        for (int s = 0; s < EPT; s++)
+            if (valid[s]) cnt += level[s] ? 0.0 : 1.0;
+        return cnt;
+    }
+    __device__ void error(int s, const double q[4], const double t[3]) {   // po_error in registers
+        double Xc[3];
+        po_transform(q, t, xw[s], Xc);
+        if (!st[s]) {
+            const double u = Xc[0] / Xc[2], v = Xc[1] / Xc[2];
+            er[s][0] = obs[s][0] - (u * k.fx + k.cx);
+            er[s][1] = obs[s][1] - (v * k.fy + k.cy);
+            er[s][2] = 0;
+        } else {
+            const float invz = (float)(1.0f / Xc[2]);
+            const double r0 = Xc[0] * invz * k.fx + k.cx;
+            const double r1 = Xc[1] * invz * k.fy + k.cy;
+            const double r2 = r0 - k.bf * invz;
+            er[s][0] = obs[s][0] - r0;
+            er[s][1] = obs[s][1] - r1;
+            er[s][2] = obs[s][2] - r2;
+        }
+    }
+    __device__ double chi2_of(int s) const {   // po_chi2
+        const double w = info[s];
+        double c = er[s][0] * (w * er[s][0]) + er[s][1] * (w * er[s][1]);
+        if (st[s]) c += er[s][2] * (w * er[s][2]);
+        return c;
+    }
+    __device__ double delta_of(int s) const { return st[s] ? 2.7955322265625 : 2.4476518630981445; }
+    __device__ double chi2(const double q[4], const double t[3]) {
+        double sum = 0.0;
+#pragma unroll
+        for (int s = 0; s < EPT; s++) {
+            if (!valid[s] || level[s]) continue;
+            error(s, q, t);
+            double chi = chi2_of(s);
+            if (robust[s]) {
+                const double delta = delta_of(s), dsqr = delta * delta;
+                if (chi > dsqr) chi = 2 * sqrt(chi) * delta - dsqr;
+            }
+            sum += chi;
+        }
+        return sum;
+    }
+    __device__ void accum(const double q[4], const double t[3], double acc[27]) const {
+#pragma unroll
+        for (int s = 0; s < EPT; s++) {
+            if (!valid[s] || level[s]) continue;
+            double Xc[3];
+            po_transform(q, t, xw[s], Xc);
+            po_accum_edge(k, Xc, st[s], info[s], robust[s], robust[s] ? chi2_of(s) : 0.0, delta_of(s), er[s], acc);
+        }
+    }
+    __device__ double classify(int it, const double q[4], const double t[3]) {
+        double bad = 0.0;
+#pragma unroll
+        for (int s = 0; s < EPT; s++) {
+            if (!valid[s]) continue;
+            if (level[s]) error(s, q, t);
+            const float chi2 = (float)chi2_of(s);
+            const float thr = st[s] ? 7.815f : 5.991f;
+            const bool o = chi2 > thr;
+            outlier[e0 + (int)threadIdx.x + kPoT * s] = o ? 1 : 0;
+            level[s] = o;
+            bad += o ? 1.0 : 0.0;
+            if (it == 2) robust[s] = false;
+        }
+        return bad;
+    }
+};
+
+// The four optimize(10) rounds over one frame's edges (any edge store above).
+template <class ES>
+__device__ void pose_rounds(ES& es, const PoseDev& d, const FrameCam& k, int f, int n, double (*part)[kPoT + 1],
+                            double* res, double* sh) {
+    const int tid = threadIdx.x;
     double q0[4], t0[3];
     for (int i = 0; i < 4; i++) q0[i] = d.q0[4 * f + i];
     for (int i = 0; i < 3; i++) t0[i] = d.t0[3 * f + i];
-    for (int e = e0 + tid; e < e1; e += kPoT) {
-        d.level[e] = 0;
-        d.robust[e] = 1;
-        d.outlier[e] = 0;
-    }
+    es.init();
     int its[4] = {0, 0, 0, 0}, trials = 0;
     double q[4], t[3];
     for (int i = 0; i < 4; i++) q[i] = q0[i];
     for (int i = 0; i < 3; i++) t[i] = t0[i];
     int nBad = 0;
+#ifdef ORB_TIMING
+    long long tChi = 0, tBuild = 0, tSolve = 0, tClass = 0, tK0 = clock64(), tc;
+#define PO_T0() tc = clock64()
+#define PO_T(acc) acc += clock64() - tc
+#else
+#define PO_T0()
+#define PO_T(acc)
+#endif
     if (n >= 3) {   // nInitialCorrespondences < 3: return 0, pose untouched
         __syncthreads();
         for (int it = 0; it < 4; it++) {
             for (int i = 0; i < 4; i++) q[i] = q0[i];   // vSE3->setEstimate(toSE3Quat(pFrame->mTcw))
             for (int i = 0; i < 3; i++) t[i] = t0[i];
-            double cnt = 0.0;
-            for (int e = e0 + tid; e < e1; e += kPoT) cnt += d.level[e] ? 0.0 : 1.0;
-            const int nact = (int)po_block_sum(cnt, sh);
+            const int nact = (int)po_block_sum(es.active_count(), sh);
             if (nact > 0) {
                 double lambda = 0.0, ni = 2.0;
                 int nBadLM = 0;
                 for (int iter = 0; iter < 10; iter++) {
-                    double currentChi = po_active_chi2(d, k, e0, e1, q, t, sh);
+                    PO_T0();
+                    double currentChi = po_block_sum(es.chi2(q, t), sh);   // computeActiveErrors + activeRobustChi2
+                    PO_T(tChi);
                     const double iniChi = currentChi;
                     double H[36], b[6];
-                    po_build(d, k, e0, e1, q, t, part, res, H, b);
+                    PO_T0();
+                    {
+                        double acc[27];
+#pragma unroll
+                        for (int i = 0; i < 27; i++) acc[i] = 0.0;
+                        es.accum(q, t, acc);
+                        po_reduce27(acc, part, res, H, b);
+                    }
+                    PO_T(tBuild);
                     if (iter == 0) {
                         double m = 0;
                         for (int j = 0; j < 6; j++) m = fmax(fabs(H[j * 7]), m);
@@ -277,11 +435,15 @@ __global__ __launch_bounds__(kPoT) void k_pose_opt(PoseDev d) {
                         for (int i = 0; i < 4; i++) bq[i] = q[i];
                         for (int i = 0; i < 3; i++) bt[i] = t[i];
                         const double lam = lambda;
+                        PO_T0();
                         const bool ok2 = po_solve(H, b, lam, x);
                         if (!ok2)
                             for (int i = 0; i < 6; i++) x[i] = 0.0;
                         d_se3_exp_left(x, q, t);
-                        double tempChi = po_active_chi2(d, k, e0, e1, q, t, sh);
+                        PO_T(tSolve);
+                        PO_T0();
+                        double tempChi = po_block_sum(es.chi2(q, t), sh);
+                        PO_T(tChi);
                         if (!ok2) tempChi = DBL_MAX;
                         rho = currentChi - tempChi;
                         double scale = 0.0;
@@ -310,23 +472,19 @@ __global__ __launch_bounds__(kPoT) void k_pose_opt(PoseDev d) {
                     if (nBadLM >= 3) break;
                 }
             }
-            // classification (R/src/Optimizer.cpp:461-520): inactive edges get their error at
-            // the final estimate, active ones keep the last computed one (e->chi2())
-            double bad = 0.0;
-            for (int e = e0 + tid; e < e1; e += kPoT) {
-                if (d.level[e]) po_error(d, k, e, q, t);
-                const float chi2 = (float)po_chi2(d, e);
-                const float thr = d.obs[3 * (size_t)e + 2] >= 0 ? 7.815f : 5.991f;
-                const uint8_t o = chi2 > thr ? 1 : 0;
-                d.outlier[e] = o;
-                d.level[e] = o;
-                bad += o;
-                if (it == 2) d.robust[e] = 0;
-            }
-            nBad = (int)po_block_sum(bad, sh);
+            PO_T0();
+            nBad = (int)po_block_sum(es.classify(it, q, t), sh);
+            PO_T(tClass);
             if (n < 10) break;   // optimizer.edges().size(): every edge of the graph
         }
     }
+#ifdef ORB_TIMING
+    if (tid == 0 && f == 0)
+        printf("pose_opt f0 n %d: total %lld cycles | chi2 passes %lld build %lld solve+exp %lld classify %lld | trials %d iters %d %d %d %d\n",
+               n, clock64() - tK0, tChi, tBuild, tSolve, tClass, trials, its[0], its[1], its[2], its[3]);
+#endif
+#undef PO_T0
+#undef PO_T
     if (tid == 0) {
         for (int i = 0; i < 4; i++) d.qo[4 * f + i] = q[i];
         for (int i = 0; i < 3; i++) d.to[3 * f + i] = t[i];
@@ -335,6 +493,26 @@ __global__ __launch_bounds__(kPoT) void k_pose_opt(PoseDev d) {
             for (int i = 0; i < 4; i++) d.iters[5 * f + i] = its[i];
             d.iters[5 * f + 4] = trials;
         }
+    }
+}
+
+constexpr int kPoEPT = 4;   // frames of up to 1024 edges keep their edges in registers
+
+__global__ __launch_bounds__(kPoT) void k_pose_opt(PoseDev d) {
+    __shared__ double part[27][kPoT + 1];
+    __shared__ double res[32];
+    __shared__ double sh[8];
+    const int f = blockIdx.x;
+    const int e0 = d.start[f], e1 = d.start[f + 1], n = e1 - e0;
+    const FrameCam k{d.cam[5 * f], d.cam[5 * f + 1], d.cam[5 * f + 2], d.cam[5 * f + 3], d.cam[5 * f + 4]};
+    if (n <= kPoT * kPoEPT) {
+        PoEdgesReg<kPoEPT> es;
+        es.k = k;
+        es.load(d, e0, e1);
+        pose_rounds(es, d, k, f, n, part, res, sh);
+    } else {
+        PoEdgesGlobal es{d, k, e0, e1};
+        pose_rounds(es, d, k, f, n, part, res, sh);
     }
 }
 

@@ -41,7 +41,20 @@ class Frame:
         return len(self.mvKeysUn)
 
     def view(self):
-        """orb_frame_view; keeps the arrays alive on the returned object."""
+        """orb_frame_view; keeps the arrays alive on the returned object.  Built once per frame and
+        reused while the frame's keypoint / descriptor / uRight arrays and bounds are the same objects
+        and values (a Frame's keypoints do not change after construction, R/src/Frame.cpp:60-180);
+        assigning new arrays rebuilds it."""
+        key = (id(self.mvKeysUn), id(self.mDescriptors), id(self.mvuRight), self.mnMinX, self.mnMinY, self.mnMaxX,
+               self.mnMaxY, self.N)
+        cached = self.__dict__.get("_view")
+        if cached is not None and cached[0] == key:
+            return cached[1]
+        v = self._build_view()
+        self.__dict__["_view"] = (key, v)
+        return v
+
+    def _build_view(self):
         k = self.mvKeysUn
         x = np.ascontiguousarray(k["x"], np.float32)
         y = np.ascontiguousarray(k["y"], np.float32)

@@ -97,7 +97,8 @@ def _sbp_setup(W=640, H=480, nf=1000, seed=0x5EED0001, stereo=False):
 
 
 @pytest.mark.parametrize("stereo,th,temporal", [(False, 15.0, False), (True, 7.0, False), (True, 15.0, False),
-                                                (True, 7.0, True), (True, 15.0, True)])
+                                                (True, 7.0, True), (True, 15.0, True), (False, 60.0, True),
+                                                (False, 60.0, False)])
 def test_search_by_projection_frame(amd, stereo, th, temporal):
     """temporal: 40 % of the last frame's map points have no observations (Tracking::UpdateLastFrame's
     temporal points, R/src/Tracking.cpp:1132-1137) and some current slots hold such a point on entry

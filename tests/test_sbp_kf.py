@@ -55,8 +55,10 @@ def _frame(k, kp):
 
 
 @pytest.mark.gpu
+# (7 / 8: wide windows and no distance cut, so many map points share a best slot: the replay's
+# clean / dirty claimant split and its re-scans are exercised)
 @pytest.mark.parametrize("seed,th,orb_dist,ori", [(3, 10.0, 100, True), (4, 10.0, 100, True), (5, 5.0, 64, False),
-                                                  (6, 3.0, 50, True)])
+                                                  (6, 3.0, 50, True), (7, 40.0, 256, True), (8, 80.0, 256, False)])
 def test_search_by_projection_kf_gpu(amd, seed, th, orb_dist, ori):
     p, kf, kfs, occ = _problem(seed)
     rn, rm = _oracle(p, kf, kfs, occ, th, orb_dist, ori)

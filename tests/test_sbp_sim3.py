@@ -20,7 +20,7 @@ def test_oracle_finds_planted_points():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed,th", [(3, 10.0), (7, 5.0), (11, 15.0)])
+@pytest.mark.parametrize("seed,th", [(3, 10.0), (7, 5.0), (11, 15.0), (13, 60.0)])
 def test_search_by_projection_sim3_gpu(amd, seed, th):
     from orb_slam2_amd import Frame
     p = _problem(seed)
