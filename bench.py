@@ -36,14 +36,19 @@ os.environ.setdefault("OMP_WAIT_POLICY", "active")
 
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md)
 VALU_PEAK_TOPS = 78.6            # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md)
-# chip-wide VALU issue rates measured by tools/micro/valu_issue.hip at 8 waves per SIMD (every
-# SIMD fed; profiles/r04_valu_issue.txt): v_fma_f32 1.78 cycles per wave64 instruction per SIMD
-# (MI355X_MICROARCH.md: 2 on a SIMD-32), 8.04e11 wave-instructions/s = 51.5 T lane-ops/s; an
-# integer VOP3 (v_xad_u32) 2.53 cycles, 5.30e11/s = 33.9 T lane-ops/s.  One wave alone on its SIMD
-# gets ~9 cycles per instruction.  The extraction kernels are integer-VOP3 code, so the integer
-# rate is their issue ceiling; the f32 rate is quoted beside it.
-VALU_MEASURED_TOPS = 33.9        # integer VOP3 issue ceiling (the extraction / matcher kernels' mix)
-VALU_MEASURED_F32_TOPS = 51.5    # v_fma_f32 issue ceiling
+# Chip-wide VALU issue rates measured by tools/micro/valu_issue.hip (profiles/r05_valu_issue.txt):
+# each workgroup stamps its loop 17 times, so the rate is taken inside the window where every
+# workgroup of the launch runs (instructions interpolated from the stamps), beside the wall-clock
+# rate; loop bodies of 8, 32 and 128 instructions give the same rate (no fetch limit).  Steady state
+# per SIMD: one wave ~5 cycles per wave64 instruction (long bodies), four waves 3.75 (integer VOP3:
+# v_perm, v_alignbyte, v_lerp_u8, v_dot4, v_bcnt, v_pk_minimum3_f16, v_xad) / 3.38 (v_fma_f32),
+# eight waves 3.23 (v_fma_f32; the integer kernels never had all eight workgroups of a CU resident
+# at once, so their 8-wave figure is the wall-clock one, 5.9e11/s).  Chip-wide: integer 6.5e11
+# wave-instructions/s = 41.7 T lane-ops/s; v_fma_f32 7.5e11/s = 48.3 T.  Round 4's 33.9 T / 51.5 T
+# summed per-workgroup rates over workgroups that were not all running at once (and a loop with
+# 3 scalar instructions per 8 VALU); they are superseded.
+VALU_MEASURED_TOPS = 41.7        # integer VOP3 issue ceiling (the extraction / matcher kernels' mix)
+VALU_MEASURED_F32_TOPS = 48.3    # v_fma_f32 issue ceiling
 STAGES = ["resize", "fast_detect", "reserved", "octree", "reserved2", "orient_blur_desc"]
 KERNELS = ["k_resize", "k_fast_cell", None, "k_octree", None, "k_orient_desc"]
 PMC_TRAFFIC = ROOT / "profiles" / "r04_pmc_traffic.json"   # tools/pmc_run.sh + tools/pmc_traffic.py
@@ -223,7 +228,7 @@ def extraction_roofline(stage_ms, ncalls, lw, lh, n_pre, n_out, W, H, NF, Bs):
                          "frac": round(ach / VALU_PEAK_TOPS, 4), "measured_issue_peak": VALU_MEASURED_TOPS,
                          "frac_of_measured_issue_peak": round(ach / VALU_MEASURED_TOPS, 4),
                          "frac_of_measured_f32_issue_peak": round(ach / VALU_MEASURED_F32_TOPS, 4),
-                         "issue_peak_source": "profiles/r04_valu_issue.txt (8 waves/SIMD; int VOP3 / f32 FMA)"}
+                         "issue_peak_source": "profiles/r05_valu_issue.txt (all-running window; int VOP3 / f32 FMA)"}
             util = pmc_lane_util(name, W, H, NF, Bs)
             if util is not None:
                 k["valu"]["active_lane_frac"] = util
@@ -995,7 +1000,7 @@ def bench_extras(args, amd, dev):
     c = buf["cnt"].cpu().numpy().astype(np.int64)
     pairs = float((c[:-1] * c[1:]).sum())
     # 16 lane-ops per pair (8 xor + 8 bcnt on dword pairs); 78.6 T lane-ops/s nominal (4 SIMD x 32
-    # lanes per CU per clock), 33.9 T measured for integer VOP3 issue at 8 waves per SIMD (profiles/r04_valu_issue.txt)
+    # lanes per CU per clock), 41.7 T measured for integer VOP3 issue (profiles/r05_valu_issue.txt)
     peak_pairs = VALU_PEAK_TOPS * 1e12 / 16
     out["knn2_bruteforce"] = {"pairs_per_s": round(pairs / dt, 1), "ms_per_batch": round(dt * 1e3, 4),
                               "frame_pairs": B, "roofline": {"bound": "valu", "unit": "pairs/s",

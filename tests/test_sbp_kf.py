@@ -55,10 +55,12 @@ def _frame(k, kp):
 
 
 @pytest.mark.gpu
-# (7 / 8: wide windows and no distance cut, so many map points share a best slot: the replay's
-# clean / dirty claimant split and its re-scans are exercised)
+# (7 / 8: wide windows and a loose distance cut, so many map points share a best slot: the replay's
+# clean / dirty claimant split and its re-scans are exercised.  ORBdist stays below 256: at 256 a
+# point whose candidates are all occupied passes `bestDist <= ORBdist` with bestIdx2 = -1 and the
+# reference writes mvpMapPoints[-1] (R/src/ORBmatcher.cpp:1806-1808; R/src/Tracking.cpp:1921, 1936 call it with 100 and 64))
 @pytest.mark.parametrize("seed,th,orb_dist,ori", [(3, 10.0, 100, True), (4, 10.0, 100, True), (5, 5.0, 64, False),
-                                                  (6, 3.0, 50, True), (7, 40.0, 256, True), (8, 80.0, 256, False)])
+                                                  (6, 3.0, 50, True), (7, 40.0, 200, True), (8, 80.0, 200, False)])
 def test_search_by_projection_kf_gpu(amd, seed, th, orb_dist, ori):
     p, kf, kfs, occ = _problem(seed)
     rn, rm = _oracle(p, kf, kfs, occ, th, orb_dist, ori)

@@ -12,7 +12,7 @@ import pkgload  # noqa: E402
 amd = pkgload.load()
 import test_sbp_kf as T  # noqa: E402
 
-for seed, th, od in ((7, 40.0, 256), (7, 10.0, 100), (3, 40.0, 256)):
+for seed, th, od in ((7, 40.0, 200), (7, 10.0, 100), (3, 40.0, 200)):
     for ori in (False, True):
         p, kf, kfs, occ = T._problem(seed)
         rn, rm = T._oracle(p, kf, kfs, occ, th, od, ori)
