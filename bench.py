@@ -199,6 +199,28 @@ EXT_KERNELS = (("k_pyramid", "resize", 0), ("k_fast_cell", "fast_detect", 1), ("
                ("k_orient_desc", "orient_blur_desc", 5))
 
 
+def measure_copy_peak(dev, mib=1024, reps=8):
+    """SURVEY 8d's second HBM denominator: the device-to-device copy rate this GPU sustains (a
+    `mib` MiB tensor copied `reps` times on one stream, HIP events around them; read + write bytes
+    per copy).  Measured in the run, so a roofline fraction can be read against what a pure
+    streaming kernel gets on this box as well as against the 8 TB/s spec."""
+    n = mib * (1 << 20) // 4
+    src = torch.empty(n, dtype=torch.float32, device=dev).fill_(1.0)
+    dst = torch.empty_like(src)
+    dst.copy_(src)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(dev)
+    e0.record()
+    for _ in range(reps):
+        dst.copy_(src)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    gbs = 2.0 * n * 4 * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del src, dst
+    torch.cuda.empty_cache()
+    return round(gbs, 1)
+
+
 def extraction_roofline(stage_ms, ncalls, lw, lh, n_pre, n_out, W, H, NF, Bs):
     """SURVEY §8d roofline of every extraction kernel of the timed region, and the dominant one
     (largest average launch time) as the line's `roofline`.  achieved = the kernel's algorithmic
@@ -1713,9 +1735,13 @@ def main():
     pre = np.zeros(8, np.int32)
     lib.orb_extractor_last_counts(ex._h, 0, _abi.ptr(pre), None)
     n_pre_frame = float(pre.sum())   # corners k_fast_cell emitted for frame 0 of the last batch
+    copy_peak = measure_copy_peak(dev)
     if nstage > 0:
         result["roofline"] = extraction_roofline(stage_ms, nstage, lw, lh, n_pre_frame, float(np.mean(cnt)), W, H, NF,
                                                  Bs)
+        if result["roofline"]:
+            result["roofline"]["measured_copy_peak_gbs"] = copy_peak
+            result["roofline"]["frac_of_measured_copy_peak"] = round(result["roofline"]["achieved"] / copy_peak, 5)
     if nstage > 0:
         result["stage_ms_per_batch"] = {k: round(float(v) / nstage, 4) for k, v in zip(STAGES, stage_ms)
                                         if not k.startswith("reserved")}
@@ -1725,7 +1751,10 @@ def main():
     P = (lw.astype(np.int64) * lh)
     b_ext = float(P[0] + 2 * P[1:].sum()) + float(np.mean(cnt)) * 60.0
     result["pipeline_roofline"] = {"bytes_per_frame": b_ext, "achieved_gbs": round(b_ext * value / 1e9, 2),
-                                   "peak_gbs": HBM_PEAK_GBS, "frac": round(b_ext * value / 1e9 / HBM_PEAK_GBS, 5)}
+                                   "peak_gbs": HBM_PEAK_GBS, "frac": round(b_ext * value / 1e9 / HBM_PEAK_GBS, 5),
+                                   "measured_copy_peak_gbs": copy_peak,
+                                   "frac_of_measured_copy_peak": round(b_ext * value / 1e9 / copy_peak, 5),
+                                   "copy_peak_source": "1 GiB device-to-device torch copy x8 in this run (read + write bytes)"}
     # the whole step against the VALU bound: every extraction + matching kernel's lane-ops per
     # frame (committed PMC pass of this configuration) x frames/s
     kern = ("k_pyramid", "k_fast_cell", "k_octree", "k_orient_desc", "k_grid_sfi", "k_cand_sfi", "k_resolve_sfi")
