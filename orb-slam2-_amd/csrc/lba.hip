@@ -2156,38 +2156,63 @@ struct DfPivot {
     }
 };
 
-// kDiag: this row block is the next panel's diagonal block.  Its panel W / L go to LDS and its
-// diagonal tile takes the panel's update (one f64 MFMA per 4 columns) as the columns become final
-// (column k is frozen from column k on), so only the last MFMA is left when the loop ends and the pivot
-// waits ~1 k cycles less for the next panel.
-template <bool kDiag>
+// Follower modes.  kPlain: follow the panel, store W / L afterwards.  kDiag: this row block is the next
+// panel's diagonal block: its W / L go to LDS four columns at a time (column k is frozen from column
+// k on), each group published on the chunk counter, and its diagonal tile T takes the panel's update
+// one f64 MFMA per group (applied a group later, behind the next group's LDS round trip); the
+// previous panel's update of T, deferred from then, is applied while the follower first waits for
+// the pivot.  kNext: the block after the next diagonal block: it stores its W / L per group the same
+// way and, as the diagonal block's chunks appear, applies this panel's update of its tile
+// (I, I - 1) — the tile it will follow next panel — to T in registers, so when the pivot starts
+// that panel this wave follows at once, its X being T (the MFMA output layout is the follow layout).
+enum { kPlain = 0, kDiag = 1, kNext = 2 };
+template <int kMode>
 struct DfFollow {
     double X[4], Y[4];
     double uq[4], gq[4];     // the current group of four published columns
-    dbl4 T;                  // kDiag: the diagonal tile, MFMA output layout
-    double pa, pb;           // kDiag: the last group's MFMA operands, applied one group later
-    int k, seq, seen, jb, rb, ld;
+    double rdk;              // 1 / d of this lane's column k (loaded with k's group)
+    bool pf;                 // uq / gq already hold the group starting at the current column
+    dbl4 T;                  // kDiag: the diagonal tile; kNext: tile (I, I - 1); MFMA output layout
+    double pa, pb;           // the last group's MFMA operands, applied one group later
+    int k, seq, seen, jb, rb, ld, rbK;   // rbK (kNext): the diagonal block's first row
+    bool defer;              // kDiag: the previous panel's update of T is still to apply
     const volatile lds_f64 *pubU, *pubRG;
     const volatile lds_i32* cnt;
+    volatile lds_i32* chunk;
     lds_f64 *A, *sinkD;
     template <int C>
     __device__ __forceinline__ void col() {
+        const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+        if constexpr (kMode == kDiag && C == 0) {
+            if (defer) {   // (the pivot has only just started: this overlaps the wait for its columns)
+                const int jp = jb - kNB;
+#pragma unroll
+                for (int s = 0; s < kNB / 4; s++) {
+                    const int pp = jp + 4 * s + lk;
+                    T = __builtin_amdgcn_mfma_f64_16x16x4f64(A[(size_t)pp * ld + rb + li], A[(size_t)(rb + li) * ld + pp], T, 0,
+                                                             0, 0);
+                }
+            }
+        }
         // the follower trails the pivot, so it takes the pivot's columns four at a time: one poll of the
         // sequence counter (wave-uniform) and one LDS round trip for the group's u and y_c / d_c instead
         // of one per column
         if constexpr ((C & 3) == 0) {
-            if (__builtin_amdgcn_readfirstlane(seen) < seq + C + 4) {
-                int v;
-                while ((v = __builtin_amdgcn_readfirstlane(*cnt)) < seq + C + 4) __builtin_amdgcn_s_sleep(1);
-                seen = v;
-            }
+            if (!(C > 0 && pf)) {   // (pf: loaded at the previous group's end)
+                if (__builtin_amdgcn_readfirstlane(seen) < seq + C + 4) {
+                    int v;
+                    while ((v = __builtin_amdgcn_readfirstlane(*cnt)) < seq + C + 4) __builtin_amdgcn_s_sleep(1);
+                    seen = v;
+                }
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                uq[j] = pubU[(C + j) * kNB + k];
-                gq[j] = pubRG[2 * (C + j) + 1];
+                for (int j = 0; j < 4; j++) {
+                    uq[j] = pubU[(C + j) * kNB + k];
+                    gq[j] = pubRG[2 * (C + j) + 1];
+                }
+                if constexpr (kMode != kPlain) rdk = pubRG[2 * k];   // (used by the lanes of this group)
             }
             // the previous group's MFMA, its operands' LDS round trip hidden behind this group's
-            if constexpr (kDiag && C > 0) T = __builtin_amdgcn_mfma_f64_16x16x4f64(pa, pb, T, 0, 0, 0);
+            if constexpr (kMode != kPlain && C > 0) T = __builtin_amdgcn_mfma_f64_16x16x4f64(pa, pb, T, 0, 0, 0);
         }
         const double u = uq[C & 3];
         const double g = gq[C & 3];
@@ -2197,22 +2222,43 @@ struct DfFollow {
             X[s] = __builtin_fma(-wi, u, X[s]);
             Y[s] = __builtin_fma(-wi, g, Y[s]);
         }
-        if constexpr (kDiag && (C & 3) == 3) {
-            // columns C-3..C are final: their -W (upper triangle) and L (lower) out, and the tile's MFMA
-            // operands read back (the MFMA itself waits for the next group, or the caller)
-            const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+        if constexpr (kMode != kPlain && (C & 3) == 3) {
+            // columns C-3..C are final: their -W (upper triangle) and L (lower) out, the MFMA operands
+            // read back (the MFMA itself waits for the next group, or the caller)
+            const double rdkThis = rdk;
+            if constexpr (kMode == kDiag && C + 1 < kNB) {
+                // the diagonal block's follower gates the pivot: when the pivot has already published the
+                // next group, its loads go out now and overlap this group's stores and operand reads
+                if (__builtin_amdgcn_readfirstlane(seen) < seq + C + 5) seen = __builtin_amdgcn_readfirstlane(*cnt);
+                pf = __builtin_amdgcn_readfirstlane(seen) >= seq + C + 5;
+                if (pf) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        uq[j] = pubU[(C + 1 + j) * kNB + k];
+                        gq[j] = pubRG[2 * (C + 1 + j) + 1];
+                    }
+                    rdk = pubRG[2 * k];
+                }
+            }
             if ((k >> 2) == (C >> 2)) {
-                const double rdk = pubRG[2 * k];
 #pragma unroll
                 for (int s = 0; s < 4; s++) {
                     const int r = rb + lk + 4 * s;
                     A[(size_t)(jb + k) * ld + r] = -X[s];
-                    A[(size_t)r * ld + jb + k] = X[s] * rdk;
+                    A[(size_t)r * ld + jb + k] = X[s] * rdkThis;
                 }
             }
             const int pc = jb + (C - 3) + lk;
-            pa = A[(size_t)pc * ld + rb + li];
-            pb = A[(size_t)(rb + li) * ld + pc];
+            const int grp = (seq + C + 1) >> 2;   // 4 kb + this group + 1
+            if constexpr (kMode == kDiag) {
+                if (lane == 0) *chunk = grp;       // (after this wave's stores: LDS is in order per wave)
+                pa = A[(size_t)pc * ld + rb + li];
+                pb = A[(size_t)(rb + li) * ld + pc];
+            } else {
+                while (__builtin_amdgcn_readfirstlane(*chunk) < grp) __builtin_amdgcn_s_sleep(1);
+                pa = A[(size_t)pc * ld + rb + li];
+                pb = A[(size_t)(rbK + li) * ld + pc];
+            }
         }
     }
 };
@@ -2225,6 +2271,9 @@ __host__ __device__ inline size_t ldlt_df_lds_bytes(int n) {
 __global__ __launch_bounds__(kLdlT) void k_ldlt_df(const double* __restrict__ Sg, const double* __restrict__ b, int n,
                                                   double* __restrict__ x, int* __restrict__ flags, const LmState* st,
                                                   PoseTail ptail) {
+#ifdef ORB_TIMING
+    const long long tEntry = clock64();
+#endif
     if (lm_off(st, 1)) return;
     extern __shared__ __attribute__((aligned(16))) double sh[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -2233,6 +2282,7 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_df(const double* __restrict__ Sg
 #ifdef ORB_TIMING
     long long tdf[40] = {0};
     tdf[0] = clock64();
+    __shared__ long long waveT[16];
 #endif
     double* A = sh;
     double* rdg = A + (size_t)np * ld;
@@ -2245,15 +2295,25 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_df(const double* __restrict__ Sg
     int* sinkI = cnt + 2;                             // 64
     volatile lds_i32* rowDone = (volatile lds_i32*)(sinkI + 64);   // [8]
     volatile lds_i32* diagReady = rowDone + 8;
+    volatile lds_i32* chunk = rowDone + 9;   // the current diagonal follower's published column groups
     __shared__ int failS;
 #ifdef ORB_TIMING
     __shared__ long long dbgT[32];
 #endif
     if (tid == 0) { failS = 0; *cnt = 0; }
-    if (tid < 9) rowDone[tid] = 0;
+    if (tid < 10) rowDone[tid] = 0;
+#ifdef ORB_TIMING
+    if (lane == 0) { waveT[wave] = tEntry; waveT[8 + wave] = tdf[0]; }
+#endif
     __syncthreads();
 #ifdef ORB_TIMING
     tdf[35] = clock64();
+    if (tid == 0) {
+        long long e0 = waveT[0], e1 = waveT[0], m1 = waveT[8];
+        for (int w = 1; w < 8; w++) { e0 = min(e0, waveT[w]); e1 = max(e1, waveT[w]); m1 = max(m1, waveT[8 + w]); }
+        printf("ldlt_df entry: wave0 %lld (rel first), last wave entry +%lld, last lm_off done +%lld, wave0 lm_off %lld, barrier exit +%lld\n",
+               waveT[0] - e0, e1 - e0, m1 - e0, waveT[8] - waveT[0], tdf[35] - e0);
+    }
 #endif
     // ---- staging, per owner, no barrier: the wave of row block I loads its rows' columns
     //      [0, 16(I+1)) (its lower tiles and the whole diagonal tile) and their b, one 16-byte load per
@@ -2359,10 +2419,11 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_df(const double* __restrict__ Sg
 #pragma unroll
         for (int s = 0; s < 4; s++) Yr[s] = y[rb + q + 4 * s];
         int seen = 0;
+        dbl4 Tn;   // tile (I, I - 1) carried from the kNext panel into the diagonal panel
+        const int li = lane & 15, lk = lane >> 4;
         for (int kb = 0; kb < I; kb++) {
             const int jb = kb * kNB;
-            const bool diagNext = kb == I - 1;
-            auto follow = [&](auto& F) {
+            auto follow = [&](auto& F, bool xFromT) {
                 F.k = k;
                 F.seq = kNB * kb;
                 F.seen = seen;
@@ -2372,11 +2433,13 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_df(const double* __restrict__ Sg
                 F.pubU = (const volatile lds_f64*)(pubU + (size_t)kb * kNB * kNB);
                 F.pubRG = (const volatile lds_f64*)(pubRG + (size_t)kb * 2 * kNB);
                 F.cnt = (const volatile lds_i32*)cnt;
+                F.chunk = chunk;
                 F.A = (lds_f64*)A;
                 F.sinkD = (lds_f64*)(sinkD + lane);
+                F.pf = false;
 #pragma unroll
                 for (int s = 0; s < 4; s++) {
-                    F.X[s] = A[(size_t)(rb + q + 4 * s) * ld + jb + k];
+                    F.X[s] = xFromT ? Tn[s] : A[(size_t)(rb + q + 4 * s) * ld + jb + k];
                     F.Y[s] = Yr[s];
                 }
                 ColUnroll<0, kNB>::run(F);
@@ -2384,28 +2447,19 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_df(const double* __restrict__ Sg
 #pragma unroll
                 for (int s = 0; s < 4; s++) Yr[s] = F.Y[s];
             };
-            if (diagNext) {
-                DfFollow<true> F;
-                const int li = lane & 15, lk = lane >> 4;
+            if (kb == I - 1) {   // this block is the next diagonal block
+                DfFollow<kDiag> F;
 #pragma unroll
                 for (int s = 0; s < 4; s++) F.T[s] = A[(size_t)(rb + lk + 4 * s) * ld + rb + li];
+                F.defer = kb >= 1;
 #ifdef ORB_TIMING
                 const long long tfs = clock64();
 #endif
-                follow(F);
+                follow(F, I >= 2);
 #ifdef ORB_TIMING
                 if (lane == 0 && kb < 8) { dbgT[2 * kb] = tfs; dbgT[2 * kb + 1] = clock64(); }
 #endif
                 F.T = __builtin_amdgcn_mfma_f64_16x16x4f64(F.pa, F.pb, F.T, 0, 0, 0);
-                if (kb >= 1) {   // the previous panel's update of this tile, deferred (see below)
-                    const int jp = jb - kNB;
-#pragma unroll
-                    for (int s = 0; s < kNB / 4; s++) {
-                        const int pp = jp + 4 * s + lk;
-                        F.T = __builtin_amdgcn_mfma_f64_16x16x4f64(A[(size_t)pp * ld + rb + li], A[(size_t)(rb + li) * ld + pp],
-                                                                   F.T, 0, 0, 0);
-                    }
-                }
 #pragma unroll
                 for (int s = 0; s < 4; s++) A[(size_t)(rb + lk + 4 * s) * ld + rb + li] = F.T[s];
 #pragma unroll
@@ -2417,9 +2471,18 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_df(const double* __restrict__ Sg
 #endif
                 *(lane == 0 ? diagReady : (volatile lds_i32*)(sinkI + lane)) = I;
                 *(lane == 0 ? rowDone + I : (volatile lds_i32*)(sinkI + lane)) = kb + 1;
+            } else if (kb == I - 2) {   // the diagonal block is I - 1: tile (I, I - 1) in registers
+                DfFollow<kNext> F;
+                F.rbK = rb - kNB;
+#pragma unroll
+                for (int s = 0; s < 4; s++) F.T[s] = A[(size_t)(rb + lk + 4 * s) * ld + rb - kNB + li];
+                follow(F, false);
+                Tn = __builtin_amdgcn_mfma_f64_16x16x4f64(F.pa, F.pb, F.T, 0, 0, 0);
+                *(lane == 0 ? rowDone + I : (volatile lds_i32*)(sinkI + lane)) = kb + 1;
+                // (tile (I, I): deferred to the diagonal panel; tile (I, I - 1): Tn)
             } else {
-                DfFollow<false> F;
-                follow(F);
+                DfFollow<kPlain> F;
+                follow(F, false);
                 const double rdk = pubRG[(size_t)kb * 2 * kNB + 2 * k];
 #pragma unroll
                 for (int s = 0; s < 4; s++) {
@@ -2428,11 +2491,8 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_df(const double* __restrict__ Sg
                     A[(size_t)r * ld + jb + k] = F.X[s] * rdk;      // L(r, jb + k)
                 }
                 *(lane == 0 ? rowDone + I : (volatile lds_i32*)(sinkI + lane)) = kb + 1;
-                // panel kb's trailing update of this row block's tiles; in the panel before the one where
-                // this block is the next diagonal block, the diagonal tile's update is deferred to after
-                // that panel's columns (above), so this wave starts following it one tile earlier
-                const int Kend = kb == I - 2 ? I - 1 : I;
-                for (int K = kb + 1; K <= Kend; K++) {
+                // panel kb's trailing update of this row block's tiles (I, K), K = kb + 1 .. I
+                for (int K = kb + 1; K <= I; K++) {
                     if (K != I) wait_ge(rowDone + K, kb + 1);
                     tile(jb, rb, kNB * K);
                 }
