@@ -51,8 +51,8 @@ VALU_MEASURED_TOPS = 41.7        # integer VOP3 issue ceiling (the extraction / 
 VALU_MEASURED_F32_TOPS = 48.3    # v_fma_f32 issue ceiling
 STAGES = ["resize", "fast_detect", "reserved", "octree", "reserved2", "orient_blur_desc"]
 KERNELS = ["k_resize", "k_fast_cell", None, "k_octree", None, "k_orient_desc"]
-PMC_TRAFFIC = ROOT / "profiles" / "r04_pmc_traffic.json"   # tools/pmc_run.sh + tools/pmc_traffic.py
-PMC_VALU = ROOT / "profiles" / "r04_valu_pmc.json"         # tools/gpu_valu_pmc.sh + tools/pmc_valu.py
+PMC_TRAFFIC = ROOT / "profiles" / "r05_pmc_traffic.json"   # tools/pmc_run.sh + tools/pmc_traffic.py
+PMC_VALU = ROOT / "profiles" / "r05_valu_pmc.json"         # tools/gpu_pmc_all.sh + tools/pmc_valu.py
 
 
 def pmc_traffic(kernel, W, H, NF, Bs):
@@ -86,7 +86,7 @@ def pmc_valu_ops(kernel, W, H, NF, Bs):
         return None
 
 
-PMC_LANES = ROOT / "profiles" / "r04_lanes_pmc.json"   # tools/pmc_run.sh lanes ... + tools/pmc_lanes.py
+PMC_LANES = ROOT / "profiles" / "r05_lanes_pmc.json"   # tools/pmc_run.sh lanes ... + tools/pmc_lanes.py
 
 
 def pmc_lane_util(kernel, W, H, NF, Bs):
@@ -197,6 +197,23 @@ def algorithmic_ops(stage, lw, lh, n_pre, n_out):
 
 EXT_KERNELS = (("k_pyramid", "resize", 0), ("k_fast_cell", "fast_detect", 1), ("k_octree", "octree", 3),
                ("k_orient_desc", "orient_blur_desc", 5))
+
+
+def pmc_capture_current():
+    """Whether the committed PMC captures (PMC_TRAFFIC / PMC_VALU / PMC_LANES) were taken from the device
+    sources in this tree (their provenance hashes, tools/pmc_provenance.py), per file."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("_pmc_prov", ROOT / "tools" / "pmc_provenance.py")
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    now = m.provenance()["csrc_sha256"]
+    out = {}
+    for f in (PMC_TRAFFIC, PMC_VALU, PMC_LANES):
+        try:
+            out[f.name] = json.loads(f.read_text()).get("provenance", {}).get("csrc_sha256") == now
+        except (OSError, ValueError):
+            out[f.name] = None
+    return out
 
 
 def measure_copy_peak(dev, mib=1024, reps=8):
@@ -1754,7 +1771,8 @@ def main():
                                    "peak_gbs": HBM_PEAK_GBS, "frac": round(b_ext * value / 1e9 / HBM_PEAK_GBS, 5),
                                    "measured_copy_peak_gbs": copy_peak,
                                    "frac_of_measured_copy_peak": round(b_ext * value / 1e9 / copy_peak, 5),
-                                   "copy_peak_source": "1 GiB device-to-device torch copy x8 in this run (read + write bytes)"}
+                                   "copy_peak_source": "1 GiB device-to-device torch copy x8 in this run (read + write bytes)",
+                                   "pmc_capture_matches_tree": pmc_capture_current()}
     # the whole step against the VALU bound: every extraction + matching kernel's lane-ops per
     # frame (committed PMC pass of this configuration) x frames/s
     kern = ("k_pyramid", "k_fast_cell", "k_octree", "k_orient_desc", "k_grid_sfi", "k_cand_sfi", "k_resolve_sfi")

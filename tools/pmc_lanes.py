@@ -10,6 +10,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_provenance import provenance  # noqa: E402
 from pmc_traffic import per_kernel  # noqa: E402
 
 
@@ -20,7 +21,7 @@ def main():
     res = {"source": "rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE "
                      "--kernel-trace -- python3 bench.py (tools/pmc_run.sh lanes)",
            "definition": "active_lane_frac = SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU * 64) (rocprof VALUUtilization)",
-           "config": config, "kernels": {}}
+           "config": config, "provenance": provenance(), "kernels": {}}
     for k, c in sorted(t.items()):
         e = {kk: round(v, 1) for kk, v in c.items()}
         act = c.get("SQ_ACTIVE_INST_VALU", 0.0)

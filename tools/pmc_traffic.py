@@ -16,6 +16,9 @@ import json
 import os
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_provenance import provenance  # noqa: E402
+
 
 def per_kernel(d):
     files = glob.glob(os.path.join(d, "*counter_collection.csv"))
@@ -71,7 +74,7 @@ def main():
     doc = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) --kernel-trace",
            "correction": "read_bytes = 2 x FETCH_SIZE x 1024 (gfx950 128-B requests tallied at 64 B); "
                          "write_bytes = WRITE_SIZE x 1024",
-           "config": config, "kernels": kernels}
+           "config": config, "provenance": provenance(), "kernels": kernels}
     with open(out, "w") as f:
         json.dump(doc, f, indent=1)
     for k, e in sorted(kernels.items(), key=lambda kv: -kv[1]["traffic_bytes_per_launch"]):

@@ -20,6 +20,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_provenance import provenance  # noqa: E402
 from pmc_traffic import per_kernel  # noqa: E402
 
 VALU_PEAK = 256 * 4 * 32 * 2.4e9
@@ -45,7 +46,7 @@ def main():
     dur = kernel_durations(d)
     res = {"source": "rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAVES "
                      "SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT --kernel-trace",
-           "valu_peak_lane_ops_per_s": VALU_PEAK, "config": config, "kernels": {}}
+           "valu_peak_lane_ops_per_s": VALU_PEAK, "config": config, "provenance": provenance(), "kernels": {}}
     for k, c in sorted(t.items()):
         e = {kk: round(v, 1) for kk, v in c.items()}
         ops = c.get("SQ_INSTS_VALU", 0.0) * 64
