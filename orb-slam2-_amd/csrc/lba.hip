@@ -113,7 +113,8 @@ struct LbaDev {
     double* HplP;               // [pose-major position][18] Hpl_e (per trial, written with Ae)
     const int32_t* poPos;       // per act position: its index in the pose-major lists (-1: fixed pose)
     const int32_t* pairs;       // pose-pair blocks of S with shared landmarks, (bi << 16 | bj), bi <= bj
-    const int32_t* npairs;      // their count
+    const int32_t* npairs;      // their count; [1] / [2]: k_schur_pairs' workgroup / wave pairs (pairUnits)
+    const int32_t* pairUnits;   // indices into pairs: [0, npairs[1]) one workgroup each, then npairs[2] one wave each
     const int32_t* tripStart;   // per listed pair: first entry of its shared-landmark list, count at +1
     const int2* trips;          // (pose-major position of pose i's edge, of pose j's edge), landmark order
     double *S, *bs, *x;         // x: [6P + 3M]
@@ -1005,69 +1006,106 @@ __device__ __forceinline__ void reduce_halve(double* cur, int lane) {
     }
 }
 
+// the product of one shared landmark: A_e1 against Hpl_e2 into acc[0 .. 36); diagonal blocks
+// (e2 == e1) also b_s's Hpl_e1 D^-1 b_l into acc[36 .. 42)
+__device__ __forceinline__ void sp_product(const LbaDev& d, double acc[64], int e1, int e2, int l, bool diag) {
+    const double2* Ui = reinterpret_cast<const double2*>(d.Ae + 18 * (size_t)e1);
+    const double2* Bj = reinterpret_cast<const double2*>(d.HplP + 18 * (size_t)e2);
+    double v[18], u[18];
+#pragma unroll
+    for (int h = 0; h < 9; h++) {
+        const double2 x = Ui[h], y = Bj[h];
+        u[2 * h] = x.x; u[2 * h + 1] = x.y;
+        v[2 * h] = y.x; v[2 * h + 1] = y.y;
+    }
+    // three fused multiply-adds per entry (the terms accumulate straight into the partial)
+#pragma unroll
+    for (int r = 0; r < 6; r++)
+#pragma unroll
+        for (int q = 0; q < 6; q++)
+            acc[r * 6 + q] = __builtin_fma(u[r * 3 + 2], v[q * 3 + 2],
+                                           __builtin_fma(u[r * 3 + 1], v[q * 3 + 1],
+                                                         __builtin_fma(u[r * 3], v[q * 3], acc[r * 6 + q])));
+    if (diag) {
+        const double* db = d.db + 3 * (size_t)l;
+        const double g0 = db[0], g1 = db[1], g2 = db[2];
+#pragma unroll
+        for (int i = 0; i < 6; i++)
+            acc[36 + i] = __builtin_fma(v[i * 3 + 2], g2, __builtin_fma(v[i * 3 + 1], g1, __builtin_fma(v[i * 3], g0, acc[36 + i])));
+    }
+}
+
+// the wave's 64 partials of 64 values -> lane v holds value v (recursive halving, fixed order)
+__device__ __forceinline__ void sp_wave_reduce(double acc[64], int lane) {
+    reduce_halve<32>(acc, lane);
+    reduce_halve<16>(acc, lane);
+    reduce_halve<8>(acc, lane);
+    reduce_halve<4>(acc, lane);
+    reduce_halve<2>(acc, lane);
+    reduce_halve<1>(acc, lane);
+}
+
+// Work units (k_pair_list, once per solve): the diagonal blocks and the off-diagonal pairs sharing
+// more than kSpSmall landmarks take a workgroup each (its four waves' partials meet in LDS); the
+// others a wave each, four per workgroup, with no LDS and no barrier — a 200 KF corridor window's
+// ~8 k pairs share ~140 landmarks each, so a workgroup per pair spent most of its time in four
+// waves' reductions and barriers at half its lanes.
 __global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag) {
-    const int np = *d.npairs;   // blocks with no shared landmark stay 0 (zeroed per solve)
+    const int np = d.npairs[0], nBig = d.npairs[1], nSmall = d.npairs[2];
     const int phase = d.lm->phase;
     if (phase != 1) return;     // lm_off(d.lm, 1)
     __shared__ double wsum[kSpW][64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nUnits = nBig + (nSmall + kSpW - 1) / kSpW;
     // XCD-aware: workgroup b runs on XCD b % 8 (gridDim.x is a multiple of 8), and each XCD takes
-    // one contiguous eighth of the pair list, so a pose's blocks are reused from that XCD's L2
-    const int chunk = (np + 7) >> 3;
+    // one contiguous eighth of the unit list (pair order), so a pose's blocks are reused from that
+    // XCD's L2
+    const int chunk = (nUnits + 7) >> 3;
+    const int n = 6 * d.P;
     for (int vb = blockIdx.x; (vb >> 3) < chunk; vb += gridDim.x) {
-        const int k = (vb & 7) * chunk + (vb >> 3);
+        const int un = (vb & 7) * chunk + (vb >> 3);
+        if (un >= nUnits) continue;
+        double acc[64];
+#pragma unroll
+        for (int i = 0; i < 64; i++) acc[i] = 0.0;
+        if (un >= nBig) {   // one pair per wave
+            const int sidx = (un - nBig) * kSpW + wave;
+            if (sidx >= nSmall) continue;
+            const int k = d.pairUnits[nBig + sidx];
+            if (k >= np) continue;
+            const int pr = __builtin_amdgcn_readfirstlane(d.pairs[k]);
+            const int bi = pr >> 16, bj = pr & 0xFFFF;
+            const int t0 = d.tripStart[2 * k], tn = d.tripStart[2 * k + 1];
+            for (int m = lane; m < tn; m += 64) {
+                const int2 tr = d.trips[t0 + m];
+                sp_product(d, acc, tr.x, tr.y, 0, false);
+            }
+            sp_wave_reduce(acc, lane);   // lane v: value v
+            if (lane < 36) {
+                const int r = lane / 6, qq = lane % 6;
+                const double val = 0.0 - acc[0];
+                d.S[(size_t)(6 * bi + r) * n + 6 * bj + qq] = val;
+                d.S[(size_t)(6 * bj + qq) * n + 6 * bi + r] = val;
+            }
+            continue;
+        }
+        const int k = d.pairUnits[un];
         if (k >= np) continue;
         const int pr = __builtin_amdgcn_readfirstlane(d.pairs[k]);
         const int bi = pr >> 16, bj = pr & 0xFFFF;
         const bool diag = bi == bj;
-        double acc[64];
-#pragma unroll
-        for (int i = 0; i < 64; i++) acc[i] = 0.0;
-        // the product of one shared landmark: A_e1 against Hpl_e2; diagonal blocks (e2 == e1) also
-        // b_s's Hpl_e1 D^-1 b_l
-        auto product = [&](int e1, int e2, int l) {
-            const double2* Ui = reinterpret_cast<const double2*>(d.Ae + 18 * (size_t)e1);
-            const double2* Bj = reinterpret_cast<const double2*>(d.HplP + 18 * (size_t)e2);
-            double v[18], u[18];
-#pragma unroll
-            for (int h = 0; h < 9; h++) {
-                const double2 x = Ui[h], y = Bj[h];
-                u[2 * h] = x.x; u[2 * h + 1] = x.y;
-                v[2 * h] = y.x; v[2 * h + 1] = y.y;
-            }
-            // three fused multiply-adds per entry (the terms accumulate straight into the partial)
-#pragma unroll
-            for (int r = 0; r < 6; r++)
-#pragma unroll
-                for (int q = 0; q < 6; q++)
-                    acc[r * 6 + q] = __builtin_fma(u[r * 3 + 2], v[q * 3 + 2],
-                                                   __builtin_fma(u[r * 3 + 1], v[q * 3 + 1],
-                                                                 __builtin_fma(u[r * 3], v[q * 3], acc[r * 6 + q])));
-            if (diag) {
-                const double* db = d.db + 3 * (size_t)l;
-                const double g0 = db[0], g1 = db[1], g2 = db[2];
-#pragma unroll
-                for (int i = 0; i < 6; i++)
-                    acc[36 + i] = __builtin_fma(v[i * 3 + 2], g2, __builtin_fma(v[i * 3 + 1], g1, __builtin_fma(v[i * 3], g0, acc[36 + i])));
-            }
-        };
         if (diag) {   // every edge of pose i pairs with itself: already a dense list
             const int a0 = d.poStart[bi], a1 = d.poStart[bi + 1];
-            for (int a = a0 + tid; a < a1; a += kSpT) product(a, a, d.poPt[a]);
+            for (int a = a0 + tid; a < a1; a += kSpT) sp_product(d, acc, a, a, d.poPt[a], true);
         } else {
             // off-diagonal: the pair's shared landmarks, listed once per solve by k_pair_trip
             const int t0 = d.tripStart[2 * k], tn = d.tripStart[2 * k + 1];
             for (int m = tid; m < tn; m += kSpT) {
                 const int2 tr = d.trips[t0 + m];
-                product(tr.x, tr.y, 0);
+                sp_product(d, acc, tr.x, tr.y, 0, false);
             }
         }
-        reduce_halve<32>(acc, lane);
-        reduce_halve<16>(acc, lane);
-        reduce_halve<8>(acc, lane);
-        reduce_halve<4>(acc, lane);
-        reduce_halve<2>(acc, lane);
-        reduce_halve<1>(acc, lane);
+        sp_wave_reduce(acc, lane);
         wsum[wave][lane] = acc[0];   // value v = lane
         __syncthreads();
         const int v = lane, nv = diag ? 42 : 36;
@@ -1080,7 +1118,6 @@ __global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag) {
         // a diagonal block's product (Hpl D^-1) Hpl^T is not bitwise symmetric: only its upper
         // triangle (r <= qq) is stored, mirrored, as g2o fills S from the upper blocks
         if (wave == 0 && v < nv && !(diag && v < 36 && v / 6 > v % 6)) {
-            const int n = 6 * d.P;
             if (v < 36) {
                 const int r = v / 6, qq = v % 6;
                 double val = 0.0;
@@ -1142,39 +1179,63 @@ __global__ __launch_bounds__(256) void k_pair_mark(LbaDev d, int32_t* __restrict
 }
 // the marked blocks compacted in index order (one workgroup): pairs[k] = bi << 16 | bj, *npairs
 // ... and, per listed pair, where its shared-landmark list starts (tripStart[2k]) and its length
-// ([2k + 1]) in the trips buffer k_pair_trip fills (offsets in list order)
+// ([2k + 1]) in the trips buffer k_pair_trip fills (offsets in list order); k_schur_pairs' work
+// units: units[0 .. npairs[1]) the pairs a workgroup takes (diagonal, or more than `small` shared
+// landmarks), then the npairs[2] pairs a wave takes, each in list order
 __global__ __launch_bounds__(1024) void k_pair_list(const int32_t* __restrict__ flag, const int32_t* __restrict__ cnt,
                                                     int P, int32_t* __restrict__ pairs, int32_t* __restrict__ npairs,
-                                                    int32_t* __restrict__ tripStart) {
-    __shared__ int wsum[16], tsum[16];
+                                                    int32_t* __restrict__ tripStart, int32_t* __restrict__ units,
+                                                    int small) {
+    __shared__ int wsum[16], tsum[16], bsum[16];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int N = P * (P + 1) / 2;
     const int chunk = (N + 1023) / 1024, c0 = min(tid * chunk, N), c1 = min(c0 + chunk, N);
-    int loc = 0, tloc = 0;
-    for (int i = c0; i < c1; i++) {
-        loc += flag[i] ? 1 : 0;
-        tloc += flag[i] ? cnt[i] : 0;
+    int bi0 = 0, bj0 = 0;
+    if (c0 < c1) {   // index -> (bi, bj) of the first entry, then walk
+        int rem = c0;
+        while (rem >= P - bi0) { rem -= P - bi0; bi0++; }
+        bj0 = bi0 + rem;
     }
-    const int incl = wave_incl_scan_i32(loc), tincl = wave_incl_scan_i32(tloc);
-    if (lane == 63) { wsum[wave] = incl; tsum[wave] = tincl; }
+    int loc = 0, tloc = 0, bloc = 0;
+    {
+        int bi = bi0, bj = bj0;
+        for (int i = c0; i < c1; i++) {
+            if (flag[i]) {
+                loc++;
+                tloc += cnt[i];
+                bloc += (bi == bj || cnt[i] > small) ? 1 : 0;
+            }
+            if (++bj == P) { bi++; bj = bi; }
+        }
+    }
+    const int incl = wave_incl_scan_i32(loc), tincl = wave_incl_scan_i32(tloc), bincl = wave_incl_scan_i32(bloc);
+    if (lane == 63) { wsum[wave] = incl; tsum[wave] = tincl; bsum[wave] = bincl; }
     __syncthreads();
-    int run = incl - loc, trun = tincl - tloc;
-    for (int w = 0; w < wave; w++) { run += wsum[w]; trun += tsum[w]; }
+    int run = incl - loc, trun = tincl - tloc, brun = bincl - bloc, nBig = 0;
+    for (int w = 0; w < 16; w++) {
+        if (w < wave) { run += wsum[w]; trun += tsum[w]; brun += bsum[w]; }
+        nBig += bsum[w];
+    }
+    int srun = nBig + (run - brun);   // the wave pairs follow the workgroup pairs
     if (c0 < c1) {
-        int bi = 0, rem = c0;   // index -> (bi, bj) of the first entry, then walk
-        while (rem >= P - bi) { rem -= P - bi; bi++; }
-        int bj = bi + rem;
+        int bi = bi0, bj = bj0;
         for (int i = c0; i < c1; i++) {
             if (flag[i]) {
                 tripStart[2 * run] = trun;
                 tripStart[2 * run + 1] = cnt[i];
                 trun += cnt[i];
+                if (bi == bj || cnt[i] > small) units[brun++] = run;
+                else units[srun++] = run;
                 pairs[run++] = (bi << 16) | bj;
             }
             if (++bj == P) { bi++; bj = bi; }
         }
     }
-    if (tid == 1023) *npairs = run;
+    if (tid == 1023) {
+        npairs[0] = run;
+        npairs[1] = nBig;
+        npairs[2] = run - nBig;
+    }
 }
 
 // the inverse of the pose-major lists: poPos[poAct[a]] = a
@@ -4662,16 +4723,17 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         for (int e = 0; e < NE; e++) kf[(size_t)p->edge_point[e]] += p->pose_fixed[p->edge_pose[e]] ? 0 : 1;
         size_t ntrip = 0;
         for (int l = 0; l < NM; l++) ntrip += (size_t)kf[(size_t)l] * (kf[(size_t)l] - 1) / 2;
-        int32_t *flag, *cnt, *pairs, *npairs, *tripStart, *poPos;
+        int32_t *flag, *cnt, *pairs, *npairs, *tripStart, *poPos, *units;
         int2* trips;
         TRY(dalloc(c, &poPos, std::max(NE, 1)));
         ORB_HIP_TRY(hipMemsetAsync(poPos, 0xFF, 4 * (size_t)std::max(NE, 1), s));   // -1: fixed-pose edges
         if (P > 0) hipLaunchKernelGGL(k_po_pos, grid(NE), dim3(256), 0, s, d, poPos);
         d.poPos = poPos;
-        TRY(dalloc(c, &flag, 2 * (size_t)np2)); TRY(dalloc(c, &pairs, np2)); TRY(dalloc(c, &npairs, 1));
+        TRY(dalloc(c, &flag, 2 * (size_t)np2)); TRY(dalloc(c, &pairs, np2)); TRY(dalloc(c, &npairs, 3));
+        TRY(dalloc(c, &units, std::max(np2, 1)));
         TRY(dalloc(c, &tripStart, 2 * (size_t)np2)); TRY(dalloc(c, &trips, std::max<size_t>(ntrip, 1)));
         cnt = flag + np2;
-        ORB_HIP_TRY(hipMemsetAsync(npairs, 0, 4, s));
+        ORB_HIP_TRY(hipMemsetAsync(npairs, 0, 12, s));
         if (P > 0) {
             ORB_HIP_TRY(hipMemsetAsync(flag, 0, 8 * (size_t)np2, s));
             ORB_HIP_TRY(hipMemsetAsync(d.S, 0, 8 * (size_t)36 * P * P, s));
@@ -4701,7 +4763,13 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
             }
             hipLaunchKernelGGL(k_pair_mark, grid(std::max(d.M, P)), dim3(256), np2 <= kPairHist ? 4 * (size_t)np2 : 0, s, d,
                                flag, cnt, 0);
-            hipLaunchKernelGGL(k_pair_list, dim3(1), dim3(1024), 0, s, flag, cnt, P, pairs, npairs, tripStart);
+            // off-diagonal pairs sharing at most this many landmarks take one wave in k_schur_pairs
+            static const int smallPair = [] {
+                const char* e = std::getenv("ORB_LBA_SMALL_PAIR");
+                return e ? std::atoi(e) : 512;
+            }();
+            hipLaunchKernelGGL(k_pair_list, dim3(1), dim3(1024), 0, s, flag, cnt, P, pairs, npairs, tripStart, units,
+                               smallPair);
             d.pairs = pairs;
             d.npairs = npairs;
             d.tripStart = tripStart;
@@ -4723,6 +4791,7 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
         }
         d.pairs = pairs;
         d.npairs = npairs;
+        d.pairUnits = units;
         d.tripStart = tripStart;
         d.trips = trips;
         return ORB_OK;
