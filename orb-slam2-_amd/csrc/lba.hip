@@ -1746,6 +1746,40 @@ __device__ __forceinline__ void pose_tail(const PoseTail& pt, const double* xs, 
     if (lane == 0) *pt.scaleOut = sc;
 }
 
+// pose_tail for at most 64 free poses in two halves: the inputs that do not depend on x (pose,
+// b_p, indices) loaded before the backward substitution, so their latency hides under it
+struct PoseTailPre {
+    double q[4], t[3], bp[6];
+    int k;
+};
+__device__ __forceinline__ void pose_tail_prefetch(const PoseTail& pt, int lane, PoseTailPre& f) {
+    const int i = min(lane, max(pt.P - 1, 0));
+    const int p = pt.freePoses[i];
+    f.k = pt.poseIdx[p];
+    for (int j = 0; j < 4; j++) f.q[j] = pt.q[4 * p + j];
+    for (int j = 0; j < 3; j++) f.t[j] = pt.t[3 * p + j];
+    for (int j = 0; j < 6; j++) f.bp[j] = pt.bp[6 * f.k + j];
+}
+__device__ __forceinline__ void pose_tail_finish(const PoseTail& pt, const double* xs, double lambda, int lane,
+                                                 PoseTailPre& f) {
+    double sc = 0.0;
+    if (lane < pt.P) {
+        const int p = pt.freePoses[lane];
+        for (int j = 0; j < 4; j++) pt.bq[4 * p + j] = f.q[j];
+        for (int j = 0; j < 3; j++) pt.bt[3 * p + j] = f.t[j];
+        double u[6];
+        for (int j = 0; j < 6; j++) {
+            u[j] = xs[6 * f.k + j];
+            sc += u[j] * (lambda * u[j] + f.bp[j]);
+        }
+        d_se3_exp_left(u, f.q, f.t);
+        for (int j = 0; j < 4; j++) pt.q[4 * p + j] = f.q[j];
+        for (int j = 0; j < 3; j++) pt.t[3 * p + j] = f.t[j];
+    }
+    sc = wave_sum_d(sc);
+    if (lane == 0) *pt.scaleOut = sc;
+}
+
 template <bool kLds>
 __global__ __launch_bounds__(kLdlT) void k_ldlt_solve(const double* __restrict__ Sg, const double* __restrict__ b,
                                                       int n, double* __restrict__ work, double* __restrict__ x,
@@ -2516,6 +2550,10 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_df(const double* __restrict__ Sg
 #ifdef ORB_TIMING
                 const long long tfs = clock64();
 #endif
+                // the diagonal block's follower gates the next panel: it takes issue priority over
+                // the plain follower sharing its SIMD (solve stage 0.484 -> 0.470 ms per config-4
+                // solve in a same-box A/B; the same for the kNext follower gained nothing more)
+                __builtin_amdgcn_s_setprio(3);
                 follow(F, I >= 2);
 #ifdef ORB_TIMING
                 if (lane == 0 && kb < 8) { dbgT[2 * kb] = tfs; dbgT[2 * kb + 1] = clock64(); }
@@ -2532,6 +2570,7 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_df(const double* __restrict__ Sg
 #endif
                 *(lane == 0 ? diagReady : (volatile lds_i32*)(sinkI + lane)) = I;
                 *(lane == 0 ? rowDone + I : (volatile lds_i32*)(sinkI + lane)) = kb + 1;
+                __builtin_amdgcn_s_setprio(0);
             } else if (kb == I - 2) {   // the diagonal block is I - 1: tile (I, I - 1) in registers
                 DfFollow<kNext> F;
                 F.rbK = rb - kNB;
@@ -2578,6 +2617,8 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_df(const double* __restrict__ Sg
     }
     __syncthreads();
     if (wave != 0) return;
+    PoseTailPre ptf;   // (P <= 21 here: np <= 128)
+    if (ptail.scaleOut) pose_tail_prefetch(ptail, lane, ptf);
     const int i1 = 64 + lane;
     double X0 = lane < np ? y[lane] * rdg[lane] : 0.0;
     double X1 = i1 < np ? y[i1] * rdg[i1] : 0.0;
@@ -2625,7 +2666,7 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_df(const double* __restrict__ Sg
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        pose_tail(ptail, y, st->lambda, lane);
+        pose_tail_finish(ptail, y, st->lambda, lane, ptf);
     }
 #ifdef ORB_TIMING
     if (lane == 0) {
