@@ -2219,6 +2219,9 @@ struct DfPivot {
     int k, seq;
     volatile lds_f64 *pU, *pRG, *rowW, *rowR;
     volatile lds_i32* pC;
+#ifdef ORB_TIMING
+    long long* tp = nullptr;   // per column: the publish time
+#endif
     template <int C>
     __device__ __forceinline__ void col() {
         double P1 = 0.0, w = 0.0, rdn = 1.0;
@@ -2242,6 +2245,9 @@ struct DfPivot {
         pRG[2 * C] = rd;
         pRG[2 * C + 1] = rd * yc;
         *pC = seq + C + 1;
+#ifdef ORB_TIMING
+        if (tp) tp[C] = clock64();
+#endif
         if constexpr (C + 1 < kNB) {
             R = __builtin_fma(-w, u, P1);
             rd = rdn;
@@ -2275,9 +2281,15 @@ struct DfFollow {
     const volatile lds_i32* cnt;
     volatile lds_i32* chunk;
     lds_f64 *A, *sinkD;
+#ifdef ORB_TIMING
+    long long* tg = nullptr;   // per group: arrival, poll satisfied, group end; [12..15]: counter seen on arrival
+#endif
     template <int C>
     __device__ __forceinline__ void col() {
         const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+#ifdef ORB_TIMING
+        if constexpr ((C & 3) == 0) if (tg) { tg[3 * (C / 4)] = clock64(); tg[12 + C / 4] = __builtin_amdgcn_readfirstlane(*cnt) - seq; }
+#endif
         if constexpr (kMode == kDiag && C == 0) {
             if (defer) {   // (the pivot has only just started: this overlaps the wait for its columns)
                 const int jp = jb - kNB;
@@ -2308,6 +2320,9 @@ struct DfFollow {
             }
             // the previous group's MFMA, its operands' LDS round trip hidden behind this group's
             if constexpr (kMode != kPlain && C > 0) T = __builtin_amdgcn_mfma_f64_16x16x4f64(pa, pb, T, 0, 0, 0);
+#ifdef ORB_TIMING
+            if (tg) tg[3 * (C / 4) + 1] = clock64();
+#endif
         }
         const double u = uq[C & 3];
         const double g = gq[C & 3];
@@ -2343,6 +2358,9 @@ struct DfFollow {
                     A[(size_t)r * ld + jb + k] = X[s] * rdkThis;
                 }
             }
+#ifdef ORB_TIMING
+            if (tg) tg[3 * (C / 4) + 2] = clock64();
+#endif
             const int pc = jb + (C - 3) + lk;
             const int grp = (seq + C + 1) >> 2;   // 4 kb + this group + 1
             if constexpr (kMode == kDiag) {
@@ -2394,6 +2412,7 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_df(const double* __restrict__ Sg
     __shared__ int failS;
 #ifdef ORB_TIMING
     __shared__ long long dbgT[32];
+    __shared__ long long tgS[16], tpS[16];
 #endif
     if (tid == 0) { failS = 0; *cnt = 0; }
     if (tid < 10) rowDone[tid] = 0;
@@ -2490,8 +2509,16 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_df(const double* __restrict__ Sg
 #ifdef ORB_TIMING
             if (kb < 8) tdf[3 + 4 * kb] = clock64();
 #endif
+#ifdef ORB_TIMING
+            long long tpl[16];
+            P.tp = kb == 3 ? tpl : nullptr;
+#endif
             if (nc >= kNB) ColUnroll<0, kNB>::run(P);
             else ColUnrollTo<0, kNB>::run(P, nc);
+#ifdef ORB_TIMING
+            if (kb == 3 && lane == 0)
+                for (int i = 0; i < 16; i++) tpS[i] = tpl[i];
+#endif
 #ifdef ORB_TIMING
             if (kb < 8) tdf[4 + 4 * kb] = clock64();
 #endif
@@ -2554,7 +2581,15 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_df(const double* __restrict__ Sg
                 // the plain follower sharing its SIMD (solve stage 0.484 -> 0.470 ms per config-4
                 // solve in a same-box A/B; the same for the kNext follower gained nothing more)
                 __builtin_amdgcn_s_setprio(3);
+#ifdef ORB_TIMING
+                long long tgl[16];
+                F.tg = kb == 3 ? tgl : nullptr;
+#endif
                 follow(F, I >= 2);
+#ifdef ORB_TIMING
+                if (kb == 3 && lane == 0)
+                    for (int i = 0; i < 16; i++) tgS[i] = tgl[i];
+#endif
 #ifdef ORB_TIMING
                 if (lane == 0 && kb < 8) { dbgT[2 * kb] = tfs; dbgT[2 * kb + 1] = clock64(); }
 #endif
@@ -2679,6 +2714,14 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_df(const double* __restrict__ Sg
         for (int kb = 0; kb + 1 < T && kb < 7; kb++)
             printf(" %lld/%lld/%lld", dbgT[2 * kb] - tdf[3 + 4 * kb], dbgT[2 * kb + 1] - tdf[4 + 4 * kb], dbgT[16 + kb] - tdf[4 + 4 * kb]);
         printf("\n");
+        if (T > 4) {   // panel 3: the pivot's column publish times and the diagonal follower's groups (vs the pivot loop start)
+            const long long t0 = tdf[3 + 4 * 3];
+            printf("ldlt_df panel 3 pivot publish:");
+            for (int i = 0; i < 16; i++) printf(" %lld", tpS[i] - t0);
+            printf(" | diag follower group arrive/polled/end (counter seen on arrival):");
+            for (int g = 0; g < 4; g++) printf(" %lld/%lld/%lld(%lld)", tgS[3 * g] - t0, tgS[3 * g + 1] - t0, tgS[3 * g + 2] - t0, tgS[12 + g]);
+            printf("\n");
+        }
     }
 #endif
 }
