@@ -4848,10 +4848,9 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
             hipLaunchKernelGGL(k_pair_mark, grid(std::max(d.M, P)), dim3(256), np2 <= kPairHist ? 4 * (size_t)np2 : 0, s, d,
                                flag, cnt, 0);
             // off-diagonal pairs sharing at most this many landmarks take one wave in k_schur_pairs
-            static const int smallPair = [] {
-                const char* e = std::getenv("ORB_LBA_SMALL_PAIR");
-                return e ? std::atoi(e) : 512;
-            }();
+            // (read per solve: tests and A/B runs switch it within one process)
+            const char* spEnv = std::getenv("ORB_LBA_SMALL_PAIR");
+            const int smallPair = spEnv ? std::atoi(spEnv) : 512;
             hipLaunchKernelGGL(k_pair_list, dim3(1), dim3(1024), 0, s, flag, cnt, P, pairs, npairs, tripStart, units,
                                smallPair);
             d.pairs = pairs;

@@ -276,6 +276,22 @@ def test_scaled_local_ba_bitwise_reproducible(amd):
             assert np.array_equal(r[k], runs[0][k]), k
 
 
+@pytest.mark.parametrize("small", ["-1", "0", "64", "100000"])
+def test_schur_pair_units_match_oracle(amd, monkeypatch, small):
+    """k_schur_pairs' work units (k_pair_list): every off-diagonal pose pair sharing at most
+    ORB_LBA_SMALL_PAIR landmarks takes one wave, the others (and the diagonal blocks) a workgroup.
+    All workgroups (-1), all waves (100000) and mixed splits stay within the oracle's tolerances,
+    with identical LM decisions, and each split is bitwise reproducible."""
+    from orb_slam2_amd import synth
+    monkeypatch.setenv("ORB_LBA_SMALL_PAIR", small)
+    pb = synth.ba_problem_corridor(n_local=40, n_fixed=2, n_points=4000, seed=25, stereo_frac=0.2)
+    got = amd.LocalBA().solve(pb)
+    _compare(O.lba_solve(pb), got)
+    again = amd.LocalBA().solve(pb)
+    for k in ("pose_q", "pose_t", "point_xyz", "trace", "edge_erase"):
+        assert np.array_equal(again[k], got[k]), k
+
+
 @pytest.mark.parametrize("kw", [dict(), dict(stereo_frac=0.5, seed=7)])
 def test_schur_mfma_mode_matches_oracle(amd, monkeypatch, kw):
     """ORB_LBA_SCHUR_MFMA=1: the Schur complement as the densified f64 MFMA GEMM S -= Y Y^T
