@@ -1,4 +1,6 @@
-# extraction-leg throughput with per-sequence HIP stream priorities (ORB_BENCH_STREAM_PRIO), interleaved
+# extraction-leg throughput with per-sequence HIP stream priorities (ORB_BENCH_STREAM_PRIO), interleaved.
+# The switch lived in bench.py (SequencePipeline: torch.cuda.Stream(dev, priority=...)) for the round-5
+# measurement only (6-9 % slower) and was removed; re-add it there to repeat the run.
 set -e
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
