@@ -1418,8 +1418,8 @@ def bench_bow(args, amd, dev, n_frames=64, n_feat=1000):
 
 def batch_sweep(amd, dev, m):
     """extract + SearchForInitialization at batch sizes B in {1, 8, 64} on one stream,
-    HBM-resident (B-1 in-batch pairs; B=1 is extraction alone), and the PCIe-inclusive rate at
-    B=64: pinned host frames copied in, keypoints + descriptors + matches copied back, per step."""
+    HBM-resident (B-1 in-batch pairs; B=1 is extraction alone), and the PCIe-inclusive rate at the
+    same sizes: pinned host frames copied in, keypoints + descriptors + matches copied back, per step."""
     from orb_slam2_amd import synth, _abi
     lib = _abi.lib()
     W, H, NF = 640, 480, 1000
@@ -1441,8 +1441,17 @@ def batch_sweep(amd, dev, m):
                 100, C.c_void_p(m12.data_ptr()), C.c_void_p(nm.data_ptr()), C.c_void_p(b["stream"])))
         dt, b = _extract_leg(amd, dev, fr, NF, 20 if B < 64 else 10, 3, sfi, matcher=m if B > 1 else None)
         res[f"B{B}"] = {"frames_per_s": round(B / dt, 1), "ms_per_step": round(dt * 1e3, 4), "status": b["status"]}
-    # PCIe-inclusive, B = 64: H2D of the frames, extraction + matching, D2H of the results
-    B = 64
+    # PCIe-inclusive, B = 1 / 8 / 64: H2D of the frames, extraction + matching, D2H of the results
+    for B in (1, 8, 64):
+        res[f"B{B}_pcie_inclusive"] = _pcie_leg(amd, dev, m, cv, W, H, NF, B)
+    return res
+
+
+def _pcie_leg(amd, dev, m, cv, W, H, NF, B):
+    """One step of B pinned host frames: H2D, extraction (+ SearchForInitialization over the B-1
+    in-batch pairs when B > 1), D2H of keypoints, descriptors and matches; 10 timed steps."""
+    from orb_slam2_amd import synth, _abi
+    lib = _abi.lib()
     fr = np.stack([synth.frame(cv, W, H, t) for t in range(B)])
     host_in = torch.from_numpy(fr).pin_memory()
     ex = amd.ORBextractor(NF, 1.2, 8, 20, 7, device=dev.index or 0, max_w=W, max_h=H, max_batch=B)
@@ -1453,8 +1462,8 @@ def batch_sweep(amd, dev, m):
     kps = torch.zeros((B, cap, 7), dtype=torch.int32, device=dev)
     desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device=dev)
     cnt = torch.zeros(B, dtype=torch.int32, device=dev)
-    m12 = torch.zeros((B - 1, cap), dtype=torch.int32, device=dev)
-    nm = torch.zeros(B - 1, dtype=torch.int32, device=dev)
+    m12 = torch.zeros((max(B - 1, 1), cap), dtype=torch.int32, device=dev)
+    nm = torch.zeros(max(B - 1, 1), dtype=torch.int32, device=dev)
     h_kps = torch.empty(kps.shape, dtype=kps.dtype).pin_memory()
     h_desc = torch.empty(desc.shape, dtype=desc.dtype).pin_memory()
     h_m12 = torch.empty(m12.shape, dtype=m12.dtype).pin_memory()
@@ -1465,14 +1474,16 @@ def batch_sweep(amd, dev, m):
         _abi.check("x", lib.orb_extract_batch_device(ex._h, C.c_void_p(imgs.data_ptr()), H * W, B, W, H,
                                                       C.c_void_p(kps.data_ptr()), C.c_void_p(desc.data_ptr()), cap,
                                                       C.c_void_p(cnt.data_ptr()), C.c_void_p(st)))
-        _abi.check("sfi", lib.orb_search_for_initialization_batch_device(
-            m._h, C.c_void_p(kps.data_ptr()), C.c_void_p(desc.data_ptr()), C.c_void_p(cnt.data_ptr()),
-            C.c_void_p(kps.data_ptr() + cap * 28), C.c_void_p(desc.data_ptr() + cap * 32),
-            C.c_void_p(cnt.data_ptr() + 4), B - 1, cap, W, H, 100, C.c_void_p(m12.data_ptr()),
-            C.c_void_p(nm.data_ptr()), C.c_void_p(st)))
+        if B > 1:
+            _abi.check("sfi", lib.orb_search_for_initialization_batch_device(
+                m._h, C.c_void_p(kps.data_ptr()), C.c_void_p(desc.data_ptr()), C.c_void_p(cnt.data_ptr()),
+                C.c_void_p(kps.data_ptr() + cap * 28), C.c_void_p(desc.data_ptr() + cap * 32),
+                C.c_void_p(cnt.data_ptr() + 4), B - 1, cap, W, H, 100, C.c_void_p(m12.data_ptr()),
+                C.c_void_p(nm.data_ptr()), C.c_void_p(st)))
         h_kps.copy_(kps, non_blocking=True)
         h_desc.copy_(desc, non_blocking=True)
-        h_m12.copy_(m12, non_blocking=True)
+        if B > 1:
+            h_m12.copy_(m12, non_blocking=True)
 
     for _ in range(3):
         step()
@@ -1483,11 +1494,10 @@ def batch_sweep(amd, dev, m):
         step()
     torch.cuda.synchronize(dev)
     dt = (time.perf_counter() - t0) / reps
-    res["B64_pcie_inclusive"] = {"frames_per_s": round(B / dt, 1), "ms_per_step": round(dt * 1e3, 4),
-                                 "status": batch_status(ex, m, "PCIe-inclusive leg"),
-                                 "h2d_bytes": int(host_in.numel()),
-                                 "d2h_bytes": int(kps.numel() * 4 + desc.numel() + m12.numel() * 4)}
-    return res
+    return {"frames_per_s": round(B / dt, 1), "ms_per_step": round(dt * 1e3, 4),
+            "status": batch_status(ex, m, f"PCIe-inclusive leg B={B}"),
+            "h2d_bytes": int(host_in.numel()),
+            "d2h_bytes": int(kps.numel() * 4 + desc.numel() + (m12.numel() * 4 if B > 1 else 0))}
 
 
 class Pipe:
