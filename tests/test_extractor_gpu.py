@@ -45,6 +45,23 @@ def test_extract_matches_oracle(amd, W, H, nf, seed):
         _compare(ref, kps, desc)
 
 
+@pytest.mark.parametrize("W,H,nf,scale,nlev,ini,minth,seed", [
+    (639, 479, 800, 1.25, 6, 15, 5, 0x5EED0011),     # odd sizes (level 0 copied into the slab), other pyramid
+    (320, 240, 500, 1.2, 8, 20, 7, 0x5EED0012),      # small frame: few cells per level
+    (1024, 768, 1500, 1.3, 5, 25, 9, 0x5EED0013),    # coarse pyramid, high thresholds
+    (800, 600, 1200, 1.15, 10, 12, 4, 0x5EED0014),   # fine pyramid, ten levels, low thresholds
+])
+def test_extract_parameters_match_oracle(amd, W, H, nf, scale, nlev, ini, minth, seed):
+    """ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST) away from the defaults
+    (R/src/ORBextractor.cpp:421-485): every geometry-derived table (level sizes, cell grids, resize
+    coefficients, per-level feature quotas) and both FAST thresholds, bit-exact against the oracle."""
+    ex = amd.ORBextractor(nf, scale, nlev, ini, minth, max_w=W, max_h=H)
+    p = O.params(nf, scale, nlev, ini, minth)
+    for img in _frames(W, H, seed, 2):
+        kps, desc = ex(img)
+        _compare(O.extract(p, img), kps, desc)
+
+
 def test_extract_geometry_changes_on_one_handle(amd):
     """One handle created for the default bound (1280 x 1024), then fed 640 x 480, KITTI and 640 x 480
     again: every geometry change rebuilds the resize tables and the pyramid band table (which an
