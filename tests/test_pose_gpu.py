@@ -26,6 +26,10 @@ def _check(amd, frames, tol=1e-5):
     dict(stereo_frac=0.5, seed=9),                     # mixed stereo / monocular
     dict(n_points=60, outlier_frac=0.3, seed=2),       # few points, many outliers
     dict(n_points=1500, seed=4, rot_noise=0.03, trans_noise=0.05),
+    dict(stereo_frac=1.0, seed=14),                    # every edge stereo (EdgeStereoSE3ProjectXYZOnlyPose)
+    dict(n_points=300, outlier_frac=0.6, seed=15),     # outliers the majority: many flips between rounds
+    dict(n_points=1024, seed=16, rot_noise=0.05, trans_noise=0.1),   # the register path's largest frame, far start
+    dict(n_points=11, seed=17),                        # just above the one-round limit (n >= 10: four rounds)
 ])
 def test_pose_optimization_matches_oracle(amd, kw):
     from orb_slam2_amd import synth
