@@ -34,13 +34,18 @@ def _compare(ref, got, tol=1e-5):
     dict(n_local=8, n_fixed=2, n_points=500, seed=3),
     dict(n_local=30, n_fixed=0, n_points=4000, seed=11, outlier_frac=0.15),
     dict(n_local=30, n_fixed=4, n_points=400, seed=13, k_range=(17, 30)),   # landmarks seen by 17-30 KFs
+    dict(stereo_frac=1.0, seed=19, n_points=2000),            # every edge stereo (EdgeStereoSE3ProjectXYZ)
+    dict(n_local=2, n_fixed=1, n_points=300, seed=20, k_range=(2, 3)),      # two local KFs (one free pose)
+    dict(n_local=21, n_fixed=4, n_points=2500, seed=26),      # 20 free poses: n = 120, the LDS-image limit
+    dict(n_local=12, n_fixed=2, n_points=1500, seed=27, outlier_frac=0.4),  # many erased edges
 ])
 def test_local_ba_matches_oracle(amd, kw):
     pb = _problem(amd, **kw)
     ref = O.lba_solve(pb)
     got = amd.LocalBA().solve(pb)
-    q0, _ = O.quat_from_Tcw(pb["Tcw"][3])
-    assert np.array_equal(got["init_q"][3], q0)      # Converter::toSE3Quat parity
+    kc = min(3, len(pb["Tcw"]) - 1)
+    q0, _ = O.quat_from_Tcw(pb["Tcw"][kc])
+    assert np.array_equal(got["init_q"][kc], q0)     # Converter::toSE3Quat parity
     _compare(ref, got)
 
 
