@@ -87,6 +87,31 @@ def pmc_valu_ops(kernel, W, H, NF, Bs):
 
 
 PMC_LANES = ROOT / "profiles" / "r05_lanes_pmc.json"   # tools/pmc_run.sh lanes ... + tools/pmc_lanes.py
+# rocprofv3 --kernel-trace --stats of the bench's own 128-frame extraction launch run alone on one
+# stream (tools/gpu_ext_isolated.sh: bench.py --streams 1 --batch 128), formatted by
+# tools/kernel_stats.py; the headline roofline's kernel durations come from it
+ISOLATED_STATS = ROOT / "profiles" / "r06_ext_isolated_stats.txt"
+
+
+def isolated_stats():
+    """{kernel: avg_us} and the header lines of the committed isolated-launch rocprof summary
+    (None when absent).  Kernel names as kernel_stats.py prints them (`void k_fast_cell<40>`)."""
+    try:
+        lines = ISOLATED_STATS.read_text().splitlines()
+    except OSError:
+        return None
+    out, head = {}, []
+    for ln in lines:
+        if "calls=" in ln and "avg_us=" in ln:
+            name = ln.split("calls=")[0].strip()
+            name = name.replace("void ", "").split("<")[0]
+            calls = int(ln.split("calls=")[1].split()[0])
+            avg = float(ln.split("avg_us=")[1].split()[0])
+            if name not in out or calls > out[name][0]:
+                out[name] = (calls, avg)
+        elif ln.strip():
+            head.append(ln.strip())
+    return {"avg_us": {k: v[1] for k, v in out.items()}, "calls": {k: v[0] for k, v in out.items()}, "header": head}
 
 
 def pmc_lane_util(kernel, W, H, NF, Bs):
@@ -238,52 +263,88 @@ def measure_copy_peak(dev, mib=1024, reps=8):
     return round(gbs, 1)
 
 
-def extraction_roofline(stage_ms, ncalls, lw, lh, n_pre, n_out, W, H, NF, Bs):
-    """SURVEY §8d roofline of every extraction kernel of the timed region, and the dominant one
-    (largest average launch time) as the line's `roofline`.  achieved = the kernel's algorithmic
-    HBM bytes per launch (algorithmic_bytes x the frames of a launch) / its average launch time
-    (HIP events on its stream, timed region); peak 8 TB/s; traffic = PMC FETCH_SIZE x 2 +
-    WRITE_SIZE per launch from the committed pass of this configuration (None when absent).  Each
-    kernel also carries its VALU view (issued lane-ops from the committed PMC pass, against the
-    78.6 T nominal and the measured wave64 issue rate) and its algorithmic-op rate (ALG_OPS)."""
+def extraction_roofline(stage_ms, ncalls, lw, lh, n_pre, n_out, W, H, NF, Bs, iso_ms=None, launches_per_step=1,
+                        ms_per_step=None):
+    """SURVEY §8d roofline of every extraction kernel, and the dominant one as the line's `roofline`.
+
+    Per kernel two durations: `shared_launch_ms` = the average launch time inside the timed region
+    (HIP events on its stream while the other streams' kernels share the chip; a span, not the
+    kernel's own duration) and `isolated_launch_ms` = the same 128-frame launch run alone on one
+    stream — from the committed rocprofv3 summary ISOLATED_STATS (`isolated_source`), with the
+    live HIP-event measurement of this run's isolated pass beside it (`isolated_live_ms`).  The
+    fractions use the isolated duration:
+      hbm:  achieved = algorithmic bytes per launch (algorithmic_bytes x frames) / duration, peak 8 TB/s;
+      valu: achieved = issued lane-ops per launch (SQ_INSTS_VALU x 64, committed PMC pass) /
+            duration, peak 78.6 T (nominal), also against the measured 41.7 T integer issue rate.
+    The dominant kernel is the one with the largest isolated duration; `bound` is whichever of
+    its two fractions (HBM of 8 TB/s, VALU of the measured issue rate) is higher."""
+    iso_file = isolated_stats()
     per = {}
     for name, stage, i in EXT_KERNELS:
-        ms = float(stage_ms[i]) / ncalls
-        if ms <= 0:
+        ms = float(stage_ms[i]) / ncalls if ncalls else 0.0
+        live = None if iso_ms is None else float(iso_ms[i])
+        f_ms = None
+        if iso_file and name in iso_file["avg_us"]:
+            f_ms = iso_file["avg_us"][name] / 1e3
+        dur = f_ms if f_ms else live
+        if not dur or dur <= 0:
             continue
         byts = algorithmic_bytes(stage, lw, lh, n_pre, n_out) * Bs
-        gbs = byts / (ms * 1e-3) / 1e9
-        k = {"launch_ms": round(ms, 4), "algorithmic_bytes_per_launch": int(byts), "achieved_gbs": round(gbs, 2),
-             "frac": round(gbs / HBM_PEAK_GBS, 5), "traffic": pmc_traffic(name, W, H, NF, Bs)}
+        gbs = byts / (dur * 1e-3) / 1e9
+        k = {"isolated_launch_ms": round(dur, 4), "isolated_source": ISOLATED_STATS.name if f_ms else "live HIP events",
+             "isolated_live_ms": None if live is None else round(live, 4),
+             "live_over_file": None if (live is None or not f_ms) else round(live / f_ms, 3),
+             "shared_launch_ms": round(ms, 4) if ms > 0 else None,
+             "algorithmic_bytes_per_launch": int(byts), "achieved_gbs": round(gbs, 2),
+             "hbm_frac": round(gbs / HBM_PEAK_GBS, 5), "traffic": pmc_traffic(name, W, H, NF, Bs)}
         if k["traffic"]:
             k["traffic_over_algorithmic"] = round(k["traffic"] / byts, 3)
+            k["traffic_gbs"] = round(k["traffic"] / (dur * 1e-3) / 1e9, 2)
         alg = algorithmic_ops(stage, lw, lh, n_pre, n_out) * Bs
-        k["algorithmic_ops"] = {"ops_per_launch": int(alg), "achieved_tops": round(alg / (ms * 1e-3) / 1e12, 3),
-                                "frac": round(alg / (ms * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4)}
+        k["algorithmic_ops"] = {"ops_per_launch": int(alg), "achieved_tops": round(alg / (dur * 1e-3) / 1e12, 3),
+                                "frac": round(alg / (dur * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4)}
         ops = pmc_valu_ops(name, W, H, NF, Bs)
         if ops is not None:
-            ach = ops / (ms * 1e-3) / 1e12
+            ach = ops / (dur * 1e-3) / 1e12
             k["valu"] = {"lane_ops_per_launch": ops, "achieved_tops": round(ach, 3), "peak": VALU_PEAK_TOPS,
                          "frac": round(ach / VALU_PEAK_TOPS, 4), "measured_issue_peak": VALU_MEASURED_TOPS,
                          "frac_of_measured_issue_peak": round(ach / VALU_MEASURED_TOPS, 4),
-                         "frac_of_measured_f32_issue_peak": round(ach / VALU_MEASURED_F32_TOPS, 4),
-                         "issue_peak_source": "profiles/r05_valu_issue.txt (all-running window; int VOP3 / f32 FMA)"}
+                         "issued_over_algorithmic": round(ops / max(alg, 1), 2),
+                         "issue_peak_source": "profiles/r05_valu_issue.txt (all-running window; int VOP3)"}
             util = pmc_lane_util(name, W, H, NF, Bs)
             if util is not None:
                 k["valu"]["active_lane_frac"] = util
         per[name] = k
     if not per:
         return None
-    dom = max(per, key=lambda n: per[n]["launch_ms"])
+    dom = max(per, key=lambda n: per[n]["isolated_launch_ms"])
     d = per[dom]
-    return {"bound": "hbm", "kernel": dom, "achieved": d["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": d["frac"], "traffic": d["traffic"],
-            "traffic_unit": "bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE, profiles/)",
-            "launch_ms": d["launch_ms"], "frames_per_launch": Bs,
-            "algorithmic_bytes_per_launch": d["algorithmic_bytes_per_launch"],
-            "bytes_model": "SURVEY 8d per kernel: k_pyramid P0 + sum_{l>=1} P_l; k_fast_cell sum_l P_l + 4 N_pre; "
-                           "k_octree 4 (N_pre + N); k_orient_desc N (43^2 + 60)",
-            "kernels": per}
+    hbm = {"achieved": d["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": d["hbm_frac"]}
+    v = d.get("valu")
+    valu = None if v is None else {"achieved": v["achieved_tops"], "peak": VALU_PEAK_TOPS, "unit": "TOP/s",
+                                   "frac": v["frac"], "measured_issue_peak": VALU_MEASURED_TOPS,
+                                   "frac_of_measured_issue_peak": v["frac_of_measured_issue_peak"]}
+    valu_binds = valu is not None and valu["frac_of_measured_issue_peak"] > hbm["frac"]
+    head = valu if valu_binds else hbm
+    out = {"bound": "valu" if valu_binds else "hbm", "kernel": dom, "achieved": head["achieved"], "peak": head["peak"],
+           "unit": head["unit"], "frac": head["frac"], "traffic": d["traffic"],
+           "traffic_unit": "bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE, profiles/)",
+           "launch_ms": d["isolated_launch_ms"], "launch_ms_source": d["isolated_source"],
+           "launch_ms_live_isolated": d["isolated_live_ms"], "live_over_file": d["live_over_file"],
+           "frames_per_launch": Bs, "hbm": hbm, "valu": valu,
+           "bound_rule": "valu when the kernel's issued lane-ops / isolated duration, as a fraction of the measured "
+                         "41.7 T integer issue rate, exceed its algorithmic bytes / isolated duration as a fraction of "
+                         "8 TB/s; headline achieved/peak/frac are the binding one's (VALU peak: the nominal 78.6 T)",
+           "algorithmic_bytes_per_launch": d["algorithmic_bytes_per_launch"],
+           "bytes_model": "SURVEY 8d per kernel: k_pyramid P0 + sum_{l>=1} P_l; k_fast_cell sum_l P_l + 4 N_pre; "
+                          "k_octree 4 (N_pre + N); k_orient_desc N (43^2 + 60)",
+           "kernels": per}
+    if ms_per_step:
+        tot = sum(k["isolated_launch_ms"] for k in per.values()) * launches_per_step
+        out["isolated_check"] = {"dominant_ms_x_launches_per_step": round(d["isolated_launch_ms"] * launches_per_step, 4),
+                                 "four_kernels_ms_x_launches_per_step": round(tot, 4), "ms_per_step": ms_per_step,
+                                 "launches_per_step": launches_per_step}
+    return out
 
 
 def progress(rank, msg):
@@ -1724,6 +1785,21 @@ def main():
             calls += nc.value
         return tot, calls
     stage_ms, nstage = stage_times() if not args.no_profile else (np.zeros(6), 0)
+    iso_ms = None
+    if not args.no_profile:
+        # the isolated pass: sequence 0's step (one 128-frame extraction launch + its matching) alone
+        # on its stream, kernels serialised, HIP events at the extraction kernels' boundaries — the
+        # live counterpart of the committed rocprofv3 summary ISOLATED_STATS
+        p0, n_iso = pipes[0], 10
+        lib.orb_extractor_profile(p0.ex._h, 3)
+        torch.cuda.synchronize(dev)
+        for s in range(n_iso):
+            p0.step(args.warmup + args.steps + s)
+        torch.cuda.synchronize(dev)
+        sm, nc = np.zeros(6), C.c_int(0)
+        lib.orb_extractor_stage_times(p0.ex._h, _abi.ptr(sm), 6, C.byref(nc))
+        lib.orb_extractor_profile(p0.ex._h, 0)
+        iso_ms = sm / max(nc.value, 1)
     frames_total = B * args.steps * world
     value = frames_total / dt
     cnt = torch.cat([p.counts[p.last][1:] for p in pipes]).cpu().numpy()
@@ -1765,15 +1841,21 @@ def main():
     copy_peak = measure_copy_peak(dev)
     if nstage > 0:
         result["roofline"] = extraction_roofline(stage_ms, nstage, lw, lh, n_pre_frame, float(np.mean(cnt)), W, H, NF,
-                                                 Bs)
+                                                 Bs, iso_ms=iso_ms, launches_per_step=S,
+                                                 ms_per_step=result["ms_per_step"])
         if result["roofline"]:
-            result["roofline"]["measured_copy_peak_gbs"] = copy_peak
-            result["roofline"]["frac_of_measured_copy_peak"] = round(result["roofline"]["achieved"] / copy_peak, 5)
+            result["roofline"]["hbm"]["measured_copy_peak_gbs"] = copy_peak
+            result["roofline"]["hbm"]["frac_of_measured_copy_peak"] = round(
+                result["roofline"]["hbm"]["achieved"] / copy_peak, 5)
     if nstage > 0:
         result["stage_ms_per_batch"] = {k: round(float(v) / nstage, 4) for k, v in zip(STAGES, stage_ms)
                                         if not k.startswith("reserved")}
         result["stage_ms_source"] = ("timed region: HIP events at the kernel boundaries on each stream, average "
-                                     "launch time under the streams' sharing")
+                                     "launch span while the other streams' kernels share the chip (not a kernel's own "
+                                     "duration; the isolated durations are roofline.kernels[*].isolated_launch_ms)")
+    if iso_ms is not None:
+        result["stage_ms_isolated_live"] = {k: round(float(v), 4) for k, v in zip(STAGES, iso_ms)
+                                            if not k.startswith("reserved")}
     # whole-pipeline roofline of SURVEY §8d: B_ext = P0 + 2 sum_{l>=1} P_l + N_kp (28 + 32) per frame
     P = (lw.astype(np.int64) * lh)
     b_ext = float(P[0] + 2 * P[1:].sum()) + float(np.mean(cnt)) * 60.0

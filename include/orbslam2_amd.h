@@ -410,7 +410,13 @@ int orb_search_by_projection_sim3(orb_matcher* m, const orb_frame_view* kf, cons
  *   mnScaleLevels, mvScaleFactors.
  * cur_mp (in/out, cur->n ints): -1 = mvpMapPoints[i2] empty, any other negative value = set
  * before the call, >= 0 on return = the keyframe map point index this call assigned.
- * Returns nmatches (after the rotation filter when the matcher checks orientation). */
+ * Returns nmatches (after the rotation filter when the matcher checks orientation).
+ * Deviation: with orb_dist >= 256 a map point whose window candidates are all occupied passes
+ * the reference's `bestDist <= ORBdist` with bestIdx2 = -1 and the reference then writes
+ * CurrentFrame.mvpMapPoints[-1] and counts a match (R/src/ORBmatcher.cpp:1806-1808, out of
+ * bounds).  Here such a point is skipped: nothing is written and it is not counted.  The
+ * reference's call sites pass 100 and 64 (R/src/Tracking.cpp:1921, 1936), where this cannot
+ * happen. */
 int orb_search_by_projection_kf(orb_matcher* m, const orb_frame_view* cur, const float* Tcw_cur, const float Ow[3],
                                 const orb_frame_view* kf, const uint8_t* mp_valid, const float* mp_xyz,
                                 const float* mp_min_dist, const float* mp_max_dist, const uint8_t* mp_desc,

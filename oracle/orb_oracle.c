@@ -1816,7 +1816,11 @@ int oracle_search_by_projection_kf(const oracle_frame* cur, const float* Tcw, co
             const int dist = oracle_descriptor_distance(dMP, cur->desc + (size_t)i2 * 32);
             if (dist < bestDist) { bestDist = dist; bestIdx2 = i2; }
         }
-        if (bestDist <= orb_dist) {
+        /* Deviation (documented in include/orbslam2_amd.h): with ORBdist >= 256 and every
+         * candidate already matched, bestIdx2 stays -1 and the reference writes
+         * CurrentFrame.mvpMapPoints[-1] (R/src/ORBmatcher.cpp:1806-1808), out of bounds; the
+         * point is skipped here (no match, not counted), as the GPU path does. */
+        if (bestDist <= orb_dist && bestIdx2 >= 0) {
             cur_mp[bestIdx2] = i;
             nmatches++;
             if (check_ori) {

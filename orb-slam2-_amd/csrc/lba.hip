@@ -1868,7 +1868,7 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_solve(const double* __restrict__
 #pragma unroll
         for (int s = 0; s < kNB / 4; s++) {
             const int p = jb + 4 * s + lk;
-            a[s] = A[(size_t)p * ld + I0 + li];   // -W        // -W(I0 + li, p)
+            a[s] = -A[(size_t)p * ld + I0 + li];   // -W(I0 + li, p): this kernel's panels store +W
             bb[s] = A[(size_t)(K0 + li) * ld + p];      //  L(K0 + li, p)
         }
 #pragma unroll
@@ -2728,7 +2728,8 @@ __global__ __launch_bounds__(kLdlT) void k_ldlt_df(const double* __restrict__ Sg
 // the dataflow solve applies to even orders that fit the LDS image (every local-BA system: n = 6P);
 // ORB_LBA_LDLT_OLD=1 keeps k_ldlt_solve<true> (A/B runs)
 static bool use_ldlt_df(int n) {
-    static const bool old = [] { const char* e = std::getenv("ORB_LBA_LDLT_OLD"); return e && e[0] == '1'; }();
+    const char* e = std::getenv("ORB_LBA_LDLT_OLD");   // read per solve, so a test can switch it
+    const bool old = e && e[0] == '1';
     const int np = (n + kNB - 1) & ~(kNB - 1);
     return !old && (n & 1) == 0 && np <= kLdlLdsMaxN;
 }

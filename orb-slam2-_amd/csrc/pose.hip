@@ -278,11 +278,21 @@ struct PoEdgesReg {
     __device__ void load(const PoseDev& d, int e0_, int e1) {
         e0 = e0_;
         outlier = d.outlier;
+        if (e1 <= e0) {   // a frame without edges touches no memory (e0 may be one past the arrays)
+#pragma unroll
+            for (int s = 0; s < EPT; s++) {
+                valid[s] = st[s] = false;
+                info[s] = 0.0;
+#pragma unroll
+                for (int c = 0; c < 3; c++) obs[s][c] = xw[s][c] = er[s][c] = 0.0;
+            }
+            return;
+        }
 #pragma unroll
         for (int s = 0; s < EPT; s++) {
             const int e = e0 + (int)threadIdx.x + kPoT * s;
             valid[s] = e < e1;
-            const int ec = valid[s] ? e : e0;
+            const int ec = valid[s] ? e : e1 - 1;   // clamped to the frame's last edge
 #pragma unroll
             for (int c = 0; c < 3; c++) {
                 obs[s][c] = d.obs[3 * (size_t)ec + c];

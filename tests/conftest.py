@@ -19,4 +19,9 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def amd():
+    # torch's HIP runtime must initialise before the library's first HIP call in this process (after
+    # it, torch reports "No HIP GPUs are available"); device_count() does not initialise the GPU
+    import torch
+    if torch.cuda.device_count() > 0:
+        torch.cuda.init()
     return sys.modules["orb_slam2_amd"]

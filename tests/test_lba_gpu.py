@@ -88,6 +88,39 @@ def test_dense_solve_vs_numpy(amd, n, seed):
     assert np.abs(S @ x - b).max() <= 1e-11 * np.abs(b).max() * n
 
 
+@pytest.mark.parametrize("n,seed,env", [
+    (7, 30, None), (125, 31, None),                          # odd n: k_ldlt_solve<true> (S in LDS)
+    (114, 32, "ORB_LBA_LDLT_OLD"), (64, 33, "ORB_LBA_LDLT_OLD"),
+    (130, 34, "ORB_LBA_LDLT_SINGLE"), (181, 35, "ORB_LBA_LDLT_SINGLE"),   # k_ldlt_solve<false>
+])
+def test_dense_solve_alt_kernels_vs_numpy(amd, monkeypatch, n, seed, env):
+    """The A/B forms of the reduced solve (k_ldlt_solve<true> for odd n or ORB_LBA_LDLT_OLD=1,
+    k_ldlt_solve<false> under ORB_LBA_LDLT_SINGLE=1): these panels store +W, so their MFMA
+    trailing tiles negate it on load (a sign slip there once went untested)."""
+    if env:
+        monkeypatch.setenv(env, "1")
+    rng = np.random.default_rng(seed)
+    G = rng.standard_normal((n, n + 8))
+    S = G @ G.T + n * np.eye(n)
+    b = rng.standard_normal(n)
+    x = amd.LocalBA().dense_solve(S, b)
+    ref = np.linalg.solve(S, b)
+    assert np.abs(x - ref).max() <= 1e-10 * np.abs(ref).max()
+    assert np.abs(S @ x - b).max() <= 1e-11 * np.abs(b).max() * n
+
+
+@pytest.mark.parametrize("env", ["ORB_LBA_LDLT_OLD", "ORB_LBA_LDLT_SINGLE"])
+def test_local_ba_alt_ldlt_matches_oracle(amd, monkeypatch, env):
+    """Local BA through the A/B reduced-solve kernels: the same LM decisions as the oracle
+    (config 4 under ORB_LBA_LDLT_OLD; 30 free poses, n = 180, under ORB_LBA_LDLT_SINGLE)."""
+    monkeypatch.setenv(env, "1")
+    kw = dict() if env == "ORB_LBA_LDLT_OLD" else dict(n_local=30, n_fixed=2, n_points=3000, seed=36)
+    pb = _problem(amd, **kw)
+    ref = O.lba_solve(pb)
+    got = amd.LocalBA().solve(pb)
+    _compare(ref, got)
+
+
 def test_dense_solve_zero_pivot_fails(amd):
     S = np.eye(20)
     S[7, 7] = 0.0

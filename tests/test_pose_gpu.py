@@ -76,3 +76,57 @@ def test_pose_optimization_vs_g2o_summation_order(amd):
         assert np.abs(g["pose_t"] - ref["pose_t"]).max() < 1e-5
         same += g["trials"] == ref["trials"] and g["iterations"] == ref["iterations"]
     print(f"GPU vs g2o-order oracle: identical LM iterations and trials on {same}/{len(frames)} frames")
+
+
+def _device_form(frames):
+    """pose_optimize_batch_device on exact-size torch tensors (edge arrays null when the batch
+    has no edges at all): the results as PoseOptimization's dicts."""
+    import ctypes as C
+    import torch
+    from orb_slam2_amd import _abi, optimizer as opt
+    dev = torch.device("cuda:0")
+    a = opt.pack_pose_frames(frames)
+    B, E = len(frames), int(a["edge_start"][-1])
+    T = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in a.items()}
+    dp = lambda x: C.c_void_p(x.data_ptr() if x.numel() else None)   # noqa: E731
+    pq = torch.zeros((B, 4), dtype=torch.float64, device=dev)
+    pt = torch.zeros((B, 3), dtype=torch.float64, device=dev)
+    outl = torch.zeros(E, dtype=torch.uint8, device=dev)
+    ninl = torch.full((B,), -1, dtype=torch.int32, device=dev)
+    work = torch.zeros(3 * E, dtype=torch.float64, device=dev)
+    flags = torch.zeros(2 * E, dtype=torch.uint8, device=dev)
+    iters = torch.zeros((B, 5), dtype=torch.int32, device=dev)
+    pb = opt.PoseBatch(B, E, dp(T["pose_q"]), dp(T["pose_t"]), dp(T["cam"]), dp(T["edge_start"]), dp(T["edge_obs"]),
+                       dp(T["edge_xw"]), dp(T["edge_info"]))
+    pr = opt.PoseBatchResult(dp(pq), dp(pt), dp(outl), dp(ninl))
+    lib = opt._pose_sig()
+    _abi.check("pose", lib.pose_optimize_batch_device(C.byref(pb), C.byref(pr), C.c_void_p(work.data_ptr() or 1),
+                                                      C.c_void_p(flags.data_ptr() or 1), dp(iters),
+                                                      C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+    torch.cuda.synchronize(dev)
+    s = a["edge_start"]
+    q, t, o, n, it = pq.cpu().numpy(), pt.cpu().numpy(), outl.cpu().numpy(), ninl.cpu().numpy(), iters.cpu().numpy()
+    return [dict(pose_q=q[b], pose_t=t[b], outlier=o[s[b]:s[b + 1]], n_inliers=int(n[b]),
+                 iterations=tuple(int(x) for x in it[b, :4]), trials=int(it[b, 4])) for b in range(B)]
+
+
+def test_pose_device_form_empty_frames(amd):
+    """The device entry point with a trailing frame that has no edges (its edge range starts one
+    past the arrays) and with a batch whose frames have no edges at all (null edge pointers):
+    empty frames return 0 with the pose untouched and read no edge memory; the others match the
+    oracle."""
+    from orb_slam2_amd import synth
+    frames = synth.pose_problems(n_frames=3, n_points=200, seed=31)
+    frames[2] = {k: (v[:0] if k in ("obs", "xw", "info") else v) for k, v in frames[2].items()}
+    got = _device_form(frames)
+    for f, g in zip(frames[:2], got[:2]):
+        ref = O.pose_optimization(f)
+        assert g["n_inliers"] == ref["n_inliers"] and np.array_equal(g["outlier"], ref["outlier"])
+        assert np.abs(g["pose_q"] - ref["pose_q"]).max() < 1e-5
+    q0, t0 = O.quat_from_Tcw(frames[2]["Tcw"])
+    assert got[2]["n_inliers"] == 0 and np.array_equal(got[2]["pose_q"], q0) and np.array_equal(got[2]["pose_t"], t0)
+    empty = [{k: (v[:0] if k in ("obs", "xw", "info") else v) for k, v in f.items()} for f in frames]
+    got = _device_form(empty)
+    for f, g in zip(empty, got):
+        q0, t0 = O.quat_from_Tcw(f["Tcw"])
+        assert g["n_inliers"] == 0 and np.array_equal(g["pose_q"], q0) and np.array_equal(g["pose_t"], t0)

@@ -42,6 +42,21 @@ def test_oracle_finds_planted_points():
     assert len(set(m[m >= 0].tolist())) == n                  # one frame slot per map point
 
 
+def test_oracle_orbdist_256_all_occupied_skips():
+    """ORBdist 256 with every frame slot occupied: every projected point has candidates, none
+    free, so bestIdx2 stays -1 with bestDist = 256 <= ORBdist.  The reference writes
+    mvpMapPoints[-1] there; the oracle skips the point (no write, not counted) and leaves the
+    slots as they were."""
+    p, kf, kfs, occ = _problem(7)
+    occ[:] = -2
+    n, m = _oracle(p, kf, kfs, occ, 40.0, 256, True)
+    assert n == 0 and np.array_equal(m, occ)
+    occ2 = occ.copy()
+    occ2[::2] = -1               # half free: the free half still matches, nothing else is touched
+    n2, m2 = _oracle(p, kf, kfs, occ2, 40.0, 256, False)
+    assert n2 > 0 and np.all(m2[1::2] == -2)
+
+
 def _frame(k, kp):
     from orb_slam2_amd import Frame
     a = np.zeros(len(k["x"]), dtype=[("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
@@ -56,11 +71,14 @@ def _frame(k, kp):
 
 @pytest.mark.gpu
 # (7 / 8: wide windows and a loose distance cut, so many map points share a best slot: the replay's
-# clean / dirty claimant split and its re-scans are exercised.  ORBdist stays below 256: at 256 a
-# point whose candidates are all occupied passes `bestDist <= ORBdist` with bestIdx2 = -1 and the
-# reference writes mvpMapPoints[-1] (R/src/ORBmatcher.cpp:1806-1808; R/src/Tracking.cpp:1921, 1936 call it with 100 and 64))
+# clean / dirty claimant split and its re-scans are exercised.  9 / 10: ORBdist 256 with wide
+# windows, where a point whose candidates are all occupied passes `bestDist <= ORBdist` with
+# bestIdx2 = -1 — the reference writes mvpMapPoints[-1] there (R/src/ORBmatcher.cpp:1806-1808);
+# both the oracle and the GPU skip such a point, the documented deviation
+# (include/orbslam2_amd.h).  R/src/Tracking.cpp:1921, 1936 call it with 100 and 64.)
 @pytest.mark.parametrize("seed,th,orb_dist,ori", [(3, 10.0, 100, True), (4, 10.0, 100, True), (5, 5.0, 64, False),
-                                                  (6, 3.0, 50, True), (7, 40.0, 200, True), (8, 80.0, 200, False)])
+                                                  (6, 3.0, 50, True), (7, 40.0, 200, True), (8, 80.0, 200, False),
+                                                  (7, 40.0, 256, True), (8, 80.0, 256, False)])
 def test_search_by_projection_kf_gpu(amd, seed, th, orb_dist, ori):
     p, kf, kfs, occ = _problem(seed)
     rn, rm = _oracle(p, kf, kfs, occ, th, orb_dist, ori)
