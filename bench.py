@@ -1505,7 +1505,152 @@ def batch_sweep(amd, dev, m):
     # PCIe-inclusive, B = 1 / 8 / 64: H2D of the frames, extraction + matching, D2H of the results
     for B in (1, 8, 64):
         res[f"B{B}_pcie_inclusive"] = _pcie_leg(amd, dev, m, cv, W, H, NF, B)
+    h2d, d2h = measure_pinned_copy(dev)
+    res["pinned_copy_gbs"] = {"h2d": h2d, "d2h": d2h, "source": "64 MiB pinned host <-> device copies x10 on one "
+                                                                "stream, HIP events, in this run"}
+    for B in (8, 64):
+        r = _pcie_pipelined_leg(amd, dev, cv, W, H, NF, B)
+        r["h2d_bound_frames_per_s"] = round(h2d * 1e9 / r["h2d_bytes_per_step"] * B, 1)
+        r["frac_of_h2d_bound"] = round(r["frames_per_s"] / r["h2d_bound_frames_per_s"], 3)
+        res[f"B{B}_pcie_pipelined"] = r
     return res
+
+
+def measure_pinned_copy(dev, mib=64, reps=10):
+    """Pinned host <-> device copy rates on one stream (HIP events around `reps` copies of `mib`
+    MiB each way): the PCIe ceiling the PCIe-inclusive legs are read against."""
+    n = mib << 20
+    h = torch.empty(n, dtype=torch.uint8).pin_memory()
+    d = torch.empty(n, dtype=torch.uint8, device=dev)
+    d.copy_(h, non_blocking=True)
+    h.copy_(d, non_blocking=True)
+    torch.cuda.synchronize(dev)
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    e[0].record()
+    for _ in range(reps):
+        d.copy_(h, non_blocking=True)
+    e[1].record()
+    for _ in range(reps):
+        h.copy_(d, non_blocking=True)
+    e[2].record()
+    torch.cuda.synchronize(dev)
+    h2d = n * reps / (e[0].elapsed_time(e[1]) * 1e-3) / 1e9
+    d2h = n * reps / (e[1].elapsed_time(e[2]) * 1e-3) / 1e9
+    return round(h2d, 2), round(d2h, 2)
+
+
+def _pcie_pipelined_leg(amd, dev, cv, W, H, NF, B, steps=16, warmup=4):
+    """The PCIe-inclusive path as a streaming host would run it, on three HIP streams: the copy
+    stream uploads batch s+1's pinned frames (one H2D, into one of three device frame buffers)
+    while two compute streams, one per batch parity with its own extractor and matcher handles,
+    run batches s and s-1: extraction, SearchForInitialization over the B-1 in-batch pairs, and
+    the compaction of keypoints / descriptors / matches12 (orb_pack_rows_device), which stores
+    exactly the counted rows straight into host-mapped pinned memory (no D2H copy command, no
+    host wait for the counts).  Events order the hand-offs: a frame buffer is refilled only after
+    the extraction that reads it in place (level 0, LEVEL-0 LIFETIME) has finished.  The host
+    outputs rotate over three sets: before enqueueing batch s the host waits for batch s-3's
+    outputs (a consumer reading them), so the GPU always holds the next batches' work."""
+    from orb_slam2_amd import synth, _abi
+    lib = _abi.lib()
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipHostMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t, C.c_uint]
+    hip.hipHostFree.argtypes = [C.c_void_p]
+    hip.hipHostGetDevicePointer.argtypes = [C.POINTER(C.c_void_p), C.c_void_p, C.c_uint]
+    nb = 4   # distinct pinned host batches (inputs)
+    host_in = [torch.from_numpy(np.stack([synth.frame(cv, W, H, t + k * B) for t in range(B)])).pin_memory()
+               for k in range(nb)]
+    exs = [amd.ORBextractor(NF, 1.2, 8, 20, 7, device=dev.index or 0, max_w=W, max_h=H, max_batch=B) for _ in range(2)]
+    ms = [amd.ORBmatcher(0.9, True, device=dev.index or 0) for _ in range(2)]
+    cap = C.c_int()
+    _abi.check("geom", lib.orb_extractor_geometry(exs[0]._h, W, H, None, None, None, C.byref(cap)))
+    cap = cap.value
+    P = max(B - 1, 1)
+    s_copy, s_comps = torch.cuda.Stream(dev), [torch.cuda.Stream(dev) for _ in range(2)]
+    NF_BUF = 3   # device frame buffers: the upload of batch s+1 never waits for batch s's extraction
+    imgs = [torch.empty((B, H, W), dtype=torch.uint8, device=dev) for _ in range(NF_BUF)]
+    ev_in = [torch.cuda.Event() for _ in range(NF_BUF)]     # frames of buffer f uploaded
+    ev_ext = [torch.cuda.Event() for _ in range(NF_BUF)]    # extraction done reading buffer f
+    kps = [torch.zeros((B, cap, 7), dtype=torch.int32, device=dev) for _ in range(2)]
+    desc = [torch.zeros((B, cap, 32), dtype=torch.uint8, device=dev) for _ in range(2)]
+    cnt = [torch.zeros(B, dtype=torch.int32, device=dev) for _ in range(2)]
+    m12 = [torch.zeros((P, cap), dtype=torch.int32, device=dev) for _ in range(2)]
+    nm = [torch.zeros(P, dtype=torch.int32, device=dev) for _ in range(2)]
+    sizes = {"pk": B * cap * 28, "pd": B * cap * 32, "pm": P * cap * 4, "off": 3 * (B + 1) * 4}
+    NO = 3   # host output sets
+    hostbufs, outs = [], []
+    for _ in range(NO):   # host-mapped, coherent: the pack kernel's stores land in host memory
+        o = {}
+        for k, n in sizes.items():
+            h, dptr = C.c_void_p(), C.c_void_p()
+            if hip.hipHostMalloc(C.byref(h), n, 0x2 | 0x40000000) != 0 or \
+                    hip.hipHostGetDevicePointer(C.byref(dptr), h, 0) != 0:
+                raise SystemExit("pipelined PCIe leg: hipHostMalloc (mapped) failed")
+            hostbufs.append(h)
+            o[k] = (h, dptr)
+        outs.append(o)
+    dp = lambda x: C.c_void_p(x.data_ptr())   # noqa: E731
+    moved = {"d2h": 0}
+    ev_done = [torch.cuda.Event() for _ in range(NO)]   # host output set j written
+
+    def enqueue(s):
+        i, f = s % 2, s % NF_BUF
+        o = outs[s % NO]
+        if s >= NF_BUF:   # buffer f's previous extraction (batch s-3) must be done reading level 0
+            s_copy.wait_event(ev_ext[f])
+        with torch.cuda.stream(s_copy):
+            imgs[f].copy_(host_in[s % nb], non_blocking=True)
+        ev_in[f].record(s_copy)
+        s_comp = s_comps[i]   # batch s-2 ran on this stream before: set i is free in stream order
+        s_comp.wait_event(ev_in[f])
+        sp = C.c_void_p(s_comp.cuda_stream)
+        k, d, c, mm = kps[i], desc[i], cnt[i], m12[i]
+        _abi.check("x", lib.orb_extract_batch_device(exs[i]._h, dp(imgs[f]), H * W, B, W, H, dp(k), dp(d), cap, dp(c),
+                                                      sp))
+        ev_ext[f].record(s_comp)
+        if B > 1:
+            _abi.check("sfi", lib.orb_search_for_initialization_batch_device(
+                ms[i]._h, dp(k), dp(d), dp(c), C.c_void_p(k.data_ptr() + cap * 28), C.c_void_p(d.data_ptr() + cap * 32),
+                C.c_void_p(c.data_ptr() + 4), B - 1, cap, W, H, 100, dp(mm), dp(nm[i]), sp))
+        off = o["off"][1].value
+        _abi.check("pack", lib.orb_pack_rows_device(dp(k), 28, cap, dp(c), B, o["pk"][1], C.c_void_p(off), sp))
+        _abi.check("pack", lib.orb_pack_rows_device(dp(d), 32, cap, dp(c), B, o["pd"][1], C.c_void_p(off + 4 * (B + 1)),
+                                                    sp))
+        if B > 1:   # vnMatches12 of pair (t-1, t) has frame t-1's N rows
+            _abi.check("pack", lib.orb_pack_rows_device(dp(mm), 4, cap, dp(c), B - 1, o["pm"][1],
+                                                        C.c_void_p(off + 8 * (B + 1)), sp))
+        ev_done[s % NO].record(s_comp)
+
+    def consume(s):   # the host reads batch s's outputs: totals from the mapped offsets
+        ev_done[s % NO].synchronize()
+        offs = np.ctypeslib.as_array(C.cast(outs[s % NO]["off"][0], C.POINTER(C.c_int32)), shape=(3, B + 1))
+        n_kp, n_m = int(offs[0, B]), int(offs[2, B - 1]) if B > 1 else 0
+        moved["d2h"] += n_kp * 60 + n_m * 4 + sizes["off"]
+
+    def run(s0, n):
+        for s in range(s0, s0 + n):
+            if s - s0 >= NO:
+                consume(s - NO)
+            enqueue(s)
+        for s in range(max(s0, s0 + n - NO), s0 + n):
+            consume(s)
+        torch.cuda.synchronize(dev)
+
+    try:
+        run(0, warmup)
+        moved["d2h"] = 0
+        t0 = time.perf_counter()
+        run(warmup, steps)
+        dt = (time.perf_counter() - t0) / steps
+        st = [batch_status(e, mt, f"pipelined PCIe leg B={B}") for e, mt in zip(exs, ms)][0]
+    finally:
+        torch.cuda.synchronize(dev)
+        for h in hostbufs:
+            hip.hipHostFree(h)
+    return {"frames_per_s": round(B / dt, 1), "ms_per_step": round(dt * 1e3, 4), "streams": 3, "status": st,
+            "h2d_bytes_per_step": int(B * H * W), "d2h_bytes_per_step": int(moved["d2h"] / steps),
+            "note": "copy stream: H2D of batch s+1 beside two compute streams (batches s, s-1); each batch's "
+                    "compaction stores exactly the counted keypoint / descriptor / matches12 rows into host-mapped "
+                    "pinned memory (orb_pack_rows_device): no D2H copy command, no host wait for counts"}
 
 
 def _pcie_leg(amd, dev, m, cv, W, H, NF, B):

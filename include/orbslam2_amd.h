@@ -102,6 +102,16 @@ int orb_extract_batch_device(orb_extractor* ex, const uint8_t* d_imgs, size_t im
                              int B, int w, int h, orb_keypoint* d_kps, uint8_t* d_desc, int cap,
                              int32_t* d_counts, void* stream);
 
+/* Compacts per-frame device rows stored at a capacity stride into one contiguous run, so a
+ * host consumer downloads exactly the rows the batch produced (Tracking builds each Frame's
+ * mvKeys / mDescriptors / the initializer's vnMatches12 from them, R/src/Frame.cpp:262-268,
+ * R/src/Tracking.cpp:780): frame b's min(d_counts[b], cap) rows of row_bytes (a multiple of 4)
+ * at d_src + b*cap*row_bytes go to d_dst + d_offsets[b]*row_bytes; d_offsets[0..B] receives the
+ * exclusive prefix and the total.  Keypoints (28 B), descriptors (32 B) and matches12 (4 B rows,
+ * d_counts = the first frames' counts) alike.  Asynchronous on `stream`. */
+int orb_pack_rows_device(const void* d_src, int row_bytes, int cap, const int32_t* d_counts, int B, void* d_dst,
+                         int32_t* d_offsets, void* stream);
+
 /* copy = 1: every later extraction of `ex` copies level 0 into the handle's pyramid slab, so
  * no later call reads the caller's frames (see LEVEL-0 LIFETIME above; one extra read + write
  * of the frame per extraction).  copy = 0 (default): level 0 is read in place when aligned. */

@@ -27,10 +27,11 @@
 // throw).
 #pragma once
 
+#include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
-#include <list>
 #include <map>
 #include <mutex>
 #include <set>
@@ -780,15 +781,72 @@ struct LbaDump {
     std::vector<int32_t> edge_point, edge_pose;
     std::vector<double> out_q, out_t, out_xyz;
     int iterations[2] = {0, 0}, trials = 0, aborted = 0;
+    // host wall time of the call's phases (steady_clock): 0 gather of the window (R :567-625),
+    // 1 the problem arrays (R :636-782), 2 lba_solve, 3 vToErase + write-back (R :850-917)
+    double phase_us[4] = {0.0, 0.0, 0.0, 0.0};
+    void clear() {   // keeps the capacity: a reused dump neither allocates nor faults pages in
+        for (auto* v : {&pose_q, &pose_t, &point_xyz, &edge_obs, &edge_info, &edge_cam, &out_q, &out_t, &out_xyz})
+            v->clear();
+        for (auto* v : {&pose_fixed, &point_bad, &edge_stereo, &edge_erase}) v->clear();
+        pose_id.clear(); point_id.clear(); edge_point.clear(); edge_pose.clear();
+        iterations[0] = iterations[1] = trials = aborted = 0;
+    }
 };
 
+// The phases (LbaDump::phase_us) of this thread's last LocalBundleAdjustment call.
+inline double* lba_last_phases() {
+    thread_local double ph[4] = {0.0, 0.0, 0.0, 0.0};
+    return ph;
+}
+
 namespace detail {
+// Per-thread working set of local_ba, reused from call to call (LocalMapping calls it once per
+// keyframe): the window lists, the problem / result arrays and the edge bookkeeping keep their
+// capacity, so a steady-state call allocates only what the reference API returns by value.
+template <class KeyFrameT, class MapPointT, class ObsT>
+struct LbaScratch {
+    LbaDump D;
+    std::vector<KeyFrameT*> localKFs, fixedKFs, edgeKF;
+    std::vector<MapPointT*> localMPs;
+    std::vector<ObsT> obs;
+    std::vector<std::pair<const KeyFrameT*, int>> poseIndex;
+    std::vector<std::pair<KeyFrameT*, MapPointT*>> toErase;
+    void clear() {
+        D.clear();
+        localKFs.clear(); fixedKFs.clear(); edgeKF.clear(); localMPs.clear(); obs.clear(); poseIndex.clear();
+        toErase.clear();
+    }
+};
+
 template <class KeyFrameT, class MapT, class Solve>
 void local_ba(KeyFrameT* pKF, bool* pbStopFlag, MapT* pMap, LbaDump* dump, Solve&& solve) {
     using MapPointT = typename std::remove_pointer<typename decltype(pKF->GetMapPointMatches())::value_type>::type;
     using MatT = typename std::decay<decltype(pKF->GetPose())>::type;
-    // ---- local keyframes, local map points, fixed cameras (R :567-625)
-    std::list<KeyFrameT*> lLocalKeyFrames;
+    using ObsT = typename std::decay<decltype(std::declval<MapPointT*>()->GetObservations())>::type;
+    using Clock = std::chrono::steady_clock;
+    auto tPhase = Clock::now();
+    double* ph = lba_last_phases();
+    auto lap = [&tPhase](double& acc) {
+        const auto now = Clock::now();
+        acc = std::chrono::duration<double, std::micro>(now - tPhase).count();
+        tPhase = now;
+    };
+    ph[0] = ph[1] = ph[2] = ph[3] = 0.0;
+    thread_local LbaScratch<KeyFrameT, MapPointT, ObsT> sc;
+    sc.clear();
+    struct Out {   // the caller's dump (tests) receives a copy of the arrays, whatever the exit
+        LbaScratch<KeyFrameT, MapPointT, ObsT>& sc;
+        LbaDump* dump;
+        double* ph;
+        ~Out() {
+            std::copy(ph, ph + 4, sc.D.phase_us);
+            if (dump) *dump = sc.D;
+        }
+    } out{sc, dump, ph};
+    LbaDump& D = sc.D;
+    // ---- local keyframes, local map points, fixed cameras (R :567-625; the reference's std::lists
+    //      as arrays, same order)
+    auto& lLocalKeyFrames = sc.localKFs;
     lLocalKeyFrames.push_back(pKF);
     pKF->mnBALocalForKF = pKF->mnId;
     const std::vector<KeyFrameT*> vNeighKFs = pKF->GetVectorCovisibleKeyFrames();
@@ -796,30 +854,42 @@ void local_ba(KeyFrameT* pKF, bool* pbStopFlag, MapT* pMap, LbaDump* dump, Solve
         pKFi->mnBALocalForKF = pKF->mnId;
         if (!pKFi->isBad()) lLocalKeyFrames.push_back(pKFi);
     }
-    std::list<MapPointT*> lLocalMapPoints;
+    auto& lLocalMapPoints = sc.localMPs;
     for (KeyFrameT* k : lLocalKeyFrames)
         for (MapPointT* pMP : k->GetMapPointMatches())
             if (pMP && !pMP->isBad() && pMP->mnBALocalForKF != pKF->mnId) {
                 lLocalMapPoints.push_back(pMP);
                 pMP->mnBALocalForKF = pKF->mnId;
             }
-    std::list<KeyFrameT*> lFixedCameras;
-    for (MapPointT* pMP : lLocalMapPoints)
-        for (const auto& ob : pMP->GetObservations()) {
+    // (each point's observations are read once here and reused for its edges below; the reference
+    // calls GetObservations() again at :740 — both are snapshots of a map other threads may grow)
+    auto& vObs = sc.obs;
+    size_t nObs = 0;
+    auto& lFixedCameras = sc.fixedKFs;
+    for (MapPointT* pMP : lLocalMapPoints) {
+        vObs.push_back(pMP->GetObservations());
+        nObs += vObs.back().size();
+        for (const auto& ob : vObs.back()) {
             KeyFrameT* pKFi = ob.first;
             if (pKFi->mnBALocalForKF != pKF->mnId && pKFi->mnBAFixedForKF != pKF->mnId) {
                 pKFi->mnBAFixedForKF = pKF->mnId;
                 if (!pKFi->isBad()) lFixedCameras.push_back(pKFi);
             }
         }
+    }
+    lap(ph[0]);
     // ---- the graph as arrays (vertices: local poses (fixed iff mnId == 0), fixed cameras, points
     //      with id mnId + maxKFid + 1; edges per point in observation order, R :636-782)
-    LbaDump own;
-    LbaDump& D = dump ? *dump : own;
-    std::map<const KeyFrameT*, int> poseIndex;
+    const size_t nPoses = lLocalKeyFrames.size() + lFixedCameras.size(), nPts = lLocalMapPoints.size();
+    D.pose_q.reserve(4 * nPoses); D.pose_t.reserve(3 * nPoses); D.pose_fixed.reserve(nPoses); D.pose_id.reserve(nPoses);
+    D.point_xyz.reserve(3 * nPts); D.point_id.reserve(nPts); D.point_bad.reserve(nPts);
+    D.edge_point.reserve(nObs); D.edge_pose.reserve(nObs); D.edge_stereo.reserve(nObs); D.edge_obs.reserve(3 * nObs);
+    D.edge_info.reserve(nObs); D.edge_cam.reserve(5 * nObs);
+    // keyframe -> vertex index: a sorted array (a window holds tens of keyframes)
+    auto& poseIndex = sc.poseIndex;
     unsigned long maxKFid = 0;
     auto addPose = [&](KeyFrameT* k, bool fixed) {
-        poseIndex[k] = (int)D.pose_fixed.size();
+        poseIndex.emplace_back(k, (int)D.pose_fixed.size());
         float T[16];
         detail::read_Tcw(k->GetPose(), T);
         double q[4], t[3];
@@ -832,22 +902,28 @@ void local_ba(KeyFrameT* pKF, bool* pbStopFlag, MapT* pMap, LbaDump* dump, Solve
     };
     for (KeyFrameT* k : lLocalKeyFrames) addPose(k, k->mnId == 0);
     for (KeyFrameT* k : lFixedCameras) addPose(k, true);
-    std::vector<MapPointT*> vpMP;
-    std::vector<KeyFrameT*> vpEdgeKF;
-    for (MapPointT* pMP : lLocalMapPoints) {
-        const int pi = (int)vpMP.size();
-        vpMP.push_back(pMP);
+    std::sort(poseIndex.begin(), poseIndex.end());
+    auto poseOf = [&poseIndex](const KeyFrameT* k) {
+        const auto it = std::lower_bound(poseIndex.begin(), poseIndex.end(), std::make_pair(k, -1));
+        if (it == poseIndex.end() || it->first != k) throw std::out_of_range("LocalBundleAdjustment: observer not in the window");
+        return it->second;
+    };
+    auto& vpMP = lLocalMapPoints;   // vertex order = the local map points' order
+    auto& vpEdgeKF = sc.edgeKF;
+    vpEdgeKF.reserve(nObs);
+    for (size_t pi = 0; pi < vpMP.size(); pi++) {
+        MapPointT* pMP = vpMP[pi];
         const MatT X = pMP->GetWorldPos();
         for (int i = 0; i < 3; i++) D.point_xyz.push_back((double)X.template at<float>(i, 0));   // Converter::toVector3d
         D.point_id.push_back((int64_t)(pMP->mnId + maxKFid + 1));
         D.point_bad.push_back(pMP->isBad() ? 1 : 0);
-        for (const auto& ob : pMP->GetObservations()) {
+        for (const auto& ob : vObs[pi]) {
             KeyFrameT* pKFi = ob.first;
             if (pKFi->isBad()) continue;
             const auto& kpUn = pKFi->mvKeysUn[ob.second];
             const float ur = pKFi->mvuRight[ob.second];
-            D.edge_point.push_back(pi);
-            D.edge_pose.push_back(poseIndex.at(pKFi));
+            D.edge_point.push_back((int32_t)pi);
+            D.edge_pose.push_back(poseOf(pKFi));
             D.edge_stereo.push_back(ur < 0 ? 0 : 1);
             D.edge_obs.push_back(kpUn.pt.x);
             D.edge_obs.push_back(kpUn.pt.y);
@@ -873,7 +949,9 @@ void local_ba(KeyFrameT* pKF, bool* pbStopFlag, MapT* pMap, LbaDump* dump, Solve
     lba_result r{D.out_q.data(), D.out_t.data(), D.out_xyz.data(), D.edge_erase.data(), nullptr, {0, 0}, 0,
                  nullptr, 0, 0};
     static_assert(sizeof(bool) == 1, "mbAbortBA is read as one byte");
+    lap(ph[1]);
     check(solve(&p, &o, reinterpret_cast<const volatile uint8_t*>(pbStopFlag), &r), "lba_solve");
+    lap(ph[2]);
     D.iterations[0] = r.iterations[0];
     D.iterations[1] = r.iterations[1];
     D.trials = r.trials;
@@ -882,7 +960,7 @@ void local_ba(KeyFrameT* pKF, bool* pbStopFlag, MapT* pMap, LbaDump* dump, Solve
     // ---- vToErase (R :850-880): the mono edges in insertion order, then the stereo edges, each
     //      skipping a point that became bad while the solve ran (isBad() read now, as R :855/:872
     //      do after optimize); the order matters to EraseObservation's choice of mpRefKF / SetBadFlag
-    std::vector<std::pair<KeyFrameT*, MapPointT*>> vToErase;
+    auto& vToErase = sc.toErase;
     for (int pass = 0; pass < 2; pass++)
         for (int e = 0; e < NE; e++) {
             if ((int)D.edge_stereo[(size_t)e] != pass || !D.edge_erase[(size_t)e]) continue;
@@ -909,6 +987,7 @@ void local_ba(KeyFrameT* pKF, bool* pbStopFlag, MapT* pMap, LbaDump* dump, Solve
         vpMP[(size_t)m]->SetWorldPos(detail::make_mat<MatT>(3, 1, X));
         vpMP[(size_t)m]->UpdateNormalAndDepth();
     }
+    lap(ph[3]);
 }
 }  // namespace detail
 

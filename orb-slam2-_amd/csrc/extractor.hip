@@ -1870,6 +1870,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     }
 }
 
+// Compaction of per-frame rows stored at a capacity stride (keypoints 28 B, descriptors 32 B,
+// matches12 4 B) into one contiguous run: workgroup b copies min(counts[b], cap) rows of frame b
+// to the exclusive prefix of the clamped counts of frames < b (every workgroup sums them itself:
+// no second launch, no inter-workgroup order).  Rows are whole dwords.
+__global__ __launch_bounds__(256) void k_pack_rows(const uint32_t* __restrict__ src, int rowWords, int cap,
+                                                   const int32_t* __restrict__ counts, int B, uint32_t* __restrict__ dst,
+                                                   int32_t* __restrict__ offsets) {
+    __shared__ int sOff;
+    const int b = blockIdx.x;
+    if (threadIdx.x == 0) sOff = 0;
+    __syncthreads();
+    int part = 0;
+    for (int i = threadIdx.x; i < b; i += 256) part += min(max(counts[i], 0), cap);
+    part = wave_sum_dpp(part);
+    if ((threadIdx.x & 63) == 0 && part) atomicAdd(&sOff, part);
+    __syncthreads();
+    const int off = sOff, n = min(max(counts[b], 0), cap);
+    if (threadIdx.x == 0) {
+        offsets[b] = off;
+        if (b == B - 1) offsets[B] = off + n;
+    }
+    const uint32_t* s = src + (size_t)b * cap * rowWords;
+    uint32_t* d = dst + (size_t)off * rowWords;
+    for (int t = threadIdx.x; t < n * rowWords; t += 256) d[t] = s[t];
+}
+
 // Copies B packed w x h frames into the pitched level-0 slots of the pyramid slab: 16 bytes
 // per thread when rows are 16-byte aligned (w % 16 == 0 and an aligned source), else bytes.
 __global__ __launch_bounds__(256) void k_load_frames(Geom g, const uint8_t* __restrict__ src, size_t frameStride,
@@ -2870,6 +2896,16 @@ int orb_compute_stereo_matches_batch_device(orb_extractor* ex, const orb_keypoin
                        d_desc + (size_t)cap * 32, d_counts + 1, 2 * cap, 2, cap, mbf, maxD, d_uright, d_depth, dsd, cap);
     hipLaunchKernelGGL(k_stereo_median, dim3(n_pairs), dim3(1024), 0, s, d_counts, 2, cap, d_uright, d_depth, dsd, cap,
                        d_nstereo, dkeys);
+    ORB_HIP_TRY(hipGetLastError());
+    return ORB_OK;
+} ORB_ABI_CATCH
+
+int orb_pack_rows_device(const void* d_src, int row_bytes, int cap, const int32_t* d_counts, int B, void* d_dst,
+                         int32_t* d_offsets, void* stream) try {
+    if (!d_src || !d_counts || !d_dst || !d_offsets || B <= 0 || cap < 0 || row_bytes <= 0 || (row_bytes & 3))
+        return ORB_EINVAL;
+    hipLaunchKernelGGL(k_pack_rows, dim3(B), dim3(256), 0, (hipStream_t)stream, (const uint32_t*)d_src, row_bytes / 4,
+                       cap, d_counts, B, (uint32_t*)d_dst, d_offsets);
     ORB_HIP_TRY(hipGetLastError());
     return ORB_OK;
 } ORB_ABI_CATCH

@@ -8,6 +8,8 @@
 //   shim_caller sbl IN OUT       ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th)
 //   shim_caller lba IN OUT       Optimizer::LocalBundleAdjustment on a mock keyframe / map-point graph
 //   shim_caller lbag IN OUT      the same through the device-list overload (lba_group, several GPUs)
+//   shim_caller lbacpu IN OUT    the same gather / write-back around the CPU oracle's solve
+//                                ($ORB_ORACLE_LIB; the routed row's like-for-like CPU column)
 //   shim_caller pose IN OUT      Optimizer::PoseOptimization on a mock Frame
 //   shim_caller stereo IN OUT    ORBextractor on a left / right image (two handles), then
 //                                Frame::ComputeStereoMatches on the mock Frame
@@ -34,6 +36,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <dlfcn.h>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -192,10 +195,10 @@ struct MapPoint {
     }
 };
 std::mutex MapPoint::mGlobalMutex;
-inline void KeyFrame::EraseMapPointMatch(MapPoint* p) {
+inline void KeyFrame::EraseMapPointMatch(MapPoint* p) {   // R/src/KeyFrame.cpp: by GetIndexInKeyFrame
     g_erase_log.emplace_back(mnId, p->mnId);
-    for (auto& m : matches)
-        if (m == p) m = nullptr;
+    const int idx = p->GetIndexInKeyFrame(this);
+    if (idx >= 0) matches[(size_t)idx] = nullptr;
 }
 inline std::set<MapPoint*> KeyFrame::GetMapPoints() {   // R/src/KeyFrame.cpp: set, not bad
     std::set<MapPoint*> s;
@@ -389,8 +392,29 @@ static void run_sbl(FILE* in, FILE* out) {
 }
 
 static double g_call_us = 0.0;   // wall time of the last timed shim call (timeit mode)
+static double g_phase_us[4] = {-1.0, 0.0, 0.0, 0.0};   // the last lba call's phases (LbaDump::phase_us)
+static bool g_timing = false;   // timeit: the lba modes call without a dump, as LocalMapping does
 
-static void run_lba(FILE* in, FILE* out, bool group) {
+// The CPU column of the routed LocalBundleAdjustment row: the same shim gather / write-back around
+// the oracle's single-threaded solve (oracle/lba_oracle.h, loaded from $ORB_ORACLE_LIB: the
+// reference's LocalMapping thread runs g2o without OpenMP), so GPU and CPU calls compare like for like.
+static int oracle_solve(const lba_problem* p, const lba_options* o, const volatile uint8_t* st, lba_result* r) {
+    using Fn = int (*)(const lba_problem*, const lba_options*, const volatile uint8_t*, lba_result*);
+    static Fn fn = [] {
+        const char* path = std::getenv("ORB_ORACLE_LIB");
+        void* h = path ? dlopen(path, RTLD_NOW | RTLD_LOCAL) : nullptr;
+        if (!h) throw std::runtime_error("lbacpu: set ORB_ORACLE_LIB to oracle/build/liborb_oracle.so");
+        Fn f = reinterpret_cast<Fn>(dlsym(h, "oracle_lba_solve"));
+        if (!f) throw std::runtime_error("lbacpu: oracle_lba_solve not found");
+        return f;
+    }();
+    // lba_result_t (oracle) is lba_result without the trailing `aborted`, which it signals by returning 1
+    const int rc = fn(p, o, st, r);
+    if (rc == 1) { r->aborted = 1; return 0; }
+    return rc;
+}
+
+static void run_lba(FILE* in, FILE* out, bool group, bool cpu = false) {
     mock::g_erase_log.clear();
     const auto Tcw = rd<float>(in);
     const auto fixedCam = rd<uint8_t>(in);
@@ -439,12 +463,17 @@ static void run_lba(FILE* in, FILE* out, bool group) {
     mock::Map map;
     bool stop = stopFlag[0] != 0;
     orbslam2_amd::LbaDump D;
+    orbslam2_amd::LbaDump* dp = g_timing ? nullptr : &D;
     const auto t0 = std::chrono::steady_clock::now();
     if (group)   // the multi-GPU overload: landmarks sharded over the listed devices
-        orbslam2_amd::LocalBundleAdjustment(pKF, &stop, &map, std::vector<int>(devices.begin(), devices.end()), &D);
+        orbslam2_amd::LocalBundleAdjustment(pKF, &stop, &map, std::vector<int>(devices.begin(), devices.end()), dp);
+    else if (cpu)
+        orbslam2_amd::detail::local_ba(pKF, &stop, &map, dp, oracle_solve);
     else
-        orbslam2_amd::LocalBundleAdjustment(pKF, &stop, &map, &D);
+        orbslam2_amd::LocalBundleAdjustment(pKF, &stop, &map, dp);
     g_call_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    const double* ph = orbslam2_amd::lba_last_phases();
+    std::copy(ph, ph + 4, g_phase_us);
     wr(out, D.pose_q); wr(out, D.pose_t); wr(out, D.pose_fixed); wr(out, D.pose_id);
     wr(out, D.point_xyz); wr(out, D.point_id); wr(out, D.point_bad);
     wr(out, D.edge_point); wr(out, D.edge_pose); wr(out, D.edge_stereo); wr(out, D.edge_obs); wr(out, D.edge_info);
@@ -883,6 +912,7 @@ static bool run_mode(const std::string& mode, FILE* in, FILE* out) {
     else if (mode == "sbl") run_sbl(in, out);
     else if (mode == "lba") run_lba(in, out, false);
     else if (mode == "lbag") run_lba(in, out, true);
+    else if (mode == "lbacpu") run_lba(in, out, false, true);
     else if (mode == "pose") run_pose(in, out);
     else if (mode == "stereo") run_stereo(in, out);
     else if (mode == "fuse") run_fuse(in, out);
@@ -972,7 +1002,8 @@ static int run_timeit(int argc, char** argv) {
     if (argc != 5) return 2;
     const int reps = std::atoi(argv[2]);
     const std::string mode = argv[3];
-    std::vector<double> ts;
+    std::vector<double> ts, ph[4];
+    g_timing = true;
     for (int r = 0; r < reps + 3; r++) {
         FILE* in = std::fopen(argv[4], "rb");
         char* buf = nullptr;
@@ -990,10 +1021,19 @@ static int run_timeit(int argc, char** argv) {
         std::fclose(mem);
         std::free(buf);
         if (g_call_us < 0) return 2;   // the mode records no call time
-        if (r >= 3) ts.push_back(g_call_us);
+        if (r >= 3) {
+            ts.push_back(g_call_us);
+            for (int i = 0; i < 4; i++) ph[i].push_back(g_phase_us[i]);
+        }
     }
     std::sort(ts.begin(), ts.end());
-    std::printf("median_us %.1f min_us %.1f\n", ts[ts.size() / 2], ts[0]);
+    std::printf("median_us %.1f min_us %.1f", ts[ts.size() / 2], ts[0]);
+    if ((mode == "lba" || mode == "lbacpu") && ph[0][0] >= 0) {   // medians of the phases: gather, arrays, lba_solve, write-back
+        for (auto& v : ph) std::sort(v.begin(), v.end());
+        std::printf(" phases_us %.1f %.1f %.1f %.1f", ph[0][ph[0].size() / 2], ph[1][ph[1].size() / 2],
+                    ph[2][ph[2].size() / 2], ph[3][ph[3].size() / 2]);
+    }
+    std::printf("\n");
     return 0;
 }
 

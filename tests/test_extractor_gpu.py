@@ -348,3 +348,33 @@ def test_level0_lifetime_contract(amd, copy):
         assert n == len(ref["kps"])
         assert kps[b, :n].cpu().numpy().view(amd._abi.KEYPOINT_DTYPE).reshape(-1).tobytes() == ref["kps"].tobytes()
         assert np.array_equal(desc[b, :n].cpu().numpy(), ref["desc"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("row_bytes,B,cap", [(28, 5, 40), (32, 64, 1062), (4, 1, 7), (4, 33, 300)])
+def test_pack_rows_device(amd, row_bytes, B, cap):
+    """orb_pack_rows_device: frame b's min(counts[b], cap) rows at a capacity stride, packed back
+    to back at the exclusive prefix; offsets[B] = the total (counts past cap, zero and negative
+    counts included)."""
+    import ctypes as C
+    import torch
+    from orb_slam2_amd import _abi
+    rng = np.random.default_rng(row_bytes * 1000 + B)
+    src = rng.integers(0, 256, (B, cap, row_bytes), dtype=np.uint8)
+    cnt = rng.integers(-2, cap + 5, B).astype(np.int32)
+    cnt[0] = cap + 3 if B > 1 else cnt[0]
+    dev = torch.device("cuda", 0)
+    ds = torch.from_numpy(src).to(dev)
+    dc = torch.from_numpy(cnt).to(dev)
+    dd = torch.zeros(B * cap * row_bytes + 4, dtype=torch.uint8, device=dev)
+    do = torch.full((B + 1,), -7, dtype=torch.int32, device=dev)
+    _abi.check("pack", _abi.lib().orb_pack_rows_device(C.c_void_p(ds.data_ptr()), row_bytes, cap,
+                                                       C.c_void_p(dc.data_ptr()), B, C.c_void_p(dd.data_ptr()),
+                                                       C.c_void_p(do.data_ptr()), None))
+    torch.cuda.synchronize(dev)
+    n = np.clip(cnt, 0, cap)
+    off = np.concatenate([[0], np.cumsum(n)]).astype(np.int32)
+    assert np.array_equal(do.cpu().numpy(), off)
+    want = np.concatenate([src[b, :n[b]].reshape(-1) for b in range(B)])
+    got = dd.cpu().numpy()
+    assert np.array_equal(got[:len(want)], want) and not got[len(want):].any()
