@@ -1318,19 +1318,32 @@ def bench_routed_calls(args, amd, dev, med, creps=9):
                     a.tofile(f)
             res = subprocess.run([str(exe), "timeit", "20", "lba", str(inp)], capture_output=True, text=True,
                                  timeout=300)
-        g = None
-        if res.returncode == 0 and res.stdout.startswith("median_us"):
-            g = float(res.stdout.split()[1])
-        c = None
-        if not args.no_cpu:
-            t0 = time.perf_counter()
-            O.lba_solve(pb)
-            c = round(1e6 * (time.perf_counter() - t0), 1)
+            resc = None
+            if not args.no_cpu:   # the same shim gather / write-back around the oracle's 1-thread solve
+                env = dict(os.environ, ORB_ORACLE_LIB=str(ROOT / "oracle" / "build" / "liborb_oracle.so"))
+                resc = subprocess.run([str(exe), "timeit", "3", "lbacpu", str(inp)], capture_output=True, text=True,
+                                      timeout=600, env=env)
+
+        def parse(r):
+            if r is None or r.returncode != 0 or not r.stdout.startswith("median_us"):
+                return None, None
+            w = r.stdout.split()
+            ph = None
+            if "phases_us" in w:
+                i = w.index("phases_us")
+                ph = dict(zip(("gather", "arrays", "lba_solve", "write_back"), (float(x) for x in w[i + 1:i + 5])))
+            return float(w[1]), ph
+        g, gph = parse(res)
+        c, cph = parse(resc)
         rows["local_bundle_adjustment_shim"] = {
             "gpu_us": g, "cpu_1thread_us": c, "gpu_over_cpu": None if (c is None or not g) else round(c / g, 2),
+            "gpu_phases_us": gph, "cpu_phases_us": cph,
+            "host_pool_threads": int(os.environ.get("ORB_SHIM_THREADS", "4")),
             "call_site": "R/src/LocalMapping.cpp:95", "size": f"{args.lba_kf} KF + 4 fixed x {args.lba_points} points",
-            "note": "whole call: graph gather from the (mock) map, lba_solve, write-back; cpu = the oracle's solve "
-                    "alone (no gather), 1 thread", "stderr_tail": None if res.returncode == 0 else res.stderr[-300:]}
+            "note": "whole call through the compiled drop-in: window gather from the (mock) map, the problem arrays, "
+                    "the solve, vToErase + write-back (phase medians); cpu = the same shim code around the oracle's "
+                    "single-threaded solve (the reference's LocalMapping runs g2o without OpenMP)",
+            "stderr_tail": None if res.returncode == 0 else res.stderr[-300:]}
     return rows
 
 

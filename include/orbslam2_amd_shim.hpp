@@ -28,15 +28,21 @@
 #pragma once
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdint>
+#include <condition_variable>
+#include <cstdlib>
 #include <cstring>
+#include <exception>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <set>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <type_traits>
 #include <utility>
 #include <vector>
@@ -800,21 +806,118 @@ inline double* lba_last_phases() {
 }
 
 namespace detail {
+// A small pool of host threads for the per-point loops of LocalBundleAdjustment's gather and
+// write-back (one pool per calling thread, created on first use; ORB_SHIM_THREADS workers, default
+// 4, 0 = run inline).  parallel_for(n, grain, fn) calls fn(begin, end) over [0, n) in chunks of
+// `grain`, the caller taking chunks too, and returns when every chunk has run; an exception in a
+// chunk is rethrown in the caller.  Every worker checks in once per call, so no worker can miss one.
+class HostPool {
+public:
+    explicit HostPool(int n) {
+        for (int i = 0; i < n; i++) th_.emplace_back([this] { run(); });
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            stop_ = true;
+            ++gen_;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    template <class F>
+    void parallel_for(size_t n, size_t grain, F&& fn) {
+        if (grain == 0) grain = 1;
+        if (th_.empty() || n <= grain) {
+            if (n) fn((size_t)0, n);
+            return;
+        }
+        std::function<void(size_t, size_t)> f(std::forward<F>(fn));
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            job_ = &f;
+            n_ = n;
+            grain_ = grain;
+            err_ = nullptr;
+            next_.store(0, std::memory_order_relaxed);
+            pending_.store((int)th_.size(), std::memory_order_relaxed);
+            ++gen_;
+        }
+        cv_.notify_all();
+        work();
+        while (pending_.load(std::memory_order_acquire) != 0) std::this_thread::yield();
+        job_ = nullptr;
+        if (err_) std::rethrow_exception(err_);
+    }
+
+private:
+    void work() {
+        for (;;) {
+            const size_t b = next_.fetch_add(grain_, std::memory_order_relaxed);
+            if (b >= n_) break;
+            try {
+                (*job_)(b, std::min(n_, b + grain_));
+            } catch (...) {
+                std::lock_guard<std::mutex> lk(errM_);
+                if (!err_) err_ = std::current_exception();
+            }
+        }
+    }
+    void run() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return gen_ != seen; });
+                seen = gen_;
+                if (stop_) return;
+            }
+            work();
+            pending_.fetch_sub(1, std::memory_order_acq_rel);
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_, errM_;
+    std::condition_variable cv_;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+    const std::function<void(size_t, size_t)>* job_ = nullptr;
+    size_t n_ = 0, grain_ = 1;
+    std::atomic<size_t> next_{0};
+    std::atomic<int> pending_{0};
+    std::exception_ptr err_;
+};
+
+inline HostPool& thread_pool() {
+    thread_local HostPool pool([] {
+        const char* e = std::getenv("ORB_SHIM_THREADS");
+        const int n = e ? std::atoi(e) : 4;
+        return n < 0 ? 0 : (n > 64 ? 64 : n);
+    }());
+    return pool;
+}
+
 // Per-thread working set of local_ba, reused from call to call (LocalMapping calls it once per
 // keyframe): the window lists, the problem / result arrays and the edge bookkeeping keep their
 // capacity, so a steady-state call allocates only what the reference API returns by value.
-template <class KeyFrameT, class MapPointT, class ObsT>
+template <class KeyFrameT, class MapPointT>
 struct LbaScratch {
+    struct Ob {   // one observation as read once from GetObservations(), with its observer's isBad()
+        KeyFrameT* kf;
+        size_t idx;
+        bool bad;
+    };
     LbaDump D;
     std::vector<KeyFrameT*> localKFs, fixedKFs, edgeKF;
     std::vector<MapPointT*> localMPs;
-    std::vector<ObsT> obs;
+    std::vector<std::vector<Ob>> obs;   // per point (the inner vectors keep their capacity across calls)
     std::vector<std::pair<const KeyFrameT*, int>> poseIndex;
     std::vector<std::pair<KeyFrameT*, MapPointT*>> toErase;
+    std::vector<int> nEdge;
     void clear() {
         D.clear();
-        localKFs.clear(); fixedKFs.clear(); edgeKF.clear(); localMPs.clear(); obs.clear(); poseIndex.clear();
-        toErase.clear();
+        localKFs.clear(); fixedKFs.clear(); edgeKF.clear(); localMPs.clear(); poseIndex.clear();
+        toErase.clear(); nEdge.clear();
     }
 };
 
@@ -822,7 +925,6 @@ template <class KeyFrameT, class MapT, class Solve>
 void local_ba(KeyFrameT* pKF, bool* pbStopFlag, MapT* pMap, LbaDump* dump, Solve&& solve) {
     using MapPointT = typename std::remove_pointer<typename decltype(pKF->GetMapPointMatches())::value_type>::type;
     using MatT = typename std::decay<decltype(pKF->GetPose())>::type;
-    using ObsT = typename std::decay<decltype(std::declval<MapPointT*>()->GetObservations())>::type;
     using Clock = std::chrono::steady_clock;
     auto tPhase = Clock::now();
     double* ph = lba_last_phases();
@@ -832,10 +934,10 @@ void local_ba(KeyFrameT* pKF, bool* pbStopFlag, MapT* pMap, LbaDump* dump, Solve
         tPhase = now;
     };
     ph[0] = ph[1] = ph[2] = ph[3] = 0.0;
-    thread_local LbaScratch<KeyFrameT, MapPointT, ObsT> sc;
+    thread_local LbaScratch<KeyFrameT, MapPointT> sc;
     sc.clear();
     struct Out {   // the caller's dump (tests) receives a copy of the arrays, whatever the exit
-        LbaScratch<KeyFrameT, MapPointT, ObsT>& sc;
+        LbaScratch<KeyFrameT, MapPointT>& sc;
         LbaDump* dump;
         double* ph;
         ~Out() {
@@ -861,30 +963,47 @@ void local_ba(KeyFrameT* pKF, bool* pbStopFlag, MapT* pMap, LbaDump* dump, Solve
                 lLocalMapPoints.push_back(pMP);
                 pMP->mnBALocalForKF = pKF->mnId;
             }
-    // (each point's observations are read once here and reused for its edges below; the reference
-    // calls GetObservations() again at :740 — both are snapshots of a map other threads may grow)
+    // (each point's observations are read once here, in parallel over the points, and reused for its
+    // edges below; the reference calls GetObservations() again at :740 — both are snapshots of a map
+    // other threads may grow).  Per point also the number of its edges (observers not bad).
+    HostPool& pool = thread_pool();
     auto& vObs = sc.obs;
-    size_t nObs = 0;
+    auto& nEdge = sc.nEdge;
+    const size_t nPts = lLocalMapPoints.size();
+    vObs.resize(nPts);
+    nEdge.assign(nPts + 1, 0);
+    pool.parallel_for(nPts, 64, [&](size_t b, size_t e) {
+        for (size_t i = b; i < e; i++) {
+            auto& v = vObs[i];
+            v.clear();
+            int n = 0;
+            for (const auto& ob : lLocalMapPoints[i]->GetObservations()) {   // isBad() read once per observation
+                const bool bad = ob.first->isBad();
+                v.push_back({ob.first, (size_t)ob.second, bad});
+                n += bad ? 0 : 1;
+            }
+            nEdge[i + 1] = n;
+        }
+    });
     auto& lFixedCameras = sc.fixedKFs;
-    for (MapPointT* pMP : lLocalMapPoints) {
-        vObs.push_back(pMP->GetObservations());
-        nObs += vObs.back().size();
-        for (const auto& ob : vObs.back()) {
-            KeyFrameT* pKFi = ob.first;
+    for (size_t i = 0; i < nPts; i++)   // first-seen order, as the reference's list
+        for (const auto& ob : vObs[i]) {
+            KeyFrameT* pKFi = ob.kf;
             if (pKFi->mnBALocalForKF != pKF->mnId && pKFi->mnBAFixedForKF != pKF->mnId) {
                 pKFi->mnBAFixedForKF = pKF->mnId;
-                if (!pKFi->isBad()) lFixedCameras.push_back(pKFi);
+                if (!ob.bad) lFixedCameras.push_back(pKFi);
             }
         }
-    }
+    for (size_t i = 0; i < nPts; i++) nEdge[i + 1] += nEdge[i];   // edge offsets per point
+    const size_t nObs = (size_t)nEdge[nPts];
     lap(ph[0]);
     // ---- the graph as arrays (vertices: local poses (fixed iff mnId == 0), fixed cameras, points
     //      with id mnId + maxKFid + 1; edges per point in observation order, R :636-782)
-    const size_t nPoses = lLocalKeyFrames.size() + lFixedCameras.size(), nPts = lLocalMapPoints.size();
+    const size_t nPoses = lLocalKeyFrames.size() + lFixedCameras.size();
     D.pose_q.reserve(4 * nPoses); D.pose_t.reserve(3 * nPoses); D.pose_fixed.reserve(nPoses); D.pose_id.reserve(nPoses);
-    D.point_xyz.reserve(3 * nPts); D.point_id.reserve(nPts); D.point_bad.reserve(nPts);
-    D.edge_point.reserve(nObs); D.edge_pose.reserve(nObs); D.edge_stereo.reserve(nObs); D.edge_obs.reserve(3 * nObs);
-    D.edge_info.reserve(nObs); D.edge_cam.reserve(5 * nObs);
+    D.point_xyz.resize(3 * nPts); D.point_id.resize(nPts); D.point_bad.resize(nPts);
+    D.edge_point.resize(nObs); D.edge_pose.resize(nObs); D.edge_stereo.resize(nObs); D.edge_obs.resize(3 * nObs);
+    D.edge_info.resize(nObs); D.edge_cam.resize(5 * nObs);
     // keyframe -> vertex index: a sorted array (a window holds tens of keyframes)
     auto& poseIndex = sc.poseIndex;
     unsigned long maxKFid = 0;
@@ -910,30 +1029,35 @@ void local_ba(KeyFrameT* pKF, bool* pbStopFlag, MapT* pMap, LbaDump* dump, Solve
     };
     auto& vpMP = lLocalMapPoints;   // vertex order = the local map points' order
     auto& vpEdgeKF = sc.edgeKF;
-    vpEdgeKF.reserve(nObs);
-    for (size_t pi = 0; pi < vpMP.size(); pi++) {
-        MapPointT* pMP = vpMP[pi];
-        const MatT X = pMP->GetWorldPos();
-        for (int i = 0; i < 3; i++) D.point_xyz.push_back((double)X.template at<float>(i, 0));   // Converter::toVector3d
-        D.point_id.push_back((int64_t)(pMP->mnId + maxKFid + 1));
-        D.point_bad.push_back(pMP->isBad() ? 1 : 0);
-        for (const auto& ob : vObs[pi]) {
-            KeyFrameT* pKFi = ob.first;
-            if (pKFi->isBad()) continue;
-            const auto& kpUn = pKFi->mvKeysUn[ob.second];
-            const float ur = pKFi->mvuRight[ob.second];
-            D.edge_point.push_back((int32_t)pi);
-            D.edge_pose.push_back(poseOf(pKFi));
-            D.edge_stereo.push_back(ur < 0 ? 0 : 1);
-            D.edge_obs.push_back(kpUn.pt.x);
-            D.edge_obs.push_back(kpUn.pt.y);
-            D.edge_obs.push_back(ur < 0 ? 0.0 : (double)ur);
-            D.edge_info.push_back((double)pKFi->mvInvLevelSigma2[kpUn.octave]);   // I * invSigma2 (float)
-            const double cam[5] = {pKFi->fx, pKFi->fy, pKFi->cx, pKFi->cy, pKFi->mbf};
-            D.edge_cam.insert(D.edge_cam.end(), cam, cam + 5);
-            vpEdgeKF.push_back(pKFi);
+    vpEdgeKF.resize(nObs);
+    // points and their edges, in parallel over the points: point pi's edges fill [nEdge[pi], nEdge[pi+1])
+    pool.parallel_for(nPts, 64, [&](size_t b, size_t e) {
+        for (size_t pi = b; pi < e; pi++) {
+            MapPointT* pMP = vpMP[pi];
+            const MatT X = pMP->GetWorldPos();
+            for (int i = 0; i < 3; i++) D.point_xyz[3 * pi + (size_t)i] = (double)X.template at<float>(i, 0);   // Converter::toVector3d
+            D.point_id[pi] = (int64_t)(pMP->mnId + maxKFid + 1);
+            D.point_bad[pi] = pMP->isBad() ? 1 : 0;
+            size_t k = (size_t)nEdge[pi];
+            for (const auto& ob : vObs[pi]) {
+                if (ob.bad) continue;
+                KeyFrameT* pKFi = ob.kf;
+                const auto& kpUn = pKFi->mvKeysUn[ob.idx];
+                const float ur = pKFi->mvuRight[ob.idx];
+                D.edge_point[k] = (int32_t)pi;
+                D.edge_pose[k] = poseOf(pKFi);
+                D.edge_stereo[k] = ur < 0 ? 0 : 1;
+                D.edge_obs[3 * k] = kpUn.pt.x;
+                D.edge_obs[3 * k + 1] = kpUn.pt.y;
+                D.edge_obs[3 * k + 2] = ur < 0 ? 0.0 : (double)ur;
+                D.edge_info[k] = (double)pKFi->mvInvLevelSigma2[kpUn.octave];   // I * invSigma2 (float)
+                double* cam = &D.edge_cam[5 * k];
+                cam[0] = pKFi->fx; cam[1] = pKFi->fy; cam[2] = pKFi->cx; cam[3] = pKFi->cy; cam[4] = pKFi->mbf;
+                vpEdgeKF[k] = pKFi;
+                k++;
+            }
         }
-    }
+    });
     const int NP = (int)D.pose_fixed.size(), NM = (int)vpMP.size(), NE = (int)D.edge_point.size();
     lba_problem p{NP, D.pose_q.data(), D.pose_t.data(), D.pose_fixed.data(), D.pose_id.data(),
                   NM, D.point_xyz.data(), D.point_id.data(), D.point_bad.data(),
@@ -981,12 +1105,15 @@ void local_ba(KeyFrameT* pKF, bool* pbStopFlag, MapT* pMap, LbaDump* dump, Solve
         k->SetPose(detail::make_mat<MatT>(4, 4, T));
         i++;
     }
-    for (int m = 0; m < NM; m++) {
-        const float X[3] = {(float)D.out_xyz[3 * (size_t)m], (float)D.out_xyz[3 * (size_t)m + 1],
-                            (float)D.out_xyz[3 * (size_t)m + 2]};
-        vpMP[(size_t)m]->SetWorldPos(detail::make_mat<MatT>(3, 1, X));
-        vpMP[(size_t)m]->UpdateNormalAndDepth();
-    }
+    // the points in parallel: each SetWorldPos + UpdateNormalAndDepth touches its own point (and reads
+    // the keyframe poses set above), as the reference's loop does one by one
+    pool.parallel_for((size_t)NM, 64, [&](size_t b, size_t e) {
+        for (size_t m = b; m < e; m++) {
+            const float X[3] = {(float)D.out_xyz[3 * m], (float)D.out_xyz[3 * m + 1], (float)D.out_xyz[3 * m + 2]};
+            vpMP[m]->SetWorldPos(detail::make_mat<MatT>(3, 1, X));
+            vpMP[m]->UpdateNormalAndDepth();
+        }
+    });
     lap(ph[3]);
 }
 }  // namespace detail

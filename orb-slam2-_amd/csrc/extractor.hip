@@ -740,17 +740,18 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
         auto even_ring4 = [&](uint32_t cL, uint32_t cC, uint32_t cR, uint32_t u3, uint32_t d3, uint32_t u2L,
                               uint32_t u2C, uint32_t u2R, uint32_t d2L, uint32_t d2C, uint32_t d2R) -> uint32_t {
             const uint32_t vE = cC & 0x00ff00ffu, vO = (cC >> 8) & 0x00ff00ffu;
-            const uint32_t A = upk(__builtin_elementwise_sub_sat(pk(vE), tt)) |
-                               (upk(__builtin_elementwise_sub_sat(pk(vO), tt)) << 8);
-            const uint32_t B = upk(__builtin_elementwise_min(pk(vE) + tt, m255)) |
-                               (upk(__builtin_elementwise_min(pk(vO) + tt, m255)) << 8);
-            const uint32_t nB = ~B;
-            uint32_t dk[8], br[8];
-            // v_lerp_u8 averages bytes without carries between them: (x + ~y) >> 1 has its top bit
-            // set iff x + 255 - y >= 256, i.e. x > y
+            const uint32_t nA = ~(upk(__builtin_elementwise_sub_sat(pk(vE), tt)) |
+                                  (upk(__builtin_elementwise_sub_sat(pk(vO), tt)) << 8));
+            const uint32_t nB = ~(upk(__builtin_elementwise_min(pk(vE) + tt, m255)) |
+                                  (upk(__builtin_elementwise_min(pk(vO) + tt, m255)) << 8));
+            uint32_t ndk[8], br[8];
+            // v_lerp_u8 averages bytes without carries between them: (x + y + r) >> 1 per byte, r the
+            // byte's rounding bit.  Bright: (p + ~B) >> 1 has its top bit set iff p + 255 - B >= 256,
+            // i.e. p > B.  Dark, complemented so no ~p is needed: (~A + p + 1) >> 1 has its top bit
+            // set iff 255 - A + p + 1 >= 256, i.e. p >= A — NOT dark (A > p)
             auto flags = [&](uint32_t p, int u) {
-                dk[u] = __builtin_amdgcn_lerp(A, ~p, 0u);   // A > p: dark
-                br[u] = __builtin_amdgcn_lerp(p, nB, 0u);   // p > B: bright
+                ndk[u] = __builtin_amdgcn_lerp(nA, p, 0x01010101u);   // !(A > p)
+                br[u] = __builtin_amdgcn_lerp(p, nB, 0u);            // p > B: bright
             };
             flags(d3, 0);
             flags(__builtin_amdgcn_alignbyte(d2R, d2C, 2), 1);
@@ -767,7 +768,12 @@ __global__ __launch_bounds__(256) void k_fast_cell(Geom g, const uint8_t* __rest
                 const uint32_t ev = ((D[0] & D[1]) | (D[4] & D[5])) & ((D[2] & D[3]) | (D[6] & D[7]));
                 return (((D[1] & D[2]) | (D[5] & D[6])) & ((D[3] & D[4]) | (D[7] & D[0]))) | ev;
             };
-            return (runs(dk) | runs(br)) & H;   // pixel k's flag in bit 8k + 7
+            // the same on complemented flags N = ~D (De Morgan): ~runs(D)
+            auto no_runs = [](const uint32_t N[8]) {
+                const uint32_t ev = ((N[0] | N[1]) & (N[4] | N[5])) | ((N[2] | N[3]) & (N[6] | N[7]));
+                return (((N[1] | N[2]) & (N[5] | N[6])) | ((N[3] | N[4]) & (N[7] | N[0]))) & ev;
+            };
+            return (~no_runs(ndk) | runs(br)) & H;   // pixel k's flag in bit 8k + 7
 
         };
         const int NG = (rw + 7) >> 3;
