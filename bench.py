@@ -93,13 +93,18 @@ PMC_LANES = ROOT / "profiles" / "r05_lanes_pmc.json"   # tools/pmc_run.sh lanes 
 ISOLATED_STATS = ROOT / "profiles" / "r06_ext_isolated_stats.txt"
 
 
-def isolated_stats():
+def isolated_stats(frames_per_launch=None):
     """{kernel: avg_us} and the header lines of the committed isolated-launch rocprof summary
-    (None when absent).  Kernel names as kernel_stats.py prints them (`void k_fast_cell<40>`)."""
+    (None when absent, or when its `frames_per_launch=` header names another launch size).  Kernel
+    names as kernel_stats.py prints them (`void k_fast_cell<40>`)."""
     try:
         lines = ISOLATED_STATS.read_text().splitlines()
     except OSError:
         return None
+    if frames_per_launch is not None:
+        fpl = [ln.split("frames_per_launch=")[1].split()[0] for ln in lines if "frames_per_launch=" in ln]
+        if not fpl or int(fpl[0]) != int(frames_per_launch):
+            return None
     out, head = {}, []
     for ln in lines:
         if "calls=" in ln and "avg_us=" in ln:
@@ -134,7 +139,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=512, help="frames per step per GPU")
+    ap.add_argument("--batch", type=int, default=1024, help="frames per step per GPU")
     ap.add_argument("--streams", type=int, default=4,
                     help="independent frame sequences per GPU, each on its own HIP stream (batch split)")
     ap.add_argument("--match-stream", action="store_true",
@@ -278,7 +283,7 @@ def extraction_roofline(stage_ms, ncalls, lw, lh, n_pre, n_out, W, H, NF, Bs, is
             duration, peak 78.6 T (nominal), also against the measured 41.7 T integer issue rate.
     The dominant kernel is the one with the largest isolated duration; `bound` is whichever of
     its two fractions (HBM of 8 TB/s, VALU of the measured issue rate) is higher."""
-    iso_file = isolated_stats()
+    iso_file = isolated_stats(Bs)
     per = {}
     for name, stage, i in EXT_KERNELS:
         ms = float(stage_ms[i]) / ncalls if ncalls else 0.0
@@ -1900,14 +1905,6 @@ def main():
     for s in range(args.warmup):
         step(s)
     torch.cuda.synchronize(dev)
-    if not args.no_profile:
-        # every stream's extractor records HIP events at its four kernels' boundaries (k_pyramid,
-        # k_fast_cell, k_octree, k_orient_desc: five events per call, mode 3) on its launch stream
-        # inside the timed region: with S streams sharing the chip a launch overlapped by other
-        # streams' kernels runs longer than one alone, and the rocprofv3 per-kernel averages
-        # (profiles/) are over the same mix
-        for p in pipes:
-            lib.orb_extractor_profile(p.ex._h, 3)
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
@@ -1932,7 +1929,18 @@ def main():
         mat_status |= m
     if ext_status or mat_status:
         raise SystemExit(f"bench: overflow status extractor={ext_status} matcher={mat_status}")
-    # per-kernel launch times (HIP events recorded on the launch streams during the timed region)
+    # per-kernel launch spans under the streams' sharing: a few more steps after the timed region
+    # with HIP events at every stream's four extraction kernels' boundaries (k_pyramid, k_fast_cell,
+    # k_octree, k_orient_desc: five events per call, mode 3) on its launch stream — kept out of the
+    # timed region, whose steps carry no instrumentation
+    n_shared = 4
+    if not args.no_profile:
+        for p in pipes:
+            lib.orb_extractor_profile(p.ex._h, 3)
+        for s in range(n_shared):
+            step(args.warmup + args.steps + s)
+        torch.cuda.synchronize(dev)
+
     def stage_times():
         tot, calls = np.zeros(6), 0
         for p in pipes:
@@ -1952,7 +1960,7 @@ def main():
         lib.orb_extractor_profile(p0.ex._h, 3)
         torch.cuda.synchronize(dev)
         for s in range(n_iso):
-            p0.step(args.warmup + args.steps + s)
+            p0.step(args.warmup + args.steps + n_shared + s)
         torch.cuda.synchronize(dev)
         sm, nc = np.zeros(6), C.c_int(0)
         lib.orb_extractor_stage_times(p0.ex._h, _abi.ptr(sm), 6, C.byref(nc))
@@ -2008,9 +2016,10 @@ def main():
     if nstage > 0:
         result["stage_ms_per_batch"] = {k: round(float(v) / nstage, 4) for k, v in zip(STAGES, stage_ms)
                                         if not k.startswith("reserved")}
-        result["stage_ms_source"] = ("timed region: HIP events at the kernel boundaries on each stream, average "
-                                     "launch span while the other streams' kernels share the chip (not a kernel's own "
-                                     "duration; the isolated durations are roofline.kernels[*].isolated_launch_ms)")
+        result["stage_ms_source"] = (f"{n_shared} steps after the timed region, the same {S} streams: HIP events at the "
+                                     "kernel boundaries on each stream, average launch span while the other streams' "
+                                     "kernels share the chip (not a kernel's own duration; the isolated durations are "
+                                     "roofline.kernels[*].isolated_launch_ms)")
     if iso_ms is not None:
         result["stage_ms_isolated_live"] = {k: round(float(v), 4) for k, v in zip(STAGES, iso_ms)
                                             if not k.startswith("reserved")}

@@ -1,7 +1,7 @@
 """The benchmark's own path against the oracle.
 
 bench.py times `Pipe.step` (orb_extract_batch_device + orb_search_for_initialization_batch_device,
-4 sequences x 128 frames, each on its own HIP stream, issued back to back so the streams run
+4 sequences x 256 frames, each on its own HIP stream, issued back to back so the streams run
 concurrently).  This test builds the same `Pipe` objects from bench.py on the same synthetic pool
 (rank 0's seed), runs two steps exactly as the timed loop does, and checks after each step:
 
@@ -38,7 +38,8 @@ def _bench():
 def test_bench_pipeline_matches_oracle(amd, match_stream):
     bench = _bench()
     from orb_slam2_amd import _abi, synth
-    W, H, NF, B, S = 640, 480, 1000, 512, 4
+    W, H, NF, S = 640, 480, 1000, 4
+    B = 512 if match_stream else 1024   # the bench's default step: 4 x 256 frames
     Bs = B // S
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
