@@ -51,8 +51,8 @@ VALU_MEASURED_TOPS = 41.7        # integer VOP3 issue ceiling (the extraction / 
 VALU_MEASURED_F32_TOPS = 48.3    # v_fma_f32 issue ceiling
 STAGES = ["resize", "fast_detect", "reserved", "octree", "reserved2", "orient_blur_desc"]
 KERNELS = ["k_resize", "k_fast_cell", None, "k_octree", None, "k_orient_desc"]
-PMC_TRAFFIC = ROOT / "profiles" / "r05_pmc_traffic.json"   # tools/pmc_run.sh + tools/pmc_traffic.py
-PMC_VALU = ROOT / "profiles" / "r05_valu_pmc.json"         # tools/gpu_pmc_all.sh + tools/pmc_valu.py
+PMC_TRAFFIC = ROOT / "profiles" / "r06_pmc_traffic.json"   # tools/pmc_run.sh + tools/pmc_traffic.py
+PMC_VALU = ROOT / "profiles" / "r06_valu_pmc.json"         # tools/gpu_pmc_all.sh + tools/pmc_valu.py
 
 
 def pmc_traffic(kernel, W, H, NF, Bs):
@@ -86,7 +86,7 @@ def pmc_valu_ops(kernel, W, H, NF, Bs):
         return None
 
 
-PMC_LANES = ROOT / "profiles" / "r05_lanes_pmc.json"   # tools/pmc_run.sh lanes ... + tools/pmc_lanes.py
+PMC_LANES = ROOT / "profiles" / "r06_lanes_pmc.json"   # tools/pmc_run.sh lanes ... + tools/pmc_lanes.py
 # rocprofv3 --kernel-trace --stats of the bench's own 128-frame extraction launch run alone on one
 # stream (tools/gpu_ext_isolated.sh: bench.py --streams 1 --batch 128), formatted by
 # tools/kernel_stats.py; the headline roofline's kernel durations come from it
@@ -102,7 +102,8 @@ def isolated_stats(frames_per_launch=None):
     except OSError:
         return None
     if frames_per_launch is not None:
-        fpl = [ln.split("frames_per_launch=")[1].split()[0] for ln in lines if "frames_per_launch=" in ln]
+        import re
+        fpl = [m.group(1) for ln in lines for m in [re.search(r"frames_per_launch=(\d+)", ln)] if m]
         if not fpl or int(fpl[0]) != int(frames_per_launch):
             return None
     out, head = {}, []

@@ -16,7 +16,7 @@ cd $R
 CSV=$(find gpurun_out/prof_iso -name 'iso_kernel_stats.csv' -print -quit)
 {
   python3 tools/kernel_stats.py "$CSV" "bench.py --streams 1 --batch 256 --steps 20 --warmup 5 --no-cpu --no-lba" \
-      "--no-extras --no-stereo --no-profile: one 256-frame extraction launch + SearchForInitialization per step," \
+      "--no-extras --no-stereo --no-profile: one 256-frame extraction launch + SearchForInitialization per step (frames_per_launch=256)," \
       "alone on one HIP stream (kernels serialised), $TAG"
   echo "provenance $(python3 tools/pmc_provenance.py | tr -d '\n ')"
   echo "bench line: $( (grep "^{\"metric" gpurun_out/prof_iso.log || true) | tail -1 | cut -c1-300)"
