@@ -70,6 +70,9 @@ struct HostScratch {
     hipStream_t stream = nullptr;
     char* base = nullptr;   // device
     char* pin = nullptr;    // pinned host staging of the same size (Staging below)
+    char* pinDev = nullptr; // its device-side address (the pull kernel reads the inputs through it)
+    char* pout = nullptr;   // host-mapped coherent outputs: kernels store results straight into host memory
+    char* poutDev = nullptr;
     size_t cap = 0;
 };
 // grow-only (rare; the caller's stream is idle between its calls), under the capture lock
@@ -78,11 +81,16 @@ inline int grow_scratch(HostScratch* h, size_t bytes) {
     std::lock_guard<std::mutex> lk(legacy_capture_mutex());
     if (h->base) (void)hipFree(h->base);
     if (h->pin) (void)hipHostFree(h->pin);
-    h->base = h->pin = nullptr;
+    if (h->pout) (void)hipHostFree(h->pout);
+    h->base = h->pin = h->pinDev = h->pout = h->poutDev = nullptr;
     h->cap = 0;
     const size_t cap = std::max(bytes + bytes / 2, (size_t)1 << 20);
     if (hipMalloc((void**)&h->base, cap) != hipSuccess) return ORB_ENOMEM;
-    if (hipHostMalloc((void**)&h->pin, cap, hipHostMallocDefault) != hipSuccess) return ORB_ENOMEM;
+    if (hipHostMalloc((void**)&h->pin, cap, hipHostMallocMapped) != hipSuccess) return ORB_ENOMEM;
+    if (hipHostGetDevicePointer((void**)&h->pinDev, h->pin, 0) != hipSuccess) return ORB_EGPU;
+    if (hipHostMalloc((void**)&h->pout, cap, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+        return ORB_ENOMEM;
+    if (hipHostGetDevicePointer((void**)&h->poutDev, h->pout, 0) != hipSuccess) return ORB_EGPU;
     h->cap = cap;
     return ORB_OK;
 }
@@ -113,9 +121,18 @@ inline int host_scratch(int device, size_t bytes, HostScratch** out) {
 // (a pageable hipMemcpyAsync per array costs ~10 us each); outputs are reserved after them in one
 // contiguous range that comes back in one copy, and the host reads them from the staging after
 // the stream sync.  Offsets advance in 256-byte steps; running past the scratch is an error.
+// The inputs' copy to the device as a kernel (Staging::upload_pull): 16-byte loads of the pinned
+// staging through its device address, coalesced over the grid — for the few-tens-of-KB inputs of a
+// matcher call the SDMA copy command's start-up (~8 us, then ~6 us before the dependent kernel
+// starts) is most of its cost; a kernel's dependent successor starts within ~1-2 us.
+static __global__ __launch_bounds__(256) void k_pull_staging(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                             size_t n16) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256) dst[i] = src[i];
+}
+
 struct Staging {
     HostScratch* h;
-    size_t off = 0, inEnd = 0;
+    size_t off = 0, inEnd = 0, ooff = 0;
     bool over = false;
     explicit Staging(HostScratch* hs) : h(hs) {}
     static size_t al(size_t b) { return (b + 255) & ~(size_t)255; }
@@ -152,6 +169,30 @@ struct Staging {
         if (off && hipMemcpyAsync(h->base, h->pin, off, hipMemcpyHostToDevice, s) != hipSuccess) return ORB_EGPU;
         return ORB_OK;
     }
+    // the inputs to the device by a kernel instead of a copy command (same bytes, same offsets)
+    int upload_pull(hipStream_t s) {
+        if (over) return ORB_EINTERNAL;
+        inEnd = off;
+        if (off) {
+            const size_t n16 = (off + 15) / 16;
+            const unsigned nb = (unsigned)std::min<size_t>((n16 + 255) / 256, 1024);
+            hipLaunchKernelGGL(k_pull_staging, dim3(nb), dim3(256), 0, s, reinterpret_cast<const uint4*>(h->pinDev),
+                               reinterpret_cast<uint4*>(h->base), n16);
+            if (hipGetLastError() != hipSuccess) return ORB_EGPU;
+        }
+        return ORB_OK;
+    }
+    // a write-once result stored by the kernel straight into host-mapped memory (no copy back):
+    // the device address to pass to the kernel; read it with host_out() after the stream sync
+    char* out_host(size_t bytes) {
+        const size_t a = al(bytes + 1);
+        if (ooff + a > h->cap) { over = true; return h->poutDev; }
+        char* d = h->poutDev + ooff;
+        ooff += a;
+        return d;
+    }
+    template <class T>
+    T* host_out(T* dptr) const { return (T*)(h->pout + ((const char*)dptr - h->poutDev)); }
     // device space after the inputs (outputs, work); `from` .. the end comes back in download()
     char* out(size_t bytes) { return take(bytes); }
     int download(hipStream_t s, const void* from) {

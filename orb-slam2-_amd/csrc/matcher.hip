@@ -1816,6 +1816,7 @@ void orb_matcher_destroy(orb_matcher* m) try {
     if (m->h_pin) (void)hipHostFree(m->h_pin);
     if (m->hs.base) (void)hipFree(m->hs.base);
     if (m->hs.pin) (void)hipHostFree(m->hs.pin);
+    if (m->hs.pout) (void)hipHostFree(m->hs.pout);
     if (m->stream) (void)hipStreamDestroy(m->stream);
     delete m;
 } ORB_ABI_CATCH_VOID
@@ -1847,7 +1848,7 @@ int orb_search_for_initialization(orb_matcher* m, const orb_frame_view* f1, cons
     auto* dSt = (int32_t*)sg.in(zero, 8);
     auto* dM12 = (int32_t*)sg.out(n1 * 4);
     auto* dNm = (int32_t*)sg.out(4);
-    if (int e_ = sg.upload(s)) return e_;
+    if (int e_ = sg.upload_pull(s)) return e_;
     const GridParams g = grid_of(f2);
     hipLaunchKernelGGL(k_grid_sfi, dim3(1), dim3(256), 0, s, dK2, dN + 1, cap, g, m->d_cs, m->d_gj, m->d_gxy);
     hipLaunchKernelGGL(k_cand_sfi, dim3(kCandWaves / 4, 1), dim3(256), 0, s, dK1, dD1, dN, dD2, m->d_cs, m->d_gj,
@@ -1964,7 +1965,7 @@ int orb_search_by_projection_frame(orb_matcher* m, const orb_frame_view* cur, co
     const int32_t zero[2] = {0, 0};
     auto* dSt = (int32_t*)sg.in(zero, 8);
     auto* dNm = (int32_t*)sg.out(4);
-    if (int e_ = sg.upload(s)) return e_;
+    if (int e_ = sg.upload_pull(s)) return e_;
     const GridParams g = grid_of(cur);
     if (last->n > 0) {
         hipLaunchKernelGGL(k_cand_sbp, dim3((last->n + 3) / 4), dim3(256), 0, s, dKc, dDc,
@@ -2023,7 +2024,7 @@ int orb_search_by_projection_kf(orb_matcher* m, const orb_frame_view* cur, const
     const int32_t zero[2] = {0, 0};
     auto* dSt = (int32_t*)sg.in(zero, 8);
     auto* dNm = (int32_t*)sg.out(4);
-    if (int e_ = sg.upload(s)) return e_;
+    if (int e_ = sg.upload_pull(s)) return e_;
     const GridParams g = grid_of(cur);
     if (nmp > 0) {
         hipLaunchKernelGGL(k_cand_sbk, dim3((nmp + 3) / 4), dim3(256), 0, s, dKc, dDc, cur->n, nmp, dVal, dXyz,
@@ -2079,7 +2080,7 @@ int orb_search_by_projection_sim3(orb_matcher* m, const orb_frame_view* kf, cons
     const int32_t zero[2] = {0, 0};
     auto* dSt = (int32_t*)sg.in(zero, 8);
     auto* dNm = (int32_t*)sg.out(4);
-    if (int e_ = sg.upload(s)) return e_;
+    if (int e_ = sg.upload_pull(s)) return e_;
     const GridParams g = grid_of(kf);
     if (n_mp > 0) {
         hipLaunchKernelGGL(k_cand_sbs, dim3((n_mp + 3) / 4), dim3(256), 0, s, dK, dD, kf->n, g, K, n_mp, dVal, dXyz,
@@ -2142,7 +2143,7 @@ int orb_search_by_projection_local(orb_matcher* m, const orb_frame_view* f, int 
     const int32_t zero[2] = {0, 0};
     auto* dSt = (int32_t*)sg.in(zero, 8);
     auto* dNm = (int32_t*)sg.out(4);
-    if (int e_ = sg.upload(s)) return e_;
+    if (int e_ = sg.upload_pull(s)) return e_;
     const GridParams g = grid_of(f);
     hipLaunchKernelGGL(k_cand_sbl, dim3((n_mp + 3) / 4), dim3(256), 0, s, dK, dD,
                        f->uright ? (const float*)dUr : (const float*)nullptr, f->n, n_mp, dIn, dProj, dLvl, dCos, dMd,
@@ -2175,7 +2176,7 @@ int orb_hamming_knn2(orb_matcher* m, const uint8_t* q, int nq, const uint8_t* t,
     auto* dBi = (int32_t*)sg.out(bq);
     auto* dBd = (int32_t*)sg.out(bq);
     auto* dSd = (int32_t*)sg.out(bq);
-    if (int e_ = sg.upload(s)) return e_;
+    if (int e_ = sg.upload_pull(s)) return e_;
     hipLaunchKernelGGL(k_knn2, dim3((nq + 3) / 4, 1), dim3(256), 0, s, dQ, dN, dT, dN + 1, cap, cap, dBi, dBd, dSd);
     ORB_HIP_TRY(hipGetLastError());
     if (int e_ = sg.download(s, dBi)) return e_;
@@ -2229,7 +2230,7 @@ int orb_distinctive_descriptors(int device, const uint8_t* desc, const int32_t* 
     int32_t* dS = (int32_t*)sg.in(nullptr, ((size_t)n_points + 1) * 4);
     int32_t* hrel = sg.host(dS);
     for (int m = 0; m <= n_points; m++) hrel[m] = start[m] - start[0];
-    if (int e_ = sg.upload(s)) return e_;
+    if (int e_ = sg.upload_pull(s)) return e_;
     int32_t* dI = (int32_t*)sg.out((size_t)n_points * 4);
     uint8_t* dB = (uint8_t*)sg.out((size_t)n_points * 32);
     int rc = orb_distinctive_descriptors_device(dD, dS, n_points, dI, best_desc ? dB : nullptr, s);
@@ -2288,20 +2289,19 @@ static int fuse_impl(int device, const orb_frame_view* kf, const orb_kf_params* 
     float* dMin = (float*)sg.in(mp_min_dist, (size_t)n_mp * 4);
     float* dMax = (float*)sg.in(mp_max_dist, (size_t)n_mp * 4);
     uint8_t* dMD = (uint8_t*)sg.in(mp_desc, (size_t)n_mp * 32);
-    if (int e_ = sg.upload(s)) return e_;
-    int32_t* dBI = (int32_t*)sg.out((size_t)n_mp * 4);
-    int32_t* dBD = (int32_t*)sg.out((size_t)n_mp * 4);
+    if (int e_ = sg.upload_pull(s)) return e_;
+    // the two results go straight into host-mapped memory: no copy back
+    int32_t* dBI = (int32_t*)sg.out_host((size_t)n_mp * 4);
+    int32_t* dBD = (int32_t*)sg.out_host((size_t)n_mp * 4);
+    if (sg.over) return ORB_EINTERNAL;
     const GridParams g = grid_of(kf);
     hipLaunchKernelGGL(k_fuse, dim3((n_mp + 3) / 4), dim3(256), 0, s, dK, dD, kf->uright ? (const float*)dU : nullptr,
                        nk, g, K, n_mp, dV, dX, dN, dMin, dMax, dMD, th, dBI, dBD, sim3);
     int rc = hipGetLastError() == hipSuccess ? ORB_OK : ORB_EGPU;
+    if (rc == ORB_OK && hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
     if (rc == ORB_OK) {
-        rc = sg.download(s, dBI);
-        if (rc == ORB_OK && hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
-        if (rc == ORB_OK) {
-            std::memcpy(best_idx, sg.host(dBI), (size_t)n_mp * 4);
-            std::memcpy(best_dist, sg.host(dBD), (size_t)n_mp * 4);
-        }
+        std::memcpy(best_idx, sg.host_out(dBI), (size_t)n_mp * 4);
+        std::memcpy(best_dist, sg.host_out(dBD), (size_t)n_mp * 4);
     }
     return rc;
 }
@@ -2374,7 +2374,7 @@ int orb_search_by_sim3(int device, const orb_frame_view* kf1, const orb_frame_vi
     auto* dMin2 = (float*)sg.in(p2->min_dist, (size_t)n2 * 4);
     auto* dMax2 = (float*)sg.in(p2->max_dist, (size_t)n2 * 4);
     auto* dMD2 = (uint8_t*)sg.in(p2->desc, (size_t)n2 * 32);
-    if (int e_ = sg.upload(s)) return e_;
+    if (int e_ = sg.upload_pull(s)) return e_;
     auto* dM1 = (int32_t*)sg.out((size_t)n1 * 4);
     auto* dM2 = (int32_t*)sg.out((size_t)n2 * 4);
     hipLaunchKernelGGL(k_sim3_match, dim3((n1 + 3) / 4), dim3(256), 0, s, dK2, dD2, n2, grid_of(kf2), S12, n1, dV1, dX1,
@@ -2468,7 +2468,7 @@ int orb_search_for_triangulation(int device, const orb_frame_view* kf1, const or
     auto* dI2 = (int32_t*)sg.in(fidx2, (size_t)L2 * 4);
     auto* dMt = (int32_t*)sg.in(matches12, (size_t)n1 * 4);
     auto* dNm = (int32_t*)sg.out(4);
-    if (int e_ = sg.upload(s)) return e_;
+    if (int e_ = sg.upload_pull(s)) return e_;
     hipLaunchKernelGGL(k_sft, dim3((unsigned)common.size()), dim3(64), 0, s, dK1, dD1, kf1->uright ? dU1 : nullptr, dM1,
                        dK2, dD2, kf2->uright ? dU2 : nullptr, dM2, dN, dI1, dI2, P, dMt);
     hipLaunchKernelGGL(k_sft_rot, dim3(1), dim3(256), 0, s, dK1, dK2, n1, check_ori ? 1 : 0, dMt, dNm);
@@ -2543,7 +2543,7 @@ static int search_by_bow(int device, const orb_frame_view* v1, const uint8_t* ok
     auto* dI2 = (int32_t*)sg.in(fidx2, (size_t)L2 * 4);
     auto* dMt = (int32_t*)sg.in(matches12, (size_t)n1 * 4);
     auto* dNm = (int32_t*)sg.out(4);
-    if (int e_ = sg.upload(s)) return e_;
+    if (int e_ = sg.upload_pull(s)) return e_;
     hipLaunchKernelGGL(k_sbb, dim3((unsigned)common.size()), dim3(64), 0, s, dD1, dO1, dD2, ok2 ? dO2 : nullptr, dN,
                        dI1, dI2, thIncl, ratio, dMt);
     hipLaunchKernelGGL(k_sft_rot, dim3(1), dim3(256), 0, s, dK1, dK2, n1, check_ori ? 1 : 0, dMt, dNm);

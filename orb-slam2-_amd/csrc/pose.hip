@@ -574,7 +574,7 @@ int pose_optimize_batch(int device, const pose_batch* p, pose_batch_result* r, i
     dp.edge_obs = (const double*)sg.in(p->edge_obs, (size_t)E * 24);
     dp.edge_xw = (const double*)sg.in(p->edge_xw, (size_t)E * 24);
     dp.edge_info = (const double*)sg.in(p->edge_info, (size_t)E * 8);
-    if (int e_ = sg.upload(s)) return e_;
+    if (int e_ = sg.upload_pull(s)) return e_;
     double* dWork = (double*)sg.out((size_t)E * 24 + 8);
     uint8_t* dFlags = (uint8_t*)sg.out(2 * (size_t)E + 2);
     pose_batch_result dr;
