@@ -1633,7 +1633,7 @@ __global__ __launch_bounds__(64) void k_sft(const orb_keypoint* __restrict__ k1,
 // counts in LDS, ComputeThreeMaxima, matches outside the three bins dropped; *nmatches.
 __global__ __launch_bounds__(256) void k_sft_rot(const orb_keypoint* __restrict__ k1, const orb_keypoint* __restrict__ k2,
                                                  int n1, int checkOri, int32_t* __restrict__ matches12,
-                                                 int32_t* __restrict__ nmatches) {
+                                                 int32_t* __restrict__ nmatches, int32_t* __restrict__ outMatches) {
     __shared__ int hcount[kHisto];
     __shared__ int ind[3], total;
     const int tid = threadIdx.x;
@@ -1661,14 +1661,14 @@ __global__ __launch_bounds__(256) void k_sft_rot(const orb_keypoint* __restrict_
     }
     __syncthreads();
     int kept = 0;
-    for (int i = tid; i < n1; i += 256) {
-        const int j = matches12[i];
-        if (j < 0) continue;
-        if (checkOri) {
+    for (int i = tid; i < n1; i += 256) {   // (outMatches: the final matches, host-mapped, every entry)
+        int j = matches12[i];
+        if (j >= 0 && checkOri) {
             const int bin = rot_bin(k1[i].angle - k2[j].angle);
-            if (bin != ind[0] && bin != ind[1] && bin != ind[2]) { matches12[i] = -1; continue; }
+            if (bin != ind[0] && bin != ind[1] && bin != ind[2]) { matches12[i] = -1; j = -1; }
         }
-        kept++;
+        if (outMatches) outMatches[i] = j;
+        kept += j >= 0 ? 1 : 0;
     }
     atomicAdd(&total, kept);
     __syncthreads();
@@ -2467,20 +2467,20 @@ int orb_search_for_triangulation(int device, const orb_frame_view* kf1, const or
     auto* dI1 = (int32_t*)sg.in(fidx1, (size_t)L1 * 4);
     auto* dI2 = (int32_t*)sg.in(fidx2, (size_t)L2 * 4);
     auto* dMt = (int32_t*)sg.in(matches12, (size_t)n1 * 4);
-    auto* dNm = (int32_t*)sg.out(4);
+    // the final matches and their count go straight into host-mapped memory (no copy back)
+    auto* hMt = (int32_t*)sg.out_host((size_t)n1 * 4);
+    auto* hNm = (int32_t*)sg.out_host(4);
+    if (sg.over) return ORB_EINTERNAL;
     if (int e_ = sg.upload_pull(s)) return e_;
     hipLaunchKernelGGL(k_sft, dim3((unsigned)common.size()), dim3(64), 0, s, dK1, dD1, kf1->uright ? dU1 : nullptr, dM1,
                        dK2, dD2, kf2->uright ? dU2 : nullptr, dM2, dN, dI1, dI2, P, dMt);
-    hipLaunchKernelGGL(k_sft_rot, dim3(1), dim3(256), 0, s, dK1, dK2, n1, check_ori ? 1 : 0, dMt, dNm);
+    hipLaunchKernelGGL(k_sft_rot, dim3(1), dim3(256), 0, s, dK1, dK2, n1, check_ori ? 1 : 0, dMt, hNm, hMt);
     int rc = hipGetLastError() == hipSuccess ? ORB_OK : ORB_EGPU;
     int nm = 0;
+    if (rc == ORB_OK && hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
     if (rc == ORB_OK) {
-        rc = sg.download(s, dMt);
-        if (rc == ORB_OK && hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
-        if (rc == ORB_OK) {
-            std::memcpy(matches12, sg.host(dMt), (size_t)n1 * 4);
-            nm = *sg.host(dNm);
-        }
+        std::memcpy(matches12, sg.host_out(hMt), (size_t)n1 * 4);
+        nm = *sg.host_out(hNm);
     }
     return rc == ORB_OK ? nm : rc;
 } ORB_ABI_CATCH
@@ -2542,20 +2542,19 @@ static int search_by_bow(int device, const orb_frame_view* v1, const uint8_t* ok
     auto* dI1 = (int32_t*)sg.in(fidx1, (size_t)L1 * 4);
     auto* dI2 = (int32_t*)sg.in(fidx2, (size_t)L2 * 4);
     auto* dMt = (int32_t*)sg.in(matches12, (size_t)n1 * 4);
-    auto* dNm = (int32_t*)sg.out(4);
+    auto* hMt = (int32_t*)sg.out_host((size_t)n1 * 4);   // final matches + count: host-mapped, no copy back
+    auto* hNm = (int32_t*)sg.out_host(4);
+    if (sg.over) return ORB_EINTERNAL;
     if (int e_ = sg.upload_pull(s)) return e_;
     hipLaunchKernelGGL(k_sbb, dim3((unsigned)common.size()), dim3(64), 0, s, dD1, dO1, dD2, ok2 ? dO2 : nullptr, dN,
                        dI1, dI2, thIncl, ratio, dMt);
-    hipLaunchKernelGGL(k_sft_rot, dim3(1), dim3(256), 0, s, dK1, dK2, n1, check_ori ? 1 : 0, dMt, dNm);
+    hipLaunchKernelGGL(k_sft_rot, dim3(1), dim3(256), 0, s, dK1, dK2, n1, check_ori ? 1 : 0, dMt, hNm, hMt);
     int rc = hipGetLastError() == hipSuccess ? ORB_OK : ORB_EGPU;
     int nm = 0;
+    if (rc == ORB_OK && hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
     if (rc == ORB_OK) {
-        rc = sg.download(s, dMt);
-        if (rc == ORB_OK && hipStreamSynchronize(s) != hipSuccess) rc = ORB_EGPU;
-        if (rc == ORB_OK) {
-            std::memcpy(matches12, sg.host(dMt), (size_t)n1 * 4);
-            nm = *sg.host(dNm);
-        }
+        std::memcpy(matches12, sg.host_out(hMt), (size_t)n1 * 4);
+        nm = *sg.host_out(hNm);
     }
     return rc == ORB_OK ? nm : rc;
 }
