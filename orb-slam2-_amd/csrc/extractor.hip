@@ -441,41 +441,47 @@ __device__ __forceinline__ void pyr_band_level(const LevelGeom& D, const LevelGe
         // shared with the previous output row — 1.2 source rows per output row instead of 2 — was
         // slower: one row of loads in flight instead of two rows' four)
         const __amdgpu_buffer_rsrc_t ro = buf_rsrc(out, (uint32_t)(D.pitch * (db.s0 + db.n)));
-        for (int r = rp; r < db.n; r += 4 * kPyrRows) {
+        // one thread iteration: output rows r, r + 4, .. (kPyrRows of them, clamped to the band) —
+        // their row coefficients and source dwords (fetch), then the sums and stores (compute)
+        struct Rows {
             int rr[kPyrRows];
             uint2 cy[kPyrRows];
+            uint32_t dd[kPyrRows][2][3];
+        };
+        auto fetch = [&](int r, Rows& f) {
 #pragma unroll
             for (int u = 0; u < kPyrRows; u++) {
-                rr[u] = min(r + 4 * u, db.n - 1);
-                cy[u] = YT[rr[u]];
+                f.rr[u] = min(r + 4 * u, db.n - 1);
+                f.cy[u] = YT[f.rr[u]];
             }
-            uint32_t hs[kPyrRows][2][4];   // [row u][source row 0/1][column]: horizontal sums
-            uint32_t dd[kPyrRows][2][3];
 #pragma unroll
             for (int u = 0; u < kPyrRows; u++) {
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
-                    const uint32_t sy = h ? (cy[u].x >> 16) : (cy[u].x & 0xFFFF);
+                    const uint32_t sy = h ? (f.cy[u].x >> 16) : (f.cy[u].x & 0xFFFF);
                     if (FromGlobal) {   // dword-aligned rows: the three dwords of the window (a dword
                                         // past the frame reads 0 and is never selected)
                         const int off = (int)__umul24(sy, (uint32_t)srcPitch) + 4 * dw;
-                        dd[u][h][0] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
-                        dd[u][h][1] = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 4, 0, 0);
-                        dd[u][h][2] = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 8, 0, 0);
+                        f.dd[u][h][0] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
+                        f.dd[u][h][1] = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 4, 0, 0);
+                        f.dd[u][h][2] = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 8, 0, 0);
                     } else {
                         const uint32_t* R = reinterpret_cast<const uint32_t*>(cur + __umul24(sy - (uint32_t)sb.s0, (uint32_t)sp)) + dw;
-                        dd[u][h][0] = R[0];
-                        dd[u][h][1] = R[1];
-                        dd[u][h][2] = R[2];
+                        f.dd[u][h][0] = R[0];
+                        f.dd[u][h][1] = R[1];
+                        f.dd[u][h][2] = R[2];
                     }
                 }
             }
+        };
+        auto compute = [&](int r, const Rows& f) {
+            uint32_t hs[kPyrRows][2][4];   // [row u][source row 0/1][column]: horizontal sums
 #pragma unroll
             for (int u = 0; u < kPyrRows; u++) {
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
-                    const uint32_t w0 = __builtin_amdgcn_alignbyte(dd[u][h][1], dd[u][h][0], sh);
-                    const uint32_t w1 = __builtin_amdgcn_alignbyte(dd[u][h][2], dd[u][h][1], sh);
+                    const uint32_t w0 = __builtin_amdgcn_alignbyte(f.dd[u][h][1], f.dd[u][h][0], sh);
+                    const uint32_t w1 = __builtin_amdgcn_alignbyte(f.dd[u][h][2], f.dd[u][h][1], sh);
 #pragma unroll
                     for (int j = 0; j < 4; j++)
                         hs[u][h][j] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(w1, w0, sel[j])),
@@ -489,15 +495,37 @@ __device__ __forceinline__ void pyr_band_level(const LevelGeom& D, const LevelGe
                 // and 4 b <= 8196 fit v_mad_u32_u24, the sum stays below 2^32 (255 * 2049^2 * 4 + 2^23)
                 // and its top byte never exceeds 255, so no shift and no clamp; two v_perm + one or
                 // pack the four
-                const uint32_t b0 = cy[u].y & 0xFFFF, b1 = cy[u].y >> 16;
+                const uint32_t b0 = f.cy[u].y & 0xFFFF, b1 = f.cy[u].y >> 16;
                 uint32_t v[4];
 #pragma unroll
                 for (int j = 0; j < 4; j++) v[j] = __umul24(hs[u][1][j], b1) + (__umul24(hs[u][0][j], b0) + (1u << 23));
                 if (u > 0 && r + 4 * u >= db.n) break;
                 const uint32_t pv = (__builtin_amdgcn_perm(v[1], v[0], 0x0c0c0703u) |
                                      __builtin_amdgcn_perm(v[3], v[2], 0x07030c0cu)) & keep;
-                *reinterpret_cast<uint32_t*>(nxt + rr[u] * dp + dx0) = pv;
-                __builtin_amdgcn_raw_buffer_store_b32(pv, ro, (int)__umul24((uint32_t)(db.s0 + rr[u]), (uint32_t)D.pitch) + dx0, 0, 0);
+                *reinterpret_cast<uint32_t*>(nxt + f.rr[u] * dp + dx0) = pv;
+                __builtin_amdgcn_raw_buffer_store_b32(pv, ro, (int)__umul24((uint32_t)(db.s0 + f.rr[u]), (uint32_t)D.pitch) + dx0, 0, 0);
+            }
+        };
+        constexpr int kStep = 4 * kPyrRows;
+        if (FromGlobal) {
+            // level 1 reads the caller's frame from L2 / HBM: the next iteration's rows are fetched
+            // before this one's are computed (two register sets in turn; a fetch past the band reads
+            // its last row again, unconditionally, so no load is exec-masked), so a thread waits one
+            // load latency per band instead of one per iteration
+            Rows fa, fb;
+            if (rp < db.n) fetch(rp, fa);
+            for (int r = rp; r < db.n; r += 2 * kStep) {
+                fetch(r + kStep, fb);
+                compute(r, fa);
+                if (r + kStep >= db.n) break;
+                fetch(r + 2 * kStep, fa);
+                compute(r + kStep, fb);
+            }
+        } else {
+            for (int r = rp; r < db.n; r += kStep) {
+                Rows f;
+                fetch(r, f);
+                compute(r, f);
             }
         }
     }
