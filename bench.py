@@ -1558,7 +1558,7 @@ def measure_pinned_copy(dev, mib=64, reps=10):
     return round(h2d, 2), round(d2h, 2)
 
 
-def _pcie_pipelined_leg(amd, dev, cv, W, H, NF, B, steps=16, warmup=4):
+def _pcie_pipelined_leg(amd, dev, cv, W, H, NF, B, steps=16, warmup=4, check=None):
     """The PCIe-inclusive path as a streaming host would run it, on three HIP streams: the copy
     stream uploads batch s+1's pinned frames (one H2D, into one of three device frame buffers)
     while two compute streams, one per batch parity with its own extractor and matcher handles,
@@ -1641,9 +1641,14 @@ def _pcie_pipelined_leg(amd, dev, cv, W, H, NF, B, steps=16, warmup=4):
 
     def consume(s):   # the host reads batch s's outputs: totals from the mapped offsets
         ev_done[s % NO].synchronize()
-        offs = np.ctypeslib.as_array(C.cast(outs[s % NO]["off"][0], C.POINTER(C.c_int32)), shape=(3, B + 1))
+        o = outs[s % NO]
+        offs = np.ctypeslib.as_array(C.cast(o["off"][0], C.POINTER(C.c_int32)), shape=(3, B + 1))
         n_kp, n_m = int(offs[0, B]), int(offs[2, B - 1]) if B > 1 else 0
         moved["d2h"] += n_kp * 60 + n_m * 4 + sizes["off"]
+        if check is not None:   # (tests: the packed host outputs of batch s against the reference)
+            view = lambda k, n, t: np.ctypeslib.as_array(C.cast(o[k][0], C.POINTER(t)), shape=(n,)).copy()  # noqa: E731
+            check(s, host_in[s % nb].numpy(), offs.copy(), view("pk", n_kp * 7, C.c_int32).reshape(-1, 7),
+                  view("pd", n_kp * 32, C.c_uint8).reshape(-1, 32), view("pm", max(n_m, 0), C.c_int32))
 
     def run(s0, n):
         for s in range(s0, s0 + n):

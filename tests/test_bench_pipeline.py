@@ -172,3 +172,42 @@ def test_bench_config5_batch_matches_oracle(amd, pairs):
         assert np.array_equal(ur[j, :nl], ur_ref), f"pair {pairs[j]}: mvuRight"
         assert np.array_equal(dep[j, :nl], dep_ref), f"pair {pairs[j]}: mvDepth"
         assert n_ref > 300
+
+
+def test_pcie_pipelined_leg_outputs_match_oracle(amd):
+    """bench.py's pipelined PCIe-inclusive leg (copy stream + two compute streams, results packed by
+    orb_pack_rows_device straight into host-mapped memory, three output sets in rotation): every
+    consumed batch's packed keypoints (all 7 fields), descriptors and matches12 equal the oracle's
+    ORBextractor::operator() and SearchForInitialization over the batch's in-batch pairs — the
+    events between the streams leave no race."""
+    bench = _bench()
+    from orb_slam2_amd import _abi, synth
+    W, H, NF, B = 640, 480, 1000, 8
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    cv = synth.canvas(0x5EED0002, W, H)
+    p = O.params(NF)
+    KP = _abi.KEYPOINT_DTYPE
+    seen = []
+
+    def check(s, frames, offs, kp, desc, m12):
+        with cf.ThreadPoolExecutor(min(16, os.cpu_count() or 1)) as ex:
+            refs = list(ex.map(lambda im: O.extract(p, im), list(frames)))
+        for b, ref in enumerate(refs):
+            a, e = int(offs[0, b]), int(offs[0, b + 1])
+            assert e - a == len(ref["kps"]), f"batch {s} frame {b}: {e - a} vs {len(ref['kps'])} keypoints"
+            assert kp[a:e].copy().view(KP).reshape(-1).tobytes() == ref["kps"].tobytes(), f"batch {s} frame {b}"
+            assert np.array_equal(desc[a:e], ref["desc"]), f"batch {s} frame {b}: descriptors"
+            assert int(offs[1, b]) == a
+        for q in range(B - 1):
+            r1, r2 = refs[q], refs[q + 1]
+            fa = O.FrameView(r1["kps"], r1["desc"], W, H)
+            fb = O.FrameView(r2["kps"], r2["desc"], W, H)
+            prev = np.stack([r1["kps"]["x"], r1["kps"]["y"]], 1).astype(np.float32).reshape(-1)
+            _, m_ref, _ = O.search_for_initialization(fa, fb, prev, nnratio=0.9, window=100)
+            a, e = int(offs[2, q]), int(offs[2, q + 1])
+            assert np.array_equal(m12[a:e], m_ref), f"batch {s} pair {q}: matches12"
+        seen.append(s)
+
+    r = bench._pcie_pipelined_leg(amd, dev, cv, W, H, NF, B, steps=5, warmup=2, check=check)
+    assert sorted(seen) == list(range(7)) and r["frames_per_s"] > 0
