@@ -110,13 +110,12 @@ struct LbaDev {
     // reduced per vertex
     double *Hll, *bl, *Dinv, *db, *Hpp, *bp;   // db = Dinv b_l
     double* Ae;                 // [pose-major position][18] Hpl_e D^-1 of the edge's landmark (per trial)
-    double* HplP;               // [pose-major position][18] Hpl_e (per trial, written with Ae)
     const int32_t* poPos;       // per act position: its index in the pose-major lists (-1: fixed pose)
     const int32_t* pairs;       // pose-pair blocks of S with shared landmarks, (bi << 16 | bj), bi <= bj
     const int32_t* npairs;      // their count; [1] / [2]: k_schur_pairs' workgroup / wave pairs (pairUnits)
     const int32_t* pairUnits;   // indices into pairs: [0, npairs[1]) one workgroup each, then npairs[2] one wave each
     const int32_t* tripStart;   // per listed pair: first entry of its shared-landmark list, count at +1
-    const int2* trips;          // (pose-major position of pose i's edge, of pose j's edge), landmark order
+    const int2* trips;          // (pose-major position of pose i's edge, act position of pose j's edge), landmark order
     double *S, *bs, *x;         // x: [6P + 3M]
     double* red;                // reduction scratch
     double *partChi, *partScale, *partMax;   // per-workgroup partials (single-process LM kernels)
@@ -813,8 +812,9 @@ __device__ __forceinline__ void dinv_store(const LbaDev& d, int l, const double 
 }
 // Hpl_e D^-1 (the product of G/core/block_solver.hpp:419) of every free-pose edge of landmark l,
 // edges a0, a0 + stride, ... of its list: formed once per edge and trial here, where D^-1 is in
-// registers, instead of once per pose pair in k_schur_pairs.  It and a copy of Hpl_e go to the
-// edge's pose-major position, so k_schur_pairs reads each pose's blocks as one contiguous run
+// registers, instead of once per pose pair in k_schur_pairs.  It goes to the edge's pose-major
+// position, so k_schur_pairs reads each pose's blocks as one contiguous run (the Hpl_e it pairs
+// them with are read in place: trips and poAct carry their act positions)
 __device__ __forceinline__ void hpl_dinv_edges(const LbaDev& d, int l, const double Di[9], int sub, int stride) {
     const int a1 = d.ptStart[l + 1];
     for (int a = d.ptStart[l] + sub; a < a1; a += stride) {
@@ -833,14 +833,9 @@ __device__ __forceinline__ void hpl_dinv_edges(const LbaDev& d, int l, const dou
 #pragma unroll
             for (int q = 0; q < 3; q++)
                 u[r * 3 + q] = __builtin_fma(w[r * 3 + 2], Di[6 + q], __builtin_fma(w[r * 3 + 1], Di[3 + q], w[r * 3] * Di[q]));
-        const size_t o = 18 * (size_t)d.poPos[k];
-        double2* U = reinterpret_cast<double2*>(d.Ae + o);
-        double2* H = reinterpret_cast<double2*>(d.HplP + o);
+        double2* U = reinterpret_cast<double2*>(d.Ae + 18 * (size_t)d.poPos[k]);
 #pragma unroll
-        for (int h = 0; h < 9; h++) {
-            U[h] = make_double2(u[2 * h], u[2 * h + 1]);
-            H[h] = make_double2(w[2 * h], w[2 * h + 1]);
-        }
+        for (int h = 0; h < 9; h++) U[h] = make_double2(u[2 * h], u[2 * h + 1]);
     }
 }
 
@@ -857,14 +852,9 @@ __device__ __forceinline__ void hpl_dinv_prefetched(const LbaDev& d, const doubl
             for (int q = 0; q < 3; q++)
                 v[r * 3 + q] = __builtin_fma(f.w[u][r * 3 + 2], Di[6 + q],
                                              __builtin_fma(f.w[u][r * 3 + 1], Di[3 + q], f.w[u][r * 3] * Di[q]));
-        const size_t o = 18 * (size_t)d.poPos[f.k[u]];
-        double2* U = reinterpret_cast<double2*>(d.Ae + o);
-        double2* H = reinterpret_cast<double2*>(d.HplP + o);
+        double2* U = reinterpret_cast<double2*>(d.Ae + 18 * (size_t)d.poPos[f.k[u]]);
 #pragma unroll
-        for (int h = 0; h < 9; h++) {
-            U[h] = make_double2(v[2 * h], v[2 * h + 1]);
-            H[h] = make_double2(f.w[u][2 * h], f.w[u][2 * h + 1]);
-        }
+        for (int h = 0; h < 9; h++) U[h] = make_double2(v[2 * h], v[2 * h + 1]);
     }
 }
 
@@ -1006,11 +996,11 @@ __device__ __forceinline__ void reduce_halve(double* cur, int lane) {
     }
 }
 
-// the product of one shared landmark: A_e1 against Hpl_e2 into acc[0 .. 36); diagonal blocks
-// (e2 == e1) also b_s's Hpl_e1 D^-1 b_l into acc[36 .. 42)
-__device__ __forceinline__ void sp_product(const LbaDev& d, double acc[64], int e1, int e2, int l, bool diag) {
+// the product of one shared landmark: A_e1 (pose-major position e1) against Hpl_k2 (act position
+// k2) into acc[0 .. 36); diagonal blocks (the same edge) also b_s's Hpl_e1 D^-1 b_l into acc[36 .. 42)
+__device__ __forceinline__ void sp_product(const LbaDev& d, double acc[64], int e1, int k2, int l, bool diag) {
     const double2* Ui = reinterpret_cast<const double2*>(d.Ae + 18 * (size_t)e1);
-    const double2* Bj = reinterpret_cast<const double2*>(d.HplP + 18 * (size_t)e2);
+    const double2* Bj = reinterpret_cast<const double2*>(d.Hpl_e + 18 * (size_t)k2);
     double v[18], u[18];
 #pragma unroll
     for (int h = 0; h < 9; h++) {
@@ -1096,7 +1086,7 @@ __global__ __launch_bounds__(kSpT) void k_schur_pairs(LbaDev d, int addDiag) {
         const bool diag = bi == bj;
         if (diag) {   // every edge of pose i pairs with itself: already a dense list
             const int a0 = d.poStart[bi], a1 = d.poStart[bi + 1];
-            for (int a = a0 + tid; a < a1; a += kSpT) sp_product(d, acc, a, a, d.poPt[a], true);
+            for (int a = a0 + tid; a < a1; a += kSpT) sp_product(d, acc, a, d.poAct[a], d.poPt[a], true);
         } else {
             // off-diagonal: the pair's shared landmarks, listed once per solve by k_pair_trip
             const int t0 = d.tripStart[2 * k], tn = d.tripStart[2 * k + 1];
@@ -1245,7 +1235,7 @@ __global__ __launch_bounds__(256) void k_po_pos(LbaDev d, int32_t* __restrict__ 
 }
 
 // Once per solve (the block structure is fixed for both optimize() rounds): every off-diagonal
-// pair's shared landmarks as (pose i's edge, pose j's edge) pose-major positions in pose i's
+// pair's shared landmarks as (pose i's edge's pose-major position, pose j's edge's act position) in pose i's
 // landmark order.  Four edges of pose i per thread are looked up in pose j's sorted landmark list (LDS up
 // to kSpList entries) and the matches compacted in thread order (a workgroup scan).
 __global__ __launch_bounds__(kSpT) void k_pair_trip(LbaDev d, int2* __restrict__ trips) {
@@ -1284,7 +1274,7 @@ __global__ __launch_bounds__(kSpT) void k_pair_trip(LbaDev d, int2* __restrict__
                 else hi = mid;
             }
             const bool hit = l >= 0 && lo < nb && Lj[lo] == l;
-            m2[u] = hit ? b0 + lo : -1;
+            m2[u] = hit ? d.poAct[b0 + lo] : -1;   // (pose j's edge by act position: Hpl_e in place)
             cnt += hit ? 1 : 0;
         }
         const int incl = wave_incl_scan_i32(cnt);
@@ -2751,8 +2741,37 @@ static bool use_ldlt_df(int n) {
 struct MwLdl {
     double *A, *rdg, *y, *yfin, *Ldg, *sink, *yb;   // yb: the backward substitution's working vector
     int* fail;
+    // the envelope (k_mw_envelope, once per solve; null: dense): per 16-row tile of the image, the
+    // first column any of its rows holds a non-zero in.  LDL^T keeps a row's leading zeros (L(r, p)
+    // = 0 for p < first(r): no fill-in outside the envelope), so a trailing tile, a panel's row
+    // group or a back-substitution row block whose operands all lie left of the envelope adds
+    // exact zeros and is skipped — a banded window (a corridor of keyframes) updates only its band
+    const int32_t* tfirst;
     int n, np;
 };
+
+// The envelope of the reduced matrix from the listed pose-pair blocks (the block pattern of
+// G/core/block_solver.hpp:192-207; block (i, j), i <= j): pose j's rows start at column
+// 6 min{i : (i, j) listed} (the diagonal is always listed), a padding row r at r.  One workgroup,
+// the per-pose minima in LDS (4 P bytes).
+__global__ __launch_bounds__(1024) void k_mw_envelope(const int32_t* __restrict__ pairs, const int32_t* __restrict__ npairs,
+                                                      int P, int np, int32_t* __restrict__ tfirst) {
+    extern __shared__ int32_t fpose[];
+    const int tid = threadIdx.x;
+    for (int j = tid; j < P; j += 1024) fpose[j] = j;
+    __syncthreads();
+    const int G = *npairs;
+    for (int k = tid; k < G; k += 1024) {
+        const int pr = pairs[k];
+        atomicMin(&fpose[pr & 0xFFFF], pr >> 16);
+    }
+    __syncthreads();
+    for (int T = tid; T < np / 16; T += 1024) {
+        int f = 16 * T;
+        for (int r = 16 * T; r < 16 * T + 16; r++) f = min(f, r < 6 * P ? 6 * fpose[r / 6] : r);
+        tfirst[T] = f;
+    }
+}
 constexpr int kMwWaves = 4;   // waves per workgroup of the panel / trailing kernels
 
 __device__ __forceinline__ void tri_index(int t, int& ti, int& tk) {   // t -> (ti, tk), tk <= ti, row-major
@@ -2779,6 +2798,23 @@ __global__ __launch_bounds__(256) void k_ldlt_mw_stage(MwLdl m, const double* __
     }
 }
 
+// With the envelope: row i of the lower triangle from its tile's first column (one workgroup per
+// row).  Nothing reads the image left of the envelope or its upper triangle before the panels
+// write W there, and the image is zeroed once per solve (build_pairs), so only this part changes
+// from trial to trial.
+__global__ __launch_bounds__(256) void k_ldlt_mw_stage_env(MwLdl m, const double* __restrict__ S, const double* __restrict__ b,
+                                                          const LmState* st) {
+    if (lm_off(st, 1)) return;
+    const int np = m.np, n = m.n, i = blockIdx.x;
+    if (i == 0 && threadIdx.x == 0) *m.fail = 0;
+    for (int j = m.tfirst[i >> 4] + (int)threadIdx.x; j <= i; j += 256)
+        m.A[(size_t)i * np + j] = (i < n && j < n) ? S[(size_t)i * n + j] : (i == j ? 1.0 : 0.0);
+    if (threadIdx.x == 0) {
+        m.y[i] = i < n ? b[i] : 0.0;
+        if (i >= n) m.rdg[i] = 1.0;
+    }
+}
+
 // Panel jb of the multi-workgroup factorisation, kMwNB columns wide (twice k_ldlt_solve's: half
 // the launches and half the passes of the trailing update over the matrix).  Lanes 0..kMwNB-1 of
 // every wave hold the panel's diagonal rows, lanes kMwNB..63 its own rows below (group g: rows
@@ -2788,25 +2824,26 @@ __host__ __device__ __forceinline__ int mw_groups(int np, int jb) {
     const int g = (np - jb - kMwNB + (64 - kMwNB) - 1) / (64 - kMwNB);
     return g > 1 ? g : 1;
 }
+// row group g of panel jb runs (group 0 always: it holds the diagonal block's results)
+__device__ __forceinline__ bool mw_group_live(const MwLdl& m, int jb, int g) {
+    constexpr int NB = kMwNB, RB = 64 - kMwNB;
+    if (g > 0 && jb + NB + RB * g >= m.np) return false;   // no rows below for this group
+    if (g > 0 && m.tfirst) {   // the group's 32 rows have no non-zero in the panel's columns
+        const int T0 = (jb + NB + RB * g) >> 4;
+        if (min(m.tfirst[T0], m.tfirst[T0 + 1]) > jb + NB - 1) return false;
+    }
+    return true;
+}
+// the panel's column recurrence for the wave's rows (lane < NB: diagonal row jb + lane; else row
+// jb + NB + RB g + lane - NB), P = the rows' panel columns after every earlier update, Y = y(row)
 template <bool kTail>
-__global__ __launch_bounds__(64 * kMwWaves) void k_ldlt_mw_panel(MwLdl m, int jb, const LmState* st) {
+__device__ __forceinline__ void mw_panel_core(const MwLdl& m, int jb, int g, int lane, double (&P)[kMwNB], double Y,
+                                              double* const wsc) {
     constexpr int NB = kMwNB, RB = 64 - kMwNB;   // diagonal lanes, rows below per wave
-    if (lm_off(st, 1)) return;
-    if (__builtin_amdgcn_readfirstlane(*m.fail)) return;
-    __shared__ double wscS[kMwWaves][NB];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int g = __builtin_amdgcn_readfirstlane((int)blockIdx.x * kMwWaves + wv);
     const int np = m.np, ld = np, nr = m.n;
-    if (g > 0 && jb + NB + RB * g >= np) return;   // no rows below for this group (group 0 always runs)
     double* const A = m.A;
-    double* const wsc = wscS[wv];
     const int r = lane < NB ? jb + lane : jb + NB + RB * g + (lane - NB);
     const bool live = r < np, inplace = live && lane >= NB;
-    const int rc = min(r, np - 1);
-    double P[NB];
-    double Y = m.y[rc];
-#pragma unroll
-    for (int c = 0; c < NB; c++) P[c] = A[(size_t)rc * ld + jb + c];
     double* const Lrow = inplace ? A + (size_t)r * ld + jb : m.sink + (size_t)(lane & (NB - 1)) * ld;
     double* const Wcol = inplace ? A + (size_t)jb * ld + r : m.sink + lane;
     double* const wst = lane < NB ? wsc + lane : m.sink + lane;
@@ -2865,21 +2902,31 @@ __global__ __launch_bounds__(64 * kMwWaves) void k_ldlt_mw_panel(MwLdl m, int jb
     }
     if (inplace) m.y[r] = Y;
 }
-
-// trailing update after the panel at column block kb (kMwNB wide): 16 x 16 tiles (I, K) of the
-// lower triangle beyond it, one per wave, kMwNB / 4 v_mfma_f64_16x16x4 each
-__global__ __launch_bounds__(64 * kMwWaves) void k_ldlt_mw_trail(MwLdl m, int kb, const LmState* st) {
+template <bool kTail>
+__global__ __launch_bounds__(64 * kMwWaves) void k_ldlt_mw_panel(MwLdl m, int jb, const LmState* st) {
+    constexpr int NB = kMwNB, RB = 64 - kMwNB;
     if (lm_off(st, 1)) return;
     if (__builtin_amdgcn_readfirstlane(*m.fail)) return;
-    const int lane = threadIdx.x & 63;
-    const int jb = kb * kMwNB, t0 = (jb + kMwNB) / 16, T = m.np / 16, mm = T - t0;
-    const int t = __builtin_amdgcn_readfirstlane((int)blockIdx.x * kMwWaves + (int)(threadIdx.x >> 6));
-    if (t >= mm * (mm + 1) / 2) return;
-    int ti, tk;
-    tri_index(t, ti, tk);
-    const int I0 = (t0 + ti) * 16, K0 = (t0 + tk) * 16, ld = m.np;
+    __shared__ double wscS[kMwWaves][NB];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int g = __builtin_amdgcn_readfirstlane((int)blockIdx.x * kMwWaves + wv);
+    if (!mw_group_live(m, jb, g)) return;
+    const int np = m.np, ld = np;
+    const int r = lane < NB ? jb + lane : jb + NB + RB * g + (lane - NB);
+    const int rc = min(r, np - 1);
+    double P[NB];
+    const double Y = m.y[rc];
+#pragma unroll
+    for (int c = 0; c < NB; c++) P[c] = m.A[(size_t)rc * ld + jb + c];
+    mw_panel_core<kTail>(m, jb, g, lane, P, Y, wscS[wv]);
+}
+
+// one 16 x 16 tile (I0, K0) of the trailing update after the panel at column jb:
+// A(I0.., K0..) - W(I0.., panel) L(K0.., panel)^T, kMwNB / 4 v_mfma_f64_16x16x4; lane (li, lk)
+// returns rows I0 + lk + 4 q of column K0 + li
+__device__ __forceinline__ dbl4 mw_tile(const MwLdl& m, int jb, int I0, int K0, int lane) {
+    const int ld = m.np, li = lane & 15, lk = lane >> 4;
     const double* __restrict__ A = m.A;
-    const int li = lane & 15, lk = lane >> 4;
     double a[kMwNB / 4], bb[kMwNB / 4];
     dbl4 acc;
 #pragma unroll
@@ -2892,8 +2939,117 @@ __global__ __launch_bounds__(64 * kMwWaves) void k_ldlt_mw_trail(MwLdl m, int kb
     for (int q = 0; q < 4; q++) acc[q] = A[(size_t)(I0 + lk + 4 * q) * ld + K0 + li];
 #pragma unroll
     for (int s = 0; s < kMwNB / 4; s++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], bb[s], acc, 0, 0, 0);
+    return acc;
+}
+// outside the envelope W(I, panel) or L(K, panel) is all zeros: the tile's update adds nothing
+__device__ __forceinline__ bool mw_tile_live(const MwLdl& m, int jb, int I, int K) {
+    return !m.tfirst || max(m.tfirst[I], m.tfirst[K]) <= jb + kMwNB - 1;
+}
+
+// trailing update after the panel at column block kb (kMwNB wide): 16 x 16 tiles (I, K) of the
+// lower triangle beyond it, one per wave (tile rows / columns from tBase: k_ldlt_mw_step's
+// trailing part starts two tile columns later)
+__device__ __forceinline__ void mw_trail_tile(const MwLdl& m, int jb, int tBase, int t, int lane) {
+    const int T = m.np / 16, mm = T - tBase;
+    if (mm <= 0 || t >= mm * (mm + 1) / 2) return;
+    int ti, tk;
+    tri_index(t, ti, tk);
+    if (!mw_tile_live(m, jb, tBase + ti, tBase + tk)) return;
+    const int I0 = (tBase + ti) * 16, K0 = (tBase + tk) * 16, ld = m.np;
+    const int li = lane & 15, lk = lane >> 4;
+    const dbl4 acc = mw_tile(m, jb, I0, K0, lane);
 #pragma unroll
     for (int q = 0; q < 4; q++) m.A[(size_t)(I0 + lk + 4 * q) * ld + K0 + li] = acc[q];
+}
+__global__ __launch_bounds__(64 * kMwWaves) void k_ldlt_mw_trail(MwLdl m, int kb, const LmState* st) {
+    if (lm_off(st, 1)) return;
+    if (__builtin_amdgcn_readfirstlane(*m.fail)) return;
+    const int jb = kb * kMwNB;
+    const int t = __builtin_amdgcn_readfirstlane((int)blockIdx.x * kMwWaves + (int)(threadIdx.x >> 6));
+    mw_trail_tile(m, jb, (jb + kMwNB) / 16, t, threadIdx.x & 63);
+}
+
+// LDS-only workgroup barrier: orders the workgroup's LDS accesses and leaves its global loads in
+// flight (a plain __syncthreads waits for every outstanding load, prefetches included)
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// Panel kb's trailing update and panel kb + 1's factorisation in one launch (one kernel boundary
+// per panel instead of two).  Workgroup g < nPanelWg takes panel kb + 1's row group g: its four
+// waves form the two tile columns of the next panel for the group's 64 rows (the diagonal block's
+// three lower tiles and the group's own four, two per wave, all loads of a wave in flight at once)
+// with the same v_mfma sequence as the trailing tiles, into a 64 x 33 LDS image, and wave 0 runs
+// the column recurrence on them; the other workgroups update the tiles right of those two columns
+// in place.  Neither part reads what the other writes (the next panel's tile columns are read only
+// by the workgroups that factor them; its L and W land left of and above the trailing tiles), and
+// the panel's values are bitwise those the separate trailing launch would have stored.
+template <bool kTail>
+__global__ __launch_bounds__(64 * kMwWaves) void k_ldlt_mw_step(MwLdl m, int kb, int nPanelWg, const LmState* st) {
+    constexpr int NB = kMwNB, RB = 64 - kMwNB;
+    if (lm_off(st, 1)) return;
+    if (__builtin_amdgcn_readfirstlane(*m.fail)) return;
+    __shared__ double wscS[NB];
+    __shared__ double tileS[64][NB + 1];   // rows: the diagonal block's 32, then the group's 32
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int jb = kb * NB, jn = jb + NB, t0 = jn / 16;
+    if ((int)blockIdx.x >= nPanelWg) {
+        const int t = __builtin_amdgcn_readfirstlane(((int)blockIdx.x - nPanelWg) * kMwWaves + wv);
+        mw_trail_tile(m, jb, t0 + 2, t, lane);
+        return;
+    }
+    const int g = blockIdx.x;
+    if (!mw_group_live(m, jn, g)) return;
+    const int np = m.np, ld = np;
+    const bool below = jn + NB + RB * g < np;   // (group 0 of the last panel has no rows below)
+    const int Ig = (jn + NB + RB * g) >> 4;
+    // tile s of 7: 0..2 the diagonal block's (t0, t0), (t0 + 1, t0), (t0 + 1, t0 + 1); 3..6 the
+    // group's (Ig + u, t0 + v); formed iff live (outside the envelope the update adds nothing)
+    auto tile_of = [&](int s, int& I, int& K, int& row0) {
+        if (s < 3) { I = t0 + (s > 0 ? 1 : 0); K = t0 + (s == 2 ? 1 : 0); row0 = 16 * (I - t0); }
+        else { I = Ig + ((s - 3) >> 1); K = t0 + ((s - 3) & 1); row0 = 32 + 16 * ((s - 3) >> 1); }
+    };
+    auto tile_on = [&](int s) {
+        if (s >= 7 || (s >= 3 && !below)) return false;
+        int I, K, row0;
+        tile_of(s, I, K, row0);
+        return mw_tile_live(m, jb, I, K);
+    };
+    const int li = lane & 15, lk = lane >> 4;
+    double P[NB];
+    double Y = 0.0;
+    if (wv == 0) {   // the recurrence wave's raw rows, in flight with the tiles' loads
+        const int r = lane < NB ? jn + lane : jn + NB + RB * g + (lane - NB);
+        const int rc = min(r, np - 1);
+        Y = m.y[rc];
+#pragma unroll
+        for (int c = 0; c < NB; c++) P[c] = m.A[(size_t)rc * ld + jn + c];   // (tiles not formed: as stored)
+    }
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const int s = wv + kMwWaves * k;
+        if (!tile_on(s)) continue;
+        int I, K, row0;
+        tile_of(s, I, K, row0);
+        const dbl4 acc = mw_tile(m, jb, 16 * I, 16 * K, lane);
+#pragma unroll
+        for (int q = 0; q < 4; q++) tileS[row0 + lk + 4 * q][16 * (K - t0) + li] = acc[q];
+    }
+    lds_barrier();
+    if (wv != 0) return;
+    {
+        const int u = lane >> 4;   // this lane's tile row: 0, 1 the diagonal block, 2, 3 the group's
+#pragma unroll
+        for (int v = 0; v < 2; v++) {
+            const int s = u == 0 ? (v == 0 ? 0 : 7) : u == 1 ? 1 + v : 3 + 2 * (u - 2) + v;   // (0, 1): upper, as stored
+            if (!tile_on(s)) continue;
+#pragma unroll
+            for (int c = 0; c < 16; c++) P[16 * v + c] = tileS[lane][16 * v + c];
+        }
+    }
+    mw_panel_core<kTail>(m, jn, g, lane, P, Y, wscS);
 }
 
 // The backward substitution x = L^-T (y / d) in super-blocks of kSB rows from the bottom, two
@@ -2999,6 +3155,11 @@ __global__ __launch_bounds__(256) void k_ldlt_mw_bupd(MwLdl m, int K0, const dou
     __shared__ double part[4][64];
     const int np = m.np, n = m.n, ld = np, nsb = min(kSB, np - K0);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (m.tfirst) {   // rows left of every super-block row's envelope: L(K0 + c, i) = 0
+        int f = K0;
+        for (int T = K0 >> 4; T < (K0 + nsb) >> 4; T++) f = min(f, m.tfirst[T]);
+        if ((int)blockIdx.x * 64 + 63 < f) return;
+    }
     for (int c = threadIdx.x; c < kSB; c += 256) xs[c] = c < nsb && K0 + c < n ? x[K0 + c] : 0.0;
     __syncthreads();
     const int i = blockIdx.x * 64 + lane;
@@ -3018,21 +3179,189 @@ __global__ __launch_bounds__(256) void k_ldlt_mw_bupd(MwLdl m, int K0, const dou
     if (w == 0 && i < K0) m.yb[i] = m.yb[i] + ((part[3][lane] + part[2][lane]) + (part[1][lane] + part[0][lane]));
 }
 
+// The whole backward substitution in one launch (one workgroup, np <= kMwBackMaxN): the working
+// vector y / d lives in LDS and the super-blocks go bottom-up as k_ldlt_mw_bsolve /
+// k_ldlt_mw_bupd take them, with the same arithmetic (the 32-row chains, and each row update's
+// four column-quarter partials added in the same order), so x is bitwise theirs; the next
+// super-block's L triangle is loaded into registers while this one's chain runs, and rows left of
+// a super-block's envelope take no update (their terms are exact zeros).  2 (np / kSB) - 1
+// dependent launches become one.
+constexpr int kMwBackMaxN = 2048;   // LDS: the 128 x 129 triangle + 64 + np doubles (148 KB at 2048)
+__global__ __launch_bounds__(512) void k_ldlt_mw_back(MwLdl m, double* __restrict__ x, int* __restrict__ flags,
+                                                      const LmState* st, PoseTail ptail) {
+    if (lm_off(st, 1)) return;
+    extern __shared__ __attribute__((aligned(16))) double bsm[];
+    double* const Ls = bsm;                       // [kSB][kSB + 1]: L(K0 + r, K0 + c), c < r (+ 64 spare)
+    double* const yb = Ls + kSB * (kSB + 1) + 64; // [np]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int np = m.np, n = m.n, ld = np;
+    if (__builtin_amdgcn_readfirstlane(*m.fail)) {   // as k_ldlt_mw_bsolve: the trial is rejected
+        if (tid == 0) flags[0] = 1;
+        if (ptail.scaleOut && wave == 0) pose_tail(ptail, x, st->lambda, lane);
+        return;
+    }
+    for (int i = tid; i < np; i += 512) yb[i] = m.yfin[i] * m.rdg[i];
+    // each super-block's envelope start: the least tile start of its rows (kSB / 16 tiles)
+    __shared__ int sLo[kMwBackMaxN / kSB];
+    if (tid < (np + kSB - 1) / kSB) {
+        const int K0 = tid * kSB, nsb = min(kSB, np - K0);
+        int lo = 0;
+        if (m.tfirst) {
+            lo = K0;
+            for (int T = K0 >> 4; T < (K0 + nsb) >> 4; T++) lo = min(lo, m.tfirst[T]);
+        }
+        sLo[tid] = lo;
+    }
+    TSTAMP(tb0);
+    long long tStage = 0, tChain = 0, tUpd = 0, tComb = 0;
+    (void)tStage; (void)tChain; (void)tUpd; (void)tComb;
+    constexpr int kPer = (kSB * (kSB - 1) / 2 + 511) / 512, kTri = kSB * (kSB - 1) / 2;
+    // this thread's entries (r, c) of a full super-block's strict lower triangle, row-major (a
+    // partial one, nsb rows, takes the entries with r < nsb: the first nsb (nsb - 1) / 2, as
+    // k_ldlt_mw_bsolve stages it); found once, not per super-block
+    int rcP[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        int r, c;
+        tri_index(min(tid + 512 * k, kTri - 1), r, c);
+        rcP[k] = tid + 512 * k < kTri ? ((r + 1) << 8) | c : -1;
+    }
+    double v[kPer];
+    int at[kPer];
+    auto load_tri = [&](int K0) {   // the super-block's strict lower triangle of L, branch-free
+        const int nsb = min(kSB, np - K0);
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const int r = rcP[k] >> 8, c = rcP[k] & 0xFF;
+            const bool ok = rcP[k] >= 0 && r < nsb;
+            const int rr = ok ? r : 1, cc = ok ? c : 0;
+            const double* pL = m.Ldg + (size_t)(K0 + rr) * kMwNB + (cc & (kMwNB - 1));   // (K0: a multiple of kMwNB)
+            const double* pA = m.A + (size_t)(K0 + rr) * ld + K0 + cc;
+            v[k] = *((rr >> 5) == (cc >> 5) ? pL : pA);   // a panel's diagonal block: from Ldg
+            at[k] = ok ? rr * (kSB + 1) + cc : kSB * (kSB + 1) + lane;
+        }
+    };
+    const int nsbk = (np + kSB - 1) / kSB;
+    load_tri((nsbk - 1) * kSB);
+    for (int q = nsbk - 1; q >= 0; q--) {
+        const int K0 = q * kSB, nsb = min(kSB, np - K0);
+        TSTAMP(tq0);
+        lds_barrier();   // the previous super-block is done with Ls (and the partials aliasing it)
+#pragma unroll
+        for (int k = 0; k < kPer; k++) Ls[at[k]] = v[k];
+        if (q > 0) load_tri(K0 - kSB);   // in flight during this super-block's chain
+        lds_barrier();
+        TACC(tStage, tq0);
+        TSTAMP(tq1);
+        double* const ysb = yb + K0;
+        constexpr int kBB = 32;
+        for (int jb = nsb - kBB; jb >= 0; jb -= kBB) {
+            if (wave == 0) {
+                const int r = lane & (kBB - 1);
+                double Lb[kBB];
+#pragma unroll
+                for (int c = 1; c < kBB; c++) Lb[c] = Ls[(jb + c) * (kSB + 1) + jb + min(r, c - 1)];
+                double xb = ysb[jb + r];
+#pragma unroll
+                for (int c = kBB - 1; c > 0; c--) {
+                    const double xc = shfl_d(xb, c);
+                    xb = r < c ? __builtin_fma(-Lb[c], xc, xb) : xb;
+                }
+                if (lane < kBB) ysb[jb + r] = xb;
+            }
+            lds_barrier();
+            for (int i = tid; i < jb; i += 512) {
+                double w4[4] = {ysb[i], 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int c = kBB - 1; c >= 0; c--)
+                    w4[c & 3] = __builtin_fma(-Ls[(jb + c) * (kSB + 1) + i], ysb[jb + c], w4[c & 3]);
+                ysb[i] = (w4[0] + w4[1]) + (w4[2] + w4[3]);
+            }
+            lds_barrier();
+        }
+        for (int r = tid; r < nsb; r += 512)
+            if (K0 + r < n) x[K0 + r] = ysb[r];
+        TACC(tChain, tq1);
+        if (q == 0) break;
+        TSTAMP(tq2);
+        // the rows above: k_ldlt_mw_bupd's four column quarters (x of the padding rows as 0), each
+        // (quarter, row) a task with its 32 loads in flight, the partials through LDS (aliasing the
+        // triangle, whose chain is done) and added in bupd's order
+        const int lo = sLo[q];
+        constexpr int kC = kSB / 4;
+        const int R = (K0 - lo + 63) & ~63;
+        double* const part = Ls;   // [4][R]
+        for (int t = tid; t < 4 * R; t += 512) {
+            const int w = t / R, i = lo + t % R;
+            if (i >= K0) continue;
+            double a[kC];
+#pragma unroll
+            for (int k = 0; k < kC; k++) {   // (loads at clamped rows, unconditional)
+                const int c = kC * w + k;
+                const double t2 = m.A[(size_t)(K0 + min(c, nsb - 1)) * ld + i];
+                a[k] = c < nsb ? t2 : 0.0;
+            }
+            double acc = 0.0;
+#pragma unroll
+            for (int k = kC - 1; k >= 0; k--) {
+                const int c = kC * w + k;
+                acc = __builtin_fma(-a[k], c < nsb && K0 + c < n ? ysb[c] : 0.0, acc);
+            }
+            part[w * R + (i - lo)] = acc;
+        }
+        lds_barrier();
+        TACC(tUpd, tq2);
+        TSTAMP(tq3);
+        for (int i = lo + tid; i < K0; i += 512) {
+            const int o = i - lo;
+            yb[i] = yb[i] + ((part[3 * R + o] + part[2 * R + o]) + (part[R + o] + part[o]));
+        }
+        TACC(tComb, tq3);
+    }
+#ifdef ORB_TIMING
+    if (tid == 0)
+        printf("mw back np %d: total %lld stage %lld chain %lld update %lld combine %lld\n", np, clock64() - tb0, tStage, tChain,
+               tUpd, tComb);
+#endif
+    if (tid == 0) flags[0] = 0;
+    if (ptail.scaleOut) {   // x as stored by this workgroup (visible after the barrier)
+        __syncthreads();
+        if (wave == 0) pose_tail(ptail, x, st->lambda, lane);
+    }
+}
+
 // enqueue the multi-workgroup solve of S x = b (n = order of S) on s
 static void enqueue_ldlt_mw(hipStream_t s, const MwLdl& m, const double* S, const double* b, double* x, int* flags,
                             const LmState* st, const PoseTail& pt) {
     const int np = m.np, T = np / kMwNB;
     const size_t tot = (size_t)np * np;
-    hipLaunchKernelGGL(k_ldlt_mw_stage, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, m, S, b, st);
+    if (m.tfirst) hipLaunchKernelGGL(k_ldlt_mw_stage_env, dim3((unsigned)np), dim3(256), 0, s, m, S, b, st);
+    else hipLaunchKernelGGL(k_ldlt_mw_stage, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, m, S, b, st);
+    // ORB_LBA_MW_SPLIT=1: a panel launch and a trailing launch per panel (A/B runs)
+    const bool split = std::getenv("ORB_LBA_MW_SPLIT") != nullptr;
+    auto wgs = [](int n) { return (n + kMwWaves - 1) / kMwWaves; };
     for (int kb = 0; kb < T; kb++) {
-        const int jb = kb * kMwNB, groups = mw_groups(np, jb);
-        const dim3 gp((unsigned)((groups + kMwWaves - 1) / kMwWaves));
-        if (jb + kMwNB > m.n) hipLaunchKernelGGL(k_ldlt_mw_panel<true>, gp, dim3(64 * kMwWaves), 0, s, m, jb, st);
-        else hipLaunchKernelGGL(k_ldlt_mw_panel<false>, gp, dim3(64 * kMwWaves), 0, s, m, jb, st);
+        const int jb = kb * kMwNB;
+        if (kb == 0 || split) {
+            const dim3 gp((unsigned)wgs(mw_groups(np, jb)));
+            if (jb + kMwNB > m.n) hipLaunchKernelGGL(k_ldlt_mw_panel<true>, gp, dim3(64 * kMwWaves), 0, s, m, jb, st);
+            else hipLaunchKernelGGL(k_ldlt_mw_panel<false>, gp, dim3(64 * kMwWaves), 0, s, m, jb, st);
+        }
         const int mm = np / 16 - (jb + kMwNB) / 16, tiles = mm * (mm + 1) / 2;
-        if (tiles > 0)
-            hipLaunchKernelGGL(k_ldlt_mw_trail, dim3((unsigned)((tiles + kMwWaves - 1) / kMwWaves)), dim3(64 * kMwWaves),
-                               0, s, m, kb, st);
+        if (tiles <= 0) continue;
+        if (split) {
+            hipLaunchKernelGGL(k_ldlt_mw_trail, dim3((unsigned)wgs(tiles)), dim3(64 * kMwWaves), 0, s, m, kb, st);
+            continue;
+        }
+        // this panel's trailing update with the next panel's factorisation
+        const int jn = jb + kMwNB, pw = mw_groups(np, jn), mr = mm - 2, rest = mr > 0 ? mr * (mr + 1) / 2 : 0;
+        const dim3 gs((unsigned)(pw + wgs(rest)));
+        if (jn + kMwNB > m.n) hipLaunchKernelGGL(k_ldlt_mw_step<true>, gs, dim3(64 * kMwWaves), 0, s, m, kb, pw, st);
+        else hipLaunchKernelGGL(k_ldlt_mw_step<false>, gs, dim3(64 * kMwWaves), 0, s, m, kb, pw, st);
+    }
+    if (np <= kMwBackMaxN && !split) {
+        hipLaunchKernelGGL(k_ldlt_mw_back, dim3(1), dim3(512), ((size_t)kSB * (kSB + 1) + 64 + np) * 8, s, m, x, flags, st, pt);
+        return;
     }
     const int nsbk = (np + kSB - 1) / kSB;
     for (int q = nsbk - 1; q >= 0; q--) {
@@ -4365,7 +4694,7 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
     TRY(dalloc(c, &d.Hpl_e, 18 * (size_t)NE)); TRY(dalloc(c, &d.bl_e, 3 * (size_t)NE));
     TRY(dalloc(c, &d.bp_e, 6 * (size_t)NE));
     TRY(dalloc(c, &d.echi, (size_t)NE + 6 * (size_t)NP + 3 * (size_t)NM));
-    TRY(dalloc(c, &d.Ae, 18 * (size_t)NE)); TRY(dalloc(c, &d.HplP, 18 * (size_t)NE));
+    TRY(dalloc(c, &d.Ae, 18 * (size_t)NE));
     TRY(dalloc(c, &d.Hll, 9 * (size_t)NM)); TRY(dalloc(c, &d.bl, 3 * (size_t)NM)); TRY(dalloc(c, &d.Dinv, 9 * (size_t)NM));
     TRY(dalloc(c, &d.db, 3 * (size_t)NM));
     TRY(dalloc(c, &d.Hpp, 36 * (size_t)NP)); TRY(dalloc(c, &d.bp, 6 * (size_t)NP));
@@ -4660,7 +4989,7 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
                 return ORB_OK;
             struct {
                 LbaDev d;
-                const void* ptrs[4];
+                const void* ptrs[5];
                 double h[2];
                 int v[8];
                 orbamd::GrpDev grp;   // a group's exchange pointers (zero without one)
@@ -4669,11 +4998,13 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
             k.d = d;
             if (c->grp) k.grp = *c->grp;
             k.ptrs[0] = d_freePoses; k.ptrs[1] = d_trace; k.ptrs[2] = d_ldlw ? (const void*)d_ldlw : (const void*)mwBase.A; k.ptrs[3] = s;
+            k.ptrs[4] = mwBase.tfirst;
             k.h[0] = hm; k.h[1] = hsv;
             k.v[0] = iterations; k.v[1] = maxTrials; k.v[2] = o->fixed_iterations; k.v[3] = root; k.v[4] = nslots;
             k.v[5] = firstGroup ? 1 : 0;
             k.v[6] = close ? 1 : 0;
-            k.v[7] = (schurMfma ? 1 : 0) | (std::getenv("ORB_LBA_EXTRA_BOUNDARY") ? 2 : 0);
+            k.v[7] = (schurMfma ? 1 : 0) | (std::getenv("ORB_LBA_EXTRA_BOUNDARY") ? 2 : 0) |
+                     (std::getenv("ORB_LBA_MW_SPLIT") ? 4 : 0);
             std::vector<char> key(reinterpret_cast<const char*>(&k), reinterpret_cast<const char*>(&k) + sizeof(k));
             for (size_t i = 0; i < c->graphs.size(); i++)
                 if (c->graphs[i].key == key) {   // most recently used last: eviction takes the front
@@ -4858,6 +5189,16 @@ static int lba_run(lba_context* c, const lba_problem* p, const lba_options* o, c
             d.npairs = npairs;
             d.tripStart = tripStart;
             hipLaunchKernelGGL(k_pair_trip, dim3(np2), dim3(kSpT), 0, s, d, trips);
+            // the multi-workgroup solve's envelope (ORB_LBA_MW_DENSE=1: the dense passes, A/B runs)
+            mwBase.tfirst = nullptr;
+            if (mwBase.A && P <= 16384 && !std::getenv("ORB_LBA_MW_DENSE")) {
+                const int npm = (6 * P + kMwNB - 1) & ~(kMwNB - 1);
+                int32_t* tf = nullptr;
+                TRY(dalloc(c, &tf, npm / 16));
+                hipLaunchKernelGGL(k_mw_envelope, dim3(1), dim3(1024), 4 * (size_t)P, s, pairs, npairs, P, npm, tf);
+                ORB_HIP_TRY(hipMemsetAsync(mwBase.A, 0, 8 * (size_t)npm * npm, s));   // (k_ldlt_mw_stage_env)
+                mwBase.tfirst = tf;
+            }
             ORB_HIP_TRY(hipGetLastError());
             if (c->world > 1) {
                 // the packed exchange carries the first gPairs blocks of d.pairs: the device's list

@@ -314,6 +314,40 @@ def test_scaled_local_ba_bitwise_reproducible(amd):
             assert np.array_equal(r[k], runs[0][k]), k
 
 
+@pytest.mark.parametrize("shuffle", [False, True])
+def test_mw_envelope_bitwise_matches_dense(amd, monkeypatch, shuffle):
+    """The multi-workgroup LDL^T skips the trailing tiles, panel row groups and back-substitution
+    row blocks left of the reduced matrix's envelope (k_mw_envelope), and runs each panel's
+    trailing update with the next panel's factorisation in one launch (k_ldlt_mw_step).  The
+    skipped work adds exact zeros and the fused panel forms the same MFMA tiles, so the solve is
+    bitwise the dense two-launch passes' (ORB_LBA_MW_DENSE=1 ORB_LBA_MW_SPLIT=1) and the envelope's
+    alone (ORB_LBA_MW_SPLIT=1) — on the corridor's band and on the same window with its keyframes
+    in shuffled order (an irregular envelope), which also stays within the oracle's tolerances."""
+    from orb_slam2_amd import synth
+    pb = synth.ba_problem_corridor(n_local=40, n_fixed=2, n_points=4000, seed=26, stereo_frac=0.2)
+    if shuffle:
+        rng = np.random.default_rng(3)
+        nk = len(pb["Tcw"])
+        perm = rng.permutation(nk)
+        inv = np.empty(nk, np.int64)
+        inv[perm] = np.arange(nk)
+        pb = dict(pb, Tcw=pb["Tcw"][perm], pose_fixed=pb["pose_fixed"][perm],
+                  pose_id=np.arange(nk, dtype=np.int64), edge_pose=inv[pb["edge_pose"]].astype(np.int32))
+    monkeypatch.setenv("ORB_LBA_MW_DENSE", "1")
+    monkeypatch.setenv("ORB_LBA_MW_SPLIT", "1")
+    dense = amd.LocalBA().solve(pb)
+    monkeypatch.delenv("ORB_LBA_MW_DENSE")
+    envelope = amd.LocalBA().solve(pb)
+    monkeypatch.delenv("ORB_LBA_MW_SPLIT")
+    fused = amd.LocalBA().solve(pb)
+    for got in (envelope, fused):
+        assert got["iterations"] == dense["iterations"] and got["trials"] == dense["trials"]
+        for k in ("pose_q", "pose_t", "point_xyz", "edge_chi2", "trace", "edge_erase"):
+            assert np.array_equal(got[k], dense[k]), k
+    if shuffle:
+        _compare(O.lba_solve(pb), fused)
+
+
 @pytest.mark.parametrize("small", ["-1", "0", "64", "100000"])
 def test_schur_pair_units_match_oracle(amd, monkeypatch, small):
     """k_schur_pairs' work units (k_pair_list): every off-diagonal pose pair sharing at most
