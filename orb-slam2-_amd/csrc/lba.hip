@@ -2835,7 +2835,8 @@ __device__ __forceinline__ bool mw_group_live(const MwLdl& m, int jb, int g) {
     return true;
 }
 // the panel's column recurrence for the wave's rows (lane < NB: diagonal row jb + lane; else row
-// jb + NB + RB g + lane - NB), P = the rows' panel columns after every earlier update, Y = y(row)
+// jb + NB + RB g + lane - NB), P = the rows' panel columns after every earlier update, Y = y(row),
+// wsc = 64 doubles of LDS
 template <bool kTail>
 __device__ __forceinline__ void mw_panel_core(const MwLdl& m, int jb, int g, int lane, double (&P)[kMwNB], double Y,
                                               double* const wsc) {
@@ -2846,7 +2847,7 @@ __device__ __forceinline__ void mw_panel_core(const MwLdl& m, int jb, int g, int
     const bool live = r < np, inplace = live && lane >= NB;
     double* const Lrow = inplace ? A + (size_t)r * ld + jb : m.sink + (size_t)(lane & (NB - 1)) * ld;
     double* const Wcol = inplace ? A + (size_t)jb * ld + r : m.sink + lane;
-    double* const wst = lane < NB ? wsc + lane : m.sink + lane;
+    double* const wst = wsc + lane;   // (wsc holds 64: the rows below write unread slots, no flat store)
     double dj = shfl_d(P[0], 0);
     bool ok = dj != 0.0 && isfinite(dj);
     double rd = rcp_nr(dj);
@@ -2907,7 +2908,7 @@ __global__ __launch_bounds__(64 * kMwWaves) void k_ldlt_mw_panel(MwLdl m, int jb
     constexpr int NB = kMwNB, RB = 64 - kMwNB;
     if (lm_off(st, 1)) return;
     if (__builtin_amdgcn_readfirstlane(*m.fail)) return;
-    __shared__ double wscS[kMwWaves][NB];
+    __shared__ double wscS[kMwWaves][64];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int g = __builtin_amdgcn_readfirstlane((int)blockIdx.x * kMwWaves + wv);
     if (!mw_group_live(m, jb, g)) return;
@@ -2924,22 +2925,32 @@ __global__ __launch_bounds__(64 * kMwWaves) void k_ldlt_mw_panel(MwLdl m, int jb
 // one 16 x 16 tile (I0, K0) of the trailing update after the panel at column jb:
 // A(I0.., K0..) - W(I0.., panel) L(K0.., panel)^T, kMwNB / 4 v_mfma_f64_16x16x4; lane (li, lk)
 // returns rows I0 + lk + 4 q of column K0 + li
-__device__ __forceinline__ dbl4 mw_tile(const MwLdl& m, int jb, int I0, int K0, int lane) {
-    const int ld = m.np, li = lane & 15, lk = lane >> 4;
-    const double* __restrict__ A = m.A;
+struct MwTileOps {
     double a[kMwNB / 4], bb[kMwNB / 4];
     dbl4 acc;
+};
+__device__ __forceinline__ void mw_tile_load(const MwLdl& m, int jb, int I0, int K0, int lane, MwTileOps& o) {
+    const int ld = m.np, li = lane & 15, lk = lane >> 4;
+    const double* __restrict__ A = m.A;
 #pragma unroll
     for (int s = 0; s < kMwNB / 4; s++) {
         const int p = jb + 4 * s + lk;
-        a[s] = -A[(size_t)p * ld + I0 + li];        // -W(I0 + li, p)
-        bb[s] = A[(size_t)(K0 + li) * ld + p];      //  L(K0 + li, p)
+        o.a[s] = -A[(size_t)p * ld + I0 + li];        // -W(I0 + li, p)
+        o.bb[s] = A[(size_t)(K0 + li) * ld + p];      //  L(K0 + li, p)
     }
 #pragma unroll
-    for (int q = 0; q < 4; q++) acc[q] = A[(size_t)(I0 + lk + 4 * q) * ld + K0 + li];
+    for (int q = 0; q < 4; q++) o.acc[q] = A[(size_t)(I0 + lk + 4 * q) * ld + K0 + li];
+}
+__device__ __forceinline__ dbl4 mw_tile_mma(const MwTileOps& o) {
+    dbl4 acc = o.acc;
 #pragma unroll
-    for (int s = 0; s < kMwNB / 4; s++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], bb[s], acc, 0, 0, 0);
+    for (int s = 0; s < kMwNB / 4; s++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(o.a[s], o.bb[s], acc, 0, 0, 0);
     return acc;
+}
+__device__ __forceinline__ dbl4 mw_tile(const MwLdl& m, int jb, int I0, int K0, int lane) {
+    MwTileOps o;
+    mw_tile_load(m, jb, I0, K0, lane, o);
+    return mw_tile_mma(o);
 }
 // outside the envelope W(I, panel) or L(K, panel) is all zeros: the tile's update adds nothing
 __device__ __forceinline__ bool mw_tile_live(const MwLdl& m, int jb, int I, int K) {
@@ -2989,67 +3000,84 @@ __device__ __forceinline__ void lds_barrier() {
 template <bool kTail>
 __global__ __launch_bounds__(64 * kMwWaves) void k_ldlt_mw_step(MwLdl m, int kb, int nPanelWg, const LmState* st) {
     constexpr int NB = kMwNB, RB = 64 - kMwNB;
-    if (lm_off(st, 1)) return;
-    if (__builtin_amdgcn_readfirstlane(*m.fail)) return;
-    __shared__ double wscS[NB];
+    __shared__ double wscS[64];
     __shared__ double tileS[64][NB + 1];   // rows: the diagonal block's 32, then the group's 32
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int jb = kb * NB, jn = jb + NB, t0 = jn / 16;
     if ((int)blockIdx.x >= nPanelWg) {
+        if (lm_off(st, 1)) return;
+        if (__builtin_amdgcn_readfirstlane(*m.fail)) return;
         const int t = __builtin_amdgcn_readfirstlane(((int)blockIdx.x - nPanelWg) * kMwWaves + wv);
         mw_trail_tile(m, jb, t0 + 2, t, lane);
         return;
     }
     const int g = blockIdx.x;
-    if (!mw_group_live(m, jn, g)) return;
     const int np = m.np, ld = np;
     const bool below = jn + NB + RB * g < np;   // (group 0 of the last panel has no rows below)
+    if (g > 0 && !below) return;
+    TSTAMP(ts0);
     const int Ig = (jn + NB + RB * g) >> 4;
     // tile s of 7: 0..2 the diagonal block's (t0, t0), (t0 + 1, t0), (t0 + 1, t0 + 1); 3..6 the
-    // group's (Ig + u, t0 + v); formed iff live (outside the envelope the update adds nothing)
+    // group's (Ig + u, t0 + v).  Formed whether or not the envelope reaches them: outside it the
+    // update adds exact zeros (L left of a row's envelope is never written: zero from the
+    // once-per-solve clear), so the values equal the skipping trailing launch's, and no load
+    // waits on the envelope table
     auto tile_of = [&](int s, int& I, int& K, int& row0) {
         if (s < 3) { I = t0 + (s > 0 ? 1 : 0); K = t0 + (s == 2 ? 1 : 0); row0 = 16 * (I - t0); }
         else { I = Ig + ((s - 3) >> 1); K = t0 + ((s - 3) & 1); row0 = 32 + 16 * ((s - 3) >> 1); }
     };
-    auto tile_on = [&](int s) {
-        if (s >= 7 || (s >= 3 && !below)) return false;
-        int I, K, row0;
-        tile_of(s, I, K, row0);
-        return mw_tile_live(m, jb, I, K);
-    };
+    auto tile_on = [&](int s) { return s < 3 || (s < 7 && below); };
     const int li = lane & 15, lk = lane >> 4;
+    // every load of the workgroup before any test of the state: the recurrence wave's raw rows
+    // and both tiles' operands of each wave in flight at once (one memory round trip: they were
+    // just written on other XCDs), then the LM phase, the failure flag and the envelope
     double P[NB];
     double Y = 0.0;
-    if (wv == 0) {   // the recurrence wave's raw rows, in flight with the tiles' loads
+    if (wv == 0) {
         const int r = lane < NB ? jn + lane : jn + NB + RB * g + (lane - NB);
         const int rc = min(r, np - 1);
         Y = m.y[rc];
 #pragma unroll
-        for (int c = 0; c < NB; c++) P[c] = m.A[(size_t)rc * ld + jn + c];   // (tiles not formed: as stored)
+        for (int c = 0; c < NB; c++) P[c] = m.A[(size_t)rc * ld + jn + c];   // (the diagonal block's upper tile: as stored)
     }
+    MwTileOps to[2];
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const int s = wv + kMwWaves * k;
+        int I, K, row0;
+        tile_of(min(s, 6), I, K, row0);
+        if (tile_on(s)) mw_tile_load(m, jb, 16 * I, 16 * K, lane, to[k]);
+    }
+    if (lm_off(st, 1)) return;
+    if (__builtin_amdgcn_readfirstlane(*m.fail)) return;
+    if (!mw_group_live(m, jn, g)) return;
 #pragma unroll
     for (int k = 0; k < 2; k++) {
         const int s = wv + kMwWaves * k;
         if (!tile_on(s)) continue;
         int I, K, row0;
         tile_of(s, I, K, row0);
-        const dbl4 acc = mw_tile(m, jb, 16 * I, 16 * K, lane);
+        const dbl4 acc = mw_tile_mma(to[k]);
 #pragma unroll
         for (int q = 0; q < 4; q++) tileS[row0 + lk + 4 * q][16 * (K - t0) + li] = acc[q];
     }
     lds_barrier();
     if (wv != 0) return;
+    TSTAMP(ts1);
     {
         const int u = lane >> 4;   // this lane's tile row: 0, 1 the diagonal block, 2, 3 the group's
 #pragma unroll
         for (int v = 0; v < 2; v++) {
             const int s = u == 0 ? (v == 0 ? 0 : 7) : u == 1 ? 1 + v : 3 + 2 * (u - 2) + v;   // (0, 1): upper, as stored
-            if (!tile_on(s)) continue;
+            if (s == 7 || !tile_on(s)) continue;
 #pragma unroll
             for (int c = 0; c < 16; c++) P[16 * v + c] = tileS[lane][16 * v + c];
         }
     }
     mw_panel_core<kTail>(m, jn, g, lane, P, Y, wscS);
+#ifdef ORB_TIMING
+    if (lane == 0 && g == 0 && kb == 5) printf("mw step kb 5 g 0: tiles %lld recurrence %lld\n", ts1 - ts0, clock64() - ts1);
+#endif
 }
 
 // The backward substitution x = L^-T (y / d) in super-blocks of kSB rows from the bottom, two
