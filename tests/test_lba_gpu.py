@@ -73,10 +73,11 @@ def test_bad_points_skip_outlier_pass(amd):
 
 
 @pytest.mark.parametrize("n,seed", [(6, 0), (114, 1), (120, 2), (128, 3), (130, 4), (180, 5), (301, 6), (600, 7),
-                                    (1194, 8)])
+                                    (1194, 8), (2100, 9)])
 def test_dense_solve_vs_numpy(amd, n, seed):
     """Reduced camera system solve (blocked MFMA LDL^T: the LDS image up to 128, the
-    multi-workgroup k_ldlt_mw_* beyond) against a float64 numpy solve of the same SPD system:
+    multi-workgroup k_ldlt_mw_* beyond; past 2048 the backward substitution takes the per-super-block
+    launches instead of k_ldlt_mw_back) against a float64 numpy solve of the same SPD system:
     relative residual at f64 rounding level."""
     rng = np.random.default_rng(seed)
     G = rng.standard_normal((n, n + 8))
