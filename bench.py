@@ -1594,7 +1594,7 @@ def measure_pinned_copy(dev, mib=64, reps=10):
     return round(h2d, 2), round(d2h, 2)
 
 
-def _pcie_pipelined_leg(amd, dev, cv, W, H, NF, B, steps=16, warmup=4, check=None):
+def _pcie_pipelined_leg(amd, dev, cv, W, H, NF, B, steps=48, warmup=4, check=None):
     """The PCIe-inclusive path as a streaming host would run it, on three HIP streams: the copy
     stream uploads batch s+1's pinned frames (one H2D, into one of three device frame buffers)
     while two compute streams, one per batch parity with its own extractor and matcher handles,
@@ -1604,7 +1604,10 @@ def _pcie_pipelined_leg(amd, dev, cv, W, H, NF, B, steps=16, warmup=4, check=Non
     host wait for the counts).  Events order the hand-offs: a frame buffer is refilled only after
     the extraction that reads it in place (level 0, LEVEL-0 LIFETIME) has finished.  The host
     outputs rotate over three sets: before enqueueing batch s the host waits for batch s-3's
-    outputs (a consumer reading them), so the GPU always holds the next batches' work."""
+    outputs (a consumer reading them), so the GPU always holds the next batches' work.  The timed
+    steps start from an idle pipeline and end with it drained (48 of them: the fill and the drain
+    are ~1 batch each, ~4 % of the time); ORB_BENCH_PCIE_DEPTH sets the frame buffers / host output
+    sets in flight (default 3)."""
     from orb_slam2_amd import synth, _abi
     lib = _abi.lib()
     hip = C.CDLL("libamdhip64.so")
@@ -1621,7 +1624,8 @@ def _pcie_pipelined_leg(amd, dev, cv, W, H, NF, B, steps=16, warmup=4, check=Non
     cap = cap.value
     P = max(B - 1, 1)
     s_copy, s_comps = torch.cuda.Stream(dev), [torch.cuda.Stream(dev) for _ in range(2)]
-    NF_BUF = 3   # device frame buffers: the upload of batch s+1 never waits for batch s's extraction
+    depth = max(3, int(os.environ.get("ORB_BENCH_PCIE_DEPTH", "3")))
+    NF_BUF = depth   # device frame buffers: the upload of batch s+1 never waits for batch s's extraction
     imgs = [torch.empty((B, H, W), dtype=torch.uint8, device=dev) for _ in range(NF_BUF)]
     ev_in = [torch.cuda.Event() for _ in range(NF_BUF)]     # frames of buffer f uploaded
     ev_ext = [torch.cuda.Event() for _ in range(NF_BUF)]    # extraction done reading buffer f
@@ -1631,7 +1635,7 @@ def _pcie_pipelined_leg(amd, dev, cv, W, H, NF, B, steps=16, warmup=4, check=Non
     m12 = [torch.zeros((P, cap), dtype=torch.int32, device=dev) for _ in range(2)]
     nm = [torch.zeros(P, dtype=torch.int32, device=dev) for _ in range(2)]
     sizes = {"pk": B * cap * 28, "pd": B * cap * 32, "pm": P * cap * 4, "off": 3 * (B + 1) * 4}
-    NO = 3   # host output sets
+    NO = depth   # host output sets
     hostbufs, outs = [], []
     for _ in range(NO):   # host-mapped, coherent: the pack kernel's stores land in host memory
         o = {}
