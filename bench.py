@@ -1607,7 +1607,11 @@ def _pcie_pipelined_leg(amd, dev, cv, W, H, NF, B, steps=48, warmup=4, check=Non
     outputs (a consumer reading them), so the GPU always holds the next batches' work.  The timed
     steps start from an idle pipeline and end with it drained (48 of them: the fill and the drain
     are ~1 batch each, ~4 % of the time); ORB_BENCH_PCIE_DEPTH sets the frame buffers / host output
-    sets in flight (default 3)."""
+    sets in flight (default 4: +0-3 % over 3 in same-box A/Bs).  What bounds it (tools/pcie_depth_ab.py,
+    one box): the uploads alone run at 167-170 k frames/s, the compute alone at 211 k, uploads +
+    compute without the compaction into host memory at 165-168 k (the overlap is complete: the
+    upload stream binds), the whole leg at 150-160 k (the compaction's PCIe stores slow the
+    uploads by 5-10 %)."""
     from orb_slam2_amd import synth, _abi
     lib = _abi.lib()
     hip = C.CDLL("libamdhip64.so")
@@ -1624,7 +1628,7 @@ def _pcie_pipelined_leg(amd, dev, cv, W, H, NF, B, steps=48, warmup=4, check=Non
     cap = cap.value
     P = max(B - 1, 1)
     s_copy, s_comps = torch.cuda.Stream(dev), [torch.cuda.Stream(dev) for _ in range(2)]
-    depth = max(3, int(os.environ.get("ORB_BENCH_PCIE_DEPTH", "3")))
+    depth = max(3, int(os.environ.get("ORB_BENCH_PCIE_DEPTH", "4")))
     NF_BUF = depth   # device frame buffers: the upload of batch s+1 never waits for batch s's extraction
     imgs = [torch.empty((B, H, W), dtype=torch.uint8, device=dev) for _ in range(NF_BUF)]
     ev_in = [torch.cuda.Event() for _ in range(NF_BUF)]     # frames of buffer f uploaded
@@ -1651,13 +1655,23 @@ def _pcie_pipelined_leg(amd, dev, cv, W, H, NF, B, steps=48, warmup=4, check=Non
     moved = {"d2h": 0}
     ev_done = [torch.cuda.Event() for _ in range(NO)]   # host output set j written
 
+    # diagnosis knobs (tools/pcie_depth_ab.py): ORB_BENCH_PCIE_PART=copy (uploads only), =compute (no
+    # uploads: the frames stay resident), =nopack (no compaction into host memory); default: all
+    part = os.environ.get("ORB_BENCH_PCIE_PART", "all")
+
     def enqueue(s):
         i, f = s % 2, s % NF_BUF
         o = outs[s % NO]
+        if part == "copy":
+            with torch.cuda.stream(s_copy):
+                imgs[f].copy_(host_in[s % nb], non_blocking=True)
+            ev_done[s % NO].record(s_copy)
+            return
         if s >= NF_BUF:   # buffer f's previous extraction (batch s-3) must be done reading level 0
             s_copy.wait_event(ev_ext[f])
-        with torch.cuda.stream(s_copy):
-            imgs[f].copy_(host_in[s % nb], non_blocking=True)
+        if part != "compute":
+            with torch.cuda.stream(s_copy):
+                imgs[f].copy_(host_in[s % nb], non_blocking=True)
         ev_in[f].record(s_copy)
         s_comp = s_comps[i]   # batch s-2 ran on this stream before: set i is free in stream order
         s_comp.wait_event(ev_in[f])
@@ -1671,6 +1685,9 @@ def _pcie_pipelined_leg(amd, dev, cv, W, H, NF, B, steps=48, warmup=4, check=Non
                 ms[i]._h, dp(k), dp(d), dp(c), C.c_void_p(k.data_ptr() + cap * 28), C.c_void_p(d.data_ptr() + cap * 32),
                 C.c_void_p(c.data_ptr() + 4), B - 1, cap, W, H, 100, dp(mm), dp(nm[i]), sp))
         off = o["off"][1].value
+        if part == "nopack":
+            ev_done[s % NO].record(s_comp)
+            return
         _abi.check("pack", lib.orb_pack_rows_device(dp(k), 28, cap, dp(c), B, o["pk"][1], C.c_void_p(off), sp))
         _abi.check("pack", lib.orb_pack_rows_device(dp(d), 32, cap, dp(c), B, o["pd"][1], C.c_void_p(off + 4 * (B + 1)),
                                                     sp))
@@ -1681,6 +1698,8 @@ def _pcie_pipelined_leg(amd, dev, cv, W, H, NF, B, steps=48, warmup=4, check=Non
 
     def consume(s):   # the host reads batch s's outputs: totals from the mapped offsets
         ev_done[s % NO].synchronize()
+        if part in ("copy", "nopack"):
+            return
         o = outs[s % NO]
         offs = np.ctypeslib.as_array(C.cast(o["off"][0], C.POINTER(C.c_int32)), shape=(3, B + 1))
         n_kp, n_m = int(offs[0, B]), int(offs[2, B - 1]) if B > 1 else 0

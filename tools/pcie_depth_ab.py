@@ -1,5 +1,6 @@
-"""The pipelined PCIe-inclusive leg (bench._pcie_pipelined_leg, B = 8 and 64) at pipeline depths 3 / 4 / 5
-(ORB_BENCH_PCIE_DEPTH: device frame buffers and host output sets in flight), interleaved, in one process."""
+"""The pipelined PCIe-inclusive leg (bench._pcie_pipelined_leg, B = 64): the whole leg and its parts
+(ORB_BENCH_PCIE_PART = copy: uploads only; compute: no uploads; nopack: no compaction into host
+memory), and pipeline depths 3 / 4 (ORB_BENCH_PCIE_DEPTH), interleaved, in one process."""
 import os
 import pathlib
 import sys
@@ -19,8 +20,9 @@ torch.cuda.set_stream(torch.cuda.Stream(dev))
 cv = synth.canvas(0x5EED0002, 640, 480)
 print("pinned copy GB/s", bench.measure_pinned_copy(dev), flush=True)
 for rep in range(2):
-    for depth in (3, 4, 5):
+    for part, depth in (("all", 3), ("all", 4), ("copy", 3), ("compute", 3), ("nopack", 3)):
         os.environ["ORB_BENCH_PCIE_DEPTH"] = str(depth)
-        for B in (8, 64):
-            r = bench._pcie_pipelined_leg(amd, dev, cv, 640, 480, 1000, B)
-            print("depth", depth, "B", B, r["frames_per_s"], r["ms_per_step"], flush=True)
+        os.environ["ORB_BENCH_PCIE_PART"] = part
+        r = bench._pcie_pipelined_leg(amd, dev, cv, 640, 480, 1000, 64)
+        print("part", part, "depth", depth, "B 64", r["frames_per_s"], r["ms_per_step"], flush=True)
+os.environ.pop("ORB_BENCH_PCIE_PART")
