@@ -1567,6 +1567,19 @@ def batch_sweep(amd, dev, m):
         r = _pcie_pipelined_leg(amd, dev, cv, W, H, NF, B)
         r["h2d_bound_frames_per_s"] = round(h2d * 1e9 / r["h2d_bytes_per_step"] * B, 1)
         r["frac_of_h2d_bound"] = round(r["frames_per_s"] / r["h2d_bound_frames_per_s"], 3)
+        # the same pipeline with its uploads alone (no compute, no compaction): the rate the copy
+        # stream sustains for this batch's frames, the bound the whole leg meets (bench._pcie_pipelined_leg)
+        old_part = os.environ.get("ORB_BENCH_PCIE_PART")
+        os.environ["ORB_BENCH_PCIE_PART"] = "copy"
+        try:
+            up = _pcie_pipelined_leg(amd, dev, cv, W, H, NF, B)
+        finally:
+            if old_part is None:
+                os.environ.pop("ORB_BENCH_PCIE_PART", None)
+            else:
+                os.environ["ORB_BENCH_PCIE_PART"] = old_part
+        r["uploads_only_frames_per_s"] = up["frames_per_s"]
+        r["frac_of_uploads_only"] = round(r["frames_per_s"] / up["frames_per_s"], 3)
         res[f"B{B}_pcie_pipelined"] = r
     return res
 
