@@ -178,9 +178,8 @@ class ORBmatcher:
         ow = np.ascontiguousarray(Ow, np.float32)
         lib = _abi.lib()
         vp = C.c_void_p
-        lib.orb_search_by_projection_kf.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, C.c_float, C.c_int, vp,
-                                                    C.c_float, C.c_int, vp]
-        lib.orb_search_by_projection_kf.restype = C.c_int
+        _abi.sig(lib.orb_search_by_projection_kf, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, C.c_float, C.c_int, vp,
+                                                    C.c_float, C.c_int, vp], C.c_int)
         n = _abi.check("orb_search_by_projection_kf", lib.orb_search_by_projection_kf(
             self._h, C.byref(vc), _abi.ptr(Tc), _abi.ptr(ow), C.byref(vk), *[_abi.ptr(x) for x in a], _abi.ptr(camv),
             float(np.float32(log_scale_factor)), len(sf), _abi.ptr(sf), float(th), int(ORBdist), _abi.ptr(cur_mp)))
@@ -204,8 +203,7 @@ class ORBmatcher:
         v = pKF.view()
         lib = _abi.lib()
         vp = C.c_void_p
-        lib.orb_search_by_projection_sim3.argtypes = [vp, vp, vp, C.c_int, vp, vp, vp, vp, vp, vp, C.c_float, vp]
-        lib.orb_search_by_projection_sim3.restype = C.c_int
+        _abi.sig(lib.orb_search_by_projection_sim3, [vp, vp, vp, C.c_int, vp, vp, vp, vp, vp, vp, C.c_float, vp], C.c_int)
         n = _abi.check("orb_search_by_projection_sim3", lib.orb_search_by_projection_sim3(
             self._h, C.byref(v), C.byref(kp), len(a[0]), *[_abi.ptr(x) for x in a], float(th), _abi.ptr(matched)))
         return n, matched
@@ -239,9 +237,8 @@ class ORBmatcher:
         v1, v2 = pKF.view(), F.view()
         lib = _abi.lib()
         vp = C.c_void_p
-        lib.orb_search_by_bow_frame.argtypes = [C.c_int, vp, vp, C.c_int, vp, vp, vp, vp, C.c_int, vp, vp, vp,
-                                                C.c_float, C.c_int, vp]
-        lib.orb_search_by_bow_frame.restype = C.c_int
+        _abi.sig(lib.orb_search_by_bow_frame, [C.c_int, vp, vp, C.c_int, vp, vp, vp, vp, C.c_int, vp, vp, vp,
+                                                C.c_float, C.c_int, vp], C.c_int)
         n = _abi.check("orb_search_by_bow_frame", lib.orb_search_by_bow_frame(
             self.device, C.byref(v1), _abi.ptr(ok), len(fk[0]), *[_abi.ptr(x) for x in fk], C.byref(v2), len(ff[0]),
             *[_abi.ptr(x) for x in ff], self.mfNNratio, int(self.mbCheckOrientation), _abi.ptr(m)))
@@ -258,9 +255,8 @@ class ORBmatcher:
         v1, v2 = pKF1.view(), pKF2.view()
         lib = _abi.lib()
         vp = C.c_void_p
-        lib.orb_search_by_bow_kf.argtypes = [C.c_int, vp, vp, C.c_int, vp, vp, vp, vp, vp, C.c_int, vp, vp, vp,
-                                             C.c_float, C.c_int, vp]
-        lib.orb_search_by_bow_kf.restype = C.c_int
+        _abi.sig(lib.orb_search_by_bow_kf, [C.c_int, vp, vp, C.c_int, vp, vp, vp, vp, vp, C.c_int, vp, vp, vp,
+                                             C.c_float, C.c_int, vp], C.c_int)
         n = _abi.check("orb_search_by_bow_kf", lib.orb_search_by_bow_kf(
             self.device, C.byref(v1), _abi.ptr(o1), len(f1[0]), *[_abi.ptr(x) for x in f1], C.byref(v2),
             _abi.ptr(o2), len(f2[0]), *[_abi.ptr(x) for x in f2], self.mfNNratio, int(self.mbCheckOrientation),
@@ -289,8 +285,7 @@ def ComputeDistinctiveDescriptors(descriptor_lists, device=0):
     best = np.zeros(M, np.int32)
     out = np.zeros((M, 32), np.uint8)
     lib = _abi.lib()
-    lib.orb_distinctive_descriptors.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
-    lib.orb_distinctive_descriptors.restype = C.c_int
+    _abi.sig(lib.orb_distinctive_descriptors, [C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p], C.c_int)
     _abi.check("orb_distinctive_descriptors",
                lib.orb_distinctive_descriptors(device, _abi.ptr(desc), _abi.ptr(start), M, _abi.ptr(best), _abi.ptr(out)))
     return best, out
@@ -337,8 +332,7 @@ def _fuse(entry, kf, Tcw, Ow, cam, log_scale_factor, scale_factors, inv_level_si
     v = kf.view()
     lib = _abi.lib()
     fn = getattr(lib, entry)
-    fn.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int] + [C.c_void_p] * 6 + [C.c_float, C.c_void_p, C.c_void_p]
-    fn.restype = C.c_int
+    _abi.sig(fn, [C.c_int, C.c_void_p, C.c_void_p, C.c_int] + [C.c_void_p] * 6 + [C.c_float, C.c_void_p, C.c_void_p], C.c_int)
     _abi.check(entry, fn(device, C.byref(v), C.byref(kp), n, *[_abi.ptr(x) for x in a], th, _abi.ptr(bi),
                          _abi.ptr(bd)))
     return bi, bd
@@ -381,8 +375,7 @@ def SearchBySim3(kf1: Frame, kf2: Frame, pts1, pts2, cam1, scale1, scale2, th=7.
     v1, v2 = kf1.view(), kf2.view()
     lib = _abi.lib()
     vp = C.c_void_p
-    lib.orb_search_by_sim3.argtypes = [C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_float, vp]
-    lib.orb_search_by_sim3.restype = C.c_int
+    _abi.sig(lib.orb_search_by_sim3, [C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_float, vp], C.c_int)
     n = _abi.check("orb_search_by_sim3", lib.orb_search_by_sim3(
         device, C.byref(v1), C.byref(v2), C.byref(p1), C.byref(p2), _abi.ptr(cam), C.byref(s1), C.byref(s2),
         float(th), _abi.ptr(m)))
@@ -404,9 +397,8 @@ def SearchForTriangulation(kf1: Frame, kf2: Frame, has_mp1, has_mp2, featvec1, f
     m = np.zeros(kf1.N, np.int32)
     lib = _abi.lib()
     vp = C.c_void_p
-    lib.orb_search_for_triangulation.argtypes = [C.c_int, vp, vp, vp, vp, C.c_int, vp, vp, vp, C.c_int, vp, vp, vp, vp,
-                                                 C.c_float, C.c_float, vp, vp, C.c_int, C.c_int, C.c_int, vp]
-    lib.orb_search_for_triangulation.restype = C.c_int
+    _abi.sig(lib.orb_search_for_triangulation, [C.c_int, vp, vp, vp, vp, C.c_int, vp, vp, vp, C.c_int, vp, vp, vp, vp,
+                                                 C.c_float, C.c_float, vp, vp, C.c_int, C.c_int, C.c_int, vp], C.c_int)
     n = _abi.check("orb_search_for_triangulation", lib.orb_search_for_triangulation(
         device, C.byref(v1), C.byref(v2), _abi.ptr(hm1), _abi.ptr(hm2), len(fv[0][0]), *[_abi.ptr(x) for x in fv[0]],
         len(fv[1][0]), *[_abi.ptr(x) for x in fv[1]], _abi.ptr(F), float(epipole[0]), float(epipole[1]), _abi.ptr(sf),

@@ -351,11 +351,9 @@ class PoseBatchResult(C.Structure):
 def _pose_sig():
     lib = _abi.lib()
     if not getattr(lib, "_pose_sig", False):
-        lib.pose_optimize_batch.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
-        lib.pose_optimize_batch.restype = C.c_int
-        lib.pose_optimize_batch_device.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
-                                                   C.c_void_p]
-        lib.pose_optimize_batch_device.restype = C.c_int
+        _abi.sig(lib.pose_optimize_batch, [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p], C.c_int)
+        _abi.sig(lib.pose_optimize_batch_device, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                   C.c_void_p], C.c_int)
         lib._pose_sig = True
     return lib
 

@@ -163,8 +163,7 @@ class ORBVocabulary:
     def _handle(self):
         if self._h is None:
             lib = _abi.lib()
-            lib.orb_vocabulary_create.argtypes = [C.c_int, C.c_void_p, C.c_void_p]
-            lib.orb_vocabulary_create.restype = C.c_int
+            _abi.sig(lib.orb_vocabulary_create, [C.c_int, C.c_void_p, C.c_void_p], C.c_int)
             s = VocabularyStruct(len(self.parent), self.m_L, _abi.ptr(self.desc), _abi.ptr(self.child_start),
                                  _abi.ptr(self.child_idx), _abi.ptr(self.word_id), _abi.ptr(self.weight))
             h = C.c_void_p()
@@ -175,8 +174,7 @@ class ORBVocabulary:
     def _release(self):
         if self._h is not None:
             lib = _abi.lib()
-            lib.orb_vocabulary_destroy.argtypes = [C.c_void_p]
-            lib.orb_vocabulary_destroy.restype = None
+            _abi.sig(lib.orb_vocabulary_destroy, [C.c_void_p], None)
             lib.orb_vocabulary_destroy(self._h)
             self._h = None
 
@@ -197,9 +195,8 @@ class ORBVocabulary:
         nid = np.zeros(n, np.int32)
         if n:
             lib = _abi.lib()
-            lib.orb_vocabulary_transform.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p,
-                                                     C.c_void_p, C.c_void_p]
-            lib.orb_vocabulary_transform.restype = C.c_int
+            _abi.sig(lib.orb_vocabulary_transform, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p,
+                                                     C.c_void_p, C.c_void_p], C.c_int)
             _abi.check("orb_vocabulary_transform",
                        lib.orb_vocabulary_transform(self._handle(), _abi.ptr(f), n, levelsup, _abi.ptr(wid),
                                                     _abi.ptr(w), _abi.ptr(nid)))

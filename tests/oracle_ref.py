@@ -55,7 +55,14 @@ def lib():
 
 
 def P(a):
-    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+    # (the same buffer-protocol address as the product's _abi.ptr, so the routed-call rows' CPU
+    # column pays the same Python marshalling as the GPU column)
+    if a is None:
+        return None
+    try:
+        return C.c_void_p(C.addressof(C.c_char.from_buffer(a)))
+    except (TypeError, ValueError, BufferError):
+        return C.c_void_p(a.ctypes.data)
 
 
 def params(nfeatures=1000, scale=1.2, nlevels=8, ini=20, minth=7):
